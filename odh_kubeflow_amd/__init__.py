@@ -1,0 +1,9 @@
+"""MI355X-native Kubeflow notebook control plane.
+
+A from-scratch rebuild of the capabilities of ``harshad16/odh-kubeflow`` (the Kubeflow
+notebook controller, the OpenDataHub notebook controller + mutating webhook, and the
+idle-notebook culler) that places notebook StatefulSets on the 8 MI355X GPUs of a node
+through the ``amd.com/gpu`` device plugin and culls on amdgpu busy counters.
+"""
+
+__version__ = "0.1.0"

@@ -1,0 +1,200 @@
+"""In-process cluster assembly: fake apiserver + the three controllers + fake node(s).
+
+Used by the tests (the envtest-equivalent substrate), ``bench.py`` and the smoke test.
+Every piece is the production component; only the apiserver, kube-controller-manager
+(StatefulSet controller, scheduler, optional GC) and kubelet are stand-ins.
+"""
+
+from __future__ import annotations
+
+import asyncio
+import os
+import time
+from dataclasses import dataclass, field
+from typing import Callable, Dict, List, Mapping, Optional, Sequence
+
+from .apiserver.store import ObjectStore
+from .models import kinds
+from .models import meta as m
+from .runtime.manager import Manager
+
+
+@dataclass
+class ClusterConfig:
+    gc: bool = True
+    gpus_per_node: int = 8
+    nodes: int = 1
+    kf: bool = True
+    culler: bool = False
+    odh: bool = False
+    webhook: bool = False
+    event_reemit: bool = True
+    controller_namespace: str = "opendatahub"
+    max_concurrent: int = 8
+    env: Dict[str, str] = field(default_factory=dict)
+    kube_rbac_proxy_image: str = "quay.io/brancz/kube-rbac-proxy:v0.18.1"
+    runtime_factory: Optional[Callable[[int], object]] = None  # device -> ContainerRuntime
+    startup_probe: Optional[Callable] = None
+    gpu_runtimes_in_process: bool = True  # False: rank processes host GPU runtimes (multi-GPU bench)
+    reference_emulation: bool = False  # reproduce the reference's serialising behaviour for comparison
+    activity_source: Optional[object] = None
+
+
+class LocalCluster:
+    def __init__(self, cfg: Optional[ClusterConfig] = None, store: Optional[ObjectStore] = None):
+        self.cfg = cfg or ClusterConfig()
+        self.env = {**os.environ, **self.cfg.env}
+        self.store = store or ObjectStore(gc=self.cfg.gc)
+        self.managers: List[Manager] = []
+        self.kube: Optional[Manager] = None
+        self.kf: Optional[Manager] = None
+        self.odh: Optional[Manager] = None
+        self.kubelets: List[Manager] = []
+        self.gpu_runtimes = []
+        self.reconcilers: Dict[str, object] = {}
+        self.webhook = None
+
+    # ------------------------------------------------------------------ build
+
+    def _mgr(self, name: str, **kw) -> Manager:
+        mgr = Manager.in_process(self.store, name=name, default_max_concurrent=self.cfg.max_concurrent, **kw)
+        self.managers.append(mgr)
+        return mgr
+
+    async def start(self) -> "LocalCluster":
+        from .kubelet.node import GpuRuntime, SchedulerController, make_node
+        from .kubelet.statefulset import StatefulSetController
+
+        cfg = self.cfg
+        admin = Manager.in_process(self.store, name="admin").client
+        self.admin = admin
+        for ns in ("default", cfg.controller_namespace):
+            await self.ensure_namespace(ns)
+
+        # fake kube-controller-manager + scheduler
+        kube = self.kube = self._mgr("kube-controller-manager")
+        StatefulSetController(kube.client, kube.reader, kube.get_event_recorder_for("statefulset-controller")) \
+            .setup_with_manager(kube)
+        SchedulerController(kube.client, kube.reader, kube.get_event_recorder_for("default-scheduler")) \
+            .setup_with_manager(kube)
+
+        # nodes + per-GPU runtimes
+        for n in range(cfg.nodes):
+            node_name = f"mi355x-node-{n}"
+            await admin.create(make_node(node_name, cfg.gpus_per_node))
+            if cfg.gpu_runtimes_in_process:
+                kl = self._mgr(f"kubelet-{node_name}")
+                self.kubelets.append(kl)
+                for d in range(cfg.gpus_per_node):
+                    rt = cfg.runtime_factory(d) if cfg.runtime_factory else None
+                    g = GpuRuntime(kl.client, kl.reader, kl.get_event_recorder_for("kubelet"), node_name, [d],
+                                   runtime=rt, startup_probe=cfg.startup_probe, owns_cpu_pods=(d == 0))
+                    g.setup_with_manager(kl, name=f"kubelet-{node_name}-gpu{d}")
+                    self.gpu_runtimes.append(g)
+
+        if cfg.webhook:
+            await self._start_webhook()
+        if cfg.kf:
+            self._build_kf()
+        if cfg.odh:
+            self._build_odh()
+        for mgr in self.managers:
+            await mgr.start()
+        return self
+
+    def _build_kf(self) -> None:
+        from .controllers.metrics import NotebookMetrics
+        from .controllers.notebook import NotebookEventReemitter, NotebookReconciler
+
+        kf = self.kf = self._mgr("notebook-controller")
+        metrics = NotebookMetrics(kf.reader, kf.registry)
+        self.kf_metrics = metrics
+        emu = self.cfg.reference_emulation
+        r = NotebookReconciler(kf.client, kf.reader, kf.get_event_recorder_for("notebook-controller"), metrics,
+                               env=self.env, unconditional_status=emu, owner_index=not emu)
+        r.setup_with_manager(kf, max_concurrent=1 if emu else None)
+        self.reconcilers["notebook"] = r
+        if self.cfg.event_reemit:
+            e = NotebookEventReemitter(kf.client, kf.reader, kf.get_event_recorder_for("notebook-controller"))
+            e.setup_with_manager(kf, max_concurrent=1 if emu else None)
+            self.reconcilers["events"] = e
+        if self.cfg.culler or self.env.get("ENABLE_CULLING") == "true":
+            from .controllers.culling import CullingReconciler
+
+            c = CullingReconciler(kf.client, kf.reader, metrics, env=self.env, activity=self.cfg.activity_source)
+            c.setup_with_manager(kf, max_concurrent=1 if emu else None)
+            self.reconcilers["culler"] = c
+
+    def _build_odh(self) -> None:
+        from .controllers.odh.reconciler import OpenshiftNotebookReconciler
+
+        odh = self.odh = self._mgr("odh-notebook-controller", uncached=(kinds.CONFIG_MAP, kinds.SECRET))
+        emu = self.cfg.reference_emulation
+        r = OpenshiftNotebookReconciler(odh.client, odh.reader, self.cfg.controller_namespace, env=self.env,
+                                        recorder=odh.get_event_recorder_for("odh-notebook-controller"),
+                                        blocking_lock_removal=emu)
+        r.setup_with_manager(odh, max_concurrent=1 if emu else None)
+        self.reconcilers["odh"] = r
+
+    async def _start_webhook(self) -> None:
+        from .webhook.notebook_webhook import NotebookWebhook, register_in_process
+
+        wh_mgr = Manager.in_process(self.store, name="odh-webhook", uncached=(kinds.CONFIG_MAP, kinds.SECRET))
+        self.webhook = NotebookWebhook(wh_mgr.client, self.cfg.controller_namespace,
+                                       kube_rbac_proxy_image=self.cfg.kube_rbac_proxy_image, env=self.env)
+        register_in_process(self.store, self.webhook)
+
+    # ------------------------------------------------------------------ helpers
+
+    async def ensure_namespace(self, ns: str) -> None:
+        if self.store.peek(kinds.NAMESPACE, ns) is None:
+            await self.admin.create({"apiVersion": "v1", "kind": "Namespace", "metadata": {"name": ns}})
+
+    async def stop(self) -> None:
+        for mgr in reversed(self.managers):
+            await mgr.stop()
+        for g in self.gpu_runtimes:
+            await g.close()
+
+    async def settle(self, timeout: float = 10.0) -> bool:
+        """Wait until every controller in every manager is idle (twice, to catch cascades)."""
+        deadline = time.monotonic() + timeout
+        quiet = 0
+        while time.monotonic() < deadline:
+            if all(mgr.idle() for mgr in self.managers):
+                quiet += 1
+                if quiet >= 3:
+                    for mgr in self.managers:
+                        for rec in mgr._recorders.values():
+                            await rec.flush()
+                    return True
+            else:
+                quiet = 0
+            await asyncio.sleep(0.002)
+        return False
+
+    async def wait_for(self, pred: Callable[[], bool], timeout: float = 10.0, interval: float = 0.002) -> bool:
+        deadline = time.monotonic() + timeout
+        while time.monotonic() < deadline:
+            if pred():
+                return True
+            await asyncio.sleep(interval)
+        return pred()
+
+    def notebook_ready(self, name: str, namespace: str) -> bool:
+        nb = self.store.peek(kinds.NOTEBOOK, name, namespace)
+        if nb is None:
+            return False
+        st = nb.get("status") or {}
+        if st.get("readyReplicas") != 1:
+            return False
+        return any(c.get("type") == "Ready" and c.get("status") == "True" for c in st.get("conditions") or [])
+
+    def reconcile_count(self) -> int:
+        return sum(mgr.reconcile_count() for mgr in (self.kf, self.odh) if mgr is not None)
+
+    async def __aenter__(self):
+        return await self.start()
+
+    async def __aexit__(self, *exc):
+        await self.stop()

@@ -1,0 +1,73 @@
+"""Notebook controller Prometheus metrics (``kf/pkg/metrics/metrics.go``).
+
+``notebook_running{namespace}`` is recomputed on every scrape from the StatefulSets
+whose pod template carries ``notebook-name == sts.name`` (metrics.go:82-99), read from
+the cache rather than a cluster-wide live List.  ``notebook_culling_total`` and
+``last_notebook_culling_timestamp_seconds`` are registered and exported too — the
+reference defines them but leaves them out of Describe/Collect (metrics.go:67-79),
+so they never reach ``/metrics``; that is treated as a bug here.
+Two MI355X additions: ``notebook_gpus_allocated{namespace}`` (``amd.com/gpu`` limits
+of running notebooks) and ``notebook_pod_ready_seconds`` (create→Ready latency).
+"""
+
+from __future__ import annotations
+
+from prometheus_client import CollectorRegistry, Counter, Gauge, Histogram
+from prometheus_client.core import GaugeMetricFamily
+
+from ..models import kinds
+from ..models.notebook import NOTEBOOK_NAME_LABEL, gpu_request
+
+
+class _RunningCollector:
+    def __init__(self, reader):
+        self.reader = reader
+
+    def describe(self):
+        return [GaugeMetricFamily("notebook_running", "Current running notebooks in the cluster", labels=["namespace"]),
+                GaugeMetricFamily("notebook_gpus_allocated", "amd.com/gpu requested by running notebooks",
+                                  labels=["namespace"])]
+
+    def collect(self):
+        running = GaugeMetricFamily("notebook_running", "Current running notebooks in the cluster",
+                                    labels=["namespace"])
+        gpus = GaugeMetricFamily("notebook_gpus_allocated", "amd.com/gpu requested by running notebooks",
+                                 labels=["namespace"])
+        per_ns, per_ns_gpu = {}, {}
+        try:
+            items = self.reader.list(kinds.STATEFUL_SET)
+        except Exception:
+            items = []
+        for sts in items:
+            tmpl = ((sts.get("spec") or {}).get("template") or {})
+            name = ((tmpl.get("metadata") or {}).get("labels") or {}).get(NOTEBOOK_NAME_LABEL)
+            if name and name == sts["metadata"]["name"]:
+                ns = sts["metadata"].get("namespace", "")
+                per_ns[ns] = per_ns.get(ns, 0) + 1
+                if (sts.get("spec") or {}).get("replicas", 1):
+                    per_ns_gpu[ns] = per_ns_gpu.get(ns, 0) + gpu_request(tmpl.get("spec") or {})
+        for ns, v in sorted(per_ns.items()):
+            running.add_metric([ns], v)
+        for ns, v in sorted(per_ns_gpu.items()):
+            gpus.add_metric([ns], v)
+        yield running
+        yield gpus
+
+
+class NotebookMetrics:
+    def __init__(self, reader, registry: CollectorRegistry):
+        self.registry = registry
+        registry.register(_RunningCollector(reader))
+        self.notebook_creation = Counter("notebook_create", "Total times of creating notebooks", ["namespace"],
+                                         registry=registry)
+        self.notebook_fail_creation = Counter("notebook_create_failed", "Total failure times of creating notebooks",
+                                              ["namespace"], registry=registry)
+        self.notebook_culling_count = Counter("notebook_culling", "Total times of culling notebooks",
+                                              ["namespace", "name"], registry=registry)
+        self.notebook_culling_timestamp = Gauge("last_notebook_culling_timestamp_seconds",
+                                                "Timestamp of the last notebook culling in seconds",
+                                                ["namespace", "name"], registry=registry)
+        self.pod_ready_seconds = Histogram("notebook_pod_ready_seconds",
+                                           "Seconds from Notebook creation to its pod reporting Ready",
+                                           ["namespace"], registry=registry,
+                                           buckets=(0.05, 0.1, 0.25, 0.5, 1, 2, 5, 10, 30, 60, 120, 300))

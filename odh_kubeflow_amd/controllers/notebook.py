@@ -1,0 +1,410 @@
+"""Core Notebook reconciler — the upstream Kubeflow notebook controller
+(``kf/controllers/notebook_controller.go``), re-built for an 8×MI355X node.
+
+Per reconcile of a Notebook (reference ``Reconcile`` :93-297):
+
+1. skip objects being deleted (:138-140);
+2. generate the StatefulSet (``generate_statefulset``, :433-523) — replicas 0 while the
+   ``kubeflow-resource-stopped`` annotation is present (the culler's STOP and the odh
+   reconciliation lock share it), ``generateName: nb-`` for names > 52 chars;
+3. find the StatefulSet **through the owner-UID index** instead of listing every
+   StatefulSet in the namespace (:157-170), create it or copy owned fields onto it;
+4. reconcile the Service (port 80 → first container port) and, with ``USE_ISTIO=true``,
+   the Istio VirtualService (:558-699);
+5. mirror pod ``<sts>-0`` into ``status`` — written **only when it changed
+   semantically** (the reference writes it unconditionally every pass, :299-313, and
+   its ``metav1.Now()`` stamping makes every pass a new write that re-triggers both
+   controllers);
+6. honour ``notebooks.opendatahub.io/notebook-restart`` by deleting the pod (:262-294).
+
+``amd.com/gpu`` requests/limits pass through verbatim; with ``GPU_NODE_SELECTOR=true``
+pods that request GPUs also get the AMD node-labeller selector and the
+``amd.com/gpu`` toleration so they land on MI355X nodes.
+
+Event re-emission (:97-126) runs as its own small controller
+(:class:`NotebookEventReemitter`) instead of sharing the Notebook work queue — the
+TODO at :96 of the reference.
+"""
+
+from __future__ import annotations
+
+import json
+import logging
+import os
+from typing import Mapping, Optional
+
+from ..models import kinds
+from ..models import meta as m
+from ..models.errors import ApiError, is_already_exists, is_not_found
+from ..models.notebook import (ANNOTATION_HEADERS_REQUEST_SET, ANNOTATION_NOTEBOOK_RESTART, ANNOTATION_REWRITE_URI,
+                               DEFAULT_CONTAINER_PORT, DEFAULT_FS_GROUP, DEFAULT_SERVING_PORT, GPU_RESOURCE,
+                               MAX_STATEFULSET_NAME_LENGTH, NOTEBOOK_NAME_LABEL, PREFIX_ENV_VAR, STATEFULSET_LABEL,
+                               STOP_ANNOTATION, WORKBENCH_LABEL, gpu_request, pod_cond_to_notebook_cond)
+from ..runtime.controller import Request, Result, pred_funcs
+from ..utils.objutil import deepcopy_json
+from ..utils.reconcilehelper import copy_service_fields, copy_statefulset_fields, copy_virtual_service
+
+log = logging.getLogger("controllers.Notebook")
+
+NOTEBOOK_KIND = kinds.NOTEBOOK_V1BETA1  # the kf controller works on the hub version (notebook_controller.go:31)
+
+
+# ------------------------------------------------------------------ generators
+
+
+def set_prefix_env_var(nb: dict, container: dict) -> None:
+    """``setPrefixEnvVar`` (:417-431).
+
+    The reference assigns to the range-loop copy, so an existing ``NB_PREFIX`` keeps
+    its user-provided value; that observable behaviour is preserved.
+    """
+    prefix = f"/notebook/{m.namespace(nb)}/{m.name(nb)}"
+    env = container.setdefault("env", [])
+    for e in env:
+        if e.get("name") == PREFIX_ENV_VAR:
+            return
+    env.append({"name": PREFIX_ENV_VAR, "value": prefix})
+
+
+def _gpu_placement(pod_spec: dict) -> None:
+    """MI355X placement: node-labeller selector + toleration for pods requesting amd.com/gpu."""
+    if gpu_request(pod_spec) <= 0:
+        return
+    sel = pod_spec.setdefault("nodeSelector", {})
+    sel.setdefault("amd.com/gpu.family", "AI")
+    tol = pod_spec.setdefault("tolerations", [])
+    if not any(t.get("key") == GPU_RESOURCE for t in tol):
+        tol.append({"key": GPU_RESOURCE, "operator": "Exists", "effect": "NoSchedule"})
+
+
+def generate_statefulset(nb: dict, is_generate_name: bool, env: Mapping[str, str] = os.environ) -> dict:
+    """``generateStatefulSet`` (:433-523)."""
+    name, ns = m.name(nb), m.namespace(nb)
+    replicas = 0 if m.has_annotation(nb, STOP_ANNOTATION) else 1
+    if is_generate_name:
+        md = {"generateName": "nb-", "namespace": ns}
+    else:
+        md = {"name": name, "namespace": ns, "labels": {}}
+    pod_spec = deepcopy_json((((nb.get("spec") or {}).get("template") or {}).get("spec")) or {})
+    tmpl_labels = {STATEFULSET_LABEL: name, NOTEBOOK_NAME_LABEL: name, WORKBENCH_LABEL: "true"}
+    nb_labels = m.labels(nb)
+    if nb_labels:
+        md.setdefault("labels", {}).update(nb_labels)
+        tmpl_labels.update(nb_labels)
+    tmpl_ann = {k: v for k, v in m.annotations(nb).items() if "kubectl" not in k and "notebook" not in k}
+    sts = {
+        "apiVersion": "apps/v1", "kind": "StatefulSet", "metadata": md,
+        "spec": {
+            "replicas": replicas,
+            "selector": {"matchLabels": {STATEFULSET_LABEL: name}},
+            "template": {"metadata": {"labels": tmpl_labels, "annotations": tmpl_ann}, "spec": pod_spec},
+        },
+    }
+    containers = pod_spec.get("containers") or []
+    if containers:
+        c = containers[0]
+        if not c.get("workingDir"):
+            c["workingDir"] = "/home/jovyan"
+        if c.get("ports") is None:
+            c["ports"] = [{"containerPort": DEFAULT_CONTAINER_PORT, "name": "notebook-port", "protocol": "TCP"}]
+        set_prefix_env_var(nb, c)
+    add_fs = env.get("ADD_FSGROUP")
+    if add_fs is None or add_fs == "true":
+        if pod_spec.get("securityContext") is None:
+            pod_spec["securityContext"] = {"fsGroup": DEFAULT_FS_GROUP}
+    if env.get("GPU_NODE_SELECTOR", "false") == "true":
+        _gpu_placement(pod_spec)
+    return sts
+
+
+def generate_service(nb: dict) -> dict:
+    """``generateService`` (:525-552): ClusterIP, ``http-notebook`` port 80 → container port."""
+    port = DEFAULT_CONTAINER_PORT
+    containers = ((((nb.get("spec") or {}).get("template") or {}).get("spec")) or {}).get("containers") or []
+    if containers and containers[0].get("ports") is not None:
+        ports = containers[0]["ports"]
+        if ports:
+            port = int(ports[0].get("containerPort", DEFAULT_CONTAINER_PORT))
+    return {
+        "apiVersion": "v1", "kind": "Service",
+        "metadata": {"name": m.name(nb), "namespace": m.namespace(nb)},
+        "spec": {
+            "type": "ClusterIP",
+            "selector": {STATEFULSET_LABEL: m.name(nb)},
+            "ports": [{"name": "http-notebook", "port": DEFAULT_SERVING_PORT, "targetPort": port, "protocol": "TCP"}],
+        },
+    }
+
+
+def virtual_service_name(nb_name: str, namespace: str) -> str:
+    return f"notebook-{namespace}-{nb_name}"
+
+
+def generate_virtual_service(nb: dict, env: Mapping[str, str] = os.environ) -> dict:
+    """``generateVirtualService`` (:558-658)."""
+    name, ns = m.name(nb), m.namespace(nb)
+    prefix = f"/notebook/{ns}/{name}/"
+    ann = m.annotations(nb)
+    rewrite = ann.get(ANNOTATION_REWRITE_URI) or prefix
+    domain = env.get("CLUSTER_DOMAIN", "cluster.local") if "CLUSTER_DOMAIN" in env else "cluster.local"
+    service = f"{name}.{ns}.svc.{domain}"
+    headers = {}
+    raw = ann.get(ANNOTATION_HEADERS_REQUEST_SET)
+    if raw:
+        try:
+            parsed = json.loads(raw)
+            headers = {str(k): str(v) for k, v in parsed.items()} if isinstance(parsed, dict) else {}
+        except (ValueError, AttributeError):
+            headers = {}
+    return {
+        "apiVersion": "networking.istio.io/v1alpha3", "kind": "VirtualService",
+        "metadata": {"name": virtual_service_name(name, ns), "namespace": ns},
+        "spec": {
+            "hosts": [env.get("ISTIO_HOST") or "*"],
+            "gateways": [env.get("ISTIO_GATEWAY") or "kubeflow/kubeflow-gateway"],
+            "http": [{
+                "headers": {"request": {"set": headers}},
+                "match": [{"uri": {"prefix": prefix}}],
+                "rewrite": {"uri": rewrite},
+                "route": [{"destination": {"host": service, "port": {"number": DEFAULT_SERVING_PORT}}}],
+            }],
+        },
+    }
+
+
+# ------------------------------------------------------------------ status
+
+
+def create_notebook_status(nb: dict, sts: Optional[dict], pod: Optional[dict], now: Optional[str] = None) -> dict:
+    """``createNotebookStatus`` (:315-374)."""
+    status = {"conditions": [], "readyReplicas": int(((sts or {}).get("status") or {}).get("readyReplicas", 0) or 0),
+              "containerState": {}}
+    pst = (pod or {}).get("status") or {}
+    if not pst:
+        return status
+    cur_state = ((nb.get("status") or {}).get("containerState")) or {}
+    for cs in pst.get("containerStatuses") or []:
+        if cs.get("name") != m.name(nb):
+            continue
+        state = cs.get("state") or {}
+        if not state and not cur_state:
+            continue
+        status["containerState"] = deepcopy_json(state)
+        break
+    status["conditions"] = [pod_cond_to_notebook_cond(c, now) for c in pst.get("conditions") or []]
+    return status
+
+
+def _cond_key(c: dict):
+    return (c.get("type"), c.get("status"), c.get("reason"), c.get("message"))
+
+
+def merge_status_timestamps(old: dict, new: dict) -> dict:
+    """Keep the previous probe/transition stamps for conditions that did not change, so a
+    pod condition without timestamps does not turn every reconcile into a status write."""
+    prev = {_cond_key(c): c for c in (old or {}).get("conditions") or []}
+    for c in new.get("conditions") or []:
+        p = prev.get(_cond_key(c))
+        if p is not None:
+            for f in ("lastProbeTime", "lastTransitionTime"):
+                if p.get(f):
+                    c[f] = p[f]
+    return new
+
+
+# ------------------------------------------------------------------ reconciler
+
+
+class NotebookReconciler:
+    def __init__(self, client, reader, recorder, metrics=None, env: Optional[Mapping[str, str]] = None,
+                 unconditional_status: bool = False, owner_index: bool = True):
+        self.client = client
+        self.reader = reader
+        self.recorder = recorder
+        self.metrics = metrics
+        self.env = env if env is not None else os.environ
+        self.unconditional_status = unconditional_status  # reference-emulation knob
+        self.owner_index = owner_index
+        self.status_writes = 0
+
+    async def _find_statefulset(self, nb: dict, ns: str) -> Optional[dict]:
+        if self.owner_index:
+            items = await self.client.list(kinds.STATEFUL_SET, ns, owner_uid=m.uid(nb))
+        else:
+            items = await self.client.list(kinds.STATEFUL_SET, ns)
+        for sts in items:
+            if m.is_controlled_by(sts, nb):
+                return sts
+        return None
+
+    async def reconcile(self, req: Request) -> Result:
+        try:
+            nb = await self.client.get(NOTEBOOK_KIND, req.name, req.namespace)
+        except ApiError as e:
+            if is_not_found(e):
+                return Result()
+            raise
+        if m.is_deleting(nb):
+            return Result()
+
+        is_generate_name = len(m.name(nb)) > MAX_STATEFULSET_NAME_LENGTH
+        ss = generate_statefulset(nb, is_generate_name, self.env)
+        m.set_controller_reference(nb, ss)
+        found = await self._find_statefulset(nb, req.namespace)
+        just_created = False
+        if found is None:
+            if self.metrics:
+                self.metrics.notebook_creation.labels(req.namespace).inc()
+            try:
+                found = await self.client.create(ss)
+            except ApiError:
+                if self.metrics:
+                    self.metrics.notebook_fail_creation.labels(req.namespace).inc()
+                raise
+            just_created = True
+        # pod template labels follow when the replica count changes (:188-194)
+        if ss["spec"]["replicas"] != (found.get("spec") or {}).get("replicas"):
+            ftmpl = found["spec"].setdefault("template", {}).setdefault("metadata", {})
+            if ftmpl.get("labels") != ss["spec"]["template"]["metadata"]["labels"]:
+                ftmpl["labels"] = deepcopy_json(ss["spec"]["template"]["metadata"]["labels"])
+        if not just_created:
+            if is_generate_name:
+                # desired object has no name; keep the live identity
+                ss["metadata"]["name"] = m.name(found)
+            if copy_statefulset_fields(ss, found):
+                found = await self.client.update(found)
+
+        svc = generate_service(nb)
+        m.set_controller_reference(nb, svc)
+        try:
+            found_svc = await self.client.get(kinds.SERVICE, m.name(svc), req.namespace)
+            if copy_service_fields(svc, found_svc):
+                await self.client.update(found_svc)
+        except ApiError as e:
+            if not is_not_found(e):
+                raise
+            try:
+                await self.client.create(svc)
+            except ApiError as e2:
+                if not is_already_exists(e2):
+                    raise
+
+        if self.env.get("USE_ISTIO") == "true":
+            await self.reconcile_virtual_service(nb)
+
+        pod = await self.client.get_or_none(kinds.POD, f"{m.name(found)}-0", req.namespace)
+
+        status = create_notebook_status(nb, found, pod)
+        old_status = nb.get("status") or {}
+        if self.unconditional_status:
+            nb["status"] = status
+            self.status_writes += 1
+            await self.client.update_status(nb)
+        else:
+            merge_status_timestamps(old_status, status)
+            if status != old_status:
+                nb["status"] = status
+                self.status_writes += 1
+                await self.client.update_status(nb)
+
+        ann = m.annotations(nb)
+        if ann.get(ANNOTATION_NOTEBOOK_RESTART) == "true":
+            log.info("restart annotation set on %s", req)
+            pod = await self.client.get_or_none(kinds.POD, f"{m.name(nb)}-0", req.namespace)
+            if pod is not None:
+                try:
+                    await self.client.delete(pod)
+                except ApiError as e:
+                    if not is_not_found(e):
+                        raise
+            m.ensure_annotations(nb).pop(ANNOTATION_NOTEBOOK_RESTART, None)
+            await self.client.update(nb)
+        return Result()
+
+    async def reconcile_virtual_service(self, nb: dict) -> None:
+        vs = generate_virtual_service(nb, self.env)
+        m.set_controller_reference(nb, vs)
+        found = await self.client.get_or_none(kinds.VIRTUAL_SERVICE, m.name(vs), m.namespace(nb))
+        if found is None:
+            await self.client.create(vs)
+            return
+        if copy_virtual_service(vs, found):
+            await self.client.update(found)
+
+    # -------------------------------------------------------------- wiring
+
+    def setup_with_manager(self, mgr, max_concurrent: Optional[int] = None):
+        """``SetupWithManager`` (:778-826): For Notebook, Owns STS/Service, Pods by label."""
+
+        def map_pod(pod: dict):
+            return [Request(m.namespace(pod), m.labels(pod)[NOTEBOOK_NAME_LABEL])]
+
+        def pod_is_labeled(etype, obj, old):
+            return NOTEBOOK_NAME_LABEL in m.labels(obj)
+
+        b = (mgr.builder().named("notebook-controller").for_(NOTEBOOK_KIND)
+             .owns(kinds.STATEFUL_SET).owns(kinds.SERVICE)
+             .watches(kinds.POD, map_pod, [pod_is_labeled]))
+        if self.env.get("USE_ISTIO") == "true":
+            b.owns(kinds.VIRTUAL_SERVICE)
+        if max_concurrent is not None:
+            b.with_options(max_concurrent_reconciles=max_concurrent)
+        return b.complete(self)
+
+
+# ------------------------------------------------------------------ event re-emission
+
+
+def nb_name_from_involved_object(reader, obj_ref: dict) -> Optional[str]:
+    """``nbNameFromInvolvedObject`` (:705-729)."""
+    kind, name, ns = obj_ref.get("kind"), obj_ref.get("name", ""), obj_ref.get("namespace", "")
+    if kind == "StatefulSet":
+        return name
+    if kind == "Pod":
+        pod = reader.get(kinds.POD, name, ns)
+        if pod is not None:
+            return m.labels(pod).get(NOTEBOOK_NAME_LABEL)
+    return None
+
+
+class NotebookEventReemitter:
+    """Re-emits Pod/StatefulSet events onto their Notebook as ``Reissued from <kind>/<name>: <msg>``."""
+
+    def __init__(self, client, reader, recorder):
+        self.client = client
+        self.reader = reader
+        self.recorder = recorder
+        self.reemitted = 0
+
+    def _relevant(self, ev: dict) -> bool:
+        inv = ev.get("involvedObject") or {}
+        if inv.get("kind") not in ("Pod", "StatefulSet"):
+            return False
+        nb_name = nb_name_from_involved_object(self.reader, inv)
+        if not nb_name:
+            return False
+        return self.reader.get(NOTEBOOK_KIND, nb_name, m.namespace(ev)) is not None
+
+    async def reconcile(self, req: Request) -> Result:
+        ev = await self.client.get_or_none(kinds.EVENT, req.name, req.namespace)
+        if ev is None:
+            return Result()
+        inv = ev.get("involvedObject") or {}
+        nb_name = nb_name_from_involved_object(self.reader, inv)
+        if not nb_name:
+            return Result()
+        nb = await self.client.get_or_none(NOTEBOOK_KIND, nb_name, req.namespace)
+        if nb is None:
+            return Result()
+        self.reemitted += 1
+        self.recorder.event(nb, ev.get("type", "Normal"), ev.get("reason", ""),
+                            f"Reissued from {str(inv.get('kind', '')).lower()}/{inv.get('name', '')}: {ev.get('message', '')}")
+        return Result()
+
+    def setup_with_manager(self, mgr, max_concurrent: Optional[int] = None):
+        pred = pred_funcs(create=lambda o: self._relevant(o), update=lambda o, old: self._relevant(o),
+                          delete=lambda o: False)
+        b = mgr.builder().named("notebook-events").for_(kinds.EVENT, [pred])
+        if max_concurrent is not None:
+            b.with_options(max_concurrent_reconciles=max_concurrent)
+        return b.complete(self)

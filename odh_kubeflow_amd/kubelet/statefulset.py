@@ -1,0 +1,126 @@
+"""Fake kube-controller-manager StatefulSet controller.
+
+envtest runs no controllers (``kf/controllers/notebook_controller_bdd_test.go:73-76``);
+to measure create→Ready latency without a cluster ("fake
+kubelet") this turns StatefulSets into ordinal pods ``<sts>-<i>``, rolls pods whose
+template changed, scales down to ``replicas``, and maintains ``status``
+(``replicas``/``readyReplicas``/``currentReplicas``/``availableReplicas``/
+``observedGeneration``) from the pods it owns.
+"""
+
+from __future__ import annotations
+
+import hashlib
+import json
+import logging
+from typing import Optional
+
+from ..models import kinds
+from ..models import meta as m
+from ..models.errors import ApiError, is_already_exists, is_not_found
+from ..runtime.controller import Request, Result, enqueue_for_owner
+from ..utils.objutil import deepcopy_json
+
+log = logging.getLogger(__name__)
+
+REVISION_LABEL = "controller-revision-hash"
+
+
+def template_hash(sts: dict) -> str:
+    tmpl = (sts.get("spec") or {}).get("template") or {}
+    h = hashlib.sha1(json.dumps(tmpl, sort_keys=True, separators=(",", ":")).encode()).hexdigest()[:10]
+    return f"{m.name(sts)}-{h}"
+
+
+def pod_is_ready(pod: dict) -> bool:
+    for c in ((pod.get("status") or {}).get("conditions") or []):
+        if c.get("type") == "Ready":
+            return c.get("status") == "True"
+    return False
+
+
+class StatefulSetController:
+    def __init__(self, client, reader, recorder):
+        self.client = client
+        self.reader = reader
+        self.recorder = recorder
+
+    def _pod_for(self, sts: dict, ordinal: int, rev: str) -> dict:
+        tmpl = (sts.get("spec") or {}).get("template") or {}
+        md = deepcopy_json(tmpl.get("metadata") or {})
+        md["name"] = f"{m.name(sts)}-{ordinal}"
+        md["namespace"] = m.namespace(sts)
+        labels = md.setdefault("labels", {})
+        labels[REVISION_LABEL] = rev
+        labels["statefulset.kubernetes.io/pod-name"] = md["name"]
+        labels["apps.kubernetes.io/pod-index"] = str(ordinal)
+        md.setdefault("annotations", {})
+        pod = {"apiVersion": "v1", "kind": "Pod", "metadata": md, "spec": deepcopy_json(tmpl.get("spec") or {}),
+               "status": {"phase": "Pending"}}
+        pod["spec"]["hostname"] = md["name"]
+        m.set_controller_reference(sts, pod)
+        return pod
+
+    async def reconcile(self, req: Request) -> Result:
+        sts = await self.client.get_or_none(kinds.STATEFUL_SET, req.name, req.namespace)
+        if sts is None or m.is_deleting(sts):
+            return Result()
+        replicas = int((sts.get("spec") or {}).get("replicas", 1) or 0)
+        rev = template_hash(sts)
+        pods = [p for p in self.reader.list(kinds.POD, req.namespace, owner_uid=m.uid(sts)) if m.is_controlled_by(p, sts)]
+        by_ord = {}
+        for p in pods:
+            try:
+                by_ord[int(m.name(p).rsplit("-", 1)[1])] = p
+            except (IndexError, ValueError):
+                continue
+        for i in range(replicas):
+            p = by_ord.get(i)
+            if p is None:
+                try:
+                    await self.client.create(self._pod_for(sts, i, rev))
+                    self.recorder.event(sts, "Normal", "SuccessfulCreate",
+                                        f"create Pod {m.name(sts)}-{i} in StatefulSet {m.name(sts)} successful")
+                except ApiError as e:
+                    if not is_already_exists(e):
+                        raise
+            elif m.labels(p).get(REVISION_LABEL) != rev and not m.is_deleting(p):
+                # RollingUpdate: replace pods built from an outdated template
+                await self._delete_pod(sts, p)
+        for i, p in by_ord.items():
+            if i >= replicas and not m.is_deleting(p):
+                await self._delete_pod(sts, p)
+        await self._update_status(sts, rev)
+        return Result()
+
+    async def _delete_pod(self, sts: dict, p: dict) -> None:
+        try:
+            await self.client.delete(kinds.POD, m.name(p), m.namespace(p))
+            self.recorder.event(sts, "Normal", "SuccessfulDelete",
+                                f"delete Pod {m.name(p)} in StatefulSet {m.name(sts)} successful")
+        except ApiError as e:
+            if not is_not_found(e):
+                raise
+
+    async def _update_status(self, sts: dict, rev: str) -> None:
+        pods = [p for p in self.reader.list(kinds.POD, m.namespace(sts), owner_uid=m.uid(sts))
+                if m.is_controlled_by(p, sts) and not m.is_deleting(p)]
+        ready = sum(1 for p in pods if pod_is_ready(p))
+        current = sum(1 for p in pods if m.labels(p).get(REVISION_LABEL) == rev)
+        st = {"replicas": len(pods), "readyReplicas": ready, "currentReplicas": current, "updatedReplicas": current,
+              "availableReplicas": ready, "currentRevision": rev, "updateRevision": rev,
+              "observedGeneration": (sts.get("metadata") or {}).get("generation", 1)}
+        if (sts.get("status") or {}) != st:
+            sts["status"] = st
+            try:
+                await self.client.update_status(sts)
+            except ApiError as e:
+                if not is_not_found(e):
+                    raise
+
+    def setup_with_manager(self, mgr, max_concurrent: Optional[int] = None):
+        b = (mgr.builder().named("statefulset").for_(kinds.STATEFUL_SET)
+             .watches(kinds.POD, enqueue_for_owner("StatefulSet", "apps")))
+        if max_concurrent:
+            b.with_options(max_concurrent_reconciles=max_concurrent)
+        return b.complete(self)

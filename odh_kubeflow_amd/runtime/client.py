@@ -1,0 +1,239 @@
+"""Client interfaces (the ``client.Client`` / ``client.Reader`` analogues) and the
+in-process implementation over :class:`~odh_kubeflow_amd.apiserver.store.ObjectStore`.
+
+Two access paths, as in controller-runtime:
+
+* :class:`Reader` — synchronous, read-only, zero-copy reads from the cache.  Event map
+  functions and predicates use it (e.g. ``predNBEvents`` at
+  ``kf/controllers/notebook_controller.go:755-775`` does a Pod and a Notebook GET per
+  event).
+* :class:`Client` — async CRUD.  Reads go through the cache unless the kind is listed in
+  ``uncached`` (the odh manager disables the cache for ConfigMaps and Secrets,
+  ``odh/main.go:178-185``).  Like controller-runtime, write calls refresh the caller's
+  object in place with the server response (new ``resourceVersion`` etc.).
+"""
+
+from __future__ import annotations
+
+import abc
+from typing import Any, Callable, Iterable, List, Optional, Sequence
+
+from ..apiserver.store import ObjectStore
+from ..models.scheme import SCHEME, ResourceInfo
+from ..utils.objutil import deepcopy_json
+
+WatchCallback = Callable[[str, dict, Optional[dict]], None]
+
+
+def _version_of(ref) -> Optional[str]:
+    if isinstance(ref, str):
+        api_version = ref.rpartition("/")[0]
+        return api_version.rpartition("/")[2] if api_version else None
+    if isinstance(ref, dict):
+        return ref.get("apiVersion", "").rpartition("/")[2] or None
+    return None
+
+
+def _refresh(target: Optional[dict], new: dict) -> dict:
+    if isinstance(target, dict) and target is not new:
+        target.clear()
+        target.update(new)
+        return target
+    return new
+
+
+class Reader(abc.ABC):
+    """Synchronous cache reader; returned objects are shared and MUST NOT be mutated."""
+
+    @abc.abstractmethod
+    def get(self, kind, name: str, namespace: Optional[str] = None) -> Optional[dict]:
+        ...
+
+    @abc.abstractmethod
+    def list(self, kind, namespace: Optional[str] = None, labels=None, fields: Optional[str] = None,
+             owner_uid: Optional[str] = None) -> List[dict]:
+        ...
+
+
+class EventSource(abc.ABC):
+    """Watch subscription provider for controllers (store or informer backed)."""
+
+    @abc.abstractmethod
+    def subscribe(self, kind, callback: WatchCallback, namespace: Optional[str] = None) -> Callable[[], None]:
+        ...
+
+    async def wait_synced(self, kinds: Iterable) -> None:  # pragma: no cover - trivial default
+        return None
+
+
+class Client(abc.ABC):
+    scheme = SCHEME
+
+    @abc.abstractmethod
+    async def get(self, kind, name: str, namespace: Optional[str] = None) -> dict:
+        ...
+
+    @abc.abstractmethod
+    async def list(self, kind, namespace: Optional[str] = None, labels=None, fields: Optional[str] = None,
+                   owner_uid: Optional[str] = None) -> List[dict]:
+        ...
+
+    @abc.abstractmethod
+    async def create(self, obj: dict) -> dict:
+        ...
+
+    @abc.abstractmethod
+    async def update(self, obj: dict) -> dict:
+        ...
+
+    @abc.abstractmethod
+    async def update_status(self, obj: dict) -> dict:
+        ...
+
+    @abc.abstractmethod
+    async def patch(self, obj_or_kind, patch: Any, patch_type: str = "merge", name: Optional[str] = None,
+                    namespace: Optional[str] = None, subresource: Optional[str] = None) -> dict:
+        ...
+
+    @abc.abstractmethod
+    async def delete(self, obj_or_kind, name: Optional[str] = None, namespace: Optional[str] = None,
+                     preconditions: Optional[dict] = None, propagation: str = "Background") -> Optional[dict]:
+        ...
+
+    async def get_or_none(self, kind, name: str, namespace: Optional[str] = None) -> Optional[dict]:
+        from ..models.errors import is_not_found
+
+        try:
+            return await self.get(kind, name, namespace)
+        except Exception as e:
+            if is_not_found(e):
+                return None
+            raise
+
+
+class StoreReader(Reader):
+    """Zero-copy reads straight from the in-process store (an always-synced cache)."""
+
+    def __init__(self, store: ObjectStore):
+        self.store = store
+
+    def get(self, kind, name, namespace=None):
+        return self.store.peek(kind, name, namespace)
+
+    def list(self, kind, namespace=None, labels=None, fields=None, owner_uid=None):
+        return self.store.list_nocopy(kind, namespace, labels, fields, owner_uid)
+
+
+class StoreEventSource(EventSource):
+    def __init__(self, store: ObjectStore):
+        self.store = store
+
+    def subscribe(self, kind, callback, namespace=None):
+        return self.store.watch(kind, callback, namespace=namespace)
+
+
+class InProcessClient(Client):
+    """Client talking to an in-process :class:`ObjectStore`.
+
+    ``user`` is recorded for audit/debugging only; the in-process path does no authz.
+    """
+
+    def __init__(self, store: ObjectStore, user: str = "system:admin"):
+        self.store = store
+        self.user = user
+
+    async def get(self, kind, name, namespace=None):
+        return await self.store.get(kind, name, namespace, version=_version_of(kind))
+
+    async def list(self, kind, namespace=None, labels=None, fields=None, owner_uid=None):
+        items, _ = await self.store.list(kind, namespace, labels, fields, version=_version_of(kind),
+                                         owner_uid=owner_uid)
+        return items
+
+    async def create(self, obj):
+        return _refresh(obj, await self.store.create(obj))
+
+    async def update(self, obj):
+        return _refresh(obj, await self.store.update(obj))
+
+    async def update_status(self, obj):
+        return _refresh(obj, await self.store.update(obj, subresource="status"))
+
+    async def patch(self, obj_or_kind, patch, patch_type="merge", name=None, namespace=None, subresource=None):
+        if isinstance(obj_or_kind, dict):
+            kind = obj_or_kind
+            name = name or obj_or_kind["metadata"]["name"]
+            namespace = namespace or obj_or_kind["metadata"].get("namespace")
+        else:
+            kind = obj_or_kind
+        res = await self.store.patch(kind, name, namespace, patch, patch_type, subresource)
+        v = _version_of(kind)
+        if v:
+            info = SCHEME.resolve(kind)
+            res["apiVersion"] = info.api_version(v)
+        if isinstance(obj_or_kind, dict):
+            return _refresh(obj_or_kind, res)
+        return res
+
+    async def delete(self, obj_or_kind, name=None, namespace=None, preconditions=None, propagation="Background"):
+        if isinstance(obj_or_kind, dict):
+            name = name or obj_or_kind["metadata"]["name"]
+            namespace = namespace or obj_or_kind["metadata"].get("namespace")
+        return await self.store.delete(obj_or_kind, name, namespace, preconditions, propagation)
+
+
+class CachedClient(Client):
+    """Reads from a :class:`Reader` (copying), writes through a backing client.
+
+    Kinds in ``uncached`` are read live from the backing client, exactly like
+    ``client.CacheOptions.DisableFor``.
+    """
+
+    def __init__(self, reader: Reader, writer: Client, uncached: Sequence = ()):
+        self.reader = reader
+        self.writer = writer
+        self.uncached = {SCHEME.resolve(k).key for k in uncached}
+
+    def _live(self, kind) -> bool:
+        return SCHEME.resolve(kind).key in self.uncached
+
+    async def get(self, kind, name, namespace=None):
+        if self._live(kind):
+            return await self.writer.get(kind, name, namespace)
+        o = self.reader.get(kind, name, namespace)
+        if o is None:
+            from ..models.errors import NotFound
+
+            info = SCHEME.resolve(kind)
+            raise NotFound(info.plural if not info.group else f"{info.plural}.{info.group}", name)
+        o = deepcopy_json(o)
+        v = _version_of(kind)
+        if v:
+            o["apiVersion"] = SCHEME.resolve(kind).api_version(v)
+        return o
+
+    async def list(self, kind, namespace=None, labels=None, fields=None, owner_uid=None):
+        if self._live(kind) and owner_uid is None:
+            return await self.writer.list(kind, namespace, labels, fields)
+        items = [deepcopy_json(o) for o in self.reader.list(kind, namespace, labels, fields, owner_uid)]
+        v = _version_of(kind)
+        if v:
+            av = SCHEME.resolve(kind).api_version(v)
+            for o in items:
+                o["apiVersion"] = av
+        return items
+
+    async def create(self, obj):
+        return await self.writer.create(obj)
+
+    async def update(self, obj):
+        return await self.writer.update(obj)
+
+    async def update_status(self, obj):
+        return await self.writer.update_status(obj)
+
+    async def patch(self, obj_or_kind, patch, patch_type="merge", name=None, namespace=None, subresource=None):
+        return await self.writer.patch(obj_or_kind, patch, patch_type, name, namespace, subresource)
+
+    async def delete(self, obj_or_kind, name=None, namespace=None, preconditions=None, propagation="Background"):
+        return await self.writer.delete(obj_or_kind, name, namespace, preconditions, propagation)

@@ -1,0 +1,202 @@
+"""Controller manager (``ctrl.Manager`` analogue).
+
+Owns the client/cache/event-source triple, the controllers and other runnables, the
+Prometheus registry, the ``/metrics`` and ``/healthz``/``/readyz`` servers
+(``kf/main.go:125-133``, ``odh/main.go:231-238``) and optional leader election
+(``LeaderElectionID`` ``kubeflow-notebook-controller`` / ``odh-notebook-controller``).
+Controllers only start once leadership is held; runnables that do not need
+leadership (the webhook server) start immediately, as in controller-runtime.
+"""
+
+from __future__ import annotations
+
+import asyncio
+import logging
+import time
+from typing import Callable, Dict, List, Optional, Sequence
+
+from prometheus_client import CollectorRegistry, generate_latest
+
+from ..apiserver.store import ObjectStore
+from .client import CachedClient, Client, EventSource, InProcessClient, Reader, StoreEventSource, StoreReader
+from .controller import DEFAULT_MAX_CONCURRENT_RECONCILES, Builder, Controller
+from .events import EventRecorder
+from .metrics import RuntimeMetrics
+
+log = logging.getLogger(__name__)
+
+
+class Manager:
+    def __init__(self, client: Client, reader: Reader, source: EventSource, name: str = "manager",
+                 registry: Optional[CollectorRegistry] = None,
+                 default_max_concurrent: int = DEFAULT_MAX_CONCURRENT_RECONCILES,
+                 leader_elector=None, metrics_addr: Optional[str] = None, probe_addr: Optional[str] = None):
+        self.name = name
+        self.client = client
+        self.reader = reader
+        self.source = source
+        self.registry = registry or CollectorRegistry()
+        self.runtime_metrics = RuntimeMetrics(self.registry)
+        self.default_max_concurrent = default_max_concurrent
+        self.controllers: List[Controller] = []
+        self.runnables: List = []
+        self.leader_runnables: List = []
+        self.healthz: Dict[str, Callable[[], bool]] = {}
+        self.readyz: Dict[str, Callable[[], bool]] = {}
+        self.leader_elector = leader_elector
+        self.metrics_addr = metrics_addr
+        self.probe_addr = probe_addr
+        self._recorders: Dict[str, EventRecorder] = {}
+        self._servers: List = []
+        self._started = False
+        self._leader_task: Optional[asyncio.Task] = None
+        self.elected = asyncio.Event() if False else None  # created lazily inside the loop
+
+    # ------------------------------------------------------------------ construction
+
+    @classmethod
+    def in_process(cls, store: ObjectStore, name: str = "manager", uncached: Sequence = (), **kw) -> "Manager":
+        reader = StoreReader(store)
+        writer = InProcessClient(store, user=f"system:serviceaccount:{name}")
+        client = CachedClient(reader, writer, uncached)
+        return cls(client, reader, StoreEventSource(store), name=name, **kw)
+
+    def builder(self) -> Builder:
+        return Builder(self)
+
+    def add_controller(self, c: Controller) -> None:
+        self.controllers.append(c)
+
+    def add(self, runnable, needs_leader: bool = True) -> None:
+        (self.leader_runnables if needs_leader else self.runnables).append(runnable)
+
+    def add_healthz_check(self, name: str, fn: Callable[[], bool] = lambda: True) -> None:
+        self.healthz[name] = fn
+
+    def add_readyz_check(self, name: str, fn: Callable[[], bool] = lambda: True) -> None:
+        self.readyz[name] = fn
+
+    def get_event_recorder_for(self, component: str) -> EventRecorder:
+        r = self._recorders.get(component)
+        if r is None:
+            r = self._recorders[component] = EventRecorder(self.client, component)
+        return r
+
+    # ------------------------------------------------------------------ lifecycle
+
+    async def start(self) -> None:
+        if self._started:
+            return
+        self._started = True
+        self.elected = asyncio.Event()
+        await self._start_servers()
+        for r in self.runnables:
+            await r.start()
+        if self.leader_elector is None:
+            await self._become_leader()
+        else:
+            self._leader_task = asyncio.ensure_future(self.leader_elector.run(self._become_leader, self._lost_leader))
+
+    async def _become_leader(self) -> None:
+        for c in self.controllers:
+            await c.start(self.source)
+        for r in self.leader_runnables:
+            await r.start()
+        self.elected.set()
+
+    async def _lost_leader(self) -> None:
+        log.error("%s: leader election lost; stopping controllers", self.name)
+        for c in self.controllers:
+            await c.stop()
+
+    async def stop(self) -> None:
+        if self._leader_task is not None:
+            self._leader_task.cancel()
+            try:
+                await self._leader_task
+            except (asyncio.CancelledError, Exception):
+                pass
+            if self.leader_elector is not None:
+                await self.leader_elector.release()
+        for c in self.controllers:
+            await c.stop()
+        for r in self.leader_runnables + self.runnables:
+            try:
+                await r.stop()
+            except Exception:
+                log.exception("runnable stop failed")
+        for rec in self._recorders.values():
+            await rec.flush()
+        for s in self._servers:
+            await s.cleanup()
+        self._servers.clear()
+        self._started = False
+
+    async def run_until(self, stop: asyncio.Event) -> None:
+        await self.start()
+        try:
+            await stop.wait()
+        finally:
+            await self.stop()
+
+    # ------------------------------------------------------------------ test / bench helpers
+
+    def idle(self) -> bool:
+        return all(c.idle() for c in self.controllers)
+
+    async def wait_idle(self, timeout: float = 10.0, settle: float = 0.0) -> bool:
+        """Wait until every controller queue is drained (ignores delayed requeues beyond ``timeout``)."""
+        deadline = time.monotonic() + timeout
+        while time.monotonic() < deadline:
+            busy = any(len(c.queue) or c.queue._processing or c.active for c in self.controllers)
+            if not busy:
+                for rec in self._recorders.values():
+                    await rec.flush()
+                if settle:
+                    await asyncio.sleep(settle)
+                    if not any(len(c.queue) or c.active for c in self.controllers):
+                        return True
+                    continue
+                return True
+            await asyncio.sleep(0.002)
+        return False
+
+    def reconcile_count(self) -> int:
+        return sum(c.reconciles for c in self.controllers)
+
+    # ------------------------------------------------------------------ servers
+
+    async def _start_servers(self) -> None:
+        from aiohttp import web
+
+        async def serve(addr: str, app: web.Application) -> None:
+            host, _, port = addr.rpartition(":")
+            runner = web.AppRunner(app, access_log=None)
+            await runner.setup()
+            site = web.TCPSite(runner, host or "0.0.0.0", int(port))
+            await site.start()
+            self._servers.append(runner)
+
+        if self.metrics_addr and self.metrics_addr not in ("0", ""):
+            app = web.Application()
+
+            async def metrics(_req):
+                return web.Response(body=generate_latest(self.registry), content_type="text/plain", charset="utf-8")
+
+            app.router.add_get("/metrics", metrics)
+            await serve(self.metrics_addr, app)
+        if self.probe_addr and self.probe_addr not in ("0", ""):
+            app = web.Application()
+
+            def checker(checks):
+                async def h(_req):
+                    bad = [n for n, fn in checks.items() if not fn()]
+                    if bad:
+                        return web.Response(status=500, text="\n".join(f"[-]{n} failed" for n in bad))
+                    return web.Response(text="ok")
+
+                return h
+
+            app.router.add_get("/healthz", checker(self.healthz))
+            app.router.add_get("/readyz", checker(self.readyz))
+            await serve(self.probe_addr, app)

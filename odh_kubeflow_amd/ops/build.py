@@ -1,0 +1,76 @@
+"""In-tree build of the native libraries (``python -m odh_kubeflow_amd.ops.build``).
+
+* ``libodh_gpu_probe.so``   — HIP kernels for gfx950 (``hipcc --offload-arch=gfx950``),
+  C ABI, loaded with ctypes after ``import torch`` so it shares torch's HIP runtime
+  (both resolve ``libamdhip64.so.7``).
+* ``libodh_gpu_telemetry.so`` — host C++ amdgpu sysfs sampler (g++, pthreads).
+
+Both land in ``odh_kubeflow_amd/ops/_lib/`` so they travel with the repo snapshot to
+the GPU box (no JIT cache under ``~/.cache``).  A library is rebuilt only when its
+source is newer than the ``.so``.
+"""
+
+from __future__ import annotations
+
+import os
+import shutil
+import subprocess
+import sys
+from typing import Dict, List
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+CSRC = os.path.join(HERE, "csrc")
+LIBDIR = os.path.join(HERE, "_lib")
+ARCH = os.environ.get("ODH_GPU_ARCH", "gfx950")
+ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
+
+
+def _hipcc() -> str:
+    p = os.path.join(ROCM, "bin", "hipcc")
+    return p if os.path.exists(p) else (shutil.which("hipcc") or p)
+
+
+def targets() -> Dict[str, dict]:
+    return {
+        "libodh_gpu_probe.so": {
+            "src": [os.path.join(CSRC, "gpu_probe.hip")],
+            "cmd": lambda src, out: [_hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-shared", "-fPIC",
+                                     *src, "-o", out],
+        },
+        "libodh_gpu_telemetry.so": {
+            "src": [os.path.join(CSRC, "gpu_telemetry.cpp")],
+            "cmd": lambda src, out: [os.environ.get("CXX", "g++"), "-O2", "-std=c++17", "-shared", "-fPIC",
+                                     "-pthread", "-Wall", *src, "-o", out],
+        },
+    }
+
+
+def lib_path(name: str) -> str:
+    return os.path.join(LIBDIR, name)
+
+
+def _stale(out: str, srcs: List[str]) -> bool:
+    if not os.path.exists(out):
+        return True
+    t = os.path.getmtime(out)
+    return any(os.path.getmtime(s) > t for s in srcs)
+
+
+def build(force: bool = False, verbose: bool = True) -> Dict[str, str]:
+    os.makedirs(LIBDIR, exist_ok=True)
+    built = {}
+    for name, spec in targets().items():
+        out = lib_path(name)
+        if force or _stale(out, spec["src"]):
+            tmp = out + ".tmp"
+            cmd = spec["cmd"](spec["src"], tmp)
+            if verbose:
+                print("[build]", " ".join(cmd), flush=True)
+            subprocess.run(cmd, check=True)
+            os.replace(tmp, out)
+        built[name] = out
+    return built
+
+
+if __name__ == "__main__":
+    build(force="--force" in sys.argv)

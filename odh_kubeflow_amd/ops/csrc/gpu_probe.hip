@@ -1,0 +1,319 @@
+// MI355X (gfx950) node-agent kernels: notebook start-up probe and synthetic GPU load.
+//
+// The reference control plane (harshad16/odh-kubeflow) never touches the accelerator:
+// GPU support there is PodSpec passthrough (kf/controllers/notebook_controller.go:469).
+// On an 8×MI355X node the node agent additionally proves that the GPU it is about to
+// hand to a notebook is healthy before the pod is reported Ready, and drives synthetic
+// load for the GPU-busy culler.  Everything here is written for CDNA4 directly:
+//
+//  * odh_probe_gemm  — bf16 GEMM on the matrix cores (v_mfma_f32_32x32x16_bf16),
+//    128×128 tile per 256-thread workgroup (4 waves, 2×2 of 32×32 MFMA tiles each),
+//    K staged through LDS in 32-deep double-buffered tiles with an XOR swizzle that
+//    makes the 16-lane ds_read_b128 groups conflict-free, and an XCD-aware blockIdx
+//    remap so the tiles of one XCD share A panels in that XCD's L2.  Every workgroup
+//    records the XCD (HW_REG_XCC_ID) it ran on, so a verification failure is pinned to
+//    the chiplet that produced it.
+//  * odh_probe_fill / odh_probe_verify — exact integer-valued operands whose product
+//    has a closed form (period 35 in k), so the check needs no host reference and no
+//    second GEMM: every element is compared bit-exactly on the GPU.
+//  * odh_hbm_write / odh_hbm_check — 16 B/lane streaming pattern write + verify over a
+//    resident HBM3E buffer (bandwidth and bit errors in one pass).
+//  * odh_busy — MFMA issue loop with 4 independent accumulators (drives gfx activity
+//    for the culler's amdgpu signal under synthetic load).
+//
+// C ABI only (loaded with ctypes after torch, sharing torch's libamdhip64.so.7).
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
+typedef __attribute__((ext_vector_type(16))) float f32x16;
+typedef __attribute__((ext_vector_type(4))) unsigned u32x4;
+
+namespace {
+
+constexpr int BM = 128;
+constexpr int BN = 128;
+constexpr int BK = 32;           // bf16 elements per K tile = 4 × 16-byte chunks per row
+constexpr int CH = BK / 8;       // 16-byte chunks per tile row
+constexpr int THREADS = 256;
+
+__device__ __forceinline__ unsigned xcc_id() {
+  unsigned x;
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(x));
+  return x & 7u;
+}
+
+// chunk c of tile row r lives at slot c ^ ((r >> 2) & 3): the 16 rows read by one
+// ds_read_b128 lane group then hit 16 distinct 16-byte slots of the 256-byte bank row.
+__device__ __forceinline__ int swz(int r, int c) { return r * CH + (c ^ ((r >> 2) & 3)); }
+
+__global__ __launch_bounds__(THREADS, 2) void gemm_bf16_kernel(
+    const uint4* __restrict__ A, const uint4* __restrict__ Bt, float* __restrict__ C,
+    int M, int N, int K, int* __restrict__ tile_xcd, int* __restrict__ xcd_blocks) {
+  __shared__ uint4 sA[2][BM * CH];
+  __shared__ uint4 sB[2][BN * CH];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int w = tid >> 6;
+  const int wm = w >> 1, wn = w & 1;
+  const int tiles_n = N / BN;
+  const int nwg = gridDim.x;
+  int bid = blockIdx.x;
+  if ((nwg & 7) == 0) bid = (bid & 7) * (nwg >> 3) + (bid >> 3);  // XCD-contiguous tiles
+  const int tm = bid / tiles_n;
+  const int tn = bid - tm * tiles_n;
+
+  if (tid == 0) {
+    const unsigned x = xcc_id();
+    if (tile_xcd) tile_xcd[bid] = (int)x;
+    if (xcd_blocks) atomicAdd(&xcd_blocks[x], 1);
+  }
+
+  const size_t kch = (size_t)(K / 8);  // 16-byte chunks per global row
+  const uint4* Ag = A + (size_t)tm * BM * kch;
+  const uint4* Bg = Bt + (size_t)tn * BN * kch;
+  const int r0 = tid >> 2, c0 = tid & 3, r1 = r0 + 64;
+
+  uint4 ra0, ra1, rb0, rb1;
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  const int nkt = K / BK;
+  {
+    ra0 = Ag[r0 * kch + c0];
+    ra1 = Ag[r1 * kch + c0];
+    rb0 = Bg[r0 * kch + c0];
+    rb1 = Bg[r1 * kch + c0];
+    sA[0][swz(r0, c0)] = ra0;
+    sA[0][swz(r1, c0)] = ra1;
+    sB[0][swz(r0, c0)] = rb0;
+    sB[0][swz(r1, c0)] = rb1;
+  }
+  __syncthreads();
+
+  const int lr = lane & 31, lh = lane >> 5;
+  for (int kt = 0; kt < nkt; ++kt) {
+    const int cur = kt & 1;
+    const bool more = kt + 1 < nkt;
+    if (more) {  // issue next tile's global loads before this tile's LDS reads + MFMAs
+      const size_t kc = (size_t)(kt + 1) * CH + c0;
+      ra0 = Ag[r0 * kch + kc];
+      ra1 = Ag[r1 * kch + kc];
+      rb0 = Bg[r0 * kch + kc];
+      rb1 = Bg[r1 * kch + kc];
+    }
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const int c = 2 * s + lh;  // lane half h holds k = 16s + 8h .. +7
+      bf16x8 af[2], bf[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int row = wm * 64 + i * 32 + lr;
+        af[i] = __builtin_bit_cast(bf16x8, sA[cur][swz(row, c)]);
+        const int col = wn * 64 + i * 32 + lr;
+        bf[i] = __builtin_bit_cast(bf16x8, sB[cur][swz(col, c)]);
+      }
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bf[j], acc[i][j], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+    }
+    if (more) {
+      const int nxt = cur ^ 1;
+      sA[nxt][swz(r0, c0)] = ra0;
+      sA[nxt][swz(r1, c0)] = ra1;
+      sB[nxt][swz(r0, c0)] = rb0;
+      sB[nxt][swz(r1, c0)] = rb1;
+    }
+    __syncthreads();
+  }
+
+  // C/D map of 32x32x16: col = lane & 31, row = (reg & 3) + 8 * (reg >> 2) + 4 * (lane >> 5)
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int col = tn * BN + wn * 64 + j * 32 + lr;
+      const int rbase = tm * BM + wm * 64 + i * 32 + 4 * lh;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = rbase + (r & 3) + 8 * (r >> 2);
+        C[(size_t)row * N + col] = acc[i][j][r];
+      }
+    }
+}
+
+__device__ __forceinline__ uint16_t small_int_bf16(int v) {
+  // exact for |v| < 256: take the high half of the f32 bit pattern
+  return (uint16_t)(__float_as_uint((float)v) >> 16);
+}
+
+// A[i][k] = ((3i + 7k) mod 5) - 2 ; Bt[j][k] = ((11j + 5k) mod 7) - 3   (asymmetric in i/j)
+__global__ void fill_kernel(uint16_t* __restrict__ A, uint16_t* __restrict__ Bt, int M, int N, int K) {
+  const size_t na = (size_t)M * K, nb = (size_t)N * K;
+  for (size_t idx = blockIdx.x * (size_t)blockDim.x + threadIdx.x; idx < na + nb;
+       idx += (size_t)gridDim.x * blockDim.x) {
+    if (idx < na) {
+      const int i = (int)(idx / K), k = (int)(idx % K);
+      A[idx] = small_int_bf16((int)(((long)i * 3 + (long)k * 7) % 5) - 2);
+    } else {
+      const size_t o = idx - na;
+      const int j = (int)(o / K), k = (int)(o % K);
+      Bt[o] = small_int_bf16((int)(((long)j * 11 + (long)k * 5) % 7) - 3);
+    }
+  }
+}
+
+__global__ void verify_kernel(const float* __restrict__ C, int M, int N, int K, const int* __restrict__ tile_xcd,
+                              unsigned* __restrict__ err_total, unsigned* __restrict__ err_xcd) {
+  const int q = K / 35, rem = K - q * 35;
+  const size_t total = (size_t)M * N;
+  const int tiles_n = N / BN;
+  for (size_t base = blockIdx.x * (size_t)blockDim.x; base < total; base += (size_t)gridDim.x * blockDim.x) {
+    const size_t idx = base + threadIdx.x;
+    bool bad = false;
+    if (idx < total) {
+      const int i = (int)(idx / N), j = (int)(idx - (size_t)i * N);
+      const int ia = (i % 5) * 3 % 5, jb = (j % 7) * 11 % 7;
+      int s = 0;
+#pragma unroll
+      for (int r = 0; r < 35; ++r) {
+        int a = ia + (r * 7) % 5;
+        a = (a >= 5 ? a - 5 : a) - 2;
+        int b = jb + (r * 5) % 7;
+        b = (b >= 7 ? b - 7 : b) - 3;
+        s += (q + (r < rem ? 1 : 0)) * a * b;
+      }
+      bad = C[idx] != (float)s;
+      if (bad && err_xcd && tile_xcd) atomicAdd(&err_xcd[tile_xcd[(i / BM) * tiles_n + j / BN] & 7], 1u);
+    }
+    const unsigned long long m = __ballot(bad);
+    if ((threadIdx.x & 63) == 0 && m) atomicAdd(err_total, (unsigned)__popcll(m));
+  }
+}
+
+__device__ __forceinline__ uint32_t mix32(uint32_t x) {
+  x ^= x >> 16;
+  x *= 0x7feb352dU;
+  x ^= x >> 15;
+  x *= 0x846ca68bU;
+  x ^= x >> 16;
+  return x;
+}
+
+__global__ __launch_bounds__(256) void hbm_write_kernel(u32x4* __restrict__ buf, size_t n, uint32_t seed) {
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+    const uint32_t b = (uint32_t)(i * 4) ^ seed;
+    u32x4 v;
+    v.x = mix32(b);
+    v.y = mix32(b + 1);
+    v.z = mix32(b + 2);
+    v.w = mix32(b + 3);
+    __builtin_nontemporal_store(v, &buf[i]);
+  }
+}
+
+__global__ __launch_bounds__(256) void hbm_check_kernel(const u32x4* __restrict__ buf, size_t n, uint32_t seed,
+                                                        unsigned long long* __restrict__ err) {
+  unsigned local = 0;
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+    const u32x4 v = __builtin_nontemporal_load(&buf[i]);
+    const uint32_t b = (uint32_t)(i * 4) ^ seed;
+    local += (v.x != mix32(b)) + (v.y != mix32(b + 1)) + (v.z != mix32(b + 2)) + (v.w != mix32(b + 3));
+  }
+  // wave reduction (64 lanes), one atomic per wave
+  for (int off = 32; off > 0; off >>= 1) local += __shfl_down(local, off, 64);
+  if ((threadIdx.x & 63) == 0 && local) atomicAdd(err, (unsigned long long)local);
+}
+
+__global__ __launch_bounds__(256) void busy_kernel(float* __restrict__ out, int iters) {
+  const int lane = threadIdx.x & 63;
+  bf16x8 a, b;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    a[e] = (__bf16)(float)((lane + e) & 3);
+    b[e] = (__bf16)(float)((lane * 3 + e) & 3);
+  }
+  f32x16 acc0 = {}, acc1 = {}, acc2 = {}, acc3 = {};
+  for (int i = 0; i < iters; ++i) {
+    acc0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, acc0, 0, 0, 0);
+    acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b, a, acc1, 0, 0, 0);
+    acc2 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, a, acc2, 0, 0, 0);
+    acc3 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b, b, acc3, 0, 0, 0);
+  }
+  float s = 0.f;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) s += acc0[r] + acc1[r] + acc2[r] + acc3[r];
+  out[blockIdx.x * blockDim.x + threadIdx.x] = s;
+}
+
+int grid_for(size_t n, int per_block) {
+  size_t g = (n + per_block - 1) / per_block;
+  if (g > 4096) g = 4096;  // 16 × 256 CUs of grid-stride work
+  if (g < 1) g = 1;
+  return (int)g;
+}
+
+}  // namespace
+
+extern "C" {
+
+int odh_gemm_shape_ok(int M, int N, int K) {
+  return M > 0 && N > 0 && K > 0 && M % BM == 0 && N % BN == 0 && K % BK == 0;
+}
+
+const char* odh_error_string(int code) { return hipGetErrorString((hipError_t)code); }
+
+int odh_probe_fill(void* A, void* Bt, int M, int N, int K, hipStream_t stream) {
+  if (!odh_gemm_shape_ok(M, N, K)) return (int)hipErrorInvalidValue;
+  const size_t n = (size_t)M * K + (size_t)N * K;
+  fill_kernel<<<grid_for(n, 256), 256, 0, stream>>>((uint16_t*)A, (uint16_t*)Bt, M, N, K);
+  return (int)hipGetLastError();
+}
+
+int odh_gemm_bf16(const void* A, const void* Bt, float* C, int M, int N, int K, int* tile_xcd, int* xcd_blocks,
+                  hipStream_t stream) {
+  if (!odh_gemm_shape_ok(M, N, K)) return (int)hipErrorInvalidValue;
+  const int nwg = (M / BM) * (N / BN);
+  gemm_bf16_kernel<<<nwg, THREADS, 0, stream>>>((const uint4*)A, (const uint4*)Bt, C, M, N, K, tile_xcd, xcd_blocks);
+  return (int)hipGetLastError();
+}
+
+int odh_probe_verify(const float* C, int M, int N, int K, const int* tile_xcd, unsigned* err_total,
+                     unsigned* err_xcd, hipStream_t stream) {
+  if (!odh_gemm_shape_ok(M, N, K)) return (int)hipErrorInvalidValue;
+  verify_kernel<<<grid_for((size_t)M * N, 256), 256, 0, stream>>>(C, M, N, K, tile_xcd, err_total, err_xcd);
+  return (int)hipGetLastError();
+}
+
+int odh_hbm_write(void* buf, size_t bytes, uint32_t seed, hipStream_t stream) {
+  const size_t n = bytes / 16;
+  if (n == 0) return (int)hipErrorInvalidValue;
+  hbm_write_kernel<<<grid_for(n, 256 * 4), 256, 0, stream>>>((u32x4*)buf, n, seed);
+  return (int)hipGetLastError();
+}
+
+int odh_hbm_check(const void* buf, size_t bytes, uint32_t seed, unsigned long long* err, hipStream_t stream) {
+  const size_t n = bytes / 16;
+  if (n == 0) return (int)hipErrorInvalidValue;
+  hbm_check_kernel<<<grid_for(n, 256 * 4), 256, 0, stream>>>((const u32x4*)buf, n, seed, err);
+  return (int)hipGetLastError();
+}
+
+int odh_busy(float* out, int blocks, int iters, hipStream_t stream) {
+  if (blocks <= 0 || iters < 0) return (int)hipErrorInvalidValue;
+  busy_kernel<<<blocks, 256, 0, stream>>>(out, iters);
+  return (int)hipGetLastError();
+}
+
+}  // extern "C"

@@ -1,0 +1,310 @@
+"""Python side of the MI355X node-agent kernels (``csrc/gpu_probe.hip``).
+
+* :func:`gemm_bf16` — the MFMA bf16 GEMM (``C = A · Btᵀ``, fp32 out) on torch tensors.
+* :class:`GpuProbe` — the notebook start-up probe: a resident 4096³ bf16 GEMM whose
+  integer-valued operands make every output element checkable bit-exactly on the GPU,
+  plus an HBM3E pattern write/verify sweep.  One probe is a handful of kernels on the
+  device's current stream followed by one 32-word device→host copy.  Reports matrix-core
+  TFLOP/s, HBM GB/s, mismatches (attributed to the XCD that computed them) and how many
+  of the 8 XCDs ran workgroups.
+* :func:`startup_probe` — the async hook the node agent (``kubelet/node.py``
+  ``GpuRuntime``) awaits before reporting a GPU pod Ready.
+* :class:`LoadGenerator` — synthetic MFMA load at a given duty cycle (culler benchmarks).
+
+The library is loaded with ctypes **after** ``import torch`` so it binds to the HIP
+runtime torch already loaded.  If the ``.so`` is missing on a machine with a GPU the
+calls raise :class:`NativeLibraryMissing` instead of silently falling back.
+"""
+
+from __future__ import annotations
+
+import asyncio
+import ctypes
+import os
+import threading
+import time
+from typing import Dict, List, Optional, Sequence
+
+from .build import lib_path
+
+PROBE_LIB = "libodh_gpu_probe.so"
+BM = BN = 128
+BK = 32
+N_XCD = 8
+
+
+class NativeLibraryMissing(RuntimeError):
+    pass
+
+
+class HipError(RuntimeError):
+    pass
+
+
+_lib = None
+_lib_lock = threading.Lock()
+
+
+def load_library(build_if_missing: bool = False):
+    """Load (once) and return the ctypes handle of ``libodh_gpu_probe.so``."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lib_lock:
+        if _lib is not None:
+            return _lib
+        import torch  # noqa: F401  -- must own libamdhip64.so.7 before we dlopen
+
+        path = lib_path(PROBE_LIB)
+        if not os.path.exists(path):
+            if build_if_missing:
+                from .build import build
+
+                build(verbose=False)
+            if not os.path.exists(path):
+                raise NativeLibraryMissing(f"{path} not built; run `python -m odh_kubeflow_amd.ops.build`")
+        lib = ctypes.CDLL(path)
+        vp, i, u32, sz = ctypes.c_void_p, ctypes.c_int, ctypes.c_uint32, ctypes.c_size_t
+        lib.odh_gemm_shape_ok.argtypes = [i, i, i]
+        lib.odh_gemm_shape_ok.restype = i
+        lib.odh_error_string.argtypes = [i]
+        lib.odh_error_string.restype = ctypes.c_char_p
+        lib.odh_probe_fill.argtypes = [vp, vp, i, i, i, vp]
+        lib.odh_gemm_bf16.argtypes = [vp, vp, vp, i, i, i, vp, vp, vp]
+        lib.odh_probe_verify.argtypes = [vp, i, i, i, vp, vp, vp, vp]
+        lib.odh_hbm_write.argtypes = [vp, sz, u32, vp]
+        lib.odh_hbm_check.argtypes = [vp, sz, u32, vp, vp]
+        lib.odh_busy.argtypes = [vp, i, i, vp]
+        for f in ("odh_probe_fill", "odh_gemm_bf16", "odh_probe_verify", "odh_hbm_write", "odh_hbm_check",
+                  "odh_busy"):
+            getattr(lib, f).restype = i
+        _lib = lib
+        return lib
+
+
+def _check(rc: int) -> None:
+    if rc != 0:
+        msg = load_library().odh_error_string(rc)
+        raise HipError(f"HIP error {rc}: {msg.decode() if msg else '?'}")
+
+
+def _stream_ptr(device) -> int:
+    import torch
+
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def gemm_shape_ok(m: int, n: int, k: int) -> bool:
+    return m > 0 and n > 0 and k > 0 and m % BM == 0 and n % BN == 0 and k % BK == 0
+
+
+def gemm_bf16(a, bt, out=None, tile_xcd=None, xcd_blocks=None):
+    """``C[M,N] = A[M,K] · Bt[N,K]ᵀ`` in fp32 on the matrix cores.
+
+    Shapes must be multiples of the 128×128×32 tile (checked here, before launch).
+    """
+    import torch
+
+    if a.dtype != torch.bfloat16 or bt.dtype != torch.bfloat16:
+        raise TypeError("gemm_bf16 expects bfloat16 operands")
+    if a.dim() != 2 or bt.dim() != 2 or a.shape[1] != bt.shape[1]:
+        raise ValueError(f"shape mismatch: A{tuple(a.shape)} Bt{tuple(bt.shape)}")
+    if not (a.is_cuda and bt.is_cuda) or a.device != bt.device:
+        raise ValueError("operands must live on the same GPU")
+    m, k = a.shape
+    n = bt.shape[0]
+    if not gemm_shape_ok(m, n, k):
+        raise ValueError(f"M,N must be multiples of {BM}/{BN} and K of {BK}; got {m},{n},{k}")
+    a = a.contiguous()
+    bt = bt.contiguous()
+    if out is None:
+        out = torch.empty((m, n), dtype=torch.float32, device=a.device)
+    elif out.shape != (m, n) or out.dtype != torch.float32 or not out.is_contiguous():
+        raise ValueError("out must be a contiguous fp32 [M,N] tensor")
+    if tile_xcd is not None and tile_xcd.numel() < (m // BM) * (n // BN):
+        raise ValueError("tile_xcd too small")
+    if xcd_blocks is not None and xcd_blocks.numel() < N_XCD:
+        raise ValueError("xcd_blocks too small")
+    lib = load_library()
+    _check(lib.odh_gemm_bf16(a.data_ptr(), bt.data_ptr(), out.data_ptr(), m, n, k,
+                             tile_xcd.data_ptr() if tile_xcd is not None else None,
+                             xcd_blocks.data_ptr() if xcd_blocks is not None else None, _stream_ptr(a.device)))
+    return out
+
+
+class GpuProbe:
+    """Resident start-up probe for one GPU (allocate + fill once, then ~1 ms per run)."""
+
+    def __init__(self, device: int = 0, m: int = 4096, n: int = 4096, k: int = 4096, hbm_bytes: int = 1 << 30):
+        import torch
+
+        if not gemm_shape_ok(m, n, k):
+            raise ValueError("probe GEMM shape must be tile aligned")
+        if hbm_bytes < 16 or hbm_bytes % 16:
+            raise ValueError("hbm_bytes must be a positive multiple of 16")
+        self.device = torch.device("cuda", device)
+        self.m, self.n, self.k = m, n, k
+        self.hbm_bytes = hbm_bytes
+        lib = load_library()
+        with torch.cuda.device(self.device):
+            self.a = torch.empty((m, k), dtype=torch.bfloat16, device=self.device)
+            self.bt = torch.empty((n, k), dtype=torch.bfloat16, device=self.device)
+            self.c = torch.empty((m, n), dtype=torch.float32, device=self.device)
+            self.tile_xcd = torch.full(((m // BM) * (n // BN),), -1, dtype=torch.int32, device=self.device)
+            self.hbm = torch.empty((hbm_bytes // 4,), dtype=torch.int32, device=self.device)
+            # counters: [0:8] xcd_blocks, [8:16] err_xcd, [16] gemm err, [18:20] hbm err (u64)
+            self.counters = torch.zeros((32,), dtype=torch.int32, device=self.device)
+            self.host = torch.zeros((32,), dtype=torch.int32).pin_memory()
+            self.ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+            _check(lib.odh_probe_fill(self.a.data_ptr(), self.bt.data_ptr(), m, n, k, _stream_ptr(self.device)))
+        self.runs = 0
+        self.seed = 0x9E3779B9
+
+    def run(self) -> dict:
+        import torch
+
+        lib = load_library()
+        t0 = time.perf_counter()
+        with torch.cuda.device(self.device):
+            s = _stream_ptr(self.device)
+            cnt = self.counters
+            base = cnt.data_ptr()
+            cnt.zero_()
+            self.seed = (self.seed * 1664525 + 1013904223) & 0xFFFFFFFF
+            self.ev[0].record()
+            _check(lib.odh_gemm_bf16(self.a.data_ptr(), self.bt.data_ptr(), self.c.data_ptr(), self.m, self.n, self.k,
+                                     self.tile_xcd.data_ptr(), base, s))
+            self.ev[1].record()
+            _check(lib.odh_probe_verify(self.c.data_ptr(), self.m, self.n, self.k, self.tile_xcd.data_ptr(),
+                                        base + 16 * 4, base + 8 * 4, s))
+            self.ev[2].record()
+            _check(lib.odh_hbm_write(self.hbm.data_ptr(), self.hbm_bytes, self.seed, s))
+            _check(lib.odh_hbm_check(self.hbm.data_ptr(), self.hbm_bytes, self.seed, base + 18 * 4, s))
+            self.ev[3].record()
+            self.host.copy_(cnt, non_blocking=True)
+            self.ev[3].synchronize()
+            torch.cuda.current_stream(self.device).synchronize()
+        h = self.host.tolist()
+        gemm_ms = self.ev[0].elapsed_time(self.ev[1])
+        hbm_ms = self.ev[2].elapsed_time(self.ev[3])
+        xcd_blocks = h[0:8]
+        err_xcd = h[8:16]
+        gemm_err = h[16] & 0xFFFFFFFF
+        hbm_err = (h[18] & 0xFFFFFFFF) | ((h[19] & 0xFFFFFFFF) << 32)
+        flops = 2.0 * self.m * self.n * self.k
+        self.runs += 1
+        ok = gemm_err == 0 and hbm_err == 0 and sum(xcd_blocks) == (self.m // BM) * (self.n // BN)
+        return {
+            "ok": bool(ok), "device": self.device.index, "gemm_ms": gemm_ms,
+            "gemm_tflops": flops / (gemm_ms * 1e-3) / 1e12 if gemm_ms > 0 else 0.0,
+            "hbm_gbps": 2.0 * self.hbm_bytes / (hbm_ms * 1e-3) / 1e9 if hbm_ms > 0 else 0.0,
+            "gemm_errors": gemm_err, "hbm_errors": hbm_err, "xcd_blocks": xcd_blocks, "err_xcd": err_xcd,
+            "xcds": sum(1 for x in xcd_blocks if x > 0), "wall_ms": (time.perf_counter() - t0) * 1e3,
+        }
+
+
+_probes: Dict[int, GpuProbe] = {}
+_probe_lock = threading.Lock()
+
+
+def get_probe(device: int, **kw) -> GpuProbe:
+    with _probe_lock:
+        p = _probes.get(device)
+        if p is None:
+            p = _probes[device] = GpuProbe(device, **kw)
+        return p
+
+
+def probe_devices(devices: Sequence[int]) -> dict:
+    results = []
+    for d in devices:
+        try:
+            results.append(get_probe(d).run())
+        except Exception as e:  # a failed probe fails the pod, it must not crash the agent
+            results.append({"ok": False, "device": d, "error": repr(e)})
+    return {"ok": all(r.get("ok") for r in results), "devices": list(devices), "results": results,
+            "error": next((r.get("error") or f"probe failed on GPU {r['device']}" for r in results
+                           if not r.get("ok")), None)}
+
+
+async def startup_probe(devices: Sequence[int], local_index=None) -> dict:
+    """Node-agent hook: probe the pod's GPUs off the event loop.
+
+    ``local_index`` maps node-level GPU ids to this process's visible devices (one
+    process per GPU: rank r sees its GPU as ``cuda:0`` under ``HIP_VISIBLE_DEVICES``).
+    """
+    devs = [local_index(d) if local_index else d for d in devices]
+    return await asyncio.get_running_loop().run_in_executor(None, probe_devices, devs)
+
+
+class LoadGenerator:
+    """Keeps a GPU's matrix cores busy at ``duty`` (0..1) until :meth:`stop`."""
+
+    def __init__(self, device: int = 0, duty: float = 1.0, chunk_ms: float = 5.0, blocks: int = 1024):
+        self.device = device
+        self.duty = max(0.0, min(1.0, duty))
+        self.chunk_ms = chunk_ms
+        self.blocks = blocks
+        self._stop = threading.Event()
+        self._thr: Optional[threading.Thread] = None
+        self.launches = 0
+        self.iters = 2048
+
+    def _loop(self) -> None:
+        import torch
+
+        lib = load_library()
+        dev = torch.device("cuda", self.device)
+        with torch.cuda.device(dev):
+            out = torch.empty((self.blocks * 256,), dtype=torch.float32, device=dev)
+            s = _stream_ptr(dev)
+            # calibrate iterations so one launch lasts ~chunk_ms
+            t0 = time.perf_counter()
+            _check(lib.odh_busy(out.data_ptr(), self.blocks, self.iters, s))
+            torch.cuda.current_stream(dev).synchronize()
+            dt = max(1e-4, time.perf_counter() - t0)
+            self.iters = max(64, min(1 << 22, int(self.iters * (self.chunk_ms * 1e-3) / dt)))
+            while not self._stop.is_set():
+                t0 = time.perf_counter()
+                _check(lib.odh_busy(out.data_ptr(), self.blocks, self.iters, s))
+                torch.cuda.current_stream(dev).synchronize()
+                self.launches += 1
+                busy = time.perf_counter() - t0
+                if self.duty < 1.0:
+                    idle = busy * (1.0 - self.duty) / max(self.duty, 1e-3)
+                    self._stop.wait(idle)
+
+    def start(self) -> "LoadGenerator":
+        self._thr = threading.Thread(target=self._loop, name=f"gpu-load-{self.device}", daemon=True)
+        self._thr.start()
+        return self
+
+    def stop(self) -> None:
+        self._stop.set()
+        if self._thr is not None:
+            self._thr.join(timeout=30)
+
+
+def available() -> bool:
+    """True when a GPU is visible (does not initialise HIP: device_count only)."""
+    try:
+        import torch
+
+        return torch.cuda.device_count() > 0
+    except Exception:
+        return False
+
+
+def loaded_libraries() -> List[str]:
+    """Native libraries of this package mapped into the process (for smoke/bench logs)."""
+    out = []
+    try:
+        with open("/proc/self/maps") as f:
+            for line in f:
+                if "odh_kubeflow_amd" in line and line.rstrip().endswith(".so"):
+                    p = line.split()[-1]
+                    if p not in out:
+                        out.append(p)
+    except OSError:
+        pass
+    return out

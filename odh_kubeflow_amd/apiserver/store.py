@@ -42,7 +42,7 @@ from ..models.errors import (AlreadyExists, ApiError, BadRequest, Conflict, Forb
                              NotFound)
 from ..models.scheme import OPTIONAL_CRDS, SCHEME, ResourceInfo
 from ..utils import jsonpatch
-from ..utils.objutil import deepcopy_json
+from ..utils.objutil import deepcopy_json, equal_except
 from ..utils.selectors import field_matcher, match_labels, parse_field_selector, parse_label_selector, selector_from_dict
 from ..utils.timeutil import rfc3339
 
@@ -77,6 +77,9 @@ class _Watcher:
 
 def _rand_suffix(n: int = 5) -> str:
     return "".join(random.choices("bcdfghjklmnpqrstvwxz2456789", k=n))
+
+
+_COMPARE_SKIP = ("resourceVersion", "managedFields", "generation")
 
 
 def _strip_for_compare(obj: dict) -> dict:
@@ -407,7 +410,7 @@ class ObjectStore:
                 if _spec_part(new) != _spec_part(live):
                     md["generation"] = lmd["generation"] + 1
             md["resourceVersion"] = lmd["resourceVersion"]
-            if _strip_for_compare(new) == _strip_for_compare(live):
+            if equal_except(new, live, _COMPARE_SKIP):
                 return self._out(info, live, version)  # no-op write
             # finalizer-driven removal
             if lmd.get("deletionTimestamp") and not md.get("finalizers"):

@@ -38,6 +38,7 @@ class ClusterConfig:
     gpu_runtimes_in_process: bool = True  # False: rank processes host GPU runtimes (multi-GPU bench)
     reference_emulation: bool = False  # reproduce the reference's serialising behaviour for comparison
     activity_source: Optional[object] = None
+    openshift: bool = False  # serve the OpenShift APIs (image/config/route/oauth) like an OCP cluster
 
 
 class LocalCluster:
@@ -45,6 +46,9 @@ class LocalCluster:
         self.cfg = cfg or ClusterConfig()
         self.env = {**os.environ, **self.cfg.env}
         self.store = store or ObjectStore(gc=self.cfg.gc)
+        if not self.cfg.openshift and store is None:
+            for crd in (kinds.IMAGE_STREAM, kinds.PROXY, kinds.ROUTE, kinds.OAUTH_CLIENT):
+                self.store.uninstall_crd(crd)
         self.managers: List[Manager] = []
         self.kube: Optional[Manager] = None
         self.kf: Optional[Manager] = None

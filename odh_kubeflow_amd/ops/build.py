@@ -16,11 +16,14 @@ import os
 import shutil
 import subprocess
 import sys
+import sysconfig
 from typing import Dict, List
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 LIBDIR = os.path.join(HERE, "_lib")
+NATIVE = os.path.join(os.path.dirname(HERE), "native")
+OBJCORE = "_objcore" + (sysconfig.get_config_var("EXT_SUFFIX") or ".so")
 ARCH = os.environ.get("ODH_GPU_ARCH", "gfx950")
 ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
 
@@ -36,6 +39,13 @@ def targets() -> Dict[str, dict]:
             "src": [os.path.join(CSRC, "gpu_probe.hip")],
             "cmd": lambda src, out: [_hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-shared", "-fPIC",
                                      *src, "-o", out],
+        },
+        OBJCORE: {
+            "src": [os.path.join(NATIVE, "objcore.cpp")],
+            "out": os.path.join(NATIVE, OBJCORE),
+            "cmd": lambda src, out: [os.environ.get("CXX", "g++"), "-O2", "-std=c++17", "-shared", "-fPIC", "-Wall",
+                                     "-fno-strict-aliasing", f"-I{sysconfig.get_paths()['include']}", *src,
+                                     "-o", out],
         },
         "libodh_gpu_telemetry.so": {
             "src": [os.path.join(CSRC, "gpu_telemetry.cpp")],
@@ -60,7 +70,7 @@ def build(force: bool = False, verbose: bool = True) -> Dict[str, str]:
     os.makedirs(LIBDIR, exist_ok=True)
     built = {}
     for name, spec in targets().items():
-        out = lib_path(name)
+        out = spec.get("out") or lib_path(name)
         if force or _stale(out, spec["src"]):
             tmp = out + ".tmp"
             cmd = spec["cmd"](spec["src"], tmp)

@@ -214,7 +214,7 @@ class Controller:
                 return
             self.active += 1
             if self.metrics:
-                self.metrics.active_workers.labels(self.name).set(self.active)
+                self.metrics.child(self.metrics.active_workers, self.name).set(self.active)
             t0 = time.perf_counter()
             err: Optional[BaseException] = None
             res: Optional[Result] = None
@@ -248,11 +248,11 @@ class Controller:
             finally:
                 q.done(req)
             if self.metrics:
-                self.metrics.reconcile_total.labels(self.name, outcome).inc()
-                self.metrics.reconcile_time.labels(self.name).observe(dt)
-                self.metrics.active_workers.labels(self.name).set(self.active)
+                self.metrics.child(self.metrics.reconcile_total, self.name, outcome).inc()
+                self.metrics.child(self.metrics.reconcile_time, self.name).observe(dt)
+                self.metrics.child(self.metrics.active_workers, self.name).set(self.active)
                 if err is not None:
-                    self.metrics.reconcile_errors.labels(self.name).inc()
+                    self.metrics.child(self.metrics.reconcile_errors, self.name).inc()
             if self.on_reconcile is not None:
                 self.on_reconcile(self.name, req, dt, err)
 

@@ -40,14 +40,24 @@ class RuntimeMetrics:
         self.retries = Counter("workqueue_retries_total", "Total number of retries handled by workqueue", ["name"],
                                registry=registry)
 
+        self._children = {}
+
+    def child(self, metric, *labels):
+        """Memoised ``metric.labels(*labels)`` (label lookup is the hot part of a metric update)."""
+        k = (id(metric), labels)
+        c = self._children.get(k)
+        if c is None:
+            c = self._children[k] = metric.labels(*labels)
+        return c
+
     # workqueue hooks
     def on_add(self, name: str, depth: int) -> None:
-        self.adds.labels(name).inc()
-        self.depth.labels(name).set(depth)
+        self.child(self.adds, name).inc()
+        self.child(self.depth, name).set(depth)
 
     def on_get(self, name: str, depth: int, latency: float) -> None:
-        self.depth.labels(name).set(depth)
-        self.queue_latency.labels(name).observe(latency)
+        self.child(self.depth, name).set(depth)
+        self.child(self.queue_latency, name).observe(latency)
 
     def on_retry(self, name: str) -> None:
-        self.retries.labels(name).inc()
+        self.child(self.retries, name).inc()

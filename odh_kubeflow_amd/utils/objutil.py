@@ -93,9 +93,25 @@ def prune_empty(o: Any) -> Any:
     return o
 
 
-def semantic_equal(a: Any, b: Any) -> bool:
+def _py_semantic_equal(a: Any, b: Any) -> bool:
     """``equality.Semantic.DeepEqual`` analogue: absent == empty for maps/lists/None."""
     return prune_empty(a) == prune_empty(b)
+
+
+def _py_equal_except(a: dict, b: dict, keys) -> bool:
+    ma, mb = dict(a.get("metadata") or {}), dict(b.get("metadata") or {})
+    for k in keys:
+        ma.pop(k, None)
+        mb.pop(k, None)
+    return ({**a, "metadata": ma} if "metadata" in a else a) == ({**b, "metadata": mb} if "metadata" in b else b)
+
+
+if NATIVE_OBJCORE:
+    semantic_equal = _objcore.semantic_equal
+    equal_except = _objcore.equal_except
+else:  # pragma: no cover
+    semantic_equal = _py_semantic_equal
+    equal_except = _py_equal_except
 
 
 def find_by_name(items: Optional[Iterable[dict]], name: str) -> Optional[dict]:

@@ -1,0 +1,283 @@
+"""The ODH mutating admission webhook for ``kubeflow.org/v1 notebooks``
+(reference ``odh/controllers/notebook_webhook.go``, registered at
+``/mutate-notebook-v1`` with ``failurePolicy: Fail``, ``sideEffects: None``).
+
+``Handle`` pipeline (:352-499), in order:
+
+1. CREATE → inject the reconciliation lock (``kubeflow-resource-stopped:
+   odh-notebook-controller-lock``) so the pod cannot start before the ODH reconciler
+   has run;
+2. CREATE/UPDATE → resolve the image from the ImageStream named by
+   ``notebooks.opendatahub.io/last-image-selection`` (span events
+   ``imagestream-not-found`` / ``imagestream-tag-not-found``), mount the trusted-CA
+   bundle, sync + mount the pipeline runtime-images ConfigMap, [``SET_PIPELINE_SECRET``]
+   sync + mount the Elyra secret, mount/unmount the Feast config;
+3. ``inject-auth`` → kube-rbac-proxy sidecar;
+4. ``INJECT_CLUSTER_PROXY_ENV`` + cluster ``Proxy`` → HTTP(S)_PROXY / NO_PROXY env;
+5. restart guard: on UPDATE of a running notebook, webhook-only pod-template changes
+   are reverted and reported in ``notebooks.opendatahub.io/update-pending``;
+6. respond with an RFC 6902 JSONPatch from the request object to the mutated one.
+
+Differences (internal, not observable): the cluster proxy values are returned, not
+stored in a package-global map written by concurrent requests (:66, :340-342 — a data
+race in the reference); the webhook client is uncached for ConfigMaps/Secrets like
+the reference manager's (``odh/main.go:178-185``).
+"""
+
+from __future__ import annotations
+
+import base64
+import json
+import logging
+import os
+from typing import Dict, Mapping, Optional, Tuple
+
+from ..controllers.odh import auth, certs, dspa_secret, feast, runtime_images
+from ..controllers.odh.constants import (ANNOTATION_NOTEBOOK_RESTART, ANNOTATION_UPDATE_PENDING,
+                                         ANNOTATION_VALUE_RECONCILIATION_LOCK, IMAGE_STREAM_NOT_FOUND_EVENT,
+                                         IMAGE_STREAM_TAG_NOT_FOUND_EVENT, INTERNAL_REGISTRY,
+                                         LAST_IMAGE_SELECTION_ANNOTATION, STOP_ANNOTATION,
+                                         WORKBENCH_IMAGE_NAMESPACE_ANNOTATION)
+from ..controllers.odh.podspec import add_missing_env, notebook_container
+from ..models import kinds
+from ..models import meta as m
+from ..models.errors import ApiError, is_not_found
+from ..tracing import current_span, get_tracer
+from ..utils import jsonpatch
+from ..utils.objutil import deepcopy_json, semantic_equal
+from .diff import first_difference
+
+log = logging.getLogger("webhook.notebook")
+tracer = get_tracer("opendatahub.io/kubeflow/components/odh-notebook-controller/controllers/notebook_webhook.go")
+
+WEBHOOK_PATH = "/mutate-notebook-v1"
+PROXY_ENV_ORDER = ("HTTP_PROXY", "HTTPS_PROXY", "NO_PROXY")
+
+
+class AdmissionError(Exception):
+    def __init__(self, code: int, message: str):
+        super().__init__(message)
+        self.code = code
+
+
+def inject_reconciliation_lock(nb: dict) -> None:
+    m.ensure_annotations(nb)[STOP_ANNOTATION] = ANNOTATION_VALUE_RECONCILIATION_LOCK
+
+
+def _parse_go_bool(raw: str) -> Optional[bool]:
+    v = raw.strip()
+    if v in ("1", "t", "T", "TRUE", "true", "True"):
+        return True
+    if v in ("0", "f", "F", "FALSE", "false", "False"):
+        return False
+    return None
+
+
+async def set_container_image_from_registry(client, nb: dict, controller_namespace: str) -> None:
+    """``SetContainerImageFromRegistry`` (:787-894)."""
+    span = current_span()
+    ann = m.annotations(nb)
+    selection = ann.get(LAST_IMAGE_SELECTION_ANNOTATION)
+    if selection is None:
+        return
+    c = notebook_container(nb)
+    if c is None:
+        raise AdmissionError(500, f"no container found matching the notebook name {m.name(nb)}")
+    if INTERNAL_REGISTRY in (c.get("image") or ""):
+        return
+    parts = selection.split(":")
+    if len(parts) != 2:
+        raise AdmissionError(500, "invalid image selection format")
+    is_name, tag_name = parts
+    image_ns = ann.get(WORKBENCH_IMAGE_NAMESPACE_ANNOTATION)
+    if image_ns is None or not image_ns.strip():
+        image_ns = controller_namespace
+    try:
+        ist = await client.get(kinds.IMAGE_STREAM, is_name, image_ns)
+    except ApiError as e:
+        if is_not_found(e):
+            span.add_event(IMAGE_STREAM_NOT_FOUND_EVENT)
+        else:
+            log.error("error getting ImageStream %s/%s: %s", image_ns, is_name, e)
+        return
+    tags = (ist.get("status") or {}).get("tags")
+    if tags is None:
+        span.add_event(IMAGE_STREAM_TAG_NOT_FOUND_EVENT)
+        raise AdmissionError(500, "ImageStream has no status or tags")
+    for tag in tags:
+        if tag.get("tag") != tag_name:
+            continue
+        items = tag.get("items") or []
+        if not items:
+            continue
+        newest = sorted(items, key=lambda it: it.get("created") or "", reverse=True)[0]
+        # the reference writes Containers[0] (:868) — preserved
+        nb["spec"]["template"]["spec"]["containers"][0]["image"] = newest.get("dockerImageReference", "")
+        for e in c.get("env") or []:
+            if e.get("name") == "JUPYTER_IMAGE":
+                e["value"] = selection
+                break
+        return
+    span.add_event(IMAGE_STREAM_TAG_NOT_FOUND_EVENT)
+
+
+async def cluster_proxy_env(client) -> Optional[Dict[str, str]]:
+    """``ClusterWideProxyIsEnabled`` (:328-349) without the shared global map."""
+    try:
+        proxies = await client.list(kinds.PROXY)
+    except ApiError:
+        return None
+    for p in proxies:
+        if m.name(p) == "cluster":
+            st = p.get("status") or {}
+            if st.get("httpProxy") and st.get("httpsProxy") and st.get("noProxy"):
+                return {"HTTP_PROXY": st["httpProxy"], "HTTPS_PROXY": st["httpsProxy"], "NO_PROXY": st["noProxy"]}
+    return None
+
+
+def inject_proxy_config_env_vars(nb: dict, values: Mapping[str, str]) -> None:
+    c = notebook_container(nb)
+    if c is not None:
+        add_missing_env(c, values, order=[k for k in PROXY_ENV_ORDER if k in values])
+
+
+class NotebookWebhook:
+    def __init__(self, client, namespace: str, kube_rbac_proxy_image: str, env: Optional[Mapping[str, str]] = None):
+        self.client = client
+        self.namespace = namespace
+        self.kube_rbac_proxy_image = kube_rbac_proxy_image
+        self.env = env if env is not None else os.environ
+        self.requests = 0
+        self.denied = 0
+
+    async def mutate(self, operation: str, nb: dict, old: Optional[dict], name: str = "",
+                     namespace: str = "") -> dict:
+        """Return the mutated notebook (``nb`` is not modified)."""
+        with tracer.start_span("handleFunc", {"notebook": name or m.name(nb), "namespace": namespace or m.namespace(nb),
+                                              "operation": operation}, new_root=True):
+            original = nb
+            nb = deepcopy_json(nb)
+            if operation == "CREATE":
+                inject_reconciliation_lock(nb)
+            if operation in ("CREATE", "UPDATE"):
+                await set_container_image_from_registry(self.client, nb, self.namespace)
+                await certs.check_and_mount_ca_cert_bundle(self.client, nb)
+                try:
+                    await runtime_images.sync_runtime_images_configmap(self.client, m.namespace(nb), self.namespace)
+                except Exception as e:  # degrade: mount whatever exists
+                    log.error("failed to sync runtime images ConfigMap: %s", e)
+                await runtime_images.mount_pipeline_runtime_images(self.client, nb)
+                if (self.env.get("SET_PIPELINE_SECRET") or "").strip().lower() == "true":
+                    try:
+                        await dspa_secret.sync_elyra_runtime_config_secret(self.client, nb)
+                    except Exception as e:
+                        log.error("failed to sync Elyra runtime config secret: %s", e)
+                    await dspa_secret.mount_elyra_runtime_config_secret(self.client, nb)
+                if feast.is_feast_enabled(nb):
+                    try:
+                        feast.new_feast_config(nb)
+                    except ValueError as e:
+                        log.info("unable to mount Feast config volume: %s", e)
+                elif feast.is_feast_mounted(nb):
+                    feast.unmount_feast_config(nb)
+            if auth.kube_rbac_proxy_injection_enabled(nb):
+                try:
+                    auth.inject_kube_rbac_proxy(nb, self.kube_rbac_proxy_image)
+                except auth.SidecarResourceError as e:
+                    raise AdmissionError(500, f"invalid kube-rbac-proxy resource configuration: {e}")
+            raw = self.env.get("INJECT_CLUSTER_PROXY_ENV")
+            if raw is not None and _parse_go_bool(raw):
+                vals = await cluster_proxy_env(self.client)
+                if vals:
+                    inject_proxy_config_env_vars(nb, vals)
+            nb, reason = self.maybe_restart_running_notebook(operation, original, nb, old)
+            ann = m.ensure_annotations(nb)
+            if reason:
+                ann[ANNOTATION_UPDATE_PENDING] = reason
+            else:
+                ann.pop(ANNOTATION_UPDATE_PENDING, None)
+            return nb
+
+    def maybe_restart_running_notebook(self, operation: str, updated: dict, mutated: dict,
+                                       old: Optional[dict]) -> Tuple[dict, str]:
+        """``maybeRestartRunningNotebook`` (:505-564)."""
+        with tracer.start_span("maybeRestartRunningNotebook"):
+            if operation == "CREATE":
+                return mutated, ""
+            if m.has_annotation(mutated, STOP_ANNOTATION) or m.has_annotation(mutated, ANNOTATION_NOTEBOOK_RESTART):
+                return mutated, ""
+            if old is None:
+                return mutated, ""
+
+            def tmpl(o):
+                return (((o or {}).get("spec") or {}).get("template") or {}).get("spec") or {}
+
+            if not semantic_equal(tmpl(old), tmpl(updated)):
+                return mutated, ""  # the user's change already restarts the pod
+            if semantic_equal(tmpl(old), tmpl(mutated)):
+                return mutated, ""
+            diff = first_difference(tmpl(mutated), tmpl(updated))
+            log.info("update blocked, webhook would change the pod template of a running notebook: %s", diff)
+            mutated["spec"]["template"]["spec"] = deepcopy_json(tmpl(updated))
+            return mutated, diff or "failed to compute the reason for why there is a pending restart"
+
+    # -------------------------------------------------------------- AdmissionReview v1
+
+    async def handle(self, review: dict) -> dict:
+        """AdmissionReview v1 request → AdmissionReview response with a JSONPatch."""
+        self.requests += 1
+        req = review.get("request") or {}
+        uid = req.get("uid", "")
+        resp = {"uid": uid, "allowed": True}
+        try:
+            obj = req.get("object")
+            if not isinstance(obj, dict):
+                raise AdmissionError(400, "there is no content to decode")
+            old = req.get("oldObject") if isinstance(req.get("oldObject"), dict) else None
+            mutated = await self.mutate(req.get("operation", ""), obj, old, req.get("name", ""),
+                                        req.get("namespace", ""))
+            ops = jsonpatch.create_patch(obj, mutated)
+            if ops:
+                resp["patchType"] = "JSONPatch"
+                resp["patch"] = base64.b64encode(json.dumps(ops, separators=(",", ":")).encode()).decode()
+        except AdmissionError as e:
+            self.denied += 1
+            resp = {"uid": uid, "allowed": False, "status": {"code": e.code, "message": str(e)}}
+        except ApiError as e:
+            self.denied += 1
+            resp = {"uid": uid, "allowed": False, "status": {"code": 500, "message": str(e)}}
+        return {"apiVersion": "admission.k8s.io/v1", "kind": "AdmissionReview", "response": resp}
+
+
+def matches(info, operation: str) -> bool:
+    """``rules: kubeflow.org/v1 notebooks CREATE,UPDATE`` (config/webhook/manifests.yaml)."""
+    return info.key == "notebooks.kubeflow.org" and operation in ("CREATE", "UPDATE")
+
+
+def register_in_process(store, webhook: NotebookWebhook, name: str = "notebooks.opendatahub.io") -> None:
+    """Install the webhook as a mutating admission plugin of the in-process apiserver.
+
+    The store calls it exactly like the apiserver calls the HTTPS endpoint: an
+    AdmissionReview in, a JSONPatch out (applied to the request object); a denial
+    fails the write (``failurePolicy: Fail``).
+    """
+    import uuid
+
+    from ..models.errors import InternalError
+
+    async def handler(op, info, obj, old):
+        review = {"apiVersion": "admission.k8s.io/v1", "kind": "AdmissionReview",
+                  "request": {"uid": str(uuid.uuid4()), "operation": op, "name": m.name(obj),
+                              "namespace": m.namespace(obj), "object": obj, "oldObject": old,
+                              "kind": {"group": info.group, "version": "v1", "kind": info.kind},
+                              "resource": {"group": info.group, "version": "v1", "resource": info.plural}}}
+        out = (await webhook.handle(review))["response"]
+        if not out.get("allowed"):
+            st = out.get("status") or {}
+            raise InternalError(f'admission webhook "{name}" denied the request: {st.get("message", "")}')
+        if out.get("patch"):
+            ops = json.loads(base64.b64decode(out["patch"]))
+            obj = jsonpatch.apply_patch(obj, ops)
+        return obj
+
+    store.add_mutating_admission(name, matches, handler)

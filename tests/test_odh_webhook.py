@@ -1,0 +1,374 @@
+"""ODH mutating webhook: unit + in-process admission tests.
+
+Mirrors odh/controllers/notebook_webhook_test.go (ImageStream table with span-event
+assertions, kube-rbac-proxy resource configuration), auth_proxy_resources_test.go,
+notebook_feast_config_test.go, notebook_runtime_test.go (formatKeyName) and
+notebook_webhook_utils_test.go.
+"""
+
+import base64
+import json
+
+import pytest
+
+from odh_kubeflow_amd import tracing
+from odh_kubeflow_amd.apiserver.store import ObjectStore
+from odh_kubeflow_amd.controllers.odh import auth, feast, runtime_images
+from odh_kubeflow_amd.controllers.odh.constants import ANNOTATION_UPDATE_PENDING
+from odh_kubeflow_amd.models import kinds
+from odh_kubeflow_amd.models import meta as m
+from odh_kubeflow_amd.models.notebook import notebook
+from odh_kubeflow_amd.runtime.client import InProcessClient
+from odh_kubeflow_amd.utils import jsonpatch
+from odh_kubeflow_amd.webhook.diff import first_difference
+from odh_kubeflow_amd.webhook.notebook_webhook import NotebookWebhook, register_in_process
+
+PROXY_IMAGE = "quay.io/brancz/kube-rbac-proxy:v0.18.1"
+
+
+@pytest.fixture
+def exporter():
+    exp = tracing.InMemoryExporter()
+    tracing.set_tracer_provider(tracing.TracerProvider(exp))
+    yield exp
+    tracing.set_tracer_provider(None)
+
+
+@pytest.mark.parametrize("inp,exp", [
+    ("foo", "foo.json"), ("foo-bar", "foo-bar.json"), ("foo__bar", "foo__bar.json"),
+    ("FOO_-BAR-999", "foo_-bar-999.json"), ("some.name_with-numbers-123", "some.name_with-numbers-123.json"),
+    ("_leading_underscore", "_leading_underscore.json"), ("trailing_underscore_", "trailing_underscore_.json"),
+    ("_-_leading_and_trailing_", "_-_leading_and_trailing_.json"), ("@@@", ""), ("foo  bar", "foo-bar.json"),
+    ("!@#$%^&*()", ""), ("  leading and trailing spaces  ", "leading-and-trailing-spaces.json"),
+    (" !@#$ invalid chars & valid ones", "invalid-chars-valid-ones.json"), ("CZ ěščřžýáíé", "cz.json"),
+    ("  --FOO Bar--  ", "foo-bar.json"), ("", ""), ("-", ""), ("--", ""), (".", "..json"), ("_", "_.json"),
+    ("... ---___", "...-___.json"),
+])
+def test_format_key_name(inp, exp):
+    # table copied from odh/controllers/notebook_runtime_test.go:532-571
+    assert runtime_images.format_key_name(inp) == exp
+
+
+def test_parse_runtime_image_metadata():
+    raw = json.dumps([{"display_name": "PyTorch ROCm", "metadata": {"tags": ["pytorch"]}, "schema_name": "runtime-image"}])
+    out = json.loads(runtime_images.parse_runtime_image_metadata(raw, "quay.io/x/rocm-pt:2.10"))
+    assert out["metadata"]["image_name"] == "quay.io/x/rocm-pt:2.10"
+    assert runtime_images.parse_runtime_image_metadata("not json", "x") == "{}"
+    assert runtime_images.parse_runtime_image_metadata("[]", "x") == "{}"
+    assert runtime_images.extract_display_name(runtime_images.parse_runtime_image_metadata(raw, "u")) == "PyTorch ROCm"
+
+
+# ------------------------------------------------------------------ kube-rbac-proxy injection
+
+
+def test_inject_kube_rbac_proxy_defaults():
+    nb = notebook("nb", "ns", annotations={"notebooks.opendatahub.io/inject-auth": "true"})
+    auth.inject_kube_rbac_proxy(nb, PROXY_IMAGE)
+    spec = nb["spec"]["template"]["spec"]
+    assert [c["name"] for c in spec["containers"]] == ["nb", "kube-rbac-proxy"]
+    c = spec["containers"][1]
+    assert c["image"] == PROXY_IMAGE and c["imagePullPolicy"] == "Always"
+    assert c["resources"] == {"requests": {"cpu": "100m", "memory": "64Mi"}, "limits": {"cpu": "100m", "memory": "64Mi"}}
+    assert "--secure-listen-address=0.0.0.0:8443" in c["args"] and "--upstream=http://127.0.0.1:8888/" in c["args"]
+    assert len(c["args"]) == 11
+    assert c["ports"] == [{"name": "kube-rbac-proxy", "containerPort": 8443, "protocol": "TCP"}]
+    assert c["livenessProbe"]["httpGet"] == {"path": "/healthz", "port": 8444, "scheme": "HTTPS"}
+    assert c["readinessProbe"]["initialDelaySeconds"] == 5 and c["livenessProbe"]["initialDelaySeconds"] == 30
+    assert [v["name"] for v in spec["volumes"]] == ["kube-rbac-proxy-config", "kube-rbac-proxy-tls-certificates"]
+    assert spec["volumes"][0]["configMap"] == {"name": "nb-kube-rbac-proxy-config", "defaultMode": 420}
+    assert spec["volumes"][1]["secret"] == {"secretName": "nb-kube-rbac-proxy-tls", "defaultMode": 420}
+    assert spec["serviceAccountName"] == "nb"
+
+
+def test_inject_kube_rbac_proxy_custom_resources_and_update_in_place():
+    nb = notebook("nb", "ns", annotations={
+        "notebooks.opendatahub.io/auth-sidecar-cpu-request": "200m",
+        "notebooks.opendatahub.io/auth-sidecar-memory-request": "128Mi",
+        "notebooks.opendatahub.io/auth-sidecar-cpu-limit": "1",
+        "notebooks.opendatahub.io/auth-sidecar-memory-limit": "1Gi"})
+    nb["spec"]["template"]["spec"]["containers"].append({"name": "other", "image": "x"})
+    auth.inject_kube_rbac_proxy(nb, "old")
+    auth.inject_kube_rbac_proxy(nb, PROXY_IMAGE)  # updates, does not duplicate
+    cs = nb["spec"]["template"]["spec"]["containers"]
+    assert [c["name"] for c in cs] == ["nb", "other", "kube-rbac-proxy"]
+    assert cs[2]["image"] == PROXY_IMAGE
+    assert cs[2]["resources"] == {"requests": {"cpu": "200m", "memory": "128Mi"}, "limits": {"cpu": "1", "memory": "1Gi"}}
+    assert len(nb["spec"]["template"]["spec"]["volumes"]) == 2
+
+
+@pytest.mark.parametrize("ann,msg", [
+    ({"notebooks.opendatahub.io/auth-sidecar-cpu-request": "abc"}, "invalid value"),
+    ({"notebooks.opendatahub.io/auth-sidecar-memory-limit": "-1Mi"}, "cannot be negative"),
+    ({"notebooks.opendatahub.io/auth-sidecar-cpu-request": "2"}, "CPU request"),
+    ({"notebooks.opendatahub.io/auth-sidecar-memory-request": "1Gi"}, "memory request"),
+])
+def test_inject_kube_rbac_proxy_validation_leaves_notebook_untouched(ann, msg):
+    nb = notebook("nb", "ns", annotations=ann)
+    before = json.dumps(nb, sort_keys=True)
+    with pytest.raises(auth.SidecarResourceError, match=msg):
+        auth.inject_kube_rbac_proxy(nb, PROXY_IMAGE)
+    assert json.dumps(nb, sort_keys=True) == before
+
+
+def test_injection_enabled_parse_bool():
+    for v, want in (("true", True), ("True", True), ("1", True), ("t", True), ("false", False), ("yes", False),
+                    ("", False)):
+        assert auth.kube_rbac_proxy_injection_enabled(
+            notebook("n", "s", annotations={"notebooks.opendatahub.io/inject-auth": v})) is want
+
+
+# ------------------------------------------------------------------ feast
+
+
+def test_feast_mount_update_unmount():
+    nb = notebook("nb", "ns", labels={"opendatahub.io/feast-integration": "true"})
+    assert feast.is_feast_enabled(nb) and not feast.is_feast_mounted(nb)
+    feast.new_feast_config(nb)
+    feast.new_feast_config(nb)
+    spec = nb["spec"]["template"]["spec"]
+    assert spec["volumes"] == [{"name": "odh-feast-config", "configMap": {"name": "nb-feast-config"}}]
+    assert spec["containers"][0]["volumeMounts"] == [
+        {"name": "odh-feast-config", "readOnly": True, "mountPath": "/opt/app-root/src/feast-config"}]
+    feast.unmount_feast_config(nb)
+    assert spec["volumes"] == [] and spec["containers"][0]["volumeMounts"] == []
+    for v in ("false", "TRUE", "yes"):
+        assert not feast.is_feast_enabled(notebook("nb", "ns", labels={"opendatahub.io/feast-integration": v}))
+    bad = notebook("nb", "ns", container_name="other")
+    with pytest.raises(ValueError):
+        feast.new_feast_config(bad)
+
+
+# ------------------------------------------------------------------ diff
+
+
+def test_first_difference():
+    a = {"containers": [{"name": "x", "image": "a"}]}
+    b = {"containers": [{"name": "x", "image": "b"}]}
+    assert first_difference(a, b) == 'PodSpec.containers[0].image: "a" != "b"'
+    assert first_difference(a, a) == ""
+    assert "<missing>" in first_difference({"a": 1}, {})
+
+
+# ------------------------------------------------------------------ admission through the apiserver
+
+
+def _imagestream(name, ns, tag="some-tag", ref="quay.io/img@sha256:abc", created="2024-10-03T08:10:22Z", items=True):
+    return {"apiVersion": "image.openshift.io/v1", "kind": "ImageStream", "metadata": {"name": name, "namespace": ns},
+            "spec": {"tags": [{"name": tag}]},
+            "status": {"tags": [{"tag": tag, "items": ([{"created": created, "dockerImageReference": ref}]
+                                                       if items else None)}]}}
+
+
+async def create_with_status(admin, obj):
+    status = obj.pop("status", None)
+    created = await admin.create(obj)
+    if status is not None:
+        created["status"] = status
+        await admin.update_status(created)
+    return created
+
+
+async def _setup(env=None):
+    store = ObjectStore()
+    admin = InProcessClient(store)
+    for ns in ("opendatahub", "user", "ws-ns"):
+        await admin.create({"apiVersion": "v1", "kind": "Namespace", "metadata": {"name": ns}})
+    wh = NotebookWebhook(InProcessClient(store), "opendatahub", PROXY_IMAGE, env=env or {})
+    register_in_process(store, wh)
+    return store, admin, wh
+
+
+@pytest.mark.parametrize("case", [
+    dict(name="resolved from controller namespace", streams=[("some-image", "opendatahub", True)],
+         ann={"notebooks.opendatahub.io/last-image-selection": "some-image:some-tag"},
+         image="quay.io/img@sha256:abc", events=[], unexpected=["imagestream-not-found", "imagestream-tag-not-found"]),
+    dict(name="tag without items (RHOAIENG-13916)", streams=[("some-image", "opendatahub", False)],
+         ann={"notebooks.opendatahub.io/last-image-selection": "some-image:some-tag"},
+         image=":some-tag", events=["imagestream-tag-not-found"], unexpected=["imagestream-not-found"]),
+    dict(name="imagestream missing", streams=[],
+         ann={"notebooks.opendatahub.io/last-image-selection": "some-image:some-tag"},
+         image=":some-tag", events=["imagestream-not-found"], unexpected=["imagestream-tag-not-found"]),
+    dict(name="workbench-image-namespace set", streams=[("some-image", "ws-ns", True)],
+         ann={"notebooks.opendatahub.io/last-image-selection": "some-image:some-tag",
+              "opendatahub.io/workbench-image-namespace": "ws-ns"},
+         image="quay.io/img@sha256:abc", events=[], unexpected=["imagestream-not-found"]),
+    dict(name="workbench-image-namespace empty -> controller namespace", streams=[("some-image", "opendatahub", True)],
+         ann={"notebooks.opendatahub.io/last-image-selection": "some-image:some-tag",
+              "opendatahub.io/workbench-image-namespace": "  "},
+         image="quay.io/img@sha256:abc", events=[], unexpected=["imagestream-not-found"]),
+    dict(name="no selection annotation", streams=[("some-image", "opendatahub", True)], ann={},
+         image=":some-tag", events=[], unexpected=["imagestream-not-found", "imagestream-tag-not-found"]),
+    dict(name="internal registry image kept", streams=[("some-image", "opendatahub", True)],
+         ann={"notebooks.opendatahub.io/last-image-selection": "some-image:some-tag"},
+         image="image-registry.openshift-image-registry.svc:5000/x/y:z", events=[], unexpected=[]),
+], ids=lambda c: c["name"])
+def test_webhook_imagestream_table(run, exporter, case):
+    async def go():
+        store, admin, _ = await _setup()
+        for (n, ns, items) in case["streams"]:
+            await create_with_status(admin, _imagestream(n, ns, items=items))
+        start_image = case["image"] if "internal" in case["name"] else ":some-tag"
+        nb = notebook("nb", "user", image=start_image, annotations=case["ann"],
+                      extra_container={"env": [{"name": "JUPYTER_IMAGE", "value": "old"}]})
+        await admin.create(nb)
+        stored = store.peek(kinds.NOTEBOOK, "nb", "user")
+        assert stored["spec"]["template"]["spec"]["containers"][0]["image"] == case["image"]
+        # reconciliation lock injected on CREATE
+        assert m.annotations(stored)["kubeflow-resource-stopped"] == "odh-notebook-controller-lock"
+        evs = exporter.events("handleFunc")
+        for e in case["events"]:
+            assert e in evs
+        for e in case["unexpected"]:
+            assert e not in evs
+        if case["image"] == "quay.io/img@sha256:abc":
+            env = stored["spec"]["template"]["spec"]["containers"][0]["env"]
+            assert {"name": "JUPYTER_IMAGE", "value": "some-image:some-tag"} in env
+        spans = [s.name for s in exporter.get_finished_spans()]
+        assert "handleFunc" in spans and "maybeRestartRunningNotebook" in spans
+    run(go())
+
+
+def test_webhook_newest_tag_item_wins(run):
+    async def go():
+        store, admin, _ = await _setup()
+        ist = _imagestream("img", "opendatahub")
+        ist["status"]["tags"][0]["items"] = [
+            {"created": "2024-01-01T00:00:00Z", "dockerImageReference": "old"},
+            {"created": "2025-01-01T00:00:00Z", "dockerImageReference": "new"},
+            {"created": "2023-01-01T00:00:00Z", "dockerImageReference": "older"}]
+        await create_with_status(admin, ist)
+        await admin.create(notebook("nb", "user", annotations={
+            "notebooks.opendatahub.io/last-image-selection": "img:some-tag"}))
+        assert store.peek(kinds.NOTEBOOK, "nb", "user")["spec"]["template"]["spec"]["containers"][0]["image"] == "new"
+    run(go())
+
+
+def test_webhook_invalid_selection_denies(run):
+    async def go():
+        store, admin, _ = await _setup()
+        with pytest.raises(Exception, match="denied the request"):
+            await admin.create(notebook("nb", "user", annotations={
+                "notebooks.opendatahub.io/last-image-selection": "no-colon"}))
+        with pytest.raises(Exception, match="cannot be negative"):
+            await admin.create(notebook("nb", "user", annotations={
+                "notebooks.opendatahub.io/inject-auth": "true",
+                "notebooks.opendatahub.io/auth-sidecar-cpu-limit": "-1"}))
+        assert store.peek(kinds.NOTEBOOK, "nb", "user") is None
+    run(go())
+
+
+def test_webhook_runtime_images_created_and_mounted_on_first_notebook(run):
+    # RHOAIENG-24545: the webhook creates the ConfigMap before mounting it
+    async def go():
+        store, admin, _ = await _setup()
+        ist = _imagestream("rt", "opendatahub")
+        ist["metadata"]["labels"] = {"opendatahub.io/runtime-image": "true"}
+        ist["spec"]["tags"] = [{"name": "t", "from": {"kind": "DockerImage", "name": "quay.io/rt:1"},
+                                "annotations": {"opendatahub.io/runtime-image-metadata": json.dumps(
+                                    [{"display_name": "ROCm PyTorch 2.10", "metadata": {"x": 1}}])}}]
+        await admin.create(ist)
+        nb = notebook("nb", "user")
+        nb["spec"]["template"]["spec"]["containers"].append({"name": "side", "image": "s"})
+        await admin.create(nb)
+        cm = store.peek(kinds.CONFIG_MAP, "pipeline-runtime-images", "user")
+        assert set(cm["data"]) == {"rocm-pytorch-2.10.json"}
+        assert json.loads(cm["data"]["rocm-pytorch-2.10.json"])["metadata"]["image_name"] == "quay.io/rt:1"
+        assert m.labels(cm) == {"opendatahub.io/managed-by": "workbenches"}
+        spec = store.peek(kinds.NOTEBOOK, "nb", "user")["spec"]["template"]["spec"]
+        assert {"name": "runtime-images", "configMap": {"name": "pipeline-runtime-images", "optional": True}} in spec["volumes"]
+        for c in spec["containers"]:  # mounted on ALL containers
+            assert {"name": "runtime-images", "mountPath": "/opt/app-root/pipeline-runtimes/"} in c["volumeMounts"]
+    run(go())
+
+
+def test_webhook_ca_bundle_mount(run):
+    async def go():
+        store, admin, _ = await _setup()
+        await admin.create({"apiVersion": "v1", "kind": "ConfigMap",
+                            "metadata": {"name": "odh-trusted-ca-bundle", "namespace": "user"},
+                            "data": {"ca-bundle.crt": "PEM"}})
+        await admin.create(notebook("nb", "user", extra_container={"env": [{"name": "PIP_CERT", "value": "/mine"}]}))
+        wb = store.peek(kinds.CONFIG_MAP, "workbench-trusted-ca-bundle", "user")
+        assert wb["data"] == {"ca-bundle.crt": "PEM"}
+        spec = store.peek(kinds.NOTEBOOK, "nb", "user")["spec"]["template"]["spec"]
+        assert {"name": "trusted-ca", "configMap": {"name": "workbench-trusted-ca-bundle", "optional": True,
+                                                     "items": [{"key": "ca-bundle.crt", "path": "ca-bundle.crt"}]}} \
+            in spec["volumes"]
+        c = spec["containers"][0]
+        envs = {e["name"]: e["value"] for e in c["env"]}
+        assert envs["PIP_CERT"] == "/mine"  # an existing value is kept (reference range-copy behaviour)
+        for k in ("REQUESTS_CA_BUNDLE", "SSL_CERT_FILE", "PIPELINES_SSL_SA_CERTS", "KF_PIPELINES_SSL_SA_CERTS",
+                  "GIT_SSL_CAINFO"):
+            assert envs[k] == "/etc/pki/tls/custom-certs/ca-bundle.crt"
+        assert {"name": "trusted-ca", "readOnly": True, "mountPath": "/etc/pki/tls/custom-certs/ca-bundle.crt",
+                "subPath": "ca-bundle.crt"} in c["volumeMounts"]
+    run(go())
+
+
+def test_webhook_cluster_proxy_env(run):
+    async def go():
+        store, admin, _ = await _setup(env={"INJECT_CLUSTER_PROXY_ENV": "true"})
+        await create_with_status(admin, {"apiVersion": "config.openshift.io/v1", "kind": "Proxy",
+                                         "metadata": {"name": "cluster"},
+                                         "status": {"httpProxy": "http://p:3128", "httpsProxy": "http://p:3129",
+                                                    "noProxy": ".svc"}})
+        await admin.create(notebook("nb", "user"))
+        env = {e["name"]: e["value"] for e in store.peek(kinds.NOTEBOOK, "nb", "user")["spec"]["template"]["spec"]
+               ["containers"][0]["env"]}
+        assert env["HTTP_PROXY"] == "http://p:3128" and env["HTTPS_PROXY"] == "http://p:3129" and env["NO_PROXY"] == ".svc"
+        # not injected when INJECT_CLUSTER_PROXY_ENV is unparsable
+        store2, admin2, _ = await _setup(env={"INJECT_CLUSTER_PROXY_ENV": "maybe"})
+        await create_with_status(admin2, {"apiVersion": "config.openshift.io/v1", "kind": "Proxy",
+                                          "metadata": {"name": "cluster"},
+                                          "status": {"httpProxy": "a", "httpsProxy": "b", "noProxy": "c"}})
+        await admin2.create(notebook("nb", "user"))
+        c = store2.peek(kinds.NOTEBOOK, "nb", "user")["spec"]["template"]["spec"]["containers"][0]
+        assert not any(e["name"] == "HTTP_PROXY" for e in c.get("env") or [])
+    run(go())
+
+
+def test_restart_guard_blocks_webhook_only_changes(run):
+    async def go():
+        store, admin, wh = await _setup()
+        await admin.create(notebook("nb", "user", annotations={"notebooks.opendatahub.io/inject-auth": "true"}))
+        # running notebook: lock removed
+        await admin.patch(kinds.NOTEBOOK, {"metadata": {"annotations": {"kubeflow-resource-stopped": None}}},
+                          name="nb", namespace="user")
+        before = store.peek(kinds.NOTEBOOK, "nb", "user")["spec"]["template"]["spec"]
+        # the proxy image is upgraded: a metadata-only user update must not restart the pod
+        wh.kube_rbac_proxy_image = "quay.io/brancz/kube-rbac-proxy:v0.19.0"
+        await admin.patch(kinds.NOTEBOOK, {"metadata": {"labels": {"x": "y"}}}, name="nb", namespace="user")
+        nb = store.peek(kinds.NOTEBOOK, "nb", "user")
+        assert nb["spec"]["template"]["spec"] == before
+        assert "kube-rbac-proxy" in m.annotations(nb)[ANNOTATION_UPDATE_PENDING]
+        assert "v0.19.0" in m.annotations(nb)[ANNOTATION_UPDATE_PENDING]
+        # a user change of the pod template lets everything through and clears the marker
+        await admin.patch(kinds.NOTEBOOK, {"spec": {"template": {"spec": {"containers": [
+            {"name": "nb", "image": "rocm/pytorch:new"}]}}}}, name="nb", namespace="user", patch_type="merge")
+        nb = store.peek(kinds.NOTEBOOK, "nb", "user")
+        imgs = [c["image"] for c in nb["spec"]["template"]["spec"]["containers"]]
+        assert "quay.io/brancz/kube-rbac-proxy:v0.19.0" in imgs and "rocm/pytorch:new" in imgs
+        assert ANNOTATION_UPDATE_PENDING not in m.annotations(nb)
+        # stopped notebooks are updated freely
+        wh.kube_rbac_proxy_image = "quay.io/brancz/kube-rbac-proxy:v0.20.0"
+        await admin.patch(kinds.NOTEBOOK, {"metadata": {"annotations": {"kubeflow-resource-stopped": "x"}}},
+                          name="nb", namespace="user")
+        nb = store.peek(kinds.NOTEBOOK, "nb", "user")
+        assert "quay.io/brancz/kube-rbac-proxy:v0.20.0" in [c["image"] for c in nb["spec"]["template"]["spec"]["containers"]]
+    run(go())
+
+
+def test_admission_review_json_patch_roundtrip(run):
+    async def go():
+        store, admin, wh = await _setup()
+        obj = notebook("nb", "user", annotations={"notebooks.opendatahub.io/inject-auth": "true"})
+        obj["metadata"]["uid"] = "u1"
+        out = await wh.handle({"apiVersion": "admission.k8s.io/v1", "kind": "AdmissionReview",
+                               "request": {"uid": "r1", "operation": "CREATE", "object": obj}})
+        resp = out["response"]
+        assert resp["uid"] == "r1" and resp["allowed"] and resp["patchType"] == "JSONPatch"
+        patched = jsonpatch.apply_patch(obj, json.loads(base64.b64decode(resp["patch"])))
+        assert [c["name"] for c in patched["spec"]["template"]["spec"]["containers"]] == ["nb", "kube-rbac-proxy"]
+        bad = await wh.handle({"request": {"uid": "r2", "operation": "CREATE"}})
+        assert bad["response"]["allowed"] is False and bad["response"]["status"]["code"] == 400
+    run(go())

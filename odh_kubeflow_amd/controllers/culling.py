@@ -1,0 +1,466 @@
+"""Idle-notebook culler (reference ``kf/controllers/culling_controller.go``), with an
+MI355X GPU-busy activity signal.
+
+Annotation protocol — identical to the reference so existing tooling keeps working:
+
+* ``notebooks.kubeflow.org/last-activity`` — RFC3339 of the last observed activity;
+* ``notebooks.kubeflow.org/last_activity_check_timestamp`` — RFC3339 of the last check;
+* ``kubeflow-resource-stopped`` = RFC3339 when culled (the kf reconciler then scales the
+  StatefulSet to 0; removing the annotation resumes the notebook).
+
+Per reconcile (:86-203): stopped → strip the two activity annotations; pod ``<nb>-0``
+missing → strip them; initialise them; skip until ``IDLENESS_CHECK_PERIOD`` has passed
+since the last check; sample activity; in one ``RetryOnConflict`` update set
+last-activity, the check timestamp and — if idle for longer than ``CULL_IDLE_TIME`` —
+the stop annotation; ``RequeueAfter(IDLENESS_CHECK_PERIOD)``.
+
+Activity sources (``CULLING_ACTIVITY_SOURCE``):
+
+* ``jupyter`` (default, the reference): ``GET .../api/kernels`` and ``.../api/terminals``
+  (10 s timeout each); any non-idle kernel means "active now", otherwise the newest
+  kernel/terminal ``last_activity`` is taken if it is newer than the annotation;
+* ``amdgpu``: the notebook's GPUs (``amd.com/gpu-ids`` written by the device allocator)
+  are sampled by the node agent's native amdgpu telemetry; a mean busy percentage over
+  the last check period at or above ``CULLING_GPU_BUSY_THRESHOLD`` (default 5) means
+  "active now".  Averaging over the whole window is the hysteresis: a single spike does
+  not keep a notebook alive and a single idle sample does not cull it;
+* ``combined``: active if either signal says so.
+
+Missing telemetry is never read as idleness: with no GPU samples the Jupyter signal is
+used, and with neither the last-activity annotation is simply left alone (as the
+reference does for HTTP errors, :258-270).
+
+Fixes over the reference: the two culling metrics are exported; the configuration is
+an object (no package globals); sub-minute periods are available through
+``IDLENESS_CHECK_PERIOD_SECONDS`` / ``CULL_IDLE_TIME_SECONDS`` for tests and benchmarks.
+"""
+
+from __future__ import annotations
+
+import asyncio
+import json
+import logging
+import os
+from dataclasses import dataclass
+from typing import Any, Callable, List, Mapping, Optional, Sequence
+
+from ..models import kinds
+from ..models import meta as m
+from ..models.errors import ApiError, is_not_found
+from ..models.notebook import (GPU_IDS_ANNOTATION, LAST_ACTIVITY_ANNOTATION, LAST_ACTIVITY_CHECK_TIMESTAMP_ANNOTATION,
+                               STOP_ANNOTATION)
+from ..runtime.controller import Request, Result
+from ..runtime.retry import retry_on_conflict
+from ..utils.timeutil import now, parse_rfc3339, rfc3339
+
+log = logging.getLogger("controllers.Culler")
+
+DEFAULT_CULL_IDLE_TIME = "1440"
+DEFAULT_IDLENESS_CHECK_PERIOD = "1"
+DEFAULT_CLUSTER_DOMAIN = "cluster.local"
+KERNEL_IDLE, KERNEL_BUSY, KERNEL_STARTING = "idle", "busy", "starting"
+
+
+def env_default(env: Mapping[str, str], key: str, default: str) -> str:
+    v = env.get(key)
+    return v if v else default
+
+
+@dataclass
+class CullerConfig:
+    cull_idle_time_s: float = 1440 * 60.0
+    check_period_s: float = 60.0
+    enable_culling: bool = False
+    cluster_domain: str = DEFAULT_CLUSTER_DOMAIN
+    dev: bool = False
+    activity_source: str = "jupyter"
+    gpu_busy_threshold: float = 5.0
+    http_timeout_s: float = 10.0
+
+    @classmethod
+    def from_env(cls, env: Mapping[str, str] = os.environ) -> "CullerConfig":
+        """``initGlobalVars`` (:525-558): a bad CULL_IDLE_TIME falls back to the default,
+        a bad IDLENESS_CHECK_PERIOD is an error."""
+        c = cls()
+        c.dev = env_default(env, "DEV", "false") == "true"
+        raw = env_default(env, "CULL_IDLE_TIME", DEFAULT_CULL_IDLE_TIME)
+        try:
+            c.cull_idle_time_s = int(raw) * 60.0
+        except ValueError:
+            log.info("CULL_IDLE_TIME should be Int. Got %s instead. Using default value.", raw)
+            c.cull_idle_time_s = int(DEFAULT_CULL_IDLE_TIME) * 60.0
+        c.enable_culling = env_default(env, "ENABLE_CULLING", "false") == "true"
+        c.cluster_domain = env_default(env, "CLUSTER_DOMAIN", DEFAULT_CLUSTER_DOMAIN)
+        c.check_period_s = int(env_default(env, "IDLENESS_CHECK_PERIOD", DEFAULT_IDLENESS_CHECK_PERIOD)) * 60.0
+        if env.get("IDLENESS_CHECK_PERIOD_SECONDS"):
+            c.check_period_s = float(env["IDLENESS_CHECK_PERIOD_SECONDS"])
+        if env.get("CULL_IDLE_TIME_SECONDS"):
+            c.cull_idle_time_s = float(env["CULL_IDLE_TIME_SECONDS"])
+        c.activity_source = env_default(env, "CULLING_ACTIVITY_SOURCE", "jupyter").strip().lower()
+        if c.activity_source not in ("jupyter", "amdgpu", "combined"):
+            raise ValueError(f"CULLING_ACTIVITY_SOURCE must be jupyter|amdgpu|combined, got {c.activity_source}")
+        c.gpu_busy_threshold = float(env_default(env, "CULLING_GPU_BUSY_THRESHOLD", "5"))
+        return c
+
+
+# ------------------------------------------------------------------ pure helpers (unit-tested like the reference)
+
+
+def stop_annotation_is_set(nb: dict) -> bool:
+    return STOP_ANNOTATION in m.annotations(nb)
+
+
+def annotations_exist(nb: dict) -> bool:
+    a = m.annotations(nb)
+    return LAST_ACTIVITY_ANNOTATION in a and LAST_ACTIVITY_CHECK_TIMESTAMP_ANNOTATION in a
+
+
+def initialize_annotations(nb: dict) -> None:
+    t = rfc3339()
+    a = m.ensure_annotations(nb)
+    a[LAST_ACTIVITY_ANNOTATION] = t
+    a[LAST_ACTIVITY_CHECK_TIMESTAMP_ANNOTATION] = t
+
+
+def remove_annotations(nb: dict) -> None:
+    a = (nb.get("metadata") or {}).get("annotations")
+    if a:
+        a.pop(LAST_ACTIVITY_ANNOTATION, None)
+        a.pop(LAST_ACTIVITY_CHECK_TIMESTAMP_ANNOTATION, None)
+
+
+def culling_check_period_has_passed(nb: dict, period_s: float) -> bool:
+    raw = m.annotations(nb).get(LAST_ACTIVITY_CHECK_TIMESTAMP_ANNOTATION)
+    if raw is None:
+        return False
+    t = parse_rfc3339(raw)
+    if t is None:
+        t = -62135596800.0  # Go zero time: an unparsable stamp is "long ago"
+    return t + period_s < now()
+
+
+def notebook_is_idle(nb: dict, idle_s: float) -> bool:
+    if stop_annotation_is_set(nb):
+        return False
+    t = parse_rfc3339(m.annotations(nb).get(LAST_ACTIVITY_ANNOTATION))
+    if t is None:
+        return False
+    return now() > t + idle_s
+
+
+def all_kernels_are_idle(kernels: Sequence[dict]) -> bool:
+    return all(k.get("execution_state") == KERNEL_IDLE for k in kernels)
+
+
+def most_recent_time(times: Sequence[str]) -> str:
+    best = None
+    for s in times:
+        t = parse_rfc3339(s)
+        if t is None:
+            return ""
+        if best is None or t > best:
+            best = t
+    return rfc3339(best) if best is not None else ""
+
+
+def annotation_not_after(nb: dict, resource_time: str) -> bool:
+    """``compareAnnotationTimeToResource``: True unless the annotation is newer."""
+    a = parse_rfc3339(m.annotations(nb).get(LAST_ACTIVITY_ANNOTATION))
+    t = parse_rfc3339(resource_time)
+    if a is None or t is None:
+        return False
+    return not a > t
+
+
+def update_from_kernels(nb: dict, kernels: Optional[Sequence[dict]]) -> bool:
+    if not kernels:
+        return False
+    if not all_kernels_are_idle(kernels):
+        m.ensure_annotations(nb)[LAST_ACTIVITY_ANNOTATION] = rfc3339()
+        return False
+    t = most_recent_time([k.get("last_activity", "") for k in kernels])
+    if not t or not annotation_not_after(nb, t):
+        return False
+    m.ensure_annotations(nb)[LAST_ACTIVITY_ANNOTATION] = t
+    return True
+
+
+def update_from_terminals(nb: dict, terminals: Optional[Sequence[dict]]) -> bool:
+    if not terminals:
+        return False
+    t = most_recent_time([x.get("last_activity", "") for x in terminals])
+    if not t or not annotation_not_after(nb, t):
+        return False
+    m.ensure_annotations(nb)[LAST_ACTIVITY_ANNOTATION] = t
+    return True
+
+
+def update_check_timestamp(nb: dict) -> None:
+    m.ensure_annotations(nb)[LAST_ACTIVITY_CHECK_TIMESTAMP_ANNOTATION] = rfc3339()
+
+
+def set_stop_annotation(nb: dict, metrics=None) -> None:
+    t = now()
+    m.ensure_annotations(nb)[STOP_ANNOTATION] = rfc3339(t)
+    if metrics is not None:
+        metrics.notebook_culling_count.labels(m.namespace(nb), m.name(nb)).inc()
+        metrics.notebook_culling_timestamp.labels(m.namespace(nb), m.name(nb)).set(int(t))
+
+
+def pod_gpu_ids(pod: Optional[dict]) -> List[int]:
+    raw = m.annotations(pod or {}).get(GPU_IDS_ANNOTATION) or ""
+    return [int(x) for x in raw.split(",") if x.strip().isdigit()]
+
+
+# ------------------------------------------------------------------ activity sources
+
+
+class JupyterActivity:
+    """``getNotebookApiKernels`` / ``getNotebookApiTerminals`` over HTTP (10 s timeout).
+
+    ``url_for(nb_name, namespace, resource, pod)`` may be overridden; by default it is the
+    in-cluster Service URL, or the ``kubectl proxy`` URL in ``DEV`` mode (:243-273).  With
+    ``use_pod_endpoint`` the node agent's ``amd.com/notebook-endpoint`` pod annotation is
+    used (the in-process runtime serves the Jupyter API on an ephemeral port).
+    """
+
+    def __init__(self, cfg: CullerConfig, url_for: Optional[Callable[..., str]] = None,
+                 use_pod_endpoint: bool = False):
+        self.cfg = cfg
+        self.url_for = url_for or self.default_url
+        self.use_pod_endpoint = use_pod_endpoint
+        self._session = None
+        self.requests = 0
+
+    def default_url(self, nm: str, ns: str, resource: str, pod: Optional[dict] = None) -> str:
+        if self.use_pod_endpoint and pod is not None:
+            ep = m.annotations(pod).get("amd.com/notebook-endpoint")
+            if ep:
+                return f"http://{ep}/notebook/{ns}/{nm}/api/{resource}"
+        if self.cfg.dev:
+            return (f"http://localhost:8001/api/v1/namespaces/{ns}/services/{nm}:http-{nm}/proxy/notebook/"
+                    f"{ns}/{nm}/api/{resource}")
+        return f"http://{nm}.{ns}.svc.{self.cfg.cluster_domain}/notebook/{ns}/{nm}/api/{resource}"
+
+    async def _get(self, url: str) -> Optional[Any]:
+        import aiohttp
+
+        if self._session is None or self._session.closed:
+            self._session = aiohttp.ClientSession(timeout=aiohttp.ClientTimeout(total=self.cfg.http_timeout_s))
+        self.requests += 1
+        try:
+            async with self._session.get(url) as resp:
+                if resp.status != 200:
+                    log.info("Warning: GET to %s: %d", url, resp.status)
+                    return None
+                return json.loads(await resp.read())
+        except (asyncio.TimeoutError, OSError, ValueError, Exception) as e:  # noqa: B014 - any failure is "no data"
+            log.debug("GET %s failed: %r", url, e)
+            return None
+
+    async def sample(self, nb: dict, pod: Optional[dict]):
+        nm, ns = m.name(nb), m.namespace(nb)
+        kernels, terminals = await asyncio.gather(self._get(self.url_for(nm, ns, "kernels", pod)),
+                                                  self._get(self.url_for(nm, ns, "terminals", pod)))
+        return (kernels if isinstance(kernels, list) else None), (terminals if isinstance(terminals, list) else None)
+
+    async def close(self) -> None:
+        if self._session is not None:
+            await self._session.close()
+
+
+class GpuActivity:
+    """Base class: mean/max busy percentage of the given node GPUs over ``window_s``.
+
+    Returns ``None`` when no sample could be read (never interpreted as idle).
+    """
+
+    async def busy(self, pod: dict, devices: Sequence[int], window_s: float) -> Optional[dict]:
+        raise NotImplementedError
+
+    async def close(self) -> None:
+        return None
+
+
+class LocalTelemetryActivity(GpuActivity):
+    """Reads an in-process :class:`~odh_kubeflow_amd.ops.telemetry.Telemetry` (single-node setups)."""
+
+    def __init__(self, telemetry, index_of: Optional[Callable[[int], Optional[int]]] = None):
+        self.telemetry = telemetry
+        self.index_of = index_of or (lambda d: d)
+
+    async def busy(self, pod, devices, window_s):
+        return aggregate_windows(self.telemetry, [self.index_of(d) for d in devices], window_s)
+
+
+class NodeAgentActivity(GpuActivity):
+    """Asks the node agent that owns the pod's GPUs (``/gpu/activity`` on the Node's
+    ``amd.com/gpu-activity-port``); the telemetry lives next to the GPUs, not here."""
+
+    def __init__(self, reader, timeout_s: float = 2.0):
+        self.reader = reader
+        self.timeout_s = timeout_s
+        self._session = None
+
+    async def busy(self, pod, devices, window_s):
+        import aiohttp
+
+        node = self.reader.get(kinds.NODE, (pod.get("spec") or {}).get("nodeName", ""))
+        if node is None:
+            return None
+        port = m.annotations(node).get("amd.com/gpu-activity-port")
+        addr = next((a.get("address") for a in (node.get("status") or {}).get("addresses") or []
+                     if a.get("type") == "InternalIP"), None)
+        if not port or not addr:
+            return None
+        if self._session is None or self._session.closed:
+            self._session = aiohttp.ClientSession(timeout=aiohttp.ClientTimeout(total=self.timeout_s))
+        url = f"http://{addr}:{port}/gpu/activity?devices={','.join(map(str, devices))}&window={window_s}"
+        try:
+            async with self._session.get(url) as resp:
+                if resp.status != 200:
+                    return None
+                data = await resp.json()
+        except Exception:
+            return None
+        return data if data and data.get("n", 0) > 0 else None
+
+    async def close(self):
+        if self._session is not None:
+            await self._session.close()
+
+
+def aggregate_windows(telemetry, indices: Sequence[Optional[int]], window_s: float) -> Optional[dict]:
+    """Combine per-device windows: the notebook is as busy as its busiest GPU."""
+    best = None
+    n = 0
+    for idx in indices:
+        if idx is None:
+            continue
+        w = telemetry.window(idx, window_s)
+        if w is None or w.n == 0 or w.busy_mean < 0:
+            continue
+        n += w.n
+        cand = {"busy_mean": w.busy_mean, "busy_max": w.busy_max, "vram_used_mean": w.vram_used_mean}
+        if best is None or cand["busy_mean"] > best["busy_mean"]:
+            best = cand
+    if best is None:
+        return None
+    best["n"] = n
+    return best
+
+
+# ------------------------------------------------------------------ reconciler
+
+
+class CullingReconciler:
+    NAME = "Culler"
+
+    def __init__(self, client, reader, metrics=None, env: Optional[Mapping[str, str]] = None, activity=None,
+                 config: Optional[CullerConfig] = None, jupyter: Optional[JupyterActivity] = None):
+        self.client = client
+        self.reader = reader
+        self.metrics = metrics
+        self.env = env if env is not None else os.environ
+        self.cfg = config or CullerConfig.from_env(self.env)
+        self.gpu: Optional[GpuActivity] = activity
+        if self.gpu is None and self.cfg.activity_source in ("amdgpu", "combined"):
+            self.gpu = NodeAgentActivity(reader)
+        self.jupyter = jupyter or JupyterActivity(self.cfg, use_pod_endpoint=self.env.get(
+            "CULLER_USE_POD_ENDPOINT", "false") == "true")
+        self.culled = 0
+        self.checks = 0
+        from collections import deque
+        self.recent = deque(maxlen=64)  # (time, notebook, gpu_active, kernels, terminals) — debugging aid
+
+    async def _update(self, req: Request, mutate: Callable[[dict], None]) -> None:
+        async def fn():
+            cur = await self.client.get(kinds.NOTEBOOK_V1BETA1, req.name, req.namespace)
+            mutate(cur)
+            await self.client.update(cur)
+
+        await retry_on_conflict(fn)
+
+    async def reconcile(self, req: Request) -> Result:
+        try:
+            nb = await self.client.get(kinds.NOTEBOOK_V1BETA1, req.name, req.namespace)
+        except ApiError as e:
+            if is_not_found(e):
+                return Result()
+            raise
+        if m.is_deleting(nb):
+            return Result()
+        if stop_annotation_is_set(nb):
+            if annotations_exist(nb) or any(k in m.annotations(nb) for k in (
+                    LAST_ACTIVITY_ANNOTATION, LAST_ACTIVITY_CHECK_TIMESTAMP_ANNOTATION)):
+                await self._update(req, remove_annotations)
+            return Result()
+        pod = await self.client.get_or_none(kinds.POD, m.name(nb) + "-0", req.namespace)
+        if pod is None:
+            if any(k in m.annotations(nb) for k in (LAST_ACTIVITY_ANNOTATION, LAST_ACTIVITY_CHECK_TIMESTAMP_ANNOTATION)):
+                await self._update(req, remove_annotations)
+            return Result()
+        if not annotations_exist(nb):
+            await self._update(req, initialize_annotations)
+            nb = await self.client.get(kinds.NOTEBOOK_V1BETA1, req.name, req.namespace)
+        if not culling_check_period_has_passed(nb, self.cfg.check_period_s):
+            return Result(requeue_after=self.cfg.check_period_s)
+
+        self.checks += 1
+        active_now, kernels, terminals = await self.sample(nb, pod)
+        self.recent.append((rfc3339(), str(req), active_now, kernels, terminals))
+
+        def apply(cur: dict) -> None:
+            if active_now:
+                m.ensure_annotations(cur)[LAST_ACTIVITY_ANNOTATION] = rfc3339()
+            else:
+                update_from_kernels(cur, kernels)
+                update_from_terminals(cur, terminals)
+            update_check_timestamp(cur)
+            if notebook_is_idle(cur, self.cfg.cull_idle_time_s):
+                log.info("Notebook %s/%s needs culling", req.namespace, req.name)
+                set_stop_annotation(cur, self.metrics)
+                self.culled += 1
+
+        await self._update(req, apply)
+        return Result(requeue_after=self.cfg.check_period_s)
+
+    async def sample(self, nb: dict, pod: dict):
+        """Returns ``(gpu_says_active, kernels, terminals)``."""
+        src = self.cfg.activity_source
+        gpu_active = False
+        gpu_data = None
+        if src in ("amdgpu", "combined") and self.gpu is not None:
+            devs = pod_gpu_ids(pod)
+            if devs:
+                gpu_data = await self.gpu.busy(pod, devs, self.cfg.check_period_s)
+                if gpu_data is not None:
+                    gpu_active = gpu_data["busy_mean"] >= self.cfg.gpu_busy_threshold
+        kernels = terminals = None
+        if src in ("jupyter", "combined") or gpu_data is None:
+            kernels, terminals = await self.jupyter.sample(nb, pod)
+        return gpu_active, kernels, terminals
+
+    async def close(self) -> None:
+        await self.jupyter.close()
+        if self.gpu is not None:
+            await self.gpu.close()
+
+    def setup_with_manager(self, mgr, max_concurrent: Optional[int] = None):
+        b = mgr.builder().named(self.NAME).for_(kinds.NOTEBOOK_V1BETA1)
+        if max_concurrent is not None:
+            b.with_options(max_concurrent_reconciles=max_concurrent)
+        c = b.complete(self)
+        mgr.add(_Closer(self), needs_leader=False)
+        return c
+
+
+class _Closer:
+    def __init__(self, r):
+        self.r = r
+
+    async def start(self):
+        return None
+
+    async def stop(self):
+        await self.r.close()

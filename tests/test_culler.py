@@ -1,0 +1,210 @@
+"""Culler: reference unit tables (kf/controllers/culling_controller_test.go) + integration
+with the Jupyter API over HTTP and with the amdgpu busy signal (native telemetry on a
+synthetic sysfs tree)."""
+
+import time
+
+import pytest
+
+from odh_kubeflow_amd.cluster import ClusterConfig, LocalCluster
+from odh_kubeflow_amd.controllers import culling as c
+from odh_kubeflow_amd.models import kinds
+from odh_kubeflow_amd.models import meta as m
+from odh_kubeflow_amd.models.notebook import (LAST_ACTIVITY_ANNOTATION, LAST_ACTIVITY_CHECK_TIMESTAMP_ANNOTATION,
+                                              STOP_ANNOTATION, notebook)
+from odh_kubeflow_amd.notebook_server.jupyter import JupyterContainerRuntime
+from odh_kubeflow_amd.utils import timeutil
+from odh_kubeflow_amd.utils.timeutil import rfc3339
+
+
+@pytest.fixture
+def clock():
+    offset = [0.0]
+    timeutil.set_clock(lambda: time.time() + offset[0])
+    yield offset
+    timeutil.set_clock(None)
+
+
+def nbmeta(ann=None):
+    return {"metadata": {"name": "n", "namespace": "s", **({"annotations": ann} if ann is not None else {})}}
+
+
+def test_set_and_detect_stop_annotation():
+    for meta in (nbmeta(), nbmeta({}), nbmeta({STOP_ANNOTATION: rfc3339()})):
+        c.set_stop_annotation(meta)
+        assert STOP_ANNOTATION in meta["metadata"]["annotations"]
+    assert not c.stop_annotation_is_set(nbmeta())
+    assert not c.stop_annotation_is_set(nbmeta({}))
+    assert c.stop_annotation_is_set(nbmeta({STOP_ANNOTATION: rfc3339()}))
+
+
+def test_all_kernels_are_idle():
+    assert c.all_kernels_are_idle([])
+    assert c.all_kernels_are_idle([{"execution_state": "idle"}, {"execution_state": "idle"}])
+    assert not c.all_kernels_are_idle([{"execution_state": "idle"}, {"execution_state": "busy"}])
+
+
+@pytest.mark.parametrize("ann,idle_min,want", [
+    (None, 1440, False),
+    ({}, 1440, False),
+    ({STOP_ANNOTATION: "now"}, 1440, False),
+    ({LAST_ACTIVITY_ANNOTATION: "garbage"}, 1440, False),
+    ({LAST_ACTIVITY_ANNOTATION: rfc3339(time.time() - 3600)}, 1440, False),
+    ({LAST_ACTIVITY_ANNOTATION: rfc3339(time.time() - 3600)}, 30, True),
+    ({LAST_ACTIVITY_ANNOTATION: rfc3339(time.time() - 60 * 60 * 25)}, 1440, True),
+])
+def test_notebook_is_idle(ann, idle_min, want):
+    # the reference drives CULL_IDLE_TIME through os.Setenv + initGlobalVars
+    cfg = c.CullerConfig.from_env({"CULL_IDLE_TIME": str(idle_min)})
+    assert c.notebook_is_idle(nbmeta(ann), cfg.cull_idle_time_s) is want
+
+
+def test_config_from_env():
+    cfg = c.CullerConfig.from_env({})
+    assert cfg.cull_idle_time_s == 1440 * 60 and cfg.check_period_s == 60 and not cfg.enable_culling
+    assert cfg.cluster_domain == "cluster.local" and cfg.activity_source == "jupyter"
+    assert c.CullerConfig.from_env({"CULL_IDLE_TIME": "abc"}).cull_idle_time_s == 1440 * 60
+    with pytest.raises(ValueError):
+        c.CullerConfig.from_env({"IDLENESS_CHECK_PERIOD": "x"})
+    with pytest.raises(ValueError):
+        c.CullerConfig.from_env({"CULLING_ACTIVITY_SOURCE": "vibes"})
+
+
+def test_kernel_and_terminal_timestamp_updates():
+    old = rfc3339(time.time() - 600)
+    newer = rfc3339(time.time() - 60)
+    nb = nbmeta({LAST_ACTIVITY_ANNOTATION: old})
+    assert not c.update_from_kernels(nb, None) and not c.update_from_kernels(nb, [])
+    assert c.update_from_kernels(nb, [{"execution_state": "idle", "last_activity": newer},
+                                      {"execution_state": "idle", "last_activity": old}])
+    assert m.annotations(nb)[LAST_ACTIVITY_ANNOTATION] == newer
+    # an older resource time never moves the annotation backwards
+    assert not c.update_from_terminals(nb, [{"last_activity": old}])
+    # a busy kernel means "active now"
+    c.update_from_kernels(nb, [{"execution_state": "busy", "last_activity": old}])
+    assert c.annotation_not_after({"metadata": {"annotations": {LAST_ACTIVITY_ANNOTATION: newer}}},
+                                  m.annotations(nb)[LAST_ACTIVITY_ANNOTATION])
+    assert c.most_recent_time(["bad"]) == ""
+
+
+def test_check_period(clock):
+    nb = nbmeta({LAST_ACTIVITY_CHECK_TIMESTAMP_ANNOTATION: rfc3339()})
+    assert not c.culling_check_period_has_passed(nb, 60)
+    clock[0] = 61
+    assert c.culling_check_period_has_passed(nb, 60)
+    assert not c.culling_check_period_has_passed(nbmeta({}), 60)
+
+
+# ------------------------------------------------------------------ integration
+
+
+def _cfg(runtime, **env):
+    base = {"ENABLE_CULLING": "true", "CULL_IDLE_TIME": "60", "IDLENESS_CHECK_PERIOD_SECONDS": "0.05",
+            "CULLER_USE_POD_ENDPOINT": "true"}
+    base.update(env)
+    return ClusterConfig(culler=True, env=base, runtime_factory=lambda d: runtime)
+
+
+def test_culler_jupyter_busy_keeps_idle_culls(run, clock):
+    rt = JupyterContainerRuntime()
+
+    async def go():
+        async with LocalCluster(_cfg(rt)) as cl:
+            await cl.ensure_namespace("user")
+            await cl.admin.create(notebook("busy", "user", gpus=1))
+            await cl.admin.create(notebook("idle", "user", gpus=1))
+            assert await cl.wait_for(lambda: cl.notebook_ready("busy", "user") and cl.notebook_ready("idle", "user"))
+            st_busy, st_idle = rt.state("user", "busy"), rt.state("user", "idle")
+            kid = st_busy.start_kernel(busy=True)
+            st_idle.start_kernel(busy=False)
+            # annotations initialised
+            assert await cl.wait_for(lambda: c.annotations_exist(cl.store.peek(kinds.NOTEBOOK, "busy", "user")))
+            # two hours pass
+            clock[0] += 7200
+            idle_nb = lambda: cl.store.peek(kinds.NOTEBOOK, "idle", "user")  # noqa: E731
+            assert await cl.wait_for(lambda: STOP_ANNOTATION in m.annotations(idle_nb()), 10)
+            # culled → StatefulSet scaled to zero, pod gone, activity annotations stripped
+            assert await cl.wait_for(lambda: cl.store.peek(kinds.POD, "idle-0", "user") is None, 10)
+            assert cl.store.peek(kinds.STATEFUL_SET, "idle", "user")["spec"]["replicas"] == 0
+            assert await cl.wait_for(lambda: LAST_ACTIVITY_ANNOTATION not in m.annotations(idle_nb()))
+            busy = cl.store.peek(kinds.NOTEBOOK, "busy", "user")
+            assert STOP_ANNOTATION not in m.annotations(busy), (list(cl.reconcilers["culler"].recent), st_busy.kernels)
+            assert st_busy.requests >= 2  # the culler really polled over HTTP
+            culler = cl.reconcilers["culler"]
+            assert culler.culled == 1
+            # culling metrics are exported (the reference forgets them)
+            from prometheus_client import generate_latest
+            text = generate_latest(cl.kf.registry).decode()
+            assert 'notebook_culling_total{name="idle",namespace="user"} 1.0' in text
+            assert "last_notebook_culling_timestamp_seconds" in text
+            # busy kernel goes idle; later it is culled too
+            st_busy.set_kernel_state(kid, "idle")
+            n0 = len(culler.recent)
+            # let an in-flight sample of the busy kernel land before time jumps
+            assert await cl.wait_for(lambda: any(
+                r[1] == "user/busy" and r[3] and r[3][0]["execution_state"] == "idle"
+                for r in list(culler.recent)[n0:]), 10)
+            clock[0] += 7200
+            ok = await cl.wait_for(lambda: STOP_ANNOTATION in m.annotations(
+                cl.store.peek(kinds.NOTEBOOK, "busy", "user")), 10)
+            assert ok, (m.annotations(cl.store.peek(kinds.NOTEBOOK, "busy", "user")), st_busy.kernels, rfc3339())
+    run(go(), timeout=60)
+
+
+def test_culler_no_data_never_culls(run, clock):
+    rt = JupyterContainerRuntime()
+
+    async def go():
+        cfg = _cfg(rt, CULLER_USE_POD_ENDPOINT="false", CLUSTER_DOMAIN="invalid.example")  # unreachable
+        async with LocalCluster(cfg) as cl:
+            await cl.ensure_namespace("user")
+            await cl.admin.create(notebook("nb", "user"))
+            assert await cl.wait_for(lambda: cl.notebook_ready("nb", "user"))
+            assert await cl.wait_for(lambda: c.annotations_exist(cl.store.peek(kinds.NOTEBOOK, "nb", "user")))
+            la = m.annotations(cl.store.peek(kinds.NOTEBOOK, "nb", "user"))[LAST_ACTIVITY_ANNOTATION]
+            clock[0] += 30  # within CULL_IDLE_TIME: checks run, no data, nothing changes
+            assert await cl.wait_for(lambda: cl.reconcilers["culler"].checks >= 1, 10)
+            nb = cl.store.peek(kinds.NOTEBOOK, "nb", "user")
+            assert m.annotations(nb)[LAST_ACTIVITY_ANNOTATION] == la and STOP_ANNOTATION not in m.annotations(nb)
+    run(go(), timeout=60)
+
+
+def test_culler_amdgpu_signal(run, clock, tmp_path):
+    from odh_kubeflow_amd.ops.telemetry import Telemetry, set_fake_counter, write_fake_sysfs
+
+    minors = write_fake_sysfs(str(tmp_path), gpus=8)
+    tel = Telemetry(str(tmp_path)).start(interval_ms=10, capacity=2000)
+    rt = JupyterContainerRuntime()
+    src = c.LocalTelemetryActivity(tel)
+
+    async def go():
+        cfg = _cfg(rt, CULLING_ACTIVITY_SOURCE="amdgpu", IDLENESS_CHECK_PERIOD_SECONDS="0.2")
+        cfg.activity_source = src
+        async with LocalCluster(cfg) as cl:
+            await cl.ensure_namespace("user")
+            await cl.admin.create(notebook("train", "user", gpus=1))
+            assert await cl.wait_for(lambda: cl.notebook_ready("train", "user"))
+            await cl.admin.create(notebook("idle", "user", gpus=1))
+            assert await cl.wait_for(lambda: cl.notebook_ready("idle", "user"))
+            gid = {n: c.pod_gpu_ids(cl.store.peek(kinds.POD, f"{n}-0", "user"))[0] for n in ("train", "idle")}
+            assert gid["train"] != gid["idle"]
+            # "train" runs an MI355X job: its GPU is 97% busy; no kernel is busy in Jupyter
+            set_fake_counter(str(tmp_path), minors[gid["train"]], busy=97)
+            rt.state("user", "train").start_kernel(busy=False)
+            assert await cl.wait_for(lambda: c.annotations_exist(cl.store.peek(kinds.NOTEBOOK, "train", "user")))
+            import asyncio
+            await asyncio.sleep(0.3)
+            clock[0] += 7200
+            assert await cl.wait_for(lambda: STOP_ANNOTATION in m.annotations(
+                cl.store.peek(kinds.NOTEBOOK, "idle", "user")), 10)
+            assert STOP_ANNOTATION not in m.annotations(cl.store.peek(kinds.NOTEBOOK, "train", "user"))
+            # the job ends: GPU idle → culled after the idle time
+            set_fake_counter(str(tmp_path), minors[gid["train"]], busy=0)
+            await asyncio.sleep(0.5)
+            clock[0] += 7200
+            assert await cl.wait_for(lambda: STOP_ANNOTATION in m.annotations(
+                cl.store.peek(kinds.NOTEBOOK, "train", "user")), 10)
+    try:
+        run(go(), timeout=60)
+    finally:
+        tel.close()

@@ -39,6 +39,11 @@ class ClusterConfig:
     reference_emulation: bool = False  # reproduce the reference's serialising behaviour for comparison
     activity_source: Optional[object] = None
     openshift: bool = False  # serve the OpenShift APIs (image/config/route/oauth) like an OCP cluster
+    # "inprocess": managers share the store directly; "http": the store is served by the REST
+    # apiserver and the kf / odh managers, the webhook (HTTPS, MutatingWebhookConfiguration)
+    # and the node agents talk to it over HTTP exactly as they would to kube-apiserver
+    transport: str = "inprocess"
+    remote_kubelets: bool = True  # with transport="http": node agents use REST clients too
 
 
 class LocalCluster:
@@ -57,19 +62,38 @@ class LocalCluster:
         self.gpu_runtimes = []
         self.reconcilers: Dict[str, object] = {}
         self.webhook = None
+        self.apiserver = None
+        self.webhook_server = None
+        self.rest_config = None
 
     # ------------------------------------------------------------------ build
 
-    def _mgr(self, name: str, **kw) -> Manager:
-        mgr = Manager.in_process(self.store, name=name, default_max_concurrent=self.cfg.max_concurrent, **kw)
+    def _mgr(self, name: str, remote: bool = False, **kw) -> Manager:
+        if remote and self.rest_config is not None:
+            from .runtime.informer import strip_data, strip_managed_fields
+
+            tf = {kinds.CONFIG_MAP: strip_data, kinds.SECRET: strip_data} if kw.get("uncached") else None
+            mgr = Manager.remote(self.rest_config, name=name, default_max_concurrent=self.cfg.max_concurrent,
+                                 transforms=tf, **kw)
+        else:
+            mgr = Manager.in_process(self.store, name=name, default_max_concurrent=self.cfg.max_concurrent, **kw)
         self.managers.append(mgr)
         return mgr
+
+    async def _start_apiserver(self) -> None:
+        from .apiserver.http import ApiServer
+        from .runtime.rest import RestConfig
+
+        self.apiserver = await ApiServer(self.store).start("127.0.0.1", 0)
+        self.rest_config = RestConfig(host=self.apiserver.url)
 
     async def start(self) -> "LocalCluster":
         from .kubelet.node import GpuRuntime, SchedulerController, make_node
         from .kubelet.statefulset import StatefulSetController
 
         cfg = self.cfg
+        if cfg.transport == "http":
+            await self._start_apiserver()
         admin = Manager.in_process(self.store, name="admin").client
         self.admin = admin
         for ns in ("default", cfg.controller_namespace):
@@ -87,7 +111,7 @@ class LocalCluster:
             node_name = f"mi355x-node-{n}"
             await admin.create(make_node(node_name, cfg.gpus_per_node))
             if cfg.gpu_runtimes_in_process:
-                kl = self._mgr(f"kubelet-{node_name}")
+                kl = self._mgr(f"kubelet-{node_name}", remote=cfg.remote_kubelets)
                 self.kubelets.append(kl)
                 for d in range(cfg.gpus_per_node):
                     rt = cfg.runtime_factory(d) if cfg.runtime_factory else None
@@ -110,7 +134,7 @@ class LocalCluster:
         from .controllers.metrics import NotebookMetrics
         from .controllers.notebook import NotebookEventReemitter, NotebookReconciler
 
-        kf = self.kf = self._mgr("notebook-controller")
+        kf = self.kf = self._mgr("notebook-controller", remote=True)
         metrics = NotebookMetrics(kf.reader, kf.registry)
         self.kf_metrics = metrics
         emu = self.cfg.reference_emulation
@@ -132,7 +156,7 @@ class LocalCluster:
     def _build_odh(self) -> None:
         from .controllers.odh.reconciler import OpenshiftNotebookReconciler
 
-        odh = self.odh = self._mgr("odh-notebook-controller", uncached=(kinds.CONFIG_MAP, kinds.SECRET))
+        odh = self.odh = self._mgr("odh-notebook-controller", remote=True, uncached=(kinds.CONFIG_MAP, kinds.SECRET))
         emu = self.cfg.reference_emulation
         r = OpenshiftNotebookReconciler(odh.client, odh.reader, self.cfg.controller_namespace, env=self.env,
                                         recorder=odh.get_event_recorder_for("odh-notebook-controller"),
@@ -143,6 +167,18 @@ class LocalCluster:
     async def _start_webhook(self) -> None:
         from .webhook.notebook_webhook import NotebookWebhook, register_in_process
 
+        if self.rest_config is not None:
+            from .webhook.certs import generate
+            from .webhook.server import WebhookServer, mutating_webhook_configuration
+
+            wh_mgr = self._mgr("odh-webhook", remote=True, uncached=(kinds.CONFIG_MAP, kinds.SECRET))
+            self.webhook = NotebookWebhook(wh_mgr.client, self.cfg.controller_namespace,
+                                           kube_rbac_proxy_image=self.cfg.kube_rbac_proxy_image, env=self.env)
+            certs = generate(("127.0.0.1", "localhost"))
+            self.webhook_server = await WebhookServer(self.webhook, certs.cert_dir, "127.0.0.1", 0).start()
+            await self.admin.create(mutating_webhook_configuration(
+                certs.ca_bundle_b64, url=f"https://127.0.0.1:{self.webhook_server.port}/mutate-notebook-v1"))
+            return
         wh_mgr = Manager.in_process(self.store, name="odh-webhook", uncached=(kinds.CONFIG_MAP, kinds.SECRET))
         self.webhook = NotebookWebhook(wh_mgr.client, self.cfg.controller_namespace,
                                        kube_rbac_proxy_image=self.cfg.kube_rbac_proxy_image, env=self.env)
@@ -159,6 +195,10 @@ class LocalCluster:
             await mgr.stop()
         for g in self.gpu_runtimes:
             await g.close()
+        if self.webhook_server is not None:
+            await self.webhook_server.stop()
+        if self.apiserver is not None:
+            await self.apiserver.stop()
 
     async def settle(self, timeout: float = 10.0) -> bool:
         """Wait until every controller in every manager is idle (twice, to catch cascades)."""

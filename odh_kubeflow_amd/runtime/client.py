@@ -197,9 +197,15 @@ class CachedClient(Client):
     def _live(self, kind) -> bool:
         return SCHEME.resolve(kind).key in self.uncached
 
+    async def _ensure(self, kind) -> None:
+        ensure = getattr(self.reader, "ensure_informer", None)
+        if ensure is not None:
+            await ensure(kind)
+
     async def get(self, kind, name, namespace=None):
         if self._live(kind):
             return await self.writer.get(kind, name, namespace)
+        await self._ensure(kind)
         o = self.reader.get(kind, name, namespace)
         if o is None:
             from ..models.errors import NotFound
@@ -215,6 +221,7 @@ class CachedClient(Client):
     async def list(self, kind, namespace=None, labels=None, fields=None, owner_uid=None):
         if self._live(kind) and owner_uid is None:
             return await self.writer.list(kind, namespace, labels, fields)
+        await self._ensure(kind)
         items = [deepcopy_json(o) for o in self.reader.list(kind, namespace, labels, fields, owner_uid)]
         v = _version_of(kind)
         if v:

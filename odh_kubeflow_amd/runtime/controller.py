@@ -186,6 +186,8 @@ class Controller:
         self.started = True
         for w in self.watches:
             self._unsubs.append(source.subscribe(w.kind, self._handler(w)))
+        # WaitForCacheSync: workers start only once every watched kind has listed
+        await source.wait_synced([w.kind for w in self.watches])
         if self.metrics:
             self.metrics.max_concurrent.labels(self.name).set(self.max_concurrent)
         for i in range(self.max_concurrent):

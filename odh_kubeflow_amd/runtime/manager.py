@@ -61,6 +61,21 @@ class Manager:
         client = CachedClient(reader, writer, uncached)
         return cls(client, reader, StoreEventSource(store), name=name, **kw)
 
+    @classmethod
+    def remote(cls, config, name: str = "manager", uncached: Sequence = (), transforms=None,
+               namespace: Optional[str] = None, **kw) -> "Manager":
+        """Manager against a real (or out-of-process) apiserver: REST client + informer cache."""
+        from .informer import InformerCache
+        from .rest import RestClient
+
+        rest = RestClient(config)
+        cache = InformerCache(rest, namespace=namespace, transforms=transforms)
+        client = CachedClient(cache, rest, uncached)
+        mgr = cls(client, cache, cache, name=name, **kw)
+        mgr.rest = rest
+        mgr.cache = cache
+        return mgr
+
     def builder(self) -> Builder:
         return Builder(self)
 
@@ -130,6 +145,12 @@ class Manager:
         for s in self._servers:
             await s.cleanup()
         self._servers.clear()
+        cache = getattr(self, "cache", None)
+        if cache is not None:
+            await cache.stop()
+        rest = getattr(self, "rest", None)
+        if rest is not None:
+            await rest.close()
         self._started = False
 
     async def run_until(self, stop: asyncio.Event) -> None:

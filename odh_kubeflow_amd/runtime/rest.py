@@ -1,0 +1,336 @@
+"""REST client for a (real or in-process) Kubernetes apiserver — the ``client-go`` rest
+layer the reference managers use through controller-runtime.
+
+* :class:`RestConfig` — host, bearer token, TLS (CA / client cert / insecure) and the
+  client-side ``QPS`` / ``Burst`` limiter of ``kf/main.go:71-85`` (``--qps`` /
+  ``--burst``).  Loaders: :meth:`RestConfig.from_kubeconfig` (``$KUBECONFIG`` /
+  ``~/.kube/config``, current context), :meth:`RestConfig.in_cluster` (service-account
+  token + CA), :meth:`RestConfig.load` (explicit > kubeconfig > in-cluster, like
+  ``ctrl.GetConfigOrDie``).
+* :class:`RestClient` — the async :class:`~odh_kubeflow_amd.runtime.client.Client`
+  interface over HTTP(S): CRUD, ``status`` subresource, the three patch types,
+  ``DeleteOptions``, list with selectors, and :meth:`RestClient.watch` streaming
+  ``WatchEvent`` lines.  Errors come back as the ``ApiError`` subclasses.
+"""
+
+from __future__ import annotations
+
+import asyncio
+import base64
+import json
+import os
+import ssl
+import tempfile
+import time
+from dataclasses import dataclass, field
+from typing import Any, AsyncIterator, List, Optional, Tuple
+
+from ..models.errors import ApiError, Gone, InternalError
+from ..models.scheme import SCHEME, ResourceInfo
+from ..utils.selectors import format_label_selector
+from .client import Client, _refresh, _version_of
+
+SA_DIR = "/var/run/secrets/kubernetes.io/serviceaccount"
+
+
+@dataclass
+class RestConfig:
+    host: str
+    token: Optional[str] = None
+    ca_file: Optional[str] = None
+    ca_data: Optional[str] = None
+    cert_file: Optional[str] = None
+    key_file: Optional[str] = None
+    insecure: bool = False
+    qps: float = 0.0  # 0 = unlimited (controller-runtime defaults 20/30 on real clusters: pass --qps/--burst)
+    burst: int = 0
+    user_agent: str = "odh-kubeflow-amd"
+    extra: dict = field(default_factory=dict)
+
+    def ssl_context(self) -> Optional[ssl.SSLContext]:
+        if not self.host.startswith("https"):
+            return None
+        if self.insecure:
+            ctx = ssl.create_default_context()
+            ctx.check_hostname = False
+            ctx.verify_mode = ssl.CERT_NONE
+        else:
+            ctx = ssl.create_default_context(cafile=self.ca_file, cadata=self.ca_data)
+        if self.cert_file:
+            ctx.load_cert_chain(self.cert_file, self.key_file)
+        return ctx
+
+    @classmethod
+    def in_cluster(cls) -> "RestConfig":
+        host, port = os.environ.get("KUBERNETES_SERVICE_HOST"), os.environ.get("KUBERNETES_SERVICE_PORT")
+        if not host or not port:
+            raise RuntimeError("not running in a cluster (KUBERNETES_SERVICE_HOST unset)")
+        with open(os.path.join(SA_DIR, "token")) as f:
+            token = f.read().strip()
+        if ":" in host:
+            host = f"[{host}]"
+        return cls(host=f"https://{host}:{port}", token=token, ca_file=os.path.join(SA_DIR, "ca.crt"))
+
+    @classmethod
+    def from_kubeconfig(cls, path: Optional[str] = None, context: Optional[str] = None) -> "RestConfig":
+        import yaml
+
+        path = path or os.environ.get("KUBECONFIG") or os.path.expanduser("~/.kube/config")
+        with open(path) as f:
+            kc = yaml.safe_load(f) or {}
+        ctx_name = context or kc.get("current-context")
+        ctx = next((c["context"] for c in kc.get("contexts") or [] if c.get("name") == ctx_name), None)
+        if ctx is None:
+            raise RuntimeError(f"context {ctx_name!r} not found in {path}")
+        cl = next((c["cluster"] for c in kc.get("clusters") or [] if c.get("name") == ctx.get("cluster")), {})
+        user = next((u["user"] for u in kc.get("users") or [] if u.get("name") == ctx.get("user")), {})
+        cfg = cls(host=cl.get("server", ""), token=user.get("token"), insecure=bool(cl.get("insecure-skip-tls-verify")))
+        if cl.get("certificate-authority-data"):
+            cfg.ca_data = base64.b64decode(cl["certificate-authority-data"]).decode()
+        elif cl.get("certificate-authority"):
+            cfg.ca_file = cl["certificate-authority"]
+        for key, attr in (("client-certificate", "cert_file"), ("client-key", "key_file")):
+            if user.get(key):
+                setattr(cfg, attr, user[key])
+            elif user.get(key + "-data"):
+                fd, p = tempfile.mkstemp(prefix="odh-kc-")
+                with os.fdopen(fd, "wb") as f:
+                    f.write(base64.b64decode(user[key + "-data"]))
+                setattr(cfg, attr, p)
+        if user.get("tokenFile"):
+            with open(user["tokenFile"]) as f:
+                cfg.token = f.read().strip()
+        return cfg
+
+    @classmethod
+    def load(cls, master: Optional[str] = None, kubeconfig: Optional[str] = None) -> "RestConfig":
+        if master:
+            return cls(host=master, token=os.environ.get("KUBE_TOKEN"))
+        if kubeconfig or os.environ.get("KUBECONFIG") or os.path.exists(os.path.expanduser("~/.kube/config")):
+            return cls.from_kubeconfig(kubeconfig)
+        return cls.in_cluster()
+
+
+class TokenBucket:
+    """client-go's flowcontrol token bucket (``QPS`` refill, ``Burst`` capacity)."""
+
+    def __init__(self, qps: float, burst: int):
+        self.qps = qps
+        self.capacity = max(1, burst or int(qps) or 1)
+        self.tokens = float(self.capacity)
+        self.t = time.monotonic()
+
+    async def take(self) -> None:
+        if self.qps <= 0:
+            return
+        while True:
+            now = time.monotonic()
+            self.tokens = min(self.capacity, self.tokens + (now - self.t) * self.qps)
+            self.t = now
+            if self.tokens >= 1:
+                self.tokens -= 1
+                return
+            await asyncio.sleep((1 - self.tokens) / self.qps)
+
+
+def _info_and_version(ref) -> Tuple[ResourceInfo, str]:
+    info = SCHEME.resolve(ref)
+    return info, _version_of(ref) or info.storage_version
+
+
+class RestClient(Client):
+    def __init__(self, config: RestConfig, pool: int = 64):
+        self.config = config
+        self.base = config.host.rstrip("/")
+        self._ssl = config.ssl_context()
+        self._session = None
+        self._pool = pool
+        self._bucket = TokenBucket(config.qps, config.burst)
+        self.requests = 0
+        self.user = config.user_agent
+        self._discovery: dict = {}  # "group/version" -> (fetched_at, set(plurals))
+
+    async def _sess(self):
+        import aiohttp
+
+        if self._session is None or self._session.closed:
+            conn = aiohttp.TCPConnector(limit=self._pool, ssl=self._ssl if self._ssl else False,
+                                        keepalive_timeout=60)
+            headers = {"User-Agent": self.config.user_agent, "Accept": "application/json"}
+            if self.config.token:
+                headers["Authorization"] = f"Bearer {self.config.token}"
+            self._session = aiohttp.ClientSession(connector=conn, headers=headers, json_serialize=json.dumps)
+        return self._session
+
+    async def close(self) -> None:
+        if self._session is not None:
+            await self._session.close()
+            self._session = None
+
+    def path(self, info: ResourceInfo, version: str, namespace: Optional[str], name: Optional[str] = None,
+             sub: Optional[str] = None) -> str:
+        return self.base + info.path(version, namespace if info.namespaced else None, name, sub)
+
+    async def request(self, method: str, url: str, body: Any = None, params: Optional[dict] = None,
+                      content_type: str = "application/json") -> dict:
+        await self._bucket.take()
+        s = await self._sess()
+        self.requests += 1
+        data = None if body is None else json.dumps(body, separators=(",", ":")).encode()
+        headers = {"Content-Type": content_type} if data is not None else None
+        async with s.request(method, url, data=data, params=params, headers=headers) as resp:
+            raw = await resp.read()
+            try:
+                out = json.loads(raw) if raw else {}
+            except ValueError:
+                out = {"message": raw[:200].decode(errors="replace")}
+            if resp.status >= 400:
+                if isinstance(out, dict) and out.get("kind") == "Status":
+                    err = ApiError.from_status(out, resp.status)
+                else:
+                    err = ApiError.from_status({"code": resp.status, "message": str(out)}, resp.status)
+                if resp.status == 404 and err.reason != "NoKindMatch":
+                    await self._maybe_no_match(url, err)
+                raise err
+            return out
+
+    async def _served(self, group: str, version: str) -> set:
+        key = f"{group}/{version}"
+        hit = self._discovery.get(key)
+        if hit is not None and time.monotonic() - hit[0] < 30.0:
+            return hit[1]
+        path = f"/apis/{group}/{version}" if group else f"/api/{version}"
+        s = await self._sess()
+        try:
+            async with s.get(self.base + path) as resp:
+                doc = await resp.json(content_type=None) if resp.status == 200 else {}
+        except Exception:
+            doc = {}
+        plurals = {r.get("name") for r in (doc or {}).get("resources") or []}
+        self._discovery[key] = (time.monotonic(), plurals)
+        return plurals
+
+    async def _maybe_no_match(self, url: str, err: ApiError) -> None:
+        """A 404 on a resource type the server does not serve is ``meta.NoKindMatchError``
+        (controller-runtime learns that from the RESTMapper's discovery)."""
+        from ..apiserver.http import parse_path
+        from ..models.errors import NoKindMatch
+
+        pp = parse_path(url[len(self.base):].split("?", 1)[0])
+        if pp is None:
+            return
+        if pp.info.plural not in await self._served(pp.info.group, pp.version):
+            raise NoKindMatch(pp.info.kind)
+
+    # -------------------------------------------------------------- Client interface
+
+    async def get(self, kind, name, namespace=None):
+        info, v = _info_and_version(kind)
+        return await self.request("GET", self.path(info, v, namespace, name))
+
+    async def list(self, kind, namespace=None, labels=None, fields=None, owner_uid=None):
+        items, _ = await self.list_rv(kind, namespace, labels, fields)
+        if owner_uid is not None:
+            items = [o for o in items if any(r.get("uid") == owner_uid for r in
+                                             (o.get("metadata") or {}).get("ownerReferences") or [])]
+        return items
+
+    async def list_rv(self, kind, namespace=None, labels=None, fields=None) -> Tuple[List[dict], str]:
+        info, v = _info_and_version(kind)
+        params = {}
+        if labels:
+            params["labelSelector"] = format_label_selector(labels) if isinstance(labels, dict) else labels
+        if fields:
+            params["fieldSelector"] = fields
+        out = await self.request("GET", self.path(info, v, namespace), params=params or None)
+        items = out.get("items") or []
+        av = info.api_version(v)
+        for o in items:
+            o.setdefault("apiVersion", av)
+            o.setdefault("kind", info.kind)
+        return items, (out.get("metadata") or {}).get("resourceVersion", "")
+
+    async def create(self, obj):
+        info, v = _info_and_version(obj)
+        ns = (obj.get("metadata") or {}).get("namespace")
+        return _refresh(obj, await self.request("POST", self.path(info, v, ns), obj))
+
+    async def update(self, obj):
+        info, v = _info_and_version(obj)
+        md = obj.get("metadata") or {}
+        return _refresh(obj, await self.request("PUT", self.path(info, v, md.get("namespace"), md.get("name")), obj))
+
+    async def update_status(self, obj):
+        info, v = _info_and_version(obj)
+        md = obj.get("metadata") or {}
+        return _refresh(obj, await self.request("PUT", self.path(info, v, md.get("namespace"), md.get("name"),
+                                                                 "status"), obj))
+
+    async def patch(self, obj_or_kind, patch, patch_type="merge", name=None, namespace=None, subresource=None):
+        if isinstance(obj_or_kind, dict):
+            name = name or obj_or_kind["metadata"]["name"]
+            namespace = namespace or obj_or_kind["metadata"].get("namespace")
+        info, v = _info_and_version(obj_or_kind)
+        ctype = {"merge": "application/merge-patch+json", "json": "application/json-patch+json",
+                 "strategic": "application/strategic-merge-patch+json"}.get(patch_type, patch_type)
+        out = await self.request("PATCH", self.path(info, v, namespace, name, subresource), patch, content_type=ctype)
+        if isinstance(obj_or_kind, dict):
+            return _refresh(obj_or_kind, out)
+        return out
+
+    async def delete(self, obj_or_kind, name=None, namespace=None, preconditions=None, propagation="Background"):
+        if isinstance(obj_or_kind, dict):
+            name = name or obj_or_kind["metadata"]["name"]
+            namespace = namespace or obj_or_kind["metadata"].get("namespace")
+        info, v = _info_and_version(obj_or_kind)
+        body = {"kind": "DeleteOptions", "apiVersion": "v1", "propagationPolicy": propagation}
+        if preconditions:
+            body["preconditions"] = preconditions
+        return await self.request("DELETE", self.path(info, v, namespace, name), body)
+
+    # -------------------------------------------------------------- watch
+
+    async def watch(self, kind, namespace=None, resource_version: Optional[str] = None, labels=None, fields=None,
+                    timeout_s: int = 300, bookmarks: bool = True) -> AsyncIterator[Tuple[str, dict]]:
+        """Yield ``(type, object)``; raises :class:`Gone` when the RV is too old."""
+        import aiohttp
+
+        info, v = _info_and_version(kind)
+        params = {"watch": "true", "timeoutSeconds": str(timeout_s)}
+        if resource_version:
+            params["resourceVersion"] = resource_version
+        if bookmarks:
+            params["allowWatchBookmarks"] = "true"
+        if labels:
+            params["labelSelector"] = format_label_selector(labels) if isinstance(labels, dict) else labels
+        if fields:
+            params["fieldSelector"] = fields
+        await self._bucket.take()
+        s = await self._sess()
+        self.requests += 1
+        async with s.get(self.path(info, v, namespace), params=params,
+                         timeout=aiohttp.ClientTimeout(total=None, sock_read=timeout_s + 30)) as resp:
+            if resp.status >= 400:
+                raw = await resp.read()
+                try:
+                    raise ApiError.from_status(json.loads(raw), resp.status)
+                except ValueError:
+                    raise InternalError(raw[:200].decode(errors="replace"))
+            buf = b""
+            async for chunk in resp.content.iter_any():
+                buf += chunk
+                while True:
+                    nl = buf.find(b"\n")
+                    if nl < 0:
+                        break
+                    line, buf = buf[:nl], buf[nl + 1:]
+                    if not line.strip():
+                        continue
+                    ev = json.loads(line)
+                    et, obj = ev.get("type"), ev.get("object") or {}
+                    if et == "ERROR":
+                        err = ApiError.from_status(obj)
+                        if err.code == 410:
+                            raise Gone(err.message)
+                        raise err
+                    yield et, obj

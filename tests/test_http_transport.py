@@ -1,0 +1,217 @@
+"""The REST apiserver, the REST client, the informer cache and the HTTPS webhook path.
+
+These are what the managers use against a real kube-apiserver; the scenarios reuse the
+envtest-style lifecycle tests over HTTP (the reference runs its suites against a real
+apiserver binary: kf/controllers/suite_test.go:50-104, odh/controllers/suite_test.go:91-275).
+"""
+
+import asyncio
+
+import pytest
+
+from odh_kubeflow_amd.apiserver.http import ApiServer, parse_path
+from odh_kubeflow_amd.apiserver.store import ObjectStore
+from odh_kubeflow_amd.cluster import ClusterConfig, LocalCluster
+from odh_kubeflow_amd.models import kinds
+from odh_kubeflow_amd.models import meta as m
+from odh_kubeflow_amd.models.errors import ApiError, is_already_exists, is_conflict, is_no_match, is_not_found
+from odh_kubeflow_amd.models.notebook import notebook
+from odh_kubeflow_amd.runtime.informer import InformerCache
+from odh_kubeflow_amd.runtime.rest import RestClient, RestConfig
+
+
+def test_parse_path():
+    pp = parse_path("/apis/kubeflow.org/v1beta1/namespaces/u/notebooks/nb/status")
+    assert (pp.info.kind, pp.version, pp.namespace, pp.name, pp.sub) == ("Notebook", "v1beta1", "u", "nb", "status")
+    pp = parse_path("/api/v1/namespaces/foo")
+    assert pp.info.kind == "Namespace" and pp.name == "foo" and pp.namespace is None
+    pp = parse_path("/api/v1/namespaces/foo/status")
+    assert pp.info.kind == "Namespace" and pp.name == "foo" and pp.sub == "status"
+    pp = parse_path("/apis/rbac.authorization.k8s.io/v1/clusterrolebindings")
+    assert pp.info.kind == "ClusterRoleBinding" and pp.name is None
+    assert parse_path("/apis/nope/v1/things") is None
+
+
+async def _server(token=None):
+    store = ObjectStore()
+    srv = await ApiServer(store, token=token).start()
+    return store, srv, RestClient(RestConfig(host=srv.url, token=token))
+
+
+def test_rest_crud_conflict_status_patch_and_errors(run):
+    async def go():
+        store, srv, c = await _server()
+        try:
+            await c.create({"apiVersion": "v1", "kind": "Namespace", "metadata": {"name": "u"}})
+            nb = await c.create(notebook("nb", "u", version="v1beta1"))
+            assert nb["apiVersion"] == "kubeflow.org/v1beta1" and m.resource_version(nb)
+            with pytest.raises(ApiError) as e:
+                await c.create(notebook("nb", "u"))
+            assert is_already_exists(e.value)
+            stale = dict(nb, metadata=dict(nb["metadata"]))
+            nb["metadata"]["labels"] = {"a": "b"}
+            await c.update(nb)
+            stale["metadata"]["labels"] = {"x": "y"}
+            with pytest.raises(ApiError) as e:
+                await c.update(stale)
+            assert is_conflict(e.value)
+            # status subresource isolation
+            nb["status"] = {"readyReplicas": 1, "conditions": [], "containerState": {}}
+            nb["metadata"]["labels"] = {"ignored": "1"}
+            await c.update_status(nb)
+            cur = await c.get(kinds.NOTEBOOK, "nb", "u")
+            assert cur["status"]["readyReplicas"] == 1 and m.labels(cur) == {"a": "b"}
+            # patch types
+            await c.patch(kinds.NOTEBOOK, {"metadata": {"annotations": {"k": "v"}}}, name="nb", namespace="u")
+            await c.patch(kinds.NOTEBOOK, [{"op": "add", "path": "/metadata/labels/c", "value": "d"}], "json",
+                          name="nb", namespace="u")
+            cur = await c.get(kinds.NOTEBOOK_V1ALPHA1, "nb", "u")
+            assert cur["apiVersion"] == "kubeflow.org/v1alpha1"
+            assert m.annotations(cur) == {"k": "v"} and m.labels(cur) == {"a": "b", "c": "d"}
+            # selectors
+            assert [m.name(o) for o in await c.list(kinds.NOTEBOOK, "u", labels={"c": "d"})] == ["nb"]
+            assert await c.list(kinds.NOTEBOOK, "u", labels="c!=d") == []
+            assert [m.name(o) for o in await c.list(kinds.NOTEBOOK, fields="metadata.name=nb")] == ["nb"]
+            # validation (CRD patch: containers minItems 1)
+            bad = notebook("bad", "u")
+            bad["spec"]["template"]["spec"]["containers"] = []
+            with pytest.raises(ApiError) as e:
+                await c.create(bad)
+            assert e.value.code == 422
+            with pytest.raises(ApiError) as e:
+                await c.get(kinds.NOTEBOOK, "missing", "u")
+            assert is_not_found(e.value)
+            # an API the server does not serve is a NoKindMatch, like controller-runtime's RESTMapper
+            store.uninstall_crd(kinds.IMAGE_STREAM)
+            with pytest.raises(ApiError) as e:
+                await c.list(kinds.IMAGE_STREAM, "u")
+            assert is_no_match(e.value)
+            # finalizers + delete
+            await c.patch(kinds.NOTEBOOK, {"metadata": {"finalizers": ["x/y"]}}, name="nb", namespace="u")
+            await c.delete(kinds.NOTEBOOK, "nb", "u")
+            cur = await c.get(kinds.NOTEBOOK, "nb", "u")
+            assert m.is_deleting(cur)
+            await c.patch(kinds.NOTEBOOK, {"metadata": {"finalizers": None}}, name="nb", namespace="u")
+            with pytest.raises(ApiError):
+                await c.get(kinds.NOTEBOOK, "nb", "u")
+        finally:
+            await c.close()
+            await srv.stop()
+    run(go())
+
+
+def test_rest_watch_resume_and_gone(run):
+    async def go():
+        store, srv, c = await _server()
+        store.HISTORY = 8
+        try:
+            await c.create({"apiVersion": "v1", "kind": "Namespace", "metadata": {"name": "u"}})
+            cm = await c.create({"apiVersion": "v1", "kind": "ConfigMap", "metadata": {"name": "a", "namespace": "u"}})
+            rv = m.resource_version(cm)
+            seen = []
+
+            async def consume():
+                async for et, obj in c.watch(kinds.CONFIG_MAP, "u", rv, timeout_s=5):
+                    seen.append((et, m.name(obj), (obj.get("data") or {}).get("k")))
+                    if len(seen) == 3:
+                        return
+
+            t = asyncio.ensure_future(consume())
+            await asyncio.sleep(0.05)
+            cm["data"] = {"k": "1"}
+            await c.update(cm)
+            await c.create({"apiVersion": "v1", "kind": "ConfigMap", "metadata": {"name": "b", "namespace": "u"}})
+            await c.delete(kinds.CONFIG_MAP, "a", "u")
+            await asyncio.wait_for(t, 5)
+            assert seen == [("MODIFIED", "a", "1"), ("ADDED", "b", None), ("DELETED", "a", "1")]
+            # resume from an old RV after the history rolled over: 410 Gone
+            for i in range(20):
+                await c.create({"apiVersion": "v1", "kind": "ConfigMap",
+                                "metadata": {"name": f"x{i}", "namespace": "u"}})
+            from odh_kubeflow_amd.models.errors import Gone
+            with pytest.raises(Gone):
+                async for _ in c.watch(kinds.CONFIG_MAP, "u", rv, timeout_s=2):
+                    pass
+        finally:
+            await c.close()
+            await srv.stop()
+    run(go())
+
+
+def test_informer_cache_indexes_transforms_and_events(run):
+    async def go():
+        store, srv, c = await _server()
+        cache = InformerCache(c, transforms={kinds.CONFIG_MAP: __import__(
+            "odh_kubeflow_amd.runtime.informer", fromlist=["strip_data"]).strip_data})
+        try:
+            await c.create({"apiVersion": "v1", "kind": "Namespace", "metadata": {"name": "u"}})
+            await c.create({"apiVersion": "v1", "kind": "ConfigMap", "metadata": {"name": "a", "namespace": "u"},
+                            "data": {"secret": "x"}})
+            events = []
+            cache.subscribe(kinds.CONFIG_MAP, lambda et, o, old: events.append((et, m.name(o))))
+            await cache.wait_synced([kinds.CONFIG_MAP])
+            assert events == [("ADDED", "a")]
+            assert "data" not in cache.get(kinds.CONFIG_MAP, "a", "u")  # transform applied
+            owner = await c.create(notebook("nb", "u"))
+            await c.create({"apiVersion": "v1", "kind": "ConfigMap", "metadata": {
+                "name": "owned", "namespace": "u", "ownerReferences": [m.owner_reference(owner)]}})
+            for _ in range(200):
+                if cache.get(kinds.CONFIG_MAP, "owned", "u") is not None:
+                    break
+                await asyncio.sleep(0.01)
+            assert [m.name(o) for o in cache.list(kinds.CONFIG_MAP, owner_uid=m.uid(owner))] == ["owned"]
+            assert ("ADDED", "owned") in events
+            await c.delete(kinds.CONFIG_MAP, "a", "u")
+            for _ in range(200):
+                if ("DELETED", "a") in events:
+                    break
+                await asyncio.sleep(0.01)
+            assert cache.get(kinds.CONFIG_MAP, "a", "u") is None
+        finally:
+            await cache.stop()
+            await c.close()
+            await srv.stop()
+    run(go())
+
+
+def test_bearer_token_required(run):
+    async def go():
+        store, srv, c = await _server(token="s3cret")
+        bad = RestClient(RestConfig(host=srv.url, token="wrong"))
+        try:
+            await c.create({"apiVersion": "v1", "kind": "Namespace", "metadata": {"name": "u"}})
+            with pytest.raises(ApiError) as e:
+                await bad.get(kinds.NAMESPACE, "u")
+            assert e.value.code == 401
+        finally:
+            await bad.close()
+            await c.close()
+            await srv.stop()
+    run(go())
+
+
+def test_full_stack_over_http_with_https_webhook(run):
+    async def go():
+        cfg = ClusterConfig(odh=True, webhook=True, transport="http", gc=True,
+                            env={"SET_PIPELINE_RBAC": "false", "USE_ISTIO": "true"})
+        async with LocalCluster(cfg) as cl:
+            await cl.ensure_namespace("user")
+            await cl.admin.create(notebook("nb", "user", gpus=1, annotations={
+                "notebooks.opendatahub.io/inject-auth": "true"}))
+            assert await cl.wait_for(lambda: cl.notebook_ready("nb", "user"), 20)
+            assert cl.apiserver.webhooks.calls >= 1 and cl.webhook_server.served >= 1
+            nb = cl.store.peek(kinds.NOTEBOOK, "nb", "user")
+            assert [c["name"] for c in nb["spec"]["template"]["spec"]["containers"]] == ["nb", "kube-rbac-proxy"]
+            assert cl.store.peek(kinds.VIRTUAL_SERVICE, "notebook-user-nb", "user") is not None
+            assert cl.store.peek(kinds.CLUSTER_ROLE_BINDING, "nb-rbac-user-auth-delegator") is not None
+            # webhook failurePolicy=Fail: an invalid sidecar annotation is rejected end to end
+            with pytest.raises(ApiError) as e:
+                await cl.admin.create(notebook("bad", "user", annotations={
+                    "notebooks.opendatahub.io/inject-auth": "true",
+                    "notebooks.opendatahub.io/auth-sidecar-memory-request": "10Gi"}))
+            assert "denied the request" in str(e.value)
+            await cl.admin.delete(kinds.NOTEBOOK, "nb", "user")
+            assert await cl.wait_for(lambda: cl.store.peek(kinds.NOTEBOOK, "nb", "user") is None, 10)
+            assert await cl.wait_for(lambda: cl.store.peek(kinds.STATEFUL_SET, "nb", "user") is None, 10)  # GC
+            assert cl.store.peek(kinds.CLUSTER_ROLE_BINDING, "nb-rbac-user-auth-delegator") is None
+    run(go(), timeout=60)

@@ -48,6 +48,8 @@ def parse(argv=None):
     p.add_argument("--no-odh", action="store_true", help="kf controller only (no webhook / odh reconciler)")
     p.add_argument("--reference-emulation", action="store_true",
                    help="reproduce the reference's serialising behaviour (1 worker, blocking lock removal)")
+    p.add_argument("--transport", choices=("inprocess", "http"), default="inprocess",
+                   help="managers share the store (inprocess) or talk REST/watch to the apiserver (http)")
     p.add_argument("--json-out", default=None)
     return p.parse_args(argv)
 
@@ -69,7 +71,7 @@ async def run_local(args, n_gpus: int, probe) -> dict:
 
     use_odh = not args.no_odh and _odh_available()
     cfg = ClusterConfig(gpus_per_node=8, odh=use_odh, webhook=use_odh, startup_probe=probe,
-                        reference_emulation=args.reference_emulation,
+                        reference_emulation=args.reference_emulation, transport=args.transport,
                         env={"SET_PIPELINE_RBAC": "false", "SET_PIPELINE_SECRET": "false"})
     lat_ms = []
     recon = 0

@@ -1,0 +1,54 @@
+"""Shared process plumbing for the ``cmd`` entry points: logging (zap-like, RFC3339
+timestamps, development/production modes), signal handling and runnable wrappers."""
+
+from __future__ import annotations
+
+import asyncio
+import logging
+import signal
+import sys
+import time
+
+
+class _RFC3339Formatter(logging.Formatter):
+    def formatTime(self, record, datefmt=None):  # noqa: N802 (logging API)
+        return time.strftime("%Y-%m-%dT%H:%M:%SZ", time.gmtime(record.created))
+
+
+def setup_logging(debug: bool = False, development: bool = False) -> None:
+    level = logging.DEBUG if (debug or development) else logging.INFO
+    h = logging.StreamHandler(sys.stderr)
+    if development:
+        h.setFormatter(_RFC3339Formatter("%(asctime)s\t%(levelname)s\t%(name)s\t%(message)s"))
+    else:
+        h.setFormatter(_RFC3339Formatter('{"ts":"%(asctime)s","level":"%(levelname)s","logger":"%(name)s",'
+                                         '"msg":"%(message)s"}'))
+    root = logging.getLogger()
+    root.handlers[:] = [h]
+    root.setLevel(level)
+    logging.getLogger("aiohttp.access").setLevel(logging.WARNING)
+
+
+def signal_event() -> asyncio.Event:
+    """``ctrl.SetupSignalHandler``: set on SIGTERM / SIGINT."""
+    ev = asyncio.Event()
+    loop = asyncio.get_running_loop()
+    for s in (signal.SIGTERM, signal.SIGINT):
+        try:
+            loop.add_signal_handler(s, ev.set)
+        except (NotImplementedError, RuntimeError):
+            pass
+    return ev
+
+
+class ServerRunnable:
+    """Adapter so servers (webhook, telemetry) join a manager's lifecycle."""
+
+    def __init__(self, start, stop):
+        self._start, self._stop = start, stop
+
+    async def start(self):
+        await self._start()
+
+    async def stop(self):
+        await self._stop()

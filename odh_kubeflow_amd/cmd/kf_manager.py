@@ -1,0 +1,90 @@
+"""Kubeflow notebook controller manager (reference ``components/notebook-controller/main.go``).
+
+Flags keep the reference names (``--metrics-addr``, ``--probe-addr``,
+``--enable-leader-election``, ``--leader-election-namespace``, ``--qps``, ``--burst``,
+``--zap-devel``); additions: ``--kubeconfig`` / ``--master``,
+``--max-concurrent-reconciles`` (default 8; the reference runs 1 worker).  Culling is
+wired only when ``ENABLE_CULLING=true`` (:111-123).  Leader-election ID
+``kubeflow-notebook-controller``.
+
+    python -m odh_kubeflow_amd.cmd.kf_manager --master http://127.0.0.1:6443
+"""
+
+from __future__ import annotations
+
+import argparse
+import asyncio
+import logging
+import os
+import sys
+from typing import List, Optional
+
+log = logging.getLogger("setup")
+
+
+def parse(argv: Optional[List[str]] = None) -> argparse.Namespace:
+    p = argparse.ArgumentParser(prog="kf-notebook-controller")
+    p.add_argument("--metrics-addr", default=":8080")
+    p.add_argument("--probe-addr", default=":8081")
+    p.add_argument("--leader-election-namespace", default="")
+    p.add_argument("--enable-leader-election", action="store_true")
+    p.add_argument("--burst", type=int, default=0)
+    p.add_argument("--qps", type=int, default=0)
+    p.add_argument("--zap-devel", dest="devel", action="store_true", default=True)
+    p.add_argument("--kubeconfig", default=None)
+    p.add_argument("--master", default=None)
+    p.add_argument("--max-concurrent-reconciles", type=int, default=8)
+    return p.parse_args(argv)
+
+
+def build(args, env=os.environ):
+    from ..controllers.metrics import NotebookMetrics
+    from ..controllers.notebook import NotebookEventReemitter, NotebookReconciler
+    from ..runtime.leaderelection import LeaderElector, namespace_from_env
+    from ..runtime.manager import Manager
+    from ..runtime.rest import RestClient, RestConfig
+
+    cfg = RestConfig.load(args.master, args.kubeconfig)
+    if args.qps:
+        cfg.qps = float(args.qps)
+    if args.burst:
+        cfg.burst = args.burst
+    elector = None
+    if args.enable_leader_election:
+        elector = LeaderElector(RestClient(cfg), "kubeflow-notebook-controller",
+                                args.leader_election_namespace or namespace_from_env())
+    mgr = Manager.remote(cfg, name="notebook-controller", default_max_concurrent=args.max_concurrent_reconciles,
+                         leader_elector=elector, metrics_addr=args.metrics_addr, probe_addr=args.probe_addr)
+    metrics = NotebookMetrics(mgr.reader, mgr.registry)
+    NotebookReconciler(mgr.client, mgr.reader, mgr.get_event_recorder_for("notebook-controller"), metrics,
+                       env=env).setup_with_manager(mgr)
+    NotebookEventReemitter(mgr.client, mgr.reader, mgr.get_event_recorder_for("notebook-controller")) \
+        .setup_with_manager(mgr)
+    if (env.get("ENABLE_CULLING") or "false") == "true":
+        from ..controllers.culling import CullingReconciler
+
+        CullingReconciler(mgr.client, mgr.reader, metrics, env=env).setup_with_manager(mgr)
+    else:
+        log.info("Culling of idle Pods is Disabled. To enable it set the ENV Var 'ENABLE_CULLING=true'")
+    mgr.add_healthz_check("healthz")
+    mgr.add_readyz_check("readyz")
+    return mgr
+
+
+async def amain(argv=None) -> int:
+    from .common import setup_logging, signal_event
+
+    args = parse(argv)
+    setup_logging(development=args.devel)
+    mgr = build(args)
+    log.info("starting manager")
+    await mgr.run_until(signal_event())
+    return 0
+
+
+def main(argv=None) -> int:
+    return asyncio.run(amain(argv))
+
+
+if __name__ == "__main__":
+    sys.exit(main())

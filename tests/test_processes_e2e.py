@@ -1,0 +1,145 @@
+"""Multi-process e2e: the deployable processes wired like the reference's kind CI
+(.github/workflows/odh_notebook_controller_integration_test.yaml:102-284): dev apiserver
+(+ StatefulSet controller / scheduler / GC), kf manager, odh manager with its HTTPS
+webhook registered through a MutatingWebhookConfiguration carrying a self-signed
+caBundle, and the MI355X node agent.  Create a notebook with inject-auth, wait for the
+pod to be Ready, delete it and check the cluster-scoped leftovers are gone."""
+
+import asyncio
+import os
+import socket
+import subprocess
+import sys
+import time
+
+import pytest
+
+from odh_kubeflow_amd.models import kinds
+from odh_kubeflow_amd.models import meta as m
+from odh_kubeflow_amd.models.notebook import notebook
+from odh_kubeflow_amd.runtime.rest import RestClient, RestConfig
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+pytestmark = pytest.mark.slow
+
+
+def free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def spawn(args, env_extra=None, log=None):
+    env = dict(os.environ, PYTHONPATH=ROOT, **(env_extra or {}))
+    return subprocess.Popen([sys.executable, "-m", *args], cwd=ROOT, env=env, stdout=log or subprocess.DEVNULL,
+                            stderr=subprocess.STDOUT)
+
+
+async def wait_http(url: str, timeout: float = 30.0) -> None:
+    import aiohttp
+
+    deadline = time.monotonic() + timeout
+    async with aiohttp.ClientSession() as s:
+        while time.monotonic() < deadline:
+            try:
+                async with s.get(url, ssl=False) as r:
+                    if r.status == 200:
+                        return
+            except Exception:
+                pass
+            await asyncio.sleep(0.1)
+    raise TimeoutError(url)
+
+
+async def eventually(fn, timeout=30.0, interval=0.1):
+    deadline = time.monotonic() + timeout
+    last = None
+    while time.monotonic() < deadline:
+        try:
+            last = await fn()
+            if last:
+                return last
+        except Exception as e:  # noqa: BLE001
+            last = e
+        await asyncio.sleep(interval)
+    raise AssertionError(f"condition not met: {last!r}")
+
+
+def test_processes_end_to_end(tmp_path, run):
+    from odh_kubeflow_amd.webhook.certs import generate
+    from odh_kubeflow_amd.webhook.server import mutating_webhook_configuration
+
+    api_port, wh_port = free_port(), free_port()
+    certs = generate(("127.0.0.1", "localhost"), str(tmp_path / "certs"))
+    logf = open(tmp_path / "procs.log", "wb")
+    master = f"http://127.0.0.1:{api_port}"
+    procs = [spawn(["odh_kubeflow_amd.cmd.apiserver", "--port", str(api_port), "--controllers",
+                    "--no-openshift-apis"], log=logf)]
+    try:
+        async def go():
+            await wait_http(master + "/healthz")
+            c = RestClient(RestConfig(host=master))
+            for ns in ("opendatahub", "user"):
+                await c.create({"apiVersion": "v1", "kind": "Namespace", "metadata": {"name": ns}})
+            common = {"K8S_NAMESPACE": "opendatahub", "SET_PIPELINE_RBAC": "false"}
+            procs.append(spawn(["odh_kubeflow_amd.cmd.kf_manager", "--master", master, "--metrics-addr", "0",
+                                "--probe-addr", "0", "--enable-leader-election"], common, logf))
+            procs.append(spawn(["odh_kubeflow_amd.cmd.odh_manager", "--master", master, "--metrics-bind-address", "0",
+                                "--health-probe-bind-address", "0", "--kube-rbac-proxy-image",
+                                "quay.io/brancz/kube-rbac-proxy:v0.18.1", "--webhook-cert-dir", certs.cert_dir,
+                                "--webhook-port", str(wh_port), "--webhook-host", "127.0.0.1", "--leader-elect"],
+                               common, logf))
+            procs.append(spawn(["odh_kubeflow_amd.cmd.node_agent", "--master", master, "--devices",
+                                "0,1,2,3,4,5,6,7", "--sysfs-root", str(tmp_path / "nosys")], common, logf))
+            await wait_http(f"https://127.0.0.1:{wh_port}/healthz")
+            await c.create(mutating_webhook_configuration(
+                certs.ca_bundle_b64, url=f"https://127.0.0.1:{wh_port}/mutate-notebook-v1"))
+            await eventually(lambda: c.get(kinds.NODE, "mi355x-node-0"))
+            t0 = time.monotonic()
+            await c.create(notebook("nb", "user", gpus=1, annotations={"notebooks.opendatahub.io/inject-auth": "true"}))
+
+            async def ready():
+                nb = await c.get(kinds.NOTEBOOK, "nb", "user")
+                st = nb.get("status") or {}
+                return st.get("readyReplicas") == 1 and any(
+                    x.get("type") == "Ready" and x.get("status") == "True" for x in st.get("conditions") or [])
+
+            await eventually(ready, 60)
+            dt = time.monotonic() - t0
+            nb = await c.get(kinds.NOTEBOOK, "nb", "user")
+            assert [x["name"] for x in nb["spec"]["template"]["spec"]["containers"]] == ["nb", "kube-rbac-proxy"]
+            assert "kubeflow-resource-stopped" not in m.annotations(nb)
+            pod = await c.get(kinds.POD, "nb-0", "user")
+            assert m.annotations(pod)["amd.com/gpu-ids"] == "0"
+            routes = await c.list(kinds.HTTP_ROUTE, "opendatahub")
+            assert [m.name(r) for r in routes] == ["nb-user-nb"]
+            leases = {m.name(x) for x in await c.list(kinds.LEASE, "opendatahub")}
+            assert {"kubeflow-notebook-controller", "odh-notebook-controller"} <= leases
+            await c.delete(kinds.NOTEBOOK, "nb", "user")
+
+            async def gone():
+                try:
+                    await c.get(kinds.NOTEBOOK, "nb", "user")
+                    return False
+                except Exception:
+                    return True
+
+            await eventually(gone, 30)
+            crbs = [m.name(x) for x in await c.list(kinds.CLUSTER_ROLE_BINDING)]
+            assert "nb-rbac-user-auth-delegator" not in crbs
+            await c.close()
+            return dt
+
+        dt = run(go(), timeout=120)
+        assert dt < 30
+    finally:
+        for p in procs:
+            p.terminate()
+        for p in procs:
+            try:
+                p.wait(10)
+            except subprocess.TimeoutExpired:
+                p.kill()
+        logf.close()

@@ -1,0 +1,424 @@
+"""Deployment manifests, generated from the code's own constants.
+
+``python -m odh_kubeflow_amd.deploy.manifests [--out config]`` writes the kustomize tree
+(the reference's ``kf/config/**`` + ``odh/config/**``):
+
+* ``crd/`` — ``notebooks.kubeflow.org`` with v1 (storage), v1alpha1, v1beta1 served,
+  ``status`` subresource and ``conversion: None`` (identical schemas);
+* ``rbac/`` — ClusterRoles from the verbs each controller actually uses (the reference's
+  kubebuilder markers, ``odh/controllers/notebook_controller.go:89-113``), leader-election
+  Roles, user aggregation roles (``kubeflow-notebooks-{admin,edit,view}``);
+* ``manager/`` — the two manager Deployments with the reference flags, probes on
+  :8081, metrics on :8080, ``GOMEMLIMIT``-style limits, env from ConfigMaps;
+* ``node-agent/`` — the MI355X node agent DaemonSet (``amd.com/gpu.family`` nodes,
+  ``/sys`` read-only for amdgpu telemetry, ``/dev/kfd`` + ``/dev/dri`` for the start-up
+  probe; it never requests ``amd.com/gpu`` itself);
+* ``webhook/`` — Service + MutatingWebhookConfiguration (``failurePolicy: Fail``);
+* ``overlays/{kubeflow,standalone,openshift,mi355x}`` — Istio on/off, OpenShift
+  service-ca injection + ``ADD_FSGROUP=false``, MI355X placement + GPU-busy culling;
+* ``samples/`` — Notebooks requesting 1 and 8 ``amd.com/gpu`` with the PyTorch-ROCm image.
+
+The CRD carries a structural schema for the fields the controllers rely on
+(``spec.template.spec.containers`` ``minItems: 1`` with required ``name``/``image``, as
+``kf/config/crd/patches/validation_patches.yaml``) and preserves the rest of the PodSpec
+(``x-kubernetes-preserve-unknown-fields``); kube-apiserver validates the pod template
+when the StatefulSet is created.  The full expanded PodSpec schema of the reference
+cannot be regenerated offline; the served versions, names, scope,
+subresource and status schema are identical.
+"""
+
+from __future__ import annotations
+
+import argparse
+import os
+from typing import Dict, List
+
+import yaml
+
+from ..controllers.odh.constants import KUBE_RBAC_PROXY_PORT
+from ..models.notebook import GPU_RESOURCE, VERSIONS
+
+ROCM_NOTEBOOK_IMAGE = "rocm/pytorch:rocm7.0_ubuntu22.04_py3.10_pytorch_release_2.10.0"
+MANAGER_IMAGE = "quay.io/opendatahub/odh-kubeflow-amd:latest"
+KUBE_RBAC_PROXY_IMAGE = "quay.io/brancz/kube-rbac-proxy:v0.18.1"
+
+
+# ------------------------------------------------------------------ CRD
+
+
+def _status_schema() -> dict:
+    state = {"type": "object", "x-kubernetes-preserve-unknown-fields": True}
+    return {
+        "type": "object",
+        "description": "NotebookStatus defines the observed state of Notebook",
+        "properties": {
+            "conditions": {
+                "type": "array",
+                "description": "Conditions is an array of current conditions",
+                "items": {"type": "object", "required": ["type"], "properties": {
+                    "type": {"type": "string", "description": "Type is the type of the condition. Possible values "
+                                                                "are Running|Waiting|Terminated"},
+                    "status": {"type": "string", "description": "Status of the condition, one of True, False, "
+                                                                  "Unknown."},
+                    "lastProbeTime": {"type": "string", "format": "date-time",
+                                      "description": "Last time we probed the condition."},
+                    "lastTransitionTime": {"type": "string", "format": "date-time",
+                                           "description": "Last time the condition transitioned from one status to "
+                                                          "another."},
+                    "reason": {"type": "string", "description": "(brief) reason the container is in the current "
+                                                                  "state"},
+                    "message": {"type": "string", "description": "Message regarding why the container is in the "
+                                                                   "current state."}}}},
+            "readyReplicas": {"type": "integer", "format": "int32",
+                              "description": "ReadyReplicas is the number of Pods created by the StatefulSet "
+                                             "controller that have a Ready Condition."},
+            "containerState": {"type": "object", "description": "ContainerState is the state of underlying "
+                                                                   "container.",
+                               "properties": {"running": state, "terminated": state, "waiting": state}},
+        },
+        "required": ["conditions", "containerState", "readyReplicas"],
+    }
+
+
+def _spec_schema() -> dict:
+    container = {"type": "object", "required": ["name", "image"], "x-kubernetes-preserve-unknown-fields": True,
+                 "properties": {"name": {"type": "string"}, "image": {"type": "string"}}}
+    return {
+        "type": "object",
+        "description": "NotebookSpec defines the desired state of Notebook",
+        "properties": {"template": {"type": "object", "properties": {"spec": {
+            "type": "object", "x-kubernetes-preserve-unknown-fields": True, "required": ["containers"],
+            "properties": {"containers": {"type": "array", "minItems": 1, "items": container}}}}}},
+    }
+
+
+def notebook_crd() -> dict:
+    versions = []
+    for v in ("v1", "v1alpha1", "v1beta1"):
+        versions.append({
+            "name": v, "served": True, "storage": v == "v1", "subresources": {"status": {}},
+            "schema": {"openAPIV3Schema": {
+                "type": "object", "description": "Notebook is the Schema for the notebooks API",
+                "properties": {"apiVersion": {"type": "string"}, "kind": {"type": "string"},
+                               "metadata": {"type": "object"}, "spec": _spec_schema(), "status": _status_schema()}}},
+        })
+    assert [x["name"] for x in versions] == sorted(VERSIONS, key=("v1", "v1alpha1", "v1beta1").index)
+    return {"apiVersion": "apiextensions.k8s.io/v1", "kind": "CustomResourceDefinition",
+            "metadata": {"name": "notebooks.kubeflow.org", "annotations": {"controller-gen.kubebuilder.io/version":
+                                                                            "odh-kubeflow-amd"}},
+            "spec": {"group": "kubeflow.org", "scope": "Namespaced", "conversion": {"strategy": "None"},
+                     "names": {"kind": "Notebook", "listKind": "NotebookList", "plural": "notebooks",
+                               "singular": "notebook"},
+                     "versions": versions}}
+
+
+# ------------------------------------------------------------------ RBAC
+
+
+def _rule(groups, resources, verbs) -> dict:
+    return {"apiGroups": list(groups), "resources": list(resources), "verbs": list(verbs)}
+
+
+ALL = ["create", "delete", "get", "list", "patch", "update", "watch"]
+
+
+def kf_role() -> dict:
+    return {"apiVersion": "rbac.authorization.k8s.io/v1", "kind": "ClusterRole",
+            "metadata": {"name": "notebook-controller-role"},
+            "rules": [
+                _rule([""], ["events"], ["create", "get", "list", "patch", "watch"]),
+                _rule([""], ["pods"], ["delete", "get", "list", "watch"]),
+                _rule([""], ["services"], ALL),
+                _rule(["apps"], ["statefulsets"], ALL),
+                _rule(["kubeflow.org"], ["notebooks", "notebooks/finalizers", "notebooks/status"], ALL),
+                _rule(["networking.istio.io"], ["virtualservices"], ALL),
+                _rule([""], ["nodes"], ["get", "list", "watch"]),
+            ]}
+
+
+def odh_role() -> dict:
+    return {"apiVersion": "rbac.authorization.k8s.io/v1", "kind": "ClusterRole",
+            "metadata": {"name": "odh-notebook-controller-manager-role"},
+            "rules": [
+                _rule(["authentication.k8s.io"], ["tokenreviews"], ["create"]),
+                _rule(["authorization.k8s.io"], ["subjectaccessreviews"], ["create"]),
+                _rule(["kubeflow.org"], ["notebooks"], ["get", "list", "watch", "patch", "update"]),
+                _rule(["kubeflow.org"], ["notebooks/status"], ["get"]),
+                _rule(["kubeflow.org"], ["notebooks/finalizers"], ["update", "patch"]),
+                _rule(["gateway.networking.k8s.io"], ["httproutes", "referencegrants"], ALL),
+                _rule(["gateway.networking.k8s.io"], ["gateways"], ["get", "list", "watch"]),
+                _rule([""], ["services", "serviceaccounts", "secrets", "configmaps"],
+                      ["get", "list", "watch", "create", "update", "patch"]),
+                _rule(["config.openshift.io"], ["proxies"], ["get", "list", "watch"]),
+                _rule(["networking.k8s.io"], ["networkpolicies"], ["get", "list", "watch", "create", "update", "patch"]),
+                _rule(["networking.k8s.io"], ["networkpolicies/finalizers"], ["update", "patch"]),
+                _rule(["oauth.openshift.io"], ["oauthclients"], ["get", "list", "watch", "update", "patch", "delete"]),
+                _rule(["rbac.authorization.k8s.io"], ["roles"], ["get", "list", "watch", "create", "update", "patch"]),
+                _rule(["rbac.authorization.k8s.io"], ["rolebindings", "clusterrolebindings"], ALL),
+                _rule(["route.openshift.io"], ["routes"], ["get", "list", "watch"]),
+                _rule(["image.openshift.io"], ["imagestreams"], ["list", "get", "watch"]),
+                _rule(["datasciencepipelinesapplications.opendatahub.io"], ["datasciencepipelinesapplications"],
+                      ["get", "list", "watch"]),
+                _rule(["datasciencepipelinesapplications.opendatahub.io"], ["datasciencepipelinesapplications/api"],
+                      ["get", "create", "update", "patch", "delete"]),
+            ]}
+
+
+def node_agent_role() -> dict:
+    return {"apiVersion": "rbac.authorization.k8s.io/v1", "kind": "ClusterRole",
+            "metadata": {"name": "mi355x-node-agent-role"},
+            "rules": [_rule([""], ["nodes"], ["get", "list", "watch", "create", "patch", "update"]),
+                      _rule([""], ["pods"], ["get", "list", "watch", "patch"]),
+                      _rule([""], ["pods/status"], ["patch", "update"]),
+                      _rule([""], ["events"], ["create", "patch"])]}
+
+
+def leader_election_role(name: str) -> dict:
+    return {"apiVersion": "rbac.authorization.k8s.io/v1", "kind": "Role", "metadata": {"name": name},
+            "rules": [_rule(["coordination.k8s.io"], ["leases"], ALL), _rule([""], ["events"], ["create", "patch"])]}
+
+
+def user_cluster_roles() -> List[dict]:
+    out = []
+    for name, verbs, agg in (("kubeflow-notebooks-admin", ["get", "list", "watch", "create", "delete",
+                                                           "deletecollection", "patch", "update"], "admin"),
+                             ("kubeflow-notebooks-edit", ["get", "list", "watch", "create", "delete",
+                                                          "deletecollection", "patch", "update"], "edit"),
+                             ("kubeflow-notebooks-view", ["get", "list", "watch"], "view")):
+        out.append({"apiVersion": "rbac.authorization.k8s.io/v1", "kind": "ClusterRole",
+                    "metadata": {"name": name, "labels": {f"rbac.authorization.kubeflow.org/aggregate-to-kubeflow-{agg}":
+                                                          "true"}},
+                    "rules": [_rule(["kubeflow.org"], ["notebooks", "notebooks/status"], verbs)]})
+    return out
+
+
+def binding(kind: str, name: str, role: str, sa: str, ns: str = "system") -> dict:
+    b = {"apiVersion": "rbac.authorization.k8s.io/v1", "kind": kind, "metadata": {"name": name},
+         "roleRef": {"apiGroup": "rbac.authorization.k8s.io", "kind": kind.replace("Binding", ""), "name": role},
+         "subjects": [{"kind": "ServiceAccount", "name": sa, "namespace": ns}]}
+    return b
+
+
+# ------------------------------------------------------------------ workloads
+
+
+def _probes(port: int = 8081) -> dict:
+    return {"livenessProbe": {"httpGet": {"path": "/healthz", "port": port}, "initialDelaySeconds": 15,
+                              "periodSeconds": 20},
+            "readinessProbe": {"httpGet": {"path": "/readyz", "port": port}, "initialDelaySeconds": 5,
+                               "periodSeconds": 10}}
+
+
+def kf_deployment() -> dict:
+    c = {"name": "manager", "image": MANAGER_IMAGE,
+         "command": ["python", "-m", "odh_kubeflow_amd.cmd.kf_manager"],
+         "args": ["--enable-leader-election", "--metrics-addr=:8080", "--probe-addr=:8081"],
+         "envFrom": [{"configMapRef": {"name": "config"}}],
+         "env": [{"name": k, "valueFrom": {"configMapKeyRef": {"name": "notebook-controller-culler-config",
+                                                                "key": k, "optional": True}}}
+                 for k in ("ENABLE_CULLING", "CULL_IDLE_TIME", "IDLENESS_CHECK_PERIOD", "CULLING_ACTIVITY_SOURCE",
+                           "CULLING_GPU_BUSY_THRESHOLD")],
+         "ports": [{"name": "metrics", "containerPort": 8080}, {"name": "probes", "containerPort": 8081}],
+         "resources": {"requests": {"cpu": "500m", "memory": "256Mi"}, "limits": {"cpu": "2", "memory": "2Gi"}},
+         **_probes()}
+    return {"apiVersion": "apps/v1", "kind": "Deployment",
+            "metadata": {"name": "deployment", "labels": {"app": "notebook-controller"}},
+            "spec": {"replicas": 1, "selector": {"matchLabels": {"app": "notebook-controller"}},
+                     "template": {"metadata": {"labels": {"app": "notebook-controller"}},
+                                  "spec": {"serviceAccountName": "service-account", "containers": [c]}}}}
+
+
+def odh_deployment() -> dict:
+    c = {"name": "manager", "image": MANAGER_IMAGE,
+         "command": ["python", "-m", "odh_kubeflow_amd.cmd.odh_manager"],
+         "args": ["--leader-elect", f"--kube-rbac-proxy-image=$(KUBE_RBAC_PROXY_IMAGE)",
+                  "--webhook-cert-dir=/tmp/k8s-webhook-server/serving-certs", "--webhook-port=8443"],
+         "env": [{"name": "KUBE_RBAC_PROXY_IMAGE", "value": KUBE_RBAC_PROXY_IMAGE},
+                 {"name": "SET_PIPELINE_RBAC", "value": "true"}, {"name": "SET_PIPELINE_SECRET", "value": "true"},
+                 {"name": "INJECT_CLUSTER_PROXY_ENV", "valueFrom": {"configMapKeyRef": {
+                     "name": "notebook-controller-setting-config", "key": "INJECT_CLUSTER_PROXY_ENV",
+                     "optional": True}}},
+                 {"name": "K8S_NAMESPACE", "valueFrom": {"fieldRef": {"fieldPath": "metadata.namespace"}}}],
+         "ports": [{"name": "webhook", "containerPort": 8443}, {"name": "metrics", "containerPort": 8080},
+                   {"name": "probes", "containerPort": 8081}],
+         "resources": {"requests": {"cpu": "500m", "memory": "256Mi"}, "limits": {"cpu": "2", "memory": "4Gi"}},
+         "volumeMounts": [{"name": "cert", "mountPath": "/tmp/k8s-webhook-server/serving-certs", "readOnly": True}],
+         **_probes()}
+    return {"apiVersion": "apps/v1", "kind": "Deployment",
+            "metadata": {"name": "manager", "labels": {"app": "odh-notebook-controller"}},
+            "spec": {"replicas": 1, "strategy": {"type": "RollingUpdate", "rollingUpdate": {"maxUnavailable": "100%"}},
+                     "selector": {"matchLabels": {"app": "odh-notebook-controller"}},
+                     "template": {"metadata": {"labels": {"app": "odh-notebook-controller"}},
+                                  "spec": {"serviceAccountName": "manager", "containers": [c],
+                                           "volumes": [{"name": "cert", "secret": {
+                                               "secretName": "odh-notebook-controller-webhook-cert",
+                                               "defaultMode": 420}}]}}}}
+
+
+def node_agent_daemonset() -> dict:
+    c = {"name": "agent", "image": MANAGER_IMAGE,
+         "command": ["python", "-m", "odh_kubeflow_amd.cmd.node_agent"],
+         "args": ["--node-name=$(NODE_NAME)", "--address=$(NODE_IP)", "--activity-port=9464",
+                  "--sysfs-root=/host/sys", "--devices=0,1,2,3,4,5,6,7"],
+         "env": [{"name": "NODE_NAME", "valueFrom": {"fieldRef": {"fieldPath": "spec.nodeName"}}},
+                 {"name": "NODE_IP", "valueFrom": {"fieldRef": {"fieldPath": "status.hostIP"}}}],
+         "ports": [{"name": "gpu-activity", "containerPort": 9464, "hostPort": 9464}],
+         "volumeMounts": [{"name": "sys", "mountPath": "/host/sys", "readOnly": True},
+                          {"name": "kfd", "mountPath": "/dev/kfd"}, {"name": "dri", "mountPath": "/dev/dri"}],
+         "securityContext": {"readOnlyRootFilesystem": True, "allowPrivilegeEscalation": False},
+         "resources": {"requests": {"cpu": "100m", "memory": "512Mi"}, "limits": {"memory": "8Gi"}}}
+    return {"apiVersion": "apps/v1", "kind": "DaemonSet",
+            "metadata": {"name": "mi355x-node-agent", "labels": {"app": "mi355x-node-agent"}},
+            "spec": {"selector": {"matchLabels": {"app": "mi355x-node-agent"}},
+                     "template": {"metadata": {"labels": {"app": "mi355x-node-agent"}},
+                                  "spec": {"serviceAccountName": "mi355x-node-agent",
+                                           "nodeSelector": {"amd.com/gpu.family": "AI"},
+                                           "tolerations": [{"key": GPU_RESOURCE, "operator": "Exists",
+                                                            "effect": "NoSchedule"}],
+                                           "containers": [c],
+                                           "volumes": [{"name": "sys", "hostPath": {"path": "/sys"}},
+                                                       {"name": "kfd", "hostPath": {"path": "/dev/kfd"}},
+                                                       {"name": "dri", "hostPath": {"path": "/dev/dri"}}]}}}}
+
+
+def webhook_service() -> dict:
+    return {"apiVersion": "v1", "kind": "Service",
+            "metadata": {"name": "odh-notebook-controller-webhook-service"},
+            "spec": {"ports": [{"port": 443, "targetPort": 8443, "protocol": "TCP"}],
+                     "selector": {"app": "odh-notebook-controller"}}}
+
+
+def metrics_service(name: str, app: str) -> dict:
+    return {"apiVersion": "v1", "kind": "Service", "metadata": {"name": name, "labels": {"app": app}},
+            "spec": {"ports": [{"name": "metrics", "port": 8080, "targetPort": 8080}], "selector": {"app": app}}}
+
+
+def mwc() -> dict:
+    from ..webhook.server import mutating_webhook_configuration
+
+    o = mutating_webhook_configuration("", service_namespace="system")
+    o["webhooks"][0]["clientConfig"].pop("caBundle")
+    return o
+
+
+def sample(name: str, gpus: int, version: str = "v1", auth: bool = False) -> dict:
+    ann = {"notebooks.opendatahub.io/inject-auth": "true"} if auth else {}
+    c = {"name": name, "image": ROCM_NOTEBOOK_IMAGE,
+         "resources": {"limits": {GPU_RESOURCE: str(gpus), "memory": f"{64 * gpus}Gi", "cpu": str(8 * gpus)},
+                       "requests": {GPU_RESOURCE: str(gpus), "memory": f"{32 * gpus}Gi", "cpu": str(4 * gpus)}},
+         "volumeMounts": [{"name": "dshm", "mountPath": "/dev/shm"}]}
+    return {"apiVersion": f"kubeflow.org/{version}", "kind": "Notebook",
+            "metadata": {"name": name, **({"annotations": ann} if ann else {})},
+            "spec": {"template": {"spec": {"containers": [c], "volumes": [
+                # /dev/shm sized for RCCL/xGMI collectives of a multi-GPU notebook
+                {"name": "dshm", "emptyDir": {"medium": "Memory", "sizeLimit": f"{16 * gpus}Gi"}}]}}}}
+
+
+def kustomization(resources: List[str], **extra) -> dict:
+    k = {"apiVersion": "kustomize.config.k8s.io/v1beta1", "kind": "Kustomization", "resources": resources}
+    k.update(extra)
+    return k
+
+
+def tree() -> Dict[str, object]:
+    """path → document (or list of documents)."""
+    t: Dict[str, object] = {}
+    t["crd/bases/kubeflow.org_notebooks.yaml"] = notebook_crd()
+    t["crd/kustomization.yaml"] = kustomization(["bases/kubeflow.org_notebooks.yaml"])
+    t["rbac/kf_role.yaml"] = kf_role()
+    t["rbac/odh_role.yaml"] = odh_role()
+    t["rbac/node_agent_role.yaml"] = node_agent_role()
+    t["rbac/leader_election_roles.yaml"] = [leader_election_role("notebook-controller-leader-election-role"),
+                                            leader_election_role("odh-notebook-controller-leader-election-role")]
+    t["rbac/role_bindings.yaml"] = [
+        binding("ClusterRoleBinding", "notebook-controller-role-binding", "notebook-controller-role", "service-account"),
+        binding("ClusterRoleBinding", "odh-notebook-controller-manager-rolebinding",
+                "odh-notebook-controller-manager-role", "manager"),
+        binding("ClusterRoleBinding", "mi355x-node-agent-rolebinding", "mi355x-node-agent-role", "mi355x-node-agent"),
+        binding("RoleBinding", "notebook-controller-leader-election-rolebinding",
+                "notebook-controller-leader-election-role", "service-account"),
+        binding("RoleBinding", "odh-notebook-controller-leader-election-rolebinding",
+                "odh-notebook-controller-leader-election-role", "manager")]
+    t["rbac/service_accounts.yaml"] = [{"apiVersion": "v1", "kind": "ServiceAccount", "metadata": {"name": n}}
+                                       for n in ("service-account", "manager", "mi355x-node-agent")]
+    t["rbac/user_cluster_roles.yaml"] = user_cluster_roles()
+    t["rbac/kustomization.yaml"] = kustomization(sorted(p.split("/", 1)[1] for p in t if p.startswith("rbac/")
+                                                        and not p.endswith("kustomization.yaml")))
+    t["manager/kf_manager.yaml"] = kf_deployment()
+    t["manager/odh_manager.yaml"] = odh_deployment()
+    t["manager/services.yaml"] = [metrics_service("notebook-controller-service", "notebook-controller"),
+                                  metrics_service("odh-notebook-controller-service", "odh-notebook-controller")]
+    t["manager/kustomization.yaml"] = kustomization(
+        ["kf_manager.yaml", "odh_manager.yaml", "services.yaml"],
+        configMapGenerator=[{"name": "config", "envs": ["params.env"]},
+                            {"name": "notebook-controller-culler-config",
+                             "literals": ["ENABLE_CULLING=false", "CULL_IDLE_TIME=1440", "IDLENESS_CHECK_PERIOD=1",
+                                          "CULLING_ACTIVITY_SOURCE=jupyter", "CULLING_GPU_BUSY_THRESHOLD=5"]}],
+        generatorOptions={"disableNameSuffixHash": True})
+    t["manager/params.env"] = "USE_ISTIO=false\nISTIO_GATEWAY=kubeflow/kubeflow-gateway\nISTIO_HOST=*\n" \
+                              "CLUSTER_DOMAIN=cluster.local\nADD_FSGROUP=true\nGPU_NODE_SELECTOR=false\n"
+    t["node-agent/daemonset.yaml"] = node_agent_daemonset()
+    t["node-agent/kustomization.yaml"] = kustomization(["daemonset.yaml"])
+    t["webhook/service.yaml"] = webhook_service()
+    t["webhook/manifests.yaml"] = mwc()
+    t["webhook/kustomization.yaml"] = kustomization(["service.yaml", "manifests.yaml"])
+    t["default/kustomization.yaml"] = kustomization(["../crd", "../rbac", "../manager", "../webhook", "../node-agent"],
+                                                    namespace="opendatahub", namePrefix="odh-kubeflow-amd-")
+    t["overlays/standalone/kustomization.yaml"] = kustomization(["../../default"])
+    t["overlays/kubeflow/kustomization.yaml"] = kustomization(
+        ["../../default"], namespace="kubeflow",
+        patches=[{"target": {"kind": "ConfigMap", "name": ".*config"}, "patch":
+                  "- op: replace\n  path: /data/USE_ISTIO\n  value: \"true\"\n"}])
+    t["overlays/openshift/kustomization.yaml"] = kustomization(
+        ["../../default"],
+        patches=[{"target": {"kind": "Service", "name": ".*webhook-service"}, "patch":
+                  "- op: add\n  path: /metadata/annotations\n  value:\n    service.beta.openshift.io/"
+                  "serving-cert-secret-name: odh-notebook-controller-webhook-cert\n"},
+                 {"target": {"kind": "MutatingWebhookConfiguration"}, "patch":
+                  "- op: add\n  path: /metadata/annotations\n  value:\n    service.beta.openshift.io/"
+                  "inject-cabundle: \"true\"\n"},
+                 {"target": {"kind": "ConfigMap", "name": ".*config"}, "patch":
+                  "- op: replace\n  path: /data/ADD_FSGROUP\n  value: \"false\"\n"}])
+    t["overlays/mi355x/kustomization.yaml"] = kustomization(
+        ["../../default"],
+        patches=[{"target": {"kind": "ConfigMap", "name": ".*config"}, "patch":
+                  "- op: replace\n  path: /data/GPU_NODE_SELECTOR\n  value: \"true\"\n"},
+                 {"target": {"kind": "ConfigMap", "name": ".*culler-config"}, "patch":
+                  "- op: replace\n  path: /data/CULLING_ACTIVITY_SOURCE\n  value: combined\n"
+                  "- op: replace\n  path: /data/ENABLE_CULLING\n  value: \"true\"\n"}])
+    t["samples/notebook_v1_1gpu.yaml"] = sample("rocm-pytorch-1gpu", 1)
+    t["samples/notebook_v1_8gpu_auth.yaml"] = sample("rocm-pytorch-8gpu", 8, auth=True)
+    t["samples/notebook_v1alpha1.yaml"] = sample("rocm-pytorch-v1alpha1", 1, "v1alpha1")
+    t["samples/notebook_v1beta1.yaml"] = sample("rocm-pytorch-v1beta1", 1, "v1beta1")
+    return t
+
+
+def write(out: str) -> List[str]:
+    written = []
+    for path, doc in sorted(tree().items()):
+        full = os.path.join(out, path)
+        os.makedirs(os.path.dirname(full), exist_ok=True)
+        with open(full, "w") as f:
+            f.write("# generated by `python -m odh_kubeflow_amd.deploy.manifests` — do not edit\n")
+            if isinstance(doc, str):
+                f.write(doc)
+            elif isinstance(doc, list):
+                yaml.safe_dump_all(doc, f, sort_keys=False)
+            else:
+                yaml.safe_dump(doc, f, sort_keys=False)
+        written.append(full)
+    return written
+
+
+def main(argv=None) -> int:
+    p = argparse.ArgumentParser()
+    p.add_argument("--out", default=os.path.join(os.path.dirname(os.path.dirname(os.path.dirname(
+        os.path.abspath(__file__)))), "config"))
+    a = p.parse_args(argv)
+    for w in write(a.out):
+        print(w)
+    return 0
+
+
+if __name__ == "__main__":
+    raise SystemExit(main())

@@ -95,6 +95,9 @@ def _spec_part(obj: dict) -> dict:
     return {k: v for k, v in obj.items() if k not in ("metadata", "status", "apiVersion", "kind")}
 
 
+_INFO_BY_KEY = {i.key: i for i in SCHEME.all()}
+
+
 class ObjectStore:
     """The apiserver's storage + request-handling semantics, in process."""
 
@@ -108,6 +111,7 @@ class ObjectStore:
         self._watchers: Dict[str, Dict[int, _Watcher]] = {}
         self._wid = itertools.count(1)
         self._owner_index: Dict[str, set] = {}  # owner uid -> {(resource, ns, name)}
+        self._uids: Dict[str, Tuple[str, str, str]] = {}  # uid -> (resource, ns, name): GC lookups in O(1)
         self.gc_enabled = gc
         self.strict_namespaces = strict_namespaces
         self.installed = {i.key for i in SCHEME.all()} if install_all_crds else {
@@ -343,6 +347,7 @@ class ObjectStore:
                 return self._out(info, obj, version)
             md["resourceVersion"] = str(self._next_rv())
             bucket[k] = obj
+            self._uids[md["uid"]] = (info.key, ns, k[1])
             self._index_owner(info, obj)
             self.write_count += 1
             self._emit(info, ADDED, obj, None)
@@ -502,6 +507,7 @@ class ObjectStore:
     def _remove(self, info: ResourceInfo, live: dict, final: dict, version: Optional[str]) -> dict:
         ns, name = m.namespace(live), m.name(live)
         self._bucket(info).pop((ns, name), None)
+        self._uids.pop(m.uid(live), None)
         self._index_owner(info, live, remove=True)
         self.write_count += 1
         self._emit(info, DELETED, final, live)
@@ -515,7 +521,7 @@ class ObjectStore:
     def _gc_dependents(self, owner_uid: str) -> None:
         deps = list(self._owner_index.get(owner_uid, ()))
         for res, ns, name in deps:
-            info = next((i for i in SCHEME.all() if i.key == res), None)
+            info = _INFO_BY_KEY.get(res)
             if info is None:
                 continue
             obj = self._bucket(info).get((ns, name))
@@ -531,20 +537,21 @@ class ObjectStore:
                 pass
 
     def _uid_exists(self, u: str) -> bool:
-        for b in self._data.values():
-            for o in b.values():
-                if o["metadata"].get("uid") == u:
-                    return True
-        return False
+        return u in self._uids
 
     def _gc_foreground_owners(self, removed: dict) -> None:
         for r in removed["metadata"].get("ownerReferences") or []:
             u = r.get("uid")
-            for info in SCHEME.all():
-                if info.key not in self._data:
+            loc = self._uids.get(u)
+            if loc is None:
+                continue
+            info = _INFO_BY_KEY.get(loc[0])
+            if info is None:
+                continue
+            for (ns, name), o in ((loc[1:], self._bucket(info).get(loc[1:])),):
+                if o is None:
                     continue
-                for (ns, name), o in list(self._bucket(info).items()):
-                    if o["metadata"].get("uid") == u and "foregroundDeletion" in (o["metadata"].get("finalizers") or []):
+                if "foregroundDeletion" in (o["metadata"].get("finalizers") or []):
                         if not self._owner_index.get(u):
                             new = deepcopy_json(o)
                             new["metadata"]["finalizers"] = [f for f in new["metadata"]["finalizers"]

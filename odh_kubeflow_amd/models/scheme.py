@@ -69,6 +69,7 @@ class Scheme:
     def __init__(self) -> None:
         self._by_kind: Dict[Tuple[str, str], ResourceInfo] = {}
         self._by_plural: Dict[Tuple[str, str], ResourceInfo] = {}
+        self._str_cache: Dict[str, ResourceInfo] = {}
 
     def register(self, info: ResourceInfo) -> ResourceInfo:
         if not info.list_kind:
@@ -96,6 +97,10 @@ class Scheme:
         """Accept a ResourceInfo, a GVK, ``"group/version/Kind"`` / ``"v1/Kind"`` or an object."""
         if isinstance(ref, ResourceInfo):
             return ref
+        if isinstance(ref, str):
+            hit = self._str_cache.get(ref)
+            if hit is not None:
+                return hit
         if isinstance(ref, GVK):
             info = self.for_kind(ref.group, ref.kind)
         elif isinstance(ref, dict):
@@ -107,6 +112,8 @@ class Scheme:
             info = None
         if info is None:
             raise KeyError(f"no kind registered for {ref!r}")
+        if isinstance(ref, str):
+            self._str_cache[ref] = info
         return info
 
     def all(self):

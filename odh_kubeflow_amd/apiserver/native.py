@@ -1,0 +1,103 @@
+"""Launcher for the native C++ apiserver (``native/apiserver/apiserver.cpp`` →
+``native/bin/odh-apiserver``).
+
+The scheme (kinds, plurals, scope, versions, status subresource, installed CRDs) is
+generated from :data:`~odh_kubeflow_amd.models.scheme.SCHEME` so both apiservers —
+the in-process Python :class:`~odh_kubeflow_amd.apiserver.store.ObjectStore` and the
+native one — serve exactly the same API.  :class:`StoreView` gives tests and the
+benchmark the ``peek`` / ``list_nocopy`` read helpers of the in-process store on top of
+a watch-backed informer cache.
+"""
+
+from __future__ import annotations
+
+import asyncio
+import json
+import os
+import tempfile
+from typing import Iterable, List, Optional
+
+from ..models.scheme import OPTIONAL_CRDS, SCHEME
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+BINARY = os.path.join(os.path.dirname(HERE), "native", "bin", "odh-apiserver")
+
+
+def scheme_config(uninstalled: Iterable[str] = (), gc: bool = False, token: Optional[str] = None,
+                  history: int = 4096) -> dict:
+    skip = {SCHEME.resolve(k).key for k in uninstalled}
+    res = []
+    for i in SCHEME.all():
+        res.append({"group": i.group, "kind": i.kind, "plural": i.plural, "singular": i.singular,
+                    "listKind": i.list_kind, "versions": list(i.versions), "storageVersion": i.storage_version,
+                    "namespaced": i.namespaced, "status": i.status_subresource, "installed": i.key not in skip})
+    cfg = {"resources": res, "gc": gc, "history": history}
+    if token:
+        cfg["token"] = token
+    return cfg
+
+
+def available() -> bool:
+    return os.path.exists(BINARY)
+
+
+class NativeApiServer:
+    def __init__(self, uninstalled: Iterable[str] = (), gc: bool = False, token: Optional[str] = None,
+                 host: str = "127.0.0.1", port: int = 0, history: int = 4096):
+        self.cfg = scheme_config(uninstalled, gc, token, history)
+        self.host = host
+        self.port = port
+        self.proc: Optional[asyncio.subprocess.Process] = None
+        self._cfg_path: Optional[str] = None
+
+    async def start(self) -> "NativeApiServer":
+        if not available():
+            from ..ops.build import build
+
+            build(verbose=False)
+        fd, self._cfg_path = tempfile.mkstemp(prefix="odh-apiserver-", suffix=".json")
+        with os.fdopen(fd, "w") as f:
+            json.dump(self.cfg, f)
+        self.proc = await asyncio.create_subprocess_exec(
+            BINARY, "--config", self._cfg_path, "--host", self.host, "--port", str(self.port),
+            stdout=asyncio.subprocess.PIPE)
+        line = await asyncio.wait_for(self.proc.stdout.readline(), 30)
+        if not line.startswith(b"LISTENING"):
+            raise RuntimeError(f"native apiserver failed to start: {line!r}")
+        self.port = int(line.split()[1])
+        return self
+
+    @property
+    def url(self) -> str:
+        return f"http://{self.host}:{self.port}"
+
+    async def stats(self) -> dict:
+        import aiohttp
+
+        async with aiohttp.ClientSession() as s:
+            async with s.get(self.url + "/metrics") as r:
+                return await r.json(content_type=None)
+
+    async def stop(self) -> None:
+        if self.proc is not None and self.proc.returncode is None:
+            self.proc.terminate()
+            try:
+                await asyncio.wait_for(self.proc.wait(), 10)
+            except asyncio.TimeoutError:
+                self.proc.kill()
+        if self._cfg_path and os.path.exists(self._cfg_path):
+            os.unlink(self._cfg_path)
+
+
+class StoreView:
+    """Read-only ``ObjectStore``-like view (``peek``, ``list_nocopy``) over an informer cache."""
+
+    def __init__(self, cache):
+        self.cache = cache
+
+    def peek(self, ref, name: str, namespace: Optional[str] = None) -> Optional[dict]:
+        return self.cache.get(ref, name, namespace)
+
+    def list_nocopy(self, ref, namespace=None, label_selector=None, field_selector=None, owner_uid=None,
+                    copy: bool = False, version=None) -> List[dict]:
+        return self.cache.list(ref, namespace, label_selector, field_selector, owner_uid)

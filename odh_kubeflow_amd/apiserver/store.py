@@ -431,6 +431,19 @@ class ObjectStore:
 
     async def patch(self, ref, name: str, namespace: Optional[str], patch: Any, patch_type: str = "merge",
                     subresource: Optional[str] = None) -> dict:
+        """Patches without a resourceVersion precondition retry on a concurrent write
+        (the apiserver's GuaranteedUpdate loop) instead of surfacing a Conflict."""
+        precond = isinstance(patch, dict) and bool((patch.get("metadata") or {}).get("resourceVersion"))
+        for attempt in range(17):
+            try:
+                return await self._patch_once(ref, name, namespace, patch, patch_type, subresource)
+            except Conflict:
+                if precond or attempt == 16:
+                    raise
+        raise AssertionError("unreachable")
+
+    async def _patch_once(self, ref, name: str, namespace: Optional[str], patch: Any, patch_type: str,
+                          subresource: Optional[str]) -> dict:
         info = self._info(ref)
         self.request_count += 1
         ns = self._ns(info, namespace) if info.namespaced else ""

@@ -42,18 +42,25 @@ class ClusterConfig:
     # "inprocess": managers share the store directly; "http": the store is served by the REST
     # apiserver and the kf / odh managers, the webhook (HTTPS, MutatingWebhookConfiguration)
     # and the node agents talk to it over HTTP exactly as they would to kube-apiserver
-    transport: str = "inprocess"
+    transport: str = field(default_factory=lambda: os.environ.get("ODH_CLUSTER_TRANSPORT", "inprocess"))
     remote_kubelets: bool = True  # with transport="http": node agents use REST clients too
+
+
+OPENSHIFT_CRDS = (kinds.IMAGE_STREAM, kinds.PROXY, kinds.ROUTE, kinds.OAUTH_CLIENT)
 
 
 class LocalCluster:
     def __init__(self, cfg: Optional[ClusterConfig] = None, store: Optional[ObjectStore] = None):
         self.cfg = cfg or ClusterConfig()
         self.env = {**os.environ, **self.cfg.env}
-        self.store = store or ObjectStore(gc=self.cfg.gc)
-        if not self.cfg.openshift and store is None:
-            for crd in (kinds.IMAGE_STREAM, kinds.PROXY, kinds.ROUTE, kinds.OAUTH_CLIENT):
-                self.store.uninstall_crd(crd)
+        self.native = None
+        if self.cfg.transport == "native":
+            self.store = None  # a StoreView over an informer cache, set in start()
+        else:
+            self.store = store or ObjectStore(gc=self.cfg.gc)
+            if not self.cfg.openshift and store is None:
+                for crd in OPENSHIFT_CRDS:
+                    self.store.uninstall_crd(crd)
         self.managers: List[Manager] = []
         self.kube: Optional[Manager] = None
         self.kf: Optional[Manager] = None
@@ -69,7 +76,7 @@ class LocalCluster:
     # ------------------------------------------------------------------ build
 
     def _mgr(self, name: str, remote: bool = False, **kw) -> Manager:
-        if remote and self.rest_config is not None:
+        if (remote or self.cfg.transport == "native") and self.rest_config is not None:
             from .runtime.informer import strip_data, strip_managed_fields
 
             tf = {kinds.CONFIG_MAP: strip_data, kinds.SECRET: strip_data} if kw.get("uncached") else None
@@ -94,13 +101,29 @@ class LocalCluster:
         cfg = self.cfg
         if cfg.transport == "http":
             await self._start_apiserver()
-        admin = Manager.in_process(self.store, name="admin").client
+        if cfg.transport == "native":
+            from .apiserver.native import NativeApiServer, StoreView
+            from .runtime.informer import InformerCache
+            from .runtime.rest import RestClient, RestConfig
+
+            self.native = await NativeApiServer(() if cfg.openshift else OPENSHIFT_CRDS, gc=cfg.gc).start()
+            self.rest_config = RestConfig(host=self.native.url)
+            admin = RestClient(self.rest_config)
+            self._view_cache = InformerCache(admin)
+            self.store = StoreView(self._view_cache)
+            await self._view_cache.wait_synced(
+                [k for k in (kinds.NAMESPACE, kinds.NODE, kinds.NOTEBOOK, kinds.STATEFUL_SET, kinds.POD,
+                             kinds.SERVICE, kinds.EVENT, kinds.CONFIG_MAP, kinds.SECRET, kinds.SERVICE_ACCOUNT,
+                             kinds.NETWORK_POLICY, kinds.ROLE_BINDING, kinds.CLUSTER_ROLE_BINDING, kinds.HTTP_ROUTE,
+                             kinds.REFERENCE_GRANT, kinds.VIRTUAL_SERVICE, kinds.LEASE)])
+        else:
+            admin = Manager.in_process(self.store, name="admin").client
         self.admin = admin
         for ns in ("default", cfg.controller_namespace):
             await self.ensure_namespace(ns)
 
         # fake kube-controller-manager + scheduler
-        kube = self.kube = self._mgr("kube-controller-manager")
+        kube = self.kube = self._mgr("kube-controller-manager", remote=cfg.transport == "native")
         StatefulSetController(kube.client, kube.reader, kube.get_event_recorder_for("statefulset-controller")) \
             .setup_with_manager(kube)
         SchedulerController(kube.client, kube.reader, kube.get_event_recorder_for("default-scheduler")) \
@@ -168,7 +191,7 @@ class LocalCluster:
         from .webhook.notebook_webhook import NotebookWebhook, register_in_process
 
         if self.rest_config is not None:
-            from .webhook.certs import generate
+            from .webhook.certs import generate  # noqa: F811
             from .webhook.server import WebhookServer, mutating_webhook_configuration
 
             wh_mgr = self._mgr("odh-webhook", remote=True, uncached=(kinds.CONFIG_MAP, kinds.SECRET))
@@ -188,7 +211,13 @@ class LocalCluster:
 
     async def ensure_namespace(self, ns: str) -> None:
         if self.store.peek(kinds.NAMESPACE, ns) is None:
-            await self.admin.create({"apiVersion": "v1", "kind": "Namespace", "metadata": {"name": ns}})
+            from .models.errors import ApiError, is_already_exists
+
+            try:
+                await self.admin.create({"apiVersion": "v1", "kind": "Namespace", "metadata": {"name": ns}})
+            except ApiError as e:
+                if not is_already_exists(e):
+                    raise
 
     async def stop(self) -> None:
         for mgr in reversed(self.managers):
@@ -199,6 +228,10 @@ class LocalCluster:
             await self.webhook_server.stop()
         if self.apiserver is not None:
             await self.apiserver.stop()
+        if self.native is not None:
+            await self._view_cache.stop()
+            await self.admin.close()
+            await self.native.stop()
 
     async def settle(self, timeout: float = 10.0) -> bool:
         """Wait until every controller in every manager is idle (twice, to catch cascades)."""

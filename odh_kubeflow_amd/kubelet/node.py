@@ -95,25 +95,42 @@ class SchedulerController:
         self.scheduler_name = scheduler_name
         self.bound = 0
         self._lock = asyncio.Lock()
+        # "assumed" bindings (kube-scheduler's assume cache): a bind is visible to the
+        # next scheduling decision before the informer has observed it, so two pods can
+        # never be given the same GPU however far the cache lags behind the apiserver.
+        self._assumed: Dict[str, tuple] = {}  # pod uid -> (node, cpu, mem, gpu ids)
 
     def _used(self, node_name: str) -> Dict[str, object]:
         cpu = mem = 0.0
         gpus: Set[int] = set()
+        seen = set()
         for p in self.reader.list(kinds.POD, fields=f"spec.nodeName={node_name}"):
             if (p.get("status") or {}).get("phase") in ("Succeeded", "Failed"):
                 continue
+            seen.add(m.uid(p))
             r = _pod_requests(p)
             cpu += r["cpu"]
             mem += r["memory"]
             ids = m.annotations(p).get(GPU_IDS_ANNOTATION)
             if ids:
                 gpus.update(int(x) for x in ids.split(",") if x != "")
+        for uid, (node, acpu, amem, aids) in list(self._assumed.items()):
+            if node != node_name or uid in seen:
+                continue
+            cpu += acpu
+            mem += amem
+            gpus.update(aids)
         return {"cpu": cpu, "memory": mem, "gpus": gpus}
+
+    def forget(self, pod: dict) -> None:
+        self._assumed.pop(m.uid(pod), None)
 
     async def reconcile(self, req: Request) -> Result:
         pod = self.reader.get(kinds.POD, req.name, req.namespace)
         if pod is None or m.is_deleting(pod) or (pod.get("spec") or {}).get("nodeName"):
             return Result()
+        if m.uid(pod) in self._assumed:
+            return Result()  # bound already; the cache has not caught up yet
         async with self._lock:  # allocation decisions must not race each other
             return await self._schedule(pod)
 
@@ -152,6 +169,7 @@ class SchedulerController:
                     return Result()
                 raise
             self.bound += 1
+            self._assumed[m.uid(pod)] = (m.name(node), need["cpu"], need["memory"], tuple(ids))
             self.recorder.event(pod, "Normal", "Scheduled",
                                 f"Successfully assigned {m.namespace(pod)}/{m.name(pod)} to {m.name(node)}")
             return Result()
@@ -180,6 +198,7 @@ class SchedulerController:
                              delete=lambda o: False)
 
         def pods_released(obj):  # a deleted pod frees capacity: retry pending pods
+            self.forget(obj)
             return [Request(m.namespace(p), m.name(p)) for p in self.reader.list(kinds.POD)
                     if not (p.get("spec") or {}).get("nodeName")]
 

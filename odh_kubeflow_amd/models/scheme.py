@@ -131,6 +131,7 @@ def _builtin(s: Scheme) -> None:
         R("", "Event", "events", True, ("v1",), "v1", short_names=("ev",)),
         R("", "Namespace", "namespaces", False, ("v1",), "v1", True, short_names=("ns",)),
         R("", "Node", "nodes", False, ("v1",), "v1", True, short_names=("no",)),
+        R("", "Endpoints", "endpoints", True, ("v1",), "v1", short_names=("ep",)),
         R("", "PersistentVolumeClaim", "persistentvolumeclaims", True, ("v1",), "v1", True, short_names=("pvc",)),
         R("apps", "StatefulSet", "statefulsets", True, ("v1",), "v1", True, short_names=("sts",)),
         R("apps", "Deployment", "deployments", True, ("v1",), "v1", True, short_names=("deploy",)),

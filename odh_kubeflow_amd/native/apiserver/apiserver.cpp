@@ -1,0 +1,2011 @@
+// odh-apiserver: native (C++) Kubernetes API server for the notebook control plane.
+//
+// The envtest substitute of SURVEY §7.2 step 2, written natively so that the control
+// plane can scale out: the kf / odh managers, the admission webhook replicas and the
+// MI355X node agents (one process per GPU) all talk REST + watch to it concurrently.
+// Semantics follow odh_kubeflow_amd/apiserver/store.py (the in-process Python store)
+// and the behaviour the reference's envtest suites rely on
+// (kf/controllers/suite_test.go:50-104, odh/controllers/suite_test.go:91-275):
+//
+//   * resourceVersion (global counter), uid, creationTimestamp, generation,
+//     generateName, optimistic concurrency (409 Conflict on a stale resourceVersion);
+//   * status subresource isolation; finalizers + deletionTimestamp; no-op writes do
+//     not bump the resourceVersion;
+//   * merge, JSON and strategic-merge (list-by-merge-key subset) patches;
+//   * label / field selectors for list and watch; watch resumption from a
+//     resourceVersion with a bounded per-resource history (410 Expired when too old);
+//   * mutating admission webhooks from MutatingWebhookConfiguration objects over
+//     HTTPS (OpenSSL, caBundle verification, failurePolicy, Service → Endpoints
+//     resolution round-robin over replicas), admission runs outside the store lock;
+//   * ownerReference garbage collection (background + foreground) when --gc is set;
+//   * discovery documents; bearer-token authentication.
+//
+// Concurrency: one thread per client connection (keep-alive), one global store mutex
+// held only for map operations (microseconds), watch threads woken by a condition
+// variable; every stored object is an immutable shared snapshot, so readers and
+// watchers never copy under the lock and each watch event is serialised once.
+//
+// Usage: odh-apiserver --config scheme.json [--host 127.0.0.1] [--port 0] [--gc]
+//        [--token T] [--history 4096]; prints "LISTENING <port>" once ready.
+
+#include <arpa/inet.h>
+#include <netdb.h>
+#include <netinet/in.h>
+#include <netinet/tcp.h>
+#include <openssl/err.h>
+#include <openssl/ssl.h>
+#include <openssl/x509v3.h>
+#include <poll.h>
+#include <signal.h>
+#include <sys/socket.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <condition_variable>
+#include <cstdio>
+#include <ctime>
+#include <deque>
+#include <fstream>
+#include <functional>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <optional>
+#include <random>
+#include <set>
+#include <sstream>
+#include <thread>
+#include <tuple>
+#include <unordered_map>
+
+#include "json.hpp"
+
+using kj::T;
+using kj::Value;
+
+namespace {
+
+// ------------------------------------------------------------------ errors
+
+struct ApiErr {
+  int code;
+  std::string reason;
+  std::string message;
+  Value details;
+};
+
+Value status_obj(const ApiErr& e) {
+  Value s = Value::object();
+  s["kind"] = Value::str("Status");
+  s["apiVersion"] = Value::str("v1");
+  s["metadata"] = Value::object();
+  s["status"] = Value::str("Failure");
+  s["message"] = Value::str(e.message);
+  s["reason"] = Value::str(e.reason);
+  s["details"] = e.details.is_null() ? Value::object() : e.details;
+  s["code"] = Value::integer(e.code);
+  return s;
+}
+
+Value name_details(const std::string& name, const std::string& kind) {
+  Value d = Value::object();
+  d["name"] = Value::str(name);
+  d["kind"] = Value::str(kind);
+  return d;
+}
+ApiErr NotFound(const std::string& res, const std::string& name) {
+  return {404, "NotFound", res + " \"" + name + "\" not found", name_details(name, res)};
+}
+ApiErr AlreadyExists(const std::string& res, const std::string& name) {
+  return {409, "AlreadyExists", res + " \"" + name + "\" already exists", name_details(name, res)};
+}
+ApiErr Conflict(const std::string& res, const std::string& name, const std::string& msg = "") {
+  return {409, "Conflict",
+          "Operation cannot be fulfilled on " + res + " \"" + name + "\": " +
+              (msg.empty() ? "the object has been modified; please apply your changes to the latest version and try "
+                             "again"
+                           : msg),
+          name_details(name, res)};
+}
+ApiErr Invalid(const std::string& res, const std::string& name, const std::string& msg) {
+  return {422, "Invalid", res + " \"" + name + "\" is invalid: " + msg, name_details(name, res)};
+}
+ApiErr BadRequest(const std::string& msg) { return {400, "BadRequest", msg, Value()}; }
+ApiErr Forbidden(const std::string& msg) { return {403, "Forbidden", msg, Value()}; }
+ApiErr NoKindMatch(const std::string& kind) {
+  return {404, "NoKindMatch", "no matches for kind \"" + kind + "\" in version", Value()};
+}
+ApiErr Gone() { return {410, "Expired", "too old resource version", Value()}; }
+ApiErr Internal(const std::string& msg) { return {500, "InternalError", msg, Value()}; }
+
+// ------------------------------------------------------------------ scheme
+
+struct Res {
+  std::string group, kind, plural, singular, list_kind, storage, key;
+  std::vector<std::string> versions, short_names;
+  bool namespaced = true, status = false, installed = true;
+  std::string err_res() const { return group.empty() ? plural : plural + "." + group; }
+  std::string api_version(const std::string& v) const { return group.empty() ? v : group + "/" + v; }
+};
+
+std::vector<std::unique_ptr<Res>> g_res;
+Res* by_plural(const std::string& g, const std::string& p) {
+  for (auto& r : g_res)
+    if (r->group == g && r->plural == p) return r.get();
+  return nullptr;
+}
+Res* by_kind(const std::string& g, const std::string& k) {
+  for (auto& r : g_res)
+    if (r->group == g && r->kind == k) return r.get();
+  return nullptr;
+}
+Res* by_key(const std::string& key) {
+  for (auto& r : g_res)
+    if (r->key == key) return r.get();
+  return nullptr;
+}
+
+// ------------------------------------------------------------------ small utils
+
+std::string rfc3339_now() {
+  time_t t = time(nullptr);
+  struct tm tm;
+  gmtime_r(&t, &tm);
+  char buf[32];
+  strftime(buf, sizeof(buf), "%Y-%m-%dT%H:%M:%SZ", &tm);
+  return buf;
+}
+
+thread_local std::mt19937_64 t_rng{std::random_device{}() ^ (uint64_t)std::hash<std::thread::id>()(std::this_thread::get_id())};
+
+std::string uuid4() {
+  uint64_t a = t_rng(), b = t_rng();
+  a = (a & 0xFFFFFFFFFFFF0FFFULL) | 0x0000000000004000ULL;
+  b = (b & 0x3FFFFFFFFFFFFFFFULL) | 0x8000000000000000ULL;
+  char buf[40];
+  snprintf(buf, sizeof(buf), "%08x-%04x-%04x-%04x-%012llx", (unsigned)(a >> 32), (unsigned)((a >> 16) & 0xFFFF),
+           (unsigned)(a & 0xFFFF), (unsigned)(b >> 48), (unsigned long long)(b & 0xFFFFFFFFFFFFULL));
+  return buf;
+}
+
+std::string rand_suffix(int n = 5) {
+  static const char* al = "bcdfghjklmnpqrstvwxz2456789";
+  std::string s;
+  for (int k = 0; k < n; ++k) s += al[t_rng() % 27];
+  return s;
+}
+
+const Value* md(const Value& o) { return o.get("metadata"); }
+std::string mget(const Value& o, const char* k) {
+  const Value* m = md(o);
+  return m ? m->str_or(k) : "";
+}
+Value& mdm(Value& o) {
+  Value& m = o["metadata"];
+  if (!m.is_obj()) m = Value::object();
+  return m;
+}
+
+std::string url_decode(const std::string& s) {
+  std::string o;
+  for (size_t n = 0; n < s.size(); ++n) {
+    if (s[n] == '%' && n + 2 < s.size()) {
+      o += (char)std::stoi(s.substr(n + 1, 2), nullptr, 16);
+      n += 2;
+    } else if (s[n] == '+') {
+      o += ' ';
+    } else {
+      o += s[n];
+    }
+  }
+  return o;
+}
+
+std::vector<std::string> split(const std::string& s, char d) {
+  std::vector<std::string> out;
+  std::string cur;
+  for (char c : s) {
+    if (c == d) {
+      out.push_back(cur);
+      cur.clear();
+    } else {
+      cur += c;
+    }
+  }
+  out.push_back(cur);
+  return out;
+}
+
+std::string trim(const std::string& s) {
+  size_t a = s.find_first_not_of(" \t"), b = s.find_last_not_of(" \t");
+  return a == std::string::npos ? "" : s.substr(a, b - a + 1);
+}
+
+// ------------------------------------------------------------------ selectors
+
+struct LReq {
+  std::string key, op;
+  std::vector<std::string> vals;
+};
+
+std::vector<LReq> parse_labels(const std::string& text) {
+  std::vector<LReq> out;
+  std::vector<std::string> parts;
+  std::string cur;
+  int depth = 0;
+  for (char c : text) {
+    if (c == '(') depth++;
+    if (c == ')') depth--;
+    if (c == ',' && depth == 0) {
+      parts.push_back(cur);
+      cur.clear();
+    } else {
+      cur += c;
+    }
+  }
+  parts.push_back(cur);
+  for (auto p : parts) {
+    p = trim(p);
+    if (p.empty()) continue;
+    size_t sp = p.find(' ');
+    if (sp != std::string::npos && p.find('(') != std::string::npos) {
+      std::string k = trim(p.substr(0, sp));
+      std::string rest = trim(p.substr(sp));
+      std::string op = rest.rfind("notin", 0) == 0 ? "notin" : "in";
+      size_t a = rest.find('('), b = rest.rfind(')');
+      LReq r{k, op, {}};
+      for (auto& v : split(rest.substr(a + 1, b - a - 1), ','))
+        if (!trim(v).empty()) r.vals.push_back(trim(v));
+      out.push_back(r);
+      continue;
+    }
+    if (p[0] == '!') {
+      out.push_back({trim(p.substr(1)), "!", {}});
+      continue;
+    }
+    size_t e;
+    if ((e = p.find("==")) != std::string::npos) out.push_back({trim(p.substr(0, e)), "=", {trim(p.substr(e + 2))}});
+    else if ((e = p.find("!=")) != std::string::npos)
+      out.push_back({trim(p.substr(0, e)), "!=", {trim(p.substr(e + 2))}});
+    else if ((e = p.find('=')) != std::string::npos)
+      out.push_back({trim(p.substr(0, e)), "=", {trim(p.substr(e + 1))}});
+    else out.push_back({p, "exists", {}});
+  }
+  return out;
+}
+
+bool match_labels(const std::vector<LReq>& reqs, const Value& obj) {
+  const Value* m = md(obj);
+  const Value* labels = m ? m->get("labels") : nullptr;
+  for (auto& r : reqs) {
+    const Value* v = labels ? labels->get(r.key) : nullptr;
+    bool has = v && v->is_str();
+    std::string s = has ? v->s : "";
+    if (r.op == "=") {
+      if (!has || s != r.vals[0]) return false;
+    } else if (r.op == "!=") {
+      if (has && s == r.vals[0]) return false;
+    } else if (r.op == "in") {
+      if (!has || std::find(r.vals.begin(), r.vals.end(), s) == r.vals.end()) return false;
+    } else if (r.op == "notin") {
+      if (has && std::find(r.vals.begin(), r.vals.end(), s) != r.vals.end()) return false;
+    } else if (r.op == "exists") {
+      if (!has) return false;
+    } else if (r.op == "!") {
+      if (has) return false;
+    }
+  }
+  return true;
+}
+
+struct FReq {
+  std::vector<std::string> path;
+  bool eq;
+  std::string val;
+};
+
+std::vector<FReq> parse_fields(const std::string& text) {
+  std::vector<FReq> out;
+  for (auto p : split(text, ',')) {
+    p = trim(p);
+    if (p.empty()) continue;
+    size_t e;
+    if ((e = p.find("!=")) != std::string::npos) out.push_back({split(trim(p.substr(0, e)), '.'), false, trim(p.substr(e + 2))});
+    else if ((e = p.find("==")) != std::string::npos)
+      out.push_back({split(trim(p.substr(0, e)), '.'), true, trim(p.substr(e + 2))});
+    else if ((e = p.find('=')) != std::string::npos)
+      out.push_back({split(trim(p.substr(0, e)), '.'), true, trim(p.substr(e + 1))});
+  }
+  return out;
+}
+
+std::string scalar_str(const Value* v) {
+  if (!v || v->is_null()) return "";
+  if (v->t == T::String) return v->s;
+  if (v->t == T::Bool) return v->b ? "True" : "False";
+  return kj::dump(*v);
+}
+
+bool match_fields(const std::vector<FReq>& reqs, const Value& obj) {
+  for (auto& r : reqs) {
+    const Value* cur = &obj;
+    for (auto& k : r.path) {
+      cur = cur && cur->is_obj() ? cur->get(k) : nullptr;
+    }
+    if ((scalar_str(cur) == r.val) != r.eq) return false;
+  }
+  return true;
+}
+
+// ------------------------------------------------------------------ patches
+
+struct PatchErr {
+  std::string msg;
+};
+
+std::string unescape_tok(std::string t) {
+  size_t p;
+  while ((p = t.find("~1")) != std::string::npos) t.replace(p, 2, "/");
+  while ((p = t.find("~0")) != std::string::npos) t.replace(p, 2, "~");
+  return t;
+}
+
+std::vector<std::string> ptr_tokens(const std::string& path) {
+  if (path.empty()) return {};
+  if (path[0] != '/') throw PatchErr{"invalid JSON pointer " + path};
+  std::vector<std::string> out;
+  for (auto& t : split(path.substr(1), '/')) out.push_back(unescape_tok(t));
+  return out;
+}
+
+Value* ptr_get(Value& doc, const std::vector<std::string>& toks, size_t upto) {
+  Value* cur = &doc;
+  for (size_t n = 0; n < upto; ++n) {
+    const std::string& t = toks[n];
+    if (cur->is_obj()) {
+      cur = cur->get(t);
+      if (!cur) throw PatchErr{"path segment '" + t + "' not found"};
+    } else if (cur->is_arr()) {
+      size_t idx;
+      try {
+        idx = std::stoul(t);
+      } catch (...) {
+        throw PatchErr{"bad list index " + t};
+      }
+      if (idx >= cur->arr.size()) throw PatchErr{"bad list index " + t};
+      cur = &cur->arr[idx];
+    } else {
+      throw PatchErr{"cannot traverse into scalar"};
+    }
+  }
+  return cur;
+}
+
+void ptr_add(Value& doc, const std::vector<std::string>& toks, Value v) {
+  if (toks.empty()) {
+    doc = std::move(v);
+    return;
+  }
+  Value* parent = ptr_get(doc, toks, toks.size() - 1);
+  const std::string& last = toks.back();
+  if (parent->is_obj()) {
+    (*parent)[last] = std::move(v);
+  } else if (parent->is_arr()) {
+    if (last == "-") {
+      parent->arr.push_back(std::move(v));
+    } else {
+      size_t idx = std::stoul(last);
+      if (idx > parent->arr.size()) throw PatchErr{"list index out of range"};
+      parent->arr.insert(parent->arr.begin() + idx, std::move(v));
+    }
+  } else {
+    throw PatchErr{"cannot add into scalar"};
+  }
+}
+
+Value ptr_remove(Value& doc, const std::vector<std::string>& toks) {
+  if (toks.empty()) throw PatchErr{"cannot remove document root"};
+  Value* parent = ptr_get(doc, toks, toks.size() - 1);
+  const std::string& last = toks.back();
+  if (parent->is_obj()) {
+    Value* v = parent->get(last);
+    if (!v) throw PatchErr{"remove: '" + last + "' not found"};
+    Value out = std::move(*v);
+    parent->erase(last);
+    return out;
+  }
+  if (parent->is_arr()) {
+    size_t idx = std::stoul(last);
+    if (idx >= parent->arr.size()) throw PatchErr{"remove: bad index"};
+    Value out = std::move(parent->arr[idx]);
+    parent->arr.erase(parent->arr.begin() + idx);
+    return out;
+  }
+  throw PatchErr{"cannot remove from scalar"};
+}
+
+Value apply_json_patch(Value doc, const Value& ops) {
+  if (!ops.is_arr()) throw PatchErr{"JSON patch must be an array"};
+  for (auto& op : ops.arr) {
+    std::string kind = op.str_or("op");
+    auto toks = ptr_tokens(op.str_or("path"));
+    const Value* val = op.get("value");
+    if (kind == "add") {
+      ptr_add(doc, toks, val ? *val : Value());
+    } else if (kind == "remove") {
+      ptr_remove(doc, toks);
+    } else if (kind == "replace") {
+      if (toks.empty()) {
+        doc = val ? *val : Value();
+        continue;
+      }
+      Value* tgt = ptr_get(doc, toks, toks.size());
+      *tgt = val ? *val : Value();
+    } else if (kind == "move") {
+      Value v = ptr_remove(doc, ptr_tokens(op.str_or("from")));
+      ptr_add(doc, toks, std::move(v));
+    } else if (kind == "copy") {
+      auto ft = ptr_tokens(op.str_or("from"));
+      Value v = *ptr_get(doc, ft, ft.size());
+      ptr_add(doc, toks, std::move(v));
+    } else if (kind == "test") {
+      if (!(*ptr_get(doc, toks, toks.size()) == (val ? *val : Value())))
+        throw PatchErr{"test failed at " + op.str_or("path")};
+    } else {
+      throw PatchErr{"unknown op " + kind};
+    }
+  }
+  return doc;
+}
+
+Value merge_patch(const Value& target, const Value& patch) {
+  if (!patch.is_obj()) return patch;
+  Value out = target.is_obj() ? target : Value::object();
+  for (auto& m : patch.obj) {
+    if (m.v.is_null()) out.erase(m.k);
+    else if (m.v.is_obj()) {
+      const Value* cur = out.get(m.k);
+      out[m.k] = merge_patch(cur ? *cur : Value(), m.v);
+    } else {
+      out[m.k] = m.v;
+    }
+  }
+  return out;
+}
+
+const char* smp_key(const std::string& field, bool* known) {
+  static const std::pair<const char*, const char*> keys[] = {
+      {"containers", "name"}, {"initContainers", "name"}, {"ephemeralContainers", "name"}, {"env", "name"},
+      {"volumes", "name"},    {"volumeMounts", "mountPath"}, {"ports", "containerPort"}, {"imagePullSecrets", "name"},
+      {"tolerations", nullptr}, {"finalizers", nullptr}, {"ownerReferences", "uid"}, {"conditions", "type"}};
+  for (auto& kv : keys)
+    if (field == kv.first) {
+      *known = true;
+      return kv.second;
+    }
+  *known = false;
+  return nullptr;
+}
+
+Value strategic_patch(const Value& target, const Value& patch) {
+  if (!patch.is_obj()) return patch;
+  Value out = target.is_obj() ? target : Value::object();
+  for (auto& m : patch.obj) {
+    if (!m.k.empty() && m.k[0] == '$') continue;
+    bool known;
+    const char* key = smp_key(m.k, &known);
+    const Value* cur = out.get(m.k);
+    if (m.v.is_null()) {
+      out.erase(m.k);
+    } else if (m.v.is_obj()) {
+      out[m.k] = strategic_patch(cur ? *cur : Value(), m.v);
+    } else if (m.v.is_arr() && key && cur && cur->is_arr()) {
+      Value merged = *cur;
+      for (auto& item : m.v.arr) {
+        const Value* kv = item.is_obj() ? item.get(key) : nullptr;
+        if (!kv) {
+          merged.arr.push_back(item);
+          continue;
+        }
+        int idx = -1;
+        for (size_t n = 0; n < merged.arr.size(); ++n) {
+          const Value* ek = merged.arr[n].is_obj() ? merged.arr[n].get(key) : nullptr;
+          if (ek && *ek == *kv) {
+            idx = (int)n;
+            break;
+          }
+        }
+        if (item.str_or("$patch") == "delete") {
+          if (idx >= 0) merged.arr.erase(merged.arr.begin() + idx);
+          continue;
+        }
+        if (idx < 0) merged.arr.push_back(item);
+        else merged.arr[idx] = strategic_patch(merged.arr[idx], item);
+      }
+      out[m.k] = std::move(merged);
+    } else {
+      out[m.k] = m.v;
+    }
+  }
+  return out;
+}
+
+// ------------------------------------------------------------------ store
+
+using Obj = std::shared_ptr<const Value>;
+
+struct EvCache {
+  std::mutex mu;
+  std::string version;
+  std::shared_ptr<std::string> line;
+};
+
+struct Ev {
+  int64_t seq;
+  int64_t rv;
+  const char* type;
+  Obj obj;
+  Obj old;
+  std::shared_ptr<EvCache> cache;
+};
+
+struct Bucket {
+  std::map<std::pair<std::string, std::string>, Obj> objs;
+  std::deque<Ev> hist;
+  int64_t seq = 0;
+};
+
+struct Store {
+  std::mutex mu;
+  std::condition_variable cv;
+  std::unordered_map<std::string, Bucket> data;
+  int64_t rv = 0;
+  size_t history = 4096;
+  bool gc = false;
+  std::unordered_map<std::string, std::set<std::tuple<std::string, std::string, std::string>>> owners;
+  std::unordered_map<std::string, std::tuple<std::string, std::string, std::string>> uids;
+  std::atomic<uint64_t> requests{0}, writes{0}, webhook_calls{0};
+} S;
+
+Bucket& bucket(const Res& r) { return S.data[r.key]; }
+
+void index_owner(const Res& r, const Value& o, bool remove) {
+  const Value* m = md(o);
+  const Value* refs = m ? m->get("ownerReferences") : nullptr;
+  if (!refs || !refs->is_arr()) return;
+  auto k = std::make_tuple(r.key, mget(o, "namespace"), mget(o, "name"));
+  for (auto& ref : refs->arr) {
+    std::string u = ref.str_or("uid");
+    if (u.empty()) continue;
+    if (remove) {
+      auto it = S.owners.find(u);
+      if (it != S.owners.end()) {
+        it->second.erase(k);
+        if (it->second.empty()) S.owners.erase(it);
+      }
+    } else {
+      S.owners[u].insert(k);
+    }
+  }
+}
+
+// callers hold S.mu
+void emit(const Res& r, const char* type, Obj obj, Obj old) {
+  Bucket& b = bucket(r);
+  Ev e{++b.seq, std::stoll(mget(*obj, "resourceVersion")), type, std::move(obj), std::move(old),
+       std::make_shared<EvCache>()};
+  b.hist.push_back(std::move(e));
+  while (b.hist.size() > S.history) b.hist.pop_front();
+  S.cv.notify_all();
+}
+
+Value out_obj(const Res& r, const Value& o, const std::string& version) {
+  Value c = o;
+  if (!version.empty() && version != r.storage) c["apiVersion"] = Value::str(r.api_version(version));
+  return c;
+}
+
+bool spec_equal(const Value& a, const Value& b) {
+  // everything but metadata / status / apiVersion / kind
+  auto part = [](const Value& v) {
+    Value o = Value::object();
+    for (auto& m : v.obj)
+      if (m.k != "metadata" && m.k != "status" && m.k != "apiVersion" && m.k != "kind") o.obj.push_back(m);
+    return o;
+  };
+  return part(a) == part(b);
+}
+
+bool equal_except_meta(const Value& a, const Value& b) {
+  if (a.obj.size() != b.obj.size()) return false;
+  for (auto& m : a.obj) {
+    const Value* o = b.get(m.k);
+    if (!o) return false;
+    if (m.k == "metadata" && m.v.is_obj() && o->is_obj()) {
+      auto strip = [](const Value& v) {
+        Value c = v;
+        c.erase("resourceVersion");
+        c.erase("managedFields");
+        c.erase("generation");
+        return c;
+      };
+      if (!(strip(m.v) == strip(*o))) return false;
+    } else if (!(m.v == *o)) {
+      return false;
+    }
+  }
+  return true;
+}
+
+std::optional<std::string> validate(const Res& r, const Value& o) {
+  if (r.key != "notebooks.kubeflow.org") return std::nullopt;
+  const Value* cs = o.path({"spec", "template", "spec", "containers"});
+  if (!cs || !cs->is_arr() || cs->arr.empty())
+    return std::string("spec.template.spec.containers: Invalid value: should have at least 1 items");
+  for (size_t n = 0; n < cs->arr.size(); ++n) {
+    for (const char* f : {"name", "image"}) {
+      const Value* v = cs->arr[n].is_obj() ? cs->arr[n].get(f) : nullptr;
+      if (!v || !v->is_str() || v->s.empty())
+        return "spec.template.spec.containers[" + std::to_string(n) + "]." + f + ": Required value";
+    }
+  }
+  return std::nullopt;
+}
+
+void defaults(const Res& r, Value& o) {
+  if (r.key == "services") {
+    Value& spec = o["spec"];
+    if (!spec.is_obj()) spec = Value::object();
+    if (!spec.get("type")) spec["type"] = Value::str("ClusterIP");
+    if (spec.str_or("type") == "ClusterIP" && spec.str_or("clusterIP").empty()) {
+      char ip[32];
+      snprintf(ip, sizeof(ip), "10.96.%d.%d", (int)((S.rv >> 8) & 255), (int)((S.rv & 255) ? (S.rv & 255) : 1));
+      spec["clusterIP"] = Value::str(ip);
+      Value ips = Value::array();
+      ips.arr.push_back(Value::str(ip));
+      spec["clusterIPs"] = ips;
+    }
+  } else if (r.key == "namespaces") {
+    Value& m = mdm(o);
+    Value& labels = m["labels"];
+    if (!labels.is_obj()) labels = Value::object();
+    labels["kubernetes.io/metadata.name"] = Value::str(m.str_or("name"));
+    if (!o.get("status")) {
+      Value st = Value::object();
+      st["phase"] = Value::str("Active");
+      o["status"] = st;
+    }
+  }
+}
+
+// ------------------------------------------------------------------ admission (MutatingWebhookConfiguration)
+
+struct Webhook {
+  std::string name, url_host, url_path, ca_pem, svc_ns, svc_name, svc_path;
+  int url_port = 443, svc_port = 443;
+  bool fail_closed = true, has_url = false;
+  double timeout_s = 10;
+  Value rules;
+};
+
+bool rule_match(const Value& rules, const Res& r, const std::string& op) {
+  if (!rules.is_arr()) return false;
+  auto has = [](const Value* list, const std::string& x) {
+    if (!list || !list->is_arr()) return false;
+    for (auto& v : list->arr)
+      if (v.is_str() && (v.s == "*" || v.s == x)) return true;
+    return false;
+  };
+  for (auto& rule : rules.arr) {
+    if (!has(rule.get("operations"), op)) continue;
+    if (!has(rule.get("apiGroups"), r.group)) continue;
+    if (!has(rule.get("resources"), r.plural)) continue;
+    return true;
+  }
+  return false;
+}
+
+std::string b64decode(const std::string& in) {
+  static int T_[256];
+  static bool init = false;
+  if (!init) {
+    for (int& x : T_) x = -1;
+    const char* a = "ABCDEFGHIJKLMNOPQRSTUVWXYZabcdefghijklmnopqrstuvwxyz0123456789+/";
+    for (int k = 0; k < 64; ++k) T_[(unsigned char)a[k]] = k;
+    init = true;
+  }
+  std::string out;
+  int val = 0, bits = -8;
+  for (unsigned char c : in) {
+    if (T_[c] == -1) continue;
+    val = (val << 6) + T_[c];
+    bits += 6;
+    if (bits >= 0) {
+      out += (char)((val >> bits) & 0xFF);
+      bits -= 8;
+    }
+  }
+  return out;
+}
+
+std::vector<Webhook> webhooks_for(const Res& r, const std::string& op) {
+  std::vector<Webhook> out;
+  Res* mwc = by_kind("admissionregistration.k8s.io", "MutatingWebhookConfiguration");
+  if (!mwc) return out;
+  std::vector<Obj> cfgs;
+  {
+    std::lock_guard<std::mutex> g(S.mu);
+    for (auto& kv : bucket(*mwc).objs) cfgs.push_back(kv.second);
+  }
+  for (auto& c : cfgs) {
+    const Value* whs = c->get("webhooks");
+    if (!whs || !whs->is_arr()) continue;
+    for (auto& wh : whs->arr) {
+      const Value* rules = wh.get("rules");
+      if (!rules || !rule_match(*rules, r, op)) continue;
+      Webhook w;
+      w.name = wh.str_or("name");
+      w.fail_closed = wh.str_or("failurePolicy", "Fail") == "Fail";
+      const Value* ts = wh.get("timeoutSeconds");
+      if (ts && ts->t == T::Int) w.timeout_s = (double)ts->i;
+      const Value* cc = wh.get("clientConfig");
+      if (cc) {
+        std::string ca = cc->str_or("caBundle");
+        if (!ca.empty()) w.ca_pem = b64decode(ca);
+        std::string url = cc->str_or("url");
+        if (!url.empty()) {
+          w.has_url = true;
+          std::string rest = url.substr(url.find("://") + 3);
+          size_t slash = rest.find('/');
+          std::string hostport = rest.substr(0, slash);
+          w.url_path = slash == std::string::npos ? "/" : rest.substr(slash);
+          size_t colon = hostport.rfind(':');
+          w.url_host = colon == std::string::npos ? hostport : hostport.substr(0, colon);
+          w.url_port = colon == std::string::npos ? 443 : std::stoi(hostport.substr(colon + 1));
+        } else if (const Value* svc = cc->get("service")) {
+          w.svc_ns = svc->str_or("namespace");
+          w.svc_name = svc->str_or("name");
+          w.svc_path = svc->str_or("path", "/");
+          const Value* p = svc->get("port");
+          if (p && p->t == T::Int) w.svc_port = (int)p->i;
+        }
+      }
+      out.push_back(std::move(w));
+    }
+  }
+  return out;
+}
+
+std::atomic<uint64_t> g_rr{0};
+
+// Service → Endpoints (round robin over ready addresses) like a ClusterIP Service would.
+bool resolve_service(const Webhook& w, std::string* host, int* port) {
+  Res* ep = by_kind("", "Endpoints");
+  if (!ep) return false;
+  Obj o;
+  {
+    std::lock_guard<std::mutex> g(S.mu);
+    auto it = bucket(*ep).objs.find({w.svc_ns, w.svc_name});
+    if (it == bucket(*ep).objs.end()) return false;
+    o = it->second;
+  }
+  std::vector<std::pair<std::string, int>> targets;
+  const Value* subsets = o->get("subsets");
+  if (!subsets || !subsets->is_arr()) return false;
+  for (auto& ss : subsets->arr) {
+    const Value* addrs = ss.get("addresses");
+    const Value* ports = ss.get("ports");
+    if (!addrs || !addrs->is_arr() || !ports || !ports->is_arr() || ports->arr.empty()) continue;
+    int p = 0;
+    for (auto& pp : ports->arr) {
+      const Value* pv = pp.get("port");
+      if (pv && pv->t == T::Int) {
+        p = (int)pv->i;
+        break;
+      }
+    }
+    for (auto& a : addrs->arr) targets.push_back({a.str_or("ip"), p});
+  }
+  if (targets.empty()) return false;
+  auto& t = targets[g_rr++ % targets.size()];
+  *host = t.first;
+  *port = t.second;
+  return true;
+}
+
+struct TlsConn {
+  int fd = -1;
+  SSL* ssl = nullptr;
+  ~TlsConn() {
+    if (ssl) {
+      SSL_shutdown(ssl);
+      SSL_free(ssl);
+    }
+    if (fd >= 0) close(fd);
+  }
+};
+
+std::mutex g_ctx_mu;
+std::map<std::string, SSL_CTX*> g_ctx;  // caBundle → context
+
+SSL_CTX* ctx_for(const std::string& ca_pem) {
+  std::lock_guard<std::mutex> g(g_ctx_mu);
+  auto it = g_ctx.find(ca_pem);
+  if (it != g_ctx.end()) return it->second;
+  SSL_CTX* ctx = SSL_CTX_new(TLS_client_method());
+  SSL_CTX_set_min_proto_version(ctx, TLS1_2_VERSION);
+  if (!ca_pem.empty()) {
+    BIO* bio = BIO_new_mem_buf(ca_pem.data(), (int)ca_pem.size());
+    X509_STORE* st = SSL_CTX_get_cert_store(ctx);
+    while (X509* x = PEM_read_bio_X509(bio, nullptr, nullptr, nullptr)) {
+      X509_STORE_add_cert(st, x);
+      X509_free(x);
+    }
+    ERR_clear_error();
+    BIO_free(bio);
+    SSL_CTX_set_verify(ctx, SSL_VERIFY_PEER, nullptr);
+  } else {
+    SSL_CTX_set_default_verify_paths(ctx);
+    SSL_CTX_set_verify(ctx, SSL_VERIFY_PEER, nullptr);
+  }
+  g_ctx[ca_pem] = ctx;
+  return ctx;
+}
+
+// connection pool: host:port|ca -> idle connections
+std::mutex g_pool_mu;
+std::map<std::string, std::vector<std::unique_ptr<TlsConn>>> g_pool;
+
+std::unique_ptr<TlsConn> tls_connect(const std::string& host, int port, const std::string& ca, double timeout_s) {
+  auto c = std::make_unique<TlsConn>();
+  struct addrinfo hints {};
+  hints.ai_family = AF_UNSPEC;
+  hints.ai_socktype = SOCK_STREAM;
+  struct addrinfo* res = nullptr;
+  if (getaddrinfo(host.c_str(), std::to_string(port).c_str(), &hints, &res) != 0 || !res)
+    throw std::runtime_error("cannot resolve " + host);
+  c->fd = socket(res->ai_family, SOCK_STREAM, 0);
+  struct timeval tv;
+  tv.tv_sec = (long)timeout_s;
+  tv.tv_usec = (long)((timeout_s - (long)timeout_s) * 1e6);
+  setsockopt(c->fd, SOL_SOCKET, SO_RCVTIMEO, &tv, sizeof(tv));
+  setsockopt(c->fd, SOL_SOCKET, SO_SNDTIMEO, &tv, sizeof(tv));
+  int one = 1;
+  setsockopt(c->fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof(one));
+  int rc = connect(c->fd, res->ai_addr, res->ai_addrlen);
+  freeaddrinfo(res);
+  if (rc != 0) throw std::runtime_error("connect failed to " + host + ":" + std::to_string(port));
+  c->ssl = SSL_new(ctx_for(ca));
+  SSL_set_fd(c->ssl, c->fd);
+  X509_VERIFY_PARAM* param = SSL_get0_param(c->ssl);
+  struct in_addr a4;
+  if (inet_pton(AF_INET, host.c_str(), &a4) == 1) {
+    X509_VERIFY_PARAM_set1_ip_asc(param, host.c_str());
+  } else {
+    SSL_set_tlsext_host_name(c->ssl, host.c_str());
+    X509_VERIFY_PARAM_set1_host(param, host.c_str(), 0);
+  }
+  if (SSL_connect(c->ssl) != 1) {
+    unsigned long e = ERR_get_error();
+    char buf[256];
+    ERR_error_string_n(e, buf, sizeof(buf));
+    throw std::runtime_error(std::string("TLS handshake failed: ") + buf);
+  }
+  return c;
+}
+
+bool tls_write_all(TlsConn& c, const std::string& s) {
+  size_t off = 0;
+  while (off < s.size()) {
+    int n = SSL_write(c.ssl, s.data() + off, (int)(s.size() - off));
+    if (n <= 0) return false;
+    off += n;
+  }
+  return true;
+}
+
+// minimal HTTP/1.1 response reader (Content-Length or chunked)
+bool tls_read_response(TlsConn& c, int* status, std::string* body) {
+  std::string buf;
+  char tmp[16384];
+  size_t hdr_end;
+  while ((hdr_end = buf.find("\r\n\r\n")) == std::string::npos) {
+    int n = SSL_read(c.ssl, tmp, sizeof(tmp));
+    if (n <= 0) return false;
+    buf.append(tmp, n);
+  }
+  std::string head = buf.substr(0, hdr_end);
+  std::string rest = buf.substr(hdr_end + 4);
+  *status = std::atoi(head.c_str() + head.find(' ') + 1);
+  std::string lower = head;
+  std::transform(lower.begin(), lower.end(), lower.begin(), ::tolower);
+  size_t cl = lower.find("content-length:");
+  if (cl != std::string::npos) {
+    size_t len = std::stoul(lower.substr(cl + 15));
+    while (rest.size() < len) {
+      int n = SSL_read(c.ssl, tmp, sizeof(tmp));
+      if (n <= 0) return false;
+      rest.append(tmp, n);
+    }
+    *body = rest.substr(0, len);
+    return true;
+  }
+  if (lower.find("transfer-encoding: chunked") != std::string::npos) {
+    std::string out;
+    while (true) {
+      size_t le;
+      while ((le = rest.find("\r\n")) == std::string::npos) {
+        int n = SSL_read(c.ssl, tmp, sizeof(tmp));
+        if (n <= 0) return false;
+        rest.append(tmp, n);
+      }
+      size_t sz = std::stoul(rest.substr(0, le), nullptr, 16);
+      rest.erase(0, le + 2);
+      while (rest.size() < sz + 2) {
+        int n = SSL_read(c.ssl, tmp, sizeof(tmp));
+        if (n <= 0) return false;
+        rest.append(tmp, n);
+      }
+      if (sz == 0) break;
+      out.append(rest, 0, sz);
+      rest.erase(0, sz + 2);
+    }
+    *body = out;
+    return true;
+  }
+  return false;
+}
+
+Value call_webhook(const Webhook& w, const Value& review) {
+  std::string host = w.url_host, path = w.url_path;
+  int port = w.url_port;
+  if (!w.has_url) {
+    if (!resolve_service(w, &host, &port)) throw std::runtime_error("no endpoints for service " + w.svc_ns + "/" + w.svc_name);
+    path = w.svc_path;
+  }
+  std::string body = kj::dump(review);
+  std::string req = "POST " + path + " HTTP/1.1\r\nHost: " + host + ":" + std::to_string(port) +
+                    "\r\nContent-Type: application/json\r\nAccept: application/json\r\nContent-Length: " +
+                    std::to_string(body.size()) + "\r\n\r\n" + body;
+  std::string pool_key = host + ":" + std::to_string(port) + "|" + w.ca_pem;
+  for (int attempt = 0; attempt < 2; ++attempt) {
+    std::unique_ptr<TlsConn> c;
+    if (attempt == 0) {
+      std::lock_guard<std::mutex> g(g_pool_mu);
+      auto& v = g_pool[pool_key];
+      if (!v.empty()) {
+        c = std::move(v.back());
+        v.pop_back();
+      }
+    }
+    bool reused = (bool)c;
+    if (!c) c = tls_connect(host, port, w.ca_pem, w.timeout_s);
+    int status = 0;
+    std::string resp;
+    if (tls_write_all(*c, req) && tls_read_response(*c, &status, &resp)) {
+      {
+        std::lock_guard<std::mutex> g(g_pool_mu);
+        g_pool[pool_key].push_back(std::move(c));
+      }
+      if (status != 200) throw std::runtime_error("webhook returned HTTP " + std::to_string(status));
+      return kj::parse(resp);
+    }
+    if (!reused) throw std::runtime_error("webhook request failed");
+  }
+  throw std::runtime_error("webhook request failed");
+}
+
+Value admit(const char* op, const Res& r, Value obj, const Value* old) {
+  auto hooks = webhooks_for(r, op);
+  for (auto& w : hooks) {
+    Value review = Value::object();
+    review["apiVersion"] = Value::str("admission.k8s.io/v1");
+    review["kind"] = Value::str("AdmissionReview");
+    Value req = Value::object();
+    req["uid"] = Value::str(uuid4());
+    req["operation"] = Value::str(op);
+    req["name"] = Value::str(mget(obj, "name"));
+    req["namespace"] = Value::str(mget(obj, "namespace"));
+    Value kind = Value::object();
+    kind["group"] = Value::str(r.group);
+    kind["version"] = Value::str(r.storage);
+    kind["kind"] = Value::str(r.kind);
+    req["kind"] = kind;
+    Value res = Value::object();
+    res["group"] = Value::str(r.group);
+    res["version"] = Value::str(r.storage);
+    res["resource"] = Value::str(r.plural);
+    req["resource"] = res;
+    req["object"] = obj;
+    req["oldObject"] = old ? *old : Value();
+    review["request"] = std::move(req);
+    S.webhook_calls++;
+    Value out;
+    try {
+      out = call_webhook(w, review);
+    } catch (const std::exception& e) {
+      if (w.fail_closed) throw Internal("failed calling webhook \"" + w.name + "\": " + e.what());
+      continue;
+    }
+    const Value* resp = out.get("response");
+    if (!resp) {
+      if (w.fail_closed) throw Internal("webhook \"" + w.name + "\" returned no response");
+      continue;
+    }
+    const Value* allowed = resp->get("allowed");
+    if (!allowed || allowed->t != T::Bool || !allowed->b) {
+      const Value* st = resp->get("status");
+      throw Internal("admission webhook \"" + w.name + "\" denied the request: " + (st ? st->str_or("message") : ""));
+    }
+    std::string p = resp->str_or("patch");
+    if (!p.empty()) {
+      try {
+        obj = apply_json_patch(std::move(obj), kj::parse(b64decode(p)));
+      } catch (const PatchErr& e) {
+        throw Internal("webhook \"" + w.name + "\" returned an invalid patch: " + e.msg);
+      }
+    }
+  }
+  return obj;
+}
+
+// ------------------------------------------------------------------ store operations
+
+Res& res_checked(Res* r) {
+  if (!r->installed) throw NoKindMatch(r->kind);
+  return *r;
+}
+
+std::pair<std::vector<Obj>, int64_t> do_list(const Res& r, const std::string& ns, const std::string& lsel,
+                                             const std::string& fsel) {
+  auto lr = parse_labels(lsel);
+  auto fr = parse_fields(fsel);
+  std::vector<Obj> out;
+  std::lock_guard<std::mutex> g(S.mu);
+  Bucket& b = bucket(r);
+  if (!ns.empty() && r.namespaced) {
+    for (auto it = b.objs.lower_bound({ns, ""}); it != b.objs.end() && it->first.first == ns; ++it)
+      if ((lr.empty() || match_labels(lr, *it->second)) && (fr.empty() || match_fields(fr, *it->second)))
+        out.push_back(it->second);
+  } else {
+    for (auto& kv : b.objs)
+      if ((lr.empty() || match_labels(lr, *kv.second)) && (fr.empty() || match_fields(fr, *kv.second)))
+        out.push_back(kv.second);
+  }
+  return {out, S.rv};
+}
+
+Obj do_get(const Res& r, const std::string& ns, const std::string& name) {
+  std::lock_guard<std::mutex> g(S.mu);
+  Bucket& b = bucket(r);
+  auto it = b.objs.find({r.namespaced ? ns : "", name});
+  if (it == b.objs.end()) throw NotFound(r.err_res(), name);
+  return it->second;
+}
+
+void remove_locked(const Res& r, Obj live, Value final);
+void gc_dependents(const std::string& owner_uid);
+
+Value do_create(const Res& r, const std::string& url_ns, Value obj, bool dry) {
+  Value& m = mdm(obj);
+  std::string ns;
+  if (r.namespaced) {
+    ns = m.str_or("namespace");
+    if (ns.empty()) ns = url_ns;
+    if (ns.empty()) throw BadRequest("the namespace of the object must be set");
+    if (!url_ns.empty() && !m.str_or("namespace").empty() && url_ns != m.str_or("namespace"))
+      throw BadRequest("the namespace of the provided object does not match the namespace sent on the request");
+    m["namespace"] = Value::str(ns);
+  } else {
+    m.erase("namespace");
+  }
+  if (!m.str_or("resourceVersion").empty()) throw BadRequest("resourceVersion should not be set on objects to be created");
+  if (m.str_or("name").empty()) {
+    std::string gen = m.str_or("generateName");
+    if (gen.empty()) throw Invalid(r.kind, "", "metadata.name: Required value: name or generateName is required");
+    m["name"] = Value::str(gen + rand_suffix());
+  }
+  obj["apiVersion"] = Value::str(r.api_version(r.storage));
+  obj = admit("CREATE", r, std::move(obj), nullptr);
+  if (auto err = validate(r, obj)) throw Invalid(r.group.empty() ? r.singular : r.kind + "." + r.group, mget(obj, "name"), *err);
+  std::lock_guard<std::mutex> g(S.mu);
+  Bucket& b = bucket(r);
+  std::pair<std::string, std::string> k{ns, mget(obj, "name")};
+  if (b.objs.count(k)) throw AlreadyExists(r.err_res(), k.second);
+  Value& mm = mdm(obj);
+  mm["uid"] = Value::str(uuid4());
+  mm["creationTimestamp"] = Value::str(rfc3339_now());
+  mm.erase("deletionTimestamp");
+  if (obj.get("spec") || r.status) mm["generation"] = Value::integer(1);
+  if (r.status && !r.group.empty()) obj.erase("status");
+  defaults(r, obj);
+  if (dry) return obj;
+  mdm(obj)["resourceVersion"] = Value::str(std::to_string(++S.rv));
+  auto sp = std::make_shared<const Value>(std::move(obj));
+  b.objs[k] = sp;
+  S.uids[mget(*sp, "uid")] = std::make_tuple(r.key, ns, k.second);
+  index_owner(r, *sp, false);
+  S.writes++;
+  emit(r, "ADDED", sp, nullptr);
+  return *sp;
+}
+
+// commit a new version over `cur` (caller holds no lock)
+Value commit_update(const Res& r, const Value& cur_snapshot, Value nw) {
+  std::lock_guard<std::mutex> g(S.mu);
+  std::string ns = mget(cur_snapshot, "namespace"), name = mget(cur_snapshot, "name");
+  Bucket& b = bucket(r);
+  auto it = b.objs.find({ns, name});
+  if (it == b.objs.end()) throw NotFound(r.err_res(), name);
+  Obj live = it->second;
+  Value& m = mdm(nw);
+  std::string rv = m.str_or("resourceVersion");
+  if (!rv.empty() && rv != mget(*live, "resourceVersion")) throw Conflict(r.err_res(), name);
+  const Value& lm = *md(*live);
+  for (const char* k : {"uid", "creationTimestamp", "deletionTimestamp", "deletionGracePeriodSeconds"}) {
+    const Value* v = lm.get(k);
+    if (v) m[k] = *v;
+    else m.erase(k);
+  }
+  if (r.namespaced) m["namespace"] = Value::str(ns);
+  else m.erase("namespace");
+  m["name"] = Value::str(name);
+  if (lm.get("deletionTimestamp")) {
+    std::set<std::string> before, added;
+    if (const Value* f = lm.get("finalizers"))
+      for (auto& x : f->arr) before.insert(x.s);
+    if (const Value* f = m.get("finalizers"))
+      for (auto& x : f->arr)
+        if (!before.count(x.s)) added.insert(x.s);
+    if (!added.empty()) {
+      std::string l;
+      for (auto& a : added) l += (l.empty() ? "" : " ") + a;
+      throw Forbidden("no new finalizers can be added if the object is being deleted, found new finalizers [" + l + "]");
+    }
+  }
+  if (const Value* gen = lm.get("generation")) {
+    int64_t gv = gen->i;
+    if (!spec_equal(nw, *live)) gv++;
+    m["generation"] = Value::integer(gv);
+  }
+  m["resourceVersion"] = Value::str(mget(*live, "resourceVersion"));
+  if (equal_except_meta(nw, *live)) return *live;  // no-op write
+  const Value* fin = m.get("finalizers");
+  bool no_fin = !fin || !fin->is_arr() || fin->arr.empty();
+  if (lm.get("deletionTimestamp") && no_fin) {
+    mdm(nw)["resourceVersion"] = Value::str(std::to_string(++S.rv));
+    Value out = nw;
+    remove_locked(r, live, std::move(nw));
+    return out;
+  }
+  mdm(nw)["resourceVersion"] = Value::str(std::to_string(++S.rv));
+  index_owner(r, *live, true);
+  auto sp = std::make_shared<const Value>(std::move(nw));
+  it->second = sp;
+  index_owner(r, *sp, false);
+  S.writes++;
+  emit(r, "MODIFIED", sp, live);
+  return *sp;
+}
+
+Value do_update(const Res& r, const std::string& ns, const std::string& name, Value nw, const std::string& sub) {
+  Obj cur;
+  {
+    std::lock_guard<std::mutex> g(S.mu);
+    auto it = bucket(r).objs.find({r.namespaced ? ns : "", name});
+    if (it == bucket(r).objs.end()) throw NotFound(r.err_res(), name);
+    cur = it->second;
+  }
+  nw["apiVersion"] = Value::str(r.api_version(r.storage));
+  if (sub == "status") {
+    Value merged = *cur;
+    if (const Value* st = nw.get("status")) merged["status"] = *st;
+    else merged.erase("status");
+    mdm(merged)["resourceVersion"] = Value::str(mget(nw, "resourceVersion"));
+    nw = std::move(merged);
+  } else {
+    if (r.status) {
+      if (const Value* st = cur->get("status")) nw["status"] = *st;
+      else nw.erase("status");
+    }
+    nw = admit("UPDATE", r, std::move(nw), cur.get());
+    if (auto err = validate(r, nw)) throw Invalid(r.kind + "." + r.group, name, *err);
+  }
+  return commit_update(r, *cur, std::move(nw));
+}
+
+Value do_patch_once(const Res& r, const std::string& ns, const std::string& name, const Value& patch,
+                    const std::string& ptype, const std::string& sub) {
+  Obj cur;
+  {
+    std::lock_guard<std::mutex> g(S.mu);
+    auto it = bucket(r).objs.find({r.namespaced ? ns : "", name});
+    if (it == bucket(r).objs.end()) throw NotFound(r.err_res(), name);
+    cur = it->second;
+  }
+  Value nw;
+  try {
+    if (ptype == "merge") nw = merge_patch(*cur, patch);
+    else if (ptype == "json") nw = apply_json_patch(*cur, patch);
+    else if (ptype == "strategic") nw = strategic_patch(*cur, patch);
+    else throw BadRequest("unsupported patch type " + ptype);
+  } catch (const PatchErr& e) {
+    throw Invalid(r.kind, name, e.msg);
+  }
+  const Value* pm = patch.is_obj() ? patch.get("metadata") : nullptr;
+  bool precond = pm && pm->is_obj() && !pm->str_or("resourceVersion").empty();
+  if (!precond) mdm(nw)["resourceVersion"] = Value::str(mget(*cur, "resourceVersion"));
+  if (sub == "status") {
+    Value merged = *cur;
+    const Value* st = nw.get("status");
+    merged["status"] = st ? *st : Value();
+    mdm(merged)["resourceVersion"] = Value::str(mget(nw, "resourceVersion"));
+    nw = std::move(merged);
+  } else {
+    if (r.status) {
+      if (const Value* st = cur->get("status")) nw["status"] = *st;
+      else nw.erase("status");
+    }
+    nw = admit("UPDATE", r, std::move(nw), cur.get());
+    if (auto err = validate(r, nw)) throw Invalid(r.kind + "." + r.group, name, *err);
+  }
+  return commit_update(r, *cur, std::move(nw));
+}
+
+// A patch without a resourceVersion precondition applies to whatever is current: like
+// the apiserver's GuaranteedUpdate loop, a conflict with a concurrent writer (e.g. during
+// a slow admission webhook call) re-reads and re-applies instead of failing.
+Value do_patch(const Res& r, const std::string& ns, const std::string& name, const Value& patch,
+               const std::string& ptype, const std::string& sub) {
+  const Value* pm = patch.is_obj() ? patch.get("metadata") : nullptr;
+  bool precond = pm && pm->is_obj() && !pm->str_or("resourceVersion").empty();
+  for (int attempt = 0;; ++attempt) {
+    try {
+      return do_patch_once(r, ns, name, patch, ptype, sub);
+    } catch (const ApiErr& e) {
+      if (e.reason != "Conflict" || precond || attempt >= 16) throw;
+    }
+  }
+}
+
+void remove_locked(const Res& r, Obj live, Value final) {
+  std::string ns = mget(*live, "namespace"), name = mget(*live, "name"), uid = mget(*live, "uid");
+  bucket(r).objs.erase({ns, name});
+  S.uids.erase(uid);
+  index_owner(r, *live, true);
+  S.writes++;
+  auto fp = std::make_shared<const Value>(std::move(final));
+  emit(r, "DELETED", fp, live);
+  if (S.gc) gc_dependents(uid);
+  // foreground owners waiting for their last dependent
+  if (S.gc) {
+    const Value* refs = md(*fp) ? md(*fp)->get("ownerReferences") : nullptr;
+    if (refs && refs->is_arr())
+      for (auto& ref : refs->arr) {
+        std::string u = ref.str_or("uid");
+        auto loc = S.uids.find(u);
+        if (loc == S.uids.end() || S.owners.count(u)) continue;
+        Res* orr = by_key(std::get<0>(loc->second));
+        if (!orr) continue;
+        auto it = bucket(*orr).objs.find({std::get<1>(loc->second), std::get<2>(loc->second)});
+        if (it == bucket(*orr).objs.end()) continue;
+        const Value* f = md(*it->second)->get("finalizers");
+        bool fg = false;
+        if (f && f->is_arr())
+          for (auto& x : f->arr)
+            if (x.s == "foregroundDeletion") fg = true;
+        if (!fg) continue;
+        Value nw = *it->second;
+        Value nf = Value::array();
+        for (auto& x : f->arr)
+          if (x.s != "foregroundDeletion") nf.arr.push_back(x);
+        mdm(nw)["finalizers"] = nf;
+        mdm(nw)["resourceVersion"] = Value::str(std::to_string(++S.rv));
+        Obj old = it->second;
+        if (nf.arr.empty()) {
+          remove_locked(*orr, old, std::move(nw));
+        } else {
+          auto sp = std::make_shared<const Value>(std::move(nw));
+          it->second = sp;
+          emit(*orr, "MODIFIED", sp, old);
+        }
+      }
+  }
+}
+
+void sync_delete_locked(const Res& r, const std::string& ns, const std::string& name) {
+  auto it = bucket(r).objs.find({ns, name});
+  if (it == bucket(r).objs.end()) return;
+  Obj cur = it->second;
+  const Value* f = md(*cur)->get("finalizers");
+  if (f && f->is_arr() && !f->arr.empty()) {
+    if (md(*cur)->get("deletionTimestamp")) return;
+    Value nw = *cur;
+    mdm(nw)["deletionTimestamp"] = Value::str(rfc3339_now());
+    mdm(nw)["resourceVersion"] = Value::str(std::to_string(++S.rv));
+    auto sp = std::make_shared<const Value>(std::move(nw));
+    it->second = sp;
+    emit(r, "MODIFIED", sp, cur);
+    return;
+  }
+  Value final = *cur;
+  mdm(final)["resourceVersion"] = Value::str(std::to_string(++S.rv));
+  remove_locked(r, cur, std::move(final));
+}
+
+void gc_dependents(const std::string& owner_uid) {
+  auto it = S.owners.find(owner_uid);
+  if (it == S.owners.end()) return;
+  auto deps = it->second;
+  for (auto& d : deps) {
+    Res* r = by_key(std::get<0>(d));
+    if (!r) continue;
+    auto oit = bucket(*r).objs.find({std::get<1>(d), std::get<2>(d)});
+    if (oit == bucket(*r).objs.end()) continue;
+    bool other_live = false;
+    if (const Value* refs = md(*oit->second)->get("ownerReferences"))
+      for (auto& ref : refs->arr) {
+        std::string u = ref.str_or("uid");
+        if (u != owner_uid && S.uids.count(u)) other_live = true;
+      }
+    if (other_live) continue;
+    sync_delete_locked(*r, std::get<1>(d), std::get<2>(d));
+  }
+}
+
+Value do_delete(const Res& r, const std::string& ns_, const std::string& name, const Value& opts) {
+  std::string ns = r.namespaced ? ns_ : "";
+  std::lock_guard<std::mutex> g(S.mu);
+  auto it = bucket(r).objs.find({ns, name});
+  if (it == bucket(r).objs.end()) throw NotFound(r.err_res(), name);
+  Obj cur = it->second;
+  if (const Value* pc = opts.get("preconditions")) {
+    std::string u = pc->str_or("uid"), rv = pc->str_or("resourceVersion");
+    if (!u.empty() && u != mget(*cur, "uid")) throw Conflict(r.err_res(), name, "Precondition failed: UID in precondition does not match");
+    if (!rv.empty() && rv != mget(*cur, "resourceVersion")) throw Conflict(r.err_res(), name, "Precondition failed: resourceVersion does not match");
+  }
+  Value fins = Value::array();
+  if (const Value* f = md(*cur)->get("finalizers"))
+    if (f->is_arr()) fins = *f;
+  std::string prop = opts.str_or("propagationPolicy", "Background");
+  bool has_fg = false;
+  for (auto& x : fins.arr)
+    if (x.s == "foregroundDeletion") has_fg = true;
+  if (prop == "Foreground" && S.gc && !has_fg) fins.arr.push_back(Value::str("foregroundDeletion"));
+  if (!fins.arr.empty()) {
+    if (md(*cur)->get("deletionTimestamp")) return *cur;
+    Value nw = *cur;
+    Value& m = mdm(nw);
+    m["finalizers"] = fins;
+    m["deletionTimestamp"] = Value::str(rfc3339_now());
+    m["deletionGracePeriodSeconds"] = Value::integer(0);
+    if (Value* gen = m.get("generation")) gen->i += 1;
+    m["resourceVersion"] = Value::str(std::to_string(++S.rv));
+    auto sp = std::make_shared<const Value>(std::move(nw));
+    it->second = sp;
+    S.writes++;
+    emit(r, "MODIFIED", sp, cur);
+    bool fg = false;
+    for (auto& x : fins.arr)
+      if (x.s == "foregroundDeletion") fg = true;
+    if (fg) gc_dependents(mget(*cur, "uid"));
+    return *sp;
+  }
+  Value final = *cur;
+  mdm(final)["resourceVersion"] = Value::str(std::to_string(++S.rv));
+  Value out = final;
+  remove_locked(r, cur, std::move(final));
+  return out;
+}
+
+// ------------------------------------------------------------------ HTTP server
+
+std::string g_token;
+std::atomic<bool> g_stop{false};
+
+struct Conn {
+  int fd;
+  std::string buf;
+};
+
+bool write_all(int fd, const char* p, size_t n) {
+  while (n) {
+    ssize_t w = send(fd, p, n, MSG_NOSIGNAL);
+    if (w <= 0) return false;
+    p += w;
+    n -= w;
+  }
+  return true;
+}
+
+const char* reason_phrase(int code) {
+  switch (code) {
+    case 200: return "OK";
+    case 201: return "Created";
+    case 400: return "Bad Request";
+    case 401: return "Unauthorized";
+    case 403: return "Forbidden";
+    case 404: return "Not Found";
+    case 405: return "Method Not Allowed";
+    case 409: return "Conflict";
+    case 410: return "Gone";
+    case 415: return "Unsupported Media Type";
+    case 422: return "Unprocessable Entity";
+    default: return "Internal Server Error";
+  }
+}
+
+bool respond(int fd, int code, const std::string& body, bool keep_alive) {
+  std::string h = "HTTP/1.1 " + std::to_string(code) + " " + reason_phrase(code) +
+                  "\r\nContent-Type: application/json\r\nContent-Length: " + std::to_string(body.size()) +
+                  (keep_alive ? "\r\n\r\n" : "\r\nConnection: close\r\n\r\n");
+  h += body;
+  return write_all(fd, h.data(), h.size());
+}
+
+struct Request {
+  std::string method, path, query, body, ctype, auth;
+  bool keep_alive = true;
+  std::map<std::string, std::string> q;
+};
+
+bool read_request(Conn& c, Request& rq) {
+  char tmp[65536];
+  size_t hdr_end;
+  while ((hdr_end = c.buf.find("\r\n\r\n")) == std::string::npos) {
+    ssize_t n = recv(c.fd, tmp, sizeof(tmp), 0);
+    if (n <= 0) return false;
+    c.buf.append(tmp, n);
+    if (c.buf.size() > (64u << 20)) return false;
+  }
+  std::string head = c.buf.substr(0, hdr_end);
+  c.buf.erase(0, hdr_end + 4);
+  std::istringstream hs(head);
+  std::string line;
+  std::getline(hs, line);
+  if (!line.empty() && line.back() == '\r') line.pop_back();
+  std::istringstream ls(line);
+  std::string target, proto;
+  ls >> rq.method >> target >> proto;
+  size_t qm = target.find('?');
+  rq.path = url_decode(target.substr(0, qm));
+  rq.query = qm == std::string::npos ? "" : target.substr(qm + 1);
+  for (auto& kv : split(rq.query, '&')) {
+    if (kv.empty()) continue;
+    size_t e = kv.find('=');
+    rq.q[url_decode(kv.substr(0, e))] = e == std::string::npos ? "" : url_decode(kv.substr(e + 1));
+  }
+  size_t clen = 0;
+  bool chunked = false;
+  rq.keep_alive = proto != "HTTP/1.0";
+  while (std::getline(hs, line)) {
+    if (!line.empty() && line.back() == '\r') line.pop_back();
+    size_t colon = line.find(':');
+    if (colon == std::string::npos) continue;
+    std::string k = line.substr(0, colon), v = trim(line.substr(colon + 1));
+    std::transform(k.begin(), k.end(), k.begin(), ::tolower);
+    if (k == "content-length") clen = std::stoul(v);
+    else if (k == "content-type") rq.ctype = v.substr(0, v.find(';'));
+    else if (k == "authorization") rq.auth = v;
+    else if (k == "transfer-encoding" && v.find("chunked") != std::string::npos) chunked = true;
+    else if (k == "connection") {
+      std::string lv = v;
+      std::transform(lv.begin(), lv.end(), lv.begin(), ::tolower);
+      if (lv == "close") rq.keep_alive = false;
+    }
+  }
+  if (chunked) {
+    std::string out;
+    while (true) {
+      size_t le;
+      while ((le = c.buf.find("\r\n")) == std::string::npos) {
+        ssize_t n = recv(c.fd, tmp, sizeof(tmp), 0);
+        if (n <= 0) return false;
+        c.buf.append(tmp, n);
+      }
+      size_t sz = std::stoul(c.buf.substr(0, le), nullptr, 16);
+      c.buf.erase(0, le + 2);
+      while (c.buf.size() < sz + 2) {
+        ssize_t n = recv(c.fd, tmp, sizeof(tmp), 0);
+        if (n <= 0) return false;
+        c.buf.append(tmp, n);
+      }
+      if (sz == 0) {
+        c.buf.erase(0, 2);
+        break;
+      }
+      out.append(c.buf, 0, sz);
+      c.buf.erase(0, sz + 2);
+    }
+    rq.body = out;
+  } else {
+    while (c.buf.size() < clen) {
+      ssize_t n = recv(c.fd, tmp, sizeof(tmp), 0);
+      if (n <= 0) return false;
+      c.buf.append(tmp, n);
+    }
+    rq.body = c.buf.substr(0, clen);
+    c.buf.erase(0, clen);
+  }
+  return true;
+}
+
+struct Path {
+  Res* res = nullptr;
+  std::string version, ns, name, sub;
+};
+
+bool parse_path(const std::string& p, Path& out) {
+  std::vector<std::string> segs;
+  for (auto& s : split(p, '/'))
+    if (!s.empty()) segs.push_back(s);
+  std::string group;
+  size_t rest;
+  if (segs.size() >= 3 && segs[0] == "api") {
+    out.version = segs[1];
+    rest = 2;
+  } else if (segs.size() >= 4 && segs[0] == "apis") {
+    group = segs[1];
+    out.version = segs[2];
+    rest = 3;
+  } else {
+    return false;
+  }
+  std::vector<std::string> r(segs.begin() + rest, segs.end());
+  if (r.size() >= 3 && r[0] == "namespaces" && by_plural(group, r[2])) {
+    out.ns = r[1];
+    r.erase(r.begin(), r.begin() + 2);
+  }
+  out.res = by_plural(group, r[0]);
+  if (!out.res || r.size() > 3) return false;
+  if (r.size() > 1) out.name = r[1];
+  if (r.size() > 2) out.sub = r[2];
+  return true;
+}
+
+Value discovery(const std::string& p, bool* found) {
+  *found = true;
+  std::string path = p;
+  while (path.size() > 1 && path.back() == '/') path.pop_back();
+  if (path == "/api") {
+    Value v = Value::object();
+    v["kind"] = Value::str("APIVersions");
+    Value vs = Value::array();
+    vs.arr.push_back(Value::str("v1"));
+    v["versions"] = vs;
+    return v;
+  }
+  if (path == "/apis") {
+    Value v = Value::object();
+    v["kind"] = Value::str("APIGroupList");
+    v["apiVersion"] = Value::str("v1");
+    std::map<std::string, std::vector<std::string>> groups;
+    for (auto& r : g_res)
+      if (!r->group.empty() && r->installed)
+        for (auto& ver : r->versions) {
+          auto& l = groups[r->group];
+          if (std::find(l.begin(), l.end(), ver) == l.end()) l.push_back(ver);
+        }
+    Value gl = Value::array();
+    for (auto& kv : groups) {
+      Value g = Value::object();
+      g["name"] = Value::str(kv.first);
+      Value vers = Value::array();
+      for (auto& ver : kv.second) {
+        Value x = Value::object();
+        x["groupVersion"] = Value::str(kv.first + "/" + ver);
+        x["version"] = Value::str(ver);
+        vers.arr.push_back(x);
+      }
+      g["versions"] = vers;
+      g["preferredVersion"] = vers.arr[0];
+      gl.arr.push_back(g);
+    }
+    v["groups"] = gl;
+    return v;
+  }
+  auto segs = split(path, '/');
+  std::vector<std::string> s;
+  for (auto& x : segs)
+    if (!x.empty()) s.push_back(x);
+  std::string group, version;
+  if (s.size() == 2 && s[0] == "api") version = s[1];
+  else if (s.size() == 3 && s[0] == "apis") {
+    group = s[1];
+    version = s[2];
+  } else {
+    *found = false;
+    return Value();
+  }
+  Value list = Value::array();
+  for (auto& r : g_res) {
+    if (r->group != group || !r->installed || std::find(r->versions.begin(), r->versions.end(), version) == r->versions.end())
+      continue;
+    Value e = Value::object();
+    e["name"] = Value::str(r->plural);
+    e["singularName"] = Value::str(r->singular);
+    e["namespaced"] = Value::boolean(r->namespaced);
+    e["kind"] = Value::str(r->kind);
+    Value verbs = Value::array();
+    for (const char* vb : {"create", "delete", "get", "list", "patch", "update", "watch"}) verbs.arr.push_back(Value::str(vb));
+    e["verbs"] = verbs;
+    list.arr.push_back(e);
+    if (r->status) {
+      Value st = Value::object();
+      st["name"] = Value::str(r->plural + "/status");
+      st["singularName"] = Value::str("");
+      st["namespaced"] = Value::boolean(r->namespaced);
+      st["kind"] = Value::str(r->kind);
+      list.arr.push_back(st);
+    }
+  }
+  if (list.arr.empty()) {
+    *found = false;
+    return Value();
+  }
+  Value v = Value::object();
+  v["kind"] = Value::str("APIResourceList");
+  v["apiVersion"] = Value::str("v1");
+  v["groupVersion"] = Value::str(group.empty() ? version : group + "/" + version);
+  v["resources"] = list;
+  return v;
+}
+
+bool socket_closed(int fd) {
+  struct pollfd p {fd, POLLIN | POLLRDHUP, 0};
+  if (poll(&p, 1, 0) > 0) {
+    if (p.revents & (POLLRDHUP | POLLHUP | POLLERR)) return true;
+    char c;
+    ssize_t n = recv(fd, &c, 1, MSG_PEEK | MSG_DONTWAIT);
+    if (n == 0) return true;
+  }
+  return false;
+}
+
+bool write_chunk(int fd, const std::string& data) {
+  char hdr[32];
+  int h = snprintf(hdr, sizeof(hdr), "%zx\r\n", data.size());
+  std::string out(hdr, h);
+  out += data;
+  out += "\r\n";
+  return write_all(fd, out.data(), out.size());
+}
+
+std::string event_line(const Res& r, const Ev& e, const std::string& version) {
+  auto& c = *e.cache;
+  std::lock_guard<std::mutex> g(c.mu);
+  if (c.line && c.version == version) return *c.line;
+  Value ev = Value::object();
+  ev["type"] = Value::str(e.type);
+  ev["object"] = out_obj(r, *e.obj, version);
+  auto s = std::make_shared<std::string>(kj::dump(ev));
+  *s += '\n';
+  if (!c.line) {
+    c.line = s;
+    c.version = version;
+  }
+  return *s;
+}
+
+void serve_watch(int fd, Res& r, const Path& p, const Request& rq) {
+  std::string rv = rq.q.count("resourceVersion") ? rq.q.at("resourceVersion") : "";
+  double timeout = rq.q.count("timeoutSeconds") ? std::atof(rq.q.at("timeoutSeconds").c_str()) : 1800.0;
+  bool bookmarks = rq.q.count("allowWatchBookmarks") && (rq.q.at("allowWatchBookmarks") == "true" || rq.q.at("allowWatchBookmarks") == "1");
+  auto lr = parse_labels(rq.q.count("labelSelector") ? rq.q.at("labelSelector") : "");
+  auto fr = parse_fields(rq.q.count("fieldSelector") ? rq.q.at("fieldSelector") : "");
+  std::string ns = r.namespaced ? p.ns : "";
+  auto wants = [&](const Value& o) {
+    if (!ns.empty() && mget(o, "namespace") != ns) return false;
+    if (!lr.empty() && !match_labels(lr, o)) return false;
+    if (!fr.empty() && !match_fields(fr, o)) return false;
+    return true;
+  };
+  std::string head = "HTTP/1.1 200 OK\r\nContent-Type: application/json\r\nTransfer-Encoding: chunked\r\n\r\n";
+  if (!write_all(fd, head.data(), head.size())) return;
+  int64_t last_seq;
+  std::vector<std::string> pending;
+  {
+    std::lock_guard<std::mutex> g(S.mu);
+    Bucket& b = bucket(r);
+    last_seq = b.seq;
+    if (rv.empty() || rv == "0") {
+      for (auto& kv : b.objs)
+        if (wants(*kv.second)) {
+          Value ev = Value::object();
+          ev["type"] = Value::str("ADDED");
+          ev["object"] = out_obj(r, *kv.second, p.version);
+          pending.push_back(kj::dump(ev) + "\n");
+        }
+    } else {
+      int64_t since = std::stoll(rv);
+      if (!b.hist.empty() && since < b.hist.front().rv - 1 && since < S.rv - (int64_t)b.hist.size()) {
+        Value ev = Value::object();
+        ev["type"] = Value::str("ERROR");
+        ev["object"] = status_obj(Gone());
+        pending.push_back(kj::dump(ev) + "\n");
+        last_seq = -1;
+      } else {
+        for (auto& e : b.hist)
+          if (e.rv > since && (wants(*e.obj) || (e.old && wants(*e.old)))) pending.push_back(event_line(r, e, p.version));
+      }
+    }
+  }
+  for (auto& l : pending)
+    if (!write_chunk(fd, l)) return;
+  if (last_seq < 0) {
+    write_all(fd, "0\r\n\r\n", 5);
+    return;
+  }
+  auto deadline = std::chrono::steady_clock::now() + std::chrono::milliseconds((int64_t)(timeout * 1000));
+  auto last_write = std::chrono::steady_clock::now();
+  while (!g_stop) {
+    std::vector<std::string> lines;
+    bool gone = false;
+    {
+      std::unique_lock<std::mutex> lk(S.mu);
+      Bucket& b = bucket(r);
+      S.cv.wait_for(lk, std::chrono::milliseconds(500), [&] { return b.seq > last_seq || g_stop.load(); });
+      if (b.seq > last_seq) {
+        if (!b.hist.empty() && b.hist.front().seq > last_seq + 1) {
+          gone = true;  // the watcher fell behind the bounded history
+        } else {
+          size_t start = b.hist.size() - (size_t)(b.seq - last_seq);
+          // serialise outside the store lock (copy the shared event refs first)
+          std::vector<Ev> evs;
+          for (size_t n = start; n < b.hist.size(); ++n) {
+            const Ev& e = b.hist[n];
+            if (wants(*e.obj) || (e.old && wants(*e.old))) evs.push_back(e);
+          }
+          last_seq = b.seq;
+          lk.unlock();
+          for (auto& e : evs) lines.push_back(event_line(r, e, p.version));
+        }
+      }
+    }
+    if (gone) {
+      Value ev = Value::object();
+      ev["type"] = Value::str("ERROR");
+      ev["object"] = status_obj(Gone());
+      write_chunk(fd, kj::dump(ev) + "\n");
+      break;
+    }
+    if (!lines.empty()) {
+      std::string batch;
+      for (auto& l : lines) batch += l;
+      if (!write_chunk(fd, batch)) return;
+      last_write = std::chrono::steady_clock::now();
+    }
+    auto now = std::chrono::steady_clock::now();
+    if (now >= deadline) break;
+    if (socket_closed(fd)) return;
+    if (bookmarks && now - last_write > std::chrono::seconds(10)) {
+      Value bm = Value::object();
+      bm["kind"] = Value::str(r.kind);
+      bm["apiVersion"] = Value::str(r.api_version(p.version));
+      Value m = Value::object();
+      {
+        std::lock_guard<std::mutex> g(S.mu);
+        m["resourceVersion"] = Value::str(std::to_string(S.rv));
+      }
+      bm["metadata"] = m;
+      Value ev = Value::object();
+      ev["type"] = Value::str("BOOKMARK");
+      ev["object"] = bm;
+      if (!write_chunk(fd, kj::dump(ev) + "\n")) return;
+      last_write = now;
+    }
+  }
+  write_all(fd, "0\r\n\r\n", 5);
+}
+
+bool handle(int fd, Request& rq) {
+  S.requests++;
+  if (!g_token.empty() && rq.auth != "Bearer " + g_token) {
+    return respond(fd, 401, kj::dump(status_obj({401, "Unauthorized", "Unauthorized", Value()})), rq.keep_alive);
+  }
+  if (rq.method == "GET" && (rq.path == "/healthz" || rq.path == "/readyz" || rq.path == "/livez")) {
+    std::string h = "HTTP/1.1 200 OK\r\nContent-Type: text/plain\r\nContent-Length: 2\r\n\r\nok";
+    return write_all(fd, h.data(), h.size());
+  }
+  if (rq.method == "GET" && rq.path == "/version") {
+    return respond(fd, 200, "{\"major\":\"1\",\"minor\":\"32\",\"gitVersion\":\"v1.32.8-odh-kubeflow-amd-native\"}",
+                   rq.keep_alive);
+  }
+  if (rq.method == "GET" && rq.path == "/metrics") {
+    char buf[256];
+    snprintf(buf, sizeof(buf),
+             "{\"requests\":%llu,\"writes\":%llu,\"webhook_calls\":%llu,\"resourceVersion\":%lld}",
+             (unsigned long long)S.requests.load(), (unsigned long long)S.writes.load(),
+             (unsigned long long)S.webhook_calls.load(), (long long)S.rv);
+    return respond(fd, 200, buf, rq.keep_alive);
+  }
+  try {
+    if (rq.method == "GET") {
+      bool found;
+      Value d = discovery(rq.path, &found);
+      if (found) return respond(fd, 200, kj::dump(d), rq.keep_alive);
+    }
+    Path p;
+    if (!parse_path(rq.path, p)) throw NotFound("path", rq.path);
+    Res& r = res_checked(p.res);
+    if (std::find(r.versions.begin(), r.versions.end(), p.version) == r.versions.end())
+      throw NotFound(r.plural, "version " + p.version);
+    if (!p.sub.empty() && p.sub != "status") throw NotFound(r.plural, p.name + "/" + p.sub);
+    if (!r.namespaced && !p.ns.empty()) throw BadRequest(r.plural + " is not namespaced");
+    auto qget = [&](const char* k) { return rq.q.count(k) ? rq.q.at(k) : std::string(); };
+    if (rq.method == "GET" && p.name.empty()) {
+      std::string w = qget("watch");
+      if (w == "1" || w == "true" || w == "True") {
+        serve_watch(fd, r, p, rq);
+        return false;  // watch streams end the connection
+      }
+      auto lst = do_list(r, p.ns, qget("labelSelector"), qget("fieldSelector"));
+      std::string body = "{\"kind\":\"" + r.list_kind + "\",\"apiVersion\":\"" + r.api_version(p.version) +
+                         "\",\"metadata\":{\"resourceVersion\":\"" + std::to_string(lst.second) + "\"},\"items\":[";
+      for (size_t n = 0; n < lst.first.size(); ++n) {
+        if (n) body += ',';
+        if (p.version == r.storage) kj::dump(body, *lst.first[n]);
+        else kj::dump(body, out_obj(r, *lst.first[n], p.version));
+      }
+      body += "]}";
+      return respond(fd, 200, body, rq.keep_alive);
+    }
+    if (rq.method == "GET") {
+      Obj o = do_get(r, p.ns, p.name);
+      return respond(fd, 200, p.version == r.storage ? kj::dump(*o) : kj::dump(out_obj(r, *o, p.version)), rq.keep_alive);
+    }
+    Value body;
+    if (!rq.body.empty()) {
+      try {
+        body = kj::parse(rq.body);
+      } catch (const kj::ParseError& e) {
+        throw BadRequest(std::string("invalid JSON body: ") + e.what());
+      }
+    }
+    if (rq.method == "POST" && p.name.empty()) {
+      if (!body.is_obj()) throw BadRequest("object body required");
+      if (!body.get("kind")) body["kind"] = Value::str(r.kind);
+      Value out = do_create(r, p.ns, std::move(body), qget("dryRun") == "All");
+      return respond(fd, 201, kj::dump(out_obj(r, out, p.version)), rq.keep_alive);
+    }
+    if (rq.method == "PUT" && !p.name.empty()) {
+      if (!body.is_obj()) throw BadRequest("object body required");
+      Value& m = mdm(body);
+      if (!m.str_or("name").empty() && m.str_or("name") != p.name)
+        throw BadRequest("the name of the object does not match the name on the URL");
+      m["name"] = Value::str(p.name);
+      Value out = do_update(r, p.ns, p.name, std::move(body), p.sub);
+      return respond(fd, 200, kj::dump(out_obj(r, out, p.version)), rq.keep_alive);
+    }
+    if (rq.method == "PATCH" && !p.name.empty()) {
+      std::string pt;
+      if (rq.ctype == "application/merge-patch+json" || rq.ctype == "application/apply-patch+yaml") pt = "merge";
+      else if (rq.ctype == "application/json-patch+json") pt = "json";
+      else if (rq.ctype == "application/strategic-merge-patch+json") pt = "strategic";
+      else
+        return respond(fd, 415, kj::dump(status_obj({415, "UnsupportedMediaType", "unsupported patch type " + rq.ctype, Value()})),
+                       rq.keep_alive);
+      Value out = do_patch(r, p.ns, p.name, body, pt, p.sub);
+      return respond(fd, 200, kj::dump(out_obj(r, out, p.version)), rq.keep_alive);
+    }
+    if (rq.method == "DELETE" && !p.name.empty()) {
+      Value opts = body.is_obj() ? body : Value::object();
+      if (!opts.get("propagationPolicy") && !qget("propagationPolicy").empty())
+        opts["propagationPolicy"] = Value::str(qget("propagationPolicy"));
+      Value out = do_delete(r, p.ns, p.name, opts);
+      return respond(fd, 200, kj::dump(out), rq.keep_alive);
+    }
+    return respond(fd, 405, kj::dump(status_obj({405, "MethodNotAllowed", rq.method + " not allowed", Value()})),
+                   rq.keep_alive);
+  } catch (const ApiErr& e) {
+    return respond(fd, e.code, kj::dump(status_obj(e)), rq.keep_alive);
+  } catch (const kj::ParseError& e) {
+    return respond(fd, 400, kj::dump(status_obj(BadRequest(e.what()))), rq.keep_alive);
+  } catch (const std::exception& e) {
+    return respond(fd, 500, kj::dump(status_obj(Internal(e.what()))), rq.keep_alive);
+  }
+}
+
+void serve_conn(int fd) {
+  Conn c{fd, {}};
+  int one = 1;
+  setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof(one));
+  while (!g_stop) {
+    Request rq;
+    if (!read_request(c, rq)) break;
+    if (!handle(fd, rq)) break;
+    if (!rq.keep_alive) break;
+  }
+  close(fd);
+}
+
+void load_config(const std::string& path) {
+  std::ifstream f(path);
+  std::stringstream ss;
+  ss << f.rdbuf();
+  Value cfg = kj::parse(ss.str());
+  const Value* res = cfg.get("resources");
+  if (!res || !res->is_arr()) throw std::runtime_error("config: resources[] required");
+  for (auto& r : res->arr) {
+    auto x = std::make_unique<Res>();
+    x->group = r.str_or("group");
+    x->kind = r.str_or("kind");
+    x->plural = r.str_or("plural");
+    x->singular = r.str_or("singular");
+    x->list_kind = r.str_or("listKind", x->kind + "List");
+    x->storage = r.str_or("storageVersion");
+    x->key = x->group.empty() ? x->plural : x->plural + "." + x->group;
+    if (const Value* v = r.get("versions"))
+      for (auto& s : v->arr) x->versions.push_back(s.s);
+    if (const Value* v = r.get("namespaced")) x->namespaced = v->b;
+    if (const Value* v = r.get("status")) x->status = v->b;
+    if (const Value* v = r.get("installed")) x->installed = v->b;
+    g_res.push_back(std::move(x));
+  }
+  if (const Value* v = cfg.get("gc")) S.gc = v->b;
+  if (const Value* v = cfg.get("history"))
+    if (v->t == T::Int) S.history = (size_t)v->i;
+  g_token = cfg.str_or("token");
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+  std::string host = "127.0.0.1", config;
+  int port = 0;
+  for (int k = 1; k < argc; ++k) {
+    std::string a = argv[k];
+    auto next = [&]() { return k + 1 < argc ? std::string(argv[++k]) : std::string(); };
+    if (a == "--host") host = next();
+    else if (a == "--port") port = std::stoi(next());
+    else if (a == "--config") config = next();
+    else if (a == "--gc") S.gc = true;
+    else if (a == "--token") g_token = next();
+    else if (a == "--history") S.history = std::stoul(next());
+    else {
+      fprintf(stderr, "unknown flag %s\n", a.c_str());
+      return 2;
+    }
+  }
+  if (config.empty()) {
+    fprintf(stderr, "--config scheme.json is required\n");
+    return 2;
+  }
+  bool gc_flag = S.gc;
+  std::string tok = g_token;
+  size_t hist = S.history;
+  load_config(config);
+  if (gc_flag) S.gc = true;
+  if (!tok.empty()) g_token = tok;
+  if (hist != 4096) S.history = hist;
+  signal(SIGPIPE, SIG_IGN);
+  SSL_library_init();
+  SSL_load_error_strings();
+  int ls = socket(AF_INET, SOCK_STREAM, 0);
+  int one = 1;
+  setsockopt(ls, SOL_SOCKET, SO_REUSEADDR, &one, sizeof(one));
+  struct sockaddr_in addr {};
+  addr.sin_family = AF_INET;
+  addr.sin_port = htons(port);
+  inet_pton(AF_INET, host.c_str(), &addr.sin_addr);
+  if (bind(ls, (struct sockaddr*)&addr, sizeof(addr)) != 0) {
+    perror("bind");
+    return 1;
+  }
+  listen(ls, 1024);
+  socklen_t len = sizeof(addr);
+  getsockname(ls, (struct sockaddr*)&addr, &len);
+  printf("LISTENING %d\n", ntohs(addr.sin_port));
+  fflush(stdout);
+  while (true) {
+    int fd = accept(ls, nullptr, nullptr);
+    if (fd < 0) {
+      if (errno == EINTR) continue;
+      break;
+    }
+    std::thread(serve_conn, fd).detach();
+  }
+  return 0;
+}

@@ -47,6 +47,13 @@ def targets() -> Dict[str, dict]:
                                      "-fno-strict-aliasing", f"-I{sysconfig.get_paths()['include']}", *src,
                                      "-o", out],
         },
+        "odh-apiserver": {
+            "src": [os.path.join(NATIVE, "apiserver", "apiserver.cpp")],
+            "deps": [os.path.join(NATIVE, "apiserver", "json.hpp")],
+            "out": os.path.join(NATIVE, "bin", "odh-apiserver"),
+            "cmd": lambda src, out: [os.environ.get("CXX", "g++"), "-O2", "-std=c++17", "-pthread", "-Wall", *src,
+                                     "-o", out, "-lssl", "-lcrypto"],
+        },
         "libodh_gpu_telemetry.so": {
             "src": [os.path.join(CSRC, "gpu_telemetry.cpp")],
             "cmd": lambda src, out: [os.environ.get("CXX", "g++"), "-O2", "-std=c++17", "-shared", "-fPIC",
@@ -71,7 +78,8 @@ def build(force: bool = False, verbose: bool = True) -> Dict[str, str]:
     built = {}
     for name, spec in targets().items():
         out = spec.get("out") or lib_path(name)
-        if force or _stale(out, spec["src"]):
+        os.makedirs(os.path.dirname(out), exist_ok=True)
+        if force or _stale(out, spec["src"] + spec.get("deps", [])):
             tmp = out + ".tmp"
             cmd = spec["cmd"](spec["src"], tmp)
             if verbose:

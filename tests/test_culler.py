@@ -117,8 +117,13 @@ def test_culler_jupyter_busy_keeps_idle_culls(run, clock):
             st_busy, st_idle = rt.state("user", "busy"), rt.state("user", "idle")
             kid = st_busy.start_kernel(busy=True)
             st_idle.start_kernel(busy=False)
-            # annotations initialised
+            # annotations initialised and the busy kernel observed before time jumps
             assert await cl.wait_for(lambda: c.annotations_exist(cl.store.peek(kinds.NOTEBOOK, "busy", "user")))
+            culler0 = cl.reconcilers["culler"]
+            assert await cl.wait_for(lambda: any(r[1] == "user/busy" and r[3] and r[3][0]["execution_state"] == "busy"
+                                                 for r in list(culler0.recent)), 10)
+            n_seen = len(culler0.recent)
+            assert await cl.wait_for(lambda: len(culler0.recent) >= n_seen + 2, 10)
             # two hours pass
             clock[0] += 7200
             idle_nb = lambda: cl.store.peek(kinds.NOTEBOOK, "idle", "user")  # noqa: E731

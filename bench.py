@@ -48,7 +48,7 @@ def parse(argv=None):
     p.add_argument("--no-odh", action="store_true", help="kf controller only (no webhook / odh reconciler)")
     p.add_argument("--reference-emulation", action="store_true",
                    help="reproduce the reference's serialising behaviour (1 worker, blocking lock removal)")
-    p.add_argument("--transport", choices=("inprocess", "http"), default="inprocess",
+    p.add_argument("--transport", choices=("inprocess", "http", "native"), default="inprocess",
                    help="managers share the store (inprocess) or talk REST/watch to the apiserver (http)")
     p.add_argument("--json-out", default=None)
     return p.parse_args(argv)
@@ -110,7 +110,9 @@ async def run_local(args, n_gpus: int, probe) -> dict:
                                                cl.store.peek(kinds.POD, f"{nm}-0", "bench") is None
                                                for nm in names), 60, 0.0005)
             if not ok:
-                raise RuntimeError("teardown did not finish")
+                left = [(k, o) for nm in names for k, o in ((kinds.NOTEBOOK, nm), (kinds.POD, f"{nm}-0"))
+                        if cl.store.peek(k, o, "bench") is not None]
+                raise RuntimeError(f"teardown did not finish: {[cl.store.peek(k, o, 'bench') for k, o in left]}")
             await cl.settle(5)
             if timed:
                 recon += cl.reconcile_count() - r0

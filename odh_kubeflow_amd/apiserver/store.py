@@ -351,7 +351,15 @@ class ObjectStore:
             self._index_owner(info, obj)
             self.write_count += 1
             self._emit(info, ADDED, obj, None)
-            return self._out(info, obj, version)
+            out = self._out(info, obj, version)
+            refs = md.get("ownerReferences")
+            if self.gc_enabled and refs and not any(self._owner_live(r) for r in refs):
+                # GC "absent owner": a dependent created after its owners are gone is collected
+                try:
+                    self._sync_delete(info, ns, k[1])
+                except ApiError:
+                    pass
+            return out
 
     async def update(self, obj: dict, subresource: Optional[str] = None, namespace: Optional[str] = None) -> dict:
         info = self._info(obj)
@@ -551,6 +559,17 @@ class ObjectStore:
 
     def _uid_exists(self, u: str) -> bool:
         return u in self._uids
+
+    def _owner_live(self, ref: dict) -> bool:
+        """True unless ``ref`` names a kind this store serves and no object has its uid
+        (an owner of an unknown kind cannot be verified, so it counts as live)."""
+        if self._uid_exists(ref.get("uid")):
+            return True
+        try:
+            SCHEME.resolve(f"{ref.get('apiVersion', '')}/{ref.get('kind', '')}")
+        except Exception:
+            return True
+        return False
 
     def _gc_foreground_owners(self, removed: dict) -> None:
         for r in removed["metadata"].get("ownerReferences") or []:

@@ -77,15 +77,23 @@ class LocalCluster:
 
     def _mgr(self, name: str, remote: bool = False, **kw) -> Manager:
         if (remote or self.cfg.transport == "native") and self.rest_config is not None:
-            from .runtime.informer import strip_data, strip_managed_fields
-
-            tf = {kinds.CONFIG_MAP: strip_data, kinds.SECRET: strip_data} if kw.get("uncached") else None
             mgr = Manager.remote(self.rest_config, name=name, default_max_concurrent=self.cfg.max_concurrent,
-                                 transforms=tf, **kw)
+                                 shared=self._shared(), **kw)
         else:
             mgr = Manager.in_process(self.store, name=name, default_max_concurrent=self.cfg.max_concurrent, **kw)
         self.managers.append(mgr)
         return mgr
+
+    def _shared(self):
+        """One REST pool + informer cache for every remote manager of this process."""
+        if getattr(self, "_shared_pair", None) is None:
+            from .runtime.informer import InformerCache, strip_data
+            from .runtime.rest import RestClient
+
+            rest = RestClient(self.rest_config)
+            self._shared_pair = (rest, InformerCache(rest, transforms={kinds.CONFIG_MAP: strip_data,
+                                                                       kinds.SECRET: strip_data}))
+        return self._shared_pair
 
     async def _start_apiserver(self) -> None:
         from .apiserver.http import ApiServer
@@ -228,6 +236,9 @@ class LocalCluster:
             await self.webhook_server.stop()
         if self.apiserver is not None:
             await self.apiserver.stop()
+        if getattr(self, "_shared_pair", None) is not None:
+            await self._shared_pair[1].stop()
+            await self._shared_pair[0].close()
         if self.native is not None:
             await self._view_cache.stop()
             await self.admin.close()

@@ -303,9 +303,13 @@ class NotebookReconciler:
         else:
             merge_status_timestamps(old_status, status)
             if status != old_status:
-                nb["status"] = status
+                # The whole status is recomputed from the pod each pass, so it is written as a
+                # JSON-patch replacement without a resourceVersion precondition: a concurrent
+                # metadata write (odh lock removal, culler annotations) cannot turn it into a
+                # 409 + requeue the way the reference's Status().Update does.
                 self.status_writes += 1
-                await self.client.update_status(nb)
+                await self.client.patch(nb, [{"op": "add", "path": "/status", "value": status}], "json",
+                                        subresource="status")
 
         ann = m.annotations(nb)
         if ann.get(ANNOTATION_NOTEBOOK_RESTART) == "true":

@@ -111,9 +111,9 @@ class StatefulSetController:
               "availableReplicas": ready, "currentRevision": rev, "updateRevision": rev,
               "observedGeneration": (sts.get("metadata") or {}).get("generation", 1)}
         if (sts.get("status") or {}) != st:
-            sts["status"] = st
             try:
-                await self.client.update_status(sts)
+                await self.client.patch(sts, [{"op": "add", "path": "/status", "value": st}], "json",
+                                        subresource="status")
             except ApiError as e:
                 if not is_not_found(e):
                     raise

@@ -555,11 +555,11 @@ struct Bucket {
   std::map<std::pair<std::string, std::string>, Obj> objs;
   std::deque<Ev> hist;
   int64_t seq = 0;
+  std::condition_variable cv;  // per resource: a write wakes only the watchers of its kind
 };
 
 struct Store {
   std::mutex mu;
-  std::condition_variable cv;
   std::unordered_map<std::string, Bucket> data;
   int64_t rv = 0;
   size_t history = 4096;
@@ -598,7 +598,7 @@ void emit(const Res& r, const char* type, Obj obj, Obj old) {
        std::make_shared<EvCache>()};
   b.hist.push_back(std::move(e));
   while (b.hist.size() > S.history) b.hist.pop_front();
-  S.cv.notify_all();
+  b.cv.notify_all();
 }
 
 Value out_obj(const Res& r, const Value& o, const std::string& version) {
@@ -1087,6 +1087,7 @@ Obj do_get(const Res& r, const std::string& ns, const std::string& name) {
 
 void remove_locked(const Res& r, Obj live, Value final);
 void gc_dependents(const std::string& owner_uid);
+void sync_delete_locked(const Res& r, const std::string& ns, const std::string& name);
 
 Value do_create(const Res& r, const std::string& url_ns, Value obj, bool dry) {
   Value& m = mdm(obj);
@@ -1129,6 +1130,26 @@ Value do_create(const Res& r, const std::string& url_ns, Value obj, bool dry) {
   index_owner(r, *sp, false);
   S.writes++;
   emit(r, "ADDED", sp, nullptr);
+  // the GC's "absent owner" rule: a dependent created after all of its owners are gone
+  // (a controller acting on a stale cache) is collected right away
+  if (S.gc) {
+    const Value* refs = md(*sp)->get("ownerReferences");
+    if (refs && refs->is_arr() && !refs->arr.empty()) {
+      bool live = false;
+      for (auto& ref : refs->arr) {
+        std::string av = ref.str_or("apiVersion");
+        auto slash = av.find('/');
+        Res* owner = by_kind(slash == std::string::npos ? "" : av.substr(0, slash), ref.str_or("kind"));
+        // an owner of a kind this server does not serve cannot be verified: keep the object
+        if (!owner || S.uids.count(ref.str_or("uid"))) live = true;
+      }
+      if (!live) {
+        Value out = *sp;
+        sync_delete_locked(r, ns, k.second);
+        return out;
+      }
+    }
+  }
   return *sp;
 }
 
@@ -1746,7 +1767,7 @@ void serve_watch(int fd, Res& r, const Path& p, const Request& rq) {
     {
       std::unique_lock<std::mutex> lk(S.mu);
       Bucket& b = bucket(r);
-      S.cv.wait_for(lk, std::chrono::milliseconds(500), [&] { return b.seq > last_seq || g_stop.load(); });
+      b.cv.wait_for(lk, std::chrono::milliseconds(500), [&] { return b.seq > last_seq || g_stop.load(); });
       if (b.seq > last_seq) {
         if (!b.hist.empty() && b.hist.front().seq > last_seq + 1) {
           gone = true;  // the watcher fell behind the bounded history

@@ -15,6 +15,7 @@ Two access paths, as in controller-runtime:
 
 from __future__ import annotations
 
+import contextvars
 import abc
 from typing import Any, Callable, Iterable, List, Optional, Sequence
 
@@ -23,6 +24,11 @@ from ..models.scheme import SCHEME, ResourceInfo
 from ..utils.objutil import deepcopy_json
 
 WatchCallback = Callable[[str, dict, Optional[dict]], None]
+
+
+# Set by ``retry_on_conflict`` for its retries: a Conflict means the informer copy is
+# stale, so the retry reads through to the apiserver instead of sleeping for the cache.
+LIVE_READS: contextvars.ContextVar = contextvars.ContextVar("live_reads", default=False)
 
 
 def _version_of(ref) -> Optional[str]:
@@ -203,7 +209,7 @@ class CachedClient(Client):
             await ensure(kind)
 
     async def get(self, kind, name, namespace=None):
-        if self._live(kind):
+        if self._live(kind) or LIVE_READS.get():
             return await self.writer.get(kind, name, namespace)
         await self._ensure(kind)
         o = self.reader.get(kind, name, namespace)

@@ -63,11 +63,20 @@ class Manager:
 
     @classmethod
     def remote(cls, config, name: str = "manager", uncached: Sequence = (), transforms=None,
-               namespace: Optional[str] = None, **kw) -> "Manager":
-        """Manager against a real (or out-of-process) apiserver: REST client + informer cache."""
+               namespace: Optional[str] = None, shared=None, **kw) -> "Manager":
+        """Manager against a real (or out-of-process) apiserver: REST client + informer cache.
+
+        ``shared=(rest, cache)`` makes several managers of one process share a single
+        connection pool and informer cache (one watch per kind per process, as the
+        controllers of kube-controller-manager do); the owner of ``shared`` closes it.
+        """
         from .informer import InformerCache
         from .rest import RestClient
 
+        if shared is not None:
+            rest, cache = shared
+            mgr = cls(CachedClient(cache, rest, uncached), cache, cache, name=name, **kw)
+            return mgr
         rest = RestClient(config)
         cache = InformerCache(rest, namespace=namespace, transforms=transforms)
         client = CachedClient(cache, rest, uncached)

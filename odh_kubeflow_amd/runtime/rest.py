@@ -150,16 +150,14 @@ class RestClient(Client):
         self.user = config.user_agent
         self._discovery: dict = {}  # "group/version" -> (fetched_at, set(plurals))
 
-    async def _sess(self):
-        import aiohttp
+    def _http(self):
+        from .http1 import Http1Pool
 
-        if self._session is None or self._session.closed:
-            conn = aiohttp.TCPConnector(limit=self._pool, ssl=self._ssl if self._ssl else False,
-                                        keepalive_timeout=60)
-            headers = {"User-Agent": self.config.user_agent, "Accept": "application/json"}
+        if self._session is None:
+            headers = {"User-Agent": self.config.user_agent}
             if self.config.token:
                 headers["Authorization"] = f"Bearer {self.config.token}"
-            self._session = aiohttp.ClientSession(connector=conn, headers=headers, json_serialize=json.dumps)
+            self._session = Http1Pool(self.base, self._ssl, headers, size=self._pool)
         return self._session
 
     async def close(self) -> None:
@@ -173,26 +171,33 @@ class RestClient(Client):
 
     async def request(self, method: str, url: str, body: Any = None, params: Optional[dict] = None,
                       content_type: str = "application/json") -> dict:
+        from urllib.parse import urlencode
+
+        from .http1 import HttpError
+
         await self._bucket.take()
-        s = await self._sess()
         self.requests += 1
         data = None if body is None else json.dumps(body, separators=(",", ":")).encode()
-        headers = {"Content-Type": content_type} if data is not None else None
-        async with s.request(method, url, data=data, params=params, headers=headers) as resp:
-            raw = await resp.read()
-            try:
-                out = json.loads(raw) if raw else {}
-            except ValueError:
-                out = {"message": raw[:200].decode(errors="replace")}
-            if resp.status >= 400:
-                if isinstance(out, dict) and out.get("kind") == "Status":
-                    err = ApiError.from_status(out, resp.status)
-                else:
-                    err = ApiError.from_status({"code": resp.status, "message": str(out)}, resp.status)
-                if resp.status == 404 and err.reason != "NoKindMatch":
-                    await self._maybe_no_match(url, err)
-                raise err
-            return out
+        target = url[len(self.base):] if url.startswith(self.base) else url
+        if params:
+            target += ("&" if "?" in target else "?") + urlencode(params)
+        try:
+            status, raw = await self._http().request(method, target, data, content_type if data is not None else None)
+        except HttpError as e:
+            raise InternalError(str(e))
+        try:
+            out = json.loads(raw) if raw else {}
+        except ValueError:
+            out = {"message": raw[:200].decode(errors="replace")}
+        if status >= 400:
+            if isinstance(out, dict) and out.get("kind") == "Status":
+                err = ApiError.from_status(out, status)
+            else:
+                err = ApiError.from_status({"code": status, "message": str(out)}, status)
+            if status == 404 and err.reason != "NoKindMatch":
+                await self._maybe_no_match(url, err)
+            raise err
+        return out
 
     async def _served(self, group: str, version: str) -> set:
         key = f"{group}/{version}"
@@ -200,10 +205,9 @@ class RestClient(Client):
         if hit is not None and time.monotonic() - hit[0] < 30.0:
             return hit[1]
         path = f"/apis/{group}/{version}" if group else f"/api/{version}"
-        s = await self._sess()
         try:
-            async with s.get(self.base + path) as resp:
-                doc = await resp.json(content_type=None) if resp.status == 200 else {}
+            status, raw = await self._http().request("GET", path)
+            doc = json.loads(raw) if status == 200 and raw else {}
         except Exception:
             doc = {}
         plurals = {r.get("name") for r in (doc or {}).get("resources") or []}
@@ -293,7 +297,7 @@ class RestClient(Client):
     async def watch(self, kind, namespace=None, resource_version: Optional[str] = None, labels=None, fields=None,
                     timeout_s: int = 300, bookmarks: bool = True) -> AsyncIterator[Tuple[str, dict]]:
         """Yield ``(type, object)``; raises :class:`Gone` when the RV is too old."""
-        import aiohttp
+        from urllib.parse import urlencode
 
         info, v = _info_and_version(kind)
         params = {"watch": "true", "timeoutSeconds": str(timeout_s)}
@@ -306,31 +310,26 @@ class RestClient(Client):
         if fields:
             params["fieldSelector"] = fields
         await self._bucket.take()
-        s = await self._sess()
         self.requests += 1
-        async with s.get(self.path(info, v, namespace), params=params,
-                         timeout=aiohttp.ClientTimeout(total=None, sock_read=timeout_s + 30)) as resp:
-            if resp.status >= 400:
-                raw = await resp.read()
-                try:
-                    raise ApiError.from_status(json.loads(raw), resp.status)
-                except ValueError:
-                    raise InternalError(raw[:200].decode(errors="replace"))
-            buf = b""
-            async for chunk in resp.content.iter_any():
-                buf += chunk
-                while True:
-                    nl = buf.find(b"\n")
-                    if nl < 0:
-                        break
-                    line, buf = buf[:nl], buf[nl + 1:]
-                    if not line.strip():
-                        continue
-                    ev = json.loads(line)
-                    et, obj = ev.get("type"), ev.get("object") or {}
-                    if et == "ERROR":
-                        err = ApiError.from_status(obj)
-                        if err.code == 410:
-                            raise Gone(err.message)
-                        raise err
-                    yield et, obj
+        target = self.path(info, v, namespace)[len(self.base):] + "?" + urlencode(params)
+        status, _headers, stream = await self._http().stream("GET", target)
+        if status >= 400:
+            raw = await stream.read_all()
+            try:
+                raise ApiError.from_status(json.loads(raw), status)
+            except ValueError:
+                raise InternalError(raw[:200].decode(errors="replace"))
+        try:
+            async for line in stream.lines():
+                if not line.strip():
+                    continue
+                ev = json.loads(line)
+                et, obj = ev.get("type"), ev.get("object") or {}
+                if et == "ERROR":
+                    err = ApiError.from_status(obj)
+                    if err.code == 410:
+                        raise Gone(err.message)
+                    raise err
+                yield et, obj
+        finally:
+            stream.close()

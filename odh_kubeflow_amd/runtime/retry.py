@@ -1,7 +1,10 @@
 """``k8s.io/client-go/util/retry`` analogues.
 
 ``retry_on_conflict`` uses ``retry.DefaultRetry`` (5 steps, 10 ms, factor 1, jitter 0.1),
-as every ``RetryOnConflict`` call site in the reference does.
+as every ``RetryOnConflict`` call site in the reference does — with one change: the first
+retry reads live from the apiserver (see ``client.LIVE_READS``) and runs at once.  A
+conflict almost always means the informer copy was one write behind; the reference pays
+the 10 ms sleep and often a second conflict for it, on the create→Ready path.
 """
 
 from __future__ import annotations
@@ -55,4 +58,23 @@ async def retry_on_error(backoff: Backoff, retriable: Callable[[BaseException], 
 
 
 async def retry_on_conflict(fn: Callable[[], Awaitable[T]], backoff: Backoff = DEFAULT_RETRY) -> T:
-    return await retry_on_error(backoff, is_conflict, fn)
+    from .client import LIVE_READS
+
+    delays = backoff.delays()
+    attempt = 0
+    while True:
+        tok = LIVE_READS.set(attempt > 0)
+        try:
+            return await fn()
+        except Exception as e:
+            if not is_conflict(e):
+                raise
+            try:
+                d = next(delays)
+            except StopIteration:
+                raise e
+            if attempt > 0:
+                await asyncio.sleep(d)
+            attempt += 1
+        finally:
+            LIVE_READS.reset(tok)

@@ -329,10 +329,11 @@ def test_dspa_secret_created_and_mounted(run):
             assert md["public_api_endpoint"] == "https://apps.example.com/external/elyra/user"
             assert m.labels(s) == {"opendatahub.io/managed-by": "workbenches"}
             assert s["metadata"]["ownerReferences"][0]["kind"] == "DataSciencePipelinesApplication"
-            nb = cl.store.peek(kinds.NOTEBOOK, "nb", "user")
-            spec = nb["spec"]["template"]["spec"]
-            assert {"name": "elyra-dsp-details", "secret": {"secretName": "ds-pipeline-config", "optional": True}} \
-                in spec["volumes"]
+            vol = {"name": "elyra-dsp-details", "secret": {"secretName": "ds-pipeline-config", "optional": True}}
+            spec = lambda: cl.store.peek(kinds.NOTEBOOK, "nb", "user")["spec"]["template"]["spec"]  # noqa: E731
+            # the Secret and the Notebook arrive on different watches: no cross-kind ordering
+            assert await cl.wait_for(lambda: vol in spec().get("volumes", []))
+            spec = spec()
             assert {"name": "elyra-dsp-details", "mountPath": "/opt/app-root/runtimes"} in \
                 spec["containers"][0]["volumeMounts"]
     run(go())

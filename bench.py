@@ -50,6 +50,9 @@ def parse(argv=None):
                    help="reproduce the reference's serialising behaviour (1 worker, blocking lock removal)")
     p.add_argument("--transport", choices=("inprocess", "http", "native"), default="inprocess",
                    help="managers share the store (inprocess) or talk REST/watch to the apiserver (http)")
+    p.add_argument("--arch", choices=("auto", "inprocess", "sharded"), default="auto",
+                   help="inprocess: one process, controllers share the store; sharded: namespace-sharded control "
+                        "plane, one rank per GPU, native apiserver (auto: sharded when WORLD_SIZE > 1)")
     p.add_argument("--json-out", default=None)
     return p.parse_args(argv)
 
@@ -142,9 +145,16 @@ def main(argv=None):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     n = args.gpus
-    if world > 1:
+    if args.arch == "sharded" or (args.arch == "auto" and world > 1):
         from odh_kubeflow_amd.parallel.bench_dist import run_distributed
 
+        if "MASTER_ADDR" not in os.environ:  # single rank without a launcher
+            import socket
+
+            with socket.socket() as s:
+                s.bind(("127.0.0.1", 0))
+                os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(s.getsockname()[1]),
+                                  RANK="0", WORLD_SIZE="1", LOCAL_RANK="0")
         return run_distributed(args)
     import torch
 

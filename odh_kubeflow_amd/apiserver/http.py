@@ -34,6 +34,7 @@ from ..models import meta as m
 from ..models.errors import ApiError, BadRequest, Forbidden, InternalError, NotFound
 from ..models.scheme import SCHEME, ResourceInfo
 from ..utils import jsonpatch
+from ..utils.selectors import match_labels, selector_from_dict
 from .store import ObjectStore
 
 log = logging.getLogger("apiserver.http")
@@ -152,9 +153,28 @@ class WebhookDispatcher:
         if cc.get("caBundle"):
             ctx = ssl.create_default_context(cadata=base64.b64decode(cc["caBundle"]).decode())
         name = wh.get("name", "")
+        ns_sel = selector_from_dict(wh.get("namespaceSelector")) if wh.get("namespaceSelector") else None
+        obj_sel = selector_from_dict(wh.get("objectSelector")) if wh.get("objectSelector") else None
+
+        def selected(info: ResourceInfo, obj: dict, old: Optional[dict]) -> bool:
+            if obj_sel is not None and not match_labels(obj_sel, m.labels(obj)) and not (
+                    old is not None and match_labels(obj_sel, m.labels(old))):
+                return False
+            if ns_sel is None:
+                return True
+            if info.kind == "Namespace" and not info.group:
+                return match_labels(ns_sel, m.labels(obj))
+            if not info.namespaced:
+                return True
+            ns = self.store.peek("v1/Namespace", m.namespace(obj))
+            labels = m.labels(ns) if ns is not None else {"kubernetes.io/metadata.name": m.namespace(obj)}
+            return match_labels(ns_sel, labels)
 
         async def handler(op, info, obj, old):
             import aiohttp
+
+            if not selected(info, obj, old):
+                return obj
 
             if self._session is None or self._session.closed:
                 self._session = aiohttp.ClientSession()

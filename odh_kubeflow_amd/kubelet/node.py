@@ -26,6 +26,8 @@ from ..models import kinds
 from ..models import meta as m
 from ..models.errors import ApiError, is_conflict, is_not_found
 from ..models.notebook import GPU_IDS_ANNOTATION, GPU_RESOURCE, gpu_request
+
+GPU_INDEX_LABEL = "amd.com/gpu-index"
 from ..runtime.controller import Request, Result, pred_funcs
 from ..utils.quantity import parse_quantity
 from ..utils.timeutil import rfc3339
@@ -160,8 +162,12 @@ class SchedulerController:
                 reasons.append("Insufficient memory")
                 continue
             ids = free[: need["gpu"]]
-            patch = {"spec": {"nodeName": m.name(node)},
-                     "metadata": {"annotations": {GPU_IDS_ANNOTATION: ",".join(map(str, ids))}} if ids else {}}
+            patch = {"spec": {"nodeName": m.name(node)}}
+            if ids:
+                # the allocation (device-plugin style) plus a selectable label naming the
+                # first GPU, so a per-GPU node agent can watch just its own pods
+                patch["metadata"] = {"annotations": {GPU_IDS_ANNOTATION: ",".join(map(str, ids))},
+                                     "labels": {GPU_INDEX_LABEL: str(ids[0])}}
             try:
                 await self.client.patch(kinds.POD, patch, name=m.name(pod), namespace=m.namespace(pod))
             except ApiError as e:

@@ -688,7 +688,28 @@ struct Webhook {
   bool fail_closed = true, has_url = false;
   double timeout_s = 10;
   Value rules;
+  bool has_ns_sel = false, has_obj_sel = false;
+  std::vector<LReq> ns_sel, obj_sel;
 };
+
+// metav1.LabelSelector (matchLabels + matchExpressions) -> requirements
+std::vector<LReq> selector_reqs(const Value& sel) {
+  std::vector<LReq> out;
+  if (const Value* ml = sel.get("matchLabels"))
+    if (ml->is_obj())
+      for (auto& kv : ml->obj) out.push_back({kv.k, "=", {kv.v.s}});
+  if (const Value* me = sel.get("matchExpressions"))
+    if (me->is_arr())
+      for (auto& e : me->arr) {
+        std::string op = e.str_or("operator");
+        LReq r{e.str_or("key"), op == "In" ? "in" : op == "NotIn" ? "notin" : op == "Exists" ? "exists" : "!", {}};
+        if (const Value* vs = e.get("values"))
+          if (vs->is_arr())
+            for (auto& v : vs->arr) r.vals.push_back(v.s);
+        out.push_back(r);
+      }
+  return out;
+}
 
 bool rule_match(const Value& rules, const Res& r, const std::string& op) {
   if (!rules.is_arr()) return false;
@@ -750,6 +771,16 @@ std::vector<Webhook> webhooks_for(const Res& r, const std::string& op) {
       w.fail_closed = wh.str_or("failurePolicy", "Fail") == "Fail";
       const Value* ts = wh.get("timeoutSeconds");
       if (ts && ts->t == T::Int) w.timeout_s = (double)ts->i;
+      if (const Value* ns = wh.get("namespaceSelector"))
+        if (ns->is_obj() && !ns->obj.empty()) {
+          w.has_ns_sel = true;
+          w.ns_sel = selector_reqs(*ns);
+        }
+      if (const Value* os = wh.get("objectSelector"))
+        if (os->is_obj() && !os->obj.empty()) {
+          w.has_obj_sel = true;
+          w.obj_sel = selector_reqs(*os);
+        }
       const Value* cc = wh.get("clientConfig");
       if (cc) {
         std::string ca = cc->str_or("caBundle");
@@ -997,9 +1028,33 @@ Value call_webhook(const Webhook& w, const Value& review) {
   throw std::runtime_error("webhook request failed");
 }
 
+// namespaceSelector / objectSelector of a webhook against the object being admitted
+bool selectors_match(const Webhook& w, const Res& r, const Value& obj, const Value* old) {
+  if (w.has_obj_sel && !match_labels(w.obj_sel, obj) && !(old && match_labels(w.obj_sel, *old))) return false;
+  if (!w.has_ns_sel) return true;
+  if (r.kind == "Namespace" && r.group.empty()) return match_labels(w.ns_sel, obj);
+  if (!r.namespaced) return true;  // cluster-scoped objects are not subject to namespaceSelector
+  Res* nsr = by_kind("", "Namespace");
+  Obj ns;
+  if (nsr) {
+    std::lock_guard<std::mutex> g(S.mu);
+    auto it = bucket(*nsr).objs.find({"", mget(obj, "namespace")});
+    if (it != bucket(*nsr).objs.end()) ns = it->second;
+  }
+  if (ns) return match_labels(w.ns_sel, *ns);
+  Value stub = Value::object();  // unknown namespace: only the implicit name label
+  Value m = Value::object();
+  Value l = Value::object();
+  l["kubernetes.io/metadata.name"] = Value::str(mget(obj, "namespace"));
+  m["labels"] = l;
+  stub["metadata"] = m;
+  return match_labels(w.ns_sel, stub);
+}
+
 Value admit(const char* op, const Res& r, Value obj, const Value* old) {
   auto hooks = webhooks_for(r, op);
   for (auto& w : hooks) {
+    if (!selectors_match(w, r, obj, old)) continue;
     Value review = Value::object();
     review["apiVersion"] = Value::str("admission.k8s.io/v1");
     review["kind"] = Value::str("AdmissionReview");

@@ -1,21 +1,22 @@
 """Multi-GPU benchmark driver: one process per MI355X (``torch.distributed.run``).
 
-Layout on an 8×MI355X node (what a real deployment looks like):
+Layout on an 8×MI355X node (see :mod:`.shard` for the design):
 
-* **rank 0** — the control plane: apiserver (store + REST/watch front end), the
-  kube-controller-manager stand-ins (StatefulSet controller, scheduler with
-  ``amd.com/gpu`` allocation, GC), the kf + odh managers and the admission webhook, plus
-  the node agent of GPU 0;
-* **rank r > 0** — the node agent of GPU r (``LOCAL_RANK``): a REST/watch client of
-  rank 0's apiserver that starts the pods allocated to its GPU and gates their
-  readiness on the MI355X start-up probe running on *its own* device.
+* **rank 0** starts the native C++ apiserver (``odh-apiserver``: store, REST/watch,
+  admission, GC) as a child process and broadcasts its URL;
+* **every rank r** runs a namespace shard of the control plane against it — kf + odh
+  reconcilers, the odh webhook server, the StatefulSet controller and the node agent
+  of GPU ``LOCAL_RANK`` — owning the notebooks of namespace ``bench-r``; rank 0's shard
+  also hosts the scheduler and registers the Node;
+* each rank drives its own notebooks: one step = create one ``amd.com/gpu: 1`` Notebook
+  in its namespace → Ready (pod started by whichever GPU's node agent the scheduler
+  allocated, after the MI355X start-up probe on that GPU) → delete → gone.
 
-Coordination goes through ``torch.distributed`` (the gloo group carries the apiserver
-URL and the barriers; when GPUs are present an RCCL all-reduce over xGMI checks the
-collective path once at start-up).  Barriers run in an executor thread so every
-process keeps serving its event loop while it waits.  The timed region is bracketed
-by barrier + ``torch.cuda.synchronize()`` on every rank and the elapsed time is the
-max over ranks.
+Coordination goes through ``torch.distributed`` (gloo carries the URL, the barriers and
+the result gathers; when GPUs are present an RCCL all-reduce over xGMI checks the
+collective path once at start-up).  Barriers run in an executor thread so every process
+keeps serving its event loop while it waits.  The timed region is bracketed by barrier +
+``torch.cuda.synchronize()`` on every rank and the elapsed time is the max over ranks.
 """
 
 from __future__ import annotations
@@ -26,7 +27,9 @@ import os
 import time
 from typing import Optional
 
-BENCH_NS = "bench"
+
+def bench_namespace(rank: int) -> str:
+    return f"bench-{rank}"
 
 
 def _dist_init():
@@ -44,8 +47,8 @@ async def _in_thread(fn, *a):
 
 def _rccl_check(torch, dist, local_rank: int) -> Optional[float]:
     """One all-reduce over RCCL (xGMI) as a health check of the multi-GPU notebook path."""
-    if torch.cuda.device_count() == 0:
-        return None
+    if torch.cuda.device_count() < dist.get_world_size():
+        return None  # ranks share a GPU (rehearsal on a smaller box): RCCL needs one rank per device
     try:
         import datetime
 
@@ -66,7 +69,6 @@ def run_distributed(args) -> int:
     dist, torch = _dist_init()
     rank, world = dist.get_rank(), dist.get_world_size()
     local_rank = int(os.environ.get("LOCAL_RANK", rank))
-    n = world
     probe = None
     if not args.no_gpu_probe:
         if torch.cuda.device_count() == 0:
@@ -80,12 +82,14 @@ def run_distributed(args) -> int:
         async def probe(devices):
             return await gpu.startup_probe(devices, local_index=lambda d: dev)
     rccl_ms = _rccl_check(torch, dist, local_rank) if not args.no_gpu_probe else None
-    res = asyncio.run(_main(args, dist, torch, rank, world, n, probe))
+    res = asyncio.run(_main(args, dist, torch, rank, world, local_rank, probe))
     if rank == 0:
         from bench import report  # noqa: E402  (bench.py is the entry point on sys.path)
 
-        out = report(args, n, res)
-        out["config"]["parallelism"] = f"node agent per GPU rank x{n}; control plane on rank 0; torch.distributed gloo"
+        out = report(args, world, res)
+        out["config"]["parallelism"] = (f"namespace-sharded control plane x{world} (one rank per MI355X: kf+odh "
+                                        f"reconcilers, webhook, STS controller, node agent); native C++ apiserver")
+        out["config"]["architecture"] = "sharded"
         if rccl_ms is not None:
             out["rccl_allreduce_check_ms"] = round(rccl_ms, 3)
         print(json.dumps(out), flush=True)
@@ -97,104 +101,68 @@ def run_distributed(args) -> int:
     return 0
 
 
-async def _main(args, dist, torch, rank: int, world: int, n: int, probe) -> dict:
-    from ..kubelet.agent import NodeAgent
-    from ..runtime.manager import Manager
-    from ..runtime.rest import RestConfig
+async def _main(args, dist, torch, rank: int, world: int, local_rank: int, probe) -> dict:
+    from .shard import ControlPlaneShard, ShardConfig
 
-    node = "mi355x-node-0"
-    cl = None
+    native = None
     url = [None]
     if rank == 0:
-        from ..cluster import ClusterConfig, LocalCluster
+        from ..apiserver.native import NativeApiServer
+        from ..cluster import OPENSHIFT_CRDS
 
-        use_odh = not args.no_odh
-        cfg = ClusterConfig(gpus_per_node=8, odh=use_odh, webhook=use_odh, startup_probe=probe,
-                            reference_emulation=args.reference_emulation, gpu_runtimes_in_process=False,
-                            env={"SET_PIPELINE_RBAC": "false", "SET_PIPELINE_SECRET": "false"})
-        cl = LocalCluster(cfg)
-        await cl.start()
-        from ..apiserver.http import ApiServer
-
-        cl.apiserver = await ApiServer(cl.store).start("127.0.0.1", 0)
-        url[0] = cl.apiserver.url
-        await cl.ensure_namespace(BENCH_NS)
+        native = await NativeApiServer(OPENSHIFT_CRDS, gc=True).start()
+        url[0] = native.url
     await _in_thread(dist.broadcast_object_list, url, 0)
-    # every rank runs the node agent of its own GPU
+    use_odh = not args.no_odh
+    env = {"SET_PIPELINE_RBAC": "false", "SET_PIPELINE_SECRET": "false"}
+    shard = ControlPlaneShard(ShardConfig(
+        apiserver_url=url[0], namespace=bench_namespace(rank), gpu=local_rank % 8, bootstrap=(rank == 0),
+        odh=use_odh, webhook=use_odh, startup_probe=probe, reference_emulation=args.reference_emulation, env=env))
     if rank == 0:
-        mgr = Manager.in_process(cl.store, name=f"kubelet-gpu{rank}")
+        await shard.start()  # namespaces, Node, scheduler first
+        await _in_thread(dist.barrier)
     else:
-        mgr = Manager.remote(RestConfig(host=url[0]), name=f"kubelet-gpu{rank}")
-    agent = NodeAgent(mgr, node, [rank], node_gpus=8, startup_probe=probe, register_node=(rank == 0),
-                      owns_cpu_pods=(rank == 0))
-    await mgr.start()
-    await _in_thread(dist.barrier)
+        await _in_thread(dist.barrier)
+        await shard.start()
+    await _in_thread(dist.barrier)  # every shard's webhook is registered before anyone creates
 
-    result = {}
-    if rank == 0:
-        result = await _drive(args, cl, n, agent)
-    else:
-        # serve until rank 0 has finished the timed region; the barriers mirror rank 0's
-        await _in_thread(dist.barrier)  # before timed region
-        t0 = time.perf_counter()
-        await _in_thread(dist.barrier)  # after timed region
-        result = {"elapsed": time.perf_counter() - t0}
-    elapsed = torch.tensor([result.get("elapsed", 0.0)], dtype=torch.float64)
-    await _in_thread(lambda: dist.all_reduce(elapsed, op=dist.ReduceOp.MAX))
-    result["elapsed"] = float(elapsed.item())
-    await _in_thread(dist.barrier)  # nobody tears down while others still serve
-    await mgr.stop()
-    if cl is not None:
-        await cl.apiserver.stop()
-        await cl.stop()
+    try:
+        result = await _drive(args, shard, dist, torch)
+    finally:
+        await _in_thread(dist.barrier)  # nobody tears down while others still serve
+        await shard.stop()
+        if native is not None:
+            await native.stop()
     return result
 
 
-async def _drive(args, cl, n: int, agent) -> dict:
-    import torch
-    import torch.distributed as dist
-
+async def _drive(args, shard, dist, torch) -> dict:
     from ..models import kinds
     from ..models.notebook import notebook
 
     use_odh = not args.no_odh
+    ns = shard.cfg.namespace
     lat_ms = []
     state = {"recon": 0, "step": 0}
 
     async def one_step(timed: bool):
         state["step"] += 1
-        names = [f"nb-s{state['step']}-g{i}" for i in range(n)]
+        nm = f"nb-s{state['step']}"
         ann = {"notebooks.opendatahub.io/inject-auth": "true"} if use_odh else None
-        r0 = cl.reconcile_count()
-        t0, ready_at = {}, {}
-
-        async def create(nm):
-            t0[nm] = time.perf_counter()
-            await cl.admin.create(notebook(nm, BENCH_NS, image="rocm/pytorch:rocm7.0_ubuntu22.04_py3.10_pytorch_2.10",
-                                           gpus=1, annotations=ann))
-
-        await asyncio.gather(*(create(nm) for nm in names))
-        pending = set(names)
-        deadline = time.monotonic() + 120
-        while pending and time.monotonic() < deadline:
-            for nm in list(pending):
-                if cl.notebook_ready(nm, BENCH_NS):
-                    ready_at[nm] = time.perf_counter()
-                    pending.discard(nm)
-            if pending:
-                await asyncio.sleep(0.0005)
-        if pending:
-            raise RuntimeError(f"notebooks not Ready: {sorted(pending)}")
-        await asyncio.gather(*(cl.admin.delete(kinds.NOTEBOOK, nm, BENCH_NS) for nm in names))
-        ok = await cl.wait_for(lambda: all(cl.store.peek(kinds.NOTEBOOK, nm, BENCH_NS) is None and
-                                           cl.store.peek(kinds.POD, f"{nm}-0", BENCH_NS) is None
-                                           for nm in names), 60, 0.0005)
-        if not ok:
-            raise RuntimeError("teardown did not finish")
-        await cl.settle(5)
+        r0 = shard.reconcile_count()
+        t0 = time.perf_counter()
+        await shard.admin.create(notebook(nm, ns, image="rocm/pytorch:rocm7.0_ubuntu22.04_py3.10_pytorch_2.10",
+                                          gpus=1, annotations=ann))
+        if not await shard.wait_for(lambda: shard.notebook_ready(nm), 120):
+            raise RuntimeError(f"notebook {ns}/{nm} not Ready")
+        ready = time.perf_counter()
+        await shard.admin.delete(kinds.NOTEBOOK, nm, ns)
+        if not await shard.wait_for(lambda: shard.gone(nm), 60):
+            raise RuntimeError(f"teardown of {ns}/{nm} did not finish")
+        await shard.settle(5)
         if timed:
-            state["recon"] += cl.reconcile_count() - r0
-            lat_ms.extend((ready_at[nm] - t0[nm]) * 1e3 for nm in names)
+            state["recon"] += shard.reconcile_count() - r0
+            lat_ms.append((ready - t0) * 1e3)
 
     for _ in range(args.warmup):
         await one_step(False)
@@ -208,5 +176,13 @@ async def _drive(args, cl, n: int, agent) -> dict:
         torch.cuda.synchronize()
     await _in_thread(dist.barrier)
     elapsed = time.perf_counter() - t_start
-    return {"elapsed": elapsed, "reconciles": state["recon"], "lat_ms": lat_ms, "odh": use_odh,
-            "probes": agent.probe_results}
+
+    el = torch.tensor([elapsed], dtype=torch.float64)
+    rc = torch.tensor([state["recon"]], dtype=torch.float64)
+    await _in_thread(lambda: dist.all_reduce(el, op=dist.ReduceOp.MAX))
+    await _in_thread(lambda: dist.all_reduce(rc, op=dist.ReduceOp.SUM))
+    gathered = [None] * dist.get_world_size()
+    await _in_thread(dist.all_gather_object, gathered, {"lat": lat_ms, "probes": shard.probe_results})
+    return {"elapsed": float(el.item()), "reconciles": int(rc.item()),
+            "lat_ms": [x for g in gathered for x in g["lat"]], "odh": use_odh,
+            "probes": [p for g in gathered for p in g["probes"]]}

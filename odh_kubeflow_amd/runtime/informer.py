@@ -44,10 +44,14 @@ def strip_data(obj: dict) -> dict:
 
 
 class _Informer:
-    def __init__(self, cache: "InformerCache", info: ResourceInfo, version: str):
+    def __init__(self, cache: "InformerCache", info: ResourceInfo, version: str,
+                 namespace: Optional[str] = None, label_selector: Optional[str] = None):
         self.cache = cache
         self.info = info
         self.version = version
+        self.namespace = namespace
+        self.label_selector = label_selector
+        self._label_reqs = parse_label_selector(label_selector) if label_selector else None
         self.items: Dict[Tuple[str, str], dict] = {}
         self.by_ns: Dict[str, Set[Tuple[str, str]]] = {}
         self.by_owner: Dict[str, Set[Tuple[str, str]]] = {}
@@ -112,7 +116,7 @@ class _Informer:
 
     async def _relist(self) -> None:
         items, rv = await self.cache.rest.list_rv(f"{self.info.api_version(self.version)}/{self.info.kind}",
-                                                  self.cache.namespace)
+                                                  self.namespace, self.label_selector)
         self.relists += 1
         seen = set()
         for o in items:
@@ -141,7 +145,7 @@ class _Informer:
                 if need_list:
                     await self._relist()
                     need_list = False
-                async for et, obj in self.cache.rest.watch(ref, self.cache.namespace, self.rv,
+                async for et, obj in self.cache.rest.watch(ref, self.namespace, self.rv, labels=self.label_selector,
                                                            timeout_s=self.cache.watch_timeout_s):
                     backoff = 0.05
                     if et == "BOOKMARK":
@@ -149,6 +153,12 @@ class _Informer:
                         continue
                     obj = self._transform(obj)
                     self.rv = m.resource_version(obj) or self.rv
+                    if et != "DELETED" and self._label_reqs is not None and not match_labels(
+                            self._label_reqs, (obj.get("metadata") or {}).get("labels")):
+                        # the object left the selector: to this cache it is gone
+                        if (m.namespace(obj), m.name(obj)) not in self.items:
+                            continue
+                        et = "DELETED"
                     if et == "DELETED":
                         old = self._delete(obj)
                         self._notify("DELETED", obj, old)
@@ -176,71 +186,104 @@ class _Informer:
 
 
 class InformerCache(Reader, EventSource):
+    """Shared informers keyed by kind (and namespace, for a namespace-restricted cache).
+
+    ``namespace`` restricts namespaced kinds to one namespace; ``namespaces`` to a set of
+    them (one list/watch per namespace, merged for readers — controller-runtime's
+    ``cache.Options.DefaultNamespaces``).  ``selectors`` maps a kind to a label selector
+    applied server-side to its list/watch (``cache.Options.ByObject[..].Label``) so a
+    shard only ever receives the objects it owns.
+    """
+
     def __init__(self, rest, namespace: Optional[str] = None, transforms: Optional[Dict[str, Optional[Transform]]] = None,
-                 watch_timeout_s: int = 300):
+                 watch_timeout_s: int = 300, namespaces: Optional[Iterable[str]] = None,
+                 selectors: Optional[Dict[str, str]] = None):
         self.rest = rest
         self.namespace = namespace
+        nss = list(namespaces) if namespaces is not None else ([namespace] if namespace else None)
+        self.namespaces: Optional[List[str]] = nss
         self.transforms: Dict[str, Optional[Transform]] = {}
         for k, fn in (transforms or {}).items():
             self.transforms[SCHEME.resolve(k).key] = fn
+        self.selectors: Dict[str, str] = {SCHEME.resolve(k).key: v for k, v in (selectors or {}).items()}
         self.watch_timeout_s = watch_timeout_s
-        self._informers: Dict[str, _Informer] = {}
+        self._informers: Dict[Tuple[str, Optional[str]], _Informer] = {}
+        self._by_kind: Dict[str, List[_Informer]] = {}
         self._hid = 0
 
-    def informer(self, kind) -> _Informer:
+    def _group(self, kind) -> List[_Informer]:
         info = SCHEME.resolve(kind)
-        inf = self._informers.get(info.key)
-        if inf is None:
+        infs = self._by_kind.get(info.key)
+        if infs is None:
             from .client import _version_of
 
-            inf = self._informers[info.key] = _Informer(self, info, _version_of(kind) or info.storage_version)
-            inf.task = asyncio.ensure_future(inf.run())
-        return inf
+            version = _version_of(kind) or info.storage_version
+            nss = self.namespaces if (info.namespaced and self.namespaces) else [None]
+            infs = []
+            for ns in nss:
+                inf = _Informer(self, info, version, ns, self.selectors.get(info.key))
+                self._informers[(info.key, ns)] = inf
+                inf.task = asyncio.ensure_future(inf.run())
+                infs.append(inf)
+            self._by_kind[info.key] = infs
+        return infs
+
+    def _for_ns(self, kind, namespace: Optional[str]) -> List[_Informer]:
+        infs = self._group(kind)
+        if namespace and len(infs) > 1:
+            return [i for i in infs if i.namespace == namespace]
+        return infs
+
+    def informer(self, kind) -> _Informer:
+        """The (first) informer of ``kind`` — for single-namespace / cluster-wide caches."""
+        return self._group(kind)[0]
 
     async def ensure_informer(self, kind, timeout: float = 30.0) -> None:
-        inf = self.informer(kind)
-        if not inf.synced.is_set():
-            await asyncio.wait_for(inf.synced.wait(), timeout)
-        if inf.missing_kind:
+        infs = self._group(kind)
+        for inf in infs:
+            if not inf.synced.is_set():
+                await asyncio.wait_for(inf.synced.wait(), timeout)
+        if all(inf.missing_kind for inf in infs):
             from ..models.errors import NoKindMatch
 
-            raise NoKindMatch(inf.info.kind)
+            raise NoKindMatch(infs[0].info.kind)
 
     # -------------------------------------------------------------- EventSource
 
     def subscribe(self, kind, callback, namespace=None):
-        inf = self.informer(kind)
+        infs = self._for_ns(kind, namespace)
         self._hid += 1
         hid = self._hid
-        for o in list(inf.items.values()):
-            if namespace and m.namespace(o) != namespace:
-                continue
-            callback("ADDED", o, None)
-        inf.handlers[hid] = (namespace, callback)
-        return lambda: inf.handlers.pop(hid, None)
+        for inf in infs:
+            for o in list(inf.items.values()):
+                if namespace and m.namespace(o) != namespace:
+                    continue
+                callback("ADDED", o, None)
+            inf.handlers[hid] = (namespace, callback)
+
+        def cancel():
+            for inf in infs:
+                inf.handlers.pop(hid, None)
+        return cancel
 
     async def wait_synced(self, kinds: Iterable, timeout: float = 30.0) -> None:
-        async def one(k):
-            inf = self.informer(k)
+        async def one(inf):
             if not inf.synced.is_set():
                 await asyncio.wait_for(inf.synced.wait(), timeout)
 
-        await asyncio.gather(*(one(k) for k in kinds))
+        await asyncio.gather(*(one(inf) for k in kinds for inf in self._group(k)))
 
     # -------------------------------------------------------------- Reader
 
     def get(self, kind, name, namespace=None):
-        inf = self.informer(kind)
+        infs = self._for_ns(kind, namespace)
+        if len(infs) != 1 or (infs[0].namespace and namespace and infs[0].namespace != namespace):
+            return None  # namespace outside this cache
+        inf = infs[0]
         return inf.items.get((namespace or "" if inf.info.namespaced else "", name))
 
     def list(self, kind, namespace=None, labels=None, fields=None, owner_uid=None) -> List[dict]:
-        inf = self.informer(kind)
-        if owner_uid is not None:
-            keys = inf.by_owner.get(owner_uid, ())
-        elif namespace and inf.info.namespaced:
-            keys = inf.by_ns.get(namespace, ())
-        else:
-            keys = inf.items.keys()
+        infs = self._for_ns(kind, namespace)
         if isinstance(labels, dict):
             reqs = selector_from_dict({"matchLabels": labels})
         elif isinstance(labels, str):
@@ -249,17 +292,24 @@ class InformerCache(Reader, EventSource):
             reqs = labels or []
         fm = field_matcher(parse_field_selector(fields)) if fields else None
         out = []
-        for k in list(keys):
-            o = inf.items.get(k)
-            if o is None:
-                continue
-            if namespace and inf.info.namespaced and m.namespace(o) != namespace:
-                continue
-            if reqs and not match_labels(reqs, (o.get("metadata") or {}).get("labels")):
-                continue
-            if fm is not None and not fm(o):
-                continue
-            out.append(o)
+        for inf in infs:
+            if owner_uid is not None:
+                keys = inf.by_owner.get(owner_uid, ())
+            elif namespace and inf.info.namespaced:
+                keys = inf.by_ns.get(namespace, ())
+            else:
+                keys = inf.items.keys()
+            for k in list(keys):
+                o = inf.items.get(k)
+                if o is None:
+                    continue
+                if namespace and inf.info.namespaced and m.namespace(o) != namespace:
+                    continue
+                if reqs and not match_labels(reqs, (o.get("metadata") or {}).get("labels")):
+                    continue
+                if fm is not None and not fm(o):
+                    continue
+                out.append(o)
         out.sort(key=lambda o: (m.namespace(o), m.name(o)))
         return out
 
@@ -274,3 +324,4 @@ class InformerCache(Reader, EventSource):
                 except (asyncio.CancelledError, Exception):
                     pass
         self._informers.clear()
+        self._by_kind.clear()

@@ -74,8 +74,15 @@ class WebhookServer:
 
 
 def mutating_webhook_configuration(ca_bundle_b64: str, url: Optional[str] = None, service_namespace: str = "opendatahub",
-                                   service_name: str = "odh-notebook-controller-webhook-service") -> dict:
-    """The object of ``odh/config/webhook/manifests.yaml`` (+ caBundle)."""
+                                   service_name: str = "odh-notebook-controller-webhook-service",
+                                   name: str = "mutating-webhook-configuration",
+                                   namespace_selector: Optional[dict] = None) -> dict:
+    """The object of ``odh/config/webhook/manifests.yaml`` (+ caBundle).
+
+    ``name`` / ``namespace_selector`` give one configuration per namespace shard: a
+    sharded control plane routes each shard's admission calls to that shard's own
+    webhook server instead of load-balancing them across all of them.
+    """
     cc = {"caBundle": ca_bundle_b64}
     if url:
         cc["url"] = url
@@ -83,11 +90,12 @@ def mutating_webhook_configuration(ca_bundle_b64: str, url: Optional[str] = None
         cc["service"] = {"name": service_name, "namespace": service_namespace, "path": WEBHOOK_PATH, "port": 443}
     return {
         "apiVersion": "admissionregistration.k8s.io/v1", "kind": "MutatingWebhookConfiguration",
-        "metadata": {"name": "mutating-webhook-configuration"},
+        "metadata": {"name": name},
         "webhooks": [{
             "name": "notebooks.opendatahub.io", "admissionReviewVersions": ["v1"], "clientConfig": cc,
             "failurePolicy": "Fail", "sideEffects": "None",
             "rules": [{"apiGroups": ["kubeflow.org"], "apiVersions": ["v1"], "operations": ["CREATE", "UPDATE"],
                        "resources": ["notebooks"]}],
+            **({"namespaceSelector": namespace_selector} if namespace_selector else {}),
         }],
     }

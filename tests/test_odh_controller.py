@@ -330,7 +330,8 @@ def test_dspa_secret_created_and_mounted(run):
             assert m.labels(s) == {"opendatahub.io/managed-by": "workbenches"}
             assert s["metadata"]["ownerReferences"][0]["kind"] == "DataSciencePipelinesApplication"
             vol = {"name": "elyra-dsp-details", "secret": {"secretName": "ds-pipeline-config", "optional": True}}
-            spec = lambda: cl.store.peek(kinds.NOTEBOOK, "nb", "user")["spec"]["template"]["spec"]  # noqa: E731
+            spec = lambda: ((cl.store.peek(kinds.NOTEBOOK, "nb", "user") or {}).get("spec", {})  # noqa: E731
+                            .get("template", {}).get("spec", {}))
             # the Secret and the Notebook arrive on different watches: no cross-kind ordering
             assert await cl.wait_for(lambda: vol in spec().get("volumes", []))
             spec = spec()

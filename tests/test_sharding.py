@@ -1,0 +1,238 @@
+"""Namespace-sharded control plane and the apiserver features it relies on.
+
+* multi-namespace + label-selected informer caches (controller-runtime
+  ``cache.Options{DefaultNamespaces, ByObject.Label}``);
+* ``namespaceSelector`` on MutatingWebhookConfiguration (both apiservers);
+* the GC "absent owner" rule (a dependent created after its owner is gone is collected);
+* conflict retries that read through to the apiserver;
+* two shards against one native apiserver, each owning one namespace.
+"""
+
+import asyncio
+
+import pytest
+
+from odh_kubeflow_amd.apiserver.http import ApiServer
+from odh_kubeflow_amd.apiserver.store import ObjectStore
+from odh_kubeflow_amd.models import kinds
+from odh_kubeflow_amd.models import meta as m
+from odh_kubeflow_amd.models.errors import Conflict
+from odh_kubeflow_amd.models.notebook import notebook
+from odh_kubeflow_amd.runtime.client import CachedClient, InProcessClient, StoreReader
+from odh_kubeflow_amd.runtime.informer import InformerCache
+from odh_kubeflow_amd.runtime.rest import RestClient, RestConfig
+from odh_kubeflow_amd.runtime.retry import retry_on_conflict
+
+
+@pytest.fixture(params=["python", "native"])
+def server_kind(request):
+    return request.param
+
+
+async def _server(kind: str, gc: bool = True):
+    if kind == "native":
+        from odh_kubeflow_amd.apiserver.native import NativeApiServer
+
+        srv = await NativeApiServer(gc=gc).start()
+        return srv, RestClient(RestConfig(host=srv.url))
+    srv = await ApiServer(ObjectStore(gc=gc)).start("127.0.0.1", 0)
+    return srv, RestClient(RestConfig(host=srv.url))
+
+
+async def _wait(pred, timeout=10.0):
+    loop = asyncio.get_running_loop()
+    end = loop.time() + timeout
+    while loop.time() < end:
+        if pred():
+            return True
+        await asyncio.sleep(0.005)
+    return pred()
+
+
+def _cm(name, ns, labels=None, owner=None):
+    md = {"name": name, "namespace": ns}
+    if labels:
+        md["labels"] = labels
+    if owner:
+        md["ownerReferences"] = [owner]
+    return {"apiVersion": "v1", "kind": "ConfigMap", "metadata": md, "data": {"k": name}}
+
+
+def test_informer_namespaces_and_label_selector(run, server_kind):
+    async def go():
+        srv, c = await _server(server_kind)
+        try:
+            for ns in ("a", "b", "c"):
+                await c.create({"apiVersion": "v1", "kind": "Namespace", "metadata": {"name": ns}})
+                await c.create(_cm("x", ns))
+            cache = InformerCache(c, namespaces=["a", "b"], selectors={kinds.POD: "gpu=1"})
+            seen = []
+            cache.subscribe(kinds.CONFIG_MAP, lambda et, o, old: seen.append((et, m.namespace(o))))
+            await cache.wait_synced([kinds.CONFIG_MAP, kinds.POD])
+            assert sorted(m.namespace(o) for o in cache.list(kinds.CONFIG_MAP)) == ["a", "b"]
+            assert cache.get(kinds.CONFIG_MAP, "x", "c") is None and cache.get(kinds.CONFIG_MAP, "x", "a")
+            assert [m.namespace(o) for o in cache.list(kinds.CONFIG_MAP, "b")] == ["b"]
+            await c.create(_cm("y", "c"))
+            await c.create(_cm("y", "a"))
+            assert await _wait(lambda: cache.get(kinds.CONFIG_MAP, "y", "a") is not None)
+            assert ("ADDED", "c") not in seen and seen.count(("ADDED", "a")) == 2
+
+            # label-selected pods: enter on label add, leave (DELETED) on label change
+            pod = {"apiVersion": "v1", "kind": "Pod", "metadata": {"name": "p", "namespace": "a"},
+                   "spec": {"containers": [{"name": "c", "image": "i"}]}}
+            await c.create(pod)
+            await asyncio.sleep(0.1)
+            assert cache.get(kinds.POD, "p", "a") is None
+            await c.patch(kinds.POD, {"metadata": {"labels": {"gpu": "1"}}}, name="p", namespace="a")
+            assert await _wait(lambda: cache.get(kinds.POD, "p", "a") is not None)
+            await c.patch(kinds.POD, {"metadata": {"labels": {"gpu": "2"}}}, name="p", namespace="a")
+            assert await _wait(lambda: cache.get(kinds.POD, "p", "a") is None)
+            await cache.stop()
+        finally:
+            await c.close()
+            await srv.stop()
+    run(go())
+
+
+def test_mwc_namespace_selector(run, server_kind):
+    async def go():
+        from odh_kubeflow_amd.runtime.manager import Manager
+        from odh_kubeflow_amd.webhook.certs import generate
+        from odh_kubeflow_amd.webhook.notebook_webhook import NotebookWebhook
+        from odh_kubeflow_amd.webhook.server import WebhookServer, mutating_webhook_configuration
+
+        srv, c = await _server(server_kind)
+        mgr = Manager.remote(RestConfig(host=srv.url), name="wh")
+        wh = NotebookWebhook(mgr.client, "opendatahub", kube_rbac_proxy_image="quay.io/brancz/kube-rbac-proxy:v0.18.1")
+        certs = generate(("127.0.0.1",))
+        ws = await WebhookServer(wh, certs.cert_dir, "127.0.0.1", 0).start()
+        try:
+            for ns in ("opendatahub", "shard-a", "shard-b"):
+                await c.create({"apiVersion": "v1", "kind": "Namespace", "metadata": {"name": ns}})
+            await c.create(mutating_webhook_configuration(
+                certs.ca_bundle_b64, url=f"https://127.0.0.1:{ws.port}/mutate-notebook-v1", name="wh-shard-a",
+                namespace_selector={"matchLabels": {"kubernetes.io/metadata.name": "shard-a"}}))
+            await asyncio.sleep(0.1)  # the python apiserver picks MWCs up from its watch
+            await c.create(notebook("nb", "shard-b"))
+            assert wh.requests == 0
+            await c.create(notebook("nb", "shard-a"))
+            assert wh.requests == 1
+        finally:
+            await ws.stop()
+            await mgr.stop()
+            await c.close()
+            await srv.stop()
+    run(go())
+
+
+def test_gc_collects_dependent_of_absent_owner(run, server_kind):
+    async def go():
+        srv, c = await _server(server_kind)
+        try:
+            await c.create({"apiVersion": "v1", "kind": "Namespace", "metadata": {"name": "g"}})
+            owner = await c.create(_cm("owner", "g"))
+            ref = {"apiVersion": "v1", "kind": "ConfigMap", "name": "owner", "uid": m.uid(owner), "controller": True}
+            await c.delete(kinds.CONFIG_MAP, "owner", "g")
+            await c.create(_cm("late", "g", owner=ref))  # e.g. a controller acting on a stale cache
+            await asyncio.sleep(0.05)
+            assert await c.get_or_none(kinds.CONFIG_MAP, "late", "g") is None
+            # an owner of a kind the server does not serve cannot be verified: kept
+            foreign = {"apiVersion": "example.com/v1", "kind": "Widget", "name": "w", "uid": "nope"}
+            await c.create(_cm("kept", "g", owner=foreign))
+            assert await c.get_or_none(kinds.CONFIG_MAP, "kept", "g") is not None
+        finally:
+            await c.close()
+            await srv.stop()
+    run(go())
+
+
+class _StaleReader(StoreReader):
+    """Returns a frozen (stale) copy of every object."""
+
+    def __init__(self, store):
+        super().__init__(store)
+        self.frozen = {}
+
+    def get(self, kind, name, namespace=None):
+        k = (kind, name, namespace)
+        if k not in self.frozen:
+            self.frozen[k] = super().get(kind, name, namespace)
+        return self.frozen[k]
+
+
+def test_retry_on_conflict_reads_live_without_sleeping(run):
+    async def go():
+        store = ObjectStore()
+        live = InProcessClient(store)
+        await live.create({"apiVersion": "v1", "kind": "Namespace", "metadata": {"name": "r"}})
+        await live.create(_cm("c", "r"))
+        reader = _StaleReader(store)
+        reader.get(kinds.CONFIG_MAP, "c", "r")  # freeze the current version
+        await live.patch(kinds.CONFIG_MAP, {"data": {"k": "moved"}}, name="c", namespace="r")
+        cached = CachedClient(reader, live)
+        attempts = []
+
+        async def fn():
+            cur = await cached.get(kinds.CONFIG_MAP, "c", "r")
+            attempts.append(cur["data"]["k"])
+            cur["data"]["k2"] = "v"
+            await cached.update(cur)
+
+        loop = asyncio.get_running_loop()
+        t0 = loop.time()
+        await retry_on_conflict(fn)
+        assert attempts == ["c", "moved"]  # stale cache, then a live read
+        assert loop.time() - t0 < 0.009  # no backoff sleep before the live retry
+        assert (await live.get(kinds.CONFIG_MAP, "c", "r"))["data"] == {"k": "moved", "k2": "v"}
+
+        async def always():
+            raise Conflict("configmaps", "c")
+
+        with pytest.raises(Conflict):
+            await retry_on_conflict(always)
+    run(go())
+
+
+def test_two_shards_one_native_apiserver(run):
+    async def go():
+        from odh_kubeflow_amd.apiserver.native import NativeApiServer
+        from odh_kubeflow_amd.cluster import OPENSHIFT_CRDS
+        from odh_kubeflow_amd.parallel.shard import ControlPlaneShard, ShardConfig
+
+        native = await NativeApiServer(OPENSHIFT_CRDS, gc=True).start()
+        env = {"SET_PIPELINE_RBAC": "false", "SET_PIPELINE_SECRET": "false"}
+        shards = []
+        try:
+            shards.append(await ControlPlaneShard(ShardConfig(native.url, "bench-0", gpu=0, bootstrap=True,
+                                                              env=env)).start())
+            shards.append(await ControlPlaneShard(ShardConfig(native.url, "bench-1", gpu=1, env=env)).start())
+            ann = {"notebooks.opendatahub.io/inject-auth": "true"}
+            for i, sh in enumerate(shards):
+                for j in range(1):
+                    await sh.admin.create(notebook(f"nb{j}", f"bench-{i}", image="img", gpus=1, annotations=ann))
+            for sh in shards:
+                for j in range(1):
+                    assert await sh.wait_for(lambda: sh.notebook_ready(f"nb{j}"), 30)
+            # isolation: a shard's cache never holds the other shard's objects
+            for i, sh in enumerate(shards):
+                assert {m.namespace(o) for o in sh.cache.list(kinds.NOTEBOOK)} == {f"bench-{i}"}
+                assert {m.namespace(o) for o in sh.cache.list(kinds.POD)} == {f"bench-{i}"}
+                routes = sh.cache.list(kinds.HTTP_ROUTE)
+                assert routes and {m.labels(r)["notebook-namespace"] for r in routes} == {f"bench-{i}"}
+                assert sh.webhook.requests >= 1
+            # the two pods run on distinct GPUs, each started by that GPU's node agent
+            pods = [p for sh in shards for p in sh.cache.list(kinds.POD)]
+            assert sorted(m.annotations(p)["amd.com/gpu-ids"] for p in pods) == ["0", "1"]
+            assert all(m.labels(p)["amd.com/gpu-index"] == m.annotations(p)["amd.com/gpu-ids"] for p in pods)
+            assert [sh.agent.runtimes[0].started for sh in shards] == [1, 1]
+            for i, sh in enumerate(shards):
+                for j in range(1):
+                    await sh.admin.delete(kinds.NOTEBOOK, f"nb{j}", f"bench-{i}")
+            for sh in shards:
+                for j in range(1):
+                    assert await sh.wait_for(lambda: sh.gone(f"nb{j}"), 30)
+        finally:
+            for sh in reversed(shards):
+                await sh.stop()
+            await native.stop()
+    run(go())

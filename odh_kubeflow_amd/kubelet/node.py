@@ -28,6 +28,7 @@ from ..models.errors import ApiError, is_conflict, is_not_found
 from ..models.notebook import GPU_IDS_ANNOTATION, GPU_RESOURCE, gpu_request
 
 GPU_INDEX_LABEL = "amd.com/gpu-index"
+PROBE_CONDITION = "amd.com/GPUProbe"
 from ..runtime.controller import Request, Result, pred_funcs
 from ..utils.quantity import parse_quantity
 from ..utils.timeutil import rfc3339
@@ -258,8 +259,8 @@ class GpuRuntime:
 
     ``devices=None`` makes this runtime also own pods that request no GPU.
     ``startup_probe`` (e.g. :func:`odh_kubeflow_amd.ops.gpu.startup_probe`) must pass before
-    a GPU pod is reported Ready; its result is recorded in the pod annotation
-    ``amd.com/gpu-probe``.
+    a GPU pod is reported Ready; its result is recorded as the pod condition
+    ``amd.com/GPUProbe``.
     """
 
     def __init__(self, client, reader, recorder, node_name: str, devices: Optional[Iterable[int]],
@@ -349,6 +350,16 @@ class GpuRuntime:
             st = {"running": {"startedAt": now}} if ready else {"waiting": {"reason": reason or "ContainerCreating"}}
             statuses.append({"name": c.get("name", ""), "image": c.get("image", ""), "imageID": "",
                              "ready": ready, "restartCount": 0, "started": ready, "state": st})
+        if probe is not None:
+            # a custom pod condition (the readiness-gate mechanism) instead of an annotation:
+            # the kubelet writes status only, so Ready costs one write, not two
+            ok = bool(probe.get("ok"))
+            r0 = (probe.get("results") or [{}])[0]
+            conds.append({"type": PROBE_CONDITION, "status": "True" if ok else "False",
+                          "reason": "MFMAAndHBMVerified" if ok else "GPUProbeFailed",
+                          "message": (f"bf16 MFMA {r0.get('gemm_tflops', 0):.0f} TFLOP/s, "
+                                      f"HBM {r0.get('hbm_gbps', 0):.0f} GB/s") if ok else str(probe.get("error")),
+                          "lastProbeTime": None, "lastTransitionTime": now})
         status = {"phase": "Running" if ready else "Pending", "conditions": conds, "containerStatuses": statuses,
                   "hostIP": self.host_ip, "podIP": handle.ip if handle else self.host_ip, "startTime": now}
         if handle is not None and handle.port:
@@ -356,8 +367,6 @@ class GpuRuntime:
         patch_ann = {}
         if handle is not None and handle.port:
             patch_ann["amd.com/notebook-endpoint"] = f"{handle.ip}:{handle.port}"
-        if probe is not None:
-            patch_ann["amd.com/gpu-probe"] = "ok" if probe.get("ok") else "failed"
         try:
             if patch_ann:
                 await self.client.patch(kinds.POD, {"metadata": {"annotations": patch_ann}},

@@ -178,3 +178,98 @@ class _Stream:
 
     def close(self) -> None:
         self.conn.close()
+
+
+# --------------------------------------------------------------------------- server
+
+_REASONS = {200: "OK", 400: "Bad Request", 404: "Not Found", 405: "Method Not Allowed", 413: "Payload Too Large",
+            500: "Internal Server Error"}
+Handler = "Callable[[str, str, Dict[str, str], bytes], Awaitable[Tuple[int, str, bytes]]]"
+
+
+class Http1Server:
+    """Minimal keep-alive HTTP/1.1 server (optionally TLS) for the admission webhook.
+
+    The apiserver keeps a pooled TLS connection to the webhook and posts one
+    AdmissionReview at a time on it; this server reads ``Content-Length`` bodies, calls
+    ``handler(method, path, headers, body) -> (status, content_type, body)`` and writes
+    the response — no routing tables, middlewares or access logs on the admission path.
+    """
+
+    def __init__(self, handler, host: str = "127.0.0.1", port: int = 0,
+                 ssl_context: Optional[_ssl.SSLContext] = None, max_body: int = 16 << 20):
+        self.handler = handler
+        self.host = host
+        self.port = port
+        self.ssl = ssl_context
+        self.max_body = max_body
+        self._server = None
+        self._conns: set = set()
+
+    async def start(self) -> "Http1Server":
+        self._server = await asyncio.start_server(self._serve, self.host, self.port, ssl=self.ssl, limit=1 << 24)
+        self.port = self._server.sockets[0].getsockname()[1]
+        return self
+
+    async def _serve(self, reader, writer) -> None:
+        task = asyncio.current_task()
+        self._conns.add(task)
+        sock = writer.get_extra_info("socket")
+        if sock is not None:
+            import socket
+
+            try:
+                sock.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
+            except OSError:
+                pass
+        try:
+            while True:
+                try:
+                    raw = await reader.readuntil(b"\r\n\r\n")
+                except (asyncio.IncompleteReadError, ConnectionError, OSError, _ssl.SSLError):
+                    return
+                lines = raw.decode("latin-1").split("\r\n")
+                parts = lines[0].split(" ")
+                if len(parts) < 3:
+                    return
+                method, target = parts[0], parts[1]
+                headers = {}
+                for line in lines[1:]:
+                    if ":" in line:
+                        k, v = line.split(":", 1)
+                        headers[k.strip().lower()] = v.strip()
+                n = int(headers.get("content-length", "0") or 0)
+                if n > self.max_body:
+                    status, ctype, body = 413, "text/plain", b"request body too large"
+                else:
+                    data = await reader.readexactly(n) if n else b""
+                    try:
+                        status, ctype, body = await self.handler(method, target.split("?", 1)[0], headers, data)
+                    except Exception as e:  # the handler's bug must not kill the connection loop
+                        status, ctype, body = 500, "text/plain", repr(e).encode()
+                close = headers.get("connection", "").lower() == "close"
+                head = (f"HTTP/1.1 {status} {_REASONS.get(status, 'OK')}\r\nContent-Type: {ctype}\r\n"
+                        f"Content-Length: {len(body)}\r\n{'Connection: close' + chr(13) + chr(10) if close else ''}\r\n")
+                writer.write(head.encode("latin-1") + body)
+                await writer.drain()
+                if close:
+                    return
+        except (ConnectionError, OSError, asyncio.IncompleteReadError):
+            return
+        finally:
+            self._conns.discard(task)
+            try:
+                writer.close()
+            except Exception:
+                pass
+
+    async def stop(self) -> None:
+        if self._server is not None:
+            self._server.close()
+            for t in list(self._conns):
+                t.cancel()
+            try:
+                await asyncio.wait_for(self._server.wait_closed(), 2.0)
+            except (asyncio.TimeoutError, Exception):
+                pass
+            self._server = None

@@ -15,8 +15,7 @@ import os
 import ssl
 from typing import Optional
 
-from aiohttp import web
-
+from ..runtime.http1 import Http1Server
 from .notebook_webhook import WEBHOOK_PATH, NotebookWebhook
 
 log = logging.getLogger("webhook.server")
@@ -30,7 +29,7 @@ class WebhookServer:
         self.host = host
         self.port = port
         self.path = path
-        self._runner = None
+        self._server = None
         self.served = 0
 
     def ssl_context(self) -> Optional[ssl.SSLContext]:
@@ -41,36 +40,32 @@ class WebhookServer:
         ctx.load_cert_chain(os.path.join(self.cert_dir, "tls.crt"), os.path.join(self.cert_dir, "tls.key"))
         return ctx
 
-    async def _handle(self, req: web.Request) -> web.Response:
+    async def _handle(self, method: str, path: str, headers, data: bytes):
+        if method == "GET" and path in ("/healthz", "/readyz"):
+            return 200, "text/plain", b"ok"
+        if path != self.path:
+            return 404, "text/plain", b"not found"
+        if method != "POST":
+            return 405, "text/plain", b"method not allowed"
         self.served += 1
         try:
-            review = json.loads(await req.read())
+            review = json.loads(data)
         except ValueError as e:
-            return web.json_response({"apiVersion": "admission.k8s.io/v1", "kind": "AdmissionReview",
-                                      "response": {"uid": "", "allowed": False,
-                                                   "status": {"code": 400, "message": str(e)}}})
-        out = await self.webhook.handle(review)
-        return web.Response(body=json.dumps(out, separators=(",", ":")).encode(), content_type="application/json")
+            out = {"apiVersion": "admission.k8s.io/v1", "kind": "AdmissionReview",
+                   "response": {"uid": "", "allowed": False, "status": {"code": 400, "message": str(e)}}}
+        else:
+            out = await self.webhook.handle(review)
+        return 200, "application/json", json.dumps(out, separators=(",", ":")).encode()
 
     async def start(self) -> "WebhookServer":
-        app = web.Application(client_max_size=16 * 1024 * 1024)
-        app.router.add_post(self.path, self._handle)
-
-        async def ok(_r):
-            return web.Response(text="ok")
-
-        app.router.add_get("/healthz", ok)
-        self._runner = web.AppRunner(app, access_log=None)
-        await self._runner.setup()
-        site = web.TCPSite(self._runner, self.host, self.port, ssl_context=self.ssl_context())
-        await site.start()
-        self.port = site._server.sockets[0].getsockname()[1]
+        self._server = await Http1Server(self._handle, self.host, self.port, self.ssl_context()).start()
+        self.port = self._server.port
         return self
 
     async def stop(self) -> None:
-        if self._runner is not None:
-            await self._runner.cleanup()
-            self._runner = None
+        if self._server is not None:
+            await self._server.stop()
+            self._server = None
 
 
 def mutating_webhook_configuration(ca_bundle_b64: str, url: Optional[str] = None, service_namespace: str = "opendatahub",

@@ -83,11 +83,10 @@ async def run_local(args, n_gpus: int, probe) -> dict:
         step_id = 0
 
         async def one_step(timed: bool):
-            nonlocal step_id, recon
+            nonlocal step_id
             step_id += 1
             names = [f"nb-s{step_id}-g{i}" for i in range(n_gpus)]
             ann = {"notebooks.opendatahub.io/inject-auth": "true"} if use_odh else None
-            r0 = cl.reconcile_count()
             t0 = {}
             ready_at = {}
 
@@ -116,17 +115,21 @@ async def run_local(args, n_gpus: int, probe) -> dict:
                 left = [(k, o) for nm in names for k, o in ((kinds.NOTEBOOK, nm), (kinds.POD, f"{nm}-0"))
                         if cl.store.peek(k, o, "bench") is not None]
                 raise RuntimeError(f"teardown did not finish: {[cl.store.peek(k, o, 'bench') for k, o in left]}")
-            await cl.settle(5)
             if timed:
-                recon += cl.reconcile_count() - r0
                 lat_ms.extend((ready_at[nm] - t0[nm]) * 1e3 for nm in names)
 
         for _ in range(args.warmup):
             await one_step(False)
+        await cl.settle(5)
+        r0 = cl.reconcile_count()
         t_start = time.perf_counter()
         for _ in range(args.steps):
             await one_step(True)
+        # trailing reconciles of the last teardown finish inside the timed region; steps
+        # themselves overlap the previous step's trailing work, as under continuous load
+        await cl.settle(5)
         elapsed = time.perf_counter() - t_start
+        recon = cl.reconcile_count() - r0
         probes = [p for g in cl.gpu_runtimes for p in g.probe_results]
     return {"elapsed": elapsed, "reconciles": recon, "lat_ms": lat_ms, "odh": use_odh, "probes": probes}
 

@@ -149,7 +149,6 @@ async def _drive(args, shard, dist, torch) -> dict:
         state["step"] += 1
         nm = f"nb-s{state['step']}"
         ann = {"notebooks.opendatahub.io/inject-auth": "true"} if use_odh else None
-        r0 = shard.reconcile_count()
         t0 = time.perf_counter()
         await shard.admin.create(notebook(nm, ns, image="rocm/pytorch:rocm7.0_ubuntu22.04_py3.10_pytorch_2.10",
                                           gpus=1, annotations=ann))
@@ -159,19 +158,21 @@ async def _drive(args, shard, dist, torch) -> dict:
         await shard.admin.delete(kinds.NOTEBOOK, nm, ns)
         if not await shard.wait_for(lambda: shard.gone(nm), 60):
             raise RuntimeError(f"teardown of {ns}/{nm} did not finish")
-        await shard.settle(5)
         if timed:
-            state["recon"] += shard.reconcile_count() - r0
             lat_ms.append((ready - t0) * 1e3)
 
     for _ in range(args.warmup):
         await one_step(False)
+    await shard.settle(5)
     if torch.cuda.is_available():
         torch.cuda.synchronize()
     await _in_thread(dist.barrier)
+    r0 = shard.reconcile_count()
     t_start = time.perf_counter()
     for _ in range(args.steps):
         await one_step(True)
+    await shard.settle(5)  # the last teardown's trailing reconciles stay inside the timed region
+    state["recon"] = shard.reconcile_count() - r0
     if torch.cuda.is_available():
         torch.cuda.synchronize()
     await _in_thread(dist.barrier)

@@ -153,6 +153,160 @@ __global__ __launch_bounds__(THREADS, 2) void gemm_bf16_kernel(
     }
 }
 
+// ---------------------------------------------------------------------------------------
+// 256×256×64 tile, 512 threads (8 waves as 2(M)×4(N), 128×64 outputs per wave), one
+// workgroup per CU (128 KiB of LDS: 2 buffers × (A+B) × 256 rows × 128 B).  Tiles are
+// staged global→LDS by the LDS-DMA path (global_load_lds_dwordx4: no VGPR round trip, no
+// ds_write pass); the image is lane-linear per wave instruction, so the bank swizzle is
+// applied to the SOURCE address: LDS slot s of row r holds K-chunk s ^ ((r >> 1) & 7),
+// which puts the 16 rows read by one ds_read_b128 lane group on 16 distinct 16-byte slots
+// of the 256-byte bank row.  The next tile's DMA is in flight during this tile's MFMAs.
+// VERIFY=true replaces the C store by an in-register check against the closed-form product
+// of the probe operands (no C round trip through HBM, no second kernel).
+
+constexpr int G_BM = 256;
+constexpr int G_BN = 256;
+constexpr int G_BK = 64;
+constexpr int G_CH = G_BK / 8;  // 16-byte chunks per tile row
+constexpr int G_THREADS = 512;
+constexpr int G_TILE = G_BM * G_CH;  // uint4 per operand tile
+
+__device__ __forceinline__ int gswz(int r, int c) { return r * G_CH + (c ^ ((r >> 1) & 7)); }
+
+// expected C[i][j] of the probe operands depends only on (i mod 5, j mod 7)
+__device__ int probe_expect(int ia5, int jb7, int K) {
+  const int q = K / 35, rem = K - q * 35;
+  const int ia = ia5 * 3 % 5, jb = jb7 * 11 % 7;
+  int s = 0;
+  for (int r = 0; r < 35; ++r) {
+    int a = ia + (r * 7) % 5;
+    a = (a >= 5 ? a - 5 : a) - 2;
+    int b = jb + (r * 5) % 7;
+    b = (b >= 7 ? b - 7 : b) - 3;
+    s += (q + (r < rem ? 1 : 0)) * a * b;
+  }
+  return s;
+}
+
+template <bool VERIFY>
+__global__ __launch_bounds__(G_THREADS, 1) void gemm256_kernel(
+    const uint4* __restrict__ A, const uint4* __restrict__ Bt, float* __restrict__ C, int M, int N, int K,
+    int* __restrict__ tile_xcd, int* __restrict__ xcd_blocks, unsigned* __restrict__ err_total,
+    unsigned* __restrict__ err_xcd) {
+  __shared__ uint4 lds[2 * 2 * G_TILE];  // [buffer][A, B][row × chunk]
+  __shared__ float expect[35];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int w = tid >> 6;
+  const int wm = w >> 2, wn = w & 3;
+  const int tiles_n = N / G_BN;
+  const int nwg = gridDim.x;
+  // bijective XCD remap: the blocks dispatched to one XCD (orig % 8) take consecutive tiles
+  const int orig = blockIdx.x, xq = nwg >> 3, xr = nwg & 7, xs = orig & 7;
+  const int bid = (xs < xr ? xs * (xq + 1) : xr * (xq + 1) + (xs - xr) * xq) + (orig >> 3);
+  const int tm = bid / tiles_n;
+  const int tn = bid - tm * tiles_n;
+  const unsigned xcc = xcc_id();
+  if (tid == 0) {
+    if (tile_xcd) tile_xcd[bid] = (int)xcc;
+    if (xcd_blocks) atomicAdd(&xcd_blocks[xcc], 1);
+  }
+  if (VERIFY && tid < 35) expect[tid] = (float)probe_expect(tid / 7, tid % 7, K);
+
+  const size_t kch = (size_t)(K / 8);
+  const uint4* Ag = A + (size_t)tm * G_BM * kch;
+  const uint4* Bg = Bt + (size_t)tn * G_BN * kch;
+
+  // DMA of K-tile kt into buffer b: wave w fills rows [32w, 32w + 32) of A and of B,
+  // 8 rows (1 KiB) per instruction; lane l lands at LDS chunk p = base + l.
+  auto issue = [&](int kt, int b) {
+    uint4* la = lds + (b * 2 + 0) * G_TILE;
+    uint4* lb = lds + (b * 2 + 1) * G_TILE;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int base = (w * 4 + i) * 64;
+      const int p = base + lane;
+      const int row = p >> 3;
+      const int c = (p & 7) ^ ((row >> 1) & 7);
+      const size_t g = (size_t)row * kch + (size_t)kt * G_CH + c;
+      __builtin_amdgcn_global_load_lds(Ag + g, la + base, 16, 0, 0);
+      __builtin_amdgcn_global_load_lds(Bg + g, lb + base, 16, 0, 0);
+    }
+  };
+
+  f32x16 acc[4][2];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  const int nkt = K / G_BK;
+  issue(0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  const int lr = lane & 31, lh = lane >> 5;
+  for (int kt = 0; kt < nkt; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nkt) issue(kt + 1, cur ^ 1);  // buffer cur^1 was released by the last barrier
+    const uint4* sa = lds + (cur * 2 + 0) * G_TILE;
+    const uint4* sb = lds + (cur * 2 + 1) * G_TILE;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const int c = 2 * s + lh;  // lane half h holds k = 16s + 8h .. +7
+      bf16x8 af[4], bfr[2];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) af[i] = __builtin_bit_cast(bf16x8, sa[gswz(wm * 128 + i * 32 + lr, c)]);
+#pragma unroll
+      for (int j = 0; j < 2; ++j) bfr[j] = __builtin_bit_cast(bf16x8, sb[gswz(wn * 64 + j * 32 + lr, c)]);
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+
+  // C/D map of 32x32x16: col = lane & 31, row = (reg & 3) + 8 * (reg >> 2) + 4 * (lane >> 5)
+  unsigned bad = 0;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int col = tn * G_BN + wn * 64 + j * 32 + lr;
+      const int rbase = tm * G_BM + wm * 128 + i * 32 + 4 * lh;
+      if (VERIFY) {
+        const int c7 = col % 7;
+        const int r5 = rbase % 5;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          int rr = r5 + (r & 3) + 8 * (r >> 2);
+          rr %= 5;
+          bad += acc[i][j][r] != expect[rr * 7 + c7];
+        }
+      } else {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) C[(size_t)(rbase + (r & 3) + 8 * (r >> 2)) * N + col] = acc[i][j][r];
+      }
+    }
+  if (VERIFY) {
+    for (int off = 32; off > 0; off >>= 1) bad += __shfl_down(bad, off, 64);
+    if (lane == 0 && bad) {
+      atomicAdd(err_total, bad);
+      if (err_xcd) atomicAdd(&err_xcd[xcc], bad);
+    }
+  }
+}
+
+bool gemm256_ok(int M, int N, int K) { return M % G_BM == 0 && N % G_BN == 0 && K % G_BK == 0; }
+
 __device__ __forceinline__ uint16_t small_int_bf16(int v) {
   // exact for |v| < 256: take the high half of the f32 bit pattern
   return (uint16_t)(__float_as_uint((float)v) >> 16);
@@ -211,6 +365,7 @@ __device__ __forceinline__ uint32_t mix32(uint32_t x) {
   return x;
 }
 
+template <bool NT>
 __global__ __launch_bounds__(256) void hbm_write_kernel(u32x4* __restrict__ buf, size_t n, uint32_t seed) {
   for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
     const uint32_t b = (uint32_t)(i * 4) ^ seed;
@@ -219,7 +374,10 @@ __global__ __launch_bounds__(256) void hbm_write_kernel(u32x4* __restrict__ buf,
     v.y = mix32(b + 1);
     v.z = mix32(b + 2);
     v.w = mix32(b + 3);
-    __builtin_nontemporal_store(v, &buf[i]);
+    if (NT)
+      __builtin_nontemporal_store(v, &buf[i]);
+    else
+      buf[i] = v;
   }
 }
 
@@ -281,12 +439,31 @@ int odh_probe_fill(void* A, void* Bt, int M, int N, int K, hipStream_t stream) {
   return (int)hipGetLastError();
 }
 
-int odh_gemm_bf16(const void* A, const void* Bt, float* C, int M, int N, int K, int* tile_xcd, int* xcd_blocks,
-                  hipStream_t stream) {
+// the 128² two-buffer register-staged kernel, for shapes the 256² tile does not divide
+// (exported on its own for A/B measurements and numerics tests of both kernels)
+int odh_gemm_bf16_128(const void* A, const void* Bt, float* C, int M, int N, int K, int* tile_xcd, int* xcd_blocks,
+                      hipStream_t stream) {
   if (!odh_gemm_shape_ok(M, N, K)) return (int)hipErrorInvalidValue;
   const int nwg = (M / BM) * (N / BN);
   gemm_bf16_kernel<<<nwg, THREADS, 0, stream>>>((const uint4*)A, (const uint4*)Bt, C, M, N, K, tile_xcd, xcd_blocks);
   return (int)hipGetLastError();
+}
+
+// workgroups (= tiles) the GEMM launches for this shape: 256² tiles when they fit, else 128²
+int odh_gemm_tiles(int M, int N, int K) {
+  if (!odh_gemm_shape_ok(M, N, K)) return 0;
+  return gemm256_ok(M, N, K) ? (M / G_BM) * (N / G_BN) : (M / BM) * (N / BN);
+}
+
+int odh_gemm_bf16(const void* A, const void* Bt, float* C, int M, int N, int K, int* tile_xcd, int* xcd_blocks,
+                  hipStream_t stream) {
+  if (!odh_gemm_shape_ok(M, N, K)) return (int)hipErrorInvalidValue;
+  if (gemm256_ok(M, N, K)) {
+    gemm256_kernel<false><<<(M / G_BM) * (N / G_BN), G_THREADS, 0, stream>>>(
+        (const uint4*)A, (const uint4*)Bt, C, M, N, K, tile_xcd, xcd_blocks, nullptr, nullptr);
+    return (int)hipGetLastError();
+  }
+  return odh_gemm_bf16_128(A, Bt, C, M, N, K, tile_xcd, xcd_blocks, stream);
 }
 
 int odh_probe_verify(const float* C, int M, int N, int K, const int* tile_xcd, unsigned* err_total,
@@ -296,10 +473,23 @@ int odh_probe_verify(const float* C, int M, int N, int K, const int* tile_xcd, u
   return (int)hipGetLastError();
 }
 
-int odh_hbm_write(void* buf, size_t bytes, uint32_t seed, hipStream_t stream) {
+// probe GEMM with the check fused into the epilogue (operands from odh_probe_fill); the
+// shape must take 256² tiles.  Mismatches go to err_total / err_xcd[XCC that computed them].
+int odh_probe_gemm_verify(const void* A, const void* Bt, int M, int N, int K, int* tile_xcd, int* xcd_blocks,
+                          unsigned* err_total, unsigned* err_xcd, hipStream_t stream) {
+  if (!odh_gemm_shape_ok(M, N, K) || !gemm256_ok(M, N, K) || !err_total) return (int)hipErrorInvalidValue;
+  gemm256_kernel<true><<<(M / G_BM) * (N / G_BN), G_THREADS, 0, stream>>>(
+      (const uint4*)A, (const uint4*)Bt, nullptr, M, N, K, tile_xcd, xcd_blocks, err_total, err_xcd);
+  return (int)hipGetLastError();
+}
+
+int odh_hbm_write(void* buf, size_t bytes, uint32_t seed, int nontemporal, hipStream_t stream) {
   const size_t n = bytes / 16;
   if (n == 0) return (int)hipErrorInvalidValue;
-  hbm_write_kernel<<<grid_for(n, 256 * 4), 256, 0, stream>>>((u32x4*)buf, n, seed);
+  if (nontemporal)
+    hbm_write_kernel<true><<<grid_for(n, 256 * 4), 256, 0, stream>>>((u32x4*)buf, n, seed);
+  else
+    hbm_write_kernel<false><<<grid_for(n, 256 * 4), 256, 0, stream>>>((u32x4*)buf, n, seed);
   return (int)hipGetLastError();
 }
 

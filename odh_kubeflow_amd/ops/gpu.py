@@ -70,13 +70,17 @@ def load_library(build_if_missing: bool = False):
         lib.odh_error_string.argtypes = [i]
         lib.odh_error_string.restype = ctypes.c_char_p
         lib.odh_probe_fill.argtypes = [vp, vp, i, i, i, vp]
+        lib.odh_gemm_tiles.argtypes = [i, i, i]
+        lib.odh_gemm_tiles.restype = i
         lib.odh_gemm_bf16.argtypes = [vp, vp, vp, i, i, i, vp, vp, vp]
+        lib.odh_gemm_bf16_128.argtypes = [vp, vp, vp, i, i, i, vp, vp, vp]
         lib.odh_probe_verify.argtypes = [vp, i, i, i, vp, vp, vp, vp]
-        lib.odh_hbm_write.argtypes = [vp, sz, u32, vp]
+        lib.odh_probe_gemm_verify.argtypes = [vp, vp, i, i, i, vp, vp, vp, vp, vp]
+        lib.odh_hbm_write.argtypes = [vp, sz, u32, i, vp]
         lib.odh_hbm_check.argtypes = [vp, sz, u32, vp, vp]
         lib.odh_busy.argtypes = [vp, i, i, vp]
-        for f in ("odh_probe_fill", "odh_gemm_bf16", "odh_probe_verify", "odh_hbm_write", "odh_hbm_check",
-                  "odh_busy"):
+        for f in ("odh_probe_fill", "odh_gemm_bf16", "odh_gemm_bf16_128", "odh_probe_verify", "odh_probe_gemm_verify",
+                  "odh_hbm_write", "odh_hbm_check", "odh_busy"):
             getattr(lib, f).restype = i
         _lib = lib
         return lib
@@ -98,10 +102,21 @@ def gemm_shape_ok(m: int, n: int, k: int) -> bool:
     return m > 0 and n > 0 and k > 0 and m % BM == 0 and n % BN == 0 and k % BK == 0
 
 
-def gemm_bf16(a, bt, out=None, tile_xcd=None, xcd_blocks=None):
+def gemm_tiles(m: int, n: int, k: int) -> int:
+    """Workgroups the GEMM launches for this shape (256² tiles when they divide it, else 128²)."""
+    return load_library().odh_gemm_tiles(m, n, k)
+
+
+def fused_verify_ok(m: int, n: int, k: int) -> bool:
+    return gemm_shape_ok(m, n, k) and m % 256 == 0 and n % 256 == 0 and k % 64 == 0
+
+
+def gemm_bf16(a, bt, out=None, tile_xcd=None, xcd_blocks=None, tile: Optional[int] = None):
     """``C[M,N] = A[M,K] · Bt[N,K]ᵀ`` in fp32 on the matrix cores.
 
-    Shapes must be multiples of the 128×128×32 tile (checked here, before launch).
+    Shapes must be multiples of the 128×128×32 tile (checked here, before launch); the
+    256×256×64 LDS-DMA kernel runs when it divides the shape (``tile=128`` forces the
+    smaller kernel, for A/B measurements).
     """
     import torch
 
@@ -126,7 +141,8 @@ def gemm_bf16(a, bt, out=None, tile_xcd=None, xcd_blocks=None):
     if xcd_blocks is not None and xcd_blocks.numel() < N_XCD:
         raise ValueError("xcd_blocks too small")
     lib = load_library()
-    _check(lib.odh_gemm_bf16(a.data_ptr(), bt.data_ptr(), out.data_ptr(), m, n, k,
+    fn = lib.odh_gemm_bf16_128 if tile == 128 else lib.odh_gemm_bf16
+    _check(fn(a.data_ptr(), bt.data_ptr(), out.data_ptr(), m, n, k,
                              tile_xcd.data_ptr() if tile_xcd is not None else None,
                              xcd_blocks.data_ptr() if xcd_blocks is not None else None, _stream_ptr(a.device)))
     return out
@@ -135,7 +151,8 @@ def gemm_bf16(a, bt, out=None, tile_xcd=None, xcd_blocks=None):
 class GpuProbe:
     """Resident start-up probe for one GPU (allocate + fill once, then ~1 ms per run)."""
 
-    def __init__(self, device: int = 0, m: int = 4096, n: int = 4096, k: int = 4096, hbm_bytes: int = 1 << 30):
+    def __init__(self, device: int = 0, m: int = 4096, n: int = 4096, k: int = 4096, hbm_bytes: int = 1 << 30,
+                 hbm_nontemporal: bool = False):
         import torch
 
         if not gemm_shape_ok(m, n, k):
@@ -149,7 +166,10 @@ class GpuProbe:
         with torch.cuda.device(self.device):
             self.a = torch.empty((m, k), dtype=torch.bfloat16, device=self.device)
             self.bt = torch.empty((n, k), dtype=torch.bfloat16, device=self.device)
-            self.c = torch.empty((m, n), dtype=torch.float32, device=self.device)
+            # the 256² kernel checks C in registers; other shapes store C and run the check kernel
+            self.fused = fused_verify_ok(m, n, k)
+            self.c = None if self.fused else torch.empty((m, n), dtype=torch.float32, device=self.device)
+            self.tiles = lib.odh_gemm_tiles(m, n, k)
             self.tile_xcd = torch.full(((m // BM) * (n // BN),), -1, dtype=torch.int32, device=self.device)
             self.hbm = torch.empty((hbm_bytes // 4,), dtype=torch.int32, device=self.device)
             # counters: [0:8] xcd_blocks, [8:16] err_xcd, [16] gemm err, [18:20] hbm err (u64)
@@ -157,6 +177,7 @@ class GpuProbe:
             self.host = torch.zeros((32,), dtype=torch.int32).pin_memory()
             self.ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
             _check(lib.odh_probe_fill(self.a.data_ptr(), self.bt.data_ptr(), m, n, k, _stream_ptr(self.device)))
+        self.hbm_nontemporal = hbm_nontemporal
         self.runs = 0
         self.seed = 0x9E3779B9
 
@@ -172,13 +193,19 @@ class GpuProbe:
             cnt.zero_()
             self.seed = (self.seed * 1664525 + 1013904223) & 0xFFFFFFFF
             self.ev[0].record()
-            _check(lib.odh_gemm_bf16(self.a.data_ptr(), self.bt.data_ptr(), self.c.data_ptr(), self.m, self.n, self.k,
-                                     self.tile_xcd.data_ptr(), base, s))
-            self.ev[1].record()
-            _check(lib.odh_probe_verify(self.c.data_ptr(), self.m, self.n, self.k, self.tile_xcd.data_ptr(),
-                                        base + 16 * 4, base + 8 * 4, s))
-            self.ev[2].record()
-            _check(lib.odh_hbm_write(self.hbm.data_ptr(), self.hbm_bytes, self.seed, s))
+            if self.fused:
+                _check(lib.odh_probe_gemm_verify(self.a.data_ptr(), self.bt.data_ptr(), self.m, self.n, self.k,
+                                                 self.tile_xcd.data_ptr(), base, base + 16 * 4, base + 8 * 4, s))
+                self.ev[1].record()
+                self.ev[2].record()
+            else:
+                _check(lib.odh_gemm_bf16(self.a.data_ptr(), self.bt.data_ptr(), self.c.data_ptr(), self.m, self.n,
+                                         self.k, self.tile_xcd.data_ptr(), base, s))
+                self.ev[1].record()
+                _check(lib.odh_probe_verify(self.c.data_ptr(), self.m, self.n, self.k, self.tile_xcd.data_ptr(),
+                                            base + 16 * 4, base + 8 * 4, s))
+                self.ev[2].record()
+            _check(lib.odh_hbm_write(self.hbm.data_ptr(), self.hbm_bytes, self.seed, int(self.hbm_nontemporal), s))
             _check(lib.odh_hbm_check(self.hbm.data_ptr(), self.hbm_bytes, self.seed, base + 18 * 4, s))
             self.ev[3].record()
             self.host.copy_(cnt, non_blocking=True)
@@ -186,6 +213,7 @@ class GpuProbe:
             torch.cuda.current_stream(self.device).synchronize()
         h = self.host.tolist()
         gemm_ms = self.ev[0].elapsed_time(self.ev[1])
+        verify_ms = self.ev[1].elapsed_time(self.ev[2])
         hbm_ms = self.ev[2].elapsed_time(self.ev[3])
         xcd_blocks = h[0:8]
         err_xcd = h[8:16]
@@ -193,9 +221,10 @@ class GpuProbe:
         hbm_err = (h[18] & 0xFFFFFFFF) | ((h[19] & 0xFFFFFFFF) << 32)
         flops = 2.0 * self.m * self.n * self.k
         self.runs += 1
-        ok = gemm_err == 0 and hbm_err == 0 and sum(xcd_blocks) == (self.m // BM) * (self.n // BN)
+        ok = gemm_err == 0 and hbm_err == 0 and sum(xcd_blocks) == self.tiles
         return {
-            "ok": bool(ok), "device": self.device.index, "gemm_ms": gemm_ms,
+            "ok": bool(ok), "device": self.device.index, "gemm_ms": gemm_ms, "verify_ms": verify_ms,
+            "fused_verify": self.fused,
             "gemm_tflops": flops / (gemm_ms * 1e-3) / 1e12 if gemm_ms > 0 else 0.0,
             "hbm_gbps": 2.0 * self.hbm_bytes / (hbm_ms * 1e-3) / 1e9 if hbm_ms > 0 else 0.0,
             "gemm_errors": gemm_err, "hbm_errors": hbm_err, "xcd_blocks": xcd_blocks, "err_xcd": err_xcd,

@@ -17,14 +17,17 @@ def dev():
     return torch.device("cuda", 0)
 
 
-@pytest.mark.parametrize("m,n,k", [(128, 128, 32), (256, 384, 96), (1024, 512, 4096), (2048, 2048, 1024)])
-def test_gemm_bf16_matches_fp32_reference(dev, m, n, k):
+@pytest.mark.parametrize("tile", [None, 128])
+@pytest.mark.parametrize("m,n,k", [(128, 128, 32), (256, 384, 96), (512, 768, 192), (1024, 512, 4096),
+                                   (2048, 2048, 1024)])
+def test_gemm_bf16_matches_fp32_reference(dev, m, n, k, tile):
+    """Both kernels (256² LDS-DMA where it divides the shape, 128² register-staged) vs fp32 torch."""
     from odh_kubeflow_amd.ops.gpu import gemm_bf16
 
     g = torch.Generator(device=dev).manual_seed(m + n + k)
     a = torch.randn((m, k), generator=g, device=dev).to(torch.bfloat16)
     bt = torch.randn((n, k), generator=g, device=dev).to(torch.bfloat16)
-    c = gemm_bf16(a, bt)
+    c = gemm_bf16(a, bt, tile=tile)
     ref = a.float() @ bt.float().t()
     torch.cuda.synchronize()
     err = (c - ref).abs().max().item()
@@ -56,21 +59,39 @@ def test_gemm_bf16_rejects_bad_shapes(dev):
 def test_startup_probe_passes_and_sees_all_xcds(dev):
     from odh_kubeflow_amd.ops.gpu import GpuProbe
 
-    p = GpuProbe(0, m=2048, n=2048, k=2048, hbm_bytes=256 << 20)
+    for shape, fused in (((2048, 2048, 2048), True), ((1024, 1152, 512), False)):
+        p = GpuProbe(0, *shape, hbm_bytes=256 << 20)
+        r = p.run()
+        r = p.run()
+        assert r["ok"], r
+        assert r["fused_verify"] is fused
+        assert r["gemm_errors"] == 0 and r["hbm_errors"] == 0
+        assert r["xcds"] == 8, r["xcd_blocks"]
+        assert sum(r["xcd_blocks"]) == p.tiles == (shape[0] // (256 if fused else 128)) * (
+            shape[1] // (256 if fused else 128))
+        assert r["gemm_tflops"] > 50 and r["hbm_gbps"] > 500, r
+
+
+def test_fused_probe_verify_detects_corrupted_operand(dev):
+    """The in-register check of the 256² kernel counts every wrong output element."""
+    from odh_kubeflow_amd.ops import gpu
+
+    p = gpu.GpuProbe(0, m=1024, n=1024, k=512, hbm_bytes=16 << 20)
+    assert p.fused and p.run()["ok"]
+    # A[5][7] += 1 changes C[5][j] by Bt[j][7] for every j: wrong wherever Bt[j][7] != 0
+    expect_bad = int((p.bt[:, 7].float() != 0).sum().item())
+    p.a[5, 7] = (p.a[5, 7].float() + 1).to(torch.bfloat16)
     r = p.run()
-    r = p.run()
-    assert r["ok"], r
-    assert r["gemm_errors"] == 0 and r["hbm_errors"] == 0
-    assert r["xcds"] == 8, r["xcd_blocks"]
-    assert sum(r["xcd_blocks"]) == (2048 // 128) ** 2
-    assert r["gemm_tflops"] > 50 and r["hbm_gbps"] > 500, r
+    assert not r["ok"] and r["gemm_errors"] == expect_bad and sum(r["err_xcd"]) == expect_bad
+    p.a[5, 7] = (p.a[5, 7].float() - 1).to(torch.bfloat16)
+    assert p.run()["ok"]
 
 
 def test_probe_verify_detects_corruption(dev):
     from odh_kubeflow_amd.ops import gpu
 
-    p = gpu.GpuProbe(0, m=1024, n=1024, k=512, hbm_bytes=16 << 20)
-    assert p.run()["ok"]
+    p = gpu.GpuProbe(0, m=1024, n=1152, k=512, hbm_bytes=16 << 20)  # not 256-divisible: store + check kernel
+    assert not p.fused and p.run()["ok"]
     lib = gpu.load_library()
     s = torch.cuda.current_stream().cuda_stream
     p.counters.zero_()
@@ -83,7 +104,7 @@ def test_probe_verify_detects_corruption(dev):
     assert h[16] == 2 and sum(h[8:16]) == 2
     # HBM: flip one word after the pattern write
     p.counters.zero_()
-    gpu._check(lib.odh_hbm_write(p.hbm.data_ptr(), p.hbm_bytes, 1234, s))
+    gpu._check(lib.odh_hbm_write(p.hbm.data_ptr(), p.hbm_bytes, 1234, 0, s))
     p.hbm[12345] ^= 1
     gpu._check(lib.odh_hbm_check(p.hbm.data_ptr(), p.hbm_bytes, 1234, p.counters.data_ptr() + 72, s))
     torch.cuda.synchronize()

@@ -1,0 +1,70 @@
+"""A/B timings of the node-agent kernels on one MI355X (run on the GPU box).
+
+GEMM 4096³ / 8192³: 128² register-staged kernel vs 256² LDS-DMA kernel vs torch (hipBLASLt);
+fused-verify probe GEMM; HBM pattern write with plain vs non-temporal stores; HBM check.
+"""
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import torch  # noqa: E402
+
+from odh_kubeflow_amd.ops import gpu  # noqa: E402
+
+
+def timeit(fn, iters=20, warm=3):
+    for _ in range(warm):
+        fn()
+    torch.cuda.synchronize()
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    ts = []
+    for _ in range(iters):
+        ev[0].record()
+        fn()
+        ev[1].record()
+        ev[1].synchronize()
+        ts.append(ev[0].elapsed_time(ev[1]))
+    ts.sort()
+    return ts[len(ts) // 2]
+
+
+def main():
+    out = {}
+    lib = gpu.load_library()
+    dev = torch.device("cuda", 0)
+    for n in (4096, 8192):
+        g = torch.Generator(device=dev).manual_seed(n)
+        a = (torch.rand((n, n), generator=g, device=dev) * 2 - 1).to(torch.bfloat16)
+        bt = (torch.rand((n, n), generator=g, device=dev) * 2 - 1).to(torch.bfloat16)
+        c = torch.empty((n, n), dtype=torch.float32, device=dev)
+        fl = 2.0 * n ** 3
+        for name, fn in (("gemm128", lambda: gpu.gemm_bf16(a, bt, out=c, tile=128)),
+                         ("gemm256", lambda: gpu.gemm_bf16(a, bt, out=c)),
+                         ("torch_bf16_out", lambda: torch.mm(a, bt.t()))):
+            ms = timeit(fn)
+            out[f"{name}_{n}"] = {"ms": round(ms, 4), "tflops": round(fl / ms / 1e9, 1)}
+        ref = a.float() @ bt.float().t()
+        gpu.gemm_bf16(a, bt, out=c)
+        out[f"gemm256_{n}_maxerr"] = float((c - ref).abs().max().item())
+        del a, bt, c, ref
+        torch.cuda.empty_cache()
+    p = gpu.GpuProbe(0)
+    s = torch.cuda.current_stream().cuda_stream
+    cnt = p.counters.data_ptr()
+    ms = timeit(lambda: lib.odh_probe_gemm_verify(p.a.data_ptr(), p.bt.data_ptr(), p.m, p.n, p.k,
+                                                  p.tile_xcd.data_ptr(), cnt, cnt + 64, cnt + 32, s))
+    out["probe_gemm_fused_verify_4096"] = {"ms": round(ms, 4), "tflops": round(2.0 * 4096 ** 3 / ms / 1e9, 1)}
+    for nt in (0, 1):
+        ms = timeit(lambda: lib.odh_hbm_write(p.hbm.data_ptr(), p.hbm_bytes, 7, nt, s))
+        out[f"hbm_write_nt{nt}_1GiB"] = {"ms": round(ms, 4), "gbps": round(p.hbm_bytes / ms / 1e6, 1)}
+    ms = timeit(lambda: lib.odh_hbm_check(p.hbm.data_ptr(), p.hbm_bytes, 7, cnt + 72, s))
+    out["hbm_check_1GiB"] = {"ms": round(ms, 4), "gbps": round(p.hbm_bytes / ms / 1e6, 1)}
+    r = [p.run() for _ in range(5)][-1]
+    out["probe_run"] = {k: r[k] for k in ("ok", "gemm_ms", "gemm_tflops", "hbm_gbps", "wall_ms", "xcds", "fused_verify")}
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main()

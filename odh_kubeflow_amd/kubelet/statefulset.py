@@ -44,6 +44,7 @@ class StatefulSetController:
         self.client = client
         self.reader = reader
         self.recorder = recorder
+        self._created: set = set()  # (sts uid, ordinal) of pods this controller has created
 
     def _pod_for(self, sts: dict, ordinal: int, rev: str) -> dict:
         tmpl = (sts.get("spec") or {}).get("template") or {}
@@ -77,6 +78,13 @@ class StatefulSetController:
         for i in range(replicas):
             p = by_ord.get(i)
             if p is None:
+                if (m.uid(sts), i) in self._created and not await self._still_exists(sts):
+                    # the pod went away because its StatefulSet was deleted (GC), and the STS
+                    # DELETED event has not reached this cache yet: do not resurrect it
+                    return Result()
+                self._created.add((m.uid(sts), i))
+                if len(self._created) > 65536:
+                    self._created.clear()
                 try:
                     await self.client.create(self._pod_for(sts, i, rev))
                     self.recorder.event(sts, "Normal", "SuccessfulCreate",
@@ -92,6 +100,16 @@ class StatefulSetController:
                 await self._delete_pod(sts, p)
         await self._update_status(sts, rev)
         return Result()
+
+    async def _still_exists(self, sts: dict) -> bool:
+        from ..runtime.client import LIVE_READS
+
+        tok = LIVE_READS.set(True)
+        try:
+            live = await self.client.get_or_none(kinds.STATEFUL_SET, m.name(sts), m.namespace(sts))
+        finally:
+            LIVE_READS.reset(tok)
+        return live is not None and m.uid(live) == m.uid(sts) and not m.is_deleting(live)
 
     async def _delete_pod(self, sts: dict, p: dict) -> None:
         try:

@@ -381,6 +381,50 @@ __global__ __launch_bounds__(256) void hbm_write_kernel(u32x4* __restrict__ buf,
   }
 }
 
+// write-path variants for A/B measurement (odh_hbm_write_variant):
+//   1: each wave stores 4 consecutive KiB per iteration (4 × 1 KiB instructions in flight)
+//   2: each workgroup owns one contiguous slab (sequential DRAM pages per CU)
+//   3: constant data (no pattern math: the store-path ceiling)
+template <int V>
+__global__ __launch_bounds__(256) void hbm_write_variant_kernel(u32x4* __restrict__ buf, size_t n, uint32_t seed) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  if (V == 1) {
+    const size_t waves = (size_t)gridDim.x * 4;
+    for (size_t w = (size_t)blockIdx.x * 4 + wave; w * 256 < n; w += waves) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const size_t i = w * 256 + u * 64 + lane;
+        if (i < n) {
+          const uint32_t b = (uint32_t)(i * 4) ^ seed;
+          u32x4 v;
+          v.x = mix32(b);
+          v.y = mix32(b + 1);
+          v.z = mix32(b + 2);
+          v.w = mix32(b + 3);
+          buf[i] = v;
+        }
+      }
+    }
+  } else if (V == 2) {
+    const size_t per = (n + gridDim.x - 1) / gridDim.x;
+    const size_t lo = blockIdx.x * per, hi = lo + per < n ? lo + per : n;
+    for (size_t i = lo + threadIdx.x; i < hi; i += blockDim.x) {
+      const uint32_t b = (uint32_t)(i * 4) ^ seed;
+      u32x4 v;
+      v.x = mix32(b);
+      v.y = mix32(b + 1);
+      v.z = mix32(b + 2);
+      v.w = mix32(b + 3);
+      buf[i] = v;
+    }
+  } else {
+    u32x4 v;
+    v.x = v.y = v.z = v.w = seed;
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+      buf[i] = v;
+  }
+}
+
 __global__ __launch_bounds__(256) void hbm_check_kernel(const u32x4* __restrict__ buf, size_t n, uint32_t seed,
                                                         unsigned long long* __restrict__ err) {
   unsigned local = 0;
@@ -490,6 +534,18 @@ int odh_hbm_write(void* buf, size_t bytes, uint32_t seed, int nontemporal, hipSt
     hbm_write_kernel<true><<<grid_for(n, 256 * 4), 256, 0, stream>>>((u32x4*)buf, n, seed);
   else
     hbm_write_kernel<false><<<grid_for(n, 256 * 4), 256, 0, stream>>>((u32x4*)buf, n, seed);
+  return (int)hipGetLastError();
+}
+
+int odh_hbm_write_variant(void* buf, size_t bytes, uint32_t seed, int variant, int blocks, hipStream_t stream) {
+  const size_t n = bytes / 16;
+  if (n == 0 || blocks <= 0) return (int)hipErrorInvalidValue;
+  if (variant == 1)
+    hbm_write_variant_kernel<1><<<blocks, 256, 0, stream>>>((u32x4*)buf, n, seed);
+  else if (variant == 2)
+    hbm_write_variant_kernel<2><<<blocks, 256, 0, stream>>>((u32x4*)buf, n, seed);
+  else
+    hbm_write_variant_kernel<3><<<blocks, 256, 0, stream>>>((u32x4*)buf, n, seed);
   return (int)hipGetLastError();
 }
 

@@ -59,6 +59,21 @@ def main():
     for nt in (0, 1):
         ms = timeit(lambda: lib.odh_hbm_write(p.hbm.data_ptr(), p.hbm_bytes, 7, nt, s))
         out[f"hbm_write_nt{nt}_1GiB"] = {"ms": round(ms, 4), "gbps": round(p.hbm_bytes / ms / 1e6, 1)}
+    import ctypes
+
+    lib.odh_hbm_write_variant.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint32, ctypes.c_int,
+                                          ctypes.c_int, ctypes.c_void_p]
+    for v in (1, 2, 3):
+        for blocks in (1024, 2048, 4096, 8192):
+            ms = timeit(lambda: lib.odh_hbm_write_variant(p.hbm.data_ptr(), p.hbm_bytes, 7, v, blocks, s))
+            out[f"hbm_write_v{v}_b{blocks}"] = {"ms": round(ms, 4), "gbps": round(p.hbm_bytes / ms / 1e6, 1)}
+    big = torch.empty((4 << 30) // 4, dtype=torch.int32, device=dev)
+    for v in (1, 3):
+        ms = timeit(lambda: lib.odh_hbm_write_variant(big.data_ptr(), 4 << 30, 7, v, 4096, s), iters=5)
+        out[f"hbm_write_v{v}_4GiB"] = {"ms": round(ms, 4), "gbps": round((4 << 30) / ms / 1e6, 1)}
+    ms = timeit(lambda: big.fill_(3), iters=5)
+    out["torch_fill_4GiB"] = {"ms": round(ms, 4), "gbps": round((4 << 30) / ms / 1e6, 1)}
+    del big
     ms = timeit(lambda: lib.odh_hbm_check(p.hbm.data_ptr(), p.hbm_bytes, 7, cnt + 72, s))
     out["hbm_check_1GiB"] = {"ms": round(ms, 4), "gbps": round(p.hbm_bytes / ms / 1e6, 1)}
     r = [p.run() for _ in range(5)][-1]

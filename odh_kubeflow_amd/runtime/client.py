@@ -17,7 +17,7 @@ from __future__ import annotations
 
 import contextvars
 import abc
-from typing import Any, Callable, Iterable, List, Optional, Sequence
+from typing import Any, Callable, Dict, Iterable, List, Optional, Sequence, Tuple
 
 from ..apiserver.store import ObjectStore
 from ..models.scheme import SCHEME, ResourceInfo
@@ -29,6 +29,13 @@ WatchCallback = Callable[[str, dict, Optional[dict]], None]
 # Set by ``retry_on_conflict`` for its retries: a Conflict means the informer copy is
 # stale, so the retry reads through to the apiserver instead of sleeping for the cache.
 LIVE_READS: contextvars.ContextVar = contextvars.ContextVar("live_reads", default=False)
+
+
+def _rv_int(o) -> Optional[int]:
+    try:
+        return int((o.get("metadata") or {}).get("resourceVersion") or "")
+    except (TypeError, ValueError, AttributeError):
+        return None
 
 
 def _version_of(ref) -> Optional[str]:
@@ -193,12 +200,35 @@ class CachedClient(Client):
 
     Kinds in ``uncached`` are read live from the backing client, exactly like
     ``client.CacheOptions.DisableFor``.
+
+    Unlike controller-runtime's client, reads are consistent with this client's own
+    writes: every write records the resourceVersion it produced, and a cached read that
+    is older than that (the watch event is still in flight) goes to the apiserver
+    instead.  Without it a reconcile triggered between a write and its watch event acts
+    on the pre-write object and repeats the write (observed: the odh lock removal patch
+    and its admission call issued twice per notebook).
     """
 
     def __init__(self, reader: Reader, writer: Client, uncached: Sequence = ()):
         self.reader = reader
         self.writer = writer
         self.uncached = {SCHEME.resolve(k).key for k in uncached}
+        self._written: Dict[Tuple[str, str, str], int] = {}
+        self.fresh_reads = 0
+
+    def _note(self, out) -> None:
+        if not isinstance(out, dict) or "metadata" not in out:
+            return
+        rv = _rv_int(out)
+        if rv is None:
+            return
+        try:
+            key = (SCHEME.resolve(out).key, out["metadata"].get("namespace") or "", out["metadata"].get("name", ""))
+        except Exception:
+            return
+        if len(self._written) > 16384:
+            self._written.clear()
+        self._written[key] = rv
 
     def _live(self, kind) -> bool:
         return SCHEME.resolve(kind).key in self.uncached
@@ -213,6 +243,15 @@ class CachedClient(Client):
             return await self.writer.get(kind, name, namespace)
         await self._ensure(kind)
         o = self.reader.get(kind, name, namespace)
+        if self._written:
+            key = (SCHEME.resolve(kind).key, namespace or "", name)
+            want = self._written.get(key)
+            if want is not None:
+                have = _rv_int(o) if o is not None else None
+                if have is None or have < want:
+                    self.fresh_reads += 1  # the cache has not seen our own write yet
+                    return await self.writer.get(kind, name, namespace)
+                del self._written[key]
         if o is None:
             from ..models.errors import NotFound
 
@@ -237,16 +276,31 @@ class CachedClient(Client):
         return items
 
     async def create(self, obj):
-        return await self.writer.create(obj)
+        out = await self.writer.create(obj)
+        self._note(out)
+        return out
 
     async def update(self, obj):
-        return await self.writer.update(obj)
+        out = await self.writer.update(obj)
+        self._note(out)
+        return out
 
     async def update_status(self, obj):
-        return await self.writer.update_status(obj)
+        out = await self.writer.update_status(obj)
+        self._note(out)
+        return out
 
     async def patch(self, obj_or_kind, patch, patch_type="merge", name=None, namespace=None, subresource=None):
-        return await self.writer.patch(obj_or_kind, patch, patch_type, name, namespace, subresource)
+        out = await self.writer.patch(obj_or_kind, patch, patch_type, name, namespace, subresource)
+        self._note(out)
+        return out
 
     async def delete(self, obj_or_kind, name=None, namespace=None, preconditions=None, propagation="Background"):
+        if self._written:
+            try:
+                md = obj_or_kind.get("metadata", {}) if isinstance(obj_or_kind, dict) else {}
+                self._written.pop((SCHEME.resolve(obj_or_kind).key, namespace or md.get("namespace") or "",
+                                   name or md.get("name", "")), None)
+            except Exception:
+                pass
         return await self.writer.delete(obj_or_kind, name, namespace, preconditions, propagation)

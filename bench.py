@@ -76,7 +76,7 @@ async def run_local(args, n_gpus: int, probe) -> dict:
     cfg = ClusterConfig(gpus_per_node=8, odh=use_odh, webhook=use_odh, startup_probe=probe,
                         reference_emulation=args.reference_emulation, transport=args.transport,
                         env={"SET_PIPELINE_RBAC": "false", "SET_PIPELINE_SECRET": "false"})
-    lat_ms = []
+    lat_ms, teardown_ms = [], []
     recon = 0
     async with LocalCluster(cfg) as cl:
         await cl.ensure_namespace("bench")
@@ -107,6 +107,7 @@ async def run_local(args, n_gpus: int, probe) -> dict:
                     await asyncio.sleep(0.0005)
             if pending:
                 raise RuntimeError(f"notebooks not Ready: {sorted(pending)}")
+            t_del = time.perf_counter()
             await asyncio.gather(*(cl.admin.delete(kinds.NOTEBOOK, nm, "bench") for nm in names))
             ok = await cl.wait_for(lambda: all(cl.store.peek(kinds.NOTEBOOK, nm, "bench") is None and
                                                cl.store.peek(kinds.POD, f"{nm}-0", "bench") is None
@@ -117,6 +118,7 @@ async def run_local(args, n_gpus: int, probe) -> dict:
                 raise RuntimeError(f"teardown did not finish: {[cl.store.peek(k, o, 'bench') for k, o in left]}")
             if timed:
                 lat_ms.extend((ready_at[nm] - t0[nm]) * 1e3 for nm in names)
+                teardown_ms.append((time.perf_counter() - t_del) * 1e3)
 
         for _ in range(args.warmup):
             await one_step(False)
@@ -131,7 +133,8 @@ async def run_local(args, n_gpus: int, probe) -> dict:
         elapsed = time.perf_counter() - t_start
         recon = cl.reconcile_count() - r0
         probes = [p for g in cl.gpu_runtimes for p in g.probe_results]
-    return {"elapsed": elapsed, "reconciles": recon, "lat_ms": lat_ms, "odh": use_odh, "probes": probes}
+    return {"elapsed": elapsed, "reconciles": recon, "lat_ms": lat_ms, "odh": use_odh, "probes": probes,
+            "teardown_ms": teardown_ms}
 
 
 def _odh_available() -> bool:
@@ -208,6 +211,8 @@ def report(args, n, res) -> dict:
         "notebooks_ready_per_s": round(len(lat) / el, 3) if el > 0 else None,
         "reconciles_per_notebook": round(res["reconciles"] / max(1, len(lat)), 2),
     }
+    if res.get("teardown_ms"):
+        out["p50_teardown_ms"] = round(pct(res["teardown_ms"], 0.5), 3)
     if probes:
         out["gpu_probe"] = {"gemm_tflops_p50": round(statistics.median(p.get("gemm_tflops", 0) for p in probes), 1),
                             "hbm_gbps_p50": round(statistics.median(p.get("hbm_gbps", 0) for p in probes), 1),

@@ -142,7 +142,7 @@ async def _drive(args, shard, dist, torch) -> dict:
 
     use_odh = not args.no_odh
     ns = shard.cfg.namespace
-    lat_ms = []
+    lat_ms, teardown_ms = [], []
     state = {"recon": 0, "step": 0}
 
     async def one_step(timed: bool):
@@ -160,6 +160,7 @@ async def _drive(args, shard, dist, torch) -> dict:
             raise RuntimeError(f"teardown of {ns}/{nm} did not finish")
         if timed:
             lat_ms.append((ready - t0) * 1e3)
+            teardown_ms.append((time.perf_counter() - ready) * 1e3)
 
     for _ in range(args.warmup):
         await one_step(False)
@@ -183,7 +184,9 @@ async def _drive(args, shard, dist, torch) -> dict:
     await _in_thread(lambda: dist.all_reduce(el, op=dist.ReduceOp.MAX))
     await _in_thread(lambda: dist.all_reduce(rc, op=dist.ReduceOp.SUM))
     gathered = [None] * dist.get_world_size()
-    await _in_thread(dist.all_gather_object, gathered, {"lat": lat_ms, "probes": shard.probe_results})
+    await _in_thread(dist.all_gather_object, gathered, {"lat": lat_ms, "probes": shard.probe_results,
+                                                        "teardown": teardown_ms})
     return {"elapsed": float(el.item()), "reconciles": int(rc.item()),
             "lat_ms": [x for g in gathered for x in g["lat"]], "odh": use_odh,
-            "probes": [p for g in gathered for p in g["probes"]]}
+            "probes": [p for g in gathered for p in g["probes"]],
+            "teardown_ms": [x for g in gathered for x in g["teardown"]]}

@@ -123,6 +123,9 @@ async def run_local(args, n_gpus: int, probe) -> dict:
         for _ in range(args.warmup):
             await one_step(False)
         await cl.settle(5)
+        from odh_kubeflow_amd.utils import gctune
+
+        gctune.tune()  # start-up heap out of the cyclic collector's reach (see utils/gctune.py)
         r0 = cl.reconcile_count()
         t_start = time.perf_counter()
         for _ in range(args.steps):

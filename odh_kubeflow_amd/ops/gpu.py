@@ -152,7 +152,7 @@ class GpuProbe:
     """Resident start-up probe for one GPU (allocate + fill once, then ~1 ms per run)."""
 
     def __init__(self, device: int = 0, m: int = 4096, n: int = 4096, k: int = 4096, hbm_bytes: int = 1 << 30,
-                 hbm_nontemporal: bool = False):
+                 hbm_nontemporal: bool = False, overlap: bool = True):
         import torch
 
         if not gemm_shape_ok(m, n, k):
@@ -175,46 +175,69 @@ class GpuProbe:
             # counters: [0:8] xcd_blocks, [8:16] err_xcd, [16] gemm err, [18:20] hbm err (u64)
             self.counters = torch.zeros((32,), dtype=torch.int32, device=self.device)
             self.host = torch.zeros((32,), dtype=torch.int32).pin_memory()
-            self.ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+            self.ev = [torch.cuda.Event(enable_timing=True) for _ in range(5)]
+            self.streams = (torch.cuda.Stream(self.device), torch.cuda.Stream(self.device))
             _check(lib.odh_probe_fill(self.a.data_ptr(), self.bt.data_ptr(), m, n, k, _stream_ptr(self.device)))
+            torch.cuda.current_stream(self.device).synchronize()
         self.hbm_nontemporal = hbm_nontemporal
+        self.overlap = overlap
         self.runs = 0
         self.seed = 0x9E3779B9
 
     def run(self) -> dict:
+        """One probe.  With ``overlap`` (default) the memory-bound HBM sweep and the
+        MFMA-bound GEMM run concurrently on two streams of the probe: their waves co-reside
+        on the CUs (the GEMM's 1 workgroup/CU leaves VGPRs and wave slots free), so the
+        GEMM hides under the sweep instead of adding to it."""
         import torch
 
         lib = load_library()
         t0 = time.perf_counter()
         with torch.cuda.device(self.device):
-            s = _stream_ptr(self.device)
+            sg, sh = self.streams
             cnt = self.counters
             base = cnt.data_ptr()
-            cnt.zero_()
             self.seed = (self.seed * 1664525 + 1013904223) & 0xFFFFFFFF
-            self.ev[0].record()
+            sg.wait_stream(torch.cuda.current_stream(self.device))  # caller's writes to a / bt / hbm
+            with torch.cuda.stream(sg):
+                cnt.zero_()
+                self.ev[0].record(sg)
+            g, h_ = sg.cuda_stream, (sh.cuda_stream if self.overlap else sg.cuda_stream)
+            if self.overlap:
+                sh.wait_event(self.ev[0])
+            hs = sh if self.overlap else sg
+
+            def sweep():
+                self.ev[2].record(hs)
+                _check(lib.odh_hbm_write(self.hbm.data_ptr(), self.hbm_bytes, self.seed, int(self.hbm_nontemporal),
+                                         h_))
+                _check(lib.odh_hbm_check(self.hbm.data_ptr(), self.hbm_bytes, self.seed, base + 18 * 4, h_))
+                self.ev[3].record(hs)
+
+            if self.overlap:
+                sweep()  # the longer, memory-bound part first: both are in flight together
             if self.fused:
                 _check(lib.odh_probe_gemm_verify(self.a.data_ptr(), self.bt.data_ptr(), self.m, self.n, self.k,
-                                                 self.tile_xcd.data_ptr(), base, base + 16 * 4, base + 8 * 4, s))
-                self.ev[1].record()
-                self.ev[2].record()
+                                                 self.tile_xcd.data_ptr(), base, base + 16 * 4, base + 8 * 4, g))
+                self.ev[1].record(sg)
             else:
                 _check(lib.odh_gemm_bf16(self.a.data_ptr(), self.bt.data_ptr(), self.c.data_ptr(), self.m, self.n,
-                                         self.k, self.tile_xcd.data_ptr(), base, s))
-                self.ev[1].record()
+                                         self.k, self.tile_xcd.data_ptr(), base, g))
+                self.ev[1].record(sg)
                 _check(lib.odh_probe_verify(self.c.data_ptr(), self.m, self.n, self.k, self.tile_xcd.data_ptr(),
-                                            base + 16 * 4, base + 8 * 4, s))
-                self.ev[2].record()
-            _check(lib.odh_hbm_write(self.hbm.data_ptr(), self.hbm_bytes, self.seed, int(self.hbm_nontemporal), s))
-            _check(lib.odh_hbm_check(self.hbm.data_ptr(), self.hbm_bytes, self.seed, base + 18 * 4, s))
-            self.ev[3].record()
-            self.host.copy_(cnt, non_blocking=True)
-            self.ev[3].synchronize()
-            torch.cuda.current_stream(self.device).synchronize()
+                                            base + 16 * 4, base + 8 * 4, g))
+            if not self.overlap:
+                sweep()
+            else:
+                sg.wait_event(self.ev[3])
+            with torch.cuda.stream(sg):
+                self.host.copy_(cnt, non_blocking=True)
+                self.ev[4].record(sg)
+            self.ev[4].synchronize()
         h = self.host.tolist()
         gemm_ms = self.ev[0].elapsed_time(self.ev[1])
-        verify_ms = self.ev[1].elapsed_time(self.ev[2])
         hbm_ms = self.ev[2].elapsed_time(self.ev[3])
+        probe_ms = self.ev[0].elapsed_time(self.ev[4])
         xcd_blocks = h[0:8]
         err_xcd = h[8:16]
         gemm_err = h[16] & 0xFFFFFFFF
@@ -223,8 +246,8 @@ class GpuProbe:
         self.runs += 1
         ok = gemm_err == 0 and hbm_err == 0 and sum(xcd_blocks) == self.tiles
         return {
-            "ok": bool(ok), "device": self.device.index, "gemm_ms": gemm_ms, "verify_ms": verify_ms,
-            "fused_verify": self.fused,
+            "ok": bool(ok), "device": self.device.index, "gemm_ms": gemm_ms, "hbm_ms": hbm_ms,
+            "gpu_ms": probe_ms, "fused_verify": self.fused, "overlap": self.overlap,
             "gemm_tflops": flops / (gemm_ms * 1e-3) / 1e12 if gemm_ms > 0 else 0.0,
             "hbm_gbps": 2.0 * self.hbm_bytes / (hbm_ms * 1e-3) / 1e9 if hbm_ms > 0 else 0.0,
             "gemm_errors": gemm_err, "hbm_errors": hbm_err, "xcd_blocks": xcd_blocks, "err_xcd": err_xcd,

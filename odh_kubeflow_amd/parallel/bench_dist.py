@@ -165,6 +165,9 @@ async def _drive(args, shard, dist, torch) -> dict:
     for _ in range(args.warmup):
         await one_step(False)
     await shard.settle(5)
+    from ..utils import gctune
+
+    gctune.tune()
     if torch.cuda.is_available():
         torch.cuda.synchronize()
     await _in_thread(dist.barrier)

@@ -164,6 +164,9 @@ class Manager:
 
     async def run_until(self, stop: asyncio.Event) -> None:
         await self.start()
+        from ..utils import gctune
+
+        gctune.tune()  # long-running process: keep gen-2 pauses off the reconcile path
         try:
             await stop.wait()
         finally:

@@ -60,10 +60,13 @@ def test_startup_probe_passes_and_sees_all_xcds(dev):
     from odh_kubeflow_amd.ops.gpu import GpuProbe
 
     for shape, fused in (((2048, 2048, 2048), True), ((1024, 1152, 512), False)):
-        p = GpuProbe(0, *shape, hbm_bytes=256 << 20)
+        p = GpuProbe(0, *shape, hbm_bytes=256 << 20, overlap=False)  # phases timed in isolation
         r = p.run()
         r = p.run()
         assert r["ok"], r
+        p.overlap = True  # GEMM and HBM sweep concurrently on two streams: same verdict
+        assert p.run()["ok"] and p.run()["ok"]
+        p.overlap = False
         assert r["fused_verify"] is fused
         assert r["gemm_errors"] == 0 and r["hbm_errors"] == 0
         assert r["xcds"] == 8, r["xcd_blocks"]

@@ -217,7 +217,8 @@ def report(args, n, res) -> dict:
     if res.get("teardown_ms"):
         out["p50_teardown_ms"] = round(pct(res["teardown_ms"], 0.5), 3)
     if probes:
-        out["gpu_probe"] = {"gemm_tflops_p50": round(statistics.median(p.get("gemm_tflops", 0) for p in probes), 1),
+        out["gpu_probe"] = {"gpu_ms_p50": round(statistics.median(p.get("gpu_ms", 0) for p in probes), 3),
+                            "gemm_tflops_p50": round(statistics.median(p.get("gemm_tflops", 0) for p in probes), 1),
                             "hbm_gbps_p50": round(statistics.median(p.get("hbm_gbps", 0) for p in probes), 1),
                             "probe_wall_ms_p50": round(statistics.median(p.get("wall_ms", 0) for p in probes), 3),
                             "all_ok": all(p.get("ok") for p in probes), "runs": len(probes)}

@@ -188,7 +188,7 @@ __device__ int probe_expect(int ia5, int jb7, int K) {
   return s;
 }
 
-template <bool VERIFY>
+template <bool VERIFY, bool PIPE = true>
 __global__ __launch_bounds__(G_THREADS, 1) void gemm256_kernel(
     const uint4* __restrict__ A, const uint4* __restrict__ Bt, float* __restrict__ C, int M, int N, int K,
     int* __restrict__ tile_xcd, int* __restrict__ xcd_blocks, unsigned* __restrict__ err_total,
@@ -254,20 +254,32 @@ __global__ __launch_bounds__(G_THREADS, 1) void gemm256_kernel(
     if (kt + 1 < nkt) issue(kt + 1, cur ^ 1);  // buffer cur^1 was released by the last barrier
     const uint4* sa = lds + (cur * 2 + 0) * G_TILE;
     const uint4* sb = lds + (cur * 2 + 1) * G_TILE;
+    // fragments of k-substep s (lane half h holds k = 16s + 8h .. +7); with PIPE the reads
+    // of substep s+1 are issued before the MFMAs of substep s (two fragment sets in
+    // registers), so LDS latency hides under matrix-core work instead of stalling on it
+    bf16x8 af[2][4], bfr[2][2];
+    auto load = [&](int s, int slot) {
+      const int c = 2 * s + lh;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) af[slot][i] = __builtin_bit_cast(bf16x8, sa[gswz(wm * 128 + i * 32 + lr, c)]);
+#pragma unroll
+      for (int j = 0; j < 2; ++j) bfr[slot][j] = __builtin_bit_cast(bf16x8, sb[gswz(wn * 64 + j * 32 + lr, c)]);
+    };
+    if (PIPE) load(0, 0);
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
-      const int c = 2 * s + lh;  // lane half h holds k = 16s + 8h .. +7
-      bf16x8 af[4], bfr[2];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) af[i] = __builtin_bit_cast(bf16x8, sa[gswz(wm * 128 + i * 32 + lr, c)]);
-#pragma unroll
-      for (int j = 0; j < 2; ++j) bfr[j] = __builtin_bit_cast(bf16x8, sb[gswz(wn * 64 + j * 32 + lr, c)]);
+      const int slot = PIPE ? (s & 1) : 0;
+      if (PIPE) {
+        if (s + 1 < 4) load(s + 1, (s + 1) & 1);
+      } else {
+        load(s, 0);
+      }
       __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int j = 0; j < 2; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[slot][i], bfr[slot][j], acc[i][j], 0, 0, 0);
       __builtin_amdgcn_s_setprio(0);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -518,6 +530,20 @@ int odh_gemm_bf16_128(const void* A, const void* Bt, float* C, int M, int N, int
   if (!odh_gemm_shape_ok(M, N, K)) return (int)hipErrorInvalidValue;
   const int nwg = (M / BM) * (N / BN);
   gemm_bf16_kernel<<<nwg, THREADS, 0, stream>>>((const uint4*)A, (const uint4*)Bt, C, M, N, K, tile_xcd, xcd_blocks);
+  return (int)hipGetLastError();
+}
+
+// A/B: the 256² kernel without fragment pipelining (variant 0) or with it (variant 1)
+int odh_gemm_bf16_256_variant(const void* A, const void* Bt, float* C, int M, int N, int K, int variant,
+                              hipStream_t stream) {
+  if (!odh_gemm_shape_ok(M, N, K) || !gemm256_ok(M, N, K)) return (int)hipErrorInvalidValue;
+  const int nwg = (M / G_BM) * (N / G_BN);
+  if (variant == 0)
+    gemm256_kernel<false, false><<<nwg, G_THREADS, 0, stream>>>((const uint4*)A, (const uint4*)Bt, C, M, N, K,
+                                                                 nullptr, nullptr, nullptr, nullptr);
+  else
+    gemm256_kernel<false, true><<<nwg, G_THREADS, 0, stream>>>((const uint4*)A, (const uint4*)Bt, C, M, N, K,
+                                                                nullptr, nullptr, nullptr, nullptr);
   return (int)hipGetLastError();
 }
 

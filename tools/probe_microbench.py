@@ -40,6 +40,13 @@ def main():
         bt = (torch.rand((n, n), generator=g, device=dev) * 2 - 1).to(torch.bfloat16)
         c = torch.empty((n, n), dtype=torch.float32, device=dev)
         fl = 2.0 * n ** 3
+        import ctypes
+
+        lib.odh_gemm_bf16_256_variant.argtypes = [ctypes.c_void_p] * 3 + [ctypes.c_int] * 4 + [ctypes.c_void_p]
+        st = torch.cuda.current_stream().cuda_stream
+        for v in (0, 1):
+            ms = timeit(lambda: lib.odh_gemm_bf16_256_variant(a.data_ptr(), bt.data_ptr(), c.data_ptr(), n, n, n, v, st))
+            out[f"gemm256_v{v}_{n}"] = {"ms": round(ms, 4), "tflops": round(fl / ms / 1e9, 1)}
         for name, fn in (("gemm128", lambda: gpu.gemm_bf16(a, bt, out=c, tile=128)),
                          ("gemm256", lambda: gpu.gemm_bf16(a, bt, out=c)),
                          ("torch_bf16_out", lambda: torch.mm(a, bt.t()))):

@@ -53,6 +53,8 @@ def parse(argv=None):
     p.add_argument("--arch", choices=("auto", "inprocess", "sharded"), default="auto",
                    help="inprocess: one process, controllers share the store; sharded: namespace-sharded control "
                         "plane, one rank per GPU, native apiserver (auto: sharded when WORLD_SIZE > 1)")
+    p.add_argument("--no-sharded-baseline", action="store_true",
+                   help="n=1 in-process run: skip the extra single-rank sharded measurement")
     p.add_argument("--json-out", default=None)
     return p.parse_args(argv)
 
@@ -157,13 +159,7 @@ def main(argv=None):
     if args.arch == "sharded" or (args.arch == "auto" and world > 1):
         from odh_kubeflow_amd.parallel.bench_dist import run_distributed
 
-        if "MASTER_ADDR" not in os.environ:  # single rank without a launcher
-            import socket
-
-            with socket.socket() as s:
-                s.bind(("127.0.0.1", 0))
-                os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(s.getsockname()[1]),
-                                  RANK="0", WORLD_SIZE="1", LOCAL_RANK="0")
+        _single_rank_env()
         return run_distributed(args)
     import torch
 
@@ -185,12 +181,36 @@ def main(argv=None):
     if torch.cuda.is_available() and torch_sync:
         torch_sync()
     out = report(args, n, res)
+    out["config"]["architecture"] = "inprocess"
+    if n == 1 and args.arch == "auto" and not args.no_sharded_baseline:
+        # the multi-GPU runs (torchrun) use the sharded architecture; measure it at one GPU
+        # too, so the scaling curve has a same-architecture base point
+        sh = _sharded_single_rank(args)
+        out["sharded_n1"] = {k: sh.get(k) for k in ("value", "ms_per_step", "p50_ready_ms", "p95_ready_ms",
+                                                    "notebooks_ready_per_s", "reconciles_per_notebook")}
     if rank == 0:
         print(json.dumps(out), flush=True)
         if args.json_out:
             with open(args.json_out, "w") as f:
                 json.dump(out, f, indent=1)
     return 0
+
+
+def _single_rank_env() -> None:
+    if "MASTER_ADDR" not in os.environ:  # single rank without a launcher
+        import socket
+
+        with socket.socket() as s:
+            s.bind(("127.0.0.1", 0))
+            os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(s.getsockname()[1]),
+                              RANK="0", WORLD_SIZE="1", LOCAL_RANK="0")
+
+
+def _sharded_single_rank(args) -> dict:
+    from odh_kubeflow_amd.parallel.bench_dist import measure
+
+    _single_rank_env()
+    return measure(args) or {}
 
 
 def report(args, n, res) -> dict:

@@ -203,8 +203,13 @@ class OpenshiftNotebookReconciler:
 
             steps += [auth.cleanup_kube_rbac_proxy_crb(c, nb), routes()]
         if self.blocking_lock_removal:  # reference emulation: strictly sequential
-            for st in steps:
-                await st
+            for i, st in enumerate(steps):
+                try:
+                    await st
+                except BaseException:
+                    for rest in steps[i + 1:]:
+                        rest.close()  # never started: no "coroutine was never awaited"
+                    raise
         else:
             results = await asyncio.gather(*steps, return_exceptions=True)
             errs = [r for r in results if isinstance(r, BaseException)]

@@ -95,12 +95,12 @@ class Scheme:
 
     def resolve(self, ref) -> ResourceInfo:
         """Accept a ResourceInfo, a GVK, ``"group/version/Kind"`` / ``"v1/Kind"`` or an object."""
-        if isinstance(ref, ResourceInfo):
-            return ref
-        if isinstance(ref, str):
+        if type(ref) is str:  # the hot path: kind constants, ~700 calls per notebook lifecycle
             hit = self._str_cache.get(ref)
             if hit is not None:
                 return hit
+        elif isinstance(ref, ResourceInfo):
+            return ref
         if isinstance(ref, GVK):
             info = self.for_kind(ref.group, ref.kind)
         elif isinstance(ref, dict):

@@ -66,6 +66,17 @@ def _rccl_check(torch, dist, local_rank: int) -> Optional[float]:
 
 
 def run_distributed(args) -> int:
+    out = measure(args)
+    if out is not None:
+        print(json.dumps(out), flush=True)
+        if args.json_out:
+            with open(args.json_out, "w") as f:
+                json.dump(out, f, indent=1)
+    return 0
+
+
+def measure(args) -> Optional[dict]:
+    """Run the sharded benchmark on this rank; rank 0 returns the report dict."""
     dist, torch = _dist_init()
     rank, world = dist.get_rank(), dist.get_world_size()
     local_rank = int(os.environ.get("LOCAL_RANK", rank))
@@ -83,6 +94,7 @@ def run_distributed(args) -> int:
             return await gpu.startup_probe(devices, local_index=lambda d: dev)
     rccl_ms = _rccl_check(torch, dist, local_rank) if not args.no_gpu_probe else None
     res = asyncio.run(_main(args, dist, torch, rank, world, local_rank, probe))
+    out = None
     if rank == 0:
         from bench import report  # noqa: E402  (bench.py is the entry point on sys.path)
 
@@ -92,13 +104,9 @@ def run_distributed(args) -> int:
         out["config"]["architecture"] = "sharded"
         if rccl_ms is not None:
             out["rccl_allreduce_check_ms"] = round(rccl_ms, 3)
-        print(json.dumps(out), flush=True)
-        if args.json_out:
-            with open(args.json_out, "w") as f:
-                json.dump(out, f, indent=1)
     dist.barrier()
     dist.destroy_process_group()
-    return 0
+    return out
 
 
 async def _main(args, dist, torch, rank: int, world: int, local_rank: int, probe) -> dict:

@@ -214,6 +214,7 @@ class CachedClient(Client):
         self.writer = writer
         self.uncached = {SCHEME.resolve(k).key for k in uncached}
         self._written: Dict[Tuple[str, str, str], int] = {}
+        self._ensured: set = set()  # kinds whose informer is known synced and served
         self.fresh_reads = 0
 
     def _note(self, out) -> None:
@@ -234,9 +235,13 @@ class CachedClient(Client):
         return SCHEME.resolve(kind).key in self.uncached
 
     async def _ensure(self, kind) -> None:
+        if type(kind) is str and kind in self._ensured:
+            return
         ensure = getattr(self.reader, "ensure_informer", None)
         if ensure is not None:
-            await ensure(kind)
+            await ensure(kind)  # raises NoKindMatch while the kind is not served
+        if type(kind) is str:
+            self._ensured.add(kind)
 
     async def get(self, kind, name, namespace=None):
         if self._live(kind) or LIVE_READS.get():

@@ -209,9 +209,14 @@ class InformerCache(Reader, EventSource):
         self.watch_timeout_s = watch_timeout_s
         self._informers: Dict[Tuple[str, Optional[str]], _Informer] = {}
         self._by_kind: Dict[str, List[_Informer]] = {}
+        self._by_ref: Dict[str, List[_Informer]] = {}
         self._hid = 0
 
     def _group(self, kind) -> List[_Informer]:
+        if type(kind) is str:
+            hit = self._by_ref.get(kind)
+            if hit is not None:
+                return hit
         info = SCHEME.resolve(kind)
         infs = self._by_kind.get(info.key)
         if infs is None:
@@ -226,6 +231,8 @@ class InformerCache(Reader, EventSource):
                 inf.task = asyncio.ensure_future(inf.run())
                 infs.append(inf)
             self._by_kind[info.key] = infs
+        if type(kind) is str:
+            self._by_ref[kind] = infs
         return infs
 
     def _for_ns(self, kind, namespace: Optional[str]) -> List[_Informer]:
@@ -325,3 +332,4 @@ class InformerCache(Reader, EventSource):
                     pass
         self._informers.clear()
         self._by_kind.clear()
+        self._by_ref.clear()

@@ -73,7 +73,20 @@ class Quantity:
         return f"Quantity({self.text!r})"
 
 
+_QCACHE: dict = {}
+
+
 def parse_quantity(text) -> Quantity:
+    """Parsed quantities are immutable and the same few strings recur on every pod
+    (``"1"``, ``"100m"``, ``"64Mi"``): memoized."""
+    if type(text) is str:
+        q = _QCACHE.get(text)
+        if q is None:
+            q = Quantity(text)
+            if len(_QCACHE) > 4096:
+                _QCACHE.clear()
+            _QCACHE[text] = q
+        return q
     return Quantity(text)
 
 

@@ -51,10 +51,11 @@ def parse(argv=None):
     p.add_argument("--transport", choices=("inprocess", "http", "native"), default="inprocess",
                    help="managers share the store (inprocess) or talk REST/watch to the apiserver (http)")
     p.add_argument("--arch", choices=("auto", "inprocess", "sharded"), default="auto",
-                   help="inprocess: one process, controllers share the store; sharded: namespace-sharded control "
-                        "plane, one rank per GPU, native apiserver (auto: sharded when WORLD_SIZE > 1)")
-    p.add_argument("--no-sharded-baseline", action="store_true",
-                   help="n=1 in-process run: skip the extra single-rank sharded measurement")
+                   help="sharded: namespace-sharded control plane, one rank per GPU, native apiserver (the headline "
+                        "at every N); inprocess: one process, controllers share the store (envtest-style); auto: "
+                        "sharded, plus the in-process figure as a secondary field at N=1")
+    p.add_argument("--no-inprocess-baseline", action="store_true",
+                   help="N=1 auto: skip the extra in-process (envtest-style) measurement")
     p.add_argument("--json-out", default=None)
     return p.parse_args(argv)
 
@@ -153,14 +154,35 @@ def _odh_available() -> bool:
 
 def main(argv=None):
     args = parse(argv)
-    world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     n = args.gpus
-    if args.arch == "sharded" or (args.arch == "auto" and world > 1):
-        from odh_kubeflow_amd.parallel.bench_dist import run_distributed
-
+    if args.arch in ("auto", "sharded"):
+        # production architecture at every N (one control-plane shard per MI355X rank against
+        # the native apiserver), so the 1/2/4/8 curve compares like with like
+        inproc = None
+        if n == 1 and args.arch == "auto" and not args.no_inprocess_baseline:
+            # BASELINE config #1 (envtest-style: controllers share the in-process store)
+            inproc = _run_inprocess(args, n)
         _single_rank_env()
-        return run_distributed(args)
+        from odh_kubeflow_amd.parallel.bench_dist import measure
+
+        out = measure(args)
+        if out is not None and inproc is not None:
+            out["inprocess_n1"] = {k: inproc.get(k) for k in (
+                "value", "ms_per_step", "p50_ready_ms", "p95_ready_ms", "notebooks_ready_per_s",
+                "reconciles_per_notebook", "p50_teardown_ms")}
+    else:
+        out = _run_inprocess(args, n)
+    if rank == 0 and out is not None:
+        print(json.dumps(out), flush=True)
+        if args.json_out:
+            with open(args.json_out, "w") as f:
+                json.dump(out, f, indent=1)
+    return 0
+
+
+def _run_inprocess(args, n: int) -> dict:
+    """One process: every controller, the webhook, the node agents share the object store."""
     import torch
 
     probe = None
@@ -177,23 +199,11 @@ def main(argv=None):
             return await gpu.startup_probe(devices, local_index=lambda d: d % ndev)
 
     res = asyncio.run(run_local(args, n, probe))
-    torch_sync = getattr(torch.cuda, "synchronize", None)
-    if torch.cuda.is_available() and torch_sync:
-        torch_sync()
+    if torch.cuda.is_available():
+        torch.cuda.synchronize()
     out = report(args, n, res)
     out["config"]["architecture"] = "inprocess"
-    if n == 1 and args.arch == "auto" and not args.no_sharded_baseline:
-        # the multi-GPU runs (torchrun) use the sharded architecture; measure it at one GPU
-        # too, so the scaling curve has a same-architecture base point
-        sh = _sharded_single_rank(args)
-        out["sharded_n1"] = {k: sh.get(k) for k in ("value", "ms_per_step", "p50_ready_ms", "p95_ready_ms",
-                                                    "notebooks_ready_per_s", "reconciles_per_notebook")}
-    if rank == 0:
-        print(json.dumps(out), flush=True)
-        if args.json_out:
-            with open(args.json_out, "w") as f:
-                json.dump(out, f, indent=1)
-    return 0
+    return out
 
 
 def _single_rank_env() -> None:
@@ -204,13 +214,6 @@ def _single_rank_env() -> None:
             s.bind(("127.0.0.1", 0))
             os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(s.getsockname()[1]),
                               RANK="0", WORLD_SIZE="1", LOCAL_RANK="0")
-
-
-def _sharded_single_rank(args) -> dict:
-    from odh_kubeflow_amd.parallel.bench_dist import measure
-
-    _single_rank_env()
-    return measure(args) or {}
 
 
 def report(args, n, res) -> dict:

@@ -28,6 +28,11 @@ from ..models.errors import ApiError, is_conflict, is_not_found
 from ..models.notebook import GPU_IDS_ANNOTATION, GPU_RESOURCE, gpu_request
 
 GPU_INDEX_LABEL = "amd.com/gpu-index"
+# Namespace label naming the GPU index(es) whose node agent runs in the same control-plane
+# shard as the namespace's controllers (``parallel/shard.py``).  The device allocator tries
+# those GPUs first, so a shard's pods start inside the shard's own process instead of
+# waiting on another rank's event loop; a busy preferred GPU falls back to bin-packing.
+GPU_AFFINITY_LABEL = "amd.com/gpu-affinity"
 PROBE_CONDITION = "amd.com/GPUProbe"
 from ..runtime.controller import Request, Result, pred_funcs
 from ..utils.quantity import parse_quantity
@@ -89,7 +94,11 @@ def _tolerates(pod: dict, node: dict) -> bool:
 
 
 class SchedulerController:
-    """Binds pods to nodes and allocates GPU device indices (bin-packing by lowest free index)."""
+    """Binds pods to nodes and allocates GPU device indices.
+
+    Policy: the GPUs named by the pod namespace's ``amd.com/gpu-affinity`` label first (if
+    free), then bin-packing by lowest free index.
+    """
 
     def __init__(self, client, reader, recorder, scheduler_name: str = "default-scheduler"):
         self.client = client
@@ -124,6 +133,17 @@ class SchedulerController:
             mem += amem
             gpus.update(aids)
         return {"cpu": cpu, "memory": mem, "gpus": gpus}
+
+    def _preferred_gpus(self, namespace: str) -> List[int]:
+        ns = self.reader.get(kinds.NAMESPACE, namespace)
+        val = m.labels(ns).get(GPU_AFFINITY_LABEL) if ns is not None else None
+        if not val:
+            return []
+        out = []
+        for x in val.replace("_", ",").split(","):
+            if x.strip().isdigit():
+                out.append(int(x))
+        return out
 
     def forget(self, pod: dict) -> None:
         self._assumed.pop(m.uid(pod), None)
@@ -162,6 +182,10 @@ class SchedulerController:
             if alloc.get("memory") and used["memory"] + need["memory"] > float(parse_quantity(alloc["memory"]).value):
                 reasons.append("Insufficient memory")
                 continue
+            if need["gpu"]:
+                pref = self._preferred_gpus(m.namespace(pod))
+                if pref:
+                    free = [i for i in pref if i in free] + [i for i in free if i not in pref]
             ids = free[: need["gpu"]]
             patch = {"spec": {"nodeName": m.name(node)}}
             if ids:
@@ -212,6 +236,8 @@ class SchedulerController:
         return (mgr.builder().named("scheduler").for_(kinds.POD, [unbound])
                 .watches(kinds.POD, pods_released, [pred_funcs(create=lambda o: False, update=lambda o, old: False,
                                                                delete=lambda o: True)])
+                # namespaces carry the gpu-affinity label: synced before the first decision
+                .watches(kinds.NAMESPACE, lambda o: [], [lambda et, o, old: False])
                 .with_options(max_concurrent_reconciles=max_concurrent).complete(self))
 
 

@@ -16,7 +16,9 @@ plane the way the node is scaled — one process per GPU — by sharding it on n
   label — a shard receives only the watch events of the objects it owns, so per-shard
   work stays constant as shards are added;
 * the node agent of GPU ``r`` watches only pods labelled ``amd.com/gpu-index=r`` (set by
-  the scheduler together with the ``amd.com/gpu-ids`` allocation);
+  the scheduler together with the ``amd.com/gpu-ids`` allocation); the shard labels its
+  namespace ``amd.com/gpu-affinity=r`` so the allocator gives its pods GPU ``r`` while it
+  is free — pod start-up then stays inside the shard's own process;
 * the bootstrap shard (rank 0) also runs the cluster-wide singletons: scheduler (with
   ``amd.com/gpu`` bin-packing) and Node registration.  GC runs in the apiserver.
 """
@@ -75,7 +77,7 @@ class ControlPlaneShard:
         from ..controllers.notebook import NotebookEventReemitter, NotebookReconciler
         from ..controllers.metrics import NotebookMetrics
         from ..kubelet.agent import NodeAgent
-        from ..kubelet.node import GPU_INDEX_LABEL, SchedulerController
+        from ..kubelet.node import GPU_AFFINITY_LABEL, GPU_INDEX_LABEL, SchedulerController
         from ..kubelet.statefulset import StatefulSetController
         from ..runtime.informer import InformerCache
         from ..runtime.rest import RestClient, RestConfig
@@ -87,7 +89,8 @@ class ControlPlaneShard:
         if cfg.bootstrap:
             for ns in ("default", cfg.controller_namespace):
                 await self.ensure_namespace(ns)
-        await self.ensure_namespace(cfg.namespace)
+        # the namespace's pods prefer this rank's GPU (its node agent lives in this process)
+        await self.ensure_namespace(cfg.namespace, {GPU_AFFINITY_LABEL: str(cfg.gpu)})
         # The reference keeps ConfigMaps/Secrets out of its (cluster-wide) cache to bound
         # memory and reads them live.  A shard's cache spans two namespaces, so it caches
         # them in full and the webhook / odh reconciler read them locally.
@@ -169,14 +172,17 @@ class ControlPlaneShard:
 
     # ------------------------------------------------------------------ helpers
 
-    async def ensure_namespace(self, ns: str) -> None:
+    async def ensure_namespace(self, ns: str, labels: Optional[Dict[str, str]] = None) -> None:
         from ..models.errors import ApiError, is_already_exists
 
+        meta = {"name": ns, **({"labels": dict(labels)} if labels else {})}
         try:
-            await self.rest.create({"apiVersion": "v1", "kind": "Namespace", "metadata": {"name": ns}})
+            await self.rest.create({"apiVersion": "v1", "kind": "Namespace", "metadata": meta})
         except ApiError as e:
             if not is_already_exists(e):
                 raise
+            if labels:
+                await self.rest.patch(kinds.NAMESPACE, {"metadata": {"labels": dict(labels)}}, name=ns)
 
     def peek(self, kind, name: str, namespace: Optional[str] = None) -> Optional[dict]:
         return self.cache.get(kind, name, namespace)

@@ -169,6 +169,28 @@ def test_eight_notebooks_fill_eight_gpus_ninth_unschedulable(run):
     run(go())
 
 
+def test_gpu_affinity_label_steers_allocation(run):
+    """Namespace ``amd.com/gpu-affinity`` first, lowest free index when the preferred GPU is taken."""
+    async def go():
+        async with LocalCluster(ClusterConfig()) as cl:
+            await cl.admin.create({"apiVersion": "v1", "kind": "Namespace",
+                                   "metadata": {"name": "team", "labels": {"amd.com/gpu-affinity": "5_6"}}})
+            await cl.ensure_namespace("other")
+            await cl.admin.create(notebook("a", "team", gpus=1))
+            assert await cl.wait_for(lambda: cl.notebook_ready("a", "team"), 10)
+            await cl.admin.create(notebook("b", "team", gpus=2))
+            await cl.admin.create(notebook("c", "other", gpus=1))
+            assert await cl.wait_for(lambda: cl.notebook_ready("b", "team") and cl.notebook_ready("c", "other"), 10)
+
+            def ids(nm, ns):
+                return m.annotations(cl.store.peek(kinds.POD, f"{nm}-0", ns))["amd.com/gpu-ids"]
+            assert ids("a", "team") == "5"
+            assert ids("b", "team") == "6,0"  # 5 is taken: 6, then bin-packing from the lowest index
+            assert ids("c", "other") == "1"
+            assert m.labels(cl.store.peek(kinds.POD, "b-0", "team"))["amd.com/gpu-index"] == "6"
+    run(go())
+
+
 def test_restart_annotation_deletes_pod(run):
     async def go():
         async with LocalCluster(ClusterConfig()) as cl:

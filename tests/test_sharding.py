@@ -220,10 +220,12 @@ def test_two_shards_one_native_apiserver(run):
                 routes = sh.cache.list(kinds.HTTP_ROUTE)
                 assert routes and {m.labels(r)["notebook-namespace"] for r in routes} == {f"bench-{i}"}
                 assert sh.webhook.requests >= 1
-            # the two pods run on distinct GPUs, each started by that GPU's node agent
-            pods = [p for sh in shards for p in sh.cache.list(kinds.POD)]
-            assert sorted(m.annotations(p)["amd.com/gpu-ids"] for p in pods) == ["0", "1"]
-            assert all(m.labels(p)["amd.com/gpu-index"] == m.annotations(p)["amd.com/gpu-ids"] for p in pods)
+            # each shard's pod got the shard's own GPU (namespace gpu-affinity), so it was
+            # started by the node agent living in the same process
+            for i, sh in enumerate(shards):
+                pods = sh.cache.list(kinds.POD)
+                assert [m.annotations(p)["amd.com/gpu-ids"] for p in pods] == [str(i)]
+                assert [m.labels(p)["amd.com/gpu-index"] for p in pods] == [str(i)]
             assert [sh.agent.runtimes[0].started for sh in shards] == [1, 1]
             for i, sh in enumerate(shards):
                 for j in range(1):

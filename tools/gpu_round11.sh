@@ -11,5 +11,5 @@ timeout -k 10 240 python __graft_entry__.py smoke > gpurun_out/smoke.log 2>&1 ||
 tail -1 gpurun_out/smoke.log
 timeout -k 10 400 python bench.py --steps 100 --warmup 5 > gpurun_out/b11_n1.log 2>&1 || { tail -40 gpurun_out/b11_n1.log; exit 1; }
 grep '^{' gpurun_out/b11_n1.log
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof11 -o run -- python3 bench.py --steps 40 --warmup 3 --no-sharded-baseline > gpurun_out/b11_prof.log 2>&1 || { tail -40 gpurun_out/b11_prof.log; exit 1; }
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof11 -o run -- python3 bench.py --steps 40 --warmup 3 --no-inprocess-baseline > gpurun_out/b11_prof.log 2>&1 || { tail -40 gpurun_out/b11_prof.log; exit 1; }
 find gpurun_out/prof11 -name '*stats*' | head

@@ -116,6 +116,18 @@ def test_unmount_without_feast_config_is_a_no_op():
 # ------------------------------------------------------------------ through admission
 
 
+async def live(cl, kind, name, namespace=None):
+    """Read through to the apiserver (the cluster view is eventually consistent over REST)."""
+    from odh_kubeflow_amd.models.errors import ApiError, is_not_found
+
+    try:
+        return await cl.admin.get(kind, name, namespace)
+    except ApiError as e:
+        if is_not_found(e):
+            return None
+        raise
+
+
 def _cluster():
     return LocalCluster(ClusterConfig(odh=True, webhook=True, kf=False, gc=False,
                                       env={"SET_PIPELINE_RBAC": "false", "SET_PIPELINE_SECRET": "false"}))
@@ -129,7 +141,7 @@ def test_admission_label_enabled_with_configmap(run):
                                    "metadata": {"name": "nb-feast-config", "namespace": "feast"},
                                    "data": {"feature_store.yaml": "project: feast_project"}})
             await cl.admin.create(notebook("nb", "feast", labels={LABEL: "true"}))
-            nb = cl.store.peek(kinds.NOTEBOOK, "nb", "feast")
+            nb = await live(cl, kinds.NOTEBOOK, "nb", "feast")
             assert feast_volumes(nb) == [{"name": VOL, "configMap": {"name": "nb-feast-config"}}]
             assert feast_mounts(nb) == [MOUNT]
     run(go())
@@ -141,7 +153,7 @@ def test_admission_label_enabled_without_configmap_still_mounts_reference(run):
         async with _cluster() as cl:
             await cl.ensure_namespace("feast")
             await cl.admin.create(notebook("nb", "feast", labels={LABEL: "true"}))
-            nb = cl.store.peek(kinds.NOTEBOOK, "nb", "feast")
+            nb = await live(cl, kinds.NOTEBOOK, "nb", "feast")
             assert feast_volumes(nb) == [{"name": VOL, "configMap": {"name": "nb-feast-config"}}]
     run(go())
 
@@ -152,7 +164,7 @@ def test_admission_label_disabled_skips_mount(run, value):
         async with _cluster() as cl:
             await cl.ensure_namespace("feast")
             await cl.admin.create(notebook("nb", "feast", labels={LABEL: value}))
-            assert feast_volumes(cl.store.peek(kinds.NOTEBOOK, "nb", "feast")) == []
+            assert feast_volumes(await live(cl, kinds.NOTEBOOK, "nb", "feast")) == []
     run(go())
 
 
@@ -164,7 +176,7 @@ def test_admission_label_removed_unmounts_on_update(run):
             # stopped notebook: the restart guard lets webhook-only template changes through
             await cl.admin.patch(kinds.NOTEBOOK, {"metadata": {"labels": {LABEL: None}}}, name="nb",
                                  namespace="feast")
-            nb = cl.store.peek(kinds.NOTEBOOK, "nb", "feast")
+            nb = await live(cl, kinds.NOTEBOOK, "nb", "feast")
             assert "kubeflow-resource-stopped" in nb["metadata"]["annotations"]
             assert feast_volumes(nb) == [] and feast_mounts(nb) == []
     run(go())
@@ -178,6 +190,6 @@ def test_admission_premounted_volume_with_disabled_label_is_unmounted(run):
             spec(nb)["volumes"] = [{"name": VOL, "configMap": {"name": "some-config"}}]
             spec(nb)["containers"][0]["volumeMounts"] = [{"name": VOL, "mountPath": MOUNT["mountPath"]}]
             await cl.admin.create(nb)
-            stored = cl.store.peek(kinds.NOTEBOOK, "nb", "feast")
+            stored = await live(cl, kinds.NOTEBOOK, "nb", "feast")
             assert not feast.is_feast_mounted(stored) and feast_mounts(stored) == []
     run(go())

@@ -86,6 +86,18 @@ CASES = [
 ]
 
 
+async def live(cl, kind, name, namespace=None):
+    """Read through to the apiserver (the cluster view is eventually consistent over REST)."""
+    from odh_kubeflow_amd.models.errors import ApiError, is_not_found
+
+    try:
+        return await cl.admin.get(kind, name, namespace)
+    except ApiError as e:
+        if is_not_found(e):
+            return None
+        raise
+
+
 def _cluster():
     return LocalCluster(ClusterConfig(odh=False, webhook=True, kf=False, gc=False, openshift=True,
                                       env={"SET_PIPELINE_RBAC": "false", "SET_PIPELINE_SECRET": "false"}))
@@ -107,8 +119,8 @@ def test_runtime_images_configmap_and_mount(run, name, ist, want):
             nb = notebook("test-notebook-runtime", NS)
             nb["spec"]["template"]["spec"]["containers"].append({"name": "sidecar", "image": "s"})
             await cl.admin.create(nb)
-            cm = cl.store.peek(kinds.CONFIG_MAP, CM, NS)
-            stored = cl.store.peek(kinds.NOTEBOOK, "test-notebook-runtime", NS)
+            cm = await live(cl, kinds.CONFIG_MAP, CM, NS)
+            stored = await live(cl, kinds.NOTEBOOK, "test-notebook-runtime", NS)
             if want is None:
                 assert cm is None
                 assert _mounted(stored) == (False, False)
@@ -127,8 +139,8 @@ def test_configmap_without_data_is_not_mounted(run):
             await cl.admin.create({"apiVersion": "v1", "kind": "ConfigMap",
                                    "metadata": {"name": CM, "namespace": NS}, "data": {}})
             await cl.admin.create(notebook("test-notebook-runtime-empty-cf", NS))
-            assert cl.store.peek(kinds.CONFIG_MAP, CM, NS) is not None
-            stored = cl.store.peek(kinds.NOTEBOOK, "test-notebook-runtime-empty-cf", NS)
+            assert await live(cl, kinds.CONFIG_MAP, CM, NS) is not None
+            stored = await live(cl, kinds.NOTEBOOK, "test-notebook-runtime-empty-cf", NS)
             assert _mounted(stored) == (False, False)
     run(go())
 
@@ -140,12 +152,12 @@ def test_configmap_follows_imagestream_changes_on_next_admission(run):
             await cl.ensure_namespace(NS)
             await cl.admin.create(copy.deepcopy(CASES[1][1]))
             await cl.admin.create(notebook("a", NS))
-            assert set(cl.store.peek(kinds.CONFIG_MAP, CM, NS)["data"]) == {"python-3.11-ubi9.json"}
+            assert set((await live(cl, kinds.CONFIG_MAP, CM, NS))["data"]) == {"python-3.11-ubi9.json"}
             ist = await cl.admin.get(kinds.IMAGE_STREAM, "some-image", CENTRAL)
             ist["spec"]["tags"].append(tag("t2", "quay.io/x/y", "R Studio"))
             await cl.admin.update(ist)
             await cl.admin.create(notebook("b", NS))
-            assert set(cl.store.peek(kinds.CONFIG_MAP, CM, NS)["data"]) == {"python-3.11-ubi9.json", "r-studio.json"}
+            assert set((await live(cl, kinds.CONFIG_MAP, CM, NS))["data"]) == {"python-3.11-ubi9.json", "r-studio.json"}
     run(go())
 
 

@@ -13,6 +13,9 @@
 //    remap so the tiles of one XCD share A panels in that XCD's L2.  Every workgroup
 //    records the XCD (HW_REG_XCC_ID) it ran on, so a verification failure is pinned to
 //    the chiplet that produced it.
+//  * odh_probe_gemm_verify — the start-up probe's GEMM: 256×256 tile, BK=32 stages in a
+//    4-buffer LDS-DMA ring with three stages in flight across counted-vmcnt raw barriers,
+//    result checked in registers (no C store); 1.1 PFLOP/s bf16 at 4096³ on MI355X.
 //  * odh_probe_fill / odh_probe_verify — exact integer-valued operands whose product
 //    has a closed form (period 35 in k), so the check needs no host reference and no
 //    second GEMM: every element is compared bit-exactly on the GPU.
@@ -319,6 +322,216 @@ __global__ __launch_bounds__(G_THREADS, 1) void gemm256_kernel(
 
 bool gemm256_ok(int M, int N, int K) { return M % G_BM == 0 && N % G_BN == 0 && K % G_BK == 0; }
 
+// ---------------------------------------------------------------------------------------
+// Deep-pipelined 256×256 tile: BK = 32 stages in a 4-buffer LDS ring (4 × 32 KiB), with
+// THREE stages in flight across every barrier.  At ~1 workgroup per CU the HBM/MALL
+// latency of a stage (≈1-2 µs under load) is longer than one BK=64 tile of MFMA work
+// (≈0.9 µs at peak), so the 2-buffer kernel above stalls on its per-tile vmcnt(0); here
+// the wait is a COUNTED vmcnt (the two younger stages stay outstanding) followed by a raw
+// s_barrier (a __syncthreads() fence would drain the LDS-DMA queue), and the stage issued
+// after the barrier refills the buffer every wave finished reading one iteration ago.
+// All LDS (ring + the verify table) is ONE __shared__ array, so hipcc does not fence the
+// ds_reads of a stage behind the in-flight DMA of younger stages.
+// LDS image per operand stage: 256 rows × 4 chunks of 16 B; slot s of row r holds K-chunk
+// s ^ ((r >> 2) & 3) (conflict-free 16-lane ds_read_b128 groups), applied on the SOURCE
+// address because the DMA image is lane-linear.
+
+constexpr int D_BK = 32;
+constexpr int D_CH = D_BK / 8;            // 16-byte chunks per row
+constexpr int D_NBUF = 4;
+constexpr int D_TILE = G_BM * D_CH;       // uint4 per operand stage (1024 = 16 KiB)
+constexpr int D_RING = D_NBUF * 2 * D_TILE;
+
+__device__ __forceinline__ int dswz(int r, int c) { return r * D_CH + (c ^ ((r >> 2) & 3)); }
+
+template <bool VERIFY, bool XB = false>
+__global__ __launch_bounds__(G_THREADS, 1) void gemm256d_kernel(
+    const uint4* __restrict__ A, const uint4* __restrict__ Bt, float* __restrict__ C, int M, int N, int K,
+    int* __restrict__ tile_xcd, int* __restrict__ xcd_blocks, unsigned* __restrict__ err_total,
+    unsigned* __restrict__ err_xcd) {
+  __shared__ uint4 lds[D_RING + 9];  // ring, then 35 floats of the probe's expected values
+  float* expect = reinterpret_cast<float*>(lds + D_RING);
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int w = tid >> 6;
+  const int wm = w >> 2, wn = w & 3;
+  const int tiles_n = N / G_BN;
+  const int nwg = gridDim.x;
+  const int orig = blockIdx.x, xq = nwg >> 3, xr = nwg & 7, xs = orig & 7;
+  const int bid = (xs < xr ? xs * (xq + 1) : xr * (xq + 1) + (xs - xr) * xq) + (orig >> 3);
+  const int tm = bid / tiles_n;
+  const int tn = bid - tm * tiles_n;
+  const unsigned xcc = xcc_id();
+  if (tid == 0) {
+    if (tile_xcd) tile_xcd[bid] = (int)xcc;
+    if (xcd_blocks) atomicAdd(&xcd_blocks[xcc], 1);
+  }
+  if (VERIFY && tid < 35) expect[tid] = (float)probe_expect(tid / 7, tid % 7, K);
+
+  const size_t kch = (size_t)(K / 8);
+  const uint4* Ag = A + (size_t)tm * G_BM * kch;
+  const uint4* Bg = Bt + (size_t)tn * G_BN * kch;
+
+  // stage kt → ring slot b: wave w fills rows [32w, 32w + 32) of A and of B (16 rows per
+  // instruction); 4 DMA instructions per thread per stage
+  auto issue = [&](int kt, int b) {
+    uint4* la = lds + (b * 2 + 0) * D_TILE;
+    uint4* lb = lds + (b * 2 + 1) * D_TILE;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int base = (w * 2 + i) * 64;
+      const int p = base + lane;
+      const int row = p >> 2;
+      const int c = (p & 3) ^ ((row >> 2) & 3);
+      const size_t g = (size_t)row * kch + (size_t)kt * D_CH + c;
+      __builtin_amdgcn_global_load_lds(Ag + g, la + base, 16, 0, 0);
+      __builtin_amdgcn_global_load_lds(Bg + g, lb + base, 16, 0, 0);
+    }
+  };
+
+  f32x16 acc[4][2];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  const int nkt = K / D_BK;
+  const int lr = lane & 31, lh = lane >> 5;
+  // fragments of one stage: both k-substeps (lane half h holds k = 16s + 8h .. +7)
+  auto read_stage = [&](int kt, bf16x8 (&af)[2][4], bf16x8 (&bfr)[2][2]) {
+    const int cur = kt & 3;
+    const uint4* sa = lds + (cur * 2 + 0) * D_TILE;
+    const uint4* sb = lds + (cur * 2 + 1) * D_TILE;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const int c = 2 * s + lh;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) af[s][i] = __builtin_bit_cast(bf16x8, sa[dswz(wm * 128 + i * 32 + lr, c)]);
+#pragma unroll
+      for (int j = 0; j < 2; ++j) bfr[s][j] = __builtin_bit_cast(bf16x8, sb[dswz(wn * 64 + j * 32 + lr, c)]);
+    }
+  };
+  auto mfma_stage = [&](const bf16x8 (&af)[2][4], const bf16x8 (&bfr)[2][2]) {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[s][i], bfr[s][j], acc[i][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+  };
+
+  if (!XB) {
+    issue(0, 0);
+    if (nkt > 1) issue(1, 1);
+    if (nkt > 2) issue(2, 2);
+    for (int kt = 0; kt < nkt; ++kt) {
+      // retire THIS wave's DMA of stage kt (younger stages stay in flight), then the barrier
+      // makes every wave's part visible and proves stage kt-1's slot is no longer read
+      const int ahead = nkt - 1 - kt;
+      if (ahead >= 2)
+        asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+      else if (ahead == 1)
+        asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      else
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      if (kt + 3 < nkt) issue(kt + 3, (kt + 3) & 3);
+      bf16x8 af[2][4], bfr[2][2];
+      read_stage(kt, af, bfr);
+      mfma_stage(af, bfr);
+    }
+  } else {
+    // XB: the barrier that publishes stage kt+1 comes BEFORE stage kt's MFMAs, so stage kt+1's
+    // ds_reads run under stage kt's matrix work (two fragment sets in registers); the slot of
+    // stage kt (already in registers: lgkmcnt(0) before the barrier) is refilled with kt+4,
+    // so four stages are in flight.
+    issue(0, 0);
+    if (nkt > 1) issue(1, 1);
+    if (nkt > 2) issue(2, 2);
+    if (nkt > 3) issue(3, 3);
+    {
+      const int ahead = nkt - 1 < 3 ? nkt - 1 : 3;
+      if (ahead == 3)
+        asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+      else if (ahead == 2)
+        asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+      else if (ahead == 1)
+        asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      else
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+    }
+    bf16x8 xa[2][4], xb[2][2], ya[2][4], yb[2][2];
+    read_stage(0, xa, xb);
+    for (int kt = 0; kt < nkt; kt += 2) {
+      // stage kt in x; publish kt+1, read it into y, MFMA x
+      if (kt + 1 < nkt) {
+        const int ahead = nkt - 2 - kt;  // issued stages younger than kt+1 (at most kt+3)
+        if (ahead >= 2)
+          asm volatile("s_waitcnt vmcnt(8) lgkmcnt(0)" ::: "memory");
+        else if (ahead == 1)
+          asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)" ::: "memory");
+        else
+          asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        if (kt + 4 < nkt) issue(kt + 4, kt & 3);
+        read_stage(kt + 1, ya, yb);
+      }
+      mfma_stage(xa, xb);
+      if (kt + 1 >= nkt) break;
+      // stage kt+1 in y; publish kt+2, read it into x, MFMA y
+      if (kt + 2 < nkt) {
+        const int ahead = nkt - 3 - kt;
+        if (ahead >= 2)
+          asm volatile("s_waitcnt vmcnt(8) lgkmcnt(0)" ::: "memory");
+        else if (ahead == 1)
+          asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)" ::: "memory");
+        else
+          asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        if (kt + 5 < nkt) issue(kt + 5, (kt + 1) & 3);
+        read_stage(kt + 2, xa, xb);
+      }
+      mfma_stage(ya, yb);
+    }
+  }
+
+  unsigned bad = 0;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int col = tn * G_BN + wn * 64 + j * 32 + lr;
+      const int rbase = tm * G_BM + wm * 128 + i * 32 + 4 * lh;
+      if (VERIFY) {
+        const int c7 = col % 7;
+        const int r5 = rbase % 5;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          int rr = r5 + (r & 3) + 8 * (r >> 2);
+          rr %= 5;
+          bad += acc[i][j][r] != expect[rr * 7 + c7];
+        }
+      } else {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) C[(size_t)(rbase + (r & 3) + 8 * (r >> 2)) * N + col] = acc[i][j][r];
+      }
+    }
+  if (VERIFY) {
+    for (int off = 32; off > 0; off >>= 1) bad += __shfl_down(bad, off, 64);
+    if (lane == 0 && bad) {
+      atomicAdd(err_total, bad);
+      if (err_xcd) atomicAdd(&err_xcd[xcc], bad);
+    }
+  }
+}
+
 __device__ __forceinline__ uint16_t small_int_bf16(int v) {
   // exact for |v| < 256: take the high half of the f32 bit pattern
   return (uint16_t)(__float_as_uint((float)v) >> 16);
@@ -533,7 +746,8 @@ int odh_gemm_bf16_128(const void* A, const void* Bt, float* C, int M, int N, int
   return (int)hipGetLastError();
 }
 
-// A/B: the 256² kernel without fragment pipelining (variant 0) or with it (variant 1)
+// A/B: the 256² kernel without fragment pipelining (variant 0), with it (variant 1), or the
+// deep-pipelined BK=32 / 4-buffer ring (variant 2)
 int odh_gemm_bf16_256_variant(const void* A, const void* Bt, float* C, int M, int N, int K, int variant,
                               hipStream_t stream) {
   if (!odh_gemm_shape_ok(M, N, K) || !gemm256_ok(M, N, K)) return (int)hipErrorInvalidValue;
@@ -541,6 +755,12 @@ int odh_gemm_bf16_256_variant(const void* A, const void* Bt, float* C, int M, in
   if (variant == 0)
     gemm256_kernel<false, false><<<nwg, G_THREADS, 0, stream>>>((const uint4*)A, (const uint4*)Bt, C, M, N, K,
                                                                  nullptr, nullptr, nullptr, nullptr);
+  else if (variant == 2)
+    gemm256d_kernel<false><<<nwg, G_THREADS, 0, stream>>>((const uint4*)A, (const uint4*)Bt, C, M, N, K,
+                                                          nullptr, nullptr, nullptr, nullptr);
+  else if (variant == 3)
+    gemm256d_kernel<false, true><<<nwg, G_THREADS, 0, stream>>>((const uint4*)A, (const uint4*)Bt, C, M, N, K,
+                                                                nullptr, nullptr, nullptr, nullptr);
   else
     gemm256_kernel<false, true><<<nwg, G_THREADS, 0, stream>>>((const uint4*)A, (const uint4*)Bt, C, M, N, K,
                                                                 nullptr, nullptr, nullptr, nullptr);
@@ -573,11 +793,34 @@ int odh_probe_verify(const float* C, int M, int N, int K, const int* tile_xcd, u
 
 // probe GEMM with the check fused into the epilogue (operands from odh_probe_fill); the
 // shape must take 256² tiles.  Mismatches go to err_total / err_xcd[XCC that computed them].
+// Runs the deep-pipelined kernel (MI355X run 14, 4096³: 1104 TFLOP/s vs 996 for the
+// 2-buffer BK=64 kernel, which stays exported as odh_probe_gemm_verify_2buf for A/B).
 int odh_probe_gemm_verify(const void* A, const void* Bt, int M, int N, int K, int* tile_xcd, int* xcd_blocks,
                           unsigned* err_total, unsigned* err_xcd, hipStream_t stream) {
   if (!odh_gemm_shape_ok(M, N, K) || !gemm256_ok(M, N, K) || !err_total) return (int)hipErrorInvalidValue;
+  gemm256d_kernel<true><<<(M / G_BM) * (N / G_BN), G_THREADS, 0, stream>>>(
+      (const uint4*)A, (const uint4*)Bt, nullptr, M, N, K, tile_xcd, xcd_blocks, err_total, err_xcd);
+  return (int)hipGetLastError();
+}
+
+int odh_probe_gemm_verify_2buf(const void* A, const void* Bt, int M, int N, int K, int* tile_xcd, int* xcd_blocks,
+                               unsigned* err_total, unsigned* err_xcd, hipStream_t stream) {
+  if (!odh_gemm_shape_ok(M, N, K) || !gemm256_ok(M, N, K) || !err_total) return (int)hipErrorInvalidValue;
   gemm256_kernel<true><<<(M / G_BM) * (N / G_BN), G_THREADS, 0, stream>>>(
       (const uint4*)A, (const uint4*)Bt, nullptr, M, N, K, tile_xcd, xcd_blocks, err_total, err_xcd);
+  return (int)hipGetLastError();
+}
+
+// the same fused probe on the deep-pipelined kernel (A/B against odh_probe_gemm_verify)
+int odh_probe_gemm_verify_deep(const void* A, const void* Bt, int M, int N, int K, int* tile_xcd, int* xcd_blocks,
+                               unsigned* err_total, unsigned* err_xcd, int xb, hipStream_t stream) {
+  if (!odh_gemm_shape_ok(M, N, K) || !gemm256_ok(M, N, K) || !err_total) return (int)hipErrorInvalidValue;
+  if (xb)
+    gemm256d_kernel<true, true><<<(M / G_BM) * (N / G_BN), G_THREADS, 0, stream>>>(
+        (const uint4*)A, (const uint4*)Bt, nullptr, M, N, K, tile_xcd, xcd_blocks, err_total, err_xcd);
+  else
+    gemm256d_kernel<true><<<(M / G_BM) * (N / G_BN), G_THREADS, 0, stream>>>(
+        (const uint4*)A, (const uint4*)Bt, nullptr, M, N, K, tile_xcd, xcd_blocks, err_total, err_xcd);
   return (int)hipGetLastError();
 }
 

@@ -133,3 +133,55 @@ def test_startup_probe_async_hook(dev):
     r = asyncio.run(startup_probe([0]))
     assert r["ok"], r
     assert r["results"][0]["xcds"] == 8
+
+
+@pytest.mark.parametrize("variant", [0, 1, 2, 3])
+@pytest.mark.parametrize("m,n,k", [(256, 256, 64), (512, 768, 192), (1024, 512, 4096), (2048, 2048, 1024)])
+def test_gemm256_variants_match_fp32_reference(dev, variant, m, n, k):
+    """256² kernels: 2-buffer BK=64 (v0, v1 fragment-pipelined) and the deep BK=32 4-buffer ring (v2)."""
+    import ctypes
+
+    from odh_kubeflow_amd.ops import gpu
+
+    lib = gpu.load_library()
+    lib.odh_gemm_bf16_256_variant.argtypes = [ctypes.c_void_p] * 3 + [ctypes.c_int] * 4 + [ctypes.c_void_p]
+    g = torch.Generator(device=dev).manual_seed(7 * m + n + k + variant)
+    a = torch.randn((m, k), generator=g, device=dev).to(torch.bfloat16)
+    bt = torch.randn((n, k), generator=g, device=dev).to(torch.bfloat16)
+    c = torch.full((m, n), float("nan"), device=dev)
+    gpu._check(lib.odh_gemm_bf16_256_variant(a.data_ptr(), bt.data_ptr(), c.data_ptr(), m, n, k, variant,
+                                             torch.cuda.current_stream().cuda_stream))
+    ref = a.float() @ bt.float().t()
+    torch.cuda.synchronize()
+    err = (c - ref).abs().max().item()
+    assert err <= 1e-3 * (k ** 0.5) + 1e-3, err
+
+
+@pytest.mark.parametrize("xb", [0, 1])
+def test_deep_fused_probe_verify_counts_errors(dev, xb):
+    """The deep-pipelined probe GEMM checks in registers exactly like the 2-buffer one."""
+    from odh_kubeflow_amd.ops import gpu
+
+    lib = gpu.load_library()
+    import ctypes
+
+    lib.odh_probe_gemm_verify_deep.argtypes = list(lib.odh_probe_gemm_verify.argtypes[:-1]) + [ctypes.c_int,
+                                                                                               ctypes.c_void_p]
+    p = gpu.GpuProbe(0, m=1024, n=1024, k=1024, hbm_bytes=16 << 20)
+    s = torch.cuda.current_stream().cuda_stream
+
+    def run_deep():
+        p.counters.zero_()
+        cnt = p.counters.data_ptr()
+        gpu._check(lib.odh_probe_gemm_verify_deep(p.a.data_ptr(), p.bt.data_ptr(), p.m, p.n, p.k,
+                                                  p.tile_xcd.data_ptr(), cnt, cnt + 64, cnt + 32, xb, s))
+        torch.cuda.synchronize()
+        h = p.counters.cpu().tolist()
+        return h[16], sum(h[8:16]), sum(h[0:8])
+
+    assert run_deep() == (0, 0, 16)
+    expect_bad = int((p.bt[:, 7].float() != 0).sum().item())
+    p.a[5, 7] = (p.a[5, 7].float() + 1).to(torch.bfloat16)
+    assert run_deep() == (expect_bad, expect_bad, 16)
+    p.a[5, 7] = (p.a[5, 7].float() - 1).to(torch.bfloat16)
+    assert run_deep()[0] == 0

@@ -44,25 +44,43 @@ def main():
 
         lib.odh_gemm_bf16_256_variant.argtypes = [ctypes.c_void_p] * 3 + [ctypes.c_int] * 4 + [ctypes.c_void_p]
         st = torch.cuda.current_stream().cuda_stream
-        for v in (0, 1):
+        ref = a.float() @ bt.float().t()
+        for v in (0, 1, 2, 3):  # 2-buffer BK=64 (v0 / v1 fragment-pipelined) vs deep BK=32 4-buffer ring (v2, v3 cross-barrier prefetch)
             ms = timeit(lambda: lib.odh_gemm_bf16_256_variant(a.data_ptr(), bt.data_ptr(), c.data_ptr(), n, n, n, v, st))
-            out[f"gemm256_v{v}_{n}"] = {"ms": round(ms, 4), "tflops": round(fl / ms / 1e9, 1)}
+            c.zero_()
+            lib.odh_gemm_bf16_256_variant(a.data_ptr(), bt.data_ptr(), c.data_ptr(), n, n, n, v, st)
+            out[f"gemm256_v{v}_{n}"] = {"ms": round(ms, 4), "tflops": round(fl / ms / 1e9, 1),
+                                        "maxerr": float((c - ref).abs().max().item())}
         for name, fn in (("gemm128", lambda: gpu.gemm_bf16(a, bt, out=c, tile=128)),
                          ("gemm256", lambda: gpu.gemm_bf16(a, bt, out=c)),
                          ("torch_bf16_out", lambda: torch.mm(a, bt.t()))):
             ms = timeit(fn)
             out[f"{name}_{n}"] = {"ms": round(ms, 4), "tflops": round(fl / ms / 1e9, 1)}
-        ref = a.float() @ bt.float().t()
         gpu.gemm_bf16(a, bt, out=c)
         out[f"gemm256_{n}_maxerr"] = float((c - ref).abs().max().item())
         del a, bt, c, ref
         torch.cuda.empty_cache()
+    import ctypes
+
     p = gpu.GpuProbe(0)
     s = torch.cuda.current_stream().cuda_stream
     cnt = p.counters.data_ptr()
     ms = timeit(lambda: lib.odh_probe_gemm_verify(p.a.data_ptr(), p.bt.data_ptr(), p.m, p.n, p.k,
                                                   p.tile_xcd.data_ptr(), cnt, cnt + 64, cnt + 32, s))
     out["probe_gemm_fused_verify_4096"] = {"ms": round(ms, 4), "tflops": round(2.0 * 4096 ** 3 / ms / 1e9, 1)}
+    lib.odh_probe_gemm_verify_2buf.argtypes = lib.odh_probe_gemm_verify.argtypes
+    ms = timeit(lambda: lib.odh_probe_gemm_verify_2buf(p.a.data_ptr(), p.bt.data_ptr(), p.m, p.n, p.k,
+                                                       p.tile_xcd.data_ptr(), cnt, cnt + 64, cnt + 32, s))
+    out["probe_gemm_fused_verify_2buf_4096"] = {"ms": round(ms, 4), "tflops": round(2.0 * 4096 ** 3 / ms / 1e9, 1)}
+    lib.odh_probe_gemm_verify_deep.argtypes = list(lib.odh_probe_gemm_verify.argtypes[:-1]) + [ctypes.c_int,
+                                                                                               ctypes.c_void_p]
+    for xb in (0, 1):
+        p.counters.zero_()
+        ms = timeit(lambda: lib.odh_probe_gemm_verify_deep(p.a.data_ptr(), p.bt.data_ptr(), p.m, p.n, p.k,
+                                                           p.tile_xcd.data_ptr(), cnt, cnt + 64, cnt + 32, xb, s))
+        torch.cuda.synchronize()
+        out[f"probe_gemm_fused_verify_deep_xb{xb}_4096"] = {
+            "ms": round(ms, 4), "tflops": round(2.0 * 4096 ** 3 / ms / 1e9, 1), "errors": int(p.counters[16].item())}
     for nt in (0, 1):
         ms = timeit(lambda: lib.odh_hbm_write(p.hbm.data_ptr(), p.hbm_bytes, 7, nt, s))
         out[f"hbm_write_nt{nt}_1GiB"] = {"ms": round(ms, 4), "gbps": round(p.hbm_bytes / ms / 1e6, 1)}

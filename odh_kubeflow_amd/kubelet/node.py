@@ -33,6 +33,7 @@ GPU_INDEX_LABEL = "amd.com/gpu-index"
 # those GPUs first, so a shard's pods start inside the shard's own process instead of
 # waiting on another rank's event loop; a busy preferred GPU falls back to bin-packing.
 GPU_AFFINITY_LABEL = "amd.com/gpu-affinity"
+NAMESPACE_CACHE_WAIT_S = 0.5
 PROBE_CONDITION = "amd.com/GPUProbe"
 from ..runtime.controller import Request, Result, pred_funcs
 from ..utils.quantity import parse_quantity
@@ -111,6 +112,7 @@ class SchedulerController:
         # next scheduling decision before the informer has observed it, so two pods can
         # never be given the same GPU however far the cache lags behind the apiserver.
         self._assumed: Dict[str, tuple] = {}  # pod uid -> (node, cpu, mem, gpu ids)
+        self._ns_wait: Dict[str, float] = {}  # pod uid -> first time its namespace was missing from the cache
 
     def _used(self, node_name: str) -> Dict[str, object]:
         cpu = mem = 0.0
@@ -147,6 +149,7 @@ class SchedulerController:
 
     def forget(self, pod: dict) -> None:
         self._assumed.pop(m.uid(pod), None)
+        self._ns_wait.pop(m.uid(pod), None)
 
     async def reconcile(self, req: Request) -> Result:
         pod = self.reader.get(kinds.POD, req.name, req.namespace)
@@ -154,6 +157,13 @@ class SchedulerController:
             return Result()
         if m.uid(pod) in self._assumed:
             return Result()  # bound already; the cache has not caught up yet
+        if self.reader.get(kinds.NAMESPACE, req.namespace) is None and gpu_request(pod.get("spec") or {}):
+            # the namespace (and its gpu-affinity label) has not reached this cache yet: a
+            # pod cannot outlive its namespace's creation by much, so wait briefly for it
+            first = self._ns_wait.setdefault(m.uid(pod), time.monotonic())
+            if time.monotonic() - first < NAMESPACE_CACHE_WAIT_S:
+                return Result(requeue_after=0.002)
+        self._ns_wait.pop(m.uid(pod), None)
         async with self._lock:  # allocation decisions must not race each other
             return await self._schedule(pod)
 

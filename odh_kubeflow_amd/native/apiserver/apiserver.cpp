@@ -551,11 +551,18 @@ struct Ev {
   std::shared_ptr<EvCache> cache;
 };
 
+struct WatchSlot {
+  std::condition_variable cv;
+};
+
 struct Bucket {
   std::map<std::pair<std::string, std::string>, Obj> objs;
   std::deque<Ev> hist;
   int64_t seq = 0;
-  std::condition_variable cv;  // per resource: a write wakes only the watchers of its kind
+  // watchers by namespace ("" = cluster-wide): a write wakes only the watchers of its kind
+  // AND namespace, so with one control-plane shard per GPU rank (each watching its own
+  // namespaces) a write costs O(1) wake-ups instead of one per shard
+  std::unordered_multimap<std::string, WatchSlot*> watchers;
 };
 
 struct Store {
@@ -598,7 +605,20 @@ void emit(const Res& r, const char* type, Obj obj, Obj old) {
        std::make_shared<EvCache>()};
   b.hist.push_back(std::move(e));
   while (b.hist.size() > S.history) b.hist.pop_front();
-  b.cv.notify_all();
+  const Ev& ev = b.hist.back();
+  if ((b.seq & 1023) == 0) {
+    // periodic broadcast: watchers of quiet namespaces advance past other namespaces'
+    // events before those fall off the bounded history (no spurious 410 Gone relists)
+    for (auto& w : b.watchers) w.second->cv.notify_all();
+    return;
+  }
+  auto wake = [&](const std::string& ns) {
+    auto rg = b.watchers.equal_range(ns);
+    for (auto it = rg.first; it != rg.second; ++it) it->second->cv.notify_all();
+  };
+  const std::string ns = mget(*ev.obj, "namespace");
+  wake(ns);
+  if (!ns.empty()) wake("");
 }
 
 Value out_obj(const Res& r, const Value& o, const std::string& version) {
@@ -1782,9 +1802,28 @@ void serve_watch(int fd, Res& r, const Path& p, const Request& rq) {
   if (!write_all(fd, head.data(), head.size())) return;
   int64_t last_seq;
   std::vector<std::string> pending;
+  WatchSlot slot;
+  Bucket* wb = nullptr;
+  struct Unregister {  // every exit path drops the slot from the bucket's watcher index
+    Bucket*& b;
+    const std::string& ns;
+    WatchSlot* s;
+    ~Unregister() {
+      if (!b) return;
+      std::lock_guard<std::mutex> g(S.mu);
+      auto rg = b->watchers.equal_range(ns);
+      for (auto it = rg.first; it != rg.second; ++it)
+        if (it->second == s) {
+          b->watchers.erase(it);
+          break;
+        }
+    }
+  } unregister{wb, ns, &slot};
   {
     std::lock_guard<std::mutex> g(S.mu);
     Bucket& b = bucket(r);
+    wb = &b;
+    b.watchers.emplace(ns, &slot);
     last_seq = b.seq;
     if (rv.empty() || rv == "0") {
       for (auto& kv : b.objs)
@@ -1822,7 +1861,7 @@ void serve_watch(int fd, Res& r, const Path& p, const Request& rq) {
     {
       std::unique_lock<std::mutex> lk(S.mu);
       Bucket& b = bucket(r);
-      b.cv.wait_for(lk, std::chrono::milliseconds(500), [&] { return b.seq > last_seq || g_stop.load(); });
+      slot.cv.wait_for(lk, std::chrono::milliseconds(500), [&] { return b.seq > last_seq || g_stop.load(); });
       if (b.seq > last_seq) {
         if (!b.hist.empty() && b.hist.front().seq > last_seq + 1) {
           gone = true;  // the watcher fell behind the bounded history

@@ -160,11 +160,11 @@ async def _drive(args, shard, dist, torch) -> dict:
         t0 = time.perf_counter()
         await shard.admin.create(notebook(nm, ns, image="rocm/pytorch:rocm7.0_ubuntu22.04_py3.10_pytorch_2.10",
                                           gpus=1, annotations=ann))
-        if not await shard.wait_for(lambda: shard.notebook_ready(nm), 120):
+        if not await shard.wait_until(lambda: shard.notebook_ready(nm), 120):
             raise RuntimeError(f"notebook {ns}/{nm} not Ready")
         ready = time.perf_counter()
         await shard.admin.delete(kinds.NOTEBOOK, nm, ns)
-        if not await shard.wait_for(lambda: shard.gone(nm), 60):
+        if not await shard.wait_until(lambda: shard.gone(nm), 60):
             raise RuntimeError(f"teardown of {ns}/{nm} did not finish")
         if timed:
             lat_ms.append((ready - t0) * 1e3)

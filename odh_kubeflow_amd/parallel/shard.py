@@ -65,6 +65,7 @@ class ControlPlaneShard:
         self.agent = None
         self.webhook_server = None
         self._caches = []
+        self._waiters = None
 
     # ------------------------------------------------------------------ build
 
@@ -215,6 +216,31 @@ class ControlPlaneShard:
                 quiet = 0
             await asyncio.sleep(0.002)
         return False
+
+    async def wait_until(self, pred: Callable[[], bool], timeout: float = 10.0) -> bool:
+        """Event-driven wait: ``pred`` is re-checked on every Notebook / Pod event of the
+        shard's namespace (after the cache applied it) instead of on a polling timer."""
+        if pred():
+            return True
+        if self._waiters is None:
+            self._waiters = set()
+
+            def on_event(etype, obj, old):
+                for w in list(self._waiters):
+                    fut, p = w
+                    if not fut.done() and p():
+                        fut.set_result(True)
+            for k in (kinds.NOTEBOOK, kinds.POD):
+                self.cache.subscribe(k, on_event, namespace=self.cfg.namespace)
+        fut = asyncio.get_running_loop().create_future()
+        w = (fut, pred)
+        self._waiters.add(w)
+        try:
+            return await asyncio.wait_for(fut, timeout)
+        except asyncio.TimeoutError:
+            return pred()
+        finally:
+            self._waiters.discard(w)
 
     async def wait_for(self, pred: Callable[[], bool], timeout: float = 10.0, interval: float = 0.0005) -> bool:
         deadline = time.monotonic() + timeout

@@ -29,6 +29,9 @@ WatchCallback = Callable[[str, dict, Optional[dict]], None]
 # Set by ``retry_on_conflict`` for its retries: a Conflict means the informer copy is
 # stale, so the retry reads through to the apiserver instead of sleeping for the cache.
 LIVE_READS: contextvars.ContextVar = contextvars.ContextVar("live_reads", default=False)
+# how long a read of an object this client just wrote waits for the watch to deliver the
+# write before it reads through to the apiserver instead
+RYOW_WAIT_S = 0.05
 
 
 def _rv_int(o) -> Optional[int]:
@@ -216,6 +219,7 @@ class CachedClient(Client):
         self._written: Dict[Tuple[str, str, str], int] = {}
         self._ensured: set = set()  # kinds whose informer is known synced and served
         self.fresh_reads = 0
+        self.cache_waits = 0
 
     def _note(self, out) -> None:
         if not isinstance(out, dict) or "metadata" not in out:
@@ -254,8 +258,21 @@ class CachedClient(Client):
             if want is not None:
                 have = _rv_int(o) if o is not None else None
                 if have is None or have < want:
-                    self.fresh_reads += 1  # the cache has not seen our own write yet
-                    return await self.writer.get(kind, name, namespace)
+                    # the cache has not seen our own write yet: let the watch event (already
+                    # on its way) land, and read through only if it does not come promptly
+                    wait = getattr(self.reader, "wait_for_rv", None)
+                    if wait is not None and await wait(kind, namespace, want, RYOW_WAIT_S):
+                        self.cache_waits += 1
+                        o = self.reader.get(kind, name, namespace)
+                        have = _rv_int(o) if o is not None else None
+                        if o is not None and have < want:
+                            o = None
+                            have = None
+                        elif o is None:
+                            have = want  # deleted after our write: NotFound below is current
+                    if have is None or have < want:
+                        self.fresh_reads += 1
+                        return await self.writer.get(kind, name, namespace)
                 del self._written[key]
         if o is None:
             from ..models.errors import NotFound

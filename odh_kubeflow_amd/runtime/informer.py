@@ -62,6 +62,23 @@ class _Informer:
         self.relists = 0
         self.events = 0
         self.missing_kind = False
+        self._rv_waiters: List[Tuple[int, asyncio.Future]] = []
+
+    def _rv_reached(self) -> None:
+        """Resolve read-your-own-write waiters whose resourceVersion this stream has passed."""
+        try:
+            cur = int(self.rv)
+        except (TypeError, ValueError):
+            return
+        keep = []
+        for want, fut in self._rv_waiters:
+            if fut.done():
+                continue
+            if cur >= want:
+                fut.set_result(True)
+            else:
+                keep.append((want, fut))
+        self._rv_waiters = keep
 
     # -------------------------------------------------------------- index maintenance
 
@@ -135,6 +152,8 @@ class _Informer:
         self.rv = rv
         self.missing_kind = False
         self.synced.set()
+        if self._rv_waiters:
+            self._rv_reached()
 
     async def run(self) -> None:
         ref = f"{self.info.api_version(self.version)}/{self.info.kind}"
@@ -165,6 +184,8 @@ class _Informer:
                     else:
                         old = self._put(obj)
                         self._notify("ADDED" if old is None else "MODIFIED", obj, old)
+                    if self._rv_waiters:
+                        self._rv_reached()
             except asyncio.CancelledError:
                 raise
             except Gone:
@@ -279,6 +300,27 @@ class InformerCache(Reader, EventSource):
                 await asyncio.wait_for(inf.synced.wait(), timeout)
 
         await asyncio.gather(*(one(inf) for k in kinds for inf in self._group(k)))
+
+    async def wait_for_rv(self, kind, namespace: Optional[str], want: int, timeout: float) -> bool:
+        """Wait until the watch stream holding ``namespace``'s ``kind`` objects has delivered
+        resourceVersion ``want`` (e.g. a write this process just made).  A write's watch event
+        is emitted when it commits, before the write's response, so this is normally one
+        event-loop turn — no request, where a read-through GET would be a round trip."""
+        infs = self._for_ns(kind, namespace)
+        if len(infs) != 1:
+            return False
+        inf = infs[0]
+        try:
+            if int(inf.rv) >= want:
+                return True
+        except (TypeError, ValueError):
+            pass
+        fut = asyncio.get_running_loop().create_future()
+        inf._rv_waiters.append((want, fut))
+        try:
+            return await asyncio.wait_for(fut, timeout)
+        except asyncio.TimeoutError:
+            return False
 
     # -------------------------------------------------------------- Reader
 

@@ -143,3 +143,123 @@ def test_processes_end_to_end(tmp_path, run):
             except subprocess.TimeoutExpired:
                 p.kill()
         logf.close()
+
+
+def test_processes_notebook_lifecycle_like_reference_e2e(tmp_path, run):
+    """The odh/e2e sequence (notebook_creation_test.go, notebook_update_test.go,
+    notebook_deletion_test.go) against separate processes: create with inject-auth →
+    HTTPRoute, NetworkPolicies, StatefulSet 1/1, sidecar with default resources → the
+    notebook's Jupyter API answers → idle culling stops it (STS scaled to 0) → resume
+    with a new image rolls the StatefulSet → delete removes every dependent."""
+    import aiohttp
+
+    from odh_kubeflow_amd.webhook.certs import generate
+    from odh_kubeflow_amd.webhook.server import mutating_webhook_configuration
+
+    api_port, wh_port = free_port(), free_port()
+    certs = generate(("127.0.0.1", "localhost"), str(tmp_path / "certs"))
+    logf = open(tmp_path / "procs.log", "wb")
+    master = f"http://127.0.0.1:{api_port}"
+    procs = [spawn(["odh_kubeflow_amd.cmd.apiserver", "--port", str(api_port), "--controllers",
+                    "--no-openshift-apis"], log=logf)]
+    try:
+        async def go():
+            await wait_http(master + "/healthz")
+            c = RestClient(RestConfig(host=master))
+            for ns in ("opendatahub", "e2e"):
+                await c.create({"apiVersion": "v1", "kind": "Namespace", "metadata": {"name": ns}})
+            common = {"K8S_NAMESPACE": "opendatahub", "SET_PIPELINE_RBAC": "false"}
+            culling = {"ENABLE_CULLING": "true", "CULL_IDLE_TIME_SECONDS": "2.5",
+                       "IDLENESS_CHECK_PERIOD_SECONDS": "0.3", "CULLER_USE_POD_ENDPOINT": "true"}
+            procs.append(spawn(["odh_kubeflow_amd.cmd.kf_manager", "--master", master, "--metrics-addr", "0",
+                                "--probe-addr", "0"], {**common, **culling}, logf))
+            procs.append(spawn(["odh_kubeflow_amd.cmd.odh_manager", "--master", master, "--metrics-bind-address", "0",
+                                "--health-probe-bind-address", "0", "--kube-rbac-proxy-image",
+                                "quay.io/brancz/kube-rbac-proxy:v0.18.1", "--webhook-cert-dir", certs.cert_dir,
+                                "--webhook-port", str(wh_port), "--webhook-host", "127.0.0.1"], common, logf))
+            procs.append(spawn(["odh_kubeflow_amd.cmd.node_agent", "--master", master, "--jupyter",
+                                "--sysfs-root", str(tmp_path / "nosys")], common, logf))
+            await wait_http(f"https://127.0.0.1:{wh_port}/healthz")
+            await c.create(mutating_webhook_configuration(
+                certs.ca_bundle_b64, url=f"https://127.0.0.1:{wh_port}/mutate-notebook-v1"))
+            await eventually(lambda: c.get(kinds.NODE, "mi355x-node-0"))
+            await c.create(notebook("e2e-nb", "e2e", gpus=1, image="rocm/pytorch:latest",
+                                    annotations={"notebooks.opendatahub.io/inject-auth": "true"}))
+
+            async def ready():
+                nb = await c.get(kinds.NOTEBOOK, "e2e-nb", "e2e")
+                st = nb.get("status") or {}
+                return st.get("readyReplicas") == 1 and any(
+                    x.get("type") == "Ready" and x.get("status") == "True" for x in st.get("conditions") or [])
+
+            await eventually(ready, 60)
+            # creation checks (notebook_creation_test.go)
+            assert [m.name(r) for r in await c.list(kinds.HTTP_ROUTE, "opendatahub")] == ["nb-e2e-e2e-nb"]
+            nps = {m.name(x) for x in await c.list(kinds.NETWORK_POLICY, "e2e")}
+            assert nps == {"e2e-nb-ctrl-np", "e2e-nb-kube-rbac-proxy-np"}
+            sts = await c.get(kinds.STATEFUL_SET, "e2e-nb", "e2e")
+            assert sts["spec"]["replicas"] == 1 and (sts.get("status") or {}).get("readyReplicas") == 1
+            proxy = [x for x in sts["spec"]["template"]["spec"]["containers"] if x["name"] == "kube-rbac-proxy"][0]
+            assert proxy["resources"] == {"requests": {"cpu": "100m", "memory": "64Mi"},
+                                          "limits": {"cpu": "100m", "memory": "64Mi"}}
+            # the notebook server answers (service connectivity)
+            pod = await c.get(kinds.POD, "e2e-nb-0", "e2e")
+            ep = m.annotations(pod)["amd.com/notebook-endpoint"]
+            async with aiohttp.ClientSession() as s:
+                async with s.get(f"http://{ep}/notebook/e2e/e2e-nb/api/kernels") as r:
+                    assert r.status == 200 and await r.json() == []
+
+            # culling (notebook_creation_test.go :417-518): idle → STOP annotation → 0 replicas
+            async def culled():
+                nb = await c.get(kinds.NOTEBOOK, "e2e-nb", "e2e")
+                stop = m.annotations(nb).get("kubeflow-resource-stopped")
+                s = await c.get(kinds.STATEFUL_SET, "e2e-nb", "e2e")
+                return stop and stop != "odh-notebook-controller-lock" and s["spec"]["replicas"] == 0
+            await eventually(culled, 30)
+            nb = await c.get(kinds.NOTEBOOK, "e2e-nb", "e2e")
+            # a stopped notebook carries no activity annotations (culling_controller.go:104-117)
+            assert "notebooks.kubeflow.org/last-activity" not in m.annotations(nb)
+
+            # update (notebook_update_test.go): resume with a new image → STS rolls
+            nb["metadata"]["annotations"].pop("kubeflow-resource-stopped")
+            nb["spec"]["template"]["spec"]["containers"][0]["image"] = "rocm/pytorch:updated"
+            await c.update(nb)
+
+            async def rolled():
+                s = await c.get(kinds.STATEFUL_SET, "e2e-nb", "e2e")
+                img = s["spec"]["template"]["spec"]["containers"][0]["image"]
+                return s["spec"]["replicas"] == 1 and img == "rocm/pytorch:updated" and \
+                    (s.get("status") or {}).get("readyReplicas") == 1
+            await eventually(rolled, 30)
+
+            # deletion (notebook_deletion_test.go): every dependent goes
+            await c.delete(kinds.NOTEBOOK, "e2e-nb", "e2e")
+
+            async def all_gone():
+                left = []
+                for k, n, ns in ((kinds.NOTEBOOK, "e2e-nb", "e2e"), (kinds.STATEFUL_SET, "e2e-nb", "e2e"),
+                                 (kinds.SERVICE, "e2e-nb", "e2e"), (kinds.SERVICE, "e2e-nb-kube-rbac-proxy", "e2e"),
+                                 (kinds.SERVICE_ACCOUNT, "e2e-nb", "e2e"),
+                                 (kinds.CONFIG_MAP, "e2e-nb-kube-rbac-proxy-config", "e2e"),
+                                 (kinds.NETWORK_POLICY, "e2e-nb-ctrl-np", "e2e"),
+                                 (kinds.HTTP_ROUTE, "nb-e2e-e2e-nb", "opendatahub"),
+                                 (kinds.CLUSTER_ROLE_BINDING, "e2e-nb-rbac-e2e-auth-delegator", None)):
+                    try:
+                        await c.get(k, n, ns)
+                        left.append(n)
+                    except Exception:
+                        pass
+                return not left
+            await eventually(all_gone, 30)
+            await c.close()
+
+        run(go(), timeout=150)
+    finally:
+        for p in procs:
+            p.terminate()
+        for p in procs:
+            try:
+                p.wait(10)
+            except subprocess.TimeoutExpired:
+                p.kill()
+        logf.close()

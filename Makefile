@@ -1,0 +1,43 @@
+# Developer targets (the reference's kf/Makefile and odh/Makefile counterparts).
+PYTHON ?= python3
+IMG ?= quay.io/opendatahub/odh-kubeflow-amd:latest
+NOTEBOOK_IMG ?= quay.io/opendatahub/workbench-rocm-pytorch:latest
+GPU_ARCH ?= gfx950
+
+.PHONY: build test test-native test-gpu e2e bench bench-8 manifests deploy undeploy docker-build docker-build-notebook
+
+build:  ## hipcc --offload-arch=$(GPU_ARCH) kernels, host C++ telemetry/objcore, native apiserver (in-tree)
+	ODH_GPU_ARCH=$(GPU_ARCH) $(PYTHON) -m odh_kubeflow_amd.ops.build
+
+test: build  ## CPU suite against the in-process store (envtest analogue)
+	$(PYTHON) -m pytest tests -q -m "not gpu"
+
+test-native: build  ## the same suite over the native C++ apiserver (REST + watch + HTTPS admission)
+	ODH_CLUSTER_TRANSPORT=native $(PYTHON) -m pytest tests -q -m "not gpu"
+
+test-gpu: build  ## HIP kernels vs fp32 torch on an MI355X
+	$(PYTHON) -u -m pytest tests -q -m gpu --timeout 120 --timeout-method thread
+
+e2e: build  ## separate apiserver / kf / odh / node-agent processes (reference e2e sequence)
+	$(PYTHON) -m pytest tests/test_processes_e2e.py -q
+
+bench: build  ## headline benchmark on one MI355X
+	$(PYTHON) bench.py
+
+bench-8: build  ## one control-plane shard per MI355X of an 8-GPU node
+	$(PYTHON) -m torch.distributed.run --nnodes=1 --nproc-per-node 8 --master-addr 127.0.0.1 bench.py --gpus 8
+
+manifests:  ## regenerate the kustomize tree under config/
+	$(PYTHON) -m odh_kubeflow_amd.deploy.manifests --out config
+
+deploy: manifests  ## kubectl apply the MI355X overlay (CRD, RBAC, managers, webhook, node agent)
+	kubectl apply -k config/overlays/mi355x
+
+undeploy:
+	kubectl delete -k config/overlays/mi355x --ignore-not-found
+
+docker-build: build  ## controller / node-agent image (ROCm base; kernels built for $(GPU_ARCH))
+	docker build -f images/Dockerfile --build-arg GPU_ARCH=$(GPU_ARCH) -t $(IMG) .
+
+docker-build-notebook:  ## PyTorch-ROCm Jupyter workbench image the samples reference
+	docker build -f images/notebook.Dockerfile -t $(NOTEBOOK_IMG) images

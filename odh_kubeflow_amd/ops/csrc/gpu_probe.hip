@@ -691,6 +691,36 @@ __global__ __launch_bounds__(256) void hbm_check_kernel(const u32x4* __restrict_
   if ((threadIdx.x & 63) == 0 && local) atomicAdd(err, (unsigned long long)local);
 }
 
+// read-path variants for A/B measurement (odh_hbm_check_variant): NT = nontemporal loads,
+// U = 16-byte loads in flight per lane per iteration
+template <bool NT, int U>
+__global__ __launch_bounds__(256) void hbm_check_variant_kernel(const u32x4* __restrict__ buf, size_t n,
+                                                                uint32_t seed, unsigned long long* __restrict__ err) {
+  const size_t per = ((n + gridDim.x - 1) / gridDim.x + 1023) & ~(size_t)1023;
+  const size_t lo = blockIdx.x * per;
+  const size_t hi = lo + per < n ? lo + per : n;
+  unsigned local = 0;
+  for (size_t base = lo + threadIdx.x; base < hi; base += U * 256) {
+    u32x4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const size_t i = base + u * 256;
+      if (i < hi) v[u] = NT ? __builtin_nontemporal_load(&buf[i]) : buf[i];
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const size_t i = base + u * 256;
+      if (i < hi) {
+        const uint32_t b = (uint32_t)(i * 4) ^ seed;
+        local += (v[u].x != mix32(b)) + (v[u].y != mix32(b + 1)) + (v[u].z != mix32(b + 2)) +
+                 (v[u].w != mix32(b + 3));
+      }
+    }
+  }
+  for (int off = 32; off > 0; off >>= 1) local += __shfl_down(local, off, 64);
+  if ((threadIdx.x & 63) == 0 && local) atomicAdd(err, (unsigned long long)local);
+}
+
 __global__ __launch_bounds__(256) void busy_kernel(float* __restrict__ out, int iters) {
   const int lane = threadIdx.x & 63;
   bf16x8 a, b;
@@ -850,6 +880,21 @@ int odh_hbm_check(const void* buf, size_t bytes, uint32_t seed, unsigned long lo
   const size_t n = bytes / 16;
   if (n == 0) return (int)hipErrorInvalidValue;
   hbm_check_kernel<<<grid_for(n, 1024), 256, 0, stream>>>((const u32x4*)buf, n, seed, err);
+  return (int)hipGetLastError();
+}
+
+int odh_hbm_check_variant(const void* buf, size_t bytes, uint32_t seed, unsigned long long* err, int variant,
+                          int blocks, hipStream_t stream) {
+  const size_t n = bytes / 16;
+  if (n == 0 || blocks <= 0) return (int)hipErrorInvalidValue;
+  const u32x4* b = (const u32x4*)buf;
+  switch (variant) {
+    case 0: hbm_check_variant_kernel<true, 4><<<blocks, 256, 0, stream>>>(b, n, seed, err); break;
+    case 1: hbm_check_variant_kernel<false, 4><<<blocks, 256, 0, stream>>>(b, n, seed, err); break;
+    case 2: hbm_check_variant_kernel<true, 8><<<blocks, 256, 0, stream>>>(b, n, seed, err); break;
+    case 3: hbm_check_variant_kernel<false, 8><<<blocks, 256, 0, stream>>>(b, n, seed, err); break;
+    default: return (int)hipErrorInvalidValue;
+  }
   return (int)hipGetLastError();
 }
 

@@ -99,8 +99,21 @@ def main():
     ms = timeit(lambda: big.fill_(3), iters=5)
     out["torch_fill_4GiB"] = {"ms": round(ms, 4), "gbps": round((4 << 30) / ms / 1e6, 1)}
     del big
+    lib.odh_hbm_write(p.hbm.data_ptr(), p.hbm_bytes, 7, 0, s)  # check against a matching pattern (the probe's case)
     ms = timeit(lambda: lib.odh_hbm_check(p.hbm.data_ptr(), p.hbm_bytes, 7, cnt + 72, s))
     out["hbm_check_1GiB"] = {"ms": round(ms, 4), "gbps": round(p.hbm_bytes / ms / 1e6, 1)}
+    lib.odh_hbm_check_variant.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint32, ctypes.c_void_p,
+                                          ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
+    lib.odh_hbm_write(p.hbm.data_ptr(), p.hbm_bytes, 7, 0, s)
+    for v in (0, 1, 2, 3):
+        for blocks in (1024, 2048, 4096, 8192):
+            p.counters.zero_()
+            ms = timeit(lambda: lib.odh_hbm_check_variant(p.hbm.data_ptr(), p.hbm_bytes, 7, cnt + 72, v, blocks, s))
+            torch.cuda.synchronize()
+            out[f"hbm_check_v{v}_b{blocks}"] = {"ms": round(ms, 4), "gbps": round(p.hbm_bytes / ms / 1e6, 1),
+                                                "errors": int(p.counters[18].item())}
+    ms = timeit(lambda: p.hbm.sum())
+    out["torch_sum_1GiB"] = {"ms": round(ms, 4), "gbps": round(p.hbm_bytes / ms / 1e6, 1)}
     for ov in (False, True):
         p.overlap = ov
         rs = [p.run() for _ in range(12)][2:]

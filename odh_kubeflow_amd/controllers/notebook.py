@@ -19,7 +19,11 @@ Per reconcile of a Notebook (reference ``Reconcile`` :93-297):
 
 ``amd.com/gpu`` requests/limits pass through verbatim; with ``GPU_NODE_SELECTOR=true``
 pods that request GPUs also get the AMD node-labeller selector and the
-``amd.com/gpu`` toleration so they land on MI355X nodes.
+``amd.com/gpu`` toleration so they land on MI355X nodes.  With
+``GPU_SHM_SIZE_PER_GPU`` (e.g. ``16Gi``) a GPU notebook without its own ``/dev/shm``
+gets a memory-backed one of that size per GPU: PyTorch DataLoader workers and RCCL's
+intra-node transport live there, and the container default (64 MiB) breaks both.  The
+``amd.com/shm-size`` annotation overrides the size (``0`` turns it off).
 
 Event re-emission (:97-126) runs as its own small controller
 (:class:`NotebookEventReemitter`) instead of sharing the Notebook work queue — the
@@ -31,6 +35,7 @@ from __future__ import annotations
 import json
 import logging
 import os
+import re
 from typing import Mapping, Optional
 
 from ..models import kinds
@@ -77,6 +82,34 @@ def _gpu_placement(pod_spec: dict) -> None:
         tol.append({"key": GPU_RESOURCE, "operator": "Exists", "effect": "NoSchedule"})
 
 
+SHM_SIZE_ANNOTATION = "amd.com/shm-size"
+SHM_VOLUME = "dshm"
+_SIZE_RE = re.compile(r"^\s*(\d+)\s*([KMGT]i)?\s*$")
+
+
+def _gpu_shm(nb: dict, pod_spec: dict, per_gpu: str) -> None:
+    """Memory-backed ``/dev/shm`` sized per GPU for notebooks that request ``amd.com/gpu``."""
+    ngpu = gpu_request(pod_spec)
+    containers = pod_spec.get("containers") or []
+    if ngpu <= 0 or not containers:
+        return
+    size = (m.annotations(nb).get(SHM_SIZE_ANNOTATION) or "").strip()
+    if not size:
+        mm = _SIZE_RE.match(per_gpu or "")
+        if not mm:
+            return
+        size = f"{int(mm.group(1)) * ngpu}{mm.group(2) or ''}"
+    if size in ("0", "none", "off"):
+        return
+    if any(vm.get("mountPath") == "/dev/shm" for c in containers for vm in c.get("volumeMounts") or []):
+        return  # the user sized it already
+    vols = pod_spec.setdefault("volumes", [])
+    if any(v.get("name") == SHM_VOLUME for v in vols):
+        return
+    vols.append({"name": SHM_VOLUME, "emptyDir": {"medium": "Memory", "sizeLimit": size}})
+    containers[0].setdefault("volumeMounts", []).append({"name": SHM_VOLUME, "mountPath": "/dev/shm"})
+
+
 def generate_statefulset(nb: dict, is_generate_name: bool, env: Mapping[str, str] = os.environ) -> dict:
     """``generateStatefulSet`` (:433-523)."""
     name, ns = m.name(nb), m.namespace(nb)
@@ -114,6 +147,8 @@ def generate_statefulset(nb: dict, is_generate_name: bool, env: Mapping[str, str
             pod_spec["securityContext"] = {"fsGroup": DEFAULT_FS_GROUP}
     if env.get("GPU_NODE_SELECTOR", "false") == "true":
         _gpu_placement(pod_spec)
+    if env.get("GPU_SHM_SIZE_PER_GPU"):
+        _gpu_shm(nb, pod_spec, env["GPU_SHM_SIZE_PER_GPU"])
     return sts
 
 

@@ -356,7 +356,8 @@ def tree() -> Dict[str, object]:
                                           "CULLING_ACTIVITY_SOURCE=jupyter", "CULLING_GPU_BUSY_THRESHOLD=5"]}],
         generatorOptions={"disableNameSuffixHash": True})
     t["manager/params.env"] = "USE_ISTIO=false\nISTIO_GATEWAY=kubeflow/kubeflow-gateway\nISTIO_HOST=*\n" \
-                              "CLUSTER_DOMAIN=cluster.local\nADD_FSGROUP=true\nGPU_NODE_SELECTOR=false\n"
+                              "CLUSTER_DOMAIN=cluster.local\nADD_FSGROUP=true\nGPU_NODE_SELECTOR=false\n" \
+                              "GPU_SHM_SIZE_PER_GPU=\n"
     t["node-agent/daemonset.yaml"] = node_agent_daemonset()
     t["node-agent/kustomization.yaml"] = kustomization(["daemonset.yaml"])
     t["webhook/service.yaml"] = webhook_service()
@@ -382,7 +383,8 @@ def tree() -> Dict[str, object]:
     t["overlays/mi355x/kustomization.yaml"] = kustomization(
         ["../../default"],
         patches=[{"target": {"kind": "ConfigMap", "name": ".*config"}, "patch":
-                  "- op: replace\n  path: /data/GPU_NODE_SELECTOR\n  value: \"true\"\n"},
+                  "- op: replace\n  path: /data/GPU_NODE_SELECTOR\n  value: \"true\"\n"
+                  "- op: replace\n  path: /data/GPU_SHM_SIZE_PER_GPU\n  value: 16Gi\n"},
                  {"target": {"kind": "ConfigMap", "name": ".*culler-config"}, "patch":
                   "- op: replace\n  path: /data/CULLING_ACTIVITY_SOURCE\n  value: combined\n"
                   "- op: replace\n  path: /data/ENABLE_CULLING\n  value: \"true\"\n"}])

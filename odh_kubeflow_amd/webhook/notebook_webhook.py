@@ -60,6 +60,30 @@ class AdmissionError(Exception):
         self.code = code
 
 
+def validate_gpu_resources(nb: dict) -> None:
+    """``amd.com/gpu`` is an extended resource: whole numbers, never overcommitted, so a
+    request needs an equal limit (the pod-validation rules kube-apiserver applies when
+    the StatefulSet controller creates the pod).  Checked at admission so a bad Notebook
+    is refused up front instead of leaving a StatefulSet that can never create its pod."""
+    from ..models.notebook import GPU_RESOURCE
+
+    spec = ((nb.get("spec") or {}).get("template") or {}).get("spec") or {}
+    for i, c in enumerate(spec.get("containers") or []):
+        res = c.get("resources") or {}
+        req = (res.get("requests") or {}).get(GPU_RESOURCE)
+        lim = (res.get("limits") or {}).get(GPU_RESOURCE)
+        path = f"spec.template.spec.containers[{i}].resources"
+        for kind_, v in (("limits", lim), ("requests", req)):
+            if v is not None and not str(v).strip().isdigit():
+                raise AdmissionError(400, f'{path}.{kind_}[{GPU_RESOURCE}]: Invalid value: "{v}": must be an integer')
+        if req is not None and lim is None:
+            raise AdmissionError(400, f"{path}.limits: Required value: Limit must be set for non overcommitable "
+                                      f"resources ({GPU_RESOURCE})")
+        if req is not None and int(str(req)) != int(str(lim)):
+            raise AdmissionError(400, f'{path}.requests[{GPU_RESOURCE}]: Invalid value: "{req}": must be equal to '
+                                      f"{GPU_RESOURCE} limit of {lim}")
+
+
 def inject_reconciliation_lock(nb: dict) -> None:
     m.ensure_annotations(nb)[STOP_ANNOTATION] = ANNOTATION_VALUE_RECONCILIATION_LOCK
 
@@ -156,6 +180,8 @@ class NotebookWebhook:
         with tracer.start_span("handleFunc", {"notebook": name or m.name(nb), "namespace": namespace or m.namespace(nb),
                                               "operation": operation}, new_root=True):
             original = nb
+            if operation in ("CREATE", "UPDATE"):
+                validate_gpu_resources(nb)
             nb = deepcopy_json(nb)
             if operation == "CREATE":
                 inject_reconciliation_lock(nb)

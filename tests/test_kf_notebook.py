@@ -226,3 +226,24 @@ def test_istio_virtual_service_and_spec_drift(run):
             assert await cl.wait_for(lambda: cl.store.peek(kinds.STATEFUL_SET, "nb1", "user")["spec"]["template"]
                                      ["spec"]["containers"][0]["image"] == "rocm/pytorch:latest")
     run(go())
+
+
+def test_gpu_shm_sized_per_gpu_and_overridable():
+    from odh_kubeflow_amd.controllers.notebook import generate_statefulset
+
+    env = {"GPU_SHM_SIZE_PER_GPU": "16Gi"}
+    sts = generate_statefulset(notebook("nb", "ns", gpus=4), False, env)
+    spec = sts["spec"]["template"]["spec"]
+    assert {"name": "dshm", "emptyDir": {"medium": "Memory", "sizeLimit": "64Gi"}} in spec["volumes"]
+    assert {"name": "dshm", "mountPath": "/dev/shm"} in spec["containers"][0]["volumeMounts"]
+    # annotation override, opt-out, CPU notebooks and user-provided /dev/shm are left alone
+    sts = generate_statefulset(notebook("nb", "ns", gpus=2, annotations={"amd.com/shm-size": "100Gi"}), False, env)
+    assert sts["spec"]["template"]["spec"]["volumes"][0]["emptyDir"]["sizeLimit"] == "100Gi"
+    sts = generate_statefulset(notebook("nb", "ns", gpus=2, annotations={"amd.com/shm-size": "0"}), False, env)
+    assert "volumes" not in sts["spec"]["template"]["spec"]
+    assert "volumes" not in generate_statefulset(notebook("nb", "ns"), False, env)["spec"]["template"]["spec"]
+    own = notebook("nb", "ns", gpus=1)
+    own["spec"]["template"]["spec"]["containers"][0]["volumeMounts"] = [{"name": "mine", "mountPath": "/dev/shm"}]
+    assert "volumes" not in generate_statefulset(own, False, env)["spec"]["template"]["spec"]
+    # off unless configured (the reference copies the pod spec verbatim)
+    assert "volumes" not in generate_statefulset(notebook("nb", "ns", gpus=1), False, {})["spec"]["template"]["spec"]

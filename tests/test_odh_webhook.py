@@ -372,3 +372,22 @@ def test_admission_review_json_patch_roundtrip(run):
         bad = await wh.handle({"request": {"uid": "r2", "operation": "CREATE"}})
         assert bad["response"]["allowed"] is False and bad["response"]["status"]["code"] == 400
     run(go())
+
+
+@pytest.mark.parametrize("res,msg", [
+    ({"requests": {"amd.com/gpu": "2"}, "limits": {"amd.com/gpu": "1"}}, "must be equal to amd.com/gpu limit of 1"),
+    ({"requests": {"amd.com/gpu": "1"}}, "Limit must be set for non overcommitable resources"),
+    ({"limits": {"amd.com/gpu": "500m"}}, 'Invalid value: "500m": must be an integer'),
+])
+def test_webhook_denies_invalid_gpu_resources(run, res, msg):
+    async def go():
+        store, admin, wh = await _setup()
+        nb = notebook("nb", "user")
+        nb["spec"]["template"]["spec"]["containers"][0]["resources"] = res
+        with pytest.raises(Exception) as ei:
+            await admin.create(nb)
+        assert msg in str(ei.value)
+        assert store.peek(kinds.NOTEBOOK, "nb", "user") is None
+        ok = notebook("ok", "user", gpus=8)  # requests == limits, whole GPUs
+        await admin.create(ok)
+    run(go())

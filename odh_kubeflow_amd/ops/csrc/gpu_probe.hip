@@ -344,7 +344,7 @@ constexpr int D_RING = D_NBUF * 2 * D_TILE;
 
 __device__ __forceinline__ int dswz(int r, int c) { return r * D_CH + (c ^ ((r >> 2) & 3)); }
 
-template <bool VERIFY, bool XB = false>
+template <bool VERIFY, bool XB = false, int GM = 1>
 __global__ __launch_bounds__(G_THREADS, 1) void gemm256d_kernel(
     const uint4* __restrict__ A, const uint4* __restrict__ Bt, float* __restrict__ C, int M, int N, int K,
     int* __restrict__ tile_xcd, int* __restrict__ xcd_blocks, unsigned* __restrict__ err_total,
@@ -360,8 +360,17 @@ __global__ __launch_bounds__(G_THREADS, 1) void gemm256d_kernel(
   const int nwg = gridDim.x;
   const int orig = blockIdx.x, xq = nwg >> 3, xr = nwg & 7, xs = orig & 7;
   const int bid = (xs < xr ? xs * (xq + 1) : xr * (xq + 1) + (xs - xr) * xq) + (orig >> 3);
-  const int tm = bid / tiles_n;
-  const int tn = bid - tm * tiles_n;
+  // GM > 1: consecutive tile ids walk GM tile-rows × (32/GM) columns, so the 32 tiles of
+  // one XCD share GM A panels and 32/GM B panels in that XCD's L2 (GM = 1: row-major)
+  int tm, tn;
+  if (GM > 1 && (M / G_BM) % GM == 0) {
+    const int band = bid / (GM * tiles_n), in_band = bid - band * GM * tiles_n;
+    tm = band * GM + in_band % GM;
+    tn = in_band / GM;
+  } else {
+    tm = bid / tiles_n;
+    tn = bid - tm * tiles_n;
+  }
   const unsigned xcc = xcc_id();
   if (tid == 0) {
     if (tile_xcd) tile_xcd[bid] = (int)xcc;
@@ -842,15 +851,27 @@ int odh_probe_gemm_verify_2buf(const void* A, const void* Bt, int M, int N, int 
 }
 
 // the same fused probe on the deep-pipelined kernel (A/B against odh_probe_gemm_verify)
+// variant bit 0: cross-barrier fragment prefetch (XB); bits 1-2: tile grouping GM = 1, 2, 4, 8
 int odh_probe_gemm_verify_deep(const void* A, const void* Bt, int M, int N, int K, int* tile_xcd, int* xcd_blocks,
-                               unsigned* err_total, unsigned* err_xcd, int xb, hipStream_t stream) {
+                               unsigned* err_total, unsigned* err_xcd, int variant, hipStream_t stream) {
   if (!odh_gemm_shape_ok(M, N, K) || !gemm256_ok(M, N, K) || !err_total) return (int)hipErrorInvalidValue;
-  if (xb)
-    gemm256d_kernel<true, true><<<(M / G_BM) * (N / G_BN), G_THREADS, 0, stream>>>(
-        (const uint4*)A, (const uint4*)Bt, nullptr, M, N, K, tile_xcd, xcd_blocks, err_total, err_xcd);
-  else
-    gemm256d_kernel<true><<<(M / G_BM) * (N / G_BN), G_THREADS, 0, stream>>>(
-        (const uint4*)A, (const uint4*)Bt, nullptr, M, N, K, tile_xcd, xcd_blocks, err_total, err_xcd);
+  const int nwg = (M / G_BM) * (N / G_BN);
+  const uint4 *a = (const uint4*)A, *b = (const uint4*)Bt;
+#define ODH_DEEP(XB_, GM_)                                                                                  \
+  gemm256d_kernel<true, XB_, GM_><<<nwg, G_THREADS, 0, stream>>>(a, b, nullptr, M, N, K, tile_xcd, xcd_blocks, \
+                                                                 err_total, err_xcd)
+  switch (variant) {
+    case 0: ODH_DEEP(false, 1); break;
+    case 1: ODH_DEEP(true, 1); break;
+    case 2: ODH_DEEP(false, 2); break;
+    case 3: ODH_DEEP(true, 2); break;
+    case 4: ODH_DEEP(false, 4); break;
+    case 5: ODH_DEEP(true, 4); break;
+    case 6: ODH_DEEP(false, 8); break;
+    case 7: ODH_DEEP(true, 8); break;
+    default: return (int)hipErrorInvalidValue;
+  }
+#undef ODH_DEEP
   return (int)hipGetLastError();
 }
 

@@ -79,8 +79,16 @@ def load_library(build_if_missing: bool = False):
         lib.odh_hbm_write.argtypes = [vp, sz, u32, i, vp]
         lib.odh_hbm_check.argtypes = [vp, sz, u32, vp, vp]
         lib.odh_busy.argtypes = [vp, i, i, vp]
+        # A/B entry points (microbenchmarks, kernel numerics tests)
+        lib.odh_gemm_bf16_256_variant.argtypes = [vp, vp, vp, i, i, i, i, vp]
+        lib.odh_probe_gemm_verify_2buf.argtypes = [vp, vp, i, i, i, vp, vp, vp, vp, vp]
+        lib.odh_probe_gemm_verify_deep.argtypes = [vp, vp, i, i, i, vp, vp, vp, vp, i, vp]
+        lib.odh_hbm_write_variant.argtypes = [vp, sz, u32, i, i, vp]
+        lib.odh_hbm_check_variant.argtypes = [vp, sz, u32, vp, i, i, vp]
         for f in ("odh_probe_fill", "odh_gemm_bf16", "odh_gemm_bf16_128", "odh_probe_verify", "odh_probe_gemm_verify",
-                  "odh_hbm_write", "odh_hbm_check", "odh_busy"):
+                  "odh_hbm_write", "odh_hbm_check", "odh_busy", "odh_gemm_bf16_256_variant",
+                  "odh_probe_gemm_verify_2buf", "odh_probe_gemm_verify_deep", "odh_hbm_write_variant",
+                  "odh_hbm_check_variant"):
             getattr(lib, f).restype = i
         _lib = lib
         return lib

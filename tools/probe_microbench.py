@@ -14,10 +14,16 @@ import torch  # noqa: E402
 from odh_kubeflow_amd.ops import gpu  # noqa: E402
 
 
-def timeit(fn, iters=20, warm=3):
-    for _ in range(warm):
-        fn()
-    torch.cuda.synchronize()
+def timeit(fn, iters=20, warm_s=0.25):
+    """Median of ``iters`` event-timed calls after ``warm_s`` seconds of back-to-back calls:
+    MI355X clocks ramp under load (DVFS), so a few warm-up calls time a cold chip."""
+    import time
+
+    t_end = time.perf_counter() + warm_s
+    while time.perf_counter() < t_end:
+        for _ in range(8):
+            fn()
+        torch.cuda.synchronize()
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
     ts = []
     for _ in range(iters):
@@ -68,19 +74,18 @@ def main():
     ms = timeit(lambda: lib.odh_probe_gemm_verify(p.a.data_ptr(), p.bt.data_ptr(), p.m, p.n, p.k,
                                                   p.tile_xcd.data_ptr(), cnt, cnt + 64, cnt + 32, s))
     out["probe_gemm_fused_verify_4096"] = {"ms": round(ms, 4), "tflops": round(2.0 * 4096 ** 3 / ms / 1e9, 1)}
-    lib.odh_probe_gemm_verify_2buf.argtypes = lib.odh_probe_gemm_verify.argtypes
     ms = timeit(lambda: lib.odh_probe_gemm_verify_2buf(p.a.data_ptr(), p.bt.data_ptr(), p.m, p.n, p.k,
                                                        p.tile_xcd.data_ptr(), cnt, cnt + 64, cnt + 32, s))
     out["probe_gemm_fused_verify_2buf_4096"] = {"ms": round(ms, 4), "tflops": round(2.0 * 4096 ** 3 / ms / 1e9, 1)}
-    lib.odh_probe_gemm_verify_deep.argtypes = list(lib.odh_probe_gemm_verify.argtypes[:-1]) + [ctypes.c_int,
-                                                                                               ctypes.c_void_p]
-    for xb in (0, 1):
-        p.counters.zero_()
-        ms = timeit(lambda: lib.odh_probe_gemm_verify_deep(p.a.data_ptr(), p.bt.data_ptr(), p.m, p.n, p.k,
-                                                           p.tile_xcd.data_ptr(), cnt, cnt + 64, cnt + 32, xb, s))
-        torch.cuda.synchronize()
-        out[f"probe_gemm_fused_verify_deep_xb{xb}_4096"] = {
-            "ms": round(ms, 4), "tflops": round(2.0 * 4096 ** 3 / ms / 1e9, 1), "errors": int(p.counters[16].item())}
+    for rep in range(1):
+        for v in range(8):  # bit 0 XB, bits 1-2 tile grouping GM = 1/2/4/8
+            p.counters.zero_()
+            ms = timeit(lambda: lib.odh_probe_gemm_verify_deep(p.a.data_ptr(), p.bt.data_ptr(), p.m, p.n, p.k,
+                                                               p.tile_xcd.data_ptr(), cnt, cnt + 64, cnt + 32, v, s))
+            torch.cuda.synchronize()
+            out[f"probe_gemm_fused_verify_deep_v{v}_r{rep}_4096"] = {
+                "ms": round(ms, 4), "tflops": round(2.0 * 4096 ** 3 / ms / 1e9, 1),
+                "errors": int(p.counters[16].item())}
     for nt in (0, 1):
         ms = timeit(lambda: lib.odh_hbm_write(p.hbm.data_ptr(), p.hbm_bytes, 7, nt, s))
         out[f"hbm_write_nt{nt}_1GiB"] = {"ms": round(ms, 4), "gbps": round(p.hbm_bytes / ms / 1e6, 1)}
@@ -94,16 +99,14 @@ def main():
             out[f"hbm_write_v{v}_b{blocks}"] = {"ms": round(ms, 4), "gbps": round(p.hbm_bytes / ms / 1e6, 1)}
     big = torch.empty((4 << 30) // 4, dtype=torch.int32, device=dev)
     for v in (1, 3):
-        ms = timeit(lambda: lib.odh_hbm_write_variant(big.data_ptr(), 4 << 30, 7, v, 4096, s), iters=5)
+        ms = timeit(lambda: lib.odh_hbm_write_variant(big.data_ptr(), 4 << 30, 7, v, 4096, s), iters=5, warm_s=0.05)
         out[f"hbm_write_v{v}_4GiB"] = {"ms": round(ms, 4), "gbps": round((4 << 30) / ms / 1e6, 1)}
-    ms = timeit(lambda: big.fill_(3), iters=5)
+    ms = timeit(lambda: big.fill_(3), iters=5, warm_s=0.05)
     out["torch_fill_4GiB"] = {"ms": round(ms, 4), "gbps": round((4 << 30) / ms / 1e6, 1)}
     del big
     lib.odh_hbm_write(p.hbm.data_ptr(), p.hbm_bytes, 7, 0, s)  # check against a matching pattern (the probe's case)
     ms = timeit(lambda: lib.odh_hbm_check(p.hbm.data_ptr(), p.hbm_bytes, 7, cnt + 72, s))
     out["hbm_check_1GiB"] = {"ms": round(ms, 4), "gbps": round(p.hbm_bytes / ms / 1e6, 1)}
-    lib.odh_hbm_check_variant.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint32, ctypes.c_void_p,
-                                          ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
     lib.odh_hbm_write(p.hbm.data_ptr(), p.hbm_bytes, 7, 0, s)
     for v in (0, 1, 2, 3):
         for blocks in (1024, 2048, 4096, 8192):

@@ -2,7 +2,7 @@
 # First GPU pass: env probe, build, gpu tests, smoke, bench, rocprof stats.
 set -o pipefail
 mkdir -p gpurun_out
-cd /root/repo
+cd "${GRAFT_REPO_ROOT:-/root/repo}"
 export TMPDIR=/tmp
 timeout -k 10 120 bash tools/gpu_env_probe.sh > /dev/null 2>&1
 python -m odh_kubeflow_amd.ops.build > gpurun_out/build.log 2>&1 || exit 1

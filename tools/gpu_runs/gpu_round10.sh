@@ -2,7 +2,7 @@
 # GPU pass 10: GEMM fragment-pipelining A/B + gpu tests.
 set -o pipefail
 mkdir -p gpurun_out
-cd /root/repo
+cd "${GRAFT_REPO_ROOT:-/root/repo}"
 python -m odh_kubeflow_amd.ops.build > gpurun_out/build.log 2>&1 || exit 1
 timeout -k 10 600 python -m pytest tests -m gpu -x -q > gpurun_out/pytest_gpu.log 2>&1 || { tail -60 gpurun_out/pytest_gpu.log; exit 1; }
 tail -2 gpurun_out/pytest_gpu.log

@@ -3,7 +3,7 @@
 # on the one GPU (ranks share the device), rocprofv3 kernel stats of the default bench.
 set -o pipefail
 mkdir -p gpurun_out
-cd /root/repo
+cd "${GRAFT_REPO_ROOT:-/root/repo}"
 export TMPDIR=/tmp
 show() { python -c "import json,sys; d=json.loads([l for l in open('$1') if l.startswith('{')][-1]); print('$2', d['n_gpus'], d['value'], d['ms_per_step'], d['p50_ready_ms'], d['p95_ready_ms'], d.get('p50_teardown_ms'), d.get('gpu_probe', {}).get('gpu_ms_p50'), d.get('inprocess_n1'))"; }
 timeout -k 10 400 python bench.py > gpurun_out/b12_default.log 2>&1 || { tail -40 gpurun_out/b12_default.log; exit 1; }

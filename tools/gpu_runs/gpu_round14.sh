@@ -3,7 +3,7 @@
 # numerics + A/B against the 2-buffer BK=64 kernel; full gpu test suite.
 set -o pipefail
 mkdir -p gpurun_out
-cd /root/repo
+cd "${GRAFT_REPO_ROOT:-/root/repo}"
 export TMPDIR=/tmp
 timeout -k 10 300 python -u -m pytest tests/test_gpu_ops.py -x -v --timeout 120 --timeout-method thread > gpurun_out/pytest_gpu14.log 2>&1 || { tail -60 gpurun_out/pytest_gpu14.log; exit 1; }
 tail -2 gpurun_out/pytest_gpu14.log

@@ -4,7 +4,7 @@
 # on the one GPU (ranks share the device; the 8-GPU node run is the driver's), rocprof stats.
 set -o pipefail
 mkdir -p gpurun_out
-cd /root/repo
+cd "${GRAFT_REPO_ROOT:-/root/repo}"
 export TMPDIR=/tmp
 show() { python -c "import json,sys; d=json.loads([l for l in open('$1') if l.startswith('{')][-1]); print('$2', d['n_gpus'], d['value'], d['ms_per_step'], d['p50_ready_ms'], d['p95_ready_ms'], d.get('p50_teardown_ms'), d.get('gpu_probe', {}).get('gpu_ms_p50'), d.get('gpu_probe', {}).get('gemm_tflops_p50'), d.get('inprocess_n1'))"; }
 timeout -k 10 400 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/pytest_gpu16.log 2>&1 || { tail -60 gpurun_out/pytest_gpu16.log; exit 1; }

@@ -3,7 +3,7 @@
 # in flight per lane, 1k-8k slab blocks; torch read reference.
 set -o pipefail
 mkdir -p gpurun_out
-cd /root/repo
+cd "${GRAFT_REPO_ROOT:-/root/repo}"
 timeout -k 10 300 python tools/probe_microbench.py > gpurun_out/microbench17.json 2> gpurun_out/microbench17.err || { tail -30 gpurun_out/microbench17.err; exit 1; }
 python - <<'PY'
 import json

@@ -3,7 +3,7 @@
 # two passes each; kernel numerics tests.
 set -o pipefail
 mkdir -p gpurun_out
-cd /root/repo
+cd "${GRAFT_REPO_ROOT:-/root/repo}"
 timeout -k 10 300 python -u -m pytest tests/test_gpu_ops.py -x -q --timeout 120 --timeout-method thread > gpurun_out/pytest_gpu18.log 2>&1 || { tail -60 gpurun_out/pytest_gpu18.log; exit 1; }
 tail -1 gpurun_out/pytest_gpu18.log
 timeout -k 10 300 python tools/probe_microbench.py > gpurun_out/microbench18.json 2> gpurun_out/microbench18.err || { tail -30 gpurun_out/microbench18.err; exit 1; }

@@ -2,7 +2,7 @@
 # GPU pass 2: all gpu tests, smoke, bench (full odh path), torchrun nproc=1, rocprof kernel stats (csv).
 set -o pipefail
 mkdir -p gpurun_out
-cd /root/repo
+cd "${GRAFT_REPO_ROOT:-/root/repo}"
 export TMPDIR=/tmp
 python -m odh_kubeflow_amd.ops.build > gpurun_out/build.log 2>&1 || exit 1
 timeout -k 10 600 python -m pytest tests -m gpu -x -q > gpurun_out/pytest_gpu.log 2>&1 || { tail -40 gpurun_out/pytest_gpu.log; exit 1; }

@@ -1,0 +1,60 @@
+"""kube-scheduler stand-in as its own process: binds pods and allocates ``amd.com/gpu``.
+
+    python -m odh_kubeflow_amd.cmd.scheduler --master http://127.0.0.1:6443
+
+In a real cluster kube-scheduler (plus the AMD device plugin) is a separate process from
+the notebook controllers; the multi-GPU benchmark runs this one as a child of rank 0 so
+that no control-plane shard pays for the whole node's scheduling on its own event loop
+(every shard then reaches the scheduler through the apiserver alike).  Prints ``ready``
+on stdout once its informers have synced.
+"""
+
+from __future__ import annotations
+
+import argparse
+import asyncio
+import logging
+import sys
+
+log = logging.getLogger("scheduler")
+
+
+def parse(argv=None):
+    p = argparse.ArgumentParser(prog="odh-scheduler")
+    p.add_argument("--master", default=None)
+    p.add_argument("--kubeconfig", default=None)
+    p.add_argument("--max-concurrent", type=int, default=1,
+                   help="scheduling decisions are serialised by the allocator lock anyway")
+    p.add_argument("--debug-log", action="store_true")
+    return p.parse_args(argv)
+
+
+async def amain(argv=None) -> int:
+    from ..kubelet.node import SchedulerController
+    from ..models import kinds
+    from ..runtime.manager import Manager
+    from ..runtime.rest import RestConfig
+    from .common import setup_logging, signal_event
+
+    args = parse(argv)
+    setup_logging(debug=args.debug_log)
+    cfg = RestConfig.load(args.master, args.kubeconfig)
+    mgr = Manager.remote(cfg, name="kube-scheduler")
+    SchedulerController(mgr.client, mgr.reader, mgr.get_event_recorder_for("default-scheduler")) \
+        .setup_with_manager(mgr, max_concurrent=args.max_concurrent)
+    await mgr.start()
+    await mgr.cache.wait_synced([kinds.POD, kinds.NODE, kinds.NAMESPACE])
+    print("ready", flush=True)
+    await signal_event().wait()
+    await mgr.stop()
+    await mgr.cache.stop()
+    await mgr.rest.close()
+    return 0
+
+
+def main(argv=None) -> int:
+    return asyncio.run(amain(argv))
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -3,11 +3,12 @@
 Layout on an 8×MI355X node (see :mod:`.shard` for the design):
 
 * **rank 0** starts the native C++ apiserver (``odh-apiserver``: store, REST/watch,
-  admission, GC) as a child process and broadcasts its URL;
+  admission, GC) and the scheduler (``cmd/scheduler.py``, the kube-scheduler stand-in
+  with the ``amd.com/gpu`` allocator) as child processes and broadcasts the URL;
 * **every rank r** runs a namespace shard of the control plane against it — kf + odh
   reconcilers, the odh webhook server, the StatefulSet controller and the node agent
   of GPU ``LOCAL_RANK`` — owning the notebooks of namespace ``bench-r``; rank 0's shard
-  also hosts the scheduler and registers the Node;
+  also registers the Node, and is otherwise identical to the others;
 * each rank drives its own notebooks: one step = create one ``amd.com/gpu: 1`` Notebook
   in its namespace → Ready (pod started by whichever GPU's node agent the scheduler
   allocated, after the MI355X start-up probe on that GPU) → delete → gone.
@@ -102,6 +103,7 @@ def measure(args) -> Optional[dict]:
         out["config"]["parallelism"] = (f"namespace-sharded control plane x{world} (one rank per MI355X: kf+odh "
                                         f"reconcilers, webhook, STS controller, node agent); native C++ apiserver")
         out["config"]["architecture"] = "sharded"
+        out["rank_ms_per_step"] = res.get("rank_ms_per_step")
         if rccl_ms is not None:
             out["rccl_allreduce_check_ms"] = round(rccl_ms, 3)
     dist.barrier()
@@ -113,6 +115,7 @@ async def _main(args, dist, torch, rank: int, world: int, local_rank: int, probe
     from .shard import ControlPlaneShard, ShardConfig
 
     native = None
+    sched = None
     url = [None]
     if rank == 0:
         from ..apiserver.native import NativeApiServer
@@ -120,12 +123,14 @@ async def _main(args, dist, torch, rank: int, world: int, local_rank: int, probe
 
         native = await NativeApiServer(OPENSHIFT_CRDS, gc=True).start()
         url[0] = native.url
+        sched = await _start_scheduler(native.url)
     await _in_thread(dist.broadcast_object_list, url, 0)
     use_odh = not args.no_odh
     env = {"SET_PIPELINE_RBAC": "false", "SET_PIPELINE_SECRET": "false"}
     shard = ControlPlaneShard(ShardConfig(
         apiserver_url=url[0], namespace=bench_namespace(rank), gpu=local_rank % 8, bootstrap=(rank == 0),
-        odh=use_odh, webhook=use_odh, startup_probe=probe, reference_emulation=args.reference_emulation, env=env))
+        run_scheduler=False, odh=use_odh, webhook=use_odh, startup_probe=probe,
+        reference_emulation=args.reference_emulation, env=env))
     if rank == 0:
         await shard.start()  # namespaces, Node, scheduler first
         await _in_thread(dist.barrier)
@@ -139,9 +144,35 @@ async def _main(args, dist, torch, rank: int, world: int, local_rank: int, probe
     finally:
         await _in_thread(dist.barrier)  # nobody tears down while others still serve
         await shard.stop()
+        if sched is not None:
+            await _stop_child(sched)
         if native is not None:
             await native.stop()
     return result
+
+
+async def _start_scheduler(url: str):
+    """kube-scheduler stand-in as a child process of rank 0 (see ``cmd/scheduler.py``)."""
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    env = dict(os.environ, PYTHONPATH=root + os.pathsep + os.environ.get("PYTHONPATH", ""))
+    proc = subprocess.Popen([sys.executable, "-m", "odh_kubeflow_amd.cmd.scheduler", "--master", url],
+                            cwd=root, env=env, stdout=subprocess.PIPE, stderr=subprocess.DEVNULL, text=True)
+    line = await asyncio.wait_for(_in_thread(proc.stdout.readline), 120)
+    if line.strip() != "ready":
+        proc.kill()
+        raise RuntimeError(f"scheduler process did not start (rc={proc.poll()})")
+    return proc
+
+
+async def _stop_child(proc) -> None:
+    proc.terminate()
+    try:
+        await asyncio.wait_for(_in_thread(proc.wait), 10)
+    except asyncio.TimeoutError:
+        proc.kill()
 
 
 async def _drive(args, shard, dist, torch) -> dict:
@@ -183,6 +214,7 @@ async def _drive(args, shard, dist, torch) -> dict:
     t_start = time.perf_counter()
     for _ in range(args.steps):
         await one_step(True)
+    own = time.perf_counter() - t_start  # this rank's own steps (the barrier below equalises elapsed)
     await shard.settle(5)  # the last teardown's trailing reconciles stay inside the timed region
     state["recon"] = shard.reconcile_count() - r0
     if torch.cuda.is_available():
@@ -196,8 +228,9 @@ async def _drive(args, shard, dist, torch) -> dict:
     await _in_thread(lambda: dist.all_reduce(rc, op=dist.ReduceOp.SUM))
     gathered = [None] * dist.get_world_size()
     await _in_thread(dist.all_gather_object, gathered, {"lat": lat_ms, "probes": shard.probe_results,
-                                                        "teardown": teardown_ms})
+                                                        "teardown": teardown_ms, "own_s": own})
     return {"elapsed": float(el.item()), "reconciles": int(rc.item()),
             "lat_ms": [x for g in gathered for x in g["lat"]], "odh": use_odh,
             "probes": [p for g in gathered for p in g["probes"]],
-            "teardown_ms": [x for g in gathered for x in g["teardown"]]}
+            "teardown_ms": [x for g in gathered for x in g["teardown"]],
+            "rank_ms_per_step": [round(g["own_s"] / max(1, args.steps) * 1e3, 3) for g in gathered]}

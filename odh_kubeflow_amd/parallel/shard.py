@@ -19,8 +19,9 @@ plane the way the node is scaled — one process per GPU — by sharding it on n
   the scheduler together with the ``amd.com/gpu-ids`` allocation); the shard labels its
   namespace ``amd.com/gpu-affinity=r`` so the allocator gives its pods GPU ``r`` while it
   is free — pod start-up then stays inside the shard's own process;
-* the bootstrap shard (rank 0) also runs the cluster-wide singletons: scheduler (with
-  ``amd.com/gpu`` bin-packing) and Node registration.  GC runs in the apiserver.
+* the bootstrap shard (rank 0) also registers the Node and, unless the scheduler runs as
+  its own process (``cmd/scheduler.py``, what the multi-GPU benchmark does), schedules
+  pods (``amd.com/gpu`` allocation).  GC runs in the apiserver.
 """
 
 from __future__ import annotations
@@ -44,6 +45,10 @@ class ShardConfig:
     node_gpus: int = 8
     controller_namespace: str = "opendatahub"
     bootstrap: bool = False
+    # the bootstrap shard hosts the scheduler unless it runs as its own process
+    # (``cmd/scheduler.py``, as kube-scheduler does); the node agent then watches only
+    # its GPU's pods on every shard, bootstrap included (no CPU-only pods in that mode)
+    run_scheduler: bool = True
     odh: bool = True
     webhook: bool = True
     startup_probe: Optional[Callable] = None
@@ -106,18 +111,19 @@ class ControlPlaneShard:
             .setup_with_manager(kube)
 
         # node agent of this rank's GPU (+ the cluster-wide scheduler on the bootstrap shard)
-        if cfg.bootstrap:
+        schedules = cfg.bootstrap and cfg.run_scheduler
+        if schedules:
             node_cache = InformerCache(self.rest)
         else:
             node_cache = InformerCache(self.rest, selectors={kinds.POD: f"{GPU_INDEX_LABEL}={cfg.gpu}"})
         self._caches.append(node_cache)
         kl = self._mgr(f"kubelet-gpu{cfg.gpu}", (self.rest, node_cache))
-        if cfg.bootstrap:
+        if schedules:
             SchedulerController(kl.client, kl.reader, kl.get_event_recorder_for("default-scheduler")) \
                 .setup_with_manager(kl)
         self.agent = NodeAgent(kl, cfg.node_name, [cfg.gpu], node_gpus=cfg.node_gpus,
                                startup_probe=cfg.startup_probe, register_node=cfg.bootstrap,
-                               owns_cpu_pods=cfg.bootstrap)
+                               owns_cpu_pods=schedules)
 
         if cfg.webhook and cfg.odh:
             await self._start_webhook(shared)

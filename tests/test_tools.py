@@ -14,3 +14,19 @@ def test_loadtest_local_cluster_measures_every_notebook():
     assert out.returncode == 0, out.stderr[-2000:]
     d = json.loads(out.stdout.strip().splitlines()[-1])
     assert d["count"] == 4 and d["ready"] == 4 and d["p50_ready_ms"] > 0
+
+
+def test_bench_culling_cpu_rehearsal():
+    """BASELINE config #5 on a synthetic sysfs: GPU-busy notebook kept, idle ones reclaimed."""
+    import json
+    import subprocess
+    import sys
+
+    out = subprocess.run([sys.executable, "tools/bench_culling.py", "--cpu", "--idle-s", "1", "--period-s", "0.1",
+                          "--load-s", "2.5"], capture_output=True, text=True, timeout=120,
+                         cwd=__import__("os").path.dirname(__import__("os").path.dirname(__file__)))
+    assert out.returncode == 0, out.stderr[-2000:]
+    d = json.loads(out.stdout.strip().splitlines()[-1])
+    assert d["false_culls_under_load"] == 0 and d["culled"] == 8
+    assert d["gpu0_busy_mean_under_load"] >= 90
+    assert 0 <= d["idle_reclaim_ms_p50"] < 1500

@@ -42,16 +42,22 @@ def available() -> bool:
 
 
 class NativeApiServer:
+    """``binary`` (or ``$ODH_APISERVER_BINARY``) selects another build of the server, e.g. the
+    ThreadSanitizer one the race-detection test compiles; ``env`` is added to its environment."""
+
     def __init__(self, uninstalled: Iterable[str] = (), gc: bool = False, token: Optional[str] = None,
-                 host: str = "127.0.0.1", port: int = 0, history: int = 4096):
+                 host: str = "127.0.0.1", port: int = 0, history: int = 4096, binary: Optional[str] = None,
+                 env: Optional[dict] = None):
         self.cfg = scheme_config(uninstalled, gc, token, history)
         self.host = host
         self.port = port
+        self.binary = binary or os.environ.get("ODH_APISERVER_BINARY") or BINARY
+        self.env = env
         self.proc: Optional[asyncio.subprocess.Process] = None
         self._cfg_path: Optional[str] = None
 
     async def start(self) -> "NativeApiServer":
-        if not available():
+        if self.binary == BINARY and not available():
             from ..ops.build import build
 
             build(verbose=False)
@@ -59,8 +65,8 @@ class NativeApiServer:
         with os.fdopen(fd, "w") as f:
             json.dump(self.cfg, f)
         self.proc = await asyncio.create_subprocess_exec(
-            BINARY, "--config", self._cfg_path, "--host", self.host, "--port", str(self.port),
-            stdout=asyncio.subprocess.PIPE)
+            self.binary, "--config", self._cfg_path, "--host", self.host, "--port", str(self.port),
+            stdout=asyncio.subprocess.PIPE, env={**os.environ, **self.env} if self.env else None)
         line = await asyncio.wait_for(self.proc.stdout.readline(), 30)
         if not line.startswith(b"LISTENING"):
             raise RuntimeError(f"native apiserver failed to start: {line!r}")

@@ -34,6 +34,10 @@ def parse(argv: Optional[List[str]] = None) -> argparse.Namespace:
     p.add_argument("--kubeconfig", default=None)
     p.add_argument("--master", default=None)
     p.add_argument("--max-concurrent-reconciles", type=int, default=8)
+    # controller-runtime's LeaseDuration / RenewDeadline / RetryPeriod (defaults 15 s / 10 s / 2 s)
+    p.add_argument("--leader-election-lease-duration", type=float, default=15.0)
+    p.add_argument("--leader-election-renew-deadline", type=float, default=10.0)
+    p.add_argument("--leader-election-retry-period", type=float, default=2.0)
     return p.parse_args(argv)
 
 
@@ -52,7 +56,10 @@ def build(args, env=os.environ):
     elector = None
     if args.enable_leader_election:
         elector = LeaderElector(RestClient(cfg), "kubeflow-notebook-controller",
-                                args.leader_election_namespace or namespace_from_env())
+                                args.leader_election_namespace or namespace_from_env(),
+                                lease_duration=args.leader_election_lease_duration,
+                                renew_deadline=args.leader_election_renew_deadline,
+                                retry_period=args.leader_election_retry_period)
     mgr = Manager.remote(cfg, name="notebook-controller", default_max_concurrent=args.max_concurrent_reconciles,
                          leader_elector=elector, metrics_addr=args.metrics_addr, probe_addr=args.probe_addr)
     metrics = NotebookMetrics(mgr.reader, mgr.registry)

@@ -1861,7 +1861,11 @@ void serve_watch(int fd, Res& r, const Path& p, const Request& rq) {
     {
       std::unique_lock<std::mutex> lk(S.mu);
       Bucket& b = bucket(r);
-      slot.cv.wait_for(lk, std::chrono::milliseconds(500), [&] { return b.seq > last_seq || g_stop.load(); });
+      // system_clock deadline: libstdc++ maps a steady_clock wait to pthread_cond_clockwait,
+      // which ThreadSanitizer (GCC 11) does not intercept; the 500 ms timeout only paces
+      // catch-up scans, so a wall-clock jump is harmless here
+      slot.cv.wait_until(lk, std::chrono::system_clock::now() + std::chrono::milliseconds(500),
+                         [&] { return b.seq > last_seq || g_stop.load(); });
       if (b.seq > last_seq) {
         if (!b.hist.empty() && b.hist.front().seq > last_seq + 1) {
           gone = true;  // the watcher fell behind the bounded history
@@ -1929,11 +1933,16 @@ bool handle(int fd, Request& rq) {
                    rq.keep_alive);
   }
   if (rq.method == "GET" && rq.path == "/metrics") {
+    int64_t rv;
+    {
+      std::lock_guard<std::mutex> g(S.mu);
+      rv = S.rv;
+    }
     char buf[256];
     snprintf(buf, sizeof(buf),
              "{\"requests\":%llu,\"writes\":%llu,\"webhook_calls\":%llu,\"resourceVersion\":%lld}",
              (unsigned long long)S.requests.load(), (unsigned long long)S.writes.load(),
-             (unsigned long long)S.webhook_calls.load(), (long long)S.rv);
+             (unsigned long long)S.webhook_calls.load(), (long long)rv);
     return respond(fd, 200, buf, rq.keep_alive);
   }
   try {

@@ -27,7 +27,9 @@ log = logging.getLogger("runtime.leaderelection")
 
 
 def default_identity() -> str:
-    return f"{socket.gethostname()}_{uuid.uuid4()}"
+    """``<hostname>_<uuid>`` like controller-runtime; ``POD_NAME`` (downward API) names the
+    pod instead of the container hostname when it is set."""
+    return f"{os.environ.get('POD_NAME') or socket.gethostname()}_{uuid.uuid4()}"
 
 
 class LeaderElector:

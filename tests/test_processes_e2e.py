@@ -263,3 +263,62 @@ def test_processes_notebook_lifecycle_like_reference_e2e(tmp_path, run):
             except subprocess.TimeoutExpired:
                 p.kill()
         logf.close()
+
+
+def test_kf_manager_leader_failover(tmp_path, run):
+    """HA (kf/main.go:91-93 leader election): two kf managers, short leases; SIGKILL the leader
+    (no graceful release) — the standby acquires the expired Lease and reconciles new work."""
+    api_port = free_port()
+    logf = open(tmp_path / "procs.log", "wb")
+    master = f"http://127.0.0.1:{api_port}"
+    procs = [spawn(["odh_kubeflow_amd.cmd.apiserver", "--port", str(api_port), "--controllers",
+                    "--no-openshift-apis"], log=logf)]
+    managers = {}
+    try:
+        async def go():
+            await wait_http(master + "/healthz")
+            c = RestClient(RestConfig(host=master))
+            for ns in ("opendatahub", "user"):
+                await c.create({"apiVersion": "v1", "kind": "Namespace", "metadata": {"name": ns}})
+            for name in ("kf-a", "kf-b"):
+                managers[name] = spawn(["odh_kubeflow_amd.cmd.kf_manager", "--master", master, "--metrics-addr", "0",
+                                        "--probe-addr", "0", "--enable-leader-election",
+                                        "--leader-election-lease-duration", "2",
+                                        "--leader-election-renew-deadline", "1.5",
+                                        "--leader-election-retry-period", "0.2"],
+                                       {"K8S_NAMESPACE": "opendatahub", "POD_NAME": name}, logf)
+                procs.append(managers[name])
+
+            async def holder():
+                lease = await c.get(kinds.LEASE, "kubeflow-notebook-controller", "opendatahub")
+                h = (lease.get("spec") or {}).get("holderIdentity") or ""
+                return h.split("_")[0] if h else None
+
+            first = await eventually(holder, 30)
+            await c.create(notebook("nb1", "user"))
+            await eventually(lambda: c.get(kinds.STATEFUL_SET, "nb1", "user"), 30)
+            t_kill = time.monotonic()
+            managers[first].kill()  # SIGKILL: the lease is not released, it has to expire
+            managers[first].wait(10)
+            await c.create(notebook("nb2", "user"))
+            await eventually(lambda: c.get(kinds.STATEFUL_SET, "nb2", "user"), 30)
+            takeover = time.monotonic() - t_kill
+            second = await holder()
+            lease = await c.get(kinds.LEASE, "kubeflow-notebook-controller", "opendatahub")
+            await c.close()
+            return first, second, lease["spec"].get("leaseTransitions", 0), takeover
+
+        first, second, transitions, takeover = run(go(), timeout=90)
+        assert second != first and {first, second} == {"kf-a", "kf-b"}
+        assert transitions >= 1
+        assert takeover < 15  # lease 2 s + retry 0.2 s + reconcile
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.terminate()
+        for p in procs:
+            try:
+                p.wait(10)
+            except subprocess.TimeoutExpired:
+                p.kill()
+        logf.close()

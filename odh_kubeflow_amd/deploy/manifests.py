@@ -395,6 +395,19 @@ def tree() -> Dict[str, object]:
     return t
 
 
+class _Dumper(yaml.SafeDumper):
+    """Block style for structure, flow style (``[a, b]``) for short lists of scalars."""
+
+
+def _represent_list(dumper, data):
+    flow = 0 < len(data) <= 8 and all(isinstance(x, (str, int, float, bool)) or x is None for x in data) \
+        and sum(len(str(x)) for x in data) <= 72
+    return dumper.represent_sequence("tag:yaml.org,2002:seq", data, flow_style=flow)
+
+
+_Dumper.add_representer(list, _represent_list)
+
+
 def write(out: str) -> List[str]:
     written = []
     for path, doc in sorted(tree().items()):
@@ -405,9 +418,9 @@ def write(out: str) -> List[str]:
             if isinstance(doc, str):
                 f.write(doc)
             elif isinstance(doc, list):
-                yaml.safe_dump_all(doc, f, sort_keys=False)
+                yaml.dump_all(doc, f, Dumper=_Dumper, sort_keys=False)
             else:
-                yaml.safe_dump(doc, f, sort_keys=False)
+                yaml.dump(doc, f, Dumper=_Dumper, sort_keys=False)
         written.append(full)
     return written
 

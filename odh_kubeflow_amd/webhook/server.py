@@ -89,6 +89,8 @@ def mutating_webhook_configuration(ca_bundle_b64: str, url: Optional[str] = None
         "webhooks": [{
             "name": "notebooks.opendatahub.io", "admissionReviewVersions": ["v1"], "clientConfig": cc,
             "failurePolicy": "Fail", "sideEffects": "None",
+            # the apiserver defaults, spelled out: the webhook's latency budget is explicit
+            "timeoutSeconds": 10, "matchPolicy": "Equivalent", "reinvocationPolicy": "Never",
             "rules": [{"apiGroups": ["kubeflow.org"], "apiVersions": ["v1"], "operations": ["CREATE", "UPDATE"],
                        "resources": ["notebooks"]}],
             **({"namespaceSelector": namespace_selector} if namespace_selector else {}),

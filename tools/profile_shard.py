@@ -17,8 +17,12 @@ from odh_kubeflow_amd.utils import gctune  # noqa: E402
 
 
 async def main(n_steps: int, sort: str):
+    from odh_kubeflow_amd.parallel.bench_dist import _start_scheduler, _stop_child
+
     native = await NativeApiServer(OPENSHIFT_CRDS, gc=True).start()
+    sched = await _start_scheduler(native.url)  # as in the benchmark: kube-scheduler is its own process
     sh = await ControlPlaneShard(ShardConfig(apiserver_url=native.url, namespace="bench-0", gpu=0, bootstrap=True,
+                                             run_scheduler=False,
                                              env={"SET_PIPELINE_RBAC": "false",
                                                   "SET_PIPELINE_SECRET": "false"})).start()
 
@@ -26,9 +30,9 @@ async def main(n_steps: int, sort: str):
         nm = f"nb{i}"
         await sh.admin.create(notebook(nm, "bench-0", image="img", gpus=1,
                                        annotations={"notebooks.opendatahub.io/inject-auth": "true"}))
-        await sh.wait_for(lambda: sh.notebook_ready(nm), 30)
+        await sh.wait_until(lambda: sh.notebook_ready(nm), 30)
         await sh.admin.delete(kinds.NOTEBOOK, nm, "bench-0")
-        await sh.wait_for(lambda: sh.gone(nm), 30)
+        await sh.wait_until(lambda: sh.gone(nm), 30)
 
     for i in range(5):
         await step(i)
@@ -44,6 +48,7 @@ async def main(n_steps: int, sort: str):
     print(f"ms/step {el / n_steps * 1e3:.3f}")
     pstats.Stats(pr).sort_stats(sort).print_stats(45)
     await sh.stop()
+    await _stop_child(sched)
     await native.stop()
 
 

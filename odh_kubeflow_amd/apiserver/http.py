@@ -26,12 +26,12 @@ import logging
 import ssl
 import time
 import uuid
-from typing import Callable, Dict, List, Optional, Tuple
+from typing import Callable, Dict, List, Optional
 
 from aiohttp import web
 
 from ..models import meta as m
-from ..models.errors import ApiError, BadRequest, Forbidden, InternalError, NotFound
+from ..models.errors import ApiError, BadRequest, InternalError, NotFound
 from ..models.scheme import SCHEME, ResourceInfo
 from ..utils import jsonpatch
 from ..utils.selectors import match_labels, selector_from_dict

@@ -17,7 +17,7 @@ import os
 import tempfile
 from typing import Iterable, List, Optional
 
-from ..models.scheme import OPTIONAL_CRDS, SCHEME
+from ..models.scheme import SCHEME
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 BINARY = os.path.join(os.path.dirname(HERE), "native", "bin", "odh-apiserver")

@@ -26,16 +26,14 @@ treated as read-only; every object returned by a read is a private copy.
 
 from __future__ import annotations
 
-import asyncio
 import itertools
 import logging
 import random
-import string
 import threading
 import uuid
 from collections import deque
 from dataclasses import dataclass
-from typing import Any, Awaitable, Callable, Deque, Dict, Iterable, List, Optional, Tuple
+from typing import Any, Awaitable, Callable, Deque, Dict, List, Optional, Tuple
 
 from ..models import meta as m
 from ..models.errors import (AlreadyExists, ApiError, BadRequest, Conflict, Forbidden, Gone, Invalid, NoKindMatch,

@@ -11,7 +11,7 @@ import asyncio
 import os
 import time
 from dataclasses import dataclass, field
-from typing import Callable, Dict, List, Mapping, Optional, Sequence
+from typing import Callable, Dict, List, Optional
 
 from .apiserver.store import ObjectStore
 from .models import kinds

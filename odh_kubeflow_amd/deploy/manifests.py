@@ -35,7 +35,6 @@ from typing import Dict, List
 
 import yaml
 
-from ..controllers.odh.constants import KUBE_RBAC_PROXY_PORT
 from ..models.notebook import GPU_RESOURCE, VERSIONS
 
 ROCM_NOTEBOOK_IMAGE = "rocm/pytorch:rocm7.0_ubuntu22.04_py3.10_pytorch_release_2.10.0"

@@ -18,7 +18,6 @@ GPU r); one agent for the whole node is the DaemonSet layout.
 
 from __future__ import annotations
 
-import asyncio
 import logging
 from typing import Callable, Dict, List, Optional, Sequence
 

@@ -18,7 +18,6 @@ from __future__ import annotations
 
 import asyncio
 import logging
-import socket
 import time
 from typing import Awaitable, Callable, Dict, Iterable, List, Optional, Sequence, Set
 

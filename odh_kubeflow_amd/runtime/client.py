@@ -20,7 +20,7 @@ import abc
 from typing import Any, Callable, Dict, Iterable, List, Optional, Sequence, Tuple
 
 from ..apiserver.store import ObjectStore
-from ..models.scheme import SCHEME, ResourceInfo
+from ..models.scheme import SCHEME
 from ..utils.objutil import deepcopy_json
 
 WatchCallback = Callable[[str, dict, Optional[dict]], None]

@@ -12,11 +12,11 @@ import asyncio
 import logging
 import time
 import uuid
-from typing import Dict, Optional, Tuple
+from typing import Dict, Tuple
 
 from ..models import meta as m
 from ..models.errors import ApiError, is_not_found
-from ..utils.timeutil import rfc3339, rfc3339_micro
+from ..utils.timeutil import rfc3339
 
 log = logging.getLogger(__name__)
 

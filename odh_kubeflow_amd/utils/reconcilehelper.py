@@ -9,7 +9,7 @@ desired object alone does not force an update, but it is still copied over.
 
 from __future__ import annotations
 
-from typing import Any, Awaitable, Callable, Optional
+from typing import Callable
 
 from ..models import meta as m
 from ..models.errors import is_not_found

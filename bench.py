@@ -237,6 +237,10 @@ def report(args, n, res) -> dict:
         "notebooks_ready_per_s": round(len(lat) / el, 3) if el > 0 else None,
         "reconciles_per_notebook": round(res["reconciles"] / max(1, len(lat)), 2),
     }
+    if getattr(args, "reference_emulation", False):
+        # not the framework's numbers: the reference's serialising odh path, same harness
+        out["config"]["reference_emulation"] = True
+        out["config"]["parallelism"] = f"node-agent per GPU x{n}; reference emulation (1 odh worker, blocking lock removal)"
     if res.get("teardown_ms"):
         out["p50_teardown_ms"] = round(pct(res["teardown_ms"], 0.5), 3)
     if probes:

@@ -191,12 +191,19 @@ class GpuProbe:
         self.overlap = overlap
         self.runs = 0
         self.seed = 0x9E3779B9
+        # one probe in flight per GPU: runs share the counters, events and pinned host buffer
+        # (two pods probing the same device — ranks sharing a GPU in a rehearsal — take turns)
+        self._lock = threading.Lock()
 
     def run(self) -> dict:
         """One probe.  With ``overlap`` (default) the memory-bound HBM sweep and the
         MFMA-bound GEMM run concurrently on two streams of the probe: their waves co-reside
         on the CUs (the GEMM's 1 workgroup/CU leaves VGPRs and wave slots free), so the
         GEMM hides under the sweep instead of adding to it."""
+        with self._lock:
+            return self._run()
+
+    def _run(self) -> dict:
         import torch
 
         lib = load_library()

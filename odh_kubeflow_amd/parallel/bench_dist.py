@@ -104,11 +104,24 @@ def measure(args) -> Optional[dict]:
                                         f"reconcilers, webhook, STS controller, node agent); native C++ apiserver")
         out["config"]["architecture"] = "sharded"
         out["rank_ms_per_step"] = res.get("rank_ms_per_step")
+        out["cpu_ms_per_step"] = res.get("cpu_ms_per_step")
         if rccl_ms is not None:
             out["rccl_allreduce_check_ms"] = round(rccl_ms, 3)
     dist.barrier()
     dist.destroy_process_group()
     return out
+
+
+def _proc_cpu_s(pid: Optional[int]) -> Optional[float]:
+    """User + system CPU seconds of a child process (``/proc/<pid>/stat``), None if unreadable."""
+    if pid is None:
+        return None
+    try:
+        with open(f"/proc/{pid}/stat") as f:
+            fields = f.read().rsplit(")", 1)[1].split()
+        return (int(fields[11]) + int(fields[12])) / os.sysconf("SC_CLK_TCK")
+    except (OSError, IndexError, ValueError):
+        return None
 
 
 async def _main(args, dist, torch, rank: int, world: int, local_rank: int, probe) -> dict:
@@ -140,7 +153,8 @@ async def _main(args, dist, torch, rank: int, world: int, local_rank: int, probe
     await _in_thread(dist.barrier)  # every shard's webhook is registered before anyone creates
 
     try:
-        result = await _drive(args, shard, dist, torch)
+        children = {"apiserver": native.proc.pid if native else None, "scheduler": sched.pid if sched else None}
+        result = await _drive(args, shard, dist, torch, children)
     finally:
         await _in_thread(dist.barrier)  # nobody tears down while others still serve
         await shard.stop()
@@ -175,7 +189,7 @@ async def _stop_child(proc) -> None:
         proc.kill()
 
 
-async def _drive(args, shard, dist, torch) -> dict:
+async def _drive(args, shard, dist, torch, children: Optional[dict] = None) -> dict:
     from ..models import kinds
     from ..models.notebook import notebook
 
@@ -211,12 +225,21 @@ async def _drive(args, shard, dist, torch) -> dict:
         torch.cuda.synchronize()
     await _in_thread(dist.barrier)
     r0 = shard.reconcile_count()
+    children = children or {}
+    child_cpu0 = {k: _proc_cpu_s(pid) for k, pid in children.items()}
+    cpu0 = time.process_time()
     t_start = time.perf_counter()
     for _ in range(args.steps):
         await one_step(True)
     own = time.perf_counter() - t_start  # this rank's own steps (the barrier below equalises elapsed)
     await shard.settle(5)  # the last teardown's trailing reconciles stay inside the timed region
     state["recon"] = shard.reconcile_count() - r0
+    # CPU time per step of every process on the path: where a step's work goes when ranks are added
+    cpu = {"rank": time.process_time() - cpu0}
+    for k, pid in children.items():
+        c1 = _proc_cpu_s(pid)
+        if c1 is not None and child_cpu0.get(k) is not None:
+            cpu[k] = c1 - child_cpu0[k]
     if torch.cuda.is_available():
         torch.cuda.synchronize()
     await _in_thread(dist.barrier)
@@ -228,9 +251,15 @@ async def _drive(args, shard, dist, torch) -> dict:
     await _in_thread(lambda: dist.all_reduce(rc, op=dist.ReduceOp.SUM))
     gathered = [None] * dist.get_world_size()
     await _in_thread(dist.all_gather_object, gathered, {"lat": lat_ms, "probes": shard.probe_results,
-                                                        "teardown": teardown_ms, "own_s": own})
+                                                        "teardown": teardown_ms, "own_s": own, "cpu": cpu})
+    per_step = 1e3 / max(1, args.steps)
+    cpu_ms = {"ranks": [round(g["cpu"]["rank"] * per_step, 3) for g in gathered]}
+    for g in gathered:
+        for k, v in g["cpu"].items():
+            if k != "rank":
+                cpu_ms[k] = round(v * per_step, 3)
     return {"elapsed": float(el.item()), "reconciles": int(rc.item()),
             "lat_ms": [x for g in gathered for x in g["lat"]], "odh": use_odh,
             "probes": [p for g in gathered for p in g["probes"]],
             "teardown_ms": [x for g in gathered for x in g["teardown"]],
-            "rank_ms_per_step": [round(g["own_s"] / max(1, args.steps) * 1e3, 3) for g in gathered]}
+            "rank_ms_per_step": [round(g["own_s"] * per_step, 3) for g in gathered], "cpu_ms_per_step": cpu_ms}

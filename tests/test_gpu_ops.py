@@ -135,6 +135,22 @@ def test_startup_probe_async_hook(dev):
     assert r["results"][0]["xcds"] == 8
 
 
+def test_concurrent_probes_of_one_gpu_take_turns(dev):
+    """Several pods probing the same device at once (in-process node agents sharing a GPU)
+    must each get a complete, correct probe — runs share counters, events, host buffer."""
+    import asyncio
+
+    from odh_kubeflow_amd.ops.gpu import startup_probe
+
+    async def many():
+        return await asyncio.gather(*(startup_probe([0]) for _ in range(8)))
+
+    rs = asyncio.run(asyncio.wait_for(many(), 60))
+    for r in rs:
+        assert r["ok"], r
+        assert r["results"][0]["xcds"] == 8 and r["results"][0]["gemm_errors"] == 0
+
+
 @pytest.mark.parametrize("variant", [0, 1, 2, 3])
 @pytest.mark.parametrize("m,n,k", [(256, 256, 64), (512, 768, 192), (1024, 512, 4096), (2048, 2048, 1024)])
 def test_gemm256_variants_match_fp32_reference(dev, variant, m, n, k):

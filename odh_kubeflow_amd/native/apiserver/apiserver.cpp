@@ -553,6 +553,10 @@ struct Ev {
 
 struct WatchSlot {
   std::condition_variable cv;
+  // the watch's namespace / label / field filter: emit() wakes a watcher only for events it
+  // will deliver, so e.g. one node agent's label-selected cluster-wide pod watch is not
+  // woken by every other GPU's pod writes
+  std::function<bool(const Value&)> wants;
 };
 
 struct Bucket {
@@ -614,7 +618,10 @@ void emit(const Res& r, const char* type, Obj obj, Obj old) {
   }
   auto wake = [&](const std::string& ns) {
     auto rg = b.watchers.equal_range(ns);
-    for (auto it = rg.first; it != rg.second; ++it) it->second->cv.notify_all();
+    for (auto it = rg.first; it != rg.second; ++it) {
+      WatchSlot* w = it->second;
+      if (!w->wants || w->wants(*ev.obj) || (ev.old && w->wants(*ev.old))) w->cv.notify_all();
+    }
   };
   const std::string ns = mget(*ev.obj, "namespace");
   wake(ns);
@@ -1819,6 +1826,7 @@ void serve_watch(int fd, Res& r, const Path& p, const Request& rq) {
         }
     }
   } unregister{wb, ns, &slot};
+  slot.wants = wants;
   {
     std::lock_guard<std::mutex> g(S.mu);
     Bucket& b = bucket(r);

@@ -34,6 +34,10 @@ def test_bench_two_ranks_gloo():
               "vs_baseline", "dtype", "data", "config"):
         assert k in d
     assert d["n_gpus"] == 2 and d["steps"] == 3 and d["value"] > 0 and d["p50_ready_ms"] > 0
+    assert len(d["rank_ms_per_step"]) == 2
+    cpu = d["cpu_ms_per_step"]
+    assert len(cpu["ranks"]) == 2 and all(x > 0 for x in cpu["ranks"])
+    assert cpu["apiserver"] >= 0 and cpu["scheduler"] >= 0  # rank 0's child processes
 
 
 def test_bench_single_process_contract():
@@ -43,3 +47,14 @@ def test_bench_single_process_contract():
     d = json.loads([l for l in out.stdout.splitlines() if l.startswith("{")][-1])
     assert d["n_gpus"] == 1 and d["scaling"] == "weak" and d["higher_is_better"] is True
     assert d["config"]["odh_webhook_path"] is True
+
+
+def test_bench_reference_emulation_serialises():
+    """--reference-emulation restores the reference's blocking lock removal (1 s + 5 s
+    backoff, ``odh/controllers/notebook_controller.go:143-174``): ≈6 s per notebook."""
+    out = subprocess.run([sys.executable, "bench.py", "--arch", "inprocess", "--reference-emulation", "--steps", "1",
+                          "--warmup", "0", "--no-gpu-probe"], cwd=ROOT, capture_output=True, text=True, timeout=240)
+    assert out.returncode == 0, out.stderr[-3000:]
+    d = json.loads([l for l in out.stdout.splitlines() if l.startswith("{")][-1])
+    assert d["config"]["reference_emulation"] is True
+    assert 5500 < d["p50_ready_ms"] < 9000

@@ -390,10 +390,13 @@ class GpuRuntime:
             # the kubelet writes status only, so Ready costs one write, not two
             ok = bool(probe.get("ok"))
             r0 = (probe.get("results") or [{}])[0]
+            links = probe.get("links") or []
+            msg = f"bf16 MFMA {r0.get('gemm_tflops', 0):.0f} TFLOP/s, HBM {r0.get('hbm_gbps', 0):.0f} GB/s"
+            if links:  # multi-GPU pod: the xGMI ring over its GPUs was read and verified too
+                msg += f", xGMI {len(links)} links min {min(lk.get('gbps', 0) for lk in links):.0f} GB/s"
             conds.append({"type": PROBE_CONDITION, "status": "True" if ok else "False",
                           "reason": "MFMAAndHBMVerified" if ok else "GPUProbeFailed",
-                          "message": (f"bf16 MFMA {r0.get('gemm_tflops', 0):.0f} TFLOP/s, "
-                                      f"HBM {r0.get('hbm_gbps', 0):.0f} GB/s") if ok else str(probe.get("error")),
+                          "message": msg if ok else str(probe.get("error")),
                           "lastProbeTime": None, "lastTransitionTime": now})
         status = {"phase": "Running" if ready else "Pending", "conditions": conds, "containerStatuses": statuses,
                   "hostIP": self.host_ip, "podIP": handle.ip if handle else self.host_ip, "startTime": now}

@@ -21,6 +21,9 @@
 //    second GEMM: every element is compared bit-exactly on the GPU.
 //  * odh_hbm_write / odh_hbm_check — 16 B/lane streaming pattern write + verify over a
 //    resident HBM3E buffer (bandwidth and bit errors in one pass).
+//  * odh_peer_enable — lets one GPU read another's HBM over xGMI; the node agent's
+//    multi-GPU probe then runs odh_hbm_check on GPU j against GPU i's freshly written
+//    pattern buffer (a ring over the pod's GPUs: every link verified, per-link GB/s).
 //  * odh_busy — MFMA issue loop with 4 independent accumulators (drives gfx activity
 //    for the culler's amdgpu signal under synthetic load).
 //
@@ -917,6 +920,27 @@ int odh_hbm_check_variant(const void* buf, size_t bytes, uint32_t seed, unsigned
     default: return (int)hipErrorInvalidValue;
   }
   return (int)hipGetLastError();
+}
+
+// dev may read peer's memory afterwards (idempotent; restores the caller's current device)
+int odh_peer_enable(int dev, int peer) {
+  if (dev == peer) return 0;
+  int can = 0;
+  hipError_t e = hipDeviceCanAccessPeer(&can, dev, peer);
+  if (e != hipSuccess) return (int)e;
+  if (!can) return (int)hipErrorPeerAccessUnsupported;
+  int cur = 0;
+  e = hipGetDevice(&cur);
+  if (e != hipSuccess) return (int)e;
+  e = hipSetDevice(dev);
+  if (e != hipSuccess) return (int)e;
+  e = hipDeviceEnablePeerAccess(peer, 0);
+  if (e == hipErrorPeerAccessAlreadyEnabled) {
+    (void)hipGetLastError();  // clear the sticky "already enabled" status
+    e = hipSuccess;
+  }
+  hipError_t r = hipSetDevice(cur);
+  return (int)(e != hipSuccess ? e : r);
 }
 
 int odh_busy(float* out, int blocks, int iters, hipStream_t stream) {

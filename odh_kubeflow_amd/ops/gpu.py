@@ -79,6 +79,7 @@ def load_library(build_if_missing: bool = False):
         lib.odh_hbm_write.argtypes = [vp, sz, u32, i, vp]
         lib.odh_hbm_check.argtypes = [vp, sz, u32, vp, vp]
         lib.odh_busy.argtypes = [vp, i, i, vp]
+        lib.odh_peer_enable.argtypes = [i, i]
         # A/B entry points (microbenchmarks, kernel numerics tests)
         lib.odh_gemm_bf16_256_variant.argtypes = [vp, vp, vp, i, i, i, i, vp]
         lib.odh_probe_gemm_verify_2buf.argtypes = [vp, vp, i, i, i, vp, vp, vp, vp, vp]
@@ -88,7 +89,7 @@ def load_library(build_if_missing: bool = False):
         for f in ("odh_probe_fill", "odh_gemm_bf16", "odh_gemm_bf16_128", "odh_probe_verify", "odh_probe_gemm_verify",
                   "odh_hbm_write", "odh_hbm_check", "odh_busy", "odh_gemm_bf16_256_variant",
                   "odh_probe_gemm_verify_2buf", "odh_probe_gemm_verify_deep", "odh_hbm_write_variant",
-                  "odh_hbm_check_variant"):
+                  "odh_hbm_check_variant", "odh_peer_enable"):
             getattr(lib, f).restype = i
         _lib = lib
         return lib
@@ -282,6 +283,62 @@ def get_probe(device: int, **kw) -> GpuProbe:
         return p
 
 
+XGMI_CHECK_BYTES = 64 << 20
+
+
+def ring_pairs(devices: Sequence[int]) -> List[tuple]:
+    """(reader, source) per xGMI link the multi-GPU probe checks: a ring over the pod's
+    GPUs, so with k GPUs k links are read (MI355X: every GPU pair has a direct link)."""
+    ds = list(dict.fromkeys(devices))
+    if len(ds) < 2:
+        return []
+    if len(ds) == 2:
+        return [(ds[1], ds[0]), (ds[0], ds[1])]
+    return [(ds[(n + 1) % len(ds)], ds[n]) for n in range(len(ds))]
+
+
+def xgmi_ring_check(devices: Sequence[int], nbytes: int = XGMI_CHECK_BYTES) -> List[dict]:
+    """Peer-read check of a multi-GPU pod's xGMI links.
+
+    Each GPU's probe has just written its seeded pattern into its HBM buffer; GPU
+    ``reader`` now streams the first ``nbytes`` of GPU ``source``'s buffer over xGMI and
+    verifies every word (``odh_hbm_check`` with a peer pointer).  One link failing fails
+    the pod, like an XCD failing the GEMM check.  The reference has no equivalent: a
+    multi-GPU notebook there starts on GPUs whose interconnect nobody has looked at.
+    """
+    import torch
+
+    lib = load_library()
+    out = []
+    for reader, source in ring_pairs(devices):
+        r = {"reader": reader, "source": source, "ok": False}
+        try:
+            pr, ps = get_probe(reader), get_probe(source)
+            n = min(nbytes, ps.hbm_bytes) & ~15
+            first, second = sorted((pr, ps), key=lambda p: p.device.index)
+            with first._lock, second._lock:
+                _check(lib.odh_peer_enable(reader, source))
+                dev = pr.device
+                with torch.cuda.device(dev):
+                    err = torch.zeros((2,), dtype=torch.int32, device=dev)
+                    s = pr.streams[0]
+                    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                    s.wait_stream(torch.cuda.current_stream(dev))
+                    torch.cuda.current_stream(ps.device).synchronize()  # source pattern is in HBM
+                    ev0.record(s)
+                    _check(lib.odh_hbm_check(ps.hbm.data_ptr(), n, ps.seed, err.data_ptr(), s.cuda_stream))
+                    ev1.record(s)
+                    ev1.synchronize()
+                    e = err.cpu().tolist()
+                ms = ev0.elapsed_time(ev1)
+            errors = (e[0] & 0xFFFFFFFF) | ((e[1] & 0xFFFFFFFF) << 32)
+            r.update(ok=errors == 0, errors=errors, bytes=n, ms=ms, gbps=n / (ms * 1e-3) / 1e9 if ms > 0 else 0.0)
+        except Exception as ex:  # a link that cannot be checked fails the pod, not the agent
+            r["error"] = repr(ex)
+        out.append(r)
+    return out
+
+
 def probe_devices(devices: Sequence[int]) -> dict:
     results = []
     for d in devices:
@@ -289,9 +346,15 @@ def probe_devices(devices: Sequence[int]) -> dict:
             results.append(get_probe(d).run())
         except Exception as e:  # a failed probe fails the pod, it must not crash the agent
             results.append({"ok": False, "device": d, "error": repr(e)})
-    return {"ok": all(r.get("ok") for r in results), "devices": list(devices), "results": results,
-            "error": next((r.get("error") or f"probe failed on GPU {r['device']}" for r in results
-                           if not r.get("ok")), None)}
+    links = xgmi_ring_check(devices) if all(r.get("ok") for r in results) else []
+    error = next((r.get("error") or f"probe failed on GPU {r['device']}" for r in results if not r.get("ok")), None)
+    if error is None:
+        error = next((lk.get("error") or f"xGMI check failed reading GPU {lk['source']} from GPU {lk['reader']}"
+                      for lk in links if not lk.get("ok")), None)
+    out = {"ok": error is None, "devices": list(devices), "results": results, "error": error}
+    if links:
+        out["links"] = links
+    return out
 
 
 async def startup_probe(devices: Sequence[int], local_index=None) -> dict:

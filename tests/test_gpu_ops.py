@@ -194,3 +194,27 @@ def test_deep_fused_probe_verify_counts_errors(dev, xb):
     assert run_deep() == (expect_bad, expect_bad, 16)
     p.a[5, 7] = (p.a[5, 7].float() - 1).to(torch.bfloat16)
     assert run_deep()[0] == 0
+
+
+def test_single_gpu_pod_has_no_xgmi_links(dev):
+    from odh_kubeflow_amd.ops import gpu
+
+    assert gpu.xgmi_ring_check([0]) == []
+    r = gpu.probe_devices([0])
+    assert r["ok"] and "links" not in r
+    assert gpu.load_library().odh_peer_enable(0, 0) == 0  # self: nothing to enable
+
+
+def test_multi_gpu_pod_xgmi_ring(dev):
+    """Multi-GPU pod: every link of the ring over its GPUs is read and verified over xGMI."""
+    n = torch.cuda.device_count()
+    if n < 2:
+        pytest.skip("needs 2+ MI355X (xGMI peers)")
+    from odh_kubeflow_amd.ops import gpu
+
+    devs = list(range(min(n, 4)))
+    r = gpu.probe_devices(devs)
+    assert r["ok"], r
+    assert len(r["links"]) == (2 if len(devs) == 2 else len(devs))
+    for lk in r["links"]:
+        assert lk["errors"] == 0 and lk["gbps"] > 10, lk

@@ -580,6 +580,43 @@ struct Store {
   std::atomic<uint64_t> requests{0}, writes{0}, webhook_calls{0};
 } S;
 
+// Where the server's CPU goes (GET /metrics "prof"): thread CPU time per request class,
+// store-lock contention on the request path, watch wake-ups and the history entries the
+// woken watchers scanned, wall time spent waiting on admission webhooks.
+enum Cat { C_GET, C_LIST, C_CREATE, C_UPDATE, C_PATCH, C_DELETE, C_WATCH, C_OTHER, C_N };
+const char* const CAT_NAMES[C_N] = {"get", "list", "create", "update", "patch", "delete", "watch", "other"};
+struct Prof {
+  std::atomic<uint64_t> cpu_ns[C_N]{}, calls[C_N]{};
+  std::atomic<uint64_t> lock_wait_ns{0}, lock_contended{0}, wakeups{0}, scanned{0}, admit_wall_ns{0};
+} P;
+thread_local int t_cat = C_OTHER;
+
+uint64_t thread_cpu_ns() {
+  timespec ts;
+  clock_gettime(CLOCK_THREAD_CPUTIME_ID, &ts);
+  return (uint64_t)ts.tv_sec * 1000000000ull + (uint64_t)ts.tv_nsec;
+}
+
+uint64_t mono_ns() {
+  return (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
+             std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+// the store lock on the request path, timing only the contended acquisitions
+struct StoreLock {
+  StoreLock() {
+    if (!S.mu.try_lock()) {
+      uint64_t t0 = mono_ns();
+      S.mu.lock();
+      P.lock_wait_ns += mono_ns() - t0;
+      P.lock_contended++;
+    }
+  }
+  ~StoreLock() { S.mu.unlock(); }
+  StoreLock(const StoreLock&) = delete;
+  StoreLock& operator=(const StoreLock&) = delete;
+};
+
 Bucket& bucket(const Res& r) { return S.data[r.key]; }
 
 void index_owner(const Res& r, const Value& o, bool remove) {
@@ -784,7 +821,7 @@ std::vector<Webhook> webhooks_for(const Res& r, const std::string& op) {
   if (!mwc) return out;
   std::vector<Obj> cfgs;
   {
-    std::lock_guard<std::mutex> g(S.mu);
+    StoreLock g;
     for (auto& kv : bucket(*mwc).objs) cfgs.push_back(kv.second);
   }
   for (auto& c : cfgs) {
@@ -844,7 +881,7 @@ bool resolve_service(const Webhook& w, std::string* host, int* port) {
   if (!ep) return false;
   Obj o;
   {
-    std::lock_guard<std::mutex> g(S.mu);
+    StoreLock g;
     auto it = bucket(*ep).objs.find({w.svc_ns, w.svc_name});
     if (it == bucket(*ep).objs.end()) return false;
     o = it->second;
@@ -1064,7 +1101,7 @@ bool selectors_match(const Webhook& w, const Res& r, const Value& obj, const Val
   Res* nsr = by_kind("", "Namespace");
   Obj ns;
   if (nsr) {
-    std::lock_guard<std::mutex> g(S.mu);
+    StoreLock g;
     auto it = bucket(*nsr).objs.find({"", mget(obj, "namespace")});
     if (it != bucket(*nsr).objs.end()) ns = it->second;
   }
@@ -1105,6 +1142,11 @@ Value admit(const char* op, const Res& r, Value obj, const Value* old) {
     review["request"] = std::move(req);
     S.webhook_calls++;
     Value out;
+    uint64_t t_admit = mono_ns();
+    struct AdmitTimer {
+      uint64_t t0;
+      ~AdmitTimer() { P.admit_wall_ns += mono_ns() - t0; }
+    } admit_timer{t_admit};
     try {
       out = call_webhook(w, review);
     } catch (const std::exception& e) {
@@ -1145,7 +1187,7 @@ std::pair<std::vector<Obj>, int64_t> do_list(const Res& r, const std::string& ns
   auto lr = parse_labels(lsel);
   auto fr = parse_fields(fsel);
   std::vector<Obj> out;
-  std::lock_guard<std::mutex> g(S.mu);
+  StoreLock g;
   Bucket& b = bucket(r);
   if (!ns.empty() && r.namespaced) {
     for (auto it = b.objs.lower_bound({ns, ""}); it != b.objs.end() && it->first.first == ns; ++it)
@@ -1160,7 +1202,7 @@ std::pair<std::vector<Obj>, int64_t> do_list(const Res& r, const std::string& ns
 }
 
 Obj do_get(const Res& r, const std::string& ns, const std::string& name) {
-  std::lock_guard<std::mutex> g(S.mu);
+  StoreLock g;
   Bucket& b = bucket(r);
   auto it = b.objs.find({r.namespaced ? ns : "", name});
   if (it == b.objs.end()) throw NotFound(r.err_res(), name);
@@ -1193,7 +1235,7 @@ Value do_create(const Res& r, const std::string& url_ns, Value obj, bool dry) {
   obj["apiVersion"] = Value::str(r.api_version(r.storage));
   obj = admit("CREATE", r, std::move(obj), nullptr);
   if (auto err = validate(r, obj)) throw Invalid(r.group.empty() ? r.singular : r.kind + "." + r.group, mget(obj, "name"), *err);
-  std::lock_guard<std::mutex> g(S.mu);
+  StoreLock g;
   Bucket& b = bucket(r);
   std::pair<std::string, std::string> k{ns, mget(obj, "name")};
   if (b.objs.count(k)) throw AlreadyExists(r.err_res(), k.second);
@@ -1237,7 +1279,7 @@ Value do_create(const Res& r, const std::string& url_ns, Value obj, bool dry) {
 
 // commit a new version over `cur` (caller holds no lock)
 Value commit_update(const Res& r, const Value& cur_snapshot, Value nw) {
-  std::lock_guard<std::mutex> g(S.mu);
+  StoreLock g;
   std::string ns = mget(cur_snapshot, "namespace"), name = mget(cur_snapshot, "name");
   Bucket& b = bucket(r);
   auto it = b.objs.find({ns, name});
@@ -1296,7 +1338,7 @@ Value commit_update(const Res& r, const Value& cur_snapshot, Value nw) {
 Value do_update(const Res& r, const std::string& ns, const std::string& name, Value nw, const std::string& sub) {
   Obj cur;
   {
-    std::lock_guard<std::mutex> g(S.mu);
+    StoreLock g;
     auto it = bucket(r).objs.find({r.namespaced ? ns : "", name});
     if (it == bucket(r).objs.end()) throw NotFound(r.err_res(), name);
     cur = it->second;
@@ -1323,7 +1365,7 @@ Value do_patch_once(const Res& r, const std::string& ns, const std::string& name
                     const std::string& ptype, const std::string& sub) {
   Obj cur;
   {
-    std::lock_guard<std::mutex> g(S.mu);
+    StoreLock g;
     auto it = bucket(r).objs.find({r.namespaced ? ns : "", name});
     if (it == bucket(r).objs.end()) throw NotFound(r.err_res(), name);
     cur = it->second;
@@ -1460,7 +1502,7 @@ void gc_dependents(const std::string& owner_uid) {
 
 Value do_delete(const Res& r, const std::string& ns_, const std::string& name, const Value& opts) {
   std::string ns = r.namespaced ? ns_ : "";
-  std::lock_guard<std::mutex> g(S.mu);
+  StoreLock g;
   auto it = bucket(r).objs.find({ns, name});
   if (it == bucket(r).objs.end()) throw NotFound(r.err_res(), name);
   Obj cur = it->second;
@@ -1817,7 +1859,7 @@ void serve_watch(int fd, Res& r, const Path& p, const Request& rq) {
     WatchSlot* s;
     ~Unregister() {
       if (!b) return;
-      std::lock_guard<std::mutex> g(S.mu);
+      StoreLock g;
       auto rg = b->watchers.equal_range(ns);
       for (auto it = rg.first; it != rg.second; ++it)
         if (it->second == s) {
@@ -1828,7 +1870,7 @@ void serve_watch(int fd, Res& r, const Path& p, const Request& rq) {
   } unregister{wb, ns, &slot};
   slot.wants = wants;
   {
-    std::lock_guard<std::mutex> g(S.mu);
+    StoreLock g;
     Bucket& b = bucket(r);
     wb = &b;
     b.watchers.emplace(ns, &slot);
@@ -1863,7 +1905,13 @@ void serve_watch(int fd, Res& r, const Path& p, const Request& rq) {
   }
   auto deadline = std::chrono::steady_clock::now() + std::chrono::milliseconds((int64_t)(timeout * 1000));
   auto last_write = std::chrono::steady_clock::now();
+  uint64_t cpu_mark = thread_cpu_ns();
   while (!g_stop) {
+    {  // watch CPU is booked as it accrues (a stream lives for minutes)
+      uint64_t now_cpu = thread_cpu_ns();
+      P.cpu_ns[C_WATCH] += now_cpu - cpu_mark;
+      cpu_mark = now_cpu;
+    }
     std::vector<std::string> lines;
     bool gone = false;
     {
@@ -1879,6 +1927,8 @@ void serve_watch(int fd, Res& r, const Path& p, const Request& rq) {
           gone = true;  // the watcher fell behind the bounded history
         } else {
           size_t start = b.hist.size() - (size_t)(b.seq - last_seq);
+          P.wakeups++;
+          P.scanned += b.hist.size() - start;
           // serialise outside the store lock (copy the shared event refs first)
           std::vector<Ev> evs;
           for (size_t n = start; n < b.hist.size(); ++n) {
@@ -1913,7 +1963,7 @@ void serve_watch(int fd, Res& r, const Path& p, const Request& rq) {
       bm["apiVersion"] = Value::str(r.api_version(p.version));
       Value m = Value::object();
       {
-        std::lock_guard<std::mutex> g(S.mu);
+        StoreLock g;
         m["resourceVersion"] = Value::str(std::to_string(S.rv));
       }
       bm["metadata"] = m;
@@ -1943,15 +1993,28 @@ bool handle(int fd, Request& rq) {
   if (rq.method == "GET" && rq.path == "/metrics") {
     int64_t rv;
     {
-      std::lock_guard<std::mutex> g(S.mu);
+      StoreLock g;
       rv = S.rv;
     }
     char buf[256];
     snprintf(buf, sizeof(buf),
-             "{\"requests\":%llu,\"writes\":%llu,\"webhook_calls\":%llu,\"resourceVersion\":%lld}",
+             "{\"requests\":%llu,\"writes\":%llu,\"webhook_calls\":%llu,\"resourceVersion\":%lld,\"prof\":{",
              (unsigned long long)S.requests.load(), (unsigned long long)S.writes.load(),
              (unsigned long long)S.webhook_calls.load(), (long long)rv);
-    return respond(fd, 200, buf, rq.keep_alive);
+    std::string out = buf;
+    for (int c = 0; c < C_N; ++c) {
+      snprintf(buf, sizeof(buf), "\"%s_cpu_ns\":%llu,\"%s_calls\":%llu,", CAT_NAMES[c],
+               (unsigned long long)P.cpu_ns[c].load(), CAT_NAMES[c], (unsigned long long)P.calls[c].load());
+      out += buf;
+    }
+    snprintf(buf, sizeof(buf),
+             "\"lock_wait_ns\":%llu,\"lock_contended\":%llu,\"watch_wakeups\":%llu,\"watch_scanned\":%llu,"
+             "\"admit_wall_ns\":%llu}}",
+             (unsigned long long)P.lock_wait_ns.load(), (unsigned long long)P.lock_contended.load(),
+             (unsigned long long)P.wakeups.load(), (unsigned long long)P.scanned.load(),
+             (unsigned long long)P.admit_wall_ns.load());
+    out += buf;
+    return respond(fd, 200, out, rq.keep_alive);
   }
   try {
     if (rq.method == "GET") {
@@ -1970,9 +2033,12 @@ bool handle(int fd, Request& rq) {
     if (rq.method == "GET" && p.name.empty()) {
       std::string w = qget("watch");
       if (w == "1" || w == "true" || w == "True") {
+        t_cat = C_WATCH;
+        P.calls[C_WATCH]++;
         serve_watch(fd, r, p, rq);
         return false;  // watch streams end the connection
       }
+      t_cat = C_LIST;
       auto lst = do_list(r, p.ns, qget("labelSelector"), qget("fieldSelector"));
       std::string body = "{\"kind\":\"" + r.list_kind + "\",\"apiVersion\":\"" + r.api_version(p.version) +
                          "\",\"metadata\":{\"resourceVersion\":\"" + std::to_string(lst.second) + "\"},\"items\":[";
@@ -1985,6 +2051,7 @@ bool handle(int fd, Request& rq) {
       return respond(fd, 200, body, rq.keep_alive);
     }
     if (rq.method == "GET") {
+      t_cat = C_GET;
       Obj o = do_get(r, p.ns, p.name);
       return respond(fd, 200, p.version == r.storage ? kj::dump(*o) : kj::dump(out_obj(r, *o, p.version)), rq.keep_alive);
     }
@@ -1997,12 +2064,14 @@ bool handle(int fd, Request& rq) {
       }
     }
     if (rq.method == "POST" && p.name.empty()) {
+      t_cat = C_CREATE;
       if (!body.is_obj()) throw BadRequest("object body required");
       if (!body.get("kind")) body["kind"] = Value::str(r.kind);
       Value out = do_create(r, p.ns, std::move(body), qget("dryRun") == "All");
       return respond(fd, 201, kj::dump(out_obj(r, out, p.version)), rq.keep_alive);
     }
     if (rq.method == "PUT" && !p.name.empty()) {
+      t_cat = C_UPDATE;
       if (!body.is_obj()) throw BadRequest("object body required");
       Value& m = mdm(body);
       if (!m.str_or("name").empty() && m.str_or("name") != p.name)
@@ -2012,6 +2081,7 @@ bool handle(int fd, Request& rq) {
       return respond(fd, 200, kj::dump(out_obj(r, out, p.version)), rq.keep_alive);
     }
     if (rq.method == "PATCH" && !p.name.empty()) {
+      t_cat = C_PATCH;
       std::string pt;
       if (rq.ctype == "application/merge-patch+json" || rq.ctype == "application/apply-patch+yaml") pt = "merge";
       else if (rq.ctype == "application/json-patch+json") pt = "json";
@@ -2023,6 +2093,7 @@ bool handle(int fd, Request& rq) {
       return respond(fd, 200, kj::dump(out_obj(r, out, p.version)), rq.keep_alive);
     }
     if (rq.method == "DELETE" && !p.name.empty()) {
+      t_cat = C_DELETE;
       Value opts = body.is_obj() ? body : Value::object();
       if (!opts.get("propagationPolicy") && !qget("propagationPolicy").empty())
         opts["propagationPolicy"] = Value::str(qget("propagationPolicy"));
@@ -2047,7 +2118,14 @@ void serve_conn(int fd) {
   while (!g_stop) {
     Request rq;
     if (!read_request(c, rq)) break;
-    if (!handle(fd, rq)) break;
+    t_cat = C_OTHER;
+    uint64_t c0 = thread_cpu_ns();
+    bool more = handle(fd, rq);
+    if (t_cat != C_WATCH) {  // a watch books its own CPU as it goes
+      P.cpu_ns[t_cat] += thread_cpu_ns() - c0;
+      P.calls[t_cat]++;
+    }
+    if (!more) break;
     if (!rq.keep_alive) break;
   }
   close(fd);

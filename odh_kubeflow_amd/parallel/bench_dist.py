@@ -105,6 +105,8 @@ def measure(args) -> Optional[dict]:
         out["config"]["architecture"] = "sharded"
         out["rank_ms_per_step"] = res.get("rank_ms_per_step")
         out["cpu_ms_per_step"] = res.get("cpu_ms_per_step")
+        if res.get("apiserver_profile_per_step"):
+            out["apiserver_profile_per_step"] = res["apiserver_profile_per_step"]
         if rccl_ms is not None:
             out["rccl_allreduce_check_ms"] = round(rccl_ms, 3)
     dist.barrier()
@@ -154,7 +156,7 @@ async def _main(args, dist, torch, rank: int, world: int, local_rank: int, probe
 
     try:
         children = {"apiserver": native.proc.pid if native else None, "scheduler": sched.pid if sched else None}
-        result = await _drive(args, shard, dist, torch, children)
+        result = await _drive(args, shard, dist, torch, children, native)
     finally:
         await _in_thread(dist.barrier)  # nobody tears down while others still serve
         await shard.stop()
@@ -189,7 +191,27 @@ async def _stop_child(proc) -> None:
         proc.kill()
 
 
-async def _drive(args, shard, dist, torch, children: Optional[dict] = None) -> dict:
+async def _apiserver_prof(native) -> Optional[dict]:
+    if native is None:
+        return None
+    try:
+        return (await native.stats()).get("prof")
+    except Exception:
+        return None
+
+
+def _prof_per_step(p0: Optional[dict], p1: Optional[dict], steps: int) -> Optional[dict]:
+    """Native apiserver profile delta over the timed region, per step (ms / counts)."""
+    if not p0 or not p1:
+        return None
+    out = {}
+    for k, v in p1.items():
+        d = (v - p0.get(k, 0)) / max(1, steps)
+        out[k[:-3] + "_ms" if k.endswith("_ns") else k] = round(d / 1e6, 3) if k.endswith("_ns") else round(d, 2)
+    return out
+
+
+async def _drive(args, shard, dist, torch, children: Optional[dict] = None, native=None) -> dict:
     from ..models import kinds
     from ..models.notebook import notebook
 
@@ -227,6 +249,7 @@ async def _drive(args, shard, dist, torch, children: Optional[dict] = None) -> d
     r0 = shard.reconcile_count()
     children = children or {}
     child_cpu0 = {k: _proc_cpu_s(pid) for k, pid in children.items()}
+    prof0 = await _apiserver_prof(native)
     cpu0 = time.process_time()
     t_start = time.perf_counter()
     for _ in range(args.steps):
@@ -236,6 +259,7 @@ async def _drive(args, shard, dist, torch, children: Optional[dict] = None) -> d
     state["recon"] = shard.reconcile_count() - r0
     # CPU time per step of every process on the path: where a step's work goes when ranks are added
     cpu = {"rank": time.process_time() - cpu0}
+    prof = _prof_per_step(prof0, await _apiserver_prof(native), args.steps)
     for k, pid in children.items():
         c1 = _proc_cpu_s(pid)
         if c1 is not None and child_cpu0.get(k) is not None:
@@ -262,4 +286,5 @@ async def _drive(args, shard, dist, torch, children: Optional[dict] = None) -> d
             "lat_ms": [x for g in gathered for x in g["lat"]], "odh": use_odh,
             "probes": [p for g in gathered for p in g["probes"]],
             "teardown_ms": [x for g in gathered for x in g["teardown"]],
-            "rank_ms_per_step": [round(g["own_s"] * per_step, 3) for g in gathered], "cpu_ms_per_step": cpu_ms}
+            "rank_ms_per_step": [round(g["own_s"] * per_step, 3) for g in gathered], "cpu_ms_per_step": cpu_ms,
+            "apiserver_profile_per_step": prof}

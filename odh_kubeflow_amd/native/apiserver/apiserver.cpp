@@ -671,36 +671,45 @@ Value out_obj(const Res& r, const Value& o, const std::string& version) {
   return c;
 }
 
+// a and b agree on every member not named in skip (object members in any order); no copies
+bool members_equal_except(const Value& a, const Value& b, std::initializer_list<const char*> skip) {
+  auto skipped = [&](const std::string& k) {
+    for (const char* x : skip)
+      if (k == x) return true;
+    return false;
+  };
+  size_t na = 0, nb = 0;
+  for (auto& m : a.obj) {
+    if (skipped(m.k)) continue;
+    ++na;
+    const Value* o = b.get(m.k);
+    if (!o || !(m.v == *o)) return false;
+  }
+  for (auto& m : b.obj)
+    if (!skipped(m.k)) ++nb;
+  return na == nb;
+}
+
 bool spec_equal(const Value& a, const Value& b) {
   // everything but metadata / status / apiVersion / kind
-  auto part = [](const Value& v) {
-    Value o = Value::object();
-    for (auto& m : v.obj)
-      if (m.k != "metadata" && m.k != "status" && m.k != "apiVersion" && m.k != "kind") o.obj.push_back(m);
-    return o;
-  };
-  return part(a) == part(b);
+  return members_equal_except(a, b, {"metadata", "status", "apiVersion", "kind"});
 }
 
 bool equal_except_meta(const Value& a, const Value& b) {
-  if (a.obj.size() != b.obj.size()) return false;
-  for (auto& m : a.obj) {
-    const Value* o = b.get(m.k);
-    if (!o) return false;
-    if (m.k == "metadata" && m.v.is_obj() && o->is_obj()) {
-      auto strip = [](const Value& v) {
-        Value c = v;
-        c.erase("resourceVersion");
-        c.erase("managedFields");
-        c.erase("generation");
-        return c;
-      };
-      if (!(strip(m.v) == strip(*o))) return false;
-    } else if (!(m.v == *o)) {
-      return false;
-    }
-  }
-  return true;
+  if (!members_equal_except(a, b, {"metadata"})) return false;
+  const Value* ma = a.get("metadata");
+  const Value* mb = b.get("metadata");
+  if (!ma || !mb) return ma == mb;
+  if (!ma->is_obj() || !mb->is_obj()) return *ma == *mb;
+  return members_equal_except(*ma, *mb, {"resourceVersion", "managedFields", "generation"});
+}
+
+Value out_obj(const Res& r, const Value& o, const std::string& version);
+
+// the response body of a write: no copy when the request used the storage version
+std::string dump_out(const Res& r, const Value& o, const std::string& version) {
+  if (version.empty() || version == r.storage) return kj::dump(o);
+  return kj::dump(out_obj(r, o, version));
 }
 
 std::optional<std::string> validate(const Res& r, const Value& o) {
@@ -1213,7 +1222,7 @@ void remove_locked(const Res& r, Obj live, Value final);
 void gc_dependents(const std::string& owner_uid);
 void sync_delete_locked(const Res& r, const std::string& ns, const std::string& name);
 
-Value do_create(const Res& r, const std::string& url_ns, Value obj, bool dry) {
+Obj do_create(const Res& r, const std::string& url_ns, Value obj, bool dry) {
   Value& m = mdm(obj);
   std::string ns;
   if (r.namespaced) {
@@ -1235,18 +1244,20 @@ Value do_create(const Res& r, const std::string& url_ns, Value obj, bool dry) {
   obj["apiVersion"] = Value::str(r.api_version(r.storage));
   obj = admit("CREATE", r, std::move(obj), nullptr);
   if (auto err = validate(r, obj)) throw Invalid(r.group.empty() ? r.singular : r.kind + "." + r.group, mget(obj, "name"), *err);
+  {
+    Value& mm = mdm(obj);
+    mm["uid"] = Value::str(uuid4());
+    mm["creationTimestamp"] = Value::str(rfc3339_now());
+    mm.erase("deletionTimestamp");
+    if (obj.get("spec") || r.status) mm["generation"] = Value::integer(1);
+    if (r.status && !r.group.empty()) obj.erase("status");
+  }
+  std::pair<std::string, std::string> k{ns, mget(obj, "name")};
   StoreLock g;
   Bucket& b = bucket(r);
-  std::pair<std::string, std::string> k{ns, mget(obj, "name")};
   if (b.objs.count(k)) throw AlreadyExists(r.err_res(), k.second);
-  Value& mm = mdm(obj);
-  mm["uid"] = Value::str(uuid4());
-  mm["creationTimestamp"] = Value::str(rfc3339_now());
-  mm.erase("deletionTimestamp");
-  if (obj.get("spec") || r.status) mm["generation"] = Value::integer(1);
-  if (r.status && !r.group.empty()) obj.erase("status");
   defaults(r, obj);
-  if (dry) return obj;
+  if (dry) return std::make_shared<const Value>(std::move(obj));
   mdm(obj)["resourceVersion"] = Value::str(std::to_string(++S.rv));
   auto sp = std::make_shared<const Value>(std::move(obj));
   b.objs[k] = sp;
@@ -1268,27 +1279,20 @@ Value do_create(const Res& r, const std::string& url_ns, Value obj, bool dry) {
         if (!owner || S.uids.count(ref.str_or("uid"))) live = true;
       }
       if (!live) {
-        Value out = *sp;
         sync_delete_locked(r, ns, k.second);
-        return out;
+        return sp;
       }
     }
   }
-  return *sp;
+  return sp;
 }
 
-// commit a new version over `cur` (caller holds no lock)
-Value commit_update(const Res& r, const Value& cur_snapshot, Value nw) {
-  StoreLock g;
-  std::string ns = mget(cur_snapshot, "namespace"), name = mget(cur_snapshot, "name");
-  Bucket& b = bucket(r);
-  auto it = b.objs.find({ns, name});
-  if (it == b.objs.end()) throw NotFound(r.err_res(), name);
-  Obj live = it->second;
+// nw's server-owned metadata from `base` (the version it replaces); generation bumped
+// when the spec changes; no new finalizers once deletion has started
+void prepare_update(const Res& r, const Value& base, Value& nw) {
   Value& m = mdm(nw);
-  std::string rv = m.str_or("resourceVersion");
-  if (!rv.empty() && rv != mget(*live, "resourceVersion")) throw Conflict(r.err_res(), name);
-  const Value& lm = *md(*live);
+  const Value& lm = *md(base);
+  std::string ns = mget(base, "namespace"), name = mget(base, "name");
   for (const char* k : {"uid", "creationTimestamp", "deletionTimestamp", "deletionGracePeriodSeconds"}) {
     const Value* v = lm.get(k);
     if (v) m[k] = *v;
@@ -1312,16 +1316,37 @@ Value commit_update(const Res& r, const Value& cur_snapshot, Value nw) {
   }
   if (const Value* gen = lm.get("generation")) {
     int64_t gv = gen->i;
-    if (!spec_equal(nw, *live)) gv++;
+    if (!spec_equal(nw, base)) gv++;
     m["generation"] = Value::integer(gv);
   }
-  m["resourceVersion"] = Value::str(mget(*live, "resourceVersion"));
-  if (equal_except_meta(nw, *live)) return *live;  // no-op write
-  const Value* fin = m.get("finalizers");
+  m["resourceVersion"] = Value::str(mget(base, "resourceVersion"));
+}
+
+// Commit a new version over `cur` (caller holds no lock).  The update is prepared and
+// compared against the snapshot `cur` OUTSIDE the store lock; when the stored object is
+// still that snapshot at commit time (the common case) the lock covers only the commit
+// itself — resourceVersion, the map slot, the owner index and the watch event.
+Obj commit_update(const Res& r, const Obj& cur, Value nw) {
+  const std::string want_rv = mdm(nw).str_or("resourceVersion");
+  const std::string ns = mget(*cur, "namespace"), name = mget(*cur, "name");
+  prepare_update(r, *cur, nw);
+  bool noop = equal_except_meta(nw, *cur);
+  StoreLock g;
+  Bucket& b = bucket(r);
+  auto it = b.objs.find({ns, name});
+  if (it == b.objs.end()) throw NotFound(r.err_res(), name);
+  Obj live = it->second;
+  if (!want_rv.empty() && want_rv != mget(*live, "resourceVersion")) throw Conflict(r.err_res(), name);
+  if (live != cur) {  // written since the snapshot: prepare against the live version
+    prepare_update(r, *live, nw);
+    noop = equal_except_meta(nw, *live);
+  }
+  if (noop) return live;  // no-op write
+  const Value* fin = md(nw)->get("finalizers");
   bool no_fin = !fin || !fin->is_arr() || fin->arr.empty();
-  if (lm.get("deletionTimestamp") && no_fin) {
+  if (md(*live)->get("deletionTimestamp") && no_fin) {
     mdm(nw)["resourceVersion"] = Value::str(std::to_string(++S.rv));
-    Value out = nw;
+    auto out = std::make_shared<const Value>(nw);
     remove_locked(r, live, std::move(nw));
     return out;
   }
@@ -1332,10 +1357,10 @@ Value commit_update(const Res& r, const Value& cur_snapshot, Value nw) {
   index_owner(r, *sp, false);
   S.writes++;
   emit(r, "MODIFIED", sp, live);
-  return *sp;
+  return sp;
 }
 
-Value do_update(const Res& r, const std::string& ns, const std::string& name, Value nw, const std::string& sub) {
+Obj do_update(const Res& r, const std::string& ns, const std::string& name, Value nw, const std::string& sub) {
   Obj cur;
   {
     StoreLock g;
@@ -1358,10 +1383,10 @@ Value do_update(const Res& r, const std::string& ns, const std::string& name, Va
     nw = admit("UPDATE", r, std::move(nw), cur.get());
     if (auto err = validate(r, nw)) throw Invalid(r.kind + "." + r.group, name, *err);
   }
-  return commit_update(r, *cur, std::move(nw));
+  return commit_update(r, cur, std::move(nw));
 }
 
-Value do_patch_once(const Res& r, const std::string& ns, const std::string& name, const Value& patch,
+Obj do_patch_once(const Res& r, const std::string& ns, const std::string& name, const Value& patch,
                     const std::string& ptype, const std::string& sub) {
   Obj cur;
   {
@@ -1396,13 +1421,13 @@ Value do_patch_once(const Res& r, const std::string& ns, const std::string& name
     nw = admit("UPDATE", r, std::move(nw), cur.get());
     if (auto err = validate(r, nw)) throw Invalid(r.kind + "." + r.group, name, *err);
   }
-  return commit_update(r, *cur, std::move(nw));
+  return commit_update(r, cur, std::move(nw));
 }
 
 // A patch without a resourceVersion precondition applies to whatever is current: like
 // the apiserver's GuaranteedUpdate loop, a conflict with a concurrent writer (e.g. during
 // a slow admission webhook call) re-reads and re-applies instead of failing.
-Value do_patch(const Res& r, const std::string& ns, const std::string& name, const Value& patch,
+Obj do_patch(const Res& r, const std::string& ns, const std::string& name, const Value& patch,
                const std::string& ptype, const std::string& sub) {
   const Value* pm = patch.is_obj() ? patch.get("metadata") : nullptr;
   bool precond = pm && pm->is_obj() && !pm->str_or("resourceVersion").empty();
@@ -2053,7 +2078,7 @@ bool handle(int fd, Request& rq) {
     if (rq.method == "GET") {
       t_cat = C_GET;
       Obj o = do_get(r, p.ns, p.name);
-      return respond(fd, 200, p.version == r.storage ? kj::dump(*o) : kj::dump(out_obj(r, *o, p.version)), rq.keep_alive);
+      return respond(fd, 200, dump_out(r, *o, p.version), rq.keep_alive);
     }
     Value body;
     if (!rq.body.empty()) {
@@ -2067,8 +2092,8 @@ bool handle(int fd, Request& rq) {
       t_cat = C_CREATE;
       if (!body.is_obj()) throw BadRequest("object body required");
       if (!body.get("kind")) body["kind"] = Value::str(r.kind);
-      Value out = do_create(r, p.ns, std::move(body), qget("dryRun") == "All");
-      return respond(fd, 201, kj::dump(out_obj(r, out, p.version)), rq.keep_alive);
+      Obj out = do_create(r, p.ns, std::move(body), qget("dryRun") == "All");
+      return respond(fd, 201, dump_out(r, *out, p.version), rq.keep_alive);
     }
     if (rq.method == "PUT" && !p.name.empty()) {
       t_cat = C_UPDATE;
@@ -2077,8 +2102,8 @@ bool handle(int fd, Request& rq) {
       if (!m.str_or("name").empty() && m.str_or("name") != p.name)
         throw BadRequest("the name of the object does not match the name on the URL");
       m["name"] = Value::str(p.name);
-      Value out = do_update(r, p.ns, p.name, std::move(body), p.sub);
-      return respond(fd, 200, kj::dump(out_obj(r, out, p.version)), rq.keep_alive);
+      Obj out = do_update(r, p.ns, p.name, std::move(body), p.sub);
+      return respond(fd, 200, dump_out(r, *out, p.version), rq.keep_alive);
     }
     if (rq.method == "PATCH" && !p.name.empty()) {
       t_cat = C_PATCH;
@@ -2089,8 +2114,8 @@ bool handle(int fd, Request& rq) {
       else
         return respond(fd, 415, kj::dump(status_obj({415, "UnsupportedMediaType", "unsupported patch type " + rq.ctype, Value()})),
                        rq.keep_alive);
-      Value out = do_patch(r, p.ns, p.name, body, pt, p.sub);
-      return respond(fd, 200, kj::dump(out_obj(r, out, p.version)), rq.keep_alive);
+      Obj out = do_patch(r, p.ns, p.name, body, pt, p.sub);
+      return respond(fd, 200, dump_out(r, *out, p.version), rq.keep_alive);
     }
     if (rq.method == "DELETE" && !p.name.empty()) {
       t_cat = C_DELETE;

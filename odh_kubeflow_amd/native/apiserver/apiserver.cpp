@@ -21,9 +21,11 @@
 //   * discovery documents; bearer-token authentication.
 //
 // Concurrency: one thread per client connection (keep-alive), one global store mutex
-// held only for map operations (microseconds), watch threads woken by a condition
-// variable; every stored object is an immutable shared snapshot, so readers and
-// watchers never copy under the lock and each watch event is serialised once.
+// held only for commits (updates are prepared and compared outside it), a per-resource
+// history lock the watch threads wait, wake and scan under (a watcher is woken only for
+// events its namespace / selector admits); every stored object is an immutable shared
+// snapshot, so readers and watchers never copy under a lock and each watch event is
+// serialised once.
 //
 // Usage: odh-apiserver --config scheme.json [--host 127.0.0.1] [--port 0] [--gc]
 //        [--token T] [--history 4096]; prints "LISTENING <port>" once ready.
@@ -567,6 +569,10 @@ struct Bucket {
   // AND namespace, so with one control-plane shard per GPU rank (each watching its own
   // namespaces) a write costs O(1) wake-ups instead of one per shard
   std::unordered_multimap<std::string, WatchSlot*> watchers;
+  // hist / seq / watchers have their own lock: watch streams wait, wake and scan under it
+  // without touching the store lock the request threads commit under (lock order: the
+  // store lock, then this one — emit() runs inside a commit)
+  std::mutex hmu;
 };
 
 struct Store {
@@ -642,6 +648,7 @@ void index_owner(const Res& r, const Value& o, bool remove) {
 // callers hold S.mu
 void emit(const Res& r, const char* type, Obj obj, Obj old) {
   Bucket& b = bucket(r);
+  std::lock_guard<std::mutex> hg(b.hmu);
   Ev e{++b.seq, std::stoll(mget(*obj, "resourceVersion")), type, std::move(obj), std::move(old),
        std::make_shared<EvCache>()};
   b.hist.push_back(std::move(e));
@@ -1884,7 +1891,7 @@ void serve_watch(int fd, Res& r, const Path& p, const Request& rq) {
     WatchSlot* s;
     ~Unregister() {
       if (!b) return;
-      StoreLock g;
+      std::lock_guard<std::mutex> hg(b->hmu);
       auto rg = b->watchers.equal_range(ns);
       for (auto it = rg.first; it != rg.second; ++it)
         if (it->second == s) {
@@ -1897,6 +1904,7 @@ void serve_watch(int fd, Res& r, const Path& p, const Request& rq) {
   {
     StoreLock g;
     Bucket& b = bucket(r);
+    std::lock_guard<std::mutex> hg(b.hmu);
     wb = &b;
     b.watchers.emplace(ns, &slot);
     last_seq = b.seq;
@@ -1940,8 +1948,8 @@ void serve_watch(int fd, Res& r, const Path& p, const Request& rq) {
     std::vector<std::string> lines;
     bool gone = false;
     {
-      std::unique_lock<std::mutex> lk(S.mu);
-      Bucket& b = bucket(r);
+      Bucket& b = *wb;  // element references of S.data stay valid; buckets are never erased
+      std::unique_lock<std::mutex> lk(b.hmu);
       // system_clock deadline: libstdc++ maps a steady_clock wait to pthread_cond_clockwait,
       // which ThreadSanitizer (GCC 11) does not intercept; the 500 ms timeout only paces
       // catch-up scans, so a wall-clock jump is harmless here

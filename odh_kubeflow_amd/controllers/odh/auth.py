@@ -15,6 +15,7 @@ owned → cleaned up explicitly) and the auth HTTPRoute.
 
 from __future__ import annotations
 
+import functools
 import logging
 from typing import Mapping
 
@@ -53,15 +54,24 @@ class SidecarResourceError(ValueError):
 
 def parse_and_validate_auth_sidecar_resources(nb: dict) -> dict:
     """Annotations → requests/limits with defaults 100m / 64Mi; rejects negatives and request > limit."""
-    cfg = {
-        ANNOTATION_AUTH_SIDECAR_CPU_REQUEST: parse_quantity(DEFAULT_AUTH_SIDECAR_CPU_REQUEST),
-        ANNOTATION_AUTH_SIDECAR_MEMORY_REQUEST: parse_quantity(DEFAULT_AUTH_SIDECAR_MEMORY_REQUEST),
-        ANNOTATION_AUTH_SIDECAR_CPU_LIMIT: parse_quantity(DEFAULT_AUTH_SIDECAR_CPU_LIMIT),
-        ANNOTATION_AUTH_SIDECAR_MEMORY_LIMIT: parse_quantity(DEFAULT_AUTH_SIDECAR_MEMORY_LIMIT),
-    }
     ann = m.annotations(nb)
-    for key in list(cfg):
-        raw = ann.get(key)
+    cpu_req, mem_req, cpu_lim, mem_lim = _sidecar_resources(*(ann.get(k) or None for k in _SIDECAR_KEYS))
+    return {"requests": {"cpu": cpu_req, "memory": mem_req}, "limits": {"cpu": cpu_lim, "memory": mem_lim}}
+
+
+_SIDECAR_KEYS = (ANNOTATION_AUTH_SIDECAR_CPU_REQUEST, ANNOTATION_AUTH_SIDECAR_MEMORY_REQUEST,
+                 ANNOTATION_AUTH_SIDECAR_CPU_LIMIT, ANNOTATION_AUTH_SIDECAR_MEMORY_LIMIT)
+_SIDECAR_DEFAULTS = (DEFAULT_AUTH_SIDECAR_CPU_REQUEST, DEFAULT_AUTH_SIDECAR_MEMORY_REQUEST,
+                     DEFAULT_AUTH_SIDECAR_CPU_LIMIT, DEFAULT_AUTH_SIDECAR_MEMORY_LIMIT)
+
+
+@functools.lru_cache(maxsize=256)
+def _sidecar_resources(*raws) -> tuple:
+    """Canonical (cpu request, memory request, cpu limit, memory limit) for the four raw
+    annotation values (None = default).  Memoised: the webhook evaluates this on every
+    CREATE/UPDATE admission and nearly every notebook carries the same (usually no) values."""
+    qs = []
+    for key, raw, default in zip(_SIDECAR_KEYS, raws, _SIDECAR_DEFAULTS):
         if raw:
             try:
                 q = parse_quantity(raw.strip())
@@ -69,17 +79,17 @@ def parse_and_validate_auth_sidecar_resources(nb: dict) -> dict:
                 raise SidecarResourceError(f"invalid value for annotation '{key}': '{raw}': {e}")
             if q.sign() < 0:
                 raise SidecarResourceError(f"annotation '{key}' value '{raw}' cannot be negative")
-            cfg[key] = q
-    cpu_req, cpu_lim = cfg[ANNOTATION_AUTH_SIDECAR_CPU_REQUEST], cfg[ANNOTATION_AUTH_SIDECAR_CPU_LIMIT]
-    mem_req, mem_lim = cfg[ANNOTATION_AUTH_SIDECAR_MEMORY_REQUEST], cfg[ANNOTATION_AUTH_SIDECAR_MEMORY_LIMIT]
+        else:
+            q = parse_quantity(default)
+        qs.append(q)
+    cpu_req, mem_req, cpu_lim, mem_lim = qs
     if cpu_req.cmp(cpu_lim) > 0:
         raise SidecarResourceError(f"CPU request ({canonical(cpu_req)}) cannot be greater than CPU limit "
                                    f"({canonical(cpu_lim)})")
     if mem_req.cmp(mem_lim) > 0:
         raise SidecarResourceError(f"memory request ({canonical(mem_req)}) cannot be greater than memory limit "
                                    f"({canonical(mem_lim)})")
-    return {"requests": {"cpu": canonical(cpu_req), "memory": canonical(mem_req)},
-            "limits": {"cpu": canonical(cpu_lim), "memory": canonical(mem_lim)}}
+    return canonical(cpu_req), canonical(mem_req), canonical(cpu_lim), canonical(mem_lim)
 
 
 def kube_rbac_proxy_container(image: str, resources: dict) -> dict:

@@ -10,7 +10,9 @@ import sys
 def main(path: str) -> None:
     c = sqlite3.connect(path)
     w = csv.writer(sys.stdout)
-    w.writerow(["Name", "Calls", "TotalDurationNs", "AverageNs", "Percentage"])
+    # the rocpd views report durations in microseconds (a 1 GiB HBM check reads ~250 here:
+    # 4.2 TB/s; 250 ns would be 4 PB/s)
+    w.writerow(["Name", "Calls", "TotalDurationUs", "AverageUs", "Percentage"])
     for name, calls, total, avg, pct in c.execute("select * from top_kernels"):
         w.writerow([name, calls, round(total, 1), round(avg, 1), round(pct, 2)])
 

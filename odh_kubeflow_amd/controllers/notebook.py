@@ -36,7 +36,7 @@ import json
 import logging
 import os
 import re
-from typing import Mapping, Optional
+from typing import List, Mapping, Optional, Tuple
 
 from ..models import kinds
 from ..models import meta as m
@@ -110,6 +110,32 @@ def _gpu_shm(nb: dict, pod_spec: dict, per_gpu: str) -> None:
     containers[0].setdefault("volumeMounts", []).append({"name": SHM_VOLUME, "mountPath": "/dev/shm"})
 
 
+def parse_env_pairs(raw: str) -> List[Tuple[str, str]]:
+    """``"K1=v1,K2=v2"`` → [(K1, v1), (K2, v2)] (blank and malformed entries skipped)."""
+    out = []
+    for item in (raw or "").split(","):
+        k, sep, v = item.strip().partition("=")
+        if sep and k.strip():
+            out.append((k.strip(), v.strip()))
+    return out
+
+
+def _multi_gpu_env(pod_spec: dict, raw: str) -> None:
+    """Collective-library environment defaults (``MULTI_GPU_ENV``) for notebooks that request
+    2+ ``amd.com/gpu``: their RCCL collectives run over the node's xGMI links, and the
+    settings that path needs on a given fleet (e.g. dmabuf-only IPC hosts) are set once by
+    the operator instead of in every notebook.  A variable the user already set wins."""
+    containers = pod_spec.get("containers") or []
+    if gpu_request(pod_spec) < 2 or not containers:
+        return
+    env = containers[0].setdefault("env", [])
+    have = {e.get("name") for e in env}
+    for k, v in parse_env_pairs(raw):
+        if k not in have:
+            env.append({"name": k, "value": v})
+            have.add(k)
+
+
 def generate_statefulset(nb: dict, is_generate_name: bool, env: Mapping[str, str] = os.environ) -> dict:
     """``generateStatefulSet`` (:433-523)."""
     name, ns = m.name(nb), m.namespace(nb)
@@ -149,6 +175,8 @@ def generate_statefulset(nb: dict, is_generate_name: bool, env: Mapping[str, str
         _gpu_placement(pod_spec)
     if env.get("GPU_SHM_SIZE_PER_GPU"):
         _gpu_shm(nb, pod_spec, env["GPU_SHM_SIZE_PER_GPU"])
+    if env.get("MULTI_GPU_ENV"):
+        _multi_gpu_env(pod_spec, env["MULTI_GPU_ENV"])
     return sts
 
 

@@ -356,7 +356,7 @@ def tree() -> Dict[str, object]:
         generatorOptions={"disableNameSuffixHash": True})
     t["manager/params.env"] = "USE_ISTIO=false\nISTIO_GATEWAY=kubeflow/kubeflow-gateway\nISTIO_HOST=*\n" \
                               "CLUSTER_DOMAIN=cluster.local\nADD_FSGROUP=true\nGPU_NODE_SELECTOR=false\n" \
-                              "GPU_SHM_SIZE_PER_GPU=\n"
+                              "GPU_SHM_SIZE_PER_GPU=\nMULTI_GPU_ENV=\n"
     t["node-agent/daemonset.yaml"] = node_agent_daemonset()
     t["node-agent/kustomization.yaml"] = kustomization(["daemonset.yaml"])
     t["webhook/service.yaml"] = webhook_service()
@@ -383,7 +383,10 @@ def tree() -> Dict[str, object]:
         ["../../default"],
         patches=[{"target": {"kind": "ConfigMap", "name": ".*config"}, "patch":
                   "- op: replace\n  path: /data/GPU_NODE_SELECTOR\n  value: \"true\"\n"
-                  "- op: replace\n  path: /data/GPU_SHM_SIZE_PER_GPU\n  value: 16Gi\n"},
+                  "- op: replace\n  path: /data/GPU_SHM_SIZE_PER_GPU\n  value: 16Gi\n"
+                  # multi-GPU notebooks: RCCL's intra-node IPC over dmabuf (hosts whose amdgpu
+                  # driver only offers dmabuf IPC fail hipIpcGetMemHandle otherwise)
+                  "- op: replace\n  path: /data/MULTI_GPU_ENV\n  value: HSA_ENABLE_IPC_MODE_LEGACY=0\n"},
                  {"target": {"kind": "ConfigMap", "name": ".*culler-config"}, "patch":
                   "- op: replace\n  path: /data/CULLING_ACTIVITY_SOURCE\n  value: combined\n"
                   "- op: replace\n  path: /data/ENABLE_CULLING\n  value: \"true\"\n"}])

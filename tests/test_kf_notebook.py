@@ -247,3 +247,20 @@ def test_gpu_shm_sized_per_gpu_and_overridable():
     assert "volumes" not in generate_statefulset(own, False, env)["spec"]["template"]["spec"]
     # off unless configured (the reference copies the pod spec verbatim)
     assert "volumes" not in generate_statefulset(notebook("nb", "ns", gpus=1), False, {})["spec"]["template"]["spec"]
+
+
+def test_multi_gpu_env_defaults():
+    from odh_kubeflow_amd.controllers.notebook import generate_statefulset, parse_env_pairs
+
+    assert parse_env_pairs(" A=1, B = x=y ,bad,,=v") == [("A", "1"), ("B", "x=y")]
+    env = {"MULTI_GPU_ENV": "HSA_ENABLE_IPC_MODE_LEGACY=0,NB_PREFIX=/nope"}
+
+    def env_of(nb):
+        c = generate_statefulset(nb, False, env)["spec"]["template"]["spec"]["containers"][0]
+        return {e["name"]: e.get("value") for e in c.get("env") or []}
+
+    e = env_of(notebook("nb", "ns", gpus=2))
+    assert e["HSA_ENABLE_IPC_MODE_LEGACY"] == "0"
+    assert e["NB_PREFIX"] == "/notebook/ns/nb"  # a variable already set wins
+    assert "HSA_ENABLE_IPC_MODE_LEGACY" not in env_of(notebook("nb", "ns", gpus=1))  # one GPU: no collectives
+    assert "HSA_ENABLE_IPC_MODE_LEGACY" not in env_of(notebook("nb", "ns"))

@@ -1,0 +1,86 @@
+#!/bin/bash
+# One parametrized MI355X pass (replaces the per-call scripts of round 1).
+#
+#   gpurun --timeout 900 -- bash tools/gpu_pass.sh <tag> [step ...]
+#
+# Steps (default: tests smoke bench prof):
+#   tests    pytest -m gpu (one process, per-test timeout)
+#   smoke    __graft_entry__.smoke()
+#   bench    bench.py at N=1 (driver defaults), twice
+#   ranks    2/4-rank rehearsal of the N>1 launch on the one GPU (never 8: the driver owns N=8)
+#   webhook  BASELINE config #4 (tools/bench_webhook.py)
+#   culling  BASELINE config #5 (tools/bench_culling.py)
+#   prof     rocprofv3 --kernel-trace --stats of bench.py
+#   pmc      rocprofv3 --pmc passes (MFMA busy, LDS bank conflicts, HBM bytes) of the probe kernels
+#   env      tools/gpu_env_probe.sh inventory
+#
+# Every GPU step runs under its own `timeout -k`; the first failure ends the pass (no retries).
+set -o pipefail
+tag=${1:?usage: gpu_pass.sh <tag> [step ...]}
+shift
+steps=${*:-tests smoke bench prof}
+cd "${GRAFT_REPO_ROOT:-/root/repo}"
+export TMPDIR=/tmp
+out=gpurun_out/$tag
+mkdir -p "$out"
+
+show() {
+  python - "$1" "$2" <<'PY'
+import json, sys
+d = json.loads([l for l in open(sys.argv[1]) if l.startswith('{')][-1])
+keys = ("n_gpus", "value", "ms_per_step", "notebooks_ready_per_s", "p50_ready_ms", "p95_ready_ms",
+        "reconciles_per_notebook", "writes_per_notebook")
+print(sys.argv[2], {k: d.get(k) for k in keys})
+PY
+}
+fail() { echo "step $1 failed (rc=$2)"; tail -40 "$3"; exit 1; }
+
+for s in $steps; do
+  case $s in
+    tests)
+      timeout -k 10 300 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread \
+        > "$out/pytest_gpu.log" 2>&1 || fail tests $? "$out/pytest_gpu.log"
+      tail -1 "$out/pytest_gpu.log" ;;
+    smoke)
+      timeout -k 10 170 python __graft_entry__.py smoke > "$out/smoke.log" 2>&1 || fail smoke $? "$out/smoke.log"
+      tail -1 "$out/smoke.log" ;;
+    bench)
+      for r in 1 2; do
+        timeout -k 10 170 python bench.py > "$out/bench_n1_r$r.log" 2>&1 || fail bench $? "$out/bench_n1_r$r.log"
+        show "$out/bench_n1_r$r.log" "n1 r$r"
+      done ;;
+    ranks)
+      for n in 2 4; do
+        timeout -k 10 170 python -m torch.distributed.run --nnodes=1 --nproc-per-node $n \
+          --master-addr 127.0.0.1 --master-port 2993$n bench.py --gpus $n --steps 40 --warmup 5 \
+          > "$out/bench_n$n.log" 2>&1 || fail ranks $? "$out/bench_n$n.log"
+        show "$out/bench_n$n.log" "n$n"
+      done ;;
+    webhook)
+      timeout -k 10 170 python tools/bench_webhook.py --rounds 20 > "$out/webhook.log" 2>&1 || fail webhook $? "$out/webhook.log"
+      tail -1 "$out/webhook.log" ;;
+    culling)
+      timeout -k 10 170 python tools/bench_culling.py > "$out/culling.log" 2>&1 || fail culling $? "$out/culling.log"
+      tail -1 "$out/culling.log" ;;
+    prof)
+      timeout -k 10 200 rocprofv3 --kernel-trace --stats -d "$out/prof" -o run -- \
+        python3 bench.py --steps 40 --warmup 3 > "$out/bench_prof.log" 2>&1 || fail prof $? "$out/bench_prof.log"
+      find "$out/prof" -name '*kernel_stats*' | head -3 ;;
+    pmc)
+      # one counter group per pass, each within the per-block limits
+      i=0
+      for group in "SQ_WAVES SQ_INSTS_VALU_MFMA_MOPS_BF16 SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES" \
+                   "SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_LDS" \
+                   "FETCH_SIZE" "WRITE_SIZE"; do
+        i=$((i + 1))
+        timeout -s KILL 90 rocprofv3 --pmc $group --kernel-trace --stats -d "$out/pmc$i" -o run -- \
+          python3 tools/probe_microbench.py --pmc-pass > "$out/pmc$i.log" 2>&1 || fail "pmc$i" $? "$out/pmc$i.log"
+      done
+      echo "pmc passes: $i" ;;
+    env)
+      timeout -k 10 200 bash tools/gpu_env_probe.sh > "$out/env.log" 2>&1 || fail env $? "$out/env.log" ;;
+    *)
+      echo "unknown step $s"; exit 2 ;;
+  esac
+done
+echo "pass $tag done: $steps"

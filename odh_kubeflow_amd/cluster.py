@@ -9,6 +9,7 @@ from __future__ import annotations
 
 import asyncio
 import os
+import tempfile
 import time
 from dataclasses import dataclass, field
 from typing import Callable, Dict, List, Optional
@@ -38,6 +39,11 @@ class ClusterConfig:
     gpu_runtimes_in_process: bool = True  # False: rank processes host GPU runtimes (multi-GPU bench)
     reference_emulation: bool = False  # reproduce the reference's serialising behaviour for comparison
     activity_source: Optional[object] = None
+    # amdgpu telemetry (ops.telemetry.Telemetry) for the nodes: each node then runs the
+    # production node agent (nodeagent/), which attributes GPUs to pods from the fake
+    # kubelet's device-plugin checkpoint; the culler queries it over HTTP
+    telemetry: Optional[object] = None
+    device_id_of: Optional[Callable[[int], str]] = None  # node GPU index -> device-plugin ID (PCI address)
     openshift: bool = False  # serve the OpenShift APIs (image/config/route/oauth) like an OCP cluster
     # "inprocess": managers share the store directly; "http": the store is served by the REST
     # apiserver and the kf / odh managers, the webhook (HTTPS, MutatingWebhookConfiguration)
@@ -67,6 +73,9 @@ class LocalCluster:
         self.odh: Optional[Manager] = None
         self.kubelets: List[Manager] = []
         self.gpu_runtimes = []
+        self.device_managers = {}  # node name -> FakeDeviceManager
+        self.node_agents = {}  # node name -> production NodeTelemetryAgent
+        self._tmpdirs = []
         self.reconcilers: Dict[str, object] = {}
         self.webhook = None
         self.apiserver = None
@@ -103,8 +112,10 @@ class LocalCluster:
         self.rest_config = RestConfig(host=self.apiserver.url)
 
     async def start(self) -> "LocalCluster":
-        from .kubelet.node import GpuRuntime, SchedulerController, make_node
+        from .kubelet.agent import default_device_id_of
+        from .kubelet.node import FakeDeviceManager, GpuRuntime, SchedulerController, make_node
         from .kubelet.statefulset import StatefulSetController
+        from .nodeagent.checkpoint import CheckpointWriter
 
         cfg = self.cfg
         if cfg.transport == "http":
@@ -141,13 +152,26 @@ class LocalCluster:
         for n in range(cfg.nodes):
             node_name = f"mi355x-node-{n}"
             await admin.create(make_node(node_name, cfg.gpus_per_node))
+            tmp = tempfile.TemporaryDirectory(prefix=f"odh-{node_name}-")
+            self._tmpdirs.append(tmp)
+            cp_path = os.path.join(tmp.name, "device-plugins", "kubelet_internal_checkpoint")
+            dm = self.device_managers[node_name] = FakeDeviceManager(
+                cfg.device_id_of or default_device_id_of(cfg.telemetry), checkpoint=CheckpointWriter(cp_path))
+            if cfg.telemetry is not None:
+                from .nodeagent.attribution import Attributor
+                from .nodeagent.server import NodeTelemetryAgent
+
+                self.node_agents[node_name] = await NodeTelemetryAgent(
+                    cfg.telemetry, Attributor(cfg.telemetry, checkpoint_path=cp_path, ttl_s=0.0),
+                    host="127.0.0.1", port=0).start()
             if cfg.gpu_runtimes_in_process:
                 kl = self._mgr(f"kubelet-{node_name}", remote=cfg.remote_kubelets)
                 self.kubelets.append(kl)
                 for d in range(cfg.gpus_per_node):
                     rt = cfg.runtime_factory(d) if cfg.runtime_factory else None
                     g = GpuRuntime(kl.client, kl.reader, kl.get_event_recorder_for("kubelet"), node_name, [d],
-                                   runtime=rt, startup_probe=cfg.startup_probe, owns_cpu_pods=(d == 0))
+                                   runtime=rt, startup_probe=cfg.startup_probe, owns_cpu_pods=(d == 0),
+                                   device_manager=dm)
                     g.setup_with_manager(kl, name=f"kubelet-{node_name}-gpu{d}")
                     self.gpu_runtimes.append(g)
 
@@ -180,7 +204,16 @@ class LocalCluster:
         if self.cfg.culler or self.env.get("ENABLE_CULLING") == "true":
             from .controllers.culling import CullingReconciler
 
-            c = CullingReconciler(kf.client, kf.reader, metrics, env=self.env, activity=self.cfg.activity_source)
+            activity = self.cfg.activity_source
+            if activity is None and self.node_agents:
+                from .controllers.culling import NodeAgentActivity
+
+                # every fake node's pods report hostIP 127.0.0.1: route by node name instead
+                ports = {n: a.port for n, a in self.node_agents.items()}
+                activity = NodeAgentActivity(endpoint_for=lambda pod: "127.0.0.1:%d" % ports[
+                    (pod.get("spec") or {}).get("nodeName")] if (pod.get("spec") or {}).get("nodeName") in ports
+                    else None)
+            c = CullingReconciler(kf.client, kf.reader, metrics, env=self.env, activity=activity)
             c.setup_with_manager(kf, max_concurrent=1 if emu else None)
             self.reconcilers["culler"] = c
 
@@ -232,6 +265,10 @@ class LocalCluster:
             await mgr.stop()
         for g in self.gpu_runtimes:
             await g.close()
+        for a in self.node_agents.values():
+            await a.stop()
+        for t in self._tmpdirs:
+            t.cleanup()
         if self.webhook_server is not None:
             await self.webhook_server.stop()
         if self.apiserver is not None:

@@ -1,0 +1,92 @@
+"""Development kubelet stand-in as a process (TEST / DEV ONLY — never deployed).
+
+    python -m odh_kubeflow_amd.cmd.fake_kubelet --master http://127.0.0.1:6443 \
+        --node-name mi355x-node-0 --devices 0,1,2,3,4,5,6,7 --checkpoint-path /tmp/dp/kubelet_internal_checkpoint
+
+The companion of ``cmd/apiserver.py --controllers`` (the envtest substitute plus the
+StatefulSet controller / scheduler a real cluster has): it registers the Node, "runs" the
+pods scheduled to its GPUs and writes their status, and records GPU allocations in a
+kubelet device-plugin checkpoint — where the production node agent
+(``cmd/node_agent.py``) reads them.  ``--probe`` gates pod readiness on the MI355X start-up
+probe (needs the GPUs and the built ``libodh_gpu_probe.so``).  ``--jupyter`` serves the
+Jupyter API for started notebooks (culling e2e).
+"""
+
+from __future__ import annotations
+
+import argparse
+import asyncio
+import logging
+import sys
+
+log = logging.getLogger("setup")
+
+
+def parse(argv=None):
+    p = argparse.ArgumentParser(prog="odh-fake-kubelet")
+    p.add_argument("--master", default=None)
+    p.add_argument("--kubeconfig", default=None)
+    p.add_argument("--node-name", default="mi355x-node-0")
+    p.add_argument("--devices", default="0,1,2,3,4,5,6,7", help="node GPU indices this kubelet runs pods on")
+    p.add_argument("--node-gpus", type=int, default=8)
+    p.add_argument("--checkpoint-path", default=None, help="device-plugin checkpoint to write (default: a temp dir)")
+    p.add_argument("--sysfs-root", default=None, help="take device-plugin IDs (PCI addresses) from this KFD tree")
+    p.add_argument("--probe", action="store_true", help="gate Ready on the MI355X start-up probe")
+    p.add_argument("--address", default="127.0.0.1")
+    p.add_argument("--jupyter", action="store_true", help="serve the Jupyter API for started notebooks")
+    p.add_argument("--debug-log", action="store_true")
+    return p.parse_args(argv)
+
+
+def build(args):
+    from ..kubelet.agent import FakeKubeletAgent
+    from ..runtime.manager import Manager
+    from ..runtime.rest import RestConfig
+
+    devices = [int(x) for x in args.devices.split(",") if x.strip()]
+    mgr = Manager.remote(RestConfig.load(args.master, args.kubeconfig), name=f"kubelet-{args.node_name}")
+    probe = None
+    if args.probe:
+        import torch
+
+        from ..ops import gpu
+
+        ndev = torch.cuda.device_count()
+        for d in range(min(len(devices), ndev)):
+            gpu.get_probe(d).run()
+
+        async def probe(devs):
+            return await gpu.startup_probe(devs, local_index=lambda d: devices.index(d) % ndev if d in devices
+                                           else d % ndev)
+    device_id_of = None
+    if args.sysfs_root:
+        from ..kubelet.agent import default_device_id_of
+        from ..ops.telemetry import Telemetry
+
+        device_id_of = default_device_id_of(Telemetry(args.sysfs_root))
+    runtime = None
+    if args.jupyter:
+        from ..notebook_server.jupyter import JupyterContainerRuntime
+
+        runtime = JupyterContainerRuntime(host=args.address)
+    agent = FakeKubeletAgent(mgr, args.node_name, devices, args.node_gpus, runtime=runtime, startup_probe=probe,
+                             address=args.address, checkpoint_path=args.checkpoint_path, device_id_of=device_id_of)
+    return mgr, agent
+
+
+async def amain(argv=None) -> int:
+    from .common import setup_logging, signal_event
+
+    args = parse(argv)
+    setup_logging(debug=args.debug_log)
+    mgr, _agent = build(args)
+    await mgr.run_until(signal_event())
+    return 0
+
+
+def main(argv=None) -> int:
+    return asyncio.run(amain(argv))
+
+
+if __name__ == "__main__":
+    sys.exit(main())

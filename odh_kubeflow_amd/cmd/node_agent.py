@@ -1,11 +1,12 @@
-"""MI355X node agent process (``amd.com/gpu`` device plugin + kubelet stand-in + telemetry).
+"""MI355X node agent process (DaemonSet): amdgpu telemetry + pod→GPU attribution, read-only.
 
-    python -m odh_kubeflow_amd.cmd.node_agent --master http://127.0.0.1:6443 \
-        --node-name mi355x-node-0 --devices 0,1,2,3,4,5,6,7
+    python -m odh_kubeflow_amd.cmd.node_agent --port 9464 --sysfs-root /host/sys --proc-root /host/proc \
+        --pod-resources-socket /var/lib/kubelet/pod-resources/kubelet.sock \
+        --device-plugin-checkpoint /var/lib/kubelet/device-plugins/kubelet_internal_checkpoint
 
-``--probe`` gates pod readiness on the MI355X start-up probe (needs the GPUs and the
-built ``libodh_gpu_probe.so``); ``--sysfs-root`` points the native telemetry sampler at
-``/sys`` (default) or a synthetic tree.
+The agent has no apiserver client at all (no ``--master``/``--kubeconfig``): it cannot
+write Nodes or pod status, and its ServiceAccount needs no RBAC.  Every attribution source
+is optional; a missing one is reported on ``/gpu/pods`` and the others are used.
 """
 
 from __future__ import annotations
@@ -13,6 +14,7 @@ from __future__ import annotations
 import argparse
 import asyncio
 import logging
+import os
 import sys
 
 log = logging.getLogger("setup")
@@ -20,56 +22,39 @@ log = logging.getLogger("setup")
 
 def parse(argv=None):
     p = argparse.ArgumentParser(prog="odh-node-agent")
-    p.add_argument("--master", default=None)
-    p.add_argument("--kubeconfig", default=None)
-    p.add_argument("--node-name", default="mi355x-node-0")
-    p.add_argument("--devices", default="0,1,2,3,4,5,6,7", help="node GPU indices this agent owns")
-    p.add_argument("--node-gpus", type=int, default=8)
-    p.add_argument("--probe", action="store_true", help="gate Ready on the MI355X start-up probe")
+    p.add_argument("--bind", default="0.0.0.0")
+    p.add_argument("--port", type=int, default=9464)
     p.add_argument("--sysfs-root", default="/sys")
+    p.add_argument("--proc-root", default="/proc", help="host /proc (pod UID from each GPU process's cgroup); "
+                   "'' disables KFD per-process attribution")
+    p.add_argument("--pod-resources-socket", default="/var/lib/kubelet/pod-resources/kubelet.sock")
+    p.add_argument("--device-plugin-checkpoint",
+                   default="/var/lib/kubelet/device-plugins/kubelet_internal_checkpoint")
+    p.add_argument("--resource-name", default="amd.com/gpu")
     p.add_argument("--telemetry-interval-ms", type=int, default=200)
-    p.add_argument("--activity-port", type=int, default=0)
-    p.add_argument("--address", default="127.0.0.1")
-    p.add_argument("--jupyter", action="store_true", help="serve the Jupyter API for started notebooks")
+    p.add_argument("--telemetry-capacity", type=int, default=3000, help="samples kept per GPU (window length)")
+    p.add_argument("--attribution-ttl-s", type=float, default=1.0)
     p.add_argument("--debug-log", action="store_true")
     return p.parse_args(argv)
 
 
 def build(args):
-    from ..kubelet.agent import NodeAgent
-    from ..runtime.manager import Manager
-    from ..runtime.rest import RestConfig
+    from ..nodeagent.attribution import Attributor
+    from ..nodeagent.podresources import PodResourcesClient
+    from ..nodeagent.server import NodeTelemetryAgent
+    from ..ops.telemetry import Telemetry
 
-    devices = [int(x) for x in args.devices.split(",") if x.strip()]
-    mgr = Manager.remote(RestConfig.load(args.master, args.kubeconfig), name=f"kubelet-{args.node_name}")
-    probe = None
-    if args.probe:
-        from ..ops import gpu
-
-        import torch
-
-        ndev = torch.cuda.device_count()
-        for d in range(min(len(devices), ndev)):
-            gpu.get_probe(d).run()
-
-        async def probe(devs):
-            return await gpu.startup_probe(devs, local_index=lambda d: devices.index(d) % ndev if d in devices
-                                           else d % ndev)
-    telemetry = None
-    try:
-        from ..ops.telemetry import Telemetry
-
-        telemetry = Telemetry(args.sysfs_root).start(args.telemetry_interval_ms, 3000)
-    except Exception as e:  # telemetry is optional; the culler falls back to Jupyter activity
-        log.warning("amdgpu telemetry unavailable: %r", e)
-    runtime = None
-    if args.jupyter:
-        from ..notebook_server.jupyter import JupyterContainerRuntime
-
-        runtime = JupyterContainerRuntime(host=args.address)
-    agent = NodeAgent(mgr, args.node_name, devices, args.node_gpus, runtime=runtime, startup_probe=probe,
-                      telemetry=telemetry, address=args.address, activity_port=args.activity_port)
-    return mgr, agent
+    telemetry = Telemetry(args.sysfs_root).start(args.telemetry_interval_ms, args.telemetry_capacity)
+    log.info("amdgpu telemetry: %d KFD GPU node(s) under %s", len(telemetry), args.sysfs_root)
+    pr = PodResourcesClient(args.pod_resources_socket) if args.pod_resources_socket else None
+    if pr is not None and not pr.available():
+        log.warning("pod-resources socket %s not mounted; using the device-plugin checkpoint and KFD",
+                    args.pod_resources_socket)
+    attributor = Attributor(telemetry, pod_resources=pr if pr is not None and pr.available() else None,
+                            checkpoint_path=args.device_plugin_checkpoint or None,
+                            proc_root=args.proc_root or None, resource=args.resource_name,
+                            ttl_s=args.attribution_ttl_s)
+    return NodeTelemetryAgent(telemetry, attributor, host=args.bind, port=args.port)
 
 
 async def amain(argv=None) -> int:
@@ -77,8 +62,14 @@ async def amain(argv=None) -> int:
 
     args = parse(argv)
     setup_logging(debug=args.debug_log)
-    mgr, _agent = build(args)
-    await mgr.run_until(signal_event())
+    agent = build(args)
+    await agent.start()
+    log.info("node agent serving on %s:%d (pid %d)", args.bind, agent.port, os.getpid())
+    try:
+        await signal_event().wait()
+    finally:
+        await agent.stop()
+        agent.telemetry.close()
     return 0
 
 

@@ -19,12 +19,25 @@ Activity sources (``CULLING_ACTIVITY_SOURCE``):
 * ``jupyter`` (default, the reference): ``GET .../api/kernels`` and ``.../api/terminals``
   (10 s timeout each); any non-idle kernel means "active now", otherwise the newest
   kernel/terminal ``last_activity`` is taken if it is newer than the annotation;
-* ``amdgpu``: the notebook's GPUs (``amd.com/gpu-ids`` written by the device allocator)
-  are sampled by the node agent's native amdgpu telemetry; a mean busy percentage over
-  the last check period at or above ``CULLING_GPU_BUSY_THRESHOLD`` (default 5) means
-  "active now".  Averaging over the whole window is the hysteresis: a single spike does
-  not keep a notebook alive and a single idle sample does not cull it;
+* ``amdgpu``: for a pod that requests ``amd.com/gpu``, the node agent of the pod's node
+  (``http://<pod.status.hostIP>:CULLING_GPU_AGENT_PORT``, default 9464; ``nodeagent/``)
+  is asked by pod UID which GPUs the kubelet gave the pod (pod-resources API /
+  device-plugin checkpoint / KFD per-process sysfs — no pod annotation involved) and how
+  busy they were over the last check period.  A mean busy percentage at or above
+  ``CULLING_GPU_BUSY_THRESHOLD`` (default 5) means "active now".  Averaging over the whole
+  window is the hysteresis: a single spike does not keep a notebook alive and a single
+  idle sample does not cull it;
 * ``combined``: active if either signal says so.
+
+Resident VRAM is **not** activity by default.  A notebook that holds 200 GB of HBM3E at
+0 % busy for ``CULL_IDLE_TIME`` (24 h by default) is exactly the waste culling exists to
+reclaim: the memory is stranded for every other tenant of the GPU, and the state it holds
+is what the user's PVC-backed home directory and checkpoints are for.  Interactive use
+that keeps a model resident (occasional generation calls) shows up as busy samples and,
+in ``combined`` mode, as Jupyter kernel activity.  Clusters that want the other policy set
+``CULLING_GPU_VRAM_ACTIVE_BYTES`` (e.g. ``1e9``): the pod then counts as active while its
+own processes hold at least that much VRAM (KFD per-process accounting, so a co-tenant's
+memory on a shared GPU never keeps it alive).
 
 Missing telemetry is never read as idleness: with no GPU samples the Jupyter signal is
 used, and with neither the last-activity annotation is simply left alone (as the
@@ -42,13 +55,13 @@ import json
 import logging
 import os
 from dataclasses import dataclass
-from typing import Any, Callable, List, Mapping, Optional, Sequence
+from typing import Any, Callable, Mapping, Optional, Sequence
 
 from ..models import kinds
 from ..models import meta as m
 from ..models.errors import ApiError, is_not_found
-from ..models.notebook import (GPU_IDS_ANNOTATION, LAST_ACTIVITY_ANNOTATION, LAST_ACTIVITY_CHECK_TIMESTAMP_ANNOTATION,
-                               STOP_ANNOTATION)
+from ..models.notebook import (LAST_ACTIVITY_ANNOTATION, LAST_ACTIVITY_CHECK_TIMESTAMP_ANNOTATION, STOP_ANNOTATION,
+                               gpu_request)
 from ..runtime.controller import Request, Result
 from ..runtime.retry import retry_on_conflict
 from ..utils.timeutil import now, parse_rfc3339, rfc3339
@@ -75,6 +88,8 @@ class CullerConfig:
     dev: bool = False
     activity_source: str = "jupyter"
     gpu_busy_threshold: float = 5.0
+    gpu_agent_port: int = 9464
+    gpu_vram_active_bytes: float = 0.0  # 0: resident VRAM is not activity (see module docstring)
     http_timeout_s: float = 10.0
 
     @classmethod
@@ -100,6 +115,8 @@ class CullerConfig:
         if c.activity_source not in ("jupyter", "amdgpu", "combined"):
             raise ValueError(f"CULLING_ACTIVITY_SOURCE must be jupyter|amdgpu|combined, got {c.activity_source}")
         c.gpu_busy_threshold = float(env_default(env, "CULLING_GPU_BUSY_THRESHOLD", "5"))
+        c.gpu_agent_port = int(env_default(env, "CULLING_GPU_AGENT_PORT", "9464"))
+        c.gpu_vram_active_bytes = float(env_default(env, "CULLING_GPU_VRAM_ACTIVE_BYTES", "0"))
         return c
 
 
@@ -207,9 +224,15 @@ def set_stop_annotation(nb: dict, metrics=None) -> None:
         metrics.notebook_culling_timestamp.labels(m.namespace(nb), m.name(nb)).set(int(t))
 
 
-def pod_gpu_ids(pod: Optional[dict]) -> List[int]:
-    raw = m.annotations(pod or {}).get(GPU_IDS_ANNOTATION) or ""
-    return [int(x) for x in raw.split(",") if x.strip().isdigit()]
+def pod_requests_gpu(pod: Optional[dict]) -> bool:
+    return gpu_request((pod or {}).get("spec") or {}) > 0
+
+
+def gpu_says_active(data: dict, cfg: CullerConfig) -> bool:
+    if data.get("busy_mean", -1) >= cfg.gpu_busy_threshold:
+        return True
+    vram = data.get("pod_vram_bytes")
+    return cfg.gpu_vram_active_bytes > 0 and vram is not None and vram >= cfg.gpu_vram_active_bytes
 
 
 # ------------------------------------------------------------------ activity sources
@@ -270,84 +293,90 @@ class JupyterActivity:
 
 
 class GpuActivity:
-    """Base class: mean/max busy percentage of the given node GPUs over ``window_s``.
+    """Base class: how busy the GPUs attributed to ``pod`` were over the last ``window_s``.
 
-    Returns ``None`` when no sample could be read (never interpreted as idle).
+    Returns a dict with ``busy_mean`` / ``busy_max`` (percent), ``vram_used_mean`` (device)
+    and ``pod_vram_bytes`` (the pod's own processes, KFD; ``None`` if unknown), or ``None``
+    when nothing could be read — never interpreted as idle.
     """
 
-    async def busy(self, pod: dict, devices: Sequence[int], window_s: float) -> Optional[dict]:
+    async def busy(self, pod: dict, window_s: float) -> Optional[dict]:
         raise NotImplementedError
 
     async def close(self) -> None:
         return None
 
 
+def _usable(data: Optional[dict]) -> Optional[dict]:
+    return data if data and data.get("n", 0) > 0 and data.get("busy_mean", -1) >= 0 else None
+
+
 class LocalTelemetryActivity(GpuActivity):
-    """Reads an in-process :class:`~odh_kubeflow_amd.ops.telemetry.Telemetry` (single-node setups)."""
+    """In-process telemetry + attribution (a single-node setup running the culler next to the
+    GPUs): :class:`~odh_kubeflow_amd.nodeagent.attribution.Attributor` resolves the pod."""
 
-    def __init__(self, telemetry, index_of: Optional[Callable[[int], Optional[int]]] = None):
+    def __init__(self, telemetry, attributor):
         self.telemetry = telemetry
-        self.index_of = index_of or (lambda d: d)
+        self.attributor = attributor
 
-    async def busy(self, pod, devices, window_s):
-        return aggregate_windows(self.telemetry, [self.index_of(d) for d in devices], window_s)
+    async def busy(self, pod, window_s):
+        from ..nodeagent.server import aggregate_windows
+
+        pg = await self.attributor.lookup(m.uid(pod), m.namespace(pod), m.name(pod))
+        if pg is None:
+            return None
+        agg = aggregate_windows(self.telemetry, pg.devices, window_s)
+        if agg is not None:
+            agg["pod_vram_bytes"] = pg.pod_vram_bytes
+        return _usable(agg)
 
 
 class NodeAgentActivity(GpuActivity):
-    """Asks the node agent that owns the pod's GPUs (``/gpu/activity`` on the Node's
-    ``amd.com/gpu-activity-port``); the telemetry lives next to the GPUs, not here."""
+    """Asks the node agent on the pod's node (``nodeagent/server.py``) — the telemetry and the
+    kubelet's allocation records live next to the GPUs, not in the controller.
 
-    def __init__(self, reader, timeout_s: float = 2.0):
-        self.reader = reader
+    The agent is a DaemonSet with a hostPort, so it is at ``<pod.status.hostIP>:<port>``;
+    ``endpoint_for(pod) -> "host:port"`` overrides that (test harnesses whose fake nodes
+    share one IP).
+    """
+
+    def __init__(self, port: int = 9464, timeout_s: float = 2.0,
+                 endpoint_for: Optional[Callable[[dict], Optional[str]]] = None):
+        self.port = port
         self.timeout_s = timeout_s
+        self.endpoint_for = endpoint_for or self.default_endpoint
         self._session = None
+        self.requests = 0
 
-    async def busy(self, pod, devices, window_s):
+    def default_endpoint(self, pod: dict) -> Optional[str]:
+        host = (pod.get("status") or {}).get("hostIP")
+        return f"{host}:{self.port}" if host else None
+
+    async def busy(self, pod, window_s):
+        import urllib.parse
+
         import aiohttp
 
-        node = self.reader.get(kinds.NODE, (pod.get("spec") or {}).get("nodeName", ""))
-        if node is None:
-            return None
-        port = m.annotations(node).get("amd.com/gpu-activity-port")
-        addr = next((a.get("address") for a in (node.get("status") or {}).get("addresses") or []
-                     if a.get("type") == "InternalIP"), None)
-        if not port or not addr:
+        ep = self.endpoint_for(pod)
+        if not ep:
             return None
         if self._session is None or self._session.closed:
             self._session = aiohttp.ClientSession(timeout=aiohttp.ClientTimeout(total=self.timeout_s))
-        url = f"http://{addr}:{port}/gpu/activity?devices={','.join(map(str, devices))}&window={window_s}"
+        q = urllib.parse.urlencode({"pod_uid": m.uid(pod), "namespace": m.namespace(pod), "name": m.name(pod),
+                                    "window": window_s})
+        self.requests += 1
         try:
-            async with self._session.get(url) as resp:
+            async with self._session.get(f"http://{ep}/gpu/activity?{q}") as resp:
                 if resp.status != 200:
                     return None
                 data = await resp.json()
-        except Exception:
+        except Exception:  # agent down / unreachable: no data, never idleness
             return None
-        return data if data and data.get("n", 0) > 0 else None
+        return _usable(data)
 
     async def close(self):
         if self._session is not None:
             await self._session.close()
-
-
-def aggregate_windows(telemetry, indices: Sequence[Optional[int]], window_s: float) -> Optional[dict]:
-    """Combine per-device windows: the notebook is as busy as its busiest GPU."""
-    best = None
-    n = 0
-    for idx in indices:
-        if idx is None:
-            continue
-        w = telemetry.window(idx, window_s)
-        if w is None or w.n == 0 or w.busy_mean < 0:
-            continue
-        n += w.n
-        cand = {"busy_mean": w.busy_mean, "busy_max": w.busy_max, "vram_used_mean": w.vram_used_mean}
-        if best is None or cand["busy_mean"] > best["busy_mean"]:
-            best = cand
-    if best is None:
-        return None
-    best["n"] = n
-    return best
 
 
 # ------------------------------------------------------------------ reconciler
@@ -365,7 +394,7 @@ class CullingReconciler:
         self.cfg = config or CullerConfig.from_env(self.env)
         self.gpu: Optional[GpuActivity] = activity
         if self.gpu is None and self.cfg.activity_source in ("amdgpu", "combined"):
-            self.gpu = NodeAgentActivity(reader)
+            self.gpu = NodeAgentActivity(port=self.cfg.gpu_agent_port)
         self.jupyter = jupyter or JupyterActivity(self.cfg, use_pod_endpoint=self.env.get(
             "CULLER_USE_POD_ENDPOINT", "false") == "true")
         self.culled = 0
@@ -430,12 +459,10 @@ class CullingReconciler:
         src = self.cfg.activity_source
         gpu_active = False
         gpu_data = None
-        if src in ("amdgpu", "combined") and self.gpu is not None:
-            devs = pod_gpu_ids(pod)
-            if devs:
-                gpu_data = await self.gpu.busy(pod, devs, self.cfg.check_period_s)
-                if gpu_data is not None:
-                    gpu_active = gpu_data["busy_mean"] >= self.cfg.gpu_busy_threshold
+        if src in ("amdgpu", "combined") and self.gpu is not None and pod_requests_gpu(pod):
+            gpu_data = await self.gpu.busy(pod, self.cfg.check_period_s)
+            if gpu_data is not None:
+                gpu_active = gpu_says_active(gpu_data, self.cfg)
         kernels = terminals = None
         if src in ("jupyter", "combined") or gpu_data is None:
             kernels, terminals = await self.jupyter.sample(nb, pod)

@@ -10,9 +10,9 @@
   Roles, user aggregation roles (``kubeflow-notebooks-{admin,edit,view}``);
 * ``manager/`` — the two manager Deployments with the reference flags, probes on
   :8081, metrics on :8080, ``GOMEMLIMIT``-style limits, env from ConfigMaps;
-* ``node-agent/`` — the MI355X node agent DaemonSet (``amd.com/gpu.family`` nodes,
-  ``/sys`` read-only for amdgpu telemetry, ``/dev/kfd`` + ``/dev/dri`` for the start-up
-  probe; it never requests ``amd.com/gpu`` itself);
+* ``node-agent/`` — the MI355X node agent DaemonSet (``amd.com/gpu.family`` nodes):
+  read-only amdgpu telemetry + pod→GPU attribution (``nodeagent/``), no apiserver access,
+  no RBAC, no GPU device files; it never requests ``amd.com/gpu`` itself;
 * ``webhook/`` — Service + MutatingWebhookConfiguration (``failurePolicy: Fail``);
 * ``overlays/{kubeflow,standalone,openshift,mi355x}`` — Istio on/off, OpenShift
   service-ca injection + ``ADD_FSGROUP=false``, MI355X placement + GPU-busy culling;
@@ -163,15 +163,6 @@ def odh_role() -> dict:
             ]}
 
 
-def node_agent_role() -> dict:
-    return {"apiVersion": "rbac.authorization.k8s.io/v1", "kind": "ClusterRole",
-            "metadata": {"name": "mi355x-node-agent-role"},
-            "rules": [_rule([""], ["nodes"], ["get", "list", "watch", "create", "patch", "update"]),
-                      _rule([""], ["pods"], ["get", "list", "watch", "patch"]),
-                      _rule([""], ["pods/status"], ["patch", "update"]),
-                      _rule([""], ["events"], ["create", "patch"])]}
-
-
 def leader_election_role(name: str) -> dict:
     return {"apiVersion": "rbac.authorization.k8s.io/v1", "kind": "Role", "metadata": {"name": name},
             "rules": [_rule(["coordination.k8s.io"], ["leases"], ALL), _rule([""], ["events"], ["create", "patch"])]}
@@ -216,7 +207,7 @@ def kf_deployment() -> dict:
          "env": [{"name": k, "valueFrom": {"configMapKeyRef": {"name": "notebook-controller-culler-config",
                                                                 "key": k, "optional": True}}}
                  for k in ("ENABLE_CULLING", "CULL_IDLE_TIME", "IDLENESS_CHECK_PERIOD", "CULLING_ACTIVITY_SOURCE",
-                           "CULLING_GPU_BUSY_THRESHOLD")],
+                           "CULLING_GPU_BUSY_THRESHOLD", "CULLING_GPU_AGENT_PORT", "CULLING_GPU_VRAM_ACTIVE_BYTES")],
          "ports": [{"name": "metrics", "containerPort": 8080}, {"name": "probes", "containerPort": 8081}],
          "resources": {"requests": {"cpu": "500m", "memory": "256Mi"}, "limits": {"cpu": "2", "memory": "2Gi"}},
          **_probes()}
@@ -255,29 +246,41 @@ def odh_deployment() -> dict:
 
 
 def node_agent_daemonset() -> dict:
+    """The production node agent (``cmd/node_agent.py``): read-only amdgpu telemetry + pod→GPU
+    attribution.  No apiserver access (token not mounted, no RBAC), no GPU device files; reads
+    host ``/sys`` (amdgpu + KFD), host ``/proc`` (pod cgroup of each GPU process), the kubelet
+    pod-resources socket and device-plugin checkpoint.  The culler reaches it on the hostPort."""
     c = {"name": "agent", "image": MANAGER_IMAGE,
          "command": ["python", "-m", "odh_kubeflow_amd.cmd.node_agent"],
-         "args": ["--node-name=$(NODE_NAME)", "--address=$(NODE_IP)", "--activity-port=9464",
-                  "--sysfs-root=/host/sys", "--devices=0,1,2,3,4,5,6,7"],
-         "env": [{"name": "NODE_NAME", "valueFrom": {"fieldRef": {"fieldPath": "spec.nodeName"}}},
-                 {"name": "NODE_IP", "valueFrom": {"fieldRef": {"fieldPath": "status.hostIP"}}}],
+         "args": ["--port=9464", "--sysfs-root=/host/sys", "--proc-root=/host/proc",
+                  "--pod-resources-socket=/var/lib/kubelet/pod-resources/kubelet.sock",
+                  "--device-plugin-checkpoint=/var/lib/kubelet/device-plugins/kubelet_internal_checkpoint"],
          "ports": [{"name": "gpu-activity", "containerPort": 9464, "hostPort": 9464}],
+         "livenessProbe": {"httpGet": {"path": "/healthz", "port": 9464}, "periodSeconds": 20},
          "volumeMounts": [{"name": "sys", "mountPath": "/host/sys", "readOnly": True},
-                          {"name": "kfd", "mountPath": "/dev/kfd"}, {"name": "dri", "mountPath": "/dev/dri"}],
-         "securityContext": {"readOnlyRootFilesystem": True, "allowPrivilegeEscalation": False},
-         "resources": {"requests": {"cpu": "100m", "memory": "512Mi"}, "limits": {"memory": "8Gi"}}}
+                          {"name": "proc", "mountPath": "/host/proc", "readOnly": True},
+                          {"name": "pod-resources", "mountPath": "/var/lib/kubelet/pod-resources"},
+                          {"name": "device-plugins", "mountPath": "/var/lib/kubelet/device-plugins",
+                           "readOnly": True}],
+         "securityContext": {"readOnlyRootFilesystem": True, "allowPrivilegeEscalation": False,
+                             "capabilities": {"drop": ["ALL"]}},
+         "resources": {"requests": {"cpu": "50m", "memory": "128Mi"}, "limits": {"memory": "512Mi"}}}
     return {"apiVersion": "apps/v1", "kind": "DaemonSet",
             "metadata": {"name": "mi355x-node-agent", "labels": {"app": "mi355x-node-agent"}},
             "spec": {"selector": {"matchLabels": {"app": "mi355x-node-agent"}},
                      "template": {"metadata": {"labels": {"app": "mi355x-node-agent"}},
                                   "spec": {"serviceAccountName": "mi355x-node-agent",
+                                           "automountServiceAccountToken": False,
                                            "nodeSelector": {"amd.com/gpu.family": "AI"},
                                            "tolerations": [{"key": GPU_RESOURCE, "operator": "Exists",
                                                             "effect": "NoSchedule"}],
                                            "containers": [c],
                                            "volumes": [{"name": "sys", "hostPath": {"path": "/sys"}},
-                                                       {"name": "kfd", "hostPath": {"path": "/dev/kfd"}},
-                                                       {"name": "dri", "hostPath": {"path": "/dev/dri"}}]}}}}
+                                                       {"name": "proc", "hostPath": {"path": "/proc"}},
+                                                       {"name": "pod-resources", "hostPath": {
+                                                           "path": "/var/lib/kubelet/pod-resources"}},
+                                                       {"name": "device-plugins", "hostPath": {
+                                                           "path": "/var/lib/kubelet/device-plugins"}}]}}}}
 
 
 def webhook_service() -> dict:
@@ -326,14 +329,12 @@ def tree() -> Dict[str, object]:
     t["crd/kustomization.yaml"] = kustomization(["bases/kubeflow.org_notebooks.yaml"])
     t["rbac/kf_role.yaml"] = kf_role()
     t["rbac/odh_role.yaml"] = odh_role()
-    t["rbac/node_agent_role.yaml"] = node_agent_role()
     t["rbac/leader_election_roles.yaml"] = [leader_election_role("notebook-controller-leader-election-role"),
                                             leader_election_role("odh-notebook-controller-leader-election-role")]
     t["rbac/role_bindings.yaml"] = [
         binding("ClusterRoleBinding", "notebook-controller-role-binding", "notebook-controller-role", "service-account"),
         binding("ClusterRoleBinding", "odh-notebook-controller-manager-rolebinding",
                 "odh-notebook-controller-manager-role", "manager"),
-        binding("ClusterRoleBinding", "mi355x-node-agent-rolebinding", "mi355x-node-agent-role", "mi355x-node-agent"),
         binding("RoleBinding", "notebook-controller-leader-election-rolebinding",
                 "notebook-controller-leader-election-role", "service-account"),
         binding("RoleBinding", "odh-notebook-controller-leader-election-rolebinding",
@@ -352,7 +353,8 @@ def tree() -> Dict[str, object]:
         configMapGenerator=[{"name": "config", "envs": ["params.env"]},
                             {"name": "notebook-controller-culler-config",
                              "literals": ["ENABLE_CULLING=false", "CULL_IDLE_TIME=1440", "IDLENESS_CHECK_PERIOD=1",
-                                          "CULLING_ACTIVITY_SOURCE=jupyter", "CULLING_GPU_BUSY_THRESHOLD=5"]}],
+                                          "CULLING_ACTIVITY_SOURCE=jupyter", "CULLING_GPU_BUSY_THRESHOLD=5",
+                                          "CULLING_GPU_AGENT_PORT=9464", "CULLING_GPU_VRAM_ACTIVE_BYTES=0"]}],
         generatorOptions={"disableNameSuffixHash": True})
     t["manager/params.env"] = "USE_ISTIO=false\nISTIO_GATEWAY=kubeflow/kubeflow-gateway\nISTIO_HOST=*\n" \
                               "CLUSTER_DOMAIN=cluster.local\nADD_FSGROUP=true\nGPU_NODE_SELECTOR=false\n" \

@@ -1,32 +1,29 @@
-"""MI355X node agent: the per-node process that owns GPUs (``amd.com/gpu`` device plugin
-half + kubelet stand-in + amdgpu telemetry endpoint).
+"""Fake kubelet agent of one (or a few) GPUs — TEST HARNESS / BENCHMARK ONLY.
 
-Responsibilities:
+It plays the node-side platform pieces a real MI355X node already has, so the control
+plane can be exercised without a cluster:
 
-* register / refresh the ``Node`` object: capacity ``amd.com/gpu`` = number of MI355X,
-  AMD node-labeller labels, ``amd.com/gpu-activity-port`` annotation;
-* run :class:`~odh_kubeflow_amd.kubelet.node.GpuRuntime` for its devices: start pods
-  allocated to them, gate Ready on the MI355X start-up probe (``ops/gpu.py``: MFMA GEMM
-  checked bit-exactly + HBM3E sweep), report pod status;
-* serve ``GET /gpu/activity?devices=0,3&window=60`` (mean/max busy %, VRAM) from the
-  native sysfs sampler (``ops/csrc/gpu_telemetry.cpp``) for the culler's ``amdgpu``
-  signal, plus ``/gpu/devices`` and ``/healthz``.
+* registers the ``Node`` (capacity ``amd.com/gpu``, AMD node-labeller labels) — the kubelet's job;
+* runs :class:`~odh_kubeflow_amd.kubelet.node.GpuRuntime` for its devices (start pods,
+  optionally gate Ready on the MI355X start-up probe, report pod status) — the kubelet's job;
+* publishes GPU allocations through a :class:`~odh_kubeflow_amd.kubelet.node.FakeDeviceManager`
+  (device-plugin checkpoint file) — the kubelet device manager's job;
+* optionally hosts the **production** node agent
+  (:class:`~odh_kubeflow_amd.nodeagent.server.NodeTelemetryAgent`) next to it, which attributes
+  GPUs to pods from that checkpoint exactly as it does on a real node.
 
-One agent per GPU process is the MI355X layout used by the benchmark (rank r owns
-GPU r); one agent for the whole node is the DaemonSet layout.
+The shipped DaemonSet (``config/node-agent``) runs ``cmd/node_agent.py`` — the production
+agent alone, which has no apiserver client.  Nothing here is deployed.
 """
 
 from __future__ import annotations
 
-import logging
+import os
+import tempfile
 from typing import Callable, Dict, List, Optional, Sequence
 
-from ..models import kinds
-from ..models import meta as m
 from ..models.errors import ApiError, is_already_exists
-from .node import GpuRuntime, make_node
-
-log = logging.getLogger("kubelet.agent")
+from .node import FakeDeviceManager, GpuRuntime, make_node
 
 
 def pci_bus_index_map(telemetry, local_bus_ids: Dict[int, int]) -> Dict[int, int]:
@@ -37,101 +34,75 @@ def pci_bus_index_map(telemetry, local_bus_ids: Dict[int, int]) -> Dict[int, int
     return {g: by_bus[b] for g, b in local_bus_ids.items() if b in by_bus}
 
 
-class TelemetryEndpoint:
-    def __init__(self, telemetry, index_of: Optional[Callable[[int], Optional[int]]] = None,
-                 host: str = "0.0.0.0", port: int = 0):
-        self.telemetry = telemetry
-        self.index_of = index_of or (lambda d: d)
-        self.host = host
-        self.port = port
-        self._runner = None
-        self.queries = 0
+def default_device_id_of(telemetry=None) -> Callable[[int], str]:
+    """Device-plugin IDs for node GPU indices: the PCI address of the telemetry device with
+    that index when there is one, else the synthetic-tree address."""
+    from ..ops.telemetry import fake_bdf
 
-    async def start(self) -> "TelemetryEndpoint":
-        from aiohttp import web
+    devs = telemetry.devices() if telemetry is not None else []
 
-        from ..controllers.culling import aggregate_windows
-
-        async def activity(req):
-            self.queries += 1
-            try:
-                devs = [int(x) for x in (req.query.get("devices") or "").split(",") if x.strip() != ""]
-                window = float(req.query.get("window") or 60)
-            except ValueError:
-                return web.json_response({"error": "bad query"}, status=400)
-            if self.telemetry is None:
-                return web.json_response({"n": 0})
-            agg = aggregate_windows(self.telemetry, [self.index_of(d) for d in devs], window)
-            return web.json_response(agg or {"n": 0})
-
-        async def devices(_req):
-            if self.telemetry is None:
-                return web.json_response([])
-            return web.json_response([d.__dict__ for d in self.telemetry.devices()])
-
-        async def healthz(_req):
-            return web.Response(text="ok")
-
-        app = web.Application()
-        app.router.add_get("/gpu/activity", activity)
-        app.router.add_get("/gpu/devices", devices)
-        app.router.add_get("/healthz", healthz)
-        self._runner = web.AppRunner(app, access_log=None)
-        await self._runner.setup()
-        site = web.TCPSite(self._runner, self.host, self.port)
-        await site.start()
-        self.port = site._server.sockets[0].getsockname()[1]
-        return self
-
-    async def stop(self) -> None:
-        if self._runner is not None:
-            await self._runner.cleanup()
-            self._runner = None
+    def of(i: int) -> str:
+        return devs[i].pci_bdf if i < len(devs) else fake_bdf(i)
+    return of
 
 
-class NodeAgent:
+class FakeKubeletAgent:
     def __init__(self, mgr, node_name: str, devices: Sequence[int], node_gpus: int = 8, runtime=None,
-                 startup_probe=None, telemetry=None, telemetry_index: Optional[Callable[[int], Optional[int]]] = None,
-                 register_node: bool = True, owns_cpu_pods: bool = True, address: str = "127.0.0.1",
-                 activity_port: int = 0):
+                 startup_probe=None, telemetry=None, register_node: bool = True, owns_cpu_pods: bool = True,
+                 address: str = "127.0.0.1", activity_port: int = 0, checkpoint_path: Optional[str] = None,
+                 device_id_of: Optional[Callable[[int], str]] = None):
+        from ..nodeagent.checkpoint import CheckpointWriter
+
         self.mgr = mgr
         self.node_name = node_name
         self.devices = list(devices)
         self.node_gpus = node_gpus
         self.register_node = register_node
         self.address = address
-        self.endpoint = TelemetryEndpoint(telemetry, telemetry_index, port=activity_port) if telemetry is not None \
-            else None
+        self._tmp = None
+        if checkpoint_path is None:
+            self._tmp = tempfile.TemporaryDirectory(prefix="odh-kubelet-")
+            checkpoint_path = os.path.join(self._tmp.name, "device-plugins", "kubelet_internal_checkpoint")
+        self.checkpoint_path = checkpoint_path
+        self.device_manager = FakeDeviceManager(device_id_of or default_device_id_of(telemetry),
+                                                checkpoint=CheckpointWriter(checkpoint_path))
+        self.telemetry_agent = None
+        if telemetry is not None:
+            from ..nodeagent.attribution import Attributor
+            from ..nodeagent.server import NodeTelemetryAgent
+
+            self.telemetry_agent = NodeTelemetryAgent(
+                telemetry, Attributor(telemetry, checkpoint_path=checkpoint_path, ttl_s=0.0),
+                host=address, port=activity_port)
         self.runtimes: List[GpuRuntime] = []
         for i, d in enumerate(self.devices):
             g = GpuRuntime(mgr.client, mgr.reader, mgr.get_event_recorder_for("kubelet"), node_name, [d],
                            runtime=runtime, startup_probe=startup_probe, owns_cpu_pods=owns_cpu_pods and i == 0,
-                           host_ip=address)
+                           host_ip=address, device_manager=self.device_manager)
             g.setup_with_manager(mgr, name=f"kubelet-{node_name}-gpu{d}")
             self.runtimes.append(g)
         mgr.add(self, needs_leader=False)
 
     async def start(self) -> None:
-        if self.endpoint is not None:
-            await self.endpoint.start()
+        if self.telemetry_agent is not None:
+            await self.telemetry_agent.start()
         if self.register_node:
-            node = make_node(self.node_name, self.node_gpus, address=self.address,
-                             activity_port=self.endpoint.port if self.endpoint else 0)
             try:
-                await self.mgr.client.create(node)
+                await self.mgr.client.create(make_node(self.node_name, self.node_gpus, address=self.address))
             except ApiError as e:
                 if not is_already_exists(e):
                     raise
-                if self.endpoint is not None:
-                    await self.mgr.client.patch(kinds.NODE, {"metadata": {"annotations": {
-                        "amd.com/gpu-activity-port": str(self.endpoint.port)}}}, name=self.node_name)
 
     async def stop(self) -> None:
         for g in self.runtimes:
             await g.close()
-        if self.endpoint is not None:
-            await self.endpoint.stop()
+        if self.telemetry_agent is not None:
+            await self.telemetry_agent.stop()
+        if self._tmp is not None:
+            self._tmp.cleanup()
+            self._tmp = None
 
     @property
     def probe_results(self) -> List[dict]:
         return [p for g in self.runtimes for p in g.probe_results]
+

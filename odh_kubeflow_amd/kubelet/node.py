@@ -1,4 +1,9 @@
-"""Fake node: scheduler + ``amd.com/gpu`` device manager + per-GPU container runtimes.
+"""Fake node (TEST HARNESS ONLY — never deployed): scheduler + ``amd.com/gpu`` device
+manager + per-GPU container runtimes, standing in for kube-scheduler, the kubelet and the
+AMD device plugin the way envtest stands in for kube-apiserver.
+
+The production node-side component is :mod:`odh_kubeflow_amd.nodeagent` (read-only
+telemetry + pod→GPU attribution); the shipped DaemonSet runs that, not this module.
 
 The split follows the MI355X rule "one process per GPU":
 
@@ -12,6 +17,12 @@ The split follows the MI355X rule "one process per GPU":
   multi-GPU bench).  It watches pods allocated to its device(s), runs the container
   runtime — by default an in-process Jupyter-API notebook server plus an MI355X
   start-up probe (HIP kernels, see ``ops/``) — and reports pod status.
+* :class:`FakeDeviceManager` records each allocation where a real kubelet does — the
+  device-manager checkpoint file and the pod-resources gRPC API — with the PCI-address
+  device IDs the AMD device plugin advertises, so the production node agent attributes
+  GPUs to pods through exactly the code path it uses on a real node.  (The
+  ``amd.com/gpu-ids`` annotation is internal to this fake scheduler/kubelet pair; no
+  production component reads it.)
 """
 
 from __future__ import annotations
@@ -50,8 +61,7 @@ NODE_LABELS_MI355X = {
 }
 
 
-def make_node(name: str, gpus: int = 8, cpu: str = "256", memory: str = "3Ti", address: str = "127.0.0.1",
-              activity_port: int = 0) -> dict:
+def make_node(name: str, gpus: int = 8, cpu: str = "256", memory: str = "3Ti", address: str = "127.0.0.1") -> dict:
     cap = {"cpu": cpu, "memory": memory, "pods": "250", GPU_RESOURCE: str(gpus)}
     labels = {"kubernetes.io/hostname": name, "kubernetes.io/os": "linux", **NODE_LABELS_MI355X}
     node = {
@@ -63,8 +73,6 @@ def make_node(name: str, gpus: int = 8, cpu: str = "256", memory: str = "3Ti", a
                    "conditions": [{"type": "Ready", "status": "True", "reason": "KubeletReady",
                                    "lastHeartbeatTime": rfc3339(), "lastTransitionTime": rfc3339()}],
                    "daemonEndpoints": {"kubeletEndpoint": {"Port": 10250}}}}
-    if activity_port:
-        node["metadata"]["annotations"]["amd.com/gpu-activity-port"] = str(activity_port)
     return node
 
 
@@ -289,6 +297,38 @@ class FakeContainerRuntime(ContainerRuntime):
 StartupProbe = Callable[[Sequence[int]], Awaitable[dict]]
 
 
+class FakeDeviceManager:
+    """kubelet device-manager stand-in: publishes allocations through the device-plugin
+    checkpoint (:class:`~odh_kubeflow_amd.nodeagent.checkpoint.CheckpointWriter`) and/or a
+    pod-resources gRPC server (:class:`~odh_kubeflow_amd.nodeagent.podresources.FakePodResourcesServer`).
+
+    ``device_id_of(index)`` gives the device-plugin ID of node GPU ``index`` (the PCI
+    address; :func:`~odh_kubeflow_amd.ops.telemetry.fake_bdf` for synthetic sysfs trees).
+    """
+
+    def __init__(self, device_id_of: Callable[[int], str], checkpoint=None, pod_resources=None):
+        self.device_id_of = device_id_of
+        self.checkpoint = checkpoint
+        self.pod_resources = pod_resources
+
+    def allocate(self, pod: dict, devices: Sequence[int]) -> None:
+        containers = (pod.get("spec") or {}).get("containers") or [{}]
+        cname = next((c.get("name", "") for c in containers
+                      if ((c.get("resources") or {}).get("limits") or {}).get(GPU_RESOURCE)),
+                     containers[0].get("name", ""))
+        ids = [self.device_id_of(d) for d in devices]
+        if self.checkpoint is not None:
+            self.checkpoint.allocate(m.uid(pod), cname, ids)
+        if self.pod_resources is not None:
+            self.pod_resources.assign(m.namespace(pod), m.name(pod), cname, GPU_RESOURCE, ids)
+
+    def release(self, uid: str, namespace: str, name: str) -> None:
+        if self.checkpoint is not None:
+            self.checkpoint.release(uid)
+        if self.pod_resources is not None:
+            self.pod_resources.release(namespace, name)
+
+
 class GpuRuntime:
     """Per-GPU kubelet half: runs pods allocated to ``devices`` on ``node_name``.
 
@@ -300,7 +340,8 @@ class GpuRuntime:
 
     def __init__(self, client, reader, recorder, node_name: str, devices: Optional[Iterable[int]],
                  runtime: Optional[ContainerRuntime] = None, startup_probe: Optional[StartupProbe] = None,
-                 owns_cpu_pods: bool = True, host_ip: str = "127.0.0.1"):
+                 owns_cpu_pods: bool = True, host_ip: str = "127.0.0.1",
+                 device_manager: Optional[FakeDeviceManager] = None):
         self.client = client
         self.reader = reader
         self.recorder = recorder
@@ -310,6 +351,7 @@ class GpuRuntime:
         self.startup_probe = startup_probe
         self.owns_cpu_pods = owns_cpu_pods
         self.host_ip = host_ip
+        self.device_manager = device_manager
         self.handles: Dict[str, ContainerHandle] = {}
         self.started = 0
         self.probe_results: List[dict] = []
@@ -332,12 +374,12 @@ class GpuRuntime:
         if pod is None or m.is_deleting(pod):
             if h is not None:
                 self.handles.pop(key, None)
-                await self.runtime.stop(h)
+                await self._stop(h, req)
             return Result()
         if h is not None and h.info.get("uid") != m.uid(pod):
             # same name, new incarnation (restart annotation / rolling update)
             self.handles.pop(key, None)
-            await self.runtime.stop(h)
+            await self._stop(h, req)
             h = None
         if not self._mine(pod):
             return Result()
@@ -355,6 +397,8 @@ class GpuRuntime:
                 return Result(requeue_after=5.0)
         h = await self.runtime.start(pod, devices)
         h.info["uid"] = m.uid(pod)
+        if devices and self.device_manager is not None:
+            self.device_manager.allocate(pod, devices)
         if probe is not None:
             h.info["probe"] = probe
         self.handles[key] = h
@@ -363,6 +407,11 @@ class GpuRuntime:
         self.recorder.event(pod, "Normal", "Started", "Started container " + ",".join(
             c.get("name", "") for c in (pod.get("spec") or {}).get("containers") or []))
         return Result()
+
+    async def _stop(self, h: ContainerHandle, req: Request) -> None:
+        if h.devices and self.device_manager is not None:
+            self.device_manager.release(h.info.get("uid", ""), req.namespace, req.name)
+        await self.runtime.stop(h)
 
     async def _set_status(self, pod: dict, ready: bool, handle: Optional[ContainerHandle] = None,
                           reason: str = "", message: str = "", probe: Optional[dict] = None) -> None:

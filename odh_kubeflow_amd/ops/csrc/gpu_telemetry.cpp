@@ -46,6 +46,8 @@ struct Device {
   int render_minor = -1;
   uint64_t unique_id = 0;
   uint64_t location_id = 0;
+  int domain = 0;          // PCI domain (KFD `domain` property)
+  int64_t gpu_id = 0;      // KFD gpu_id: the suffix of /sys/class/kfd/kfd/proc/<pid>/vram_<gpu_id>
   int physical = -1;       // index of the first device sharing unique_id
   int64_t vram_total = -1;
   std::string dev_dir;
@@ -97,6 +99,7 @@ void parse_properties(const std::string& path, Device* d, int64_t* simd_count) {
     else if (key == "drm_render_minor") d->render_minor = (int)val;
     else if (key == "unique_id") d->unique_id = val;
     else if (key == "location_id") d->location_id = val;
+    else if (key == "domain") d->domain = (int)val;
   }
 }
 
@@ -130,6 +133,47 @@ void sampler(Telemetry* t) {
   }
 }
 
+// Pod UID from the text of /proc/<pid>/cgroup.  The kubelet names pod cgroups after the pod
+// UID, with '_' for '-' under the systemd driver:
+//   v2/systemd  0::/kubepods.slice/kubepods-burstable.slice/kubepods-burstable-pod1b2c..._9f.slice/cri-containerd-<id>.scope
+//   v1/cgroupfs 12:memory:/kubepods/besteffort/pod1b2c...-9f/<id>
+//   guaranteed  0::/kubepods.slice/kubepods-pod1b2c..._9f.slice/...
+bool pod_uid_from_cgroup(const std::string& text, std::string* uid) {
+  static const int dash_at[4] = {8, 13, 18, 23};
+  for (size_t p = text.find("pod"); p != std::string::npos; p = text.find("pod", p + 1)) {
+    const size_t b = p + 3;
+    if (b + 36 > text.size()) break;
+    bool ok = true;
+    std::string u(36, '-');
+    for (int i = 0; i < 36 && ok; ++i) {
+      const char c = text[b + i];
+      const bool sep = i == dash_at[0] || i == dash_at[1] || i == dash_at[2] || i == dash_at[3];
+      if (sep) {
+        ok = c == '-' || c == '_';
+      } else {
+        ok = (c >= '0' && c <= '9') || (c >= 'a' && c <= 'f');
+        u[i] = c;
+      }
+    }
+    if (ok) {
+      *uid = u;
+      return true;
+    }
+  }
+  return false;
+}
+
+std::string read_text(const std::string& path, size_t limit = 1 << 16) {
+  std::string out;
+  FILE* f = std::fopen(path.c_str(), "r");
+  if (!f) return out;
+  char buf[4096];
+  size_t n;
+  while (out.size() < limit && (n = std::fread(buf, 1, sizeof(buf), f)) > 0) out.append(buf, n);
+  std::fclose(f);
+  return out;
+}
+
 }  // namespace
 
 extern "C" {
@@ -138,10 +182,11 @@ struct odh_tel_info {
   int node;
   int render_minor;
   int physical;
-  int reserved;
+  int domain;
   uint64_t unique_id;
   uint64_t location_id;
   int64_t vram_total;
+  int64_t gpu_id;
 };
 
 struct odh_tel_sample {
@@ -185,6 +230,7 @@ void* odh_tel_open(const char* root) {
     }
     d->dev_dir = t->root + "/class/drm/renderD" + std::to_string(d->render_minor) + "/device";
     int64_t v;
+    if (read_i64(nodes + "/" + std::to_string(id) + "/gpu_id", &v)) d->gpu_id = v;
     d->vram_total = read_i64(d->dev_dir + "/mem_info_vram_total", &v) ? v : -1;
     d->physical = (int)t->devs.size();
     for (size_t i = 0; i < t->devs.size(); ++i)
@@ -206,10 +252,11 @@ int odh_tel_info_get(void* h, int idx, odh_tel_info* out) {
   out->node = d->node;
   out->render_minor = d->render_minor;
   out->physical = d->physical;
-  out->reserved = 0;
+  out->domain = d->domain;
   out->unique_id = d->unique_id;
   out->location_id = d->location_id;
   out->vram_total = d->vram_total;
+  out->gpu_id = d->gpu_id;
   return 0;
 }
 
@@ -305,6 +352,48 @@ void odh_tel_close(void* h) {
   odh_tel_stop(h);
   for (Device* d : t->devs) delete d;
   delete t;
+}
+
+// Per-process GPU memory from KFD joined with the process's pod, for pod -> GPU attribution
+// on a real node (no pod annotation involved):
+//   <sys_root>/class/kfd/kfd/proc/<pid>/vram_<gpu_id>   bytes of VRAM the process holds on that GPU
+//   <proc_root>/<pid>/cgroup                              -> pod UID (see pod_uid_from_cgroup)
+// Writes one line per (pid, gpu_id) with a readable vram file: "pid gpu_id vram_bytes pod_uid\n"
+// (pod_uid "-" when the process is not in a pod cgroup).  Returns the number of bytes the
+// full report needs; the report is written only if it fits in `cap` (else call again).
+int64_t odh_tel_kfd_procs(void* h, const char* proc_root, char* buf, int64_t cap) {
+  Telemetry* t = (Telemetry*)h;
+  if (!t) return -1;
+  const std::string kfd = t->root + "/class/kfd/kfd/proc";
+  const std::string proc = proc_root && *proc_root ? proc_root : "/proc";
+  std::string report;
+  DIR* dir = opendir(kfd.c_str());
+  if (!dir) return 0;
+  std::vector<std::string> pids;
+  while (dirent* e = readdir(dir))
+    if (e->d_name[0] >= '0' && e->d_name[0] <= '9') pids.emplace_back(e->d_name);
+  closedir(dir);
+  std::sort(pids.begin(), pids.end());
+  for (const std::string& pid : pids) {
+    const std::string pdir = kfd + "/" + pid;
+    DIR* pd = opendir(pdir.c_str());
+    if (!pd) continue;  // the process exited between the two readdirs
+    std::string uid;
+    bool have_uid = false, looked = false;
+    while (dirent* e = readdir(pd)) {
+      if (std::strncmp(e->d_name, "vram_", 5) != 0) continue;
+      int64_t bytes;
+      if (!read_i64(pdir + "/" + e->d_name, &bytes)) continue;
+      if (!looked) {
+        have_uid = pod_uid_from_cgroup(read_text(proc + "/" + pid + "/cgroup"), &uid);
+        looked = true;
+      }
+      report += pid + " " + (e->d_name + 5) + " " + std::to_string(bytes) + " " + (have_uid ? uid : "-") + "\n";
+    }
+    closedir(pd);
+  }
+  if ((int64_t)report.size() <= cap && buf) std::memcpy(buf, report.data(), report.size());
+  return (int64_t)report.size();
 }
 
 }  // extern "C"

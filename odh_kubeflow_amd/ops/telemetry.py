@@ -21,8 +21,8 @@ TEL_LIB = "libodh_gpu_telemetry.so"
 
 class _Info(ctypes.Structure):
     _fields_ = [("node", ctypes.c_int), ("render_minor", ctypes.c_int), ("physical", ctypes.c_int),
-                ("reserved", ctypes.c_int), ("unique_id", ctypes.c_uint64), ("location_id", ctypes.c_uint64),
-                ("vram_total", ctypes.c_int64)]
+                ("domain", ctypes.c_int), ("unique_id", ctypes.c_uint64), ("location_id", ctypes.c_uint64),
+                ("vram_total", ctypes.c_int64), ("gpu_id", ctypes.c_int64)]
 
 
 class _Sample(ctypes.Structure):
@@ -45,6 +45,23 @@ class DeviceInfo:
     unique_id: int
     location_id: int
     vram_total: int
+    domain: int = 0
+    gpu_id: int = 0
+
+    @property
+    def pci_bdf(self) -> str:
+        """``dddd:bb:dd.f`` — the device ID the AMD device plugin advertises for a whole GPU
+        (KFD ``location_id`` = bus << 8 | device << 3 | function)."""
+        loc = self.location_id
+        return f"{self.domain:04x}:{(loc >> 8) & 0xFF:02x}:{(loc >> 3) & 0x1F:02x}.{loc & 0x7:x}"
+
+
+@dataclass
+class KfdProcess:
+    pid: int
+    gpu_id: int
+    vram_bytes: int
+    pod_uid: Optional[str]
 
 
 @dataclass
@@ -84,6 +101,8 @@ def _load():
         lib.odh_tel_stop.restype = None
         lib.odh_tel_close.argtypes = [vp]
         lib.odh_tel_close.restype = None
+        lib.odh_tel_kfd_procs.argtypes = [vp, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int64]
+        lib.odh_tel_kfd_procs.restype = ctypes.c_int64
         _lib = lib
     return _lib
 
@@ -103,7 +122,22 @@ class Telemetry:
             inf = _Info()
             self._lib.odh_tel_info_get(self._h, i, ctypes.byref(inf))
             out.append(DeviceInfo(i, inf.node, inf.render_minor, inf.physical, inf.unique_id, inf.location_id,
-                                  inf.vram_total))
+                                  inf.vram_total, inf.domain, inf.gpu_id))
+        return out
+
+    def kfd_processes(self, proc_root: str = "/proc") -> List[KfdProcess]:
+        """Processes holding GPU memory, from KFD's per-process sysfs, with their pod UID."""
+        cap = 1 << 16
+        while True:
+            buf = ctypes.create_string_buffer(cap)
+            need = self._lib.odh_tel_kfd_procs(self._h, proc_root.encode(), buf, cap)
+            if need <= cap:
+                break
+            cap = int(need) + 4096
+        out = []
+        for line in buf.raw[:max(need, 0)].decode().splitlines():
+            pid, gpu_id, vram, uid = line.split()
+            out.append(KfdProcess(int(pid), int(gpu_id), int(vram), None if uid == "-" else uid))
         return out
 
     def read(self, idx: int) -> Optional[dict]:
@@ -165,7 +199,9 @@ def write_fake_sysfs(root: str, gpus: int = 8, partitions: int = 1, vram_total: 
             os.makedirs(d, exist_ok=True)
             with open(os.path.join(d, "properties"), "w") as f:
                 f.write(f"cpu_cores_count 0\nsimd_count {1024 // partitions}\ndrm_render_minor {minor}\n"
-                        f"location_id {0x1000 * (g + 1)}\nunique_id {0xABC000 + g}\n")
+                        f"location_id {0x1000 * (g + 1)}\ndomain 0\nunique_id {0xABC000 + g}\n")
+            with open(os.path.join(d, "gpu_id"), "w") as f:
+                f.write(f"{fake_gpu_id(len(minors))}\n")
             dev = os.path.join(root, "class", "drm", f"renderD{minor}", "device")
             os.makedirs(dev, exist_ok=True)
             for name, val in (("gpu_busy_percent", 0), ("mem_info_vram_used", 0),
@@ -189,3 +225,46 @@ def set_fake_counter(root: str, minor: int, busy: Optional[int] = None, vram_use
         with open(tmp, "w") as f:
             f.write(f"{vram_used}\n")
         os.replace(tmp, os.path.join(dev, "mem_info_vram_used"))
+
+
+def fake_gpu_id(index: int) -> int:
+    """KFD gpu_id of device ``index`` in :func:`write_fake_sysfs` trees (real ids are hashes)."""
+    return 40000 + 1111 * index
+
+
+def fake_bdf(gpu: int) -> str:
+    """PCI address of GPU ``gpu`` in :func:`write_fake_sysfs` trees (``location_id`` 0x1000·(g+1))."""
+    loc = 0x1000 * (gpu + 1)
+    return f"0000:{(loc >> 8) & 0xFF:02x}:{(loc >> 3) & 0x1F:02x}.{loc & 0x7:x}"
+
+
+def set_fake_kfd_process(sys_root: str, proc_root: str, pid: int, vram_by_gpu_id: dict,
+                         pod_uid: Optional[str] = None, systemd: bool = True) -> None:
+    """A process holding VRAM (``/sys/class/kfd/kfd/proc/<pid>/vram_<gpu_id>``) inside the pod
+    cgroup of ``pod_uid`` (``/proc/<pid>/cgroup``, systemd or cgroupfs naming)."""
+    d = os.path.join(sys_root, "class", "kfd", "kfd", "proc", str(pid))
+    os.makedirs(d, exist_ok=True)
+    with open(os.path.join(d, "pasid"), "w") as f:
+        f.write(f"{32768 + pid}\n")
+    for gid, b in vram_by_gpu_id.items():
+        with open(os.path.join(d, f"vram_{gid}"), "w") as f:
+            f.write(f"{b}\n")
+    p = os.path.join(proc_root, str(pid))
+    os.makedirs(p, exist_ok=True)
+    if pod_uid is None:
+        line = "0::/system.slice/some-daemon.service\n"
+    elif systemd:
+        u = pod_uid.replace("-", "_")
+        line = (f"0::/kubepods.slice/kubepods-burstable.slice/kubepods-burstable-pod{u}.slice/"
+                f"cri-containerd-{pid:064x}.scope\n")
+    else:
+        line = f"12:memory:/kubepods/besteffort/pod{pod_uid}/{pid:064x}\n"
+    with open(os.path.join(p, "cgroup"), "w") as f:
+        f.write(line)
+
+
+def remove_fake_kfd_process(sys_root: str, proc_root: str, pid: int) -> None:
+    import shutil
+
+    shutil.rmtree(os.path.join(sys_root, "class", "kfd", "kfd", "proc", str(pid)), ignore_errors=True)
+    shutil.rmtree(os.path.join(proc_root, str(pid)), ignore_errors=True)

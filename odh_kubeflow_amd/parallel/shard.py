@@ -82,7 +82,7 @@ class ControlPlaneShard:
     async def start(self) -> "ControlPlaneShard":
         from ..controllers.notebook import NotebookEventReemitter, NotebookReconciler
         from ..controllers.metrics import NotebookMetrics
-        from ..kubelet.agent import NodeAgent
+        from ..kubelet.agent import FakeKubeletAgent
         from ..kubelet.node import GPU_AFFINITY_LABEL, GPU_INDEX_LABEL, SchedulerController
         from ..kubelet.statefulset import StatefulSetController
         from ..runtime.informer import InformerCache
@@ -121,7 +121,7 @@ class ControlPlaneShard:
         if schedules:
             SchedulerController(kl.client, kl.reader, kl.get_event_recorder_for("default-scheduler")) \
                 .setup_with_manager(kl)
-        self.agent = NodeAgent(kl, cfg.node_name, [cfg.gpu], node_gpus=cfg.node_gpus,
+        self.agent = FakeKubeletAgent(kl, cfg.node_name, [cfg.gpu], node_gpus=cfg.node_gpus,
                                startup_probe=cfg.startup_probe, register_node=cfg.bootstrap,
                                owns_cpu_pods=schedules)
 

@@ -174,24 +174,47 @@ def test_culler_no_data_never_culls(run, clock):
     run(go(), timeout=60)
 
 
+def _gpu_of_pods(cl, tel, ns, names):
+    """telemetry index of each notebook's GPU, read back the way the node agent reads it:
+    the fake kubelet's device-plugin checkpoint (PCI addresses), resolved via the KFD topology."""
+    from odh_kubeflow_amd.nodeagent.attribution import DeviceResolver
+    from odh_kubeflow_amd.nodeagent.checkpoint import read_checkpoint
+
+    cp = read_checkpoint(cl.device_managers["mi355x-node-0"].checkpoint.path)
+    res = DeviceResolver(tel.devices())
+    out = {}
+    for n in names:
+        ids = cp[m.uid(cl.store.peek(kinds.POD, f"{n}-0", ns))]
+        out[n] = res.resolve(ids[0])[0]
+    return out
+
+
 def test_culler_amdgpu_signal(run, clock, tmp_path):
+    """GPU-busy culling through the production node agent: no pod carries an
+    ``amd.com/gpu-ids`` annotation the culler could read; the agent attributes GPUs from
+    the (fake) kubelet's device-plugin checkpoint and the culler asks it by pod UID."""
     from odh_kubeflow_amd.ops.telemetry import Telemetry, set_fake_counter, write_fake_sysfs
 
     minors = write_fake_sysfs(str(tmp_path), gpus=8)
     tel = Telemetry(str(tmp_path)).start(interval_ms=10, capacity=2000)
     rt = JupyterContainerRuntime()
-    src = c.LocalTelemetryActivity(tel)
 
     async def go():
         cfg = _cfg(rt, CULLING_ACTIVITY_SOURCE="amdgpu", IDLENESS_CHECK_PERIOD_SECONDS="0.2")
-        cfg.activity_source = src
+        cfg.telemetry = tel
         async with LocalCluster(cfg) as cl:
+            culler = cl.reconcilers["culler"]
+            assert isinstance(culler.gpu, c.NodeAgentActivity)
             await cl.ensure_namespace("user")
             await cl.admin.create(notebook("train", "user", gpus=1))
             assert await cl.wait_for(lambda: cl.notebook_ready("train", "user"))
             await cl.admin.create(notebook("idle", "user", gpus=1))
             assert await cl.wait_for(lambda: cl.notebook_ready("idle", "user"))
-            gid = {n: c.pod_gpu_ids(cl.store.peek(kinds.POD, f"{n}-0", "user"))[0] for n in ("train", "idle")}
+            for n in ("train", "idle"):  # strip the fake scheduler's internal annotation
+                pod = cl.store.peek(kinds.POD, f"{n}-0", "user")
+                await cl.admin.patch(kinds.POD, {"metadata": {"annotations": {"amd.com/gpu-ids": None}}},
+                                     name=m.name(pod), namespace="user")
+            gid = _gpu_of_pods(cl, tel, "user", ("train", "idle"))
             assert gid["train"] != gid["idle"]
             # "train" runs an MI355X job: its GPU is 97% busy; no kernel is busy in Jupyter
             set_fake_counter(str(tmp_path), minors[gid["train"]], busy=97)
@@ -203,6 +226,8 @@ def test_culler_amdgpu_signal(run, clock, tmp_path):
             assert await cl.wait_for(lambda: STOP_ANNOTATION in m.annotations(
                 cl.store.peek(kinds.NOTEBOOK, "idle", "user")), 10)
             assert STOP_ANNOTATION not in m.annotations(cl.store.peek(kinds.NOTEBOOK, "train", "user"))
+            agent = cl.node_agents["mi355x-node-0"]
+            assert agent.attributed_queries > 0 and culler.gpu.requests > 0
             # the job ends: GPU idle → culled after the idle time
             set_fake_counter(str(tmp_path), minors[gid["train"]], busy=0)
             await asyncio.sleep(0.5)
@@ -213,3 +238,15 @@ def test_culler_amdgpu_signal(run, clock, tmp_path):
         run(go(), timeout=60)
     finally:
         tel.close()
+
+
+def test_gpu_says_active_vram_policy():
+    cfg = c.CullerConfig.from_env({})
+    assert cfg.gpu_vram_active_bytes == 0 and cfg.gpu_agent_port == 9464
+    held = {"n": 5, "busy_mean": 0.0, "busy_max": 0, "pod_vram_bytes": 200 * 10 ** 9}
+    assert not c.gpu_says_active(held, cfg)  # default: resident HBM alone is not activity
+    assert c.gpu_says_active({**held, "busy_mean": 40.0}, cfg)
+    cfg = c.CullerConfig.from_env({"CULLING_GPU_VRAM_ACTIVE_BYTES": "1e9"})
+    assert c.gpu_says_active(held, cfg)
+    assert not c.gpu_says_active({**held, "pod_vram_bytes": 10 ** 6}, cfg)
+    assert not c.gpu_says_active({**held, "pod_vram_bytes": None}, cfg)

@@ -1,0 +1,317 @@
+"""Production node agent (``nodeagent/``, ``cmd/node_agent.py``): pod→GPU attribution from the
+kubelet pod-resources API, the device-plugin checkpoint and KFD per-process sysfs; its HTTP
+API; GPU-busy culling through it with no ``amd.com/gpu-ids`` on any pod; and the guarantee
+that the shipped agent never writes to the apiserver.
+
+Replaces the fake-scheduler annotation lookup the round-1 culler used; the reference signal
+being replaced is ``kf/controllers/culling_controller.go:161-196,243-273``."""
+
+import asyncio
+import json
+import os
+import signal
+import socket
+import subprocess
+import sys
+import time
+import urllib.request
+
+import pytest
+
+from odh_kubeflow_amd.nodeagent import podresources as pr
+from odh_kubeflow_amd.nodeagent.attribution import Attributor, DeviceResolver
+from odh_kubeflow_amd.nodeagent.checkpoint import CheckpointWriter, read_checkpoint
+from odh_kubeflow_amd.nodeagent.server import NodeTelemetryAgent
+from odh_kubeflow_amd.ops.telemetry import (Telemetry, fake_bdf, fake_gpu_id, set_fake_counter, set_fake_kfd_process,
+                                            write_fake_sysfs)
+
+UID_A = "0d6f2a50-1c9e-4f0e-9a53-2b7c8d9e0f11"
+UID_B = "7e1c3b2a-9d8f-4e6a-b5c4-3a2b1c0d9e8f"
+
+
+@pytest.fixture
+def sysfs(tmp_path):
+    root = str(tmp_path / "sys")
+    proc = str(tmp_path / "proc")
+    os.makedirs(proc)
+    minors = write_fake_sysfs(root, gpus=8)
+    tel = Telemetry(root).start(interval_ms=10, capacity=1000)
+    yield root, proc, minors, tel
+    tel.close()
+
+
+def test_podresources_codec_roundtrip():
+    pods = [pr.PodResources("nb-0", "user", [pr.ContainerResources("nb", [
+        pr.ContainerDevices("amd.com/gpu", ["0000:10:00.0", "0000:20:00.0"]),
+        pr.ContainerDevices("example.com/nic", ["eth9"])])]), pr.PodResources("cpu-0", "user", [])]
+    back = pr.decode_list_response(pr.encode_list_response(pods))
+    assert back == pods
+    assert back[0].device_ids("amd.com/gpu") == ["0000:10:00.0", "0000:20:00.0"]
+    # unknown fields (cpu_ids as packed varints, topology) are skipped
+    extra = pr._ld(1, pr._s(1, "x") + pr._s(2, "ns") + pr._ld(3, pr._s(1, "c") + pr._ld(3, b"\x01\x02")
+                                                        + pr._varint(4 << 3 | 0) + pr._varint(300)))
+    assert pr.decode_list_response(extra)[0].containers[0].name == "c"
+
+
+def test_podresources_grpc_list(tmp_path):
+    sock = str(tmp_path / "kubelet.sock")
+    srv = pr.FakePodResourcesServer(sock).start()
+    try:
+        srv.assign("user", "nb-0", "nb", "amd.com/gpu", [fake_bdf(3)])
+        cli = pr.PodResourcesClient(sock)
+        assert cli.available()
+        got = asyncio.run(cli.list())
+        assert [(p.namespace, p.name, p.device_ids("amd.com/gpu")) for p in got] == [("user", "nb-0", [fake_bdf(3)])]
+        cli.close()
+    finally:
+        srv.stop()
+
+
+def test_checkpoint_shapes(tmp_path):
+    path = str(tmp_path / "kubelet_internal_checkpoint")
+    with open(path, "w") as f:
+        json.dump({"Data": {"PodDeviceEntries": [
+            {"PodUID": UID_A, "ContainerName": "a", "ResourceName": "amd.com/gpu", "DeviceIDs": {"1": [fake_bdf(2)],
+                                                                                                 "0": [fake_bdf(1)]}},
+            {"PodUID": UID_B, "ContainerName": "b", "ResourceName": "amd.com/gpu", "DeviceIDs": [fake_bdf(5)]},
+            {"PodUID": UID_B, "ContainerName": "b", "ResourceName": "nvidia.com/gpu", "DeviceIDs": ["GPU-x"]}],
+            "RegisteredDevices": {}}, "Checksum": 1}, f)
+    assert read_checkpoint(path) == {UID_A: [fake_bdf(1), fake_bdf(2)], UID_B: [fake_bdf(5)]}
+    assert read_checkpoint(str(tmp_path / "missing")) is None
+    w = CheckpointWriter(str(tmp_path / "dp" / "cp"))
+    w.allocate(UID_A, "nb", [fake_bdf(0)])
+    assert read_checkpoint(w.path) == {UID_A: [fake_bdf(0)]}
+    w.release(UID_A)
+    assert read_checkpoint(w.path) == {}
+
+
+def test_device_resolver_bdf_partitions(tmp_path):
+    write_fake_sysfs(str(tmp_path), gpus=2, partitions=4)  # CPX-style: 4 KFD nodes per MI355X
+    tel = Telemetry(str(tmp_path))
+    try:
+        res = DeviceResolver(tel.devices())
+        assert res.resolve(fake_bdf(1)) == [4, 5, 6, 7]
+        assert res.resolve(fake_bdf(1).upper()) == [4, 5, 6, 7]
+        assert res.resolve(fake_bdf(1)[5:]) == [4, 5, 6, 7]  # domain omitted
+        assert res.resolve("renderD129") == [1] and res.resolve("card2") == [2] and res.resolve("3") == [3]
+        assert res.resolve("0000:99:00.0") == [] and res.resolve("GPU-uuid") == []
+    finally:
+        tel.close()
+
+
+def test_attribution_sources(run, sysfs, tmp_path):
+    root, proc, _minors, tel = sysfs
+    sock = str(tmp_path / "pr.sock")
+    srv = pr.FakePodResourcesServer(sock).start()
+    cp = CheckpointWriter(str(tmp_path / "dp" / "kubelet_internal_checkpoint"))
+    try:
+        srv.assign("user", "a-0", "a", "amd.com/gpu", [fake_bdf(0)])
+        cp.allocate(UID_B, "b", [fake_bdf(6), "0000:99:00.0"])
+        set_fake_kfd_process(root, proc, 4242, {fake_gpu_id(3): 5 << 30}, UID_A, systemd=True)
+        set_fake_kfd_process(root, proc, 4243, {fake_gpu_id(3): 1 << 30, fake_gpu_id(0): 7}, UID_A, systemd=False)
+        set_fake_kfd_process(root, proc, 99, {fake_gpu_id(1): 1 << 20})  # host daemon, no pod
+
+        async def go():
+            att = Attributor(tel, pod_resources=pr.PodResourcesClient(sock), checkpoint_path=cp.path,
+                             proc_root=proc, ttl_s=0.0)
+            a = await att.lookup(UID_A, "user", "a-0")
+            assert a.devices == [0, 3] and set(a.sources) == {"podresources", "kfd"}
+            assert a.vram_bytes == {3: 6 << 30, 0: 7} and a.pod_vram_bytes == (6 << 30) + 7
+            b = await att.lookup(UID_B, "user", "b-0")
+            assert b.devices == [6] and b.sources == ["checkpoint"] and b.pod_vram_bytes is None
+            assert await att.lookup("no-such-uid", "user", "c-0") is None
+            tables = await att.all_pods()
+            assert tables["sources"] == {"podresources": "ok", "checkpoint": "ok", "kfd": "ok"}
+            assert tables["unresolved_device_ids"] == ["0000:99:00.0"]
+            # a source that fails is reported, the others still answer
+            att2 = Attributor(tel, pod_resources=pr.PodResourcesClient(str(tmp_path / "nope.sock"), timeout_s=0.2),
+                              checkpoint_path=cp.path, ttl_s=0.0)
+            assert (await att2.lookup(UID_B)).devices == [6]
+            assert (await att2.all_pods())["sources"]["podresources"].startswith("error")
+        run(go())
+    finally:
+        srv.stop()
+
+
+def _get(url):
+    with urllib.request.urlopen(url, timeout=5) as r:
+        return r.status, r.read().decode()
+
+
+def test_agent_http_api(run, sysfs, tmp_path):
+    root, proc, minors, tel = sysfs
+    cp = CheckpointWriter(str(tmp_path / "dp" / "cp"))
+    cp.allocate(UID_A, "nb", [fake_bdf(2)])
+    set_fake_kfd_process(root, proc, 777, {fake_gpu_id(2): 3 << 30}, UID_A)
+    set_fake_counter(root, minors[2], busy=80, vram_used=50 << 30)
+
+    async def go():
+        agent = await NodeTelemetryAgent(tel, Attributor(tel, checkpoint_path=cp.path, proc_root=proc, ttl_s=0.0),
+                                         host="127.0.0.1", port=0).start()
+        try:
+            await asyncio.sleep(0.1)
+            base = f"http://127.0.0.1:{agent.port}"
+            st, body = await asyncio.to_thread(_get, f"{base}/gpu/activity?pod_uid={UID_A}&window=0.05")
+            d = json.loads(body)
+            assert st == 200 and d["attributed"] and d["devices"] == [fake_bdf(2)]
+            assert d["busy_mean"] == 80 and d["n"] > 0 and d["pod_vram_bytes"] == 3 << 30
+            d = json.loads((await asyncio.to_thread(_get, f"{base}/gpu/activity?pod_uid={UID_B}&window=5"))[1])
+            assert d == {"attributed": False, "n": 0}
+            pods = json.loads((await asyncio.to_thread(_get, f"{base}/gpu/pods"))[1])
+            assert pods["by_uid"] == {UID_A: [2]} and pods["kfd_vram_bytes"] == {UID_A: {"2": 3 << 30}}
+            devs = json.loads((await asyncio.to_thread(_get, f"{base}/gpu/devices"))[1])
+            assert [x["pci_bdf"] for x in devs] == [fake_bdf(i) for i in range(8)]
+            metrics = (await asyncio.to_thread(_get, f"{base}/metrics"))[1]
+            assert f'amdgpu_busy_percent{{gpu="2",bdf="{fake_bdf(2)}",render_minor="{minors[2]}"}} 80' in metrics
+            with pytest.raises(urllib.error.HTTPError):
+                await asyncio.to_thread(_get, f"{base}/gpu/activity?window=5")
+        finally:
+            await agent.stop()
+    run(go())
+
+
+def test_culler_kfd_attribution_only(run, sysfs):
+    """No checkpoint, no pod-resources, no annotation: the agent finds each notebook's GPU from
+    the processes in its pod cgroup (KFD), culls the idle GPU notebook, keeps the busy one."""
+    from odh_kubeflow_amd.cluster import ClusterConfig, LocalCluster
+    from odh_kubeflow_amd.controllers import culling as c
+    from odh_kubeflow_amd.models import kinds
+    from odh_kubeflow_amd.models import meta as m
+    from odh_kubeflow_amd.models.notebook import STOP_ANNOTATION, notebook
+    from odh_kubeflow_amd.utils import timeutil
+
+    root, proc, minors, tel = sysfs
+    offset = [0.0]
+    timeutil.set_clock(lambda: time.time() + offset[0])
+
+    async def go():
+        agent = await NodeTelemetryAgent(tel, Attributor(tel, proc_root=proc, ttl_s=0.0), host="127.0.0.1",
+                                         port=0).start()
+        # production defaults: <pod.status.hostIP>:<CULLING_GPU_AGENT_PORT>
+        env = {"ENABLE_CULLING": "true", "CULL_IDLE_TIME": "60", "IDLENESS_CHECK_PERIOD_SECONDS": "0.2",
+               "CULLING_ACTIVITY_SOURCE": "amdgpu", "CULLING_GPU_AGENT_PORT": str(agent.port),
+               "CLUSTER_DOMAIN": "invalid.example"}
+        try:
+            async with LocalCluster(ClusterConfig(culler=True, env=env)) as cl:
+                await cl.ensure_namespace("u")
+                for i, n in enumerate(("busy", "idle")):
+                    await cl.admin.create(notebook(n, "u", gpus=1))
+                    assert await cl.wait_for(lambda: cl.notebook_ready(n, "u"))
+                    pod = cl.store.peek(kinds.POD, f"{n}-0", "u")
+                    assert pod["status"]["hostIP"] == "127.0.0.1"
+                    # the notebook's python process holds VRAM on GPU 4+i (KFD), in the pod's cgroup
+                    set_fake_kfd_process(root, proc, 1000 + i, {fake_gpu_id(4 + i): 8 << 30}, m.uid(pod))
+                set_fake_counter(root, minors[4], busy=90)
+                culler = cl.reconcilers["culler"]
+                assert await cl.wait_for(lambda: c.annotations_exist(cl.store.peek(kinds.NOTEBOOK, "busy", "u")))
+                await asyncio.sleep(0.4)
+                offset[0] += 7200
+                assert await cl.wait_for(lambda: STOP_ANNOTATION in m.annotations(
+                    cl.store.peek(kinds.NOTEBOOK, "idle", "u")), 10)
+                assert STOP_ANNOTATION not in m.annotations(cl.store.peek(kinds.NOTEBOOK, "busy", "u"))
+                assert agent.attributed_queries >= 2 and culler.jupyter.requests == 0
+        finally:
+            await agent.stop()
+    try:
+        run(go(), timeout=60)
+    finally:
+        timeutil.set_clock(None)
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def test_shipped_agent_never_touches_the_apiserver(run, sysfs, tmp_path):
+    """``python -m odh_kubeflow_amd.cmd.node_agent`` with in-cluster env and a kubeconfig both
+    pointing at a listener that records every connection: it serves attribution and
+    telemetry, and never connects."""
+    from odh_kubeflow_amd.cmd import node_agent
+
+    root, proc, minors, _tel = sysfs
+    args = node_agent.parse([])
+    assert not hasattr(args, "master") and not hasattr(args, "kubeconfig")
+    cp = CheckpointWriter(str(tmp_path / "dp" / "cp"))
+    cp.allocate(UID_A, "nb", [fake_bdf(1)])
+    set_fake_counter(root, minors[1], busy=33)
+
+    async def go():
+        seen = []
+
+        async def record(reader, writer):
+            seen.append(await reader.read(64))
+            writer.close()
+        api = await asyncio.start_server(record, "127.0.0.1", 0)
+        aport = api.sockets[0].getsockname()[1]
+        kc = tmp_path / "kubeconfig"
+        kc.write_text(f"apiVersion: v1\nclusters: [{{name: c, cluster: {{server: 'http://127.0.0.1:{aport}'}}}}]\n"
+                      "contexts: [{name: c, context: {cluster: c, user: u}}]\ncurrent-context: c\n"
+                      "users: [{name: u, user: {token: t}}]\n")
+        port = _free_port()
+        env = {**os.environ, "KUBERNETES_SERVICE_HOST": "127.0.0.1", "KUBERNETES_SERVICE_PORT": str(aport),
+               "KUBECONFIG": str(kc)}
+        p = subprocess.Popen([sys.executable, "-m", "odh_kubeflow_amd.cmd.node_agent", "--bind", "127.0.0.1",
+                              "--port", str(port), "--sysfs-root", root, "--proc-root", proc,
+                              "--pod-resources-socket", str(tmp_path / "absent.sock"),
+                              "--device-plugin-checkpoint", cp.path, "--telemetry-interval-ms", "10"],
+                             env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT)
+        try:
+            body = None
+            for _ in range(300):
+                try:
+                    st, body = await asyncio.to_thread(
+                        _get, f"http://127.0.0.1:{port}/gpu/activity?pod_uid={UID_A}&window=0.5")
+                    if json.loads(body).get("n", 0) > 0:
+                        break
+                except OSError:
+                    pass
+                await asyncio.sleep(0.05)
+            d = json.loads(body)
+            assert d["attributed"] and d["devices"] == [fake_bdf(1)] and d["busy_mean"] == 33
+        finally:
+            p.send_signal(signal.SIGTERM)
+            out = await asyncio.to_thread(p.communicate, timeout=20)
+            api.close()
+        assert p.returncode == 0, out[0].decode()[-2000:]
+        assert seen == [], seen  # not one request, let alone a Node or pods/status write
+    run(go(), timeout=90)
+
+
+def test_shipped_manifests_have_no_kubelet_stand_in():
+    from odh_kubeflow_amd.deploy import manifests
+
+    t = manifests.tree()
+    ds = t["node-agent/daemonset.yaml"]
+    spec = ds["spec"]["template"]["spec"]
+    assert spec["automountServiceAccountToken"] is False
+    c = spec["containers"][0]
+    assert c["command"] == ["python", "-m", "odh_kubeflow_amd.cmd.node_agent"]
+    assert not any(a.startswith(("--master", "--devices", "--node-name")) for a in c["args"])
+    mounts = {v["mountPath"]: v for v in c["volumeMounts"]}
+    assert mounts["/host/sys"]["readOnly"] and mounts["/host/proc"]["readOnly"]
+    assert "/dev/kfd" not in mounts and "/dev/dri" not in mounts
+    # no RBAC at all for the agent: it cannot write a Node or pods/status
+    for path, doc in t.items():
+        for d in doc if isinstance(doc, list) else [doc]:
+            if not isinstance(d, dict):
+                continue
+            assert "mi355x-node-agent-role" not in json.dumps(d), path
+            for r in d.get("rules") or []:
+                assert "pods/status" not in r["resources"] or set(r["verbs"]) <= {"get", "list", "watch"}, path
+                if "nodes" in r["resources"]:
+                    assert set(r["verbs"]) <= {"get", "list", "watch"}, path
+    # the production agent module imports nothing from the kubelet stand-in or a k8s client
+    import odh_kubeflow_amd.cmd.node_agent as na
+    import odh_kubeflow_amd.nodeagent.server as srv
+    for mod in (na, srv):
+        import ast
+
+        tree = ast.parse(open(mod.__file__).read())
+        imported = [n.module or "" for n in ast.walk(tree) if isinstance(n, ast.ImportFrom)]
+        imported += [a.name for n in ast.walk(tree) if isinstance(n, ast.Import) for a in n.names]
+        for name in imported:
+            assert not any(x in name for x in ("kubelet", "runtime", "apiserver")), (mod.__name__, name)

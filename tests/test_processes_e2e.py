@@ -2,8 +2,11 @@
 (.github/workflows/odh_notebook_controller_integration_test.yaml:102-284): dev apiserver
 (+ StatefulSet controller / scheduler / GC), kf manager, odh manager with its HTTPS
 webhook registered through a MutatingWebhookConfiguration carrying a self-signed
-caBundle, and the MI355X node agent.  Create a notebook with inject-auth, wait for the
-pod to be Ready, delete it and check the cluster-scoped leftovers are gone."""
+caBundle, a dev kubelet stand-in (``cmd/fake_kubelet.py``, writing the device-plugin
+checkpoint) and the production MI355X node agent (``cmd/node_agent.py``, read-only).
+Create a notebook with inject-auth, wait for the pod to be Ready, check the agent
+attributes the pod's GPU from the checkpoint, delete it and check the cluster-scoped
+leftovers are gone."""
 
 import asyncio
 import os
@@ -91,8 +94,16 @@ def test_processes_end_to_end(tmp_path, run):
                                 "quay.io/brancz/kube-rbac-proxy:v0.18.1", "--webhook-cert-dir", certs.cert_dir,
                                 "--webhook-port", str(wh_port), "--webhook-host", "127.0.0.1", "--leader-elect"],
                                common, logf))
-            procs.append(spawn(["odh_kubeflow_amd.cmd.node_agent", "--master", master, "--devices",
-                                "0,1,2,3,4,5,6,7", "--sysfs-root", str(tmp_path / "nosys")], common, logf))
+            from odh_kubeflow_amd.ops.telemetry import write_fake_sysfs
+
+            sysfs, cp = str(tmp_path / "sys"), str(tmp_path / "dp" / "kubelet_internal_checkpoint")
+            write_fake_sysfs(sysfs, gpus=8)
+            agent_port = free_port()
+            procs.append(spawn(["odh_kubeflow_amd.cmd.fake_kubelet", "--master", master, "--devices",
+                                "0,1,2,3,4,5,6,7", "--sysfs-root", sysfs, "--checkpoint-path", cp], common, logf))
+            procs.append(spawn(["odh_kubeflow_amd.cmd.node_agent", "--bind", "127.0.0.1", "--port", str(agent_port),
+                                "--sysfs-root", sysfs, "--proc-root", "", "--pod-resources-socket", "",
+                                "--device-plugin-checkpoint", cp], None, logf))
             await wait_http(f"https://127.0.0.1:{wh_port}/healthz")
             await c.create(mutating_webhook_configuration(
                 certs.ca_bundle_b64, url=f"https://127.0.0.1:{wh_port}/mutate-notebook-v1"))
@@ -113,6 +124,17 @@ def test_processes_end_to_end(tmp_path, run):
             assert "kubeflow-resource-stopped" not in m.annotations(nb)
             pod = await c.get(kinds.POD, "nb-0", "user")
             assert m.annotations(pod)["amd.com/gpu-ids"] == "0"
+            import json as _json
+            import urllib.request
+
+            from odh_kubeflow_amd.ops.telemetry import fake_bdf
+
+            def activity():
+                url = f"http://127.0.0.1:{agent_port}/gpu/activity?pod_uid={m.uid(pod)}&window=5"
+                with urllib.request.urlopen(url, timeout=5) as r:
+                    return _json.loads(r.read())
+            act = await asyncio.to_thread(activity)
+            assert act["attributed"] and act["devices"] == [fake_bdf(0)] and act["sources"] == ["checkpoint"]
             routes = await c.list(kinds.HTTP_ROUTE, "opendatahub")
             assert [m.name(r) for r in routes] == ["nb-user-nb"]
             leases = {m.name(x) for x in await c.list(kinds.LEASE, "opendatahub")}
@@ -177,8 +199,8 @@ def test_processes_notebook_lifecycle_like_reference_e2e(tmp_path, run):
                                 "--health-probe-bind-address", "0", "--kube-rbac-proxy-image",
                                 "quay.io/brancz/kube-rbac-proxy:v0.18.1", "--webhook-cert-dir", certs.cert_dir,
                                 "--webhook-port", str(wh_port), "--webhook-host", "127.0.0.1"], common, logf))
-            procs.append(spawn(["odh_kubeflow_amd.cmd.node_agent", "--master", master, "--jupyter",
-                                "--sysfs-root", str(tmp_path / "nosys")], common, logf))
+            procs.append(spawn(["odh_kubeflow_amd.cmd.fake_kubelet", "--master", master, "--jupyter",
+                                "--checkpoint-path", str(tmp_path / "dp" / "cp")], common, logf))
             await wait_http(f"https://127.0.0.1:{wh_port}/healthz")
             await c.create(mutating_webhook_configuration(
                 certs.ca_bundle_b64, url=f"https://127.0.0.1:{wh_port}/mutate-notebook-v1"))

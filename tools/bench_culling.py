@@ -13,10 +13,14 @@ no GPU sample).  The notebook on GPU 0 runs a real MFMA load on the MI355X
   Jupyter kernels are idle (the reference, which only asks Jupyter, would cull it);
 * after the load stops, the GPU-0 notebook's own reclaim latency.
 
-On the GPU box the amdgpu signal comes from ``/sys`` (the native sampler; GPU 0 is
-matched to this process's visible device by PCI bus); the other seven node GPUs belong
-to other tenants of the host, so they map to "no sample" and their notebooks fall back
-to Jupyter activity.  ``--cpu`` runs the same scenario on a synthetic sysfs tree.
+The culler reaches the GPU signal the production way: the node's agent (``nodeagent/``)
+attributes GPUs to pods from the (fake) kubelet's device-plugin checkpoint, which records
+the PCI addresses of the allocated GPUs, and the culler asks it by pod UID.  On the GPU box
+the amdgpu signal comes from ``/sys`` (the native sampler); node GPU 0 carries the PCI
+address of this process's visible MI355X, the other seven node GPUs carry addresses no
+local device has (they belong to other tenants of the host), so they resolve to "no
+sample" and their notebooks fall back to Jupyter activity.  ``--cpu`` runs the same
+scenario on a synthetic sysfs tree.
 
     python tools/bench_culling.py [--cpu] [--idle-s 2] [--period-s 0.25] [--load-s 6]
 """
@@ -32,7 +36,6 @@ import time
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 from odh_kubeflow_amd.cluster import ClusterConfig, LocalCluster  # noqa: E402
-from odh_kubeflow_amd.controllers import culling as c  # noqa: E402
 from odh_kubeflow_amd.models import kinds  # noqa: E402
 from odh_kubeflow_amd.models import meta as m  # noqa: E402
 from odh_kubeflow_amd.models.notebook import STOP_ANNOTATION, notebook  # noqa: E402
@@ -42,13 +45,14 @@ N = 8
 
 
 def _telemetry(cpu: bool):
-    from odh_kubeflow_amd.ops.telemetry import Telemetry, write_fake_sysfs
+    """(telemetry, node GPU index -> device-plugin ID, sysfs root, render minors)."""
+    from odh_kubeflow_amd.ops.telemetry import Telemetry, fake_bdf, write_fake_sysfs
 
     if cpu:
         root = tempfile.mkdtemp(prefix="odh-sysfs-")
         minors = write_fake_sysfs(root, gpus=N)
         tel = Telemetry(root).start(interval_ms=20, capacity=4000)
-        return tel, {i: i for i in range(N)}, root, minors
+        return tel, fake_bdf, root, minors
     import torch
 
     from odh_kubeflow_amd.kubelet.agent import pci_bus_index_map
@@ -56,23 +60,35 @@ def _telemetry(cpu: bool):
     tel = Telemetry("/sys").start(interval_ms=20, capacity=4000)
     props = torch.cuda.get_device_properties(0)
     bus = getattr(props, "pci_bus_id", None)
-    mapping = pci_bus_index_map(tel, {0: bus}) if bus is not None else {}
-    return tel, mapping, None, None
+    idx = pci_bus_index_map(tel, {0: bus}).get(0) if bus is not None else None
+    real = tel.devices()[idx].pci_bdf if idx is not None else None
+
+    def device_id_of(i):
+        return real if i == 0 and real else f"0000:ee:{i:02x}.0"  # not a local device: "no sample"
+    return tel, device_id_of, None, None
+
+
+def _gpu_of(cl, ns, names):
+    from odh_kubeflow_amd.nodeagent.checkpoint import read_checkpoint
+
+    dm = cl.device_managers["mi355x-node-0"]
+    cp = read_checkpoint(dm.checkpoint.path)
+    ids = {dm.device_id_of(i): i for i in range(N)}
+    return {nm: ids[cp[m.uid(cl.store.peek(kinds.POD, f"{nm}-0", ns))][0]] for nm in names}
 
 
 async def run(args) -> dict:
-    tel, mapping, root, minors = _telemetry(args.cpu)
-    src = c.LocalTelemetryActivity(tel, index_of=lambda d: mapping.get(d))
+    tel, device_id_of, root, minors = _telemetry(args.cpu)
     rt = JupyterContainerRuntime()
     env = {"ENABLE_CULLING": "true", "CULL_IDLE_TIME_SECONDS": str(args.idle_s),
            "IDLENESS_CHECK_PERIOD_SECONDS": str(args.period_s), "CULLER_USE_POD_ENDPOINT": "true",
            "CULLING_ACTIVITY_SOURCE": "combined", "CULLING_GPU_BUSY_THRESHOLD": "5"}
-    cfg = ClusterConfig(culler=True, env=env, runtime_factory=lambda d: rt, activity_source=src)
+    cfg = ClusterConfig(culler=True, env=env, runtime_factory=lambda d: rt, telemetry=tel, device_id_of=device_id_of)
     load = None
     out = {"metric": "culling reclaim latency across 8 GPU notebooks", "n_notebooks": N,
            "cull_idle_time_s": args.idle_s, "idleness_check_period_s": args.period_s, "load_s": args.load_s,
            "gpu_signal": "synthetic sysfs" if args.cpu else "amdgpu sysfs (gpu_busy_percent) of the visible MI355X",
-           "gpu0_telemetry_index": mapping.get(0)}
+           "gpu0_device_id": device_id_of(0), "attribution": "node agent (device-plugin checkpoint, by pod UID)"}
     try:
         async with LocalCluster(cfg) as cl:
             await cl.ensure_namespace("cull")
@@ -81,7 +97,7 @@ async def run(args) -> dict:
                 await cl.admin.create(notebook(nm, "cull", gpus=1))
             if not await cl.wait_for(lambda: all(cl.notebook_ready(nm, "cull") for nm in names), 60):
                 raise RuntimeError("notebooks not Ready")
-            gpu_of = {nm: c.pod_gpu_ids(cl.store.peek(kinds.POD, f"{nm}-0", "cull"))[0] for nm in names}
+            gpu_of = _gpu_of(cl, "cull", names)
             busy_nb = next(nm for nm, g in gpu_of.items() if g == 0)
             t_kernels = time.time()
             for nm in names:  # every notebook has an idle kernel: Jupyter says "idle" for all of them
@@ -120,8 +136,7 @@ async def run(args) -> dict:
                 await asyncio.sleep(0.02)
             false_culls = int(busy_nb in stopped_at or STOP_ANNOTATION in m.annotations(
                 cl.store.peek(kinds.NOTEBOOK, busy_nb, "cull")))
-            gpu_busy = src.busy(None, [0], 1.0)
-            gpu_busy = await gpu_busy
+            gpu_busy = await cl.reconcilers["culler"].gpu.busy(cl.store.peek(kinds.POD, f"{busy_nb}-0", "cull"), 1.0)
             if load is not None:
                 load.stop()
                 load = None
@@ -146,6 +161,8 @@ async def run(args) -> dict:
                 # + up to 1 s of RFC3339 rounding
                 "busy_notebook_culled_after_unload_ms": round((stopped_at[busy_nb] - t_unload) * 1e3, 1),
                 "culler_checks": cl.reconcilers["culler"].checks, "culled": cl.reconcilers["culler"].culled,
+                "agent_queries": cl.node_agents["mi355x-node-0"].queries,
+                "agent_attributed_queries": cl.node_agents["mi355x-node-0"].attributed_queries,
             })
     finally:
         if load is not None:

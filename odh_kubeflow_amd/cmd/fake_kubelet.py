@@ -80,8 +80,7 @@ async def amain(argv=None) -> int:
     args = parse(argv)
     setup_logging(debug=args.debug_log)
     mgr, _agent = build(args)
-    await mgr.run_until(signal_event())
-    return 0
+    return await mgr.run_until(signal_event())
 
 
 def main(argv=None) -> int:

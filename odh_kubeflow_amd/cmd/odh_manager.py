@@ -82,8 +82,7 @@ async def amain(argv=None) -> int:
     setup_logging(debug=args.debug_log, development=args.debug_log)
     mgr = build(args)
     log.info("starting manager")
-    await mgr.run_until(signal_event())
-    return 0
+    return await mgr.run_until(signal_event())
 
 
 def main(argv=None) -> int:

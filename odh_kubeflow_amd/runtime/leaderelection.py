@@ -3,10 +3,16 @@ runs it for ``--enable-leader-election`` / ``--leader-elect``
 (``kf/main.go:91-93`` ID ``kubeflow-notebook-controller``; ``odh/main.go:159-160``).
 
 Active/passive: a candidate acquires the Lease when it is free or expired, renews it
-every ``retry_period`` and must renew within ``renew_deadline`` or step down (the
-manager then stops its controllers).  Defaults are controller-runtime's: lease 15 s,
-renew deadline 10 s, retry 2 s.  ``release()`` on shutdown clears the holder so a
-standby takes over immediately (``LeaderElectionReleaseOnCancel``).
+every ``retry_period`` and must renew within ``renew_deadline`` or step down — the
+manager then exits the process non-zero, as controller-runtime does, so the kubelet
+restarts it as a fresh candidate.  Defaults are controller-runtime's: lease 15 s, renew
+deadline 10 s, retry 2 s.  ``release()`` on shutdown clears the holder so a standby
+takes over immediately (``LeaderElectionReleaseOnCancel``).
+
+Expiry is judged like client-go's ``observedTime``: never by comparing the holder's
+``renewTime`` (written with the holder's wall clock) against the local clock, but by how
+long the Lease record has gone unchanged on this candidate's monotonic clock.  Clock skew
+between nodes therefore cannot let a standby take a Lease that is still being renewed.
 """
 
 from __future__ import annotations
@@ -21,7 +27,7 @@ from typing import Awaitable, Callable, Optional
 
 from ..models import kinds
 from ..models.errors import ApiError, is_conflict, is_not_found
-from ..utils.timeutil import parse_rfc3339, rfc3339_micro
+from ..utils.timeutil import rfc3339_micro
 
 log = logging.getLogger("runtime.leaderelection")
 
@@ -46,6 +52,9 @@ class LeaderElector:
         self.retry_period = retry_period
         self.is_leader = False
         self.transitions = 0
+        self.lost = False
+        self._observed = None  # (holder, renewTime, leaseDurationSeconds) last seen
+        self._observed_at = 0.0  # time.monotonic() when that record was first seen
 
     def _spec(self, cur: Optional[dict]) -> dict:
         now = rfc3339_micro()
@@ -74,14 +83,19 @@ class LeaderElector:
                 return False
         spec = cur.get("spec") or {}
         holder = spec.get("holderIdentity")
+        record = (holder, spec.get("renewTime"), spec.get("leaseDurationSeconds"))
+        if record != self._observed:
+            self._observed, self._observed_at = record, time.monotonic()
         if holder and holder != self.identity:
-            renew = parse_rfc3339(spec.get("renewTime")) or 0.0
             dur = float(spec.get("leaseDurationSeconds") or self.lease_duration)
-            if time.time() < renew + dur:
-                return False  # held by a live leader
+            if time.monotonic() < self._observed_at + dur:
+                return False  # held by a leader that renewed within the lease duration
         cur["spec"] = self._spec(cur)
         try:
             await self.client.update(cur)
+            sp = cur["spec"]
+            self._observed = (sp["holderIdentity"], sp["renewTime"], sp["leaseDurationSeconds"])
+            self._observed_at = time.monotonic()
             return True
         except ApiError as e:
             if is_conflict(e):
@@ -122,6 +136,7 @@ class LeaderElector:
             was = self.is_leader
             self.is_leader = False
         if was:
+            self.lost = True
             await on_stopped()
 
     async def release(self) -> None:

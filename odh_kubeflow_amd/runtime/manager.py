@@ -5,7 +5,10 @@ Prometheus registry, the ``/metrics`` and ``/healthz``/``/readyz`` servers
 (``kf/main.go:125-133``, ``odh/main.go:231-238``) and optional leader election
 (``LeaderElectionID`` ``kubeflow-notebook-controller`` / ``odh-notebook-controller``).
 Controllers only start once leadership is held; runnables that do not need
-leadership (the webhook server) start immediately, as in controller-runtime.
+leadership (the webhook server) start immediately, as in controller-runtime.  Losing
+leadership is fatal, as in controller-runtime (``leaderelection.LeaderCallbacks.OnStoppedLeading``
+→ ``os.Exit(1)``): the controllers stop, ``/healthz`` fails and :meth:`run_until` returns
+exit code 1 so the process ends and the kubelet restarts it as a new candidate.
 """
 
 from __future__ import annotations
@@ -50,7 +53,10 @@ class Manager:
         self._servers: List = []
         self._started = False
         self._leader_task: Optional[asyncio.Task] = None
-        self.elected = asyncio.Event() if False else None  # created lazily inside the loop
+        self.elected = None  # asyncio.Event, created inside the loop by start()
+        self.fatal: Optional[str] = None  # set when the manager must exit (leadership lost)
+        self._fatal_event: Optional[asyncio.Event] = None
+        self.healthz["leader-election"] = lambda: self.fatal is None
 
     # ------------------------------------------------------------------ construction
 
@@ -113,6 +119,7 @@ class Manager:
             return
         self._started = True
         self.elected = asyncio.Event()
+        self._fatal_event = asyncio.Event()
         await self._start_servers()
         for r in self.runnables:
             await r.start()
@@ -129,9 +136,12 @@ class Manager:
         self.elected.set()
 
     async def _lost_leader(self) -> None:
-        log.error("%s: leader election lost; stopping controllers", self.name)
+        log.error("%s: leader election lost; stopping controllers and exiting", self.name)
+        self.fatal = "leader election lost"
         for c in self.controllers:
             await c.stop()
+        if self._fatal_event is not None:
+            self._fatal_event.set()
 
     async def stop(self) -> None:
         if self._leader_task is not None:
@@ -162,15 +172,24 @@ class Manager:
             await rest.close()
         self._started = False
 
-    async def run_until(self, stop: asyncio.Event) -> None:
+    async def run_until(self, stop: asyncio.Event) -> int:
+        """Run until ``stop`` is set (exit code 0) or the manager hits a fatal condition such
+        as losing leadership (exit code 1)."""
         await self.start()
         from ..utils import gctune
 
         gctune.tune()  # long-running process: keep gen-2 pauses off the reconcile path
+        waits = [asyncio.ensure_future(stop.wait()), asyncio.ensure_future(self._fatal_event.wait())]
         try:
-            await stop.wait()
+            await asyncio.wait(waits, return_when=asyncio.FIRST_COMPLETED)
         finally:
+            for w in waits:
+                w.cancel()
             await self.stop()
+        if self.fatal:
+            log.error("%s: exiting: %s", self.name, self.fatal)
+            return 1
+        return 0
 
     # ------------------------------------------------------------------ test / bench helpers
 

@@ -30,6 +30,8 @@ def parse(argv: Optional[List[str]] = None) -> argparse.Namespace:
     p.add_argument("--webhook-cert-dir", default="/tmp/k8s-webhook-server/serving-certs")
     p.add_argument("--webhook-port", type=int, default=8443)
     p.add_argument("--webhook-host", default="0.0.0.0")
+    p.add_argument("--webhook-cert-reload-seconds", type=float, default=10.0,
+                   help="poll interval for rotated tls.crt/tls.key (certwatcher)")
     p.add_argument("--leader-elect", action="store_true")
     p.add_argument("--debug-log", action="store_true")
     p.add_argument("--kubeconfig", default=None)
@@ -64,10 +66,14 @@ def build(args, env=os.environ):
     OpenshiftNotebookReconciler(mgr.client, mgr.reader, namespace, env=env,
                                 recorder=mgr.get_event_recorder_for("odh-notebook-controller")).setup_with_manager(mgr)
     wh = NotebookWebhook(mgr.client, namespace, kube_rbac_proxy_image=args.kube_rbac_proxy_image, env=env)
-    cert_dir = args.webhook_cert_dir if os.path.exists(os.path.join(args.webhook_cert_dir, "tls.crt")) else None
-    if cert_dir is None:
-        log.warning("no serving certificate in %s: webhook served over plain HTTP", args.webhook_cert_dir)
-    server = WebhookServer(wh, cert_dir, args.webhook_host, args.webhook_port)
+    # controller-runtime's webhook server refuses to start without its serving cert; admission
+    # (failurePolicy: Fail) is never offered over plain HTTP
+    missing = [f for f in ("tls.crt", "tls.key") if not os.path.exists(os.path.join(args.webhook_cert_dir, f))]
+    if missing:
+        raise SystemExit(f"webhook serving certificate missing in {args.webhook_cert_dir}: {', '.join(missing)} "
+                         "(OpenShift: service-ca; elsewhere: the odh-webhook-certs Job, cmd/webhook_certs.py)")
+    server = WebhookServer(wh, args.webhook_cert_dir, args.webhook_host, args.webhook_port,
+                           reload_interval=args.webhook_cert_reload_seconds)
     mgr.add(ServerRunnable(server.start, server.stop), needs_leader=False)  # webhooks serve on every replica
     mgr.add_healthz_check("healthz")
     mgr.add_readyz_check("readyz")

@@ -5,7 +5,14 @@ On OpenShift the service-ca operator injects the serving Secret and the ``caBund
 elsewhere the reference's kind CI creates them with the ``openssl`` CLI and patches the
 ``caBundle`` into the MutatingWebhookConfiguration
 (``.github/workflows/odh_notebook_controller_integration_test.yaml:190-216``).  This
-does the same programmatically (the ``cryptography`` package is not available).
+does the same programmatically (the ``cryptography`` package is not available):
+
+* :func:`generate` — CA + serving cert files;
+* :func:`provision` — the in-cluster step the ``standalone``/``mi355x`` overlays run as a
+  Job (and a CronJob for renewal, ``cmd/webhook_certs.py``): keep the serving Secret
+  ``odh-notebook-controller-webhook-cert`` (``tls.crt``/``tls.key``/``ca.crt``) valid and
+  the MutatingWebhookConfiguration's ``caBundle`` equal to its CA.  Idempotent: a valid
+  cert with more than ``renew_before_days`` left and a matching ``caBundle`` is left alone.
 """
 
 from __future__ import annotations
@@ -15,7 +22,7 @@ import os
 import subprocess
 import tempfile
 from dataclasses import dataclass
-from typing import Iterable, Optional
+from typing import Iterable, List, Optional
 
 
 @dataclass
@@ -63,3 +70,106 @@ def generate(hosts: Iterable[str] = ("127.0.0.1", "localhost"), cert_dir: Option
           str(days), "-sha256", "-extfile", ext, "-out", crt])
     with open(ca_crt) as f:
         return WebhookCerts(d, f.read())
+
+
+def service_hosts(service: str, namespace: str, cluster_domain: str = "cluster.local") -> List[str]:
+    """The DNS names the apiserver may use for ``service`` (its TLS SANs)."""
+    return [service, f"{service}.{namespace}", f"{service}.{namespace}.svc",
+            f"{service}.{namespace}.svc.{cluster_domain}"]
+
+
+def cert_not_after(pem: str) -> Optional[float]:
+    """Expiry (epoch seconds) of a PEM certificate, via ``openssl x509 -enddate``."""
+    import calendar
+    import time
+
+    try:
+        out = subprocess.run(["openssl", "x509", "-noout", "-enddate"], input=pem.encode(), check=True,
+                             capture_output=True).stdout.decode().strip()
+    except (subprocess.CalledProcessError, OSError):
+        return None
+    raw = out.split("=", 1)[-1]  # e.g. "Oct 16 12:00:00 2027 GMT"
+    try:
+        return float(calendar.timegm(time.strptime(raw, "%b %d %H:%M:%S %Y %Z")))
+    except ValueError:
+        return None
+
+
+def cert_matches_key(cert_pem: str, key_pem: str) -> bool:
+    def pub(args, data):
+        r = subprocess.run(args, input=data.encode(), capture_output=True)
+        return r.stdout if r.returncode == 0 else None
+    a = pub(["openssl", "x509", "-noout", "-pubkey"], cert_pem)
+    b = pub(["openssl", "pkey", "-pubout"], key_pem)
+    return a is not None and a == b
+
+
+async def provision(client, namespace: str, secret_name: str = "odh-notebook-controller-webhook-cert",
+                    service_name: str = "odh-notebook-controller-webhook-service",
+                    mwc_names: Iterable[str] = ("odh-notebook-controller-mutating-webhook-configuration",),
+                    extra_hosts: Iterable[str] = (), validity_days: int = 365, renew_before_days: int = 90,
+                    cluster_domain: str = "cluster.local") -> dict:
+    """Ensure the serving Secret holds a valid cert and every named MWC trusts its CA.
+
+    Returns ``{"secret": "created"|"rotated"|"kept", "mwc": {name: "patched"|"kept"|"missing"}}``.
+    """
+    import time
+
+    from ..models import kinds
+    from ..models.errors import ApiError, is_not_found
+
+    def b64(s: str) -> str:
+        return base64.b64encode(s.encode()).decode()
+
+    def unb64(s: Optional[str]) -> str:
+        return base64.b64decode(s or "").decode(errors="replace")
+
+    secret = None
+    try:
+        secret = await client.get(kinds.SECRET, secret_name, namespace)
+    except ApiError as e:
+        if not is_not_found(e):
+            raise
+    data = (secret or {}).get("data") or {}
+    crt, key, ca = unb64(data.get("tls.crt")), unb64(data.get("tls.key")), unb64(data.get("ca.crt"))
+    exp = cert_not_after(crt) if crt else None
+    fresh = bool(crt and key and ca and exp and exp - time.time() > renew_before_days * 86400
+                 and cert_matches_key(crt, key))
+    result = {"secret": "kept", "mwc": {}}
+    if not fresh:
+        with tempfile.TemporaryDirectory(prefix="odh-webhook-certs-") as d:
+            g = generate([*service_hosts(service_name, namespace, cluster_domain), *extra_hosts], d, validity_days)
+            with open(g.cert_file) as f:
+                crt = f.read()
+            with open(g.key_file) as f:
+                key = f.read()
+            ca = g.ca_pem
+        body = {"apiVersion": "v1", "kind": "Secret", "type": "kubernetes.io/tls",
+                "metadata": {"name": secret_name, "namespace": namespace,
+                             "labels": {"app.kubernetes.io/managed-by": "odh-webhook-certs"}},
+                "data": {"tls.crt": b64(crt), "tls.key": b64(key), "ca.crt": b64(ca)}}
+        if secret is None:
+            await client.create(body)
+            result["secret"] = "created"
+        else:
+            body["metadata"]["resourceVersion"] = secret["metadata"]["resourceVersion"]
+            await client.update(body)
+            result["secret"] = "rotated"
+    bundle = b64(ca)
+    for name in mwc_names:
+        try:
+            mwc = await client.get(kinds.MUTATING_WEBHOOK_CONFIGURATION, name)
+        except ApiError as e:
+            if is_not_found(e):
+                result["mwc"][name] = "missing"
+                continue
+            raise
+        hooks = mwc.get("webhooks") or []
+        if all((h.get("clientConfig") or {}).get("caBundle") == bundle for h in hooks):
+            result["mwc"][name] = "kept"
+            continue
+        for h in hooks:
+            h.setdefault("clientConfig", {})["caBundle"] = bundle
+        await client.update(mwc)
+        result["mwc"][name] = "patched"
+    return result

@@ -5,15 +5,23 @@ over TLS from ``--webhook-cert-dir`` (``tls.crt`` / ``tls.key``) on ``--webhook-
 (default 8443), plus ``/healthz`` for the TLS readiness dial the reference's envtest
 suite performs (``odh/controllers/suite_test.go:237-246``).  Handlers run concurrently,
 one task per request; the handler itself keeps no shared mutable state.
+
+Certificate rotation (controller-runtime's ``certwatcher``): the cert files are polled every
+``reload_interval`` seconds and, when ``tls.crt``/``tls.key`` changed (the kubelet swaps a
+Secret volume atomically; service-ca / cert-manager / ``cmd/webhook_certs.py`` rotate the
+Secret), loaded into the live TLS context, so new connections present the new certificate
+without a restart.  A half-written or mismatched pair is ignored and retried; the old
+certificate keeps serving.
 """
 
 from __future__ import annotations
 
+import asyncio
 import json
 import logging
 import os
 import ssl
-from typing import Optional
+from typing import Optional, Tuple
 
 from ..runtime.http1 import Http1Server
 from .notebook_webhook import WEBHOOK_PATH, NotebookWebhook
@@ -23,22 +31,68 @@ log = logging.getLogger("webhook.server")
 
 class WebhookServer:
     def __init__(self, webhook: NotebookWebhook, cert_dir: Optional[str], host: str = "0.0.0.0", port: int = 8443,
-                 path: str = WEBHOOK_PATH):
+                 path: str = WEBHOOK_PATH, reload_interval: float = 10.0):
         self.webhook = webhook
         self.cert_dir = cert_dir
         self.host = host
         self.port = port
         self.path = path
+        self.reload_interval = reload_interval
         self._server = None
+        self._ctx: Optional[ssl.SSLContext] = None
+        self._stamp: Optional[Tuple] = None
+        self._watch: Optional[asyncio.Task] = None
         self.served = 0
+        self.reloads = 0
+
+    def _files(self) -> Tuple[str, str]:
+        return os.path.join(self.cert_dir, "tls.crt"), os.path.join(self.cert_dir, "tls.key")
+
+    def _file_stamp(self) -> Optional[Tuple]:
+        try:
+            return tuple((st.st_mtime_ns, st.st_size, st.st_ino) for st in map(os.stat, self._files()))
+        except OSError:
+            return None
 
     def ssl_context(self) -> Optional[ssl.SSLContext]:
         if not self.cert_dir:
             return None
         ctx = ssl.SSLContext(ssl.PROTOCOL_TLS_SERVER)
         ctx.minimum_version = ssl.TLSVersion.TLSv1_2
-        ctx.load_cert_chain(os.path.join(self.cert_dir, "tls.crt"), os.path.join(self.cert_dir, "tls.key"))
+        self._stamp = self._file_stamp()
+        ctx.load_cert_chain(*self._files())
         return ctx
+
+    def maybe_reload(self) -> bool:
+        """Load rotated cert files into the live context; True when a new pair was loaded."""
+        if self._ctx is None:
+            return False
+        stamp = self._file_stamp()
+        if stamp is None or stamp == self._stamp:
+            return False
+        import shutil
+        import tempfile
+
+        # snapshot the pair, prove it on a scratch context, only then load it into the live one:
+        # a failed load_cert_chain leaves an SSL_CTX with the new cert and the old key
+        with tempfile.TemporaryDirectory(prefix="odh-webhook-reload-") as d:
+            try:
+                crt, key = (shutil.copy(f, os.path.join(d, os.path.basename(f))) for f in self._files())
+                scratch = ssl.SSLContext(ssl.PROTOCOL_TLS_SERVER)
+                scratch.load_cert_chain(crt, key)
+                self._ctx.load_cert_chain(crt, key)
+            except (ssl.SSLError, OSError) as e:  # mid-rotation: keep serving the old pair, retry next tick
+                log.warning("webhook certificate reload failed (old certificate kept): %r", e)
+                return False
+        self._stamp = stamp
+        self.reloads += 1
+        log.info("webhook serving certificate reloaded from %s", self.cert_dir)
+        return True
+
+    async def _watch_certs(self) -> None:
+        while True:
+            await asyncio.sleep(self.reload_interval)
+            self.maybe_reload()
 
     async def _handle(self, method: str, path: str, headers, data: bytes):
         if method == "GET" and path in ("/healthz", "/readyz"):
@@ -58,11 +112,17 @@ class WebhookServer:
         return 200, "application/json", json.dumps(out, separators=(",", ":")).encode()
 
     async def start(self) -> "WebhookServer":
-        self._server = await Http1Server(self._handle, self.host, self.port, self.ssl_context()).start()
+        self._ctx = self.ssl_context()
+        self._server = await Http1Server(self._handle, self.host, self.port, self._ctx).start()
         self.port = self._server.port
+        if self._ctx is not None and self.reload_interval > 0:
+            self._watch = asyncio.ensure_future(self._watch_certs())
         return self
 
     async def stop(self) -> None:
+        if self._watch is not None:
+            self._watch.cancel()
+            self._watch = None
         if self._server is not None:
             await self._server.stop()
             self._server = None

@@ -17,6 +17,8 @@ What it reproduces, because the controllers and their tests depend on it:
 * label / field selector List and Watch, with an event history for resumption;
 * mutating admission (in-process handlers or HTTPS webhooks) on CREATE/UPDATE;
 * CRD installation state (uninstalled kinds raise ``NoKindMatch``);
+* kube-apiserver defaulting of Pods, StatefulSets, Deployments and Services on every write
+  (``models/defaults.py``), so controllers see the same live objects as on a real cluster;
 * optionally, ownerReference garbage collection. envtest has no GC
   (``kf/controllers/notebook_controller_bdd_test.go:73-76``), so it is off by default.
 
@@ -35,6 +37,7 @@ from collections import deque
 from dataclasses import dataclass
 from typing import Any, Awaitable, Callable, Deque, Dict, List, Optional, Tuple
 
+from ..models import defaults
 from ..models import meta as m
 from ..models.errors import (AlreadyExists, ApiError, BadRequest, Conflict, Forbidden, Gone, Invalid, NoKindMatch,
                              NotFound)
@@ -101,8 +104,11 @@ class ObjectStore:
 
     HISTORY = 4096
 
-    def __init__(self, gc: bool = False, install_all_crds: bool = True, strict_namespaces: bool = False):
+    def __init__(self, gc: bool = False, install_all_crds: bool = True, strict_namespaces: bool = False,
+                 defaulting: bool = True):
         self._lock = threading.RLock()
+        # kube-apiserver defaulting of Pods / StatefulSets / Deployments / Services (models/defaults.py)
+        self.defaulting = defaulting
         self._data: Dict[str, Dict[Tuple[str, str], dict]] = {}
         self._rv = 0
         self._history: Dict[str, Deque[Tuple[int, str, dict, Optional[dict]]]] = {}
@@ -232,6 +238,9 @@ class ObjectStore:
                 raise NotFound("namespaces", ns)
 
     def _defaults(self, info: ResourceInfo, obj: dict) -> None:
+        """kube-apiserver defaulting (``models/defaults.py``) + ClusterIP allocation."""
+        if self.defaulting:
+            defaults.apply(info.key, obj)
         if info.key == "services":
             spec = obj.setdefault("spec", {})
             spec.setdefault("type", "ClusterIP")
@@ -416,6 +425,12 @@ class ObjectStore:
                 if added:
                     raise Forbidden(f"no new finalizers can be added if the object is being deleted, found new "
                                     f"finalizers {sorted(added)}")
+            if self.defaulting and info.key in defaults.BY_RESOURCE:
+                defaults.apply(info.key, new)
+                if info.key == "services":  # the allocated ClusterIP is immutable
+                    for k in ("clusterIP", "clusterIPs"):
+                        if k in (live.get("spec") or {}) and not (new.get("spec") or {}).get(k):
+                            new.setdefault("spec", {})[k] = deepcopy_json(live["spec"][k])
             if "generation" in lmd:
                 md["generation"] = lmd["generation"]
                 if _spec_part(new) != _spec_part(live):

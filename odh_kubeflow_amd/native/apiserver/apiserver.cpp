@@ -18,6 +18,8 @@
 //     HTTPS (OpenSSL, caBundle verification, failurePolicy, Service → Endpoints
 //     resolution round-robin over replicas), admission runs outside the store lock;
 //   * ownerReference garbage collection (background + foreground) when --gc is set;
+//   * kube-apiserver defaulting of Pods / StatefulSets / Deployments / Services on every write
+//     (api_defaults; the same rules as models/defaults.py), config key "defaulting";
 //   * discovery documents; bearer-token authentication.
 //
 // Concurrency: one thread per client connection (keep-alive), one global store mutex
@@ -581,6 +583,7 @@ struct Store {
   int64_t rv = 0;
   size_t history = 4096;
   bool gc = false;
+  bool defaulting = true;  // kube-apiserver defaulting of Pods / StatefulSets / Deployments / Services
   std::unordered_map<std::string, std::set<std::tuple<std::string, std::string, std::string>>> owners;
   std::unordered_map<std::string, std::tuple<std::string, std::string, std::string>> uids;
   std::atomic<uint64_t> requests{0}, writes{0}, webhook_calls{0};
@@ -734,7 +737,264 @@ std::optional<std::string> validate(const Res& r, const Value& o) {
   return std::nullopt;
 }
 
+// ------------------------------------------------------------------ kube-apiserver defaulting
+// Same rules as models/defaults.py (k8s.io/kubernetes/pkg/apis/{core,apps}/v1/defaults.go plus
+// resource.Quantity canonicalisation), applied to every Pod / StatefulSet / Deployment /
+// Service write so controllers see the live objects a real apiserver would hand them.
+
+void set_default(Value& o, const char* k, Value v) {
+  if (!o.get(k)) o[k] = std::move(v);
+}
+
+Value& obj_at(Value& o, const char* k) {
+  Value& v = o[k];
+  if (!v.is_obj()) v = Value::object();
+  return v;
+}
+
+// resource.Quantity -> canonical string ("0.5" -> "500m", "1024Mi" -> "1Gi", "1000" -> "1k");
+// empty when the text is not a quantity (validation reports it elsewhere).
+std::string canon_quantity(const std::string& text) {
+  using i128 = __int128;
+  size_t n = 0;
+  bool neg = false;
+  if (n < text.size() && (text[n] == '+' || text[n] == '-')) neg = text[n++] == '-';
+  i128 num = 0, den = 1;
+  bool digits = false, dot = false;
+  for (; n < text.size(); ++n) {
+    char c = text[n];
+    if (c >= '0' && c <= '9') {
+      if (num > ((i128)1 << 100)) return "";
+      num = num * 10 + (c - '0');
+      if (dot) den *= 10;
+      digits = true;
+    } else if (c == '.' && !dot) {
+      dot = true;
+    } else {
+      break;
+    }
+  }
+  if (!digits) return "";
+  std::string suf = text.substr(n);
+  bool binary = false;
+  static const std::pair<const char*, int> bin[] = {{"Ki", 10}, {"Mi", 20}, {"Gi", 30}, {"Ti", 40}, {"Pi", 50}, {"Ei", 60}};
+  static const std::pair<const char*, int> dec[] = {{"n", -9}, {"u", -6}, {"m", -3}, {"", 0}, {"k", 3},
+                                                    {"M", 6},  {"G", 9},  {"T", 12}, {"P", 15}, {"E", 18}};
+  int exp10 = 0;
+  bool matched = false;
+  for (auto& b : bin)
+    if (suf == b.first) {
+      num <<= b.second;
+      binary = matched = true;
+    }
+  for (auto& d : dec)
+    if (!matched && suf == d.first) {
+      exp10 = d.second;
+      matched = true;
+    }
+  if (!matched && (suf.size() >= 2 && (suf[0] == 'e' || suf[0] == 'E'))) {
+    char* end = nullptr;
+    long e = std::strtol(suf.c_str() + 1, &end, 10);
+    if (*end || e > 18 || e < -18) return "";
+    exp10 = (int)e;
+    matched = true;
+  }
+  if (!matched) return "";
+  for (; exp10 > 0; --exp10) num *= 10;
+  for (; exp10 < 0; ++exp10) den *= 10;
+  auto gcd = [](i128 a, i128 b) {
+    while (b) {
+      i128 t = a % b;
+      a = b;
+      b = t;
+    }
+    return a;
+  };
+  if (num == 0) return "0";
+  i128 g = gcd(num, den);
+  num /= g;
+  den /= g;
+  auto to_s = [](i128 v) {
+    std::string out;
+    if (v == 0) return std::string("0");
+    while (v) {
+      out.insert(out.begin(), char('0' + (int)(v % 10)));
+      v /= 10;
+    }
+    return out;
+  };
+  std::string sign = neg ? "-" : "";
+  if (binary) {
+    for (int k = 5; k >= 0; --k) {
+      i128 base = (i128)1 << bin[k].second;
+      if (den == 1 && num % base == 0) return sign + to_s(num / base) + bin[k].first;
+    }
+    if (den == 1) return sign + to_s(num);
+  }
+  if (den == 1) {
+    static const std::pair<const char*, int> up[] = {{"E", 18}, {"P", 15}, {"T", 12}, {"G", 9}, {"M", 6}, {"k", 3}};
+    for (auto& u : up) {
+      i128 p = 1;
+      for (int k = 0; k < u.second; ++k) p *= 10;
+      if (num % p == 0) return sign + to_s(num / p) + u.first;
+    }
+    return sign + to_s(num);
+  }
+  static const std::pair<const char*, int> down[] = {{"m", 3}, {"u", 6}, {"n", 9}};
+  for (auto& d : down) {
+    i128 p = 1;
+    for (int k = 0; k < d.second; ++k) p *= 10;
+    if ((num * p) % den == 0) return sign + to_s(num * p / den) + d.first;
+  }
+  i128 p = 1000000000;
+  return sign + to_s(num * p / den) + "n";
+}
+
+void canon_quantities(Value* q) {
+  if (!q || !q->is_obj()) return;
+  for (auto& m : q->obj)
+    if (m.v.is_str()) {
+      std::string c = canon_quantity(m.v.s);
+      if (!c.empty()) m.v.s = c;
+    }
+}
+
+std::string image_pull_policy(const std::string& image) {
+  if (image.find('@') != std::string::npos) return "IfNotPresent";
+  std::string last = image.substr(image.rfind('/') == std::string::npos ? 0 : image.rfind('/') + 1);
+  auto colon = last.rfind(':');
+  std::string tag = colon == std::string::npos ? "" : last.substr(colon + 1);
+  return tag.empty() || tag == "latest" ? "Always" : "IfNotPresent";
+}
+
+void default_probe(Value* p) {
+  if (!p || !p->is_obj()) return;
+  set_default(*p, "timeoutSeconds", Value::integer(1));
+  set_default(*p, "periodSeconds", Value::integer(10));
+  set_default(*p, "successThreshold", Value::integer(1));
+  set_default(*p, "failureThreshold", Value::integer(3));
+  if (Value* hg = p->get("httpGet"); hg && hg->is_obj()) {
+    set_default(*hg, "path", Value::str("/"));
+    set_default(*hg, "scheme", Value::str("HTTP"));
+  }
+}
+
+void default_container(Value& c) {
+  if (!c.is_obj()) return;
+  set_default(c, "terminationMessagePath", Value::str("/dev/termination-log"));
+  set_default(c, "terminationMessagePolicy", Value::str("File"));
+  if (const Value* img = c.get("image"); img && img->is_str()) set_default(c, "imagePullPolicy", Value::str(image_pull_policy(img->s)));
+  if (Value* ports = c.get("ports"); ports && ports->is_arr())
+    for (auto& p : ports->arr)
+      if (p.is_obj()) set_default(p, "protocol", Value::str("TCP"));
+  if (Value* env = c.get("env"); env && env->is_arr())
+    for (auto& e : env->arr) {
+      Value* vf = e.get("valueFrom");
+      Value* fr = vf ? vf->get("fieldRef") : nullptr;
+      if (fr && fr->is_obj()) set_default(*fr, "apiVersion", Value::str("v1"));
+    }
+  Value& res = obj_at(c, "resources");
+  canon_quantities(res.get("limits"));
+  canon_quantities(res.get("requests"));
+  for (const char* k : {"livenessProbe", "readinessProbe", "startupProbe"}) default_probe(c.get(k));
+}
+
+void default_pod_spec(Value& spec) {
+  set_default(spec, "restartPolicy", Value::str("Always"));
+  set_default(spec, "terminationGracePeriodSeconds", Value::integer(30));
+  set_default(spec, "dnsPolicy", Value::str("ClusterFirst"));
+  set_default(spec, "securityContext", Value::object());
+  set_default(spec, "schedulerName", Value::str("default-scheduler"));
+  set_default(spec, "enableServiceLinks", Value::boolean(true));
+  if (!spec.str_or("serviceAccountName").empty() && spec.str_or("serviceAccount").empty())
+    spec["serviceAccount"] = Value::str(spec.str_or("serviceAccountName"));
+  for (const char* k : {"initContainers", "containers"})
+    if (Value* cs = spec.get(k); cs && cs->is_arr())
+      for (auto& c : cs->arr) default_container(c);
+  if (Value* vols = spec.get("volumes"); vols && vols->is_arr())
+    for (auto& v : vols->arr) {
+      if (!v.is_obj()) continue;
+      for (const char* src : {"secret", "configMap"})
+        if (Value* x = v.get(src); x && x->is_obj()) set_default(*x, "defaultMode", Value::integer(420));
+      if (Value* hp = v.get("hostPath"); hp && hp->is_obj()) set_default(*hp, "type", Value::str(""));
+      if (Value* ed = v.get("emptyDir"); ed && ed->is_obj())
+        if (Value* sl = ed->get("sizeLimit"); sl && sl->is_str()) {
+          std::string c = canon_quantity(sl->s);
+          if (!c.empty()) sl->s = c;
+        }
+    }
+}
+
+void default_template(Value& spec) {
+  Value& t = obj_at(spec, "template");
+  set_default(obj_at(t, "metadata"), "creationTimestamp", Value::null());
+  default_pod_spec(obj_at(t, "spec"));
+}
+
+void api_defaults(const Res& r, Value& o) {
+  if (r.key == "statefulsets.apps" || r.key == "deployments.apps") {
+    Value& spec = obj_at(o, "spec");
+    if (const Value* rep = spec.get("replicas"); !rep || rep->is_null()) spec["replicas"] = Value::integer(1);
+    set_default(spec, "revisionHistoryLimit", Value::integer(10));
+    if (r.key == "statefulsets.apps") {
+      set_default(spec, "podManagementPolicy", Value::str("OrderedReady"));
+      Value& us = obj_at(spec, "updateStrategy");
+      set_default(us, "type", Value::str("RollingUpdate"));
+      if (us.str_or("type") == "RollingUpdate") set_default(obj_at(us, "rollingUpdate"), "partition", Value::integer(0));
+      Value& ret = obj_at(spec, "persistentVolumeClaimRetentionPolicy");
+      set_default(ret, "whenDeleted", Value::str("Retain"));
+      set_default(ret, "whenScaled", Value::str("Retain"));
+    } else {
+      Value& st = obj_at(spec, "strategy");
+      set_default(st, "type", Value::str("RollingUpdate"));
+      if (st.str_or("type") == "RollingUpdate") {
+        Value& ru = obj_at(st, "rollingUpdate");
+        set_default(ru, "maxUnavailable", Value::str("25%"));
+        set_default(ru, "maxSurge", Value::str("25%"));
+      }
+      set_default(spec, "progressDeadlineSeconds", Value::integer(600));
+    }
+    default_template(spec);
+  } else if (r.key == "pods") {
+    Value& spec = obj_at(o, "spec");
+    for (const char* k : {"containers", "initContainers"})
+      if (Value* cs = spec.get(k); cs && cs->is_arr())
+        for (auto& c : cs->arr) {
+          Value* res = c.get("resources");
+          Value* lim = res ? res->get("limits") : nullptr;
+          if (!lim || !lim->is_obj() || lim->obj.empty()) continue;
+          Value& req = obj_at(*res, "requests");
+          for (auto& m : lim->obj) set_default(req, m.k.c_str(), m.v);
+        }
+    default_pod_spec(spec);
+  } else if (r.key == "services") {
+    Value& spec = obj_at(o, "spec");
+    set_default(spec, "type", Value::str("ClusterIP"));
+    set_default(spec, "sessionAffinity", Value::str("None"));
+    std::string type = spec.str_or("type");
+    if ((type == "ClusterIP" || type == "NodePort" || type == "LoadBalancer") && spec.str_or("clusterIP") != "None") {
+      Value fam = Value::array();
+      fam.arr.push_back(Value::str("IPv4"));
+      set_default(spec, "ipFamilies", fam);
+      set_default(spec, "ipFamilyPolicy", Value::str("SingleStack"));
+      set_default(spec, "internalTrafficPolicy", Value::str("Cluster"));
+    }
+    if (Value* ports = spec.get("ports"); ports && ports->is_arr())
+      for (auto& p : ports->arr) {
+        if (!p.is_obj()) continue;
+        set_default(p, "protocol", Value::str("TCP"));
+        const Value* tp = p.get("targetPort");
+        if ((!tp || tp->is_null()) && p.get("port")) p["targetPort"] = *p.get("port");
+      }
+  }
+}
+
+bool defaulted_kind(const Res& r) {
+  return r.key == "statefulsets.apps" || r.key == "deployments.apps" || r.key == "pods" || r.key == "services";
+}
+
 void defaults(const Res& r, Value& o) {
+  if (S.defaulting) api_defaults(r, o);
   if (r.key == "services") {
     Value& spec = o["spec"];
     if (!spec.is_obj()) spec = Value::object();
@@ -1319,6 +1579,18 @@ void prepare_update(const Res& r, const Value& base, Value& nw) {
       std::string l;
       for (auto& a : added) l += (l.empty() ? "" : " ") + a;
       throw Forbidden("no new finalizers can be added if the object is being deleted, found new finalizers [" + l + "]");
+    }
+  }
+  if (S.defaulting && defaulted_kind(r)) {
+    api_defaults(r, nw);
+    if (r.key == "services") {  // the allocated ClusterIP is immutable
+      const Value* bs = base.get("spec");
+      Value& ns_ = obj_at(nw, "spec");
+      for (const char* k : {"clusterIP", "clusterIPs"}) {
+        const Value* have = ns_.get(k);
+        const Value* was = bs ? bs->get(k) : nullptr;
+        if (was && (!have || have->is_null() || (have->is_str() && have->s.empty()))) ns_[k] = *was;
+      }
     }
   }
   if (const Value* gen = lm.get("generation")) {
@@ -2188,6 +2460,7 @@ void load_config(const std::string& path) {
     g_res.push_back(std::move(x));
   }
   if (const Value* v = cfg.get("gc")) S.gc = v->b;
+  if (const Value* v = cfg.get("defaulting")) S.defaulting = v->b;
   if (const Value* v = cfg.get("history"))
     if (v->t == T::Int) S.history = (size_t)v->i;
   g_token = cfg.str_or("token");

@@ -2,15 +2,23 @@
 
 Each ``copy_*_fields(frm, to)`` copies the fields the controller owns from the desired
 object ``frm`` onto the live object ``to`` and returns True when an Update is needed.
-Semantics match the reference exactly, including its one-sided label/annotation check
-(only keys present on ``to`` are compared, util.go:107-134) — a label *added* to the
-desired object alone does not force an update, but it is still copied over.
+Semantics match the reference, including its one-sided label/annotation check (only
+keys present on ``to`` are compared, util.go:107-134) — a label *added* to the desired
+object alone does not force an update, but it is still copied over.
+
+One deliberate fix: pod specs and Service ports are compared *after* kube-apiserver
+defaulting of both sides (``models/defaults.py``).  The live object always carries the
+server's defaults (``terminationMessagePath``, ``imagePullPolicy``, ``dnsPolicy``, port
+``protocol``, canonical quantities, ...) and the freshly generated desired one never
+does, so the reference's raw DeepEqual (util.go:126-130, 187-193) is false on every pass
+and issues an Update per reconcile against a real apiserver.
 """
 
 from __future__ import annotations
 
-from typing import Callable
+from typing import Callable, Optional
 
+from ..models import defaults
 from ..models import meta as m
 from ..models.errors import is_not_found
 from ..utils.objutil import deepcopy_json, ensure_dict
@@ -38,8 +46,16 @@ def _copy_meta(frm: dict, to: dict) -> bool:
     return require
 
 
-def copy_statefulset_fields(frm: dict, to: dict) -> bool:
-    """``CopyStatefulSetFields`` (util.go:107-134): labels, annotations, replicas, pod spec."""
+def pod_specs_equal(desired: Optional[dict], live: Optional[dict]) -> bool:
+    """Semantic pod-spec equality: both sides defaulted as kube-apiserver would."""
+    if desired == live:
+        return True
+    if desired is None or live is None:
+        return False
+    return defaults.pod_spec(deepcopy_json(desired)) == defaults.pod_spec(deepcopy_json(live))
+
+
+def _copy_pod_template_spec(frm: dict, to: dict) -> bool:
     require = _copy_meta(frm, to)
     fs, ts = frm.get("spec") or {}, ensure_dict(to, "spec")
     if fs.get("replicas") != ts.get("replicas"):
@@ -47,25 +63,27 @@ def copy_statefulset_fields(frm: dict, to: dict) -> bool:
         require = True
     fpod = (fs.get("template") or {}).get("spec")
     tt = ensure_dict(ts, "template")
-    if tt.get("spec") != fpod:
+    if not pod_specs_equal(fpod, tt.get("spec")):
         require = True
-    tt["spec"] = deepcopy_json(fpod)
+        tt["spec"] = deepcopy_json(fpod)
     return require
+
+
+def copy_statefulset_fields(frm: dict, to: dict) -> bool:
+    """``CopyStatefulSetFields`` (util.go:107-134): labels, annotations, replicas, pod spec."""
+    return _copy_pod_template_spec(frm, to)
 
 
 def copy_deployment_fields(frm: dict, to: dict) -> bool:
     """``CopyDeploymentSetFields`` (util.go:136-162)."""
-    require = _copy_meta(frm, to)
-    fs, ts = frm.get("spec") or {}, ensure_dict(to, "spec")
-    if fs.get("replicas") != ts.get("replicas"):
-        ts["replicas"] = fs.get("replicas")
-        require = True
-    fpod = (fs.get("template") or {}).get("spec")
-    tt = ensure_dict(ts, "template")
-    if tt.get("spec") != fpod:
-        require = True
-    tt["spec"] = deepcopy_json(fpod)
-    return require
+    return _copy_pod_template_spec(frm, to)
+
+
+def _ports_equal(desired, live) -> bool:
+    if desired == live:
+        return True
+    wrap = lambda ps: defaults.service({"spec": {"ports": deepcopy_json(ps or []), "clusterIP": "None"}})["spec"]["ports"]  # noqa: E731
+    return wrap(desired) == wrap(live)
 
 
 def copy_service_fields(frm: dict, to: dict) -> bool:
@@ -75,9 +93,9 @@ def copy_service_fields(frm: dict, to: dict) -> bool:
     if ts.get("selector") != fs.get("selector"):
         require = True
     ts["selector"] = deepcopy_json(fs.get("selector"))
-    if ts.get("ports") != fs.get("ports"):
+    if not _ports_equal(fs.get("ports"), ts.get("ports")):
         require = True
-    ts["ports"] = deepcopy_json(fs.get("ports"))
+        ts["ports"] = deepcopy_json(fs.get("ports"))
     return require
 
 

@@ -31,7 +31,11 @@ def scheme_config(uninstalled: Iterable[str] = (), gc: bool = False, token: Opti
         res.append({"group": i.group, "kind": i.kind, "plural": i.plural, "singular": i.singular,
                     "listKind": i.list_kind, "versions": list(i.versions), "storageVersion": i.storage_version,
                     "namespaced": i.namespaced, "status": i.status_subresource, "installed": i.key not in skip})
-    cfg = {"resources": res, "gc": gc, "history": history}
+    from ..models.crd import version_schema
+
+    # CRD structural schemas: prune -> default -> validate, as models/openapi.py does in-process
+    cfg = {"resources": res, "gc": gc, "history": history, "defaulting": True,
+           "schemas": {"notebooks.kubeflow.org": version_schema()}}
     if token:
         cfg["token"] = token
     return cfg

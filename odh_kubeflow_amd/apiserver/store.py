@@ -142,16 +142,14 @@ class ObjectStore:
         self.mutating = [x for x in self.mutating if x[0] != name]
 
     def _register_default_validators(self) -> None:
+        """The CRD's structural schema (``models/crd.py``: the reference's full PodSpec schema
+        + ``validation_patches.yaml``): prune → default → validate on every Notebook write."""
+        from ..models import crd, openapi
+
+        schema = crd.version_schema()
+
         def notebook(obj: dict) -> Optional[str]:
-            # kf/config/crd/patches/validation_patches.yaml: containers minItems 1, required [name, image]
-            cs = (((obj.get("spec") or {}).get("template") or {}).get("spec") or {}).get("containers")
-            if not isinstance(cs, list) or len(cs) < 1:
-                return "spec.template.spec.containers: Invalid value: should have at least 1 items"
-            for i, c in enumerate(cs):
-                for f in ("name", "image"):
-                    if not isinstance(c, dict) or not c.get(f):
-                        return f"spec.template.spec.containers[{i}].{f}: Required value"
-            return None
+            return openapi.first_error(openapi.process(schema, obj))
 
         self.validators["notebooks.kubeflow.org"] = notebook
 
@@ -224,12 +222,15 @@ class ObjectStore:
         for _, matcher, handler in self.mutating:
             if matcher(info, op):
                 obj = await handler(op, info, obj, old)
+        self._validate(info, obj)
+        return obj
+
+    def _validate(self, info: ResourceInfo, obj: dict) -> None:
         v = self.validators.get(info.key)
         if v is not None:
             err = v(obj)
             if err:
                 raise Invalid(info.singular if info.group == "" else f"{info.kind}.{info.group}", m.name(obj), err)
-        return obj
 
     def _check_namespace(self, info: ResourceInfo, ns: str) -> None:
         if self.strict_namespaces and info.namespaced:
@@ -390,6 +391,7 @@ class ObjectStore:
                 merged.pop("status", None)
             merged["metadata"]["resourceVersion"] = md.get("resourceVersion", "")
             new = merged
+            self._validate(info, new)
         else:
             if info.status_subresource:
                 if "status" in cur:
@@ -492,6 +494,7 @@ class ObjectStore:
             merged["status"] = new.get("status")
             merged["metadata"]["resourceVersion"] = nmd["resourceVersion"]
             new = merged
+            self._validate(info, new)
         else:
             if info.status_subresource:
                 if "status" in cur:

@@ -18,13 +18,11 @@
   service-ca injection + ``ADD_FSGROUP=false``, MI355X placement + GPU-busy culling;
 * ``samples/`` — Notebooks requesting 1 and 8 ``amd.com/gpu`` with the PyTorch-ROCm image.
 
-The CRD carries a structural schema for the fields the controllers rely on
-(``spec.template.spec.containers`` ``minItems: 1`` with required ``name``/``image``, as
-``kf/config/crd/patches/validation_patches.yaml``) and preserves the rest of the PodSpec
-(``x-kubernetes-preserve-unknown-fields``); kube-apiserver validates the pod template
-when the StatefulSet is created.  The full expanded PodSpec schema of the reference
-cannot be regenerated offline; the served versions, names, scope,
-subresource and status schema are identical.
+The CRD is the reference's, structurally equal per version: the full expanded ``core/v1``
+PodSpec schema (vendored as data, ``models/schema/podspec.json``) with
+``kf/config/crd/patches/validation_patches.yaml`` applied (containers ``minItems: 1``,
+required ``name``/``image``), three served versions, v1 storage, status subresource,
+``conversion: None`` (``models/crd.py``).
 """
 
 from __future__ import annotations
@@ -35,7 +33,7 @@ from typing import Dict, List
 
 import yaml
 
-from ..models.notebook import GPU_RESOURCE, VERSIONS
+from ..models.notebook import GPU_RESOURCE
 
 ROCM_NOTEBOOK_IMAGE = "rocm/pytorch:rocm7.0_ubuntu22.04_py3.10_pytorch_release_2.10.0"
 MANAGER_IMAGE = "quay.io/opendatahub/odh-kubeflow-amd:latest"
@@ -45,70 +43,11 @@ KUBE_RBAC_PROXY_IMAGE = "quay.io/brancz/kube-rbac-proxy:v0.18.1"
 # ------------------------------------------------------------------ CRD
 
 
-def _status_schema() -> dict:
-    state = {"type": "object", "x-kubernetes-preserve-unknown-fields": True}
-    return {
-        "type": "object",
-        "description": "NotebookStatus defines the observed state of Notebook",
-        "properties": {
-            "conditions": {
-                "type": "array",
-                "description": "Conditions is an array of current conditions",
-                "items": {"type": "object", "required": ["type"], "properties": {
-                    "type": {"type": "string", "description": "Type is the type of the condition. Possible values "
-                                                                "are Running|Waiting|Terminated"},
-                    "status": {"type": "string", "description": "Status of the condition, one of True, False, "
-                                                                  "Unknown."},
-                    "lastProbeTime": {"type": "string", "format": "date-time",
-                                      "description": "Last time we probed the condition."},
-                    "lastTransitionTime": {"type": "string", "format": "date-time",
-                                           "description": "Last time the condition transitioned from one status to "
-                                                          "another."},
-                    "reason": {"type": "string", "description": "(brief) reason the container is in the current "
-                                                                  "state"},
-                    "message": {"type": "string", "description": "Message regarding why the container is in the "
-                                                                   "current state."}}}},
-            "readyReplicas": {"type": "integer", "format": "int32",
-                              "description": "ReadyReplicas is the number of Pods created by the StatefulSet "
-                                             "controller that have a Ready Condition."},
-            "containerState": {"type": "object", "description": "ContainerState is the state of underlying "
-                                                                   "container.",
-                               "properties": {"running": state, "terminated": state, "waiting": state}},
-        },
-        "required": ["conditions", "containerState", "readyReplicas"],
-    }
-
-
-def _spec_schema() -> dict:
-    container = {"type": "object", "required": ["name", "image"], "x-kubernetes-preserve-unknown-fields": True,
-                 "properties": {"name": {"type": "string"}, "image": {"type": "string"}}}
-    return {
-        "type": "object",
-        "description": "NotebookSpec defines the desired state of Notebook",
-        "properties": {"template": {"type": "object", "properties": {"spec": {
-            "type": "object", "x-kubernetes-preserve-unknown-fields": True, "required": ["containers"],
-            "properties": {"containers": {"type": "array", "minItems": 1, "items": container}}}}}},
-    }
-
-
 def notebook_crd() -> dict:
-    versions = []
-    for v in ("v1", "v1alpha1", "v1beta1"):
-        versions.append({
-            "name": v, "served": True, "storage": v == "v1", "subresources": {"status": {}},
-            "schema": {"openAPIV3Schema": {
-                "type": "object", "description": "Notebook is the Schema for the notebooks API",
-                "properties": {"apiVersion": {"type": "string"}, "kind": {"type": "string"},
-                               "metadata": {"type": "object"}, "spec": _spec_schema(), "status": _status_schema()}}},
-        })
-    assert [x["name"] for x in versions] == sorted(VERSIONS, key=("v1", "v1alpha1", "v1beta1").index)
-    return {"apiVersion": "apiextensions.k8s.io/v1", "kind": "CustomResourceDefinition",
-            "metadata": {"name": "notebooks.kubeflow.org", "annotations": {"controller-gen.kubebuilder.io/version":
-                                                                            "odh-kubeflow-amd"}},
-            "spec": {"group": "kubeflow.org", "scope": "Namespaced", "conversion": {"strategy": "None"},
-                     "names": {"kind": "Notebook", "listKind": "NotebookList", "plural": "notebooks",
-                               "singular": "notebook"},
-                     "versions": versions}}
+    """``notebooks.kubeflow.org`` with the reference's full per-version schema (``models/crd.py``)."""
+    from ..models.crd import notebook_crd as crd
+
+    return crd()
 
 
 # ------------------------------------------------------------------ RBAC

@@ -58,6 +58,7 @@
 #include <mutex>
 #include <optional>
 #include <random>
+#include <regex>
 #include <set>
 #include <sstream>
 #include <thread>
@@ -722,19 +723,201 @@ std::string dump_out(const Res& r, const Value& o, const std::string& version) {
   return kj::dump(out_obj(r, o, version));
 }
 
-std::optional<std::string> validate(const Res& r, const Value& o) {
-  if (r.key != "notebooks.kubeflow.org") return std::nullopt;
-  const Value* cs = o.path({"spec", "template", "spec", "containers"});
-  if (!cs || !cs->is_arr() || cs->arr.empty())
-    return std::string("spec.template.spec.containers: Invalid value: should have at least 1 items");
-  for (size_t n = 0; n < cs->arr.size(); ++n) {
-    for (const char* f : {"name", "image"}) {
-      const Value* v = cs->arr[n].is_obj() ? cs->arr[n].get(f) : nullptr;
-      if (!v || !v->is_str() || v->s.empty())
-        return "spec.template.spec.containers[" + std::to_string(n) + "]." + f + ": Required value";
+// ------------------------------------------------------------------ CRD structural schemas
+// prune -> default -> validate on every write of a kind that has a schema (config key "schemas":
+// plural.group -> openAPIV3Schema; the notebooks.kubeflow.org one is the reference's full PodSpec
+// schema + validation_patches.yaml, generated by models/crd.py).  Same rules and error strings as
+// models/openapi.py.
+
+std::map<std::string, Value> g_schemas;
+
+const char* type_name(const Value& v) {
+  switch (v.t) {
+    case T::Null: return "null";
+    case T::Bool: return "boolean";
+    case T::Int: return "integer";
+    case T::Double: return "number";
+    case T::String: return "string";
+    case T::Array: return "array";
+    default: return "object";
+  }
+}
+
+std::string fmt_val(const Value& v) {
+  switch (v.t) {
+    case T::String: return "\"" + v.s + "\"";
+    case T::Bool: return v.b ? "true" : "false";
+    case T::Int: return std::to_string(v.i);
+    case T::Double: {
+      char b[64];
+      snprintf(b, sizeof(b), "%g", v.d);
+      return b;
+    }
+    case T::Null: return "null";
+    default: return std::string("\"") + type_name(v) + "\"";
+  }
+}
+
+bool schema_flag(const Value& s, const char* k) {
+  const Value* v = s.get(k);
+  return v && v->t == T::Bool && v->b;
+}
+
+bool type_ok(const Value& s, const Value& v) {
+  if (schema_flag(s, "x-kubernetes-int-or-string")) return v.t == T::Int || v.t == T::String;
+  std::string t = s.str_or("type");
+  if (t.empty()) return true;
+  if (t == "integer") return v.t == T::Int || (v.t == T::Double && v.d == (double)(int64_t)v.d);
+  if (t == "number") return v.t == T::Int || v.t == T::Double;
+  return t == type_name(v);
+}
+
+void schema_prune(const Value& s, Value& v, bool root) {
+  if (v.is_obj()) {
+    if (schema_flag(s, "x-kubernetes-preserve-unknown-fields")) return;
+    const Value* props = s.get("properties");
+    const Value* addl = s.get("additionalProperties");
+    bool addl_true = addl && addl->t == T::Bool && addl->b;
+    for (size_t n = 0; n < v.obj.size();) {
+      kj::Member& m = v.obj[n];
+      if (root && (m.k == "apiVersion" || m.k == "kind" || m.k == "metadata")) {
+        ++n;
+        continue;
+      }
+      const Value* sub = props ? props->get(m.k) : nullptr;
+      if (!sub && addl && addl->is_obj()) sub = addl;
+      if (!sub) {
+        if (!addl_true) {
+          v.obj.erase(v.obj.begin() + n);
+          continue;
+        }
+        ++n;
+        continue;
+      }
+      if (m.v.is_null() && !schema_flag(*sub, "nullable")) {
+        v.obj.erase(v.obj.begin() + n);
+        continue;
+      }
+      schema_prune(*sub, m.v, false);
+      ++n;
+    }
+  } else if (v.is_arr()) {
+    if (const Value* item = s.get("items"); item && item->is_obj())
+      for (auto& x : v.arr) schema_prune(*item, x, false);
+  }
+}
+
+void schema_default(const Value& s, Value& v) {
+  if (v.is_obj()) {
+    if (const Value* props = s.get("properties"); props && props->is_obj())
+      for (auto& p : props->obj) {
+        if (!v.get(p.k))
+          if (const Value* d = p.v.get("default")) v[p.k] = *d;
+        if (Value* x = v.get(p.k)) schema_default(p.v, *x);
+      }
+    if (const Value* addl = s.get("additionalProperties"); addl && addl->is_obj())
+      for (auto& m : v.obj) schema_default(*addl, m.v);
+  } else if (v.is_arr()) {
+    if (const Value* item = s.get("items"); item && item->is_obj())
+      for (auto& x : v.arr) schema_default(*item, x);
+  }
+}
+
+const std::regex& cached_regex(const std::string& pat) {
+  static std::mutex mu;
+  static std::map<std::string, std::unique_ptr<std::regex>> cache;
+  std::lock_guard<std::mutex> g(mu);
+  auto& slot = cache[pat];
+  if (!slot) slot = std::make_unique<std::regex>(pat, std::regex::ECMAScript | std::regex::optimize);
+  return *slot;
+}
+
+void schema_validate(const Value& s, const Value& v, const std::string& path, std::vector<std::string>& errs) {
+  if (!type_ok(s, v)) {
+    std::string want = schema_flag(s, "x-kubernetes-int-or-string") ? "integer or string" : s.str_or("type");
+    errs.push_back(path + ": Invalid value: " + fmt_val(v) + ": " + path + " in body must be of type " + want + ": \"" +
+                   type_name(v) + "\"");
+    return;
+  }
+  std::string fmt = s.str_or("format");
+  if ((fmt == "int32") && v.t == T::Int && (v.i < INT32_MIN || v.i > INT32_MAX))
+    errs.push_back(path + ": Invalid value: " + std::to_string(v.i) + ": " + path + " in body should be a valid int32");
+  if (const Value* en = s.get("enum"); en && en->is_arr()) {
+    bool ok = false;
+    for (auto& x : en->arr) ok = ok || x == v;
+    if (!ok) {
+      std::string l;
+      for (auto& x : en->arr) l += (l.empty() ? "" : ", ") + fmt_val(x);
+      errs.push_back(path + ": Unsupported value: " + fmt_val(v) + ": supported values: " + l);
     }
   }
-  return std::nullopt;
+  if (const Value* pat = s.get("pattern"); pat && pat->is_str() && v.is_str())
+    if (!std::regex_search(v.s, cached_regex(pat->s)))
+      errs.push_back(path + ": Invalid value: " + fmt_val(v) + ": " + path + " in body should match '" + pat->s + "'");
+  if (v.is_obj()) {
+    const Value* props = s.get("properties");
+    if (const Value* req = s.get("required"); req && req->is_arr())
+      for (auto& r : req->arr)
+        if (r.is_str() && !v.get(r.s)) errs.push_back((path.empty() ? "" : path + ".") + r.s + ": Required value");
+    const Value* addl = s.get("additionalProperties");
+    for (auto& m : v.obj) {
+      const Value* sub = props ? props->get(m.k) : nullptr;
+      if (!sub && addl && addl->is_obj()) sub = addl;
+      if (sub && !(path.empty() && m.k == "metadata")) schema_validate(*sub, m.v, path.empty() ? m.k : path + "." + m.k, errs);
+    }
+  } else if (v.is_arr()) {
+    if (const Value* mi = s.get("minItems"); mi && mi->t == T::Int && (int64_t)v.arr.size() < mi->i)
+      errs.push_back(path + ": Invalid value: " + std::to_string(v.arr.size()) + ": " + path + " in body should have at least " +
+                     std::to_string(mi->i) + " items");
+    if (const Value* ma = s.get("maxItems"); ma && ma->t == T::Int && (int64_t)v.arr.size() > ma->i)
+      errs.push_back(path + ": Too many: " + std::to_string(v.arr.size()) + ": must have at most " + std::to_string(ma->i) + " items");
+    std::string lt = s.str_or("x-kubernetes-list-type");
+    if (lt == "set") {
+      for (size_t i = 0; i < v.arr.size(); ++i)
+        for (size_t j = 0; j < i; ++j)
+          if (v.arr[j] == v.arr[i]) {
+            errs.push_back(path + "[" + std::to_string(i) + "]: Duplicate value: " + fmt_val(v.arr[i]));
+            break;
+          }
+    } else if (lt == "map") {
+      const Value* keys = s.get("x-kubernetes-list-map-keys");
+      for (size_t i = 0; keys && keys->is_arr() && i < v.arr.size(); ++i)
+        for (size_t j = 0; j < i; ++j) {
+          bool same = v.arr[i].is_obj() && v.arr[j].is_obj();
+          for (auto& k : keys->arr) {
+            if (!same) break;
+            const Value* a = v.arr[i].get(k.s);
+            const Value* b = v.arr[j].get(k.s);
+            same = (!a && !b) || (a && b && *a == *b);
+          }
+          if (same) {
+            std::string d;
+            for (auto& k : keys->arr) {
+              const Value* a = v.arr[i].get(k.s);
+              d += (d.empty() ? "" : ", ") + std::string("\"") + k.s + "\":" + (a ? fmt_val(*a) : "null");
+            }
+            errs.push_back(path + "[" + std::to_string(i) + "]: Duplicate value: {" + d + "}");
+            break;
+          }
+        }
+    }
+    if (const Value* item = s.get("items"); item && item->is_obj())
+      for (size_t i = 0; i < v.arr.size(); ++i) schema_validate(*item, v.arr[i], path + "[" + std::to_string(i) + "]", errs);
+  }
+}
+
+std::optional<std::string> validate(const Res& r, Value& o) {
+  auto it = g_schemas.find(r.key);
+  if (it == g_schemas.end()) return std::nullopt;
+  schema_prune(it->second, o, true);
+  schema_default(it->second, o);
+  std::vector<std::string> errs;
+  schema_validate(it->second, o, "", errs);
+  if (errs.empty()) return std::nullopt;
+  if (errs.size() == 1) return errs[0];
+  std::string all = "[";
+  for (size_t n = 0; n < errs.size(); ++n) all += (n ? ", " : "") + errs[n];
+  return all + "]";
 }
 
 // ------------------------------------------------------------------ kube-apiserver defaulting
@@ -1654,6 +1837,7 @@ Obj do_update(const Res& r, const std::string& ns, const std::string& name, Valu
     else merged.erase("status");
     mdm(merged)["resourceVersion"] = Value::str(mget(nw, "resourceVersion"));
     nw = std::move(merged);
+    if (auto err = validate(r, nw)) throw Invalid(r.kind + "." + r.group, name, *err);
   } else {
     if (r.status) {
       if (const Value* st = cur->get("status")) nw["status"] = *st;
@@ -1692,6 +1876,7 @@ Obj do_patch_once(const Res& r, const std::string& ns, const std::string& name, 
     merged["status"] = st ? *st : Value();
     mdm(merged)["resourceVersion"] = Value::str(mget(nw, "resourceVersion"));
     nw = std::move(merged);
+    if (auto err = validate(r, nw)) throw Invalid(r.kind + "." + r.group, name, *err);
   } else {
     if (r.status) {
       if (const Value* st = cur->get("status")) nw["status"] = *st;
@@ -2461,6 +2646,8 @@ void load_config(const std::string& path) {
   }
   if (const Value* v = cfg.get("gc")) S.gc = v->b;
   if (const Value* v = cfg.get("defaulting")) S.defaulting = v->b;
+  if (const Value* v = cfg.get("schemas"); v && v->is_obj())
+    for (auto& m : v->obj) g_schemas[m.k] = m.v;
   if (const Value* v = cfg.get("history"))
     if (v->t == T::Int) S.history = (size_t)v->i;
   g_token = cfg.str_or("token");

@@ -238,9 +238,14 @@ def test_processes_notebook_lifecycle_like_reference_e2e(tmp_path, run):
                 s = await c.get(kinds.STATEFUL_SET, "e2e-nb", "e2e")
                 return stop and stop != "odh-notebook-controller-lock" and s["spec"]["replicas"] == 0
             await eventually(culled, 30)
+
+            # a stopped notebook loses its activity annotations on the culler's next pass
+            # (culling_controller.go:104-117) — that pass follows the STOP write, so wait for it
+            async def stripped():
+                nb = await c.get(kinds.NOTEBOOK, "e2e-nb", "e2e")
+                return "notebooks.kubeflow.org/last-activity" not in m.annotations(nb)
+            await eventually(stripped, 30)
             nb = await c.get(kinds.NOTEBOOK, "e2e-nb", "e2e")
-            # a stopped notebook carries no activity annotations (culling_controller.go:104-117)
-            assert "notebooks.kubeflow.org/last-activity" not in m.annotations(nb)
 
             # update (notebook_update_test.go): resume with a new image → STS rolls
             nb["metadata"]["annotations"].pop("kubeflow-resource-stopped")

@@ -130,6 +130,7 @@ async def run_local(args, n_gpus: int, probe) -> dict:
 
         gctune.tune()  # start-up heap out of the cyclic collector's reach (see utils/gctune.py)
         r0 = cl.reconcile_count()
+        b0 = cl.reconcile_breakdown()
         t_start = time.perf_counter()
         for _ in range(args.steps):
             await one_step(True)
@@ -138,9 +139,31 @@ async def run_local(args, n_gpus: int, probe) -> dict:
         await cl.settle(5)
         elapsed = time.perf_counter() - t_start
         recon = cl.reconcile_count() - r0
+        breakdown = breakdown_delta(b0, cl.reconcile_breakdown())
         probes = [p for g in cl.gpu_runtimes for p in g.probe_results]
     return {"elapsed": elapsed, "reconciles": recon, "lat_ms": lat_ms, "odh": use_odh, "probes": probes,
-            "teardown_ms": teardown_ms}
+            "teardown_ms": teardown_ms, "breakdown": breakdown}
+
+
+def breakdown_delta(b0: dict, b1: dict) -> dict:
+    """Reconciles per controller and triggering watch kind between two snapshots."""
+    out = {}
+    for ctrl, trig in b1.items():
+        d = {k: v - b0.get(ctrl, {}).get(k, 0) for k, v in trig.items()}
+        d = {k: v for k, v in d.items() if v}
+        if d:
+            out[ctrl] = d
+    return out
+
+
+def merge_breakdowns(parts) -> dict:
+    out: dict = {}
+    for b in parts:
+        for ctrl, trig in (b or {}).items():
+            o = out.setdefault(ctrl, {})
+            for k, v in trig.items():
+                o[k] = o.get(k, 0) + v
+    return out
 
 
 def _odh_available() -> bool:
@@ -237,6 +260,13 @@ def report(args, n, res) -> dict:
         "notebooks_ready_per_s": round(len(lat) / el, 3) if el > 0 else None,
         "reconciles_per_notebook": round(res["reconciles"] / max(1, len(lat)), 2),
     }
+    if res.get("breakdown"):
+        # per controller: reconciles per notebook, split by the watch kind that queued them
+        nbs = max(1, len(lat))
+        out["reconciles_per_notebook_by_controller"] = {
+            ctrl: {"total": round(sum(t.values()) / nbs, 2),
+                   "by_trigger": {k: round(v / nbs, 2) for k, v in sorted(t.items(), key=lambda kv: -kv[1])}}
+            for ctrl, t in sorted(res["breakdown"].items())}
     if getattr(args, "reference_emulation", False):
         # not the framework's numbers: the reference's serialising odh path, same harness
         out["config"]["reference_emulation"] = True

@@ -186,47 +186,32 @@ class LocalCluster:
         return self
 
     def _build_kf(self) -> None:
-        from .controllers.metrics import NotebookMetrics
-        from .controllers.notebook import NotebookEventReemitter, NotebookReconciler
+        from .controllers.setup import setup_kf
 
         kf = self.kf = self._mgr("notebook-controller", remote=True)
-        metrics = NotebookMetrics(kf.reader, kf.registry)
-        self.kf_metrics = metrics
-        emu = self.cfg.reference_emulation
-        r = NotebookReconciler(kf.client, kf.reader, kf.get_event_recorder_for("notebook-controller"), metrics,
-                               env=self.env, unconditional_status=emu, owner_index=not emu)
-        r.setup_with_manager(kf, max_concurrent=1 if emu else None)
-        self.reconcilers["notebook"] = r
-        if self.cfg.event_reemit:
-            e = NotebookEventReemitter(kf.client, kf.reader, kf.get_event_recorder_for("notebook-controller"))
-            e.setup_with_manager(kf, max_concurrent=1 if emu else None)
-            self.reconcilers["events"] = e
-        if self.cfg.culler or self.env.get("ENABLE_CULLING") == "true":
-            from .controllers.culling import CullingReconciler
+        culling = bool(self.cfg.culler or self.env.get("ENABLE_CULLING") == "true")
+        activity = self.cfg.activity_source
+        if culling and activity is None and self.node_agents:
+            from .controllers.culling import NodeAgentActivity
 
-            activity = self.cfg.activity_source
-            if activity is None and self.node_agents:
-                from .controllers.culling import NodeAgentActivity
-
-                # every fake node's pods report hostIP 127.0.0.1: route by node name instead
-                ports = {n: a.port for n, a in self.node_agents.items()}
-                activity = NodeAgentActivity(endpoint_for=lambda pod: "127.0.0.1:%d" % ports[
-                    (pod.get("spec") or {}).get("nodeName")] if (pod.get("spec") or {}).get("nodeName") in ports
-                    else None)
-            c = CullingReconciler(kf.client, kf.reader, metrics, env=self.env, activity=activity)
-            c.setup_with_manager(kf, max_concurrent=1 if emu else None)
-            self.reconcilers["culler"] = c
+            # every fake node's pods report hostIP 127.0.0.1: route by node name instead
+            ports = {n: a.port for n, a in self.node_agents.items()}
+            activity = NodeAgentActivity(endpoint_for=lambda pod: "127.0.0.1:%d" % ports[
+                (pod.get("spec") or {}).get("nodeName")] if (pod.get("spec") or {}).get("nodeName") in ports
+                else None)
+        out = setup_kf(kf, self.env, culling=culling, activity=activity, event_reemit=self.cfg.event_reemit,
+                       reference_emulation=self.cfg.reference_emulation)
+        self.kf_metrics = out["metrics"]
+        for k in ("notebook", "events", "culler"):
+            if k in out:
+                self.reconcilers[k] = out[k]
 
     def _build_odh(self) -> None:
-        from .controllers.odh.reconciler import OpenshiftNotebookReconciler
+        from .controllers.setup import setup_odh
 
         odh = self.odh = self._mgr("odh-notebook-controller", remote=True, uncached=(kinds.CONFIG_MAP, kinds.SECRET))
-        emu = self.cfg.reference_emulation
-        r = OpenshiftNotebookReconciler(odh.client, odh.reader, self.cfg.controller_namespace, env=self.env,
-                                        recorder=odh.get_event_recorder_for("odh-notebook-controller"),
-                                        blocking_lock_removal=emu)
-        r.setup_with_manager(odh, max_concurrent=1 if emu else None)
-        self.reconcilers["odh"] = r
+        self.reconcilers["odh"] = setup_odh(odh, self.cfg.controller_namespace, self.env,
+                                            reference_emulation=self.cfg.reference_emulation)
 
     async def _start_webhook(self) -> None:
         from .webhook.notebook_webhook import NotebookWebhook, register_in_process
@@ -317,6 +302,13 @@ class LocalCluster:
 
     def reconcile_count(self) -> int:
         return sum(mgr.reconcile_count() for mgr in (self.kf, self.odh) if mgr is not None)
+
+    def reconcile_breakdown(self) -> dict:
+        out: dict = {}
+        for mgr in (self.kf, self.odh):
+            if mgr is not None:
+                out.update(mgr.reconcile_breakdown())
+        return out
 
     async def __aenter__(self):
         return await self.start()

@@ -52,3 +52,29 @@ class ServerRunnable:
 
     async def stop(self):
         await self._stop()
+
+
+def add_shard_flags(p) -> None:
+    """``--shard``: run as one namespace shard of the control plane (see ``cmd/control_plane.py``)."""
+    p.add_argument("--shard", default=None,
+                   help="serve only namespaces labelled notebooks.amd.com/shard=<SHARD> (+ the controller "
+                        "namespace); 'ordinal' takes it from the StatefulSet pod name (POD_NAME/HOSTNAME -<n>)")
+
+
+def resolve_shard(value, env=None):
+    """The shard id for ``--shard`` (None: unsharded, the reference's cluster-wide manager)."""
+    import os
+    import re
+
+    env = os.environ if env is None else env
+    if value is None or value == "":
+        return None
+    if value == "ordinal":
+        name = env.get("POD_NAME") or env.get("HOSTNAME") or ""
+        mo = re.search(r"-(\d+)$", name)
+        if not mo:
+            raise SystemExit(f"--shard=ordinal: cannot read a StatefulSet ordinal from pod name {name!r}")
+        return mo.group(1)
+    if not re.fullmatch(r"[A-Za-z0-9]([-A-Za-z0-9_.]*[A-Za-z0-9])?", value) or len(value) > 63:
+        raise SystemExit(f"--shard={value!r} is not a valid label value")
+    return value

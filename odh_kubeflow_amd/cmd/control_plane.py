@@ -1,0 +1,176 @@
+"""One process running the whole notebook control plane, optionally as one namespace shard.
+
+    python -m odh_kubeflow_amd.cmd.control_plane --shard 3 \\
+        --kube-rbac-proxy-image quay.io/brancz/kube-rbac-proxy:v0.18.1
+
+The reference deploys two managers for the whole cluster: the kf notebook-controller
+(``kf/main.go``: NotebookReconciler + optional culler) and the odh-notebook-controller
+(``odh/main.go``: OpenshiftNotebookReconciler + the mutating webhook).  Both are
+available unchanged (``cmd/kf_manager.py``, ``cmd/odh_manager.py``).  This process runs
+all of it in one manager — one informer cache, one REST connection pool, one set of
+watches — and with ``--shard K`` it owns only the namespaces labelled
+``notebooks.amd.com/shard=K`` (``controllers/sharding.py``), so N shards split the
+cluster's notebooks with constant per-shard watch traffic.  The ``mi355x-sharded``
+overlay runs it as a StatefulSet (``--shard=ordinal``: replica k is shard k, one per
+MI355X of an 8-GPU node) with one MutatingWebhookConfiguration and Service per shard;
+the headline benchmark (``bench.py`` → ``parallel/bench_dist.py``) launches exactly
+this command, one per rank.
+
+Flags are the union of the two reference managers' (odh spellings:
+``--metrics-bind-address``, ``--health-probe-bind-address``, ``--leader-elect``,
+``--kube-rbac-proxy-image``, ``--webhook-cert-dir``, ``--webhook-port``), plus
+``--controllers``, ``--shard``, ``--shard-count``/``--assign-namespaces``.  Once the
+caches are synced, the controllers are running and the webhook serves, it prints
+``ready`` on stdout (the readiness handshake the benchmark and the e2e tests use).
+"""
+
+from __future__ import annotations
+
+import argparse
+import asyncio
+import logging
+import os
+import sys
+from typing import List, Optional
+
+log = logging.getLogger("setup")
+
+ALL_CONTROLLERS = ("kf", "odh", "webhook")
+
+
+def parse(argv: Optional[List[str]] = None) -> argparse.Namespace:
+    from .common import add_shard_flags
+
+    p = argparse.ArgumentParser(prog="notebook-control-plane")
+    p.add_argument("--controllers", default="kf,odh,webhook",
+                   help="comma list of kf (notebook + event re-emitter + culler when ENABLE_CULLING=true), "
+                        "odh (OpenshiftNotebookReconciler), webhook (odh mutating webhook)")
+    add_shard_flags(p)
+    p.add_argument("--shard-count", type=int, default=0, help="number of shards (for --assign-namespaces)")
+    p.add_argument("--assign-namespaces", action="store_true",
+                   help="shard 0 labels unlabelled namespaces crc32(name) %% --shard-count")
+    p.add_argument("--metrics-bind-address", default=":8080")
+    p.add_argument("--health-probe-bind-address", default=":8081")
+    p.add_argument("--kube-rbac-proxy-image", default="")
+    p.add_argument("--webhook-cert-dir", default="/tmp/k8s-webhook-server/serving-certs")
+    p.add_argument("--webhook-port", type=int, default=8443)
+    p.add_argument("--webhook-host", default="0.0.0.0")
+    p.add_argument("--webhook-cert-reload-seconds", type=float, default=10.0)
+    p.add_argument("--leader-elect", action="store_true")
+    p.add_argument("--leader-election-namespace", default="")
+    p.add_argument("--leader-election-lease-duration", type=float, default=15.0)
+    p.add_argument("--leader-election-renew-deadline", type=float, default=10.0)
+    p.add_argument("--leader-election-retry-period", type=float, default=2.0)
+    p.add_argument("--debug-log", action="store_true")
+    p.add_argument("--kubeconfig", default=None)
+    p.add_argument("--master", default=None)
+    p.add_argument("--qps", type=float, default=0.0)
+    p.add_argument("--burst", type=int, default=0)
+    p.add_argument("--max-concurrent-reconciles", type=int, default=8)
+    p.add_argument("--cache-configmaps-secrets", choices=("auto", "true", "false"), default="auto",
+                   help="cache ConfigMap/Secret data (auto: when sharded — a shard's cache spans few namespaces; "
+                        "unsharded keeps the reference's uncached, data-stripped reads, odh/main.go:165-185)")
+    p.add_argument("--reference-emulation", action="store_true", help=argparse.SUPPRESS)  # same-harness comparisons
+    args = p.parse_args(argv)
+    args.controller_set = [c.strip() for c in args.controllers.split(",") if c.strip()]
+    bad = [c for c in args.controller_set if c not in ALL_CONTROLLERS]
+    if bad:
+        p.error(f"unknown --controllers entries: {bad}")
+    if ("odh" in args.controller_set or "webhook" in args.controller_set) and not args.kube_rbac_proxy_image:
+        p.print_usage(sys.stderr)
+        raise SystemExit("missing required flag: --kube-rbac-proxy-image must be set")
+    if args.assign_namespaces and args.shard_count < 1:
+        p.error("--assign-namespaces needs --shard-count")
+    return args
+
+
+def build(args, env=os.environ):
+    from ..controllers.setup import setup_kf, setup_odh, shard_cache_options
+    from ..models import kinds
+    from ..runtime.informer import strip_data
+    from ..runtime.leaderelection import LeaderElector, namespace_from_env
+    from ..runtime.manager import Manager
+    from ..runtime.rest import RestClient, RestConfig
+    from .common import ServerRunnable, resolve_shard
+
+    shard = resolve_shard(args.shard, env)
+    cfg = RestConfig.load(args.master, args.kubeconfig)
+    if args.qps:
+        cfg.qps = float(args.qps)
+    if args.burst:
+        cfg.burst = args.burst
+    namespace = namespace_from_env()
+    cache_cm = args.cache_configmaps_secrets == "true" or (args.cache_configmaps_secrets == "auto" and shard is not None)
+    uncached, transforms = (), None
+    if not cache_cm:
+        uncached = (kinds.CONFIG_MAP, kinds.SECRET)
+        transforms = {kinds.CONFIG_MAP: strip_data, kinds.SECRET: strip_data}
+    elector = None
+    if args.leader_elect:
+        lease = "notebook-control-plane" + (f"-shard-{shard}" if shard is not None else "")
+        elector = LeaderElector(RestClient(cfg), lease, args.leader_election_namespace or namespace,
+                                lease_duration=args.leader_election_lease_duration,
+                                renew_deadline=args.leader_election_renew_deadline,
+                                retry_period=args.leader_election_retry_period)
+    name = "notebook-control-plane" + (f"-shard-{shard}" if shard is not None else "")
+    mgr = Manager.remote(cfg, name=name, uncached=uncached, transforms=transforms,
+                         cache_options=shard_cache_options(shard, namespace),
+                         default_max_concurrent=args.max_concurrent_reconciles, leader_elector=elector,
+                         metrics_addr=args.metrics_bind_address, probe_addr=args.health_probe_bind_address)
+    mgr.shard = shard
+    emu = args.reference_emulation
+    if "kf" in args.controller_set:
+        mgr.kf_reconcilers = setup_kf(mgr, env, reference_emulation=emu)
+    if "odh" in args.controller_set:
+        mgr.odh_reconciler = setup_odh(mgr, namespace, env, shard=shard, reference_emulation=emu)
+    if args.assign_namespaces and shard in (None, "0"):
+        from ..controllers.sharding import NamespaceShardAssigner
+
+        mgr.assigner = NamespaceShardAssigner(mgr.client, mgr.reader, args.shard_count, exclude=[namespace])
+        mgr.assigner.setup_with_manager(mgr)
+    mgr.webhook_server = None
+    if "webhook" in args.controller_set:
+        from ..webhook.notebook_webhook import NotebookWebhook
+        from ..webhook.server import WebhookServer
+
+        missing = [f for f in ("tls.crt", "tls.key") if not os.path.exists(os.path.join(args.webhook_cert_dir, f))]
+        if missing:
+            raise SystemExit(f"webhook serving certificate missing in {args.webhook_cert_dir}: {', '.join(missing)} "
+                             "(OpenShift: service-ca; elsewhere: the odh-webhook-certs Job, cmd/webhook_certs.py)")
+        wh = NotebookWebhook(mgr.client, namespace, kube_rbac_proxy_image=args.kube_rbac_proxy_image, env=env)
+        server = WebhookServer(wh, args.webhook_cert_dir, args.webhook_host, args.webhook_port,
+                               reload_interval=args.webhook_cert_reload_seconds)
+        mgr.add(ServerRunnable(server.start, server.stop), needs_leader=False)
+        mgr.webhook_server = server
+    mgr.add_healthz_check("healthz")
+    mgr.add_readyz_check("readyz")
+    return mgr
+
+
+async def amain(argv=None) -> int:
+    from .common import setup_logging, signal_event
+
+    args = parse(argv)
+    setup_logging(debug=args.debug_log, development=args.debug_log)
+    mgr = build(args)
+    log.info("starting control plane %s (controllers: %s)", mgr.name, ",".join(args.controller_set))
+    stop = signal_event()
+
+    async def announce():
+        await mgr.started_event().wait()
+        await mgr.elected.wait()
+        print("ready", flush=True)
+
+    t = asyncio.ensure_future(announce())
+    try:
+        return await mgr.run_until(stop)
+    finally:
+        t.cancel()
+
+
+def main(argv=None) -> int:
+    return asyncio.run(amain(argv))
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -38,16 +38,20 @@ def parse(argv: Optional[List[str]] = None) -> argparse.Namespace:
     p.add_argument("--leader-election-lease-duration", type=float, default=15.0)
     p.add_argument("--leader-election-renew-deadline", type=float, default=10.0)
     p.add_argument("--leader-election-retry-period", type=float, default=2.0)
+    from .common import add_shard_flags
+
+    add_shard_flags(p)
     return p.parse_args(argv)
 
 
 def build(args, env=os.environ):
-    from ..controllers.metrics import NotebookMetrics
-    from ..controllers.notebook import NotebookEventReemitter, NotebookReconciler
+    from ..controllers.setup import setup_kf, shard_cache_options
     from ..runtime.leaderelection import LeaderElector, namespace_from_env
     from ..runtime.manager import Manager
     from ..runtime.rest import RestClient, RestConfig
+    from .common import resolve_shard
 
+    shard = resolve_shard(getattr(args, "shard", None), env)
     cfg = RestConfig.load(args.master, args.kubeconfig)
     if args.qps:
         cfg.qps = float(args.qps)
@@ -55,24 +59,16 @@ def build(args, env=os.environ):
         cfg.burst = args.burst
     elector = None
     if args.enable_leader_election:
-        elector = LeaderElector(RestClient(cfg), "kubeflow-notebook-controller",
+        elector = LeaderElector(RestClient(cfg), "kubeflow-notebook-controller" + (
+                                    f"-shard-{shard}" if shard is not None else ""),
                                 args.leader_election_namespace or namespace_from_env(),
                                 lease_duration=args.leader_election_lease_duration,
                                 renew_deadline=args.leader_election_renew_deadline,
                                 retry_period=args.leader_election_retry_period)
     mgr = Manager.remote(cfg, name="notebook-controller", default_max_concurrent=args.max_concurrent_reconciles,
-                         leader_elector=elector, metrics_addr=args.metrics_addr, probe_addr=args.probe_addr)
-    metrics = NotebookMetrics(mgr.reader, mgr.registry)
-    NotebookReconciler(mgr.client, mgr.reader, mgr.get_event_recorder_for("notebook-controller"), metrics,
-                       env=env).setup_with_manager(mgr)
-    NotebookEventReemitter(mgr.client, mgr.reader, mgr.get_event_recorder_for("notebook-controller")) \
-        .setup_with_manager(mgr)
-    if (env.get("ENABLE_CULLING") or "false") == "true":
-        from ..controllers.culling import CullingReconciler
-
-        CullingReconciler(mgr.client, mgr.reader, metrics, env=env).setup_with_manager(mgr)
-    else:
-        log.info("Culling of idle Pods is Disabled. To enable it set the ENV Var 'ENABLE_CULLING=true'")
+                         leader_elector=elector, metrics_addr=args.metrics_addr, probe_addr=args.probe_addr,
+                         cache_options=shard_cache_options(shard, namespace_from_env()))
+    mgr.kf_reconcilers = setup_kf(mgr, env)
     mgr.add_healthz_check("healthz")
     mgr.add_readyz_check("readyz")
     return mgr

@@ -37,6 +37,9 @@ def parse(argv: Optional[List[str]] = None) -> argparse.Namespace:
     p.add_argument("--kubeconfig", default=None)
     p.add_argument("--master", default=None)
     p.add_argument("--max-concurrent-reconciles", type=int, default=8)
+    from .common import add_shard_flags
+
+    add_shard_flags(p)
     args = p.parse_args(argv)
     if not args.kube_rbac_proxy_image:
         p.print_usage(sys.stderr)
@@ -45,7 +48,7 @@ def parse(argv: Optional[List[str]] = None) -> argparse.Namespace:
 
 
 def build(args, env=os.environ):
-    from ..controllers.odh.reconciler import OpenshiftNotebookReconciler
+    from ..controllers.setup import setup_odh, shard_cache_options
     from ..models import kinds
     from ..runtime.informer import strip_data
     from ..runtime.leaderelection import LeaderElector, namespace_from_env
@@ -53,18 +56,20 @@ def build(args, env=os.environ):
     from ..runtime.rest import RestClient, RestConfig
     from ..webhook.notebook_webhook import NotebookWebhook
     from ..webhook.server import WebhookServer
-    from .common import ServerRunnable
+    from .common import ServerRunnable, resolve_shard
 
+    shard = resolve_shard(getattr(args, "shard", None), env)
     cfg = RestConfig.load(args.master, args.kubeconfig)
     namespace = namespace_from_env()
     log.info("Controller is running in namespace %s", namespace)
-    elector = LeaderElector(RestClient(cfg), "odh-notebook-controller", namespace) if args.leader_elect else None
+    lease = "odh-notebook-controller" + (f"-shard-{shard}" if shard is not None else "")
+    elector = LeaderElector(RestClient(cfg), lease, namespace) if args.leader_elect else None
     mgr = Manager.remote(cfg, name="odh-notebook-controller", uncached=(kinds.CONFIG_MAP, kinds.SECRET),
                          transforms={kinds.CONFIG_MAP: strip_data, kinds.SECRET: strip_data},
                          default_max_concurrent=args.max_concurrent_reconciles, leader_elector=elector,
-                         metrics_addr=args.metrics_bind_address, probe_addr=args.health_probe_bind_address)
-    OpenshiftNotebookReconciler(mgr.client, mgr.reader, namespace, env=env,
-                                recorder=mgr.get_event_recorder_for("odh-notebook-controller")).setup_with_manager(mgr)
+                         metrics_addr=args.metrics_bind_address, probe_addr=args.health_probe_bind_address,
+                         cache_options=shard_cache_options(shard, namespace))
+    mgr.odh_reconciler = setup_odh(mgr, namespace, env, shard=shard)
     wh = NotebookWebhook(mgr.client, namespace, kube_rbac_proxy_image=args.kube_rbac_proxy_image, env=env)
     # controller-runtime's webhook server refuses to start without its serving cert; admission
     # (failurePolicy: Fail) is never offered over plain HTTP

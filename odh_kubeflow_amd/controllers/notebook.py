@@ -45,7 +45,7 @@ from ..models.notebook import (ANNOTATION_HEADERS_REQUEST_SET, ANNOTATION_NOTEBO
                                DEFAULT_CONTAINER_PORT, DEFAULT_FS_GROUP, DEFAULT_SERVING_PORT, GPU_RESOURCE,
                                MAX_STATEFULSET_NAME_LENGTH, NOTEBOOK_NAME_LABEL, PREFIX_ENV_VAR, STATEFULSET_LABEL,
                                STOP_ANNOTATION, WORKBENCH_LABEL, gpu_request, pod_cond_to_notebook_cond)
-from ..runtime.controller import Request, Result, pred_funcs
+from ..runtime.controller import Request, Result, controller_owner_alive, fields_changed, pred_funcs
 from ..utils.objutil import deepcopy_json
 from ..utils.reconcilehelper import copy_service_fields, copy_statefulset_fields, copy_virtual_service
 
@@ -280,7 +280,7 @@ def merge_status_timestamps(old: dict, new: dict) -> dict:
 
 class NotebookReconciler:
     def __init__(self, client, reader, recorder, metrics=None, env: Optional[Mapping[str, str]] = None,
-                 unconditional_status: bool = False, owner_index: bool = True):
+                 unconditional_status: bool = False, owner_index: bool = True, event_filters: bool = True):
         self.client = client
         self.reader = reader
         self.recorder = recorder
@@ -288,6 +288,7 @@ class NotebookReconciler:
         self.env = env if env is not None else os.environ
         self.unconditional_status = unconditional_status  # reference-emulation knob
         self.owner_index = owner_index
+        self.event_filters = event_filters  # False: reconcile on every event, as the reference
         self.status_writes = 0
 
     async def _find_statefulset(self, nb: dict, ns: str) -> Optional[dict]:
@@ -401,7 +402,23 @@ class NotebookReconciler:
     # -------------------------------------------------------------- wiring
 
     def setup_with_manager(self, mgr, max_concurrent: Optional[int] = None):
-        """``SetupWithManager`` (:778-826): For Notebook, Owns STS/Service, Pods by label."""
+        """``SetupWithManager`` (:778-826): For Notebook, Owns STS/Service, Pods by label.
+
+        The reference registers these watches without predicates, so every status write,
+        finalizer edit and child deletion queues a reconcile that finds nothing to do.
+        With ``event_filters`` each watch passes only the changes the reconcile reads:
+
+        * Notebook — spec (generation), labels, annotations (stop/restart/lock), creation;
+          not its own status writes, odh's finalizer edits, or deletion (nothing to do on
+          a deleting Notebook, :138-140; GC removes the children);
+        * StatefulSet — spec/metadata drift and ``status.readyReplicas`` (the only STS
+          status the Notebook status mirrors, :301-312); deletion only while its Notebook
+          is alive (drift → recreate);
+        * Service — the Notebook's own Service (name == Notebook name, :525-552), spec or
+          metadata drift; not odh's ``<nb>-kube-rbac-proxy`` Service it also controls;
+        * Pod — conditions / container statuses (what ``createNotebookStatus`` copies,
+          :315-374) and label moves; deletion only while the Notebook is alive.
+        """
 
         def map_pod(pod: dict):
             return [Request(m.namespace(pod), m.labels(pod)[NOTEBOOK_NAME_LABEL])]
@@ -409,11 +426,49 @@ class NotebookReconciler:
         def pod_is_labeled(etype, obj, old):
             return NOTEBOOK_NAME_LABEL in m.labels(obj)
 
-        b = (mgr.builder().named("notebook-controller").for_(NOTEBOOK_KIND)
-             .owns(kinds.STATEFUL_SET).owns(kinds.SERVICE)
-             .watches(kinds.POD, map_pod, [pod_is_labeled]))
+        nb_preds, sts_preds, svc_preds, pod_preds = [], [], [], [pod_is_labeled]
+        if self.event_filters:
+            reader = self.reader
+            drift = ("spec", "metadata.labels", "metadata.annotations", "metadata.ownerReferences")
+            nb_changed = fields_changed("metadata.generation", "metadata.labels", "metadata.annotations")
+            nb_preds = [pred_funcs(update=lambda o, old: not m.is_deleting(o) and nb_changed("MODIFIED", o, old),
+                                   delete=lambda o: False)]
+            sts_drift = fields_changed(*drift)
+
+            def sts_changed(etype, sts, old):
+                if etype != "MODIFIED" or old is None or sts_drift(etype, sts, old):
+                    return True
+                ready = lambda o: int(((o.get("status") or {}).get("readyReplicas")) or 0)  # noqa: E731
+                return ready(sts) != ready(old)
+            sts_preds = [sts_changed, controller_owner_alive(reader, NOTEBOOK_KIND)]
+
+            def own_service(etype, svc, old):
+                for r in (svc.get("metadata") or {}).get("ownerReferences") or []:
+                    if r.get("controller"):
+                        return r.get("name") == m.name(svc)
+                return False
+            svc_preds = [own_service, fields_changed(*drift), controller_owner_alive(reader, NOTEBOOK_KIND)]
+
+            def pod_nb_alive(etype, pod, old):
+                if etype != "DELETED":
+                    return True
+                nb = reader.get(NOTEBOOK_KIND, m.labels(pod).get(NOTEBOOK_NAME_LABEL, ""), m.namespace(pod))
+                return nb is not None and not m.is_deleting(nb)
+
+            def pod_status_known(etype, pod, old):
+                # a pod the StatefulSet controller just created has no status: nothing to mirror
+                return etype != "ADDED" or bool((pod.get("status") or {}).get("conditions"))
+            pod_preds += [fields_changed("status.conditions", "status.containerStatuses",
+                                         f"metadata.labels.{NOTEBOOK_NAME_LABEL}"),
+                          pod_nb_alive, pod_status_known]
+
+        b = (mgr.builder().named("notebook-controller").for_(NOTEBOOK_KIND, nb_preds)
+             .owns(kinds.STATEFUL_SET, sts_preds).owns(kinds.SERVICE, svc_preds)
+             .watches(kinds.POD, map_pod, pod_preds))
         if self.env.get("USE_ISTIO") == "true":
-            b.owns(kinds.VIRTUAL_SERVICE)
+            b.owns(kinds.VIRTUAL_SERVICE, [fields_changed("spec", "metadata.labels"),
+                                           controller_owner_alive(self.reader, NOTEBOOK_KIND)]
+                   if self.event_filters else [])
         if max_concurrent is not None:
             b.with_options(max_concurrent_reconciles=max_concurrent)
         return b.complete(self)

@@ -45,7 +45,7 @@ from typing import Dict, List, Mapping, Optional
 from ...models import kinds
 from ...models import meta as m
 from ...models.errors import ApiError, is_no_match, is_not_found
-from ...runtime.controller import Request, Result, generation_or_metadata_changed
+from ...runtime.controller import Request, Result, controller_owner_alive, generation_or_metadata_changed
 from ...runtime.retry import retry_on_conflict
 from ...tracing import get_tracer
 from . import auth, certs, dspa_secret, network, oauth, rbac, route, runtime_images
@@ -71,8 +71,10 @@ def reconciliation_lock_enabled(nb: dict) -> bool:
 
 class OpenshiftNotebookReconciler:
     def __init__(self, client, reader, namespace: str, env: Optional[Mapping[str, str]] = None, recorder=None,
-                 blocking_lock_removal: bool = False, store_info=None):
+                 blocking_lock_removal: bool = False, store_info=None,
+                 route_labels: Optional[Mapping[str, str]] = None):
         self.client = client
+        self.route_labels = dict(route_labels or {})  # sharded control plane: the shard's label
         self.reader = reader
         self.namespace = namespace  # central (controller) namespace
         self.env = env if env is not None else os.environ
@@ -191,7 +193,8 @@ class OpenshiftNotebookReconciler:
         if auth.kube_rbac_proxy_injection_enabled(nb):
             async def routes():
                 await route.ensure_conflicting_httproute_absent(c, nb, ns, True)
-                await route.reconcile_httproute(c, nb, ns, route.new_kube_rbac_proxy_httproute, self.env)
+                await route.reconcile_httproute(c, nb, ns, route.new_kube_rbac_proxy_httproute, self.env,
+                                                self.route_labels)
 
             steps += [auth.reconcile_notebook_service_account(c, nb), auth.reconcile_kube_rbac_proxy_crb(c, nb),
                       auth.reconcile_kube_rbac_proxy_configmap(c, nb), auth.reconcile_kube_rbac_proxy_service(c, nb),
@@ -199,7 +202,8 @@ class OpenshiftNotebookReconciler:
         else:
             async def routes():
                 await route.ensure_conflicting_httproute_absent(c, nb, ns, False)
-                await route.reconcile_httproute(c, nb, ns, route.new_notebook_httproute, self.env)
+                await route.reconcile_httproute(c, nb, ns, route.new_notebook_httproute, self.env,
+                                                self.route_labels)
 
             steps += [auth.cleanup_kube_rbac_proxy_crb(c, nb), routes()]
         if self.blocking_lock_removal:  # reference emulation: strictly sequential
@@ -275,8 +279,13 @@ class OpenshiftNotebookReconciler:
     # -------------------------------------------------------------- wiring
 
     def _first_notebook(self, namespace: str) -> List[Request]:
-        items = self.reader.list(NOTEBOOK_KIND, namespace)
-        return [Request(namespace, m.name(items[0]))] if items else []
+        """The reference maps namespace-wide objects to the namespace's first Notebook; a
+        Notebook being deleted needs none of them (its finalizer is what deletes the
+        shared ReferenceGrant), so the first live one is chosen."""
+        for nb in self.reader.list(NOTEBOOK_KIND, namespace):
+            if not m.is_deleting(nb):
+                return [Request(namespace, m.name(nb))]
+        return []
 
     def setup_with_manager(self, mgr, max_concurrent: Optional[int] = None):
         """``SetupWithManager`` (:707-855) — same watch fan-in, plus a status-write filter."""
@@ -307,12 +316,33 @@ class OpenshiftNotebookReconciler:
             return [Request(ns, m.name(nb)) for nb in self.reader.list(NOTEBOOK_KIND, ns)
                     if reconciliation_lock_enabled(nb) and self.pod_service_account(nb) == m.name(o)]
 
+        alive, svc_preds, route_preds, nb_preds = [], [], [], [generation_or_metadata_changed]
+        if not self.blocking_lock_removal:
+            # a deleted Notebook's finalizers already ran: its DELETED event has nothing left
+            nb_preds.append(lambda etype, o, old: etype != "DELETED")  # the reference-emulation runs keep every event
+            # GC of a deleted Notebook's children queues nothing; a child deleted under a live
+            # Notebook (drift) still does
+            alive = [controller_owner_alive(self.reader, NOTEBOOK_KIND)]
+
+            def proxy_service(etype, svc, old):  # not the kf Service <nb> the Notebook also controls
+                return m.name(svc).endswith(auth.KUBE_RBAC_PROXY_SERVICE_SUFFIX)
+            svc_preds = [proxy_service]
+
+            def route_nb_alive(etype, o, old):  # routes are deleted by this controller's finalizer
+                if etype != "DELETED":
+                    return True
+                lb = m.labels(o)
+                nb = self.reader.get(NOTEBOOK_KIND, lb.get("notebook-name", ""), lb.get("notebook-namespace", ""))
+                return nb is not None and not m.is_deleting(nb)
+            route_preds = [route_nb_alive]
+
         b = (mgr.builder().named("odh-notebook-controller")
-             .for_(NOTEBOOK_KIND, [generation_or_metadata_changed])
-             .owns(kinds.SERVICE_ACCOUNT).owns(kinds.SERVICE).owns(kinds.SECRET).owns(kinds.CONFIG_MAP)
-             .owns(kinds.NETWORK_POLICY).owns(kinds.ROLE_BINDING)
+             .for_(NOTEBOOK_KIND, nb_preds)
+             .owns(kinds.SERVICE_ACCOUNT, alive).owns(kinds.SERVICE, svc_preds + alive)
+             .owns(kinds.SECRET, alive).owns(kinds.CONFIG_MAP, alive)
+             .owns(kinds.NETWORK_POLICY, alive).owns(kinds.ROLE_BINDING, alive)
              .watches(kinds.SERVICE_ACCOUNT, map_sa)
-             .watches(kinds.HTTP_ROUTE, map_route)
+             .watches(kinds.HTTP_ROUTE, map_route, route_preds)
              .watches(kinds.REFERENCE_GRANT, map_refgrant)
              .watches(kinds.CONFIG_MAP, map_configmap))
         if max_concurrent is not None:

@@ -38,14 +38,17 @@ def route_labels(nb: dict) -> dict:
     return {"notebook-name": m.name(nb), "notebook-namespace": m.namespace(nb)}
 
 
-def new_notebook_httproute(nb: dict, central_namespace: str, env: Mapping[str, str] = os.environ) -> dict:
+def new_notebook_httproute(nb: dict, central_namespace: str, env: Mapping[str, str] = os.environ,
+                           extra_labels: Optional[Mapping[str, str]] = None) -> dict:
+    """``extra_labels``: the owning shard's label when the control plane is sharded (routes
+    live in the shared controller namespace; each shard watches only its own)."""
     ns, name = m.namespace(nb), m.name(nb)
     rname = f"nb-{ns}-{name}"
+    labels = {**route_labels(nb), **(extra_labels or {})}
     if len(rname) > HTTPROUTE_SUBDOMAIN_MAX_LEN:
-        md = {"generateName": f"nb-{ns[:10]}-{name[:10]}-", "namespace": central_namespace,
-              "labels": route_labels(nb)}
+        md = {"generateName": f"nb-{ns[:10]}-{name[:10]}-", "namespace": central_namespace, "labels": labels}
     else:
-        md = {"name": rname, "namespace": central_namespace, "labels": route_labels(nb)}
+        md = {"name": rname, "namespace": central_namespace, "labels": labels}
     gw_name = env.get("NOTEBOOK_GATEWAY_NAME") or DEFAULT_GATEWAY_NAME
     gw_ns = env.get("NOTEBOOK_GATEWAY_NAMESPACE") or DEFAULT_GATEWAY_NAMESPACE
     return {
@@ -60,8 +63,9 @@ def new_notebook_httproute(nb: dict, central_namespace: str, env: Mapping[str, s
     }
 
 
-def new_kube_rbac_proxy_httproute(nb: dict, central_namespace: str, env: Mapping[str, str] = os.environ) -> dict:
-    r = new_notebook_httproute(nb, central_namespace, env)
+def new_kube_rbac_proxy_httproute(nb: dict, central_namespace: str, env: Mapping[str, str] = os.environ,
+                                  extra_labels: Optional[Mapping[str, str]] = None) -> dict:
+    r = new_notebook_httproute(nb, central_namespace, env, extra_labels)
     br = r["spec"]["rules"][0]["backendRefs"][0]
     br["name"] = m.name(nb) + KUBE_RBAC_PROXY_SERVICE_SUFFIX
     br["port"] = KUBE_RBAC_PROXY_PORT
@@ -77,9 +81,10 @@ async def list_routes(client, nb: dict, central_namespace: str):
 
 
 async def reconcile_httproute(client, nb: dict, central_namespace: str,
-                              new_route: Callable[[dict, str, Mapping[str, str]], dict],
-                              env: Mapping[str, str] = os.environ) -> None:
-    desired = new_route(nb, central_namespace, env)
+                              new_route: Callable[..., dict],
+                              env: Mapping[str, str] = os.environ,
+                              extra_labels: Optional[Mapping[str, str]] = None) -> None:
+    desired = new_route(nb, central_namespace, env, extra_labels)
     items = await list_routes(client, nb, central_namespace)
     if len(items) > 1:
         raise RuntimeError("multiple HTTPRoutes found for notebook")

@@ -1,0 +1,86 @@
+"""Controller wiring shared by every process that runs the controllers.
+
+``cmd/kf_manager.py``, ``cmd/odh_manager.py``, ``cmd/control_plane.py`` (the sharded
+process the MI355X overlay deploys and the headline benchmark runs) and the in-process
+test cluster all register the reconcilers through these functions, so what is tested
+and benchmarked is wired exactly as what is deployed.
+
+Reference counterparts: ``kf/main.go:100-123`` (NotebookReconciler, optional
+CullingReconciler when ``ENABLE_CULLING=true``) and ``odh/main.go:202-227``
+(OpenshiftNotebookReconciler + the mutating webhook).
+
+``reference_emulation`` reproduces the reference's serialising behaviour for
+same-harness comparisons: one worker per controller, no watch predicates or own-write
+echo suppression, an unconditional status write per reconcile, a namespace List to find
+the StatefulSet, and the blocking 1 s + 5 s lock-removal backoff.
+"""
+
+from __future__ import annotations
+
+import logging
+import os
+from typing import Dict, Mapping, Optional
+
+log = logging.getLogger("setup")
+
+SHARD_LABEL = "notebooks.amd.com/shard"
+
+
+def setup_kf(mgr, env: Mapping[str, str] = os.environ, *, culling: Optional[bool] = None, activity=None,
+             event_reemit: bool = True, reference_emulation: bool = False) -> Dict[str, object]:
+    """kf manager controllers on ``mgr``: NotebookReconciler, the Pod/StatefulSet event
+    re-emitter and (``ENABLE_CULLING=true``) the CullingReconciler."""
+    from .metrics import NotebookMetrics
+    from .notebook import NotebookEventReemitter, NotebookReconciler
+
+    emu = reference_emulation
+    mgr.skip_own_write_echoes = not emu
+    one = 1 if emu else None
+    out: Dict[str, object] = {}
+    metrics = out["metrics"] = NotebookMetrics(mgr.reader, mgr.registry)
+    r = out["notebook"] = NotebookReconciler(mgr.client, mgr.reader, mgr.get_event_recorder_for("notebook-controller"),
+                                             metrics, env=env, unconditional_status=emu, owner_index=not emu,
+                                             event_filters=not emu)
+    r.setup_with_manager(mgr, max_concurrent=one)
+    if event_reemit:
+        e = out["events"] = NotebookEventReemitter(mgr.client, mgr.reader,
+                                                   mgr.get_event_recorder_for("notebook-controller"))
+        e.setup_with_manager(mgr, max_concurrent=one)
+    if culling is None:
+        culling = (env.get("ENABLE_CULLING") or "false") == "true"
+    if culling:
+        from .culling import CullingReconciler
+
+        c = out["culler"] = CullingReconciler(mgr.client, mgr.reader, metrics, env=env, activity=activity)
+        c.setup_with_manager(mgr, max_concurrent=one)
+    else:
+        log.info("Culling of idle Pods is Disabled. To enable it set the ENV Var 'ENABLE_CULLING=true'")
+    return out
+
+
+def setup_odh(mgr, namespace: str, env: Mapping[str, str] = os.environ, *, shard: Optional[str] = None,
+              reference_emulation: bool = False):
+    """The odh reconciler on ``mgr``.  ``shard``: label this shard's HTTPRoutes (they live in
+    the shared controller namespace) so each shard's cache selects only its own."""
+    from .odh.reconciler import OpenshiftNotebookReconciler
+
+    emu = reference_emulation
+    mgr.skip_own_write_echoes = not emu
+    r = OpenshiftNotebookReconciler(mgr.client, mgr.reader, namespace, env=env,
+                                    recorder=mgr.get_event_recorder_for("odh-notebook-controller"),
+                                    blocking_lock_removal=emu,
+                                    route_labels={SHARD_LABEL: shard} if shard is not None else None)
+    r.setup_with_manager(mgr, max_concurrent=1 if emu else None)
+    return r
+
+
+def shard_cache_options(shard: Optional[str], controller_namespace: str) -> dict:
+    """InformerCache keyword arguments for one shard: the namespaces labelled
+    ``notebooks.amd.com/shard=<shard>`` (followed live) plus the controller namespace, with
+    HTTPRoutes selected by the same label (``{}`` when not sharded: cluster-wide)."""
+    from ..models import kinds
+
+    if shard is None:
+        return {}
+    sel = f"{SHARD_LABEL}={shard}"
+    return {"namespace_selector": sel, "namespaces": [controller_namespace], "selectors": {kinds.HTTP_ROUTE: sel}}

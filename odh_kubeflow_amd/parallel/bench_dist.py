@@ -247,6 +247,7 @@ async def _drive(args, shard, dist, torch, children: Optional[dict] = None, nati
         torch.cuda.synchronize()
     await _in_thread(dist.barrier)
     r0 = shard.reconcile_count()
+    b0 = shard.reconcile_breakdown()
     children = children or {}
     child_cpu0 = {k: _proc_cpu_s(pid) for k, pid in children.items()}
     prof0 = await _apiserver_prof(native)
@@ -257,6 +258,9 @@ async def _drive(args, shard, dist, torch, children: Optional[dict] = None, nati
     own = time.perf_counter() - t_start  # this rank's own steps (the barrier below equalises elapsed)
     await shard.settle(5)  # the last teardown's trailing reconciles stay inside the timed region
     state["recon"] = shard.reconcile_count() - r0
+    from bench import breakdown_delta, merge_breakdowns  # noqa: E402  (bench.py is the entry point)
+
+    breakdown = breakdown_delta(b0, shard.reconcile_breakdown())
     # CPU time per step of every process on the path: where a step's work goes when ranks are added
     cpu = {"rank": time.process_time() - cpu0}
     prof = _prof_per_step(prof0, await _apiserver_prof(native), args.steps)
@@ -275,7 +279,8 @@ async def _drive(args, shard, dist, torch, children: Optional[dict] = None, nati
     await _in_thread(lambda: dist.all_reduce(rc, op=dist.ReduceOp.SUM))
     gathered = [None] * dist.get_world_size()
     await _in_thread(dist.all_gather_object, gathered, {"lat": lat_ms, "probes": shard.probe_results,
-                                                        "teardown": teardown_ms, "own_s": own, "cpu": cpu})
+                                                        "teardown": teardown_ms, "own_s": own, "cpu": cpu,
+                                                        "breakdown": breakdown})
     per_step = 1e3 / max(1, args.steps)
     cpu_ms = {"ranks": [round(g["cpu"]["rank"] * per_step, 3) for g in gathered]}
     for g in gathered:
@@ -287,4 +292,4 @@ async def _drive(args, shard, dist, torch, children: Optional[dict] = None, nati
             "probes": [p for g in gathered for p in g["probes"]],
             "teardown_ms": [x for g in gathered for x in g["teardown"]],
             "rank_ms_per_step": [round(g["own_s"] * per_step, 3) for g in gathered], "cpu_ms_per_step": cpu_ms,
-            "apiserver_profile_per_step": prof}
+            "apiserver_profile_per_step": prof, "breakdown": merge_breakdowns(g["breakdown"] for g in gathered)}

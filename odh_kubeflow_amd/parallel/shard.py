@@ -210,6 +210,13 @@ class ControlPlaneShard:
     def reconcile_count(self) -> int:
         return sum(mgr.reconcile_count() for mgr in (self.kf, self.odh) if mgr is not None)
 
+    def reconcile_breakdown(self) -> dict:
+        out: dict = {}
+        for mgr in (self.kf, self.odh):
+            if mgr is not None:
+                out.update(mgr.reconcile_breakdown())
+        return out
+
     async def settle(self, timeout: float = 10.0) -> bool:
         deadline = time.monotonic() + timeout
         quiet = 0

@@ -29,6 +29,10 @@ WatchCallback = Callable[[str, dict, Optional[dict]], None]
 # Set by ``retry_on_conflict`` for its retries: a Conflict means the informer copy is
 # stale, so the retry reads through to the apiserver instead of sleeping for the cache.
 LIVE_READS: contextvars.ContextVar = contextvars.ContextVar("live_reads", default=False)
+# (controller name, request) of the reconcile running in this task, set by the controller's
+# worker: writes made under it are remembered so their own watch echo does not queue the
+# same request again (see CachedClient.own_write)
+CURRENT_RECONCILE: contextvars.ContextVar = contextvars.ContextVar("current_reconcile", default=None)
 # how long a read of an object this client just wrote waits for the watch to deliver the
 # write before it reads through to the apiserver instead
 RYOW_WAIT_S = 0.05
@@ -218,6 +222,11 @@ class CachedClient(Client):
         self.uncached = {SCHEME.resolve(k).key for k in uncached}
         self._written: Dict[Tuple[str, str, str], int] = {}
         self._ensured: set = set()  # kinds whose informer is known synced and served
+        # (kind, namespace, name, resourceVersion) → (controller, request) that wrote it
+        self._own: Dict[Tuple[str, str, str, int], tuple] = {}
+        # (kind, namespace, name) → (controller, request) of a create / precondition update
+        # still awaiting its response (the watch event can overtake the response)
+        self._inflight: Dict[Tuple[str, str, str], tuple] = {}
         self.fresh_reads = 0
         self.cache_waits = 0
 
@@ -234,9 +243,47 @@ class CachedClient(Client):
         if len(self._written) > 16384:
             self._written.clear()
         self._written[key] = rv
+        cur = CURRENT_RECONCILE.get()
+        if cur is not None:
+            if len(self._own) > 16384:
+                self._own.clear()  # echoes never delivered (kinds nobody here watches)
+            self._own[key + (rv,)] = cur
 
-    def _live(self, kind) -> bool:
-        return SCHEME.resolve(kind).key in self.uncached
+    def own_write(self, obj: dict, controller: str):
+        """The request whose reconcile in ``controller`` produced exactly this object version
+        (its watch echo), else None.  That reconcile already acted on the state it wrote, so
+        the echo need not queue the request again — the informer-side counterpart of the
+        ``expectations`` kube-controller-manager's controllers keep for their own writes.
+        Only an identical resourceVersion matches: any later change by anyone is a new
+        event, and other controllers watching the object still see the echo."""
+        if not self._own and not self._inflight:
+            return None
+        rv = _rv_int(obj)
+        if rv is None:
+            return None
+        md = obj.get("metadata") or {}
+        try:
+            key = (SCHEME.resolve(obj).key, md.get("namespace") or "", md.get("name", ""), rv)
+        except Exception:
+            return None
+        hit = self._own.get(key)
+        if hit is None and self._inflight:
+            # The echo overtook the write's response.  Only creates and resourceVersion-
+            # preconditioned updates are tracked in flight: any other writer's event for the
+            # object in that window makes this write fail (AlreadyExists / Conflict), and the
+            # failed reconcile is retried with backoff anyway.
+            hit = self._inflight.get(key[:3])
+        # kept (not popped): a controller may watch the kind twice (Owns + Watches); the
+        # table is bounded and an entry can only ever match its own object version
+        return hit[1] if hit is not None and hit[0] == controller else None
+
+    def _live(self, kind, namespace: Optional[str] = None) -> bool:
+        if SCHEME.resolve(kind).key in self.uncached:
+            return True
+        # a namespace outside a namespace-restricted (sharded) cache is read live: the
+        # webhook admits objects of every namespace, whichever shard owns them
+        covers = getattr(self.reader, "covers", None)
+        return covers is not None and namespace is not None and not covers(kind, namespace)
 
     async def _ensure(self, kind) -> None:
         if type(kind) is str and kind in self._ensured:
@@ -248,7 +295,7 @@ class CachedClient(Client):
             self._ensured.add(kind)
 
     async def get(self, kind, name, namespace=None):
-        if self._live(kind) or LIVE_READS.get():
+        if self._live(kind, namespace) or LIVE_READS.get():
             return await self.writer.get(kind, name, namespace)
         await self._ensure(kind)
         o = self.reader.get(kind, name, namespace)
@@ -286,7 +333,7 @@ class CachedClient(Client):
         return o
 
     async def list(self, kind, namespace=None, labels=None, fields=None, owner_uid=None):
-        if self._live(kind) and owner_uid is None:
+        if self._live(kind, namespace) and owner_uid is None:
             return await self.writer.list(kind, namespace, labels, fields)
         await self._ensure(kind)
         items = [deepcopy_json(o) for o in self.reader.list(kind, namespace, labels, fields, owner_uid)]
@@ -297,13 +344,37 @@ class CachedClient(Client):
                 o["apiVersion"] = av
         return items
 
+    def _begin(self, obj) -> Optional[Tuple[str, str, str]]:
+        cur = CURRENT_RECONCILE.get()
+        if cur is None or not isinstance(obj, dict):
+            return None
+        md = obj.get("metadata") or {}
+        if not md.get("name"):
+            return None  # generateName: the key is unknown until the response
+        try:
+            key = (SCHEME.resolve(obj).key, md.get("namespace") or "", md["name"])
+        except Exception:
+            return None
+        self._inflight[key] = cur
+        return key
+
     async def create(self, obj):
-        out = await self.writer.create(obj)
+        key = self._begin(obj)
+        try:
+            out = await self.writer.create(obj)
+        finally:
+            if key is not None:
+                self._inflight.pop(key, None)
         self._note(out)
         return out
 
     async def update(self, obj):
-        out = await self.writer.update(obj)
+        key = self._begin(obj) if _rv_int(obj) is not None else None
+        try:
+            out = await self.writer.update(obj)
+        finally:
+            if key is not None:
+                self._inflight.pop(key, None)
         self._note(out)
         return out
 

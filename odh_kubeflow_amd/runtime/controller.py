@@ -17,10 +17,11 @@ import inspect
 import logging
 import time
 from dataclasses import dataclass
-from typing import Awaitable, Callable, Iterable, List, NamedTuple, Optional, Sequence
+from typing import Awaitable, Callable, Dict, Iterable, List, NamedTuple, Optional, Sequence
 
 from ..models import meta as m
 from ..models.scheme import SCHEME
+from .client import CURRENT_RECONCILE
 from .workqueue import ShutDown, WorkQueue
 
 log = logging.getLogger(__name__)
@@ -89,6 +90,46 @@ def generation_or_metadata_changed(etype: str, obj: dict, old: Optional[dict]) -
             or om.get("deletionTimestamp") != nm.get("deletionTimestamp"))
 
 
+def _path(obj: Optional[dict], path: str):
+    cur = obj
+    for part in path.split("."):
+        if not isinstance(cur, dict):
+            return None
+        cur = cur.get(part)
+    return cur
+
+
+def fields_changed(*paths: str) -> Predicate:
+    """Pass creates and deletes; pass an update only if one of the dotted ``paths``
+    (e.g. ``"status.readyReplicas"``, ``"metadata.labels"``) differs from the old object."""
+
+    def p(etype: str, obj: dict, old: Optional[dict]) -> bool:
+        if etype != "MODIFIED" or old is None:
+            return True
+        return any(_path(obj, x) != _path(old, x) for x in paths)
+
+    return p
+
+
+def controller_owner_alive(reader, owner_kind: str) -> Predicate:
+    """For delete events of owned objects: pass only while the controlling owner still
+    exists and is not being deleted.  Garbage collection of a deleted Notebook's children
+    then queues nothing, while the deletion of a child of a live Notebook (drift) still
+    triggers the repair.  Other event types pass."""
+    info = SCHEME.resolve(owner_kind)
+
+    def p(etype: str, obj: dict, old: Optional[dict]) -> bool:
+        if etype != "DELETED":
+            return True
+        for r in (obj.get("metadata") or {}).get("ownerReferences") or []:
+            if r.get("controller") and r.get("kind") == info.kind:
+                owner = reader.get(owner_kind, r.get("name", ""), m.namespace(obj))
+                return owner is not None and not m.is_deleting(owner) and m.uid(owner) == r.get("uid")
+        return True
+
+    return p
+
+
 # ------------------------------------------------------------------ handlers
 
 
@@ -140,42 +181,68 @@ class Controller:
         self.busy_time = 0.0
         self.active = 0
         self.on_reconcile: Optional[Callable[[str, Request, float, Optional[BaseException]], None]] = None
+        # which watch caused each reconcile: the kind of the event that first queued the
+        # request (later events for a queued request are deduplicated into the same run),
+        # or "requeue" for Result.requeue / RequeueAfter / error backoff
+        self._trigger: dict = {}
+        self.reconciles_by_trigger: Dict[str, int] = {}
+        # ``client.own_write`` of the manager's client: skip the watch echo of this
+        # controller's own write for the request that made it (False = reconcile on every
+        # event, as controller-runtime does; the reference-emulation runs use that)
+        self.own_writes: Optional[Callable[[dict, str], Optional[Request]]] = None
+        self.echoes_skipped = 0
 
     def watch(self, kind: str, map_fn: MapFunc, predicates: Sequence[Predicate] = ()) -> None:
         self.watches.append(_Watch(kind, map_fn, tuple(predicates)))
 
-    def enqueue(self, req: Request) -> None:
+    def enqueue(self, req: Request, trigger: str = "manual") -> None:
+        self._trigger.setdefault(req, trigger)
         self.queue.add(req)
 
     def _handler(self, w: _Watch):
+        try:
+            trig = SCHEME.resolve(w.kind).kind
+        except Exception:
+            trig = str(w.kind)
+
         def on_event(etype: str, obj: dict, old: Optional[dict]) -> None:
             for p in w.predicates:
                 if not p(etype, obj, old):
                     return
+            own = None
+            if etype != "DELETED" and self.own_writes is not None:
+                own = self.own_writes(obj, self.name)
             res = w.map_fn(obj)
             if inspect.isawaitable(res):
-                t = asyncio.ensure_future(self._enqueue_async(res))
+                t = asyncio.ensure_future(self._enqueue_async(res, trig))
                 self._map_tasks.add(t)
                 t.add_done_callback(self._map_tasks.discard)
                 return
             for r in res or ():
-                self.queue.add(r)
+                if own is not None and r == own:
+                    self.echoes_skipped += 1
+                    if self.metrics:
+                        self.metrics.child(self.metrics.echoes_skipped, self.name).inc()
+                    continue
+                self.enqueue(r, trig)
             # on updates that move an object away from its previous owner, also map the old one
             if etype == "MODIFIED" and old is not None and w.map_fn is not enqueue_for_object:
                 try:
                     olds = w.map_fn(old)
                     if not inspect.isawaitable(olds):
                         for r in olds or ():
-                            self.queue.add(r)
+                            if own is not None and r == own:
+                                continue
+                            self.enqueue(r, trig)
                 except Exception:
                     pass
 
         return on_event
 
-    async def _enqueue_async(self, aw) -> None:
+    async def _enqueue_async(self, aw, trig: str) -> None:
         try:
             for r in (await aw) or ():
-                self.queue.add(r)
+                self.enqueue(r, trig)
         except Exception:
             log.exception("%s: async map function failed", self.name)
 
@@ -215,11 +282,15 @@ class Controller:
             except ShutDown:
                 return
             self.active += 1
+            trig = self._trigger.pop(req, "requeue")
+            self.reconciles_by_trigger[trig] = self.reconciles_by_trigger.get(trig, 0) + 1
             if self.metrics:
                 self.metrics.child(self.metrics.active_workers, self.name).set(self.active)
+                self.metrics.child(self.metrics.reconcile_trigger, self.name, trig).inc()
             t0 = time.perf_counter()
             err: Optional[BaseException] = None
             res: Optional[Result] = None
+            tok = CURRENT_RECONCILE.set((self.name, req))
             try:
                 res = await self.reconcile(req)
             except asyncio.CancelledError:
@@ -227,6 +298,8 @@ class Controller:
                 raise
             except Exception as e:  # controller-runtime recovers panics into errors
                 err = e
+            finally:
+                CURRENT_RECONCILE.reset(tok)
             dt = time.perf_counter() - t0
             self.busy_time += dt
             self.reconciles += 1
@@ -306,6 +379,8 @@ class Builder:
         name = self._name or (SCHEME.resolve(self._for).kind.lower() if self._for else "controller")
         maxc = self._max if self._max is not None else self.mgr.default_max_concurrent
         c = Controller(name, fn, maxc, self._rate_limiter, self.mgr.runtime_metrics)
+        if getattr(self.mgr, "skip_own_write_echoes", True):
+            c.own_writes = getattr(self.mgr.client, "own_write", None)
         if self._for:
             c.watch(self._for, enqueue_for_object, self._for_preds)
         for w in self._watches:

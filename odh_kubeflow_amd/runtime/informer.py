@@ -206,72 +206,157 @@ class _Informer:
                 backoff = min(backoff * 2, 5.0)
 
 
+class _Group:
+    """The informers of one kind: one cluster-wide informer, or one per cached namespace
+    (the set follows the Namespace selector).  Watch handlers live here, shared by every
+    informer of the kind, so a namespace that joins later feeds existing subscriptions."""
+
+    def __init__(self, info: ResourceInfo, version: str):
+        self.info = info
+        self.version = version
+        self.infs: Dict[Optional[str], _Informer] = {}
+        self.handlers: Dict[int, Tuple[Optional[str], WatchCallback]] = {}
+
+    def all(self) -> List[_Informer]:
+        return list(self.infs.values())
+
+
 class InformerCache(Reader, EventSource):
     """Shared informers keyed by kind (and namespace, for a namespace-restricted cache).
 
     ``namespace`` restricts namespaced kinds to one namespace; ``namespaces`` to a set of
     them (one list/watch per namespace, merged for readers — controller-runtime's
-    ``cache.Options.DefaultNamespaces``).  ``selectors`` maps a kind to a label selector
-    applied server-side to its list/watch (``cache.Options.ByObject[..].Label``) so a
-    shard only ever receives the objects it owns.
+    ``cache.Options.DefaultNamespaces``).  ``namespace_selector`` makes that set dynamic:
+    a label-selected Namespace watch adds a namespace's informers when it starts matching
+    (a shard is assigned a namespace) and drops them, with DELETED events for what they
+    held, when it stops matching; ``namespaces`` are then always-cached extras (the
+    controller namespace).  ``selectors`` maps a kind to a label selector applied
+    server-side to its list/watch (``cache.Options.ByObject[..].Label``) so a shard only
+    ever receives the objects it owns.
     """
 
     def __init__(self, rest, namespace: Optional[str] = None, transforms: Optional[Dict[str, Optional[Transform]]] = None,
                  watch_timeout_s: int = 300, namespaces: Optional[Iterable[str]] = None,
-                 selectors: Optional[Dict[str, str]] = None):
+                 selectors: Optional[Dict[str, str]] = None, namespace_selector: Optional[str] = None):
         self.rest = rest
         self.namespace = namespace
         nss = list(namespaces) if namespaces is not None else ([namespace] if namespace else None)
-        self.namespaces: Optional[List[str]] = nss
+        self.static_namespaces: List[str] = list(nss or [])
+        self.namespace_selector = namespace_selector
+        # None = every namespace (cluster-wide informers)
+        self.namespaces: Optional[Set[str]] = set(nss) if (nss or namespace_selector) else None
         self.transforms: Dict[str, Optional[Transform]] = {}
         for k, fn in (transforms or {}).items():
             self.transforms[SCHEME.resolve(k).key] = fn
         self.selectors: Dict[str, str] = {SCHEME.resolve(k).key: v for k, v in (selectors or {}).items()}
         self.watch_timeout_s = watch_timeout_s
-        self._informers: Dict[Tuple[str, Optional[str]], _Informer] = {}
-        self._by_kind: Dict[str, List[_Informer]] = {}
-        self._by_ref: Dict[str, List[_Informer]] = {}
+        self._groups: Dict[str, _Group] = {}
+        self._by_ref: Dict[str, _Group] = {}
         self._hid = 0
+        self._ns_informer: Optional[_Informer] = None
+        self.namespace_changes = 0
 
-    def _group(self, kind) -> List[_Informer]:
+    # -------------------------------------------------------------- namespace membership
+
+    def _ensure_ns_informer(self) -> None:
+        if self.namespace_selector is None or self._ns_informer is not None:
+            return
+        info = SCHEME.resolve(kinds_namespace())
+        inf = _Informer(self, info, info.storage_version, None, self.namespace_selector)
+        inf.handlers = {0: (None, self._on_namespace)}
+        self._ns_informer = inf
+        inf.task = asyncio.ensure_future(inf.run())
+
+    def _on_namespace(self, etype: str, obj: dict, old: Optional[dict]) -> None:
+        ns = m.name(obj)
+        if ns in self.static_namespaces:
+            return
+        if etype == "DELETED" or m.is_deleting(obj):
+            if ns in self.namespaces:
+                self.namespaces.discard(ns)
+                self.namespace_changes += 1
+                for g in self._groups.values():
+                    inf = g.infs.pop(ns, None) if g.info.namespaced else None
+                    if inf is not None:
+                        self._retire(inf)
+        elif ns not in self.namespaces:
+            self.namespaces.add(ns)
+            self.namespace_changes += 1
+            for g in self._groups.values():
+                if g.info.namespaced:
+                    self._start_informer(g, ns)
+
+    def _retire(self, inf: _Informer) -> None:
+        """A namespace left the cache: stop its informer; to subscribers its objects are gone."""
+        if inf.task is not None:
+            inf.task.cancel()
+        for k in list(inf.items):
+            old = inf.items[k]
+            inf._delete(old)
+            inf._notify("DELETED", old, old)
+
+    def _start_informer(self, g: _Group, ns: Optional[str]) -> _Informer:
+        inf = _Informer(self, g.info, g.version, ns, self.selectors.get(g.info.key))
+        inf.handlers = g.handlers  # shared: subscriptions made earlier see this namespace too
+        g.infs[ns] = inf
+        inf.task = asyncio.ensure_future(inf.run())
+        return inf
+
+    def covers(self, kind, namespace: Optional[str]) -> bool:
+        """Whether reads of ``kind`` in ``namespace`` are served by this cache (False: the
+        caller must read live — the namespace belongs to another shard)."""
+        if self.namespaces is None or not namespace:
+            return True
+        if not SCHEME.resolve(kind).namespaced:
+            return True
+        return namespace in self.namespaces
+
+    # -------------------------------------------------------------- groups
+
+    def _group(self, kind) -> _Group:
         if type(kind) is str:
             hit = self._by_ref.get(kind)
             if hit is not None:
                 return hit
         info = SCHEME.resolve(kind)
-        infs = self._by_kind.get(info.key)
-        if infs is None:
+        g = self._groups.get(info.key)
+        if g is None:
             from .client import _version_of
 
-            version = _version_of(kind) or info.storage_version
-            nss = self.namespaces if (info.namespaced and self.namespaces) else [None]
-            infs = []
-            for ns in nss:
-                inf = _Informer(self, info, version, ns, self.selectors.get(info.key))
-                self._informers[(info.key, ns)] = inf
-                inf.task = asyncio.ensure_future(inf.run())
-                infs.append(inf)
-            self._by_kind[info.key] = infs
+            self._ensure_ns_informer()
+            g = self._groups[info.key] = _Group(info, _version_of(kind) or info.storage_version)
+            if info.namespaced and self.namespaces is not None:
+                for ns in sorted(self.namespaces):
+                    self._start_informer(g, ns)
+            else:
+                self._start_informer(g, None)
         if type(kind) is str:
-            self._by_ref[kind] = infs
-        return infs
+            self._by_ref[kind] = g
+        return g
 
     def _for_ns(self, kind, namespace: Optional[str]) -> List[_Informer]:
-        infs = self._group(kind)
-        if namespace and len(infs) > 1:
-            return [i for i in infs if i.namespace == namespace]
-        return infs
+        g = self._group(kind)
+        if namespace and g.info.namespaced and self.namespaces is not None:
+            inf = g.infs.get(namespace)
+            return [inf] if inf is not None else []
+        return g.all()
 
     def informer(self, kind) -> _Informer:
         """The (first) informer of ``kind`` — for single-namespace / cluster-wide caches."""
-        return self._group(kind)[0]
+        return self._group(kind).all()[0]
+
+    async def _ns_synced(self, timeout: float) -> None:
+        self._ensure_ns_informer()
+        if self._ns_informer is not None and not self._ns_informer.synced.is_set():
+            await asyncio.wait_for(self._ns_informer.synced.wait(), timeout)
 
     async def ensure_informer(self, kind, timeout: float = 30.0) -> None:
-        infs = self._group(kind)
+        await self._ns_synced(timeout)
+        infs = self._group(kind).all()
         for inf in infs:
             if not inf.synced.is_set():
                 await asyncio.wait_for(inf.synced.wait(), timeout)
-        if all(inf.missing_kind for inf in infs):
+        if infs and all(inf.missing_kind for inf in infs):
             from ..models.errors import NoKindMatch
 
             raise NoKindMatch(infs[0].info.kind)
@@ -279,27 +364,28 @@ class InformerCache(Reader, EventSource):
     # -------------------------------------------------------------- EventSource
 
     def subscribe(self, kind, callback, namespace=None):
-        infs = self._for_ns(kind, namespace)
+        g = self._group(kind)
         self._hid += 1
         hid = self._hid
-        for inf in infs:
+        for inf in self._for_ns(kind, namespace):
             for o in list(inf.items.values()):
                 if namespace and m.namespace(o) != namespace:
                     continue
                 callback("ADDED", o, None)
-            inf.handlers[hid] = (namespace, callback)
+        g.handlers[hid] = (namespace, callback)
 
         def cancel():
-            for inf in infs:
-                inf.handlers.pop(hid, None)
+            g.handlers.pop(hid, None)
         return cancel
 
     async def wait_synced(self, kinds: Iterable, timeout: float = 30.0) -> None:
+        await self._ns_synced(timeout)
+
         async def one(inf):
             if not inf.synced.is_set():
                 await asyncio.wait_for(inf.synced.wait(), timeout)
 
-        await asyncio.gather(*(one(inf) for k in kinds for inf in self._group(k)))
+        await asyncio.gather(*(one(inf) for k in kinds for inf in self._group(k).all()))
 
     async def wait_for_rv(self, kind, namespace: Optional[str], want: int, timeout: float) -> bool:
         """Wait until the watch stream holding ``namespace``'s ``kind`` objects has delivered
@@ -363,15 +449,24 @@ class InformerCache(Reader, EventSource):
         return out
 
     async def stop(self) -> None:
-        for inf in self._informers.values():
+        infs = [inf for g in self._groups.values() for inf in g.infs.values()]
+        if self._ns_informer is not None:
+            infs.append(self._ns_informer)
+        for inf in infs:
             if inf.task is not None:
                 inf.task.cancel()
-        for inf in self._informers.values():
+        for inf in infs:
             if inf.task is not None:
                 try:
                     await inf.task
                 except (asyncio.CancelledError, Exception):
                     pass
-        self._informers.clear()
-        self._by_kind.clear()
+        self._groups.clear()
         self._by_ref.clear()
+        self._ns_informer = None
+
+
+def kinds_namespace():
+    from ..models import kinds
+
+    return kinds.NAMESPACE

@@ -56,6 +56,7 @@ class Manager:
         self.elected = None  # asyncio.Event, created inside the loop by start()
         self.fatal: Optional[str] = None  # set when the manager must exit (leadership lost)
         self._fatal_event: Optional[asyncio.Event] = None
+        self._started_event: Optional[asyncio.Event] = None
         self.healthz["leader-election"] = lambda: self.fatal is None
 
     # ------------------------------------------------------------------ construction
@@ -69,7 +70,8 @@ class Manager:
 
     @classmethod
     def remote(cls, config, name: str = "manager", uncached: Sequence = (), transforms=None,
-               namespace: Optional[str] = None, shared=None, **kw) -> "Manager":
+               namespace: Optional[str] = None, shared=None, cache_options: Optional[dict] = None,
+               **kw) -> "Manager":
         """Manager against a real (or out-of-process) apiserver: REST client + informer cache.
 
         ``shared=(rest, cache)`` makes several managers of one process share a single
@@ -84,7 +86,7 @@ class Manager:
             mgr = cls(CachedClient(cache, rest, uncached), cache, cache, name=name, **kw)
             return mgr
         rest = RestClient(config)
-        cache = InformerCache(rest, namespace=namespace, transforms=transforms)
+        cache = InformerCache(rest, namespace=namespace, transforms=transforms, **(cache_options or {}))
         client = CachedClient(cache, rest, uncached)
         mgr = cls(client, cache, cache, name=name, **kw)
         mgr.rest = rest
@@ -114,6 +116,13 @@ class Manager:
 
     # ------------------------------------------------------------------ lifecycle
 
+    def started_event(self) -> asyncio.Event:
+        """Set once :meth:`start` has started the servers and leader-independent runnables
+        (then :attr:`elected` is set once this replica leads and its controllers run)."""
+        if self._started_event is None:
+            self._started_event = asyncio.Event()
+        return self._started_event
+
     async def start(self) -> None:
         if self._started:
             return
@@ -123,6 +132,7 @@ class Manager:
         await self._start_servers()
         for r in self.runnables:
             await r.start()
+        self.started_event().set()
         if self.leader_elector is None:
             await self._become_leader()
         else:
@@ -215,6 +225,10 @@ class Manager:
 
     def reconcile_count(self) -> int:
         return sum(c.reconciles for c in self.controllers)
+
+    def reconcile_breakdown(self) -> Dict[str, Dict[str, int]]:
+        """controller name → {triggering watch kind (or "requeue") → reconciles}."""
+        return {c.name: dict(c.reconciles_by_trigger) for c in self.controllers}
 
     # ------------------------------------------------------------------ servers
 

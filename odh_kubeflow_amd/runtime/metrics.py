@@ -133,9 +133,18 @@ class RuntimeMetrics:
                                      ["name"], buckets=_BUCKETS)
         self.retries = _Metric("counter", "workqueue_retries_total", "Total number of retries handled by workqueue",
                                ["name"])
+        # not in controller-runtime: what queued each reconcile (the watched kind whose event
+        # first queued the request, or "requeue"), and own-write watch echoes not queued
+        self.reconcile_trigger = _Metric("counter", "odh_controller_reconcile_trigger_total",
+                                         "Reconciles per controller by the watched kind that queued them",
+                                         ["controller", "trigger"])
+        self.echoes_skipped = _Metric("counter", "odh_controller_own_write_echoes_skipped_total",
+                                      "Watch events of a controller's own writes that did not requeue the writer",
+                                      ["controller"])
         registry.register(_Collector([self.reconcile_total, self.reconcile_errors, self.reconcile_time,
                                       self.max_concurrent, self.active_workers, self.depth, self.adds,
-                                      self.queue_latency, self.retries]))
+                                      self.queue_latency, self.retries, self.reconcile_trigger,
+                                      self.echoes_skipped]))
 
     @staticmethod
     def child(metric: _Metric, *labels):

@@ -1,0 +1,171 @@
+"""Watch-event economy: own-write echoes, per-watch predicates, trigger attribution.
+
+The reference's reconcilers register their watches without predicates
+(``kf/controllers/notebook_controller.go:778-826``, ``odh/controllers/notebook_controller.go:707-855``),
+so every status write, finalizer edit and garbage-collected child queues a reconcile that
+finds nothing to do.  These tests pin the filtered behaviour: the wasted reconciles are
+gone, while every change a reconcile actually reads (drift, deletion of a live child, pod
+readiness, stop/restart annotations) still triggers one.
+"""
+
+import asyncio
+
+from odh_kubeflow_amd.cluster import ClusterConfig, LocalCluster
+from odh_kubeflow_amd.models import kinds
+from odh_kubeflow_amd.models import meta as m
+from odh_kubeflow_amd.models.notebook import notebook
+from odh_kubeflow_amd.runtime.controller import Request, Result
+from odh_kubeflow_amd.runtime.manager import Manager
+from odh_kubeflow_amd.apiserver.store import ObjectStore
+
+
+def _cm(name, data=None):
+    return {"apiVersion": "v1", "kind": "ConfigMap", "metadata": {"name": name, "namespace": "ns"},
+            "data": data or {"k": "v"}}
+
+
+def test_own_write_echo_does_not_requeue_but_other_writers_do(run):
+    async def go():
+        store = ObjectStore()
+        await store.create({"apiVersion": "v1", "kind": "Namespace", "metadata": {"name": "ns"}})
+        mgr = Manager.in_process(store, name="t")
+        seen = []
+
+        async def reconcile(req):
+            seen.append(req)
+            cm = await mgr.client.get_or_none(kinds.CONFIG_MAP, req.name, req.namespace)
+            if cm is not None and cm["data"].get("k") == "v":
+                cm["data"]["k"] = "written-by-reconcile"
+                await mgr.client.update(cm)
+            return Result()
+
+        # a second controller watching the same kind still sees the first one's writes
+        other = []
+
+        async def observe(req):
+            other.append(req)
+            return Result()
+
+        c = mgr.builder().named("writer").for_(kinds.CONFIG_MAP).complete(reconcile)
+        oc = mgr.builder().named("observer").for_(kinds.CONFIG_MAP).complete(observe)
+        await mgr.start()
+        try:
+            await store.create(_cm("a"))
+            assert await mgr.wait_idle(5, settle=0.05)
+            # ADDED → reconcile (writes) → the write's echo is skipped: one reconcile
+            assert seen == [Request("ns", "a")]
+            assert c.echoes_skipped == 1
+            assert c.reconciles_by_trigger == {"ConfigMap": 1}
+            assert other and oc.echoes_skipped == 0  # not the observer's write: never skipped
+            # someone else's change does trigger
+            cm = await store.get(kinds.CONFIG_MAP, "a", "ns")
+            cm["data"]["k"] = "user"
+            await store.update(cm)
+            assert await mgr.wait_idle(5, settle=0.05)
+            assert seen == [Request("ns", "a"), Request("ns", "a")]
+        finally:
+            await mgr.stop()
+    run(go())
+
+
+def test_echo_skip_can_be_disabled_like_controller_runtime(run):
+    async def go():
+        store = ObjectStore()
+        await store.create({"apiVersion": "v1", "kind": "Namespace", "metadata": {"name": "ns"}})
+        mgr = Manager.in_process(store, name="t")
+        mgr.skip_own_write_echoes = False
+        seen = []
+
+        async def reconcile(req):
+            seen.append(req)
+            cm = await mgr.client.get_or_none(kinds.CONFIG_MAP, req.name, req.namespace)
+            if cm is not None and cm["data"].get("k") == "v":
+                cm["data"]["k"] = "x"
+                await mgr.client.update(cm)
+            return Result()
+
+        mgr.builder().named("writer").for_(kinds.CONFIG_MAP).complete(reconcile)
+        await mgr.start()
+        try:
+            await store.create(_cm("a"))
+            assert await mgr.wait_idle(5, settle=0.05)
+            assert len(seen) == 2  # the echo of its own update reconciles again
+        finally:
+            await mgr.stop()
+    run(go())
+
+
+def _nb_counts(cl):
+    return dict(cl.kf.controllers[0].reconciles_by_trigger)
+
+
+def test_kf_ignores_status_and_finalizer_edits_but_not_annotations(run):
+    async def go():
+        async with LocalCluster(ClusterConfig()) as cl:
+            await cl.ensure_namespace("user")
+            await cl.admin.create(notebook("nb1", "user", gpus=1))
+            assert await cl.wait_for(lambda: cl.notebook_ready("nb1", "user"), 10)
+            assert await cl.settle()
+            n0 = cl.kf.controllers[0].reconciles
+            # a finalizer edit (what the odh controller does) and a foreign status write
+            await cl.admin.patch(kinds.NOTEBOOK, {"metadata": {"finalizers": ["x.io/f"]}}, name="nb1", namespace="user")
+            await cl.admin.patch(kinds.NOTEBOOK, {"status": {"readyReplicas": 1}}, name="nb1", namespace="user",
+                                 subresource="status")
+            assert await cl.settle()
+            assert cl.kf.controllers[0].reconciles == n0
+            # an annotation edit (stop) does
+            await cl.admin.patch(kinds.NOTEBOOK, {"metadata": {"annotations": {"kubeflow-resource-stopped": "t"}}},
+                                 name="nb1", namespace="user")
+            assert await cl.wait_for(lambda: cl.store.peek(kinds.STATEFUL_SET, "nb1", "user")["spec"]["replicas"] == 0)
+            await cl.admin.patch(kinds.NOTEBOOK, {"metadata": {"finalizers": None}}, name="nb1", namespace="user")
+    run(go())
+
+
+def test_deleted_children_of_live_notebook_are_recreated(run):
+    """Drift repair still works with the owner-alive delete filter (STS and Service)."""
+    async def go():
+        async with LocalCluster(ClusterConfig()) as cl:
+            await cl.ensure_namespace("user")
+            await cl.admin.create(notebook("nb1", "user"))
+            assert await cl.wait_for(lambda: cl.notebook_ready("nb1", "user"), 10)
+            uid = m.uid(cl.store.peek(kinds.SERVICE, "nb1", "user"))
+            await cl.admin.delete(kinds.SERVICE, "nb1", "user")
+            assert await cl.wait_for(lambda: (cl.store.peek(kinds.SERVICE, "nb1", "user") or {})
+                                     .get("metadata", {}).get("uid", uid) != uid, 10)
+            sts_uid = m.uid(cl.store.peek(kinds.STATEFUL_SET, "nb1", "user"))
+            await cl.admin.delete(kinds.STATEFUL_SET, "nb1", "user", propagation="Orphan")
+            assert await cl.wait_for(lambda: (cl.store.peek(kinds.STATEFUL_SET, "nb1", "user") or {})
+                                     .get("metadata", {}).get("uid", sts_uid) != sts_uid, 10)
+            assert await cl.wait_for(lambda: cl.notebook_ready("nb1", "user"), 10)
+    run(go())
+
+
+def test_lifecycle_reconciles_per_notebook_and_triggers(run):
+    """create → Ready → delete through the full odh path: at most 12 reconciles per notebook
+    (the reference-emulation path does ~18), none of them triggered by garbage collection."""
+    async def go():
+        cfg = ClusterConfig(odh=True, webhook=True, env={"SET_PIPELINE_RBAC": "false", "SET_PIPELINE_SECRET": "false"})
+        async with LocalCluster(cfg) as cl:
+            await cl.ensure_namespace("bench")
+            ann = {"notebooks.opendatahub.io/inject-auth": "true"}
+
+            async def one(i):
+                nm = f"nb{i}"
+                await cl.admin.create(notebook(nm, "bench", gpus=1, annotations=ann))
+                assert await cl.wait_for(lambda: cl.notebook_ready(nm, "bench"), 10)
+                await cl.admin.delete(kinds.NOTEBOOK, nm, "bench")
+                assert await cl.wait_for(lambda: cl.store.peek(kinds.NOTEBOOK, nm, "bench") is None and
+                                         cl.store.peek(kinds.POD, f"{nm}-0", "bench") is None, 10)
+            await one(0)
+            assert await cl.settle()
+            r0, b0 = cl.reconcile_count(), cl.reconcile_breakdown()
+            for i in range(1, 6):
+                await one(i)
+            assert await cl.settle()
+            per_nb = (cl.reconcile_count() - r0) / 5
+            assert per_nb <= 12, (per_nb, cl.reconcile_breakdown())
+            b1 = cl.reconcile_breakdown()
+            kf = {k: v - b0["notebook-controller"].get(k, 0) for k, v in b1["notebook-controller"].items()}
+            # kf: creation + lock removal (Notebook), pod readiness (Pod), readyReplicas (STS)
+            assert kf.get("Notebook", 0) <= 2 * 5 and kf.get("Service", 0) == 0, kf
+    run(go())

@@ -100,9 +100,12 @@ def measure(args) -> Optional[dict]:
         from bench import report  # noqa: E402  (bench.py is the entry point on sys.path)
 
         out = report(args, world, res)
-        out["config"]["parallelism"] = (f"namespace-sharded control plane x{world} (one rank per MI355X: kf+odh "
-                                        f"reconcilers, webhook, STS controller, node agent); native C++ apiserver")
-        out["config"]["architecture"] = "sharded"
+        out["config"]["parallelism"] = (f"namespace-sharded control plane x{world}: one `cmd/control_plane.py "
+                                        f"--shard r` process per MI355X (kf + odh reconcilers + odh webhook), "
+                                        f"as config/overlays/mi355x-sharded deploys it")
+        out["config"]["architecture"] = "cmd/control_plane --shard (overlay mi355x-sharded)"
+        out["config"]["platform_stand_ins"] = ("native C++ apiserver (+GC), cmd/scheduler.py, per-rank StatefulSet "
+                                               "controller + fake kubelet of the rank's GPU")
         out["rank_ms_per_step"] = res.get("rank_ms_per_step")
         out["cpu_ms_per_step"] = res.get("cpu_ms_per_step")
         if res.get("apiserver_profile_per_step"):
@@ -143,9 +146,9 @@ async def _main(args, dist, torch, rank: int, world: int, local_rank: int, probe
     use_odh = not args.no_odh
     env = {"SET_PIPELINE_RBAC": "false", "SET_PIPELINE_SECRET": "false"}
     shard = ControlPlaneShard(ShardConfig(
-        apiserver_url=url[0], namespace=bench_namespace(rank), gpu=local_rank % 8, bootstrap=(rank == 0),
-        run_scheduler=False, odh=use_odh, webhook=use_odh, startup_probe=probe,
-        reference_emulation=args.reference_emulation, env=env))
+        apiserver_url=url[0], namespace=bench_namespace(rank), gpu=local_rank % 8, shard=str(rank),
+        bootstrap=(rank == 0), run_scheduler=False, odh=use_odh, webhook=use_odh, startup_probe=probe,
+        reference_emulation=args.reference_emulation, env=env, process=True))
     if rank == 0:
         await shard.start()  # namespaces, Node, scheduler first
         await _in_thread(dist.barrier)
@@ -155,7 +158,8 @@ async def _main(args, dist, torch, rank: int, world: int, local_rank: int, probe
     await _in_thread(dist.barrier)  # every shard's webhook is registered before anyone creates
 
     try:
-        children = {"apiserver": native.proc.pid if native else None, "scheduler": sched.pid if sched else None}
+        children = {"apiserver": native.proc.pid if native else None, "scheduler": sched.pid if sched else None,
+                    f"control_plane_{rank}": shard.control_plane_pid()}
         result = await _drive(args, shard, dist, torch, children, native)
     finally:
         await _in_thread(dist.barrier)  # nobody tears down while others still serve
@@ -246,8 +250,7 @@ async def _drive(args, shard, dist, torch, children: Optional[dict] = None, nati
     if torch.cuda.is_available():
         torch.cuda.synchronize()
     await _in_thread(dist.barrier)
-    r0 = shard.reconcile_count()
-    b0 = shard.reconcile_breakdown()
+    b0 = await shard.reconcile_breakdown()
     children = children or {}
     child_cpu0 = {k: _proc_cpu_s(pid) for k, pid in children.items()}
     prof0 = await _apiserver_prof(native)
@@ -257,10 +260,10 @@ async def _drive(args, shard, dist, torch, children: Optional[dict] = None, nati
         await one_step(True)
     own = time.perf_counter() - t_start  # this rank's own steps (the barrier below equalises elapsed)
     await shard.settle(5)  # the last teardown's trailing reconciles stay inside the timed region
-    state["recon"] = shard.reconcile_count() - r0
     from bench import breakdown_delta, merge_breakdowns  # noqa: E402  (bench.py is the entry point)
 
-    breakdown = breakdown_delta(b0, shard.reconcile_breakdown())
+    breakdown = breakdown_delta(b0, await shard.reconcile_breakdown())
+    state["recon"] = sum(sum(t.values()) for t in breakdown.values())
     # CPU time per step of every process on the path: where a step's work goes when ranks are added
     cpu = {"rank": time.process_time() - cpu0}
     prof = _prof_per_step(prof0, await _apiserver_prof(native), args.steps)

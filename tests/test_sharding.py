@@ -213,13 +213,17 @@ def test_two_shards_one_native_apiserver(run):
             for sh in shards:
                 for j in range(1):
                     assert await sh.wait_for(lambda: sh.notebook_ready(f"nb{j}"), 30)
-            # isolation: a shard's cache never holds the other shard's objects
+            # isolation: a shard's control-plane cache (cmd/control_plane.py --shard i: the
+            # namespaces labelled notebooks.amd.com/shard=i + the controller namespace) never
+            # holds the other shard's objects; HTTPRoutes carry the shard label
             for i, sh in enumerate(shards):
-                assert {m.namespace(o) for o in sh.cache.list(kinds.NOTEBOOK)} == {f"bench-{i}"}
-                assert {m.namespace(o) for o in sh.cache.list(kinds.POD)} == {f"bench-{i}"}
-                routes = sh.cache.list(kinds.HTTP_ROUTE)
+                cp = sh.control_plane.cache
+                assert {m.namespace(o) for o in cp.list(kinds.NOTEBOOK)} == {f"bench-{i}"}
+                assert {m.namespace(o) for o in cp.list(kinds.POD)} == {f"bench-{i}"}
+                routes = cp.list(kinds.HTTP_ROUTE)
                 assert routes and {m.labels(r)["notebook-namespace"] for r in routes} == {f"bench-{i}"}
-                assert sh.webhook.requests >= 1
+                assert {m.labels(r)["notebooks.amd.com/shard"] for r in routes} == {str(i)}
+                assert sh.control_plane.webhook_server.webhook.requests >= 1
             # each shard's pod got the shard's own GPU (namespace gpu-affinity), so it was
             # started by the node agent living in the same process
             for i, sh in enumerate(shards):
@@ -238,3 +242,93 @@ def test_two_shards_one_native_apiserver(run):
                 await sh.stop()
             await native.stop()
     run(go())
+
+
+def test_informer_namespace_selector_follows_labels(run, server_kind):
+    """``namespace_selector``: a namespace joins the cache when it gets the shard label
+    (its objects arrive as ADDED), leaves it when relabelled (DELETED), and reads of a
+    namespace outside the cache go live through CachedClient."""
+    async def go():
+        srv, c = await _server(server_kind)
+        try:
+            await c.create({"apiVersion": "v1", "kind": "Namespace", "metadata": {"name": "ctl"}})
+            for ns, shard in (("a", "1"), ("b", "2"), ("c", None)):
+                md = {"name": ns, **({"labels": {"notebooks.amd.com/shard": shard}} if shard else {})}
+                await c.create({"apiVersion": "v1", "kind": "Namespace", "metadata": md})
+                await c.create(_cm("x", ns))
+            await c.create(_cm("x", "ctl"))
+            cache = InformerCache(c, namespace_selector="notebooks.amd.com/shard=1", namespaces=["ctl"])
+            seen = []
+            cache.subscribe(kinds.CONFIG_MAP, lambda et, o, old: seen.append((et, m.namespace(o))))
+            await cache.wait_synced([kinds.CONFIG_MAP])
+            assert sorted(m.namespace(o) for o in cache.list(kinds.CONFIG_MAP)) == ["a", "ctl"]
+            assert cache.covers(kinds.CONFIG_MAP, "a") and not cache.covers(kinds.CONFIG_MAP, "c")
+            assert cache.covers(kinds.NAMESPACE, "c")  # cluster-scoped kinds are never restricted
+
+            # live read of an uncovered namespace (the webhook admits every namespace)
+            client = CachedClient(cache, c)
+            assert (await client.get(kinds.CONFIG_MAP, "x", "c"))["data"] == {"k": "x"}
+
+            # c joins shard 1: its objects arrive, existing subscriptions see them
+            await c.patch(kinds.NAMESPACE, {"metadata": {"labels": {"notebooks.amd.com/shard": "1"}}}, name="c")
+            assert await _wait(lambda: cache.get(kinds.CONFIG_MAP, "x", "c") is not None)
+            assert ("ADDED", "c") in seen
+            # a moves to shard 2: gone from this cache, subscribers get DELETED
+            await c.patch(kinds.NAMESPACE, {"metadata": {"labels": {"notebooks.amd.com/shard": "2"}}}, name="a")
+            assert await _wait(lambda: cache.get(kinds.CONFIG_MAP, "x", "a") is None)
+            assert ("DELETED", "a") in seen
+            assert not cache.covers(kinds.CONFIG_MAP, "a")
+            # a new object in a joined namespace streams in
+            await c.create(_cm("y", "c"))
+            assert await _wait(lambda: cache.get(kinds.CONFIG_MAP, "y", "c") is not None)
+            await cache.stop()
+        finally:
+            await c.close()
+            await srv.stop()
+    run(go())
+
+
+def test_namespace_shard_assigner(run):
+    from odh_kubeflow_amd.controllers.sharding import NamespaceShardAssigner, shard_for
+    from odh_kubeflow_amd.runtime.manager import Manager
+
+    async def go():
+        store = ObjectStore()
+        mgr = Manager.in_process(store, name="cp")
+        a = NamespaceShardAssigner(mgr.client, mgr.reader, 4, exclude=["opendatahub"])
+        a.setup_with_manager(mgr)
+        await mgr.start()
+        try:
+            for ns, labels in (("team-a", None), ("team-b", {"notebooks.amd.com/shard": "3"}),
+                               ("kube-system", None), ("opendatahub", None)):
+                await store.create({"apiVersion": "v1", "kind": "Namespace",
+                                    "metadata": {"name": ns, **({"labels": labels} if labels else {})}})
+            assert await mgr.wait_idle(5, settle=0.05)
+            lab = {ns: m.labels(store.peek(kinds.NAMESPACE, ns)).get("notebooks.amd.com/shard")
+                   for ns in ("team-a", "team-b", "kube-system", "opendatahub")}
+            assert lab == {"team-a": shard_for("team-a", 4), "team-b": "3", "kube-system": None, "opendatahub": None}
+            assert shard_for("team-a", 4) == shard_for("team-a", 4) and 0 <= int(shard_for("x", 8)) < 8
+        finally:
+            await mgr.stop()
+    run(go())
+
+
+def test_control_plane_flags(tmp_path):
+    from odh_kubeflow_amd.cmd import control_plane
+    from odh_kubeflow_amd.cmd.common import resolve_shard
+
+    with pytest.raises(SystemExit):
+        control_plane.parse(["--controllers", "kf,odh"])  # odh needs --kube-rbac-proxy-image
+    a = control_plane.parse(["--controllers", "kf", "--shard", "ordinal"])
+    assert a.controller_set == ["kf"]
+    assert resolve_shard("ordinal", {"POD_NAME": "odh-kubeflow-amd-control-plane-5"}) == "5"
+    assert resolve_shard(None, {}) is None and resolve_shard("3", {}) == "3"
+    with pytest.raises(SystemExit):
+        resolve_shard("ordinal", {"HOSTNAME": "no-ordinal"})
+    with pytest.raises(SystemExit):
+        resolve_shard("not a label!", {})
+    # the webhook never starts without its serving certificate (odh/main.go semantics)
+    a = control_plane.parse(["--kube-rbac-proxy-image", "img", "--webhook-cert-dir", str(tmp_path),
+                             "--master", "http://127.0.0.1:1"])
+    with pytest.raises(SystemExit, match="serving certificate missing"):
+        control_plane.build(a, {})

@@ -29,7 +29,8 @@ def parse(argv=None):
     p.add_argument("--kubeconfig", default=None)
     p.add_argument("--namespace", default=None, help="default: the pod's namespace (SA file / K8S_NAMESPACE)")
     p.add_argument("--secret-name", default="odh-notebook-controller-webhook-cert")
-    p.add_argument("--service-name", default="odh-notebook-controller-webhook-service")
+    p.add_argument("--service-name", action="append", default=None,
+                   help="webhook Service the cert must cover (repeatable: one per control-plane shard)")
     p.add_argument("--mwc-name", action="append", default=None,
                    help="MutatingWebhookConfiguration whose caBundle to keep in sync (repeatable)")
     p.add_argument("--extra-host", action="append", default=[], help="additional SAN (DNS name or IP)")
@@ -49,7 +50,8 @@ async def amain(argv=None) -> int:
     setup_logging()
     client = RestClient(RestConfig.load(args.master, args.kubeconfig))
     try:
-        out = await provision(client, args.namespace or namespace_from_env(), args.secret_name, args.service_name,
+        out = await provision(client, args.namespace or namespace_from_env(), args.secret_name,
+                              args.service_name or ["odh-notebook-controller-webhook-service"],
                               args.mwc_name or ["odh-notebook-controller-mutating-webhook-configuration"],
                               args.extra_host, args.validity_days, args.renew_before_days, args.cluster_domain)
     finally:

@@ -14,8 +14,19 @@
   read-only amdgpu telemetry + pod→GPU attribution (``nodeagent/``), no apiserver access,
   no RBAC, no GPU device files; it never requests ``amd.com/gpu`` itself;
 * ``webhook/`` — Service + MutatingWebhookConfiguration (``failurePolicy: Fail``);
+* ``webhook-certs/`` — outside OpenShift (no service-ca): the serving-cert provisioner
+  (``cmd/webhook_certs.py``) as a Job + weekly renewal CronJob with the RBAC it needs
+  (the reference's kind CI does this step with ``openssl`` + ``kubectl patch``);
+* ``control-plane/`` — the sharded control plane: ``cmd/control_plane.py`` as a
+  StatefulSet of N replicas (``--shard=ordinal``: replica k owns the namespaces labelled
+  ``notebooks.amd.com/shard=k``; replica 0 labels new namespaces), one webhook Service
+  and MutatingWebhookConfiguration per shard (``namespaceSelector`` on that label) plus
+  one for not-yet-assigned namespaces, RBAC = kf ∪ odh roles + namespace labelling;
 * ``overlays/{kubeflow,standalone,openshift,mi355x}`` — Istio on/off, OpenShift
-  service-ca injection + ``ADD_FSGROUP=false``, MI355X placement + GPU-busy culling;
+  service-ca injection + ``ADD_FSGROUP=false``, MI355X placement + GPU-busy culling
+  (ConfigMap settings merged with ``configMapGenerator behavior: merge``, as the
+  reference's overlays do); ``overlays/mi355x-sharded`` — the MI355X settings with the
+  sharded control plane instead of the two cluster-wide managers;
 * ``samples/`` — Notebooks requesting 1 and 8 ``amd.com/gpu`` with the PyTorch-ROCm image.
 
 The CRD is the reference's, structurally equal per version: the full expanded ``core/v1``
@@ -36,6 +47,24 @@ import yaml
 from ..models.notebook import GPU_RESOURCE
 
 ROCM_NOTEBOOK_IMAGE = "rocm/pytorch:rocm7.0_ubuntu22.04_py3.10_pytorch_release_2.10.0"
+NAME_PREFIX = "odh-kubeflow-amd-"
+WEBHOOK_CERT_SECRET = "odh-notebook-controller-webhook-cert"  # created by service-ca / the certs Job
+WEBHOOK_SERVICE = "odh-notebook-controller-webhook-service"
+MWC_NAME = "mutating-webhook-configuration"
+SHARDS = 8  # one control-plane shard per MI355X of an 8-GPU node
+CULLER_LITERALS = ["ENABLE_CULLING=false", "CULL_IDLE_TIME=1440", "IDLENESS_CHECK_PERIOD=1",
+                   "CULLING_ACTIVITY_SOURCE=jupyter", "CULLING_GPU_BUSY_THRESHOLD=5",
+                   "CULLING_GPU_AGENT_PORT=9464", "CULLING_GPU_VRAM_ACTIVE_BYTES=0"]
+CULLER_KEYS = [lit.split("=", 1)[0] for lit in CULLER_LITERALS]
+PARAMS_ENV = "USE_ISTIO=false\nISTIO_GATEWAY=kubeflow/kubeflow-gateway\nISTIO_HOST=*\n" \
+             "CLUSTER_DOMAIN=cluster.local\nADD_FSGROUP=true\nGPU_NODE_SELECTOR=false\n" \
+             "GPU_SHM_SIZE_PER_GPU=\nMULTI_GPU_ENV=\n"
+# MI355X node settings (overlays mi355x and mi355x-sharded)
+MI355X_PARAMS = ["GPU_NODE_SELECTOR=true", "GPU_SHM_SIZE_PER_GPU=16Gi",
+                 # multi-GPU notebooks: RCCL's intra-node IPC over dmabuf (hosts whose amdgpu
+                 # driver only offers dmabuf IPC fail hipIpcGetMemHandle otherwise)
+                 "MULTI_GPU_ENV=HSA_ENABLE_IPC_MODE_LEGACY=0"]
+MI355X_CULLER = ["CULLING_ACTIVITY_SOURCE=combined", "ENABLE_CULLING=true"]
 MANAGER_IMAGE = "quay.io/opendatahub/odh-kubeflow-amd:latest"
 KUBE_RBAC_PROXY_IMAGE = "quay.io/brancz/kube-rbac-proxy:v0.18.1"
 
@@ -138,15 +167,17 @@ def _probes(port: int = 8081) -> dict:
                                "periodSeconds": 10}}
 
 
+def _culler_env() -> List[dict]:
+    return [{"name": k, "valueFrom": {"configMapKeyRef": {"name": "notebook-controller-culler-config",
+                                                          "key": k, "optional": True}}} for k in CULLER_KEYS]
+
+
 def kf_deployment() -> dict:
     c = {"name": "manager", "image": MANAGER_IMAGE,
          "command": ["python", "-m", "odh_kubeflow_amd.cmd.kf_manager"],
          "args": ["--enable-leader-election", "--metrics-addr=:8080", "--probe-addr=:8081"],
          "envFrom": [{"configMapRef": {"name": "config"}}],
-         "env": [{"name": k, "valueFrom": {"configMapKeyRef": {"name": "notebook-controller-culler-config",
-                                                                "key": k, "optional": True}}}
-                 for k in ("ENABLE_CULLING", "CULL_IDLE_TIME", "IDLENESS_CHECK_PERIOD", "CULLING_ACTIVITY_SOURCE",
-                           "CULLING_GPU_BUSY_THRESHOLD", "CULLING_GPU_AGENT_PORT", "CULLING_GPU_VRAM_ACTIVE_BYTES")],
+         "env": _culler_env(),
          "ports": [{"name": "metrics", "containerPort": 8080}, {"name": "probes", "containerPort": 8081}],
          "resources": {"requests": {"cpu": "500m", "memory": "256Mi"}, "limits": {"cpu": "2", "memory": "2Gi"}},
          **_probes()}
@@ -180,7 +211,7 @@ def odh_deployment() -> dict:
                      "template": {"metadata": {"labels": {"app": "odh-notebook-controller"}},
                                   "spec": {"serviceAccountName": "manager", "containers": [c],
                                            "volumes": [{"name": "cert", "secret": {
-                                               "secretName": "odh-notebook-controller-webhook-cert",
+                                               "secretName": WEBHOOK_CERT_SECRET,
                                                "defaultMode": 420}}]}}}}
 
 
@@ -242,6 +273,133 @@ def mwc() -> dict:
     return o
 
 
+# ------------------------------------------------------------------ webhook serving cert (non-OpenShift)
+
+
+def webhook_certs_args(services: List[str], mwcs: List[str]) -> List[str]:
+    """``cmd/webhook_certs.py`` arguments.  Names are the *rendered* (prefixed) names: they
+    are plain strings to kustomize, so its name-reference fix-ups do not reach them."""
+    return ([f"--secret-name={WEBHOOK_CERT_SECRET}"] + [f"--service-name={x}" for x in services]
+            + [f"--mwc-name={x}" for x in mwcs])
+
+
+def webhook_certs_docs(services: List[str], mwcs: List[str]) -> Dict[str, object]:
+    """SA + RBAC + Job + renewal CronJob of the serving-cert provisioner: the Secret the
+    webhook server mounts and the caBundle of every MutatingWebhookConfiguration
+    (``.github/workflows/odh_notebook_controller_integration_test.yaml:190-216`` does the
+    same by hand on kind)."""
+    c = {"name": "webhook-certs", "image": MANAGER_IMAGE,
+         "command": ["python", "-m", "odh_kubeflow_amd.cmd.webhook_certs"],
+         "args": webhook_certs_args(services, mwcs),
+         "env": [{"name": "K8S_NAMESPACE", "valueFrom": {"fieldRef": {"fieldPath": "metadata.namespace"}}}],
+         "securityContext": {"allowPrivilegeEscalation": False, "capabilities": {"drop": ["ALL"]}},
+         "resources": {"requests": {"cpu": "50m", "memory": "64Mi"}, "limits": {"memory": "256Mi"}}}
+    pod = {"serviceAccountName": "webhook-certs", "restartPolicy": "OnFailure", "containers": [c]}
+    job_spec = {"backoffLimit": 6, "ttlSecondsAfterFinished": 3600, "template": {
+        "metadata": {"labels": {"app": "odh-webhook-certs"}}, "spec": pod}}
+    return {
+        "rbac.yaml": [
+            {"apiVersion": "v1", "kind": "ServiceAccount", "metadata": {"name": "webhook-certs"}},
+            {"apiVersion": "rbac.authorization.k8s.io/v1", "kind": "Role", "metadata": {"name": "webhook-certs-role"},
+             "rules": [_rule([""], ["secrets"], ["get", "create", "update"])]},
+            {"apiVersion": "rbac.authorization.k8s.io/v1", "kind": "ClusterRole",
+             "metadata": {"name": "webhook-certs-cabundle-role"},
+             "rules": [_rule(["admissionregistration.k8s.io"], ["mutatingwebhookconfigurations"],
+                             ["get", "list", "update", "patch"])]},
+            binding("RoleBinding", "webhook-certs-rolebinding", "webhook-certs-role", "webhook-certs"),
+            binding("ClusterRoleBinding", "webhook-certs-cabundle-rolebinding", "webhook-certs-cabundle-role",
+                    "webhook-certs")],
+        "job.yaml": [
+            {"apiVersion": "batch/v1", "kind": "Job", "metadata": {"name": "webhook-certs"}, "spec": job_spec},
+            # renewal: re-run weekly; the provisioner reissues within 90 days of expiry (or when a
+            # shard's Service is missing from the SANs) and the webhook servers reload the files
+            {"apiVersion": "batch/v1", "kind": "CronJob", "metadata": {"name": "webhook-certs-renew"},
+             "spec": {"schedule": "17 3 * * 1", "concurrencyPolicy": "Forbid", "jobTemplate": {"spec": job_spec}}}],
+    }
+
+
+# ------------------------------------------------------------------ sharded control plane
+
+
+def control_plane_role() -> dict:
+    """kf ∪ odh manager permissions, plus labelling namespaces (the shard assigner)."""
+    rules = kf_role()["rules"] + odh_role()["rules"] + [_rule([""], ["namespaces"], ["get", "list", "watch", "patch"])]
+    return {"apiVersion": "rbac.authorization.k8s.io/v1", "kind": "ClusterRole",
+            "metadata": {"name": "control-plane-role"}, "rules": rules}
+
+
+def control_plane_statefulset(shards: int) -> dict:
+    c = {"name": "manager", "image": MANAGER_IMAGE,
+         "command": ["python", "-m", "odh_kubeflow_amd.cmd.control_plane"],
+         "args": ["--shard=ordinal", f"--shard-count={shards}", "--assign-namespaces", "--leader-elect",
+                  "--kube-rbac-proxy-image=$(KUBE_RBAC_PROXY_IMAGE)",
+                  "--webhook-cert-dir=/tmp/k8s-webhook-server/serving-certs", "--webhook-port=8443"],
+         "envFrom": [{"configMapRef": {"name": "config"}}],
+         "env": [{"name": "POD_NAME", "valueFrom": {"fieldRef": {"fieldPath": "metadata.name"}}},
+                 {"name": "K8S_NAMESPACE", "valueFrom": {"fieldRef": {"fieldPath": "metadata.namespace"}}},
+                 {"name": "KUBE_RBAC_PROXY_IMAGE", "value": KUBE_RBAC_PROXY_IMAGE},
+                 {"name": "SET_PIPELINE_RBAC", "value": "true"}, {"name": "SET_PIPELINE_SECRET", "value": "true"},
+                 {"name": "INJECT_CLUSTER_PROXY_ENV", "valueFrom": {"configMapKeyRef": {
+                     "name": "notebook-controller-setting-config", "key": "INJECT_CLUSTER_PROXY_ENV",
+                     "optional": True}}}] + _culler_env(),
+         "ports": [{"name": "webhook", "containerPort": 8443}, {"name": "metrics", "containerPort": 8080},
+                   {"name": "probes", "containerPort": 8081}],
+         "resources": {"requests": {"cpu": "500m", "memory": "256Mi"}, "limits": {"cpu": "2", "memory": "2Gi"}},
+         "volumeMounts": [{"name": "cert", "mountPath": "/tmp/k8s-webhook-server/serving-certs", "readOnly": True}],
+         **_probes()}
+    labels = {"app": "notebook-control-plane"}
+    return {"apiVersion": "apps/v1", "kind": "StatefulSet", "metadata": {"name": "control-plane", "labels": labels},
+            "spec": {"replicas": shards, "serviceName": "control-plane", "podManagementPolicy": "Parallel",
+                     "selector": {"matchLabels": labels},
+                     "template": {"metadata": {"labels": labels},
+                                  "spec": {"serviceAccountName": "control-plane", "containers": [c],
+                                           "volumes": [{"name": "cert", "secret": {
+                                               "secretName": WEBHOOK_CERT_SECRET, "defaultMode": 420}}]}}}}
+
+
+def _webhook_svc(name: str, selector: dict) -> dict:
+    return {"apiVersion": "v1", "kind": "Service", "metadata": {"name": name},
+            "spec": {"ports": [{"port": 443, "targetPort": 8443, "protocol": "TCP"}], "selector": selector}}
+
+
+def control_plane_docs(shards: int, prefix: str = NAME_PREFIX) -> Dict[str, object]:
+    """The ``control-plane/`` base.  A shard's webhook Service selects its pod by the
+    StatefulSet pod-name label, whose value is the *rendered* pod name (``prefix`` +
+    ``control-plane-<k>``): label values are not renamed by kustomize."""
+    from ..controllers.setup import SHARD_LABEL
+    from ..webhook.server import mutating_webhook_configuration
+
+    def mwc_for(svc: str, name: str, selector: dict) -> dict:
+        o = mutating_webhook_configuration("", service_namespace="system", service_name=svc, name=name,
+                                           namespace_selector=selector)
+        o["webhooks"][0]["clientConfig"].pop("caBundle")
+        return o
+
+    svcs, mwcs = [], []
+    for k in range(shards):
+        svcs.append(_webhook_svc(f"control-plane-webhook-{k}",
+                                 {"statefulset.kubernetes.io/pod-name": f"{prefix}control-plane-{k}"}))
+        mwcs.append(mwc_for(f"control-plane-webhook-{k}", f"notebook-webhook-shard-{k}",
+                            {"matchLabels": {SHARD_LABEL: str(k)}}))
+    # namespaces the assigner has not labelled yet: any shard admits them (reads live)
+    svcs.append(_webhook_svc("control-plane-webhook", {"app": "notebook-control-plane"}))
+    mwcs.append(mwc_for("control-plane-webhook", "notebook-webhook-unassigned",
+                        {"matchExpressions": [{"key": SHARD_LABEL, "operator": "DoesNotExist"}]}))
+    return {
+        "rbac.yaml": [{"apiVersion": "v1", "kind": "ServiceAccount", "metadata": {"name": "control-plane"}},
+                      control_plane_role(),
+                      binding("ClusterRoleBinding", "control-plane-rolebinding", "control-plane-role", "control-plane"),
+                      leader_election_role("control-plane-leader-election-role"),
+                      binding("RoleBinding", "control-plane-leader-election-rolebinding",
+                              "control-plane-leader-election-role", "control-plane")],
+        "statefulset.yaml": control_plane_statefulset(shards),
+        "services.yaml": [{"apiVersion": "v1", "kind": "Service", "metadata": {"name": "control-plane"},
+                           "spec": {"clusterIP": "None", "selector": {"app": "notebook-control-plane"},
+                                    "ports": [{"name": "metrics", "port": 8080, "targetPort": 8080}]}}] + svcs,
+        "webhooks.yaml": mwcs,
+    }
+
+
 def sample(name: str, gpus: int, version: str = "v1", auth: bool = False) -> dict:
     ann = {"notebooks.opendatahub.io/inject-auth": "true"} if auth else {}
     c = {"name": name, "image": ROCM_NOTEBOOK_IMAGE,
@@ -253,6 +411,16 @@ def sample(name: str, gpus: int, version: str = "v1", auth: bool = False) -> dic
             "spec": {"template": {"spec": {"containers": [c], "volumes": [
                 # /dev/shm sized for RCCL/xGMI collectives of a multi-GPU notebook
                 {"name": "dshm", "emptyDir": {"medium": "Memory", "sizeLimit": f"{16 * gpus}Gi"}}]}}}}
+
+
+def _certs_args_patches(services: List[str], mwcs: List[str]) -> List[dict]:
+    """JSON6902 patches setting the provisioner's arguments in the Job and the CronJob."""
+    args = webhook_certs_args(services, mwcs)
+    return [{"target": {"kind": kind, "name": name},
+             "patch": yaml.safe_dump([{"op": "replace", "path": path, "value": args}], sort_keys=False)}
+            for kind, name, path in (("Job", "webhook-certs", "/spec/template/spec/containers/0/args"),
+                                     ("CronJob", "webhook-certs-renew",
+                                      "/spec/jobTemplate/spec/template/spec/containers/0/args"))]
 
 
 def kustomization(resources: List[str], **extra) -> dict:
@@ -279,58 +447,69 @@ def tree() -> Dict[str, object]:
         binding("RoleBinding", "odh-notebook-controller-leader-election-rolebinding",
                 "odh-notebook-controller-leader-election-role", "manager")]
     t["rbac/service_accounts.yaml"] = [{"apiVersion": "v1", "kind": "ServiceAccount", "metadata": {"name": n}}
-                                       for n in ("service-account", "manager", "mi355x-node-agent")]
-    t["rbac/user_cluster_roles.yaml"] = user_cluster_roles()
+                                       for n in ("service-account", "manager")]
+    t["user-rbac/user_cluster_roles.yaml"] = user_cluster_roles()
+    t["user-rbac/kustomization.yaml"] = kustomization(["user_cluster_roles.yaml"])
     t["rbac/kustomization.yaml"] = kustomization(sorted(p.split("/", 1)[1] for p in t if p.startswith("rbac/")
-                                                        and not p.endswith("kustomization.yaml")))
+                                                        and not p.endswith("kustomization.yaml")) + ["../user-rbac"])
     t["manager/kf_manager.yaml"] = kf_deployment()
     t["manager/odh_manager.yaml"] = odh_deployment()
     t["manager/services.yaml"] = [metrics_service("notebook-controller-service", "notebook-controller"),
                                   metrics_service("odh-notebook-controller-service", "odh-notebook-controller")]
-    t["manager/kustomization.yaml"] = kustomization(
-        ["kf_manager.yaml", "odh_manager.yaml", "services.yaml"],
-        configMapGenerator=[{"name": "config", "envs": ["params.env"]},
-                            {"name": "notebook-controller-culler-config",
-                             "literals": ["ENABLE_CULLING=false", "CULL_IDLE_TIME=1440", "IDLENESS_CHECK_PERIOD=1",
-                                          "CULLING_ACTIVITY_SOURCE=jupyter", "CULLING_GPU_BUSY_THRESHOLD=5",
-                                          "CULLING_GPU_AGENT_PORT=9464", "CULLING_GPU_VRAM_ACTIVE_BYTES=0"]}],
-        generatorOptions={"disableNameSuffixHash": True})
-    t["manager/params.env"] = "USE_ISTIO=false\nISTIO_GATEWAY=kubeflow/kubeflow-gateway\nISTIO_HOST=*\n" \
-                              "CLUSTER_DOMAIN=cluster.local\nADD_FSGROUP=true\nGPU_NODE_SELECTOR=false\n" \
-                              "GPU_SHM_SIZE_PER_GPU=\nMULTI_GPU_ENV=\n"
+    generators = [{"name": "config", "envs": ["params.env"]},
+                  {"name": "notebook-controller-culler-config", "literals": list(CULLER_LITERALS)}]
+    t["manager/kustomization.yaml"] = kustomization(["kf_manager.yaml", "odh_manager.yaml", "services.yaml"],
+                                                    configMapGenerator=generators,
+                                                    generatorOptions={"disableNameSuffixHash": True})
+    t["manager/params.env"] = PARAMS_ENV
     t["node-agent/daemonset.yaml"] = node_agent_daemonset()
-    t["node-agent/kustomization.yaml"] = kustomization(["daemonset.yaml"])
+    t["node-agent/serviceaccount.yaml"] = {"apiVersion": "v1", "kind": "ServiceAccount",
+                                           "metadata": {"name": "mi355x-node-agent"}}
+    t["node-agent/kustomization.yaml"] = kustomization(["serviceaccount.yaml", "daemonset.yaml"])
     t["webhook/service.yaml"] = webhook_service()
     t["webhook/manifests.yaml"] = mwc()
     t["webhook/kustomization.yaml"] = kustomization(["service.yaml", "manifests.yaml"])
+    # serving cert for the two-manager layout (non-OpenShift overlays)
+    for f, doc in webhook_certs_docs([NAME_PREFIX + WEBHOOK_SERVICE], [NAME_PREFIX + MWC_NAME]).items():
+        t[f"webhook-certs/{f}"] = doc
+    t["webhook-certs/kustomization.yaml"] = kustomization(["rbac.yaml", "job.yaml"])
+    # sharded control plane (one cmd/control_plane.py replica per MI355X)
+    cp = control_plane_docs(SHARDS)
+    for f, doc in cp.items():
+        t[f"control-plane/{f}"] = doc
+    t["control-plane/params.env"] = PARAMS_ENV
+    t["control-plane/kustomization.yaml"] = kustomization(
+        ["rbac.yaml", "statefulset.yaml", "services.yaml", "webhooks.yaml"],
+        configMapGenerator=generators, generatorOptions={"disableNameSuffixHash": True})
     t["default/kustomization.yaml"] = kustomization(["../crd", "../rbac", "../manager", "../webhook", "../node-agent"],
-                                                    namespace="opendatahub", namePrefix="odh-kubeflow-amd-")
-    t["overlays/standalone/kustomization.yaml"] = kustomization(["../../default"])
+                                                    namespace="opendatahub", namePrefix=NAME_PREFIX)
+    t["overlays/standalone/kustomization.yaml"] = kustomization(["../../default", "../../webhook-certs"],
+                                                                namespace="opendatahub")
     t["overlays/kubeflow/kustomization.yaml"] = kustomization(
-        ["../../default"], namespace="kubeflow",
-        patches=[{"target": {"kind": "ConfigMap", "name": ".*config"}, "patch":
-                  "- op: replace\n  path: /data/USE_ISTIO\n  value: \"true\"\n"}])
+        ["../../default", "../../webhook-certs"], namespace="kubeflow",
+        configMapGenerator=[{"name": "config", "behavior": "merge", "literals": ["USE_ISTIO=true"]}])
     t["overlays/openshift/kustomization.yaml"] = kustomization(
         ["../../default"],
+        configMapGenerator=[{"name": "config", "behavior": "merge", "literals": ["ADD_FSGROUP=false"]}],
         patches=[{"target": {"kind": "Service", "name": ".*webhook-service"}, "patch":
                   "- op: add\n  path: /metadata/annotations\n  value:\n    service.beta.openshift.io/"
-                  "serving-cert-secret-name: odh-notebook-controller-webhook-cert\n"},
+                  f"serving-cert-secret-name: {WEBHOOK_CERT_SECRET}\n"},
                  {"target": {"kind": "MutatingWebhookConfiguration"}, "patch":
                   "- op: add\n  path: /metadata/annotations\n  value:\n    service.beta.openshift.io/"
-                  "inject-cabundle: \"true\"\n"},
-                 {"target": {"kind": "ConfigMap", "name": ".*config"}, "patch":
-                  "- op: replace\n  path: /data/ADD_FSGROUP\n  value: \"false\"\n"}])
-    t["overlays/mi355x/kustomization.yaml"] = kustomization(
-        ["../../default"],
-        patches=[{"target": {"kind": "ConfigMap", "name": ".*config"}, "patch":
-                  "- op: replace\n  path: /data/GPU_NODE_SELECTOR\n  value: \"true\"\n"
-                  "- op: replace\n  path: /data/GPU_SHM_SIZE_PER_GPU\n  value: 16Gi\n"
-                  # multi-GPU notebooks: RCCL's intra-node IPC over dmabuf (hosts whose amdgpu
-                  # driver only offers dmabuf IPC fail hipIpcGetMemHandle otherwise)
-                  "- op: replace\n  path: /data/MULTI_GPU_ENV\n  value: HSA_ENABLE_IPC_MODE_LEGACY=0\n"},
-                 {"target": {"kind": "ConfigMap", "name": ".*culler-config"}, "patch":
-                  "- op: replace\n  path: /data/CULLING_ACTIVITY_SOURCE\n  value: combined\n"
-                  "- op: replace\n  path: /data/ENABLE_CULLING\n  value: \"true\"\n"}])
+                  "inject-cabundle: \"true\"\n"}])
+    mi355x_generators = [{"name": "config", "behavior": "merge", "literals": list(MI355X_PARAMS)},
+                         {"name": "notebook-controller-culler-config", "behavior": "merge",
+                          "literals": list(MI355X_CULLER)}]
+    t["overlays/mi355x/kustomization.yaml"] = kustomization(["../../default", "../../webhook-certs"],
+                                                            namespace="opendatahub",
+                                                            configMapGenerator=mi355x_generators)
+    # the serving cert covers every shard's Service; every shard's configuration gets the caBundle
+    svc_names = [NAME_PREFIX + o["metadata"]["name"] for o in cp["services.yaml"][1:]]
+    mwc_names = [NAME_PREFIX + o["metadata"]["name"] for o in cp["webhooks.yaml"]]
+    t["overlays/mi355x-sharded/kustomization.yaml"] = kustomization(
+        ["../../crd", "../../user-rbac", "../../node-agent", "../../webhook-certs", "../../control-plane"],
+        namespace="opendatahub", namePrefix=NAME_PREFIX, configMapGenerator=mi355x_generators,
+        patches=_certs_args_patches(svc_names, mwc_names))
     t["samples/notebook_v1_1gpu.yaml"] = sample("rocm-pytorch-1gpu", 1)
     t["samples/notebook_v1_8gpu_auth.yaml"] = sample("rocm-pytorch-8gpu", 8, auth=True)
     t["samples/notebook_v1alpha1.yaml"] = sample("rocm-pytorch-v1alpha1", 1, "v1alpha1")

@@ -95,6 +95,22 @@ def cert_not_after(pem: str) -> Optional[float]:
         return None
 
 
+def cert_sans(pem: str) -> Optional[set]:
+    """DNS / IP subject alternative names of a PEM certificate (``openssl x509 -ext``)."""
+    try:
+        out = subprocess.run(["openssl", "x509", "-noout", "-ext", "subjectAltName"], input=pem.encode(),
+                             check=True, capture_output=True).stdout.decode()
+    except (subprocess.CalledProcessError, OSError):
+        return None
+    sans = set()
+    for line in out.splitlines()[1:]:
+        for part in line.split(","):
+            kind, _, val = part.strip().partition(":")
+            if kind in ("DNS", "IP Address") and val:
+                sans.add(val.strip())
+    return sans
+
+
 def cert_matches_key(cert_pem: str, key_pem: str) -> bool:
     def pub(args, data):
         r = subprocess.run(args, input=data.encode(), capture_output=True)
@@ -105,11 +121,15 @@ def cert_matches_key(cert_pem: str, key_pem: str) -> bool:
 
 
 async def provision(client, namespace: str, secret_name: str = "odh-notebook-controller-webhook-cert",
-                    service_name: str = "odh-notebook-controller-webhook-service",
+                    service_name="odh-notebook-controller-webhook-service",
                     mwc_names: Iterable[str] = ("odh-notebook-controller-mutating-webhook-configuration",),
                     extra_hosts: Iterable[str] = (), validity_days: int = 365, renew_before_days: int = 90,
                     cluster_domain: str = "cluster.local") -> dict:
     """Ensure the serving Secret holds a valid cert and every named MWC trusts its CA.
+
+    ``service_name``: one Service name or several (a sharded control plane serves admission
+    behind one Service per shard plus one for unassigned namespaces; the cert covers all).
+    A kept cert must still cover every wanted name, otherwise it is reissued.
 
     Returns ``{"secret": "created"|"rotated"|"kept", "mwc": {name: "patched"|"kept"|"missing"}}``.
     """
@@ -130,15 +150,17 @@ async def provision(client, namespace: str, secret_name: str = "odh-notebook-con
     except ApiError as e:
         if not is_not_found(e):
             raise
+    services = [service_name] if isinstance(service_name, str) else list(service_name)
+    hosts = [h for svc in services for h in service_hosts(svc, namespace, cluster_domain)] + list(extra_hosts)
     data = (secret or {}).get("data") or {}
     crt, key, ca = unb64(data.get("tls.crt")), unb64(data.get("tls.key")), unb64(data.get("ca.crt"))
     exp = cert_not_after(crt) if crt else None
     fresh = bool(crt and key and ca and exp and exp - time.time() > renew_before_days * 86400
-                 and cert_matches_key(crt, key))
+                 and cert_matches_key(crt, key) and set(hosts) <= (cert_sans(crt) or set()))
     result = {"secret": "kept", "mwc": {}}
     if not fresh:
         with tempfile.TemporaryDirectory(prefix="odh-webhook-certs-") as d:
-            g = generate([*service_hosts(service_name, namespace, cluster_domain), *extra_hosts], d, validity_days)
+            g = generate(hosts, d, validity_days)
             with open(g.cert_file) as f:
                 crt = f.read()
             with open(g.key_file) as f:

@@ -72,7 +72,9 @@ def test_startup_probe_passes_and_sees_all_xcds(dev):
         assert r["xcds"] == 8, r["xcd_blocks"]
         assert sum(r["xcd_blocks"]) == p.tiles == (shape[0] // (256 if fused else 128)) * (
             shape[1] // (256 if fused else 128))
-        assert r["gemm_tflops"] > 50 and r["hbm_gbps"] > 500, r
+        # sanity floors, far below the MFMA rates (a non-MFMA fallback would sit near 1 TFLOP/s):
+        # the 1.2 GFLOP shape runs ~25 us, so its rate is launch- and clock-ramp-bound
+        assert r["gemm_tflops"] > (50 if fused else 15) and r["hbm_gbps"] > 500, r
 
 
 def test_fused_probe_verify_detects_corrupted_operand(dev):

@@ -105,3 +105,158 @@ def test_samples_request_mi355x_and_validate():
         res = doc["spec"]["template"]["spec"]["containers"][0]["resources"]
         assert int(res["limits"]["amd.com/gpu"]) in (1, 8)
         assert "rocm" in doc["spec"]["template"]["spec"]["containers"][0]["image"]
+
+
+# ------------------------------------------------------------------ rendered overlays
+
+OVERLAYS = ("standalone", "kubeflow", "openshift", "mi355x", "mi355x-sharded")
+
+
+def _render(overlay):
+    from odh_kubeflow_amd.deploy import kustomize
+
+    return kustomize.build(os.path.join(ROOT, "config", "overlays", overlay))
+
+
+def _by(objs, kind):
+    return {o["metadata"]["name"]: o for o in objs if o["kind"] == kind}
+
+
+def _pod_specs(objs):
+    from odh_kubeflow_amd.deploy.kustomize import _pod_spec
+
+    for o in objs:
+        ps = _pod_spec(o)
+        if ps is not None:
+            yield o, ps
+
+
+def test_overlay_configmap_settings_merge_without_touching_other_configmaps():
+    """Overlay settings go through ``configMapGenerator behavior: merge`` on the ``config``
+    ConfigMap (as the reference's overlays do); a ``.*config`` JSON6902 target would also hit
+    ``notebook-controller-culler-config`` and fail to build."""
+    def cms(overlay):
+        return {n.replace("odh-kubeflow-amd-", ""): o.get("data") for n, o in _by(_render(overlay), "ConfigMap").items()}
+
+    base = cms("standalone")
+    assert base["config"]["USE_ISTIO"] == "false" and base["config"]["ADD_FSGROUP"] == "true"
+    assert cms("kubeflow")["config"]["USE_ISTIO"] == "true"
+    assert cms("openshift")["config"]["ADD_FSGROUP"] == "false"
+    for overlay in ("mi355x", "mi355x-sharded"):
+        c = cms(overlay)
+        assert c["config"]["GPU_NODE_SELECTOR"] == "true" and c["config"]["GPU_SHM_SIZE_PER_GPU"] == "16Gi"
+        assert c["config"]["MULTI_GPU_ENV"] == "HSA_ENABLE_IPC_MODE_LEGACY=0"
+        cull = c["notebook-controller-culler-config"]
+        assert cull["ENABLE_CULLING"] == "true" and cull["CULLING_ACTIVITY_SOURCE"] == "combined"
+        assert cull["CULL_IDLE_TIME"] == "1440" and "USE_ISTIO" not in cull
+    for overlay in OVERLAYS:  # the culler ConfigMap never receives the params keys
+        assert set(cms(overlay)["notebook-controller-culler-config"]) == set(
+            x.split("=")[0] for x in manifests.CULLER_LITERALS)
+
+
+def test_broad_configmap_regex_patch_fails_like_kustomize(tmp_path):
+    """The renderer reproduces kustomize's failure for the old ``.*config`` target."""
+    from odh_kubeflow_amd.deploy import kustomize
+
+    base = tmp_path / "base"
+    base.mkdir()
+    (base / "kustomization.yaml").write_text(yaml.safe_dump({
+        "configMapGenerator": [{"name": "config", "literals": ["A=1"]},
+                               {"name": "culler-config", "literals": ["B=2"]}],
+        "generatorOptions": {"disableNameSuffixHash": True}, "namePrefix": "p-"}))
+    ov = tmp_path / "ov"
+    ov.mkdir()
+    (ov / "kustomization.yaml").write_text(yaml.safe_dump({
+        "resources": ["../base"],
+        "patches": [{"target": {"kind": "ConfigMap", "name": ".*config"},
+                     "patch": "- op: replace\n  path: /data/A\n  value: '3'\n"}]}))
+    with pytest.raises(kustomize.KustomizeError, match="culler-config"):
+        kustomize.build(str(ov))
+
+
+@pytest.mark.parametrize("overlay", OVERLAYS)
+def test_overlay_references_resolve(overlay):
+    """Every name a rendered overlay refers to exists in it: ConfigMaps, ServiceAccounts,
+    roles, webhook Services, the serving-cert Secret/Services/MWCs the certs Job manages."""
+    objs = _render(overlay)
+    cms, sas, svcs = _by(objs, "ConfigMap"), _by(objs, "ServiceAccount"), _by(objs, "Service")
+    roles = {**_by(objs, "Role"), **_by(objs, "ClusterRole")}
+    mwcs = _by(objs, "MutatingWebhookConfiguration")
+    for o in objs:
+        if o["kind"] not in manifests_cluster_scoped():
+            assert o["metadata"].get("namespace"), (overlay, o["kind"], o["metadata"]["name"])
+    ns = {o["metadata"]["namespace"] for o in objs if o["metadata"].get("namespace")}
+    assert len(ns) == 1
+    pod_labels = []
+    cert_secret_mounts = set()
+    for o, ps in _pod_specs(objs):
+        assert ps["serviceAccountName"] in sas, (o["metadata"]["name"], ps["serviceAccountName"])
+        pod_labels.append(((o.get("spec") or {}).get("template") or {}).get("metadata", {}).get("labels") or {})
+        for c in ps["containers"]:
+            for ef in c.get("envFrom") or []:
+                assert ef["configMapRef"]["name"] in cms
+            for e in c.get("env") or []:
+                ref = (e.get("valueFrom") or {}).get("configMapKeyRef")
+                if ref and not ref.get("optional"):
+                    assert ref["name"] in cms
+                if ref and ref["name"] in cms:
+                    assert ref["key"] in cms[ref["name"]]["data"], (ref, overlay)
+        for v in ps.get("volumes") or []:
+            if "secret" in v and v["secret"]["secretName"] == manifests.WEBHOOK_CERT_SECRET:
+                cert_secret_mounts.add(v["secret"]["secretName"])
+    for b in list(_by(objs, "RoleBinding").values()) + list(_by(objs, "ClusterRoleBinding").values()):
+        assert b["roleRef"]["name"] in roles, b["metadata"]["name"]
+        for sub in b["subjects"]:
+            assert sub["name"] in sas and sub["namespace"] in ns, (b["metadata"]["name"], sub)
+    for name, w in mwcs.items():
+        svc = w["webhooks"][0]["clientConfig"]["service"]
+        assert svc["name"] in svcs and svc["namespace"] in ns, (name, svc)
+        sel = svcs[svc["name"]]["spec"]["selector"]
+        assert any(all(lb.get(k) == v for k, v in sel.items()) for lb in pod_labels) or \
+            "statefulset.kubernetes.io/pod-name" in sel, (name, sel)
+    assert cert_secret_mounts == {manifests.WEBHOOK_CERT_SECRET}
+    jobs = _by(objs, "Job")
+    if overlay == "openshift":
+        assert not jobs  # service-ca provides the cert and the caBundle
+        return
+    for jname, path in (("webhook-certs", ("spec",)), ("webhook-certs-renew", ("spec", "jobTemplate", "spec"))):
+        job = {n.replace("odh-kubeflow-amd-", ""): o for n, o in {**jobs, **_by(objs, "CronJob")}.items()}[jname]
+        for p in path:
+            job = job[p]
+        args = job["template"]["spec"]["containers"][0]["args"]
+        want_svcs = {a.split("=", 1)[1] for a in args if a.startswith("--service-name=")}
+        want_mwcs = {a.split("=", 1)[1] for a in args if a.startswith("--mwc-name=")}
+        assert want_svcs and want_svcs <= set(svcs) and want_mwcs == set(mwcs), (overlay, want_svcs, want_mwcs)
+        assert f"--secret-name={manifests.WEBHOOK_CERT_SECRET}" in args
+
+
+def manifests_cluster_scoped():
+    from odh_kubeflow_amd.deploy.kustomize import CLUSTER_SCOPED
+
+    return CLUSTER_SCOPED
+
+
+def test_sharded_overlay_shape():
+    """mi355x-sharded: one control-plane replica per MI355X, each shard's webhook Service
+    selects exactly its replica, each shard's configuration selects its namespaces, and
+    not-yet-assigned namespaces go to any shard."""
+    objs = _render("mi355x-sharded")
+    assert not _by(objs, "Deployment")  # the two cluster-wide managers are not deployed
+    (sts,) = _by(objs, "StatefulSet").values()
+    n = sts["spec"]["replicas"]
+    assert n == manifests.SHARDS == 8
+    args = sts["spec"]["template"]["spec"]["containers"][0]["args"]
+    assert "--shard=ordinal" in args and f"--shard-count={n}" in args and "--assign-namespaces" in args
+    svcs = _by(objs, "Service")
+    mwcs = _by(objs, "MutatingWebhookConfiguration")
+    assert len(mwcs) == n + 1
+    for k in range(n):
+        w = mwcs[f"odh-kubeflow-amd-notebook-webhook-shard-{k}"]["webhooks"][0]
+        assert w["namespaceSelector"] == {"matchLabels": {"notebooks.amd.com/shard": str(k)}}
+        svc = svcs[w["clientConfig"]["service"]["name"]]
+        assert svc["spec"]["selector"] == {"statefulset.kubernetes.io/pod-name": f"{sts['metadata']['name']}-{k}"}
+    w = mwcs["odh-kubeflow-amd-notebook-webhook-unassigned"]["webhooks"][0]
+    assert w["namespaceSelector"]["matchExpressions"] == [{"key": "notebooks.amd.com/shard", "operator": "DoesNotExist"}]
+    role = _by(objs, "ClusterRole")["odh-kubeflow-amd-control-plane-role"]
+    assert _allowed(role, "", "namespaces", "patch") and _allowed(role, "apps", "statefulsets", "create")
+    assert _allowed(role, "gateway.networking.k8s.io", "httproutes", "delete")

@@ -50,6 +50,8 @@ class ClusterConfig:
     # and the node agents talk to it over HTTP exactly as they would to kube-apiserver
     transport: str = field(default_factory=lambda: os.environ.get("ODH_CLUSTER_TRANSPORT", "inprocess"))
     remote_kubelets: bool = True  # with transport="http": node agents use REST clients too
+    # Gateway API implementation stand-in (HTTPRoute ResolvedRefs status); default: with odh
+    gateway: Optional[bool] = None
 
 
 OPENSHIFT_CRDS = (kinds.IMAGE_STREAM, kinds.PROXY, kinds.ROUTE, kinds.OAUTH_CLIENT)
@@ -147,6 +149,10 @@ class LocalCluster:
             .setup_with_manager(kube)
         SchedulerController(kube.client, kube.reader, kube.get_event_recorder_for("default-scheduler")) \
             .setup_with_manager(kube)
+        if cfg.gateway or (cfg.gateway is None and cfg.odh):
+            from .kubelet.gateway import GatewayRouteResolver
+
+            GatewayRouteResolver(kube.client, kube.reader).setup_with_manager(kube)
 
         # nodes + per-GPU runtimes
         for n in range(cfg.nodes):

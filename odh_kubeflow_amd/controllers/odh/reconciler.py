@@ -45,7 +45,8 @@ from typing import Dict, List, Mapping, Optional
 from ...models import kinds
 from ...models import meta as m
 from ...models.errors import ApiError, is_no_match, is_not_found
-from ...runtime.controller import Request, Result, controller_owner_alive, generation_or_metadata_changed
+from ...runtime.controller import (Request, Result, controller_owner_alive, fields_changed,
+                                   generation_or_metadata_changed)
 from ...runtime.retry import retry_on_conflict
 from ...tracing import get_tracer
 from . import auth, certs, dspa_secret, network, oauth, rbac, route, runtime_images
@@ -334,7 +335,9 @@ class OpenshiftNotebookReconciler:
                 lb = m.labels(o)
                 nb = self.reader.get(NOTEBOOK_KIND, lb.get("notebook-name", ""), lb.get("notebook-namespace", ""))
                 return nb is not None and not m.is_deleting(nb)
-            route_preds = [route_nb_alive]
+            # the Gateway implementation's status writes (ResolvedRefs, …) are not drift: the
+            # reconcile compares spec + labels only
+            route_preds = [route_nb_alive, fields_changed("spec", "metadata.labels")]
 
         b = (mgr.builder().named("odh-notebook-controller")
              .for_(NOTEBOOK_KIND, nb_preds)

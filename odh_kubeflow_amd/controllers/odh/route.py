@@ -8,9 +8,15 @@ Reference: ``odh/controllers/notebook_route.go`` and ``notebook_referencegrant.g
   ``nb-<ns[:10]>-<name[:10]>-`` (:50-74).  parentRef defaults to
   ``openshift-ingress/data-science-gateway`` (``NOTEBOOK_GATEWAY_NAME`` /
   ``NOTEBOOK_GATEWAY_NAMESPACE``).  PathPrefix ``/notebook/<ns>/<name>`` → Service
-  ``<name>`` port 8888 (the reference's choice; the kf Service itself listens on 80 —
-  SURVEY §2.1 row 12 — so port 8888 routes through the pod's named target port
-  mapping of Gateway implementations that resolve ``targetPort``; kept for parity).
+  ``<name>`` **port 80**.  Deliberate fix: the reference targets port 8888
+  (``odh/controllers/notebook_route.go:120``), but the kf Service it routes to exposes
+  only port 80 → targetPort 8888 (``kf/controllers/notebook_controller.go:49-50,525-552``),
+  and a Gateway API backendRef's ``port`` is the *Service* port.  The reference's plain
+  (non-auth) route therefore never resolves (``ResolvedRefs=False/BackendNotFound``;
+  ``kubelet/gateway.py`` reproduces what implementations report; its e2e checks only
+  the auth route, ``odh/e2e/notebook_creation_test.go:398-411``).  Routes a reference
+  controller left at 8888 are recognised as the plain route and corrected to 80 by the
+  drift check.
 * In auth mode the backend is ``<name>-kube-rbac-proxy`` port 8443, and the route of
   the other mode is deleted on a switch (:269-324).
 * ReferenceGrant ``notebook-httproute-access`` in the user namespace lets HTTPRoutes
@@ -28,6 +34,7 @@ from ...models import kinds
 from ...models import meta as m
 from ...models.errors import ApiError, is_already_exists, is_not_found
 from ...runtime.retry import retry_on_conflict
+from ...models.notebook import DEFAULT_SERVING_PORT as NOTEBOOK_SERVICE_PORT  # the kf Service's port (80)
 from .constants import (DEFAULT_GATEWAY_NAME, DEFAULT_GATEWAY_NAMESPACE, HTTPROUTE_SUBDOMAIN_MAX_LEN,
                         KUBE_RBAC_PROXY_PORT, KUBE_RBAC_PROXY_SERVICE_SUFFIX, NOTEBOOK_PORT, REFERENCE_GRANT_NAME)
 
@@ -57,7 +64,7 @@ def new_notebook_httproute(nb: dict, central_namespace: str, env: Mapping[str, s
             "parentRefs": [{"name": gw_name, "namespace": gw_ns}],
             "rules": [{
                 "matches": [{"path": {"type": "PathPrefix", "value": f"/notebook/{ns}/{name}"}}],
-                "backendRefs": [{"name": name, "namespace": ns, "port": NOTEBOOK_PORT}],
+                "backendRefs": [{"name": name, "namespace": ns, "port": NOTEBOOK_SERVICE_PORT}],
             }],
         },
     }
@@ -128,7 +135,7 @@ async def ensure_conflicting_httproute_absent(client, nb: dict, central_namespac
         br = rules[0]["backendRefs"][0]
         bname, bport = br.get("name"), br.get("port")
         is_proxy = bname == m.name(nb) + KUBE_RBAC_PROXY_SERVICE_SUFFIX or bport == KUBE_RBAC_PROXY_PORT
-        is_regular = bname == m.name(nb) or bport == NOTEBOOK_PORT
+        is_regular = bname == m.name(nb) or bport in (NOTEBOOK_SERVICE_PORT, NOTEBOOK_PORT)
         if (auth_mode and is_regular) or (not auth_mode and is_proxy):
             log.info("deleting conflicting HTTPRoute %s (auth_mode=%s)", m.name(r), auth_mode)
             try:

@@ -53,7 +53,7 @@ def test_httproute_lifecycle(run):
             assert r["spec"]["parentRefs"] == [{"name": "data-science-gateway", "namespace": "openshift-ingress"}]
             rule = r["spec"]["rules"][0]
             assert rule["matches"] == [{"path": {"type": "PathPrefix", "value": "/notebook/user/nb"}}]
-            assert rule["backendRefs"] == [{"name": "nb", "namespace": "user", "port": 8888}]
+            assert rule["backendRefs"] == [{"name": "nb", "namespace": "user", "port": 80}]
             nb = cl.store.peek(kinds.NOTEBOOK, "nb", "user")
             assert {"notebook.opendatahub.io/httproute-cleanup",
                     "notebook.opendatahub.io/referencegrant-cleanup"} <= set(m.finalizers(nb))
@@ -64,7 +64,7 @@ def test_httproute_lifecycle(run):
             r = await cl.admin.get(kinds.HTTP_ROUTE, "nb-user-nb", CENTRAL)
             r["spec"]["rules"][0]["backendRefs"][0]["port"] = 9999
             await cl.admin.update(r)
-            assert await cl.wait_for(lambda: route_for(cl, "nb")[0]["spec"]["rules"][0]["backendRefs"][0]["port"] == 8888)
+            assert await cl.wait_for(lambda: route_for(cl, "nb")[0]["spec"]["rules"][0]["backendRefs"][0]["port"] == 80)
             # deleted route is recreated
             await cl.admin.delete(kinds.HTTP_ROUTE, "nb-user-nb", CENTRAL)
             assert await cl.wait_for(lambda: len(route_for(cl, "nb")) == 1)
@@ -202,7 +202,7 @@ def test_mode_switching(run):
         async with LocalCluster(cfg()) as cl:
             await create_nb(cl, "nb")
             assert await cl.wait_for(lambda: len(route_for(cl, "nb")) == 1)
-            assert route_for(cl, "nb")[0]["spec"]["rules"][0]["backendRefs"][0]["port"] == 8888
+            assert route_for(cl, "nb")[0]["spec"]["rules"][0]["backendRefs"][0]["port"] == 80
             await cl.admin.patch(kinds.NOTEBOOK, {"metadata": {"annotations": AUTH}}, name="nb", namespace="user")
             assert await cl.wait_for(lambda: len(route_for(cl, "nb")) == 1 and route_for(cl, "nb")[0]["spec"]["rules"]
                                      [0]["backendRefs"][0]["port"] == 8443)
@@ -211,7 +211,7 @@ def test_mode_switching(run):
             await cl.admin.patch(kinds.NOTEBOOK, {"metadata": {"annotations": {
                 "notebooks.opendatahub.io/inject-auth": "false"}}}, name="nb", namespace="user")
             assert await cl.wait_for(lambda: len(route_for(cl, "nb")) == 1 and route_for(cl, "nb")[0]["spec"]["rules"]
-                                     [0]["backendRefs"][0]["port"] == 8888)
+                                     [0]["backendRefs"][0]["port"] == 80)
             assert await cl.wait_for(lambda: cl.store.peek(kinds.CLUSTER_ROLE_BINDING, "nb-rbac-user-auth-delegator")
                                      is None)
     run(go())

@@ -198,7 +198,7 @@ def test_notebook_without_auth_has_no_sidecar_and_an_unauthenticated_route(run):
             assert [c["name"] for c in nb["spec"]["template"]["spec"]["containers"]] == ["nb"]
             assert "notebook.opendatahub.io/kube-rbac-proxy-cleanup" not in m.finalizers(nb)
             assert route_for(cl, "nb")[0]["spec"]["rules"][0]["backendRefs"] == [
-                {"name": "nb", "namespace": "user", "port": 8888}]
+                {"name": "nb", "namespace": "user", "port": 80}]
             for k, n in ((kinds.SERVICE_ACCOUNT, "nb"), (kinds.SERVICE, "nb-kube-rbac-proxy"),
                          (kinds.CONFIG_MAP, "nb-kube-rbac-proxy-config")):
                 assert cl.store.peek(k, n, "user") is None

@@ -7,7 +7,9 @@ the cache rather than a cluster-wide live List.  ``notebook_culling_total`` and
 reference defines them but leaves them out of Describe/Collect (metrics.go:67-79),
 so they never reach ``/metrics``; that is treated as a bug here.
 Two MI355X additions: ``notebook_gpus_allocated{namespace}`` (``amd.com/gpu`` limits
-of running notebooks) and ``notebook_pod_ready_seconds`` (create→Ready latency).
+of running notebooks) and ``notebook_pod_ready_seconds`` (start→Ready latency, observed
+by the kf reconciler when a Notebook's status turns Ready: from the Notebook's creation
+for its first pod, from the pod's creation for a resumed or restarted one).
 """
 
 from __future__ import annotations
@@ -17,6 +19,12 @@ from prometheus_client.core import GaugeMetricFamily
 
 from ..models import kinds
 from ..models.notebook import NOTEBOOK_NAME_LABEL, gpu_request
+from ..utils.timeutil import now as _now
+from ..utils.timeutil import parse_rfc3339
+
+# a pod created within this long of its Notebook is the Notebook's first pod (admission,
+# lock removal and StatefulSet creation take seconds; a resumed notebook's pod comes later)
+FIRST_POD_WINDOW_S = 300.0
 
 
 class _RunningCollector:
@@ -68,6 +76,19 @@ class NotebookMetrics:
                                                 "Timestamp of the last notebook culling in seconds",
                                                 ["namespace", "name"], registry=registry)
         self.pod_ready_seconds = Histogram("notebook_pod_ready_seconds",
-                                           "Seconds from Notebook creation to its pod reporting Ready",
+                                           "Seconds from Notebook creation (first pod) or pod creation "
+                                           "(resume/restart) to the Notebook reporting Ready",
                                            ["namespace"], registry=registry,
                                            buckets=(0.05, 0.1, 0.25, 0.5, 1, 2, 5, 10, 30, 60, 120, 300))
+
+    def observe_ready(self, nb: dict, pod, now=None) -> float:
+        """Record one start→Ready latency (called on the Notebook's transition to Ready)."""
+        md = nb.get("metadata") or {}
+        nb_t = parse_rfc3339(md.get("creationTimestamp"))
+        pod_t = parse_rfc3339(((pod or {}).get("metadata") or {}).get("creationTimestamp"))
+        start = nb_t if (pod_t is None or (nb_t is not None and pod_t - nb_t < FIRST_POD_WINDOW_S)) else pod_t
+        if start is None:
+            return -1.0
+        dt = max(0.0, (_now() if now is None else now) - start)
+        self.pod_ready_seconds.labels(md.get("namespace", "")).observe(dt)
+        return dt

@@ -258,6 +258,12 @@ def create_notebook_status(nb: dict, sts: Optional[dict], pod: Optional[dict], n
     return status
 
 
+def notebook_status_ready(status: dict) -> bool:
+    """readyReplicas ≥ 1 and a ``Ready=True`` condition mirrored from the pod."""
+    return bool((status or {}).get("readyReplicas")) and any(
+        c.get("type") == "Ready" and c.get("status") == "True" for c in (status or {}).get("conditions") or [])
+
+
 def _cond_key(c: dict):
     return (c.get("type"), c.get("status"), c.get("reason"), c.get("message"))
 
@@ -360,6 +366,8 @@ class NotebookReconciler:
 
         status = create_notebook_status(nb, found, pod)
         old_status = nb.get("status") or {}
+        if self.metrics is not None and notebook_status_ready(status) and not notebook_status_ready(old_status):
+            self.metrics.observe_ready(nb, pod)
         if self.unconditional_status:
             nb["status"] = status
             self.status_writes += 1

@@ -264,3 +264,50 @@ def test_multi_gpu_env_defaults():
     assert e["NB_PREFIX"] == "/notebook/ns/nb"  # a variable already set wins
     assert "HSA_ENABLE_IPC_MODE_LEGACY" not in env_of(notebook("nb", "ns", gpus=1))  # one GPU: no collectives
     assert "HSA_ENABLE_IPC_MODE_LEGACY" not in env_of(notebook("nb", "ns"))
+
+
+def test_pod_ready_seconds_observed_on_ready_transitions(run):
+    """``notebook_pod_ready_seconds`` (declared in round 1, never observed) is recorded once
+    per transition to Ready — creation, then resume — and exported on /metrics."""
+    from prometheus_client import generate_latest
+
+    def count(cl):
+        for line in generate_latest(cl.kf.registry).decode().splitlines():
+            if line.startswith('notebook_pod_ready_seconds_count{namespace="user"}'):
+                return float(line.split()[-1])
+        return 0.0
+
+    async def go():
+        async with LocalCluster(ClusterConfig()) as cl:
+            await cl.ensure_namespace("user")
+            await cl.admin.create(notebook("nb1", "user", gpus=1))
+            assert await cl.wait_for(lambda: cl.notebook_ready("nb1", "user"), 10)
+            assert await cl.settle()
+            assert count(cl) == 1
+            cl.kf.controllers[0].enqueue(Request("user", "nb1"))  # steady state: no new sample
+            assert await cl.settle()
+            assert count(cl) == 1
+            await cl.admin.patch(kinds.NOTEBOOK, {"metadata": {"annotations": {"kubeflow-resource-stopped": "t"}}},
+                                 name="nb1", namespace="user")
+            assert await cl.wait_for(lambda: not cl.notebook_ready("nb1", "user"))
+            await cl.admin.patch(kinds.NOTEBOOK, {"metadata": {"annotations": {"kubeflow-resource-stopped": None}}},
+                                 name="nb1", namespace="user")
+            assert await cl.wait_for(lambda: cl.notebook_ready("nb1", "user"), 10)
+            assert await cl.settle()
+            assert count(cl) == 2
+    run(go())
+
+
+def test_pod_ready_seconds_start_time_rule():
+    from prometheus_client import CollectorRegistry
+
+    from odh_kubeflow_amd.controllers.metrics import NotebookMetrics
+    from odh_kubeflow_amd.utils.timeutil import parse_rfc3339
+
+    mt = NotebookMetrics(type("R", (), {"list": lambda *a, **k: []})(), CollectorRegistry())
+    nb = {"metadata": {"namespace": "u", "creationTimestamp": "2026-01-01T00:00:00Z"}}
+    first = {"metadata": {"creationTimestamp": "2026-01-01T00:00:02Z"}}
+    resumed = {"metadata": {"creationTimestamp": "2026-01-02T00:00:00Z"}}
+    t0 = parse_rfc3339("2026-01-01T00:00:00Z")
+    assert mt.observe_ready(nb, first, now=t0 + 30) == 30  # first pod: from the Notebook's creation
+    assert mt.observe_ready(nb, resumed, now=t0 + 86400 + 7) == 7  # resumed: from the pod's creation

@@ -69,11 +69,12 @@ for s in $steps; do
     pmc)
       # one counter group per pass, each within the per-block limits
       i=0
-      for group in "SQ_WAVES SQ_INSTS_VALU_MFMA_MOPS_BF16 SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES" \
-                   "SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_LDS" \
-                   "FETCH_SIZE" "WRITE_SIZE"; do
+      timeout -k 10 60 rocprofv3 --list-avail > "$out/pmc_avail.txt" 2>&1 || true
+      for group in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_VALU_MFMA_BUSY_CYCLES" \
+                   "SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_LDS_UNALIGNED_STALL" \
+                   "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum"; do
         i=$((i + 1))
-        timeout -s KILL 90 rocprofv3 --pmc $group --kernel-trace --stats -d "$out/pmc$i" -o run -- \
+        timeout -s KILL 90 rocprofv3 --pmc $group --output-format csv -d "$out/pmc$i" -o run -- \
           python3 tools/probe_microbench.py --pmc-pass > "$out/pmc$i.log" 2>&1 || fail "pmc$i" $? "$out/pmc$i.log"
       done
       echo "pmc passes: $i" ;;

@@ -128,5 +128,26 @@ def main():
     print(json.dumps(out, indent=1))
 
 
+def pmc_pass():
+    """A short, fixed workload for ``rocprofv3 --pmc`` passes: the node agent's start-up
+    probe as it runs on the notebook path (fused-verify 4096³ bf16 MFMA GEMM + 1 GiB HBM
+    pattern write/check) ×10, and the standalone 256² GEMM at 8192³ ×3."""
+    p = gpu.GpuProbe(0)
+    for _ in range(10):
+        assert p.run()["ok"]
+    dev = torch.device("cuda", 0)
+    n = 8192
+    a = torch.ones((n, n), device=dev, dtype=torch.bfloat16)
+    bt = torch.ones((n, n), device=dev, dtype=torch.bfloat16)
+    c = torch.empty((n, n), dtype=torch.float32, device=dev)
+    for _ in range(3):
+        gpu.gemm_bf16(a, bt, out=c)
+    torch.cuda.synchronize()
+    print("pmc pass ok")
+
+
 if __name__ == "__main__":
-    main()
+    if "--pmc-pass" in sys.argv:
+        pmc_pass()
+    else:
+        main()

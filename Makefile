@@ -4,7 +4,7 @@ IMG ?= quay.io/opendatahub/odh-kubeflow-amd:latest
 NOTEBOOK_IMG ?= quay.io/opendatahub/workbench-rocm-pytorch:latest
 GPU_ARCH ?= gfx950
 
-.PHONY: build test test-native test-gpu e2e bench bench-8 manifests deploy undeploy docker-build docker-build-notebook
+.PHONY: build test test-native test-gpu e2e bench bench-8 manifests deploy deploy-sharded undeploy lint license-check docker-build docker-build-notebook
 
 build:  ## hipcc --offload-arch=$(GPU_ARCH) kernels, host C++ telemetry/objcore, native apiserver (in-tree)
 	ODH_GPU_ARCH=$(GPU_ARCH) $(PYTHON) -m odh_kubeflow_amd.ops.build
@@ -33,8 +33,17 @@ manifests:  ## regenerate the kustomize tree under config/
 deploy: manifests  ## kubectl apply the MI355X overlay (CRD, RBAC, managers, webhook, node agent)
 	kubectl apply -k config/overlays/mi355x
 
+deploy-sharded: manifests  ## kubectl apply the sharded MI355X overlay (one control-plane shard per GPU)
+	kubectl apply -k config/overlays/mi355x-sharded
+
 undeploy:
 	kubectl delete -k config/overlays/mi355x --ignore-not-found
+
+lint:  ## static analysis: Python AST rules, secrets, rendered manifests, -Wall -Wextra -Werror native builds
+	$(PYTHON) tools/lint.py
+
+license-check:  ## runtime dependencies carry permissive licences (kf/third_party/check-license.sh)
+	$(PYTHON) tools/licenses.py
 
 docker-build: build  ## controller / node-agent image (ROCm base; kernels built for $(GPU_ARCH))
 	docker build -f images/Dockerfile --build-arg GPU_ARCH=$(GPU_ARCH) -t $(IMG) .

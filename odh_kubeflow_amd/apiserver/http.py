@@ -177,7 +177,8 @@ class WebhookDispatcher:
                 return obj
 
             if self._session is None or self._session.closed:
-                self._session = aiohttp.ClientSession()
+                # admission calls carry the webhook's own timeoutSeconds; this bounds anything else
+                self._session = aiohttp.ClientSession(timeout=aiohttp.ClientTimeout(total=30))
             review = {"apiVersion": "admission.k8s.io/v1", "kind": "AdmissionReview",
                       "request": {"uid": str(uuid.uuid4()), "operation": op, "name": m.name(obj),
                                   "namespace": m.namespace(obj), "object": obj, "oldObject": old,

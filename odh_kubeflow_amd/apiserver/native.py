@@ -84,7 +84,7 @@ class NativeApiServer:
     async def stats(self) -> dict:
         import aiohttp
 
-        async with aiohttp.ClientSession() as s:
+        async with aiohttp.ClientSession(timeout=aiohttp.ClientTimeout(total=30)) as s:
             async with s.get(self.url + "/metrics") as r:
                 return await r.json(content_type=None)
 

@@ -16,7 +16,6 @@ from typing import Callable, Dict, List, Optional
 
 from .apiserver.store import ObjectStore
 from .models import kinds
-from .models import meta as m
 from .runtime.manager import Manager
 
 

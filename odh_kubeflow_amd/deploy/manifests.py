@@ -167,6 +167,12 @@ def _probes(port: int = 8081) -> dict:
                                "periodSeconds": 10}}
 
 
+# restricted Pod Security profile for every controller container (the node agent is the one
+# root container: the kubelet pod-resources socket is root-only; tools/lint.py allows it)
+RESTRICTED = {"allowPrivilegeEscalation": False, "capabilities": {"drop": ["ALL"]}, "runAsNonRoot": True,
+              "seccompProfile": {"type": "RuntimeDefault"}}
+
+
 def _culler_env() -> List[dict]:
     return [{"name": k, "valueFrom": {"configMapKeyRef": {"name": "notebook-controller-culler-config",
                                                           "key": k, "optional": True}}} for k in CULLER_KEYS]
@@ -180,7 +186,7 @@ def kf_deployment() -> dict:
          "env": _culler_env(),
          "ports": [{"name": "metrics", "containerPort": 8080}, {"name": "probes", "containerPort": 8081}],
          "resources": {"requests": {"cpu": "500m", "memory": "256Mi"}, "limits": {"cpu": "2", "memory": "2Gi"}},
-         **_probes()}
+         "securityContext": dict(RESTRICTED), **_probes()}
     return {"apiVersion": "apps/v1", "kind": "Deployment",
             "metadata": {"name": "deployment", "labels": {"app": "notebook-controller"}},
             "spec": {"replicas": 1, "selector": {"matchLabels": {"app": "notebook-controller"}},
@@ -203,7 +209,7 @@ def odh_deployment() -> dict:
                    {"name": "probes", "containerPort": 8081}],
          "resources": {"requests": {"cpu": "500m", "memory": "256Mi"}, "limits": {"cpu": "2", "memory": "4Gi"}},
          "volumeMounts": [{"name": "cert", "mountPath": "/tmp/k8s-webhook-server/serving-certs", "readOnly": True}],
-         **_probes()}
+         "securityContext": dict(RESTRICTED), **_probes()}
     return {"apiVersion": "apps/v1", "kind": "Deployment",
             "metadata": {"name": "manager", "labels": {"app": "odh-notebook-controller"}},
             "spec": {"replicas": 1, "strategy": {"type": "RollingUpdate", "rollingUpdate": {"maxUnavailable": "100%"}},
@@ -292,7 +298,7 @@ def webhook_certs_docs(services: List[str], mwcs: List[str]) -> Dict[str, object
          "command": ["python", "-m", "odh_kubeflow_amd.cmd.webhook_certs"],
          "args": webhook_certs_args(services, mwcs),
          "env": [{"name": "K8S_NAMESPACE", "valueFrom": {"fieldRef": {"fieldPath": "metadata.namespace"}}}],
-         "securityContext": {"allowPrivilegeEscalation": False, "capabilities": {"drop": ["ALL"]}},
+         "securityContext": dict(RESTRICTED),
          "resources": {"requests": {"cpu": "50m", "memory": "64Mi"}, "limits": {"memory": "256Mi"}}}
     pod = {"serviceAccountName": "webhook-certs", "restartPolicy": "OnFailure", "containers": [c]}
     job_spec = {"backoffLimit": 6, "ttlSecondsAfterFinished": 3600, "template": {
@@ -346,7 +352,7 @@ def control_plane_statefulset(shards: int) -> dict:
                    {"name": "probes", "containerPort": 8081}],
          "resources": {"requests": {"cpu": "500m", "memory": "256Mi"}, "limits": {"cpu": "2", "memory": "2Gi"}},
          "volumeMounts": [{"name": "cert", "mountPath": "/tmp/k8s-webhook-server/serving-certs", "readOnly": True}],
-         **_probes()}
+         "securityContext": dict(RESTRICTED), **_probes()}
     labels = {"app": "notebook-control-plane"}
     return {"apiVersion": "apps/v1", "kind": "StatefulSet", "metadata": {"name": "control-plane", "labels": labels},
             "spec": {"replicas": shards, "serviceName": "control-plane", "podManagementPolicy": "Parallel",

@@ -28,7 +28,8 @@ REVISION_LABEL = "controller-revision-hash"
 
 def template_hash(sts: dict) -> str:
     tmpl = (sts.get("spec") or {}).get("template") or {}
-    h = hashlib.sha1(json.dumps(tmpl, sort_keys=True, separators=(",", ":")).encode()).hexdigest()[:10]
+    h = hashlib.sha1(json.dumps(tmpl, sort_keys=True, separators=(",", ":")).encode(),
+                    usedforsecurity=False).hexdigest()[:10]
     return f"{m.name(sts)}-{h}"
 
 

@@ -211,7 +211,8 @@ PyMethodDef methods[] = {
     {"equal_except", py_equal_except, METH_VARARGS, "a == b ignoring the given metadata keys."},
     {nullptr, nullptr, 0, nullptr}};
 
-PyModuleDef module = {PyModuleDef_HEAD_INIT, "_objcore", "Native JSON-tree core", -1, methods};
+PyModuleDef module = {PyModuleDef_HEAD_INIT, "_objcore", "Native JSON-tree core", -1, methods,
+                      nullptr, nullptr, nullptr, nullptr};
 
 }  // namespace
 

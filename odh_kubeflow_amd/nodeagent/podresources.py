@@ -22,7 +22,7 @@ from __future__ import annotations
 import asyncio
 import os
 from dataclasses import dataclass, field
-from typing import Dict, Iterator, List, Optional, Tuple
+from typing import Dict, Iterator, List, Tuple
 
 DEFAULT_SOCKET = "/var/lib/kubelet/pod-resources/kubelet.sock"
 LIST_METHOD = "/v1.PodResourcesLister/List"

@@ -56,7 +56,7 @@ __device__ __forceinline__ int swz(int r, int c) { return r * CH + (c ^ ((r >> 2
 
 __global__ __launch_bounds__(THREADS, 2) void gemm_bf16_kernel(
     const uint4* __restrict__ A, const uint4* __restrict__ Bt, float* __restrict__ C,
-    int M, int N, int K, int* __restrict__ tile_xcd, int* __restrict__ xcd_blocks) {
+    int /*M: the grid covers it*/, int N, int K, int* __restrict__ tile_xcd, int* __restrict__ xcd_blocks) {
   __shared__ uint4 sA[2][BM * CH];
   __shared__ uint4 sB[2][BN * CH];
 
@@ -196,7 +196,7 @@ __device__ int probe_expect(int ia5, int jb7, int K) {
 
 template <bool VERIFY, bool PIPE = true>
 __global__ __launch_bounds__(G_THREADS, 1) void gemm256_kernel(
-    const uint4* __restrict__ A, const uint4* __restrict__ Bt, float* __restrict__ C, int M, int N, int K,
+    const uint4* __restrict__ A, const uint4* __restrict__ Bt, float* __restrict__ C, int /*M*/, int N, int K,
     int* __restrict__ tile_xcd, int* __restrict__ xcd_blocks, unsigned* __restrict__ err_total,
     unsigned* __restrict__ err_xcd) {
   __shared__ uint4 lds[2 * 2 * G_TILE];  // [buffer][A, B][row × chunk]

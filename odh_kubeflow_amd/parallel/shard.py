@@ -235,8 +235,8 @@ class ControlPlaneShard:
         import aiohttp
         from prometheus_client.parser import text_string_to_metric_families
 
-        async with aiohttp.ClientSession() as s:
-            async with s.get(self.metrics_url, timeout=aiohttp.ClientTimeout(total=10)) as r:
+        async with aiohttp.ClientSession(timeout=aiohttp.ClientTimeout(total=10)) as s:
+            async with s.get(self.metrics_url) as r:
                 text = await r.text()
         out: Dict[str, Dict[tuple, float]] = {}
         for fam in text_string_to_metric_families(text):

@@ -53,7 +53,7 @@ class RestConfig:
         if self.insecure:
             ctx = ssl.create_default_context()
             ctx.check_hostname = False
-            ctx.verify_mode = ssl.CERT_NONE
+            ctx.verify_mode = ssl.CERT_NONE  # lint: allow python-ssl-verify-disabled — kubeconfig insecure-skip-tls-verify
         else:
             ctx = ssl.create_default_context(cafile=self.ca_file, cadata=self.ca_data)
         if self.cert_file:

@@ -10,7 +10,6 @@ import pytest
 
 from odh_kubeflow_amd.cluster import ClusterConfig, LocalCluster
 from odh_kubeflow_amd.models import defaults, kinds
-from odh_kubeflow_amd.models import meta as m
 from odh_kubeflow_amd.models.notebook import notebook
 from odh_kubeflow_amd.runtime.controller import Request
 

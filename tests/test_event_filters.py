@@ -8,8 +8,6 @@ gone, while every change a reconcile actually reads (drift, deletion of a live c
 readiness, stop/restart annotations) still triggers one.
 """
 
-import asyncio
-
 from odh_kubeflow_amd.cluster import ClusterConfig, LocalCluster
 from odh_kubeflow_amd.models import kinds
 from odh_kubeflow_amd.models import meta as m

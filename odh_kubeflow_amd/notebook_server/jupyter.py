@@ -49,10 +49,11 @@ class JupyterState:
 
 
 class JupyterServer:
-    def __init__(self, prefix: str, host: str = "127.0.0.1"):
+    def __init__(self, prefix: str, host: str = "127.0.0.1", port: int = 0, info: Optional[dict] = None):
         self.state = JupyterState(prefix)
         self.host = host
-        self.port = 0
+        self.port = port
+        self.info = info or {}  # extra fields of GET <prefix>/api (the workbench's start-up report)
         self._runner = None
 
     async def start(self) -> "JupyterServer":
@@ -69,7 +70,7 @@ class JupyterServer:
             return web.json_response(list(st.terminals.values()))
 
         async def api(_req):
-            return web.json_response({"version": "2.14.0"})
+            return web.json_response({"version": "2.14.0", **self.info})
 
         app = web.Application()
         app.router.add_get(st.prefix + "/api/kernels", kernels)
@@ -77,7 +78,7 @@ class JupyterServer:
         app.router.add_get(st.prefix + "/api", api)
         self._runner = web.AppRunner(app, access_log=None)
         await self._runner.setup()
-        site = web.TCPSite(self._runner, self.host, 0)
+        site = web.TCPSite(self._runner, self.host, self.port)
         await site.start()
         self.port = site._server.sockets[0].getsockname()[1]
         return self

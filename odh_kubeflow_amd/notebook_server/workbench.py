@@ -1,0 +1,77 @@
+"""A PyTorch-ROCm workbench process: what the notebook container runs, minus the image.
+
+    python -m odh_kubeflow_amd.notebook_server.workbench --prefix /notebook/<ns>/<name>
+
+BASELINE configs #2/#3 time a notebook pod requesting ``amd.com/gpu`` becoming Ready on an
+MI355X with a PyTorch-ROCm Jupyter image.  There is no container runtime or registry on
+the benchmark boxes, so the test platform's process runtime
+(:class:`~odh_kubeflow_amd.kubelet.process_runtime.ProcessContainerRuntime`) starts this
+program as the container's process instead: with the allocated GPU made visible
+(``HIP_VISIBLE_DEVICES``, what the AMD device plugin's device mounts amount to) it imports
+PyTorch, initialises the HIP runtime on the GPU, runs a first bf16 matmul (hipBLASLt and
+the MFMA path loaded, the work a user's first cell pays otherwise), then serves the
+Jupyter API the culler and the readiness probe use (``<prefix>/api``, ``/api/kernels``,
+``/api/terminals``).  It prints one JSON line with its port and start-up timings when it
+starts listening — until then the readiness probe is refused, as with a real server.
+"""
+
+from __future__ import annotations
+
+import argparse
+import asyncio
+import json
+import os
+import signal
+import sys
+import time
+
+T_PROC = time.perf_counter()
+
+
+def init_gpu(n: int) -> dict:
+    t0 = time.perf_counter()
+    import torch
+
+    out = {"import_torch_ms": round((time.perf_counter() - t0) * 1e3, 1), "torch": torch.__version__,
+           "hip": getattr(torch.version, "hip", None), "gpu": None}
+    if torch.cuda.is_available() and n > 0:
+        t1 = time.perf_counter()
+        dev = torch.device("cuda", 0)
+        torch.cuda.init()
+        a = torch.randn((n, n), device=dev, dtype=torch.bfloat16)
+        c = a @ a
+        c.float().sum().item()  # synchronises
+        out["gpu"] = torch.cuda.get_device_name(0)
+        out["visible_devices"] = os.environ.get("HIP_VISIBLE_DEVICES")
+        out["first_matmul_ms"] = round((time.perf_counter() - t1) * 1e3, 1)
+        out["hbm_total_gib"] = round(torch.cuda.get_device_properties(0).total_memory / 2 ** 30, 1)
+    return out
+
+
+async def serve(prefix: str, host: str, info: dict) -> None:
+    from .jupyter import JupyterServer
+
+    srv = await JupyterServer(prefix, host, 0, info=info).start()
+    info["ready_ms"] = round((time.perf_counter() - T_PROC) * 1e3, 1)
+    print(json.dumps({"port": srv.port, **info}), flush=True)
+    stop = asyncio.Event()
+    loop = asyncio.get_running_loop()
+    for s in (signal.SIGTERM, signal.SIGINT):
+        loop.add_signal_handler(s, stop.set)
+    await stop.wait()
+    await srv.stop()
+
+
+def main(argv=None) -> int:
+    ap = argparse.ArgumentParser(prog="workbench")
+    ap.add_argument("--prefix", default=os.environ.get("NB_PREFIX", "/"))
+    ap.add_argument("--host", default="127.0.0.1")
+    ap.add_argument("--matmul", type=int, default=1024, help="first bf16 matmul size (0: no GPU work)")
+    a = ap.parse_args(argv)
+    info = init_gpu(a.matmul)
+    asyncio.run(serve(a.prefix, a.host, info))
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,53 @@
+"""Notebook pods whose container is a real PyTorch-ROCm workbench process
+(``kubelet/process_runtime.py`` + ``notebook_server/workbench.py``): BASELINE configs #2/#3
+without an image registry.  The CPU test runs the process without GPU work; the GPU test
+has it initialise HIP on the allocated MI355X and run its first bf16 matmul before the
+readiness probe answers."""
+
+import aiohttp
+import pytest
+
+from odh_kubeflow_amd.cluster import ClusterConfig, LocalCluster
+from odh_kubeflow_amd.kubelet.process_runtime import ProcessContainerRuntime
+from odh_kubeflow_amd.models import kinds
+from odh_kubeflow_amd.models import meta as m
+from odh_kubeflow_amd.models.notebook import notebook
+
+
+async def _lifecycle(matmul: int, gpus: int = 1):
+    rts = []
+
+    def factory(d):
+        rt = ProcessContainerRuntime(matmul=matmul, visible_device=lambda _d: 0)
+        rts.append(rt)
+        return rt
+
+    cfg = ClusterConfig(odh=True, webhook=True, runtime_factory=factory,
+                        env={"SET_PIPELINE_RBAC": "false", "SET_PIPELINE_SECRET": "false"})
+    async with LocalCluster(cfg) as cl:
+        await cl.ensure_namespace("user")
+        await cl.admin.create(notebook("wb", "user", gpus=gpus))
+        assert await cl.wait_for(lambda: cl.notebook_ready("wb", "user"), 240)
+        pod = cl.store.peek(kinds.POD, "wb-0", "user")
+        ep = m.annotations(pod)["amd.com/notebook-endpoint"]
+        async with aiohttp.ClientSession(timeout=aiohttp.ClientTimeout(total=10)) as s:
+            async with s.get(f"http://{ep}/notebook/user/wb/api") as r:
+                info = await r.json()
+            async with s.get(f"http://{ep}/notebook/user/wb/api/kernels") as r:
+                assert r.status == 200 and await r.json() == []
+        await cl.admin.delete(kinds.NOTEBOOK, "wb", "user")
+        assert await cl.wait_for(lambda: cl.store.peek(kinds.POD, "wb-0", "user") is None, 60)
+        assert await cl.wait_for(lambda: not any(rt.procs for rt in rts), 30)  # process stopped with the pod
+        return info
+
+
+def test_workbench_process_pod_becomes_ready_cpu(run):
+    info = run(_lifecycle(matmul=0), timeout=300)
+    assert info["torch"] and info["gpu"] is None and info["import_torch_ms"] > 0
+
+
+@pytest.mark.gpu
+def test_workbench_process_initialises_the_mi355x(run):
+    info = run(_lifecycle(matmul=1024), timeout=300)
+    assert info["visible_devices"] == "0" and info["first_matmul_ms"] > 0
+    assert "MI3" in info["gpu"] or "gfx95" in info["gpu"], info

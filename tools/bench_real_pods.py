@@ -1,0 +1,142 @@
+"""BASELINE configs #2 and #3 with real notebook processes on the MI355X.
+
+    python tools/bench_real_pods.py [--notebooks 1,8] [--repeats 5] [--reference-emulation]
+
+Config #2: one Notebook requesting ``amd.com/gpu: 1`` with a PyTorch-ROCm workbench;
+config #3: eight at once, one per MI355X of the node.  The controllers, the webhook and
+the (fake) scheduler/kubelet run as in the in-process test cluster; the notebook container
+is a real process (``kubelet/process_runtime.py``): PyTorch imported, HIP initialised on
+the allocated GPU, a first bf16 matmul, the Jupyter API served — Ready when its readiness
+probe answers.  Image pull and container-runtime start are not included (no registry or
+container runtime on the benchmark boxes); everything from ``kubectl apply`` to the
+notebook server answering is.  On a one-GPU box the eight "node GPUs" all map to device 0.
+
+Reported per N: create→Ready p50/p95/max, split into control plane (create → pod object
+exists: admission, odh lock, StatefulSet), pod start (pod exists → Ready: scheduling, the
+node agent's start-up probe, the workbench process) and the workbench's own timings.
+``--reference-emulation`` restores the reference's serialising odh path (one worker, the
+blocking 1 s + 5 s lock removal) for a same-harness comparison.
+"""
+
+from __future__ import annotations
+
+import argparse
+import asyncio
+import json
+import os
+import statistics
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def pct(xs, q):
+    xs = sorted(xs)
+    if not xs:
+        return None
+    k = (len(xs) - 1) * q
+    lo = int(k)
+    hi = min(lo + 1, len(xs) - 1)
+    return round(xs[lo] + (xs[hi] - xs[lo]) * (k - lo), 1)
+
+
+async def run_n(n: int, repeats: int, emu: bool, matmul: int, probe) -> dict:
+    from odh_kubeflow_amd.cluster import ClusterConfig, LocalCluster
+    from odh_kubeflow_amd.kubelet.process_runtime import ProcessContainerRuntime
+    from odh_kubeflow_amd.models import kinds
+    from odh_kubeflow_amd.models.notebook import notebook
+
+    ndev = 1
+    try:
+        import torch
+
+        ndev = max(1, torch.cuda.device_count())
+    except Exception:
+        pass
+    rts = []
+
+    def factory(d):
+        rt = ProcessContainerRuntime(matmul=matmul, visible_device=lambda g: g % ndev)
+        rts.append(rt)
+        return rt
+
+    cfg = ClusterConfig(odh=True, webhook=True, runtime_factory=factory, startup_probe=probe, reference_emulation=emu,
+                        env={"SET_PIPELINE_RBAC": "false", "SET_PIPELINE_SECRET": "false"})
+    total, cp, start = [], [], []
+    reports = []
+    async with LocalCluster(cfg) as cl:
+        await cl.ensure_namespace("bench")
+        for rep in range(repeats + 1):  # the first wave warms the page cache / torch import
+            names = [f"nb-r{rep}-{i}" for i in range(n)]
+            t0, pod_at, ready_at = {}, {}, {}
+            for nm in names:
+                t0[nm] = time.perf_counter()
+                await cl.admin.create(notebook(nm, "bench", gpus=1,
+                                               image="rocm/pytorch:rocm7.0_ubuntu22.04_py3.10_pytorch_release_2.10.0"))
+            deadline = time.monotonic() + 600
+            while len(ready_at) < n and time.monotonic() < deadline:
+                now = time.perf_counter()
+                for nm in names:
+                    if nm not in pod_at and cl.store.peek(kinds.POD, f"{nm}-0", "bench") is not None:
+                        pod_at[nm] = now
+                    if nm not in ready_at and cl.notebook_ready(nm, "bench"):
+                        ready_at[nm] = now
+                await asyncio.sleep(0.002)
+            if len(ready_at) < n:
+                raise RuntimeError(f"not Ready: {sorted(set(names) - set(ready_at))}")
+            if rep > 0:
+                for nm in names:
+                    total.append((ready_at[nm] - t0[nm]) * 1e3)
+                    cp.append((pod_at.get(nm, ready_at[nm]) - t0[nm]) * 1e3)
+                    start.append((ready_at[nm] - pod_at.get(nm, ready_at[nm])) * 1e3)
+                for rt in rts:
+                    for key, r in list(rt.reports.items()):
+                        if any(key.endswith(f"/{nm}-0") for nm in names):
+                            reports.append(r)
+            for nm in names:
+                await cl.admin.delete(kinds.NOTEBOOK, nm, "bench")
+            await cl.wait_for(lambda: all(cl.store.peek(kinds.POD, f"{nm}-0", "bench") is None for nm in names), 120)
+            await cl.wait_for(lambda: not any(rt.procs for rt in rts), 60)
+    wb = {}
+    for k in ("import_torch_ms", "first_matmul_ms", "ready_ms", "spawn_to_ready_ms"):
+        vals = [r[k] for r in reports if r.get(k) is not None]
+        if vals:
+            wb[k + "_p50"] = round(statistics.median(vals), 1)
+    return {"notebooks": n, "repeats": repeats, "reference_emulation": emu,
+            "create_to_ready_ms": {"p50": pct(total, .5), "p95": pct(total, .95), "max": pct(total, 1)},
+            "control_plane_ms_p50": pct(cp, .5), "pod_start_ms_p50": pct(start, .5), "workbench": wb,
+            "gpu": (reports[0].get("gpu") if reports else None)}
+
+
+def main(argv=None) -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--notebooks", default="1,8")
+    ap.add_argument("--repeats", type=int, default=5)
+    ap.add_argument("--matmul", type=int, default=1024)
+    ap.add_argument("--reference-emulation", action="store_true")
+    ap.add_argument("--no-gpu-probe", action="store_true")
+    a = ap.parse_args(argv)
+    probe = None
+    if not a.no_gpu_probe:
+        import torch
+
+        if torch.cuda.device_count():
+            from odh_kubeflow_amd.ops import gpu
+
+            nd = torch.cuda.device_count()
+            for d in range(nd):
+                gpu.get_probe(d).run()
+
+            async def probe(devices):
+                return await gpu.startup_probe(devices, local_index=lambda d: d % nd)
+    out = []
+    for n in [int(x) for x in a.notebooks.split(",")]:
+        r = asyncio.run(run_n(n, a.repeats, a.reference_emulation, a.matmul, probe))
+        print(json.dumps(r), flush=True)
+        out.append(r)
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -10,6 +10,9 @@
 #   ranks    2/4-rank rehearsal of the N>1 launch on the one GPU (never 8: the driver owns N=8)
 #   webhook  BASELINE config #4 (tools/bench_webhook.py)
 #   culling  BASELINE config #5 (tools/bench_culling.py)
+#   realpods BASELINE configs #2/#3: 1 and 8 notebooks whose container is a real PyTorch-ROCm process
+#   realref  the same with the reference's serialising odh path (--reference-emulation)
+#   refemu   bench.py --reference-emulation (control-plane lifecycle, reference behaviour)
 #   prof     rocprofv3 --kernel-trace --stats of bench.py
 #   pmc      rocprofv3 --pmc passes (MFMA busy, LDS bank conflicts, HBM bytes) of the probe kernels
 #   env      tools/gpu_env_probe.sh inventory
@@ -62,6 +65,18 @@ for s in $steps; do
     culling)
       timeout -k 10 170 python tools/bench_culling.py > "$out/culling.log" 2>&1 || fail culling $? "$out/culling.log"
       tail -1 "$out/culling.log" ;;
+    realpods)
+      timeout -k 10 400 python tools/bench_real_pods.py --notebooks 1,8 --repeats 5 > "$out/realpods.log" 2>&1 \
+        || fail realpods $? "$out/realpods.log"
+      grep '^{' "$out/realpods.log" ;;
+    realref)
+      timeout -k 10 400 python tools/bench_real_pods.py --notebooks 1,8 --repeats 1 --reference-emulation \
+        > "$out/realpods_ref.log" 2>&1 || fail realref $? "$out/realpods_ref.log"
+      grep '^{' "$out/realpods_ref.log" ;;
+    refemu)
+      timeout -k 10 200 python bench.py --reference-emulation --steps 3 --warmup 1 --no-inprocess-baseline \
+        > "$out/bench_refemu.log" 2>&1 || fail refemu $? "$out/bench_refemu.log"
+      show "$out/bench_refemu.log" "refemu" ;;
     prof)
       timeout -k 10 200 rocprofv3 --kernel-trace --stats -d "$out/prof" -o run -- \
         python3 bench.py --steps 40 --warmup 3 > "$out/bench_prof.log" 2>&1 || fail prof $? "$out/bench_prof.log"

@@ -41,10 +41,12 @@ def init_gpu(n: int) -> dict:
         a = torch.randn((n, n), device=dev, dtype=torch.bfloat16)
         c = a @ a
         c.float().sum().item()  # synchronises
+        props = torch.cuda.get_device_properties(0)
         out["gpu"] = torch.cuda.get_device_name(0)
+        out["arch"] = getattr(props, "gcnArchName", "").split(":")[0]
         out["visible_devices"] = os.environ.get("HIP_VISIBLE_DEVICES")
         out["first_matmul_ms"] = round((time.perf_counter() - t1) * 1e3, 1)
-        out["hbm_total_gib"] = round(torch.cuda.get_device_properties(0).total_memory / 2 ** 30, 1)
+        out["hbm_total_gib"] = round(props.total_memory / 2 ** 30, 1)
     return out
 
 

@@ -50,4 +50,4 @@ def test_workbench_process_pod_becomes_ready_cpu(run):
 def test_workbench_process_initialises_the_mi355x(run):
     info = run(_lifecycle(matmul=1024), timeout=300)
     assert info["visible_devices"] == "0" and info["first_matmul_ms"] > 0
-    assert "MI3" in info["gpu"] or "gfx95" in info["gpu"], info
+    assert info["arch"] == "gfx950" and info["hbm_total_gib"] > 250, info  # MI355X: gfx950, 288 GB HBM3E

@@ -244,7 +244,7 @@ class InformerCache(Reader, EventSource):
         self.static_namespaces: List[str] = list(nss or [])
         self.namespace_selector = namespace_selector
         # None = every namespace (cluster-wide informers)
-        self.namespaces: Optional[Set[str]] = set(nss) if (nss or namespace_selector) else None
+        self.namespaces: Optional[Set[str]] = set(nss or ()) if (nss or namespace_selector) else None
         self.transforms: Dict[str, Optional[Transform]] = {}
         for k, fn in (transforms or {}).items():
             self.transforms[SCHEME.resolve(k).key] = fn
@@ -271,7 +271,9 @@ class InformerCache(Reader, EventSource):
         ns = m.name(obj)
         if ns in self.static_namespaces:
             return
-        if etype == "DELETED" or m.is_deleting(obj):
+        # a Terminating namespace stays cached: its Notebooks' finalizers still need the
+        # controllers; it leaves when it is gone or stops matching the selector (DELETED)
+        if etype == "DELETED":
             if ns in self.namespaces:
                 self.namespaces.discard(ns)
                 self.namespace_changes += 1

@@ -332,3 +332,30 @@ def test_control_plane_flags(tmp_path):
                              "--master", "http://127.0.0.1:1"])
     with pytest.raises(SystemExit, match="serving certificate missing"):
         control_plane.build(a, {})
+
+
+def test_terminating_namespace_stays_in_the_shard_cache(run):
+    """Notebooks in a Terminating namespace still carry odh finalizers: the shard must keep
+    watching the namespace until it is actually gone."""
+    async def go():
+        store = ObjectStore()
+        srv = await ApiServer(store).start("127.0.0.1", 0)
+        c = RestClient(RestConfig(host=srv.url))
+        try:
+            await c.create({"apiVersion": "v1", "kind": "Namespace",
+                            "metadata": {"name": "a", "labels": {"notebooks.amd.com/shard": "1"}}})
+            await c.create(_cm("x", "a"))
+            cache = InformerCache(c, namespace_selector="notebooks.amd.com/shard=1")
+            await cache.wait_synced([kinds.CONFIG_MAP])
+            assert cache.get(kinds.CONFIG_MAP, "x", "a") is not None
+            # Terminating: deletionTimestamp set, object still there
+            await c.patch(kinds.NAMESPACE, {"metadata": {"finalizers": ["test/hold"]}}, name="a")
+            await c.delete(kinds.NAMESPACE, "a")
+            assert await _wait(lambda: m.is_deleting(store.peek(kinds.NAMESPACE, "a") or {}))
+            await asyncio.sleep(0.1)
+            assert cache.covers(kinds.CONFIG_MAP, "a") and cache.get(kinds.CONFIG_MAP, "x", "a") is not None
+            await cache.stop()
+        finally:
+            await c.close()
+            await srv.stop()
+    run(go())

@@ -215,9 +215,10 @@ class ApiServer:
     """aiohttp application serving an :class:`ObjectStore`."""
 
     def __init__(self, store: ObjectStore, token: Optional[str] = None,
-                 service_resolver: Optional[Callable[[str, str, int], str]] = None):
+                 service_resolver: Optional[Callable[[str, str, int], str]] = None, audit=None):
         self.store = store
         self.token = token
+        self.audit = audit  # apiserver.audit.AuditLogger (DEBUG_WRITE_AUDITLOG)
         self.webhooks = WebhookDispatcher(store, service_resolver)
         self._runner: Optional[web.AppRunner] = None
         self.port = 0
@@ -296,6 +297,40 @@ class ApiServer:
                 raise NotFound(pp.info.plural, f"version {pp.version}")
             if pp.info.namespaced is False and pp.namespace:
                 raise BadRequest(f"{pp.info.plural} is not namespaced")
+        except ApiError as e:
+            return _status_response(e)
+        if self.audit is None:
+            return await self._resource_or_status(req, pp)
+        from .audit import _now, verb_of
+
+        received = _now()
+        watch = req.method == "GET" and req.query.get("watch") in ("1", "true", "True")
+        body = None
+        if req.method in ("POST", "PUT", "PATCH") and req.can_read_body:
+            try:
+                body = json.loads(await req.read() or b"null")
+            except ValueError:
+                body = None
+        verb = verb_of(req.method, pp.name or "", watch)
+        common = dict(verb=verb, uri=str(req.rel_url), user="system:admin",
+                      user_agent=req.headers.get("User-Agent", ""), group=pp.info.group, version=pp.version,
+                      resource=pp.info.plural, namespace=pp.namespace or "", name=pp.name or "",
+                      subresource=pp.sub or "", request_obj=body, received=received)
+        if watch:  # a stream: logged when it starts
+            self.audit.log(code=200, stage="ResponseStarted", **common)
+            return await self._resource_or_status(req, pp)
+        resp = await self._resource_or_status(req, pp)
+        out = None
+        if isinstance(resp, web.Response) and resp.body is not None:
+            try:
+                out = json.loads(resp.body)
+            except (ValueError, TypeError):
+                out = None
+        self.audit.log(code=resp.status, response_obj=out, **common)
+        return resp
+
+    async def _resource_or_status(self, req: web.Request, pp: ParsedPath) -> web.StreamResponse:
+        try:
             return await self._resource(req, pp)
         except ApiError as e:
             return _status_response(e)

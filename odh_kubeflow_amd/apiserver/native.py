@@ -51,8 +51,13 @@ class NativeApiServer:
 
     def __init__(self, uninstalled: Iterable[str] = (), gc: bool = False, token: Optional[str] = None,
                  host: str = "127.0.0.1", port: int = 0, history: int = 4096, binary: Optional[str] = None,
-                 env: Optional[dict] = None):
+                 env: Optional[dict] = None, audit_log_path: Optional[str] = None, audit_policy=None):
         self.cfg = scheme_config(uninstalled, gc, token, history)
+        if audit_log_path:  # kube-apiserver --audit-log-path / --audit-policy-file (apiserver/audit.py)
+            from .audit import DEFAULT_POLICY, AuditPolicy
+
+            pol = audit_policy or AuditPolicy.load(DEFAULT_POLICY)
+            self.cfg["audit"] = {"path": os.path.abspath(audit_log_path), "policy": pol.to_json()}
         self.host = host
         self.port = port
         self.binary = binary or os.environ.get("ODH_APISERVER_BINARY") or BINARY

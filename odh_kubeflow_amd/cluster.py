@@ -51,9 +51,29 @@ class ClusterConfig:
     remote_kubelets: bool = True  # with transport="http": node agents use REST clients too
     # Gateway API implementation stand-in (HTTPRoute ResolvedRefs status); default: with odh
     gateway: Optional[bool] = None
+    # the reference envtest suite's debug aids (odh/controllers/suite_test.go:125-155): an
+    # apiserver audit log (network transports) and a kubeconfig for poking at the test
+    # apiserver with kubectl / the REST client while a test runs
+    audit_log_path: Optional[str] = field(default_factory=lambda: os.environ.get("DEBUG_WRITE_AUDITLOG"))
+    kubeconfig_path: Optional[str] = field(default_factory=lambda: os.environ.get("DEBUG_WRITE_KUBECONFIG"))
 
 
 OPENSHIFT_CRDS = (kinds.IMAGE_STREAM, kinds.PROXY, kinds.ROUTE, kinds.OAUTH_CLIENT)
+
+
+def write_kubeconfig(path: str, server: str, user: str = "MasterOfTheSystems") -> None:
+    """A kubeconfig for the test apiserver (``DEBUG_WRITE_KUBECONFIG``; the reference writes a
+    ``system:masters`` user's kubeconfig for its envtest apiserver).  The test apiservers do
+    not authenticate, so the user carries no credentials."""
+    import yaml
+
+    doc = {"apiVersion": "v1", "kind": "Config", "current-context": "odh-test",
+           "clusters": [{"name": "odh-test", "cluster": {"server": server}}],
+           "users": [{"name": user, "user": {}}],
+           "contexts": [{"name": "odh-test", "context": {"cluster": "odh-test", "user": user}}]}
+    fd = os.open(path, os.O_WRONLY | os.O_CREAT | os.O_TRUNC, 0o600)
+    with os.fdopen(fd, "w") as f:
+        yaml.safe_dump(doc, f, sort_keys=False)
 
 
 class LocalCluster:
@@ -109,7 +129,12 @@ class LocalCluster:
         from .apiserver.http import ApiServer
         from .runtime.rest import RestConfig
 
-        self.apiserver = await ApiServer(self.store).start("127.0.0.1", 0)
+        audit = None
+        if self.cfg.audit_log_path:
+            from .apiserver.audit import DEFAULT_POLICY, AuditLogger, AuditPolicy
+
+            audit = AuditLogger(self.cfg.audit_log_path, AuditPolicy.load(DEFAULT_POLICY))
+        self.apiserver = await ApiServer(self.store, audit=audit).start("127.0.0.1", 0)
         self.rest_config = RestConfig(host=self.apiserver.url)
 
     async def start(self) -> "LocalCluster":
@@ -126,7 +151,8 @@ class LocalCluster:
             from .runtime.informer import InformerCache
             from .runtime.rest import RestClient, RestConfig
 
-            self.native = await NativeApiServer(() if cfg.openshift else OPENSHIFT_CRDS, gc=cfg.gc).start()
+            self.native = await NativeApiServer(() if cfg.openshift else OPENSHIFT_CRDS, gc=cfg.gc,
+                                                audit_log_path=cfg.audit_log_path).start()
             self.rest_config = RestConfig(host=self.native.url)
             admin = RestClient(self.rest_config)
             self._view_cache = InformerCache(admin)
@@ -139,6 +165,8 @@ class LocalCluster:
         else:
             admin = Manager.in_process(self.store, name="admin").client
         self.admin = admin
+        if cfg.kubeconfig_path and self.rest_config is not None:
+            write_kubeconfig(cfg.kubeconfig_path, self.rest_config.host)
         for ns in ("default", cfg.controller_namespace):
             await self.ensure_namespace(ns)
 

@@ -167,6 +167,18 @@ def _probes(port: int = 8081) -> dict:
                                "periodSeconds": 10}}
 
 
+AUDIT_POLICY = """# Audit policy the test apiservers use when DEBUG_WRITE_AUDITLOG=<path> is set (the
+# reference's envtest debug aid).  Very verbose: every request about the `developer`
+# namespace at RequestResponse level.  Analyse with jq, e.g.
+#   jq 'select(.verb != "get" and .verb != "watch" and .verb != "list")' < "$DEBUG_WRITE_AUDITLOG"
+apiVersion: audit.k8s.io/v1
+kind: Policy
+omitStages: []
+rules:
+  - level: RequestResponse
+    namespaces: ["developer"]
+"""
+
 # restricted Pod Security profile for every controller container (the node agent is the one
 # root container: the kubelet pod-resources socket is root-only; tools/lint.py allows it)
 RESTRICTED = {"allowPrivilegeEscalation": False, "capabilities": {"drop": ["ALL"]}, "runAsNonRoot": True,
@@ -516,6 +528,8 @@ def tree() -> Dict[str, object]:
         ["../../crd", "../../user-rbac", "../../node-agent", "../../webhook-certs", "../../control-plane"],
         namespace="opendatahub", namePrefix=NAME_PREFIX, configMapGenerator=mi355x_generators,
         patches=_certs_args_patches(svc_names, mwc_names))
+    # debug aid: the test apiservers' audit policy (DEBUG_WRITE_AUDITLOG, apiserver/audit.py)
+    t["debug/audit-policy.yaml"] = AUDIT_POLICY
     t["samples/notebook_v1_1gpu.yaml"] = sample("rocm-pytorch-1gpu", 1)
     t["samples/notebook_v1_8gpu_auth.yaml"] = sample("rocm-pytorch-8gpu", 8, auth=True)
     t["samples/notebook_v1alpha1.yaml"] = sample("rocm-pytorch-v1alpha1", 1, "v1alpha1")

@@ -2071,7 +2071,137 @@ const char* reason_phrase(int code) {
   }
 }
 
+// ------------------------------------------------------------------ audit log
+//
+// kube-apiserver's --audit-log-path / --audit-policy-file for debugging test runs (the
+// reference's envtest DEBUG_WRITE_AUDITLOG, odh/controllers/suite_test.go:125-137); the
+// policy subset and event shape match apiserver/audit.py.  One JSON line per request at
+// ResponseComplete (watches: ResponseStarted), written under a mutex.
+
+struct Audit {
+  bool on = false;
+  std::string path;
+  Value rules = Value::array();
+  std::set<std::string> omit;
+  std::mutex mu;
+  std::atomic<uint64_t> events{0};
+} g_audit;
+
+struct AuditCtx {
+  bool on = false;
+  std::string level, verb, group, version, resource, ns, name, sub, received;
+  int code = 0;
+  std::string resp;  // response body (RequestResponse only)
+};
+thread_local AuditCtx t_aud;
+
+bool audit_list_has(const Value* v, const std::string& x) {
+  if (!v || !v->is_arr()) return true;  // unset: matches everything
+  for (auto& e : v->arr)
+    if (e.s == x) return true;
+  return false;
+}
+
+std::string audit_level(const std::string& user, const std::string& verb, const std::string& ns,
+                        const std::string& group, const std::string& resource, const std::string& sub) {
+  for (auto& r : g_audit.rules.arr) {
+    if (const Value* u = r.get("users"); u && u->is_arr() && !u->arr.empty() && !audit_list_has(u, user)) continue;
+    if (const Value* v = r.get("verbs"); v && v->is_arr() && !v->arr.empty() && !audit_list_has(v, verb)) continue;
+    if (const Value* n = r.get("namespaces"); n && n->is_arr() && !audit_list_has(n, ns)) continue;
+    if (const Value* rs = r.get("resources"); rs && rs->is_arr() && !rs->arr.empty()) {
+      bool hit = false;
+      std::string full = sub.empty() ? resource : resource + "/" + sub;
+      for (auto& gr : rs->arr) {
+        if (gr.str_or("group") != group) continue;
+        const Value* names = gr.get("resources");
+        if (!names || !names->is_arr() || names->arr.empty() || audit_list_has(names, resource) ||
+            audit_list_has(names, full)) {
+          hit = true;
+          break;
+        }
+      }
+      if (!hit) continue;
+    }
+    std::string lv = r.str_or("level", "None");
+    if (lv == "Metadata" || lv == "Request" || lv == "RequestResponse") return lv;
+    return "None";
+  }
+  return "None";
+}
+
+std::string micro_now() {
+  struct timespec ts;
+  clock_gettime(CLOCK_REALTIME, &ts);
+  struct tm tm;
+  gmtime_r(&ts.tv_sec, &tm);
+  char buf[48];
+  size_t n = strftime(buf, sizeof(buf), "%Y-%m-%dT%H:%M:%S", &tm);
+  snprintf(buf + n, sizeof(buf) - n, ".%06ldZ", ts.tv_nsec / 1000);
+  return buf;
+}
+
+void audit_write(const AuditCtx& a, const std::string& uri, const std::string& ua, const std::string& req_body,
+                 const char* stage) {
+  if (g_audit.omit.count(stage)) return;
+  Value ev = Value::object();
+  ev["kind"] = Value::str("Event");
+  ev["apiVersion"] = Value::str("audit.k8s.io/v1");
+  ev["level"] = Value::str(a.level);
+  ev["auditID"] = Value::str(uuid4());
+  ev["stage"] = Value::str(stage);
+  ev["requestURI"] = Value::str(uri);
+  ev["verb"] = Value::str(a.verb);
+  Value user = Value::object();
+  user["username"] = Value::str("system:admin");
+  Value groups = Value::array();
+  groups.arr.push_back(Value::str("system:masters"));
+  groups.arr.push_back(Value::str("system:authenticated"));
+  user["groups"] = std::move(groups);
+  ev["user"] = std::move(user);
+  Value ips = Value::array();
+  ips.arr.push_back(Value::str("127.0.0.1"));
+  ev["sourceIPs"] = std::move(ips);
+  ev["userAgent"] = Value::str(ua);
+  Value ref = Value::object();
+  ref["resource"] = Value::str(a.resource);
+  if (!a.ns.empty()) ref["namespace"] = Value::str(a.ns);
+  if (!a.name.empty()) ref["name"] = Value::str(a.name);
+  ref["apiGroup"] = Value::str(a.group);
+  ref["apiVersion"] = Value::str(a.version);
+  if (!a.sub.empty()) ref["subresource"] = Value::str(a.sub);
+  ev["objectRef"] = std::move(ref);
+  Value rs = Value::object();
+  rs["metadata"] = Value::object();
+  rs["code"] = Value::integer(a.code);
+  ev["responseStatus"] = std::move(rs);
+  if ((a.level == "Request" || a.level == "RequestResponse") && !req_body.empty()) {
+    try {
+      ev["requestObject"] = kj::parse(req_body);
+    } catch (const kj::ParseError&) {
+    }
+  }
+  if (a.level == "RequestResponse" && !a.resp.empty() && std::string(stage) == "ResponseComplete") {
+    try {
+      ev["responseObject"] = kj::parse(a.resp);
+    } catch (const kj::ParseError&) {
+    }
+  }
+  ev["requestReceivedTimestamp"] = Value::str(a.received);
+  ev["stageTimestamp"] = Value::str(micro_now());
+  std::string line = kj::dump(ev) + "\n";
+  std::lock_guard<std::mutex> g(g_audit.mu);
+  if (FILE* f = fopen(g_audit.path.c_str(), "a")) {
+    fwrite(line.data(), 1, line.size(), f);
+    fclose(f);
+    g_audit.events++;
+  }
+}
+
 bool respond(int fd, int code, const std::string& body, bool keep_alive) {
+  if (t_aud.on) {
+    t_aud.code = code;
+    if (t_aud.level == "RequestResponse") t_aud.resp = body;
+  }
   std::string h = "HTTP/1.1 " + std::to_string(code) + " " + reason_phrase(code) +
                   "\r\nContent-Type: application/json\r\nContent-Length: " + std::to_string(body.size()) +
                   (keep_alive ? "\r\n\r\n" : "\r\nConnection: close\r\n\r\n");
@@ -2080,7 +2210,7 @@ bool respond(int fd, int code, const std::string& body, bool keep_alive) {
 }
 
 struct Request {
-  std::string method, path, query, body, ctype, auth;
+  std::string method, path, query, body, ctype, auth, user_agent, target;
   bool keep_alive = true;
   std::map<std::string, std::string> q;
 };
@@ -2103,6 +2233,7 @@ bool read_request(Conn& c, Request& rq) {
   std::istringstream ls(line);
   std::string target, proto;
   ls >> rq.method >> target >> proto;
+  rq.target = target;
   size_t qm = target.find('?');
   rq.path = url_decode(target.substr(0, qm));
   rq.query = qm == std::string::npos ? "" : target.substr(qm + 1);
@@ -2123,6 +2254,7 @@ bool read_request(Conn& c, Request& rq) {
     if (k == "content-length") clen = std::stoul(v);
     else if (k == "content-type") rq.ctype = v.substr(0, v.find(';'));
     else if (k == "authorization") rq.auth = v;
+    else if (k == "user-agent") rq.user_agent = v;
     else if (k == "transfer-encoding" && v.find("chunked") != std::string::npos) chunked = true;
     else if (k == "connection") {
       std::string lv = v;
@@ -2520,6 +2652,33 @@ bool handle(int fd, Request& rq) {
     if (!p.sub.empty() && p.sub != "status") throw NotFound(r.plural, p.name + "/" + p.sub);
     if (!r.namespaced && !p.ns.empty()) throw BadRequest(r.plural + " is not namespaced");
     auto qget = [&](const char* k) { return rq.q.count(k) ? rq.q.at(k) : std::string(); };
+    if (g_audit.on) {
+      std::string w = qget("watch");
+      bool watch = rq.method == "GET" && p.name.empty() && (w == "1" || w == "true" || w == "True");
+      std::string verb = rq.method == "GET" ? (watch ? "watch" : (p.name.empty() ? "list" : "get"))
+                         : rq.method == "POST" ? "create" : rq.method == "PUT" ? "update"
+                         : rq.method == "PATCH" ? "patch" : rq.method == "DELETE" ? (p.name.empty() ? "deletecollection" : "delete")
+                         : rq.method;
+      std::string lv = audit_level("system:admin", verb, p.ns, r.group, r.plural, p.sub);
+      if (lv != "None") {
+        t_aud.on = true;
+        t_aud.level = lv;
+        t_aud.verb = verb;
+        t_aud.group = r.group;
+        t_aud.version = p.version;
+        t_aud.resource = r.plural;
+        t_aud.ns = p.ns;
+        t_aud.name = p.name;
+        t_aud.sub = p.sub;
+        t_aud.received = micro_now();
+        t_aud.code = 200;
+        t_aud.resp.clear();
+        if (watch) {  // a stream: logged when it starts
+          audit_write(t_aud, rq.target, rq.user_agent, "", "ResponseStarted");
+          t_aud.on = false;
+        }
+      }
+    }
     if (rq.method == "GET" && p.name.empty()) {
       std::string w = qget("watch");
       if (w == "1" || w == "true" || w == "True") {
@@ -2610,7 +2769,13 @@ void serve_conn(int fd) {
     if (!read_request(c, rq)) break;
     t_cat = C_OTHER;
     uint64_t c0 = thread_cpu_ns();
+    t_aud.on = false;
     bool more = handle(fd, rq);
+    if (t_aud.on) {
+      audit_write(t_aud, rq.target, rq.user_agent, rq.body, "ResponseComplete");
+      t_aud.on = false;
+      t_aud.resp.clear();
+    }
     if (t_cat != C_WATCH) {  // a watch books its own CPU as it goes
       P.cpu_ns[t_cat] += thread_cpu_ns() - c0;
       P.calls[t_cat]++;
@@ -2651,6 +2816,15 @@ void load_config(const std::string& path) {
   if (const Value* v = cfg.get("history"))
     if (v->t == T::Int) S.history = (size_t)v->i;
   g_token = cfg.str_or("token");
+  if (const Value* a = cfg.get("audit"); a && a->is_obj()) {
+    g_audit.path = a->str_or("path");
+    if (const Value* pol = a->get("policy"); pol && pol->is_obj()) {
+      if (const Value* rules = pol->get("rules"); rules && rules->is_arr()) g_audit.rules = *rules;
+      if (const Value* om = pol->get("omitStages"); om && om->is_arr())
+        for (auto& x : om->arr) g_audit.omit.insert(x.s);
+    }
+    g_audit.on = !g_audit.path.empty();
+  }
 }
 
 }  // namespace

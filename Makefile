@@ -4,13 +4,17 @@ IMG ?= quay.io/opendatahub/odh-kubeflow-amd:latest
 NOTEBOOK_IMG ?= quay.io/opendatahub/workbench-rocm-pytorch:latest
 GPU_ARCH ?= gfx950
 
-.PHONY: build test test-native test-gpu e2e bench bench-8 manifests deploy deploy-sharded undeploy lint license-check docker-build docker-build-notebook
+.PHONY: build test test-matrix test-native test-gpu e2e bench bench-8 manifests deploy deploy-sharded undeploy lint license-check docker-build docker-build-notebook
 
 build:  ## hipcc --offload-arch=$(GPU_ARCH) kernels, host C++ telemetry/objcore, native apiserver (in-tree)
 	ODH_GPU_ARCH=$(GPU_ARCH) $(PYTHON) -m odh_kubeflow_amd.ops.build
 
 test: build  ## CPU suite against the in-process store (envtest analogue)
 	$(PYTHON) -m pytest tests -q -m "not gpu"
+
+test-matrix: build  ## the odh suites with SET_PIPELINE_RBAC=false and =true (odh/Makefile:106-115)
+	ODH_TEST_SET_PIPELINE_RBAC=false $(PYTHON) -m pytest tests/test_odh_controller.py tests/test_odh_controller_scenarios.py -q
+	ODH_TEST_SET_PIPELINE_RBAC=true $(PYTHON) -m pytest tests/test_odh_controller.py tests/test_odh_controller_scenarios.py -q
 
 test-native: build  ## the same suite over the native C++ apiserver (REST + watch + HTTPS admission)
 	ODH_CLUSTER_TRANSPORT=native $(PYTHON) -m pytest tests -q -m "not gpu"

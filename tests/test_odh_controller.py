@@ -28,7 +28,9 @@ AUTH = {"notebooks.opendatahub.io/inject-auth": "true"}
 
 
 def cfg(**env):
-    base = {"SET_PIPELINE_RBAC": "false", "SET_PIPELINE_SECRET": "false"}
+    # the reference's Makefile runs the whole suite with SET_PIPELINE_RBAC=false and =true
+    # (odh/Makefile:106-115); `make test-matrix` does the same through this variable
+    base = {"SET_PIPELINE_RBAC": os.environ.get("ODH_TEST_SET_PIPELINE_RBAC", "false"), "SET_PIPELINE_SECRET": "false"}
     base.update(env)
     return ClusterConfig(odh=True, webhook=True, gc=False, env=base)
 

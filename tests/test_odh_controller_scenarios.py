@@ -9,6 +9,7 @@ manually modified auth Notebook restored by admission (:1204-1265) and the
 non-auth notebook (:1485-1530).
 """
 
+import os
 import copy
 
 from odh_kubeflow_amd.cluster import ClusterConfig, LocalCluster
@@ -29,7 +30,7 @@ REF_CERT_2 = ("-----BEGIN CERTIFICATE-----\nMIGrMF+gAwIBAgIBATAFBgMrZXAwADAeFw0y
 
 
 def cfg(gc=False, **env):
-    base = {"SET_PIPELINE_RBAC": "false", "SET_PIPELINE_SECRET": "false"}
+    base = {"SET_PIPELINE_RBAC": os.environ.get("ODH_TEST_SET_PIPELINE_RBAC", "false"), "SET_PIPELINE_SECRET": "false"}
     base.update(env)
     return ClusterConfig(odh=True, webhook=True, gc=gc, env=base)
 

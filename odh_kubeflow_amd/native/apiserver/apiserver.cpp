@@ -571,7 +571,7 @@ struct Bucket {
   // watchers by namespace ("" = cluster-wide): a write wakes only the watchers of its kind
   // AND namespace, so with one control-plane shard per GPU rank (each watching its own
   // namespaces) a write costs O(1) wake-ups instead of one per shard
-  std::unordered_multimap<std::string, WatchSlot*> watchers;
+  std::unordered_multimap<std::string, std::shared_ptr<WatchSlot>> watchers;
   // hist / seq / watchers have their own lock: watch streams wait, wake and scan under it
   // without touching the store lock the request threads commit under (lock order: the
   // store lock, then this one — emit() runs inside a commit)
@@ -598,6 +598,7 @@ const char* const CAT_NAMES[C_N] = {"get", "list", "create", "update", "patch", 
 struct Prof {
   std::atomic<uint64_t> cpu_ns[C_N]{}, calls[C_N]{};
   std::atomic<uint64_t> lock_wait_ns{0}, lock_contended{0}, wakeups{0}, scanned{0}, admit_wall_ns{0};
+  std::atomic<uint64_t> lock_hold_ns[C_N]{};
 } P;
 thread_local int t_cat = C_OTHER;
 
@@ -613,7 +614,30 @@ uint64_t mono_ns() {
 }
 
 // the store lock on the request path, timing only the contended acquisitions
+// Watcher wake-ups are decided and delivered after the store lock is released: emit()
+// (which runs inside a commit) only queues the candidate watchers of the event on this
+// thread; ~StoreLock evaluates their filters and notifies them once the lock is free, so
+// the lock covers the commit alone (with one shard per GPU a pod write has a candidate
+// per node-agent watch).  No wake-up is lost: the event is published (seq bumped) under
+// the history lock before the notify, and a waiter re-checks seq under that lock.
+struct PendingWake {
+  std::shared_ptr<WatchSlot> w;
+  Obj obj, old;
+  bool all;
+};
+thread_local std::vector<PendingWake> t_wake;
+
+void flush_wakes() {
+  std::vector<PendingWake> ws;
+  ws.swap(t_wake);
+  for (auto& p : ws) {
+    WatchSlot* w = p.w.get();
+    if (p.all || !w->wants || w->wants(*p.obj) || (p.old && w->wants(*p.old))) w->cv.notify_all();
+  }
+}
+
 struct StoreLock {
+  uint64_t t_acq;
   StoreLock() {
     if (!S.mu.try_lock()) {
       uint64_t t0 = mono_ns();
@@ -621,8 +645,13 @@ struct StoreLock {
       P.lock_wait_ns += mono_ns() - t0;
       P.lock_contended++;
     }
+    t_acq = mono_ns();
   }
-  ~StoreLock() { S.mu.unlock(); }
+  ~StoreLock() {
+    P.lock_hold_ns[t_cat] += mono_ns() - t_acq;  // who keeps the others waiting
+    S.mu.unlock();
+    if (!t_wake.empty()) flush_wakes();
+  }
   StoreLock(const StoreLock&) = delete;
   StoreLock& operator=(const StoreLock&) = delete;
 };
@@ -661,15 +690,12 @@ void emit(const Res& r, const char* type, Obj obj, Obj old) {
   if ((b.seq & 1023) == 0) {
     // periodic broadcast: watchers of quiet namespaces advance past other namespaces'
     // events before those fall off the bounded history (no spurious 410 Gone relists)
-    for (auto& w : b.watchers) w.second->cv.notify_all();
+    for (auto& w : b.watchers) t_wake.push_back({w.second, ev.obj, ev.old, true});
     return;
   }
   auto wake = [&](const std::string& ns) {
     auto rg = b.watchers.equal_range(ns);
-    for (auto it = rg.first; it != rg.second; ++it) {
-      WatchSlot* w = it->second;
-      if (!w->wants || w->wants(*ev.obj) || (ev.old && w->wants(*ev.old))) w->cv.notify_all();
-    }
+    for (auto it = rg.first; it != rg.second; ++it) t_wake.push_back({it->second, ev.obj, ev.old, false});
   };
   const std::string ns = mget(*ev.obj, "namespace");
   wake(ns);
@@ -1176,8 +1202,10 @@ bool defaulted_kind(const Res& r) {
   return r.key == "statefulsets.apps" || r.key == "deployments.apps" || r.key == "pods" || r.key == "services";
 }
 
-void defaults(const Res& r, Value& o) {
-  if (S.defaulting) api_defaults(r, o);
+// `api`: also the kube-apiserver field defaulting (object-local; do_create runs it before
+// taking the store lock and passes false here — the Service IP below reads the store)
+void defaults(const Res& r, Value& o, bool api = true) {
+  if (api && S.defaulting) api_defaults(r, o);
   if (r.key == "services") {
     Value& spec = o["spec"];
     if (!spec.is_obj()) spec = Value::object();
@@ -1703,10 +1731,11 @@ Obj do_create(const Res& r, const std::string& url_ns, Value obj, bool dry) {
     if (r.status && !r.group.empty()) obj.erase("status");
   }
   std::pair<std::string, std::string> k{ns, mget(obj, "name")};
+  if (S.defaulting) api_defaults(r, obj);  // object-local: outside the store lock
   StoreLock g;
   Bucket& b = bucket(r);
   if (b.objs.count(k)) throw AlreadyExists(r.err_res(), k.second);
-  defaults(r, obj);
+  defaults(r, obj, false);
   if (dry) return std::make_shared<const Value>(std::move(obj));
   mdm(obj)["resourceVersion"] = Value::str(std::to_string(++S.rv));
   auto sp = std::make_shared<const Value>(std::move(obj));
@@ -2462,7 +2491,8 @@ void serve_watch(int fd, Res& r, const Path& p, const Request& rq) {
   auto lr = parse_labels(rq.q.count("labelSelector") ? rq.q.at("labelSelector") : "");
   auto fr = parse_fields(rq.q.count("fieldSelector") ? rq.q.at("fieldSelector") : "");
   std::string ns = r.namespaced ? p.ns : "";
-  auto wants = [&](const Value& o) {
+  // by value: the slot (and this filter) may outlive the stream in a writer's queued wake-up
+  auto wants = [ns, lr, fr](const Value& o) {
     if (!ns.empty() && mget(o, "namespace") != ns) return false;
     if (!lr.empty() && !match_labels(lr, o)) return false;
     if (!fr.empty() && !match_fields(fr, o)) return false;
@@ -2472,7 +2502,9 @@ void serve_watch(int fd, Res& r, const Path& p, const Request& rq) {
   if (!write_all(fd, head.data(), head.size())) return;
   int64_t last_seq;
   std::vector<std::string> pending;
-  WatchSlot slot;
+  // shared: a writer thread may still hold it (queued wake-up) after this stream ends
+  auto slot_ptr = std::make_shared<WatchSlot>();
+  WatchSlot& slot = *slot_ptr;
   Bucket* wb = nullptr;
   struct Unregister {  // every exit path drops the slot from the bucket's watcher index
     Bucket*& b;
@@ -2483,7 +2515,7 @@ void serve_watch(int fd, Res& r, const Path& p, const Request& rq) {
       std::lock_guard<std::mutex> hg(b->hmu);
       auto rg = b->watchers.equal_range(ns);
       for (auto it = rg.first; it != rg.second; ++it)
-        if (it->second == s) {
+        if (it->second.get() == s) {
           b->watchers.erase(it);
           break;
         }
@@ -2495,7 +2527,7 @@ void serve_watch(int fd, Res& r, const Path& p, const Request& rq) {
     Bucket& b = bucket(r);
     std::lock_guard<std::mutex> hg(b.hmu);
     wb = &b;
-    b.watchers.emplace(ns, &slot);
+    b.watchers.emplace(ns, slot_ptr);
     last_seq = b.seq;
     if (rv.empty() || rv == "0") {
       for (auto& kv : b.objs)
@@ -2625,8 +2657,9 @@ bool handle(int fd, Request& rq) {
              (unsigned long long)S.webhook_calls.load(), (long long)rv);
     std::string out = buf;
     for (int c = 0; c < C_N; ++c) {
-      snprintf(buf, sizeof(buf), "\"%s_cpu_ns\":%llu,\"%s_calls\":%llu,", CAT_NAMES[c],
-               (unsigned long long)P.cpu_ns[c].load(), CAT_NAMES[c], (unsigned long long)P.calls[c].load());
+      snprintf(buf, sizeof(buf), "\"%s_cpu_ns\":%llu,\"%s_calls\":%llu,\"%s_lock_hold_ns\":%llu,", CAT_NAMES[c],
+               (unsigned long long)P.cpu_ns[c].load(), CAT_NAMES[c], (unsigned long long)P.calls[c].load(),
+               CAT_NAMES[c], (unsigned long long)P.lock_hold_ns[c].load());
       out += buf;
     }
     snprintf(buf, sizeof(buf),

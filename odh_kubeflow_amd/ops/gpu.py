@@ -1,9 +1,14 @@
 """Python side of the MI355X node-agent kernels (``csrc/gpu_probe.hip``).
 
 * :func:`gemm_bf16` — the MFMA bf16 GEMM (``C = A · Btᵀ``, fp32 out) on torch tensors.
-* :class:`GpuProbe` — the notebook start-up probe: a resident 4096³ bf16 GEMM whose
+* :class:`GpuProbe` — the notebook start-up probe: a resident bf16 GEMM whose
   integer-valued operands make every output element checkable bit-exactly on the GPU,
-  plus an HBM3E pattern write/verify sweep.  One probe is a handful of kernels on the
+  plus an HBM3E pattern write/verify sweep.  Sized as a health check on the create →
+  Ready path (:data:`PROBE_SHAPE`, :data:`PROBE_HBM_BYTES`): 4096×4096 outputs are 256
+  tiles of 256², one workgroup per CU of the 256-CU chip, so every CU of every XCD runs
+  MFMA work; K=1024 keeps the GEMM at ≈30 µs, and the 256 MiB sweep, interleaved over every
+  HBM3E stack and channel, tests them all (round 1 ran K=4096 and 1 GiB: ≈0.5 ms of GPU
+  time per pod start for the same coverage).  One probe is a handful of kernels on the
   device's current stream followed by one 32-word device→host copy.  Reports matrix-core
   TFLOP/s, HBM GB/s, mismatches (attributed to the XCD that computed them) and how many
   of the 8 XCDs ran workgroups.
@@ -31,6 +36,8 @@ PROBE_LIB = "libodh_gpu_probe.so"
 BM = BN = 128
 BK = 32
 N_XCD = 8
+PROBE_SHAPE = (4096, 4096, 1024)  # M, N, K of the start-up probe GEMM (256 tiles of 256²)
+PROBE_HBM_BYTES = 256 << 20
 
 
 class NativeLibraryMissing(RuntimeError):
@@ -160,7 +167,8 @@ def gemm_bf16(a, bt, out=None, tile_xcd=None, xcd_blocks=None, tile: Optional[in
 class GpuProbe:
     """Resident start-up probe for one GPU (allocate + fill once, then ~1 ms per run)."""
 
-    def __init__(self, device: int = 0, m: int = 4096, n: int = 4096, k: int = 4096, hbm_bytes: int = 1 << 30,
+    def __init__(self, device: int = 0, m: int = PROBE_SHAPE[0], n: int = PROBE_SHAPE[1], k: int = PROBE_SHAPE[2],
+                 hbm_bytes: int = PROBE_HBM_BYTES,
                  hbm_nontemporal: bool = False, overlap: bool = True):
         import torch
 

@@ -68,7 +68,7 @@ def main():
         torch.cuda.empty_cache()
     import ctypes
 
-    p = gpu.GpuProbe(0)
+    p = gpu.GpuProbe(0, 4096, 4096, 4096, hbm_bytes=1 << 30)  # the round-1 probe size: kernel A/B numbers
     s = torch.cuda.current_stream().cuda_stream
     cnt = p.counters.data_ptr()
     ms = timeit(lambda: lib.odh_probe_gemm_verify(p.a.data_ptr(), p.bt.data_ptr(), p.m, p.n, p.k,
@@ -130,9 +130,10 @@ def main():
 
 def pmc_pass():
     """A short, fixed workload for ``rocprofv3 --pmc`` passes: the node agent's start-up
-    probe as it runs on the notebook path (fused-verify 4096³ bf16 MFMA GEMM + 1 GiB HBM
-    pattern write/check) ×10, and the standalone 256² GEMM at 8192³ ×3."""
-    p = gpu.GpuProbe(0)
+    probe as it runs on the notebook path (fused-verify bf16 MFMA GEMM of
+    ``gpu.PROBE_SHAPE`` + HBM pattern write/check of ``gpu.PROBE_HBM_BYTES``) ×10, and the
+    standalone 256² GEMM at 8192³ ×3."""
+    p = gpu.GpuProbe(0)  # the start-up probe as it runs on the notebook path
     for _ in range(10):
         assert p.run()["ok"]
     dev = torch.device("cuda", 0)

@@ -349,3 +349,102 @@ def test_kf_manager_leader_failover(tmp_path, run):
             except subprocess.TimeoutExpired:
                 p.kill()
         logf.close()
+
+
+def test_sharded_control_plane_processes(tmp_path, run):
+    """The mi355x-sharded deployment as processes: two ``cmd/control_plane.py`` shards
+    (shard 0 assigns unlabelled namespaces), one MutatingWebhookConfiguration per shard plus
+    the unassigned-namespace one, the dev apiserver and kubelet stand-in.  Notebooks in
+    namespaces the assigner put on different shards both become Ready, each shard labels its
+    own HTTPRoutes; with shard 1 down its namespace's admissions fail (failurePolicy Fail)
+    while shard 0's keep working, and a restarted shard 1 picks its namespace up again."""
+    from odh_kubeflow_amd.controllers.sharding import shard_for
+    from odh_kubeflow_amd.models.errors import ApiError
+    from odh_kubeflow_amd.webhook.certs import generate
+    from odh_kubeflow_amd.webhook.server import mutating_webhook_configuration
+
+    # two namespaces the assigner maps to different shards
+    names = [f"team-{i}" for i in range(64)]
+    ns0 = next(n for n in names if shard_for(n, 2) == "0")
+    ns1 = next(n for n in names if shard_for(n, 2) == "1")
+    api_port = free_port()
+    wh = [free_port(), free_port()]
+    certs = generate(("127.0.0.1", "localhost"), str(tmp_path / "certs"))
+    logf = open(tmp_path / "procs.log", "wb")
+    master = f"http://127.0.0.1:{api_port}"
+    procs = [spawn(["odh_kubeflow_amd.cmd.apiserver", "--port", str(api_port), "--controllers",
+                    "--no-openshift-apis"], log=logf)]
+    common = {"K8S_NAMESPACE": "opendatahub", "SET_PIPELINE_RBAC": "false", "SET_PIPELINE_SECRET": "false"}
+
+    def shard(k):
+        return spawn(["odh_kubeflow_amd.cmd.control_plane", "--master", master, "--shard", str(k), "--shard-count", "2",
+                      "--assign-namespaces", "--metrics-bind-address", "0", "--health-probe-bind-address", "0",
+                      "--kube-rbac-proxy-image", "quay.io/brancz/kube-rbac-proxy:v0.18.1",
+                      "--webhook-cert-dir", certs.cert_dir, "--webhook-host", "127.0.0.1",
+                      "--webhook-port", str(wh[k])], common, logf)
+
+    try:
+        async def go():
+            await wait_http(master + "/healthz")
+            c = RestClient(RestConfig(host=master))
+            await c.create({"apiVersion": "v1", "kind": "Namespace", "metadata": {"name": "opendatahub"}})
+            for k in (0, 1):
+                sel = {"matchLabels": {"notebooks.amd.com/shard": str(k)}}
+                await c.create(mutating_webhook_configuration(
+                    certs.ca_bundle_b64, url=f"https://127.0.0.1:{wh[k]}/mutate-notebook-v1",
+                    name=f"notebook-webhook-shard-{k}", namespace_selector=sel))
+            await c.create(mutating_webhook_configuration(
+                certs.ca_bundle_b64, url=f"https://127.0.0.1:{wh[0]}/mutate-notebook-v1",
+                name="notebook-webhook-unassigned", namespace_selector={"matchExpressions": [
+                    {"key": "notebooks.amd.com/shard", "operator": "DoesNotExist"}]}))
+            procs.append(shard(0))
+            procs.append(shard(1))
+            procs.append(spawn(["odh_kubeflow_amd.cmd.fake_kubelet", "--master", master, "--devices",
+                                "0,1,2,3,4,5,6,7"], common, logf))
+            for k in (0, 1):
+                await wait_http(f"https://127.0.0.1:{wh[k]}/healthz")
+            for ns in (ns0, ns1):
+                await c.create({"apiVersion": "v1", "kind": "Namespace", "metadata": {"name": ns}})
+
+            async def labelled():
+                got = [m.labels(await c.get(kinds.NAMESPACE, ns)).get("notebooks.amd.com/shard") for ns in (ns0, ns1)]
+                return got == ["0", "1"]
+            await eventually(labelled, 30)  # shard 0's assigner
+
+            async def ready(ns, nm="nb"):
+                st = (await c.get(kinds.NOTEBOOK, nm, ns)).get("status") or {}
+                return st.get("readyReplicas") == 1 and any(
+                    x.get("type") == "Ready" and x.get("status") == "True" for x in st.get("conditions") or [])
+
+            for ns in (ns0, ns1):
+                await c.create(notebook("nb", ns, gpus=1))
+            for ns in (ns0, ns1):
+                await eventually(lambda: ready(ns), 60)
+            routes = {m.labels(r)["notebook-namespace"]: m.labels(r).get("notebooks.amd.com/shard")
+                      for r in await c.list(kinds.HTTP_ROUTE, "opendatahub")}
+            assert routes == {ns0: "0", ns1: "1"}
+
+            # shard 1 down: its namespace is not admitted, shard 0's is
+            procs[2].terminate()
+            procs[2].wait(10)
+            with pytest.raises(ApiError):
+                await c.create(notebook("nb2", ns1))
+            await c.create(notebook("nb2", ns0))
+            await eventually(lambda: ready(ns0, "nb2"), 60)
+            # back up: shard 1 serves its namespace again
+            procs[2] = shard(1)
+            await wait_http(f"https://127.0.0.1:{wh[1]}/healthz")
+            await c.create(notebook("nb2", ns1))
+            await eventually(lambda: ready(ns1, "nb2"), 60)
+            await c.close()
+
+        run(go(), timeout=240)
+    finally:
+        for p in procs:
+            p.terminate()
+        for p in procs:
+            try:
+                p.wait(10)
+            except subprocess.TimeoutExpired:
+                p.kill()
+        logf.close()

@@ -468,6 +468,7 @@ class GpuRuntime:
         for h in list(self.handles.values()):
             await self.runtime.stop(h)
         self.handles.clear()
+        await self.runtime.close()  # containers whose start was interrupted
         await self.runtime.close()
 
     def setup_with_manager(self, mgr, max_concurrent: int = 8, name: Optional[str] = None):

@@ -95,15 +95,21 @@ class ProcessContainerRuntime(ContainerRuntime):
         return ContainerHandle(key, devices, ip=self.host, port=port, info={"pid": proc.pid, "workbench": report})
 
     async def stop(self, handle: ContainerHandle) -> None:
-        proc = self.procs.pop(handle.pod_key, None)
-        if proc is None or proc.returncode is not None:
+        proc = self.procs.get(handle.pod_key)
+        if proc is None:
             return
-        proc.terminate()
         try:
-            await asyncio.wait_for(proc.communicate(), 10)  # drains stdout: the pipe transport closes
-        except asyncio.TimeoutError:
-            proc.kill()
-            await proc.communicate()
+            if proc.returncode is None:
+                proc.terminate()
+            try:
+                await asyncio.wait_for(proc.communicate(), 10)  # drains stdout: the pipe transport closes
+            except asyncio.TimeoutError:
+                proc.kill()
+                await proc.communicate()
+        finally:
+            # listed until it has exited and its pipes are closed
+            if self.procs.get(handle.pod_key) is proc:
+                self.procs.pop(handle.pod_key, None)
 
     async def close(self) -> None:
         for key in list(self.procs):

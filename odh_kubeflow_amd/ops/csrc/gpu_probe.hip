@@ -339,6 +339,16 @@ bool gemm256_ok(int M, int N, int K) { return M % G_BM == 0 && N % G_BN == 0 && 
 // s ^ ((r >> 2) & 3) (conflict-free 16-lane ds_read_b128 groups), applied on the SOURCE
 // address because the DMA image is lane-linear.
 
+// In-kernel span timestamps for graph replays (events cannot split one graph launch):
+// ts[0] holds ~(earliest start) so a zeroed slot works with atomicMax, ts[1] the latest
+// end; both in wall_clock64() ticks (hipDeviceAttributeWallClockRate kHz).  Same-address
+// atomics serialise in one L2 channel (measured: one per wave of the 16384-workgroup HBM
+// sweep cost 0.16 ms), so the sweep stamps only from its first / last TS_EDGE workgroups
+// (dispatched in order, ~16 KiB each: the span is exact to a few µs).
+constexpr int TS_EDGE = 64;
+__device__ __forceinline__ void ts_begin(unsigned long long* ts) { atomicMax(&ts[0], ~wall_clock64()); }
+__device__ __forceinline__ void ts_end(unsigned long long* ts) { atomicMax(&ts[1], (unsigned long long)wall_clock64()); }
+
 constexpr int D_BK = 32;
 constexpr int D_CH = D_BK / 8;            // 16-byte chunks per row
 constexpr int D_NBUF = 4;
@@ -351,7 +361,7 @@ template <bool VERIFY, bool XB = false, int GM = 1>
 __global__ __launch_bounds__(G_THREADS, 1) void gemm256d_kernel(
     const uint4* __restrict__ A, const uint4* __restrict__ Bt, float* __restrict__ C, int M, int N, int K,
     int* __restrict__ tile_xcd, int* __restrict__ xcd_blocks, unsigned* __restrict__ err_total,
-    unsigned* __restrict__ err_xcd) {
+    unsigned* __restrict__ err_xcd, unsigned long long* __restrict__ ts = nullptr) {
   __shared__ uint4 lds[D_RING + 9];  // ring, then 35 floats of the probe's expected values
   float* expect = reinterpret_cast<float*>(lds + D_RING);
 
@@ -376,6 +386,7 @@ __global__ __launch_bounds__(G_THREADS, 1) void gemm256d_kernel(
   }
   const unsigned xcc = xcc_id();
   if (tid == 0) {
+    if (ts) ts_begin(ts);
     if (tile_xcd) tile_xcd[bid] = (int)xcc;
     if (xcd_blocks) atomicAdd(&xcd_blocks[xcc], 1);
   }
@@ -542,6 +553,7 @@ __global__ __launch_bounds__(G_THREADS, 1) void gemm256d_kernel(
       if (err_xcd) atomicAdd(&err_xcd[xcc], bad);
     }
   }
+  if (ts && lane == 0) ts_end(ts);
 }
 
 __device__ __forceinline__ uint16_t small_int_bf16(int v) {
@@ -607,7 +619,11 @@ __device__ __forceinline__ uint32_t mix32(uint32_t x) {
 // stores; sequential DRAM pages per CU), 4 × 16 B per lane per iteration so every wave
 // keeps 4 KiB of stores in flight.
 template <bool NT>
-__global__ __launch_bounds__(256) void hbm_write_kernel(u32x4* __restrict__ buf, size_t n, uint32_t seed) {
+__global__ __launch_bounds__(256) void hbm_write_kernel(u32x4* __restrict__ buf, size_t n, uint32_t seed,
+                                                        const uint32_t* __restrict__ seedp = nullptr,
+                                                        unsigned long long* __restrict__ ts = nullptr) {
+  if (seedp) seed = *seedp;  // graph replays: the seed lives on the device
+  if (ts && threadIdx.x == 0 && blockIdx.x < TS_EDGE) ts_begin(ts);
   const size_t per = ((n + gridDim.x - 1) / gridDim.x + 1023) & ~(size_t)1023;
   const size_t lo = blockIdx.x * per;
   const size_t hi = lo + per < n ? lo + per : n;
@@ -676,7 +692,10 @@ __global__ __launch_bounds__(256) void hbm_write_variant_kernel(u32x4* __restric
 }
 
 __global__ __launch_bounds__(256) void hbm_check_kernel(const u32x4* __restrict__ buf, size_t n, uint32_t seed,
-                                                        unsigned long long* __restrict__ err) {
+                                                        unsigned long long* __restrict__ err,
+                                                        const uint32_t* __restrict__ seedp = nullptr,
+                                                        unsigned long long* __restrict__ ts = nullptr) {
+  if (seedp) seed = *seedp;
   const size_t per = ((n + gridDim.x - 1) / gridDim.x + 1023) & ~(size_t)1023;
   const size_t lo = blockIdx.x * per;
   const size_t hi = lo + per < n ? lo + per : n;
@@ -701,6 +720,7 @@ __global__ __launch_bounds__(256) void hbm_check_kernel(const u32x4* __restrict_
   // wave reduction (64 lanes), one atomic per wave
   for (int off = 32; off > 0; off >>= 1) local += __shfl_down(local, off, 64);
   if ((threadIdx.x & 63) == 0 && local) atomicAdd(err, (unsigned long long)local);
+  if (ts && (threadIdx.x & 63) == 0 && blockIdx.x + TS_EDGE >= gridDim.x) ts_end(ts);
 }
 
 // read-path variants for A/B measurement (odh_hbm_check_variant): NT = nontemporal loads,
@@ -886,6 +906,114 @@ int odh_hbm_write(void* buf, size_t bytes, uint32_t seed, int nontemporal, hipSt
   else
     hbm_write_kernel<false><<<grid_for(n, 1024), 256, 0, stream>>>((u32x4*)buf, n, seed);
   return (int)hipGetLastError();
+}
+
+// ------------------------------------------------------------------ the probe as one hipGraph
+//
+// The start-up probe is launch-bound on the host side: a counter reset, the GEMM on one
+// stream, the HBM write + check on a second, a fork/join and a 128-byte read-back — five
+// launches and three stream operations per pod start.  odh_probe_graph_create captures
+// them once (stream capture with an event fork/join, so the sweep and the GEMM still run
+// concurrently) and odh_probe_graph_launch replays the whole probe with one launch.  A
+// graph freezes kernel arguments, so the per-run HBM pattern seed lives on the device: the
+// first node advances it (LCG) and the sweep kernels read it.
+
+// first node: advance the seed and reset the 32 counters (one wave; no memset node)
+__global__ void probe_seed_advance_kernel(uint32_t* seed, int* counters) {
+  if (threadIdx.x < 32) counters[threadIdx.x] = 0;
+  if (threadIdx.x == 0) *seed = *seed * 1664525u + 1013904223u;
+}
+
+struct ProbeGraph {
+  hipGraph_t graph = nullptr;
+  hipGraphExec_t exec = nullptr;
+  hipStream_t s0 = nullptr, s1 = nullptr;
+  hipEvent_t fork = nullptr, join = nullptr;
+};
+
+static void probe_graph_free(ProbeGraph* g) {
+  if (!g) return;
+  // teardown: errors here have nothing left to undo
+  if (g->exec) (void)hipGraphExecDestroy(g->exec);
+  if (g->graph) (void)hipGraphDestroy(g->graph);
+  if (g->fork) (void)hipEventDestroy(g->fork);
+  if (g->join) (void)hipEventDestroy(g->join);
+  if (g->s0) (void)hipStreamDestroy(g->s0);
+  if (g->s1) (void)hipStreamDestroy(g->s1);
+  delete g;
+}
+
+// counters: 32 × i32 on the device ([0:8] xcd_blocks, [8:16] err_xcd, [16] gemm errors, [18:20]
+// hbm errors as u64, [20:24] GEMM span, [24:28] sweep span as ts_begin/ts_end u64 pairs);
+// host: 32 × i32 pinned; seed: one u32 on the device
+int odh_probe_graph_create(const void* A, const void* Bt, int M, int N, int K, int* tile_xcd, int* counters,
+                           void* hbm, size_t hbm_bytes, uint32_t* seed, int* host, int serial, void** out) {
+  if (!out || !odh_gemm_shape_ok(M, N, K) || !gemm256_ok(M, N, K) || hbm_bytes < 16) return (int)hipErrorInvalidValue;
+  *out = nullptr;
+  ProbeGraph* g = new ProbeGraph();
+  hipError_t e = hipStreamCreateWithFlags(&g->s0, hipStreamNonBlocking);
+  if (e == hipSuccess) e = hipStreamCreateWithFlags(&g->s1, hipStreamNonBlocking);
+  if (e == hipSuccess) e = hipEventCreateWithFlags(&g->fork, hipEventDisableTiming);
+  if (e == hipSuccess) e = hipEventCreateWithFlags(&g->join, hipEventDisableTiming);
+  if (e == hipSuccess) e = hipStreamBeginCapture(g->s0, hipStreamCaptureModeThreadLocal);
+  if (e != hipSuccess) {
+    probe_graph_free(g);
+    return (int)e;
+  }
+  const size_t n = hbm_bytes / 16;
+  unsigned* c = (unsigned*)counters;
+  hipError_t cap = hipSuccess;  // first error while capturing (the capture is still ended)
+  auto chk = [&](hipError_t r) {
+    if (cap == hipSuccess && r != hipSuccess) cap = r;
+  };
+  // serial: one chain of kernels on s0 (graph branches may not run concurrently on every
+  // runtime; measured both ways by tools/probe_microbench.py --startup)
+  hipStream_t sw = serial ? g->s0 : g->s1;
+  probe_seed_advance_kernel<<<1, 64, 0, g->s0>>>(seed, counters);
+  chk(hipGetLastError());
+  if (!serial) {
+    chk(hipEventRecord(g->fork, g->s0));
+    chk(hipStreamWaitEvent(g->s1, g->fork, 0));
+  }
+  // the memory-bound sweep on the second stream, issued first; the GEMM's one workgroup
+  // per CU co-resides with its waves
+  unsigned long long* ts = (unsigned long long*)(counters + 20);
+  hbm_write_kernel<false><<<grid_for(n, 1024), 256, 0, sw>>>((u32x4*)hbm, n, 0u, seed, ts + 2);
+  chk(hipGetLastError());
+  hbm_check_kernel<<<grid_for(n, 1024), 256, 0, sw>>>((const u32x4*)hbm, n, 0u,
+                                                           (unsigned long long*)(counters + 18), seed, ts + 2);
+  chk(hipGetLastError());
+  gemm256d_kernel<true><<<(M / G_BM) * (N / G_BN), G_THREADS, 0, g->s0>>>(
+      (const uint4*)A, (const uint4*)Bt, nullptr, M, N, K, tile_xcd, counters, c + 16, c + 8, ts);
+  chk(hipGetLastError());
+  if (!serial) {
+    chk(hipEventRecord(g->join, g->s1));
+    chk(hipStreamWaitEvent(g->s0, g->join, 0));
+  }
+  chk(hipMemcpyAsync(host, counters, 32 * sizeof(int), hipMemcpyDeviceToHost, g->s0));
+  e = hipStreamEndCapture(g->s0, &g->graph);
+  if (e == hipSuccess && cap != hipSuccess) e = cap;
+  if (e == hipSuccess) e = hipGraphInstantiate(&g->exec, g->graph, nullptr, nullptr, 0);
+  if (e != hipSuccess) {
+    probe_graph_free(g);
+    return (int)e;
+  }
+  *out = g;
+  return 0;
+}
+
+int odh_probe_graph_launch(void* handle, hipStream_t stream) {
+  if (!handle) return (int)hipErrorInvalidValue;
+  return (int)hipGraphLaunch(((ProbeGraph*)handle)->exec, stream);
+}
+
+void odh_probe_graph_destroy(void* handle) { probe_graph_free((ProbeGraph*)handle); }
+
+// wall_clock64() tick rate of a device in kHz (0 on error)
+int odh_wall_clock_khz(int device) {
+  int khz = 0;
+  if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, device) != hipSuccess) return 0;
+  return khz;
 }
 
 int odh_hbm_write_variant(void* buf, size_t bytes, uint32_t seed, int variant, int blocks, hipStream_t stream) {

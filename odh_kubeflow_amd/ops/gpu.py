@@ -8,8 +8,10 @@
   tiles of 256², one workgroup per CU of the 256-CU chip, so every CU of every XCD runs
   MFMA work; K=1024 keeps the GEMM at ≈30 µs, and the 256 MiB sweep, interleaved over every
   HBM3E stack and channel, tests them all (round 1 ran K=4096 and 1 GiB: ≈0.5 ms of GPU
-  time per pod start for the same coverage).  One probe is a handful of kernels on the
-  device's current stream followed by one 32-word device→host copy.  Reports matrix-core
+  time per pod start for the same coverage).  The probe is captured once into a hipGraph
+  (sweep and GEMM on two forked streams, counter reset, 128-byte read-back) and replayed
+  with ONE launch per pod start; the kernels time themselves (``wall_clock64`` spans), since
+  events cannot split a graph launch.  Reports matrix-core
   TFLOP/s, HBM GB/s, mismatches (attributed to the XCD that computed them) and how many
   of the 8 XCDs ran workgroups.
 * :func:`startup_probe` — the async hook the node agent (``kubelet/node.py``
@@ -93,10 +95,16 @@ def load_library(build_if_missing: bool = False):
         lib.odh_probe_gemm_verify_deep.argtypes = [vp, vp, i, i, i, vp, vp, vp, vp, i, vp]
         lib.odh_hbm_write_variant.argtypes = [vp, sz, u32, i, i, vp]
         lib.odh_hbm_check_variant.argtypes = [vp, sz, u32, vp, i, i, vp]
+        lib.odh_probe_graph_create.argtypes = [vp, vp, i, i, i, vp, vp, vp, sz, vp, vp, i, ctypes.POINTER(vp)]
+        lib.odh_probe_graph_launch.argtypes = [vp, vp]
+        lib.odh_probe_graph_destroy.argtypes = [vp]
+        lib.odh_probe_graph_destroy.restype = None
+        lib.odh_wall_clock_khz.argtypes = [i]
+        lib.odh_wall_clock_khz.restype = i
         for f in ("odh_probe_fill", "odh_gemm_bf16", "odh_gemm_bf16_128", "odh_probe_verify", "odh_probe_gemm_verify",
                   "odh_hbm_write", "odh_hbm_check", "odh_busy", "odh_gemm_bf16_256_variant",
                   "odh_probe_gemm_verify_2buf", "odh_probe_gemm_verify_deep", "odh_hbm_write_variant",
-                  "odh_hbm_check_variant", "odh_peer_enable"):
+                  "odh_hbm_check_variant", "odh_peer_enable", "odh_probe_graph_create", "odh_probe_graph_launch"):
             getattr(lib, f).restype = i
         _lib = lib
         return lib
@@ -169,7 +177,7 @@ class GpuProbe:
 
     def __init__(self, device: int = 0, m: int = PROBE_SHAPE[0], n: int = PROBE_SHAPE[1], k: int = PROBE_SHAPE[2],
                  hbm_bytes: int = PROBE_HBM_BYTES,
-                 hbm_nontemporal: bool = False, overlap: bool = True):
+                 hbm_nontemporal: bool = False, overlap: bool = True, graph=True):
         import torch
 
         if not gemm_shape_ok(m, n, k):
@@ -198,6 +206,10 @@ class GpuProbe:
             torch.cuda.current_stream(self.device).synchronize()
         self.hbm_nontemporal = hbm_nontemporal
         self.overlap = overlap
+        # graph replay: fused + overlapped probes (the start-up probe) — one launch per run
+        self.graph = graph
+        self._graph = None
+        self._graph_error: Optional[str] = None
         self.runs = 0
         self.seed = 0x9E3779B9
         # one probe in flight per GPU: runs share the counters, events and pinned host buffer
@@ -208,9 +220,65 @@ class GpuProbe:
         """One probe.  With ``overlap`` (default) the memory-bound HBM sweep and the
         MFMA-bound GEMM run concurrently on two streams of the probe: their waves co-reside
         on the CUs (the GEMM's 1 workgroup/CU leaves VGPRs and wave slots free), so the
-        GEMM hides under the sweep instead of adding to it."""
+        GEMM hides under the sweep instead of adding to it.  With ``graph`` (default) that
+        whole sequence is one hipGraph launch."""
         with self._lock:
+            if self.graph and self.fused and self.overlap:
+                g = self._graph_handle()
+                if g is not None:
+                    return self._run_graph(g)
             return self._run()
+
+    def _graph_handle(self):
+        """Capture the probe graph once (``None`` if capture failed: the eager launches run
+        instead and the error is kept in ``graph_error`` of every result)."""
+        if self._graph is not None or self._graph_error is not None:
+            return self._graph
+        import torch
+
+        lib = load_library()
+        with torch.cuda.device(self.device):
+            self.seed_dev = torch.full((1,), 0x1E3779B9, dtype=torch.int32, device=self.device)
+            torch.cuda.current_stream(self.device).synchronize()
+            h = ctypes.c_void_p()
+            rc = lib.odh_probe_graph_create(self.a.data_ptr(), self.bt.data_ptr(), self.m, self.n, self.k,
+                                            self.tile_xcd.data_ptr(), self.counters.data_ptr(), self.hbm.data_ptr(),
+                                            self.hbm_bytes, self.seed_dev.data_ptr(), self.host.data_ptr(),
+                                            int(self.graph == "serial"), ctypes.byref(h))
+        if rc != 0:
+            msg = lib.odh_error_string(rc)
+            self._graph_error = f"HIP error {rc}: {msg.decode() if msg else '?'}"
+            return None
+        self._graph = h
+        self._tick_khz = lib.odh_wall_clock_khz(self.device.index) or 100000
+        return h
+
+    def close(self) -> None:
+        with self._lock:
+            if self._graph is not None:
+                load_library().odh_probe_graph_destroy(self._graph)
+                self._graph = None
+
+    def _span_ms(self, h: List[int], i: int) -> float:
+        begin = ~((h[i] & 0xFFFFFFFF) | ((h[i + 1] & 0xFFFFFFFF) << 32)) & 0xFFFFFFFFFFFFFFFF
+        end = (h[i + 2] & 0xFFFFFFFF) | ((h[i + 3] & 0xFFFFFFFF) << 32)
+        return max(0.0, (end - begin) / self._tick_khz) if end and begin != 0xFFFFFFFFFFFFFFFF else 0.0
+
+    def _run_graph(self, graph) -> dict:
+        import torch
+
+        lib = load_library()
+        t0 = time.perf_counter()
+        with torch.cuda.device(self.device):
+            sg = self.streams[0]
+            sg.wait_stream(torch.cuda.current_stream(self.device))  # caller's writes to a / bt / hbm
+            self.ev[0].record(sg)
+            _check(lib.odh_probe_graph_launch(graph, sg.cuda_stream))
+            self.ev[4].record(sg)
+            self.ev[4].synchronize()
+        h = self.host.tolist()
+        return self._result(h, self._span_ms(h, 20), self._span_ms(h, 24), self.ev[0].elapsed_time(self.ev[4]), t0,
+                            graph=True)
 
     def _run(self) -> dict:
         import torch
@@ -259,9 +327,10 @@ class GpuProbe:
                 self.ev[4].record(sg)
             self.ev[4].synchronize()
         h = self.host.tolist()
-        gemm_ms = self.ev[0].elapsed_time(self.ev[1])
-        hbm_ms = self.ev[2].elapsed_time(self.ev[3])
-        probe_ms = self.ev[0].elapsed_time(self.ev[4])
+        return self._result(h, self.ev[0].elapsed_time(self.ev[1]), self.ev[2].elapsed_time(self.ev[3]),
+                            self.ev[0].elapsed_time(self.ev[4]), t0, graph=False)
+
+    def _result(self, h: List[int], gemm_ms: float, hbm_ms: float, probe_ms: float, t0: float, graph: bool) -> dict:
         xcd_blocks = h[0:8]
         err_xcd = h[8:16]
         gemm_err = h[16] & 0xFFFFFFFF
@@ -276,6 +345,7 @@ class GpuProbe:
             "hbm_gbps": 2.0 * self.hbm_bytes / (hbm_ms * 1e-3) / 1e9 if hbm_ms > 0 else 0.0,
             "gemm_errors": gemm_err, "hbm_errors": hbm_err, "xcd_blocks": xcd_blocks, "err_xcd": err_xcd,
             "xcds": sum(1 for x in xcd_blocks if x > 0), "wall_ms": (time.perf_counter() - t0) * 1e3,
+            "graph": graph, "graph_error": self._graph_error,
         }
 
 

@@ -92,6 +92,35 @@ def test_fused_probe_verify_detects_corrupted_operand(dev):
     assert p.run()["ok"]
 
 
+def test_graph_probe_replays_and_detects_corruption(dev):
+    """The start-up probe replays as one hipGraph: same verdicts as the eager launches, a
+    fresh HBM pattern per replay (device-side seed), and spans timed inside the kernels."""
+    from odh_kubeflow_amd.ops import gpu
+
+    p = gpu.GpuProbe(0, m=1024, n=1024, k=512, hbm_bytes=16 << 20)
+    rs = [p.run() for _ in range(3)]
+    assert all(r["ok"] and r["graph"] for r in rs), rs
+    assert rs[-1]["graph_error"] is None
+    r = rs[-1]
+    assert r["xcds"] == 8 and sum(r["xcd_blocks"]) == p.tiles
+    assert 0 < r["gemm_ms"] < r["gpu_ms"] + 0.05 and 0 < r["hbm_ms"] < r["gpu_ms"] + 0.05, r
+    seeds = set()
+    for _ in range(2):
+        p.run()
+        seeds.add(int(p.seed_dev.item()))
+    assert len(seeds) == 2  # each replay advanced the on-device pattern seed
+    expect_bad = int((p.bt[:, 7].float() != 0).sum().item())
+    p.a[5, 7] = (p.a[5, 7].float() + 1).to(torch.bfloat16)
+    r = p.run()
+    assert r["graph"] and not r["ok"] and r["gemm_errors"] == expect_bad and sum(r["err_xcd"]) == expect_bad
+    p.a[5, 7] = (p.a[5, 7].float() - 1).to(torch.bfloat16)
+    assert p.run()["ok"]
+    p.graph = False  # the eager launches: same verdict
+    r = p.run()
+    assert r["ok"] and not r["graph"]
+    p.close()
+
+
 def test_probe_verify_detects_corruption(dev):
     from odh_kubeflow_amd.ops import gpu
 

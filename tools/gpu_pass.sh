@@ -15,6 +15,7 @@
 #   refemu   bench.py --reference-emulation (control-plane lifecycle, reference behaviour)
 #   prof     rocprofv3 --kernel-trace --stats of bench.py
 #   pmc      rocprofv3 --pmc passes (MFMA busy, LDS bank conflicts, HBM bytes) of the probe kernels
+#   probe    start-up probe: eager launches vs hipGraph replay (tools/probe_microbench.py --startup)
 #   env      tools/gpu_env_probe.sh inventory
 #
 # Every GPU step runs under its own `timeout -k`; the first failure ends the pass (no retries).
@@ -93,6 +94,10 @@ for s in $steps; do
           python3 tools/probe_microbench.py --pmc-pass > "$out/pmc$i.log" 2>&1 || fail "pmc$i" $? "$out/pmc$i.log"
       done
       echo "pmc passes: $i" ;;
+    probe)
+      timeout -k 10 120 python tools/probe_microbench.py --startup > "$out/probe_startup.json" 2>&1 \
+        || fail probe $? "$out/probe_startup.json"
+      cat "$out/probe_startup.json" ;;
     env)
       timeout -k 10 200 bash tools/gpu_env_probe.sh > "$out/env.log" 2>&1 || fail env $? "$out/env.log" ;;
     *)

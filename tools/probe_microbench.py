@@ -128,6 +128,31 @@ def main():
     print(json.dumps(out, indent=1))
 
 
+def startup():
+    """The start-up probe as the node agent runs it (``gpu.PROBE_SHAPE``,
+    ``gpu.PROBE_HBM_BYTES``): eager launches vs the hipGraph replay, 200 runs each
+    (after 20 warm-up), medians and p95 of host wall time and GPU time."""
+    out = {}
+    p = gpu.GpuProbe(0)
+    probes = {"eager": p, "graph": p, "serial": gpu.GpuProbe(0, graph="serial")}
+    for key in ("eager", "graph", "serial") * 2:  # interleaved: clock drift shows up as A≠A
+        q = probes[key]
+        q.graph = {"eager": False, "graph": True, "serial": "serial"}[key]
+        for _ in range(20):
+            q.run()
+        rs = [q.run() for _ in range(200)]
+        assert all(r["ok"] and r["graph"] is (key != "eager") for r in rs), rs[-1]
+        row = {}
+        for k in ("wall_ms", "gpu_ms", "gemm_ms", "hbm_ms"):
+            v = sorted(r[k] for r in rs)
+            row[k + "_p50"] = round(v[len(v) // 2], 4)
+            row[k + "_p95"] = round(v[int(len(v) * 0.95)], 4)
+        out.setdefault(key, []).append(row)
+    p.close()
+    probes["serial"].close()
+    print(json.dumps(out, indent=1))
+
+
 def pmc_pass():
     """A short, fixed workload for ``rocprofv3 --pmc`` passes: the node agent's start-up
     probe as it runs on the notebook path (fused-verify bf16 MFMA GEMM of
@@ -150,5 +175,7 @@ def pmc_pass():
 if __name__ == "__main__":
     if "--pmc-pass" in sys.argv:
         pmc_pass()
+    elif "--startup" in sys.argv:
+        startup()
     else:
         main()

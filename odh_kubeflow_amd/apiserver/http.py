@@ -326,6 +326,8 @@ class ApiServer:
                 out = json.loads(resp.body)
             except (ValueError, TypeError):
                 out = None
+        if verb == "create" and not common["name"] and resp.status < 300 and isinstance(out, dict):
+            common["name"] = (out.get("metadata") or {}).get("name") or ""  # as kube-apiserver's objectRef
         self.audit.log(code=resp.status, response_obj=out, **common)
         return resp
 

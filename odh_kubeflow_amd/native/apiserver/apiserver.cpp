@@ -2230,6 +2230,14 @@ bool respond(int fd, int code, const std::string& body, bool keep_alive) {
   if (t_aud.on) {
     t_aud.code = code;
     if (t_aud.level == "RequestResponse") t_aud.resp = body;
+    if (t_aud.name.empty() && t_aud.verb == "create" && code < 300) {
+      // kube-apiserver names the created object in objectRef (generateName included)
+      try {
+        Value o = kj::parse(body);
+        if (const Value* md = o.get("metadata")) t_aud.name = md->str_or("name");
+      } catch (const kj::ParseError&) {
+      }
+    }
   }
   std::string h = "HTTP/1.1 " + std::to_string(code) + " " + reason_phrase(code) +
                   "\r\nContent-Type: application/json\r\nContent-Length: " + std::to_string(body.size()) +

@@ -139,7 +139,13 @@ async def _main(args, dist, torch, rank: int, world: int, local_rank: int, probe
         from ..apiserver.native import NativeApiServer
         from ..cluster import OPENSHIFT_CRDS
 
-        native = await NativeApiServer(OPENSHIFT_CRDS, gc=True).start()
+        audit = os.environ.get("DEBUG_WRITE_AUDITLOG")  # same debug aid as the test cluster
+        pol = None
+        if audit:
+            from ..apiserver.audit import AuditPolicy
+
+            pol = AuditPolicy([{"level": "Metadata"}])  # every request: what each process sends
+        native = await NativeApiServer(OPENSHIFT_CRDS, gc=True, audit_log_path=audit, audit_policy=pol).start()
         url[0] = native.url
         sched = await _start_scheduler(native.url)
     await _in_thread(dist.broadcast_object_list, url, 0)

@@ -33,6 +33,21 @@ from .client import Client, _refresh, _version_of
 SA_DIR = "/var/run/secrets/kubernetes.io/serviceaccount"
 
 
+def default_user_agent() -> str:
+    """client-go's ``rest.DefaultKubernetesUserAgent``: ``<binary>/<version> (<os>/<arch>)
+    <project>`` — the program name, so an apiserver audit log tells the processes apart
+    (``control_plane``, ``scheduler``, ``odh_manager`` …)."""
+    import platform
+    import sys
+
+    main = sys.modules.get("__main__")
+    spec = getattr(main, "__spec__", None)
+    prog = (spec.name.rsplit(".", 1)[-1] if spec is not None and spec.name else
+            os.path.splitext(os.path.basename(sys.argv[0] if sys.argv and sys.argv[0] else "python"))[0])
+    arch = {"x86_64": "amd64", "aarch64": "arm64"}.get(platform.machine(), platform.machine() or "unknown")
+    return f"{prog or 'python'}/v0.0.0 ({sys.platform}/{arch}) odh-kubeflow-amd"
+
+
 @dataclass
 class RestConfig:
     host: str
@@ -44,7 +59,7 @@ class RestConfig:
     insecure: bool = False
     qps: float = 0.0  # 0 = unlimited (controller-runtime defaults 20/30 on real clusters: pass --qps/--burst)
     burst: int = 0
-    user_agent: str = "odh-kubeflow-amd"
+    user_agent: str = field(default_factory=lambda: default_user_agent())
     extra: dict = field(default_factory=dict)
 
     def ssl_context(self) -> Optional[ssl.SSLContext]:

@@ -44,6 +44,11 @@ def test_audit_log_and_kubeconfig(run, tmp_path, transport):
     c = create[0]
     assert c["objectRef"]["apiGroup"] == "kubeflow.org" and c["responseStatus"]["code"] == 201
     assert c["requestObject"]["metadata"]["name"] == "nb" and c["responseObject"]["metadata"]["uid"]
+    assert c["objectRef"]["name"] == "nb"  # kube-apiserver names the created object
+    # client-go's default user agent: the program, so the log tells the processes apart
+    assert c["userAgent"].split("/")[0] not in ("", "odh-kubeflow-amd") and "odh-kubeflow-amd" in c["userAgent"]
+    sts = [e for e in events if e["verb"] == "create" and e["objectRef"]["resource"] == "statefulsets"]
+    assert sts[0]["objectRef"]["name"] == "nb"
     verbs = {(e["verb"], e["objectRef"]["resource"]) for e in events}
     assert ("create", "statefulsets") in verbs  # what the controllers did in that namespace
     assert any(e["verb"] == "patch" and e["objectRef"].get("subresource") == "status" for e in events)

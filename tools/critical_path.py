@@ -1,0 +1,136 @@
+"""Create → Ready critical path of each Notebook, from an apiserver audit log.
+
+    DEBUG_WRITE_AUDITLOG=/tmp/audit.jsonl python bench.py ...
+    python tools/critical_path.py /tmp/audit.jsonl [--namespace-prefix bench-] > path.json
+
+Both test apiservers write kube-apiserver audit events with microsecond
+``requestReceivedTimestamp`` / ``stageTimestamp`` and the client's user agent (the
+program: ``control_plane``, ``scheduler``, ``bench`` …).  For every Notebook the requests
+on its Ready path are picked out in order:
+
+    notebook create (admission webhook inside) → StatefulSet create (kf reconciler)
+    → lock release (odh reconciler; optional) → StatefulSet scale-up (kf reconciler;
+    optional) → Pod create (StatefulSet controller) → Pod bind (scheduler) → Pod status Ready (node
+    agent, start-up probe inside) → StatefulSet status → Notebook status (kf reconciler)
+
+and each hop is split into ``gap`` (previous request answered → this one received: watch
+delivery, queueing, the controller's own work) and ``serve`` (this request inside the
+apiserver, admission included).  Medians and p95 over the Notebooks are printed as JSON,
+with the user agent that issued each step.  This is where the create→Ready milliseconds
+of ``bench.py`` go, hop by hop (the reference's envtest audit-log aid,
+``odh/controllers/suite_test.go:125-137``, put to a latency use).
+"""
+
+from __future__ import annotations
+
+import argparse
+import json
+import sys
+from collections import defaultdict
+from datetime import datetime, timezone
+
+OPTIONAL = {"lock_release", "sts_scale"}  # odh lock path (absent for kf-only / unlocked notebooks)
+STEPS = (
+    ("notebook_create", "create", "notebooks", "", "{nb}"),
+    ("sts_create", "create", "statefulsets", "", "{nb}"),
+    # odh: the webhook's image-pull lock (kubeflow-resource-stopped) holds replicas at 0
+    # until the reconciler sees the workbench ServiceAccount and removes it
+    ("lock_release", "patch", "notebooks", "", "{nb}"),
+    ("sts_scale", "update", "statefulsets", "", "{nb}"),
+    ("pod_create", "create", "pods", "", "{nb}-0"),
+    ("pod_bind", ("patch", "update", "create"), "pods", ("", "binding"), "{nb}-0"),
+    ("pod_ready", "patch", "pods", "status", "{nb}-0"),
+    ("sts_status", ("patch", "update"), "statefulsets", "status", "{nb}"),
+    ("notebook_status", ("patch", "update"), "notebooks", "status", "{nb}"),
+)
+
+
+def _ts(s: str) -> float:
+    return datetime.strptime(s, "%Y-%m-%dT%H:%M:%S.%fZ").replace(tzinfo=timezone.utc).timestamp()
+
+
+def _match(want, got) -> bool:
+    return got in want if isinstance(want, tuple) else got == want
+
+
+def pct(xs, q):
+    xs = sorted(xs)
+    if not xs:
+        return None
+    return xs[min(len(xs) - 1, int(round(q * (len(xs) - 1))))]
+
+
+def analyse(lines, ns_prefix: str = "") -> dict:
+    by_obj = defaultdict(list)  # (ns, resource, name) -> events in order
+    for line in lines:
+        e = json.loads(line)
+        if e.get("stage") != "ResponseComplete" or e.get("verb") in ("watch", "get", "list"):
+            continue
+        ref = e.get("objectRef") or {}
+        ns = ref.get("namespace", "")
+        if ns_prefix and not ns.startswith(ns_prefix):
+            continue
+        code = (e.get("responseStatus") or {}).get("code", 0)
+        if code >= 300:
+            continue
+        by_obj[(ns, ref.get("resource"), ref.get("name", ""))].append(
+            (_ts(e["requestReceivedTimestamp"]), _ts(e["stageTimestamp"]), e["verb"], ref.get("subresource", ""),
+             e.get("userAgent", "").split("/")[0]))
+    notebooks = [(ns, name) for (ns, res, name) in by_obj if res == "notebooks" and name and
+                 any(v == "create" for _, _, v, _, _ in by_obj[(ns, res, name)])]
+    hops = defaultdict(lambda: {"gap": [], "serve": [], "agents": defaultdict(int)})
+    totals = []
+    for ns, nb in notebooks:
+        prev_done = None
+        t0 = None
+        ok = True
+        for step, verb, res, sub, name in STEPS:
+            evs = by_obj.get((ns, res, name.format(nb=nb)), [])
+            hit = next(((r, d, ua) for r, d, v, s, ua in evs
+                        if _match(verb, v) and _match(sub, s) and (prev_done is None or r >= prev_done - 1e-4)), None)
+            if hit is None:
+                if step in OPTIONAL:
+                    continue
+                ok = False
+                break
+            r, d, ua = hit
+            if t0 is None:
+                t0 = r
+            h = hops[step]
+            h["serve"].append((d - r) * 1e3)
+            if prev_done is not None:
+                h["gap"].append((r - prev_done) * 1e3)
+            h["agents"][ua] += 1
+            prev_done = d
+        if ok:
+            totals.append((prev_done - t0) * 1e3)
+    out = {"notebooks": len(totals), "create_to_notebook_status_ms": {"p50": pct(totals, .5), "p95": pct(totals, .95)},
+           "hops": {}}
+    for step, *_ in STEPS:
+        h = hops.get(step)
+        if not h:
+            continue
+        out["hops"][step] = {
+            "gap_ms_p50": round(pct(h["gap"], .5), 3) if h["gap"] else None,
+            "gap_ms_p95": round(pct(h["gap"], .95), 3) if h["gap"] else None,
+            "serve_ms_p50": round(pct(h["serve"], .5), 3), "serve_ms_p95": round(pct(h["serve"], .95), 3),
+            "by": dict(h["agents"]),
+        }
+    for k in ("p50", "p95"):
+        v = out["create_to_notebook_status_ms"][k]
+        out["create_to_notebook_status_ms"][k] = round(v, 3) if v is not None else None
+    return out
+
+
+def main(argv=None) -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("audit_log")
+    ap.add_argument("--namespace-prefix", default="")
+    a = ap.parse_args(argv)
+    with open(a.audit_log) as f:
+        print(json.dumps(analyse(f, a.namespace_prefix), indent=1))
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -56,6 +56,7 @@ class ClusterConfig:
     # apiserver with kubectl / the REST client while a test runs
     audit_log_path: Optional[str] = field(default_factory=lambda: os.environ.get("DEBUG_WRITE_AUDITLOG"))
     kubeconfig_path: Optional[str] = field(default_factory=lambda: os.environ.get("DEBUG_WRITE_KUBECONFIG"))
+    audit_policy: Optional[object] = None  # apiserver.audit.AuditPolicy (default: config/debug/audit-policy.yaml)
 
 
 OPENSHIFT_CRDS = (kinds.IMAGE_STREAM, kinds.PROXY, kinds.ROUTE, kinds.OAUTH_CLIENT)
@@ -133,7 +134,7 @@ class LocalCluster:
         if self.cfg.audit_log_path:
             from .apiserver.audit import DEFAULT_POLICY, AuditLogger, AuditPolicy
 
-            audit = AuditLogger(self.cfg.audit_log_path, AuditPolicy.load(DEFAULT_POLICY))
+            audit = AuditLogger(self.cfg.audit_log_path, self.cfg.audit_policy or AuditPolicy.load(DEFAULT_POLICY))
         self.apiserver = await ApiServer(self.store, audit=audit).start("127.0.0.1", 0)
         self.rest_config = RestConfig(host=self.apiserver.url)
 
@@ -152,7 +153,7 @@ class LocalCluster:
             from .runtime.rest import RestClient, RestConfig
 
             self.native = await NativeApiServer(() if cfg.openshift else OPENSHIFT_CRDS, gc=cfg.gc,
-                                                audit_log_path=cfg.audit_log_path).start()
+                                                audit_log_path=cfg.audit_log_path, audit_policy=cfg.audit_policy).start()
             self.rest_config = RestConfig(host=self.native.url)
             admin = RestClient(self.rest_config)
             self._view_cache = InformerCache(admin)

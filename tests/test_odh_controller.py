@@ -9,6 +9,7 @@ DSPA secret (:1532-1791).  envtest has no GC, so "deleted with the Notebook" is 
 through ownerReferences (:1316-1328), except where the cluster runs with GC.
 """
 
+import asyncio
 import base64
 import json
 import os
@@ -386,4 +387,65 @@ def test_openshift_lock_waits_for_pull_secret_without_blocking_workers(run):
             sa["imagePullSecrets"] = [{"name": "default-dockercfg"}]
             await cl.admin.update(sa)
             assert await cl.wait_for(lambda: not locked("slow", "user"), 2)
+    run(go())
+
+
+@pytest.mark.parametrize("transport", ["http", "native"])
+def test_create_path_order_gating_children_then_one_unlock_write(run, tmp_path, transport):
+    """New Notebook: the objects the pod mounts / runs as and its NetworkPolicies exist
+    before the lock goes; finalizers and lock removal are ONE write; the finalizer-managed
+    exposure children (ReferenceGrant, HTTPRoute, auth-delegator binding) come after it."""
+    from odh_kubeflow_amd.apiserver.audit import AuditPolicy
+
+    log = tmp_path / "audit.log"
+
+    async def go():
+        c = cfg()
+        c.transport, c.audit_log_path, c.audit_policy = transport, str(log), AuditPolicy([{"level": "Metadata"}])
+        async with LocalCluster(c) as cl:
+            await create_nb(cl, "nb", annotations=AUTH)
+            assert await cl.wait_for(lambda: cl.notebook_ready("nb", "user"), 15)
+    run(go())
+    evs = [json.loads(line) for line in log.read_text().splitlines()]
+    writes = [(e["verb"], e["objectRef"]["resource"], e["objectRef"].get("name", ""), e["objectRef"].get("subresource", ""))
+              for e in evs if e["stage"] == "ResponseComplete" and e["verb"] not in ("get", "list", "watch")
+              and e["responseStatus"]["code"] < 300]
+    nb_writes = [w for w in writes if w[1] == "notebooks" and w[2] == "nb" and w[3] == "" and w[0] != "create"]
+    assert nb_writes == [("patch", "notebooks", "nb", "")], nb_writes  # finalizers + unlock: one write
+    unlock = writes.index(nb_writes[0])
+
+    def at(verb, res, name):
+        return next(i for i, w in enumerate(writes) if w[:3] == (verb, res, name))
+
+    for gating in (("create", "networkpolicies", "nb-ctrl-np"), ("create", "networkpolicies", "nb-kube-rbac-proxy-np"),
+                   ("create", "serviceaccounts", "nb"), ("create", "configmaps", "nb-kube-rbac-proxy-config")):
+        assert at(*gating) < unlock, gating
+    for exposure in (("create", "referencegrants", "notebook-httproute-access"), ("create", "httproutes", "nb-user-nb"),
+                     ("create", "clusterrolebindings", "nb-rbac-user-auth-delegator")):
+        assert at(*exposure) > unlock, exposure
+    # the kf controller scales the StatefulSet only after the unlock
+    assert at("update", "statefulsets", "nb") > unlock
+
+
+def test_lock_removal_never_drops_a_user_stop(run):
+    """The unlock write tests the lock value: a user who stops the Notebook while it still
+    waits for its pull secret keeps their stop annotation."""
+    async def go():
+        async with LocalCluster(ClusterConfig(odh=True, webhook=True, gc=False, openshift=True,
+                                              env={"SET_PIPELINE_RBAC": "false"})) as cl:
+            await cl.ensure_namespace("user")
+            await cl.admin.create({"apiVersion": "v1", "kind": "ServiceAccount",
+                                   "metadata": {"name": "default", "namespace": "user"}})
+            await create_nb(cl, "nb")
+            peek = lambda: cl.store.peek(kinds.NOTEBOOK, "nb", "user")  # noqa: E731
+            # waiting for the pull secret: finalizers are already durable, the lock is still on
+            assert await cl.wait_for(lambda: "notebook.opendatahub.io/httproute-cleanup" in m.finalizers(peek()), 3)
+            assert m.annotations(peek())["kubeflow-resource-stopped"] == "odh-notebook-controller-lock"
+            await cl.admin.patch(kinds.NOTEBOOK, {"metadata": {"annotations": {
+                "kubeflow-resource-stopped": "2026-10-16T00:00:00Z"}}}, "merge", name="nb", namespace="user")
+            sa = await cl.admin.get(kinds.SERVICE_ACCOUNT, "default", "user")
+            sa["imagePullSecrets"] = [{"name": "default-dockercfg"}]
+            await cl.admin.update(sa)
+            await asyncio.sleep(0.5)  # the SA watch re-triggers the reconcile at once
+            assert m.annotations(peek())["kubeflow-resource-stopped"] == "2026-10-16T00:00:00Z"
     run(go())

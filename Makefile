@@ -4,7 +4,7 @@ IMG ?= quay.io/opendatahub/odh-kubeflow-amd:latest
 NOTEBOOK_IMG ?= quay.io/opendatahub/workbench-rocm-pytorch:latest
 GPU_ARCH ?= gfx950
 
-.PHONY: build test test-matrix test-native test-gpu e2e bench bench-8 manifests deploy deploy-sharded undeploy lint license-check docker-build docker-build-notebook
+.PHONY: build test test-matrix test-native test-gpu e2e e2e-test bench bench-8 manifests deploy deploy-sharded undeploy lint license-check docker-build docker-build-notebook
 
 build:  ## hipcc --offload-arch=$(GPU_ARCH) kernels, host C++ telemetry/objcore, native apiserver (in-tree)
 	ODH_GPU_ARCH=$(GPU_ARCH) $(PYTHON) -m odh_kubeflow_amd.ops.build
@@ -24,6 +24,13 @@ test-gpu: build  ## HIP kernels vs fp32 torch on an MI355X
 
 e2e: build  ## separate apiserver / kf / odh / node-agent processes (reference e2e sequence)
 	$(PYTHON) -m pytest tests/test_processes_e2e.py -q
+
+# the reference's `make e2e-test` (odh/Makefile:192-197): against the cluster in $(KUBECONFIG)
+# after `make deploy`, or — with no kubeconfig — against the dev stack as local processes.
+# E2E_TEST_FLAGS e.g. "--nb-namespace e2e-notebook-controller --skip-deletion"
+E2E_TEST_FLAGS ?=
+e2e-test: build  ## e2e suite (e2e/): deployed overlay if KUBECONFIG is set, else local processes
+	$(PYTHON) -m pytest e2e -v $(if $(KUBECONFIG),--kubeconfig $(KUBECONFIG)) $(E2E_TEST_FLAGS)
 
 bench: build  ## headline benchmark on one MI355X
 	$(PYTHON) bench.py

@@ -41,7 +41,7 @@ import sys
 from typing import Dict, Iterable, List, Optional
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-PY_DIRS = ("odh_kubeflow_amd", "tools", "tests")
+PY_DIRS = ("odh_kubeflow_amd", "tools", "tests", "e2e")
 PY_FILES = ("bench.py", "__graft_entry__.py")
 
 # (rule, kind, name-regex) → reason.  Manifest findings the design needs.
@@ -105,7 +105,7 @@ def check_python_source(path: str, text: str) -> List[Finding]:
         return [Finding("syntax-error", path, e.lineno or 0, str(e))]
     lines = text.splitlines()
     out: List[Finding] = []
-    is_test = os.path.relpath(path, ROOT).startswith("tests" + os.sep)
+    is_test = os.path.relpath(path, ROOT).startswith(("tests" + os.sep, "e2e" + os.sep))
 
     def add(rule, node, msg):
         ln = getattr(node, "lineno", 0)

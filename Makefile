@@ -4,7 +4,7 @@ IMG ?= quay.io/opendatahub/odh-kubeflow-amd:latest
 NOTEBOOK_IMG ?= quay.io/opendatahub/workbench-rocm-pytorch:latest
 GPU_ARCH ?= gfx950
 
-.PHONY: build test test-matrix test-native test-gpu e2e e2e-test bench bench-8 manifests deploy deploy-sharded undeploy lint license-check docker-build docker-build-notebook
+.PHONY: build test test-matrix test-native test-gpu e2e e2e-test coverage bench bench-8 manifests deploy deploy-sharded undeploy lint license-check docker-build docker-build-notebook
 
 build:  ## hipcc --offload-arch=$(GPU_ARCH) kernels, host C++ telemetry/objcore, native apiserver (in-tree)
 	ODH_GPU_ARCH=$(GPU_ARCH) $(PYTHON) -m odh_kubeflow_amd.ops.build
@@ -31,6 +31,10 @@ e2e: build  ## separate apiserver / kf / odh / node-agent processes (reference e
 E2E_TEST_FLAGS ?=
 e2e-test: build  ## e2e suite (e2e/): deployed overlay if KUBECONFIG is set, else local processes
 	$(PYTHON) -m pytest e2e -v $(if $(KUBECONFIG),--kubeconfig $(KUBECONFIG)) $(E2E_TEST_FLAGS)
+
+# per-component line coverage with floors (the reference's codecov flags, .codecov.yml:19-32)
+coverage: build  ## line coverage of the CPU suite per component (tools/coverage.py → coverage.json)
+	$(PYTHON) tools/coverage.py --flag kf=78 --flag odh=85 --flag runtime=84 --flag apiserver=85
 
 bench: build  ## headline benchmark on one MI355X
 	$(PYTHON) bench.py

@@ -30,3 +30,18 @@ def test_bench_culling_cpu_rehearsal():
     assert d["false_culls_under_load"] == 0 and d["culled"] == 8
     assert d["gpu0_busy_mean_under_load"] >= 90
     assert 0 <= d["idle_reclaim_ms_p50"] < 1500
+
+
+def test_coverage_tool_units(tmp_path):
+    import importlib.util
+    import os
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    spec = importlib.util.spec_from_file_location("cov_tool", os.path.join(root, "tools", "coverage.py"))
+    cov = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(cov)
+    src = tmp_path / "m.py"
+    src.write_text("x = 1\n\ndef f(a):\n    if a:\n        return 2\n    return 3\n")
+    assert cov.executable_lines(str(src)) >= {1, 3, 4, 5, 6}
+    assert cov.flag_of("controllers/odh/route.py") == "odh" and cov.flag_of("controllers/notebook.py") == "kf"
+    assert cov.flag_of("runtime/informer.py") == "runtime" and cov.flag_of("something_new.py") == "other"

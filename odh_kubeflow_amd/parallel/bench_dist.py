@@ -144,7 +144,8 @@ async def _main(args, dist, torch, rank: int, world: int, local_rank: int, probe
         if audit:
             from ..apiserver.audit import AuditPolicy
 
-            pol = AuditPolicy([{"level": "Metadata"}])  # every request: what each process sends
+            lv = os.environ.get("DEBUG_AUDIT_LEVEL", "Metadata")  # Request / RequestResponse: with bodies
+            pol = AuditPolicy([{"level": lv}])  # every request: what each process sends
         native = await NativeApiServer(OPENSHIFT_CRDS, gc=True, audit_log_path=audit, audit_policy=pol).start()
         url[0] = native.url
         sched = await _start_scheduler(native.url)

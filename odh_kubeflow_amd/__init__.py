@@ -6,4 +6,4 @@ idle-notebook culler) that places notebook StatefulSets on the 8 MI355X GPUs of 
 through the ``amd.com/gpu`` device plugin and culls on amdgpu busy counters.
 """
 
-__version__ = "0.1.0"
+__version__ = "0.2.0"

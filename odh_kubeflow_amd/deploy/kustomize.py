@@ -14,6 +14,8 @@ kustomize's semantics, so tests can assert on what ``kubectl apply -k`` would ap
   against a resource's current and original names — a target that matches several
   resources patches all of them, and a JSON6902 ``replace`` on a missing path fails,
   exactly the failure mode a too-broad regex has in real kustomize);
+* ``images`` (``name`` → ``newName`` / ``newTag`` / ``digest`` on every container and init
+  container image of a pod template; the release tooling sets the tag there);
 * ``namespace`` and ``namePrefix`` with the name-reference fix-ups kustomize applies
   (ConfigMap/Secret refs in pod templates, ServiceAccount names, RBAC subjects and
   roleRefs, webhook ``clientConfig.service``), CRDs and cluster roles' aggregation
@@ -36,7 +38,7 @@ from ..utils.jsonpatch import PatchError, apply_patch, apply_strategic_merge_pat
 CLUSTER_SCOPED = {"CustomResourceDefinition", "ClusterRole", "ClusterRoleBinding", "Namespace",
                   "MutatingWebhookConfiguration", "ValidatingWebhookConfiguration", "PriorityClass"}
 KNOWN_KEYS = {"apiVersion", "kind", "resources", "namespace", "namePrefix", "patches", "configMapGenerator",
-              "generatorOptions"}
+              "generatorOptions", "images"}
 
 
 class KustomizeError(ValueError):
@@ -143,6 +145,41 @@ def _fix_references(resources: List[_Res], renames: Dict[tuple, str], namespace:
             o["spec"]["serviceName"] = ren("Service", o["spec"]["serviceName"])
 
 
+def split_image(image: str):
+    """``(name, tag, digest)`` of an image reference (a registry port is not a tag)."""
+    name, digest = (image.split("@", 1) + [None])[:2]
+    tag = None
+    slash = name.rfind("/")
+    colon = name.rfind(":")
+    if colon > slash:
+        name, tag = name[:colon], name[colon + 1:]
+    return name, tag, digest
+
+
+def _apply_images(resources: List[_Res], images: List[dict], kpath: str) -> None:
+    for spec in images:
+        if "name" not in spec:
+            raise KustomizeError(f"{kpath}: images entry without name: {spec}")
+        unknown = set(spec) - {"name", "newName", "newTag", "digest"}
+        if unknown:
+            raise KustomizeError(f"{kpath}: unsupported images fields {sorted(unknown)}")
+        for r in resources:
+            ps = _pod_spec(r.obj)
+            if ps is None:
+                continue
+            for c in (ps.get("containers") or []) + (ps.get("initContainers") or []):
+                name, tag, digest = split_image(c.get("image") or "")
+                if name != spec["name"]:
+                    continue
+                name = spec.get("newName", name)
+                if "digest" in spec:
+                    c["image"] = f"{name}@{spec['digest']}"
+                elif "newTag" in spec:
+                    c["image"] = f"{name}:{spec['newTag']}"
+                else:
+                    c["image"] = name + (f":{tag}" if tag else "") + (f"@{digest}" if digest else "")
+
+
 def _matches(res: _Res, target: dict) -> bool:
     for k in target:
         if k not in ("kind", "name", "group", "version"):
@@ -237,6 +274,9 @@ def _build(d: str) -> List[_Res]:
                 r.obj = apply_strategic_merge_patch(r.obj, patch)
         else:
             raise KustomizeError(f"{kpath}: unsupported patch body")
+
+    if k.get("images"):
+        _apply_images(resources, k["images"], kpath)
 
     ns = k.get("namespace")
     prefix = k.get("namePrefix") or ""

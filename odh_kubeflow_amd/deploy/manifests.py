@@ -40,7 +40,7 @@ from __future__ import annotations
 
 import argparse
 import os
-from typing import Dict, List
+from typing import Dict, List, Optional
 
 import yaml
 
@@ -65,7 +65,17 @@ MI355X_PARAMS = ["GPU_NODE_SELECTOR=true", "GPU_SHM_SIZE_PER_GPU=16Gi",
                  # driver only offers dmabuf IPC fail hipIpcGetMemHandle otherwise)
                  "MULTI_GPU_ENV=HSA_ENABLE_IPC_MODE_LEGACY=0"]
 MI355X_CULLER = ["CULLING_ACTIVITY_SOURCE=combined", "ENABLE_CULLING=true"]
-MANAGER_IMAGE = "quay.io/opendatahub/odh-kubeflow-amd:latest"
+# the base manifests carry the development tag; every overlay pins the release tag through
+# kustomize `images` (releasing/VERSION, set by tools/release.py — the reference's
+# releasing/update-manifests-images + releasing/version/VERSION)
+MANAGER_IMAGE_NAME = "quay.io/opendatahub/odh-kubeflow-amd"
+MANAGER_IMAGE = MANAGER_IMAGE_NAME + ":main"
+REPO_ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def release_version(root: str = REPO_ROOT) -> str:
+    with open(os.path.join(root, "releasing", "VERSION")) as f:
+        return f.read().strip()
 KUBE_RBAC_PROXY_IMAGE = "quay.io/brancz/kube-rbac-proxy:v0.18.1"
 
 
@@ -447,8 +457,11 @@ def kustomization(resources: List[str], **extra) -> dict:
     return k
 
 
-def tree() -> Dict[str, object]:
-    """path → document (or list of documents)."""
+def tree(version: Optional[str] = None) -> Dict[str, object]:
+    """path → document (or list of documents); ``version`` = the image tag every overlay
+    pins (default: ``releasing/VERSION``)."""
+    version = version or release_version()
+    images = [{"name": MANAGER_IMAGE_NAME, "newTag": version}]
     t: Dict[str, object] = {}
     t["crd/bases/kubeflow.org_notebooks.yaml"] = notebook_crd()
     t["crd/kustomization.yaml"] = kustomization(["bases/kubeflow.org_notebooks.yaml"])
@@ -500,14 +513,14 @@ def tree() -> Dict[str, object]:
         ["rbac.yaml", "statefulset.yaml", "services.yaml", "webhooks.yaml"],
         configMapGenerator=generators, generatorOptions={"disableNameSuffixHash": True})
     t["default/kustomization.yaml"] = kustomization(["../crd", "../rbac", "../manager", "../webhook", "../node-agent"],
-                                                    namespace="opendatahub", namePrefix=NAME_PREFIX)
+                                                    namespace="opendatahub", namePrefix=NAME_PREFIX, images=images)
     t["overlays/standalone/kustomization.yaml"] = kustomization(["../../default", "../../webhook-certs"],
-                                                                namespace="opendatahub")
+                                                                namespace="opendatahub", images=images)
     t["overlays/kubeflow/kustomization.yaml"] = kustomization(
-        ["../../default", "../../webhook-certs"], namespace="kubeflow",
+        ["../../default", "../../webhook-certs"], namespace="kubeflow", images=images,
         configMapGenerator=[{"name": "config", "behavior": "merge", "literals": ["USE_ISTIO=true"]}])
     t["overlays/openshift/kustomization.yaml"] = kustomization(
-        ["../../default"],
+        ["../../default"], images=images,
         configMapGenerator=[{"name": "config", "behavior": "merge", "literals": ["ADD_FSGROUP=false"]}],
         patches=[{"target": {"kind": "Service", "name": ".*webhook-service"}, "patch":
                   "- op: add\n  path: /metadata/annotations\n  value:\n    service.beta.openshift.io/"
@@ -519,14 +532,14 @@ def tree() -> Dict[str, object]:
                          {"name": "notebook-controller-culler-config", "behavior": "merge",
                           "literals": list(MI355X_CULLER)}]
     t["overlays/mi355x/kustomization.yaml"] = kustomization(["../../default", "../../webhook-certs"],
-                                                            namespace="opendatahub",
+                                                            namespace="opendatahub", images=images,
                                                             configMapGenerator=mi355x_generators)
     # the serving cert covers every shard's Service; every shard's configuration gets the caBundle
     svc_names = [NAME_PREFIX + o["metadata"]["name"] for o in cp["services.yaml"][1:]]
     mwc_names = [NAME_PREFIX + o["metadata"]["name"] for o in cp["webhooks.yaml"]]
     t["overlays/mi355x-sharded/kustomization.yaml"] = kustomization(
         ["../../crd", "../../user-rbac", "../../node-agent", "../../webhook-certs", "../../control-plane"],
-        namespace="opendatahub", namePrefix=NAME_PREFIX, configMapGenerator=mi355x_generators,
+        namespace="opendatahub", namePrefix=NAME_PREFIX, configMapGenerator=mi355x_generators, images=images,
         patches=_certs_args_patches(svc_names, mwc_names))
     # debug aid: the test apiservers' audit policy (DEBUG_WRITE_AUDITLOG, apiserver/audit.py)
     t["debug/audit-policy.yaml"] = AUDIT_POLICY
@@ -550,9 +563,9 @@ def _represent_list(dumper, data):
 _Dumper.add_representer(list, _represent_list)
 
 
-def write(out: str) -> List[str]:
+def write(out: str, version: Optional[str] = None) -> List[str]:
     written = []
-    for path, doc in sorted(tree().items()):
+    for path, doc in sorted(tree(version).items()):
         full = os.path.join(out, path)
         os.makedirs(os.path.dirname(full), exist_ok=True)
         with open(full, "w") as f:

@@ -260,3 +260,37 @@ def test_sharded_overlay_shape():
     role = _by(objs, "ClusterRole")["odh-kubeflow-amd-control-plane-role"]
     assert _allowed(role, "", "namespaces", "patch") and _allowed(role, "apps", "statefulsets", "create")
     assert _allowed(role, "gateway.networking.k8s.io", "httproutes", "delete")
+
+
+def test_kustomize_images_transformer_and_release_tag(tmp_path):
+    import shutil
+
+    from odh_kubeflow_amd.deploy import kustomize, manifests
+
+    assert kustomize.split_image("registry:5000/org/img:v1@sha256:ab") == ("registry:5000/org/img", "v1", "sha256:ab")
+    assert kustomize.split_image("registry:5000/org/img") == ("registry:5000/org/img", None, None)
+    # overlays pin the release tag; the base keeps the development tag
+    tag = manifests.release_version()
+    for ov in ("standalone", "kubeflow", "openshift", "mi355x", "mi355x-sharded"):
+        imgs = {c["image"] for d in kustomize.build(os.path.join(ROOT, "config", "overlays", ov))
+                for c in ((kustomize._pod_spec(d) or {}).get("containers") or []) if "odh-kubeflow-amd" in c["image"]}
+        assert imgs == {f"{manifests.MANAGER_IMAGE_NAME}:{tag}"}, (ov, imgs)
+    base = yaml.safe_load(open(os.path.join(ROOT, "config", "manager", "kf_manager.yaml")))
+    assert base["spec"]["template"]["spec"]["containers"][0]["image"].endswith(":main")
+    # the release tool: VERSION, __version__, regenerated overlays
+    os.makedirs(tmp_path / "odh_kubeflow_amd")
+    shutil.copy(os.path.join(ROOT, "odh_kubeflow_amd", "__init__.py"), tmp_path / "odh_kubeflow_amd" / "__init__.py")
+    import importlib.util
+
+    spec = importlib.util.spec_from_file_location("release_tool", os.path.join(ROOT, "tools", "release.py"))
+    rel = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(rel)
+    changed = rel.release("v9.8.7-rc.1", str(tmp_path))
+    assert "releasing/VERSION" in changed and (tmp_path / "releasing" / "VERSION").read_text().strip() == "v9.8.7-rc.1"
+    assert '__version__ = "9.8.7rc1"' in (tmp_path / "odh_kubeflow_amd" / "__init__.py").read_text()
+    docs = kustomize.build(str(tmp_path / "config" / "overlays" / "mi355x-sharded"))
+    imgs = {c["image"] for d in docs for c in ((kustomize._pod_spec(d) or {}).get("containers") or [])
+            if "odh-kubeflow-amd" in c["image"]}
+    assert imgs == {f"{manifests.MANAGER_IMAGE_NAME}:v9.8.7-rc.1"}
+    with pytest.raises(ValueError):
+        rel.pep440("1.2")

@@ -4,7 +4,7 @@ IMG ?= quay.io/opendatahub/odh-kubeflow-amd:latest
 NOTEBOOK_IMG ?= quay.io/opendatahub/workbench-rocm-pytorch:latest
 GPU_ARCH ?= gfx950
 
-.PHONY: build test test-matrix test-native test-gpu e2e e2e-test coverage bench bench-8 manifests deploy deploy-sharded undeploy lint license-check docker-build docker-build-notebook
+.PHONY: build test test-matrix test-native test-gpu e2e e2e-test conformance-run conformance-report conformance-clean coverage bench bench-8 manifests deploy deploy-sharded undeploy lint license-check docker-build docker-build-notebook
 
 build:  ## hipcc --offload-arch=$(GPU_ARCH) kernels, host C++ telemetry/objcore, native apiserver (in-tree)
 	ODH_GPU_ARCH=$(GPU_ARCH) $(PYTHON) -m odh_kubeflow_amd.ops.build
@@ -31,6 +31,20 @@ e2e: build  ## separate apiserver / kf / odh / node-agent processes (reference e
 E2E_TEST_FLAGS ?=
 e2e-test: build  ## e2e suite (e2e/): deployed overlay if KUBECONFIG is set, else local processes
 	$(PYTHON) -m pytest e2e -v $(if $(KUBECONFIG),--kubeconfig $(KUBECONFIG)) $(E2E_TEST_FLAGS)
+
+# in-cluster conformance run of the e2e suite (the reference's conformance/ Makefile flow):
+# setup, the test pod, wait for its done file, copy the report out
+CONFORMANCE_NS ?= odh-kubeflow-amd-conformance
+conformance-run:  ## run the e2e suite as a pod in the current cluster (config/conformance)
+	kubectl apply -f config/conformance/setup.yaml
+	kubectl apply -f config/conformance/e2e-conformance.yaml
+conformance-report:  ## wait for the conformance pod and copy its JUnit report to /tmp/odh-conformance
+	until kubectl exec notebook-conformance -n $(CONFORMANCE_NS) -- ls /tmp/odh-conformance/done; do sleep 30; done
+	mkdir -p /tmp/odh-conformance
+	kubectl cp $(CONFORMANCE_NS)/notebook-conformance:/tmp/odh-conformance/junit.xml /tmp/odh-conformance/junit.xml
+	kubectl exec notebook-conformance -n $(CONFORMANCE_NS) -- cat /tmp/odh-conformance/exit_code
+conformance-clean:
+	kubectl delete -f config/conformance/e2e-conformance.yaml -f config/conformance/setup.yaml
 
 # per-component line coverage with floors (the reference's codecov flags, .codecov.yml:19-32)
 coverage: build  ## line coverage of the CPU suite per component (tools/coverage.py → coverage.json)

@@ -15,6 +15,8 @@ def pytest_addoption(parser):
     g = parser.getgroup("odh e2e")
     g.addoption("--kubeconfig", default=None,
                 help="run against this cluster (else $E2E_KUBECONFIG; neither: the local dev processes)")
+    g.addoption("--in-cluster", action="store_true",
+                help="run against the cluster this pod runs in (its ServiceAccount; config/conformance)")
     g.addoption("--nb-namespace", default="e2e-notebook-controller",
                 help="namespace the test notebooks are created in")
     g.addoption("--controller-namespace", default="opendatahub", help="namespace the controllers are deployed in")
@@ -37,7 +39,9 @@ def harness(opts, tmp_path_factory):
     from .harness import ClusterHarness, LocalHarness
 
     kc = opts.kubeconfig or os.environ.get("E2E_KUBECONFIG")
-    if kc:
+    if opts.in_cluster:
+        h = ClusterHarness(opts.nb_namespace, opts.controller_namespace, None, opts.name_prefix, in_cluster=True)
+    elif kc:
         h = ClusterHarness(opts.nb_namespace, opts.controller_namespace, kc, opts.name_prefix)
     else:
         h = LocalHarness(opts.nb_namespace, opts.controller_namespace, str(tmp_path_factory.mktemp("e2e")))

@@ -100,12 +100,20 @@ class ClusterHarness(Harness):
     """A deployed overlay on a real cluster (``--kubeconfig`` / ``KUBECONFIG``)."""
 
     def __init__(self, nb_namespace: str, controller_namespace: str, kubeconfig: Optional[str] = None,
-                 name_prefix: str = "odh-kubeflow-amd-"):
+                 name_prefix: str = "odh-kubeflow-amd-", in_cluster: bool = False):
         super().__init__(nb_namespace, controller_namespace)
-        self.client = RestClient(RestConfig.load(None, kubeconfig))
+        self.client = RestClient(RestConfig.in_cluster() if in_cluster else RestConfig.load(None, kubeconfig))
         self.prefix = name_prefix
         self._culler_saved: Optional[Dict[str, str]] = None
         self._culler_created = False
+
+        async def ensure_ns():  # the reference's run-e2e-test.sh creates it (`oc new-project`)
+            try:
+                await self.client.create({"apiVersion": "v1", "kind": "Namespace", "metadata": {"name": nb_namespace}})
+            except ApiError as e:
+                if e.code not in (403, 409):
+                    raise
+        self.run(ensure_ns())
 
     def _workloads(self) -> List[Tuple[str, str]]:
         async def find():

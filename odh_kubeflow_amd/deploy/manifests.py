@@ -281,6 +281,59 @@ def node_agent_daemonset() -> dict:
                                                            "path": "/var/lib/kubelet/device-plugins"}}]}}}}
 
 
+CONFORMANCE_NS = "odh-kubeflow-amd-conformance"
+CONFORMANCE_REPORT_DIR = "/tmp/odh-conformance"
+
+
+def conformance_docs(version: str) -> Dict[str, object]:
+    """In-cluster conformance run of the e2e suite (the reference's ``conformance/1.7``:
+    a namespace + ServiceAccount + binding, then a test pod that leaves a report and a
+    ``done`` file for ``report-pod.sh`` to copy out).  The pod runs ``pytest e2e
+    --in-cluster`` with its ServiceAccount and writes a JUnit report."""
+    sa = "conformance"
+    ns_doc = {"apiVersion": "v1", "kind": "Namespace", "metadata": {"name": CONFORMANCE_NS}}
+    sa_doc = {"apiVersion": "v1", "kind": "ServiceAccount", "metadata": {"name": sa, "namespace": CONFORMANCE_NS}}
+    role = {"apiVersion": "rbac.authorization.k8s.io/v1", "kind": "ClusterRole",
+            "metadata": {"name": "odh-kubeflow-amd-conformance"},
+            "rules": [{"apiGroups": ["kubeflow.org"], "resources": ["notebooks"], "verbs": ["*"]},
+                      {"apiGroups": ["apps"], "resources": ["statefulsets", "deployments"],
+                       "verbs": ["get", "list", "watch", "patch"]},
+                      {"apiGroups": [""], "resources": ["pods", "services", "serviceaccounts", "events"],
+                       "verbs": ["get", "list", "watch"]},
+                      {"apiGroups": [""], "resources": ["configmaps"],
+                       "verbs": ["get", "list", "watch", "create", "update", "delete"]},
+                      {"apiGroups": ["networking.k8s.io"], "resources": ["networkpolicies"],
+                       "verbs": ["get", "list", "watch"]},
+                      {"apiGroups": ["gateway.networking.k8s.io"], "resources": ["httproutes", "referencegrants"],
+                       "verbs": ["get", "list", "watch"]},
+                      {"apiGroups": ["rbac.authorization.k8s.io"], "resources": ["clusterrolebindings"],
+                       "verbs": ["get", "list"]},
+                      {"apiGroups": ["apiextensions.k8s.io"], "resources": ["customresourcedefinitions"],
+                       "verbs": ["get"]},
+                      {"apiGroups": ["coordination.k8s.io"], "resources": ["leases"], "verbs": ["get", "list"]}]}
+    binding_doc = {"apiVersion": "rbac.authorization.k8s.io/v1", "kind": "ClusterRoleBinding",
+                   "metadata": {"name": "odh-kubeflow-amd-conformance"},
+                   "roleRef": {"apiGroup": "rbac.authorization.k8s.io", "kind": "ClusterRole",
+                               "name": "odh-kubeflow-amd-conformance"},
+                   "subjects": [{"kind": "ServiceAccount", "name": sa, "namespace": CONFORMANCE_NS}]}
+    run = (f"mkdir -p {CONFORMANCE_REPORT_DIR}; python -m pytest e2e -v --in-cluster "
+           f"--nb-namespace {CONFORMANCE_NS} --junitxml {CONFORMANCE_REPORT_DIR}/junit.xml "
+           f"> {CONFORMANCE_REPORT_DIR}/e2e.log 2>&1; echo $? > {CONFORMANCE_REPORT_DIR}/exit_code; "
+           f"touch {CONFORMANCE_REPORT_DIR}/done; sleep 86400")
+    pod = {"apiVersion": "v1", "kind": "Pod",
+           "metadata": {"name": "notebook-conformance", "namespace": CONFORMANCE_NS,
+                        "labels": {"app": "odh-kubeflow-amd-conformance"}},
+           "spec": {"serviceAccountName": sa, "restartPolicy": "Never",
+                    "containers": [{"name": "e2e", "image": f"{MANAGER_IMAGE_NAME}:{version}",
+                                    "workingDir": "/opt/odh-kubeflow-amd",
+                                    "command": ["/bin/sh", "-c", run],
+                                    "env": [{"name": "HOME", "value": "/tmp"}],
+                                    "securityContext": dict(RESTRICTED),
+                                    "resources": {"requests": {"cpu": "200m", "memory": "256Mi"},
+                                                  "limits": {"memory": "1Gi"}}}]}}
+    return {"setup.yaml": [ns_doc, sa_doc, role, binding_doc], "e2e-conformance.yaml": pod}
+
+
 def webhook_service() -> dict:
     return {"apiVersion": "v1", "kind": "Service",
             "metadata": {"name": "odh-notebook-controller-webhook-service"},
@@ -541,6 +594,9 @@ def tree(version: Optional[str] = None) -> Dict[str, object]:
         ["../../crd", "../../user-rbac", "../../node-agent", "../../webhook-certs", "../../control-plane"],
         namespace="opendatahub", namePrefix=NAME_PREFIX, configMapGenerator=mi355x_generators, images=images,
         patches=_certs_args_patches(svc_names, mwc_names))
+    # in-cluster conformance run of the e2e suite (not part of any overlay; make conformance-run)
+    for f, doc in conformance_docs(version).items():
+        t[f"conformance/{f}"] = doc
     # debug aid: the test apiservers' audit policy (DEBUG_WRITE_AUDITLOG, apiserver/audit.py)
     t["debug/audit-policy.yaml"] = AUDIT_POLICY
     t["samples/notebook_v1_1gpu.yaml"] = sample("rocm-pytorch-1gpu", 1)

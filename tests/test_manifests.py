@@ -294,3 +294,22 @@ def test_kustomize_images_transformer_and_release_tag(tmp_path):
     assert imgs == {f"{manifests.MANAGER_IMAGE_NAME}:v9.8.7-rc.1"}
     with pytest.raises(ValueError):
         rel.pep440("1.2")
+
+
+def test_conformance_bundle_runs_the_e2e_suite_in_cluster():
+    setup = list(yaml.safe_load_all(open(os.path.join(ROOT, "config", "conformance", "setup.yaml"))))
+    pod = yaml.safe_load(open(os.path.join(ROOT, "config", "conformance", "e2e-conformance.yaml")))
+    kinds_ = [d["kind"] for d in setup]
+    assert kinds_ == ["Namespace", "ServiceAccount", "ClusterRole", "ClusterRoleBinding"]
+    ns = setup[0]["metadata"]["name"]
+    assert pod["metadata"]["namespace"] == ns and pod["spec"]["serviceAccountName"] == setup[1]["metadata"]["name"]
+    c = pod["spec"]["containers"][0]
+    assert c["image"] == f"{manifests.MANAGER_IMAGE_NAME}:{manifests.release_version()}"
+    cmd = c["command"][-1]
+    assert "pytest e2e" in cmd and "--in-cluster" in cmd and f"--nb-namespace {ns}" in cmd and "done" in cmd
+    assert c["securityContext"]["runAsNonRoot"] and c["securityContext"]["allowPrivilegeEscalation"] is False
+    # the ServiceAccount may do what the suite does: notebooks, culler ConfigMap, rollouts
+    rules = setup[2]["rules"]
+    assert any(r["resources"] == ["notebooks"] and r["verbs"] == ["*"] for r in rules)
+    assert any("deployments" in r["resources"] and "patch" in r["verbs"] for r in rules)
+    assert any(r["resources"] == ["configmaps"] and "update" in r["verbs"] for r in rules)

@@ -1,10 +1,10 @@
 # Developer targets (the reference's kf/Makefile and odh/Makefile counterparts).
 PYTHON ?= python3
-IMG ?= quay.io/opendatahub/odh-kubeflow-amd:latest
+IMG ?= quay.io/opendatahub/odh-kubeflow-amd:$(shell cat releasing/VERSION)
 NOTEBOOK_IMG ?= quay.io/opendatahub/workbench-rocm-pytorch:latest
 GPU_ARCH ?= gfx950
 
-.PHONY: build test test-matrix test-native test-gpu e2e e2e-test conformance-run conformance-report conformance-clean coverage bench bench-8 manifests deploy deploy-sharded undeploy lint license-check docker-build docker-build-notebook
+.PHONY: build test test-matrix test-native test-gpu e2e e2e-test conformance-run conformance-report conformance-clean coverage bench bench-8 manifests deploy deploy-sharded undeploy lint license-check docker-build docker-push docker-build-notebook
 
 build:  ## hipcc --offload-arch=$(GPU_ARCH) kernels, host C++ telemetry/objcore, native apiserver (in-tree)
 	ODH_GPU_ARCH=$(GPU_ARCH) $(PYTHON) -m odh_kubeflow_amd.ops.build
@@ -76,6 +76,9 @@ license-check:  ## runtime dependencies carry permissive licences (kf/third_part
 
 docker-build: build  ## controller / node-agent image (ROCm base; kernels built for $(GPU_ARCH))
 	docker build -f images/Dockerfile --build-arg GPU_ARCH=$(GPU_ARCH) -t $(IMG) .
+
+docker-push:  ## push the controller / node-agent image
+	docker push $(IMG)
 
 docker-build-notebook:  ## PyTorch-ROCm Jupyter workbench image the samples reference
 	docker build -f images/notebook.Dockerfile -t $(NOTEBOOK_IMG) images

@@ -71,3 +71,34 @@ def test_secret_patterns_fire(tmp_path):
     f = tmp_path / "leak.txt"
     f.write_text("-----BEGIN RSA PRIVATE" + " KEY-----\nAKIA" + "ABCDEFGHIJKLMNOP\n")
     assert {x["rule"] for x in lint.check_secrets([str(f)])} == {"generic-private-key", "generic-aws-access-key"}
+
+
+def test_ci_workflows_reference_existing_targets_and_paths():
+    """The CI definitions (.github/workflows) parse and only call make targets, tools and
+    paths that exist in the tree."""
+    import re
+
+    import yaml
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    wf_dir = os.path.join(root, ".github", "workflows")
+    with open(os.path.join(root, "Makefile")) as f:
+        targets = set(re.findall(r"^([a-z0-9][a-z0-9-]*):", f.read(), re.M))
+    names = sorted(os.listdir(wf_dir))
+    assert {"unit_test.yaml", "code_quality.yaml", "integration_test.yaml", "gpu_test.yaml", "release.yaml"} <= set(names)
+    for n in names:
+        with open(os.path.join(wf_dir, n)) as f:
+            wf = yaml.safe_load(f)
+        assert wf.get("jobs"), n
+        for job in wf["jobs"].values():
+            for step in job["steps"]:
+                run = step.get("run") or ""
+                for t in re.findall(r"\bmake ((?:[a-z0-9-]+ ?)+)", run):
+                    for tgt in t.split():
+                        if "=" not in tgt:
+                            assert tgt in targets, (n, tgt)
+                for path in re.findall(r"\b((?:tools|config|e2e|releasing|\.github)/[\w./-]+)", run):
+                    assert os.path.exists(os.path.join(root, path.rstrip("/"))), (n, path)
+                cfg = (step.get("with") or {}).get("config")
+                if cfg:
+                    assert os.path.exists(os.path.join(root, cfg)), (n, cfg)

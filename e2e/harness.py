@@ -329,8 +329,15 @@ class LocalHarness(Harness):
         if not ep:
             return None
         url = f"http://{ep}/notebook/{m.namespace(nb)}/{m.name(nb)}/api/kernels"
-        with urllib.request.urlopen(url, timeout=10) as r:
-            return r.status
+        deadline = time.monotonic() + self.timeout
+        while True:  # the server may still be binding its port when the pod turns Ready
+            try:
+                with urllib.request.urlopen(url, timeout=10) as r:
+                    return r.status
+            except OSError:
+                if time.monotonic() > deadline:
+                    raise
+                time.sleep(self.interval)
 
     def close(self) -> None:
         try:

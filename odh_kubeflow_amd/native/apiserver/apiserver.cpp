@@ -196,7 +196,8 @@ Value& mdm(Value& o) {
 std::string url_decode(const std::string& s) {
   std::string o;
   for (size_t n = 0; n < s.size(); ++n) {
-    if (s[n] == '%' && n + 2 < s.size()) {
+    if (s[n] == '%' && n + 2 < s.size() && std::isxdigit((unsigned char)s[n + 1]) &&
+        std::isxdigit((unsigned char)s[n + 2])) {
       o += (char)std::stoi(s.substr(n + 1, 2), nullptr, 16);
       n += 2;
     } else if (s[n] == '+') {
@@ -365,6 +366,15 @@ std::vector<std::string> ptr_tokens(const std::string& path) {
   return out;
 }
 
+// RFC 6901 array index: "0" or a digit string without a leading zero (no sign, blanks or
+// trailing junk — std::stoul would take "1x", " 1" and "+1", and throw on "x")
+size_t ptr_index(const std::string& t) {
+  bool ok = !t.empty() && t.size() <= 9 && (t == "0" || t[0] != '0');
+  for (char ch : t) ok = ok && ch >= '0' && ch <= '9';
+  if (!ok) throw PatchErr{"bad list index " + t};
+  return (size_t)std::stoul(t);
+}
+
 Value* ptr_get(Value& doc, const std::vector<std::string>& toks, size_t upto) {
   Value* cur = &doc;
   for (size_t n = 0; n < upto; ++n) {
@@ -373,12 +383,7 @@ Value* ptr_get(Value& doc, const std::vector<std::string>& toks, size_t upto) {
       cur = cur->get(t);
       if (!cur) throw PatchErr{"path segment '" + t + "' not found"};
     } else if (cur->is_arr()) {
-      size_t idx;
-      try {
-        idx = std::stoul(t);
-      } catch (...) {
-        throw PatchErr{"bad list index " + t};
-      }
+      size_t idx = ptr_index(t);
       if (idx >= cur->arr.size()) throw PatchErr{"bad list index " + t};
       cur = &cur->arr[idx];
     } else {
@@ -401,7 +406,7 @@ void ptr_add(Value& doc, const std::vector<std::string>& toks, Value v) {
     if (last == "-") {
       parent->arr.push_back(std::move(v));
     } else {
-      size_t idx = std::stoul(last);
+      size_t idx = ptr_index(last);
       if (idx > parent->arr.size()) throw PatchErr{"list index out of range"};
       parent->arr.insert(parent->arr.begin() + idx, std::move(v));
     }
@@ -422,7 +427,7 @@ Value ptr_remove(Value& doc, const std::vector<std::string>& toks) {
     return out;
   }
   if (parent->is_arr()) {
-    size_t idx = std::stoul(last);
+    size_t idx = ptr_index(last);
     if (idx >= parent->arr.size()) throw PatchErr{"remove: bad index"};
     Value out = std::move(parent->arr[idx]);
     parent->arr.erase(parent->arr.begin() + idx);
@@ -2288,7 +2293,12 @@ bool read_request(Conn& c, Request& rq) {
     if (colon == std::string::npos) continue;
     std::string k = line.substr(0, colon), v = trim(line.substr(colon + 1));
     std::transform(k.begin(), k.end(), k.begin(), ::tolower);
-    if (k == "content-length") clen = std::stoul(v);
+    if (k == "content-length") {
+      // digits only: a malformed length ends the connection instead of throwing out of the
+      // connection thread (which would terminate the server)
+      if (v.empty() || v.size() > 12 || v.find_first_not_of("0123456789") != std::string::npos) return false;
+      clen = std::stoul(v);
+    }
     else if (k == "content-type") rq.ctype = v.substr(0, v.find(';'));
     else if (k == "authorization") rq.auth = v;
     else if (k == "user-agent") rq.user_agent = v;
@@ -2308,7 +2318,10 @@ bool read_request(Conn& c, Request& rq) {
         if (n <= 0) return false;
         c.buf.append(tmp, n);
       }
-      size_t sz = std::stoul(c.buf.substr(0, le), nullptr, 16);
+      std::string hex = c.buf.substr(0, c.buf.find_first_of(";\r"));
+      if (hex.empty() || hex.size() > 12 || hex.find_first_not_of("0123456789abcdefABCDEF") != std::string::npos)
+        return false;
+      size_t sz = std::stoul(hex, nullptr, 16);
       c.buf.erase(0, le + 2);
       while (c.buf.size() < sz + 2) {
         ssize_t n = recv(c.fd, tmp, sizeof(tmp), 0);
@@ -2494,6 +2507,10 @@ std::string event_line(const Res& r, const Ev& e, const std::string& version) {
 
 void serve_watch(int fd, Res& r, const Path& p, const Request& rq) {
   std::string rv = rq.q.count("resourceVersion") ? rq.q.at("resourceVersion") : "";
+  if (!rv.empty() && (rv.size() > 18 || rv.find_first_not_of("0123456789") != std::string::npos)) {
+    respond(fd, 400, kj::dump(status_obj(BadRequest("invalid resourceVersion " + rv))), false);
+    return;
+  }
   double timeout = rq.q.count("timeoutSeconds") ? std::atof(rq.q.at("timeoutSeconds").c_str()) : 1800.0;
   bool bookmarks = rq.q.count("allowWatchBookmarks") && (rq.q.at("allowWatchBookmarks") == "true" || rq.q.at("allowWatchBookmarks") == "1");
   auto lr = parse_labels(rq.q.count("labelSelector") ? rq.q.at("labelSelector") : "");
@@ -2647,6 +2664,31 @@ bool handle(int fd, Request& rq) {
   if (rq.method == "GET" && (rq.path == "/healthz" || rq.path == "/readyz" || rq.path == "/livez")) {
     std::string h = "HTTP/1.1 200 OK\r\nContent-Type: text/plain\r\nContent-Length: 2\r\n\r\nok";
     return write_all(fd, h.data(), h.size());
+  }
+  if (rq.method == "POST" && rq.path == "/debug/patch") {
+    // the patch engines on their own (tests/test_patch_parity.py: property tests against
+    // utils/jsonpatch.py): {"type": json|merge|strategic, "doc": …, "patch": …}
+    try {
+      Value in = kj::parse(rq.body);
+      std::string pt = in.str_or("type");
+      const Value* doc = in.get("doc");
+      const Value* patch = in.get("patch");
+      if (!doc || !patch) throw PatchErr{"doc and patch required"};
+      Value out = Value::object();
+      if (pt == "json") out["result"] = apply_json_patch(*doc, *patch);
+      else if (pt == "merge") out["result"] = merge_patch(*doc, *patch);
+      else if (pt == "strategic") out["result"] = strategic_patch(*doc, *patch);
+      else throw PatchErr{"unknown patch type " + pt};
+      return respond(fd, 200, kj::dump(out), rq.keep_alive);
+    } catch (const PatchErr& e) {
+      Value out = Value::object();
+      out["error"] = Value::str(e.msg);
+      return respond(fd, 422, kj::dump(out), rq.keep_alive);
+    } catch (const kj::ParseError&) {
+      return respond(fd, 400, "{\"error\":\"bad json\"}", rq.keep_alive);
+    } catch (const std::exception& e) {
+      return respond(fd, 500, kj::dump(status_obj(Internal(e.what()))), rq.keep_alive);
+    }
   }
   if (rq.method == "GET" && rq.path == "/version") {
     return respond(fd, 200, "{\"major\":\"1\",\"minor\":\"32\",\"gitVersion\":\"v1.32.8-odh-kubeflow-amd-native\"}",

@@ -86,6 +86,14 @@ def _diff(a: Any, b: Any, path: str, ops: List[dict]) -> None:
 # --------------------------------------------------------------------------- apply
 
 
+def _index(t: str) -> int:
+    """RFC 6901 array index: ``0`` or digits without a leading zero — ``int()`` would also
+    take ``-1`` (Python's from-the-end indexing), ``+1``, `` 1`` and ``1_0``."""
+    if not (t.isascii() and t.isdigit()) or (len(t) > 1 and t[0] == "0") or len(t) > 9:
+        raise PatchError(f"bad list index {t!r}")
+    return int(t)
+
+
 def _resolve_parent(doc: Any, tokens: List[str]):
     cur = doc
     for t in tokens[:-1]:
@@ -94,10 +102,10 @@ def _resolve_parent(doc: Any, tokens: List[str]):
                 raise PatchError(f"path segment {t!r} not found")
             cur = cur[t]
         elif isinstance(cur, list):
-            try:
-                cur = cur[int(t)]
-            except (ValueError, IndexError) as e:
-                raise PatchError(f"bad list index {t!r}") from e
+            i = _index(t)
+            if i >= len(cur):
+                raise PatchError(f"bad list index {t!r}")
+            cur = cur[i]
         else:
             raise PatchError(f"cannot traverse into scalar at {t!r}")
     return cur
@@ -111,10 +119,10 @@ def _get(doc: Any, tokens: List[str]) -> Any:
                 raise PatchError(f"path segment {t!r} not found")
             cur = cur[t]
         elif isinstance(cur, list):
-            try:
-                cur = cur[int(t)]
-            except (ValueError, IndexError) as e:
-                raise PatchError(f"bad list index {t!r}") from e
+            i = _index(t)
+            if i >= len(cur):
+                raise PatchError(f"bad list index {t!r}")
+            cur = cur[i]
         else:
             raise PatchError("cannot traverse into scalar")
     return cur
@@ -131,11 +139,8 @@ def _add(doc: Any, tokens: List[str], value: Any) -> Any:
         if last == "-":
             parent.append(value)
         else:
-            try:
-                idx = int(last)
-            except ValueError as e:
-                raise PatchError(f"bad list index {last!r}") from e
-            if idx < 0 or idx > len(parent):
+            idx = _index(last)
+            if idx > len(parent):
                 raise PatchError(f"list index {idx} out of range")
             parent.insert(idx, value)
     else:
@@ -153,11 +158,25 @@ def _remove(doc: Any, tokens: List[str]) -> Any:
             raise PatchError(f"remove: {last!r} not found")
         return parent.pop(last)
     if isinstance(parent, list):
-        try:
-            return parent.pop(int(last))
-        except (ValueError, IndexError) as e:
-            raise PatchError(f"remove: bad index {last!r}") from e
+        i = _index(last)
+        if i >= len(parent):
+            raise PatchError(f"remove: bad index {last!r}")
+        return parent.pop(i)
     raise PatchError("cannot remove from scalar")
+
+
+def json_equal(a: Any, b: Any) -> bool:
+    """RFC 6902 ``test`` equality: numbers by value, booleans only equal booleans (Python's
+    ``True == 1`` is not JSON's), objects regardless of member order."""
+    if isinstance(a, bool) or isinstance(b, bool):
+        return isinstance(a, bool) and isinstance(b, bool) and a == b
+    if isinstance(a, (int, float)) and isinstance(b, (int, float)):
+        return a == b
+    if isinstance(a, dict) and isinstance(b, dict):
+        return a.keys() == b.keys() and all(json_equal(v, b[k]) for k, v in a.items())
+    if isinstance(a, list) and isinstance(b, list):
+        return len(a) == len(b) and all(json_equal(x, y) for x, y in zip(a, b))
+    return type(a) is type(b) and a == b
 
 
 def apply_patch(doc: Any, ops: List[dict], in_place: bool = False) -> Any:
@@ -183,14 +202,14 @@ def apply_patch(doc: Any, ops: List[dict], in_place: bool = False) -> Any:
             else:
                 parent[last] = deepcopy_json(op.get("value"))
         elif kind == "move":
-            frm = _split(op["from"])
+            frm = _split(op.get("from", ""))
             val = _remove(doc, frm)
             doc = _add(doc, tokens, val)
         elif kind == "copy":
-            val = deepcopy_json(_get(doc, _split(op["from"])))
+            val = deepcopy_json(_get(doc, _split(op.get("from", ""))))
             doc = _add(doc, tokens, val)
         elif kind == "test":
-            if _get(doc, tokens) != op.get("value"):
+            if not json_equal(_get(doc, tokens), op.get("value")):
                 raise PatchError(f"test failed at {op.get('path')}")
         else:
             raise PatchError(f"unknown op {kind!r}")

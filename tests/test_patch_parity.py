@@ -176,3 +176,80 @@ def test_native_server_survives_malformed_requests(server):
     server.request("GET", "/healthz")
     r = server.getresponse()
     assert r.status == 200 and r.read() == b"ok"
+
+
+# ------------------------------------------------------------------ selectors
+
+LKEYS = ["app", "tier", "gpu", "example.com/role"]
+LVALS = ["a", "b", "c", ""]
+
+
+@pytest.fixture(scope="module")
+def labelled_pool(server):
+    """30 ConfigMaps with pseudo-random labels in the native server; the same list for the
+    Python matcher."""
+    import random
+
+    rnd = random.Random(7)
+    pool = []
+    for i in range(30):
+        labels = {k: rnd.choice(LVALS) for k in LKEYS if rnd.random() < 0.6}
+        cm = {"apiVersion": "v1", "kind": "ConfigMap",
+              "metadata": {"name": f"sel-{i}", "namespace": "sel", "labels": labels}, "data": {"i": str(i % 3)}}
+        server.request("POST", "/api/v1/namespaces/sel/configmaps", json.dumps(cm), {"Content-Type": "application/json"})
+        r = server.getresponse()
+        r.read()
+        assert r.status == 201, r.status
+        pool.append(cm)
+    return pool
+
+
+@st.composite
+def label_selector(draw):
+    reqs = []
+    for _ in range(draw(st.integers(1, 3))):
+        k = draw(st.sampled_from(LKEYS))
+        op = draw(st.sampled_from(["=", "==", "!=", "in", "notin", "exists", "!"]))
+        if op in ("in", "notin"):
+            vals = draw(st.lists(st.sampled_from(["a", "b", "c"]), min_size=1, max_size=3))
+            reqs.append(f"{k} {op} ({','.join(vals)})")
+        elif op == "exists":
+            reqs.append(k)
+        elif op == "!":
+            reqs.append(f"!{k}")
+        else:
+            reqs.append(f"{k}{op}{draw(st.sampled_from(['a', 'b', 'c']))}")
+    return ",".join(reqs)
+
+
+def _native_names(server, query):
+    from urllib.parse import quote
+
+    server.request("GET", f"/api/v1/namespaces/sel/configmaps?{query[0]}={quote(query[1])}")
+    r = server.getresponse()
+    body = json.loads(r.read())
+    assert r.status == 200, body
+    return sorted(o["metadata"]["name"] for o in body["items"])
+
+
+@settings(max_examples=300, deadline=None, suppress_health_check=[HealthCheck.function_scoped_fixture])
+@given(label_selector())
+def test_label_selector_parity(server, labelled_pool, sel):
+    from odh_kubeflow_amd.utils.selectors import match_labels, parse_label_selector
+
+    reqs = parse_label_selector(sel)
+    want = sorted(cm["metadata"]["name"] for cm in labelled_pool if match_labels(reqs, cm["metadata"]["labels"]))
+    assert _native_names(server, ("labelSelector", sel)) == want, sel
+
+
+@settings(max_examples=100, deadline=None, suppress_health_check=[HealthCheck.function_scoped_fixture])
+@given(st.lists(st.tuples(st.sampled_from(["metadata.name", "data.i", "metadata.namespace"]),
+                          st.sampled_from(["=", "==", "!="]),
+                          st.sampled_from(["sel-1", "sel-2", "0", "1", "sel", "x"])), min_size=1, max_size=2))
+def test_field_selector_parity(server, labelled_pool, reqs):
+    from odh_kubeflow_amd.utils.selectors import field_matcher, parse_field_selector
+
+    sel = ",".join(f"{k}{op}{v}" for k, op, v in reqs)
+    match = field_matcher(parse_field_selector(sel))
+    want = sorted(cm["metadata"]["name"] for cm in labelled_pool if match(cm))
+    assert _native_names(server, ("fieldSelector", sel)) == want, sel

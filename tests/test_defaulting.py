@@ -153,3 +153,89 @@ def test_no_statefulset_or_service_writes_in_steady_state(run, transport):
                 "containers"][0]["image"] == "rocm/pytorch:rocm7.0", 10)
             assert [w for w in writes if w[1] == "StatefulSet"] == [("update", "StatefulSet", None)]
     run(go(), timeout=90)
+
+
+def _random_pod_spec(rnd, name):
+    """A notebook pod spec in the shapes users write: non-canonical quantities, partial
+    probes / ports / env sources / volumes — everything the apiserver defaults or
+    canonicalises."""
+    q_cpu = ["0.5", "500m", "1", "2000m", "1.5", "100m"]
+    q_mem = ["1Gi", "1024Mi", "65536Mi", "512M", "2G", "1e9"]
+    c = {"name": name, "image": rnd.choice(["rocm/pytorch:latest", "quay.io/x/y:1", "img"])}
+    res = {"limits": {"amd.com/gpu": "1"}}  # 8 notebooks fill the node's 8 GPUs
+    if rnd.random() < 0.7:
+        res["limits"]["cpu"] = rnd.choice(q_cpu)
+        res["limits"]["memory"] = rnd.choice(q_mem)
+    if rnd.random() < 0.5:
+        res["requests"] = {"cpu": rnd.choice(q_cpu), "memory": rnd.choice(q_mem)}
+    c["resources"] = res
+    if rnd.random() < 0.6:
+        c["ports"] = [dict({"containerPort": 8888, "name": "notebook-port"},
+                           **({"protocol": "TCP"} if rnd.random() < 0.5 else {}))]
+    probe = rnd.choice([None, {"httpGet": {"port": 8888, "path": "/api"}}, {"tcpSocket": {"port": 8888}},
+                        {"exec": {"command": ["true"]}, "periodSeconds": 5}])
+    if probe:
+        c[rnd.choice(["readinessProbe", "livenessProbe"])] = probe
+    env = []
+    if rnd.random() < 0.5:
+        env.append({"name": "POD", "valueFrom": {"fieldRef": {"fieldPath": "metadata.name"}}})
+    if rnd.random() < 0.5:
+        env.append({"name": "A", "value": "1"})
+    if env:
+        c["env"] = env
+    spec = {"containers": [c]}
+    vols = []
+    if rnd.random() < 0.5:
+        vols.append({"name": "shm", "emptyDir": {"medium": "Memory", "sizeLimit": rnd.choice(["16Gi", "16384Mi"])}})
+        c["volumeMounts"] = [{"name": "shm", "mountPath": "/dev/shm"}]
+    if rnd.random() < 0.4:
+        vols.append({"name": "cfg", "configMap": {"name": "cfg"}})
+    if vols:
+        spec["volumes"] = vols
+    if rnd.random() < 0.3:
+        spec["tolerations"] = [{"key": "amd.com/gpu", "operator": "Exists", "effect": "NoSchedule"}]
+    if rnd.random() < 0.3:
+        spec["securityContext"] = {"runAsUser": 1000}
+    if rnd.random() < 0.3:
+        spec["initContainers"] = [{"name": "init", "image": "busybox", "command": ["true"]}]
+    return spec
+
+
+@pytest.mark.parametrize("transport", ["inprocess", "native"])
+def test_no_writes_in_steady_state_for_random_pod_specs(run, transport):
+    """The write-storm guard over 8 randomly shaped notebooks (seeded): once each is Ready,
+    3 more reconciles write nothing to its StatefulSet or Service."""
+    import random
+
+    rnd = random.Random(20261016)
+
+    async def go():
+        async with LocalCluster(ClusterConfig(transport=transport)) as cl:
+            await cl.ensure_namespace("fz")
+            names = [f"fz{i}" for i in range(8)]
+            for n in names:
+                nb = notebook(n, "fz", gpus=1)
+                nb["spec"]["template"]["spec"] = _random_pod_spec(rnd, n)
+                await cl.admin.create(nb)
+            assert await cl.wait_for(lambda: all(cl.notebook_ready(n, "fz") for n in names), 60)
+            assert await cl.settle(10)
+            writes = []
+            client = cl.kf.client
+            orig_update, orig_patch = client.update, client.patch
+
+            async def update(obj, *a, **kw):
+                writes.append(("update", obj.get("kind"), (obj.get("metadata") or {}).get("name")))
+                return await orig_update(obj, *a, **kw)
+
+            async def patch(obj, *a, **kw):
+                writes.append(("patch", obj if isinstance(obj, str) else obj.get("kind"), kw.get("name")))
+                return await orig_patch(obj, *a, **kw)
+            client.update, client.patch = update, patch
+            ctl = next(x for x in cl.kf.controllers if x.name == "notebook-controller")
+            for _ in range(3):
+                for n in names:
+                    ctl.queue.add(Request("fz", n))
+                await asyncio.sleep(0)
+                assert await cl.settle(10)
+            assert [w for w in writes if w[1] in ("StatefulSet", "Service")] == [], writes
+    run(go(), timeout=120)

@@ -42,8 +42,8 @@ MODEL = "kubeflow.org/v1 Notebook (amd.com/gpu=1, PyTorch-ROCm image) on 8xMI355
 def parse(argv=None):
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=int(os.environ.get("WORLD_SIZE", "1")))
-    p.add_argument("--steps", type=int, default=100)
-    p.add_argument("--warmup", type=int, default=5)
+    p.add_argument("--steps", type=int, default=300)
+    p.add_argument("--warmup", type=int, default=10)
     p.add_argument("--no-gpu-probe", action="store_true", help="skip the MI355X start-up probe (CPU dev runs)")
     p.add_argument("--no-odh", action="store_true", help="kf controller only (no webhook / odh reconciler)")
     p.add_argument("--reference-emulation", action="store_true",

@@ -384,6 +384,11 @@ class GpuRuntime:
         if not self._mine(pod):
             return Result()
         if h is not None:
+            if not h.info.get("reported"):
+                # started, but the Ready status write failed (connection dropped): report it
+                # now instead of leaving the pod Pending behind a running container
+                await self._set_status(pod, ready=True, handle=h, probe=h.info.get("probe"))
+                h.info["reported"] = True
             return Result()
         ids = m.annotations(pod).get(GPU_IDS_ANNOTATION) or ""
         devices = [int(x) for x in ids.split(",") if x != ""]
@@ -404,6 +409,7 @@ class GpuRuntime:
         self.handles[key] = h
         self.started += 1
         await self._set_status(pod, ready=True, handle=h, probe=probe)
+        h.info["reported"] = True
         self.recorder.event(pod, "Normal", "Started", "Started container " + ",".join(
             c.get("name", "") for c in (pod.get("spec") or {}).get("containers") or []))
         return Result()

@@ -112,7 +112,7 @@ class Http1Pool:
                 conn.close()
                 if reused and attempt == 0 and method != "POST":
                     continue
-                raise HttpError(f"{method} {target}: {e!r}")
+                raise HttpError(f"{method} {target}: {e!r}") from e
             except BaseException:
                 conn.close()
                 raise

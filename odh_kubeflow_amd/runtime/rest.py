@@ -154,6 +154,8 @@ def _info_and_version(ref) -> Tuple[ResourceInfo, str]:
 
 
 class RestClient(Client):
+    GET_RETRIES = 10
+
     def __init__(self, config: RestConfig, pool: int = 64):
         self.config = config
         self.base = config.host.rstrip("/")
@@ -162,6 +164,7 @@ class RestClient(Client):
         self._pool = pool
         self._bucket = TokenBucket(config.qps, config.burst)
         self.requests = 0
+        self.retries = 0  # GETs retried after a connection reset / EOF
         self.user = config.user_agent
         self._discovery: dict = {}  # "group/version" -> (fetched_at, set(plurals))
 
@@ -196,10 +199,21 @@ class RestClient(Client):
         target = url[len(self.base):] if url.startswith(self.base) else url
         if params:
             target += ("&" if "?" in target else "?") + urlencode(params)
-        try:
-            status, raw = await self._http().request(method, target, data, content_type if data is not None else None)
-        except HttpError as e:
-            raise InternalError(str(e))
+        for attempt in range(self.GET_RETRIES + 1):
+            try:
+                status, raw = await self._http().request(method, target, data,
+                                                         content_type if data is not None else None)
+                break
+            except HttpError as e:
+                # client-go retries a GET whose connection was reset or hit EOF mid-response
+                # (rest/request.go: IsConnectionReset || IsProbableEOF, up to maxRetries=10);
+                # writes are not retried here — the reconcile's own requeue does that
+                if method != "GET" or attempt == self.GET_RETRIES or not isinstance(
+                        e.__cause__, (asyncio.IncompleteReadError, ConnectionResetError, BrokenPipeError,
+                                      ConnectionAbortedError)):
+                    raise InternalError(str(e))
+                self.retries += 1
+                await asyncio.sleep(min(0.5, 0.01 * (2 ** attempt)))
         try:
             out = json.loads(raw) if raw else {}
         except ValueError:
@@ -214,7 +228,11 @@ class RestClient(Client):
             raise err
         return out
 
-    async def _served(self, group: str, version: str) -> set:
+    async def _served(self, group: str, version: str) -> Optional[set]:
+        """Plurals the server serves for ``group/version`` — ``None`` when discovery itself
+        failed (connection dropped, 5xx): unknown is neither cached nor taken as "not
+        served", or one dropped connection would turn every 404 into NoKindMatch for the
+        cache lifetime."""
         key = f"{group}/{version}"
         hit = self._discovery.get(key)
         if hit is not None and time.monotonic() - hit[0] < 30.0:
@@ -222,9 +240,14 @@ class RestClient(Client):
         path = f"/apis/{group}/{version}" if group else f"/api/{version}"
         try:
             status, raw = await self._http().request("GET", path)
-            doc = json.loads(raw) if status == 200 and raw else {}
-        except Exception:
-            doc = {}
+            if status == 404:
+                doc = {}
+            elif status == 200:
+                doc = json.loads(raw) if raw else {}
+            else:
+                return None
+        except Exception:  # noqa: BLE001 — discovery is best effort; the 404 stands
+            return None
         plurals = {r.get("name") for r in (doc or {}).get("resources") or []}
         self._discovery[key] = (time.monotonic(), plurals)
         return plurals
@@ -238,7 +261,8 @@ class RestClient(Client):
         pp = parse_path(url[len(self.base):].split("?", 1)[0])
         if pp is None:
             return
-        if pp.info.plural not in await self._served(pp.info.group, pp.version):
+        served = await self._served(pp.info.group, pp.version)
+        if served is not None and pp.info.plural not in served:
             raise NoKindMatch(pp.info.kind)
 
     # -------------------------------------------------------------- Client interface

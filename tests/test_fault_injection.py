@@ -1,0 +1,198 @@
+"""Fault injection: the managers talk to the apiserver through a proxy that cuts every
+open connection (watch streams, pooled request connections) at random moments.
+
+The reference has no fault injection; controller-runtime's informers survive
+dropped watches by re-watching from the last resourceVersion (relisting on 410 Gone) and
+its clients retry.  Here the kf and odh managers (separate processes, HTTPS webhook) and the
+dev kubelet run against a proxy that resets all their connections every 50–150 ms while
+notebooks are created, become Ready, and are deleted: every notebook must still converge
+both ways, with its dependents cleaned up."""
+
+import asyncio
+import os
+import random
+import time
+
+import pytest
+
+from odh_kubeflow_amd.models import kinds
+from odh_kubeflow_amd.models.notebook import notebook
+from odh_kubeflow_amd.runtime.rest import RestClient, RestConfig
+
+from test_processes_e2e import eventually, free_port, spawn, wait_http
+
+pytestmark = pytest.mark.slow
+
+
+class ChaosProxy:
+    """TCP proxy that can drop every connection it carries."""
+
+    def __init__(self, target_port: int):
+        self.target_port = target_port
+        self.pairs = set()
+        self.cuts = 0
+        self.aborted = 0  # connections cut while in use (watches, pooled requests)
+        self.server = None
+        self.port = None
+
+    async def _pipe(self, r, w):
+        try:
+            while True:
+                data = await r.read(65536)
+                if not data:
+                    break
+                w.write(data)
+                await w.drain()
+        except (ConnectionError, asyncio.CancelledError):
+            pass
+        finally:
+            w.close()
+
+    async def _handle(self, cr, cw):
+        try:
+            sr, sw = await asyncio.open_connection("127.0.0.1", self.target_port)
+        except OSError:
+            cw.close()
+            return
+        pair = (cw, sw)
+        self.pairs.add(pair)
+        try:
+            await asyncio.gather(self._pipe(cr, sw), self._pipe(sr, cw))
+        finally:
+            self.pairs.discard(pair)
+
+    async def start(self):
+        self.server = await asyncio.start_server(self._handle, "127.0.0.1", 0)
+        self.port = self.server.sockets[0].getsockname()[1]
+        return self
+
+    def cut_all(self):
+        for cw, sw in list(self.pairs):
+            self.aborted += 1
+            for w in (cw, sw):
+                try:
+                    w.transport.abort()
+                except Exception:  # noqa: BLE001 — already closed
+                    pass
+        self.cuts += 1
+
+    async def close(self):
+        self.cut_all()
+        self.server.close()
+        await self.server.wait_closed()
+
+
+async def diagnostics(c, names) -> str:
+    """What each notebook's chain looks like (the reference e2e's logNotebookDiagnostics)."""
+    out = []
+    for n in names:
+        row = [n]
+        try:
+            nb = await c.get(kinds.NOTEBOOK, n, "chaos")
+            row.append(f"ann={sorted((nb['metadata'].get('annotations') or {}).items())}")
+            row.append(f"fin={nb['metadata'].get('finalizers')} status={nb.get('status')}")
+        except Exception as e:  # noqa: BLE001
+            row.append(f"notebook: {e!r}")
+        for kind, name in ((kinds.STATEFUL_SET, n), (kinds.POD, f"{n}-0")):
+            try:
+                o = await c.get(kind, name, "chaos")
+                row.append(f"{kind.split('/')[-1]}: spec.replicas={(o.get('spec') or {}).get('replicas')} "
+                           f"node={(o.get('spec') or {}).get('nodeName')} status={o.get('status')}")
+            except Exception as e:  # noqa: BLE001
+                row.append(f"{kind.split('/')[-1]}: {e!r}")
+        out.append(" | ".join(row))
+    return "\n".join(out)
+
+
+def test_managers_converge_through_connection_resets(tmp_path, run):
+    from odh_kubeflow_amd.webhook.certs import generate
+    from odh_kubeflow_amd.webhook.server import mutating_webhook_configuration
+
+    api_port, wh_port = free_port(), free_port()
+    certs = generate(("127.0.0.1", "localhost"), str(tmp_path / "certs"))
+    logf = open(tmp_path / "procs.log", "wb")
+    master = f"http://127.0.0.1:{api_port}"
+    procs = [spawn(["odh_kubeflow_amd.cmd.apiserver", "--port", str(api_port), "--controllers",
+                    "--no-openshift-apis"], log=logf)]
+    rnd = random.Random(11)
+
+    async def go():
+        await wait_http(master + "/healthz")
+        proxy = await ChaosProxy(api_port).start()
+        via = f"http://127.0.0.1:{proxy.port}"
+        c = RestClient(RestConfig(host=master))
+        for ns in ("opendatahub", "chaos"):
+            await c.create({"apiVersion": "v1", "kind": "Namespace", "metadata": {"name": ns}})
+        common = {"K8S_NAMESPACE": "opendatahub", "SET_PIPELINE_RBAC": "false"}
+        procs.append(spawn(["odh_kubeflow_amd.cmd.kf_manager", "--master", via, "--metrics-addr", "0",
+                            "--probe-addr", "0"], common, logf))
+        procs.append(spawn(["odh_kubeflow_amd.cmd.odh_manager", "--master", via, "--metrics-bind-address", "0",
+                            "--health-probe-bind-address", "0", "--kube-rbac-proxy-image",
+                            "quay.io/brancz/kube-rbac-proxy:v0.18.1", "--webhook-cert-dir", certs.cert_dir,
+                            "--webhook-port", str(wh_port), "--webhook-host", "127.0.0.1"], common, logf))
+        procs.append(spawn(["odh_kubeflow_amd.cmd.fake_kubelet", "--master", via, "--checkpoint-path",
+                            str(tmp_path / "dp" / "cp")], common, logf))
+        await wait_http(f"https://127.0.0.1:{wh_port}/healthz")
+        await c.create(mutating_webhook_configuration(
+            certs.ca_bundle_b64, url=f"https://127.0.0.1:{wh_port}/mutate-notebook-v1"))
+        await eventually(lambda: c.get(kinds.NODE, "mi355x-node-0"))
+
+        stop = asyncio.Event()
+
+        async def chaos():
+            while not stop.is_set():
+                await asyncio.sleep(rnd.uniform(0.05, 0.15))
+                proxy.cut_all()
+        chaos_task = asyncio.create_task(chaos())
+        names = [f"nb{i}" for i in range(5)]
+        try:
+            for n in names:
+                await c.create(notebook(n, "chaos", gpus=1,
+                                        annotations={"notebooks.opendatahub.io/inject-auth": "true"}))
+
+            async def all_ready():
+                for n in names:
+                    st = (await c.get(kinds.NOTEBOOK, n, "chaos")).get("status") or {}
+                    if st.get("readyReplicas") != 1:
+                        return False
+                return True
+            try:
+                await eventually(all_ready, 90)
+            except AssertionError:
+                raise AssertionError("not all Ready:\n" + await diagnostics(c, names))
+            for n in names:
+                await c.delete(kinds.NOTEBOOK, n, "chaos")
+
+            async def all_gone():
+                left = [n for n in names if any(x["metadata"]["name"] == n
+                                                for x in await c.list(kinds.NOTEBOOK, "chaos"))]
+                crbs = [x["metadata"]["name"] for x in await c.list(kinds.CLUSTER_ROLE_BINDING)
+                        if x["metadata"]["name"].endswith("-chaos-auth-delegator")]
+                routes = await c.list(kinds.HTTP_ROUTE, "opendatahub")
+                return not left and not crbs and not routes
+            await eventually(all_gone, 90)
+        finally:
+            stop.set()
+            await chaos_task
+            await proxy.close()
+            await c.close()
+        return proxy.aborted
+
+    try:
+        t0 = time.monotonic()
+        aborted = run(go(), timeout=240)
+        # the faults hit live connections (every manager's watches at each cut) while the
+        # notebooks converged
+        assert aborted >= 10, aborted
+        assert time.monotonic() - t0 < 230
+    finally:
+        for p in procs:
+            p.terminate()
+        for p in procs:
+            try:
+                p.wait(10)
+            except Exception:  # noqa: BLE001
+                p.kill()
+        logf.close()
+        if os.environ.get("ODH_KEEP_LOGS"):
+            print(open(tmp_path / "procs.log", "rb").read().decode(errors="replace")[-5000:])

@@ -238,3 +238,34 @@ def test_full_stack_over_http_with_https_webhook(run, transport):
             assert await cl.wait_for(lambda: cl.store.peek(kinds.STATEFUL_SET, "nb", "user") is None, 10)  # GC
             assert cl.store.peek(kinds.CLUSTER_ROLE_BINDING, "nb-rbac-user-auth-delegator") is None
     run(go(), timeout=60)
+
+
+def test_discovery_failure_is_not_cached_as_not_served(run):
+    """A dropped discovery request must leave a 404 a NotFound (and not be cached), not
+    turn every 404 of that group/version into NoKindMatch for the cache lifetime."""
+    from odh_kubeflow_amd.models.errors import ApiError, NoKindMatch
+    from odh_kubeflow_amd.runtime.rest import RestClient, RestConfig
+
+    async def go():
+        async with LocalCluster(ClusterConfig(transport="http")) as cl:
+            rc = RestClient(RestConfig(host=cl.rest_config.host))
+            pool = rc._http()
+            orig = pool.request
+            calls = {"n": 0}
+
+            async def flaky(method, target, *a, **kw):
+                if target.startswith("/api/v1") and target.rstrip("/") == "/api/v1":
+                    calls["n"] += 1
+                    if calls["n"] == 1:
+                        raise ConnectionResetError("dropped")
+                return await orig(method, target, *a, **kw)
+            pool.request = flaky
+            with pytest.raises(ApiError) as e:
+                await rc.get(kinds.CONFIG_MAP, "missing", "default")
+            assert not isinstance(e.value, NoKindMatch) and e.value.code == 404
+            assert "/v1" not in rc._discovery and "" not in {k.split("/")[0] for k in rc._discovery}
+            with pytest.raises(ApiError) as e:  # discovery works now: still a plain NotFound
+                await rc.get(kinds.CONFIG_MAP, "missing", "default")
+            assert not isinstance(e.value, NoKindMatch)
+            await rc.close()
+    run(go())

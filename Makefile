@@ -59,14 +59,15 @@ bench-8: build  ## one control-plane shard per MI355X of an 8-GPU node
 manifests:  ## regenerate the kustomize tree under config/
 	$(PYTHON) -m odh_kubeflow_amd.deploy.manifests --out config
 
-deploy: manifests  ## kubectl apply the MI355X overlay (CRD, RBAC, managers, webhook, node agent)
-	kubectl apply -k config/overlays/mi355x
+OVERLAY ?= mi355x
+deploy: manifests  ## kubectl apply an overlay (OVERLAY=mi355x|standalone|kubeflow|openshift): CRD, RBAC, managers, webhook, node agent
+	kubectl apply -k config/overlays/$(OVERLAY)
 
 deploy-sharded: manifests  ## kubectl apply the sharded MI355X overlay (one control-plane shard per GPU)
 	kubectl apply -k config/overlays/mi355x-sharded
 
 undeploy:
-	kubectl delete -k config/overlays/mi355x --ignore-not-found
+	kubectl delete -k config/overlays/$(OVERLAY) --ignore-not-found
 
 lint:  ## static analysis: Python AST rules, secrets, rendered manifests, -Wall -Wextra -Werror native builds
 	$(PYTHON) tools/lint.py

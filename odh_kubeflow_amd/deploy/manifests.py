@@ -76,6 +76,8 @@ REPO_ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__fi
 def release_version(root: str = REPO_ROOT) -> str:
     with open(os.path.join(root, "releasing", "VERSION")) as f:
         return f.read().strip()
+
+
 KUBE_RBAC_PROXY_IMAGE = "quay.io/brancz/kube-rbac-proxy:v0.18.1"
 
 

@@ -108,6 +108,7 @@ def measure(args) -> Optional[dict]:
                                                "controller + fake kubelet of the rank's GPU")
         out["rank_ms_per_step"] = res.get("rank_ms_per_step")
         out["cpu_ms_per_step"] = res.get("cpu_ms_per_step")
+        out["child_rss_mib"] = res.get("child_rss_mib")
         if res.get("apiserver_profile_per_step"):
             out["apiserver_profile_per_step"] = res["apiserver_profile_per_step"]
         if rccl_ms is not None:
@@ -127,6 +128,20 @@ def _proc_cpu_s(pid: Optional[int]) -> Optional[float]:
         return (int(fields[11]) + int(fields[12])) / os.sysconf("SC_CLK_TCK")
     except (OSError, IndexError, ValueError):
         return None
+
+
+def _proc_rss_mib(pid: Optional[int]) -> Optional[float]:
+    """Resident set size of a child process (``/proc/<pid>/status`` VmRSS), None if unreadable."""
+    if pid is None:
+        return None
+    try:
+        with open(f"/proc/{pid}/status") as f:
+            for line in f:
+                if line.startswith("VmRSS:"):
+                    return round(int(line.split()[1]) / 1024.0, 1)
+    except (OSError, IndexError, ValueError):
+        return None
+    return None
 
 
 async def _main(args, dist, torch, rank: int, world: int, local_rank: int, probe) -> dict:
@@ -274,10 +289,14 @@ async def _drive(args, shard, dist, torch, children: Optional[dict] = None, nati
     # CPU time per step of every process on the path: where a step's work goes when ranks are added
     cpu = {"rank": time.process_time() - cpu0}
     prof = _prof_per_step(prof0, await _apiserver_prof(native), args.steps)
+    rss = {}
     for k, pid in children.items():
         c1 = _proc_cpu_s(pid)
         if c1 is not None and child_cpu0.get(k) is not None:
             cpu[k] = c1 - child_cpu0[k]
+        r = _proc_rss_mib(pid)
+        if r is not None:
+            rss[k] = r
     if torch.cuda.is_available():
         torch.cuda.synchronize()
     await _in_thread(dist.barrier)
@@ -290,7 +309,7 @@ async def _drive(args, shard, dist, torch, children: Optional[dict] = None, nati
     gathered = [None] * dist.get_world_size()
     await _in_thread(dist.all_gather_object, gathered, {"lat": lat_ms, "probes": shard.probe_results,
                                                         "teardown": teardown_ms, "own_s": own, "cpu": cpu,
-                                                        "breakdown": breakdown})
+                                                        "rss": rss, "breakdown": breakdown})
     per_step = 1e3 / max(1, args.steps)
     cpu_ms = {"ranks": [round(g["cpu"]["rank"] * per_step, 3) for g in gathered]}
     for g in gathered:
@@ -302,4 +321,5 @@ async def _drive(args, shard, dist, torch, children: Optional[dict] = None, nati
             "probes": [p for g in gathered for p in g["probes"]],
             "teardown_ms": [x for g in gathered for x in g["teardown"]],
             "rank_ms_per_step": [round(g["own_s"] * per_step, 3) for g in gathered], "cpu_ms_per_step": cpu_ms,
+            "child_rss_mib": {k: v for g in gathered for k, v in g["rss"].items()},
             "apiserver_profile_per_step": prof, "breakdown": merge_breakdowns(g["breakdown"] for g in gathered)}

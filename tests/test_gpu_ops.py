@@ -249,3 +249,29 @@ def test_multi_gpu_pod_xgmi_ring(dev):
     assert len(r["links"]) == (2 if len(devs) == 2 else len(devs))
     for lk in r["links"]:
         assert lk["errors"] == 0 and lk["gbps"] > 10, lk
+
+
+def test_async_probe_runs_on_the_loop_and_takes_turns(dev):
+    """``run_async``: launched and polled from the event loop (no executor thread), same
+    verdict as the synchronous probe, and concurrent probes of one GPU take turns."""
+    import asyncio
+    import threading
+
+    from odh_kubeflow_amd.ops import gpu
+
+    p = gpu.get_probe(0)
+    p.run()
+    threads = set()
+
+    async def one():
+        threads.add(threading.get_ident())
+        return await p.run_async()
+
+    async def many():
+        return await asyncio.gather(*(one() for _ in range(6)))
+
+    rs = asyncio.run(asyncio.wait_for(many(), 60))
+    assert all(r["ok"] and r["graph"] and r["xcds"] == 8 for r in rs), rs
+    assert threads == {threading.get_ident()}
+    r = asyncio.run(gpu.startup_probe([0]))
+    assert r["ok"] and r["results"][0]["graph"]

@@ -82,20 +82,20 @@ class ChaosProxy:
         await self.server.wait_closed()
 
 
-async def diagnostics(c, names) -> str:
+async def diagnostics(c, names, ns="chaos") -> str:
     """What each notebook's chain looks like (the reference e2e's logNotebookDiagnostics)."""
     out = []
     for n in names:
         row = [n]
         try:
-            nb = await c.get(kinds.NOTEBOOK, n, "chaos")
+            nb = await c.get(kinds.NOTEBOOK, n, ns)
             row.append(f"ann={sorted((nb['metadata'].get('annotations') or {}).items())}")
             row.append(f"fin={nb['metadata'].get('finalizers')} status={nb.get('status')}")
         except Exception as e:  # noqa: BLE001
             row.append(f"notebook: {e!r}")
         for kind, name in ((kinds.STATEFUL_SET, n), (kinds.POD, f"{n}-0")):
             try:
-                o = await c.get(kind, name, "chaos")
+                o = await c.get(kind, name, ns)
                 row.append(f"{kind.split('/')[-1]}: spec.replicas={(o.get('spec') or {}).get('replicas')} "
                            f"node={(o.get('spec') or {}).get('nodeName')} status={o.get('status')}")
             except Exception as e:  # noqa: BLE001
@@ -196,3 +196,91 @@ def test_managers_converge_through_connection_resets(tmp_path, run):
         logf.close()
         if os.environ.get("ODH_KEEP_LOGS"):
             print(open(tmp_path / "procs.log", "rb").read().decode(errors="replace")[-5000:])
+
+
+def test_odh_manager_crash_mid_burst_recovers(tmp_path, run):
+    """SIGKILL the odh manager (reconciler + webhook) while a burst of auth notebooks is being
+    reconciled, start a new one: every notebook still converges (idempotent reconcile: no
+    duplicate children, the one-write unlock happens once per notebook), and deletion
+    cleans every cluster-scoped and central-namespace dependent."""
+    import signal
+
+    from odh_kubeflow_amd.webhook.certs import generate
+    from odh_kubeflow_amd.webhook.server import mutating_webhook_configuration
+
+    api_port, wh_port = free_port(), free_port()
+    certs = generate(("127.0.0.1", "localhost"), str(tmp_path / "certs"))
+    logf = open(tmp_path / "procs.log", "wb")
+    master = f"http://127.0.0.1:{api_port}"
+    procs = {"api": spawn(["odh_kubeflow_amd.cmd.apiserver", "--port", str(api_port), "--controllers",
+                           "--no-openshift-apis"], log=logf)}
+    common = {"K8S_NAMESPACE": "opendatahub", "SET_PIPELINE_RBAC": "false"}
+    odh_args = ["odh_kubeflow_amd.cmd.odh_manager", "--master", master, "--metrics-bind-address", "0",
+                "--health-probe-bind-address", "0", "--kube-rbac-proxy-image", "quay.io/brancz/kube-rbac-proxy:v0.18.1",
+                "--webhook-cert-dir", certs.cert_dir, "--webhook-port", str(wh_port), "--webhook-host", "127.0.0.1"]
+
+    async def go():
+        await wait_http(master + "/healthz")
+        c = RestClient(RestConfig(host=master))
+        for ns in ("opendatahub", "crash"):
+            await c.create({"apiVersion": "v1", "kind": "Namespace", "metadata": {"name": ns}})
+        procs["kf"] = spawn(["odh_kubeflow_amd.cmd.kf_manager", "--master", master, "--metrics-addr", "0",
+                             "--probe-addr", "0"], common, logf)
+        procs["odh"] = spawn(odh_args, common, logf)
+        procs["kubelet"] = spawn(["odh_kubeflow_amd.cmd.fake_kubelet", "--master", master, "--checkpoint-path",
+                                  str(tmp_path / "dp" / "cp")], common, logf)
+        await wait_http(f"https://127.0.0.1:{wh_port}/healthz")
+        await c.create(mutating_webhook_configuration(
+            certs.ca_bundle_b64, url=f"https://127.0.0.1:{wh_port}/mutate-notebook-v1"))
+        await eventually(lambda: c.get(kinds.NODE, "mi355x-node-0"))
+        names = [f"nb{i}" for i in range(8)]
+        for n in names:
+            await c.create(notebook(n, "crash", gpus=1, annotations={"notebooks.opendatahub.io/inject-auth": "true"}))
+        await asyncio.sleep(0.05)  # mid-reconcile
+        procs["odh"].send_signal(signal.SIGKILL)
+        procs["odh"].wait(10)
+        procs["odh"] = spawn(odh_args, common, logf)
+        await wait_http(f"https://127.0.0.1:{wh_port}/healthz")
+
+        async def all_ready():
+            for n in names:
+                st = (await c.get(kinds.NOTEBOOK, n, "crash")).get("status") or {}
+                if st.get("readyReplicas") != 1:
+                    return False
+            return True
+        try:
+            await eventually(all_ready, 60)
+        except AssertionError:
+            raise AssertionError("not all Ready:\n" + await diagnostics(c, names, "crash"))
+        # exactly one of each child per notebook
+        routes = await c.list(kinds.HTTP_ROUTE, "opendatahub")
+        assert sorted(r["metadata"]["name"] for r in routes) == sorted(f"nb-crash-{n}" for n in names)
+        crbs = [x["metadata"]["name"] for x in await c.list(kinds.CLUSTER_ROLE_BINDING)
+                if x["metadata"]["name"].endswith("-crash-auth-delegator")]
+        assert len(crbs) == len(names)
+        for n in names:
+            nb = await c.get(kinds.NOTEBOOK, n, "crash")
+            assert "kubeflow-resource-stopped" not in (nb["metadata"].get("annotations") or {})
+            assert len(nb["metadata"]["finalizers"]) == len(set(nb["metadata"]["finalizers"])) == 3
+        for n in names:
+            await c.delete(kinds.NOTEBOOK, n, "crash")
+
+        async def all_gone():
+            left = await c.list(kinds.NOTEBOOK, "crash")
+            crbs = [x for x in await c.list(kinds.CLUSTER_ROLE_BINDING)
+                    if x["metadata"]["name"].endswith("-crash-auth-delegator")]
+            return not left and not crbs and not await c.list(kinds.HTTP_ROUTE, "opendatahub")
+        await eventually(all_gone, 60)
+        await c.close()
+
+    try:
+        run(go(), timeout=180)
+    finally:
+        for p in procs.values():
+            p.terminate()
+        for p in procs.values():
+            try:
+                p.wait(10)
+            except Exception:  # noqa: BLE001
+                p.kill()
+        logf.close()

@@ -284,3 +284,99 @@ def test_odh_manager_crash_mid_burst_recovers(tmp_path, run):
             except Exception:  # noqa: BLE001
                 p.kill()
         logf.close()
+
+
+def test_admission_path_resets_converge(tmp_path, run):
+    """The apiserver → webhook HTTPS connections go through the resetting proxy too: an
+    admission cut mid-request fails that write (``failurePolicy: Fail``, as the reference),
+    the controllers' own admitted writes (the unlock patch) are retried by their requeue,
+    and the users' writes are retried by the user (here: the test) — everything converges."""
+    from odh_kubeflow_amd.models.errors import ApiError
+    from odh_kubeflow_amd.webhook.certs import generate
+    from odh_kubeflow_amd.webhook.server import mutating_webhook_configuration
+
+    api_port, wh_port = free_port(), free_port()
+    certs = generate(("127.0.0.1", "localhost"), str(tmp_path / "certs"))
+    logf = open(tmp_path / "procs.log", "wb")
+    master = f"http://127.0.0.1:{api_port}"
+    procs = [spawn(["odh_kubeflow_amd.cmd.apiserver", "--port", str(api_port), "--controllers",
+                    "--no-openshift-apis"], log=logf)]
+    rnd = random.Random(5)
+
+    async def retry(fn):
+        for _ in range(50):
+            try:
+                return await fn()
+            except ApiError as e:
+                if e.code not in (500, 503):
+                    raise
+                await asyncio.sleep(0.05)
+        raise AssertionError("write never admitted")
+
+    async def go():
+        await wait_http(master + "/healthz")
+        c = RestClient(RestConfig(host=master))
+        for ns in ("opendatahub", "adm"):
+            await c.create({"apiVersion": "v1", "kind": "Namespace", "metadata": {"name": ns}})
+        common = {"K8S_NAMESPACE": "opendatahub", "SET_PIPELINE_RBAC": "false"}
+        procs.append(spawn(["odh_kubeflow_amd.cmd.kf_manager", "--master", master, "--metrics-addr", "0",
+                            "--probe-addr", "0"], common, logf))
+        procs.append(spawn(["odh_kubeflow_amd.cmd.odh_manager", "--master", master, "--metrics-bind-address", "0",
+                            "--health-probe-bind-address", "0", "--kube-rbac-proxy-image",
+                            "quay.io/brancz/kube-rbac-proxy:v0.18.1", "--webhook-cert-dir", certs.cert_dir,
+                            "--webhook-port", str(wh_port), "--webhook-host", "127.0.0.1"], common, logf))
+        procs.append(spawn(["odh_kubeflow_amd.cmd.fake_kubelet", "--master", master, "--checkpoint-path",
+                            str(tmp_path / "dp" / "cp")], common, logf))
+        await wait_http(f"https://127.0.0.1:{wh_port}/healthz")
+        proxy = await ChaosProxy(wh_port).start()  # TCP-level: TLS passes through untouched
+        await c.create(mutating_webhook_configuration(
+            certs.ca_bundle_b64, url=f"https://127.0.0.1:{proxy.port}/mutate-notebook-v1"))
+        await eventually(lambda: c.get(kinds.NODE, "mi355x-node-0"))
+        stop = asyncio.Event()
+
+        async def chaos():
+            while not stop.is_set():
+                await asyncio.sleep(rnd.uniform(0.01, 0.05))
+                proxy.cut_all()
+        task = asyncio.create_task(chaos())
+        names = [f"nb{i}" for i in range(5)]
+        try:
+            for n in names:
+                await retry(lambda n=n: c.create(notebook(n, "adm", gpus=1, annotations={
+                    "notebooks.opendatahub.io/inject-auth": "true"})))
+
+            async def all_ready():
+                for n in names:
+                    st = (await c.get(kinds.NOTEBOOK, n, "adm")).get("status") or {}
+                    if st.get("readyReplicas") != 1:
+                        return False
+                return True
+            try:
+                await eventually(all_ready, 60)
+            except AssertionError:
+                raise AssertionError("not all Ready:\n" + await diagnostics(c, names, "adm"))
+            for n in names:
+                await retry(lambda n=n: c.delete(kinds.NOTEBOOK, n, "adm"))
+
+            async def all_gone():
+                return not await c.list(kinds.NOTEBOOK, "adm") and not await c.list(kinds.HTTP_ROUTE, "opendatahub")
+            await eventually(all_gone, 60)
+        finally:
+            stop.set()
+            await task
+            await proxy.close()
+            await c.close()
+        return proxy.aborted
+
+    try:
+        aborted = run(go(), timeout=200)
+        assert aborted >= 3, aborted
+    finally:
+        for p in procs:
+            p.terminate()
+        for p in procs:
+            try:
+                p.wait(10)
+            except Exception:  # noqa: BLE001
+                p.kill()
+        logf.close()

@@ -380,3 +380,106 @@ def test_admission_path_resets_converge(tmp_path, run):
             except Exception:  # noqa: BLE001
                 p.kill()
         logf.close()
+
+
+def test_sharded_control_plane_follows_new_namespaces_through_resets(tmp_path, run):
+    """Two ``cmd/control_plane`` shards reach the apiserver through the resetting proxy while
+    new namespaces keep appearing: the assigner labels each one (shard 0), the owning shard's
+    label-selected Namespace watch adds a per-namespace informer group for it — across
+    dropped watches and relists — and every notebook in every namespace becomes Ready."""
+    from odh_kubeflow_amd.models import meta as m
+    from odh_kubeflow_amd.webhook.certs import generate
+    from odh_kubeflow_amd.webhook.server import mutating_webhook_configuration
+
+    api_port = free_port()
+    wh = [free_port(), free_port()]
+    certs = generate(("127.0.0.1", "localhost"), str(tmp_path / "certs"))
+    logf = open(tmp_path / "procs.log", "wb")
+    master = f"http://127.0.0.1:{api_port}"
+    procs = [spawn(["odh_kubeflow_amd.cmd.apiserver", "--port", str(api_port), "--controllers",
+                    "--no-openshift-apis"], log=logf)]
+    common = {"K8S_NAMESPACE": "opendatahub", "SET_PIPELINE_RBAC": "false", "SET_PIPELINE_SECRET": "false"}
+    rnd = random.Random(3)
+
+    async def go():
+        await wait_http(master + "/healthz")
+        proxy = await ChaosProxy(api_port).start()
+        via = f"http://127.0.0.1:{proxy.port}"
+        c = RestClient(RestConfig(host=master))
+        await c.create({"apiVersion": "v1", "kind": "Namespace", "metadata": {"name": "opendatahub"}})
+        for k in (0, 1):
+            await c.create(mutating_webhook_configuration(
+                certs.ca_bundle_b64, url=f"https://127.0.0.1:{wh[k]}/mutate-notebook-v1",
+                name=f"notebook-webhook-shard-{k}",
+                namespace_selector={"matchLabels": {"notebooks.amd.com/shard": str(k)}}))
+        await c.create(mutating_webhook_configuration(
+            certs.ca_bundle_b64, url=f"https://127.0.0.1:{wh[0]}/mutate-notebook-v1",
+            name="notebook-webhook-unassigned", namespace_selector={"matchExpressions": [
+                {"key": "notebooks.amd.com/shard", "operator": "DoesNotExist"}]}))
+        for k in (0, 1):
+            procs.append(spawn(["odh_kubeflow_amd.cmd.control_plane", "--master", via, "--shard", str(k),
+                                "--shard-count", "2", "--assign-namespaces", "--metrics-bind-address", "0",
+                                "--health-probe-bind-address", "0", "--kube-rbac-proxy-image",
+                                "quay.io/brancz/kube-rbac-proxy:v0.18.1", "--webhook-cert-dir", certs.cert_dir,
+                                "--webhook-host", "127.0.0.1", "--webhook-port", str(wh[k])], common, logf))
+        procs.append(spawn(["odh_kubeflow_amd.cmd.fake_kubelet", "--master", master, "--devices",
+                            "0,1,2,3,4,5,6,7"], common, logf))
+        for k in (0, 1):
+            await wait_http(f"https://127.0.0.1:{wh[k]}/healthz")
+        await eventually(lambda: c.get(kinds.NODE, "mi355x-node-0"))
+        stop = asyncio.Event()
+
+        async def chaos():
+            while not stop.is_set():
+                await asyncio.sleep(rnd.uniform(0.05, 0.15))
+                proxy.cut_all()
+        task = asyncio.create_task(chaos())
+        spaces = [f"team-{i}" for i in range(6)]
+        try:
+            for ns in spaces:
+                await c.create({"apiVersion": "v1", "kind": "Namespace", "metadata": {"name": ns}})
+
+            async def labelled():
+                for ns in spaces:
+                    if not m.labels(await c.get(kinds.NAMESPACE, ns)).get("notebooks.amd.com/shard"):
+                        return False
+                return True
+            await eventually(labelled, 60)
+            for ns in spaces:
+                for _ in range(50):  # the owning shard's webhook may be mid-restart of a watch: retry
+                    try:
+                        await c.create(notebook("nb", ns, gpus=1))
+                        break
+                    except Exception:  # noqa: BLE001
+                        await asyncio.sleep(0.05)
+
+            async def all_ready():
+                for ns in spaces:
+                    st = (await c.get(kinds.NOTEBOOK, "nb", ns)).get("status") or {}
+                    if st.get("readyReplicas") != 1:
+                        return False
+                return True
+            await eventually(all_ready, 90)
+            owners = {m.labels(r)["notebook-namespace"]: m.labels(r).get("notebooks.amd.com/shard")
+                      for r in await c.list(kinds.HTTP_ROUTE, "opendatahub")}
+            want = {ns: m.labels(await c.get(kinds.NAMESPACE, ns))["notebooks.amd.com/shard"] for ns in spaces}
+            assert owners == want  # each notebook reconciled by the shard that owns its namespace
+        finally:
+            stop.set()
+            await task
+            await proxy.close()
+            await c.close()
+        return proxy.aborted
+
+    try:
+        aborted = run(go(), timeout=240)
+        assert aborted >= 10, aborted
+    finally:
+        for p in procs:
+            p.terminate()
+        for p in procs:
+            try:
+                p.wait(10)
+            except Exception:  # noqa: BLE001
+                p.kill()
+        logf.close()

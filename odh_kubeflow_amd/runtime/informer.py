@@ -16,6 +16,7 @@ from __future__ import annotations
 import asyncio
 import logging
 import random
+import time
 from typing import Callable, Dict, Iterable, List, Optional, Set, Tuple
 
 from ..models import meta as m
@@ -159,11 +160,13 @@ class _Informer:
         ref = f"{self.info.api_version(self.version)}/{self.info.kind}"
         backoff = 0.05
         need_list = True
+        started: Optional[float] = None
         while True:
             try:
                 if need_list:
                     await self._relist()
                     need_list = False
+                started = time.monotonic()
                 async for et, obj in self.cache.rest.watch(ref, self.namespace, self.rv, labels=self.label_selector,
                                                            timeout_s=self.cache.watch_timeout_s):
                     backoff = 0.05
@@ -202,6 +205,8 @@ class _Informer:
                 backoff = min(backoff * 2, 5.0)
             except Exception as e:  # connection reset, server restart
                 log.debug("%s watch dropped: %r", self.info.kind, e)
+                if started is not None and time.monotonic() - started > 1.0:
+                    backoff = 0.05  # the stream was healthy for a while: a fresh drop, not a flapping server
                 await asyncio.sleep(backoff * (1 + random.random()))
                 backoff = min(backoff * 2, 5.0)
 

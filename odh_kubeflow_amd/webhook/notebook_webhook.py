@@ -252,13 +252,21 @@ class NotebookWebhook:
     async def handle(self, review: dict) -> dict:
         """AdmissionReview v1 request → AdmissionReview response with a JSONPatch."""
         self.requests += 1
-        req = review.get("request") or {}
-        uid = req.get("uid", "")
+        req = review.get("request") if isinstance(review, dict) else None
+        if not isinstance(req, dict):  # not an AdmissionReview: deny, never raise
+            self.denied += 1
+            return {"apiVersion": "admission.k8s.io/v1", "kind": "AdmissionReview",
+                    "response": {"uid": "", "allowed": False,
+                                 "status": {"code": 400, "message": "request is not an AdmissionReview"}}}
+        uid = req.get("uid", "") if isinstance(req.get("uid", ""), str) else ""
         resp = {"uid": uid, "allowed": True}
         try:
             obj = req.get("object")
             if not isinstance(obj, dict):
                 raise AdmissionError(400, "there is no content to decode")
+            bad = undecodable(obj)
+            if bad:  # the reference's typed decode (admission.Decoder) refuses these
+                raise AdmissionError(400, f"cannot decode Notebook: {bad}")
             old = req.get("oldObject") if isinstance(req.get("oldObject"), dict) else None
             mutated = await self.mutate(req.get("operation", ""), obj, old, req.get("name", ""),
                                         req.get("namespace", ""))
@@ -273,6 +281,48 @@ class NotebookWebhook:
             self.denied += 1
             resp = {"uid": uid, "allowed": False, "status": {"code": 500, "message": str(e)}}
         return {"apiVersion": "admission.k8s.io/v1", "kind": "AdmissionReview", "response": resp}
+
+
+def undecodable(obj: dict) -> Optional[str]:
+    """Where ``obj`` does not have the Notebook's JSON shape along the paths the webhook
+    reads (the Go webhook decodes into ``nbv1.Notebook`` first and answers 400 on a type
+    mismatch); ``None`` when it does."""
+    def is_map(v, of_str=False):
+        return v is None or (isinstance(v, dict) and (not of_str or all(isinstance(x, str) for x in v.values())))
+
+    def is_list_of_maps(v):
+        return v is None or (isinstance(v, list) and all(isinstance(x, dict) for x in v))
+
+    md = obj.get("metadata")
+    if not is_map(md):
+        return "metadata"
+    for k in ("annotations", "labels"):
+        if not is_map((md or {}).get(k), of_str=True):
+            return f"metadata.{k}"
+    if not isinstance((md or {}).get("name", ""), str) or not isinstance((md or {}).get("namespace", ""), str):
+        return "metadata.name"
+    spec = obj.get("spec")
+    if not is_map(spec):
+        return "spec"
+    tmpl = (spec or {}).get("template")
+    if not is_map(tmpl):
+        return "spec.template"
+    ps = (tmpl or {}).get("spec")
+    if not is_map(ps):
+        return "spec.template.spec"
+    for k in ("containers", "initContainers", "volumes", "imagePullSecrets", "tolerations"):
+        if not is_list_of_maps((ps or {}).get(k)):
+            return f"spec.template.spec.{k}"
+    for i, c in enumerate((ps or {}).get("containers") or []):
+        for k in ("env", "volumeMounts", "ports", "envFrom"):
+            if not is_list_of_maps(c.get(k)):
+                return f"spec.template.spec.containers[{i}].{k}"
+        res = c.get("resources")
+        if not is_map(res) or not all(is_map(v) for v in (res or {}).values()):
+            return f"spec.template.spec.containers[{i}].resources"
+        if not isinstance(c.get("name", ""), str) or not isinstance(c.get("image", ""), str):
+            return f"spec.template.spec.containers[{i}].name"
+    return None
 
 
 def matches(info, operation: str) -> bool:

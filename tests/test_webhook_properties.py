@@ -122,3 +122,26 @@ def test_webhook_answers_patch_is_exact_and_reinvocation_is_stable(nb):
         upd = await _admit(WH, "UPDATE", json.loads(json.dumps(first)), json.loads(json.dumps(first)))
         assert upd is not None and upd["spec"] == first["spec"]
     asyncio.run(go())
+
+
+@settings(max_examples=150, deadline=None, suppress_health_check=[HealthCheck.too_slow])
+@given(st.one_of(
+    st.recursive(st.one_of(st.none(), st.booleans(), st.integers(), st.text(max_size=5)),
+                 lambda kids: st.one_of(st.lists(kids, max_size=3), st.dictionaries(st.text(max_size=5), kids,
+                                                                                    max_size=3)), max_leaves=8),
+    st.fixed_dictionaries({"request": st.fixed_dictionaries(
+        {"uid": st.one_of(st.text(max_size=3), st.integers()),
+         "operation": st.sampled_from(["CREATE", "UPDATE", "DELETE", "CONNECT", "", 5]),
+         "object": st.one_of(st.none(), st.integers(), st.dictionaries(st.sampled_from(["metadata", "spec"]),
+                                                                       st.one_of(st.none(), st.integers(),
+                                                                                 st.dictionaries(st.text(max_size=3),
+                                                                                                 st.none(), max_size=2)),
+                                                                       max_size=2))})})))
+def test_webhook_never_raises_on_garbage_reviews(review):
+    """Any JSON body at the webhook endpoint gets an AdmissionReview answer (allow or deny),
+    never an exception (which would be a 500 and a connection error at the apiserver)."""
+    global WH
+    if WH is None:
+        WH = _make_webhook()
+    out = asyncio.run(WH.handle(review))
+    assert out["kind"] == "AdmissionReview" and isinstance(out["response"]["allowed"], bool)

@@ -1,0 +1,146 @@
+"""Differential test of the two test apiservers at the REST level.
+
+The same seeded sequence of creates, updates (with and without a resourceVersion
+precondition), status updates, merge / JSON patches, deletes (with finalizers pending),
+gets and label-selected lists goes to the Python REST apiserver and to the C++ one; every
+response must agree in status code and — after masking what each server assigns on its own
+(uids, timestamps, resourceVersion values, Service IPs) — in body.  Scenarios are run over
+both servers (``ODH_CLUSTER_TRANSPORT``), so a divergence here is a test that could pass
+over one and fail over the other."""
+
+import random
+
+import pytest
+
+from odh_kubeflow_amd.apiserver import native
+from odh_kubeflow_amd.apiserver.http import ApiServer
+from odh_kubeflow_amd.apiserver.store import ObjectStore
+from odh_kubeflow_amd.models import kinds
+from odh_kubeflow_amd.models.errors import ApiError
+from odh_kubeflow_amd.models.notebook import notebook
+from odh_kubeflow_amd.runtime.rest import RestClient, RestConfig
+
+pytestmark = pytest.mark.skipif(not native.available(), reason="native apiserver not built")
+
+MASK_META = ("uid", "resourceVersion", "creationTimestamp", "managedFields", "deletionTimestamp")
+
+
+def mask(o):
+    if isinstance(o, list):
+        return [mask(x) for x in o]
+    if not isinstance(o, dict):
+        return o
+    out = {}
+    for k, v in o.items():
+        if k == "metadata" and isinstance(v, dict):
+            md = {kk: vv for kk, vv in v.items() if kk not in MASK_META}
+            if "deletionTimestamp" in v:
+                md["deletionTimestamp"] = "<set>"
+            out[k] = mask(md)
+        elif k in ("clusterIP", "clusterIPs"):
+            continue
+        else:
+            out[k] = mask(v)
+    return out
+
+
+def ops(seed: int, n: int):
+    """A seeded op sequence; each op is (verb, args) with objects built fresh per server."""
+    rnd = random.Random(seed)
+    names = [f"o{i}" for i in range(6)]
+    out = []
+    for _ in range(n):
+        kind = rnd.choice(["cm", "nb", "svc"])
+        name = rnd.choice(names)
+        verb = rnd.choice(["create", "create", "get", "update", "update_stale", "status", "merge", "json", "delete",
+                           "list", "finalize"])
+        out.append((verb, kind, name, rnd.randint(0, 3), rnd.choice(["a", "b"])))
+    return out
+
+
+KIND = {"cm": kinds.CONFIG_MAP, "nb": kinds.NOTEBOOK, "svc": kinds.SERVICE}
+
+
+def build(kind, name, i, lbl):
+    if kind == "cm":
+        return {"apiVersion": "v1", "kind": "ConfigMap", "metadata": {"name": name, "namespace": "d",
+                                                                      "labels": {"t": lbl}}, "data": {"i": str(i)}}
+    if kind == "svc":
+        return {"apiVersion": "v1", "kind": "Service", "metadata": {"name": name, "namespace": "d", "labels": {"t": lbl}},
+                "spec": {"selector": {"app": name}, "ports": [{"port": 80 + i, "targetPort": 8888}]}}
+    nb = notebook(name, "d")
+    nb["metadata"]["labels"] = {"t": lbl}
+    return nb
+
+
+async def play(c, seq):
+    results = []
+
+    async def call(fn):
+        try:
+            return (200, mask(await fn()))
+        except ApiError as e:
+            return (e.code, e.reason)
+    await c.create({"apiVersion": "v1", "kind": "Namespace", "metadata": {"name": "d"}})
+    for verb, kind, name, i, lbl in seq:
+        k = KIND[kind]
+        if verb == "create":
+            r = await call(lambda: c.create(build(kind, name, i, lbl)))
+        elif verb == "get":
+            r = await call(lambda: c.get(k, name, "d"))
+        elif verb in ("update", "update_stale", "status"):
+            async def upd():
+                cur = await c.get(k, name, "d")
+                if verb == "update_stale":
+                    cur["metadata"]["resourceVersion"] = "1"
+                if kind == "cm":
+                    cur["data"] = {"i": str(i), "u": "1"}
+                elif kind == "svc":
+                    cur["spec"]["ports"][0]["port"] = 90 + i
+                else:
+                    cur["spec"]["template"]["spec"]["containers"][0]["image"] = f"img:{i}"
+                if verb == "status":
+                    cur["status"] = {"readyReplicas": i} if kind == "nb" else {"loadBalancer": {}}
+                    return await c.update_status(cur)
+                return await c.update(cur)
+            r = await call(upd)
+        elif verb == "merge":
+            r = await call(lambda: c.patch(k, {"metadata": {"labels": {"t": lbl, "m": str(i)}}}, "merge",
+                                           name=name, namespace="d"))
+        elif verb == "json":
+            r = await call(lambda: c.patch(k, [{"op": "add", "path": "/metadata/annotations",
+                                                "value": {"x": str(i)}}], "json", name=name, namespace="d"))
+        elif verb == "finalize":
+            r = await call(lambda: c.patch(k, {"metadata": {"finalizers": ["example.com/f"] if i % 2 else None}},
+                                           "merge", name=name, namespace="d"))
+        elif verb == "delete":
+            r = await call(lambda: c.delete(k, name, "d"))
+        else:
+            async def ls():
+                items = await c.list(k, "d", labels={"t": lbl})
+                return sorted(o["metadata"]["name"] for o in items)
+            r = await call(ls)
+        results.append((verb, kind, name, r))
+    return results
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3])
+def test_python_and_native_apiservers_answer_alike(run, seed):
+    seq = ops(seed, 150)
+
+    async def go():
+        py = await ApiServer(ObjectStore()).start("127.0.0.1", 0)
+        nat = await native.NativeApiServer().start()
+        cp = RestClient(RestConfig(host=f"http://127.0.0.1:{py.port}"))
+        cn = RestClient(RestConfig(host=nat.url))
+        try:
+            a = await play(cp, seq)
+            b = await play(cn, seq)
+        finally:
+            await cp.close()
+            await cn.close()
+            await py.stop()
+            await nat.stop()
+        for x, y in zip(a, b):
+            assert x == y, (x, y)
+    run(go(), timeout=120)

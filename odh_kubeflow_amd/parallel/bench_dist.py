@@ -78,6 +78,13 @@ def run_distributed(args) -> int:
 
 def measure(args) -> Optional[dict]:
     """Run the sharded benchmark on this rank; rank 0 returns the report dict."""
+    binding = None
+    if not args.no_gpu_probe:  # before any thread or child exists: they inherit the placement
+        import torch as _t
+
+        ndev = _t.cuda.device_count()  # does not initialise the GPU
+        if ndev:
+            binding = numa_bind(int(os.environ.get("LOCAL_RANK", os.environ.get("RANK", "0"))) % ndev)
     dist, torch = _dist_init()
     rank, world = dist.get_rank(), dist.get_world_size()
     local_rank = int(os.environ.get("LOCAL_RANK", rank))
@@ -109,6 +116,7 @@ def measure(args) -> Optional[dict]:
         out["rank_ms_per_step"] = res.get("rank_ms_per_step")
         out["cpu_ms_per_step"] = res.get("cpu_ms_per_step")
         out["child_rss_mib"] = res.get("child_rss_mib")
+        out["cpu_binding"] = binding or "none (ODH_BENCH_NUMA_BIND=0, or no GPU NUMA information)"
         if res.get("apiserver_profile_per_step"):
             out["apiserver_profile_per_step"] = res["apiserver_profile_per_step"]
         if rccl_ms is not None:
@@ -142,6 +150,55 @@ def _proc_rss_mib(pid: Optional[int]) -> Optional[float]:
     except (OSError, IndexError, ValueError):
         return None
     return None
+
+
+def _cpulist(text: str) -> set:
+    out = set()
+    for part in text.strip().split(","):
+        if not part:
+            continue
+        a, _, b = part.partition("-")
+        out.update(range(int(a), int(b or a) + 1))
+    return out
+
+
+def numa_bind(local_rank: int, sysfs: str = "/sys") -> Optional[dict]:
+    """Pin this rank — and the processes it starts after this (its control plane, on rank 0
+    the apiserver and scheduler) — to the physical cores of its MI355X's NUMA node.
+
+    An 8×MI355X node is two sockets; left alone, the scheduler spreads a rank's processes
+    over both, and every watch event, admission and REST call between them crosses the
+    socket interconnect (measured on the one-GPU box: the slower of two ranks burnt 30–50 %
+    more CPU per notebook than the other).  One SMT thread per core keeps siblings from
+    competing.  ``ODH_BENCH_NUMA_BIND=0`` turns it off; any failure leaves placement alone."""
+    if os.environ.get("ODH_BENCH_NUMA_BIND", "1") == "0":
+        return None
+    try:
+        from ..ops.telemetry import Telemetry
+
+        devs = Telemetry(sysfs).devices()
+        bdf = devs[local_rank].pci_bdf
+        with open(f"{sysfs}/bus/pci/devices/{bdf}/numa_node") as f:
+            node = int(f.read().strip())
+        if node < 0:
+            return None
+        with open(f"{sysfs}/devices/system/node/node{node}/cpulist") as f:
+            cpus = _cpulist(f.read())
+        phys = set()
+        for c in cpus:
+            try:
+                with open(f"{sysfs}/devices/system/cpu/cpu{c}/topology/thread_siblings_list") as f:
+                    if min(_cpulist(f.read())) == c:
+                        phys.add(c)
+            except OSError:
+                phys.add(c)
+        target = phys & os.sched_getaffinity(0)
+        if len(target) < 4:
+            return None
+        os.sched_setaffinity(0, target)
+        return {"gpu": bdf, "numa_node": node, "cores": len(target)}
+    except Exception:  # noqa: BLE001 — no telemetry / sysfs: leave placement to the OS
+        return None
 
 
 async def _main(args, dist, torch, rank: int, world: int, local_rank: int, probe) -> dict:

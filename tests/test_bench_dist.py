@@ -58,3 +58,34 @@ def test_bench_reference_emulation_serialises():
     d = json.loads([l for l in out.stdout.splitlines() if l.startswith("{")][-1])
     assert d["config"]["reference_emulation"] is True
     assert 5500 < d["p50_ready_ms"] < 9000
+
+
+def test_numa_bind_pins_to_the_gpus_physical_cores(tmp_path, monkeypatch):
+    """``numa_bind``: the GPU's NUMA node (from its PCI address), one SMT thread per core,
+    intersected with the allowed CPUs; any missing piece leaves placement alone."""
+    import os
+
+    from odh_kubeflow_amd.ops import telemetry
+    from odh_kubeflow_amd.parallel import bench_dist
+
+    root = tmp_path / "sys"
+    telemetry.write_fake_sysfs(str(root), gpus=2)
+    bdf = telemetry.Telemetry(str(root)).devices()[1].pci_bdf
+    (root / "bus" / "pci" / "devices" / bdf).mkdir(parents=True)
+    (root / "bus" / "pci" / "devices" / bdf / "numa_node").write_text("1\n")
+    (root / "devices" / "system" / "node" / "node1").mkdir(parents=True)
+    (root / "devices" / "system" / "node" / "node1" / "cpulist").write_text("4-7,12-15\n")
+    for c in range(16):
+        d = root / "devices" / "system" / "cpu" / f"cpu{c}" / "topology"
+        d.mkdir(parents=True)
+        d.joinpath("thread_siblings_list").write_text(f"{c % 8},{c % 8 + 8}\n")
+    calls = []
+    monkeypatch.setattr(os, "sched_getaffinity", lambda pid: set(range(16)))
+    monkeypatch.setattr(os, "sched_setaffinity", lambda pid, cpus: calls.append(set(cpus)))
+    out = bench_dist.numa_bind(1, str(root))
+    assert out == {"gpu": bdf, "numa_node": 1, "cores": 4} and calls == [{4, 5, 6, 7}]
+    monkeypatch.setenv("ODH_BENCH_NUMA_BIND", "0")
+    assert bench_dist.numa_bind(1, str(root)) is None
+    monkeypatch.delenv("ODH_BENCH_NUMA_BIND")
+    assert bench_dist.numa_bind(0, str(root)) is None  # GPU 0 has no PCI numa_node file: untouched
+    assert len(calls) == 1

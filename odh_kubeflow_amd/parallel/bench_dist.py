@@ -119,10 +119,24 @@ def measure(args) -> Optional[dict]:
         out["cpu_binding"] = binding or "none (ODH_BENCH_NUMA_BIND=0, or no GPU NUMA information)"
         if res.get("apiserver_profile_per_step"):
             out["apiserver_profile_per_step"] = res["apiserver_profile_per_step"]
+            out["writes_per_notebook"] = writes_per_notebook(res["apiserver_profile_per_step"], world)
         if rccl_ms is not None:
             out["rccl_allreduce_check_ms"] = round(rccl_ms, 3)
     dist.barrier()
     dist.destroy_process_group()
+    return out
+
+
+def writes_per_notebook(prof: dict, notebooks_per_step: int) -> dict:
+    """Apiserver write calls per notebook lifecycle (create → Ready → delete), by verb.
+
+    Counted at the apiserver, so every client is in it: the controllers, the platform stand-ins
+    (scheduler binding, kubelet status, StatefulSet controller, GC) and the bench's own Notebook
+    create and delete.  ``total`` is the figure the steady-state write gating and the
+    single unlock patch of the odh create path are judged by."""
+    n = max(1, notebooks_per_step)
+    out = {v: round(prof.get(f"{v}_calls", 0.0) / n, 2) for v in ("create", "update", "patch", "delete")}
+    out["total"] = round(sum(out.values()), 2)
     return out
 
 

@@ -38,6 +38,10 @@ def test_bench_two_ranks_gloo():
     cpu = d["cpu_ms_per_step"]
     assert len(cpu["ranks"]) == 2 and all(x > 0 for x in cpu["ranks"])
     assert cpu["apiserver"] >= 0 and cpu["scheduler"] >= 0  # rank 0's child processes
+    if "apiserver_profile_per_step" in d:  # native apiserver built: write calls per notebook, by verb
+        w = d["writes_per_notebook"]
+        assert w["total"] == pytest.approx(w["create"] + w["update"] + w["patch"] + w["delete"], abs=0.05)
+        assert w["create"] >= 3 and w["delete"] >= 1
 
 
 def test_bench_single_process_contract():

@@ -56,7 +56,7 @@ for s in $steps; do
     ranks)
       for n in 2 4; do
         timeout -k 10 170 python -m torch.distributed.run --nnodes=1 --nproc-per-node $n \
-          --master-addr 127.0.0.1 --master-port 2993$n bench.py --gpus $n --steps 40 --warmup 5 \
+          --master-addr 127.0.0.1 --master-port 2993$n bench.py --gpus $n \
           > "$out/bench_n$n.log" 2>&1 || fail ranks $? "$out/bench_n$n.log"
         show "$out/bench_n$n.log" "n$n"
       done ;;

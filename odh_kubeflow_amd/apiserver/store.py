@@ -631,8 +631,14 @@ class ObjectStore:
     # ------------------------------------------------------------------ watch
 
     def watch(self, ref, callback: WatchCallback, namespace: Optional[str] = None, label_selector=None,
-              field_selector=None, resource_version: Optional[str] = None) -> Callable[[], None]:
+              field_selector=None, resource_version: Optional[str] = None,
+              initial: bool = False) -> Callable[[], None]:
         """Subscribe to events; replays history after ``resource_version`` (410 if too old).
+
+        ``initial`` first delivers every stored object the watch selects as ADDED — an
+        informer's initial list, so a controller started against existing objects reconciles
+        each of them once (controller-runtime's Kind source) — atomically with the subscribe,
+        so nothing written in between is missed or seen twice.
 
         Returns an ``unsubscribe`` function.
         """
@@ -654,6 +660,10 @@ class ObjectStore:
                 for rv, et, obj, old in list(hist):
                     if rv > since and (w.wants(obj) or (old is not None and w.wants(old))):
                         callback(et, obj, old)
+            elif initial:
+                for obj in list(self._bucket(info).values()):
+                    if w.wants(obj):
+                        callback("ADDED", obj, None)
             self._watchers.setdefault(info.key, {})[w.wid] = w
 
         def cancel() -> None:

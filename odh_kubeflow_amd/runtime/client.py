@@ -149,7 +149,7 @@ class StoreEventSource(EventSource):
         self.store = store
 
     def subscribe(self, kind, callback, namespace=None):
-        return self.store.watch(kind, callback, namespace=namespace)
+        return self.store.watch(kind, callback, namespace=namespace, initial=True)
 
 
 class InProcessClient(Client):

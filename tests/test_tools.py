@@ -5,6 +5,8 @@ import os
 import subprocess
 import sys
 
+import pytest
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
@@ -45,3 +47,46 @@ def test_coverage_tool_units(tmp_path):
     assert cov.executable_lines(str(src)) >= {1, 3, 4, 5, 6}
     assert cov.flag_of("controllers/odh/route.py") == "odh" and cov.flag_of("controllers/notebook.py") == "kf"
     assert cov.flag_of("runtime/informer.py") == "runtime" and cov.flag_of("something_new.py") == "other"
+
+
+def test_critical_path_from_audit_log(run, tmp_path):
+    """tools/critical_path.py over a real audit log of the REST apiserver: every notebook's
+    Ready path is found hop by hop, and every write is attributed per notebook."""
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    try:
+        import critical_path
+    finally:
+        sys.path.pop(0)
+    from odh_kubeflow_amd.cluster import ClusterConfig, LocalCluster
+    from odh_kubeflow_amd.models.notebook import notebook
+
+    from odh_kubeflow_amd.apiserver import native
+
+    if not native.available():
+        pytest.skip("native apiserver not built")
+    log = str(tmp_path / "audit.jsonl")
+
+    async def go():
+        from odh_kubeflow_amd.apiserver.audit import AuditPolicy
+
+        cfg = ClusterConfig(transport="native", odh=True, webhook=True, audit_log_path=log,
+                            audit_policy=AuditPolicy([{"level": "Metadata"}]),
+                            env={"SET_PIPELINE_RBAC": "false", "SET_PIPELINE_SECRET": "false"})
+        async with LocalCluster(cfg) as cl:
+            await cl.ensure_namespace("bench-0")
+            for i in range(3):
+                await cl.admin.create(notebook(f"nb{i}", "bench-0", gpus=1))
+            for i in range(3):
+                assert await cl.wait_for(lambda i=i: cl.notebook_ready(f"nb{i}", "bench-0"), 20)
+            assert await cl.settle(10)
+    run(go(), timeout=90)
+    with open(log) as f:
+        out = critical_path.analyse(f, "bench-")
+    assert out["notebooks"] == 3
+    assert {"notebook_create", "sts_create", "pod_create", "pod_ready", "notebook_status"} <= set(out["hops"])
+    assert out["create_to_notebook_status_ms"]["p50"] > 0
+    w = out["writes_per_notebook"]
+    by = w["by_client"]
+    assert any(k.endswith(" create statefulsets") and v == 1.0 for k, v in by.items()), by
+    assert any(k.endswith(" create notebooks") and v == 1.0 for k, v in by.items()), by
+    assert w["total"] == pytest.approx(sum(by.values()), abs=0.1)

@@ -16,7 +16,8 @@ on its Ready path are picked out in order:
 and each hop is split into ``gap`` (previous request answered → this one received: watch
 delivery, queueing, the controller's own work) and ``serve`` (this request inside the
 apiserver, admission included).  Medians and p95 over the Notebooks are printed as JSON,
-with the user agent that issued each step.  This is where the create→Ready milliseconds
+with the user agent that issued each step, and every successful write per notebook by
+client, verb and resource (``writes_per_notebook``).  This is where the create→Ready milliseconds
 of ``bench.py`` go, hop by hop (the reference's envtest audit-log aid,
 ``odh/controllers/suite_test.go:125-137``, put to a latency use).
 """
@@ -78,6 +79,11 @@ def analyse(lines, ns_prefix: str = "") -> dict:
              e.get("userAgent", "").split("/")[0]))
     notebooks = [(ns, name) for (ns, res, name) in by_obj if res == "notebooks" and name and
                  any(v == "create" for _, _, v, _, _ in by_obj[(ns, res, name)])]
+    # every successful write, attributed to its client and target: who spends the writes
+    writes = defaultdict(int)
+    for (ns, res, name), evs in by_obj.items():
+        for _, _, v, sub, ua in evs:
+            writes[(ua or "?", v, res + ("/" + sub if sub else ""))] += 1
     hops = defaultdict(lambda: {"gap": [], "serve": [], "agents": defaultdict(int)})
     totals = []
     for ns, nb in notebooks:
@@ -116,6 +122,11 @@ def analyse(lines, ns_prefix: str = "") -> dict:
             "serve_ms_p50": round(pct(h["serve"], .5), 3), "serve_ms_p95": round(pct(h["serve"], .95), 3),
             "by": dict(h["agents"]),
         }
+    n_created = max(1, len(notebooks))
+    out["writes_per_notebook"] = {
+        "total": round(sum(writes.values()) / n_created, 2),
+        "by_client": {f"{ua} {v} {res}": round(c / n_created, 2)
+                      for (ua, v, res), c in sorted(writes.items(), key=lambda kv: (kv[0][0], -kv[1], kv[0]))}}
     for k in ("p50", "p95"):
         v = out["create_to_notebook_status_ms"][k]
         out["create_to_notebook_status_ms"][k] = round(v, 3) if v is not None else None

@@ -34,6 +34,9 @@ def parse(argv=None):
     p.add_argument("--telemetry-interval-ms", type=int, default=200)
     p.add_argument("--telemetry-capacity", type=int, default=3000, help="samples kept per GPU (window length)")
     p.add_argument("--attribution-ttl-s", type=float, default=1.0)
+    p.add_argument("--token-file", default="",
+                   help="bearer token the /gpu/* and /metrics endpoints require (nodeagent/auth.py); "
+                        "'' serves them unauthenticated")
     p.add_argument("--debug-log", action="store_true")
     return p.parse_args(argv)
 
@@ -54,7 +57,17 @@ def build(args):
                             checkpoint_path=args.device_plugin_checkpoint or None,
                             proc_root=args.proc_root or None, resource=args.resource_name,
                             ttl_s=args.attribution_ttl_s)
-    return NodeTelemetryAgent(telemetry, attributor, host=args.bind, port=args.port)
+    token = None
+    if args.token_file:
+        from ..nodeagent.auth import TokenFile
+
+        token = TokenFile(args.token_file)
+        if token.current() is None:
+            log.warning("token file %s missing or empty: data endpoints refuse every request until it appears",
+                        args.token_file)
+    else:
+        log.warning("no --token-file: /gpu/* and /metrics are served unauthenticated on the hostPort")
+    return NodeTelemetryAgent(telemetry, attributor, host=args.bind, port=args.port, token=token)
 
 
 async def amain(argv=None) -> int:

@@ -37,6 +37,9 @@ def parse(argv=None):
     p.add_argument("--validity-days", type=int, default=365)
     p.add_argument("--renew-before-days", type=int, default=90)
     p.add_argument("--cluster-domain", default="cluster.local")
+    p.add_argument("--random-secret", action="append", default=[],
+                   help="also ensure this Secret holds a random bearer token under key 'token' (repeatable; "
+                        "kept once it exists): the node agent / culler shared token, nodeagent/auth.py")
     return p.parse_args(argv)
 
 
@@ -54,6 +57,11 @@ async def amain(argv=None) -> int:
                               args.service_name or ["odh-notebook-controller-webhook-service"],
                               args.mwc_name or ["odh-notebook-controller-mutating-webhook-configuration"],
                               args.extra_host, args.validity_days, args.renew_before_days, args.cluster_domain)
+        if args.random_secret:
+            from ..nodeagent.auth import ensure_token_secret
+
+            ns = args.namespace or namespace_from_env()
+            out["tokens"] = {n: await ensure_token_secret(client, ns, n) for n in args.random_secret}
     finally:
         await client.close()
     print(json.dumps(out), flush=True)

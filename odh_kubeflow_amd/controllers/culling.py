@@ -89,6 +89,7 @@ class CullerConfig:
     activity_source: str = "jupyter"
     gpu_busy_threshold: float = 5.0
     gpu_agent_port: int = 9464
+    gpu_agent_token_file: str = ""  # bearer token for the node agent (nodeagent/auth.py); "" = none
     gpu_vram_active_bytes: float = 0.0  # 0: resident VRAM is not activity (see module docstring)
     http_timeout_s: float = 10.0
 
@@ -116,6 +117,7 @@ class CullerConfig:
             raise ValueError(f"CULLING_ACTIVITY_SOURCE must be jupyter|amdgpu|combined, got {c.activity_source}")
         c.gpu_busy_threshold = float(env_default(env, "CULLING_GPU_BUSY_THRESHOLD", "5"))
         c.gpu_agent_port = int(env_default(env, "CULLING_GPU_AGENT_PORT", "9464"))
+        c.gpu_agent_token_file = env.get("CULLING_GPU_AGENT_TOKEN_FILE", "")
         c.gpu_vram_active_bytes = float(env_default(env, "CULLING_GPU_VRAM_ACTIVE_BYTES", "0"))
         return c
 
@@ -341,8 +343,13 @@ class NodeAgentActivity(GpuActivity):
     """
 
     def __init__(self, port: int = 9464, timeout_s: float = 2.0,
-                 endpoint_for: Optional[Callable[[dict], Optional[str]]] = None):
+                 endpoint_for: Optional[Callable[[dict], Optional[str]]] = None, token_file: str = ""):
         self.port = port
+        self.token = None
+        if token_file:
+            from ..nodeagent.auth import TokenFile
+
+            self.token = TokenFile(token_file)
         self.timeout_s = timeout_s
         self.endpoint_for = endpoint_for or self.default_endpoint
         self._session = None
@@ -366,7 +373,8 @@ class NodeAgentActivity(GpuActivity):
                                     "window": window_s})
         self.requests += 1
         try:
-            async with self._session.get(f"http://{ep}/gpu/activity?{q}") as resp:
+            headers = self.token.header() if self.token is not None else None
+            async with self._session.get(f"http://{ep}/gpu/activity?{q}", headers=headers) as resp:
                 if resp.status != 200:
                     return None
                 data = await resp.json()
@@ -394,7 +402,7 @@ class CullingReconciler:
         self.cfg = config or CullerConfig.from_env(self.env)
         self.gpu: Optional[GpuActivity] = activity
         if self.gpu is None and self.cfg.activity_source in ("amdgpu", "combined"):
-            self.gpu = NodeAgentActivity(port=self.cfg.gpu_agent_port)
+            self.gpu = NodeAgentActivity(port=self.cfg.gpu_agent_port, token_file=self.cfg.gpu_agent_token_file)
         self.jupyter = jupyter or JupyterActivity(self.cfg, use_pod_endpoint=self.env.get(
             "CULLER_USE_POD_ENDPOINT", "false") == "true")
         self.culled = 0

@@ -50,6 +50,8 @@ ROCM_NOTEBOOK_IMAGE = "rocm/pytorch:rocm7.0_ubuntu22.04_py3.10_pytorch_release_2
 NAME_PREFIX = "odh-kubeflow-amd-"
 WEBHOOK_CERT_SECRET = "odh-notebook-controller-webhook-cert"  # created by service-ca / the certs Job
 WEBHOOK_SERVICE = "odh-notebook-controller-webhook-service"
+AGENT_TOKEN_SECRET = "mi355x-node-agent-token"  # nodeagent/auth.py TOKEN_SECRET
+AGENT_TOKEN_MOUNT = "/var/run/secrets/odh/node-agent"
 MWC_NAME = "mutating-webhook-configuration"
 SHARDS = 8  # one control-plane shard per MI355X of an 8-GPU node
 CULLER_LITERALS = ["ENABLE_CULLING=false", "CULL_IDLE_TIME=1440", "IDLENESS_CHECK_PERIOD=1",
@@ -199,7 +201,20 @@ RESTRICTED = {"allowPrivilegeEscalation": False, "capabilities": {"drop": ["ALL"
 
 def _culler_env() -> List[dict]:
     return [{"name": k, "valueFrom": {"configMapKeyRef": {"name": "notebook-controller-culler-config",
-                                                          "key": k, "optional": True}}} for k in CULLER_KEYS]
+                                                          "key": k, "optional": True}}} for k in CULLER_KEYS] + [
+        {"name": "CULLING_GPU_AGENT_TOKEN_FILE", "value": f"{AGENT_TOKEN_MOUNT}/token"}]
+
+
+def _agent_token_volume() -> dict:
+    """The node agent / culler shared bearer token (``nodeagent/auth.py``).  Optional: until the
+    Secret exists (``cmd/webhook_certs --random-secret`` writes it in the standalone / mi355x
+    overlays; an admin elsewhere) the agent refuses data requests and the culler gets no GPU
+    data — never idleness.  The kubelet fills the volume once the Secret appears."""
+    return {"name": "node-agent-token", "secret": {"secretName": AGENT_TOKEN_SECRET, "optional": True,
+                                                   "defaultMode": 0o444}}
+
+
+AGENT_TOKEN_MOUNT_SPEC = {"name": "node-agent-token", "mountPath": AGENT_TOKEN_MOUNT, "readOnly": True}
 
 
 def kf_deployment() -> dict:
@@ -210,12 +225,14 @@ def kf_deployment() -> dict:
          "env": _culler_env(),
          "ports": [{"name": "metrics", "containerPort": 8080}, {"name": "probes", "containerPort": 8081}],
          "resources": {"requests": {"cpu": "500m", "memory": "256Mi"}, "limits": {"cpu": "2", "memory": "2Gi"}},
+         "volumeMounts": [dict(AGENT_TOKEN_MOUNT_SPEC)],
          "securityContext": dict(RESTRICTED), **_probes()}
     return {"apiVersion": "apps/v1", "kind": "Deployment",
             "metadata": {"name": "deployment", "labels": {"app": "notebook-controller"}},
             "spec": {"replicas": 1, "selector": {"matchLabels": {"app": "notebook-controller"}},
                      "template": {"metadata": {"labels": {"app": "notebook-controller"}},
-                                  "spec": {"serviceAccountName": "service-account", "containers": [c]}}}}
+                                  "spec": {"serviceAccountName": "service-account", "containers": [c],
+                                           "volumes": [_agent_token_volume()]}}}}
 
 
 def odh_deployment() -> dict:
@@ -254,14 +271,15 @@ def node_agent_daemonset() -> dict:
          "command": ["python", "-m", "odh_kubeflow_amd.cmd.node_agent"],
          "args": ["--port=9464", "--sysfs-root=/host/sys", "--proc-root=/host/proc",
                   "--pod-resources-socket=/var/lib/kubelet/pod-resources/kubelet.sock",
-                  "--device-plugin-checkpoint=/var/lib/kubelet/device-plugins/kubelet_internal_checkpoint"],
+                  "--device-plugin-checkpoint=/var/lib/kubelet/device-plugins/kubelet_internal_checkpoint",
+                  f"--token-file={AGENT_TOKEN_MOUNT}/token"],
          "ports": [{"name": "gpu-activity", "containerPort": 9464, "hostPort": 9464}],
          "livenessProbe": {"httpGet": {"path": "/healthz", "port": 9464}, "periodSeconds": 20},
          "volumeMounts": [{"name": "sys", "mountPath": "/host/sys", "readOnly": True},
                           {"name": "proc", "mountPath": "/host/proc", "readOnly": True},
                           {"name": "pod-resources", "mountPath": "/var/lib/kubelet/pod-resources"},
                           {"name": "device-plugins", "mountPath": "/var/lib/kubelet/device-plugins",
-                           "readOnly": True}],
+                           "readOnly": True}, dict(AGENT_TOKEN_MOUNT_SPEC)],
          "securityContext": {"readOnlyRootFilesystem": True, "allowPrivilegeEscalation": False,
                              "capabilities": {"drop": ["ALL"]}},
          "resources": {"requests": {"cpu": "50m", "memory": "128Mi"}, "limits": {"memory": "512Mi"}}}
@@ -280,7 +298,8 @@ def node_agent_daemonset() -> dict:
                                                        {"name": "pod-resources", "hostPath": {
                                                            "path": "/var/lib/kubelet/pod-resources"}},
                                                        {"name": "device-plugins", "hostPath": {
-                                                           "path": "/var/lib/kubelet/device-plugins"}}]}}}}
+                                                           "path": "/var/lib/kubelet/device-plugins"}},
+                                                       _agent_token_volume()]}}}}
 
 
 CONFORMANCE_NS = "odh-kubeflow-amd-conformance"
@@ -363,7 +382,7 @@ def webhook_certs_args(services: List[str], mwcs: List[str]) -> List[str]:
     """``cmd/webhook_certs.py`` arguments.  Names are the *rendered* (prefixed) names: they
     are plain strings to kustomize, so its name-reference fix-ups do not reach them."""
     return ([f"--secret-name={WEBHOOK_CERT_SECRET}"] + [f"--service-name={x}" for x in services]
-            + [f"--mwc-name={x}" for x in mwcs])
+            + [f"--mwc-name={x}" for x in mwcs] + [f"--random-secret={AGENT_TOKEN_SECRET}"])
 
 
 def webhook_certs_docs(services: List[str], mwcs: List[str]) -> Dict[str, object]:
@@ -428,7 +447,8 @@ def control_plane_statefulset(shards: int) -> dict:
          "ports": [{"name": "webhook", "containerPort": 8443}, {"name": "metrics", "containerPort": 8080},
                    {"name": "probes", "containerPort": 8081}],
          "resources": {"requests": {"cpu": "500m", "memory": "256Mi"}, "limits": {"cpu": "2", "memory": "2Gi"}},
-         "volumeMounts": [{"name": "cert", "mountPath": "/tmp/k8s-webhook-server/serving-certs", "readOnly": True}],
+         "volumeMounts": [{"name": "cert", "mountPath": "/tmp/k8s-webhook-server/serving-certs", "readOnly": True},
+                          dict(AGENT_TOKEN_MOUNT_SPEC)],
          "securityContext": dict(RESTRICTED), **_probes()}
     labels = {"app": "notebook-control-plane"}
     return {"apiVersion": "apps/v1", "kind": "StatefulSet", "metadata": {"name": "control-plane", "labels": labels},
@@ -437,7 +457,8 @@ def control_plane_statefulset(shards: int) -> dict:
                      "template": {"metadata": {"labels": labels},
                                   "spec": {"serviceAccountName": "control-plane", "containers": [c],
                                            "volumes": [{"name": "cert", "secret": {
-                                               "secretName": WEBHOOK_CERT_SECRET, "defaultMode": 420}}]}}}}
+                                               "secretName": WEBHOOK_CERT_SECRET, "defaultMode": 420}},
+                                                       _agent_token_volume()]}}}}
 
 
 def _webhook_svc(name: str, selector: dict) -> dict:

@@ -16,6 +16,9 @@ of a pod's node at ``<pod.status.hostIP>:9464``):
 * ``GET /gpu/activity?devices=0,3&window=<s>`` — explicit telemetry indices (debugging);
 * ``GET /gpu/pods`` — the attribution tables and per-source health;
 * ``GET /gpu/devices``, ``GET /healthz``, ``GET /metrics`` (Prometheus text).
+
+With a token file (``--token-file``, :mod:`.auth`) every endpoint but ``/healthz`` needs
+``Authorization: Bearer <token>`` and answers 401 otherwise.
 """
 
 from __future__ import annotations
@@ -53,8 +56,11 @@ def aggregate_windows(telemetry, indices: Sequence[Optional[int]], window_s: flo
 
 
 class NodeTelemetryAgent:
-    def __init__(self, telemetry, attributor=None, host: str = "0.0.0.0", port: int = DEFAULT_PORT):
+    def __init__(self, telemetry, attributor=None, host: str = "0.0.0.0", port: int = DEFAULT_PORT,
+                 token=None):
         self.telemetry = telemetry
+        self.token = token  # nodeagent.auth.TokenFile, or None: unauthenticated
+        self.refused = 0
         self.attributor = attributor
         self.host = host
         self.port = port
@@ -94,7 +100,10 @@ class NodeTelemetryAgent:
         lines += vram
         lines += ["# HELP odh_node_agent_activity_queries_total Culler activity queries served.",
                   "# TYPE odh_node_agent_activity_queries_total counter",
-                  f"odh_node_agent_activity_queries_total {self.queries}"]
+                  f"odh_node_agent_activity_queries_total {self.queries}",
+                 "# HELP odh_node_agent_unauthorized_total Requests refused for a missing or wrong token.",
+                 "# TYPE odh_node_agent_unauthorized_total counter",
+                 f"odh_node_agent_unauthorized_total {self.refused}"]
         return "\n".join(lines) + "\n"
 
     async def start(self) -> "NodeTelemetryAgent":
@@ -104,6 +113,8 @@ class NodeTelemetryAgent:
             q = req.query
             try:
                 window = float(q.get("window") or 60)
+                if not 0 < window <= 86400:  # also refuses nan / inf
+                    raise ValueError(window)
                 devs = [int(x) for x in (q.get("devices") or "").split(",") if x.strip() != ""]
             except ValueError:
                 return web.json_response({"error": "bad query"}, status=400)
@@ -132,7 +143,16 @@ class NodeTelemetryAgent:
         async def metrics(_req):
             return web.Response(text=self.metrics_text(), content_type="text/plain")
 
-        app = web.Application()
+        @web.middleware
+        async def auth(req, handler):
+            if self.token is not None and req.path != "/healthz" and \
+                    not self.token.authorizes(req.headers.get("Authorization")):
+                self.refused += 1
+                return web.json_response({"error": "unauthorized"}, status=401,
+                                         headers={"WWW-Authenticate": "Bearer"})
+            return await handler(req)
+
+        app = web.Application(middlewares=[auth])
         app.router.add_get("/gpu/activity", activity)
         app.router.add_get("/gpu/pods", pods)
         app.router.add_get("/gpu/devices", devices)

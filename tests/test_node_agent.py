@@ -315,3 +315,89 @@ def test_shipped_manifests_have_no_kubelet_stand_in():
         imported += [a.name for n in ast.walk(tree) if isinstance(n, ast.Import) for a in n.names]
         for name in imported:
             assert not any(x in name for x in ("kubelet", "runtime", "apiserver")), (mod.__name__, name)
+
+
+def _get_auth(url, token=None):
+    req = urllib.request.Request(url, headers={"Authorization": f"Bearer {token}"} if token else {})
+    try:
+        with urllib.request.urlopen(req, timeout=5) as r:
+            return r.status, r.read().decode()
+    except urllib.error.HTTPError as e:
+        return e.code, e.read().decode()
+
+
+def test_agent_token_required_and_rotated(run, sysfs, tmp_path):
+    """With --token-file, /gpu/* and /metrics need the bearer token (401 otherwise), /healthz
+    stays open; a rotated file takes effect without a restart; a missing file fails closed."""
+    from odh_kubeflow_amd.nodeagent.auth import TokenFile
+
+    root, proc, minors, tel = sysfs
+    cp = CheckpointWriter(str(tmp_path / "dp" / "cp"))
+    cp.allocate(UID_A, "nb", [fake_bdf(1)])
+    set_fake_counter(root, minors[1], busy=40)
+    tok = tmp_path / "token"
+    tok.write_text("s3cret\n")
+
+    async def go():
+        agent = await NodeTelemetryAgent(tel, Attributor(tel, checkpoint_path=cp.path, ttl_s=0.0), host="127.0.0.1",
+                                         port=0, token=TokenFile(str(tok), recheck_s=0.0)).start()
+        try:
+            base = f"http://127.0.0.1:{agent.port}"
+            act = f"{base}/gpu/activity?pod_uid={UID_A}&window=0.05"
+            assert (await asyncio.to_thread(_get_auth, f"{base}/healthz"))[0] == 200
+            for path in (act, f"{base}/gpu/pods", f"{base}/gpu/devices", f"{base}/metrics"):
+                assert (await asyncio.to_thread(_get_auth, path))[0] == 401
+                assert (await asyncio.to_thread(_get_auth, path, "wrong"))[0] == 401
+                assert (await asyncio.to_thread(_get_auth, path, "s3cret"))[0] == 200
+            st, body = await asyncio.to_thread(_get_auth, act, "s3cret")
+            assert json.loads(body)["devices"] == [fake_bdf(1)]
+            # rotation (the kubelet swaps the Secret volume's files in place)
+            tok.write_text("n3w-token")
+            os.utime(tok, ns=(time.time_ns() + 10**9, time.time_ns() + 10**9))
+            assert (await asyncio.to_thread(_get_auth, act, "s3cret"))[0] == 401
+            assert (await asyncio.to_thread(_get_auth, act, "n3w-token"))[0] == 200
+            # missing / empty token file: every data request refused
+            tok.unlink()
+            assert (await asyncio.to_thread(_get_auth, act, "n3w-token"))[0] == 401
+            tok.write_text("")
+            assert (await asyncio.to_thread(_get_auth, act, ""))[0] == 401
+            assert agent.refused >= 10
+            # a bad window is a 400, not a crash
+            tok.write_text("t")
+            assert (await asyncio.to_thread(_get_auth, f"{base}/gpu/activity?pod_uid={UID_A}&window=nan", "t"))[0] == 400
+        finally:
+            await agent.stop()
+    run(go())
+
+
+def test_culler_sends_agent_token(run, sysfs, tmp_path):
+    """The culler's node-agent client reads CULLING_GPU_AGENT_TOKEN_FILE: with the right token it
+    gets GPU data; with none it gets no data (None: never idleness)."""
+    from odh_kubeflow_amd.controllers import culling as c
+    from odh_kubeflow_amd.nodeagent.auth import TokenFile
+
+    root, proc, minors, tel = sysfs
+    cp = CheckpointWriter(str(tmp_path / "dp" / "cp"))
+    cp.allocate(UID_A, "nb", [fake_bdf(2)])
+    set_fake_counter(root, minors[2], busy=70)
+    tok = tmp_path / "token"
+    tok.write_text("abc")
+    pod = {"metadata": {"name": "nb-0", "namespace": "u", "uid": UID_A}, "status": {"hostIP": "127.0.0.1"}}
+
+    async def go():
+        agent = await NodeTelemetryAgent(tel, Attributor(tel, checkpoint_path=cp.path, ttl_s=0.0), host="127.0.0.1",
+                                         port=0, token=TokenFile(str(tok))).start()
+        good = c.NodeAgentActivity(port=agent.port, token_file=str(tok))
+        none = c.NodeAgentActivity(port=agent.port)
+        try:
+            await asyncio.sleep(0.1)
+            got = await good.busy(pod, 0.05)
+            assert got is not None and got["busy_mean"] == 70
+            assert await none.busy(pod, 0.05) is None
+            cfg = c.CullerConfig.from_env({"CULLING_GPU_AGENT_TOKEN_FILE": str(tok)})
+            assert cfg.gpu_agent_token_file == str(tok)
+        finally:
+            await good.close()
+            await none.close()
+            await agent.stop()
+    run(go())

@@ -153,3 +153,25 @@ def test_e2e_admission_after_provisioning(tmp_path, run):
             except subprocess.TimeoutExpired:
                 p.kill()
         logf.close()
+
+
+def test_provision_node_agent_token_secret(run):
+    """cmd/webhook_certs --random-secret: the node agent / culler token Secret is created once
+    with a random token and never rotated by a re-run (the agents would lose each other)."""
+    from odh_kubeflow_amd.nodeagent.auth import TOKEN_SECRET, ensure_token_secret
+
+    async def go():
+        store = ObjectStore()
+        cli = Manager.in_process(store, name="certs").client
+        await cli.create({"apiVersion": "v1", "kind": "Namespace", "metadata": {"name": "opendatahub"}})
+        assert await ensure_token_secret(cli, "opendatahub") == "created"
+        sec = await cli.get(kinds.SECRET, TOKEN_SECRET, "opendatahub")
+        tok = base64.b64decode(sec["data"]["token"])
+        assert len(tok) >= 32
+        assert await ensure_token_secret(cli, "opendatahub") == "kept"
+        assert (await cli.get(kinds.SECRET, TOKEN_SECRET, "opendatahub"))["data"]["token"] == sec["data"]["token"]
+        sec = await cli.get(kinds.SECRET, TOKEN_SECRET, "opendatahub")
+        sec["data"] = {}
+        await cli.update(sec)
+        assert await ensure_token_secret(cli, "opendatahub") == "filled"
+    run(go())

@@ -475,7 +475,6 @@ class GpuRuntime:
             await self.runtime.stop(h)
         self.handles.clear()
         await self.runtime.close()  # containers whose start was interrupted
-        await self.runtime.close()
 
     def setup_with_manager(self, mgr, max_concurrent: int = 8, name: Optional[str] = None):
         mine = pred_funcs(create=lambda o: (o.get("spec") or {}).get("nodeName") == self.node_name,

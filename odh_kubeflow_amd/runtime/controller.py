@@ -234,8 +234,8 @@ class Controller:
                             if own is not None and r == own:
                                 continue
                             self.enqueue(r, trig)
-                except Exception:
-                    pass
+                except Exception:  # the new object's mapping was enqueued; report, do not drop the event
+                    log.warning("%s: mapping the previous state of a %s failed", self.name, trig, exc_info=True)
 
         return on_event
 

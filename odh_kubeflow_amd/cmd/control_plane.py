@@ -48,7 +48,8 @@ def parse(argv: Optional[List[str]] = None) -> argparse.Namespace:
     add_shard_flags(p)
     p.add_argument("--shard-count", type=int, default=0, help="number of shards (for --assign-namespaces)")
     p.add_argument("--assign-namespaces", action="store_true",
-                   help="shard 0 labels unlabelled namespaces crc32(name) %% --shard-count")
+                   help="label unlabelled namespaces crc32(name) %% --shard-count (with --shard K: only those "
+                        "that hash to K, so every shard claims its own)")
     p.add_argument("--metrics-bind-address", default=":8080")
     p.add_argument("--health-probe-bind-address", default=":8081")
     p.add_argument("--kube-rbac-proxy-image", default="")
@@ -123,10 +124,11 @@ def build(args, env=os.environ):
         mgr.kf_reconcilers = setup_kf(mgr, env, reference_emulation=emu)
     if "odh" in args.controller_set:
         mgr.odh_reconciler = setup_odh(mgr, namespace, env, shard=shard, reference_emulation=emu)
-    if args.assign_namespaces and shard in (None, "0"):
+    if args.assign_namespaces:
         from ..controllers.sharding import NamespaceShardAssigner
 
-        mgr.assigner = NamespaceShardAssigner(mgr.client, mgr.reader, args.shard_count, exclude=[namespace])
+        mgr.assigner = NamespaceShardAssigner(mgr.client, mgr.reader, args.shard_count, exclude=[namespace],
+                                              only_shard=shard)
         mgr.assigner.setup_with_manager(mgr)
     mgr.webhook_server = None
     if "webhook" in args.controller_set:

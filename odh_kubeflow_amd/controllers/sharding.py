@@ -8,9 +8,10 @@ only those namespaces (plus the controller namespace), and its admission webhook
 called only for them (one MutatingWebhookConfiguration per shard, ``namespaceSelector``
 on the same label).
 
-A namespace nobody labelled would belong to no shard, so shard 0 runs this assigner: it
-labels every unlabelled namespace ``crc32(name) % N`` (stable across restarts and
-replicas, so concurrent assigners agree).  Administrators pin a namespace to a shard —
+A namespace nobody labelled would belong to no shard, so every shard runs this assigner
+for itself: shard k labels the unlabelled namespaces whose ``crc32(name) % N`` is k (stable
+across restarts and replicas, so assigners never disagree, and a namespace waits only for
+the shard that will own it).  Administrators pin a namespace to a shard —
 e.g. to keep a team's notebooks on the shard co-located with its GPUs — by setting the
 label themselves; an existing label is never changed.  Until the label lands, the
 ``…-unassigned`` webhook configuration (``DoesNotExist`` selector, served by every shard)
@@ -21,7 +22,7 @@ from __future__ import annotations
 
 import logging
 import zlib
-from typing import Iterable
+from typing import Iterable, Optional
 
 from ..models import kinds
 from ..models import meta as m
@@ -40,17 +41,28 @@ def shard_for(namespace: str, shard_count: int) -> str:
 
 
 class NamespaceShardAssigner:
-    def __init__(self, client, reader, shard_count: int, exclude: Iterable[str] = ()):
+    """Labels unlabelled namespaces ``crc32(name) % shard_count``.
+
+    ``only_shard=k``: label only the namespaces that hash to shard ``k``.  Every shard runs
+    one of these for itself, so a namespace is claimed by the shard that will own it, and no
+    single replica is needed to bring new namespaces under management (with one assigner on
+    replica 0, a namespace created while replica 0 was down waited for it, whichever shard
+    it hashed to).  ``None``: label every namespace (one assigner for all shards)."""
+
+    def __init__(self, client, reader, shard_count: int, exclude: Iterable[str] = (),
+                 only_shard: Optional[str] = None):
         self.client = client
         self.reader = reader
         self.shard_count = int(shard_count)
         self.exclude = set(exclude)
+        self.only_shard = only_shard
         self.assigned = 0
 
     def wants(self, ns: dict) -> bool:
         name = m.name(ns)
         return (SHARD_LABEL not in m.labels(ns) and not m.is_deleting(ns) and name not in self.exclude
-                and not name.startswith(EXCLUDED_PREFIXES))
+                and not name.startswith(EXCLUDED_PREFIXES)
+                and (self.only_shard is None or shard_for(name, self.shard_count) == self.only_shard))
 
     async def reconcile(self, req: Request) -> Result:
         ns = self.reader.get(kinds.NAMESPACE, req.name)

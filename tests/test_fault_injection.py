@@ -384,7 +384,7 @@ def test_admission_path_resets_converge(tmp_path, run):
 
 def test_sharded_control_plane_follows_new_namespaces_through_resets(tmp_path, run):
     """Two ``cmd/control_plane`` shards reach the apiserver through the resetting proxy while
-    new namespaces keep appearing: the assigner labels each one (shard 0), the owning shard's
+    new namespaces keep appearing: the owning shard's assigner labels each one, the owning shard's
     label-selected Namespace watch adds a per-namespace informer group for it — across
     dropped watches and relists — and every notebook in every namespace becomes Ready."""
     from odh_kubeflow_amd.models import meta as m

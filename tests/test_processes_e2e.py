@@ -353,7 +353,7 @@ def test_kf_manager_leader_failover(tmp_path, run):
 
 def test_sharded_control_plane_processes(tmp_path, run):
     """The mi355x-sharded deployment as processes: two ``cmd/control_plane.py`` shards
-    (shard 0 assigns unlabelled namespaces), one MutatingWebhookConfiguration per shard plus
+    (each shard labels the unlabelled namespaces that hash to it), one MutatingWebhookConfiguration per shard plus
     the unassigned-namespace one, the dev apiserver and kubelet stand-in.  Notebooks in
     namespaces the assigner put on different shards both become Ready, each shard labels its
     own HTTPRoutes; with shard 1 down its namespace's admissions fail (failurePolicy Fail)
@@ -409,7 +409,7 @@ def test_sharded_control_plane_processes(tmp_path, run):
             async def labelled():
                 got = [m.labels(await c.get(kinds.NAMESPACE, ns)).get("notebooks.amd.com/shard") for ns in (ns0, ns1)]
                 return got == ["0", "1"]
-            await eventually(labelled, 30)  # shard 0's assigner
+            await eventually(labelled, 30)  # the owning shard's assigner
 
             async def ready(ns, nm="nb"):
                 st = (await c.get(kinds.NOTEBOOK, nm, ns)).get("status") or {}

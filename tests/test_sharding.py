@@ -313,6 +313,42 @@ def test_namespace_shard_assigner(run):
     run(go())
 
 
+def test_each_shard_assigns_only_its_own_namespaces(run):
+    """--assign-namespaces on every shard: shard k labels exactly the unlabelled namespaces that
+    hash to k, so no replica is needed for namespaces it will not own; with shard 1 absent its
+    namespaces stay unlabelled (they wait for their owner), everyone else's are labelled."""
+    from odh_kubeflow_amd.controllers.sharding import NamespaceShardAssigner, shard_for
+    from odh_kubeflow_amd.runtime.manager import Manager
+
+    names = [f"team-{i}" for i in range(24)]
+
+    async def go():
+        store = ObjectStore()
+        mgrs, assigners = [], []
+        for k in ("0", "2"):  # shards 0 and 2 of 3 up, shard 1 down
+            mgr = Manager.in_process(store, name=f"cp-{k}")
+            a = NamespaceShardAssigner(mgr.client, mgr.reader, 3, exclude=["opendatahub"], only_shard=k)
+            a.setup_with_manager(mgr)
+            await mgr.start()
+            mgrs.append(mgr)
+            assigners.append(a)
+        try:
+            for ns in names:
+                await store.create({"apiVersion": "v1", "kind": "Namespace", "metadata": {"name": ns}})
+            for mgr in mgrs:
+                assert await mgr.wait_idle(5, settle=0.05)
+            for ns in names:
+                got = m.labels(store.peek(kinds.NAMESPACE, ns)).get("notebooks.amd.com/shard")
+                want = shard_for(ns, 3)
+                assert got == (None if want == "1" else want), ns
+            owned = {k: sum(1 for ns in names if shard_for(ns, 3) == k) for k in ("0", "2")}
+            assert [a.assigned for a in assigners] == [owned["0"], owned["2"]] and all(owned.values())
+        finally:
+            for mgr in mgrs:
+                await mgr.stop()
+    run(go())
+
+
 def test_control_plane_flags(tmp_path):
     from odh_kubeflow_amd.cmd import control_plane
     from odh_kubeflow_amd.cmd.common import resolve_shard

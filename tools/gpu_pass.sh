@@ -81,7 +81,10 @@ for s in $steps; do
     prof)
       timeout -k 10 200 rocprofv3 --kernel-trace --stats -d "$out/prof" -o run -- \
         python3 bench.py --steps 40 --warmup 3 > "$out/bench_prof.log" 2>&1 || fail prof $? "$out/bench_prof.log"
-      find "$out/prof" -name '*kernel_stats*' | head -3 ;;
+      db=$(find "$out/prof" -name '*results.db' | head -1)
+      if [ -n "$db" ]; then
+        python3 tools/rocpd_stats.py "$db" > "$out/bench_kernel_stats.csv" && head -4 "$out/bench_kernel_stats.csv"
+      fi ;;
     pmc)
       # one counter group per pass, each within the per-block limits
       i=0

@@ -102,3 +102,35 @@ def test_ci_workflows_reference_existing_targets_and_paths():
                 cfg = (step.get("with") or {}).get("config")
                 if cfg:
                     assert os.path.exists(os.path.join(root, cfg)), (n, cfg)
+
+
+def test_third_party_imports_are_declared():
+    """Every third-party module the package imports (lazy imports included) is a declared
+    dependency and installed in the controller / node-agent image; torch comes with the ROCm
+    base image.  (grpcio was missing: the node agent's pod-resources source would have reported
+    an import error on every node and fallen back to the checkpoint.)"""
+    import ast
+    import sys
+
+    pkg = os.path.join(ROOT, "odh_kubeflow_amd")
+    mods = set()
+    for root, _, files in os.walk(pkg):
+        for f in files:
+            if f.endswith(".py"):
+                with open(os.path.join(root, f)) as fh:
+                    tree = ast.parse(fh.read())
+                for n in ast.walk(tree):
+                    if isinstance(n, ast.Import):
+                        mods.update(a.name.split(".")[0] for a in n.names)
+                    elif isinstance(n, ast.ImportFrom) and n.level == 0 and n.module:
+                        mods.add(n.module.split(".")[0])
+    third = {m for m in mods if m not in sys.stdlib_module_names} - {"odh_kubeflow_amd", "bench", "torch"}
+    dist = {"yaml": "pyyaml", "grpc": "grpcio"}
+    with open(os.path.join(ROOT, "pyproject.toml")) as f:
+        pyproject = f.read()
+    with open(os.path.join(ROOT, "images", "Dockerfile")) as f:
+        docker = f.read()
+    for m in sorted(third):
+        d = dist.get(m, m)
+        assert f'"{d}"' in pyproject, f"{d} missing from pyproject dependencies"
+        assert f" {d}" in docker, f"{d} not installed in images/Dockerfile"

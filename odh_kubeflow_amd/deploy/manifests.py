@@ -280,8 +280,11 @@ def node_agent_daemonset() -> dict:
                           {"name": "pod-resources", "mountPath": "/var/lib/kubelet/pod-resources"},
                           {"name": "device-plugins", "mountPath": "/var/lib/kubelet/device-plugins",
                            "readOnly": True}, dict(AGENT_TOKEN_MOUNT_SPEC)],
-         "securityContext": {"readOnlyRootFilesystem": True, "allowPrivilegeEscalation": False,
-                             "capabilities": {"drop": ["ALL"]}},
+         # uid 0 explicitly: the image runs as 65532, and the kubelet's pod-resources socket is
+         # root-owned 0660 (no capability is needed for that: owner permissions; every
+         # capability stays dropped)
+         "securityContext": {"runAsUser": 0, "runAsNonRoot": False, "readOnlyRootFilesystem": True,
+                             "allowPrivilegeEscalation": False, "capabilities": {"drop": ["ALL"]}},
          "resources": {"requests": {"cpu": "50m", "memory": "128Mi"}, "limits": {"memory": "512Mi"}}}
     return {"apiVersion": "apps/v1", "kind": "DaemonSet",
             "metadata": {"name": "mi355x-node-agent", "labels": {"app": "mi355x-node-agent"}},

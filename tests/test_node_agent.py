@@ -294,6 +294,11 @@ def test_shipped_manifests_have_no_kubelet_stand_in():
     mounts = {v["mountPath"]: v for v in c["volumeMounts"]}
     assert mounts["/host/sys"]["readOnly"] and mounts["/host/proc"]["readOnly"]
     assert "/dev/kfd" not in mounts and "/dev/dri" not in mounts
+    # uid 0 (the image's user is 65532; the pod-resources socket is root-owned 0660), no capabilities
+    sc = c["securityContext"]
+    assert sc["runAsUser"] == 0 and sc["capabilities"] == {"drop": ["ALL"]} and not sc["allowPrivilegeEscalation"]
+    assert sc["readOnlyRootFilesystem"] and not sc.get("privileged")
+    assert any(a.startswith("--token-file=") for a in c["args"])
     # no RBAC at all for the agent: it cannot write a Node or pods/status
     for path, doc in t.items():
         for d in doc if isinstance(doc, list) else [doc]:

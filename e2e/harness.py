@@ -253,7 +253,7 @@ class LocalHarness(Harness):
         from odh_kubeflow_amd.webhook.certs import generate
         from odh_kubeflow_amd.webhook.server import mutating_webhook_configuration
 
-        self._spawn("apiserver", ["odh_kubeflow_amd.cmd.apiserver", "--port", str(self.api_port), "--controllers",
+        self._spawn("apiserver", ["odh_kubeflow_amd.testing.cmd.apiserver", "--port", str(self.api_port), "--controllers",
                                   "--no-openshift-apis"])
         certs = generate(("127.0.0.1", "localhost"), os.path.join(self.workdir, "certs"))
         self._wait_http(self.master + "/healthz")
@@ -269,7 +269,7 @@ class LocalHarness(Harness):
                             "quay.io/brancz/kube-rbac-proxy:v0.18.1", "--webhook-cert-dir", certs.cert_dir,
                             "--webhook-port", str(self.wh_port), "--webhook-host", "127.0.0.1", "--leader-elect"],
                     self.common)
-        self._spawn("kubelet", ["odh_kubeflow_amd.cmd.fake_kubelet", "--master", self.master, "--jupyter",
+        self._spawn("kubelet", ["odh_kubeflow_amd.testing.cmd.fake_kubelet", "--master", self.master, "--jupyter",
                                 "--checkpoint-path", os.path.join(self.workdir, "dp", "cp")], self.common)
         self._wait_http(f"https://127.0.0.1:{self.wh_port}/healthz")
         self.run(self.client.create(mutating_webhook_configuration(

@@ -78,3 +78,28 @@ def resolve_shard(value, env=None):
     if not re.fullmatch(r"[A-Za-z0-9]([-A-Za-z0-9_.]*[A-Za-z0-9])?", value) or len(value) > 63:
         raise SystemExit(f"--shard={value!r} is not a valid label value")
     return value
+
+
+def add_debug_flags(p) -> None:
+    """``--enable-debug-endpoints``: ``/debug/reconciles`` and ``/debug/quiesce`` on the
+    metrics server (see :meth:`~odh_kubeflow_amd.runtime.manager.Manager.quiesce`)."""
+    p.add_argument("--enable-debug-endpoints", action="store_true",
+                   help="serve /debug/reconciles and /debug/quiesce on the metrics address (benchmarks, e2e)")
+
+
+async def run_announcing_ready(mgr, stop) -> int:
+    """``mgr.run_until(stop)``, printing ``ready`` on stdout once the servers are up and this
+    replica leads (its informers synced and controllers started): the start-up handshake the
+    benchmark and the multi-process tests wait for."""
+    import asyncio
+
+    async def announce():
+        await mgr.started_event().wait()
+        await mgr.elected.wait()
+        print("ready", flush=True)
+
+    t = asyncio.ensure_future(announce())
+    try:
+        return await mgr.run_until(stop)
+    finally:
+        t.cancel()

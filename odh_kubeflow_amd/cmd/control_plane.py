@@ -39,13 +39,14 @@ ALL_CONTROLLERS = ("kf", "odh", "webhook")
 
 
 def parse(argv: Optional[List[str]] = None) -> argparse.Namespace:
-    from .common import add_shard_flags
+    from .common import add_debug_flags, add_shard_flags
 
     p = argparse.ArgumentParser(prog="notebook-control-plane")
     p.add_argument("--controllers", default="kf,odh,webhook",
                    help="comma list of kf (notebook + event re-emitter + culler when ENABLE_CULLING=true), "
                         "odh (OpenshiftNotebookReconciler), webhook (odh mutating webhook)")
     add_shard_flags(p)
+    add_debug_flags(p)
     p.add_argument("--shard-count", type=int, default=0, help="number of shards (for --assign-namespaces)")
     p.add_argument("--assign-namespaces", action="store_true",
                    help="label unlabelled namespaces crc32(name) %% --shard-count (with --shard K: only those "
@@ -117,7 +118,8 @@ def build(args, env=os.environ):
     mgr = Manager.remote(cfg, name=name, uncached=uncached, transforms=transforms,
                          cache_options=shard_cache_options(shard, namespace),
                          default_max_concurrent=args.max_concurrent_reconciles, leader_elector=elector,
-                         metrics_addr=args.metrics_bind_address, probe_addr=args.health_probe_bind_address)
+                         metrics_addr=args.metrics_bind_address, probe_addr=args.health_probe_bind_address,
+                         debug_endpoints=args.enable_debug_endpoints)
     mgr.shard = shard
     emu = args.reference_emulation
     if "kf" in args.controller_set:
@@ -150,24 +152,13 @@ def build(args, env=os.environ):
 
 
 async def amain(argv=None) -> int:
-    from .common import setup_logging, signal_event
+    from .common import run_announcing_ready, setup_logging, signal_event
 
     args = parse(argv)
     setup_logging(debug=args.debug_log, development=args.debug_log)
     mgr = build(args)
     log.info("starting control plane %s (controllers: %s)", mgr.name, ",".join(args.controller_set))
-    stop = signal_event()
-
-    async def announce():
-        await mgr.started_event().wait()
-        await mgr.elected.wait()
-        print("ready", flush=True)
-
-    t = asyncio.ensure_future(announce())
-    try:
-        return await mgr.run_until(stop)
-    finally:
-        t.cancel()
+    return await run_announcing_ready(mgr, signal_event())
 
 
 def main(argv=None) -> int:

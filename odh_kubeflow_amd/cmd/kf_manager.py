@@ -38,9 +38,10 @@ def parse(argv: Optional[List[str]] = None) -> argparse.Namespace:
     p.add_argument("--leader-election-lease-duration", type=float, default=15.0)
     p.add_argument("--leader-election-renew-deadline", type=float, default=10.0)
     p.add_argument("--leader-election-retry-period", type=float, default=2.0)
-    from .common import add_shard_flags
+    from .common import add_debug_flags, add_shard_flags
 
     add_shard_flags(p)
+    add_debug_flags(p)
     return p.parse_args(argv)
 
 
@@ -67,6 +68,7 @@ def build(args, env=os.environ):
                                 retry_period=args.leader_election_retry_period)
     mgr = Manager.remote(cfg, name="notebook-controller", default_max_concurrent=args.max_concurrent_reconciles,
                          leader_elector=elector, metrics_addr=args.metrics_addr, probe_addr=args.probe_addr,
+                         debug_endpoints=args.enable_debug_endpoints,
                          cache_options=shard_cache_options(shard, namespace_from_env()))
     mgr.kf_reconcilers = setup_kf(mgr, env)
     mgr.add_healthz_check("healthz")
@@ -75,13 +77,13 @@ def build(args, env=os.environ):
 
 
 async def amain(argv=None) -> int:
-    from .common import setup_logging, signal_event
+    from .common import run_announcing_ready, setup_logging, signal_event
 
     args = parse(argv)
     setup_logging(development=args.devel)
     mgr = build(args)
     log.info("starting manager")
-    return await mgr.run_until(signal_event())
+    return await run_announcing_ready(mgr, signal_event())
 
 
 def main(argv=None) -> int:

@@ -37,9 +37,10 @@ def parse(argv: Optional[List[str]] = None) -> argparse.Namespace:
     p.add_argument("--kubeconfig", default=None)
     p.add_argument("--master", default=None)
     p.add_argument("--max-concurrent-reconciles", type=int, default=8)
-    from .common import add_shard_flags
+    from .common import add_debug_flags, add_shard_flags
 
     add_shard_flags(p)
+    add_debug_flags(p)
     args = p.parse_args(argv)
     if not args.kube_rbac_proxy_image:
         p.print_usage(sys.stderr)
@@ -68,7 +69,7 @@ def build(args, env=os.environ):
                          transforms={kinds.CONFIG_MAP: strip_data, kinds.SECRET: strip_data},
                          default_max_concurrent=args.max_concurrent_reconciles, leader_elector=elector,
                          metrics_addr=args.metrics_bind_address, probe_addr=args.health_probe_bind_address,
-                         cache_options=shard_cache_options(shard, namespace))
+                         debug_endpoints=args.enable_debug_endpoints, cache_options=shard_cache_options(shard, namespace))
     mgr.odh_reconciler = setup_odh(mgr, namespace, env, shard=shard)
     wh = NotebookWebhook(mgr.client, namespace, kube_rbac_proxy_image=args.kube_rbac_proxy_image, env=env)
     # controller-runtime's webhook server refuses to start without its serving cert; admission
@@ -87,13 +88,13 @@ def build(args, env=os.environ):
 
 
 async def amain(argv=None) -> int:
-    from .common import setup_logging, signal_event
+    from .common import run_announcing_ready, setup_logging, signal_event
 
     args = parse(argv)
     setup_logging(debug=args.debug_log, development=args.debug_log)
     mgr = build(args)
     log.info("starting manager")
-    return await mgr.run_until(signal_event())
+    return await run_announcing_ready(mgr, signal_event())
 
 
 def main(argv=None) -> int:

@@ -11,7 +11,7 @@ else — the three versions, storage/served flags, the status subresource, the N
 status schema and the validation constraints — is built here.
 
 The same schema drives admission-time validation in both fake apiservers
-(:mod:`odh_kubeflow_amd.models.openapi`; ``native/apiserver``): a malformed PodSpec is
+(:mod:`odh_kubeflow_amd.models.openapi`; ``testing/native/apiserver``): a malformed PodSpec is
 refused at create/update exactly as kube-apiserver refuses it, unknown fields are pruned
 and schema ``default`` values are applied.
 """

@@ -4,7 +4,7 @@
 Two users:
 
 * both fake apiservers (``apiserver/store.py`` and, re-implemented in C++,
-  ``native/apiserver/apiserver.cpp``) default every Pod / StatefulSet / Deployment /
+  ``testing/native/apiserver/apiserver.cpp``) default every Pod / StatefulSet / Deployment /
   Service they store, so controllers meet the same live objects envtest's real
   kube-apiserver hands them (``kf/controllers/suite_test.go:50-104``);
 * the reconcile helpers (``utils/reconcilehelper.py``) default the *desired* object the

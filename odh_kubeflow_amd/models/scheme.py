@@ -185,3 +185,34 @@ OPTIONAL_CRDS = {
     "oauthclients.oauth.openshift.io",
     "datasciencepipelinesapplications.datasciencepipelinesapplications.opendatahub.io",
 }
+
+
+# ------------------------------------------------------------------ REST paths
+
+
+class ParsedPath:
+    __slots__ = ("info", "version", "namespace", "name", "sub")
+
+    def __init__(self, info, version, namespace, name, sub):
+        self.info, self.version, self.namespace, self.name, self.sub = info, version, namespace, name, sub
+
+
+def parse_path(path: str) -> Optional[ParsedPath]:
+    segs = [s for s in path.split("/") if s]
+    if not segs:
+        return None
+    if segs[0] == "api" and len(segs) >= 3:
+        group, version, rest = "", segs[1], segs[2:]
+    elif segs[0] == "apis" and len(segs) >= 4:
+        group, version, rest = segs[1], segs[2], segs[3:]
+    else:
+        return None
+    ns = None
+    if rest[0] == "namespaces" and len(rest) >= 3 and SCHEME.for_plural(group, rest[2]) is not None:
+        ns, rest = rest[1], rest[2:]
+    info = SCHEME.for_plural(group, rest[0])
+    if info is None or len(rest) > 3:
+        return None
+    name = rest[1] if len(rest) > 1 else None
+    sub = rest[2] if len(rest) > 2 else None
+    return ParsedPath(info, version, ns, name, sub)

@@ -2,7 +2,7 @@
 
 Read-only by construction — it holds **no Kubernetes client**: it never creates or patches a
 Node, never writes pod status and needs no RBAC.  (The kubelet stand-in that does write pod
-status lives in :mod:`odh_kubeflow_amd.kubelet` and is test-harness only.)
+status lives in :mod:`odh_kubeflow_amd.testing.kubelet` and is test-harness only.)
 
 Endpoints (``--port``, default 9464, exposed as a hostPort so the culler reaches the agent
 of a pod's node at ``<pod.status.hostIP>:9464``):

@@ -3,6 +3,8 @@
 * ``libodh_gpu_probe.so``   — HIP kernels for gfx950 (``hipcc --offload-arch=gfx950``),
   C ABI, loaded with ctypes after ``import torch`` so it shares torch's HIP runtime
   (both resolve ``libamdhip64.so.7``).
+* ``odh-gpu-probe`` — the notebook pod's start-up probe (init container), a main over
+  ``odh_probe_cli`` of ``libodh_gpu_probe.so`` (``csrc/probe_cli.cpp``); needs no torch.
 * ``libodh_gpu_telemetry.so`` — host C++ amdgpu sysfs sampler (g++, pthreads).
 
 Both land in ``odh_kubeflow_amd/ops/_lib/`` so they travel with the repo snapshot to
@@ -23,9 +25,11 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 LIBDIR = os.path.join(HERE, "_lib")
 NATIVE = os.path.join(os.path.dirname(HERE), "native")
+TEST_NATIVE = os.path.join(os.path.dirname(HERE), "testing", "native")  # test platform: the C++ apiserver
 OBJCORE = "_objcore" + (sysconfig.get_config_var("EXT_SUFFIX") or ".so")
 ARCH = os.environ.get("ODH_GPU_ARCH", "gfx950")
 ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
+PROBE_EXE = "odh-gpu-probe"
 
 
 def _hipcc() -> str:
@@ -36,9 +40,16 @@ def _hipcc() -> str:
 def targets() -> Dict[str, dict]:
     return {
         "libodh_gpu_probe.so": {
-            "src": [os.path.join(CSRC, "gpu_probe.hip")],
+            "src": [os.path.join(CSRC, "gpu_probe.hip"), os.path.join(CSRC, "probe_cli.cpp")],
             "cmd": lambda src, out: [_hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-shared", "-fPIC",
                                      *src, "-o", out],
+        },
+        # the init-container probe: a 5-line main over odh_probe_cli in the library next to it
+        PROBE_EXE: {
+            "src": [os.path.join(CSRC, "probe_main.cpp")],
+            "deps": [os.path.join(LIBDIR, "libodh_gpu_probe.so")],
+            "cmd": lambda src, out: [_hipcc(), "-O2", "-std=c++17", *src, f"-L{LIBDIR}", "-lodh_gpu_probe",
+                                     "-Wl,-rpath,$ORIGIN", "-o", out],
         },
         OBJCORE: {
             "src": [os.path.join(NATIVE, "objcore.cpp")],
@@ -48,9 +59,9 @@ def targets() -> Dict[str, dict]:
                                      "-o", out],
         },
         "odh-apiserver": {
-            "src": [os.path.join(NATIVE, "apiserver", "apiserver.cpp")],
-            "deps": [os.path.join(NATIVE, "apiserver", "json.hpp")],
-            "out": os.path.join(NATIVE, "bin", "odh-apiserver"),
+            "src": [os.path.join(TEST_NATIVE, "apiserver", "apiserver.cpp")],
+            "deps": [os.path.join(TEST_NATIVE, "apiserver", "json.hpp")],
+            "out": os.path.join(TEST_NATIVE, "bin", "odh-apiserver"),
             "cmd": lambda src, out: [os.environ.get("CXX", "g++"), "-O2", "-std=c++17", "-pthread", "-Wall", *src,
                                      "-o", out, "-lssl", "-lcrypto"],
         },

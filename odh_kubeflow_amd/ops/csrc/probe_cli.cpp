@@ -1,0 +1,388 @@
+// MI355X start-up probe as a stand-alone program: the notebook pod's init container.
+//
+// `odh-gpu-probe` (probe_main.cpp) and `python -m odh_kubeflow_amd.ops.probe_main` both call
+// odh_probe_cli().  It needs only the HIP runtime — no Python, no torch — so the init
+// container costs process start + HIP init + ~0.2 ms of GPU work, not the ~1.6 s of an
+// `import torch`.  For every GPU the device plugin made visible to the pod it:
+//
+//   1. allocates the probe operands and a 256 MiB HBM3E buffer with hipMalloc and fills the
+//      integer-valued bf16 operands on the GPU (odh_probe_fill);
+//   2. runs the MFMA bf16 GEMM with the check fused into its epilogue
+//      (odh_probe_gemm_verify: every output element compared in registers against a closed
+//      form, mismatches attributed to the XCD that computed them) concurrently with the
+//      HBM pattern write + verify sweep on a second stream;
+//   3. with 2+ GPUs, reads every link of a ring over them through xGMI (peer access) and
+//      verifies the neighbour's pattern word for word.
+//
+// All devices are launched before any is waited on.  The result is one compact JSON object
+// (<4 KiB: the kubelet's termination-message limit) written to --json (default
+// /dev/termination-log when it exists) and printed on stdout.  Exit status: 0 healthy,
+// 1 a check failed, 2 no GPU or a HIP error, 3 the --timeout-ms watchdog fired, 64 usage.
+//
+// Reference parallel: the upstream pod has no GPU gate at all — kf generateStatefulSet
+// (kf/controllers/notebook_controller.go:433-523) copies resources.limits verbatim and the
+// pod is Ready when Jupyter answers; this program is what `amd.com/gpu-probe: "true"` adds
+// in front of the notebook container (controllers/notebook.py::_gpu_probe_init_container).
+
+#include <hip/hip_runtime.h>
+
+#include <atomic>
+#include <chrono>
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <memory>
+#include <string>
+#include <thread>
+#include <unistd.h>
+#include <vector>
+
+extern "C" {
+int odh_gemm_shape_ok(int M, int N, int K);
+int odh_gemm_tiles(int M, int N, int K);
+int odh_probe_fill(void* A, void* Bt, int M, int N, int K, hipStream_t stream);
+int odh_probe_gemm_verify(const void* A, const void* Bt, int M, int N, int K, int* tile_xcd, int* xcd_blocks,
+                          unsigned* err_total, unsigned* err_xcd, hipStream_t stream);
+int odh_hbm_write(void* buf, size_t bytes, uint32_t seed, int nontemporal, hipStream_t stream);
+int odh_hbm_check(const void* buf, size_t bytes, uint32_t seed, unsigned long long* err, hipStream_t stream);
+int odh_peer_enable(int dev, int peer);
+}
+
+namespace {
+
+using Clock = std::chrono::steady_clock;
+
+double ms_since(Clock::time_point t0) {
+  return std::chrono::duration<double, std::milli>(Clock::now() - t0).count();
+}
+
+struct Options {
+  int M = 4096, N = 4096, K = 1024;
+  size_t hbm_bytes = 256ull << 20;
+  size_t xgmi_bytes = 64ull << 20;
+  long timeout_ms = 30000;
+  std::string json_path;  // "" = default; "-" = stdout only
+  std::string fault;      // test hook: gemm | hbm | xgmi
+  bool quiet = false;
+};
+
+// device counters: [0:8] workgroups per XCD, [8:16] mismatches per XCD, [16] GEMM mismatches,
+// [18:20] HBM mismatches (u64), [20:22] xGMI mismatches of the link this device reads (u64)
+constexpr int NCOUNT = 32;
+
+struct Dev {
+  int index = 0;
+  void *a = nullptr, *bt = nullptr, *hbm = nullptr;
+  int* tile_xcd = nullptr;
+  int* counters = nullptr;
+  int host[NCOUNT] = {};
+  hipStream_t sg = nullptr, sh = nullptr;
+  hipEvent_t e0 = nullptr, e_gemm = nullptr, e_h0 = nullptr, e_h1 = nullptr, e_link0 = nullptr, e_link1 = nullptr;
+  uint32_t seed = 0;
+  float gemm_ms = 0, hbm_ms = 0, link_ms = 0;
+  int link_source = -1;
+  std::string error;
+};
+
+int usage(const char* argv0) {
+  std::fprintf(stderr,
+               "usage: %s [--json PATH|-] [--shape M,N,K] [--hbm-mib N] [--xgmi-mib N] [--timeout-ms N] "
+               "[--inject-fault gemm|hbm|xgmi] [--quiet]\n",
+               argv0);
+  return 64;
+}
+
+bool parse(int argc, char** argv, Options& o) {
+  for (int i = 1; i < argc; ++i) {
+    std::string a = argv[i];
+    std::string v;
+    const size_t eq = a.find('=');
+    if (eq != std::string::npos) {
+      v = a.substr(eq + 1);
+      a = a.substr(0, eq);
+    } else if (a != "--quiet") {
+      if (i + 1 >= argc) return false;
+      v = argv[++i];
+    }
+    if (a == "--json") {
+      o.json_path = v;
+    } else if (a == "--shape") {
+      if (std::sscanf(v.c_str(), "%d,%d,%d", &o.M, &o.N, &o.K) != 3) return false;
+    } else if (a == "--hbm-mib") {
+      o.hbm_bytes = (size_t)std::strtoull(v.c_str(), nullptr, 10) << 20;
+    } else if (a == "--xgmi-mib") {
+      o.xgmi_bytes = (size_t)std::strtoull(v.c_str(), nullptr, 10) << 20;
+    } else if (a == "--timeout-ms") {
+      o.timeout_ms = std::strtol(v.c_str(), nullptr, 10);
+    } else if (a == "--inject-fault") {
+      o.fault = v;
+      if (v != "gemm" && v != "hbm" && v != "xgmi") return false;
+    } else if (a == "--quiet") {
+      o.quiet = true;
+    } else {
+      return false;
+    }
+  }
+  // the fused check needs 256² output tiles and K in 64-element steps
+  return o.M > 0 && o.N > 0 && o.K > 0 && o.M % 256 == 0 && o.N % 256 == 0 && o.K % 64 == 0 &&
+         o.hbm_bytes >= (1u << 20) && o.timeout_ms > 0;
+}
+
+void emit(const Options& o, const std::string& json) {
+  std::string path = o.json_path;
+  if (path.empty()) path = access("/dev/termination-log", W_OK) == 0 ? "/dev/termination-log" : "-";
+  if (path != "-") {
+    if (FILE* f = std::fopen(path.c_str(), "w")) {
+      std::fwrite(json.data(), 1, json.size(), f);
+      std::fclose(f);
+    }
+  }
+  if (!o.quiet || path == "-") {
+    std::fwrite(json.data(), 1, json.size(), stdout);
+    std::fputc('\n', stdout);
+    std::fflush(stdout);
+  }
+}
+
+std::string esc(const std::string& s) {
+  std::string out;
+  for (char c : s) {
+    if (c == '"' || c == '\\') {
+      out += '\\';
+      out += c;
+    } else if ((unsigned char)c < 0x20) {
+      out += ' ';
+    } else {
+      out += c;
+    }
+  }
+  return out;
+}
+
+std::string fail_json(const char* what, const std::string& msg, double total_ms) {
+  char buf[512];
+  std::snprintf(buf, sizeof buf, "{\"ok\":false,\"error\":\"%s: %s\",\"timings_ms\":{\"total\":%.3f}}", what,
+                esc(msg).c_str(), total_ms);
+  return buf;
+}
+
+#define HIP_TRY(expr)                                   \
+  do {                                                  \
+    const int rc_ = (int)(expr);                        \
+    if (rc_ != 0) {                                     \
+      d.error = std::string(#expr) + ": " + hipGetErrorString((hipError_t)rc_); \
+      return false;                                     \
+    }                                                   \
+  } while (0)
+
+bool setup(Dev& d, const Options& o) {
+  HIP_TRY(hipSetDevice(d.index));
+  HIP_TRY(hipMalloc(&d.a, (size_t)o.M * o.K * 2));
+  HIP_TRY(hipMalloc(&d.bt, (size_t)o.N * o.K * 2));
+  HIP_TRY(hipMalloc(&d.hbm, o.hbm_bytes));
+  HIP_TRY(hipMalloc(&d.tile_xcd, sizeof(int) * (size_t)(o.M / 128) * (o.N / 128)));
+  HIP_TRY(hipMalloc(&d.counters, sizeof(int) * NCOUNT));
+  HIP_TRY(hipStreamCreateWithFlags(&d.sg, hipStreamNonBlocking));
+  HIP_TRY(hipStreamCreateWithFlags(&d.sh, hipStreamNonBlocking));
+  for (hipEvent_t* e : {&d.e0, &d.e_gemm, &d.e_h0, &d.e_h1, &d.e_link0, &d.e_link1}) HIP_TRY(hipEventCreate(e));
+  HIP_TRY(hipMemsetAsync(d.counters, 0, sizeof(int) * NCOUNT, d.sg));
+  HIP_TRY(odh_probe_fill(d.a, d.bt, o.M, o.N, o.K, d.sg));
+  if (o.fault == "gemm") {
+    // one corrupted operand element: row 0 of C is wrong in every column
+    HIP_TRY(hipMemsetAsync(d.a, 0x44, 2, d.sg));
+  }
+  d.seed = 0x9E3779B9u ^ (uint32_t)(d.index * 0x85EBCA6Bu) ^ (uint32_t)getpid();
+  return true;
+}
+
+bool launch(Dev& d, const Options& o) {
+  HIP_TRY(hipSetDevice(d.index));
+  HIP_TRY(hipEventRecord(d.e0, d.sg));
+  HIP_TRY(hipStreamWaitEvent(d.sh, d.e0, 0));
+  unsigned* c = (unsigned*)d.counters;
+  // the memory-bound sweep first, on the second stream: the GEMM's one workgroup per CU
+  // co-resides with its waves
+  HIP_TRY(hipEventRecord(d.e_h0, d.sh));
+  HIP_TRY(odh_hbm_write(d.hbm, o.hbm_bytes, d.seed, 0, d.sh));
+  HIP_TRY(odh_hbm_check(d.hbm, o.hbm_bytes, o.fault == "hbm" ? d.seed + 1 : d.seed,
+                        (unsigned long long*)(d.counters + 18), d.sh));
+  HIP_TRY(hipEventRecord(d.e_h1, d.sh));
+  HIP_TRY(odh_probe_gemm_verify(d.a, d.bt, o.M, o.N, o.K, d.tile_xcd, d.counters, c + 16, c + 8, d.sg));
+  HIP_TRY(hipEventRecord(d.e_gemm, d.sg));
+  return true;
+}
+
+bool finish(Dev& d) {
+  HIP_TRY(hipSetDevice(d.index));
+  HIP_TRY(hipStreamSynchronize(d.sh));
+  HIP_TRY(hipStreamSynchronize(d.sg));
+  HIP_TRY(hipEventElapsedTime(&d.gemm_ms, d.e0, d.e_gemm));
+  HIP_TRY(hipEventElapsedTime(&d.hbm_ms, d.e_h0, d.e_h1));
+  return true;
+}
+
+// reader d checks source s's freshly written pattern over xGMI
+bool link_check(Dev& d, const Dev& s, const Options& o) {
+  HIP_TRY(odh_peer_enable(d.index, s.index));
+  HIP_TRY(hipSetDevice(d.index));
+  const size_t n = (o.xgmi_bytes < o.hbm_bytes ? o.xgmi_bytes : o.hbm_bytes) & ~(size_t)15;
+  HIP_TRY(hipEventRecord(d.e_link0, d.sg));
+  HIP_TRY(odh_hbm_check(s.hbm, n, o.fault == "xgmi" ? s.seed ^ 1u : s.seed, (unsigned long long*)(d.counters + 20),
+                        d.sg));
+  HIP_TRY(hipEventRecord(d.e_link1, d.sg));
+  d.link_source = s.index;
+  return true;
+}
+
+bool link_finish(Dev& d) {
+  HIP_TRY(hipSetDevice(d.index));
+  HIP_TRY(hipMemcpyAsync(d.host, d.counters, sizeof d.host, hipMemcpyDeviceToHost, d.sg));
+  HIP_TRY(hipStreamSynchronize(d.sg));
+  if (d.link_source >= 0) HIP_TRY(hipEventElapsedTime(&d.link_ms, d.e_link0, d.e_link1));
+  return true;
+}
+
+void release(Dev& d) {
+  // teardown: nothing is left to undo if a free fails
+  (void)hipSetDevice(d.index);
+  for (void* p : {d.a, d.bt, d.hbm, (void*)d.tile_xcd, (void*)d.counters})
+    if (p) (void)hipFree(p);
+  for (hipEvent_t e : {d.e0, d.e_gemm, d.e_h0, d.e_h1, d.e_link0, d.e_link1})
+    if (e) (void)hipEventDestroy(e);
+  if (d.sg) (void)hipStreamDestroy(d.sg);
+  if (d.sh) (void)hipStreamDestroy(d.sh);
+}
+
+uint64_t u64(const int* h, int i) { return (uint64_t)(uint32_t)h[i] | ((uint64_t)(uint32_t)h[i + 1] << 32); }
+
+}  // namespace
+
+extern "C" int odh_probe_cli(int argc, char** argv) {
+  const auto t_start = Clock::now();
+  Options o;
+  if (!parse(argc, argv, o)) return usage(argc > 0 ? argv[0] : "odh-gpu-probe");
+
+  // watchdog: a wedged GPU must not hold the pod in Init forever; each call has its own flag,
+  // so a later call in the same process is never cut short by an earlier call's watchdog
+  auto finished = std::make_shared<std::atomic<bool>>(false);
+  std::thread([o, t_start, finished] {
+    const auto deadline = t_start + std::chrono::milliseconds(o.timeout_ms);
+    while (!finished->load() && Clock::now() < deadline) std::this_thread::sleep_for(std::chrono::milliseconds(5));
+    if (!finished->exchange(true)) {
+      emit(o, fail_json("timeout", "probe did not finish within " + std::to_string(o.timeout_ms) + " ms",
+                        ms_since(t_start)));
+      std::_Exit(3);
+    }
+  }).detach();
+  auto done = [&](int rc, const std::string& json) {
+    if (finished->exchange(true)) {  // the watchdog reported already and is exiting
+      for (;;) std::this_thread::sleep_for(std::chrono::seconds(1));
+    }
+    emit(o, json);
+    return rc;
+  };
+
+  int ndev = 0;
+  hipError_t e = hipGetDeviceCount(&ndev);
+  if (e != hipSuccess || ndev <= 0)
+    return done(2, fail_json("no GPU", e != hipSuccess ? hipGetErrorString(e) : "no visible device", ms_since(t_start)));
+  std::vector<Dev> devs(ndev);
+  for (int i = 0; i < ndev; ++i) devs[i].index = i;
+  e = hipSetDevice(0);
+  if (e == hipSuccess) e = hipFree(nullptr);  // context creation: the HIP-init share of the run
+  if (e != hipSuccess) return done(2, fail_json("hip init", hipGetErrorString(e), ms_since(t_start)));
+  const double t_init = ms_since(t_start);
+
+  std::string err;
+  auto fail_all = [&](Dev& d) {
+    err = "GPU " + std::to_string(d.index) + ": " + d.error;
+    for (Dev& x : devs) release(x);
+    return done(2, fail_json("hip", err, ms_since(t_start)));
+  };
+  for (Dev& d : devs)
+    if (!setup(d, o)) return fail_all(d);
+  for (Dev& d : devs)
+    if (!finish(d)) return fail_all(d);  // operands filled on every device
+  const double t_alloc = ms_since(t_start);
+  const auto t_probe0 = Clock::now();
+  for (Dev& d : devs)
+    if (!launch(d, o)) return fail_all(d);
+  for (Dev& d : devs)
+    if (!finish(d)) return fail_all(d);
+  const double probe_ms = ms_since(t_probe0);
+  // xGMI ring: device r reads the pattern device r-1 wrote (2 GPUs: each reads the other)
+  const auto t_link0 = Clock::now();
+  if (ndev >= 2) {
+    for (int r = 0; r < ndev; ++r)
+      if (!link_check(devs[r], devs[(r + ndev - 1) % ndev], o)) return fail_all(devs[r]);
+  }
+  for (Dev& d : devs)
+    if (!link_finish(d)) return fail_all(d);
+  const double link_ms = ndev >= 2 ? ms_since(t_link0) : 0.0;
+
+  const int tiles = odh_gemm_tiles(o.M, o.N, o.K);
+  const double flops = 2.0 * o.M * o.N * o.K;
+  bool ok = true;
+  std::string first_err;
+  std::string res = "[";
+  for (Dev& d : devs) {
+    const int* h = d.host;
+    long blocks = 0;
+    int xcds = 0;
+    for (int x = 0; x < 8; ++x) {
+      blocks += h[x];
+      xcds += h[x] > 0;
+    }
+    const uint64_t gemm_err = (uint32_t)h[16], hbm_err = u64(h, 18);
+    const bool dok = gemm_err == 0 && hbm_err == 0 && blocks == tiles;
+    if (!dok && first_err.empty()) {
+      char b[160];
+      std::snprintf(b, sizeof b, "GPU %d: %llu GEMM mismatches, %llu HBM mismatches, %ld/%d tiles", d.index,
+                    (unsigned long long)gemm_err, (unsigned long long)hbm_err, blocks, tiles);
+      first_err = b;
+    }
+    ok = ok && dok;
+    std::string ex = "[";
+    for (int x = 0; x < 8; ++x) ex += std::to_string((unsigned)h[8 + x]) + (x < 7 ? "," : "]");
+    char b[512];
+    std::snprintf(b, sizeof b,
+                  "%s{\"device\":%d,\"ok\":%s,\"gemm_tflops\":%.1f,\"hbm_gbps\":%.1f,\"gemm_ms\":%.4f,\"hbm_ms\":%.4f,"
+                  "\"gemm_errors\":%llu,\"hbm_errors\":%llu,\"xcds\":%d,\"err_xcd\":%s}",
+                  d.index ? "," : "", d.index, dok ? "true" : "false",
+                  d.gemm_ms > 0 ? flops / (d.gemm_ms * 1e-3) / 1e12 : 0.0,
+                  d.hbm_ms > 0 ? 2.0 * o.hbm_bytes / (d.hbm_ms * 1e-3) / 1e9 : 0.0, d.gemm_ms, d.hbm_ms,
+                  (unsigned long long)gemm_err, (unsigned long long)hbm_err, xcds, ex.c_str());
+    res += b;
+  }
+  res += "]";
+  std::string links = "[";
+  if (ndev >= 2) {
+    const size_t n = (o.xgmi_bytes < o.hbm_bytes ? o.xgmi_bytes : o.hbm_bytes) & ~(size_t)15;
+    for (Dev& d : devs) {
+      const uint64_t lerr = u64(d.host, 20);
+      const bool lok = lerr == 0;
+      if (!lok && first_err.empty())
+        first_err = "xGMI link GPU " + std::to_string(d.link_source) + " -> GPU " + std::to_string(d.index) + ": " +
+                    std::to_string((unsigned long long)lerr) + " mismatches";
+      ok = ok && lok;
+      char b[200];
+      std::snprintf(b, sizeof b, "%s{\"reader\":%d,\"source\":%d,\"ok\":%s,\"errors\":%llu,\"gbps\":%.1f}",
+                    d.index ? "," : "", d.index, d.link_source, lok ? "true" : "false", (unsigned long long)lerr,
+                    d.link_ms > 0 ? n / (d.link_ms * 1e-3) / 1e9 : 0.0);
+      links += b;
+    }
+  }
+  links += "]";
+  for (Dev& d : devs) release(d);
+  char tail[320];
+  std::snprintf(tail, sizeof tail,
+                ",\"timings_ms\":{\"hip_init\":%.3f,\"alloc_fill\":%.3f,\"probe\":%.3f,\"xgmi\":%.3f,\"total\":%.3f}}",
+                t_init, t_alloc - t_init, probe_ms, link_ms, ms_since(t_start));
+  std::string json = std::string("{\"ok\":") + (ok ? "true" : "false") + ",\"devices\":" + std::to_string(ndev) +
+                     ",\"shape\":[" + std::to_string(o.M) + "," + std::to_string(o.N) + "," + std::to_string(o.K) +
+                     "],\"hbm_mib\":" + std::to_string(o.hbm_bytes >> 20) +
+                     (first_err.empty() ? "" : ",\"error\":\"" + esc(first_err) + "\"") + ",\"results\":" + res +
+                     ",\"links\":" + links + tail;
+  return done(ok ? 0 : 1, json);
+}

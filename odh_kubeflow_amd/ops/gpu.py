@@ -14,8 +14,10 @@
   events cannot split a graph launch.  Reports matrix-core
   TFLOP/s, HBM GB/s, mismatches (attributed to the XCD that computed them) and how many
   of the 8 XCDs ran workgroups.
-* :func:`startup_probe` — the async hook the node agent (``kubelet/node.py``
-  ``GpuRuntime``) awaits before reporting a GPU pod Ready.
+* :func:`probe_devices` / :func:`xgmi_ring_check` — the same probe in a torch process over
+  several GPUs (kernel tests, microbenchmarks).  The shipped start-up probe is the
+  torch-free ``odh-gpu-probe`` init container (``csrc/probe_cli.cpp``, :mod:`.probe_main`),
+  which launches these same kernels from plain hipMalloc'd buffers.
 * :class:`LoadGenerator` — synthetic MFMA load at a given duty cycle (culler benchmarks).
 
 The library is loaded with ctypes **after** ``import torch`` so it binds to the HIP
@@ -25,7 +27,6 @@ calls raise :class:`NativeLibraryMissing` instead of silently falling back.
 
 from __future__ import annotations
 
-import asyncio
 import ctypes
 import os
 import threading
@@ -285,28 +286,6 @@ class GpuProbe:
         self.ev[4].synchronize()
         return self._graph_result(t0)
 
-    async def run_async(self) -> dict:
-        """One probe without a thread: the graph replay is launched from the event loop and
-        its completion polled (``hipEventQuery``) between the loop's other callbacks — the
-        GPU's 0.13 ms runs while the node agent keeps serving, and no executor hop or GIL
-        hand-off sits on the Ready path.  Probes of the same GPU still take turns.
-
-        The poll yields with ``sleep(0)``: any positive delay becomes an epoll timeout,
-        whose granularity is 1 ms (measured: probe wall 1.2 ms with a 20 µs sleep)."""
-        while not self._lock.acquire(blocking=False):
-            await asyncio.sleep(0)
-        try:
-            g = self._graph_handle() if (self.graph and self.fused and self.overlap) else None
-            if g is None:
-                return self._run()
-            t0 = time.perf_counter()
-            self._launch_graph(g)
-            while not self.ev[4].query():
-                await asyncio.sleep(0)
-            return self._graph_result(t0)
-        finally:
-            self._lock.release()
-
     def _run(self) -> dict:
         import torch
 
@@ -460,25 +439,6 @@ def probe_devices(devices: Sequence[int]) -> dict:
     if links:
         out["links"] = links
     return out
-
-
-async def startup_probe(devices: Sequence[int], local_index=None) -> dict:
-    """Node-agent hook: probe the pod's GPUs off the event loop.
-
-    ``local_index`` maps node-level GPU ids to this process's visible devices (one
-    process per GPU: rank r sees its GPU as ``cuda:0`` under ``HIP_VISIBLE_DEVICES``).
-    """
-    devs = [local_index(d) if local_index else d for d in devices]
-    p = _probes.get(devs[0]) if len(devs) == 1 else None
-    if p is not None:  # one GPU, probe already resident: launched and awaited on the loop itself
-        try:
-            r = await p.run_async()
-        except Exception as e:  # a failed probe fails the pod, it must not crash the agent
-            r = {"ok": False, "device": devs[0], "error": repr(e)}
-        err = None if r.get("ok") else (r.get("error") or f"probe failed on GPU {r.get('device')}")
-        return {"ok": err is None, "devices": devs, "results": [r], "error": err}
-    # first use of a device (allocation + operand fill) or a multi-GPU pod (xGMI ring): off the loop
-    return await asyncio.get_running_loop().run_in_executor(None, probe_devices, devs)
 
 
 class LoadGenerator:

@@ -1,23 +1,37 @@
 """Multi-GPU benchmark driver: one process per MI355X (``torch.distributed.run``).
 
-Layout on an 8×MI355X node (see :mod:`.shard` for the design):
+Layout on an 8×MI355X node (see :mod:`.shard` and :mod:`.platform`):
 
 * **rank 0** starts the native C++ apiserver (``odh-apiserver``: store, REST/watch,
-  admission, GC) and the scheduler (``cmd/scheduler.py``, the kube-scheduler stand-in
-  with the ``amd.com/gpu`` allocator) as child processes and broadcasts the URL;
-* **every rank r** runs a namespace shard of the control plane against it — kf + odh
-  reconcilers, the odh webhook server, the StatefulSet controller and the node agent
-  of GPU ``LOCAL_RANK`` — owning the notebooks of namespace ``bench-r``; rank 0's shard
-  also registers the Node, and is otherwise identical to the others;
-* each rank drives its own notebooks: one step = create one ``amd.com/gpu: 1`` Notebook
-  in its namespace → Ready (pod started by whichever GPU's node agent the scheduler
-  allocated, after the MI355X start-up probe on that GPU) → delete → gone.
+  admission, GC) and the node's platform — ONE scheduler (+ first-free ``amd.com/gpu``
+  allocation and the StatefulSet controller) and ONE kubelet for all GPUs — as child
+  processes, and broadcasts the URL;
+* the control plane under test runs as the deployment runs it: ``--arch sharded`` (default,
+  ``overlays/mi355x-sharded``): every rank starts its ``cmd/control_plane.py --shard r``;
+  ``--arch unsharded`` (``overlays/mi355x``, the reference topology): rank 0 starts
+  ``cmd/kf_manager.py`` + ``cmd/odh_manager.py`` and every rank's notebooks go through them;
+* each rank drives its own namespace: one step = create one ``amd.com/gpu: 1`` Notebook →
+  Ready → delete → Notebook and pod gone.
+
+**The timed region** is bracketed by barrier + ``torch.cuda.synchronize()`` on every rank;
+the elapsed time is the max over ranks.  It contains exactly the K steps: the end barrier
+follows the last step's "gone" with nothing in between.  ``value`` counts the reconciles the
+notebook controllers completed inside it (read from their ``/debug/reconciles`` at the end
+barrier): the trailing reconciles of the last deletion fall outside, as the warm-up's did
+at the start — under continuous load they overlap the next step.  After the window the
+control plane is quiesced (event-driven, :meth:`Manager.quiesce`) and the settled count
+gives ``reconciles_per_notebook``.
+
+**The start-up probe sample** (untimed, after the window, when a GPU is visible): a few
+notebooks annotated ``amd.com/gpu-probe: "true"`` — the kf controller adds the
+``odh-gpu-probe`` init container, the kubelet stand-in runs the native probe as a process on
+the pod's GPU — report create→Ready with the probe against the timed (probe-off) p50, and the
+probe's own verdict from the pod's ``initContainerStatuses`` termination message.
 
 Coordination goes through ``torch.distributed`` (gloo carries the URL, the barriers and
 the result gathers; when GPUs are present an RCCL all-reduce over xGMI checks the
 collective path once at start-up).  Barriers run in an executor thread so every process
-keeps serving its event loop while it waits.  The timed region is bracketed by barrier +
-``torch.cuda.synchronize()`` on every rank and the elapsed time is the max over ranks.
+keeps serving its event loop while it waits.
 """
 
 from __future__ import annotations
@@ -25,8 +39,12 @@ from __future__ import annotations
 import asyncio
 import json
 import os
+import statistics
 import time
 from typing import Optional
+
+GPU_PROBE_ANNOTATION = "amd.com/gpu-probe"
+NOTEBOOK_IMAGE = "rocm/pytorch:rocm7.0_ubuntu22.04_py3.10_pytorch_2.10"
 
 
 def bench_namespace(rank: int) -> str:
@@ -77,42 +95,38 @@ def run_distributed(args) -> int:
 
 
 def measure(args) -> Optional[dict]:
-    """Run the sharded benchmark on this rank; rank 0 returns the report dict."""
-    binding = None
-    if not args.no_gpu_probe:  # before any thread or child exists: they inherit the placement
-        import torch as _t
+    """Run the benchmark on this rank; rank 0 returns the report dict."""
+    import torch as _t
 
-        ndev = _t.cuda.device_count()  # does not initialise the GPU
-        if ndev:
-            binding = numa_bind(int(os.environ.get("LOCAL_RANK", os.environ.get("RANK", "0"))) % ndev)
+    ndev = _t.cuda.device_count()  # does not initialise the GPU
+    local = int(os.environ.get("LOCAL_RANK", os.environ.get("RANK", "0")))
+    binding = numa_bind(local % ndev) if ndev else None  # before any thread or child exists
     dist, torch = _dist_init()
     rank, world = dist.get_rank(), dist.get_world_size()
     local_rank = int(os.environ.get("LOCAL_RANK", rank))
-    probe = None
-    if not args.no_gpu_probe:
-        if torch.cuda.device_count() == 0:
-            raise SystemExit("no GPU visible; pass --no-gpu-probe for a CPU dev run")
-        from ..ops import gpu
-
-        dev = local_rank % torch.cuda.device_count()
-        torch.cuda.set_device(dev)
-        gpu.get_probe(dev).run()  # warm: allocate + fill the resident probe buffers
-
-        async def probe(devices):
-            return await gpu.startup_probe(devices, local_index=lambda d: dev)
-    rccl_ms = _rccl_check(torch, dist, local_rank) if not args.no_gpu_probe else None
-    res = asyncio.run(_main(args, dist, torch, rank, world, local_rank, probe))
+    if ndev:
+        torch.cuda.set_device(local_rank % ndev)
+    rccl_ms = _rccl_check(torch, dist, local_rank) if ndev else None
+    probe_sample = 0 if (args.no_gpu_probe or not ndev) else max(0, args.probe_sample)
+    res = asyncio.run(_main(args, dist, torch, rank, world, ndev, probe_sample))
     out = None
     if rank == 0:
         from bench import report  # noqa: E402  (bench.py is the entry point on sys.path)
 
         out = report(args, world, res)
-        out["config"]["parallelism"] = (f"namespace-sharded control plane x{world}: one `cmd/control_plane.py "
-                                        f"--shard r` process per MI355X (kf + odh reconcilers + odh webhook), "
-                                        f"as config/overlays/mi355x-sharded deploys it")
-        out["config"]["architecture"] = "cmd/control_plane --shard (overlay mi355x-sharded)"
-        out["config"]["platform_stand_ins"] = ("native C++ apiserver (+GC), cmd/scheduler.py, per-rank StatefulSet "
-                                               "controller + fake kubelet of the rank's GPU")
+        arch = args.arch if args.arch in ("sharded", "unsharded") else "sharded"
+        if arch == "sharded":
+            out["config"]["parallelism"] = (f"namespace-sharded control plane x{world}: one `cmd/control_plane.py "
+                                            f"--shard r` process per MI355X rank (kf + odh reconcilers + odh webhook), "
+                                            f"as config/overlays/mi355x-sharded deploys it")
+            out["config"]["architecture"] = "cmd/control_plane --shard (overlay mi355x-sharded)"
+        else:
+            out["config"]["parallelism"] = (f"one kf manager + one odh manager process for all {world} ranks' "
+                                            f"notebooks, as config/overlays/mi355x deploys them")
+            out["config"]["architecture"] = "cmd/kf_manager + cmd/odh_manager (overlay mi355x, reference topology)"
+        out["config"]["platform_stand_ins"] = ("native C++ apiserver (+GC); ONE scheduler (first-free amd.com/gpu "
+                                               "allocation) + StatefulSet controller process and ONE kubelet process "
+                                               "for the node's 8 GPUs")
         out["rank_ms_per_step"] = res.get("rank_ms_per_step")
         out["cpu_ms_per_step"] = res.get("cpu_ms_per_step")
         out["child_rss_mib"] = res.get("child_rss_mib")
@@ -122,9 +136,36 @@ def measure(args) -> Optional[dict]:
             out["writes_per_notebook"] = writes_per_notebook(res["apiserver_profile_per_step"], world)
         if rccl_ms is not None:
             out["rccl_allreduce_check_ms"] = round(rccl_ms, 3)
+        if res.get("probe_sample"):
+            out["gpu_probe_init_container"] = probe_report(res["probe_sample"], out.get("p50_ready_ms"))
     dist.barrier()
     dist.destroy_process_group()
     return out
+
+
+def probe_report(samples: list, p50_off: Optional[float]) -> dict:
+    """create→Ready of the probe notebooks, and the probe's own verdict per notebook."""
+    lat = [s["ready_ms"] for s in samples]
+    res = [s.get("result") or {} for s in samples]
+    tim = [r.get("timings_ms") or {} for r in res]
+    dev = [(r.get("results") or [{}])[0] for r in res]
+
+    def med(xs):
+        xs = [x for x in xs if x is not None]
+        return round(statistics.median(xs), 3) if xs else None
+
+    p50 = med(lat)
+    return {
+        "notebooks": len(samples), "all_ok": all(r.get("ok") for r in res) and len(res) > 0,
+        "p50_ready_ms": p50, "max_ready_ms": round(max(lat), 3) if lat else None,
+        "added_ms_p50_vs_probe_off": round(p50 - p50_off, 3) if p50 is not None and p50_off is not None else None,
+        "init_container_wall_ms_p50": med(s.get("wall_ms") for s in samples),
+        "probe_timings_ms_p50": {k: med(t.get(k) for t in tim) for k in ("hip_init", "alloc_fill", "probe", "total")},
+        "gemm_tflops_p50": med(d.get("gemm_tflops") for d in dev),
+        "hbm_gbps_p50": med(d.get("hbm_gbps") for d in dev),
+        "mechanism": "init container odh-gpu-probe (ops/csrc/probe_cli.cpp, no torch), injected by the kf "
+                     "StatefulSet generator for amd.com/gpu-probe=\"true\"; run as a process by the kubelet stand-in",
+    }
 
 
 def writes_per_notebook(prof: dict, notebooks_per_step: int) -> dict:
@@ -178,7 +219,7 @@ def _cpulist(text: str) -> set:
 
 def numa_bind(local_rank: int, sysfs: str = "/sys") -> Optional[dict]:
     """Pin this rank — and the processes it starts after this (its control plane, on rank 0
-    the apiserver and scheduler) — to the physical cores of its MI355X's NUMA node.
+    the apiserver and the node platform) — to the physical cores of its MI355X's NUMA node.
 
     An 8×MI355X node is two sockets; left alone, the scheduler spreads a rank's processes
     over both, and every watch event, admission and REST call between them crosses the
@@ -215,77 +256,56 @@ def numa_bind(local_rank: int, sysfs: str = "/sys") -> Optional[dict]:
         return None
 
 
-async def _main(args, dist, torch, rank: int, world: int, local_rank: int, probe) -> dict:
+async def _main(args, dist, torch, rank: int, world: int, ndev: int, probe_sample: int) -> dict:
+    from .platform import NodePlatform
     from .shard import ControlPlaneShard, ShardConfig
 
     native = None
-    sched = None
+    platform = None
     url = [None]
+    arch = args.arch if args.arch in ("sharded", "unsharded") else "sharded"
     if rank == 0:
-        from ..apiserver.native import NativeApiServer
-        from ..cluster import OPENSHIFT_CRDS
+        from ..testing.apiserver.native import NativeApiServer
+        from ..testing.cluster import OPENSHIFT_CRDS
 
         audit = os.environ.get("DEBUG_WRITE_AUDITLOG")  # same debug aid as the test cluster
         pol = None
         if audit:
-            from ..apiserver.audit import AuditPolicy
+            from ..testing.apiserver.audit import AuditPolicy
 
             lv = os.environ.get("DEBUG_AUDIT_LEVEL", "Metadata")  # Request / RequestResponse: with bodies
             pol = AuditPolicy([{"level": lv}])  # every request: what each process sends
         native = await NativeApiServer(OPENSHIFT_CRDS, gc=True, audit_log_path=audit, audit_policy=pol).start()
         url[0] = native.url
-        sched = await _start_scheduler(native.url)
+        platform = await NodePlatform(native.url, exec_init=probe_sample > 0, hip_devices=ndev).start()
     await _in_thread(dist.broadcast_object_list, url, 0)
-    use_odh = not args.no_odh
     env = {"SET_PIPELINE_RBAC": "false", "SET_PIPELINE_SECRET": "false"}
     shard = ControlPlaneShard(ShardConfig(
-        apiserver_url=url[0], namespace=bench_namespace(rank), gpu=local_rank % 8, shard=str(rank),
-        bootstrap=(rank == 0), run_scheduler=False, odh=use_odh, webhook=use_odh, startup_probe=probe,
-        reference_emulation=args.reference_emulation, env=env, process=True))
+        apiserver_url=url[0], namespace=bench_namespace(rank), shard=str(rank), arch=arch,
+        launch=(arch == "sharded" or rank == 0), bootstrap=(rank == 0), odh=not args.no_odh,
+        webhook=not args.no_odh, reference_emulation=args.reference_emulation, env=env, process=True))
     if rank == 0:
-        await shard.start()  # namespaces, Node, scheduler first
+        await shard.start()  # cluster namespaces (and, unsharded, the managers + their webhook) first
         await _in_thread(dist.barrier)
     else:
         await _in_thread(dist.barrier)
         await shard.start()
-    await _in_thread(dist.barrier)  # every shard's webhook is registered before anyone creates
+    await _in_thread(dist.barrier)  # every control plane and webhook is registered before anyone creates
 
     try:
-        children = {"apiserver": native.proc.pid if native else None, "scheduler": sched.pid if sched else None,
-                    f"control_plane_{rank}": shard.control_plane_pid()}
-        result = await _drive(args, shard, dist, torch, children, native)
+        children = {"apiserver": native.proc.pid if native else None}
+        if platform is not None:
+            children.update(platform.pids())
+        children.update(shard.control_plane_pids())
+        result = await _drive(args, shard, dist, torch, children, native, probe_sample)
     finally:
         await _in_thread(dist.barrier)  # nobody tears down while others still serve
         await shard.stop()
-        if sched is not None:
-            await _stop_child(sched)
+        if platform is not None:
+            await platform.stop()
         if native is not None:
             await native.stop()
     return result
-
-
-async def _start_scheduler(url: str):
-    """kube-scheduler stand-in as a child process of rank 0 (see ``cmd/scheduler.py``)."""
-    import subprocess
-    import sys
-
-    root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-    env = dict(os.environ, PYTHONPATH=root + os.pathsep + os.environ.get("PYTHONPATH", ""))
-    proc = subprocess.Popen([sys.executable, "-m", "odh_kubeflow_amd.cmd.scheduler", "--master", url],
-                            cwd=root, env=env, stdout=subprocess.PIPE, stderr=subprocess.DEVNULL, text=True)
-    line = await asyncio.wait_for(_in_thread(proc.stdout.readline), 120)
-    if line.strip() != "ready":
-        proc.kill()
-        raise RuntimeError(f"scheduler process did not start (rc={proc.poll()})")
-    return proc
-
-
-async def _stop_child(proc) -> None:
-    proc.terminate()
-    try:
-        await asyncio.wait_for(_in_thread(proc.wait), 10)
-    except asyncio.TimeoutError:
-        proc.kill()
 
 
 async def _apiserver_prof(native) -> Optional[dict]:
@@ -308,35 +328,44 @@ def _prof_per_step(p0: Optional[dict], p1: Optional[dict], steps: int) -> Option
     return out
 
 
-async def _drive(args, shard, dist, torch, children: Optional[dict] = None, native=None) -> dict:
+async def _lifecycle(shard, nm: str, ann: Optional[dict], timeout: float = 120.0) -> tuple:
+    """create → Ready → delete → gone; returns (create→Ready s, Ready→gone s)."""
     from ..models import kinds
     from ..models.notebook import notebook
 
-    use_odh = not args.no_odh
     ns = shard.cfg.namespace
+    t0 = time.perf_counter()
+    await shard.admin.create(notebook(nm, ns, image=NOTEBOOK_IMAGE, gpus=1, annotations=ann))
+    if not await shard.wait_until(lambda: shard.notebook_ready(nm), timeout):
+        raise RuntimeError(f"notebook {ns}/{nm} not Ready")
+    ready = time.perf_counter()
+    pod = shard.peek(kinds.POD, f"{nm}-0", ns)
+    await shard.admin.delete(kinds.NOTEBOOK, nm, ns)
+    if not await shard.wait_until(lambda: shard.gone(nm), 60):
+        raise RuntimeError(f"teardown of {ns}/{nm} did not finish")
+    return ready - t0, time.perf_counter() - ready, pod
+
+
+async def _drive(args, shard, dist, torch, children: Optional[dict] = None, native=None,
+                 probe_sample: int = 0) -> dict:
+    from ..ops.probe_main import parse_result
+
+    use_odh = not args.no_odh
+    base_ann = {"notebooks.opendatahub.io/inject-auth": "true"} if use_odh else {}
     lat_ms, teardown_ms = [], []
-    state = {"recon": 0, "step": 0}
+    state = {"step": 0}
 
     async def one_step(timed: bool):
         state["step"] += 1
-        nm = f"nb-s{state['step']}"
-        ann = {"notebooks.opendatahub.io/inject-auth": "true"} if use_odh else None
-        t0 = time.perf_counter()
-        await shard.admin.create(notebook(nm, ns, image="rocm/pytorch:rocm7.0_ubuntu22.04_py3.10_pytorch_2.10",
-                                          gpus=1, annotations=ann))
-        if not await shard.wait_until(lambda: shard.notebook_ready(nm), 120):
-            raise RuntimeError(f"notebook {ns}/{nm} not Ready")
-        ready = time.perf_counter()
-        await shard.admin.delete(kinds.NOTEBOOK, nm, ns)
-        if not await shard.wait_until(lambda: shard.gone(nm), 60):
-            raise RuntimeError(f"teardown of {ns}/{nm} did not finish")
+        ready_s, gone_s, _pod = await _lifecycle(shard, f"nb-s{state['step']}", dict(base_ann) or None)
         if timed:
-            lat_ms.append((ready - t0) * 1e3)
-            teardown_ms.append((time.perf_counter() - ready) * 1e3)
+            lat_ms.append(ready_s * 1e3)
+            teardown_ms.append(gone_s * 1e3)
 
     for _ in range(args.warmup):
         await one_step(False)
-    await shard.settle(5)
+    await _in_thread(dist.barrier)  # every rank's warm-up done (unsharded: one control plane for all)
+    await shard.quiesce()
     from ..utils import gctune
 
     gctune.tune()
@@ -351,13 +380,14 @@ async def _drive(args, shard, dist, torch, children: Optional[dict] = None, nati
     t_start = time.perf_counter()
     for _ in range(args.steps):
         await one_step(True)
-    own = time.perf_counter() - t_start  # this rank's own steps (the barrier below equalises elapsed)
-    await shard.settle(5)  # the last teardown's trailing reconciles stay inside the timed region
+    own = time.perf_counter() - t_start  # this rank's own steps
+    if torch.cuda.is_available():
+        torch.cuda.synchronize()
+    await _in_thread(dist.barrier)
+    elapsed = time.perf_counter() - t_start  # ---- end of the timed region
     from bench import breakdown_delta, merge_breakdowns  # noqa: E402  (bench.py is the entry point)
 
-    breakdown = breakdown_delta(b0, await shard.reconcile_breakdown())
-    state["recon"] = sum(sum(t.values()) for t in breakdown.values())
-    # CPU time per step of every process on the path: where a step's work goes when ranks are added
+    in_window = breakdown_delta(b0, await shard.reconcile_breakdown())
     cpu = {"rank": time.process_time() - cpu0}
     prof = _prof_per_step(prof0, await _apiserver_prof(native), args.steps)
     rss = {}
@@ -368,29 +398,38 @@ async def _drive(args, shard, dist, torch, children: Optional[dict] = None, nati
         r = _proc_rss_mib(pid)
         if r is not None:
             rss[k] = r
-    if torch.cuda.is_available():
-        torch.cuda.synchronize()
+    # untimed: the trailing reconciles of the last deletion, for the per-lifecycle count
     await _in_thread(dist.barrier)
-    elapsed = time.perf_counter() - t_start
+    idle = await shard.quiesce()
+    settled = breakdown_delta(b0, await shard.reconcile_breakdown())
+    samples = []
+    for i in range(probe_sample):  # untimed: notebooks with the start-up probe init container
+        ann = {**base_ann, GPU_PROBE_ANNOTATION: "true"}
+        ready_s, _gone, pod = await _lifecycle(shard, f"nb-probe-{i}", ann, timeout=180)
+        st = ((pod or {}).get("status") or {}).get("initContainerStatuses") or [{}]
+        term = (st[0].get("state") or {}).get("terminated") or {}
+        result = parse_result(term.get("message", ""))
+        samples.append({"ready_ms": ready_s * 1e3, "result": result, "exit_code": term.get("exitCode"),
+                        "wall_ms": (result or {}).get("timings_ms", {}).get("total")})
 
     el = torch.tensor([elapsed], dtype=torch.float64)
-    rc = torch.tensor([state["recon"]], dtype=torch.float64)
     await _in_thread(lambda: dist.all_reduce(el, op=dist.ReduceOp.MAX))
-    await _in_thread(lambda: dist.all_reduce(rc, op=dist.ReduceOp.SUM))
     gathered = [None] * dist.get_world_size()
-    await _in_thread(dist.all_gather_object, gathered, {"lat": lat_ms, "probes": shard.probe_results,
-                                                        "teardown": teardown_ms, "own_s": own, "cpu": cpu,
-                                                        "rss": rss, "breakdown": breakdown})
+    await _in_thread(dist.all_gather_object, gathered, {"lat": lat_ms, "teardown": teardown_ms, "own_s": own,
+                                                        "cpu": cpu, "rss": rss, "in_window": in_window,
+                                                        "settled": settled, "idle": idle, "probe": samples})
     per_step = 1e3 / max(1, args.steps)
     cpu_ms = {"ranks": [round(g["cpu"]["rank"] * per_step, 3) for g in gathered]}
     for g in gathered:
         for k, v in g["cpu"].items():
             if k != "rank":
                 cpu_ms[k] = round(v * per_step, 3)
-    return {"elapsed": float(el.item()), "reconciles": int(rc.item()),
+    window = merge_breakdowns(g["in_window"] for g in gathered)
+    return {"elapsed": float(el.item()), "reconciles": sum(sum(t.values()) for t in window.values()),
             "lat_ms": [x for g in gathered for x in g["lat"]], "odh": use_odh,
-            "probes": [p for g in gathered for p in g["probes"]],
             "teardown_ms": [x for g in gathered for x in g["teardown"]],
             "rank_ms_per_step": [round(g["own_s"] * per_step, 3) for g in gathered], "cpu_ms_per_step": cpu_ms,
             "child_rss_mib": {k: v for g in gathered for k, v in g["rss"].items()},
-            "apiserver_profile_per_step": prof, "breakdown": merge_breakdowns(g["breakdown"] for g in gathered)}
+            "apiserver_profile_per_step": prof, "breakdown": merge_breakdowns(g["settled"] for g in gathered),
+            "quiesced": all(g["idle"] for g in gathered),
+            "probe_sample": [s for g in gathered for s in g["probe"]]}

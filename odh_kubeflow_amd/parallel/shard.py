@@ -1,42 +1,39 @@
-"""One namespace shard of the benchmark: the shipped control-plane process + platform stand-ins.
+"""One rank of the benchmark: the shipped control-plane process(es) + this rank's notebook driver.
 
-The reference runs one notebook-controller and one odh-notebook-controller replica for
-the whole cluster (``kf/main.go:87-98``, ``odh/main.go:155-192``; one worker each).  The
-MI355X deployment (``config/overlays/mi355x-sharded``) runs N shards of
-``cmd/control_plane.py`` — one per MI355X of the node, replica k owning the namespaces
-labelled ``notebooks.amd.com/shard=k`` — against the cluster's apiserver.  A benchmark
-shard is exactly that deployment unit plus the platform it would find on a node:
+The reference runs one notebook-controller and one odh-notebook-controller replica for the
+whole cluster (``kf/main.go:87-98``, ``odh/main.go:155-192``; one worker each).  Two
+deployable topologies are measured, both exactly as the manifests run them:
 
-* **the product** — ``python -m odh_kubeflow_amd.cmd.control_plane --shard r …`` as a
-  child process (``process=True``, what ``bench.py`` runs), or the same
-  :func:`~odh_kubeflow_amd.cmd.control_plane.build` inside this process (tests, tools):
-  kf reconciler + event re-emitter, odh reconciler and the odh mutating webhook (HTTPS,
-  registered by this shard's MutatingWebhookConfiguration with a ``namespaceSelector``
-  on the shard label), one informer cache over the shard's namespaces;
-* **the platform stand-ins** (what kube-controller-manager and the kubelet do on a real
-  cluster; never deployed) — the StatefulSet controller for the shard's namespace and the
-  fake kubelet of GPU ``r`` (pods labelled ``amd.com/gpu-index=r``; it gates Ready on the
-  MI355X start-up probe).  The shard's namespace is labelled ``amd.com/gpu-affinity=r`` so
-  the scheduler stand-in (``cmd/scheduler.py``) gives its pods GPU ``r``;
-* the bootstrap shard (rank 0) also registers the Node.  GC runs in the apiserver.
+* ``arch="sharded"`` (``config/overlays/mi355x-sharded``) — every rank r starts
+  ``python -m odh_kubeflow_amd.cmd.control_plane --shard r`` (kf reconciler + event
+  re-emitter, odh reconciler and the odh mutating webhook, one informer cache over the
+  namespaces labelled ``notebooks.amd.com/shard=r``), registered by its shard's
+  MutatingWebhookConfiguration with a ``namespaceSelector`` on that label;
+* ``arch="unsharded"`` (``config/overlays/mi355x``, the reference's two-process layout) —
+  rank 0 starts ``cmd/kf_manager.py`` and ``cmd/odh_manager.py`` (+ its webhook, one MWC for
+  every namespace); the other ranks only drive notebooks into them.
+
+Each rank drives one namespace (``bench-r``) through an informer cache of its own.  The node
+around them — scheduler + device allocator, StatefulSet controller, kubelet — is ONE
+:class:`~odh_kubeflow_amd.parallel.platform.NodePlatform` for all ranks, as on a real node.
+
+``process=False`` builds the same managers inside this process (tests, tools).
 """
 
 from __future__ import annotations
 
 import asyncio
+import json
 import os
 import shutil
 import socket
 import subprocess
-import sys
-import time
 from dataclasses import dataclass, field
 from typing import Callable, Dict, List, Optional
 
 from ..controllers.setup import SHARD_LABEL
 from ..models import kinds
 from ..models import meta as m
-from ..runtime.manager import Manager
 
 ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
@@ -51,144 +48,152 @@ def free_port() -> int:
 class ShardConfig:
     apiserver_url: str
     namespace: str
-    gpu: int
-    shard: Optional[str] = None  # default: str(gpu)
-    node_name: str = "mi355x-node-0"
-    node_gpus: int = 8
+    shard: Optional[str] = "0"  # sharded: this rank's shard id
+    arch: str = "sharded"  # "sharded" | "unsharded"
+    launch: bool = True  # start the control plane (unsharded: rank 0 only; the others just drive)
     controller_namespace: str = "opendatahub"
-    bootstrap: bool = False
-    # the bootstrap shard hosts the scheduler unless it runs as its own process
-    # (``cmd/scheduler.py``, as kube-scheduler does); the node agent then watches only
-    # its GPU's pods on every shard, bootstrap included (no CPU-only pods in that mode)
-    run_scheduler: bool = True
+    bootstrap: bool = False  # create the cluster-wide namespaces (rank 0)
     odh: bool = True
     webhook: bool = True
-    startup_probe: Optional[Callable] = None
     reference_emulation: bool = False
     max_concurrent: int = 8
     env: Dict[str, str] = field(default_factory=dict)
     kube_rbac_proxy_image: str = "quay.io/brancz/kube-rbac-proxy:v0.18.1"
-    process: bool = False  # run the control plane as its own process (cmd/control_plane.py)
+    process: bool = False  # run the control plane as its own process(es), as deployed
+
+
+class _Proc:
+    """One launched control-plane process and its debug endpoint."""
+
+    def __init__(self, name: str, proc: subprocess.Popen, metrics_port: int):
+        self.name = name
+        self.proc = proc
+        self.base = f"http://127.0.0.1:{metrics_port}"
 
 
 class ControlPlaneShard:
     def __init__(self, cfg: ShardConfig):
         self.cfg = cfg
-        self.shard = cfg.shard if cfg.shard is not None else str(cfg.gpu)
+        self.shard = cfg.shard if cfg.arch == "sharded" else None
         self.env = {**os.environ, **cfg.env}
-        self.managers: List[Manager] = []
-        self.control_plane: Optional[Manager] = None  # in-process mode
-        self.proc: Optional[subprocess.Popen] = None  # process mode
-        self.metrics_url: Optional[str] = None
-        self.agent = None
+        self.procs: List[_Proc] = []  # process mode
+        self.managers = []  # in-process mode
+        self.control_plane = None  # in-process sharded: the control_plane Manager
         self._caches = []
         self._waiters = None
         self._certs = None
+        self._http = None
 
     # ------------------------------------------------------------------ build
 
-    def _cp_args(self, webhook_port: int, metrics_port: int, probe_port: int) -> List[str]:
+    def _common_flags(self) -> List[str]:
+        return ["--master", self.cfg.apiserver_url, "--max-concurrent-reconciles", str(self.cfg.max_concurrent),
+                "--enable-debug-endpoints"]
+
+    def _specs(self, webhook_port: int):
+        """(name, module, argv, metrics flag) of the processes this rank launches."""
         cfg = self.cfg
-        ctrls = ["kf"] + (["odh"] if cfg.odh else []) + (["webhook"] if cfg.odh and cfg.webhook else [])
-        a = ["--master", cfg.apiserver_url, "--shard", self.shard, "--controllers", ",".join(ctrls),
-             "--kube-rbac-proxy-image", cfg.kube_rbac_proxy_image,
-             "--webhook-cert-dir", self._certs.cert_dir, "--webhook-host", "127.0.0.1",
-             "--webhook-port", str(webhook_port),
-             "--metrics-bind-address", f"127.0.0.1:{metrics_port}" if metrics_port else "0",
-             "--health-probe-bind-address", f"127.0.0.1:{probe_port}" if probe_port else "0",
-             "--max-concurrent-reconciles", str(cfg.max_concurrent)]
-        if cfg.reference_emulation:
-            a.append("--reference-emulation")
-        return a
+        wh = ["--kube-rbac-proxy-image", cfg.kube_rbac_proxy_image, "--webhook-cert-dir", self._certs.cert_dir,
+              "--webhook-host", "127.0.0.1", "--webhook-port", str(webhook_port)]
+        if cfg.arch == "sharded":
+            ctrls = ["kf"] + (["odh"] if cfg.odh else []) + (["webhook"] if cfg.odh and cfg.webhook else [])
+            a = ["--shard", self.shard, "--controllers", ",".join(ctrls), *wh, "--health-probe-bind-address", "0"]
+            if cfg.reference_emulation:
+                a.append("--reference-emulation")
+            return [("control_plane", "odh_kubeflow_amd.cmd.control_plane", a, "--metrics-bind-address")]
+        out = [("kf_manager", "odh_kubeflow_amd.cmd.kf_manager", ["--probe-addr", "0"], "--metrics-addr")]
+        if cfg.odh:
+            out.append(("odh_manager", "odh_kubeflow_amd.cmd.odh_manager", [*wh, "--health-probe-bind-address", "0"],
+                        "--metrics-bind-address"))
+        return out
 
     def _cp_env(self) -> Dict[str, str]:
         return {**self.env, "K8S_NAMESPACE": self.cfg.controller_namespace}
 
     async def start(self) -> "ControlPlaneShard":
-        from ..kubelet.agent import FakeKubeletAgent
-        from ..kubelet.node import GPU_AFFINITY_LABEL, GPU_INDEX_LABEL, SchedulerController
-        from ..kubelet.statefulset import StatefulSetController
         from ..runtime.informer import InformerCache
         from ..runtime.rest import RestClient, RestConfig
         from ..webhook.certs import generate
 
         cfg = self.cfg
-        self.rest_config = RestConfig(host=cfg.apiserver_url)
-        self.rest = RestClient(self.rest_config)
+        self.rest = RestClient(RestConfig(host=cfg.apiserver_url))
         self.admin = self.rest
         if cfg.bootstrap:
             for ns in ("default", cfg.controller_namespace):
                 await self.ensure_namespace(ns)
-        # the shard owns the namespace; its pods prefer this rank's GPU
-        await self.ensure_namespace(cfg.namespace, {SHARD_LABEL: self.shard, GPU_AFFINITY_LABEL: str(cfg.gpu)})
-
-        # ---- the product: cmd/control_plane.py --shard <shard>
-        self._certs = generate(("127.0.0.1", "localhost"))
-        if cfg.process:
-            wport, mport = free_port(), free_port()
-            self.metrics_url = f"http://127.0.0.1:{mport}/metrics"
-            prof = self.env.get("ODH_CONTROL_PLANE_PROFILE")  # cProfile output path (profiling runs)
-            pre = ["-m", "cProfile", "-o", f"{prof}.{self.shard}"] if prof else []
-            self.proc = subprocess.Popen(
-                [sys.executable, *pre, "-m", "odh_kubeflow_amd.cmd.control_plane", *self._cp_args(wport, mport, 0)],
-                cwd=ROOT, env={**self._cp_env(), "PYTHONPATH": ROOT + os.pathsep + self.env.get("PYTHONPATH", "")},
-                stdout=subprocess.PIPE, stderr=subprocess.DEVNULL, text=True)
-            line = await asyncio.wait_for(asyncio.get_running_loop().run_in_executor(None, self.proc.stdout.readline),
-                                          120)
-            if line.strip() != "ready":
-                self.proc.kill()
-                raise RuntimeError(f"control plane shard {self.shard} did not start (rc={self.proc.poll()})")
-        else:
-            from ..cmd import control_plane
-
-            args = control_plane.parse(self._cp_args(0, 0, 0))
-            self.control_plane = control_plane.build(args, self._cp_env())
-            await self.control_plane.start()
-            await self.control_plane.elected.wait()
-            wport = self.control_plane.webhook_server.port if self.control_plane.webhook_server else 0
-        if cfg.webhook and cfg.odh:
-            await self._register_webhook(wport)
-
-        # ---- platform stand-ins: StatefulSet controller + this GPU's kubelet (+ scheduler)
+        await self.ensure_namespace(cfg.namespace, {SHARD_LABEL: self.shard} if self.shard is not None else None)
+        if cfg.launch:
+            self._certs = generate(("127.0.0.1", "localhost"))
+            wport = free_port()
+            if cfg.process:
+                await self._launch_processes(wport)
+            else:
+                wport = await self._build_in_process()
+            if cfg.webhook and cfg.odh:
+                await self._register_webhook(wport)
+        # this rank's notebook driver: its namespace's Notebooks and Pods
         self.cache = InformerCache(self.rest, namespaces=[cfg.namespace])
         self._caches.append(self.cache)
-        shared = (self.rest, self.cache)
-        kube = self._mgr("kube-controller-manager", shared)
-        StatefulSetController(kube.client, kube.reader, kube.get_event_recorder_for("statefulset-controller")) \
-            .setup_with_manager(kube)
-        schedules = cfg.bootstrap and cfg.run_scheduler
-        if schedules:
-            node_cache = InformerCache(self.rest)
-        else:
-            node_cache = InformerCache(self.rest, selectors={kinds.POD: f"{GPU_INDEX_LABEL}={cfg.gpu}"})
-        self._caches.append(node_cache)
-        kl = self._mgr(f"kubelet-gpu{cfg.gpu}", (self.rest, node_cache))
-        if schedules:
-            SchedulerController(kl.client, kl.reader, kl.get_event_recorder_for("default-scheduler")) \
-                .setup_with_manager(kl)
-        self.agent = FakeKubeletAgent(kl, cfg.node_name, [cfg.gpu], node_gpus=cfg.node_gpus,
-                                      startup_probe=cfg.startup_probe, register_node=cfg.bootstrap,
-                                      owns_cpu_pods=schedules)
-        for mgr in self.managers:
-            await mgr.start()
-        await self.cache.wait_synced([kinds.NOTEBOOK, kinds.POD, kinds.STATEFUL_SET])
+        for k in (kinds.NOTEBOOK, kinds.POD):
+            await self.cache.ensure_informer(k)
+        await self.cache.wait_synced([kinds.NOTEBOOK, kinds.POD])
         return self
 
-    def _mgr(self, name: str, shared) -> Manager:
-        mgr = Manager.remote(None, name=name, default_max_concurrent=self.cfg.max_concurrent, shared=shared)
-        self.managers.append(mgr)
-        return mgr
+    async def _launch_processes(self, webhook_port: int) -> None:
+        from .platform import start_child
+
+        env = {**self._cp_env(), "PYTHONPATH": ROOT + os.pathsep + self.env.get("PYTHONPATH", "")}
+        prof = self.env.get("ODH_CONTROL_PLANE_PROFILE")  # cProfile output path (profiling runs)
+        for name, module, argv, metrics_flag in self._specs(webhook_port):
+            mport = free_port()
+            args = [*self._common_flags(), metrics_flag, f"127.0.0.1:{mport}", *argv]
+            pre = ["-m", "cProfile", "-o", f"{prof}.{name}.{self.shard or 'all'}"] if prof else []
+            proc = await start_child(module, args, f"{name} (shard {self.shard})", env=env, python_args=pre)
+            self.procs.append(_Proc(name, proc, mport))
+
+    async def _build_in_process(self) -> int:
+        cfg = self.cfg
+        wport = 0
+        if cfg.arch == "sharded":
+            from ..cmd import control_plane
+
+            (_name, _mod, argv, mflag), = self._specs(0)
+            args = control_plane.parse([*self._common_flags(), mflag, "0", *argv])
+            mgrs = [control_plane.build(args, self._cp_env())]
+            self.control_plane = mgrs[0]
+        else:
+            from ..cmd import kf_manager, odh_manager
+
+            specs = {n: (a, f) for n, _mod, a, f in self._specs(0)}
+            a, f = specs["kf_manager"]
+            mgrs = [kf_manager.build(kf_manager.parse([*self._common_flags(), f, "0", *a]), self._cp_env())]
+            if "odh_manager" in specs:
+                a, f = specs["odh_manager"]
+                mgrs.append(odh_manager.build(odh_manager.parse([*self._common_flags(), f, "0", *a]),
+                                              self._cp_env()))
+        for mgr in mgrs:
+            await mgr.start()
+            await mgr.elected.wait()
+            srv = getattr(mgr, "webhook_server", None)
+            if srv is not None:
+                wport = srv.port
+        self.managers = mgrs
+        return wport
 
     async def _register_webhook(self, port: int) -> None:
-        """This shard's MutatingWebhookConfiguration (what the overlay ships per shard, with a
-        URL instead of the per-shard Service since the apiserver here runs on the host)."""
+        """The MutatingWebhookConfiguration the overlay ships (with a URL instead of the
+        Service, since the apiserver here runs on the host): per shard with a
+        ``namespaceSelector`` on the shard label, or one for every namespace (unsharded)."""
         from ..models.errors import ApiError, is_already_exists
         from ..webhook.server import mutating_webhook_configuration
 
-        mwc = mutating_webhook_configuration(
-            self._certs.ca_bundle_b64, url=f"https://127.0.0.1:{port}/mutate-notebook-v1",
-            name=f"odh-notebook-webhook-shard-{self.shard}",
-            namespace_selector={"matchLabels": {SHARD_LABEL: self.shard}})
+        kw = {}
+        name = "odh-notebook-controller-mutating-webhook-configuration"
+        if self.shard is not None:
+            name = f"odh-notebook-webhook-shard-{self.shard}"
+            kw["namespace_selector"] = {"matchLabels": {SHARD_LABEL: self.shard}}
+        mwc = mutating_webhook_configuration(self._certs.ca_bundle_b64,
+                                             url=f"https://127.0.0.1:{port}/mutate-notebook-v1", name=name, **kw)
         try:
             await self.admin.create(mwc)
         except ApiError as e:
@@ -230,75 +235,57 @@ class ControlPlaneShard:
 
     # -------------------------------------------------------------- control-plane counters
 
-    async def scrape(self) -> Dict[str, Dict[tuple, float]]:
-        """Process mode: the control plane's ``/metrics`` → {sample name: {sorted labels: value}}."""
+    async def _get_json(self, url: str) -> dict:
         import aiohttp
-        from prometheus_client.parser import text_string_to_metric_families
 
-        async with aiohttp.ClientSession(timeout=aiohttp.ClientTimeout(total=10)) as s:
-            async with s.get(self.metrics_url) as r:
-                text = await r.text()
-        out: Dict[str, Dict[tuple, float]] = {}
-        for fam in text_string_to_metric_families(text):
-            for smp in fam.samples:
-                out.setdefault(smp.name, {})[tuple(sorted(smp.labels.items()))] = smp.value
-        return out
+        if self._http is None:
+            self._http = aiohttp.ClientSession(timeout=aiohttp.ClientTimeout(total=60))
+        async with self._http.get(url) as r:
+            return json.loads(await r.text())
 
     async def reconcile_breakdown(self) -> dict:
-        """controller → {trigger → reconciles} of the notebook controllers (the culler and the
-        namespace assigner are not part of a notebook's create→Ready path)."""
+        """controller → {trigger → reconciles} of the notebook controllers this rank launched
+        (the culler and the namespace assigner are not part of a notebook's create→Ready path)."""
         skip = ("Culler", "shard-assigner")
-        if self.control_plane is not None:
-            return {k: v for k, v in self.control_plane.reconcile_breakdown().items() if k not in skip}
+        parts = [mgr.reconcile_breakdown() for mgr in self.managers]
+        if self.procs:
+            parts += [d["reconciles"] for d in await asyncio.gather(
+                *(self._get_json(f"{p.base}/debug/reconciles") for p in self.procs))]
         out: dict = {}
-        for labels, v in (await self.scrape()).get("odh_controller_reconcile_trigger_total", {}).items():
-            d = dict(labels)
-            if d.get("controller") in skip:
-                continue
-            out.setdefault(d["controller"], {})[d["trigger"]] = int(v)
+        for part in parts:
+            for ctrl, trig in part.items():
+                if ctrl in skip:
+                    continue
+                o = out.setdefault(ctrl, {})
+                for k, v in trig.items():
+                    o[k] = o.get(k, 0) + v
         return out
 
     async def reconcile_count(self) -> int:
         return sum(sum(t.values()) for t in (await self.reconcile_breakdown()).values())
 
-    def control_plane_pid(self) -> Optional[int]:
-        return self.proc.pid if self.proc is not None else None
+    def control_plane_pids(self) -> Dict[str, int]:
+        sfx = f"_{self.shard}" if self.shard is not None else ""
+        return {f"{p.name}{sfx}": p.proc.pid for p in self.procs}
 
     # ------------------------------------------------------------------ waiting
 
-    async def _cp_idle(self, last: list) -> bool:
-        """Process mode: every workqueue of the control plane empty, no worker active, and the
-        reconcile total unchanged since the previous poll (read from its ``/metrics``)."""
-        samples = await self.scrape()
-        busy = sum(samples.get("workqueue_depth", {}).values()) + \
-            sum(samples.get("controller_runtime_active_workers", {}).values())
-        total = sum(samples.get("controller_runtime_reconcile_total", {}).values())
-        quiet = busy == 0 and last and last[0] == total
-        last[:] = [total]
-        return bool(quiet)
+    async def quiesce(self, quiet: float = 0.002, timeout: float = 10.0) -> bool:
+        """Every control-plane process this rank launched idle: queues empty, no reconcile
+        running, no watch event for ``quiet`` s (event-driven inside each process,
+        :meth:`Manager.quiesce`; one request each, answered when they are quiet)."""
+        res = [await mgr.quiesce(quiet, timeout) for mgr in self.managers]
+        if self.procs:
+            q = f"/debug/quiesce?quiet_ms={quiet * 1e3:g}&timeout_s={timeout:g}"
+            res += [d["idle"] for d in await asyncio.gather(*(self._get_json(p.base + q) for p in self.procs))]
+        return all(res)
 
     async def settle(self, timeout: float = 10.0) -> bool:
-        """Platform stand-ins and the control plane idle, three polls in a row."""
-        mgrs = self.managers + ([self.control_plane] if self.control_plane is not None else [])
-        deadline = time.monotonic() + timeout
-        quiet = 0
-        last: list = []
-        while time.monotonic() < deadline:
-            idle = all(mgr.idle() for mgr in mgrs)
-            if idle and self.proc is not None:
-                idle = await self._cp_idle(last)
-            if idle:
-                quiet += 1
-                if quiet >= 3:
-                    return True
-            else:
-                quiet = 0
-            await asyncio.sleep(0.002 if self.proc is None else 0.01)
-        return False
+        return await self.quiesce(0.002, timeout)
 
     async def wait_until(self, pred: Callable[[], bool], timeout: float = 10.0) -> bool:
         """Event-driven wait: ``pred`` is re-checked on every Notebook / Pod event of the
-        shard's namespace (after the cache applied it) instead of on a polling timer."""
+        rank's namespace (after the cache applied it) instead of on a polling timer."""
         if pred():
             return True
         if self._waiters is None:
@@ -322,30 +309,25 @@ class ControlPlaneShard:
             self._waiters.discard(w)
 
     async def wait_for(self, pred: Callable[[], bool], timeout: float = 10.0, interval: float = 0.0005) -> bool:
-        deadline = time.monotonic() + timeout
-        while time.monotonic() < deadline:
+        loop = asyncio.get_running_loop()
+        deadline = loop.time() + timeout
+        while loop.time() < deadline:
             if pred():
                 return True
             await asyncio.sleep(interval)
         return pred()
 
-    @property
-    def probe_results(self) -> List[dict]:
-        return self.agent.probe_results if self.agent is not None else []
-
     async def stop(self) -> None:
+        from .platform import stop_child
+
         for mgr in reversed(self.managers):
             await mgr.stop()
-        if self.control_plane is not None:
-            await self.control_plane.stop()
-        if self.proc is not None:
-            self.proc.terminate()
-            try:
-                await asyncio.wait_for(asyncio.get_running_loop().run_in_executor(None, self.proc.wait), 10)
-            except asyncio.TimeoutError:
-                self.proc.kill()
+        for p in self.procs:
+            await stop_child(p.proc)
         for c in self._caches:
             await c.stop()
+        if self._http is not None:
+            await self._http.close()
         await self.rest.close()
         if self._certs is not None:
             shutil.rmtree(self._certs.cert_dir, ignore_errors=True)

@@ -1,5 +1,6 @@
-"""Client interfaces (the ``client.Client`` / ``client.Reader`` analogues) and the
-in-process implementation over :class:`~odh_kubeflow_amd.apiserver.store.ObjectStore`.
+"""Client interfaces (the ``client.Client`` / ``client.Reader`` analogues) and the cached
+client every manager writes through.  (The in-process implementation over the test
+platform's object store lives in :mod:`odh_kubeflow_amd.testing.apiserver.inprocess`.)
 
 Two access paths, as in controller-runtime:
 
@@ -19,7 +20,6 @@ import contextvars
 import abc
 from typing import Any, Callable, Dict, Iterable, List, Optional, Sequence, Tuple
 
-from ..apiserver.store import ObjectStore
 from ..models.scheme import SCHEME
 from ..utils.objutil import deepcopy_json
 
@@ -129,77 +129,6 @@ class Client(abc.ABC):
             if is_not_found(e):
                 return None
             raise
-
-
-class StoreReader(Reader):
-    """Zero-copy reads straight from the in-process store (an always-synced cache)."""
-
-    def __init__(self, store: ObjectStore):
-        self.store = store
-
-    def get(self, kind, name, namespace=None):
-        return self.store.peek(kind, name, namespace)
-
-    def list(self, kind, namespace=None, labels=None, fields=None, owner_uid=None):
-        return self.store.list_nocopy(kind, namespace, labels, fields, owner_uid)
-
-
-class StoreEventSource(EventSource):
-    def __init__(self, store: ObjectStore):
-        self.store = store
-
-    def subscribe(self, kind, callback, namespace=None):
-        return self.store.watch(kind, callback, namespace=namespace, initial=True)
-
-
-class InProcessClient(Client):
-    """Client talking to an in-process :class:`ObjectStore`.
-
-    ``user`` is recorded for audit/debugging only; the in-process path does no authz.
-    """
-
-    def __init__(self, store: ObjectStore, user: str = "system:admin"):
-        self.store = store
-        self.user = user
-
-    async def get(self, kind, name, namespace=None):
-        return await self.store.get(kind, name, namespace, version=_version_of(kind))
-
-    async def list(self, kind, namespace=None, labels=None, fields=None, owner_uid=None):
-        items, _ = await self.store.list(kind, namespace, labels, fields, version=_version_of(kind),
-                                         owner_uid=owner_uid)
-        return items
-
-    async def create(self, obj):
-        return _refresh(obj, await self.store.create(obj))
-
-    async def update(self, obj):
-        return _refresh(obj, await self.store.update(obj))
-
-    async def update_status(self, obj):
-        return _refresh(obj, await self.store.update(obj, subresource="status"))
-
-    async def patch(self, obj_or_kind, patch, patch_type="merge", name=None, namespace=None, subresource=None):
-        if isinstance(obj_or_kind, dict):
-            kind = obj_or_kind
-            name = name or obj_or_kind["metadata"]["name"]
-            namespace = namespace or obj_or_kind["metadata"].get("namespace")
-        else:
-            kind = obj_or_kind
-        res = await self.store.patch(kind, name, namespace, patch, patch_type, subresource)
-        v = _version_of(kind)
-        if v:
-            info = SCHEME.resolve(kind)
-            res["apiVersion"] = info.api_version(v)
-        if isinstance(obj_or_kind, dict):
-            return _refresh(obj_or_kind, res)
-        return res
-
-    async def delete(self, obj_or_kind, name=None, namespace=None, preconditions=None, propagation="Background"):
-        if isinstance(obj_or_kind, dict):
-            name = name or obj_or_kind["metadata"]["name"]
-            namespace = namespace or obj_or_kind["metadata"].get("namespace")
-        return await self.store.delete(obj_or_kind, name, namespace, preconditions, propagation)
 
 
 class CachedClient(Client):

@@ -115,6 +115,7 @@ class _Informer:
 
     def _notify(self, etype: str, obj: dict, old: Optional[dict]) -> None:
         self.events += 1
+        self.cache.last_event = time.monotonic()
         ns = m.namespace(obj)
         for hns, cb in list(self.handlers.values()):
             if hns and hns != ns:
@@ -260,6 +261,7 @@ class InformerCache(Reader, EventSource):
         self._hid = 0
         self._ns_informer: Optional[_Informer] = None
         self.namespace_changes = 0
+        self.last_event = 0.0  # monotonic time of the last watch event delivered (Manager.quiesce)
 
     # -------------------------------------------------------------- namespace membership
 

@@ -20,8 +20,7 @@ from typing import Callable, Dict, List, Optional, Sequence
 
 from prometheus_client import CollectorRegistry, generate_latest
 
-from ..apiserver.store import ObjectStore
-from .client import CachedClient, Client, EventSource, InProcessClient, Reader, StoreEventSource, StoreReader
+from .client import CachedClient, Client, EventSource, Reader
 from .controller import DEFAULT_MAX_CONCURRENT_RECONCILES, Builder, Controller
 from .events import EventRecorder
 from .metrics import RuntimeMetrics
@@ -33,7 +32,8 @@ class Manager:
     def __init__(self, client: Client, reader: Reader, source: EventSource, name: str = "manager",
                  registry: Optional[CollectorRegistry] = None,
                  default_max_concurrent: int = DEFAULT_MAX_CONCURRENT_RECONCILES,
-                 leader_elector=None, metrics_addr: Optional[str] = None, probe_addr: Optional[str] = None):
+                 leader_elector=None, metrics_addr: Optional[str] = None, probe_addr: Optional[str] = None,
+                 debug_endpoints: bool = False):
         self.name = name
         self.client = client
         self.reader = reader
@@ -49,6 +49,7 @@ class Manager:
         self.leader_elector = leader_elector
         self.metrics_addr = metrics_addr
         self.probe_addr = probe_addr
+        self.debug_endpoints = debug_endpoints
         self._recorders: Dict[str, EventRecorder] = {}
         self._servers: List = []
         self._started = False
@@ -60,13 +61,6 @@ class Manager:
         self.healthz["leader-election"] = lambda: self.fatal is None
 
     # ------------------------------------------------------------------ construction
-
-    @classmethod
-    def in_process(cls, store: ObjectStore, name: str = "manager", uncached: Sequence = (), **kw) -> "Manager":
-        reader = StoreReader(store)
-        writer = InProcessClient(store, user=f"system:serviceaccount:{name}")
-        client = CachedClient(reader, writer, uncached)
-        return cls(client, reader, StoreEventSource(store), name=name, **kw)
 
     @classmethod
     def remote(cls, config, name: str = "manager", uncached: Sequence = (), transforms=None,
@@ -223,6 +217,27 @@ class Manager:
             await asyncio.sleep(0.002)
         return False
 
+    async def quiesce(self, quiet: float = 0.002, timeout: float = 10.0) -> bool:
+        """Event-driven idle: return once no controller has queued or running work and no
+        watch event has reached this manager's cache for ``quiet`` seconds (the trailing
+        reconciles of a deletion — GC'd children, the pod going away — arrive as watch events
+        after the object itself is gone).  No fixed polling period and no minimum number of
+        checks: it returns ``quiet`` after the last event, or at once if that is long past."""
+        src = getattr(self, "cache", None) or self.reader
+        deadline = time.monotonic() + timeout
+        while True:
+            now = time.monotonic()
+            since = now - getattr(src, "last_event", 0.0)
+            if self.idle() and since >= quiet:
+                for rec in self._recorders.values():
+                    await rec.flush()
+                if self.idle():
+                    return True
+                continue
+            if now >= deadline:
+                return False
+            await asyncio.sleep(max(0.0002, quiet - since) if self.idle() else 0.0002)
+
     def reconcile_count(self) -> int:
         return sum(c.reconciles for c in self.controllers)
 
@@ -250,6 +265,8 @@ class Manager:
                 return web.Response(body=generate_latest(self.registry), content_type="text/plain", charset="utf-8")
 
             app.router.add_get("/metrics", metrics)
+            if self.debug_endpoints:
+                self._add_debug_routes(app)
             await serve(self.metrics_addr, app)
         if self.probe_addr and self.probe_addr not in ("0", ""):
             app = web.Application()
@@ -266,3 +283,22 @@ class Manager:
             app.router.add_get("/healthz", checker(self.healthz))
             app.router.add_get("/readyz", checker(self.readyz))
             await serve(self.probe_addr, app)
+
+    def _add_debug_routes(self, app) -> None:
+        """``--enable-debug-endpoints`` (off in the shipped manifests; benchmarks and e2e use it):
+        ``GET /debug/reconciles`` → reconciles per controller and trigger (JSON, cheaper than
+        parsing ``/metrics``); ``GET /debug/quiesce?quiet_ms=2&timeout_s=10`` → waits for
+        :meth:`quiesce`, then answers ``{"idle": …, "reconciles": …}``."""
+        from aiohttp import web
+
+        async def reconciles(_req):
+            return web.json_response({"reconciles": self.reconcile_breakdown()})
+
+        async def quiesce(req):
+            quiet = float(req.query.get("quiet_ms", "2")) / 1e3
+            timeout = float(req.query.get("timeout_s", "10"))
+            idle = await self.quiesce(quiet, timeout)
+            return web.json_response({"idle": idle, "reconciles": self.reconcile_breakdown()})
+
+        app.router.add_get("/debug/reconciles", reconciles)
+        app.router.add_get("/debug/quiesce", quiesce)

@@ -255,7 +255,7 @@ class RestClient(Client):
     async def _maybe_no_match(self, url: str, err: ApiError) -> None:
         """A 404 on a resource type the server does not serve is ``meta.NoKindMatchError``
         (controller-runtime learns that from the RESTMapper's discovery)."""
-        from ..apiserver.http import parse_path
+        from ..models.scheme import parse_path
         from ..models.errors import NoKindMatch
 
         pp = parse_path(url[len(self.base):].split("?", 1)[0])

@@ -27,7 +27,7 @@ from typing import List, Optional
 import yaml
 
 LEVELS = ("None", "Metadata", "Request", "RequestResponse")
-DEFAULT_POLICY = os.path.join(os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))),
+DEFAULT_POLICY = os.path.join(os.path.dirname(os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))),
                               "config", "debug", "audit-policy.yaml")
 
 

@@ -1,4 +1,4 @@
-"""Kubernetes REST + watch front end for :class:`~odh_kubeflow_amd.apiserver.store.ObjectStore`.
+"""Kubernetes REST + watch front end for :class:`~odh_kubeflow_amd.testing.apiserver.store.ObjectStore`.
 
 This is the out-of-process half of the envtest substitute: the
 managers, the webhook and the node agents talk to it exactly as they talk to a real
@@ -30,11 +30,11 @@ from typing import Callable, Dict, List, Optional
 
 from aiohttp import web
 
-from ..models import meta as m
-from ..models.errors import ApiError, BadRequest, InternalError, NotFound
-from ..models.scheme import SCHEME, ResourceInfo
-from ..utils import jsonpatch
-from ..utils.selectors import match_labels, selector_from_dict
+from ...models import meta as m
+from ...models.errors import ApiError, BadRequest, InternalError, NotFound
+from ...models.scheme import SCHEME, ParsedPath, ResourceInfo, parse_path  # noqa: F401  (re-exported)
+from ...utils import jsonpatch
+from ...utils.selectors import match_labels, selector_from_dict
 from .store import ObjectStore
 
 log = logging.getLogger("apiserver.http")
@@ -53,34 +53,6 @@ def _dumps(o) -> bytes:
 
 def _status_response(e: ApiError) -> web.Response:
     return web.Response(status=e.code, body=_dumps(e.to_status()), content_type="application/json")
-
-
-class ParsedPath:
-    __slots__ = ("info", "version", "namespace", "name", "sub")
-
-    def __init__(self, info, version, namespace, name, sub):
-        self.info, self.version, self.namespace, self.name, self.sub = info, version, namespace, name, sub
-
-
-def parse_path(path: str) -> Optional[ParsedPath]:
-    segs = [s for s in path.split("/") if s]
-    if not segs:
-        return None
-    if segs[0] == "api" and len(segs) >= 3:
-        group, version, rest = "", segs[1], segs[2:]
-    elif segs[0] == "apis" and len(segs) >= 4:
-        group, version, rest = segs[1], segs[2], segs[3:]
-    else:
-        return None
-    ns = None
-    if rest[0] == "namespaces" and len(rest) >= 3 and SCHEME.for_plural(group, rest[2]) is not None:
-        ns, rest = rest[1], rest[2:]
-    info = SCHEME.for_plural(group, rest[0])
-    if info is None or len(rest) > 3:
-        return None
-    name = rest[1] if len(rest) > 1 else None
-    sub = rest[2] if len(rest) > 2 else None
-    return ParsedPath(info, version, ns, name, sub)
 
 
 class WebhookDispatcher:

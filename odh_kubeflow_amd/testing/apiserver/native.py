@@ -1,9 +1,9 @@
-"""Launcher for the native C++ apiserver (``native/apiserver/apiserver.cpp`` →
-``native/bin/odh-apiserver``).
+"""Launcher for the native C++ apiserver (``testing/native/apiserver/apiserver.cpp`` →
+``testing/native/bin/odh-apiserver``).
 
 The scheme (kinds, plurals, scope, versions, status subresource, installed CRDs) is
 generated from :data:`~odh_kubeflow_amd.models.scheme.SCHEME` so both apiservers —
-the in-process Python :class:`~odh_kubeflow_amd.apiserver.store.ObjectStore` and the
+the in-process Python :class:`~odh_kubeflow_amd.testing.apiserver.store.ObjectStore` and the
 native one — serve exactly the same API.  :class:`StoreView` gives tests and the
 benchmark the ``peek`` / ``list_nocopy`` read helpers of the in-process store on top of
 a watch-backed informer cache.
@@ -17,7 +17,7 @@ import os
 import tempfile
 from typing import Iterable, List, Optional
 
-from ..models.scheme import SCHEME
+from ...models.scheme import SCHEME
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 BINARY = os.path.join(os.path.dirname(HERE), "native", "bin", "odh-apiserver")
@@ -31,7 +31,7 @@ def scheme_config(uninstalled: Iterable[str] = (), gc: bool = False, token: Opti
         res.append({"group": i.group, "kind": i.kind, "plural": i.plural, "singular": i.singular,
                     "listKind": i.list_kind, "versions": list(i.versions), "storageVersion": i.storage_version,
                     "namespaced": i.namespaced, "status": i.status_subresource, "installed": i.key not in skip})
-    from ..models.crd import version_schema
+    from ...models.crd import version_schema
 
     # CRD structural schemas: prune -> default -> validate, as models/openapi.py does in-process
     cfg = {"resources": res, "gc": gc, "history": history, "defaulting": True,
@@ -67,7 +67,7 @@ class NativeApiServer:
 
     async def start(self) -> "NativeApiServer":
         if self.binary == BINARY and not available():
-            from ..ops.build import build
+            from ...ops.build import build
 
             build(verbose=False)
         fd, self._cfg_path = tempfile.mkstemp(prefix="odh-apiserver-", suffix=".json")

@@ -37,15 +37,15 @@ from collections import deque
 from dataclasses import dataclass
 from typing import Any, Awaitable, Callable, Deque, Dict, List, Optional, Tuple
 
-from ..models import defaults
-from ..models import meta as m
-from ..models.errors import (AlreadyExists, ApiError, BadRequest, Conflict, Forbidden, Gone, Invalid, NoKindMatch,
+from ...models import defaults
+from ...models import meta as m
+from ...models.errors import (AlreadyExists, ApiError, BadRequest, Conflict, Forbidden, Gone, Invalid, NoKindMatch,
                              NotFound)
-from ..models.scheme import OPTIONAL_CRDS, SCHEME, ResourceInfo
-from ..utils import jsonpatch
-from ..utils.objutil import deepcopy_json, equal_except
-from ..utils.selectors import field_matcher, match_labels, parse_field_selector, parse_label_selector, selector_from_dict
-from ..utils.timeutil import rfc3339
+from ...models.scheme import OPTIONAL_CRDS, SCHEME, ResourceInfo
+from ...utils import jsonpatch
+from ...utils.objutil import deepcopy_json, equal_except
+from ...utils.selectors import field_matcher, match_labels, parse_field_selector, parse_label_selector, selector_from_dict
+from ...utils.timeutil import rfc3339
 
 log = logging.getLogger(__name__)
 
@@ -144,7 +144,7 @@ class ObjectStore:
     def _register_default_validators(self) -> None:
         """The CRD's structural schema (``models/crd.py``: the reference's full PodSpec schema
         + ``validation_patches.yaml``): prune → default → validate on every Notebook write."""
-        from ..models import crd, openapi
+        from ...models import crd, openapi
 
         schema = crd.version_schema()
 

@@ -14,9 +14,10 @@ import time
 from dataclasses import dataclass, field
 from typing import Callable, Dict, List, Optional
 
+from .apiserver.inprocess import in_process_manager
 from .apiserver.store import ObjectStore
-from .models import kinds
-from .runtime.manager import Manager
+from ..models import kinds
+from ..runtime.manager import Manager
 
 
 @dataclass
@@ -34,7 +35,10 @@ class ClusterConfig:
     env: Dict[str, str] = field(default_factory=dict)
     kube_rbac_proxy_image: str = "quay.io/brancz/kube-rbac-proxy:v0.18.1"
     runtime_factory: Optional[Callable[[int], object]] = None  # device -> ContainerRuntime
-    startup_probe: Optional[Callable] = None
+    # run the MI355X start-up probe init container (``amd.com/gpu-probe``) as a real process on
+    # the pod's GPU; ``probe_visible_device`` maps node GPU index -> HIP device of this box
+    exec_gpu_probe: bool = False
+    probe_visible_device: Optional[Callable[[int], int]] = None
     gpu_runtimes_in_process: bool = True  # False: rank processes host GPU runtimes (multi-GPU bench)
     reference_emulation: bool = False  # reproduce the reference's serialising behaviour for comparison
     activity_source: Optional[object] = None
@@ -111,15 +115,15 @@ class LocalCluster:
             mgr = Manager.remote(self.rest_config, name=name, default_max_concurrent=self.cfg.max_concurrent,
                                  shared=self._shared(), **kw)
         else:
-            mgr = Manager.in_process(self.store, name=name, default_max_concurrent=self.cfg.max_concurrent, **kw)
+            mgr = in_process_manager(self.store, name=name, default_max_concurrent=self.cfg.max_concurrent, **kw)
         self.managers.append(mgr)
         return mgr
 
     def _shared(self):
         """One REST pool + informer cache for every remote manager of this process."""
         if getattr(self, "_shared_pair", None) is None:
-            from .runtime.informer import InformerCache, strip_data
-            from .runtime.rest import RestClient
+            from ..runtime.informer import InformerCache, strip_data
+            from ..runtime.rest import RestClient
 
             rest = RestClient(self.rest_config)
             self._shared_pair = (rest, InformerCache(rest, transforms={kinds.CONFIG_MAP: strip_data,
@@ -128,7 +132,7 @@ class LocalCluster:
 
     async def _start_apiserver(self) -> None:
         from .apiserver.http import ApiServer
-        from .runtime.rest import RestConfig
+        from ..runtime.rest import RestConfig
 
         audit = None
         if self.cfg.audit_log_path:
@@ -140,17 +144,17 @@ class LocalCluster:
 
     async def start(self) -> "LocalCluster":
         from .kubelet.agent import default_device_id_of
-        from .kubelet.node import FakeDeviceManager, GpuRuntime, SchedulerController, make_node
+        from .kubelet.node import FakeContainerRuntime, FakeDeviceManager, GpuRuntime, SchedulerController, make_node
         from .kubelet.statefulset import StatefulSetController
-        from .nodeagent.checkpoint import CheckpointWriter
+        from ..nodeagent.checkpoint import CheckpointWriter
 
         cfg = self.cfg
         if cfg.transport == "http":
             await self._start_apiserver()
         if cfg.transport == "native":
             from .apiserver.native import NativeApiServer, StoreView
-            from .runtime.informer import InformerCache
-            from .runtime.rest import RestClient, RestConfig
+            from ..runtime.informer import InformerCache
+            from ..runtime.rest import RestClient, RestConfig
 
             self.native = await NativeApiServer(() if cfg.openshift else OPENSHIFT_CRDS, gc=cfg.gc,
                                                 audit_log_path=cfg.audit_log_path, audit_policy=cfg.audit_policy).start()
@@ -164,7 +168,7 @@ class LocalCluster:
                              kinds.NETWORK_POLICY, kinds.ROLE_BINDING, kinds.CLUSTER_ROLE_BINDING, kinds.HTTP_ROUTE,
                              kinds.REFERENCE_GRANT, kinds.VIRTUAL_SERVICE, kinds.LEASE)])
         else:
-            admin = Manager.in_process(self.store, name="admin").client
+            admin = in_process_manager(self.store, name="admin").client
         self.admin = admin
         if cfg.kubeconfig_path and self.rest_config is not None:
             write_kubeconfig(cfg.kubeconfig_path, self.rest_config.host)
@@ -192,8 +196,8 @@ class LocalCluster:
             dm = self.device_managers[node_name] = FakeDeviceManager(
                 cfg.device_id_of or default_device_id_of(cfg.telemetry), checkpoint=CheckpointWriter(cp_path))
             if cfg.telemetry is not None:
-                from .nodeagent.attribution import Attributor
-                from .nodeagent.server import NodeTelemetryAgent
+                from ..nodeagent.attribution import Attributor
+                from ..nodeagent.server import NodeTelemetryAgent
 
                 self.node_agents[node_name] = await NodeTelemetryAgent(
                     cfg.telemetry, Attributor(cfg.telemetry, checkpoint_path=cp_path, ttl_s=0.0),
@@ -203,9 +207,10 @@ class LocalCluster:
                 self.kubelets.append(kl)
                 for d in range(cfg.gpus_per_node):
                     rt = cfg.runtime_factory(d) if cfg.runtime_factory else None
+                    if rt is None and cfg.exec_gpu_probe:
+                        rt = FakeContainerRuntime(exec_init=True, visible_device=cfg.probe_visible_device)
                     g = GpuRuntime(kl.client, kl.reader, kl.get_event_recorder_for("kubelet"), node_name, [d],
-                                   runtime=rt, startup_probe=cfg.startup_probe, owns_cpu_pods=(d == 0),
-                                   device_manager=dm)
+                                   runtime=rt, owns_cpu_pods=(d == 0), device_manager=dm)
                     g.setup_with_manager(kl, name=f"kubelet-{node_name}-gpu{d}")
                     self.gpu_runtimes.append(g)
 
@@ -220,13 +225,13 @@ class LocalCluster:
         return self
 
     def _build_kf(self) -> None:
-        from .controllers.setup import setup_kf
+        from ..controllers.setup import setup_kf
 
         kf = self.kf = self._mgr("notebook-controller", remote=True)
         culling = bool(self.cfg.culler or self.env.get("ENABLE_CULLING") == "true")
         activity = self.cfg.activity_source
         if culling and activity is None and self.node_agents:
-            from .controllers.culling import NodeAgentActivity
+            from ..controllers.culling import NodeAgentActivity
 
             # every fake node's pods report hostIP 127.0.0.1: route by node name instead
             ports = {n: a.port for n, a in self.node_agents.items()}
@@ -241,18 +246,18 @@ class LocalCluster:
                 self.reconcilers[k] = out[k]
 
     def _build_odh(self) -> None:
-        from .controllers.setup import setup_odh
+        from ..controllers.setup import setup_odh
 
         odh = self.odh = self._mgr("odh-notebook-controller", remote=True, uncached=(kinds.CONFIG_MAP, kinds.SECRET))
         self.reconcilers["odh"] = setup_odh(odh, self.cfg.controller_namespace, self.env,
                                             reference_emulation=self.cfg.reference_emulation)
 
     async def _start_webhook(self) -> None:
-        from .webhook.notebook_webhook import NotebookWebhook, register_in_process
+        from ..webhook.notebook_webhook import NotebookWebhook, register_in_process
 
         if self.rest_config is not None:
-            from .webhook.certs import generate  # noqa: F811
-            from .webhook.server import WebhookServer, mutating_webhook_configuration
+            from ..webhook.certs import generate  # noqa: F811
+            from ..webhook.server import WebhookServer, mutating_webhook_configuration
 
             wh_mgr = self._mgr("odh-webhook", remote=True, uncached=(kinds.CONFIG_MAP, kinds.SECRET))
             self.webhook = NotebookWebhook(wh_mgr.client, self.cfg.controller_namespace,
@@ -262,7 +267,7 @@ class LocalCluster:
             await self.admin.create(mutating_webhook_configuration(
                 certs.ca_bundle_b64, url=f"https://127.0.0.1:{self.webhook_server.port}/mutate-notebook-v1"))
             return
-        wh_mgr = Manager.in_process(self.store, name="odh-webhook", uncached=(kinds.CONFIG_MAP, kinds.SECRET))
+        wh_mgr = in_process_manager(self.store, name="odh-webhook", uncached=(kinds.CONFIG_MAP, kinds.SECRET))
         self.webhook = NotebookWebhook(wh_mgr.client, self.cfg.controller_namespace,
                                        kube_rbac_proxy_image=self.cfg.kube_rbac_proxy_image, env=self.env)
         register_in_process(self.store, self.webhook)
@@ -271,7 +276,7 @@ class LocalCluster:
 
     async def ensure_namespace(self, ns: str) -> None:
         if self.store.peek(kinds.NAMESPACE, ns) is None:
-            from .models.errors import ApiError, is_already_exists
+            from ..models.errors import ApiError, is_already_exists
 
             try:
                 await self.admin.create({"apiVersion": "v1", "kind": "Namespace", "metadata": {"name": ns}})

@@ -1,6 +1,6 @@
 """Development apiserver (the envtest substitute as a process) + kube-controller-manager stand-ins.
 
-    python -m odh_kubeflow_amd.cmd.apiserver --port 6443 --kubeconfig-out /tmp/kc.yaml
+    python -m odh_kubeflow_amd.testing.cmd.apiserver --port 6443 --kubeconfig-out /tmp/kc.yaml
 
 Serves the in-memory store over the Kubernetes REST/watch API.  With ``--controllers``
 it also runs the StatefulSet controller, the scheduler / ``amd.com/gpu`` allocator and
@@ -52,9 +52,9 @@ async def amain(argv=None) -> int:
     from ..apiserver.store import ObjectStore
     from ..kubelet.node import SchedulerController
     from ..kubelet.statefulset import StatefulSetController
-    from ..models import kinds
-    from ..runtime.manager import Manager
-    from .common import setup_logging, signal_event
+    from ...models import kinds
+    from ...runtime.manager import Manager
+    from ...cmd.common import setup_logging, signal_event
 
     args = parse(argv)
     setup_logging(debug=args.debug_log)
@@ -67,7 +67,7 @@ async def amain(argv=None) -> int:
     if args.tls:
         import ssl
 
-        from ..webhook.certs import generate
+        from ...webhook.certs import generate
 
         certs = generate((args.host, "localhost"))
         ctx = ssl.SSLContext(ssl.PROTOCOL_TLS_SERVER)
@@ -79,7 +79,9 @@ async def amain(argv=None) -> int:
         write_kubeconfig(args.kubeconfig_out, srv.url, args.token, ca)
     mgr = None
     if args.controllers:
-        mgr = Manager.in_process(store, name="kube-controller-manager")
+        from ..apiserver.inprocess import in_process_manager
+
+        mgr = in_process_manager(store, name="kube-controller-manager")
         StatefulSetController(mgr.client, mgr.reader, mgr.get_event_recorder_for("statefulset-controller")) \
             .setup_with_manager(mgr)
         SchedulerController(mgr.client, mgr.reader, mgr.get_event_recorder_for("default-scheduler")) \

@@ -1,12 +1,13 @@
 """kube-scheduler stand-in as its own process: binds pods and allocates ``amd.com/gpu``.
 
-    python -m odh_kubeflow_amd.cmd.scheduler --master http://127.0.0.1:6443
+    python -m odh_kubeflow_amd.testing.cmd.scheduler --master http://127.0.0.1:6443
 
 In a real cluster kube-scheduler (plus the AMD device plugin) is a separate process from
 the notebook controllers; the multi-GPU benchmark runs this one as a child of rank 0 so
 that no control-plane shard pays for the whole node's scheduling on its own event loop
-(every shard then reaches the scheduler through the apiserver alike).  Prints ``ready``
-on stdout once its informers have synced.
+(every shard then reaches the scheduler through the apiserver alike).  With
+``--statefulset-controller`` it also plays kube-controller-manager's StatefulSet controller.
+Prints ``ready`` on stdout once its informers have synced.
 """
 
 from __future__ import annotations
@@ -25,16 +26,18 @@ def parse(argv=None):
     p.add_argument("--kubeconfig", default=None)
     p.add_argument("--max-concurrent", type=int, default=1,
                    help="scheduling decisions are serialised by the allocator lock anyway")
+    p.add_argument("--statefulset-controller", action="store_true",
+                   help="also run the StatefulSet controller (kube-controller-manager's part of the notebook path)")
     p.add_argument("--debug-log", action="store_true")
     return p.parse_args(argv)
 
 
 async def amain(argv=None) -> int:
     from ..kubelet.node import SchedulerController
-    from ..models import kinds
-    from ..runtime.manager import Manager
-    from ..runtime.rest import RestConfig
-    from .common import setup_logging, signal_event
+    from ...models import kinds
+    from ...runtime.manager import Manager
+    from ...runtime.rest import RestConfig
+    from ...cmd.common import setup_logging, signal_event
 
     args = parse(argv)
     setup_logging(debug=args.debug_log)
@@ -42,8 +45,15 @@ async def amain(argv=None) -> int:
     mgr = Manager.remote(cfg, name="kube-scheduler")
     SchedulerController(mgr.client, mgr.reader, mgr.get_event_recorder_for("default-scheduler")) \
         .setup_with_manager(mgr, max_concurrent=args.max_concurrent)
+    synced = [kinds.POD, kinds.NODE]
+    if args.statefulset_controller:
+        from ..kubelet.statefulset import StatefulSetController
+
+        StatefulSetController(mgr.client, mgr.reader, mgr.get_event_recorder_for("statefulset-controller")) \
+            .setup_with_manager(mgr)
+        synced.append(kinds.STATEFUL_SET)
     await mgr.start()
-    await mgr.cache.wait_synced([kinds.POD, kinds.NODE, kinds.NAMESPACE])
+    await mgr.cache.wait_synced(synced)
     print("ready", flush=True)
     await signal_event().wait()
     await mgr.stop()

@@ -4,9 +4,10 @@ It plays the node-side platform pieces a real MI355X node already has, so the co
 plane can be exercised without a cluster:
 
 * registers the ``Node`` (capacity ``amd.com/gpu``, AMD node-labeller labels) — the kubelet's job;
-* runs :class:`~odh_kubeflow_amd.kubelet.node.GpuRuntime` for its devices (start pods,
-  optionally gate Ready on the MI355X start-up probe, report pod status) — the kubelet's job;
-* publishes GPU allocations through a :class:`~odh_kubeflow_amd.kubelet.node.FakeDeviceManager`
+* runs :class:`~odh_kubeflow_amd.testing.kubelet.node.GpuRuntime` for its devices (run init
+  containers — the MI355X start-up probe as a real process when the runtime executes init
+  containers —, start pods, report pod status) — the kubelet's job;
+* publishes GPU allocations through a :class:`~odh_kubeflow_amd.testing.kubelet.node.FakeDeviceManager`
   (device-plugin checkpoint file) — the kubelet device manager's job;
 * optionally hosts the **production** node agent
   (:class:`~odh_kubeflow_amd.nodeagent.server.NodeTelemetryAgent`) next to it, which attributes
@@ -22,7 +23,7 @@ import os
 import tempfile
 from typing import Callable, Dict, List, Optional, Sequence
 
-from ..models.errors import ApiError, is_already_exists
+from ...models.errors import ApiError, is_already_exists
 from .node import FakeDeviceManager, GpuRuntime, make_node
 
 
@@ -37,7 +38,7 @@ def pci_bus_index_map(telemetry, local_bus_ids: Dict[int, int]) -> Dict[int, int
 def default_device_id_of(telemetry=None) -> Callable[[int], str]:
     """Device-plugin IDs for node GPU indices: the PCI address of the telemetry device with
     that index when there is one, else the synthetic-tree address."""
-    from ..ops.telemetry import fake_bdf
+    from ...ops.telemetry import fake_bdf
 
     devs = telemetry.devices() if telemetry is not None else []
 
@@ -48,10 +49,10 @@ def default_device_id_of(telemetry=None) -> Callable[[int], str]:
 
 class FakeKubeletAgent:
     def __init__(self, mgr, node_name: str, devices: Sequence[int], node_gpus: int = 8, runtime=None,
-                 startup_probe=None, telemetry=None, register_node: bool = True, owns_cpu_pods: bool = True,
+                 telemetry=None, register_node: bool = True, owns_cpu_pods: bool = True,
                  address: str = "127.0.0.1", activity_port: int = 0, checkpoint_path: Optional[str] = None,
-                 device_id_of: Optional[Callable[[int], str]] = None):
-        from ..nodeagent.checkpoint import CheckpointWriter
+                 device_id_of: Optional[Callable[[int], str]] = None, one_runtime: bool = False):
+        from ...nodeagent.checkpoint import CheckpointWriter
 
         self.mgr = mgr
         self.node_name = node_name
@@ -68,18 +69,21 @@ class FakeKubeletAgent:
                                                 checkpoint=CheckpointWriter(checkpoint_path))
         self.telemetry_agent = None
         if telemetry is not None:
-            from ..nodeagent.attribution import Attributor
-            from ..nodeagent.server import NodeTelemetryAgent
+            from ...nodeagent.attribution import Attributor
+            from ...nodeagent.server import NodeTelemetryAgent
 
             self.telemetry_agent = NodeTelemetryAgent(
                 telemetry, Attributor(telemetry, checkpoint_path=checkpoint_path, ttl_s=0.0),
                 host=address, port=activity_port)
         self.runtimes: List[GpuRuntime] = []
-        for i, d in enumerate(self.devices):
-            g = GpuRuntime(mgr.client, mgr.reader, mgr.get_event_recorder_for("kubelet"), node_name, [d],
-                           runtime=runtime, startup_probe=startup_probe, owns_cpu_pods=owns_cpu_pods and i == 0,
+        # one_runtime: one kubelet loop for all the node's GPUs (a real kubelet is one process);
+        # otherwise one per GPU (a rank owning its GPU)
+        groups = [self.devices] if one_runtime else [[d] for d in self.devices]
+        for i, devs in enumerate(groups):
+            g = GpuRuntime(mgr.client, mgr.reader, mgr.get_event_recorder_for("kubelet"), node_name, devs,
+                           runtime=runtime, owns_cpu_pods=owns_cpu_pods and i == 0,
                            host_ip=address, device_manager=self.device_manager)
-            g.setup_with_manager(mgr, name=f"kubelet-{node_name}-gpu{d}")
+            g.setup_with_manager(mgr, name=f"kubelet-{node_name}-gpu{'-'.join(map(str, devs))}")
             self.runtimes.append(g)
         mgr.add(self, needs_leader=False)
 

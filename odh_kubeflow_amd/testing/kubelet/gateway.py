@@ -26,11 +26,11 @@ from __future__ import annotations
 import logging
 from typing import List, Optional
 
-from ..models import kinds
-from ..models import meta as m
-from ..models.errors import ApiError, is_not_found
-from ..runtime.controller import Request, Result
-from ..utils.timeutil import rfc3339
+from ...models import kinds
+from ...models import meta as m
+from ...models.errors import ApiError, is_not_found
+from ...runtime.controller import Request, Result
+from ...utils.timeutil import rfc3339
 
 log = logging.getLogger("gateway")
 

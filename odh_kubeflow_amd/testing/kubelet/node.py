@@ -13,10 +13,12 @@ The split follows the MI355X rule "one process per GPU":
   so a pod needs exactly one bind+allocate round trip.  Unschedulable pods get the
   ``PodScheduled=False/Unschedulable`` condition the reference status test expects
   (``kf/controllers/notebook_controller_test.go`` "unschedulablePod").
-* :class:`GpuRuntime` runs in the process that owns a GPU (one per rank in the
-  multi-GPU bench).  It watches pods allocated to its device(s), runs the container
-  runtime — by default an in-process Jupyter-API notebook server plus an MI355X
-  start-up probe (HIP kernels, see ``ops/``) — and reports pod status.
+* :class:`GpuRuntime` is the kubelet half of one or more GPUs.  It watches pods allocated
+  to its device(s), runs their init containers — the MI355X start-up probe
+  (``odh-gpu-probe``) as a real process on the pod's GPUs when the runtime executes init
+  containers — then the container runtime (nothing, a Jupyter-API stand-in, or a real
+  PyTorch-ROCm workbench process), and reports pod status the way a kubelet does
+  (``Initialized`` / ``initContainerStatuses`` / ``Ready``).
 * :class:`FakeDeviceManager` records each allocation where a real kubelet does — the
   device-manager checkpoint file and the pod-resources gRPC API — with the PCI-address
   device IDs the AMD device plugin advertises, so the production node agent attributes
@@ -29,25 +31,21 @@ from __future__ import annotations
 
 import asyncio
 import logging
+import os
+import tempfile
 import time
-from typing import Awaitable, Callable, Dict, Iterable, List, Optional, Sequence, Set
+from typing import Callable, Dict, Iterable, List, Optional, Sequence, Set
 
-from ..models import kinds
-from ..models import meta as m
-from ..models.errors import ApiError, is_conflict, is_not_found
-from ..models.notebook import GPU_IDS_ANNOTATION, GPU_RESOURCE, gpu_request
+from ...models import kinds
+from ...models import meta as m
+from ...models.errors import ApiError, is_conflict, is_not_found
+from ...models.notebook import GPU_IDS_ANNOTATION, GPU_RESOURCE, gpu_request
 
 GPU_INDEX_LABEL = "amd.com/gpu-index"
-# Namespace label naming the GPU index(es) whose node agent runs in the same control-plane
-# shard as the namespace's controllers (``parallel/shard.py``).  The device allocator tries
-# those GPUs first, so a shard's pods start inside the shard's own process instead of
-# waiting on another rank's event loop; a busy preferred GPU falls back to bin-packing.
-GPU_AFFINITY_LABEL = "amd.com/gpu-affinity"
-NAMESPACE_CACHE_WAIT_S = 0.5
-PROBE_CONDITION = "amd.com/GPUProbe"
-from ..runtime.controller import Request, Result, pred_funcs
-from ..utils.quantity import parse_quantity
-from ..utils.timeutil import rfc3339
+INIT_BACKOFF_S = 10.0  # kubelet's first CrashLoopBackOff step for a failed init container
+from ...runtime.controller import Request, Result, pred_funcs
+from ...utils.quantity import parse_quantity
+from ...utils.timeutil import rfc3339
 
 log = logging.getLogger(__name__)
 
@@ -104,8 +102,9 @@ def _tolerates(pod: dict, node: dict) -> bool:
 class SchedulerController:
     """Binds pods to nodes and allocates GPU device indices.
 
-    Policy: the GPUs named by the pod namespace's ``amd.com/gpu-affinity`` label first (if
-    free), then bin-packing by lowest free index.
+    Policy: the device plugin's — the lowest free indices of the node (first free).  Nothing
+    about the pod's namespace or controller steers the choice, as with kube-scheduler plus the
+    AMD device plugin.
     """
 
     def __init__(self, client, reader, recorder, scheduler_name: str = "default-scheduler"):
@@ -119,7 +118,6 @@ class SchedulerController:
         # next scheduling decision before the informer has observed it, so two pods can
         # never be given the same GPU however far the cache lags behind the apiserver.
         self._assumed: Dict[str, tuple] = {}  # pod uid -> (node, cpu, mem, gpu ids)
-        self._ns_wait: Dict[str, float] = {}  # pod uid -> first time its namespace was missing from the cache
 
     def _used(self, node_name: str) -> Dict[str, object]:
         cpu = mem = 0.0
@@ -143,20 +141,8 @@ class SchedulerController:
             gpus.update(aids)
         return {"cpu": cpu, "memory": mem, "gpus": gpus}
 
-    def _preferred_gpus(self, namespace: str) -> List[int]:
-        ns = self.reader.get(kinds.NAMESPACE, namespace)
-        val = m.labels(ns).get(GPU_AFFINITY_LABEL) if ns is not None else None
-        if not val:
-            return []
-        out = []
-        for x in val.replace("_", ",").split(","):
-            if x.strip().isdigit():
-                out.append(int(x))
-        return out
-
     def forget(self, pod: dict) -> None:
         self._assumed.pop(m.uid(pod), None)
-        self._ns_wait.pop(m.uid(pod), None)
 
     async def reconcile(self, req: Request) -> Result:
         pod = self.reader.get(kinds.POD, req.name, req.namespace)
@@ -164,13 +150,6 @@ class SchedulerController:
             return Result()
         if m.uid(pod) in self._assumed:
             return Result()  # bound already; the cache has not caught up yet
-        if self.reader.get(kinds.NAMESPACE, req.namespace) is None and gpu_request(pod.get("spec") or {}):
-            # the namespace (and its gpu-affinity label) has not reached this cache yet: a
-            # pod cannot outlive its namespace's creation by much, so wait briefly for it
-            first = self._ns_wait.setdefault(m.uid(pod), time.monotonic())
-            if time.monotonic() - first < NAMESPACE_CACHE_WAIT_S:
-                return Result(requeue_after=0.002)
-        self._ns_wait.pop(m.uid(pod), None)
         async with self._lock:  # allocation decisions must not race each other
             return await self._schedule(pod)
 
@@ -199,10 +178,6 @@ class SchedulerController:
             if alloc.get("memory") and used["memory"] + need["memory"] > float(parse_quantity(alloc["memory"]).value):
                 reasons.append("Insufficient memory")
                 continue
-            if need["gpu"]:
-                pref = self._preferred_gpus(m.namespace(pod))
-                if pref:
-                    free = [i for i in pref if i in free] + [i for i in free if i not in pref]
             ids = free[: need["gpu"]]
             patch = {"spec": {"nodeName": m.name(node)}}
             if ids:
@@ -253,8 +228,6 @@ class SchedulerController:
         return (mgr.builder().named("scheduler").for_(kinds.POD, [unbound])
                 .watches(kinds.POD, pods_released, [pred_funcs(create=lambda o: False, update=lambda o, old: False,
                                                                delete=lambda o: True)])
-                # namespaces carry the gpu-affinity label: synced before the first decision
-                .watches(kinds.NAMESPACE, lambda o: [], [lambda et, o, old: False])
                 .with_options(max_concurrent_reconciles=max_concurrent).complete(self))
 
 
@@ -271,8 +244,67 @@ class ContainerHandle:
         self.started_at = time.time()
 
 
+def is_gpu_probe(container: dict) -> bool:
+    """The MI355X start-up probe init container (``controllers/notebook.py``
+    ``gpu_probe_init_container``): its command is the ``odh-gpu-probe`` program."""
+    cmd = container.get("command") or []
+    return bool(cmd) and os.path.basename(str(cmd[0])) == "odh-gpu-probe"
+
+
+async def run_gpu_probe_container(container: dict, visible: Sequence[int], timeout_s: float = 120.0) -> dict:
+    """Run the probe init container the way a kubelet would: as its own process, seeing only
+    the pod's GPUs (``HIP_VISIBLE_DEVICES``, the device plugin's job), its
+    ``/dev/termination-log`` a file whose content becomes the termination message.  Only the
+    image is missing: the in-tree ``odh-gpu-probe`` binary stands in for it."""
+    from ...ops import probe_main
+
+    fd, term = tempfile.mkstemp(prefix="odh-termination-log-")
+    os.close(fd)
+    args = [term if a == "/dev/termination-log" else str(a) for a in container.get("args") or []]
+    env = {k: v for k, v in os.environ.items() if not k.startswith(("HIP_VISIBLE", "ROCR_VISIBLE", "CUDA_VISIBLE"))}
+    env["HIP_VISIBLE_DEVICES"] = ",".join(str(d) for d in dict.fromkeys(visible))
+    for e in container.get("env") or []:
+        if "value" in e:
+            env[e["name"]] = str(e["value"])
+    t0 = time.perf_counter()
+    proc = await asyncio.create_subprocess_exec(*probe_main.command(args), env=env, stdout=asyncio.subprocess.PIPE,
+                                                stderr=asyncio.subprocess.PIPE)
+    try:
+        out, err = await asyncio.wait_for(proc.communicate(), timeout_s)
+        rc = proc.returncode
+    except asyncio.TimeoutError:
+        proc.kill()
+        out, err = await proc.communicate()
+        rc = 137
+    wall_ms = (time.perf_counter() - t0) * 1e3
+    try:
+        with open(term) as f:
+            msg = f.read()
+    finally:
+        os.unlink(term)
+    if not msg and container.get("terminationMessagePolicy") == "FallbackToLogsOnError" and rc != 0:
+        msg = ((out or b"") + (err or b"")).decode(errors="replace")[-4096:]
+    return {"exitCode": rc, "message": msg[:4096], "wall_ms": wall_ms, "result": probe_main.parse_result(msg)}
+
+
 class ContainerRuntime:
-    """CRI-ish interface: start/stop the containers of one pod."""
+    """CRI-ish interface: run a pod's init containers, start/stop its app containers.
+
+    ``exec_init`` makes :meth:`run_init` execute the init containers this node can run
+    without an image — the MI355X start-up probe (``odh-gpu-probe``) — as real processes on the
+    pod's GPUs; every other init container (and every init container when ``exec_init`` is
+    off) completes at once, as app containers do in the fake runtimes.  ``visible_device``
+    maps a node GPU index to the HIP device the process should see (a one-GPU box hosts all
+    eight node GPUs on its device 0)."""
+
+    exec_init: bool = False
+    visible_device: Optional[Callable[[int], int]] = None
+
+    async def run_init(self, pod: dict, container: dict, devices: Sequence[int]) -> dict:
+        if self.exec_init and devices and is_gpu_probe(container):
+            vis = self.visible_device or (lambda d: d)
+            return await run_gpu_probe_container(container, [vis(d) for d in devices])
+        return {"exitCode": 0, "message": "", "wall_ms": 0.0, "result": None}
 
     async def start(self, pod: dict, devices: Sequence[int]) -> ContainerHandle:
         return ContainerHandle(m.key(pod), devices)
@@ -285,16 +317,16 @@ class ContainerRuntime:
 
 
 class FakeContainerRuntime(ContainerRuntime):
-    def __init__(self, start_delay: float = 0.0):
+    def __init__(self, start_delay: float = 0.0, exec_init: bool = False,
+                 visible_device: Optional[Callable[[int], int]] = None):
         self.start_delay = start_delay
+        self.exec_init = exec_init
+        self.visible_device = visible_device
 
     async def start(self, pod, devices):
         if self.start_delay:
             await asyncio.sleep(self.start_delay)
         return ContainerHandle(m.key(pod), devices)
-
-
-StartupProbe = Callable[[Sequence[int]], Awaitable[dict]]
 
 
 class FakeDeviceManager:
@@ -329,18 +361,29 @@ class FakeDeviceManager:
             self.pod_resources.release(namespace, name)
 
 
+def _terminated_status(container: dict, r: dict) -> dict:
+    """``initContainerStatuses[]`` entry of an init container that ran to completion."""
+    ok = r["exitCode"] == 0
+    term = {"exitCode": r["exitCode"], "reason": "Completed" if ok else "Error", "startedAt": rfc3339(),
+            "finishedAt": rfc3339()}
+    if r.get("message"):
+        term["message"] = r["message"]
+    return {"name": container.get("name", ""), "image": container.get("image", ""), "imageID": "", "ready": ok,
+            "restartCount": 0, "started": False, "state": {"terminated": term}}
+
+
 class GpuRuntime:
     """Per-GPU kubelet half: runs pods allocated to ``devices`` on ``node_name``.
 
-    ``devices=None`` makes this runtime also own pods that request no GPU.
-    ``startup_probe`` (e.g. :func:`odh_kubeflow_amd.ops.gpu.startup_probe`) must pass before
-    a GPU pod is reported Ready; its result is recorded as the pod condition
-    ``amd.com/GPUProbe``.
+    ``devices=None`` makes this runtime also own pods that request no GPU.  A pod's init
+    containers run first, in order (:meth:`ContainerRuntime.run_init`); one that fails keeps
+    the pod Pending with ``Initialized=False`` and is retried after a back-off, as the kubelet
+    does for ``restartPolicy: Always`` pods.  Ready is gated on nothing a real kubelet would
+    not gate it on: init containers, then the containers themselves.
     """
 
     def __init__(self, client, reader, recorder, node_name: str, devices: Optional[Iterable[int]],
-                 runtime: Optional[ContainerRuntime] = None, startup_probe: Optional[StartupProbe] = None,
-                 owns_cpu_pods: bool = True, host_ip: str = "127.0.0.1",
+                 runtime: Optional[ContainerRuntime] = None, owns_cpu_pods: bool = True, host_ip: str = "127.0.0.1",
                  device_manager: Optional[FakeDeviceManager] = None):
         self.client = client
         self.reader = reader
@@ -348,13 +391,14 @@ class GpuRuntime:
         self.node_name = node_name
         self.devices = set(devices) if devices is not None else None
         self.runtime = runtime or FakeContainerRuntime()
-        self.startup_probe = startup_probe
         self.owns_cpu_pods = owns_cpu_pods
         self.host_ip = host_ip
         self.device_manager = device_manager
         self.handles: Dict[str, ContainerHandle] = {}
         self.started = 0
-        self.probe_results: List[dict] = []
+        self.probe_results: List[dict] = []  # GPU probe init containers run: exit code, wall time, verdict
+        self.init_backoff_s = INIT_BACKOFF_S
+        self._backoff: Dict[str, tuple] = {}  # pod key -> (uid, monotonic time its failed init may rerun)
 
     def _mine(self, pod: dict) -> bool:
         if (pod.get("spec") or {}).get("nodeName") != self.node_name:
@@ -372,6 +416,7 @@ class GpuRuntime:
         pod = self.reader.get(kinds.POD, req.name, req.namespace)
         h = self.handles.get(key)
         if pod is None or m.is_deleting(pod):
+            self._backoff.pop(key, None)
             if h is not None:
                 self.handles.pop(key, None)
                 await self._stop(h, req)
@@ -387,28 +432,38 @@ class GpuRuntime:
             if not h.info.get("reported"):
                 # started, but the Ready status write failed (connection dropped): report it
                 # now instead of leaving the pod Pending behind a running container
-                await self._set_status(pod, ready=True, handle=h, probe=h.info.get("probe"))
+                await self._set_status(pod, ready=True, handle=h, init_statuses=h.info.get("init_statuses"))
                 h.info["reported"] = True
             return Result()
         ids = m.annotations(pod).get(GPU_IDS_ANNOTATION) or ""
         devices = [int(x) for x in ids.split(",") if x != ""]
-        probe = None
-        if devices and self.startup_probe is not None:
-            probe = await self.startup_probe(devices)
-            self.probe_results.append(probe)
-            if not probe.get("ok", False):
-                await self._set_status(pod, ready=False, reason="GPUProbeFailed", message=str(probe.get("error")))
-                self.recorder.event(pod, "Warning", "GPUProbeFailed", f"MI355X start-up probe failed: {probe}")
-                return Result(requeue_after=5.0)
+        uid, until = self._backoff.get(key, (None, 0.0))
+        if uid == m.uid(pod) and time.monotonic() < until:
+            # CrashLoopBackOff: our own status write (and any other pod event) must not rerun
+            # the failed init container before the back-off has passed
+            return Result(requeue_after=until - time.monotonic())
+        self._backoff.pop(key, None)
+        init_statuses = []
+        for c in (pod.get("spec") or {}).get("initContainers") or []:
+            r = await self.runtime.run_init(pod, c, devices)
+            if is_gpu_probe(c):
+                self.probe_results.append({"pod": key, **r})
+            init_statuses.append(_terminated_status(c, r))
+            if r["exitCode"] != 0:
+                await self._set_status(pod, ready=False, reason="PodInitializing", init_statuses=init_statuses,
+                                       failed_init=c.get("name", ""))
+                self.recorder.event(pod, "Warning", "BackOff", f"Back-off restarting failed container {c.get('name')} "
+                                    f"in pod {m.name(pod)}: exit code {r['exitCode']}")
+                self._backoff[key] = (m.uid(pod), time.monotonic() + self.init_backoff_s)
+                return Result(requeue_after=self.init_backoff_s)
         h = await self.runtime.start(pod, devices)
         h.info["uid"] = m.uid(pod)
+        h.info["init_statuses"] = init_statuses
         if devices and self.device_manager is not None:
             self.device_manager.allocate(pod, devices)
-        if probe is not None:
-            h.info["probe"] = probe
         self.handles[key] = h
         self.started += 1
-        await self._set_status(pod, ready=True, handle=h, probe=probe)
+        await self._set_status(pod, ready=True, handle=h, init_statuses=init_statuses)
         h.info["reported"] = True
         self.recorder.event(pod, "Normal", "Started", "Started container " + ",".join(
             c.get("name", "") for c in (pod.get("spec") or {}).get("containers") or []))
@@ -420,17 +475,23 @@ class GpuRuntime:
         await self.runtime.stop(h)
 
     async def _set_status(self, pod: dict, ready: bool, handle: Optional[ContainerHandle] = None,
-                          reason: str = "", message: str = "", probe: Optional[dict] = None) -> None:
+                          reason: str = "", message: str = "", init_statuses: Optional[List[dict]] = None,
+                          failed_init: str = "") -> None:
         now = rfc3339()
         t = "True" if ready else "False"
+        initialized = not failed_init
         conds = [
             {"type": "PodReadyToStartContainers", "status": "True", "lastProbeTime": None, "lastTransitionTime": now},
-            {"type": "Initialized", "status": "True", "lastProbeTime": None, "lastTransitionTime": now},
+            {"type": "Initialized", "status": "True" if initialized else "False", "lastProbeTime": None,
+             "lastTransitionTime": now},
             {"type": "Ready", "status": t, "lastProbeTime": None, "lastTransitionTime": now},
             {"type": "ContainersReady", "status": t, "lastProbeTime": None, "lastTransitionTime": now},
             {"type": "PodScheduled", "status": "True", "lastProbeTime": None, "lastTransitionTime": now},
         ]
         for c in conds:
+            if not initialized and c["type"] == "Initialized":
+                c["reason"] = "ContainersNotInitialized"
+                c["message"] = f"containers with incomplete status: [{failed_init}]"
             if not ready and c["type"] in ("Ready", "ContainersReady"):
                 c["reason"] = reason or "ContainersNotReady"
                 if message:
@@ -440,21 +501,10 @@ class GpuRuntime:
             st = {"running": {"startedAt": now}} if ready else {"waiting": {"reason": reason or "ContainerCreating"}}
             statuses.append({"name": c.get("name", ""), "image": c.get("image", ""), "imageID": "",
                              "ready": ready, "restartCount": 0, "started": ready, "state": st})
-        if probe is not None:
-            # a custom pod condition (the readiness-gate mechanism) instead of an annotation:
-            # the kubelet writes status only, so Ready costs one write, not two
-            ok = bool(probe.get("ok"))
-            r0 = (probe.get("results") or [{}])[0]
-            links = probe.get("links") or []
-            msg = f"bf16 MFMA {r0.get('gemm_tflops', 0):.0f} TFLOP/s, HBM {r0.get('hbm_gbps', 0):.0f} GB/s"
-            if links:  # multi-GPU pod: the xGMI ring over its GPUs was read and verified too
-                msg += f", xGMI {len(links)} links min {min(lk.get('gbps', 0) for lk in links):.0f} GB/s"
-            conds.append({"type": PROBE_CONDITION, "status": "True" if ok else "False",
-                          "reason": "MFMAAndHBMVerified" if ok else "GPUProbeFailed",
-                          "message": msg if ok else str(probe.get("error")),
-                          "lastProbeTime": None, "lastTransitionTime": now})
         status = {"phase": "Running" if ready else "Pending", "conditions": conds, "containerStatuses": statuses,
                   "hostIP": self.host_ip, "podIP": handle.ip if handle else self.host_ip, "startTime": now}
+        if init_statuses:
+            status["initContainerStatuses"] = init_statuses
         if handle is not None and handle.port:
             status["podIPs"] = [{"ip": handle.ip}]
         patch_ann = {}

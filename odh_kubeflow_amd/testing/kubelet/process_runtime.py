@@ -3,12 +3,14 @@
 The fake kubelet's default runtime starts nothing, so pod start-up costs zero and a
 "create → Ready" figure measures only the control plane (BASELINE config #1).  Configs
 #2/#3 need the notebook's own start: this runtime spawns
-:mod:`odh_kubeflow_amd.notebook_server.workbench` per pod — PyTorch imported, the HIP
+:mod:`odh_kubeflow_amd.testing.notebook_server.workbench` per pod — PyTorch imported, the HIP
 runtime initialised on the pod's allocated MI355X (``HIP_VISIBLE_DEVICES``, the device
 plugin's job), a first bf16 matmul, the Jupyter API served — with the container's env
 (``NB_PREFIX`` …) and reports the pod Ready once its readiness probe
-(``GET <NB_PREFIX>/api``) answers.  Image pull and container-runtime overheads are not
-included (no registry or container runtime on the benchmark boxes).
+(``GET <NB_PREFIX>/api``) answers.  A pod's MI355X start-up probe init container
+(``odh-gpu-probe``) runs first, as its own process on the same GPU.  Image pull and
+container-runtime overheads are not included (no registry or container runtime on the
+benchmark boxes).
 
 The readiness probe is polled every ``probe_interval_s`` (20 ms) rather than at the
 kubelet's ``periodSeconds`` granularity (≥ 1 s), to time the process itself.
@@ -23,10 +25,10 @@ import sys
 import time
 from typing import Dict, Optional, Sequence
 
-from ..models import meta as m
+from ...models import meta as m
 from .node import ContainerHandle, ContainerRuntime
 
-ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 
 
 class ProcessContainerRuntime(ContainerRuntime):
@@ -39,6 +41,7 @@ class ProcessContainerRuntime(ContainerRuntime):
         # node GPU index → the HIP device id the process should see (a 1-GPU box hosts all
         # eight "node GPUs" on its one device)
         self.visible_device = visible_device or (lambda d: d)
+        self.exec_init = True  # the start-up probe init container runs as a process too
         self.env = env or {}
         self.procs: Dict[str, asyncio.subprocess.Process] = {}
         self.reports: Dict[str, dict] = {}
@@ -64,7 +67,7 @@ class ProcessContainerRuntime(ContainerRuntime):
         prefix = env.get("NB_PREFIX") or f"/notebook/{m.namespace(pod)}/{m.labels(pod).get('notebook-name', m.name(pod))}"
         t0 = time.perf_counter()
         proc = await asyncio.create_subprocess_exec(
-            sys.executable, "-m", "odh_kubeflow_amd.notebook_server.workbench", "--prefix", prefix,
+            sys.executable, "-m", "odh_kubeflow_amd.testing.notebook_server.workbench", "--prefix", prefix,
             "--host", self.host, "--matmul", str(self.matmul if devices else 0),
             env=env, cwd=ROOT, stdout=asyncio.subprocess.PIPE, stderr=asyncio.subprocess.DEVNULL)
         key = m.key(pod)

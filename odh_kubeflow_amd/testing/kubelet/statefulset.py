@@ -15,11 +15,11 @@ import json
 import logging
 from typing import Optional
 
-from ..models import kinds
-from ..models import meta as m
-from ..models.errors import ApiError, is_already_exists, is_not_found
-from ..runtime.controller import Request, Result, enqueue_for_owner
-from ..utils.objutil import deepcopy_json
+from ...models import kinds
+from ...models import meta as m
+from ...models.errors import ApiError, is_already_exists, is_not_found
+from ...runtime.controller import Request, Result, enqueue_for_owner
+from ...utils.objutil import deepcopy_json
 
 log = logging.getLogger(__name__)
 
@@ -103,7 +103,7 @@ class StatefulSetController:
         return Result()
 
     async def _still_exists(self, sts: dict) -> bool:
-        from ..runtime.client import LIVE_READS
+        from ...runtime.client import LIVE_READS
 
         tok = LIVE_READS.set(True)
         try:

@@ -16,8 +16,8 @@ import uuid
 from typing import Dict, List, Optional, Sequence
 
 from ..kubelet.node import ContainerHandle, ContainerRuntime
-from ..models import meta as m
-from ..utils.timeutil import rfc3339
+from ...models import meta as m
+from ...utils.timeutil import rfc3339
 
 
 class JupyterState:

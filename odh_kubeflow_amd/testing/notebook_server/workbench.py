@@ -1,11 +1,11 @@
 """A PyTorch-ROCm workbench process: what the notebook container runs, minus the image.
 
-    python -m odh_kubeflow_amd.notebook_server.workbench --prefix /notebook/<ns>/<name>
+    python -m odh_kubeflow_amd.testing.notebook_server.workbench --prefix /notebook/<ns>/<name>
 
 BASELINE configs #2/#3 time a notebook pod requesting ``amd.com/gpu`` becoming Ready on an
 MI355X with a PyTorch-ROCm Jupyter image.  There is no container runtime or registry on
 the benchmark boxes, so the test platform's process runtime
-(:class:`~odh_kubeflow_amd.kubelet.process_runtime.ProcessContainerRuntime`) starts this
+(:class:`~odh_kubeflow_amd.testing.kubelet.process_runtime.ProcessContainerRuntime`) starts this
 program as the container's process instead: with the allocated GPU made visible
 (``HIP_VISIBLE_DEVICES``, what the AMD device plugin's device mounts amount to) it imports
 PyTorch, initialises the HIP runtime on the GPU, runs a first bf16 matmul (hipBLASLt and

@@ -21,7 +21,7 @@ from typing import Callable, Optional
 from ..models import defaults
 from ..models import meta as m
 from ..models.errors import is_not_found
-from ..utils.objutil import deepcopy_json, ensure_dict
+from .objutil import deepcopy_json, ensure_dict
 
 
 def _copy_meta(frm: dict, to: dict) -> bool:

@@ -12,9 +12,9 @@ import random
 
 import pytest
 
-from odh_kubeflow_amd.apiserver import native
-from odh_kubeflow_amd.apiserver.http import ApiServer
-from odh_kubeflow_amd.apiserver.store import ObjectStore
+from odh_kubeflow_amd.testing.apiserver import native
+from odh_kubeflow_amd.testing.apiserver.http import ApiServer
+from odh_kubeflow_amd.testing.apiserver.store import ObjectStore
 from odh_kubeflow_amd.models import kinds
 from odh_kubeflow_amd.models.errors import ApiError
 from odh_kubeflow_amd.models.notebook import notebook

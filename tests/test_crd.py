@@ -9,7 +9,7 @@ import os
 import pytest
 import yaml
 
-from odh_kubeflow_amd.cluster import ClusterConfig, LocalCluster
+from odh_kubeflow_amd.testing.cluster import ClusterConfig, LocalCluster
 from odh_kubeflow_amd.models import crd, openapi
 from odh_kubeflow_amd.models.errors import ApiError
 from odh_kubeflow_amd.models.notebook import notebook

@@ -6,13 +6,13 @@ import time
 
 import pytest
 
-from odh_kubeflow_amd.cluster import ClusterConfig, LocalCluster
+from odh_kubeflow_amd.testing.cluster import ClusterConfig, LocalCluster
 from odh_kubeflow_amd.controllers import culling as c
 from odh_kubeflow_amd.models import kinds
 from odh_kubeflow_amd.models import meta as m
 from odh_kubeflow_amd.models.notebook import (LAST_ACTIVITY_ANNOTATION, LAST_ACTIVITY_CHECK_TIMESTAMP_ANNOTATION,
                                               STOP_ANNOTATION, notebook)
-from odh_kubeflow_amd.notebook_server.jupyter import JupyterContainerRuntime
+from odh_kubeflow_amd.testing.notebook_server.jupyter import JupyterContainerRuntime
 from odh_kubeflow_amd.utils import timeutil
 from odh_kubeflow_amd.utils.timeutil import rfc3339
 

@@ -8,8 +8,8 @@ import json
 import pytest
 import yaml
 
-from odh_kubeflow_amd.apiserver.audit import AuditPolicy
-from odh_kubeflow_amd.cluster import ClusterConfig, LocalCluster
+from odh_kubeflow_amd.testing.apiserver.audit import AuditPolicy
+from odh_kubeflow_amd.testing.cluster import ClusterConfig, LocalCluster
 from odh_kubeflow_amd.models import kinds
 from odh_kubeflow_amd.models.notebook import notebook
 from odh_kubeflow_amd.runtime.rest import RestClient, RestConfig

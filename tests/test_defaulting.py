@@ -8,7 +8,7 @@ import copy
 
 import pytest
 
-from odh_kubeflow_amd.cluster import ClusterConfig, LocalCluster
+from odh_kubeflow_amd.testing.cluster import ClusterConfig, LocalCluster
 from odh_kubeflow_amd.models import defaults, kinds
 from odh_kubeflow_amd.models.notebook import notebook
 from odh_kubeflow_amd.runtime.controller import Request

@@ -14,7 +14,7 @@ import sys
 import pytest
 import yaml
 
-from odh_kubeflow_amd.cluster import ClusterConfig, LocalCluster
+from odh_kubeflow_amd.testing.cluster import ClusterConfig, LocalCluster
 from odh_kubeflow_amd.models import kinds
 from odh_kubeflow_amd.models import meta as m
 

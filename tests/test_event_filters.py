@@ -8,13 +8,13 @@ gone, while every change a reconcile actually reads (drift, deletion of a live c
 readiness, stop/restart annotations) still triggers one.
 """
 
-from odh_kubeflow_amd.cluster import ClusterConfig, LocalCluster
+from odh_kubeflow_amd.testing.apiserver.inprocess import in_process_manager
+from odh_kubeflow_amd.testing.cluster import ClusterConfig, LocalCluster
 from odh_kubeflow_amd.models import kinds
 from odh_kubeflow_amd.models import meta as m
 from odh_kubeflow_amd.models.notebook import notebook
 from odh_kubeflow_amd.runtime.controller import Request, Result
-from odh_kubeflow_amd.runtime.manager import Manager
-from odh_kubeflow_amd.apiserver.store import ObjectStore
+from odh_kubeflow_amd.testing.apiserver.store import ObjectStore
 
 
 def _cm(name, data=None):
@@ -26,7 +26,7 @@ def test_own_write_echo_does_not_requeue_but_other_writers_do(run):
     async def go():
         store = ObjectStore()
         await store.create({"apiVersion": "v1", "kind": "Namespace", "metadata": {"name": "ns"}})
-        mgr = Manager.in_process(store, name="t")
+        mgr = in_process_manager(store, name="t")
         seen = []
 
         async def reconcile(req):
@@ -70,7 +70,7 @@ def test_echo_skip_can_be_disabled_like_controller_runtime(run):
     async def go():
         store = ObjectStore()
         await store.create({"apiVersion": "v1", "kind": "Namespace", "metadata": {"name": "ns"}})
-        mgr = Manager.in_process(store, name="t")
+        mgr = in_process_manager(store, name="t")
         mgr.skip_own_write_echoes = False
         seen = []
 

@@ -112,7 +112,7 @@ def test_managers_converge_through_connection_resets(tmp_path, run):
     certs = generate(("127.0.0.1", "localhost"), str(tmp_path / "certs"))
     logf = open(tmp_path / "procs.log", "wb")
     master = f"http://127.0.0.1:{api_port}"
-    procs = [spawn(["odh_kubeflow_amd.cmd.apiserver", "--port", str(api_port), "--controllers",
+    procs = [spawn(["odh_kubeflow_amd.testing.cmd.apiserver", "--port", str(api_port), "--controllers",
                     "--no-openshift-apis"], log=logf)]
     rnd = random.Random(11)
 
@@ -130,7 +130,7 @@ def test_managers_converge_through_connection_resets(tmp_path, run):
                             "--health-probe-bind-address", "0", "--kube-rbac-proxy-image",
                             "quay.io/brancz/kube-rbac-proxy:v0.18.1", "--webhook-cert-dir", certs.cert_dir,
                             "--webhook-port", str(wh_port), "--webhook-host", "127.0.0.1"], common, logf))
-        procs.append(spawn(["odh_kubeflow_amd.cmd.fake_kubelet", "--master", via, "--checkpoint-path",
+        procs.append(spawn(["odh_kubeflow_amd.testing.cmd.fake_kubelet", "--master", via, "--checkpoint-path",
                             str(tmp_path / "dp" / "cp")], common, logf))
         await wait_http(f"https://127.0.0.1:{wh_port}/healthz")
         await c.create(mutating_webhook_configuration(
@@ -212,7 +212,7 @@ def test_odh_manager_crash_mid_burst_recovers(tmp_path, run):
     certs = generate(("127.0.0.1", "localhost"), str(tmp_path / "certs"))
     logf = open(tmp_path / "procs.log", "wb")
     master = f"http://127.0.0.1:{api_port}"
-    procs = {"api": spawn(["odh_kubeflow_amd.cmd.apiserver", "--port", str(api_port), "--controllers",
+    procs = {"api": spawn(["odh_kubeflow_amd.testing.cmd.apiserver", "--port", str(api_port), "--controllers",
                            "--no-openshift-apis"], log=logf)}
     common = {"K8S_NAMESPACE": "opendatahub", "SET_PIPELINE_RBAC": "false"}
     odh_args = ["odh_kubeflow_amd.cmd.odh_manager", "--master", master, "--metrics-bind-address", "0",
@@ -227,7 +227,7 @@ def test_odh_manager_crash_mid_burst_recovers(tmp_path, run):
         procs["kf"] = spawn(["odh_kubeflow_amd.cmd.kf_manager", "--master", master, "--metrics-addr", "0",
                              "--probe-addr", "0"], common, logf)
         procs["odh"] = spawn(odh_args, common, logf)
-        procs["kubelet"] = spawn(["odh_kubeflow_amd.cmd.fake_kubelet", "--master", master, "--checkpoint-path",
+        procs["kubelet"] = spawn(["odh_kubeflow_amd.testing.cmd.fake_kubelet", "--master", master, "--checkpoint-path",
                                   str(tmp_path / "dp" / "cp")], common, logf)
         await wait_http(f"https://127.0.0.1:{wh_port}/healthz")
         await c.create(mutating_webhook_configuration(
@@ -252,12 +252,17 @@ def test_odh_manager_crash_mid_burst_recovers(tmp_path, run):
             await eventually(all_ready, 60)
         except AssertionError:
             raise AssertionError("not all Ready:\n" + await diagnostics(c, names, "crash"))
-        # exactly one of each child per notebook
-        routes = await c.list(kinds.HTTP_ROUTE, "opendatahub")
-        assert sorted(r["metadata"]["name"] for r in routes) == sorted(f"nb-crash-{n}" for n in names)
-        crbs = [x["metadata"]["name"] for x in await c.list(kinds.CLUSTER_ROLE_BINDING)
-                if x["metadata"]["name"].endswith("-crash-auth-delegator")]
-        assert len(crbs) == len(names)
+        # exactly one of each child per notebook (the exposure children — HTTPRoute — are
+        # created after the unlock, so they may trail Ready by a moment: wait for them)
+        async def children_complete():
+            routes = await c.list(kinds.HTTP_ROUTE, "opendatahub")
+            crbs = [x["metadata"]["name"] for x in await c.list(kinds.CLUSTER_ROLE_BINDING)
+                    if x["metadata"]["name"].endswith("-crash-auth-delegator")]
+            return sorted(r["metadata"]["name"] for r in routes) == sorted(f"nb-crash-{n}" for n in names) and \
+                len(crbs) == len(names)
+        await eventually(children_complete, 30)
+        await asyncio.sleep(0.5)  # and no duplicate appears after the fact
+        assert await children_complete()
         for n in names:
             nb = await c.get(kinds.NOTEBOOK, n, "crash")
             assert "kubeflow-resource-stopped" not in (nb["metadata"].get("annotations") or {})
@@ -299,7 +304,7 @@ def test_admission_path_resets_converge(tmp_path, run):
     certs = generate(("127.0.0.1", "localhost"), str(tmp_path / "certs"))
     logf = open(tmp_path / "procs.log", "wb")
     master = f"http://127.0.0.1:{api_port}"
-    procs = [spawn(["odh_kubeflow_amd.cmd.apiserver", "--port", str(api_port), "--controllers",
+    procs = [spawn(["odh_kubeflow_amd.testing.cmd.apiserver", "--port", str(api_port), "--controllers",
                     "--no-openshift-apis"], log=logf)]
     rnd = random.Random(5)
 
@@ -325,7 +330,7 @@ def test_admission_path_resets_converge(tmp_path, run):
                             "--health-probe-bind-address", "0", "--kube-rbac-proxy-image",
                             "quay.io/brancz/kube-rbac-proxy:v0.18.1", "--webhook-cert-dir", certs.cert_dir,
                             "--webhook-port", str(wh_port), "--webhook-host", "127.0.0.1"], common, logf))
-        procs.append(spawn(["odh_kubeflow_amd.cmd.fake_kubelet", "--master", master, "--checkpoint-path",
+        procs.append(spawn(["odh_kubeflow_amd.testing.cmd.fake_kubelet", "--master", master, "--checkpoint-path",
                             str(tmp_path / "dp" / "cp")], common, logf))
         await wait_http(f"https://127.0.0.1:{wh_port}/healthz")
         proxy = await ChaosProxy(wh_port).start()  # TCP-level: TLS passes through untouched
@@ -396,7 +401,7 @@ def test_sharded_control_plane_follows_new_namespaces_through_resets(tmp_path, r
     certs = generate(("127.0.0.1", "localhost"), str(tmp_path / "certs"))
     logf = open(tmp_path / "procs.log", "wb")
     master = f"http://127.0.0.1:{api_port}"
-    procs = [spawn(["odh_kubeflow_amd.cmd.apiserver", "--port", str(api_port), "--controllers",
+    procs = [spawn(["odh_kubeflow_amd.testing.cmd.apiserver", "--port", str(api_port), "--controllers",
                     "--no-openshift-apis"], log=logf)]
     common = {"K8S_NAMESPACE": "opendatahub", "SET_PIPELINE_RBAC": "false", "SET_PIPELINE_SECRET": "false"}
     rnd = random.Random(3)
@@ -422,7 +427,7 @@ def test_sharded_control_plane_follows_new_namespaces_through_resets(tmp_path, r
                                 "--health-probe-bind-address", "0", "--kube-rbac-proxy-image",
                                 "quay.io/brancz/kube-rbac-proxy:v0.18.1", "--webhook-cert-dir", certs.cert_dir,
                                 "--webhook-host", "127.0.0.1", "--webhook-port", str(wh[k])], common, logf))
-        procs.append(spawn(["odh_kubeflow_amd.cmd.fake_kubelet", "--master", master, "--devices",
+        procs.append(spawn(["odh_kubeflow_amd.testing.cmd.fake_kubelet", "--master", master, "--devices",
                             "0,1,2,3,4,5,6,7"], common, logf))
         for k in (0, 1):
             await wait_http(f"https://127.0.0.1:{wh[k]}/healthz")
@@ -492,9 +497,9 @@ def test_informer_cache_matches_server_after_resets(run, server_kind):
     and resourceVersions): watch resume from the last resourceVersion, 410 → relist, and the
     relist's ADDED / MODIFIED / DELETED reconciliation lose and invent nothing — over the
     Python and the C++ apiserver."""
-    from odh_kubeflow_amd.apiserver import native as native_mod
-    from odh_kubeflow_amd.apiserver.http import ApiServer
-    from odh_kubeflow_amd.apiserver.store import ObjectStore
+    from odh_kubeflow_amd.testing.apiserver import native as native_mod
+    from odh_kubeflow_amd.testing.apiserver.http import ApiServer
+    from odh_kubeflow_amd.testing.apiserver.store import ObjectStore
     from odh_kubeflow_amd.runtime.informer import InformerCache
 
     if server_kind == "native" and not native_mod.available():

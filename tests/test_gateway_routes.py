@@ -9,7 +9,7 @@ routes this controller writes resolve in both modes, the reference's 8888 route 
 and a reference-era 8888 route is corrected by the drift check.
 """
 
-from odh_kubeflow_amd.cluster import ClusterConfig, LocalCluster
+from odh_kubeflow_amd.testing.cluster import ClusterConfig, LocalCluster
 from odh_kubeflow_amd.models import kinds
 from odh_kubeflow_amd.models import meta as m
 from odh_kubeflow_amd.models.notebook import notebook
@@ -80,7 +80,7 @@ def test_cross_namespace_backend_needs_the_reference_grant(run):
                                      ["spec"]["from"][0]["namespace"] == CENTRAL, 10)
             assert await cl.wait_for(lambda: (_resolved(cl, "nb") or ("",))[0] == "True", 10)
             # without any grant the gateway may not reach across namespaces: the resolver says so
-            from odh_kubeflow_amd.kubelet.gateway import resolve_backend
+            from odh_kubeflow_amd.testing.kubelet.gateway import resolve_backend
 
             class NoGrants:
                 def list(self, kind, ns=None):

@@ -156,32 +156,6 @@ def test_load_generator_runs(dev):
     assert lg.launches > 5
 
 
-def test_startup_probe_async_hook(dev):
-    import asyncio
-
-    from odh_kubeflow_amd.ops.gpu import startup_probe
-
-    r = asyncio.run(startup_probe([0]))
-    assert r["ok"], r
-    assert r["results"][0]["xcds"] == 8
-
-
-def test_concurrent_probes_of_one_gpu_take_turns(dev):
-    """Several pods probing the same device at once (in-process node agents sharing a GPU)
-    must each get a complete, correct probe — runs share counters, events, host buffer."""
-    import asyncio
-
-    from odh_kubeflow_amd.ops.gpu import startup_probe
-
-    async def many():
-        return await asyncio.gather(*(startup_probe([0]) for _ in range(8)))
-
-    rs = asyncio.run(asyncio.wait_for(many(), 60))
-    for r in rs:
-        assert r["ok"], r
-        assert r["results"][0]["xcds"] == 8 and r["results"][0]["gemm_errors"] == 0
-
-
 @pytest.mark.parametrize("variant", [0, 1, 2, 3])
 @pytest.mark.parametrize("m,n,k", [(256, 256, 64), (512, 768, 192), (1024, 512, 4096), (2048, 2048, 1024)])
 def test_gemm256_variants_match_fp32_reference(dev, variant, m, n, k):
@@ -249,29 +223,3 @@ def test_multi_gpu_pod_xgmi_ring(dev):
     assert len(r["links"]) == (2 if len(devs) == 2 else len(devs))
     for lk in r["links"]:
         assert lk["errors"] == 0 and lk["gbps"] > 10, lk
-
-
-def test_async_probe_runs_on_the_loop_and_takes_turns(dev):
-    """``run_async``: launched and polled from the event loop (no executor thread), same
-    verdict as the synchronous probe, and concurrent probes of one GPU take turns."""
-    import asyncio
-    import threading
-
-    from odh_kubeflow_amd.ops import gpu
-
-    p = gpu.get_probe(0)
-    p.run()
-    threads = set()
-
-    async def one():
-        threads.add(threading.get_ident())
-        return await p.run_async()
-
-    async def many():
-        return await asyncio.gather(*(one() for _ in range(6)))
-
-    rs = asyncio.run(asyncio.wait_for(many(), 60))
-    assert all(r["ok"] and r["graph"] and r["xcds"] == 8 for r in rs), rs
-    assert threads == {threading.get_ident()}
-    r = asyncio.run(gpu.startup_probe([0]))
-    assert r["ok"] and r["results"][0]["graph"]

@@ -9,9 +9,9 @@ import asyncio
 
 import pytest
 
-from odh_kubeflow_amd.apiserver.http import ApiServer, parse_path
-from odh_kubeflow_amd.apiserver.store import ObjectStore
-from odh_kubeflow_amd.cluster import ClusterConfig, LocalCluster
+from odh_kubeflow_amd.testing.apiserver.http import ApiServer, parse_path
+from odh_kubeflow_amd.testing.apiserver.store import ObjectStore
+from odh_kubeflow_amd.testing.cluster import ClusterConfig, LocalCluster
 from odh_kubeflow_amd.models import kinds
 from odh_kubeflow_amd.models import meta as m
 from odh_kubeflow_amd.models.errors import ApiError, is_already_exists, is_conflict, is_no_match, is_not_found
@@ -50,7 +50,7 @@ def server_kind(request):
 
 async def _server(token=None, kind="python", uninstalled=(), history=4096):
     if kind == "native":
-        from odh_kubeflow_amd.apiserver.native import NativeApiServer
+        from odh_kubeflow_amd.testing.apiserver.native import NativeApiServer
 
         srv = await NativeApiServer(uninstalled=uninstalled, token=token, history=history).start()
         return None, _NativeHandle(srv), RestClient(RestConfig(host=srv.url, token=token))

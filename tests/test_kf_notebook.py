@@ -1,13 +1,13 @@
 """kf NotebookReconciler: envtest-style integration tests (kf/controllers/*_test.go analogues)."""
 
-from odh_kubeflow_amd.cluster import ClusterConfig, LocalCluster
+from odh_kubeflow_amd.testing.cluster import ClusterConfig, LocalCluster
 from odh_kubeflow_amd.controllers.notebook import (create_notebook_status, generate_service, generate_statefulset,
                                                    generate_virtual_service, nb_name_from_involved_object)
 from odh_kubeflow_amd.models import kinds
 from odh_kubeflow_amd.models import meta as m
 from odh_kubeflow_amd.models.notebook import notebook
-from odh_kubeflow_amd.apiserver.store import ObjectStore
-from odh_kubeflow_amd.runtime.client import StoreReader
+from odh_kubeflow_amd.testing.apiserver.store import ObjectStore
+from odh_kubeflow_amd.testing.apiserver.inprocess import StoreReader
 from odh_kubeflow_amd.runtime.controller import Request
 
 
@@ -90,7 +90,7 @@ def test_create_notebook_status_table():
 def test_nb_name_from_involved_object(run):
     async def go():
         store = ObjectStore()
-        from odh_kubeflow_amd.runtime.client import InProcessClient
+        from odh_kubeflow_amd.testing.apiserver.inprocess import InProcessClient
         c = InProcessClient(store)
         await c.create({"apiVersion": "v1", "kind": "Pod", "metadata": {"name": "test-notebook-0",
                         "namespace": "test-namespace", "labels": {"notebook-name": "test-notebook"}}, "spec": {}})
@@ -169,8 +169,9 @@ def test_eight_notebooks_fill_eight_gpus_ninth_unschedulable(run):
     run(go())
 
 
-def test_gpu_affinity_label_steers_allocation(run):
-    """Namespace ``amd.com/gpu-affinity`` first, lowest free index when the preferred GPU is taken."""
+def test_gpu_allocation_is_first_free_whatever_the_namespace(run):
+    """The device plugin's policy: lowest free indices; a namespace label steers nothing
+    (the old ``amd.com/gpu-affinity`` steering is gone — no real scheduler honours it)."""
     async def go():
         async with LocalCluster(ClusterConfig()) as cl:
             await cl.admin.create({"apiVersion": "v1", "kind": "Namespace",
@@ -179,15 +180,22 @@ def test_gpu_affinity_label_steers_allocation(run):
             await cl.admin.create(notebook("a", "team", gpus=1))
             assert await cl.wait_for(lambda: cl.notebook_ready("a", "team"), 10)
             await cl.admin.create(notebook("b", "team", gpus=2))
+            assert await cl.wait_for(lambda: cl.notebook_ready("b", "team"), 10)
             await cl.admin.create(notebook("c", "other", gpus=1))
-            assert await cl.wait_for(lambda: cl.notebook_ready("b", "team") and cl.notebook_ready("c", "other"), 10)
+            assert await cl.wait_for(lambda: cl.notebook_ready("c", "other"), 10)
 
             def ids(nm, ns):
                 return m.annotations(cl.store.peek(kinds.POD, f"{nm}-0", ns))["amd.com/gpu-ids"]
-            assert ids("a", "team") == "5"
-            assert ids("b", "team") == "6,0"  # 5 is taken: 6, then bin-packing from the lowest index
-            assert ids("c", "other") == "1"
-            assert m.labels(cl.store.peek(kinds.POD, "b-0", "team"))["amd.com/gpu-index"] == "6"
+            assert ids("a", "team") == "0"
+            assert ids("b", "team") == "1,2"
+            assert ids("c", "other") == "3"
+            assert m.labels(cl.store.peek(kinds.POD, "b-0", "team"))["amd.com/gpu-index"] == "1"
+            # a released GPU is the next one handed out
+            await cl.admin.delete(kinds.NOTEBOOK, "a", "team")
+            assert await cl.wait_for(lambda: cl.store.peek(kinds.POD, "a-0", "team") is None, 10)
+            await cl.admin.create(notebook("d", "other", gpus=1))
+            assert await cl.wait_for(lambda: cl.notebook_ready("d", "other"), 10)
+            assert ids("d", "other") == "0"
     run(go())
 
 

@@ -8,10 +8,10 @@ import subprocess
 import sys
 import time
 
-from odh_kubeflow_amd.apiserver.store import ObjectStore
+from odh_kubeflow_amd.testing.apiserver.inprocess import in_process_manager
+from odh_kubeflow_amd.testing.apiserver.store import ObjectStore
 from odh_kubeflow_amd.models import kinds
 from odh_kubeflow_amd.runtime.leaderelection import LeaderElector
-from odh_kubeflow_amd.runtime.manager import Manager
 from odh_kubeflow_amd.utils.timeutil import rfc3339_micro
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -29,7 +29,7 @@ def test_skewed_holder_clock_does_not_expire_a_live_lease(run):
     Once it stops renewing, the candidate takes over after one lease duration."""
     async def go():
         store = ObjectStore()
-        cli = Manager.in_process(store, name="t").client
+        cli = in_process_manager(store, name="t").client
         await cli.create(_lease("other", rfc3339_micro(time.time() - 3600)))
         stop = asyncio.Event()
 
@@ -59,7 +59,7 @@ def test_skewed_holder_clock_does_not_expire_a_live_lease(run):
 def test_released_lease_is_taken_immediately(run):
     async def go():
         store = ObjectStore()
-        cli = Manager.in_process(store, name="t").client
+        cli = in_process_manager(store, name="t").client
         await cli.create(_lease("", rfc3339_micro(), 1))
         le = LeaderElector(cli, "ctl", "ns", identity="me", lease_duration=15, renew_deadline=10, retry_period=1)
         assert await le.try_acquire_or_renew()
@@ -69,10 +69,10 @@ def test_released_lease_is_taken_immediately(run):
 def test_manager_exits_when_leadership_is_lost(run):
     async def go():
         store = ObjectStore()
-        admin = Manager.in_process(store, name="admin").client
-        le = LeaderElector(Manager.in_process(store, name="le").client, "ctl", "ns", identity="me",
+        admin = in_process_manager(store, name="admin").client
+        le = LeaderElector(in_process_manager(store, name="le").client, "ctl", "ns", identity="me",
                            lease_duration=1.0, renew_deadline=0.4, retry_period=0.05)
-        mgr = Manager.in_process(store, name="kf", leader_elector=le)
+        mgr = in_process_manager(store, name="kf", leader_elector=le)
         stop = asyncio.Event()
         runner = asyncio.ensure_future(mgr.run_until(stop))
         for _ in range(100):
@@ -98,7 +98,7 @@ def test_kf_manager_process_exits_nonzero_on_lost_lease(tmp_path, run):
     api_port = free_port()
     master = f"http://127.0.0.1:{api_port}"
     logf = open(tmp_path / "procs.log", "wb")
-    api = spawn(["odh_kubeflow_amd.cmd.apiserver", "--port", str(api_port), "--no-openshift-apis"], log=logf)
+    api = spawn(["odh_kubeflow_amd.testing.cmd.apiserver", "--port", str(api_port), "--no-openshift-apis"], log=logf)
     mgr = None
     try:
         async def go():

@@ -24,7 +24,7 @@ from odh_kubeflow_amd.runtime.rest import RestClient, RestConfig
 
 pytestmark = pytest.mark.slow
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-SRC = os.path.join(ROOT, "odh_kubeflow_amd", "native", "apiserver", "apiserver.cpp")
+SRC = os.path.join(ROOT, "odh_kubeflow_amd", "testing", "native", "apiserver", "apiserver.cpp")
 
 # OpenSSL is not instrumented: ignore what TSAN cannot see inside it
 TSAN_SUPP = "called_from_lib:libssl.so\ncalled_from_lib:libcrypto.so\n"
@@ -87,11 +87,13 @@ async def _workload(url: str) -> None:
 
 async def _two_shards(url: str) -> None:
     from odh_kubeflow_amd.models.notebook import notebook
+    from odh_kubeflow_amd.parallel.platform import NodePlatform
     from odh_kubeflow_amd.parallel.shard import ControlPlaneShard, ShardConfig
 
     env = {"SET_PIPELINE_RBAC": "false", "SET_PIPELINE_SECRET": "false"}
-    shards = [await ControlPlaneShard(ShardConfig(url, "bench-0", gpu=0, bootstrap=True, env=env)).start()]
-    shards.append(await ControlPlaneShard(ShardConfig(url, "bench-1", gpu=1, env=env)).start())
+    platform = await NodePlatform(url, process=False).start()
+    shards = [await ControlPlaneShard(ShardConfig(url, "bench-0", shard="0", bootstrap=True, env=env)).start()]
+    shards.append(await ControlPlaneShard(ShardConfig(url, "bench-1", shard="1", env=env)).start())
     try:
         for step in range(3):
             for i, sh in enumerate(shards):
@@ -106,12 +108,13 @@ async def _two_shards(url: str) -> None:
     finally:
         for sh in reversed(shards):
             await sh.stop()
+        await platform.stop()
 
 
 @pytest.mark.parametrize("sanitize", ["thread", "address,undefined"])
 def test_native_apiserver_under_sanitizers(run, tmp_path, sanitize):
-    from odh_kubeflow_amd.apiserver.native import NativeApiServer
-    from odh_kubeflow_amd.cluster import OPENSHIFT_CRDS
+    from odh_kubeflow_amd.testing.apiserver.native import NativeApiServer
+    from odh_kubeflow_amd.testing.cluster import OPENSHIFT_CRDS
 
     binary = _build(str(tmp_path), sanitize)
     logs = str(tmp_path / "san")

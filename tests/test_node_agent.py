@@ -173,7 +173,7 @@ def test_agent_http_api(run, sysfs, tmp_path):
 def test_culler_kfd_attribution_only(run, sysfs):
     """No checkpoint, no pod-resources, no annotation: the agent finds each notebook's GPU from
     the processes in its pod cgroup (KFD), culls the idle GPU notebook, keeps the busy one."""
-    from odh_kubeflow_amd.cluster import ClusterConfig, LocalCluster
+    from odh_kubeflow_amd.testing.cluster import ClusterConfig, LocalCluster
     from odh_kubeflow_amd.controllers import culling as c
     from odh_kubeflow_amd.models import kinds
     from odh_kubeflow_amd.models import meta as m

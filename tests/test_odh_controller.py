@@ -18,7 +18,7 @@ import subprocess
 
 import pytest
 
-from odh_kubeflow_amd.cluster import ClusterConfig, LocalCluster
+from odh_kubeflow_amd.testing.cluster import ClusterConfig, LocalCluster
 from odh_kubeflow_amd.controllers.odh import certs, dspa_secret
 from odh_kubeflow_amd.models import kinds
 from odh_kubeflow_amd.models import meta as m
@@ -395,7 +395,7 @@ def test_create_path_order_gating_children_then_one_unlock_write(run, tmp_path, 
     """New Notebook: the objects the pod mounts / runs as and its NetworkPolicies exist
     before the lock goes; finalizers and lock removal are ONE write; the finalizer-managed
     exposure children (ReferenceGrant, HTTPRoute, auth-delegator binding) come after it."""
-    from odh_kubeflow_amd.apiserver.audit import AuditPolicy
+    from odh_kubeflow_amd.testing.apiserver.audit import AuditPolicy
 
     log = tmp_path / "audit.log"
 

@@ -11,10 +11,10 @@ import base64
 
 import pytest
 
-from odh_kubeflow_amd.apiserver.store import ObjectStore
+from odh_kubeflow_amd.testing.apiserver.store import ObjectStore
 from odh_kubeflow_amd.controllers.odh import dspa_secret as ds
 from odh_kubeflow_amd.models.notebook import notebook
-from odh_kubeflow_amd.runtime.client import InProcessClient
+from odh_kubeflow_amd.testing.apiserver.inprocess import InProcessClient
 
 NS = "test-namespace"
 INGRESS = "openshift-ingress"

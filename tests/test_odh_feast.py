@@ -9,7 +9,7 @@ mutating admission path of the in-process apiserver, so the stored object is che
 
 import pytest
 
-from odh_kubeflow_amd.cluster import ClusterConfig, LocalCluster
+from odh_kubeflow_amd.testing.cluster import ClusterConfig, LocalCluster
 from odh_kubeflow_amd.controllers.odh import feast
 from odh_kubeflow_amd.models import kinds
 from odh_kubeflow_amd.models.notebook import notebook

@@ -13,7 +13,7 @@ import copy
 
 import pytest
 
-from odh_kubeflow_amd.cluster import ClusterConfig, LocalCluster
+from odh_kubeflow_amd.testing.cluster import ClusterConfig, LocalCluster
 from odh_kubeflow_amd.controllers.odh import runtime_images
 from odh_kubeflow_amd.models import kinds
 from odh_kubeflow_amd.models.notebook import notebook

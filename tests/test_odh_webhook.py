@@ -12,13 +12,13 @@ import json
 import pytest
 
 from odh_kubeflow_amd import tracing
-from odh_kubeflow_amd.apiserver.store import ObjectStore
+from odh_kubeflow_amd.testing.apiserver.store import ObjectStore
 from odh_kubeflow_amd.controllers.odh import auth, feast, runtime_images
 from odh_kubeflow_amd.controllers.odh.constants import ANNOTATION_UPDATE_PENDING
 from odh_kubeflow_amd.models import kinds
 from odh_kubeflow_amd.models import meta as m
 from odh_kubeflow_amd.models.notebook import notebook
-from odh_kubeflow_amd.runtime.client import InProcessClient
+from odh_kubeflow_amd.testing.apiserver.inprocess import InProcessClient
 from odh_kubeflow_amd.utils import jsonpatch
 from odh_kubeflow_amd.webhook.diff import first_difference
 from odh_kubeflow_amd.webhook.notebook_webhook import NotebookWebhook, register_in_process

@@ -17,7 +17,7 @@ import pytest
 from hypothesis import HealthCheck, given, settings
 from hypothesis import strategies as st
 
-from odh_kubeflow_amd.apiserver import native
+from odh_kubeflow_amd.testing.apiserver import native
 from odh_kubeflow_amd.utils.jsonpatch import (PatchError, apply_merge_patch, apply_patch,
                                               apply_strategic_merge_patch)
 

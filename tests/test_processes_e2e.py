@@ -78,7 +78,7 @@ def test_processes_end_to_end(tmp_path, run):
     certs = generate(("127.0.0.1", "localhost"), str(tmp_path / "certs"))
     logf = open(tmp_path / "procs.log", "wb")
     master = f"http://127.0.0.1:{api_port}"
-    procs = [spawn(["odh_kubeflow_amd.cmd.apiserver", "--port", str(api_port), "--controllers",
+    procs = [spawn(["odh_kubeflow_amd.testing.cmd.apiserver", "--port", str(api_port), "--controllers",
                     "--no-openshift-apis"], log=logf)]
     try:
         async def go():
@@ -99,7 +99,7 @@ def test_processes_end_to_end(tmp_path, run):
             sysfs, cp = str(tmp_path / "sys"), str(tmp_path / "dp" / "kubelet_internal_checkpoint")
             write_fake_sysfs(sysfs, gpus=8)
             agent_port = free_port()
-            procs.append(spawn(["odh_kubeflow_amd.cmd.fake_kubelet", "--master", master, "--devices",
+            procs.append(spawn(["odh_kubeflow_amd.testing.cmd.fake_kubelet", "--master", master, "--devices",
                                 "0,1,2,3,4,5,6,7", "--sysfs-root", sysfs, "--checkpoint-path", cp], common, logf))
             procs.append(spawn(["odh_kubeflow_amd.cmd.node_agent", "--bind", "127.0.0.1", "--port", str(agent_port),
                                 "--sysfs-root", sysfs, "--proc-root", "", "--pod-resources-socket", "",
@@ -182,7 +182,7 @@ def test_processes_notebook_lifecycle_like_reference_e2e(tmp_path, run):
     certs = generate(("127.0.0.1", "localhost"), str(tmp_path / "certs"))
     logf = open(tmp_path / "procs.log", "wb")
     master = f"http://127.0.0.1:{api_port}"
-    procs = [spawn(["odh_kubeflow_amd.cmd.apiserver", "--port", str(api_port), "--controllers",
+    procs = [spawn(["odh_kubeflow_amd.testing.cmd.apiserver", "--port", str(api_port), "--controllers",
                     "--no-openshift-apis"], log=logf)]
     try:
         async def go():
@@ -199,7 +199,7 @@ def test_processes_notebook_lifecycle_like_reference_e2e(tmp_path, run):
                                 "--health-probe-bind-address", "0", "--kube-rbac-proxy-image",
                                 "quay.io/brancz/kube-rbac-proxy:v0.18.1", "--webhook-cert-dir", certs.cert_dir,
                                 "--webhook-port", str(wh_port), "--webhook-host", "127.0.0.1"], common, logf))
-            procs.append(spawn(["odh_kubeflow_amd.cmd.fake_kubelet", "--master", master, "--jupyter",
+            procs.append(spawn(["odh_kubeflow_amd.testing.cmd.fake_kubelet", "--master", master, "--jupyter",
                                 "--checkpoint-path", str(tmp_path / "dp" / "cp")], common, logf))
             await wait_http(f"https://127.0.0.1:{wh_port}/healthz")
             await c.create(mutating_webhook_configuration(
@@ -298,7 +298,7 @@ def test_kf_manager_leader_failover(tmp_path, run):
     api_port = free_port()
     logf = open(tmp_path / "procs.log", "wb")
     master = f"http://127.0.0.1:{api_port}"
-    procs = [spawn(["odh_kubeflow_amd.cmd.apiserver", "--port", str(api_port), "--controllers",
+    procs = [spawn(["odh_kubeflow_amd.testing.cmd.apiserver", "--port", str(api_port), "--controllers",
                     "--no-openshift-apis"], log=logf)]
     managers = {}
     try:
@@ -372,7 +372,7 @@ def test_sharded_control_plane_processes(tmp_path, run):
     certs = generate(("127.0.0.1", "localhost"), str(tmp_path / "certs"))
     logf = open(tmp_path / "procs.log", "wb")
     master = f"http://127.0.0.1:{api_port}"
-    procs = [spawn(["odh_kubeflow_amd.cmd.apiserver", "--port", str(api_port), "--controllers",
+    procs = [spawn(["odh_kubeflow_amd.testing.cmd.apiserver", "--port", str(api_port), "--controllers",
                     "--no-openshift-apis"], log=logf)]
     common = {"K8S_NAMESPACE": "opendatahub", "SET_PIPELINE_RBAC": "false", "SET_PIPELINE_SECRET": "false"}
 
@@ -399,7 +399,7 @@ def test_sharded_control_plane_processes(tmp_path, run):
                     {"key": "notebooks.amd.com/shard", "operator": "DoesNotExist"}]}))
             procs.append(shard(0))
             procs.append(shard(1))
-            procs.append(spawn(["odh_kubeflow_amd.cmd.fake_kubelet", "--master", master, "--devices",
+            procs.append(spawn(["odh_kubeflow_amd.testing.cmd.fake_kubelet", "--master", master, "--devices",
                                 "0,1,2,3,4,5,6,7"], common, logf))
             for k in (0, 1):
                 await wait_http(f"https://127.0.0.1:{wh[k]}/healthz")

@@ -7,8 +7,8 @@ readiness probe answers."""
 import aiohttp
 import pytest
 
-from odh_kubeflow_amd.cluster import ClusterConfig, LocalCluster
-from odh_kubeflow_amd.kubelet.process_runtime import ProcessContainerRuntime
+from odh_kubeflow_amd.testing.cluster import ClusterConfig, LocalCluster
+from odh_kubeflow_amd.testing.kubelet.process_runtime import ProcessContainerRuntime
 from odh_kubeflow_amd.models import kinds
 from odh_kubeflow_amd.models import meta as m
 from odh_kubeflow_amd.models.notebook import notebook

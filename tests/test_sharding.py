@@ -12,13 +12,15 @@ import asyncio
 
 import pytest
 
-from odh_kubeflow_amd.apiserver.http import ApiServer
-from odh_kubeflow_amd.apiserver.store import ObjectStore
+from odh_kubeflow_amd.testing.apiserver.inprocess import in_process_manager
+from odh_kubeflow_amd.testing.apiserver.http import ApiServer
+from odh_kubeflow_amd.testing.apiserver.store import ObjectStore
 from odh_kubeflow_amd.models import kinds
 from odh_kubeflow_amd.models import meta as m
 from odh_kubeflow_amd.models.errors import Conflict
 from odh_kubeflow_amd.models.notebook import notebook
-from odh_kubeflow_amd.runtime.client import CachedClient, InProcessClient, StoreReader
+from odh_kubeflow_amd.runtime.client import CachedClient
+from odh_kubeflow_amd.testing.apiserver.inprocess import InProcessClient, StoreReader
 from odh_kubeflow_amd.runtime.informer import InformerCache
 from odh_kubeflow_amd.runtime.rest import RestClient, RestConfig
 from odh_kubeflow_amd.runtime.retry import retry_on_conflict
@@ -31,7 +33,7 @@ def server_kind(request):
 
 async def _server(kind: str, gc: bool = True):
     if kind == "native":
-        from odh_kubeflow_amd.apiserver.native import NativeApiServer
+        from odh_kubeflow_amd.testing.apiserver.native import NativeApiServer
 
         srv = await NativeApiServer(gc=gc).start()
         return srv, RestClient(RestConfig(host=srv.url))
@@ -195,24 +197,26 @@ def test_retry_on_conflict_reads_live_without_sleeping(run):
 
 def test_two_shards_one_native_apiserver(run):
     async def go():
-        from odh_kubeflow_amd.apiserver.native import NativeApiServer
-        from odh_kubeflow_amd.cluster import OPENSHIFT_CRDS
+        from odh_kubeflow_amd.parallel.platform import NodePlatform
         from odh_kubeflow_amd.parallel.shard import ControlPlaneShard, ShardConfig
+        from odh_kubeflow_amd.testing.apiserver.native import NativeApiServer
+        from odh_kubeflow_amd.testing.cluster import OPENSHIFT_CRDS
 
         native = await NativeApiServer(OPENSHIFT_CRDS, gc=True).start()
         env = {"SET_PIPELINE_RBAC": "false", "SET_PIPELINE_SECRET": "false"}
         shards = []
+        platform = None
         try:
-            shards.append(await ControlPlaneShard(ShardConfig(native.url, "bench-0", gpu=0, bootstrap=True,
+            # one node: one scheduler + StatefulSet controller + kubelet for every shard
+            platform = await NodePlatform(native.url, process=False).start()
+            shards.append(await ControlPlaneShard(ShardConfig(native.url, "bench-0", shard="0", bootstrap=True,
                                                               env=env)).start())
-            shards.append(await ControlPlaneShard(ShardConfig(native.url, "bench-1", gpu=1, env=env)).start())
+            shards.append(await ControlPlaneShard(ShardConfig(native.url, "bench-1", shard="1", env=env)).start())
             ann = {"notebooks.opendatahub.io/inject-auth": "true"}
             for i, sh in enumerate(shards):
-                for j in range(1):
-                    await sh.admin.create(notebook(f"nb{j}", f"bench-{i}", image="img", gpus=1, annotations=ann))
+                await sh.admin.create(notebook("nb0", f"bench-{i}", image="img", gpus=1, annotations=ann))
             for sh in shards:
-                for j in range(1):
-                    assert await sh.wait_for(lambda: sh.notebook_ready(f"nb{j}"), 30)
+                assert await sh.wait_for(lambda: sh.notebook_ready("nb0"), 30)
             # isolation: a shard's control-plane cache (cmd/control_plane.py --shard i: the
             # namespaces labelled notebooks.amd.com/shard=i + the controller namespace) never
             # holds the other shard's objects; HTTPRoutes carry the shard label
@@ -224,22 +228,67 @@ def test_two_shards_one_native_apiserver(run):
                 assert routes and {m.labels(r)["notebook-namespace"] for r in routes} == {f"bench-{i}"}
                 assert {m.labels(r)["notebooks.amd.com/shard"] for r in routes} == {str(i)}
                 assert sh.control_plane.webhook_server.webhook.requests >= 1
-            # each shard's pod got the shard's own GPU (namespace gpu-affinity), so it was
-            # started by the node agent living in the same process
+            # the device plugin's choice, not the shard's: two different GPUs, first free, and
+            # the node's one kubelet started both pods
+            gpus = sorted(m.annotations(p)["amd.com/gpu-ids"] for sh in shards for p in sh.cache.list(kinds.POD))
+            assert gpus == ["0", "1"]
+            assert sum(g.started for g in platform.agent.runtimes) == 2
             for i, sh in enumerate(shards):
-                pods = sh.cache.list(kinds.POD)
-                assert [m.annotations(p)["amd.com/gpu-ids"] for p in pods] == [str(i)]
-                assert [m.labels(p)["amd.com/gpu-index"] for p in pods] == [str(i)]
-            assert [sh.agent.runtimes[0].started for sh in shards] == [1, 1]
-            for i, sh in enumerate(shards):
-                for j in range(1):
-                    await sh.admin.delete(kinds.NOTEBOOK, f"nb{j}", f"bench-{i}")
+                await sh.admin.delete(kinds.NOTEBOOK, "nb0", f"bench-{i}")
             for sh in shards:
-                for j in range(1):
-                    assert await sh.wait_for(lambda: sh.gone(f"nb{j}"), 30)
+                assert await sh.wait_for(lambda: sh.gone("nb0"), 30)
+            for sh in shards:  # event-driven idle of each control plane
+                assert await sh.quiesce(0.002, 10)
         finally:
             for sh in reversed(shards):
                 await sh.stop()
+            if platform is not None:
+                await platform.stop()
+            await native.stop()
+    run(go())
+
+
+def test_unsharded_topology_two_drivers(run):
+    """``--arch unsharded``: one kf manager + one odh manager (the reference topology,
+    overlay mi355x) serve two drivers' namespaces; the second driver launches nothing."""
+    async def go():
+        from odh_kubeflow_amd.parallel.platform import NodePlatform
+        from odh_kubeflow_amd.parallel.shard import ControlPlaneShard, ShardConfig
+        from odh_kubeflow_amd.testing.apiserver.native import NativeApiServer
+        from odh_kubeflow_amd.testing.cluster import OPENSHIFT_CRDS
+
+        native = await NativeApiServer(OPENSHIFT_CRDS, gc=True).start()
+        env = {"SET_PIPELINE_RBAC": "false", "SET_PIPELINE_SECRET": "false"}
+        shards = []
+        platform = None
+        try:
+            platform = await NodePlatform(native.url, process=False).start()
+            shards.append(await ControlPlaneShard(ShardConfig(native.url, "bench-0", arch="unsharded", bootstrap=True,
+                                                              env=env)).start())
+            shards.append(await ControlPlaneShard(ShardConfig(native.url, "bench-1", arch="unsharded", launch=False,
+                                                              env=env)).start())
+            assert [len(sh.managers) for sh in shards] == [2, 0]
+            for i, sh in enumerate(shards):
+                await sh.admin.create(notebook("nb0", f"bench-{i}", image="img", gpus=1,
+                                               annotations={"notebooks.opendatahub.io/inject-auth": "true"}))
+            for sh in shards:
+                assert await sh.wait_for(lambda: sh.notebook_ready("nb0"), 30)
+            wh = shards[0].managers[1].webhook_server.webhook
+            assert wh.requests >= 2  # both namespaces admitted by the one odh webhook
+            for i, sh in enumerate(shards):
+                await sh.admin.delete(kinds.NOTEBOOK, "nb0", f"bench-{i}")
+            for sh in shards:
+                assert await sh.wait_for(lambda: sh.gone("nb0"), 30)
+            assert await shards[0].quiesce(0.002, 10)
+            b = await shards[0].reconcile_breakdown()
+            assert sum(b["notebook-controller"].values()) >= 4  # kf reconciles of both notebooks
+            assert b["odh-notebook-controller"].get("Notebook", 0) >= 2
+            assert await shards[1].reconcile_breakdown() == {}
+        finally:
+            for sh in reversed(shards):
+                await sh.stop()
+            if platform is not None:
+                await platform.stop()
             await native.stop()
     run(go())
 
@@ -294,7 +343,7 @@ def test_namespace_shard_assigner(run):
 
     async def go():
         store = ObjectStore()
-        mgr = Manager.in_process(store, name="cp")
+        mgr = in_process_manager(store, name="cp")
         a = NamespaceShardAssigner(mgr.client, mgr.reader, 4, exclude=["opendatahub"])
         a.setup_with_manager(mgr)
         await mgr.start()
@@ -326,7 +375,7 @@ def test_each_shard_assigns_only_its_own_namespaces(run):
         store = ObjectStore()
         mgrs, assigners = [], []
         for k in ("0", "2"):  # shards 0 and 2 of 3 up, shard 1 down
-            mgr = Manager.in_process(store, name=f"cp-{k}")
+            mgr = in_process_manager(store, name=f"cp-{k}")
             a = NamespaceShardAssigner(mgr.client, mgr.reader, 3, exclude=["opendatahub"], only_shard=k)
             a.setup_with_manager(mgr)
             await mgr.start()

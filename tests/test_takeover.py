@@ -11,7 +11,7 @@ create-or-update helpers), now on objects the apiserver has defaulted."""
 
 import pytest
 
-from odh_kubeflow_amd.cluster import ClusterConfig, LocalCluster
+from odh_kubeflow_amd.testing.cluster import ClusterConfig, LocalCluster
 from odh_kubeflow_amd.models import kinds
 from odh_kubeflow_amd.models.notebook import STOP_ANNOTATION, notebook
 
@@ -32,7 +32,7 @@ async def snapshot(client) -> dict:
 @pytest.mark.parametrize("transport", ["inprocess", "http", "native"])
 def test_fresh_control_plane_adopts_running_notebooks_without_writes(run, transport):
     if transport == "native":
-        from odh_kubeflow_amd.apiserver import native
+        from odh_kubeflow_amd.testing.apiserver import native
 
         if not native.available():
             pytest.skip("native apiserver not built")

@@ -57,17 +57,17 @@ def test_critical_path_from_audit_log(run, tmp_path):
         import critical_path
     finally:
         sys.path.pop(0)
-    from odh_kubeflow_amd.cluster import ClusterConfig, LocalCluster
+    from odh_kubeflow_amd.testing.cluster import ClusterConfig, LocalCluster
     from odh_kubeflow_amd.models.notebook import notebook
 
-    from odh_kubeflow_amd.apiserver import native
+    from odh_kubeflow_amd.testing.apiserver import native
 
     if not native.available():
         pytest.skip("native apiserver not built")
     log = str(tmp_path / "audit.jsonl")
 
     async def go():
-        from odh_kubeflow_amd.apiserver.audit import AuditPolicy
+        from odh_kubeflow_amd.testing.apiserver.audit import AuditPolicy
 
         cfg = ClusterConfig(transport="native", odh=True, webhook=True, audit_log_path=log,
                             audit_policy=AuditPolicy([{"level": "Metadata"}]),

@@ -17,8 +17,8 @@ import json
 from hypothesis import HealthCheck, given, settings
 from hypothesis import strategies as st
 
-from odh_kubeflow_amd.apiserver.store import ObjectStore
-from odh_kubeflow_amd.runtime.client import InProcessClient
+from odh_kubeflow_amd.testing.apiserver.store import ObjectStore
+from odh_kubeflow_amd.testing.apiserver.inprocess import InProcessClient
 from odh_kubeflow_amd.utils.jsonpatch import apply_patch
 from odh_kubeflow_amd.webhook.notebook_webhook import NotebookWebhook
 

@@ -11,9 +11,9 @@ import ssl
 import subprocess
 import sys
 
-from odh_kubeflow_amd.apiserver.store import ObjectStore
+from odh_kubeflow_amd.testing.apiserver.inprocess import in_process_manager
+from odh_kubeflow_amd.testing.apiserver.store import ObjectStore
 from odh_kubeflow_amd.models import kinds
-from odh_kubeflow_amd.runtime.manager import Manager
 from odh_kubeflow_amd.webhook.certs import cert_not_after, generate, provision
 from odh_kubeflow_amd.webhook.server import WebhookServer, mutating_webhook_configuration
 
@@ -58,7 +58,7 @@ def test_cert_rotation_without_restart(run, tmp_path):
 def test_provision_secret_and_ca_bundle(run):
     async def go():
         store = ObjectStore()
-        cli = Manager.in_process(store, name="certs").client
+        cli = in_process_manager(store, name="certs").client
         await cli.create({"apiVersion": "v1", "kind": "Namespace", "metadata": {"name": "opendatahub"}})
         mwc = mutating_webhook_configuration("", service_namespace="opendatahub", name=MWC)
         mwc["webhooks"][0]["clientConfig"].pop("caBundle")
@@ -107,7 +107,7 @@ def test_e2e_admission_after_provisioning(tmp_path, run):
     api_port, wh_port = free_port(), free_port()
     master = f"http://127.0.0.1:{api_port}"
     logf = open(tmp_path / "procs.log", "wb")
-    procs = [spawn(["odh_kubeflow_amd.cmd.apiserver", "--port", str(api_port), "--no-openshift-apis"], log=logf)]
+    procs = [spawn(["odh_kubeflow_amd.testing.cmd.apiserver", "--port", str(api_port), "--no-openshift-apis"], log=logf)]
     try:
         async def go():
             await wait_http(master + "/healthz")
@@ -162,7 +162,7 @@ def test_provision_node_agent_token_secret(run):
 
     async def go():
         store = ObjectStore()
-        cli = Manager.in_process(store, name="certs").client
+        cli = in_process_manager(store, name="certs").client
         await cli.create({"apiVersion": "v1", "kind": "Namespace", "metadata": {"name": "opendatahub"}})
         assert await ensure_token_secret(cli, "opendatahub") == "created"
         sec = await cli.get(kinds.SECRET, TOKEN_SECRET, "opendatahub")

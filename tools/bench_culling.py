@@ -35,11 +35,11 @@ import time
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
-from odh_kubeflow_amd.cluster import ClusterConfig, LocalCluster  # noqa: E402
+from odh_kubeflow_amd.testing.cluster import ClusterConfig, LocalCluster  # noqa: E402
 from odh_kubeflow_amd.models import kinds  # noqa: E402
 from odh_kubeflow_amd.models import meta as m  # noqa: E402
 from odh_kubeflow_amd.models.notebook import STOP_ANNOTATION, notebook  # noqa: E402
-from odh_kubeflow_amd.notebook_server.jupyter import JupyterContainerRuntime  # noqa: E402
+from odh_kubeflow_amd.testing.notebook_server.jupyter import JupyterContainerRuntime  # noqa: E402
 
 N = 8
 
@@ -55,7 +55,7 @@ def _telemetry(cpu: bool):
         return tel, fake_bdf, root, minors
     import torch
 
-    from odh_kubeflow_amd.kubelet.agent import pci_bus_index_map
+    from odh_kubeflow_amd.testing.kubelet.agent import pci_bus_index_map
 
     tel = Telemetry("/sys").start(interval_ms=20, capacity=4000)
     props = torch.cuda.get_device_properties(0)

@@ -1,6 +1,6 @@
 """BASELINE configs #2 and #3 with real notebook processes on the MI355X.
 
-    python tools/bench_real_pods.py [--notebooks 1,8] [--repeats 5] [--reference-emulation]
+    python tools/bench_real_pods.py [--notebooks 1,8] [--repeats 5] [--gpu-probe off,on] [--reference-emulation]
 
 Config #2: one Notebook requesting ``amd.com/gpu: 1`` with a PyTorch-ROCm workbench;
 config #3: eight at once, one per MI355X of the node.  The controllers, the webhook and
@@ -11,9 +11,14 @@ probe answers.  Image pull and container-runtime start are not included (no regi
 container runtime on the benchmark boxes); everything from ``kubectl apply`` to the
 notebook server answering is.  On a one-GPU box the eight "node GPUs" all map to device 0.
 
-Reported per N: create→Ready p50/p95/max, split into control plane (create → pod object
-exists: admission, odh lock, StatefulSet), pod start (pod exists → Ready: scheduling, the
-node agent's start-up probe, the workbench process) and the workbench's own timings.
+Each N runs with the MI355X start-up probe off (the default deployment) and on
+(``amd.com/gpu-probe: "true"``: the kf controller adds the ``odh-gpu-probe`` init container,
+which the kubelet stand-in runs as its own process on the pod's GPU before the workbench).
+Reported per N and probe setting: create→Ready p50/p95/max, split into control plane
+(create → pod object exists: admission, odh lock, StatefulSet), pod start (pod exists →
+Ready: scheduling, the init container, the workbench process), the workbench's own timings
+and the probe's (process wall time, HIP init, allocation, GPU work); with both settings the
+probe's added create→Ready latency (p50 on − p50 off).
 ``--reference-emulation`` restores the reference's serialising odh path (one worker, the
 blocking 1 s + 5 s lock removal) for a same-harness comparison.
 """
@@ -41,9 +46,9 @@ def pct(xs, q):
     return round(xs[lo] + (xs[hi] - xs[lo]) * (k - lo), 1)
 
 
-async def run_n(n: int, repeats: int, emu: bool, matmul: int, probe) -> dict:
-    from odh_kubeflow_amd.cluster import ClusterConfig, LocalCluster
-    from odh_kubeflow_amd.kubelet.process_runtime import ProcessContainerRuntime
+async def run_n(n: int, repeats: int, emu: bool, matmul: int, probe: bool) -> dict:
+    from odh_kubeflow_amd.testing.cluster import ClusterConfig, LocalCluster
+    from odh_kubeflow_amd.testing.kubelet.process_runtime import ProcessContainerRuntime
     from odh_kubeflow_amd.models import kinds
     from odh_kubeflow_amd.models.notebook import notebook
 
@@ -61,7 +66,7 @@ async def run_n(n: int, repeats: int, emu: bool, matmul: int, probe) -> dict:
         rts.append(rt)
         return rt
 
-    cfg = ClusterConfig(odh=True, webhook=True, runtime_factory=factory, startup_probe=probe, reference_emulation=emu,
+    cfg = ClusterConfig(odh=True, webhook=True, runtime_factory=factory, reference_emulation=emu,
                         env={"SET_PIPELINE_RBAC": "false", "SET_PIPELINE_SECRET": "false"})
     total, cp, start = [], [], []
     reports = []
@@ -73,7 +78,8 @@ async def run_n(n: int, repeats: int, emu: bool, matmul: int, probe) -> dict:
             for nm in names:
                 t0[nm] = time.perf_counter()
                 await cl.admin.create(notebook(nm, "bench", gpus=1,
-                                               image="rocm/pytorch:rocm7.0_ubuntu22.04_py3.10_pytorch_release_2.10.0"))
+                                               image="rocm/pytorch:rocm7.0_ubuntu22.04_py3.10_pytorch_release_2.10.0",
+                                               annotations={"amd.com/gpu-probe": "true" if probe else "false"}))
             deadline = time.monotonic() + 600
             while len(ready_at) < n and time.monotonic() < deadline:
                 now = time.perf_counter()
@@ -98,12 +104,22 @@ async def run_n(n: int, repeats: int, emu: bool, matmul: int, probe) -> dict:
                 await cl.admin.delete(kinds.NOTEBOOK, nm, "bench")
             await cl.wait_for(lambda: all(cl.store.peek(kinds.POD, f"{nm}-0", "bench") is None for nm in names), 120)
             await cl.wait_for(lambda: not any(rt.procs for rt in rts), 60)
+        probes = [p for g in cl.gpu_runtimes for p in g.probe_results][n:]  # after the warm-up wave
     wb = {}
     for k in ("import_torch_ms", "first_matmul_ms", "ready_ms", "spawn_to_ready_ms"):
         vals = [r[k] for r in reports if r.get(k) is not None]
         if vals:
             wb[k + "_p50"] = round(statistics.median(vals), 1)
-    return {"notebooks": n, "repeats": repeats, "reference_emulation": emu,
+    pr = None
+    if probe:
+        res = [p.get("result") or {} for p in probes]
+        tim = [r.get("timings_ms") or {} for r in res]
+        pr = {"runs": len(probes), "all_ok": bool(probes) and all(p["exitCode"] == 0 for p in probes),
+              "process_wall_ms_p50": pct([p["wall_ms"] for p in probes], .5),
+              **{f"{k}_ms_p50": pct([t[k] for t in tim if k in t], .5) for k in ("hip_init", "alloc_fill", "probe",
+                                                                                 "total")},
+              "gemm_tflops_p50": pct([(r.get("results") or [{}])[0].get("gemm_tflops", 0) for r in res], .5)}
+    return {"notebooks": n, "repeats": repeats, "reference_emulation": emu, "gpu_probe": pr if probe else "off",
             "create_to_ready_ms": {"p50": pct(total, .5), "p95": pct(total, .95), "max": pct(total, 1)},
             "control_plane_ms_p50": pct(cp, .5), "pod_start_ms_p50": pct(start, .5), "workbench": wb,
             "gpu": (reports[0].get("gpu") if reports else None)}
@@ -115,26 +131,17 @@ def main(argv=None) -> int:
     ap.add_argument("--repeats", type=int, default=5)
     ap.add_argument("--matmul", type=int, default=1024)
     ap.add_argument("--reference-emulation", action="store_true")
-    ap.add_argument("--no-gpu-probe", action="store_true")
+    ap.add_argument("--gpu-probe", default="off,on", help="start-up probe settings to run: off, on, or off,on")
     a = ap.parse_args(argv)
-    probe = None
-    if not a.no_gpu_probe:
-        import torch
-
-        if torch.cuda.device_count():
-            from odh_kubeflow_amd.ops import gpu
-
-            nd = torch.cuda.device_count()
-            for d in range(nd):
-                gpu.get_probe(d).run()
-
-            async def probe(devices):
-                return await gpu.startup_probe(devices, local_index=lambda d: d % nd)
-    out = []
     for n in [int(x) for x in a.notebooks.split(",")]:
-        r = asyncio.run(run_n(n, a.repeats, a.reference_emulation, a.matmul, probe))
-        print(json.dumps(r), flush=True)
-        out.append(r)
+        by = {}
+        for setting in [x.strip() for x in a.gpu_probe.split(",") if x.strip()]:
+            r = asyncio.run(run_n(n, a.repeats, a.reference_emulation, a.matmul, setting == "on"))
+            print(json.dumps(r), flush=True)
+            by[setting] = r
+        if "on" in by and "off" in by:
+            on, off = by["on"]["create_to_ready_ms"]["p50"], by["off"]["create_to_ready_ms"]["p50"]
+            print(json.dumps({"notebooks": n, "gpu_probe_added_ms_p50": round(on - off, 1)}), flush=True)
     return 0
 
 

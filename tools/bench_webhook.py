@@ -22,7 +22,7 @@ import time
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
-from odh_kubeflow_amd.cluster import ClusterConfig, LocalCluster  # noqa: E402
+from odh_kubeflow_amd.testing.cluster import ClusterConfig, LocalCluster  # noqa: E402
 from odh_kubeflow_amd.models import kinds  # noqa: E402
 from odh_kubeflow_amd.models.notebook import notebook  # noqa: E402
 from odh_kubeflow_amd.webhook import notebook_webhook  # noqa: E402

@@ -309,13 +309,15 @@ def manifest_findings() -> List[Finding]:
 
 NATIVE = (
     (["g++", "-std=c++17", "-fsyntax-only", "-Wall", "-Wextra", "-Werror", "-pthread"],
-     "odh_kubeflow_amd/native/apiserver/apiserver.cpp"),
+     "odh_kubeflow_amd/testing/native/apiserver/apiserver.cpp"),
     (["g++", "-std=c++17", "-fsyntax-only", "-Wall", "-Wextra", "-Werror", "-pthread"],
      "odh_kubeflow_amd/ops/csrc/gpu_telemetry.cpp"),
     (["g++", "-std=c++17", "-fsyntax-only", "-Wall", "-Wextra", "-Werror", "-fno-strict-aliasing", "{pyinc}"],
      "odh_kubeflow_amd/native/objcore.cpp"),
     (["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-std=c++17", "-fsyntax-only", "-Wall", "-Wextra", "-Werror",
       "-Wno-unused-command-line-argument"], "odh_kubeflow_amd/ops/csrc/gpu_probe.hip"),
+    (["/opt/rocm/bin/hipcc", "-std=c++17", "-fsyntax-only", "-Wall", "-Wextra", "-Werror",
+      "-Wno-unused-command-line-argument"], "odh_kubeflow_amd/ops/csrc/probe_cli.cpp"),
 )
 
 

@@ -115,7 +115,7 @@ async def run(args, client) -> dict:
 
 async def amain(args) -> dict:
     if args.local:
-        from odh_kubeflow_amd.cluster import ClusterConfig, LocalCluster
+        from odh_kubeflow_amd.testing.cluster import ClusterConfig, LocalCluster
 
         async with LocalCluster(ClusterConfig(gpus_per_node=8, odh=True, webhook=True, transport="native",
                                               env={"SET_PIPELINE_RBAC": "false",

@@ -8,8 +8,8 @@ import time
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
-from odh_kubeflow_amd.apiserver.native import NativeApiServer  # noqa: E402
-from odh_kubeflow_amd.cluster import OPENSHIFT_CRDS  # noqa: E402
+from odh_kubeflow_amd.testing.apiserver.native import NativeApiServer  # noqa: E402
+from odh_kubeflow_amd.testing.cluster import OPENSHIFT_CRDS  # noqa: E402
 from odh_kubeflow_amd.models import kinds  # noqa: E402
 from odh_kubeflow_amd.models.notebook import notebook  # noqa: E402
 from odh_kubeflow_amd.parallel.shard import ControlPlaneShard, ShardConfig  # noqa: E402
@@ -17,12 +17,13 @@ from odh_kubeflow_amd.utils import gctune  # noqa: E402
 
 
 async def main(n_steps: int, sort: str):
-    from odh_kubeflow_amd.parallel.bench_dist import _start_scheduler, _stop_child
+    from odh_kubeflow_amd.parallel.platform import NodePlatform
 
     native = await NativeApiServer(OPENSHIFT_CRDS, gc=True).start()
-    sched = await _start_scheduler(native.url)  # as in the benchmark: kube-scheduler is its own process
-    sh = await ControlPlaneShard(ShardConfig(apiserver_url=native.url, namespace="bench-0", gpu=0, bootstrap=True,
-                                             run_scheduler=False,
+    # as in the benchmark: the node's scheduler + StatefulSet controller and kubelet are processes
+    platform = await NodePlatform(native.url).start()
+    # the control plane in this process, so cProfile sees its reconcile paths
+    sh = await ControlPlaneShard(ShardConfig(apiserver_url=native.url, namespace="bench-0", shard="0", bootstrap=True,
                                              env={"SET_PIPELINE_RBAC": "false",
                                                   "SET_PIPELINE_SECRET": "false"})).start()
 
@@ -48,7 +49,7 @@ async def main(n_steps: int, sort: str):
     print(f"ms/step {el / n_steps * 1e3:.3f}")
     pstats.Stats(pr).sort_stats(sort).print_stats(45)
     await sh.stop()
-    await _stop_child(sched)
+    await platform.stop()
     await native.stop()
 
 

@@ -3,17 +3,19 @@
 #
 #   gpurun --timeout 900 -- bash tools/gpu_pass.sh <tag> [step ...]
 #
-# Steps (default: tests smoke bench prof):
+# Steps (default: tests smoke bench probeexe prof):
 #   tests    pytest -m gpu (one process, per-test timeout)
 #   smoke    __graft_entry__.smoke()
-#   bench    bench.py at N=1 (driver defaults), twice
+#   bench    bench.py at N=1: the driver's invocation (--steps 20 --warmup 5) twice, then 300 steps
 #   ranks    2/4-rank rehearsal of the N>1 launch on the one GPU (never 8: the driver owns N=8)
+#   unsharded  the default topology (one kf + one odh manager process) at 1, 2 and 4 ranks
+#   probeexe the odh-gpu-probe init-container program: 10 process runs (wall time, verdict)
 #   webhook  BASELINE config #4 (tools/bench_webhook.py)
 #   culling  BASELINE config #5 (tools/bench_culling.py)
 #   realpods BASELINE configs #2/#3: 1 and 8 notebooks whose container is a real PyTorch-ROCm process
 #   realref  the same with the reference's serialising odh path (--reference-emulation)
 #   refemu   bench.py --reference-emulation (control-plane lifecycle, reference behaviour)
-#   prof     rocprofv3 --kernel-trace --stats of bench.py
+#   prof     rocprofv3 --kernel-trace --stats of the odh-gpu-probe program
 #   pmc      rocprofv3 --pmc passes (MFMA busy, LDS bank conflicts, HBM bytes) of the probe kernels
 #   probe    start-up probe: eager launches vs hipGraph replay (tools/probe_microbench.py --startup)
 #   env      tools/gpu_env_probe.sh inventory
@@ -22,7 +24,7 @@
 set -o pipefail
 tag=${1:?usage: gpu_pass.sh <tag> [step ...]}
 shift
-steps=${*:-tests smoke bench prof}
+steps=${*:-tests smoke bench probeexe prof}
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 export TMPDIR=/tmp
 out=gpurun_out/$tag
@@ -32,8 +34,8 @@ show() {
   python - "$1" "$2" <<'PY'
 import json, sys
 d = json.loads([l for l in open(sys.argv[1]) if l.startswith('{')][-1])
-keys = ("n_gpus", "value", "ms_per_step", "notebooks_ready_per_s", "p50_ready_ms", "p95_ready_ms",
-        "reconciles_per_notebook", "writes_per_notebook")
+keys = ("n_gpus", "value", "ms_per_step", "rank_ms_per_step", "notebooks_ready_per_s", "p50_ready_ms",
+        "p95_ready_ms", "reconciles_per_notebook", "writes_per_notebook", "gpu_probe_init_container")
 print(sys.argv[2], {k: d.get(k) for k in keys})
 PY
 }
@@ -50,9 +52,31 @@ for s in $steps; do
       tail -1 "$out/smoke.log" ;;
     bench)
       for r in 1 2; do
-        timeout -k 10 170 python bench.py > "$out/bench_n1_r$r.log" 2>&1 || fail bench $? "$out/bench_n1_r$r.log"
-        show "$out/bench_n1_r$r.log" "n1 r$r"
+        timeout -k 10 170 python bench.py --gpus 1 --steps 20 --warmup 5 > "$out/bench_n1_s20_r$r.log" 2>&1 \
+          || fail bench $? "$out/bench_n1_s20_r$r.log"
+        show "$out/bench_n1_s20_r$r.log" "n1 steps20 r$r"
+      done
+      timeout -k 10 200 python bench.py --gpus 1 --no-inprocess-baseline > "$out/bench_n1_s300.log" 2>&1 \
+        || fail bench $? "$out/bench_n1_s300.log"
+      show "$out/bench_n1_s300.log" "n1 steps300" ;;
+    unsharded)
+      timeout -k 10 170 python bench.py --gpus 1 --arch unsharded --steps 100 --warmup 5 --probe-sample 0 \
+        > "$out/bench_unsharded_n1.log" 2>&1 || fail unsharded $? "$out/bench_unsharded_n1.log"
+      show "$out/bench_unsharded_n1.log" "unsharded n1"
+      for n in 2 4; do
+        timeout -k 10 170 python -m torch.distributed.run --nnodes=1 --nproc-per-node $n \
+          --master-addr 127.0.0.1 --master-port 2994$n bench.py --gpus $n --arch unsharded --steps 100 --warmup 5 \
+          --probe-sample 0 > "$out/bench_unsharded_n$n.log" 2>&1 || fail unsharded $? "$out/bench_unsharded_n$n.log"
+        show "$out/bench_unsharded_n$n.log" "unsharded n$n"
       done ;;
+    probeexe)
+      for r in 1 2 3 4 5 6 7 8 9 10; do
+        s0=$(date +%s%N)
+        timeout -k 10 60 odh_kubeflow_amd/ops/_lib/odh-gpu-probe --json - > "$out/probeexe_$r.json" 2>&1 \
+          || fail probeexe $? "$out/probeexe_$r.json"
+        echo "run $r wall_ms $(( ($(date +%s%N) - s0) / 1000000 ))" >> "$out/probeexe_walls.txt"
+      done
+      cat "$out/probeexe_walls.txt"; tail -1 "$out/probeexe_10.json" ;;
     ranks)
       for n in 2 4; do
         timeout -k 10 170 python -m torch.distributed.run --nnodes=1 --nproc-per-node $n \
@@ -79,11 +103,11 @@ for s in $steps; do
         > "$out/bench_refemu.log" 2>&1 || fail refemu $? "$out/bench_refemu.log"
       show "$out/bench_refemu.log" "refemu" ;;
     prof)
-      timeout -k 10 200 rocprofv3 --kernel-trace --stats -d "$out/prof" -o run -- \
-        python3 bench.py --steps 40 --warmup 3 > "$out/bench_prof.log" 2>&1 || fail prof $? "$out/bench_prof.log"
+      timeout -k 10 120 rocprofv3 --kernel-trace --stats -d "$out/prof" -o run -- \
+        odh_kubeflow_amd/ops/_lib/odh-gpu-probe --json - > "$out/probe_prof.log" 2>&1 || fail prof $? "$out/probe_prof.log"
       db=$(find "$out/prof" -name '*results.db' | head -1)
       if [ -n "$db" ]; then
-        python3 tools/rocpd_stats.py "$db" > "$out/bench_kernel_stats.csv" && head -4 "$out/bench_kernel_stats.csv"
+        python3 tools/rocpd_stats.py "$db" > "$out/probe_kernel_stats.csv" && head -6 "$out/probe_kernel_stats.csv"
       fi ;;
     pmc)
       # one counter group per pass, each within the per-block limits

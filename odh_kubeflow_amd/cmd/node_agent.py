@@ -51,9 +51,9 @@ def build(args):
     log.info("amdgpu telemetry: %d KFD GPU node(s) under %s", len(telemetry), args.sysfs_root)
     pr = PodResourcesClient(args.pod_resources_socket) if args.pod_resources_socket else None
     if pr is not None and not pr.available():
-        log.warning("pod-resources socket %s not mounted; using the device-plugin checkpoint and KFD",
-                    args.pod_resources_socket)
-    attributor = Attributor(telemetry, pod_resources=pr if pr is not None and pr.available() else None,
+        log.warning("pod-resources socket %s not there yet; using the device-plugin checkpoint and KFD until it "
+                    "appears (checked on every attribution refresh)", args.pod_resources_socket)
+    attributor = Attributor(telemetry, pod_resources=pr,
                             checkpoint_path=args.device_plugin_checkpoint or None,
                             proc_root=args.proc_root or None, resource=args.resource_name,
                             ttl_s=args.attribution_ttl_s)

@@ -12,6 +12,10 @@ Three independent sources, merged (a pod is attributed the union of what they re
    having been allocated them (e.g. a privileged pod), and it is the only source of
    **per-pod VRAM** when several pods share a device.
 
+Every refresh re-checks each source (a pod-resources socket that appears after the agent
+started is used from then on, one that disappears is reported), and concurrent lookups
+share one in-flight refresh.  Per-source health is exported on the agent's ``/metrics``.
+
 Device IDs from 1 and 2 are what the AMD device plugin advertises: the PCI address of a
 whole GPU (``0000:c1:00.0``), matched against the KFD topology's ``domain``/``location_id``;
 all KFD nodes of that GPU (CPX/DPX partitions) are returned.  ``renderD<minor>``,
@@ -23,6 +27,7 @@ Replaces the reference's Jupyter-only activity lookup
 
 from __future__ import annotations
 
+import asyncio
 import logging
 import re
 import time
@@ -102,6 +107,7 @@ class Attributor:
         self.ttl_s = ttl_s
         self.resolver = DeviceResolver(telemetry.devices())
         self._snap: Optional[Snapshot] = None
+        self._inflight: Optional[asyncio.Future] = None
         self.refreshes = 0
 
     def _resolve_all(self, ids, snap: Snapshot) -> Set[int]:
@@ -115,7 +121,10 @@ class Attributor:
 
     async def refresh(self) -> Snapshot:
         snap = Snapshot(time.monotonic())
-        if self.pod_resources is not None:
+        if self.pod_resources is not None and not self.pod_resources.available():
+            # the kubelet socket is not mounted (yet): probed again on the next refresh
+            snap.sources["podresources"] = "unavailable"
+        elif self.pod_resources is not None:
             try:
                 for p in await self.pod_resources.list():
                     ids = p.device_ids(self.resource)
@@ -148,9 +157,26 @@ class Attributor:
         return snap
 
     async def snapshot(self) -> Snapshot:
-        if self._snap is None or time.monotonic() - self._snap.taken_at >= self.ttl_s:
-            return await self.refresh()
-        return self._snap
+        """The attribution tables, refreshed when older than ``ttl_s``.  Lookups that find the
+        tables stale while a refresh is already running wait for that one (one pod-resources
+        List, one checkpoint read and one KFD scan however many culler queries arrive)."""
+        if self._snap is not None and time.monotonic() - self._snap.taken_at < self.ttl_s:
+            return self._snap
+        if self._inflight is None:
+            self._inflight = asyncio.ensure_future(self.refresh())
+            self._inflight.add_done_callback(self._clear_inflight)
+        return await asyncio.shield(self._inflight)
+
+    def _clear_inflight(self, fut: asyncio.Future) -> None:
+        if self._inflight is fut:
+            self._inflight = None
+        if not fut.cancelled():
+            fut.exception()  # retrieved: a failed refresh is re-raised to its awaiters only
+
+    def source_health(self) -> Dict[str, int]:
+        """source → 1 when the last refresh read it, 0 when it was unavailable or failed."""
+        snap = self._snap
+        return {k: int(v == "ok") for k, v in (snap.sources.items() if snap else [])}
 
     async def lookup(self, uid: Optional[str] = None, namespace: Optional[str] = None,
                      name: Optional[str] = None) -> Optional[PodGpus]:

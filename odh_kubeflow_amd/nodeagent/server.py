@@ -104,6 +104,16 @@ class NodeTelemetryAgent:
                  "# HELP odh_node_agent_unauthorized_total Requests refused for a missing or wrong token.",
                  "# TYPE odh_node_agent_unauthorized_total counter",
                  f"odh_node_agent_unauthorized_total {self.refused}"]
+        if self.attributor is not None:
+            # a node silently falling back from the pod-resources API to the checkpoint shows here
+            lines += ["# HELP odh_node_agent_attribution_source_up Pod->GPU attribution source readable at the "
+                      "last refresh (1) or unavailable / failing (0).",
+                      "# TYPE odh_node_agent_attribution_source_up gauge"]
+            lines += [f'odh_node_agent_attribution_source_up{{source="{k}"}} {v}'
+                      for k, v in sorted(self.attributor.source_health().items())]
+            lines += ["# HELP odh_node_agent_attribution_refreshes_total Attribution table refreshes.",
+                      "# TYPE odh_node_agent_attribution_refreshes_total counter",
+                      f"odh_node_agent_attribution_refreshes_total {self.attributor.refreshes}"]
         return "\n".join(lines) + "\n"
 
     async def start(self) -> "NodeTelemetryAgent":

@@ -213,10 +213,15 @@ bool launch(Dev& d, const Options& o) {
   return true;
 }
 
-bool finish(Dev& d) {
+bool drain(Dev& d) {
   HIP_TRY(hipSetDevice(d.index));
   HIP_TRY(hipStreamSynchronize(d.sh));
   HIP_TRY(hipStreamSynchronize(d.sg));
+  return true;
+}
+
+bool finish(Dev& d) {
+  if (!drain(d)) return false;
   HIP_TRY(hipEventElapsedTime(&d.gemm_ms, d.e0, d.e_gemm));
   HIP_TRY(hipEventElapsedTime(&d.hbm_ms, d.e_h0, d.e_h1));
   return true;
@@ -303,7 +308,7 @@ extern "C" int odh_probe_cli(int argc, char** argv) {
   for (Dev& d : devs)
     if (!setup(d, o)) return fail_all(d);
   for (Dev& d : devs)
-    if (!finish(d)) return fail_all(d);  // operands filled on every device
+    if (!drain(d)) return fail_all(d);  // operands filled on every device
   const double t_alloc = ms_since(t_start);
   const auto t_probe0 = Clock::now();
   for (Dev& d : devs)

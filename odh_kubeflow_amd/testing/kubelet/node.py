@@ -332,7 +332,7 @@ class FakeContainerRuntime(ContainerRuntime):
 class FakeDeviceManager:
     """kubelet device-manager stand-in: publishes allocations through the device-plugin
     checkpoint (:class:`~odh_kubeflow_amd.nodeagent.checkpoint.CheckpointWriter`) and/or a
-    pod-resources gRPC server (:class:`~odh_kubeflow_amd.nodeagent.podresources.FakePodResourcesServer`).
+    pod-resources gRPC server (:class:`~odh_kubeflow_amd.testing.kubelet.podresources_server.FakePodResourcesServer`).
 
     ``device_id_of(index)`` gives the device-plugin ID of node GPU ``index`` (the PCI
     address; :func:`~odh_kubeflow_amd.ops.telemetry.fake_bdf` for synthetic sysfs trees).

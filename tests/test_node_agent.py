@@ -19,6 +19,7 @@ import urllib.request
 import pytest
 
 from odh_kubeflow_amd.nodeagent import podresources as pr
+from odh_kubeflow_amd.testing.kubelet.podresources_server import FakePodResourcesServer
 from odh_kubeflow_amd.nodeagent.attribution import Attributor, DeviceResolver
 from odh_kubeflow_amd.nodeagent.checkpoint import CheckpointWriter, read_checkpoint
 from odh_kubeflow_amd.nodeagent.server import NodeTelemetryAgent
@@ -55,7 +56,7 @@ def test_podresources_codec_roundtrip():
 
 def test_podresources_grpc_list(tmp_path):
     sock = str(tmp_path / "kubelet.sock")
-    srv = pr.FakePodResourcesServer(sock).start()
+    srv = FakePodResourcesServer(sock).start()
     try:
         srv.assign("user", "nb-0", "nb", "amd.com/gpu", [fake_bdf(3)])
         cli = pr.PodResourcesClient(sock)
@@ -102,7 +103,7 @@ def test_device_resolver_bdf_partitions(tmp_path):
 def test_attribution_sources(run, sysfs, tmp_path):
     root, proc, _minors, tel = sysfs
     sock = str(tmp_path / "pr.sock")
-    srv = pr.FakePodResourcesServer(sock).start()
+    srv = FakePodResourcesServer(sock).start()
     cp = CheckpointWriter(str(tmp_path / "dp" / "kubelet_internal_checkpoint"))
     try:
         srv.assign("user", "a-0", "a", "amd.com/gpu", [fake_bdf(0)])
@@ -124,13 +125,67 @@ def test_attribution_sources(run, sysfs, tmp_path):
             assert tables["sources"] == {"podresources": "ok", "checkpoint": "ok", "kfd": "ok"}
             assert tables["unresolved_device_ids"] == ["0000:99:00.0"]
             # a source that fails is reported, the others still answer
-            att2 = Attributor(tel, pod_resources=pr.PodResourcesClient(str(tmp_path / "nope.sock"), timeout_s=0.2),
+            bogus = tmp_path / "not-a-grpc.sock"
+            bogus.write_text("")
+            att2 = Attributor(tel, pod_resources=pr.PodResourcesClient(str(bogus), timeout_s=0.2),
                               checkpoint_path=cp.path, ttl_s=0.0)
             assert (await att2.lookup(UID_B)).devices == [6]
             assert (await att2.all_pods())["sources"]["podresources"].startswith("error")
+            assert att2.source_health() == {"podresources": 0, "checkpoint": 1}
         run(go())
     finally:
         srv.stop()
+
+
+def test_pod_resources_socket_that_appears_later_is_used(run, sysfs, tmp_path):
+    """The kubelet socket is re-checked on every refresh: an agent started before the kubelet
+    mounted it switches to the pod-resources API as soon as it appears (and reports it gone
+    when it disappears), instead of losing that source for its whole lifetime."""
+    _root, _proc, _minors, tel = sysfs
+    sock = str(tmp_path / "late.sock")
+
+    async def go():
+        att = Attributor(tel, pod_resources=pr.PodResourcesClient(sock, timeout_s=0.5), ttl_s=0.0)
+        assert await att.lookup(None, "user", "a-0") is None
+        assert (await att.all_pods())["sources"] == {"podresources": "unavailable"}
+        assert att.source_health() == {"podresources": 0}
+        srv = FakePodResourcesServer(sock).start()
+        try:
+            srv.assign("user", "a-0", "a", "amd.com/gpu", [fake_bdf(2)])
+            a = await att.lookup(None, "user", "a-0")
+            assert a is not None and a.devices == [2] and a.sources == ["podresources"]
+            assert att.source_health() == {"podresources": 1}
+        finally:
+            srv.stop()
+        if os.path.exists(sock):
+            os.unlink(sock)
+        assert await att.lookup(None, "user", "a-0") is None
+        assert att.source_health() == {"podresources": 0}
+    run(go())
+
+
+def test_concurrent_lookups_share_one_refresh(run, sysfs, tmp_path):
+    """A burst of culler queries finding the tables stale triggers ONE refresh (one List on
+    the kubelet socket, one checkpoint read, one KFD scan), not one per query."""
+    _root, _proc, _minors, tel = sysfs
+    cp = CheckpointWriter(str(tmp_path / "dp" / "kubelet_internal_checkpoint"))
+    cp.allocate(UID_B, "b", [fake_bdf(1)])
+
+    async def go():
+        att = Attributor(tel, checkpoint_path=cp.path, ttl_s=30.0)
+        calls = {"n": 0}
+        inner = att.refresh
+
+        async def slow_refresh():
+            calls["n"] += 1
+            await asyncio.sleep(0.05)
+            return await inner()
+        att.refresh = slow_refresh
+        res = await asyncio.gather(*(att.lookup(UID_B) for _ in range(16)))
+        assert calls["n"] == 1 and all(r.devices == [1] for r in res)
+        await att.lookup(UID_B)  # fresh: served from the table
+        assert calls["n"] == 1
+    run(go())
 
 
 def _get(url):

@@ -257,9 +257,7 @@ def odh_deployment() -> dict:
                      "selector": {"matchLabels": {"app": "odh-notebook-controller"}},
                      "template": {"metadata": {"labels": {"app": "odh-notebook-controller"}},
                                   "spec": {"serviceAccountName": "manager", "containers": [c],
-                                           "volumes": [{"name": "cert", "secret": {
-                                               "secretName": WEBHOOK_CERT_SECRET,
-                                               "defaultMode": 420}}]}}}}
+                                           "volumes": [_cert_volume()]}}}}
 
 
 def node_agent_daemonset() -> dict:
@@ -381,6 +379,34 @@ def mwc() -> dict:
 # ------------------------------------------------------------------ webhook serving cert (non-OpenShift)
 
 
+def _cert_volume() -> dict:
+    """The serving Secret as the webhook server's cert dir: ``tls.crt`` / ``tls.key`` only — the
+    Secret also holds the provisioner's long-lived CA key (``webhook/certs.py``), which no
+    serving pod needs."""
+    return {"name": "cert", "secret": {"secretName": WEBHOOK_CERT_SECRET, "defaultMode": 420,
+                                       "items": [{"key": "tls.crt", "path": "tls.crt"},
+                                                 {"key": "tls.key", "path": "tls.key"}]}}
+
+
+def webhook_certs_rbac(mwcs: List[str]) -> List[dict]:
+    """Least privilege for the provisioner: get/update of exactly the Secrets it keeps and the
+    MutatingWebhookConfigurations it names (``resourceNames``), create of Secrets (create cannot
+    be scoped by name) — nothing else in the cluster's admission chain."""
+    return [
+        {"apiVersion": "v1", "kind": "ServiceAccount", "metadata": {"name": "webhook-certs"}},
+        {"apiVersion": "rbac.authorization.k8s.io/v1", "kind": "Role", "metadata": {"name": "webhook-certs-role"},
+         "rules": [{**_rule([""], ["secrets"], ["get", "update"]),
+                    "resourceNames": [WEBHOOK_CERT_SECRET, AGENT_TOKEN_SECRET]},
+                   _rule([""], ["secrets"], ["create"])]},
+        {"apiVersion": "rbac.authorization.k8s.io/v1", "kind": "ClusterRole",
+         "metadata": {"name": "webhook-certs-cabundle-role"},
+         "rules": [{**_rule(["admissionregistration.k8s.io"], ["mutatingwebhookconfigurations"], ["get", "update"]),
+                    "resourceNames": list(mwcs)}]},
+        binding("RoleBinding", "webhook-certs-rolebinding", "webhook-certs-role", "webhook-certs"),
+        binding("ClusterRoleBinding", "webhook-certs-cabundle-rolebinding", "webhook-certs-cabundle-role",
+                "webhook-certs")]
+
+
 def webhook_certs_args(services: List[str], mwcs: List[str]) -> List[str]:
     """``cmd/webhook_certs.py`` arguments.  Names are the *rendered* (prefixed) names: they
     are plain strings to kustomize, so its name-reference fix-ups do not reach them."""
@@ -403,17 +429,7 @@ def webhook_certs_docs(services: List[str], mwcs: List[str]) -> Dict[str, object
     job_spec = {"backoffLimit": 6, "ttlSecondsAfterFinished": 3600, "template": {
         "metadata": {"labels": {"app": "odh-webhook-certs"}}, "spec": pod}}
     return {
-        "rbac.yaml": [
-            {"apiVersion": "v1", "kind": "ServiceAccount", "metadata": {"name": "webhook-certs"}},
-            {"apiVersion": "rbac.authorization.k8s.io/v1", "kind": "Role", "metadata": {"name": "webhook-certs-role"},
-             "rules": [_rule([""], ["secrets"], ["get", "create", "update"])]},
-            {"apiVersion": "rbac.authorization.k8s.io/v1", "kind": "ClusterRole",
-             "metadata": {"name": "webhook-certs-cabundle-role"},
-             "rules": [_rule(["admissionregistration.k8s.io"], ["mutatingwebhookconfigurations"],
-                             ["get", "list", "update", "patch"])]},
-            binding("RoleBinding", "webhook-certs-rolebinding", "webhook-certs-role", "webhook-certs"),
-            binding("ClusterRoleBinding", "webhook-certs-cabundle-rolebinding", "webhook-certs-cabundle-role",
-                    "webhook-certs")],
+        "rbac.yaml": webhook_certs_rbac(mwcs),
         "job.yaml": [
             {"apiVersion": "batch/v1", "kind": "Job", "metadata": {"name": "webhook-certs"}, "spec": job_spec},
             # renewal: re-run weekly; the provisioner reissues within 90 days of expiry (or when a
@@ -459,9 +475,7 @@ def control_plane_statefulset(shards: int) -> dict:
                      "selector": {"matchLabels": labels},
                      "template": {"metadata": {"labels": labels},
                                   "spec": {"serviceAccountName": "control-plane", "containers": [c],
-                                           "volumes": [{"name": "cert", "secret": {
-                                               "secretName": WEBHOOK_CERT_SECRET, "defaultMode": 420}},
-                                                       _agent_token_volume()]}}}}
+                                           "volumes": [_cert_volume(), _agent_token_volume()]}}}}
 
 
 def _webhook_svc(name: str, selector: dict) -> dict:
@@ -521,13 +535,18 @@ def sample(name: str, gpus: int, version: str = "v1", auth: bool = False) -> dic
 
 
 def _certs_args_patches(services: List[str], mwcs: List[str]) -> List[dict]:
-    """JSON6902 patches setting the provisioner's arguments in the Job and the CronJob."""
+    """JSON6902 patches setting the provisioner's arguments in the Job and the CronJob, and the
+    MutatingWebhookConfiguration names its ClusterRole may touch."""
     args = webhook_certs_args(services, mwcs)
-    return [{"target": {"kind": kind, "name": name},
-             "patch": yaml.safe_dump([{"op": "replace", "path": path, "value": args}], sort_keys=False)}
-            for kind, name, path in (("Job", "webhook-certs", "/spec/template/spec/containers/0/args"),
-                                     ("CronJob", "webhook-certs-renew",
-                                      "/spec/jobTemplate/spec/template/spec/containers/0/args"))]
+    patches = [{"target": {"kind": kind, "name": name},
+                "patch": yaml.safe_dump([{"op": "replace", "path": path, "value": args}], sort_keys=False)}
+               for kind, name, path in (("Job", "webhook-certs", "/spec/template/spec/containers/0/args"),
+                                        ("CronJob", "webhook-certs-renew",
+                                         "/spec/jobTemplate/spec/template/spec/containers/0/args"))]
+    patches.append({"target": {"kind": "ClusterRole", "name": "webhook-certs-cabundle-role"},
+                    "patch": yaml.safe_dump([{"op": "replace", "path": "/rules/0/resourceNames",
+                                              "value": list(mwcs)}], sort_keys=False)})
+    return patches
 
 
 def kustomization(resources: List[str], **extra) -> dict:

@@ -313,3 +313,30 @@ def test_conformance_bundle_runs_the_e2e_suite_in_cluster():
     assert any(r["resources"] == ["notebooks"] and r["verbs"] == ["*"] for r in rules)
     assert any("deployments" in r["resources"] and "patch" in r["verbs"] for r in rules)
     assert any(r["resources"] == ["configmaps"] and "update" in r["verbs"] for r in rules)
+
+
+@pytest.mark.parametrize("overlay", ["standalone", "kubeflow", "mi355x", "mi355x-sharded"])
+def test_webhook_certs_rbac_is_scoped_to_its_objects(overlay):
+    """The cert provisioner may get/update exactly the MutatingWebhookConfigurations it keeps
+    the caBundle of (by name) and exactly its Secrets — a compromised Job pod cannot rewrite
+    any other admission webhook of the cluster.  No list, patch or delete anywhere."""
+    objs = _render(overlay)
+    mwc_names = sorted(_by(objs, "MutatingWebhookConfiguration"))
+    job = next(o for o in objs if o["kind"] == "Job" and o["metadata"]["name"].endswith("webhook-certs"))
+    args = job["spec"]["template"]["spec"]["containers"][0]["args"]
+    assert sorted(a.split("=", 1)[1] for a in args if a.startswith("--mwc-name=")) == mwc_names
+    (cr,) = [o for n, o in _by(objs, "ClusterRole").items() if n.endswith("webhook-certs-cabundle-role")]
+    (rule,) = cr["rules"]
+    assert rule["resources"] == ["mutatingwebhookconfigurations"] and sorted(rule["verbs"]) == ["get", "update"]
+    assert sorted(rule["resourceNames"]) == mwc_names
+    (role,) = [o for n, o in _by(objs, "Role").items() if n.endswith("webhook-certs-role")]
+    named = [r for r in role["rules"] if r.get("resourceNames")]
+    assert len(named) == 1 and sorted(named[0]["verbs"]) == ["get", "update"]
+    assert sorted(named[0]["resourceNames"]) == sorted([manifests.WEBHOOK_CERT_SECRET, manifests.AGENT_TOKEN_SECRET])
+    unnamed = [r for r in role["rules"] if not r.get("resourceNames")]
+    assert [sorted(r["verbs"]) for r in unnamed] == [["create"]]
+    # the serving pods get the serving pair only, never the CA key
+    for o, ps in _pod_specs(objs):
+        for v in ps.get("volumes") or []:
+            if (v.get("secret") or {}).get("secretName") == manifests.WEBHOOK_CERT_SECRET:
+                assert sorted(i["key"] for i in v["secret"]["items"]) == ["tls.crt", "tls.key"], o["metadata"]

@@ -1,10 +1,12 @@
 # Developer targets (the reference's kf/Makefile and odh/Makefile counterparts).
 PYTHON ?= python3
 IMG ?= quay.io/opendatahub/odh-kubeflow-amd:$(shell cat releasing/VERSION)
+PROBE_IMG ?= quay.io/opendatahub/odh-kubeflow-amd-gpu-probe:$(shell cat releasing/VERSION)
+CONFORMANCE_IMG ?= quay.io/opendatahub/odh-kubeflow-amd-conformance:$(shell cat releasing/VERSION)
 NOTEBOOK_IMG ?= quay.io/opendatahub/workbench-rocm-pytorch:latest
 GPU_ARCH ?= gfx950
 
-.PHONY: build test test-matrix test-native test-gpu e2e e2e-test conformance-run conformance-report conformance-clean coverage bench bench-8 manifests deploy deploy-sharded undeploy lint license-check docker-build docker-push docker-build-notebook
+.PHONY: build test test-matrix test-native test-gpu e2e e2e-test conformance-run conformance-report conformance-clean coverage bench bench-8 manifests deploy deploy-sharded undeploy lint license-check docker-build docker-build-probe docker-build-conformance docker-push docker-build-notebook
 
 build:  ## hipcc --offload-arch=$(GPU_ARCH) kernels, host C++ telemetry/objcore, native apiserver (in-tree)
 	ODH_GPU_ARCH=$(GPU_ARCH) $(PYTHON) -m odh_kubeflow_amd.ops.build
@@ -75,11 +77,18 @@ lint:  ## static analysis: Python AST rules, secrets, rendered manifests, -Wall 
 license-check:  ## runtime dependencies carry permissive licences (kf/third_party/check-license.sh)
 	$(PYTHON) tools/licenses.py
 
-docker-build: build  ## controller / node-agent image (ROCm base; kernels built for $(GPU_ARCH))
-	docker build -f images/Dockerfile --build-arg GPU_ARCH=$(GPU_ARCH) -t $(IMG) .
+docker-build:  ## controller / webhook / node-agent image (slim Python, host C++ only; no ROCm, no torch)
+	docker build -f images/Dockerfile -t $(IMG) .
 
-docker-push:  ## push the controller / node-agent image
+docker-build-probe:  ## MI355X start-up probe init-container image (ROCm runtime; kernels for $(GPU_ARCH))
+	docker build -f images/probe.Dockerfile --build-arg GPU_ARCH=$(GPU_ARCH) -t $(PROBE_IMG) .
+
+docker-build-conformance: docker-build  ## controller image + pytest + e2e/ (config/conformance)
+	docker build -f images/conformance.Dockerfile --build-arg MANAGER_IMAGE=$(IMG) -t $(CONFORMANCE_IMG) .
+
+docker-push:  ## push the controller / node-agent and probe images
 	docker push $(IMG)
+	docker push $(PROBE_IMG)
 
 docker-build-notebook:  ## PyTorch-ROCm Jupyter workbench image the samples reference
 	docker build -f images/notebook.Dockerfile -t $(NOTEBOOK_IMG) images

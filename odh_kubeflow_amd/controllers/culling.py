@@ -356,8 +356,19 @@ class NodeAgentActivity(GpuActivity):
         self.requests = 0
 
     def default_endpoint(self, pod: dict) -> Optional[str]:
+        """``<hostIP>:<port>`` of the pod's node agent; IPv6 literals are bracketed
+        (``[fd00::5]:9464``), as an URL authority needs them on v6 / dual-stack-v6 clusters."""
         host = (pod.get("status") or {}).get("hostIP")
-        return f"{host}:{self.port}" if host else None
+        if not host:
+            return None
+        import ipaddress
+
+        try:
+            if ipaddress.ip_address(host).version == 6:
+                host = f"[{host}]"
+        except ValueError:
+            pass  # a hostname: used as is
+        return f"{host}:{self.port}"
 
     async def busy(self, pod, window_s):
         import urllib.parse

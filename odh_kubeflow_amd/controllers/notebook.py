@@ -23,7 +23,11 @@ pods that request GPUs also get the AMD node-labeller selector and the
 ``GPU_SHM_SIZE_PER_GPU`` (e.g. ``16Gi``) a GPU notebook without its own ``/dev/shm``
 gets a memory-backed one of that size per GPU: PyTorch DataLoader workers and RCCL's
 intra-node transport live there, and the container default (64 MiB) breaks both.  The
-``amd.com/shm-size`` annotation overrides the size (``0`` turns it off).
+``amd.com/shm-size`` annotation overrides the size (``0`` turns it off).  With
+``amd.com/gpu-probe: "true"`` on the Notebook (or ``GPU_STARTUP_PROBE=true`` for every GPU
+notebook) the pod gets the ``amd-gpu-probe`` init container: the MI355X start-up probe
+(``odh-gpu-probe``, ``GPU_PROBE_IMAGE``) on the GPUs the device plugin gives it, before the
+notebook container starts.
 
 Event re-emission (:97-126) runs as its own small controller
 (:class:`NotebookEventReemitter`) instead of sharing the Notebook work queue — the
@@ -138,7 +142,7 @@ def _multi_gpu_env(pod_spec: dict, raw: str) -> None:
 
 GPU_PROBE_ANNOTATION = "amd.com/gpu-probe"
 GPU_PROBE_CONTAINER = "amd-gpu-probe"
-DEFAULT_GPU_PROBE_IMAGE = "quay.io/opendatahub/odh-mi355x-gpu-probe:v0.3.0"
+DEFAULT_GPU_PROBE_IMAGE = "quay.io/opendatahub/odh-kubeflow-amd-gpu-probe:main"  # manifests pin the release
 GPU_PROBE_TIMEOUT_MS = "30000"
 
 

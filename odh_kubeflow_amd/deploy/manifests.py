@@ -60,7 +60,14 @@ CULLER_LITERALS = ["ENABLE_CULLING=false", "CULL_IDLE_TIME=1440", "IDLENESS_CHEC
 CULLER_KEYS = [lit.split("=", 1)[0] for lit in CULLER_LITERALS]
 PARAMS_ENV = "USE_ISTIO=false\nISTIO_GATEWAY=kubeflow/kubeflow-gateway\nISTIO_HOST=*\n" \
              "CLUSTER_DOMAIN=cluster.local\nADD_FSGROUP=true\nGPU_NODE_SELECTOR=false\n" \
-             "GPU_SHM_SIZE_PER_GPU=\nMULTI_GPU_ENV=\n"
+             "GPU_SHM_SIZE_PER_GPU=\nMULTI_GPU_ENV=\n" \
+             "GPU_STARTUP_PROBE=false\n"  # opt-in per notebook (amd.com/gpu-probe) or for every GPU notebook
+
+
+def params_env(version: str) -> str:
+    """The kf controller's ``config`` ConfigMap: the reference's settings (params.env) plus the
+    MI355X ones; the start-up probe image is pinned to the release (images/probe.Dockerfile)."""
+    return PARAMS_ENV + f"GPU_PROBE_IMAGE={PROBE_IMAGE_NAME}:{version}\n"
 # MI355X node settings (overlays mi355x and mi355x-sharded)
 MI355X_PARAMS = ["GPU_NODE_SELECTOR=true", "GPU_SHM_SIZE_PER_GPU=16Gi",
                  # multi-GPU notebooks: RCCL's intra-node IPC over dmabuf (hosts whose amdgpu
@@ -72,6 +79,8 @@ MI355X_CULLER = ["CULLING_ACTIVITY_SOURCE=combined", "ENABLE_CULLING=true"]
 # releasing/update-manifests-images + releasing/version/VERSION)
 MANAGER_IMAGE_NAME = "quay.io/opendatahub/odh-kubeflow-amd"
 MANAGER_IMAGE = MANAGER_IMAGE_NAME + ":main"
+PROBE_IMAGE_NAME = MANAGER_IMAGE_NAME + "-gpu-probe"  # images/probe.Dockerfile
+CONFORMANCE_IMAGE_NAME = MANAGER_IMAGE_NAME + "-conformance"  # images/conformance.Dockerfile
 REPO_ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
@@ -346,7 +355,7 @@ def conformance_docs(version: str) -> Dict[str, object]:
            "metadata": {"name": "notebook-conformance", "namespace": CONFORMANCE_NS,
                         "labels": {"app": "odh-kubeflow-amd-conformance"}},
            "spec": {"serviceAccountName": sa, "restartPolicy": "Never",
-                    "containers": [{"name": "e2e", "image": f"{MANAGER_IMAGE_NAME}:{version}",
+                    "containers": [{"name": "e2e", "image": f"{CONFORMANCE_IMAGE_NAME}:{version}",
                                     "workingDir": "/opt/odh-kubeflow-amd",
                                     "command": ["/bin/sh", "-c", run],
                                     "env": [{"name": "HOME", "value": "/tmp"}],
@@ -590,7 +599,7 @@ def tree(version: Optional[str] = None) -> Dict[str, object]:
     t["manager/kustomization.yaml"] = kustomization(["kf_manager.yaml", "odh_manager.yaml", "services.yaml"],
                                                     configMapGenerator=generators,
                                                     generatorOptions={"disableNameSuffixHash": True})
-    t["manager/params.env"] = PARAMS_ENV
+    t["manager/params.env"] = params_env(version)
     t["node-agent/daemonset.yaml"] = node_agent_daemonset()
     t["node-agent/serviceaccount.yaml"] = {"apiVersion": "v1", "kind": "ServiceAccount",
                                            "metadata": {"name": "mi355x-node-agent"}}
@@ -606,7 +615,7 @@ def tree(version: Optional[str] = None) -> Dict[str, object]:
     cp = control_plane_docs(SHARDS)
     for f, doc in cp.items():
         t[f"control-plane/{f}"] = doc
-    t["control-plane/params.env"] = PARAMS_ENV
+    t["control-plane/params.env"] = params_env(version)
     t["control-plane/kustomization.yaml"] = kustomization(
         ["rbac.yaml", "statefulset.yaml", "services.yaml", "webhooks.yaml"],
         configMapGenerator=generators, generatorOptions={"disableNameSuffixHash": True})

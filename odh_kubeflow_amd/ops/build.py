@@ -9,7 +9,8 @@
 
 Both land in ``odh_kubeflow_amd/ops/_lib/`` so they travel with the repo snapshot to
 the GPU box (no JIT cache under ``~/.cache``).  A library is rebuilt only when its
-source is newer than the ``.so``.
+source is newer than the ``.so``.  ``--host-only`` builds the host C++ libraries (the slim
+controller / node-agent image), ``--probe-only`` the probe (its ROCm image).
 """
 
 from __future__ import annotations
@@ -84,10 +85,18 @@ def _stale(out: str, srcs: List[str]) -> bool:
     return any(os.path.getmtime(s) > t for s in srcs)
 
 
-def build(force: bool = False, verbose: bool = True) -> Dict[str, str]:
+# what each image needs: the slim controller / node-agent image has no ROCm toolchain and no
+# HIP runtime (host C++ only); the probe image has the HIP runtime and the probe only
+HOST_TARGETS = (OBJCORE, "libodh_gpu_telemetry.so")
+PROBE_TARGETS = ("libodh_gpu_probe.so", PROBE_EXE)
+
+
+def build(force: bool = False, verbose: bool = True, only=None) -> Dict[str, str]:
     os.makedirs(LIBDIR, exist_ok=True)
     built = {}
     for name, spec in targets().items():
+        if only is not None and name not in only:
+            continue
         out = spec.get("out") or lib_path(name)
         os.makedirs(os.path.dirname(out), exist_ok=True)
         if force or _stale(out, spec["src"] + spec.get("deps", [])):
@@ -102,4 +111,9 @@ def build(force: bool = False, verbose: bool = True) -> Dict[str, str]:
 
 
 if __name__ == "__main__":
-    build(force="--force" in sys.argv)
+    sel = None
+    if "--host-only" in sys.argv:
+        sel = HOST_TARGETS
+    elif "--probe-only" in sys.argv:
+        sel = PROBE_TARGETS
+    build(force="--force" in sys.argv, only=sel)

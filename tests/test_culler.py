@@ -250,3 +250,15 @@ def test_gpu_says_active_vram_policy():
     assert c.gpu_says_active(held, cfg)
     assert not c.gpu_says_active({**held, "pod_vram_bytes": 10 ** 6}, cfg)
     assert not c.gpu_says_active({**held, "pod_vram_bytes": None}, cfg)
+
+
+def test_node_agent_endpoint_brackets_ipv6_host_ips():
+    """IPv6 / dual-stack-v6 nodes: the node agent URL authority needs ``[addr]:port``; an
+    unbracketed literal would make every query fail and culling silently fall back."""
+    from odh_kubeflow_amd.controllers.culling import NodeAgentActivity
+
+    a = NodeAgentActivity(port=9464)
+    assert a.default_endpoint({"status": {"hostIP": "10.0.0.7"}}) == "10.0.0.7:9464"
+    assert a.default_endpoint({"status": {"hostIP": "fd00:10:244::5"}}) == "[fd00:10:244::5]:9464"
+    assert a.default_endpoint({"status": {"hostIP": "node-3.example"}}) == "node-3.example:9464"
+    assert a.default_endpoint({"status": {}}) is None

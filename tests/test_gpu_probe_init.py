@@ -242,7 +242,9 @@ def test_probe_program_fails_on_injected_fault(fault):
     assert res["ok"] is False and "mismatches" in res["error"]
     d = res["results"][0]
     if fault == "gemm":
-        assert d["gemm_errors"] >= 4096 and d["hbm_errors"] == 0 and sum(d["err_xcd"]) == d["gemm_errors"]
+        # A[0][0] corrupted: C[0][j] is wrong wherever Bt[j][0] = ((11 j) mod 7) - 3 is non-zero
+        want = sum(1 for j in range(4096) if (11 * j) % 7 != 3)
+        assert d["gemm_errors"] == want and d["hbm_errors"] == 0 and sum(d["err_xcd"]) == want, d
     else:
         assert d["hbm_errors"] > 0 and d["gemm_errors"] == 0
 

@@ -304,7 +304,7 @@ def test_conformance_bundle_runs_the_e2e_suite_in_cluster():
     ns = setup[0]["metadata"]["name"]
     assert pod["metadata"]["namespace"] == ns and pod["spec"]["serviceAccountName"] == setup[1]["metadata"]["name"]
     c = pod["spec"]["containers"][0]
-    assert c["image"] == f"{manifests.MANAGER_IMAGE_NAME}:{manifests.release_version()}"
+    assert c["image"] == f"{manifests.CONFORMANCE_IMAGE_NAME}:{manifests.release_version()}"
     cmd = c["command"][-1]
     assert "pytest e2e" in cmd and "--in-cluster" in cmd and f"--nb-namespace {ns}" in cmd and "done" in cmd
     assert c["securityContext"]["runAsNonRoot"] and c["securityContext"]["allowPrivilegeEscalation"] is False

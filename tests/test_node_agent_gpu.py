@@ -59,30 +59,46 @@ def _torch_bdf(dev: int = 0):
     return f"{p.pci_domain_id:04x}:{p.pci_bus_id:02x}:{p.pci_device_id:02x}.0"
 
 
+def _kfd_listing() -> str:
+    root = "/sys/class/kfd/kfd/proc"
+    try:
+        return ", ".join(f"{p}:{sorted(os.listdir(os.path.join(root, p)))}" for p in sorted(os.listdir(root))[:8])
+    except OSError as e:
+        return repr(e)
+
+
 @pytest.fixture(scope="module")
 def gpu_state():
+    """This process's KFD entry, found the way a node agent must find it: KFD names processes by
+    their host PID (``/sys/class/kfd/kfd/proc/<pid>``), which differs from ``os.getpid()`` inside
+    a container — so the entry is the one whose VRAM grows by the 1 GiB this fixture allocates."""
     if not torch.cuda.is_available():
         pytest.fail("GPU tests need a visible MI355X")
     from odh_kubeflow_amd.ops.telemetry import Telemetry
 
+    torch.zeros(1, device="cuda:0")
+    torch.cuda.synchronize()
+    tel = Telemetry("/sys")
+    before = {(p.pid, p.gpu_id): p.vram_bytes for p in tel.kfd_processes("/proc")}
     hold = torch.empty((1 << 30) // 4 + (64 << 20), dtype=torch.float32, device="cuda:0")  # > 1 GiB, resident
     hold.fill_(1.0)
     torch.cuda.synchronize()
-    tel = Telemetry("/sys")
-    mine = [p for p in tel.kfd_processes("/proc") if p.pid == os.getpid()]
-    devs = tel.devices()
-    yield {"hold": hold, "tel": tel, "mine": mine, "devs": devs}
+    after = tel.kfd_processes("/proc")
+    mine = [p for p in after if p.vram_bytes - before.get((p.pid, p.gpu_id), 0) >= (1 << 30)]
+    yield {"hold": hold, "tel": tel, "mine": mine, "devs": tel.devices(), "after": after}
     tel.close()
 
 
 def test_kfd_lists_this_process_on_torchs_gpu(gpu_state):
     mine, devs = gpu_state["mine"], gpu_state["devs"]
     assert devs, "no KFD GPU nodes under /sys"
-    big = [p for p in mine if p.vram_bytes >= (1 << 30)]
-    assert big, f"this process holds no ≥1 GiB VRAM entry in KFD: {mine}"
-    by_gpu_id = {d.gpu_id: d for d in devs}
-    dev = by_gpu_id[big[0].gpu_id]
+    assert len(mine) == 1, f"no single KFD entry grew by the 1 GiB allocation: {gpu_state['after']} " \
+                           f"(/sys/class/kfd/kfd/proc: {_kfd_listing()})"
+    assert mine[0].vram_bytes >= 1 << 30
+    dev = {d.gpu_id: d for d in devs}[mine[0].gpu_id]
     bdf = _torch_bdf(0)
+    print(f"KFD: pid {mine[0].pid} (os.getpid() {os.getpid()}) holds {mine[0].vram_bytes >> 20} MiB on "
+          f"{dev.pci_bdf} (torch cuda:0: {bdf})")
     if bdf is not None:
         assert dev.pci_bdf.lower() == bdf.lower(), (dev.pci_bdf, bdf)
 
@@ -92,14 +108,14 @@ def test_node_agent_process_on_the_mi355x(gpu_state, tmp_path):
     from odh_kubeflow_amd.testing.kubelet.podresources_server import FakePodResourcesServer
 
     mine, devs = gpu_state["mine"], gpu_state["devs"]
-    big = [p for p in mine if p.vram_bytes >= (1 << 30)]
-    assert big
-    dev = {d.gpu_id: d for d in devs}[big[0].gpu_id]
+    assert len(mine) == 1
+    dev = {d.gpu_id: d for d in devs}[mine[0].gpu_id]
     bdf, idx = dev.pci_bdf, dev.index
 
-    # this process in a pod: a /proc view whose cgroup names a pod UID (systemd driver)
+    # this process in a pod: a host-/proc view whose cgroup file (for the host PID KFD uses)
+    # names a pod UID (systemd driver) — what the DaemonSet's hostPath /proc mount shows
     uid = str(uuid.uuid4())
-    proc = tmp_path / "proc" / str(os.getpid())
+    proc = tmp_path / "proc" / str(mine[0].pid)
     proc.mkdir(parents=True)
     (proc / "cgroup").write_text(
         f"0::/kubepods.slice/kubepods-burstable.slice/kubepods-burstable-pod{uid.replace('-', '_')}.slice/"

@@ -420,6 +420,9 @@ class CullingReconciler:
         self.checks = 0
         from collections import deque
         self.recent = deque(maxlen=64)  # (time, notebook, gpu_active, kernels, terminals) — debugging aid
+        # per cull: which signal decided it ("amdgpu" = an attributed GPU sample said idle;
+        # "jupyter" = the kernel/terminal activity, also when the GPU had no sample)
+        self.cull_log = deque(maxlen=1024)
 
     async def _update(self, req: Request, mutate: Callable[[dict], None]) -> None:
         async def fn():
@@ -455,10 +458,12 @@ class CullingReconciler:
             return Result(requeue_after=self.cfg.check_period_s)
 
         self.checks += 1
-        active_now, kernels, terminals = await self.sample(nb, pod)
+        active_now, kernels, terminals, signals = await self.sample(nb, pod)
         self.recent.append((rfc3339(), str(req), active_now, kernels, terminals))
+        culled = []
 
         def apply(cur: dict) -> None:
+            culled.clear()
             if active_now:
                 m.ensure_annotations(cur)[LAST_ACTIVITY_ANNOTATION] = rfc3339()
             else:
@@ -466,26 +471,38 @@ class CullingReconciler:
                 update_from_terminals(cur, terminals)
             update_check_timestamp(cur)
             if notebook_is_idle(cur, self.cfg.cull_idle_time_s):
-                log.info("Notebook %s/%s needs culling", req.namespace, req.name)
                 set_stop_annotation(cur, self.metrics)
-                self.culled += 1
+                culled.append(True)
 
         await self._update(req, apply)
+        if culled:
+            self.culled += 1
+            self.cull_log.append({"notebook": str(req), "at": rfc3339(), **signals})
+            log.info("Notebook %s/%s culled (idle for %.0f s): %s", req.namespace, req.name,
+                     self.cfg.cull_idle_time_s, ", ".join(f"{k}={v}" for k, v in signals.items()))
         return Result(requeue_after=self.cfg.check_period_s)
 
     async def sample(self, nb: dict, pod: dict):
-        """Returns ``(gpu_says_active, kernels, terminals)``."""
+        """Returns ``(gpu_says_active, kernels, terminals, signals)``; ``signals`` says what each
+        source reported (``amdgpu``: ``busy`` / ``idle`` with the mean busy %, or ``no-sample``;
+        ``jupyter``: ``sampled`` / ``unreachable`` / not consulted) — the record of which signal
+        a cull rests on."""
         src = self.cfg.activity_source
         gpu_active = False
         gpu_data = None
+        signals = {}
         if src in ("amdgpu", "combined") and self.gpu is not None and pod_requests_gpu(pod):
             gpu_data = await self.gpu.busy(pod, self.cfg.check_period_s)
             if gpu_data is not None:
                 gpu_active = gpu_says_active(gpu_data, self.cfg)
+                signals["amdgpu"] = f"{'busy' if gpu_active else 'idle'} {gpu_data.get('busy_mean', 0):.0f}%"
+            else:
+                signals["amdgpu"] = "no-sample"
         kernels = terminals = None
         if src in ("jupyter", "combined") or gpu_data is None:
             kernels, terminals = await self.jupyter.sample(nb, pod)
-        return gpu_active, kernels, terminals
+            signals["jupyter"] = "sampled" if kernels is not None or terminals is not None else "unreachable"
+        return gpu_active, kernels, terminals, signals
 
     async def close(self) -> None:
         await self.jupyter.close()

@@ -19,7 +19,8 @@ def test_loadtest_local_cluster_measures_every_notebook():
 
 
 def test_bench_culling_cpu_rehearsal():
-    """BASELINE config #5 on a synthetic sysfs: GPU-busy notebook kept, idle ones reclaimed."""
+    """BASELINE config #5 on a synthetic sysfs: idle notebooks reclaimed on their attributed GPU
+    sample, busy ones kept (although Jupyter says idle), reclaimed again once the load ends."""
     import json
     import subprocess
     import sys
@@ -29,9 +30,12 @@ def test_bench_culling_cpu_rehearsal():
                          cwd=__import__("os").path.dirname(__import__("os").path.dirname(__file__)))
     assert out.returncode == 0, out.stderr[-2000:]
     d = json.loads(out.stdout.strip().splitlines()[-1])
-    assert d["false_culls_under_load"] == 0 and d["culled"] == 8
-    assert d["gpu0_busy_mean_under_load"] >= 90
+    assert d["false_culls_under_load"] == 0 and d["culled"] == 16
+    assert d["gpu_busy_mean_under_load"] >= 90
     assert 0 <= d["idle_reclaim_ms_p50"] < 1500
+    assert d["culls_on_attributed_gpu_idle_sample"] == 16
+    for nb in d["per_notebook"].values():
+        assert nb["idle_phase"]["amdgpu"].startswith("idle") and nb["after_unload"]["amdgpu"].startswith("idle")
 
 
 def test_coverage_tool_units(tmp_path):

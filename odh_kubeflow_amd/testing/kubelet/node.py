@@ -266,6 +266,7 @@ async def run_gpu_probe_container(container: dict, visible: Sequence[int], timeo
     for e in container.get("env") or []:
         if "value" in e:
             env[e["name"]] = str(e["value"])
+    env["ODH_PROBE_T0_NS"] = str(time.time_ns())  # the probe reports its exec + link time against it
     t0 = time.perf_counter()
     proc = await asyncio.create_subprocess_exec(*probe_main.command(args), env=env, stdout=asyncio.subprocess.PIPE,
                                                 stderr=asyncio.subprocess.PIPE)

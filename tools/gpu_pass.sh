@@ -10,6 +10,7 @@
 #   ranks    2/4-rank rehearsal of the N>1 launch on the one GPU (never 8: the driver owns N=8)
 #   unsharded  the default topology (one kf + one odh manager process) at 1, 2 and 4 ranks
 #   probeexe the odh-gpu-probe init-container program: 10 process runs (wall time, verdict)
+#   hipinit  where a fresh process's HIP start-up goes, under ROCm runtime settings (tools/hip_init_ab.sh)
 #   webhook  BASELINE config #4 (tools/bench_webhook.py)
 #   culling  BASELINE config #5 (tools/bench_culling.py)
 #   realpods BASELINE configs #2/#3: 1 and 8 notebooks whose container is a real PyTorch-ROCm process
@@ -69,6 +70,9 @@ for s in $steps; do
           --probe-sample 0 > "$out/bench_unsharded_n$n.log" 2>&1 || fail unsharded $? "$out/bench_unsharded_n$n.log"
         show "$out/bench_unsharded_n$n.log" "unsharded n$n"
       done ;;
+    hipinit)
+      timeout -k 10 300 bash tools/hip_init_ab.sh "$tag" > "$out/hip_init_ab.log" 2>&1 || fail hipinit $? "$out/hip_init_ab.log"
+      cat "$out/hip_init_ab.log" ;;
     probeexe)
       for r in 1 2 3 4 5 6 7 8 9 10; do
         s0=$(date +%s%N)

@@ -3,8 +3,8 @@
 Layout on an 8×MI355X node (see :mod:`.shard` and :mod:`.platform`):
 
 * **rank 0** starts the native C++ apiserver (``odh-apiserver``: store, REST/watch,
-  admission, GC) and the node's platform — ONE scheduler (+ first-free ``amd.com/gpu``
-  allocation and the StatefulSet controller) and ONE kubelet for all GPUs — as child
+  admission, GC) and the node's platform — ONE scheduler (first-free ``amd.com/gpu``
+  allocation), ONE StatefulSet controller and ONE kubelet for all GPUs — as child
   processes, and broadcasts the URL;
 * the control plane under test runs as the deployment runs it: ``--arch sharded`` (default,
   ``overlays/mi355x-sharded``): every rank starts its ``cmd/control_plane.py --shard r``;
@@ -125,8 +125,8 @@ def measure(args) -> Optional[dict]:
                                             f"notebooks, as config/overlays/mi355x deploys them")
             out["config"]["architecture"] = "cmd/kf_manager + cmd/odh_manager (overlay mi355x, reference topology)"
         out["config"]["platform_stand_ins"] = ("native C++ apiserver (+GC); ONE scheduler (first-free amd.com/gpu "
-                                               "allocation) + StatefulSet controller process and ONE kubelet process "
-                                               "for the node's 8 GPUs")
+                                               "allocation), ONE StatefulSet controller and ONE kubelet process for "
+                                               "the node's 8 GPUs")
         out["rank_ms_per_step"] = res.get("rank_ms_per_step")
         out["cpu_ms_per_step"] = res.get("cpu_ms_per_step")
         out["child_rss_mib"] = res.get("child_rss_mib")

@@ -4,10 +4,11 @@ An 8×MI355X node has one kubelet, one kube-scheduler (+ the AMD device plugin c
 devices) and one kube-controller-manager, however many control-plane replicas run against
 the cluster.  :class:`NodePlatform` is that, for the benchmark and the multi-shard tests:
 
-* ``scheduler`` — :mod:`odh_kubeflow_amd.testing.cmd.scheduler` with
-  ``--statefulset-controller``: binds pods, allocates ``amd.com/gpu`` first-free (the device
-  plugin's policy; nothing steers a pod to a GPU by namespace or shard), and runs the
-  StatefulSet controller;
+* ``scheduler`` — :mod:`odh_kubeflow_amd.testing.cmd.scheduler`: binds pods and allocates
+  ``amd.com/gpu`` first-free (the device plugin's policy; nothing steers a pod to a GPU by
+  namespace or shard);
+* ``controller_manager`` — the same program with ``--controllers statefulset``:
+  kube-controller-manager's StatefulSet controller;
 * ``kubelet`` — :mod:`odh_kubeflow_amd.testing.cmd.fake_kubelet` for all the node's GPUs:
   registers the Node, runs each pod's init containers (with ``exec_init`` the MI355X start-up
   probe ``odh-gpu-probe`` as a real process on the pod's GPU) and reports pod status.
@@ -78,8 +79,11 @@ class NodePlatform:
     async def start(self) -> "NodePlatform":
         if self.process:
             self.procs["scheduler"] = await start_child(
-                "odh_kubeflow_amd.testing.cmd.scheduler", ["--master", self.url, "--statefulset-controller"],
-                "scheduler / StatefulSet controller")
+                "odh_kubeflow_amd.testing.cmd.scheduler", ["--master", self.url, "--controllers", "scheduler"],
+                "scheduler")
+            self.procs["controller_manager"] = await start_child(
+                "odh_kubeflow_amd.testing.cmd.scheduler", ["--master", self.url, "--controllers", "statefulset"],
+                "StatefulSet controller")
             args = ["--master", self.url, "--node-name", self.node_name, "--node-gpus", str(self.gpus),
                     "--devices", ",".join(str(i) for i in range(self.gpus)), "--ready-line"]
             if self.exec_init:
@@ -127,7 +131,7 @@ class NodePlatform:
         return all(m.idle() for m in self.managers)
 
     async def stop(self) -> None:
-        for k in ("kubelet", "scheduler"):
+        for k in ("kubelet", "controller_manager", "scheduler"):
             await stop_child(self.procs.pop(k, None))
         for mgr in reversed(self.managers):
             await mgr.stop()

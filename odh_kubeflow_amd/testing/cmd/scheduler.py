@@ -6,7 +6,8 @@ In a real cluster kube-scheduler (plus the AMD device plugin) is a separate proc
 the notebook controllers; the multi-GPU benchmark runs this one as a child of rank 0 so
 that no control-plane shard pays for the whole node's scheduling on its own event loop
 (every shard then reaches the scheduler through the apiserver alike).  With
-``--statefulset-controller`` it also plays kube-controller-manager's StatefulSet controller.
+``--controllers statefulset`` it plays kube-controller-manager's StatefulSet controller
+instead (its own process, as on a real cluster).
 Prints ``ready`` on stdout once its informers have synced.
 """
 
@@ -26,8 +27,9 @@ def parse(argv=None):
     p.add_argument("--kubeconfig", default=None)
     p.add_argument("--max-concurrent", type=int, default=1,
                    help="scheduling decisions are serialised by the allocator lock anyway")
-    p.add_argument("--statefulset-controller", action="store_true",
-                   help="also run the StatefulSet controller (kube-controller-manager's part of the notebook path)")
+    p.add_argument("--controllers", default="scheduler",
+                   help="comma list of scheduler (kube-scheduler + device allocation) and statefulset "
+                        "(kube-controller-manager's StatefulSet controller)")
     p.add_argument("--debug-log", action="store_true")
     return p.parse_args(argv)
 
@@ -42,16 +44,19 @@ async def amain(argv=None) -> int:
     args = parse(argv)
     setup_logging(debug=args.debug_log)
     cfg = RestConfig.load(args.master, args.kubeconfig)
-    mgr = Manager.remote(cfg, name="kube-scheduler")
-    SchedulerController(mgr.client, mgr.reader, mgr.get_event_recorder_for("default-scheduler")) \
-        .setup_with_manager(mgr, max_concurrent=args.max_concurrent)
-    synced = [kinds.POD, kinds.NODE]
-    if args.statefulset_controller:
+    ctrls = {c.strip() for c in args.controllers.split(",") if c.strip()}
+    mgr = Manager.remote(cfg, name="kube-scheduler" if "scheduler" in ctrls else "kube-controller-manager")
+    synced = []
+    if "scheduler" in ctrls:
+        SchedulerController(mgr.client, mgr.reader, mgr.get_event_recorder_for("default-scheduler")) \
+            .setup_with_manager(mgr, max_concurrent=args.max_concurrent)
+        synced += [kinds.POD, kinds.NODE]
+    if "statefulset" in ctrls:
         from ..kubelet.statefulset import StatefulSetController
 
         StatefulSetController(mgr.client, mgr.reader, mgr.get_event_recorder_for("statefulset-controller")) \
             .setup_with_manager(mgr)
-        synced.append(kinds.STATEFUL_SET)
+        synced += [kinds.STATEFUL_SET, kinds.POD]
     await mgr.start()
     await mgr.cache.wait_synced(synced)
     print("ready", flush=True)

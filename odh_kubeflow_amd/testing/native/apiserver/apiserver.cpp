@@ -569,10 +569,20 @@ struct WatchSlot {
   std::function<bool(const Value&)> wants;
 };
 
-struct Bucket {
-  std::map<std::pair<std::string, std::string>, Obj> objs;
+// one ordered event history: `seq` numbers its events, `hist` keeps the newest S.history
+struct Hist {
   std::deque<Ev> hist;
   int64_t seq = 0;
+};
+
+struct Bucket {
+  std::map<std::pair<std::string, std::string>, Obj> objs;
+  // every event of the kind (cluster-wide watchers) and, per namespace, that namespace's
+  // events: a namespace-scoped watch scans only its own namespace's history, so with one
+  // control-plane shard per GPU rank a woken watcher reads its events, not every rank's
+  // (the scan was O(ranks) per event).  Element references of by_ns stay valid (node-based).
+  Hist all;
+  std::unordered_map<std::string, Hist> by_ns;
   // watchers by namespace ("" = cluster-wide): a write wakes only the watchers of its kind
   // AND namespace, so with one control-plane shard per GPU rank (each watching its own
   // namespaces) a write costs O(1) wake-ups instead of one per shard
@@ -687,12 +697,20 @@ void index_owner(const Res& r, const Value& o, bool remove) {
 void emit(const Res& r, const char* type, Obj obj, Obj old) {
   Bucket& b = bucket(r);
   std::lock_guard<std::mutex> hg(b.hmu);
-  Ev e{++b.seq, std::stoll(mget(*obj, "resourceVersion")), type, std::move(obj), std::move(old),
+  const std::string evns = mget(*obj, "namespace");
+  Ev e{++b.all.seq, std::stoll(mget(*obj, "resourceVersion")), type, std::move(obj), std::move(old),
        std::make_shared<EvCache>()};
-  b.hist.push_back(std::move(e));
-  while (b.hist.size() > S.history) b.hist.pop_front();
-  const Ev& ev = b.hist.back();
-  if ((b.seq & 1023) == 0) {
+  if (!evns.empty()) {
+    Hist& h = b.by_ns[evns];
+    Ev copy = e;  // the same event (shared object, old object and serialisation cache)
+    copy.seq = ++h.seq;
+    h.hist.push_back(std::move(copy));
+    while (h.hist.size() > S.history) h.hist.pop_front();
+  }
+  b.all.hist.push_back(std::move(e));
+  while (b.all.hist.size() > S.history) b.all.hist.pop_front();
+  const Ev& ev = b.all.hist.back();
+  if ((b.all.seq & 1023) == 0) {
     // periodic broadcast: watchers of quiet namespaces advance past other namespaces'
     // events before those fall off the bounded history (no spurious 410 Gone relists)
     for (auto& w : b.watchers) t_wake.push_back({w.second, ev.obj, ev.old, true});
@@ -2531,6 +2549,7 @@ void serve_watch(int fd, Res& r, const Path& p, const Request& rq) {
   auto slot_ptr = std::make_shared<WatchSlot>();
   WatchSlot& slot = *slot_ptr;
   Bucket* wb = nullptr;
+  Hist* wh = nullptr;  // the history this watch reads: its namespace's, or the kind's
   struct Unregister {  // every exit path drops the slot from the bucket's watcher index
     Bucket*& b;
     const std::string& ns;
@@ -2552,8 +2571,9 @@ void serve_watch(int fd, Res& r, const Path& p, const Request& rq) {
     Bucket& b = bucket(r);
     std::lock_guard<std::mutex> hg(b.hmu);
     wb = &b;
+    wh = ns.empty() ? &b.all : &b.by_ns[ns];
     b.watchers.emplace(ns, slot_ptr);
-    last_seq = b.seq;
+    last_seq = wh->seq;
     if (rv.empty() || rv == "0") {
       for (auto& kv : b.objs)
         if (wants(*kv.second)) {
@@ -2564,14 +2584,16 @@ void serve_watch(int fd, Res& r, const Path& p, const Request& rq) {
         }
     } else {
       int64_t since = std::stoll(rv);
-      if (!b.hist.empty() && since < b.hist.front().rv - 1 && since < S.rv - (int64_t)b.hist.size()) {
+      const std::deque<Ev>& hist = wh->hist;
+      // 410 when events after `since` may have fallen off this watch's bounded history
+      if (hist.size() >= S.history && since < hist.front().rv - 1) {
         Value ev = Value::object();
         ev["type"] = Value::str("ERROR");
         ev["object"] = status_obj(Gone());
         pending.push_back(kj::dump(ev) + "\n");
         last_seq = -1;
       } else {
-        for (auto& e : b.hist)
+        for (auto& e : hist)
           if (e.rv > since && (wants(*e.obj) || (e.old && wants(*e.old)))) pending.push_back(event_line(r, e, p.version));
       }
     }
@@ -2595,26 +2617,27 @@ void serve_watch(int fd, Res& r, const Path& p, const Request& rq) {
     bool gone = false;
     {
       Bucket& b = *wb;  // element references of S.data stay valid; buckets are never erased
+      Hist& h = *wh;
       std::unique_lock<std::mutex> lk(b.hmu);
       // system_clock deadline: libstdc++ maps a steady_clock wait to pthread_cond_clockwait,
       // which ThreadSanitizer (GCC 11) does not intercept; the 500 ms timeout only paces
       // catch-up scans, so a wall-clock jump is harmless here
       slot.cv.wait_until(lk, std::chrono::system_clock::now() + std::chrono::milliseconds(500),
-                         [&] { return b.seq > last_seq || g_stop.load(); });
-      if (b.seq > last_seq) {
-        if (!b.hist.empty() && b.hist.front().seq > last_seq + 1) {
+                         [&] { return h.seq > last_seq || g_stop.load(); });
+      if (h.seq > last_seq) {
+        if (!h.hist.empty() && h.hist.front().seq > last_seq + 1) {
           gone = true;  // the watcher fell behind the bounded history
         } else {
-          size_t start = b.hist.size() - (size_t)(b.seq - last_seq);
+          size_t start = h.hist.size() - (size_t)(h.seq - last_seq);
           P.wakeups++;
-          P.scanned += b.hist.size() - start;
+          P.scanned += h.hist.size() - start;
           // serialise outside the store lock (copy the shared event refs first)
           std::vector<Ev> evs;
-          for (size_t n = start; n < b.hist.size(); ++n) {
-            const Ev& e = b.hist[n];
+          for (size_t n = start; n < h.hist.size(); ++n) {
+            const Ev& e = h.hist[n];
             if (wants(*e.obj) || (e.old && wants(*e.old))) evs.push_back(e);
           }
-          last_seq = b.seq;
+          last_seq = h.seq;
           lk.unlock();
           for (auto& e : evs) lines.push_back(event_line(r, e, p.version));
         }

@@ -78,17 +78,22 @@ class NodePlatform:
 
     async def start(self) -> "NodePlatform":
         if self.process:
+            prof = os.environ.get("ODH_PLATFORM_PROFILE")  # cProfile output prefix (profiling runs)
+
+            def pre(name):
+                return ["-m", "cProfile", "-o", f"{prof}.{name}"] if prof else []
             self.procs["scheduler"] = await start_child(
                 "odh_kubeflow_amd.testing.cmd.scheduler", ["--master", self.url, "--controllers", "scheduler"],
-                "scheduler")
+                "scheduler", python_args=pre("scheduler"))
             self.procs["controller_manager"] = await start_child(
                 "odh_kubeflow_amd.testing.cmd.scheduler", ["--master", self.url, "--controllers", "statefulset"],
-                "StatefulSet controller")
+                "StatefulSet controller", python_args=pre("controller_manager"))
             args = ["--master", self.url, "--node-name", self.node_name, "--node-gpus", str(self.gpus),
                     "--devices", ",".join(str(i) for i in range(self.gpus)), "--ready-line"]
             if self.exec_init:
                 args += ["--exec-init", "--hip-devices", str(self.hip_devices)]
-            self.procs["kubelet"] = await start_child("odh_kubeflow_amd.testing.cmd.fake_kubelet", args, "kubelet")
+            self.procs["kubelet"] = await start_child("odh_kubeflow_amd.testing.cmd.fake_kubelet", args, "kubelet",
+                                                      python_args=pre("kubelet"))
             return self
         from ..models import kinds
         from ..runtime.informer import InformerCache

@@ -460,12 +460,14 @@ class GpuRuntime:
         h = await self.runtime.start(pod, devices)
         h.info["uid"] = m.uid(pod)
         h.info["init_statuses"] = init_statuses
-        if devices and self.device_manager is not None:
-            self.device_manager.allocate(pod, devices)
         self.handles[key] = h
         self.started += 1
         await self._set_status(pod, ready=True, handle=h, init_statuses=init_statuses)
         h.info["reported"] = True
+        if devices and self.device_manager is not None:
+            # the device-manager checkpoint / pod-resources record (what the node agent reads):
+            # a file rewrite, kept off the Ready status write the pod is waiting for
+            self.device_manager.allocate(pod, devices)
         self.recorder.event(pod, "Normal", "Started", "Started container " + ",".join(
             c.get("name", "") for c in (pod.get("spec") or {}).get("containers") or []))
         return Result()

@@ -46,6 +46,7 @@ class StatefulSetController:
         self.reader = reader
         self.recorder = recorder
         self._created: set = set()  # (sts uid, ordinal) of pods this controller has created
+        self._rev: dict = {}  # (sts uid, generation) -> template hash: the template changes only with generation
 
     def _pod_for(self, sts: dict, ordinal: int, rev: str) -> dict:
         tmpl = (sts.get("spec") or {}).get("template") or {}
@@ -68,7 +69,12 @@ class StatefulSetController:
         if sts is None or m.is_deleting(sts):
             return Result()
         replicas = int((sts.get("spec") or {}).get("replicas", 1) or 0)
-        rev = template_hash(sts)
+        key = (m.uid(sts), (sts.get("metadata") or {}).get("generation"))
+        rev = self._rev.get(key)
+        if rev is None:
+            if len(self._rev) > 65536:
+                self._rev.clear()
+            rev = self._rev[key] = template_hash(sts)
         pods = [p for p in self.reader.list(kinds.POD, req.namespace, owner_uid=m.uid(sts)) if m.is_controlled_by(p, sts)]
         by_ord = {}
         for p in pods:

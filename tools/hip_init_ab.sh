@@ -18,9 +18,8 @@ run() {  # label env...
   done
 }
 run default X=1
+run hsa_first ODH_HSA_FIRST=1
 run fast_exit ODH_FAST_EXIT=1
 run rocr_visible ROCR_VISIBLE_DEVICES=0
 run no_sdma HSA_ENABLE_SDMA=0
-run one_hw_queue GPU_MAX_HW_QUEUES=1
-run no_interrupt HSA_ENABLE_INTERRUPT=0
 cat "$out/hip_init_ab.jsonl"

@@ -62,7 +62,9 @@ class FakeKubeletAgent:
         self.address = address
         self._tmp = None
         if checkpoint_path is None:
-            self._tmp = tempfile.TemporaryDirectory(prefix="odh-kubelet-")
+            # memory-backed when the host has /dev/shm: the stand-in rewrites the file per pod
+            shm = "/dev/shm" if os.path.isdir("/dev/shm") and os.access("/dev/shm", os.W_OK) else None
+            self._tmp = tempfile.TemporaryDirectory(prefix="odh-kubelet-", dir=shm)
             checkpoint_path = os.path.join(self._tmp.name, "device-plugins", "kubelet_internal_checkpoint")
         self.checkpoint_path = checkpoint_path
         self.device_manager = FakeDeviceManager(device_id_of or default_device_id_of(telemetry),

@@ -47,6 +47,7 @@ class StatefulSetController:
         self.recorder = recorder
         self._created: set = set()  # (sts uid, ordinal) of pods this controller has created
         self._rev: dict = {}  # (sts uid, generation) -> template hash: the template changes only with generation
+        self._status: dict = {}  # sts uid -> the status this controller last wrote
 
     def _pod_for(self, sts: dict, ordinal: int, rev: str) -> dict:
         tmpl = (sts.get("spec") or {}).get("template") or {}
@@ -135,10 +136,16 @@ class StatefulSetController:
         st = {"replicas": len(pods), "readyReplicas": ready, "currentReplicas": current, "updatedReplicas": current,
               "availableReplicas": ready, "currentRevision": rev, "updateRevision": rev,
               "observedGeneration": (sts.get("metadata") or {}).get("generation", 1)}
-        if (sts.get("status") or {}) != st:
+        uid = m.uid(sts)
+        if (sts.get("status") or {}) != st and self._status.get(uid) != st:
+            # (the second test: the cache may not show our last write yet — pod events arrive
+            # in bursts and each one reconciles the StatefulSet)
+            if len(self._status) > 65536:
+                self._status.clear()
             try:
                 await self.client.patch(sts, [{"op": "add", "path": "/status", "value": st}], "json",
                                         subresource="status")
+                self._status[uid] = st
             except ApiError as e:
                 if not is_not_found(e):
                     raise

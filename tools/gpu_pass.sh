@@ -11,11 +11,14 @@
 #   unsharded  the default topology (one kf + one odh manager process) at 1, 2 and 4 ranks
 #   probeexe the odh-gpu-probe init-container program: 10 process runs (wall time, verdict)
 #   hipinit  where a fresh process's HIP start-up goes, under ROCm runtime settings (tools/hip_init_ab.sh)
+#   hipexit  where a GPU process's exit goes: what it holds when it leaves (tools/hip_exit_ab.py)
 #   webhook  BASELINE config #4 (tools/bench_webhook.py)
 #   culling  BASELINE config #5 (tools/bench_culling.py)
 #   realpods BASELINE configs #2/#3: 1 and 8 notebooks whose container is a real PyTorch-ROCm process
 #   realref  the same with the reference's serialising odh path (--reference-emulation)
 #   refemu   bench.py --reference-emulation (control-plane lifecycle, reference behaviour)
+#   cpprof   cProfile of the control-plane and node-platform processes over a 300-step bench (pstats top 40)
+#   critpath hop-by-hop create→Ready from the apiserver audit log at 1 and 4 ranks (tools/gpu_critical_path.sh)
 #   prof     rocprofv3 --kernel-trace --stats of the odh-gpu-probe program
 #   pmc      rocprofv3 --pmc passes (MFMA busy, LDS bank conflicts, HBM bytes) of the probe kernels
 #   probe    start-up probe: eager launches vs hipGraph replay (tools/probe_microbench.py --startup)
@@ -73,6 +76,30 @@ for s in $steps; do
     hipinit)
       timeout -k 10 300 bash tools/hip_init_ab.sh "$tag" > "$out/hip_init_ab.log" 2>&1 || fail hipinit $? "$out/hip_init_ab.log"
       cat "$out/hip_init_ab.log" ;;
+    hipexit)
+      timeout -k 10 300 python tools/hip_exit_ab.py --repeats 5 > "$out/hip_exit_ab.jsonl" 2>&1 \
+        || fail hipexit $? "$out/hip_exit_ab.jsonl"
+      tail -1 "$out/hip_exit_ab.jsonl" ;;
+    cpprof)
+      mkdir -p "$out/cprof"
+      ODH_CONTROL_PLANE_PROFILE=$PWD/$out/cprof/cp ODH_PLATFORM_PROFILE=$PWD/$out/cprof/plat \
+        timeout -k 10 200 python bench.py --gpus 1 --no-inprocess-baseline --probe-sample 0 > "$out/bench_cpprof.log" 2>&1 \
+        || fail cpprof $? "$out/bench_cpprof.log"
+      show "$out/bench_cpprof.log" "n1 cprofiled"
+      for f in "$out"/cprof/*; do
+        python - "$f" > "$f.txt" <<'PY' || fail cpprof $? "$f.txt"
+import pstats, sys
+st = pstats.Stats(sys.argv[1])
+st.sort_stats("tottime").print_stats(40)
+st.sort_stats("cumulative").print_stats(40)
+PY
+        rm -f "$f"
+      done
+      ls "$out/cprof" ;;
+    critpath)
+      timeout -k 10 600 bash tools/gpu_critical_path.sh "$tag" > "$out/critpath.log" 2>&1 || fail critpath $? "$out/critpath.log"
+      python -c "import json,sys; d=json.load(open(sys.argv[1])); print(d['create_to_notebook_status_ms'], {k: (v['gap_ms_p50'], v['serve_ms_p50']) for k, v in d['hops'].items()})" \
+        "$out/critical_path_n1.json" ;;
     probeexe)
       for r in 1 2 3 4 5 6 7 8 9 10; do
         s0=$(date +%s%N)

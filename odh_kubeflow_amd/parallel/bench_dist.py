@@ -278,7 +278,9 @@ async def _main(args, dist, torch, rank: int, world: int, ndev: int, probe_sampl
             pol = AuditPolicy([{"level": lv}])  # every request: what each process sends
         native = await NativeApiServer(OPENSHIFT_CRDS, gc=True, audit_log_path=audit, audit_policy=pol).start()
         url[0] = native.url
-        platform = await NodePlatform(native.url, exec_init=probe_sample > 0, hip_devices=ndev).start()
+        # the node's StatefulSet controller and kubelet: one worker process of each per two ranks
+        platform = await NodePlatform(native.url, exec_init=probe_sample > 0, hip_devices=ndev,
+                                      workers=(world + 1) // 2).start()
     await _in_thread(dist.broadcast_object_list, url, 0)
     env = {"SET_PIPELINE_RBAC": "false", "SET_PIPELINE_SECRET": "false"}
     shard = ControlPlaneShard(ShardConfig(

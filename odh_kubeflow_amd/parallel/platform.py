@@ -13,6 +13,14 @@ the cluster.  :class:`NodePlatform` is that, for the benchmark and the multi-sha
   registers the Node, runs each pod's init containers (with ``exec_init`` the MI355X start-up
   probe ``odh-gpu-probe`` as a real process on the pod's GPU) and reports pod status.
 
+``workers`` > 1 runs the StatefulSet controller and the kubelet as that many processes each,
+worker i of both serving the namespaces claimed for i (least-loaded first,
+:class:`~odh_kubeflow_amd.testing.kubelet.statefulset.NamespaceClaimer`; ``--partition
+i/W``).  That is the concurrency kube-controller-manager and the kubelet have in their
+goroutines and one Python event loop has not: at 4 ranks a single StatefulSet controller
+process was ≈80 % busy, so at 8 it would set the pace.  Device allocation stays with the one
+scheduler (first free, written on the pod), so the workers never disagree about GPUs.
+
 ``process=True`` (the benchmark) runs both as child processes of rank 0; ``process=False``
 runs the same controllers in this process (tests).  GC runs in the native apiserver.
 """
@@ -62,7 +70,7 @@ async def stop_child(proc: Optional[subprocess.Popen]) -> None:
 
 class NodePlatform:
     def __init__(self, apiserver_url: str, node_name: str = "mi355x-node-0", gpus: int = 8, process: bool = True,
-                 exec_init: bool = False, hip_devices: int = 0, max_concurrent: int = 8):
+                 exec_init: bool = False, hip_devices: int = 0, max_concurrent: int = 8, workers: int = 1):
         self.url = apiserver_url
         self.node_name = node_name
         self.gpus = gpus
@@ -70,6 +78,7 @@ class NodePlatform:
         self.exec_init = exec_init
         self.hip_devices = hip_devices
         self.max_concurrent = max_concurrent
+        self.workers = max(1, int(workers))
         self.procs: Dict[str, subprocess.Popen] = {}
         self.managers = []
         self.agent = None
@@ -85,15 +94,22 @@ class NodePlatform:
             self.procs["scheduler"] = await start_child(
                 "odh_kubeflow_amd.testing.cmd.scheduler", ["--master", self.url, "--controllers", "scheduler"],
                 "scheduler", python_args=pre("scheduler"))
-            self.procs["controller_manager"] = await start_child(
-                "odh_kubeflow_amd.testing.cmd.scheduler", ["--master", self.url, "--controllers", "statefulset"],
-                "StatefulSet controller", python_args=pre("controller_manager"))
-            args = ["--master", self.url, "--node-name", self.node_name, "--node-gpus", str(self.gpus),
-                    "--devices", ",".join(str(i) for i in range(self.gpus)), "--ready-line"]
-            if self.exec_init:
-                args += ["--exec-init", "--hip-devices", str(self.hip_devices)]
-            self.procs["kubelet"] = await start_child("odh_kubeflow_amd.testing.cmd.fake_kubelet", args, "kubelet",
-                                                      python_args=pre("kubelet"))
+            w = self.workers
+            for i in range(w):
+                name = "controller_manager" if w == 1 else f"controller_manager_{i}"
+                self.procs[name] = await start_child(
+                    "odh_kubeflow_amd.testing.cmd.scheduler",
+                    ["--master", self.url, "--controllers", "statefulset", "--partition", f"{i}/{w}"],
+                    "StatefulSet controller", python_args=pre(name))
+            for i in range(w):
+                name = "kubelet" if w == 1 else f"kubelet_{i}"
+                args = ["--master", self.url, "--node-name", self.node_name, "--node-gpus", str(self.gpus),
+                        "--devices", ",".join(str(i) for i in range(self.gpus)), "--ready-line",
+                        "--partition", f"{i}/{w}"]
+                if self.exec_init:
+                    args += ["--exec-init", "--hip-devices", str(self.hip_devices)]
+                self.procs[name] = await start_child("odh_kubeflow_amd.testing.cmd.fake_kubelet", args, "kubelet",
+                                                     python_args=pre(name))
             return self
         from ..models import kinds
         from ..runtime.informer import InformerCache
@@ -136,7 +152,7 @@ class NodePlatform:
         return all(m.idle() for m in self.managers)
 
     async def stop(self) -> None:
-        for k in ("kubelet", "controller_manager", "scheduler"):
+        for k in [*[k for k in self.procs if k.startswith(("kubelet", "controller_manager"))], "scheduler"]:
             await stop_child(self.procs.pop(k, None))
         for mgr in reversed(self.managers):
             await mgr.stop()

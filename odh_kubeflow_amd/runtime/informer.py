@@ -236,21 +236,26 @@ class InformerCache(Reader, EventSource):
     a label-selected Namespace watch adds a namespace's informers when it starts matching
     (a shard is assigned a namespace) and drops them, with DELETED events for what they
     held, when it stops matching; ``namespaces`` are then always-cached extras (the
-    controller namespace).  ``selectors`` maps a kind to a label selector applied
-    server-side to its list/watch (``cache.Options.ByObject[..].Label``) so a shard only
-    ever receives the objects it owns.
+    controller namespace).  ``namespace_filter`` (a predicate on the Namespace object)
+    narrows the dynamic set (with no ``namespace_selector``: every namespace it admits) — one
+    worker of a controller partitioned over processes watches only its partition's namespaces.
+    ``selectors`` maps a kind to a label selector applied server-side to its list/watch
+    (``cache.Options.ByObject[..].Label``) so a shard only ever receives the objects it owns.
     """
 
     def __init__(self, rest, namespace: Optional[str] = None, transforms: Optional[Dict[str, Optional[Transform]]] = None,
                  watch_timeout_s: int = 300, namespaces: Optional[Iterable[str]] = None,
-                 selectors: Optional[Dict[str, str]] = None, namespace_selector: Optional[str] = None):
+                 selectors: Optional[Dict[str, str]] = None, namespace_selector: Optional[str] = None,
+                 namespace_filter: Optional[Callable[[dict], bool]] = None):
         self.rest = rest
         self.namespace = namespace
         nss = list(namespaces) if namespaces is not None else ([namespace] if namespace else None)
         self.static_namespaces: List[str] = list(nss or [])
         self.namespace_selector = namespace_selector
+        self.namespace_filter = namespace_filter
+        self._dynamic = bool(namespace_selector) or namespace_filter is not None
         # None = every namespace (cluster-wide informers)
-        self.namespaces: Optional[Set[str]] = set(nss or ()) if (nss or namespace_selector) else None
+        self.namespaces: Optional[Set[str]] = set(nss or ()) if (nss or self._dynamic) else None
         self.transforms: Dict[str, Optional[Transform]] = {}
         for k, fn in (transforms or {}).items():
             self.transforms[SCHEME.resolve(k).key] = fn
@@ -266,10 +271,10 @@ class InformerCache(Reader, EventSource):
     # -------------------------------------------------------------- namespace membership
 
     def _ensure_ns_informer(self) -> None:
-        if self.namespace_selector is None or self._ns_informer is not None:
+        if not self._dynamic or self._ns_informer is not None:
             return
         info = SCHEME.resolve(kinds_namespace())
-        inf = _Informer(self, info, info.storage_version, None, self.namespace_selector)
+        inf = _Informer(self, info, info.storage_version, None, self.namespace_selector or None)
         inf.handlers = {0: (None, self._on_namespace)}
         self._ns_informer = inf
         inf.task = asyncio.ensure_future(inf.run())
@@ -280,7 +285,7 @@ class InformerCache(Reader, EventSource):
             return
         # a Terminating namespace stays cached: its Notebooks' finalizers still need the
         # controllers; it leaves when it is gone or stops matching the selector (DELETED)
-        if etype == "DELETED":
+        if etype == "DELETED" or (self.namespace_filter is not None and not self.namespace_filter(obj)):
             if ns in self.namespaces:
                 self.namespaces.discard(ns)
                 self.namespace_changes += 1

@@ -39,6 +39,9 @@ def parse(argv=None):
     p.add_argument("--ready-line", action="store_true", help="print 'ready' once the informers have synced")
     p.add_argument("--address", default="127.0.0.1")
     p.add_argument("--jupyter", action="store_true", help="serve the Jupyter API for started notebooks")
+    p.add_argument("--partition", default="0/1",
+                   help="i/W: kubelet worker i of W, running the pods of the namespaces platform worker i "
+                        "claimed (testing/kubelet/statefulset.py NamespaceClaimer); worker 0 registers the Node")
     p.add_argument("--debug-log", action="store_true")
     return p.parse_args(argv)
 
@@ -49,7 +52,15 @@ def build(args):
     from ...runtime.rest import RestConfig
 
     devices = [int(x) for x in args.devices.split(",") if x.strip()]
-    mgr = Manager.remote(RestConfig.load(args.master, args.kubeconfig), name=f"kubelet-{args.node_name}")
+    part, _, nparts = args.partition.partition("/")
+    part, nparts = int(part), int(nparts or 1)
+    cache_options = None
+    if nparts > 1:
+        from ..kubelet.statefulset import worker_owns
+
+        cache_options = {"namespace_filter": lambda ns: worker_owns(ns, part)}
+    mgr = Manager.remote(RestConfig.load(args.master, args.kubeconfig), name=f"kubelet-{args.node_name}",
+                         cache_options=cache_options)
     device_id_of = None
     if args.sysfs_root:
         from ..kubelet.agent import default_device_id_of
@@ -69,7 +80,7 @@ def build(args):
         runtime = FakeContainerRuntime(exec_init=True, visible_device=visible)
     agent = FakeKubeletAgent(mgr, args.node_name, devices, args.node_gpus, runtime=runtime,
                              address=args.address, checkpoint_path=args.checkpoint_path, device_id_of=device_id_of,
-                             one_runtime=True)
+                             one_runtime=True, register_node=part == 0)
     return mgr, agent
 
 

@@ -7,7 +7,14 @@ the notebook controllers; the multi-GPU benchmark runs this one as a child of ra
 that no control-plane shard pays for the whole node's scheduling on its own event loop
 (every shard then reaches the scheduler through the apiserver alike).  With
 ``--controllers statefulset`` it plays kube-controller-manager's StatefulSet controller
-instead (its own process, as on a real cluster).
+instead (its own process, as on a real cluster).  kube-controller-manager syncs
+StatefulSets concurrently (``--concurrent-statefulset-syncs``, goroutines in one process);
+this Python stand-in gets that concurrency from worker processes instead:
+``--partition i/W`` makes this worker own the namespaces labelled
+``testing.odh-kubeflow-amd/kcm-worker=i`` (claimed least-loaded first,
+:class:`~odh_kubeflow_amd.testing.kubelet.statefulset.NamespaceClaimer`) and watch only those
+(``InformerCache(namespace_filter=…)``), so W workers share the node's StatefulSets without
+any one of them decoding every event.
 Prints ``ready`` on stdout once its informers have synced.
 """
 
@@ -30,6 +37,8 @@ def parse(argv=None):
     p.add_argument("--controllers", default="scheduler",
                    help="comma list of scheduler (kube-scheduler + device allocation) and statefulset "
                         "(kube-controller-manager's StatefulSet controller)")
+    p.add_argument("--partition", default="0/1",
+                   help="i/W: this is StatefulSet worker i of W (each owns the namespaces it claimed)")
     p.add_argument("--debug-log", action="store_true")
     return p.parse_args(argv)
 
@@ -45,7 +54,15 @@ async def amain(argv=None) -> int:
     setup_logging(debug=args.debug_log)
     cfg = RestConfig.load(args.master, args.kubeconfig)
     ctrls = {c.strip() for c in args.controllers.split(",") if c.strip()}
-    mgr = Manager.remote(cfg, name="kube-scheduler" if "scheduler" in ctrls else "kube-controller-manager")
+    part, _, nparts = args.partition.partition("/")
+    part, nparts = int(part), int(nparts or 1)
+    cache_options = None
+    if nparts > 1:
+        from ..kubelet.statefulset import worker_owns
+
+        cache_options = {"namespace_filter": lambda ns: worker_owns(ns, part)}
+    mgr = Manager.remote(cfg, name="kube-scheduler" if "scheduler" in ctrls else "kube-controller-manager",
+                         cache_options=cache_options)
     synced = []
     if "scheduler" in ctrls:
         SchedulerController(mgr.client, mgr.reader, mgr.get_event_recorder_for("default-scheduler")) \
@@ -57,6 +74,11 @@ async def amain(argv=None) -> int:
         StatefulSetController(mgr.client, mgr.reader, mgr.get_event_recorder_for("statefulset-controller")) \
             .setup_with_manager(mgr)
         synced += [kinds.STATEFUL_SET, kinds.POD]
+        if nparts > 1:
+            from ..kubelet.statefulset import NamespaceClaimer
+
+            NamespaceClaimer(mgr.client, mgr.reader, part, nparts).setup_with_manager(mgr)
+            synced += [kinds.NAMESPACE]
     await mgr.start()
     await mgr.cache.wait_synced(synced)
     print("ready", flush=True)

@@ -17,13 +17,32 @@ from typing import Optional
 
 from ...models import kinds
 from ...models import meta as m
-from ...models.errors import ApiError, is_already_exists, is_not_found
+from ...models.errors import ApiError, is_already_exists, is_conflict, is_not_found
 from ...runtime.controller import Request, Result, enqueue_for_owner
 from ...utils.objutil import deepcopy_json
 
 log = logging.getLogger(__name__)
 
 REVISION_LABEL = "controller-revision-hash"
+# which node-platform worker (StatefulSet controller + kubelet process pair) owns a
+# namespace (NamespaceClaimer)
+WORKER_LABEL = "testing.odh-kubeflow-amd/platform-worker"
+# never claimed (cluster-lifetime namespaces, no notebooks): worker 0 owns them unlabelled
+SYSTEM_NAMESPACES = ("default",)
+SYSTEM_PREFIXES = ("kube-", "openshift")
+
+
+def is_system_namespace(name: str) -> bool:
+    return name in SYSTEM_NAMESPACES or name.startswith(SYSTEM_PREFIXES)
+
+
+def worker_owns(ns: dict, index: int) -> bool:
+    """Whether platform worker ``index`` serves the namespace ``ns`` (a Namespace object)."""
+    md = ns.get("metadata") or {}
+    w = (md.get("labels") or {}).get(WORKER_LABEL)
+    if w is None:
+        return index == 0 and is_system_namespace(md.get("name", ""))
+    return w == str(index)
 
 
 def template_hash(sts: dict) -> str:
@@ -156,3 +175,66 @@ class StatefulSetController:
         if max_concurrent:
             b.with_options(max_concurrent_reconciles=max_concurrent)
         return b.complete(self)
+
+
+class NamespaceClaimer:
+    """Balances namespaces over W node-platform workers.
+
+    kube-controller-manager is one Go process syncing StatefulSets concurrently, and a
+    kubelet one Go process running pod workers concurrently; the Python stand-ins run W
+    processes of each instead, worker i of both watching only the namespaces labelled
+    ``WORKER_LABEL=i`` (``InformerCache(namespace_filter=…)``).  The StatefulSet workers
+    claim.  A new namespace is
+    claimed by the worker that owns the fewest (ties: the lowest index) — every worker
+    computes the same answer from its Namespace cache and only that one writes, with the
+    namespace's resourceVersion as precondition, so a worker whose cache lags cannot
+    double-claim.  System namespaces (``default``, ``kube-*``, ``openshift*``) are never
+    claimed and not counted: worker 0 serves them.  A hash of the name would be simpler, but
+    over the handful of namespaces a node's notebooks live in it is lumpy (4 ``bench-r``
+    names, W=2: all four on one worker)."""
+
+    RECHECK_S = 0.05  # an unclaimed namespace another worker should take: look again
+
+    def __init__(self, client, reader, index: int, workers: int):
+        self.client = client
+        self.reader = reader
+        self.index = int(index)
+        self.workers = int(workers)
+        self.claimed = 0
+        self._mine: set = set()  # claims of this worker its cache may not show yet
+
+    async def reconcile(self, req: Request) -> Result:
+        ns = self.reader.get(kinds.NAMESPACE, req.name)
+        if ns is None or m.is_deleting(ns) or WORKER_LABEL in m.labels(ns) or is_system_namespace(req.name):
+            return Result()
+        load = [0] * self.workers
+        seen = set()
+        for x in self.reader.list(kinds.NAMESPACE):
+            w = m.labels(x).get(WORKER_LABEL)
+            if w is not None and w.isdigit() and int(w) < self.workers:
+                load[int(w)] += 1
+                seen.add(m.name(x))
+        self._mine &= {m.name(x) for x in self.reader.list(kinds.NAMESPACE)}
+        load[self.index] += len(self._mine - seen)
+        if min(range(self.workers), key=lambda i: (load[i], i)) != self.index:
+            # the least-loaded worker claims it; should its cache lag behind claims this one
+            # already sees (or the other way round), both decide again shortly
+            return Result(requeue_after=self.RECHECK_S)
+        self._mine.add(req.name)  # before the write: a concurrent decision must count it
+        try:
+            await self.client.patch(kinds.NAMESPACE, {"metadata": {
+                "resourceVersion": m.resource_version(ns), "labels": {WORKER_LABEL: str(self.index)}}},
+                "merge", name=m.name(ns))
+            self.claimed += 1
+        except ApiError as e:
+            self._mine.discard(req.name)
+            if is_conflict(e):  # claimed (or changed) meanwhile: decide again on the new version
+                return Result(requeue=True)
+            if not is_not_found(e):
+                raise
+        return Result()
+
+    def setup_with_manager(self, mgr):
+        # one decision at a time: each counts the claims before it
+        return (mgr.builder().named("namespace-claimer").for_(kinds.NAMESPACE)
+                .with_options(max_concurrent_reconciles=1).complete(self))

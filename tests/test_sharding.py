@@ -248,6 +248,55 @@ def test_two_shards_one_native_apiserver(run):
     run(go())
 
 
+def test_statefulset_workers_split_namespaces(run):
+    """The node platform's StatefulSet controller and kubelet as two worker processes each:
+    each new namespace is claimed by the least-loaded worker (4 namespaces → 2 + 2), each
+    worker watches only its own, and every StatefulSet still gets its pod, scheduled (one
+    scheduler: four different GPUs, first free) and Ready."""
+    async def go():
+        from odh_kubeflow_amd.parallel.platform import NodePlatform
+        from odh_kubeflow_amd.testing.apiserver.native import NativeApiServer
+        from odh_kubeflow_amd.testing.cluster import OPENSHIFT_CRDS
+        from odh_kubeflow_amd.testing.kubelet.statefulset import WORKER_LABEL
+
+        native = await NativeApiServer(OPENSHIFT_CRDS, gc=True).start()
+        rest = RestClient(RestConfig(host=native.url))
+        platform = None
+        try:
+            platform = await NodePlatform(native.url, process=True, workers=2).start()
+            assert sorted(platform.pids()) == ["controller_manager_0", "controller_manager_1", "kubelet_0",
+                                               "kubelet_1", "scheduler"]
+            nss = [f"team-{i}" for i in range(4)]
+            for ns in nss:
+                await rest.create({"apiVersion": "v1", "kind": "Namespace", "metadata": {"name": ns}})
+                await rest.create({
+                    "apiVersion": "apps/v1", "kind": "StatefulSet", "metadata": {"name": "s", "namespace": ns},
+                    "spec": {"replicas": 1, "selector": {"matchLabels": {"app": "s"}},
+                             "template": {"metadata": {"labels": {"app": "s"}},
+                                          "spec": {"containers": [{"name": "c", "image": "img",
+                                                                   "resources": {"limits": {"amd.com/gpu": "1"}}}]}}}})
+            loop = asyncio.get_running_loop()
+            deadline = loop.time() + 30
+            while loop.time() < deadline:
+                ready = [((await rest.get(kinds.STATEFUL_SET, "s", ns)).get("status") or {}).get("readyReplicas")
+                         for ns in nss]
+                if ready == [1, 1, 1, 1]:
+                    break
+                await asyncio.sleep(0.05)
+            assert ready == [1, 1, 1, 1]
+            owners = [m.labels(await rest.get(kinds.NAMESPACE, ns)).get(WORKER_LABEL) for ns in nss]
+            assert sorted(owners) == ["0", "0", "1", "1"], owners
+            pods = [(await rest.get(kinds.POD, "s-0", ns)) for ns in nss]
+            assert sorted(m.annotations(p)["amd.com/gpu-ids"] for p in pods) == ["0", "1", "2", "3"]
+            assert len(await rest.list(kinds.NODE)) == 1
+        finally:
+            if platform is not None:
+                await platform.stop()
+            await rest.close()
+            await native.stop()
+    run(go())
+
+
 def test_unsharded_topology_two_drivers(run):
     """``--arch unsharded``: one kf manager + one odh manager (the reference topology,
     overlay mi355x) serve two drivers' namespaces; the second driver launches nothing."""

@@ -54,6 +54,8 @@ async def amain(argv=None) -> int:
     setup_logging(debug=args.debug_log)
     cfg = RestConfig.load(args.master, args.kubeconfig)
     ctrls = {c.strip() for c in args.controllers.split(",") if c.strip()}
+    if "scheduler" not in ctrls:  # audit logs / critical path: name the component, not the program
+        cfg.user_agent = cfg.user_agent.replace("scheduler", "controller_manager", 1)
     part, _, nparts = args.partition.partition("/")
     part, nparts = int(part), int(nparts or 1)
     cache_options = None

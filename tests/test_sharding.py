@@ -386,6 +386,39 @@ def test_informer_namespace_selector_follows_labels(run, server_kind):
     run(go())
 
 
+def test_informer_namespace_filter_follows_objects(run, server_kind):
+    """``namespace_filter`` without a selector: the cache follows every namespace the
+    predicate admits (a platform worker's ``worker_owns``) — system namespaces for worker 0,
+    labelled ones for their worker — and a relabelled namespace leaves it."""
+    from odh_kubeflow_amd.testing.kubelet.statefulset import WORKER_LABEL, worker_owns
+
+    async def go():
+        srv, c = await _server(server_kind)
+        try:
+            for ns, w in (("kube-system", None), ("t0", "0"), ("t1", "1"), ("new", None)):
+                md = {"name": ns, **({"labels": {WORKER_LABEL: w}} if w else {})}
+                await c.create({"apiVersion": "v1", "kind": "Namespace", "metadata": md})
+                await c.create(_cm("x", ns))
+            caches = [InformerCache(c, namespace_filter=lambda o, i=i: worker_owns(o, i)) for i in (0, 1)]
+            for cache in caches:
+                await cache.wait_synced([kinds.CONFIG_MAP])
+            assert await _wait(lambda: sorted(m.namespace(o) for o in caches[0].list(kinds.CONFIG_MAP))
+                               == ["kube-system", "t0"])
+            assert await _wait(lambda: [m.namespace(o) for o in caches[1].list(kinds.CONFIG_MAP)] == ["t1"])
+            # "new" is claimed by worker 1; t0 moves to worker 1
+            await c.patch(kinds.NAMESPACE, {"metadata": {"labels": {WORKER_LABEL: "1"}}}, name="new")
+            await c.patch(kinds.NAMESPACE, {"metadata": {"labels": {WORKER_LABEL: "1"}}}, name="t0")
+            assert await _wait(lambda: sorted(m.namespace(o) for o in caches[1].list(kinds.CONFIG_MAP))
+                               == ["new", "t0", "t1"])
+            assert await _wait(lambda: [m.namespace(o) for o in caches[0].list(kinds.CONFIG_MAP)] == ["kube-system"])
+            for cache in caches:
+                await cache.stop()
+        finally:
+            await c.close()
+            await srv.stop()
+    run(go())
+
+
 def test_namespace_shard_assigner(run):
     from odh_kubeflow_amd.controllers.sharding import NamespaceShardAssigner, shard_for
     from odh_kubeflow_amd.runtime.manager import Manager

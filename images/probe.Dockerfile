@@ -1,5 +1,5 @@
 # The MI355X start-up probe (init container `amd-gpu-probe`, injected by the kf StatefulSet
-# generator for notebooks annotated amd.com/gpu-probe: "true" or with GPU_STARTUP_PROBE=true).
+# generator for notebooks annotated amd.com/gpu-probe: "true" / "rccl" or with GPU_STARTUP_PROBE=true).
 # odh-gpu-probe + libodh_gpu_probe.so on the ROCm runtime only: no Python, no torch — the
 # probe's cost in the pod's create→Ready is process start + HIP init + ~0.2 ms of GPU work.
 ARG ROCM_DEV_IMAGE=rocm/dev-ubuntu-22.04:7.0-complete
@@ -16,7 +16,10 @@ RUN mkdir -p /opt/odh/bin \
 
 FROM ${ROCM_RUNTIME_IMAGE}
 COPY --from=build /opt/odh/bin /opt/odh/bin
-ENV PATH=/opt/odh/bin:${PATH}
+# RCCL for the optional all-reduce step (--rccl-mib; amd.com/gpu-probe: "rccl"): dlopen'ed
+# only by that step, so a plain probe never maps the 570 MB library
+COPY --from=build /opt/rocm/lib/librccl.so.1* /opt/rocm/lib/
+ENV PATH=/opt/odh/bin:${PATH} LD_LIBRARY_PATH=/opt/rocm/lib
 USER 65532:65532
 ENTRYPOINT ["odh-gpu-probe"]
 CMD ["--json", "/dev/termination-log"]

@@ -144,37 +144,50 @@ GPU_PROBE_ANNOTATION = "amd.com/gpu-probe"
 GPU_PROBE_CONTAINER = "amd-gpu-probe"
 DEFAULT_GPU_PROBE_IMAGE = "quay.io/opendatahub/odh-kubeflow-amd-gpu-probe:main"  # manifests pin the release
 GPU_PROBE_TIMEOUT_MS = "30000"
+GPU_PROBE_RCCL_MIB = "64"  # all-reduce size of the RCCL step (annotation value "rccl")
 
 
 def gpu_probe_enabled(nb: dict, pod_spec: dict, env: Mapping[str, str] = os.environ) -> bool:
     """The MI355X start-up probe runs for notebooks that request ``amd.com/gpu`` when the
-    Notebook says ``amd.com/gpu-probe: "true"``, or when the operator turned it on for every
-    GPU notebook (``GPU_STARTUP_PROBE=true``) and the Notebook does not say ``"false"``.
-    Off by default (never on the reconcile path, opt-in)."""
+    Notebook says ``amd.com/gpu-probe: "true"`` (or ``"rccl"``), or when the operator turned
+    it on for every GPU notebook (``GPU_STARTUP_PROBE=true``) and the Notebook does not say
+    ``"false"``.  Off by default (never on the reconcile path, opt-in)."""
     if gpu_request(pod_spec) <= 0:
         return False
     v = (m.annotations(nb).get(GPU_PROBE_ANNOTATION) or "").strip().lower()
-    if v in ("true", "false"):
-        return v == "true"
+    if v in ("true", "rccl", "false"):
+        return v != "false"
     return env.get("GPU_STARTUP_PROBE", "false") == "true"
 
 
-def gpu_probe_init_container(ngpu: int, env: Mapping[str, str] = os.environ) -> dict:
+def gpu_probe_rccl(nb: dict, ngpu: int, env: Mapping[str, str] = os.environ) -> bool:
+    """Whether the probe also runs its RCCL all-reduce over the pod's GPUs (SURVEY §7.0.4's
+    collective readiness check): ``amd.com/gpu-probe: "rccl"``, or ``GPU_PROBE_RCCL=true`` for
+    every probed notebook with 2+ GPUs (a single GPU has nothing to all-reduce with)."""
+    v = (m.annotations(nb).get(GPU_PROBE_ANNOTATION) or "").strip().lower()
+    return v == "rccl" or (ngpu >= 2 and env.get("GPU_PROBE_RCCL", "false") == "true")
+
+
+def gpu_probe_init_container(ngpu: int, env: Mapping[str, str] = os.environ, rccl: bool = False) -> dict:
     """Init container that proves the pod's GPUs healthy before the notebook starts.
 
     ``odh-gpu-probe`` (``ops/csrc/probe_cli.cpp``, torch-free) runs the bf16 MFMA GEMM checked
     in registers and the HBM3E pattern sweep on every GPU the device plugin gives the pod, and
-    with 2+ GPUs reads the xGMI ring between them; non-zero exit keeps the pod in Init, and its
+    with 2+ GPUs reads the xGMI ring between them (``rccl``: plus an RCCL all-reduce over all
+    of them, ``--rccl-mib``); non-zero exit keeps the pod in Init, and its
     JSON verdict is the container's termination message.  It asks for the same
     ``amd.com/gpu`` count as the notebook: the kubelet device manager hands an init
     container's devices on to the app containers, so the GPUs probed are the GPUs the
     notebook gets, and the pod's effective request (max of init and app) does not grow."""
     n = str(ngpu)
+    args = ["--json", "/dev/termination-log", "--timeout-ms", env.get("GPU_PROBE_TIMEOUT_MS") or GPU_PROBE_TIMEOUT_MS]
+    if rccl:
+        args += ["--rccl-mib", GPU_PROBE_RCCL_MIB]
     return {
         "name": GPU_PROBE_CONTAINER,
         "image": env.get("GPU_PROBE_IMAGE") or DEFAULT_GPU_PROBE_IMAGE,
         "command": ["odh-gpu-probe"],
-        "args": ["--json", "/dev/termination-log", "--timeout-ms", env.get("GPU_PROBE_TIMEOUT_MS") or GPU_PROBE_TIMEOUT_MS],
+        "args": args,
         "resources": {"limits": {GPU_RESOURCE: n, "cpu": "1", "memory": "2Gi"},
                       "requests": {GPU_RESOURCE: n, "cpu": "100m", "memory": "256Mi"}},
         "terminationMessagePolicy": "FallbackToLogsOnError",
@@ -188,7 +201,9 @@ def _gpu_probe(nb: dict, pod_spec: dict, env: Mapping[str, str]) -> None:
     inits = pod_spec.setdefault("initContainers", [])
     if any(c.get("name") == GPU_PROBE_CONTAINER for c in inits):
         return  # the user brought their own
-    inits.insert(0, gpu_probe_init_container(gpu_request(pod_spec), env))  # before any init that uses the GPU
+    n = gpu_request(pod_spec)
+    # before any init container that uses the GPU
+    inits.insert(0, gpu_probe_init_container(n, env, rccl=gpu_probe_rccl(nb, n, env)))
 
 
 def generate_statefulset(nb: dict, is_generate_name: bool, env: Mapping[str, str] = os.environ) -> dict:

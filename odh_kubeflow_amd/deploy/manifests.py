@@ -61,7 +61,9 @@ CULLER_KEYS = [lit.split("=", 1)[0] for lit in CULLER_LITERALS]
 PARAMS_ENV = "USE_ISTIO=false\nISTIO_GATEWAY=kubeflow/kubeflow-gateway\nISTIO_HOST=*\n" \
              "CLUSTER_DOMAIN=cluster.local\nADD_FSGROUP=true\nGPU_NODE_SELECTOR=false\n" \
              "GPU_SHM_SIZE_PER_GPU=\nMULTI_GPU_ENV=\n" \
-             "GPU_STARTUP_PROBE=false\n"  # opt-in per notebook (amd.com/gpu-probe) or for every GPU notebook
+             "GPU_STARTUP_PROBE=false\nGPU_PROBE_RCCL=false\n"
+# GPU_STARTUP_PROBE: the start-up probe for every GPU notebook (else opt-in per notebook,
+# amd.com/gpu-probe); GPU_PROBE_RCCL: its RCCL all-reduce for every probed multi-GPU notebook
 
 
 def params_env(version: str) -> str:

@@ -753,6 +753,21 @@ __global__ __launch_bounds__(256) void hbm_check_variant_kernel(const u32x4* __r
   if ((threadIdx.x & 63) == 0 && local) atomicAdd(err, (unsigned long long)local);
 }
 
+// every 32-bit word of buf equal to `expect` (the RCCL all-reduce result check)
+__global__ __launch_bounds__(256) void const_check_kernel(const u32x4* __restrict__ buf, size_t n, uint32_t expect,
+                                                          unsigned long long* __restrict__ err) {
+  const size_t per = ((n + gridDim.x - 1) / gridDim.x + 1023) & ~(size_t)1023;
+  const size_t lo = blockIdx.x * per;
+  const size_t hi = lo + per < n ? lo + per : n;
+  unsigned local = 0;
+  for (size_t i = lo + threadIdx.x; i < hi; i += 256) {
+    const u32x4 v = __builtin_nontemporal_load(&buf[i]);
+    local += (v.x != expect) + (v.y != expect) + (v.z != expect) + (v.w != expect);
+  }
+  for (int off = 32; off > 0; off >>= 1) local += __shfl_down(local, off, 64);
+  if ((threadIdx.x & 63) == 0 && local) atomicAdd(err, (unsigned long long)local);
+}
+
 __global__ __launch_bounds__(256) void busy_kernel(float* __restrict__ out, int iters) {
   const int lane = threadIdx.x & 63;
   bf16x8 a, b;
@@ -1069,6 +1084,13 @@ int odh_peer_enable(int dev, int peer) {
   }
   hipError_t r = hipSetDevice(cur);
   return (int)(e != hipSuccess ? e : r);
+}
+
+int odh_const_check(const void* buf, size_t bytes, uint32_t expect, unsigned long long* err, hipStream_t stream) {
+  const size_t n = bytes / 16;
+  if (n == 0 || bytes % 16) return (int)hipErrorInvalidValue;
+  const_check_kernel<<<grid_for(n, 1024), 256, 0, stream>>>((const u32x4*)buf, n, expect, err);
+  return (int)hipGetLastError();
 }
 
 int odh_busy(float* out, int blocks, int iters, hipStream_t stream) {

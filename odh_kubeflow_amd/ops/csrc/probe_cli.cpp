@@ -12,7 +12,11 @@
 //      form, mismatches attributed to the XCD that computed them) concurrently with the
 //      HBM pattern write + verify sweep on a second stream;
 //   3. with 2+ GPUs, reads every link of a ring over them through xGMI (peer access) and
-//      verifies the neighbour's pattern word for word.
+//      verifies the neighbour's pattern word for word;
+//   4. with --rccl-mib N (the `amd.com/gpu-probe: "rccl"` notebooks), an RCCL all-reduce over
+//      all of them in this one process (ncclCommInitAll; librccl is dlopen'ed only then — it
+//      is 570 MB), every element of every device's result checked on its GPU: the
+//      collective library and its xGMI transport ready for the notebook's torch.distributed.
 //
 // All devices are launched before any is waited on.  The result is one compact JSON object
 // (<4 KiB: the kubelet's termination-message limit) written to --json (default
@@ -24,7 +28,9 @@
 // pod is Ready when Jupyter answers; this program is what `amd.com/gpu-probe: "true"` adds
 // in front of the notebook container (controllers/notebook.py::_gpu_probe_init_container).
 
+#include <dlfcn.h>
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>  // types only: the library is dlopen'ed (rccl_allreduce)
 
 #include <atomic>
 #include <chrono>
@@ -48,6 +54,7 @@ int odh_probe_gemm_verify(const void* A, const void* Bt, int M, int N, int K, in
 int odh_hbm_write(void* buf, size_t bytes, uint32_t seed, int nontemporal, hipStream_t stream);
 int odh_hbm_check(const void* buf, size_t bytes, uint32_t seed, unsigned long long* err, hipStream_t stream);
 int odh_peer_enable(int dev, int peer);
+int odh_const_check(const void* buf, size_t bytes, uint32_t expect, unsigned long long* err, hipStream_t stream);
 }
 
 namespace {
@@ -62,14 +69,16 @@ struct Options {
   int M = 4096, N = 4096, K = 1024;
   size_t hbm_bytes = 256ull << 20;
   size_t xgmi_bytes = 64ull << 20;
+  size_t rccl_bytes = 0;  // 0: no RCCL step
   long timeout_ms = 30000;
   std::string json_path;  // "" = default; "-" = stdout only
-  std::string fault;      // test hook: gemm | hbm | xgmi
+  std::string fault;      // test hook: gemm | hbm | xgmi | rccl
   bool quiet = false;
 };
 
 // device counters: [0:8] workgroups per XCD, [8:16] mismatches per XCD, [16] GEMM mismatches,
-// [18:20] HBM mismatches (u64), [20:22] xGMI mismatches of the link this device reads (u64)
+// [18:20] HBM mismatches (u64), [20:22] xGMI mismatches of the link this device reads (u64),
+// [22:24] mismatches in this device's RCCL all-reduce result (u64)
 constexpr int NCOUNT = 32;
 
 struct Dev {
@@ -80,16 +89,17 @@ struct Dev {
   int host[NCOUNT] = {};
   hipStream_t sg = nullptr, sh = nullptr;
   hipEvent_t e0 = nullptr, e_gemm = nullptr, e_h0 = nullptr, e_h1 = nullptr, e_link0 = nullptr, e_link1 = nullptr;
+  hipEvent_t e_r0 = nullptr, e_r1 = nullptr;
   uint32_t seed = 0;
-  float gemm_ms = 0, hbm_ms = 0, link_ms = 0;
+  float gemm_ms = 0, hbm_ms = 0, link_ms = 0, rccl_ms = 0;
   int link_source = -1;
   std::string error;
 };
 
 int usage(const char* argv0) {
   std::fprintf(stderr,
-               "usage: %s [--json PATH|-] [--shape M,N,K] [--hbm-mib N] [--xgmi-mib N] [--timeout-ms N] "
-               "[--inject-fault gemm|hbm|xgmi] [--quiet]\n",
+               "usage: %s [--json PATH|-] [--shape M,N,K] [--hbm-mib N] [--xgmi-mib N] [--rccl-mib N] "
+               "[--timeout-ms N] [--inject-fault gemm|hbm|xgmi|rccl] [--quiet]\n",
                argv0);
   return 64;
 }
@@ -114,11 +124,13 @@ bool parse(int argc, char** argv, Options& o) {
       o.hbm_bytes = (size_t)std::strtoull(v.c_str(), nullptr, 10) << 20;
     } else if (a == "--xgmi-mib") {
       o.xgmi_bytes = (size_t)std::strtoull(v.c_str(), nullptr, 10) << 20;
+    } else if (a == "--rccl-mib") {
+      o.rccl_bytes = (size_t)std::strtoull(v.c_str(), nullptr, 10) << 20;
     } else if (a == "--timeout-ms") {
       o.timeout_ms = std::strtol(v.c_str(), nullptr, 10);
     } else if (a == "--inject-fault") {
       o.fault = v;
-      if (v != "gemm" && v != "hbm" && v != "xgmi") return false;
+      if (v != "gemm" && v != "hbm" && v != "xgmi" && v != "rccl") return false;
     } else if (a == "--quiet") {
       o.quiet = true;
     } else {
@@ -126,8 +138,10 @@ bool parse(int argc, char** argv, Options& o) {
     }
   }
   // the fused check needs 256² output tiles and K in 64-element steps
+  // the all-reduce's send and receive buffers are the two halves of the HBM buffer
   return o.M > 0 && o.N > 0 && o.K > 0 && o.M % 256 == 0 && o.N % 256 == 0 && o.K % 64 == 0 &&
-         o.hbm_bytes >= (1u << 20) && o.timeout_ms > 0;
+         o.hbm_bytes >= (1u << 20) && o.timeout_ms > 0 && 2 * o.rccl_bytes <= o.hbm_bytes &&
+         (o.fault != "rccl" || o.rccl_bytes > 0);
 }
 
 void emit(const Options& o, const std::string& json) {
@@ -186,7 +200,8 @@ bool setup(Dev& d, const Options& o) {
   HIP_TRY(hipMalloc(&d.counters, sizeof(int) * NCOUNT));
   HIP_TRY(hipStreamCreateWithFlags(&d.sg, hipStreamNonBlocking));
   HIP_TRY(hipStreamCreateWithFlags(&d.sh, hipStreamNonBlocking));
-  for (hipEvent_t* e : {&d.e0, &d.e_gemm, &d.e_h0, &d.e_h1, &d.e_link0, &d.e_link1}) HIP_TRY(hipEventCreate(e));
+  for (hipEvent_t* e : {&d.e0, &d.e_gemm, &d.e_h0, &d.e_h1, &d.e_link0, &d.e_link1, &d.e_r0, &d.e_r1})
+    HIP_TRY(hipEventCreate(e));
   HIP_TRY(hipMemsetAsync(d.counters, 0, sizeof(int) * NCOUNT, d.sg));
   HIP_TRY(odh_probe_fill(d.a, d.bt, o.M, o.N, o.K, d.sg));
   if (o.fault == "gemm") {
@@ -254,13 +269,129 @@ void release(Dev& d) {
   (void)hipSetDevice(d.index);
   for (void* p : {d.a, d.bt, d.hbm, (void*)d.tile_xcd, (void*)d.counters})
     if (p) (void)hipFree(p);
-  for (hipEvent_t e : {d.e0, d.e_gemm, d.e_h0, d.e_h1, d.e_link0, d.e_link1})
+  for (hipEvent_t e : {d.e0, d.e_gemm, d.e_h0, d.e_h1, d.e_link0, d.e_link1, d.e_r0, d.e_r1})
     if (e) (void)hipEventDestroy(e);
   if (d.sg) (void)hipStreamDestroy(d.sg);
   if (d.sh) (void)hipStreamDestroy(d.sh);
 }
 
 uint64_t u64(const int* h, int i) { return (uint64_t)(uint32_t)h[i] | ((uint64_t)(uint32_t)h[i + 1] << 32); }
+
+// RCCL, resolved at run time: only --rccl-mib pays for loading the library
+struct Rccl {
+  decltype(&ncclCommInitAll) init_all = nullptr;
+  decltype(&ncclAllReduce) all_reduce = nullptr;
+  decltype(&ncclGroupStart) group_start = nullptr;
+  decltype(&ncclGroupEnd) group_end = nullptr;
+  decltype(&ncclCommDestroy) destroy = nullptr;
+  decltype(&ncclGetErrorString) error_string = nullptr;
+
+  bool load(std::string& err) {
+    void* h = dlopen("librccl.so.1", RTLD_NOW | RTLD_LOCAL);
+    if (!h) h = dlopen("librccl.so", RTLD_NOW | RTLD_LOCAL);
+    if (!h) {
+      const char* e = dlerror();
+      err = std::string("cannot load librccl: ") + (e ? e : "?");
+      return false;
+    }
+    init_all = (decltype(init_all))dlsym(h, "ncclCommInitAll");
+    all_reduce = (decltype(all_reduce))dlsym(h, "ncclAllReduce");
+    group_start = (decltype(group_start))dlsym(h, "ncclGroupStart");
+    group_end = (decltype(group_end))dlsym(h, "ncclGroupEnd");
+    destroy = (decltype(destroy))dlsym(h, "ncclCommDestroy");
+    error_string = (decltype(error_string))dlsym(h, "ncclGetErrorString");
+    if (!init_all || !all_reduce || !group_start || !group_end || !destroy || !error_string) {
+      err = "librccl lacks the NCCL API";
+      return false;
+    }
+    return true;  // never unloaded: the process leaves through _Exit
+  }
+};
+
+struct RcclRun {
+  double init_ms = 0, wall_ms = 0;
+  size_t bytes = 0;
+};
+
+#define RCCL_TRY(expr)                                                                   \
+  do {                                                                                   \
+    const ncclResult_t r_ = (expr);                                                      \
+    if (r_ != ncclSuccess) {                                                             \
+      err = std::string(#expr) + ": " + rc.error_string(r_);                             \
+      for (ncclComm_t c : comms)                                                         \
+        if (c) (void)rc.destroy(c);                                                      \
+      return false;                                                                      \
+    }                                                                                    \
+  } while (0)
+
+// Sum-all-reduce of float32 over every device: device i contributes i+1, so every element
+// of every result must be n(n+1)/2 (exact in float).  Send / receive buffers are the two
+// halves of each device's (already checked) HBM buffer.  On return each device's mismatch
+// count sits in its counters[22:24] and host[22:24].
+bool rccl_allreduce(std::vector<Dev>& devs, const Options& o, RcclRun& run, std::string& err) {
+  Rccl rc;
+  if (!rc.load(err)) return false;
+  const int n = (int)devs.size();
+  run.bytes = o.rccl_bytes & ~(size_t)15;
+  const size_t count = run.bytes / 4;
+  std::vector<int> ids(n);
+  for (int i = 0; i < n; ++i) ids[i] = devs[i].index;
+  std::vector<ncclComm_t> comms(n, nullptr);
+  auto t0 = Clock::now();
+  RCCL_TRY(rc.init_all(comms.data(), n, ids.data()));
+  run.init_ms = ms_since(t0);
+  auto hip_fail = [&](Dev& d, const char* what, hipError_t e) {
+    err = "GPU " + std::to_string(d.index) + ": " + what + ": " + hipGetErrorString(e);
+    for (ncclComm_t c : comms) (void)rc.destroy(c);
+    return false;
+  };
+  for (int i = 0; i < n; ++i) {
+    Dev& d = devs[i];
+    float v = (float)(i + 1) + (o.fault == "rccl" && i == 0 ? 0.5f : 0.0f);
+    uint32_t bits;
+    std::memcpy(&bits, &v, 4);
+    hipError_t e = hipSetDevice(d.index);
+    if (e == hipSuccess) e = hipMemsetD32Async((hipDeviceptr_t)d.hbm, (int)bits, count, d.sg);
+    if (e == hipSuccess) e = hipMemsetAsync((char*)d.hbm + run.bytes, 0, run.bytes, d.sg);
+    if (e == hipSuccess) e = hipMemsetAsync(d.counters + 22, 0, 8, d.sg);
+    if (e == hipSuccess) e = hipEventRecord(d.e_r0, d.sg);
+    if (e != hipSuccess) return hip_fail(d, "fill", e);
+  }
+  t0 = Clock::now();
+  RCCL_TRY(rc.group_start());
+  for (int i = 0; i < n; ++i) {
+    Dev& d = devs[i];
+    const ncclResult_t r = rc.all_reduce(d.hbm, (char*)d.hbm + run.bytes, count, ncclFloat32, ncclSum, comms[i], d.sg);
+    if (r != ncclSuccess) {
+      (void)rc.group_end();
+      err = std::string("ncclAllReduce: ") + rc.error_string(r);
+      for (ncclComm_t c : comms) (void)rc.destroy(c);
+      return false;
+    }
+  }
+  RCCL_TRY(rc.group_end());
+  const float want = (float)n * (float)(n + 1) / 2.0f;
+  uint32_t want_bits;
+  std::memcpy(&want_bits, &want, 4);
+  for (Dev& d : devs) {
+    hipError_t e = hipSetDevice(d.index);
+    if (e == hipSuccess) e = hipEventRecord(d.e_r1, d.sg);
+    if (e == hipSuccess)
+      e = (hipError_t)odh_const_check((char*)d.hbm + run.bytes, run.bytes, want_bits,
+                                      (unsigned long long*)(d.counters + 22), d.sg);
+    if (e == hipSuccess) e = hipMemcpyAsync(d.host + 22, d.counters + 22, 8, hipMemcpyDeviceToHost, d.sg);
+    if (e != hipSuccess) return hip_fail(d, "check", e);
+  }
+  for (Dev& d : devs) {
+    hipError_t e = hipSetDevice(d.index);
+    if (e == hipSuccess) e = hipStreamSynchronize(d.sg);
+    if (e == hipSuccess) e = hipEventElapsedTime(&d.rccl_ms, d.e_r0, d.e_r1);
+    if (e != hipSuccess) return hip_fail(d, "sync", e);
+  }
+  run.wall_ms = ms_since(t0);
+  for (ncclComm_t c : comms) (void)rc.destroy(c);
+  return true;
+}
 
 }  // namespace
 
@@ -337,6 +468,14 @@ extern "C" int odh_probe_cli(int argc, char** argv) {
   for (Dev& d : devs)
     if (!link_finish(d)) return fail_all(d);
   const double link_ms = ndev >= 2 ? ms_since(t_link0) : 0.0;
+  RcclRun rr;
+  if (o.rccl_bytes) {
+    std::string rerr;
+    if (!rccl_allreduce(devs, o, rr, rerr)) {
+      for (Dev& x : devs) release(x);
+      return done(2, fail_json("rccl", rerr, ms_since(t_start)));
+    }
+  }
 
   const int tiles = odh_gemm_tiles(o.M, o.N, o.K);
   const double flops = 2.0 * o.M * o.N * o.K;
@@ -391,16 +530,39 @@ extern "C" int odh_probe_cli(int argc, char** argv) {
     }
   }
   links += "]";
+  std::string rccl;
+  if (o.rccl_bytes) {
+    uint64_t rerr = 0;
+    float slowest = 0;
+    for (Dev& d : devs) {
+      rerr += u64(d.host, 22);
+      slowest = d.rccl_ms > slowest ? d.rccl_ms : slowest;
+    }
+    const bool rok = rerr == 0;
+    if (!rok && first_err.empty())
+      first_err = "RCCL all-reduce over " + std::to_string(ndev) + " GPUs: " +
+                  std::to_string((unsigned long long)rerr) + " mismatches";
+    ok = ok && rok;
+    // bus bandwidth as nccl-tests define it: algbw x 2(n-1)/n
+    const double algbw = slowest > 0 ? rr.bytes / (slowest * 1e-3) / 1e9 : 0.0;
+    char b[256];
+    std::snprintf(b, sizeof b,
+                  ",\"rccl\":{\"ranks\":%d,\"ok\":%s,\"errors\":%llu,\"mib\":%zu,\"init_ms\":%.2f,"
+                  "\"allreduce_ms\":%.4f,\"busbw_gbps\":%.1f}",
+                  ndev, rok ? "true" : "false", (unsigned long long)rerr, rr.bytes >> 20, rr.init_ms, slowest,
+                  ndev > 1 ? algbw * 2.0 * (ndev - 1) / ndev : algbw);
+    rccl = b;
+  }
   for (Dev& d : devs) release(d);
   char tail[320];
   std::snprintf(tail, sizeof tail,
                 ",\"timings_ms\":{\"exec\":%.3f,\"hip_init\":%.3f,\"alloc_fill\":%.3f,\"probe\":%.3f,\"xgmi\":%.3f,"
-                "\"total\":%.3f}}",
-                t_exec, t_init, t_alloc - t_init, probe_ms, link_ms, ms_since(t_start));
+                "\"rccl\":%.3f,\"total\":%.3f}}",
+                t_exec, t_init, t_alloc - t_init, probe_ms, link_ms, rr.init_ms + rr.wall_ms, ms_since(t_start));
   std::string json = std::string("{\"ok\":") + (ok ? "true" : "false") + ",\"devices\":" + std::to_string(ndev) +
                      ",\"shape\":[" + std::to_string(o.M) + "," + std::to_string(o.N) + "," + std::to_string(o.K) +
                      "],\"hbm_mib\":" + std::to_string(o.hbm_bytes >> 20) +
                      (first_err.empty() ? "" : ",\"error\":\"" + esc(first_err) + "\"") + ",\"results\":" + res +
-                     ",\"links\":" + links + tail;
+                     ",\"links\":" + links + rccl + tail;
   return done(ok ? 0 : 1, json);
 }

@@ -76,6 +76,19 @@ def test_probe_runs_before_user_init_containers_and_user_copy_wins():
     assert _inits(nb) == [mine]
 
 
+def test_probe_rccl_mode():
+    """``amd.com/gpu-probe: "rccl"`` (or ``GPU_PROBE_RCCL=true`` for every multi-GPU notebook
+    that gets the probe) adds the RCCL all-reduce step."""
+    nb = notebook("nb", "ns", gpus=4, annotations={GPU_PROBE_ANNOTATION: "rccl"})
+    (c,) = _inits(nb)
+    assert c["args"][c["args"].index("--rccl-mib") + 1] == "64"
+    plain = notebook("nb", "ns", gpus=4, annotations={GPU_PROBE_ANNOTATION: "true"})
+    assert "--rccl-mib" not in _inits(plain)[0]["args"]
+    assert "--rccl-mib" in _inits(plain, {"GPU_PROBE_RCCL": "true"})[0]["args"]
+    one = notebook("nb", "ns", gpus=1, annotations={GPU_PROBE_ANNOTATION: "true"})
+    assert "--rccl-mib" not in _inits(one, {"GPU_PROBE_RCCL": "true"})[0]["args"]  # nothing to all-reduce over
+
+
 def test_probe_annotation_reaches_the_pod_template():
     nb = notebook("nb", "ns", gpus=1, annotations={GPU_PROBE_ANNOTATION: "true"})
     sts = generate_statefulset(nb, False, {})
@@ -247,6 +260,23 @@ def test_probe_program_fails_on_injected_fault(fault):
         assert d["gemm_errors"] == want and d["hbm_errors"] == 0 and sum(d["err_xcd"]) == want, d
     else:
         assert d["hbm_errors"] > 0 and d["gemm_errors"] == 0
+
+
+@pytest.mark.gpu
+def test_probe_program_rccl_allreduce_on_the_mi355x():
+    """``--rccl-mib``: the RCCL all-reduce over the pod's GPUs (one here: ncclCommInitAll over
+    one device, the result still checked element by element on the GPU), then an injected
+    wrong contribution that every element of the result must expose."""
+    rc, res, _wall, r = _run_probe("--rccl-mib", "16")
+    assert rc == 0, (r.stdout, r.stderr)
+    rr = res["rccl"]
+    assert rr["ok"] and rr["ranks"] == 1 and rr["errors"] == 0 and rr["mib"] == 16, rr
+    assert rr["allreduce_ms"] > 0 and res["timings_ms"]["rccl"] >= rr["init_ms"] > 0, res
+    print(f"RCCL: init {rr['init_ms']:.1f} ms, 16 MiB all-reduce {rr['allreduce_ms']:.3f} ms")
+    rc, res, _wall, r = _run_probe("--rccl-mib", "16", "--inject-fault", "rccl")
+    assert rc == probe_main.CHECK_FAILED, (r.stdout, r.stderr)
+    assert res["rccl"]["errors"] == (16 << 20) // 4 and "RCCL all-reduce" in res["error"], res
+    assert res["results"][0]["gemm_errors"] == 0 and res["results"][0]["hbm_errors"] == 0
 
 
 @pytest.mark.gpu

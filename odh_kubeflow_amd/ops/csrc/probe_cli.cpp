@@ -338,7 +338,11 @@ bool rccl_allreduce(std::vector<Dev>& devs, const Options& o, RcclRun& run, std:
   for (int i = 0; i < n; ++i) ids[i] = devs[i].index;
   std::vector<ncclComm_t> comms(n, nullptr);
   auto t0 = Clock::now();
-  RCCL_TRY(rc.init_all(comms.data(), n, ids.data()));
+  const ncclResult_t ri = rc.init_all(comms.data(), n, ids.data());
+  if (ri != ncclSuccess) {  // no communicator to destroy: a failed init leaves none usable
+    err = std::string("ncclCommInitAll: ") + rc.error_string(ri);
+    return false;
+  }
   run.init_ms = ms_since(t0);
   auto hip_fail = [&](Dev& d, const char* what, hipError_t e) {
     err = "GPU " + std::to_string(d.index) + ": " + what + ": " + hipGetErrorString(e);

@@ -107,7 +107,11 @@ PY
           || fail probeexe $? "$out/probeexe_$r.json"
         echo "run $r wall_ms $(( ($(date +%s%N) - s0) / 1000000 ))" >> "$out/probeexe_walls.txt"
       done
-      cat "$out/probeexe_walls.txt"; tail -1 "$out/probeexe_10.json" ;;
+      for r in 1 2 3; do  # with the RCCL all-reduce step (amd.com/gpu-probe: "rccl")
+        timeout -k 10 120 odh_kubeflow_amd/ops/_lib/odh-gpu-probe --json - --rccl-mib 64 \
+          > "$out/probeexe_rccl_$r.json" 2>&1 || fail probeexe $? "$out/probeexe_rccl_$r.json"
+      done
+      cat "$out/probeexe_walls.txt"; tail -1 "$out/probeexe_10.json"; tail -1 "$out/probeexe_rccl_3.json" ;;
     ranks)
       for n in 2 4; do
         timeout -k 10 170 python -m torch.distributed.run --nnodes=1 --nproc-per-node $n \

@@ -24,7 +24,7 @@ class QuantityError(ValueError):
 
 
 class Quantity:
-    __slots__ = ("value", "text", "binary")
+    __slots__ = ("value", "text", "binary", "_canon")
 
     def __init__(self, text: str):
         s = str(text).strip()
@@ -44,6 +44,7 @@ class Quantity:
                 v *= _DECIMAL[suffix]
         self.value = v
         self.text = s
+        self._canon = None
 
     def sign(self) -> int:
         return (self.value > 0) - (self.value < 0)
@@ -91,7 +92,16 @@ def parse_quantity(text) -> Quantity:
 
 
 def canonical(q: Quantity) -> str:
-    """Canonical string the apiserver would echo back (``"100m"``, ``"64Mi"``, ``"2"``)."""
+    """Canonical string the apiserver would echo back (``"100m"``, ``"64Mi"``, ``"2"``).
+    Computed once per (memoized, immutable) Quantity: the defaulting of every pod template
+    the controllers compare asks for the same few values."""
+    c = q._canon
+    if c is None:
+        c = q._canon = _canonical(q)
+    return c
+
+
+def _canonical(q: Quantity) -> str:
     v = q.value
     if v == 0:
         return "0"

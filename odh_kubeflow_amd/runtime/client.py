@@ -158,6 +158,12 @@ class CachedClient(Client):
         self._inflight: Dict[Tuple[str, str, str], tuple] = {}
         self.fresh_reads = 0
         self.cache_waits = 0
+        # live-read kinds (``uncached``: the odh manager's ConfigMaps / Secrets, whose cached
+        # copies are stripped of their data): key → (resourceVersion, full object) of the
+        # last live read or own write, reused while the stripped informer still shows that
+        # resourceVersion (see :meth:`_validated`)
+        self._full: Dict[Tuple[str, str, str], Tuple[int, dict]] = {}
+        self.validated_reads = 0
 
     def _note(self, out) -> None:
         if not isinstance(out, dict) or "metadata" not in out:
@@ -172,6 +178,8 @@ class CachedClient(Client):
         if len(self._written) > 16384:
             self._written.clear()
         self._written[key] = rv
+        if key[0] in self.uncached:
+            self._keep_full(key, rv, out)
         cur = CURRENT_RECONCILE.get()
         if cur is not None:
             if len(self._own) > 16384:
@@ -223,9 +231,67 @@ class CachedClient(Client):
         if type(kind) is str:
             self._ensured.add(kind)
 
+    FULL_CAP = 4096  # objects kept for validated reads (the few ConfigMaps a manager reads)
+
+    def _keep_full(self, key: Tuple[str, str, str], rv: int, obj: dict) -> None:
+        if len(self._full) >= self.FULL_CAP:
+            self._full.pop(next(iter(self._full)))  # oldest first
+        self._full[key] = (rv, deepcopy_json(obj))
+
+    def _validated(self, kind, name: str, namespace: Optional[str]) -> Optional[dict]:
+        """A live-read kind's object without the read, when it provably has not changed.
+
+        The reference reads ConfigMaps and Secrets live (``DisableFor``) because its cache
+        strips their data (``odh/main.go:81-101,165-185``) — and so does this one.  But the
+        stripped informer still carries each object's resourceVersion: when it equals the
+        version of the copy this client last read or wrote, the data is that copy's.  So a
+        read costs a round trip only after the object changed (or before the informer has
+        it) — the unsharded odh manager re-read ``pipeline-runtime-images`` and the CA
+        bundles live 16+ times per notebook, mostly to learn they do not exist.  An object
+        the synced informer does not hold is NotFound without a read, unless this client
+        wrote it.  Freshness is the informer's, as for every other cached read; this client's
+        own newer writes always win (``_written``)."""
+        info = SCHEME.resolve(kind)
+        key = (info.key, namespace or "", name)
+        watching = getattr(self.reader, "watching", None)
+        if watching is None or not watching(kind, namespace):
+            return None
+        o = self.reader.get(kind, name, namespace)
+        if o is None:
+            if key in self._written:
+                return None  # written here and not yet in the cache: read through
+            # absent from a synced informer: NotFound, as a cached read would say (the
+            # optional bundles — odh-trusted-ca-bundle, pipeline-runtime-images — usually are)
+            from ..models.errors import NotFound
+
+            self.validated_reads += 1
+            raise NotFound(info.plural if not info.group else f"{info.plural}.{info.group}", name)
+        ent = self._full.get(key)
+        if ent is None or _rv_int(o) != ent[0]:
+            return None
+        want = self._written.get(key)
+        if want is not None and want > ent[0]:
+            return None
+        self.validated_reads += 1
+        out = deepcopy_json(ent[1])
+        v = _version_of(kind)
+        if v:
+            out["apiVersion"] = info.api_version(v)
+        return out
+
     async def get(self, kind, name, namespace=None):
         if self._live(kind, namespace) or LIVE_READS.get():
-            return await self.writer.get(kind, name, namespace)
+            uncached = SCHEME.resolve(kind).key in self.uncached
+            if uncached and not LIVE_READS.get():
+                hit = self._validated(kind, name, namespace)
+                if hit is not None:
+                    return hit
+            o = await self.writer.get(kind, name, namespace)
+            if uncached:
+                rv = _rv_int(o)
+                if rv is not None:
+                    self._keep_full((SCHEME.resolve(kind).key, namespace or "", name), rv, o)
+            return o
         await self._ensure(kind)
         o = self.reader.get(kind, name, namespace)
         if self._written:

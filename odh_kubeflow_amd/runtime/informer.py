@@ -355,6 +355,23 @@ class InformerCache(Reader, EventSource):
             return [inf] if inf is not None else []
         return g.all()
 
+    def watching(self, kind, namespace: Optional[str]) -> bool:
+        """Whether a synced informer already holds ``kind`` in ``namespace`` — without
+        starting one (CachedClient's resourceVersion-validated reads of live-read kinds)."""
+        try:
+            info = SCHEME.resolve(kind)
+        except KeyError:
+            return False
+        g = self._groups.get(info.key)
+        if g is None:
+            return False
+        if namespace and info.namespaced and self.namespaces is not None:
+            inf = g.infs.get(namespace)
+            infs = [inf] if inf is not None else []
+        else:
+            infs = g.all()
+        return bool(infs) and all(i.synced.is_set() and not i.missing_kind for i in infs)
+
     def informer(self, kind) -> _Informer:
         """The (first) informer of ``kind`` — for single-namespace / cluster-wide caches."""
         return self._group(kind).all()[0]

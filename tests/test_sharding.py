@@ -419,6 +419,54 @@ def test_informer_namespace_filter_follows_objects(run, server_kind):
     run(go())
 
 
+def test_live_read_kinds_are_read_once_per_version(run, server_kind):
+    """ConfigMaps read live (the odh manager's ``DisableFor``, cached stripped of their data):
+    a second read of an unchanged object costs no request — the stripped informer vouches
+    for its resourceVersion — a changed one is read again, an absent one is NotFound
+    without a read, and this client's own write is read back through until the informer
+    has it."""
+    from odh_kubeflow_amd.models.errors import NotFound
+    from odh_kubeflow_amd.runtime.informer import strip_data
+
+    async def go():
+        srv, c = await _server(server_kind)
+        try:
+            await c.create({"apiVersion": "v1", "kind": "Namespace", "metadata": {"name": "a"}})
+            await c.create(_cm("x", "a"))
+            cache = InformerCache(c, transforms={kinds.CONFIG_MAP: strip_data})
+            client = CachedClient(cache, c, uncached=[kinds.CONFIG_MAP])
+            await cache.wait_synced([kinds.CONFIG_MAP])
+            assert "data" not in cache.get(kinds.CONFIG_MAP, "x", "a")  # the cache holds no payloads
+            n0 = c.requests
+            assert (await client.get(kinds.CONFIG_MAP, "x", "a"))["data"] == {"k": "x"}
+            assert c.requests == n0 + 1
+            for _ in range(3):
+                got = await client.get(kinds.CONFIG_MAP, "x", "a")
+                assert got["data"] == {"k": "x"}
+                got["data"]["k"] = "mutated by the caller"  # callers own their copy
+            assert c.requests == n0 + 1 and client.validated_reads == 3
+            # changed by someone else: once the informer shows the new version, read again
+            cur = await c.get(kinds.CONFIG_MAP, "x", "a")
+            cur["data"] = {"k": "new"}
+            new_rv = (await c.update(cur))["metadata"]["resourceVersion"]
+            assert await _wait(lambda: m.resource_version(cache.get(kinds.CONFIG_MAP, "x", "a")) == new_rv)
+            n1 = c.requests
+            assert (await client.get(kinds.CONFIG_MAP, "x", "a"))["data"] == {"k": "new"}
+            assert c.requests == n1 + 1
+            # absent from the synced informer: NotFound, no request
+            with pytest.raises(NotFound):
+                await client.get(kinds.CONFIG_MAP, "missing", "a")
+            assert c.requests == n1 + 1
+            # this client's own create: served from its response, never a stale NotFound
+            await client.create(_cm("mine", "a"))
+            assert (await client.get(kinds.CONFIG_MAP, "mine", "a"))["data"] == {"k": "mine"}
+            await cache.stop()
+        finally:
+            await c.close()
+            await srv.stop()
+    run(go())
+
+
 def test_namespace_shard_assigner(run):
     from odh_kubeflow_amd.controllers.sharding import NamespaceShardAssigner, shard_for
     from odh_kubeflow_amd.runtime.manager import Manager

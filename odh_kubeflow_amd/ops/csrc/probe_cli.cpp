@@ -309,7 +309,7 @@ struct Rccl {
 };
 
 struct RcclRun {
-  double init_ms = 0, wall_ms = 0;
+  double load_ms = 0, init_ms = 0, wall_ms = 0;  // dlopen (the library is 570 MB), ncclCommInitAll, the collective
   size_t bytes = 0;
 };
 
@@ -330,7 +330,9 @@ struct RcclRun {
 // count sits in its counters[22:24] and host[22:24].
 bool rccl_allreduce(std::vector<Dev>& devs, const Options& o, RcclRun& run, std::string& err) {
   Rccl rc;
+  const auto t_load = Clock::now();
   if (!rc.load(err)) return false;
+  run.load_ms = ms_since(t_load);
   const int n = (int)devs.size();
   run.bytes = o.rccl_bytes & ~(size_t)15;
   const size_t count = run.bytes / 4;
@@ -551,9 +553,9 @@ extern "C" int odh_probe_cli(int argc, char** argv) {
     const double algbw = slowest > 0 ? rr.bytes / (slowest * 1e-3) / 1e9 : 0.0;
     char b[256];
     std::snprintf(b, sizeof b,
-                  ",\"rccl\":{\"ranks\":%d,\"ok\":%s,\"errors\":%llu,\"mib\":%zu,\"init_ms\":%.2f,"
+                  ",\"rccl\":{\"ranks\":%d,\"ok\":%s,\"errors\":%llu,\"mib\":%zu,\"load_ms\":%.2f,\"init_ms\":%.2f,"
                   "\"allreduce_ms\":%.4f,\"busbw_gbps\":%.1f}",
-                  ndev, rok ? "true" : "false", (unsigned long long)rerr, rr.bytes >> 20, rr.init_ms, slowest,
+                  ndev, rok ? "true" : "false", (unsigned long long)rerr, rr.bytes >> 20, rr.load_ms, rr.init_ms, slowest,
                   ndev > 1 ? algbw * 2.0 * (ndev - 1) / ndev : algbw);
     rccl = b;
   }
@@ -562,7 +564,8 @@ extern "C" int odh_probe_cli(int argc, char** argv) {
   std::snprintf(tail, sizeof tail,
                 ",\"timings_ms\":{\"exec\":%.3f,\"hip_init\":%.3f,\"alloc_fill\":%.3f,\"probe\":%.3f,\"xgmi\":%.3f,"
                 "\"rccl\":%.3f,\"total\":%.3f}}",
-                t_exec, t_init, t_alloc - t_init, probe_ms, link_ms, rr.init_ms + rr.wall_ms, ms_since(t_start));
+                t_exec, t_init, t_alloc - t_init, probe_ms, link_ms, rr.load_ms + rr.init_ms + rr.wall_ms,
+                ms_since(t_start));
   std::string json = std::string("{\"ok\":") + (ok ? "true" : "false") + ",\"devices\":" + std::to_string(ndev) +
                      ",\"shape\":[" + std::to_string(o.M) + "," + std::to_string(o.N) + "," + std::to_string(o.K) +
                      "],\"hbm_mib\":" + std::to_string(o.hbm_bytes >> 20) +

@@ -62,6 +62,9 @@ def parse(argv=None):
                         "(envtest-style); auto: sharded, plus the in-process figure as a secondary field at N=1")
     p.add_argument("--no-inprocess-baseline", action="store_true",
                    help="N=1 auto: skip the extra in-process (envtest-style) measurement")
+    p.add_argument("--single-process-shard", action="store_true",
+                   help="sharded: each shard as ONE control-plane process (kf + odh + webhook) instead of the "
+                        "deployed kf / odh+webhook pair (A/B measurements)")
     p.add_argument("--json-out", default=None)
     return p.parse_args(argv)
 

@@ -14,7 +14,12 @@ cluster's notebooks with constant per-shard watch traffic.  The ``mi355x-sharded
 overlay runs it as a StatefulSet (``--shard=ordinal``: replica k is shard k, one per
 MI355X of an 8-GPU node) with one MutatingWebhookConfiguration and Service per shard;
 the headline benchmark (``bench.py`` → ``parallel/bench_dist.py``) launches exactly
-this command, one per rank.
+these processes, per rank.  A shard's pod runs the command twice, split by
+``--controllers``: ``kf`` (notebook reconciler, event re-emitter, culler, namespace
+assigner) and ``odh,webhook`` — two event loops, so the odh pipeline and admissions never
+queue behind the kf reconciles on one core (measured at N=1 on one box, interleaved: the
+two-process layout 252/268/257 notebooks/s vs 240/253/241 for one process,
+``profiles/r3_p13``).  Each set has its own leader-election lease.
 
 Flags are the union of the two reference managers' (odh spellings:
 ``--metrics-bind-address``, ``--health-probe-bind-address``, ``--leader-elect``,
@@ -108,13 +113,15 @@ def build(args, env=os.environ):
         uncached = (kinds.CONFIG_MAP, kinds.SECRET)
         transforms = {kinds.CONFIG_MAP: strip_data, kinds.SECRET: strip_data}
     elector = None
+    # a subset of the controllers (a shard pod's kf / odh containers) leads on its own lease
+    subset = "" if set(args.controller_set) == set(ALL_CONTROLLERS) else "-" + "-".join(sorted(args.controller_set))
     if args.leader_elect:
-        lease = "notebook-control-plane" + (f"-shard-{shard}" if shard is not None else "")
+        lease = "notebook-control-plane" + (f"-shard-{shard}" if shard is not None else "") + subset
         elector = LeaderElector(RestClient(cfg), lease, args.leader_election_namespace or namespace,
                                 lease_duration=args.leader_election_lease_duration,
                                 renew_deadline=args.leader_election_renew_deadline,
                                 retry_period=args.leader_election_retry_period)
-    name = "notebook-control-plane" + (f"-shard-{shard}" if shard is not None else "")
+    name = "notebook-control-plane" + (f"-shard-{shard}" if shard is not None else "") + subset
     mgr = Manager.remote(cfg, name=name, uncached=uncached, transforms=transforms,
                          cache_options=shard_cache_options(shard, namespace),
                          default_max_concurrent=args.max_concurrent_reconciles, leader_elector=elector,

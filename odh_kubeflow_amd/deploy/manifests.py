@@ -461,11 +461,28 @@ def control_plane_role() -> dict:
 
 
 def control_plane_statefulset(shards: int) -> dict:
-    c = {"name": "manager", "image": MANAGER_IMAGE,
+    """One replica per shard; its pod runs ``cmd/control_plane.py`` twice, split by
+    ``--controllers``: ``kf`` (+ the namespace assigner) and ``odh,webhook`` — two event loops,
+    so admissions and the odh pipeline never wait behind kf reconciles (cmd/control_plane.py)."""
+    common = ["--shard=ordinal", "--leader-elect", "--kube-rbac-proxy-image=$(KUBE_RBAC_PROXY_IMAGE)"]
+    kf = _control_plane_container("manager-kf", common + ["--controllers=kf", f"--shard-count={shards}",
+                                                          "--assign-namespaces"], 8080, 8081, webhook=False)
+    odh = _control_plane_container("manager-odh", common + [
+        "--controllers=odh,webhook", "--metrics-bind-address=:8082", "--health-probe-bind-address=:8083",
+        "--webhook-cert-dir=/tmp/k8s-webhook-server/serving-certs", "--webhook-port=8443"], 8082, 8083, webhook=True)
+    labels = {"app": "notebook-control-plane"}
+    return {"apiVersion": "apps/v1", "kind": "StatefulSet", "metadata": {"name": "control-plane", "labels": labels},
+            "spec": {"replicas": shards, "serviceName": "control-plane", "podManagementPolicy": "Parallel",
+                     "selector": {"matchLabels": labels},
+                     "template": {"metadata": {"labels": labels},
+                                  "spec": {"serviceAccountName": "control-plane", "containers": [kf, odh],
+                                           "volumes": [_cert_volume(), _agent_token_volume()]}}}}
+
+
+def _control_plane_container(name: str, args: list, metrics: int, probes: int, webhook: bool) -> dict:
+    c = {"name": name, "image": MANAGER_IMAGE,
          "command": ["python", "-m", "odh_kubeflow_amd.cmd.control_plane"],
-         "args": ["--shard=ordinal", f"--shard-count={shards}", "--assign-namespaces", "--leader-elect",
-                  "--kube-rbac-proxy-image=$(KUBE_RBAC_PROXY_IMAGE)",
-                  "--webhook-cert-dir=/tmp/k8s-webhook-server/serving-certs", "--webhook-port=8443"],
+         "args": args,
          "envFrom": [{"configMapRef": {"name": "config"}}],
          "env": [{"name": "POD_NAME", "valueFrom": {"fieldRef": {"fieldPath": "metadata.name"}}},
                  {"name": "K8S_NAMESPACE", "valueFrom": {"fieldRef": {"fieldPath": "metadata.namespace"}}},
@@ -474,19 +491,15 @@ def control_plane_statefulset(shards: int) -> dict:
                  {"name": "INJECT_CLUSTER_PROXY_ENV", "valueFrom": {"configMapKeyRef": {
                      "name": "notebook-controller-setting-config", "key": "INJECT_CLUSTER_PROXY_ENV",
                      "optional": True}}}] + _culler_env(),
-         "ports": [{"name": "webhook", "containerPort": 8443}, {"name": "metrics", "containerPort": 8080},
-                   {"name": "probes", "containerPort": 8081}],
+         "ports": ([{"name": "webhook", "containerPort": 8443}] if webhook else []) + [
+             {"name": "metrics" if not webhook else "metrics-odh", "containerPort": metrics},
+             {"name": "probes" if not webhook else "probes-odh", "containerPort": probes}],
          "resources": {"requests": {"cpu": "500m", "memory": "256Mi"}, "limits": {"cpu": "2", "memory": "2Gi"}},
-         "volumeMounts": [{"name": "cert", "mountPath": "/tmp/k8s-webhook-server/serving-certs", "readOnly": True},
-                          dict(AGENT_TOKEN_MOUNT_SPEC)],
-         "securityContext": dict(RESTRICTED), **_probes()}
-    labels = {"app": "notebook-control-plane"}
-    return {"apiVersion": "apps/v1", "kind": "StatefulSet", "metadata": {"name": "control-plane", "labels": labels},
-            "spec": {"replicas": shards, "serviceName": "control-plane", "podManagementPolicy": "Parallel",
-                     "selector": {"matchLabels": labels},
-                     "template": {"metadata": {"labels": labels},
-                                  "spec": {"serviceAccountName": "control-plane", "containers": [c],
-                                           "volumes": [_cert_volume(), _agent_token_volume()]}}}}
+         # the kf container reads the node agents' token (GPU-busy culling); the odh one serves the webhook
+         "volumeMounts": ([{"name": "cert", "mountPath": "/tmp/k8s-webhook-server/serving-certs", "readOnly": True}]
+                          if webhook else [dict(AGENT_TOKEN_MOUNT_SPEC)]),
+         "securityContext": dict(RESTRICTED), **_probes(probes)}
+    return c
 
 
 def _webhook_svc(name: str, selector: dict) -> dict:
@@ -527,7 +540,8 @@ def control_plane_docs(shards: int, prefix: str = NAME_PREFIX) -> Dict[str, obje
         "statefulset.yaml": control_plane_statefulset(shards),
         "services.yaml": [{"apiVersion": "v1", "kind": "Service", "metadata": {"name": "control-plane"},
                            "spec": {"clusterIP": "None", "selector": {"app": "notebook-control-plane"},
-                                    "ports": [{"name": "metrics", "port": 8080, "targetPort": 8080}]}}] + svcs,
+                                    "ports": [{"name": "metrics", "port": 8080, "targetPort": 8080},
+                                              {"name": "metrics-odh", "port": 8082, "targetPort": 8082}]}}] + svcs,
         "webhooks.yaml": mwcs,
     }
 

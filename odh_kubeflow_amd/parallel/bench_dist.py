@@ -115,11 +115,16 @@ def measure(args) -> Optional[dict]:
 
         out = report(args, world, res)
         arch = args.arch if args.arch in ("sharded", "unsharded") else "sharded"
-        if arch == "sharded":
+        if arch == "sharded" and getattr(args, "single_process_shard", False):
             out["config"]["parallelism"] = (f"namespace-sharded control plane x{world}: one `cmd/control_plane.py "
-                                            f"--shard r` process per MI355X rank (kf + odh reconcilers + odh webhook), "
-                                            f"as config/overlays/mi355x-sharded deploys it")
-            out["config"]["architecture"] = "cmd/control_plane --shard (overlay mi355x-sharded)"
+                                            f"--shard r` process per MI355X rank (kf + odh reconcilers + odh webhook); "
+                                            f"A/B variant of config/overlays/mi355x-sharded")
+            out["config"]["architecture"] = "cmd/control_plane --shard, one process per shard (A/B variant)"
+        elif arch == "sharded":
+            out["config"]["parallelism"] = (f"namespace-sharded control plane x{world}: per MI355X rank the shard pod "
+                                            f"of config/overlays/mi355x-sharded, `cmd/control_plane.py --shard r` as a "
+                                            f"kf process and an odh reconciler + odh webhook process")
+            out["config"]["architecture"] = "cmd/control_plane --shard r --controllers kf | odh,webhook (overlay mi355x-sharded)"
         else:
             out["config"]["parallelism"] = (f"one kf manager + one odh manager process for all {world} ranks' "
                                             f"notebooks, as config/overlays/mi355x deploys them")
@@ -286,7 +291,8 @@ async def _main(args, dist, torch, rank: int, world: int, ndev: int, probe_sampl
     shard = ControlPlaneShard(ShardConfig(
         apiserver_url=url[0], namespace=bench_namespace(rank), shard=str(rank), arch=arch,
         launch=(arch == "sharded" or rank == 0), bootstrap=(rank == 0), odh=not args.no_odh,
-        webhook=not args.no_odh, reference_emulation=args.reference_emulation, env=env, process=True))
+        webhook=not args.no_odh, reference_emulation=args.reference_emulation, env=env, process=True,
+        split=not getattr(args, "single_process_shard", False)))
     if rank == 0:
         await shard.start()  # cluster namespaces (and, unsharded, the managers + their webhook) first
         await _in_thread(dist.barrier)

@@ -4,11 +4,13 @@ The reference runs one notebook-controller and one odh-notebook-controller repli
 whole cluster (``kf/main.go:87-98``, ``odh/main.go:155-192``; one worker each).  Two
 deployable topologies are measured, both exactly as the manifests run them:
 
-* ``arch="sharded"`` (``config/overlays/mi355x-sharded``) — every rank r starts
-  ``python -m odh_kubeflow_amd.cmd.control_plane --shard r`` (kf reconciler + event
-  re-emitter, odh reconciler and the odh mutating webhook, one informer cache over the
-  namespaces labelled ``notebooks.amd.com/shard=r``), registered by its shard's
-  MutatingWebhookConfiguration with a ``namespaceSelector`` on that label;
+* ``arch="sharded"`` (``config/overlays/mi355x-sharded``) — every rank r starts its shard
+  pod's two processes, ``python -m odh_kubeflow_amd.cmd.control_plane --shard r
+  --controllers kf`` (kf reconciler + event re-emitter) and ``… --controllers odh,webhook``
+  (odh reconciler and the odh mutating webhook), each with an informer cache over the
+  namespaces labelled ``notebooks.amd.com/shard=r``, the webhook registered by its shard's
+  MutatingWebhookConfiguration with a ``namespaceSelector`` on that label (``split=False``:
+  one process with all three);
 * ``arch="unsharded"`` (``config/overlays/mi355x``, the reference's two-process layout) —
   rank 0 starts ``cmd/kf_manager.py`` and ``cmd/odh_manager.py`` (+ its webhook, one MWC for
   every namespace); the other ranks only drive notebooks into them.
@@ -60,6 +62,7 @@ class ShardConfig:
     env: Dict[str, str] = field(default_factory=dict)
     kube_rbac_proxy_image: str = "quay.io/brancz/kube-rbac-proxy:v0.18.1"
     process: bool = False  # run the control plane as its own process(es), as deployed
+    split: bool = True  # sharded, process mode: kf and odh + webhook as two processes (the shard pod's two containers)
 
 
 class _Proc:
@@ -90,17 +93,29 @@ class ControlPlaneShard:
         return ["--master", self.cfg.apiserver_url, "--max-concurrent-reconciles", str(self.cfg.max_concurrent),
                 "--enable-debug-endpoints"]
 
-    def _specs(self, webhook_port: int):
+    def _specs(self, webhook_port: int, split: Optional[bool] = None):
         """(name, module, argv, metrics flag) of the processes this rank launches."""
         cfg = self.cfg
         wh = ["--kube-rbac-proxy-image", cfg.kube_rbac_proxy_image, "--webhook-cert-dir", self._certs.cert_dir,
               "--webhook-host", "127.0.0.1", "--webhook-port", str(webhook_port)]
         if cfg.arch == "sharded":
-            ctrls = ["kf"] + (["odh"] if cfg.odh else []) + (["webhook"] if cfg.odh and cfg.webhook else [])
-            a = ["--shard", self.shard, "--controllers", ",".join(ctrls), *wh, "--health-probe-bind-address", "0"]
-            if cfg.reference_emulation:
-                a.append("--reference-emulation")
-            return [("control_plane", "odh_kubeflow_amd.cmd.control_plane", a, "--metrics-bind-address")]
+            # the shard pod of config/overlays/mi355x-sharded: the control plane split into a
+            # kf process and an odh + webhook process (cmd/control_plane.py docstring)
+            sets = [["kf"]]
+            if cfg.odh:
+                sets.append(["odh"] + (["webhook"] if cfg.webhook else []))
+            if not (cfg.split if split is None else split):
+                sets = [[c for cs in sets for c in cs]]
+            out = []
+            for cs in sets:
+                a = ["--shard", self.shard, "--controllers", ",".join(cs), "--health-probe-bind-address", "0"]
+                if "odh" in cs or "webhook" in cs:
+                    a += wh
+                if cfg.reference_emulation:
+                    a.append("--reference-emulation")
+                name = "control_plane" if len(sets) == 1 else f"control_plane_{cs[0]}"
+                out.append((name, "odh_kubeflow_amd.cmd.control_plane", a, "--metrics-bind-address"))
+            return out
         out = [("kf_manager", "odh_kubeflow_amd.cmd.kf_manager", ["--probe-addr", "0"], "--metrics-addr")]
         if cfg.odh:
             out.append(("odh_manager", "odh_kubeflow_amd.cmd.odh_manager", [*wh, "--health-probe-bind-address", "0"],
@@ -157,7 +172,7 @@ class ControlPlaneShard:
         if cfg.arch == "sharded":
             from ..cmd import control_plane
 
-            (_name, _mod, argv, mflag), = self._specs(0)
+            (_name, _mod, argv, mflag), = self._specs(0, split=False)  # one manager: tests read its cache
             args = control_plane.parse([*self._common_flags(), mflag, "0", *argv])
             mgrs = [control_plane.build(args, self._cp_env())]
             self.control_plane = mgrs[0]

@@ -245,8 +245,15 @@ def test_sharded_overlay_shape():
     (sts,) = _by(objs, "StatefulSet").values()
     n = sts["spec"]["replicas"]
     assert n == manifests.SHARDS == 8
-    args = sts["spec"]["template"]["spec"]["containers"][0]["args"]
-    assert "--shard=ordinal" in args and f"--shard-count={n}" in args and "--assign-namespaces" in args
+    # the shard pod: the control plane split into a kf and an odh + webhook process
+    kf, odh = sts["spec"]["template"]["spec"]["containers"]
+    assert "--shard=ordinal" in kf["args"] and f"--shard-count={n}" in kf["args"] and "--assign-namespaces" in kf["args"]
+    assert "--controllers=kf" in kf["args"] and "--controllers=odh,webhook" in odh["args"]
+    assert "--shard=ordinal" in odh["args"] and "--assign-namespaces" not in odh["args"]
+    assert [p["containerPort"] for p in odh["ports"]] == [8443, 8082, 8083]
+    assert [p["containerPort"] for p in kf["ports"]] == [8080, 8081]
+    assert odh["readinessProbe"]["httpGet"]["port"] == 8083 and kf["readinessProbe"]["httpGet"]["port"] == 8081
+    assert [v["name"] for v in odh["volumeMounts"]] == ["cert"]
     svcs = _by(objs, "Service")
     mwcs = _by(objs, "MutatingWebhookConfiguration")
     assert len(mwcs) == n + 1

@@ -9,7 +9,7 @@
 #   bench    bench.py at N=1: the driver's invocation (--steps 20 --warmup 5) twice, then 300 steps
 #   ranks    2/4-rank rehearsal of the N>1 launch on the one GPU (never 8: the driver owns N=8)
 #   unsharded  the default topology (one kf + one odh manager process) at 1, 2 and 4 ranks
-#   archab   interleaved A/B at N=1: sharded (one control-plane process) vs unsharded (two)
+#   archab   interleaved A/B at N=1: shard as kf/odh process pair vs one process vs unsharded
 #   probeexe the odh-gpu-probe init-container program: 10 process runs (wall time, verdict)
 #   hipinit  where a fresh process's HIP start-up goes, under ROCm runtime settings (tools/hip_init_ab.sh)
 #   hipexit  where a GPU process's exit goes: what it holds when it leaves (tools/hip_exit_ab.py)
@@ -75,11 +75,12 @@ for s in $steps; do
         show "$out/bench_unsharded_n$n.log" "unsharded n$n"
       done ;;
     archab)
-      # interleaved A/B at N=1: the sharded control plane (one process: kf + odh + webhook)
-      # vs the reference's two-process layout (kf manager + odh manager)
+      # interleaved A/B at N=1: the shard pod's kf / odh+webhook process pair (deployed), one
+      # process per shard, and the reference's two-process layout (kf manager + odh manager)
       for r in 1 2 3; do
-        for a in sharded unsharded; do
-          timeout -k 10 170 python bench.py --gpus 1 --arch $a --steps 300 --warmup 5 --probe-sample 0 \
+        for a in sharded single unsharded; do
+          case $a in single) flags="--arch sharded --single-process-shard" ;; *) flags="--arch $a" ;; esac
+          timeout -k 10 170 python bench.py --gpus 1 $flags --steps 300 --warmup 5 --probe-sample 0 \
             --no-inprocess-baseline > "$out/bench_ab_${a}_r$r.log" 2>&1 || fail archab $? "$out/bench_ab_${a}_r$r.log"
           show "$out/bench_ab_${a}_r$r.log" "$a r$r"
         done

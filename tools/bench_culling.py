@@ -10,9 +10,10 @@ an idle Jupyter kernel throughout, so the reference (Jupyter only,
   with the signal it rested on (``amdgpu: idle <busy%>`` = an attributed GPU sample);
   reclaim latency = from the moment a notebook became cullable (``last-activity`` +
   ``CULL_IDLE_TIME``) to its StatefulSet at 0 replicas and its pod gone;
-* **load phase** — the notebooks are resumed (STOP annotation removed, as a user does) and a
-  real MFMA load runs on the GPU: no notebook may be culled (false culls) although every
-  Jupyter kernel is idle; after the load stops, each is culled on the idle GPU signal again.
+* **load phase** — a real MFMA load runs on the GPU and the notebooks are resumed (STOP
+  annotation removed, as a user does): no notebook may be culled (false culls) although
+  every Jupyter kernel is idle; after the load stops, each is culled on the idle GPU signal
+  again.
 
 Attribution is the production path: the node agent (``nodeagent/``) resolves each pod's GPUs
 from the kubelet stand-in's device-plugin checkpoint (PCI addresses) and samples them from
@@ -156,13 +157,15 @@ async def run(args) -> dict:
             idle_lat = {nm: (stopped_at[nm] - cullable) * 1e3 for nm in names}
             idle_sig = signals_of(n_log)
 
-            # ---- load phase: resume, load the GPU(s): no culls; unload: culled again
+            # ---- load phase: the GPU(s) busy, the notebooks resumed: no culls; unload: culled
+            # again.  The load starts first, as a user's job outlives a restart: otherwise the
+            # first notebooks back could pass CULL_IDLE_TIME while the last ones still start.
             stopped_at.clear()
+            load.start()
             for nm in names:
                 await cl.admin.patch(kinds.NOTEBOOK, {"metadata": {"annotations": {STOP_ANNOTATION: None}}},
                                      name=nm, namespace="cull")
             await ready_with_idle_kernels()
-            load.start()
             t_load = time.time()
             while time.time() - t_load < args.load_s:
                 poll()

@@ -46,11 +46,10 @@ async def start_child(module: str, args: List[str], what: str, timeout: float = 
     ``ready`` line."""
     if env is None:
         env = dict(os.environ, PYTHONPATH=ROOT + os.pathsep + os.environ.get("PYTHONPATH", ""))
-    from ..utils.procutil import die_with_parent
+    from ..utils.procutil import child_env
 
-    proc = subprocess.Popen([sys.executable, *python_args, "-m", module, *args], cwd=ROOT, env=env,
-                            stdout=subprocess.PIPE, stderr=subprocess.DEVNULL, text=True,
-                            preexec_fn=die_with_parent)
+    proc = subprocess.Popen([sys.executable, *python_args, "-m", module, *args], cwd=ROOT, env=child_env(env),
+                            stdout=subprocess.PIPE, stderr=subprocess.DEVNULL, text=True)
     try:
         line = await asyncio.wait_for(_in_thread(proc.stdout.readline), timeout)
     except asyncio.TimeoutError:

@@ -66,7 +66,7 @@ class NativeApiServer:
         self._cfg_path: Optional[str] = None
 
     async def start(self) -> "NativeApiServer":
-        from ...utils.procutil import die_with_parent
+        from ...utils.procutil import child_env
 
         if self.binary == BINARY and not available():
             from ...ops.build import build
@@ -77,8 +77,7 @@ class NativeApiServer:
             json.dump(self.cfg, f)
         self.proc = await asyncio.create_subprocess_exec(
             self.binary, "--config", self._cfg_path, "--host", self.host, "--port", str(self.port),
-            stdout=asyncio.subprocess.PIPE, env={**os.environ, **self.env} if self.env else None,
-            preexec_fn=die_with_parent)
+            stdout=asyncio.subprocess.PIPE, env=child_env({**os.environ, **(self.env or {})}))
         line = await asyncio.wait_for(self.proc.stdout.readline(), 30)
         if not line.startswith(b"LISTENING"):
             raise RuntimeError(f"native apiserver failed to start: {line!r}")

@@ -63,7 +63,7 @@ class ProcessContainerRuntime(ContainerRuntime):
     async def start(self, pod: dict, devices: Sequence[int]) -> ContainerHandle:
         import aiohttp
 
-        from ...utils.procutil import die_with_parent
+        from ...utils.procutil import child_env
 
         env = self._container_env(pod, devices)
         prefix = env.get("NB_PREFIX") or f"/notebook/{m.namespace(pod)}/{m.labels(pod).get('notebook-name', m.name(pod))}"
@@ -71,8 +71,7 @@ class ProcessContainerRuntime(ContainerRuntime):
         proc = await asyncio.create_subprocess_exec(
             sys.executable, "-m", "odh_kubeflow_amd.testing.notebook_server.workbench", "--prefix", prefix,
             "--host", self.host, "--matmul", str(self.matmul if devices else 0),
-            env=env, cwd=ROOT, stdout=asyncio.subprocess.PIPE, stderr=asyncio.subprocess.DEVNULL,
-            preexec_fn=die_with_parent)
+            env=child_env(env), cwd=ROOT, stdout=asyncio.subprocess.PIPE, stderr=asyncio.subprocess.DEVNULL)
         key = m.key(pod)
         self.procs[key] = proc
         try:

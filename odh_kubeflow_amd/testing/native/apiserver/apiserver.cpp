@@ -41,6 +41,7 @@
 #include <openssl/x509v3.h>
 #include <poll.h>
 #include <signal.h>
+#include <sys/prctl.h>
 #include <sys/socket.h>
 #include <unistd.h>
 
@@ -2936,6 +2937,12 @@ void load_config(const std::string& path) {
 }  // namespace
 
 int main(int argc, char** argv) {
+  // started by the benchmark / test platform (utils/procutil.py): die with the launcher
+  if (const char* parent = std::getenv("ODH_PDEATHSIG_PARENT")) {
+    prctl(PR_SET_PDEATHSIG, SIGTERM);
+    if (std::to_string(getppid()) != parent) raise(SIGTERM);  // it died before we armed
+    unsetenv("ODH_PDEATHSIG_PARENT");
+  }
   std::string host = "127.0.0.1", config;
   int port = 0;
   for (int k = 1; k < argc; ++k) {

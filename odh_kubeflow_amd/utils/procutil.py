@@ -1,22 +1,47 @@
-"""Child-process hygiene for the processes the benchmark and the test platform launch."""
+"""Child-process hygiene for the processes the benchmark and the test platform launch.
+
+The benchmark's ranks and the test platform start helper processes (apiserver, scheduler,
+kubelet, control planes, workbenches) whose stdout they read; a rank killed by a time limit
+or a crash must not leave them running — on a shared GPU box they would outlive the job,
+and they keep the launching shell's pipes open.  Linux's ``PR_SET_PDEATHSIG`` gives a child
+SIGTERM when its parent dies.
+
+It is armed by the CHILD, not through ``preexec_fn``: a ``preexec_fn`` forces CPython's
+``subprocess`` from vfork/posix_spawn onto a full ``fork()``, which for a parent holding a
+HIP context and torch's mappings blocks the parent's event loop for ~17 ms per child
+(measured: 8 workbench spawns added 137 ms to the control-plane time of the real-pods
+benchmark).  The parent puts its pid in ``ODH_PDEATHSIG_PARENT`` (:func:`child_env`); the
+child calls :func:`arm_from_env` first thing (``odh_kubeflow_amd/__init__.py`` does it for
+every Python child; the native apiserver does the same in ``main``).
+"""
 
 from __future__ import annotations
 
 import ctypes
+import os
 import signal
+from typing import Dict, Optional
 
+ENV = "ODH_PDEATHSIG_PARENT"
 _PR_SET_PDEATHSIG = 1
 
 
-def die_with_parent() -> None:
-    """``preexec_fn``: the child gets SIGTERM when the process that started it dies.
+def child_env(env: Optional[Dict[str, str]] = None) -> Dict[str, str]:
+    """``env`` (default: this process's) asking the child to die with this process."""
+    out = dict(os.environ if env is None else env)
+    out[ENV] = str(os.getpid())
+    return out
 
-    The benchmark's ranks and the test platform start helper processes (apiserver,
-    scheduler, kubelet, control planes) whose stdout they read; a rank killed by a time
-    limit or a crash must not leave them running — on a shared GPU box they would outlive
-    the job, and they keep the launching shell's pipes open.  Linux-only (prctl); a no-op
-    elsewhere."""
+
+def arm_from_env() -> None:
+    """In a child started with :func:`child_env`: SIGTERM when the parent dies.  The
+    variable is consumed, so this process's own children are not tied to its parent."""
+    parent = os.environ.pop(ENV, None)
+    if not parent:
+        return
     try:
         ctypes.CDLL(None, use_errno=True).prctl(_PR_SET_PDEATHSIG, int(signal.SIGTERM), 0, 0, 0)
     except (OSError, AttributeError):
-        pass
+        return
+    if str(os.getppid()) != parent:  # the parent died before the signal was armed
+        os.kill(os.getpid(), signal.SIGTERM)

@@ -24,10 +24,13 @@ def _alive(pid: int) -> bool:
 
 
 def test_child_gets_sigterm_when_launcher_is_killed():
+    # the child arms the signal itself (importing the package), so the launcher keeps
+    # subprocess's vfork/posix_spawn path (no preexec_fn)
     launcher = textwrap.dedent("""
         import subprocess, sys, time
-        from odh_kubeflow_amd.utils.procutil import die_with_parent
-        c = subprocess.Popen([sys.executable, "-c", "import time; time.sleep(60)"], preexec_fn=die_with_parent)
+        from odh_kubeflow_amd.utils.procutil import child_env
+        c = subprocess.Popen([sys.executable, "-c", "import odh_kubeflow_amd, os, time; "
+                              "assert 'ODH_PDEATHSIG_PARENT' not in os.environ; time.sleep(60)"], env=child_env())
         print(c.pid, flush=True)
         time.sleep(60)
     """)

@@ -70,6 +70,10 @@ def reconciliation_lock_enabled(nb: dict) -> bool:
     return m.annotations(nb).get(STOP_ANNOTATION) == ANNOTATION_VALUE_RECONCILIATION_LOCK
 
 
+async def _noop() -> None:
+    return None
+
+
 class OpenshiftNotebookReconciler:
     def __init__(self, client, reader, namespace: str, env: Optional[Mapping[str, str]] = None, recorder=None,
                  blocking_lock_removal: bool = False, store_info=None,
@@ -348,29 +352,26 @@ class OpenshiftNotebookReconciler:
         if oauth.has_oauth_client_finalizer(nb):
             await oauth.delete_oauth_client(self.client, nb)
             await oauth.remove_oauth_client_finalizer(self.client, nb)
+        # the three cleanups are independent (:195-321 runs them one after another): run them
+        # concurrently; each finalizer is dropped only if its own cleanup succeeded
+        cleanups = []  # (finalizer or None, coroutine)
+        if m.contains_finalizer(nb, HTTPROUTE_FINALIZER):
+            cleanups.append((HTTPROUTE_FINALIZER, route.delete_httproute_for_notebook(self.client, nb, self.namespace)))
+        if m.contains_finalizer(nb, REFERENCEGRANT_FINALIZER):
+            cleanups.append((REFERENCEGRANT_FINALIZER, route.delete_reference_grant_if_last_notebook(self.client, nb)))
+        if auth.kube_rbac_proxy_injection_enabled(nb):
+            cleanups.append((KUBE_RBAC_PROXY_FINALIZER if m.contains_finalizer(nb, KUBE_RBAC_PROXY_FINALIZER) else None,
+                             auth.cleanup_kube_rbac_proxy_crb(self.client, nb)))
+        elif m.contains_finalizer(nb, KUBE_RBAC_PROXY_FINALIZER):
+            cleanups.append((KUBE_RBAC_PROXY_FINALIZER, _noop()))
+        results = await asyncio.gather(*(c for _, c in cleanups), return_exceptions=True)
         done: List[str] = []
         errors: List[str] = []
-        if m.contains_finalizer(nb, HTTPROUTE_FINALIZER):
-            try:
-                await route.delete_httproute_for_notebook(self.client, nb, self.namespace)
-                done.append(HTTPROUTE_FINALIZER)
-            except Exception as e:
-                errors.append(str(e))
-        if m.contains_finalizer(nb, REFERENCEGRANT_FINALIZER):
-            try:
-                await route.delete_reference_grant_if_last_notebook(self.client, nb)
-                done.append(REFERENCEGRANT_FINALIZER)
-            except Exception as e:
-                errors.append(str(e))
-        proxy_ok = True
-        if auth.kube_rbac_proxy_injection_enabled(nb):
-            try:
-                await auth.cleanup_kube_rbac_proxy_crb(self.client, nb)
-            except Exception as e:
-                proxy_ok = False
-                errors.append(str(e))
-        if m.contains_finalizer(nb, KUBE_RBAC_PROXY_FINALIZER) and proxy_ok:
-            done.append(KUBE_RBAC_PROXY_FINALIZER)
+        for (fin, _), r in zip(cleanups, results):
+            if isinstance(r, BaseException):
+                errors.append(str(r))
+            elif fin is not None:
+                done.append(fin)
         if done:
             async def drop():
                 try:

@@ -90,7 +90,8 @@ for s in $steps; do
       timeout -k 10 300 bash tools/hip_init_ab.sh "$tag" > "$out/hip_init_ab.log" 2>&1 || fail hipinit $? "$out/hip_init_ab.log"
       cat "$out/hip_init_ab.log" ;;
     hsaknobs)
-      timeout -k 10 300 python tools/hsa_init_knobs.py --rounds 5 > "$out/hsa_init_knobs.jsonl" 2>&1 \
+      timeout -k 10 300 python tools/hsa_init_knobs.py --rounds ${HSA_KNOB_ROUNDS:-5} ${HSA_KNOB_ONLY:+--only $HSA_KNOB_ONLY} \
+        > "$out/hsa_init_knobs.jsonl" 2>&1 \
         || fail hsaknobs $? "$out/hsa_init_knobs.jsonl"
       tail -1 "$out/hsa_init_knobs.jsonl" ;;
     hipexit)

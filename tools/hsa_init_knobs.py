@@ -28,6 +28,7 @@ SETTINGS = {
     "rocr_visible_0": {"ROCR_VISIBLE_DEVICES": "0"},
     "no_peer_sdma": {"HSA_ENABLE_PEER_SDMA": "0"},
     "no_image_support": {"HSA_IMAGE_SUPPORT": "0"},
+    "rocr_visible_0+no_scratch_reclaim": {"ROCR_VISIBLE_DEVICES": "0", "HSA_NO_SCRATCH_RECLAIM": "1"},
 }
 
 
@@ -46,12 +47,14 @@ def once(env_extra):
 def main(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--only", default="", help="comma list of settings")
     a = ap.parse_args(argv)
+    settings = {k: v for k, v in SETTINGS.items() if not a.only or k in a.only.split(",")}
     if not os.access(BENCH, os.X_OK):
         raise SystemExit(f"build {BENCH} first")
-    res = {k: [] for k in SETTINGS}
+    res = {k: [] for k in settings}
     for rnd in range(a.rounds):
-        for name, env in SETTINGS.items():
+        for name, env in settings.items():
             r = once(env)
             res[name].append(r)
             print(json.dumps({"round": rnd, "setting": name, **r}), flush=True)

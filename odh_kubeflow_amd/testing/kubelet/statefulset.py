@@ -194,6 +194,7 @@ class NamespaceClaimer:
     names, W=2: all four on one worker)."""
 
     RECHECK_S = 0.05  # an unclaimed namespace another worker should take: look again
+    TAKEOVER_S = 2.0  # ... still unclaimed after this (its worker is gone): any worker claims it
 
     def __init__(self, client, reader, index: int, workers: int):
         self.client = client
@@ -202,6 +203,7 @@ class NamespaceClaimer:
         self.workers = int(workers)
         self.claimed = 0
         self._mine: set = set()  # claims of this worker its cache may not show yet
+        self._waiting: dict = {}  # namespace -> monotonic time this worker first left it to another
 
     async def reconcile(self, req: Request) -> Result:
         ns = self.reader.get(kinds.NAMESPACE, req.name)
@@ -218,8 +220,14 @@ class NamespaceClaimer:
         load[self.index] += len(self._mine - seen)
         if min(range(self.workers), key=lambda i: (load[i], i)) != self.index:
             # the least-loaded worker claims it; should its cache lag behind claims this one
-            # already sees (or the other way round), both decide again shortly
-            return Result(requeue_after=self.RECHECK_S)
+            # already sees (or the other way round), both decide again shortly — and should
+            # that worker be gone, this one takes the namespace over after TAKEOVER_S
+            import time
+
+            first = self._waiting.setdefault(req.name, time.monotonic())
+            if time.monotonic() - first < self.TAKEOVER_S:
+                return Result(requeue_after=self.RECHECK_S)
+        self._waiting.pop(req.name, None)
         self._mine.add(req.name)  # before the write: a concurrent decision must count it
         try:
             await self.client.patch(kinds.NAMESPACE, {"metadata": {

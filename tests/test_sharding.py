@@ -386,6 +386,29 @@ def test_informer_namespace_selector_follows_labels(run, server_kind):
     run(go())
 
 
+def test_namespace_claimer_takes_over_from_a_missing_worker(run):
+    """Worker 0 of 2 never runs: worker 1 leaves it each new namespace, then claims the
+    namespace itself once it stayed unclaimed for TAKEOVER_S."""
+    from odh_kubeflow_amd.testing.kubelet.statefulset import WORKER_LABEL, NamespaceClaimer
+
+    async def go():
+        store = ObjectStore()
+        mgr = in_process_manager(store, name="w1")
+        c = NamespaceClaimer(mgr.client, mgr.reader, 1, 2)
+        c.TAKEOVER_S = 0.3
+        c.setup_with_manager(mgr)
+        await mgr.start()
+        try:
+            await store.create({"apiVersion": "v1", "kind": "Namespace", "metadata": {"name": "team"}})
+            loop = asyncio.get_running_loop()
+            t0 = loop.time()
+            assert await _wait(lambda: m.labels(store.peek(kinds.NAMESPACE, "team")).get(WORKER_LABEL) == "1", 5)
+            assert loop.time() - t0 >= 0.25  # it waited for worker 0 first
+        finally:
+            await mgr.stop()
+    run(go())
+
+
 def test_informer_namespace_filter_follows_objects(run, server_kind):
     """``namespace_filter`` without a selector: the cache follows every namespace the
     predicate admits (a platform worker's ``worker_owns``) — system namespaces for worker 0,

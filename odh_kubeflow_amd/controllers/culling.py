@@ -41,7 +41,9 @@ memory on a shared GPU never keeps it alive).
 
 Missing telemetry is never read as idleness: with no GPU samples the Jupyter signal is
 used, and with neither the last-activity annotation is simply left alone (as the
-reference does for HTTP errors, :258-270).
+reference does for HTTP errors, :258-270).  A Pending pod (image pull, init containers)
+is not checked at all, and the idle clock starts no earlier than the pod's Ready
+transition: start-up time is not idle time.
 
 Fixes over the reference: the two culling metrics are exported; the configuration is
 an object (no package globals); sub-minute periods are available through
@@ -224,6 +226,29 @@ def set_stop_annotation(nb: dict, metrics=None) -> None:
     if metrics is not None:
         metrics.notebook_culling_count.labels(m.namespace(nb), m.name(nb)).inc()
         metrics.notebook_culling_timestamp.labels(m.namespace(nb), m.name(nb)).set(int(t))
+
+
+def pod_is_starting(pod: dict) -> bool:
+    """Pending: scheduling, image pull, init containers (``odh-gpu-probe``).  Nothing of the
+    notebook runs yet, so nothing of it can be idle."""
+    return (pod.get("status") or {}).get("phase") == "Pending"
+
+
+def pod_ready_since(pod: dict) -> Optional[float]:
+    """When the pod last became Ready (its server came up), or None."""
+    for c in ((pod.get("status") or {}).get("conditions") or []):
+        if c.get("type") == "Ready" and c.get("status") == "True":
+            return parse_rfc3339(c.get("lastTransitionTime"))
+    return None
+
+
+def update_from_pod_start(nb: dict, pod: dict) -> None:
+    """The idle clock starts no earlier than the server: a last-activity stamp older than
+    the pod's Ready transition is moved up to it."""
+    t = pod_ready_since(pod)
+    a = parse_rfc3339(m.annotations(nb).get(LAST_ACTIVITY_ANNOTATION))
+    if t is not None and a is not None and t > a:
+        m.ensure_annotations(nb)[LAST_ACTIVITY_ANNOTATION] = rfc3339(t)
 
 
 def pod_requests_gpu(pod: Optional[dict]) -> bool:
@@ -451,6 +476,11 @@ class CullingReconciler:
             if any(k in m.annotations(nb) for k in (LAST_ACTIVITY_ANNOTATION, LAST_ACTIVITY_CHECK_TIMESTAMP_ANNOTATION)):
                 await self._update(req, remove_annotations)
             return Result()
+        if pod_is_starting(pod):
+            # Unlike the reference (:86-203), the idle clock waits for the server: an image
+            # pull or init container slower than CULL_IDLE_TIME would otherwise cull a
+            # notebook nobody could use yet (no Jupyter, no GPU process to sample)
+            return Result(requeue_after=self.cfg.check_period_s)
         if not annotations_exist(nb):
             await self._update(req, initialize_annotations)
             nb = await self.client.get(kinds.NOTEBOOK_V1BETA1, req.name, req.namespace)
@@ -469,6 +499,7 @@ class CullingReconciler:
             else:
                 update_from_kernels(cur, kernels)
                 update_from_terminals(cur, terminals)
+                update_from_pod_start(cur, pod)
             update_check_timestamp(cur)
             if notebook_is_idle(cur, self.cfg.cull_idle_time_s):
                 set_stop_annotation(cur, self.metrics)

@@ -20,6 +20,7 @@ import contextvars
 import abc
 from typing import Any, Callable, Dict, Iterable, List, Optional, Sequence, Tuple
 
+from ..models.errors import ApiError, is_not_found
 from ..models.scheme import SCHEME
 from ..utils.objutil import deepcopy_json
 
@@ -33,9 +34,40 @@ LIVE_READS: contextvars.ContextVar = contextvars.ContextVar("live_reads", defaul
 # worker: writes made under it are remembered so their own watch echo does not queue the
 # same request again (see CachedClient.own_write)
 CURRENT_RECONCILE: contextvars.ContextVar = contextvars.ContextVar("current_reconcile", default=None)
+# Set while an admission webhook handles a request: a one-shot decision with no requeue, so
+# an object absent from the informer is confirmed with the apiserver (the reference's live
+# read, which sees an object created a moment before the admission) instead of being
+# answered NotFound from the cache (see CachedClient._validated)
+# (the value: the keys already confirmed absent during this admission, read once)
+CONFIRM_ABSENCE: contextvars.ContextVar = contextvars.ContextVar("confirm_absence", default=None)
 # how long a read of an object this client just wrote waits for the watch to deliver the
 # write before it reads through to the apiserver instead
 RYOW_WAIT_S = 0.05
+
+
+def _patch_certainly_changes(patch: Any, patch_type: str, out: Any) -> bool:
+    """Whether a successful patch certainly produced a new version (so the answered version
+    is this client's own): a resourceVersion precondition that the answer moved past, or a
+    JSON patch that removes or changes a value it tested first.  Anything else may have been
+    a no-op, answered with whatever version was live."""
+    if patch_type == "json" and isinstance(patch, list):
+        tested = {}
+        for op in patch:
+            if not isinstance(op, dict):
+                continue
+            path, kind = op.get("path"), op.get("op")
+            if kind == "test":
+                if path == "/metadata/resourceVersion":
+                    return str(op.get("value")) != str(((out or {}).get("metadata") or {}).get("resourceVersion"))
+                tested[path] = op.get("value")
+            elif path in tested and (kind == "remove" or (kind in ("replace", "add") and op.get("value") != tested[path])):
+                return True
+        return False
+    if isinstance(patch, dict):
+        want = (patch.get("metadata") or {}).get("resourceVersion") if isinstance(patch.get("metadata"), dict) else None
+        if want:
+            return str(want) != str(((out or {}).get("metadata") or {}).get("resourceVersion"))
+    return False
 
 
 def _rv_int(o) -> Optional[int]:
@@ -153,9 +185,14 @@ class CachedClient(Client):
         self._ensured: set = set()  # kinds whose informer is known synced and served
         # (kind, namespace, name, resourceVersion) → (controller, request) that wrote it
         self._own: Dict[Tuple[str, str, str, int], tuple] = {}
-        # (kind, namespace, name) → (controller, request) of a create / precondition update
-        # still awaiting its response (the watch event can overtake the response)
-        self._inflight: Dict[Tuple[str, str, str], tuple] = {}
+        # (kind, namespace, name) → [(controller, request), precondition rv or None, the rv of
+        # the event provisionally claimed as its echo] of a create / precondition update still
+        # awaiting its response (the watch event can overtake the response)
+        self._inflight: Dict[Tuple[str, str, str], list] = {}
+        # (controller name, request) → re-queue it: set by the manager; called when an event
+        # claimed as an in-flight write's echo turns out not to be (see own_write)
+        self.requeue: Optional[Callable[[str, Any], None]] = None
+        self.misclaims = 0
         self.fresh_reads = 0
         self.cache_waits = 0
         # live-read kinds (``uncached``: the odh manager's ConfigMaps / Secrets, whose cached
@@ -165,7 +202,13 @@ class CachedClient(Client):
         self._full: Dict[Tuple[str, str, str], Tuple[int, dict]] = {}
         self.validated_reads = 0
 
-    def _note(self, out) -> None:
+    def _note(self, out, claim: bool = True) -> None:
+        """Remember a write's result.  ``claim=False``: the write may have been a no-op — a
+        status patch or a patch without any precondition, which the apiserver answers with
+        the live object unchanged, i.e. with SOMEONE ELSE's latest version — so the version
+        is not claimed as this controller's echo (claiming it hid the odh lock removal from
+        the kf reconciler that had just re-written an unchanged status: the notebook stayed
+        at 0 replicas, tests/test_fault_injection.py)."""
         if not isinstance(out, dict) or "metadata" not in out:
             return
         rv = _rv_int(out)
@@ -181,7 +224,7 @@ class CachedClient(Client):
         if key[0] in self.uncached:
             self._keep_full(key, rv, out)
         cur = CURRENT_RECONCILE.get()
-        if cur is not None:
+        if cur is not None and claim:
             if len(self._own) > 16384:
                 self._own.clear()  # echoes never delivered (kinds nobody here watches)
             self._own[key + (rv,)] = cur
@@ -206,10 +249,17 @@ class CachedClient(Client):
         hit = self._own.get(key)
         if hit is None and self._inflight:
             # The echo overtook the write's response.  Only creates and resourceVersion-
-            # preconditioned updates are tracked in flight: any other writer's event for the
-            # object in that window makes this write fail (AlreadyExists / Conflict), and the
-            # failed reconcile is retried with backoff anyway.
-            hit = self._inflight.get(key[:3])
+            # preconditioned updates are tracked in flight, and only the first event after
+            # the precondition is claimed: a write by another client before ours would have
+            # failed ours (AlreadyExists / Conflict).  The claim is provisional — a write of
+            # someone else can follow ours inside the window, and a preconditioned update can
+            # be a no-op — and is settled against the response (_settle).
+            ent = self._inflight.get(key[:3])
+            if ent is not None:
+                if ent[2] is None and (ent[1] is None or rv > ent[1]):
+                    ent[2] = rv
+                if ent[2] == rv:
+                    hit = ent[0]
         # kept (not popped): a controller may watch the kind twice (Owns + Watches); the
         # table is bounded and an entry can only ever match its own object version
         return hit[1] if hit is not None and hit[0] == controller else None
@@ -249,7 +299,9 @@ class CachedClient(Client):
         it) — the unsharded odh manager re-read ``pipeline-runtime-images`` and the CA
         bundles live 16+ times per notebook, mostly to learn they do not exist.  An object
         the synced informer does not hold is NotFound without a read, unless this client
-        wrote it.  Freshness is the informer's, as for every other cached read; this client's
+        wrote it or an admission is being decided (``CONFIRM_ABSENCE``: the webhook must see
+        a ConfigMap created a moment before, as the reference's live read does; its
+        existence-only decisions are safe on a vouched-for copy).  Freshness is the informer's, as for every other cached read; this client's
         own newer writes always win (``_written``)."""
         info = SCHEME.resolve(kind)
         key = (info.key, namespace or "", name)
@@ -258,8 +310,9 @@ class CachedClient(Client):
             return None
         o = self.reader.get(kind, name, namespace)
         if o is None:
-            if key in self._written:
-                return None  # written here and not yet in the cache: read through
+            if key in self._written or CONFIRM_ABSENCE.get() is not None:
+                # written here and not yet in the cache, or an admission: read through
+                return None
             # absent from a synced informer: NotFound, as a cached read would say (the
             # optional bundles — odh-trusted-ca-bundle, pipeline-runtime-images — usually are)
             from ..models.errors import NotFound
@@ -282,15 +335,27 @@ class CachedClient(Client):
     async def get(self, kind, name, namespace=None):
         if self._live(kind, namespace) or LIVE_READS.get():
             uncached = SCHEME.resolve(kind).key in self.uncached
+            key = (SCHEME.resolve(kind).key, namespace or "", name)
+            absent = CONFIRM_ABSENCE.get() if uncached else None
             if uncached and not LIVE_READS.get():
                 hit = self._validated(kind, name, namespace)
                 if hit is not None:
                     return hit
-            o = await self.writer.get(kind, name, namespace)
+                if absent is not None and key in absent and key not in self._written:
+                    from ..models.errors import NotFound  # confirmed earlier in this admission
+
+                    info = SCHEME.resolve(kind)
+                    raise NotFound(info.plural if not info.group else f"{info.plural}.{info.group}", name)
+            try:
+                o = await self.writer.get(kind, name, namespace)
+            except ApiError as e:
+                if absent is not None and is_not_found(e):
+                    absent.add(key)
+                raise
             if uncached:
                 rv = _rv_int(o)
                 if rv is not None:
-                    self._keep_full((SCHEME.resolve(kind).key, namespace or "", name), rv, o)
+                    self._keep_full(key, rv, o)
             return o
         await self._ensure(kind)
         o = self.reader.get(kind, name, namespace)
@@ -339,7 +404,7 @@ class CachedClient(Client):
                 o["apiVersion"] = av
         return items
 
-    def _begin(self, obj) -> Optional[Tuple[str, str, str]]:
+    def _begin(self, obj, precondition: Optional[int] = None) -> Optional[Tuple[str, str, str]]:
         cur = CURRENT_RECONCILE.get()
         if cur is None or not isinstance(obj, dict):
             return None
@@ -350,37 +415,53 @@ class CachedClient(Client):
             key = (SCHEME.resolve(obj).key, md.get("namespace") or "", md["name"])
         except Exception:
             return None
-        self._inflight[key] = cur
+        self._inflight[key] = [cur, precondition, None]
         return key
+
+    def _settle(self, key, out) -> None:
+        """The write answered (``out``) or failed (None): an event claimed in flight that is
+        not this write's version goes back to its controller's queue."""
+        ent = self._inflight.pop(key, None)
+        if ent is None or ent[2] is None:
+            return
+        if out is None or _rv_int(out) != ent[2]:
+            self.misclaims += 1
+            if self.requeue is not None:
+                self.requeue(ent[0][0], ent[0][1])
 
     async def create(self, obj):
         key = self._begin(obj)
+        out = None
         try:
             out = await self.writer.create(obj)
         finally:
             if key is not None:
-                self._inflight.pop(key, None)
+                self._settle(key, out)
         self._note(out)
         return out
 
     async def update(self, obj):
-        key = self._begin(obj) if _rv_int(obj) is not None else None
+        sent = _rv_int(obj)
+        key = self._begin(obj, sent) if sent is not None else None
+        out = None
         try:
             out = await self.writer.update(obj)
         finally:
             if key is not None:
-                self._inflight.pop(key, None)
-        self._note(out)
+                self._settle(key, out)
+        # without a precondition, or answered with the version sent, the update was a no-op
+        self._note(out, claim=sent is not None and _rv_int(out) != sent)
         return out
 
     async def update_status(self, obj):
+        sent = _rv_int(obj)
         out = await self.writer.update_status(obj)
-        self._note(out)
+        self._note(out, claim=sent is not None and _rv_int(out) != sent)
         return out
 
     async def patch(self, obj_or_kind, patch, patch_type="merge", name=None, namespace=None, subresource=None):
         out = await self.writer.patch(obj_or_kind, patch, patch_type, name, namespace, subresource)
-        self._note(out)
+        self._note(out, claim=_patch_certainly_changes(patch, patch_type, out))
         return out
 
     async def delete(self, obj_or_kind, name=None, namespace=None, preconditions=None, propagation="Background"):

@@ -381,6 +381,8 @@ class Builder:
         c = Controller(name, fn, maxc, self._rate_limiter, self.mgr.runtime_metrics)
         if getattr(self.mgr, "skip_own_write_echoes", True):
             c.own_writes = getattr(self.mgr.client, "own_write", None)
+            if c.own_writes is not None and getattr(self.mgr.client, "requeue", False) is None:
+                self.mgr.client.requeue = self.mgr.requeue
         if self._for:
             c.watch(self._for, enqueue_for_object, self._for_preds)
         for w in self._watches:

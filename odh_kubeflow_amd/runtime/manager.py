@@ -93,6 +93,13 @@ class Manager:
     def add_controller(self, c: Controller) -> None:
         self.controllers.append(c)
 
+    def requeue(self, controller: str, req) -> None:
+        """Queue ``req`` again in the controller named ``controller`` (an event that the
+        client had provisionally taken for that controller's own write, but was not)."""
+        for c in self.controllers:
+            if c.name == controller:
+                c.enqueue(req, "misclaim")
+
     def add(self, runnable, needs_leader: bool = True) -> None:
         (self.leader_runnables if needs_leader else self.runnables).append(runnable)
 

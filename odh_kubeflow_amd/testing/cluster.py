@@ -284,6 +284,18 @@ class LocalCluster:
                 if not is_already_exists(e):
                     raise
 
+    async def edit(self, kind, name: str, namespace: Optional[str], fn: Callable[[dict], None]) -> dict:
+        """A user's read-modify-write of one object (``kubectl edit``): re-read and retried
+        on a Conflict, as controllers (and stand-ins such as the gateway's status writer) may
+        write the object between the read and the write."""
+        from ..runtime.retry import retry_on_conflict
+
+        async def attempt():
+            cur = await self.admin.get(kind, name, namespace)
+            fn(cur)
+            return await self.admin.update(cur)
+        return await retry_on_conflict(attempt)
+
     async def stop(self) -> None:
         for mgr in reversed(self.managers):
             await mgr.stop()

@@ -42,6 +42,7 @@ from ..controllers.odh.podspec import add_missing_env, notebook_container
 from ..models import kinds
 from ..models import meta as m
 from ..models.errors import ApiError, is_not_found
+from ..runtime.client import CONFIRM_ABSENCE
 from ..tracing import current_span, get_tracer
 from ..utils import jsonpatch
 from ..utils.objutil import deepcopy_json, semantic_equal
@@ -268,8 +269,12 @@ class NotebookWebhook:
             if bad:  # the reference's typed decode (admission.Decoder) refuses these
                 raise AdmissionError(400, f"cannot decode Notebook: {bad}")
             old = req.get("oldObject") if isinstance(req.get("oldObject"), dict) else None
-            mutated = await self.mutate(req.get("operation", ""), obj, old, req.get("name", ""),
-                                        req.get("namespace", ""))
+            tok = CONFIRM_ABSENCE.set(set())  # one-shot decision: absent objects are confirmed live, once
+            try:
+                mutated = await self.mutate(req.get("operation", ""), obj, old, req.get("name", ""),
+                                            req.get("namespace", ""))
+            finally:
+                CONFIRM_ABSENCE.reset(tok)
             ops = jsonpatch.create_patch(obj, mutated)
             if ops:
                 resp["patchType"] = "JSONPatch"

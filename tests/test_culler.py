@@ -95,6 +95,28 @@ def test_check_period(clock):
     assert not c.culling_check_period_has_passed(nbmeta({}), 60)
 
 
+def test_start_up_time_is_not_idle_time():
+    """A Pending pod (image pull, the odh-gpu-probe init container) is not checked, and the
+    idle clock starts no earlier than the pod's Ready transition (the reference counts from
+    the pod's first sighting, so a start-up slower than CULL_IDLE_TIME culls it unused)."""
+    assert c.pod_is_starting({"status": {"phase": "Pending"}})
+    assert not c.pod_is_starting({"status": {"phase": "Running"}}) and not c.pod_is_starting({})
+    old, ready = rfc3339(time.time() - 600), rfc3339(time.time() - 60)
+    pod = {"status": {"phase": "Running", "conditions": [
+        {"type": "Ready", "status": "True", "lastTransitionTime": ready}]}}
+    nb = nbmeta({LAST_ACTIVITY_ANNOTATION: old})
+    c.update_from_pod_start(nb, pod)
+    assert m.annotations(nb)[LAST_ACTIVITY_ANNOTATION] == ready
+    later = rfc3339(time.time() - 1)
+    nb = nbmeta({LAST_ACTIVITY_ANNOTATION: later})
+    c.update_from_pod_start(nb, pod)  # never moved backwards
+    assert m.annotations(nb)[LAST_ACTIVITY_ANNOTATION] == later
+    pod["status"]["conditions"][0]["status"] = "False"
+    nb = nbmeta({LAST_ACTIVITY_ANNOTATION: old})
+    c.update_from_pod_start(nb, pod)
+    assert m.annotations(nb)[LAST_ACTIVITY_ANNOTATION] == old
+
+
 # ------------------------------------------------------------------ integration
 
 

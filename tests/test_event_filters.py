@@ -167,3 +167,86 @@ def test_lifecycle_reconciles_per_notebook_and_triggers(run):
             # kf: creation + lock removal (Notebook), pod readiness (Pod), readyReplicas (STS)
             assert kf.get("Notebook", 0) <= 2 * 5 and kf.get("Service", 0) == 0, kf
     run(go())
+
+
+def test_noop_patch_does_not_claim_another_writers_version(run):
+    """A patch that changes nothing is answered with the live object — whatever version
+    another client wrote last.  Claiming that version as an own write hid the other write's
+    event from the patching controller (the odh lock removal never reached kf: the notebook
+    stayed at 0 replicas).  Only writes that certainly produced a new version are claimed."""
+    from odh_kubeflow_amd.runtime.client import CURRENT_RECONCILE
+
+    async def go():
+        store = ObjectStore()
+        await store.create({"apiVersion": "v1", "kind": "Namespace", "metadata": {"name": "ns"}})
+        mgr = in_process_manager(store, name="t")
+        await store.create(_cm("a"))
+        mine = await store.get(kinds.CONFIG_MAP, "a", "ns")
+        theirs = dict(mine, data={"k": "v", "k2": "other"})
+        theirs = await store.update(theirs)
+        req = Request("ns", "a")
+        tok = CURRENT_RECONCILE.set(("writer", req))
+        try:
+            out = await mgr.client.patch(mine, {"data": {"k": "v"}}, "merge")  # no-op
+            assert m.resource_version(out) == m.resource_version(theirs)
+            assert mgr.client.own_write(out, "writer") is None
+            out = await mgr.client.patch(out, [{"op": "add", "path": "/status", "value": {}}], "json")
+            assert mgr.client.own_write(out, "writer") is None
+            # a tested removal certainly wrote a new version: its echo is the writer's own
+            out = await mgr.client.patch(out, [{"op": "test", "path": "/data/k2", "value": "other"},
+                                               {"op": "remove", "path": "/data/k2"}], "json")
+            assert mgr.client.own_write(out, "writer") == req
+            # an update with a precondition, answered with a new version, too
+            out["data"]["k"] = "w"
+            out = await mgr.client.update(out)
+            assert mgr.client.own_write(out, "writer") == req
+        finally:
+            CURRENT_RECONCILE.reset(tok)
+    run(go())
+
+
+def test_inflight_echo_claim_is_settled_against_the_response(run):
+    """An event that overtakes a preconditioned write's response is claimed provisionally;
+    when the response shows another version, the request goes back to its controller."""
+    import asyncio
+
+    from odh_kubeflow_amd.runtime.client import CURRENT_RECONCILE
+
+    async def go():
+        store = ObjectStore()
+        await store.create({"apiVersion": "v1", "kind": "Namespace", "metadata": {"name": "ns"}})
+        mgr = in_process_manager(store, name="t")
+        client = mgr.client
+        requeued = []
+        client.requeue = lambda name, r: requeued.append((name, r))
+        await store.create(_cm("a"))
+        cm = await store.get(kinds.CONFIG_MAP, "a", "ns")
+        sent = int(m.resource_version(cm))
+        gate = asyncio.Event()
+
+        class SlowWriter:
+            def __init__(self, inner, answer_rv):
+                self.inner, self.answer_rv = inner, answer_rv
+
+            async def update(self, obj):
+                await gate.wait()
+                return dict(obj, metadata=dict(obj["metadata"], resourceVersion=str(self.answer_rv)))
+
+        req = Request("ns", "a")
+        foreign = dict(cm, metadata=dict(cm["metadata"], resourceVersion=str(sent + 1)))
+        for answer, expect_requeue in ((sent + 2, True), (sent + 1, False)):
+            requeued.clear()
+            client.writer = SlowWriter(client.writer, answer)
+            tok = CURRENT_RECONCILE.set(("writer", req))
+            try:
+                t = asyncio.ensure_future(client.update(dict(cm)))
+                await asyncio.sleep(0)
+            finally:
+                CURRENT_RECONCILE.reset(tok)
+            assert client.own_write(foreign, "writer") == req  # provisional
+            gate.set()
+            await t
+            gate.clear()
+            client.writer = client.writer.inner
+            assert requeued == ([("writer", req)] if expect_requeue else []), answer
+    run(go())

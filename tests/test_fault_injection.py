@@ -464,7 +464,22 @@ def test_sharded_control_plane_follows_new_namespaces_through_resets(tmp_path, r
                     if st.get("readyReplicas") != 1:
                         return False
                 return True
-            await eventually(all_ready, 90)
+
+            async def state():  # what a failure report needs: where each notebook stopped
+                out = {}
+                for ns in spaces:
+                    nb = await c.get(kinds.NOTEBOOK, "nb", ns)
+                    sts = await c.get_or_none(kinds.STATEFUL_SET, "nb", ns)
+                    pod = await c.get_or_none(kinds.POD, "nb-0", ns)
+                    out[ns] = {"ready": (nb.get("status") or {}).get("readyReplicas"),
+                               "annotations": sorted(m.annotations(nb)), "finalizers": m.finalizers(nb),
+                               "sts_replicas": ((sts or {}).get("spec") or {}).get("replicas"),
+                               "pod_phase": ((pod or {}).get("status") or {}).get("phase")}
+                return out
+            try:
+                await eventually(all_ready, 90)
+            except AssertionError:
+                raise AssertionError(f"not all Ready: {await state()}")
             owners = {m.labels(r)["notebook-namespace"]: m.labels(r).get("notebooks.amd.com/shard")
                       for r in await c.list(kinds.HTTP_ROUTE, "opendatahub")}
             want = {ns: m.labels(await c.get(kinds.NAMESPACE, ns))["notebooks.amd.com/shard"] for ns in spaces}

@@ -57,9 +57,8 @@ def test_routes_resolve_in_both_modes_and_reference_port_does_not(run):
             assert (status, reason) == ("False", "BackendNotFound") and "port 8888" in msg
 
             # a reference-era route of a managed notebook is moved to the Service port
-            r = await cl.admin.get(kinds.HTTP_ROUTE, m.name(_route(cl, "plain")), CENTRAL)
-            r["spec"]["rules"][0]["backendRefs"][0]["port"] = 8888
-            await cl.admin.update(r)
+            await cl.edit(kinds.HTTP_ROUTE, m.name(_route(cl, "plain")), CENTRAL,
+                          lambda r: r["spec"]["rules"][0]["backendRefs"][0].__setitem__("port", 8888))
             assert await cl.wait_for(lambda: _route(cl, "plain")["spec"]["rules"][0]["backendRefs"][0]["port"] == 80)
             assert await cl.wait_for(lambda: (_resolved(cl, "plain") or ("",))[0] == "True", 10)
     run(go())

@@ -260,11 +260,14 @@ def test_culler_kfd_attribution_only(run, sysfs):
                 culler = cl.reconcilers["culler"]
                 assert await cl.wait_for(lambda: c.annotations_exist(cl.store.peek(kinds.NOTEBOOK, "busy", "u")))
                 await asyncio.sleep(0.4)
+                # checks made before the fake KFD entries existed fell back to Jupyter (no GPU
+                # sample yet — how early depends on the transport); from here on none may
+                jupyter0 = culler.jupyter.requests
                 offset[0] += 7200
                 assert await cl.wait_for(lambda: STOP_ANNOTATION in m.annotations(
                     cl.store.peek(kinds.NOTEBOOK, "idle", "u")), 10)
                 assert STOP_ANNOTATION not in m.annotations(cl.store.peek(kinds.NOTEBOOK, "busy", "u"))
-                assert agent.attributed_queries >= 2 and culler.jupyter.requests == 0
+                assert agent.attributed_queries >= 2 and culler.jupyter.requests == jupyter0
         finally:
             await agent.stop()
     try:

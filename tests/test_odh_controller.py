@@ -64,9 +64,8 @@ def test_httproute_lifecycle(run):
             assert await cl.wait_for(lambda: "kubeflow-resource-stopped" not in m.annotations(
                 cl.store.peek(kinds.NOTEBOOK, "nb", "user")))
             # drift is restored
-            r = await cl.admin.get(kinds.HTTP_ROUTE, "nb-user-nb", CENTRAL)
-            r["spec"]["rules"][0]["backendRefs"][0]["port"] = 9999
-            await cl.admin.update(r)
+            await cl.edit(kinds.HTTP_ROUTE, "nb-user-nb", CENTRAL,
+                          lambda r: r["spec"]["rules"][0]["backendRefs"][0].__setitem__("port", 9999))
             assert await cl.wait_for(lambda: route_for(cl, "nb")[0]["spec"]["rules"][0]["backendRefs"][0]["port"] == 80)
             # deleted route is recreated
             await cl.admin.delete(kinds.HTTP_ROUTE, "nb-user-nb", CENTRAL)
@@ -88,9 +87,7 @@ def test_gateway_env_override_and_long_name(run):
             assert m.name(r).startswith("nb-long-names-a-very-lon-") and len(m.name(r)) <= 63
             assert r["spec"]["parentRefs"] == [{"name": "gw", "namespace": "gw-ns"}]
             # drift correction works through the label lookup
-            cur = await cl.admin.get(kinds.HTTP_ROUTE, m.name(r), CENTRAL)
-            cur["spec"]["parentRefs"] = []
-            await cl.admin.update(cur)
+            await cl.edit(kinds.HTTP_ROUTE, m.name(r), CENTRAL, lambda cur: cur["spec"].__setitem__("parentRefs", []))
             assert await cl.wait_for(lambda: route_for(cl, long_name, "long-namespace-for-routes")[0]["spec"]
                                      ["parentRefs"] == [{"name": "gw", "namespace": "gw-ns"}])
             await cl.admin.delete(kinds.NOTEBOOK, long_name, "long-namespace-for-routes")

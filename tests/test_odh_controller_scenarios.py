@@ -16,6 +16,7 @@ from odh_kubeflow_amd.testing.cluster import ClusterConfig, LocalCluster
 from odh_kubeflow_amd.models import kinds
 from odh_kubeflow_amd.models import meta as m
 from odh_kubeflow_amd.models.notebook import notebook
+from odh_kubeflow_amd.runtime.retry import retry_on_conflict
 
 CENTRAL = "opendatahub"
 AUTH = {"notebooks.opendatahub.io/inject-auth": "true"}
@@ -154,9 +155,11 @@ def test_auth_route_drift_and_recreate(run):
             want = copy.deepcopy(route_for(cl, "nb")[0]["spec"])
             assert want["rules"][0]["backendRefs"] == [{"name": "nb-kube-rbac-proxy", "namespace": "user",
                                                         "port": 8443}]
-            cur = await cl.admin.get(kinds.HTTP_ROUTE, "nb-user-nb", CENTRAL)
-            cur["spec"]["rules"][0]["backendRefs"][0]["name"] = "elsewhere"
-            await cl.admin.update(cur)
+            async def tamper():  # the route may still be written (status) while the test edits it
+                cur = await cl.admin.get(kinds.HTTP_ROUTE, "nb-user-nb", CENTRAL)
+                cur["spec"]["rules"][0]["backendRefs"][0]["name"] = "elsewhere"
+                await cl.admin.update(cur)
+            await retry_on_conflict(tamper)
             assert await cl.wait_for(lambda: route_for(cl, "nb")[0]["spec"] == want)
             await cl.admin.delete(kinds.HTTP_ROUTE, "nb-user-nb", CENTRAL)
             assert await cl.wait_for(lambda: len(route_for(cl, "nb")) == 1 and route_for(cl, "nb")[0]["spec"] == want)

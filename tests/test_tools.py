@@ -25,12 +25,14 @@ def test_bench_culling_cpu_rehearsal():
     import subprocess
     import sys
 
-    out = subprocess.run([sys.executable, "tools/bench_culling.py", "--cpu", "--idle-s", "1", "--period-s", "0.1",
+    # idle 2 s: last-activity has whole-second resolution, so 1 s could leave a resumed
+    # notebook cullable before its GPU's first attributed sample
+    out = subprocess.run([sys.executable, "tools/bench_culling.py", "--cpu", "--idle-s", "2", "--period-s", "0.1",
                           "--load-s", "2.5"], capture_output=True, text=True, timeout=120,
                          cwd=__import__("os").path.dirname(__import__("os").path.dirname(__file__)))
     assert out.returncode == 0, out.stderr[-2000:]
     d = json.loads(out.stdout.strip().splitlines()[-1])
-    assert d["false_culls_under_load"] == 0 and d["culled"] == 16
+    assert d["false_culls_under_load"] == 0 and d["culled"] == 16, d.get("false_cull_signals")
     assert d["gpu_busy_mean_under_load"] >= 90
     assert 0 <= d["idle_reclaim_ms_p50"] < 1500
     assert d["culls_on_attributed_gpu_idle_sample"] == 16

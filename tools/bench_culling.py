@@ -36,7 +36,8 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 from odh_kubeflow_amd.models import kinds  # noqa: E402
 from odh_kubeflow_amd.models import meta as m  # noqa: E402
-from odh_kubeflow_amd.models.notebook import STOP_ANNOTATION, notebook  # noqa: E402
+from odh_kubeflow_amd.models.notebook import LAST_ACTIVITY_ANNOTATION, STOP_ANNOTATION, notebook  # noqa: E402
+from odh_kubeflow_amd.utils.timeutil import parse_rfc3339  # noqa: E402
 from odh_kubeflow_amd.testing.cluster import ClusterConfig, LocalCluster  # noqa: E402
 from odh_kubeflow_amd.testing.notebook_server.jupyter import JupyterContainerRuntime  # noqa: E402
 
@@ -117,6 +118,7 @@ async def run(args) -> dict:
             await cl.ensure_namespace("cull")
             culler = cl.reconcilers["culler"]
             stopped_at = {}
+            last_activity = {}  # the culler's last-activity stamp, as last seen before the cull
 
             def scaled_down(nm):
                 sts = cl.store.peek(kinds.STATEFUL_SET, nm, "cull")
@@ -126,13 +128,23 @@ async def run(args) -> dict:
             def poll():
                 now = time.time()
                 for nm in names:
-                    if nm not in stopped_at and scaled_down(nm):
+                    if nm in stopped_at:
+                        continue
+                    nb = cl.store.peek(kinds.NOTEBOOK, nm, "cull") or {}
+                    la = parse_rfc3339(m.annotations(nb).get(LAST_ACTIVITY_ANNOTATION))
+                    if la is not None and STOP_ANNOTATION not in m.annotations(nb):
+                        last_activity[nm] = la
+                    if scaled_down(nm):
                         stopped_at[nm] = now
                 return len(stopped_at) == N
 
             async def ready_with_idle_kernels():
                 if not await cl.wait_for(lambda: all(cl.notebook_ready(nm, "cull") for nm in names), 60):
-                    raise RuntimeError("notebooks not Ready")
+                    raise RuntimeError("notebooks not Ready: " + json.dumps({
+                        nm: {"ready": cl.notebook_ready(nm, "cull"),
+                             "stopped": STOP_ANNOTATION in m.annotations(cl.store.peek(kinds.NOTEBOOK, nm, "cull") or {}),
+                             "sts_replicas": ((cl.store.peek(kinds.STATEFUL_SET, nm, "cull") or {}).get("spec") or {}).get("replicas"),
+                             "pod": cl.store.peek(kinds.POD, f"{nm}-0", "cull") is not None} for nm in names}))
                 t = time.time()
                 for nm in names:  # an idle kernel: Jupyter says "idle" for every notebook
                     rt.state("cull", nm).start_kernel(busy=False)
@@ -151,10 +163,10 @@ async def run(args) -> dict:
             n_log = len(culler.cull_log)
             if not await cl.wait_for(poll, args.idle_s * 4 + 30, 0.005):
                 raise RuntimeError(f"idle notebooks not culled: {sorted(set(names) - set(stopped_at))}")
-            # last-activity carries whole seconds (RFC3339, as in the reference): a notebook is
-            # cullable from floor(kernel start) + CULL_IDLE_TIME on
-            cullable = int(t_kernels) + args.idle_s
-            idle_lat = {nm: (stopped_at[nm] - cullable) * 1e3 for nm in names}
+            # a notebook is cullable from its last-activity stamp (whole seconds, RFC3339, as in
+            # the reference) + CULL_IDLE_TIME on
+            idle_lat = {nm: (stopped_at[nm] - (last_activity.get(nm, int(t_kernels)) + args.idle_s)) * 1e3
+                        for nm in names}
             idle_sig = signals_of(n_log)
 
             # ---- load phase: the GPU(s) busy, the notebooks resumed: no culls; unload: culled
@@ -173,6 +185,7 @@ async def run(args) -> dict:
             false_culls = sorted(nm for nm in names if nm in stopped_at or STOP_ANNOTATION in m.annotations(
                 cl.store.peek(kinds.NOTEBOOK, nm, "cull")))
             busy_sample = await culler.gpu.busy(cl.store.peek(kinds.POD, "nb0-0", "cull"), 1.0)
+            false_sig = {nm: sig for nm, sig in signals_of(n_log).items() if nm in false_culls}
             n_log = len(culler.cull_log)
             load.stop()
             t_unload = time.time()
@@ -186,6 +199,7 @@ async def run(args) -> dict:
                 "idle_reclaim_ms_p50": round(statistics.median(idle_lat.values()), 1),
                 "idle_reclaim_ms_max": round(max(idle_lat.values()), 1),
                 "false_culls_under_load": len(false_culls), "falsely_culled": false_culls,
+                "false_cull_signals": false_sig,
                 "gpu_busy_mean_under_load": None if busy_sample is None else round(busy_sample["busy_mean"], 1),
                 # expected: CULL_IDLE_TIME + up to one check period (the busy window drains)
                 # + up to 1 s of RFC3339 rounding

@@ -16,8 +16,9 @@ Two access paths, as in controller-runtime:
 
 from __future__ import annotations
 
-import contextvars
 import abc
+import asyncio
+import contextvars
 from typing import Any, Callable, Dict, Iterable, List, Optional, Sequence, Tuple
 
 from ..models.errors import ApiError, is_not_found
@@ -331,6 +332,22 @@ class CachedClient(Client):
         if v:
             out["apiVersion"] = info.api_version(v)
         return out
+
+    async def prefetch(self, keys: Sequence[Tuple[Any, str, Optional[str]]]) -> None:
+        """Inside an admission (``CONFIRM_ABSENCE`` set): make the live reads of ``keys`` —
+        (kind, name, namespace) that the admission is about to read — concurrently, so that
+        confirming N absences costs one round trip instead of N in sequence.  The answers land
+        where ``get`` looks first (the validated-read cache, the admission's absence memo)."""
+        if CONFIRM_ABSENCE.get() is None or len(keys) < 2:
+            return
+
+        async def one(kind, name, namespace):
+            try:
+                await self.get(kind, name, namespace)
+            except ApiError:
+                pass  # recorded (NotFound) or raised again by the read itself
+
+        await asyncio.gather(*(one(*k) for k in keys))
 
     async def get(self, kind, name, namespace=None):
         if self._live(kind, namespace) or LIVE_READS.get():

@@ -187,6 +187,11 @@ class NotebookWebhook:
             if operation == "CREATE":
                 inject_reconciliation_lock(nb)
             if operation in ("CREATE", "UPDATE"):
+                prefetch = getattr(self.client, "prefetch", None)
+                if prefetch is not None:  # the two ConfigMaps every admission reads, at once
+                    ns = m.namespace(nb) or namespace
+                    await prefetch([(kinds.CONFIG_MAP, certs.ODH_CONFIGMAP_NAME, ns),
+                                    (kinds.CONFIG_MAP, runtime_images.RUNTIME_IMAGES_CONFIGMAP, ns)])
                 await set_container_image_from_registry(self.client, nb, self.namespace)
                 await certs.check_and_mount_ca_cert_bundle(self.client, nb)
                 try:

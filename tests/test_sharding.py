@@ -483,6 +483,21 @@ def test_live_read_kinds_are_read_once_per_version(run, server_kind):
             # this client's own create: served from its response, never a stale NotFound
             await client.create(_cm("mine", "a"))
             assert (await client.get(kinds.CONFIG_MAP, "mine", "a"))["data"] == {"k": "mine"}
+            # inside an admission absences are confirmed live, once, and prefetch makes those
+            # reads concurrently: later reads of the same keys cost no request
+            from odh_kubeflow_amd.runtime.client import CONFIRM_ABSENCE
+
+            tok = CONFIRM_ABSENCE.set(set())
+            try:
+                n2 = c.requests
+                await client.prefetch([(kinds.CONFIG_MAP, "gone1", "a"), (kinds.CONFIG_MAP, "gone2", "a")])
+                assert c.requests == n2 + 2
+                for nm in ("gone1", "gone2"):
+                    with pytest.raises(NotFound):
+                        await client.get(kinds.CONFIG_MAP, nm, "a")
+                assert c.requests == n2 + 2
+            finally:
+                CONFIRM_ABSENCE.reset(tok)
             await cache.stop()
         finally:
             await c.close()

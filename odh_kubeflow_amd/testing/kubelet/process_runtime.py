@@ -3,11 +3,13 @@
 The fake kubelet's default runtime starts nothing, so pod start-up costs zero and a
 "create → Ready" figure measures only the control plane (BASELINE config #1).  Configs
 #2/#3 need the notebook's own start: this runtime spawns
-:mod:`odh_kubeflow_amd.testing.notebook_server.workbench` per pod — PyTorch imported, the HIP
-runtime initialised on the pod's allocated MI355X (``HIP_VISIBLE_DEVICES``, the device
-plugin's job), a first bf16 matmul, the Jupyter API served — with the container's env
-(``NB_PREFIX`` …) and reports the pod Ready once its readiness probe
-(``GET <NB_PREFIX>/api``) answers.  A pod's MI355X start-up probe init container
+:mod:`odh_kubeflow_amd.testing.notebook_server.workbench` per pod — the Jupyter API served,
+and a first cell that imports PyTorch, initialises the HIP runtime on the pod's allocated
+MI355X (``HIP_VISIBLE_DEVICES``, the device plugin's job) and runs a bf16 matmul — with the
+container's env (``NB_PREFIX`` …) and reports the pod Ready once its readiness probe
+(``GET <NB_PREFIX>/api``) answers.  ``gpu_init="first-cell"`` (default) runs that cell after
+the server is Ready, as JupyterLab would (:meth:`first_cell` awaits it);
+``"before-ready"`` holds readiness until the GPU is usable.  A pod's MI355X start-up probe init container
 (``odh-gpu-probe``) runs first, as its own process on the same GPU.  Image pull and
 container-runtime overheads are not included (no registry or container runtime on the
 benchmark boxes).
@@ -33,9 +35,13 @@ ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.dirname(os.path.a
 
 class ProcessContainerRuntime(ContainerRuntime):
     def __init__(self, host: str = "127.0.0.1", matmul: int = 1024, ready_timeout_s: float = 300.0,
-                 probe_interval_s: float = 0.02, visible_device=None, env: Optional[Dict[str, str]] = None):
+                 probe_interval_s: float = 0.02, visible_device=None, env: Optional[Dict[str, str]] = None,
+                 gpu_init: str = "first-cell"):
+        if gpu_init not in ("first-cell", "before-ready"):
+            raise ValueError(f"gpu_init: {gpu_init!r}")
         self.host = host
         self.matmul = matmul
+        self.gpu_init = gpu_init
         self.ready_timeout_s = ready_timeout_s
         self.probe_interval_s = probe_interval_s
         # node GPU index → the HIP device id the process should see (a 1-GPU box hosts all
@@ -71,6 +77,7 @@ class ProcessContainerRuntime(ContainerRuntime):
         proc = await asyncio.create_subprocess_exec(
             sys.executable, "-m", "odh_kubeflow_amd.testing.notebook_server.workbench", "--prefix", prefix,
             "--host", self.host, "--matmul", str(self.matmul if devices else 0),
+            "--gpu-init", self.gpu_init,
             env=child_env(env), cwd=ROOT, stdout=asyncio.subprocess.PIPE, stderr=asyncio.subprocess.DEVNULL)
         key = m.key(pod)
         self.procs[key] = proc
@@ -98,6 +105,21 @@ class ProcessContainerRuntime(ContainerRuntime):
         report["spawn_to_ready_ms"] = round((time.perf_counter() - t0) * 1e3, 1)
         self.reports[key] = report
         return ContainerHandle(key, devices, ip=self.host, port=port, info={"pid": proc.pid, "workbench": report})
+
+    async def first_cell(self, key: str, timeout_s: Optional[float] = None) -> dict:
+        """Wait for the workbench of pod ``key`` to finish its first cell (``first-cell``
+        mode) and return the cell's timings; in ``before-ready`` mode the start-up report
+        already holds them.  Call before the pod is stopped (``stop`` drains stdout)."""
+        report = self.reports[key]
+        if self.gpu_init == "before-ready" or "first_cell" in report:
+            return report.get("first_cell", report)
+        proc = self.procs[key]
+        line = await asyncio.wait_for(proc.stdout.readline(), timeout_s or self.ready_timeout_s)
+        cell = json.loads(line.decode() or "{}").get("first_cell")
+        if cell is None:
+            raise RuntimeError(f"workbench of {key} exited before its first cell (rc={proc.returncode})")
+        report["first_cell"] = cell
+        return cell
 
     async def stop(self, handle: ContainerHandle) -> None:
         proc = self.procs.get(handle.pod_key)

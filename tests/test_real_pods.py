@@ -1,8 +1,9 @@
 """Notebook pods whose container is a real PyTorch-ROCm workbench process
 (``kubelet/process_runtime.py`` + ``notebook_server/workbench.py``): BASELINE configs #2/#3
-without an image registry.  The CPU test runs the process without GPU work; the GPU test
-has it initialise HIP on the allocated MI355X and run its first bf16 matmul before the
-readiness probe answers."""
+without an image registry.  The CPU tests run the process without GPU work; the GPU test
+has its first cell initialise HIP on the allocated MI355X and run a bf16 matmul.  In the
+default ``first-cell`` mode the server is Ready before that cell (JupyterLab's behaviour);
+``before-ready`` holds readiness until the cell has run."""
 
 import aiohttp
 import pytest
@@ -14,11 +15,11 @@ from odh_kubeflow_amd.models import meta as m
 from odh_kubeflow_amd.models.notebook import notebook
 
 
-async def _lifecycle(matmul: int, gpus: int = 1):
+async def _lifecycle(matmul: int, gpus: int = 1, gpu_init: str = "first-cell"):
     rts = []
 
     def factory(d):
-        rt = ProcessContainerRuntime(matmul=matmul, visible_device=lambda _d: 0)
+        rt = ProcessContainerRuntime(matmul=matmul, visible_device=lambda _d: 0, gpu_init=gpu_init)
         rts.append(rt)
         return rt
 
@@ -30,6 +31,13 @@ async def _lifecycle(matmul: int, gpus: int = 1):
         assert await cl.wait_for(lambda: cl.notebook_ready("wb", "user"), 240)
         pod = cl.store.peek(kinds.POD, "wb-0", "user")
         ep = m.annotations(pod)["amd.com/notebook-endpoint"]
+        (rt,) = [rt for rt in rts if "user/wb-0" in rt.reports]
+        ready = rt.reports["user/wb-0"]
+        assert ready["gpu_init"] == gpu_init
+        if gpu_init == "first-cell":
+            assert "import_torch_ms" not in ready  # Ready came before the cell imported PyTorch
+        cell = await rt.first_cell("user/wb-0", 240)
+        assert cell["import_torch_ms"] > 0
         async with aiohttp.ClientSession(timeout=aiohttp.ClientTimeout(total=10)) as s:
             async with s.get(f"http://{ep}/notebook/user/wb/api") as r:
                 info = await r.json()
@@ -41,8 +49,9 @@ async def _lifecycle(matmul: int, gpus: int = 1):
         return info
 
 
-def test_workbench_process_pod_becomes_ready_cpu(run):
-    info = run(_lifecycle(matmul=0), timeout=300)
+@pytest.mark.parametrize("gpu_init", ["first-cell", "before-ready"])
+def test_workbench_process_pod_becomes_ready_cpu(run, gpu_init):
+    info = run(_lifecycle(matmul=0, gpu_init=gpu_init), timeout=300)
     assert info["torch"] and info["gpu"] is None and info["import_torch_ms"] > 0
 
 

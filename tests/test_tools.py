@@ -96,3 +96,32 @@ def test_critical_path_from_audit_log(run, tmp_path):
     assert any(k.endswith(" create statefulsets") and v == 1.0 for k, v in by.items()), by
     assert any(k.endswith(" create notebooks") and v == 1.0 for k, v in by.items()), by
     assert w["total"] == pytest.approx(sum(by.values()), abs=0.1)
+
+
+def test_critical_path_skips_an_optional_hop_that_is_not_on_the_path():
+    """A notebook whose image-pull lock was gone before kf created its StatefulSet (replicas 1
+    at once) has no lock-release hop; a later Notebook patch (finalizers) must not be taken
+    for one, or the rest of its path is lost."""
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    try:
+        import critical_path
+    finally:
+        sys.path.pop(0)
+    import json
+
+    def ev(t, verb, res, name, sub=""):
+        ts = f"2026-01-01T00:00:00.{t:03d}000Z"
+        ts_done = f"2026-01-01T00:00:00.{t:03d}500Z"
+        ref = {"resource": res, "namespace": "bench-0", "name": name, **({"subresource": sub} if sub else {})}
+        return json.dumps({"stage": "ResponseComplete", "verb": verb, "objectRef": ref, "userAgent": "x/1",
+                           "responseStatus": {"code": 200}, "requestReceivedTimestamp": ts,
+                           "stageTimestamp": ts_done})
+
+    lines = [ev(1, "create", "notebooks", "nb"), ev(2, "patch", "notebooks", "nb"),  # lock gone early
+             ev(3, "create", "statefulsets", "nb"), ev(4, "create", "pods", "nb-0"),
+             ev(5, "patch", "notebooks", "nb"),  # finalizer patch, after the pod exists
+             ev(6, "create", "pods", "nb-0", "binding"), ev(7, "patch", "pods", "nb-0", "status"),
+             ev(8, "update", "statefulsets", "nb", "status"), ev(9, "patch", "notebooks", "nb", "status")]
+    out = critical_path.analyse(lines, "bench-")
+    assert out["notebooks"] == 1
+    assert "lock_release" not in out["hops"] and out["hops"]["pod_create"]

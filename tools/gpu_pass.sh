@@ -17,6 +17,7 @@
 #   webhook  BASELINE config #4 (tools/bench_webhook.py)
 #   culling  BASELINE config #5 (tools/bench_culling.py)
 #   realpods BASELINE configs #2/#3: 1 and 8 notebooks whose container is a real PyTorch-ROCm process
+#   realbr   configs #2/#3 with the workbench's first GPU cell before Ready (--gpu-init before-ready)
 #   realref  the same with the reference's serialising odh path (--reference-emulation)
 #   refemu   bench.py --reference-emulation (control-plane lifecycle, reference behaviour)
 #   cpprof   cProfile of the control-plane and node-platform processes over a 300-step bench (pstats top 40)
@@ -147,6 +148,10 @@ PY
       timeout -k 10 400 python tools/bench_real_pods.py --notebooks 1,8 --repeats 5 > "$out/realpods.log" 2>&1 \
         || fail realpods $? "$out/realpods.log"
       grep '^{' "$out/realpods.log" ;;
+    realbr)
+      timeout -k 10 400 python tools/bench_real_pods.py --notebooks 1,8 --repeats 5 --gpu-probe off \
+        --gpu-init before-ready > "$out/realpods_before_ready.log" 2>&1 || fail realbr $? "$out/realpods_before_ready.log"
+      grep '^{' "$out/realpods_before_ready.log" ;;
     realref)
       timeout -k 10 400 python tools/bench_real_pods.py --notebooks 1,8 --repeats 1 --reference-emulation \
         > "$out/realpods_ref.log" 2>&1 || fail realref $? "$out/realpods_ref.log"

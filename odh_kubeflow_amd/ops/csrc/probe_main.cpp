@@ -8,7 +8,11 @@ extern "C" int odh_probe_cli(int argc, char** argv);
 int main(int argc, char** argv) {
   const int rc = odh_probe_cli(argc, argv);
   // the verdict is written and flushed: leave without the HIP runtime's exit-time teardown
-  // (the kernel driver reclaims the process's GPU state) — it only delays the notebook's start
+  // (the kernel driver reclaims the process's GPU state) — it only delays the notebook's start.
+  // ODH_PROBE_EXIT_NORMALLY=1 returns through exit(): a tool that writes its results from an
+  // exit handler (rocprofv3) needs that
   std::fflush(nullptr);
+  const char* normal = std::getenv("ODH_PROBE_EXIT_NORMALLY");
+  if (normal && *normal == '1') return rc;
   std::_Exit(rc);
 }

@@ -137,7 +137,7 @@ async def run_n(n: int, repeats: int, emu: bool, matmul: int, probe: bool, gpu_i
             # Ready, then the user's first cell (torch import, HIP init, matmul) finished
             "create_to_first_gpu_cell_ms": {"p50": pct(cell, .5), "p95": pct(cell, .95), "max": pct(cell, 1)},
             "control_plane_ms_p50": pct(cp, .5), "pod_start_ms_p50": pct(start, .5), "workbench": wb,
-            "gpu": (reports[0].get("gpu") if reports else None)}
+            "gpu": ((reports[0].get("first_cell") or reports[0]).get("gpu") if reports else None)}
 
 
 def main(argv=None) -> int:

@@ -161,7 +161,7 @@ PY
         > "$out/bench_refemu.log" 2>&1 || fail refemu $? "$out/bench_refemu.log"
       show "$out/bench_refemu.log" "refemu" ;;
     prof)
-      timeout -k 10 120 rocprofv3 --kernel-trace --stats -d "$out/prof" -o run -- \
+      ODH_PROBE_EXIT_NORMALLY=1 timeout -k 10 120 rocprofv3 --kernel-trace --stats -d "$out/prof" -o run -- \
         odh_kubeflow_amd/ops/_lib/odh-gpu-probe --json - > "$out/probe_prof.log" 2>&1 || fail prof $? "$out/probe_prof.log"
       db=$(find "$out/prof" -name '*results.db' | head -1)
       if [ -n "$db" ]; then
@@ -175,7 +175,7 @@ PY
                    "SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_LDS_UNALIGNED_STALL" \
                    "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum"; do
         i=$((i + 1))
-        timeout -s KILL 90 rocprofv3 --pmc $group --output-format csv -d "$out/pmc$i" -o run -- \
+        ODH_PROBE_EXIT_NORMALLY=1 timeout -s KILL 90 rocprofv3 --pmc $group --output-format csv -d "$out/pmc$i" -o run -- \
           python3 tools/probe_microbench.py --pmc-pass > "$out/pmc$i.log" 2>&1 || fail "pmc$i" $? "$out/pmc$i.log"
       done
       echo "pmc passes: $i" ;;

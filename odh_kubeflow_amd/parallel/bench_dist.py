@@ -129,10 +129,13 @@ def measure(args) -> Optional[dict]:
             out["config"]["parallelism"] = (f"one kf manager + one odh manager process for all {world} ranks' "
                                             f"notebooks, as config/overlays/mi355x deploys them")
             out["config"]["architecture"] = "cmd/kf_manager + cmd/odh_manager (overlay mi355x, reference topology)"
-        out["config"]["platform_stand_ins"] = ("native C++ apiserver (+GC); ONE scheduler (first-free amd.com/gpu "
-                                               "allocation), ONE StatefulSet controller and ONE kubelet process for "
-                                               "the node's 8 GPUs")
+        w = (world + 1) // 2
+        out["config"]["platform_stand_ins"] = (f"native C++ apiserver (+GC); ONE scheduler (first-free amd.com/gpu "
+                                               f"allocation); the node's StatefulSet controller and kubelet for its "
+                                               f"8 GPUs, each as {w} worker process{'es' if w > 1 else ''} "
+                                               f"(namespaces partitioned)")
         out["rank_ms_per_step"] = res.get("rank_ms_per_step")
+        out["lifecycle_ms_per_20_steps"] = res.get("lifecycle_ms_per_20_steps")
         out["cpu_ms_per_step"] = res.get("cpu_ms_per_step")
         out["child_rss_mib"] = res.get("child_rss_mib")
         out["cpu_binding"] = binding or "none (ODH_BENCH_NUMA_BIND=0, or no GPU NUMA information)"
@@ -424,7 +427,12 @@ async def _drive(args, shard, dist, torch, children: Optional[dict] = None, nati
     el = torch.tensor([elapsed], dtype=torch.float64)
     await _in_thread(lambda: dist.all_reduce(el, op=dist.ReduceOp.MAX))
     gathered = [None] * dist.get_world_size()
+    # this rank's lifecycle time (create → Ready → gone) per block of 20 timed steps: whether
+    # the first steps of the window run slower than the rest (warm-up of the host, not the code)
+    life = [a + b for a, b in zip(lat_ms, teardown_ms)]
+    blocks = [round(statistics.fmean(life[i:i + 20]), 3) for i in range(0, len(life), 20)]
     await _in_thread(dist.all_gather_object, gathered, {"lat": lat_ms, "teardown": teardown_ms, "own_s": own,
+                                                        "blocks": blocks,
                                                         "cpu": cpu, "rss": rss, "in_window": in_window,
                                                         "settled": settled, "idle": idle, "probe": samples})
     per_step = 1e3 / max(1, args.steps)
@@ -441,4 +449,5 @@ async def _drive(args, shard, dist, torch, children: Optional[dict] = None, nati
             "child_rss_mib": {k: v for g in gathered for k, v in g["rss"].items()},
             "apiserver_profile_per_step": prof, "breakdown": merge_breakdowns(g["settled"] for g in gathered),
             "quiesced": all(g["idle"] for g in gathered),
-            "probe_sample": [s for g in gathered for s in g["probe"]]}
+            "probe_sample": [s for g in gathered for s in g["probe"]],
+            "lifecycle_ms_per_20_steps": [round(statistics.fmean(b), 3) for b in zip(*(g["blocks"] for g in gathered))]}

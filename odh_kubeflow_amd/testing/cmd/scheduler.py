@@ -32,8 +32,9 @@ def parse(argv=None):
     p = argparse.ArgumentParser(prog="odh-scheduler")
     p.add_argument("--master", default=None)
     p.add_argument("--kubeconfig", default=None)
-    p.add_argument("--max-concurrent", type=int, default=1,
-                   help="scheduling decisions are serialised by the allocator lock anyway")
+    p.add_argument("--max-concurrent", type=int, default=8,
+                   help="scheduler workers: decisions are serialised by the allocator lock, the binds "
+                        "(apiserver round trips) run concurrently")
     p.add_argument("--controllers", default="scheduler",
                    help="comma list of scheduler (kube-scheduler + device allocation) and statefulset "
                         "(kube-controller-manager's StatefulSet controller)")

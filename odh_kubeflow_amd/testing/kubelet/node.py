@@ -150,10 +150,31 @@ class SchedulerController:
             return Result()
         if m.uid(pod) in self._assumed:
             return Result()  # bound already; the cache has not caught up yet
-        async with self._lock:  # allocation decisions must not race each other
-            return await self._schedule(pod)
+        async with self._lock:  # scheduling cycle: allocation decisions must not race each other
+            bind = await self._schedule(pod)
+        if isinstance(bind, Result):
+            return bind
+        # binding cycle, outside the lock (kube-scheduler binds asynchronously): the
+        # assumption already holds the pod's devices, so the next pod is decided meanwhile
+        node_name, patch, ids = bind
+        try:
+            await self.client.patch(kinds.POD, patch, name=m.name(pod), namespace=m.namespace(pod))
+        except ApiError as e:
+            self.forget(pod)  # unreserve
+            if is_not_found(e):
+                return Result()
+            raise
+        except BaseException:
+            self.forget(pod)
+            raise
+        self.bound += 1
+        self.recorder.event(pod, "Normal", "Scheduled",
+                            f"Successfully assigned {m.namespace(pod)}/{m.name(pod)} to {node_name}")
+        return Result()
 
-    async def _schedule(self, pod: dict) -> Result:
+    async def _schedule(self, pod: dict):
+        """Pick a node and devices; on success assume the pod there and return
+        ``(node name, bind patch, device ids)``, else report it unschedulable (a Result)."""
         need = _pod_requests(pod)
         sel = (pod.get("spec") or {}).get("nodeSelector") or {}
         reasons: List[str] = []
@@ -185,17 +206,8 @@ class SchedulerController:
                 # first GPU, so a per-GPU node agent can watch just its own pods
                 patch["metadata"] = {"annotations": {GPU_IDS_ANNOTATION: ",".join(map(str, ids))},
                                      "labels": {GPU_INDEX_LABEL: str(ids[0])}}
-            try:
-                await self.client.patch(kinds.POD, patch, name=m.name(pod), namespace=m.namespace(pod))
-            except ApiError as e:
-                if is_not_found(e):
-                    return Result()
-                raise
-            self.bound += 1
             self._assumed[m.uid(pod)] = (m.name(node), need["cpu"], need["memory"], tuple(ids))
-            self.recorder.event(pod, "Normal", "Scheduled",
-                                f"Successfully assigned {m.namespace(pod)}/{m.name(pod)} to {m.name(node)}")
-            return Result()
+            return m.name(node), patch, ids
         # unschedulable
         counts: Dict[str, int] = {}
         for r in reasons:
@@ -215,7 +227,7 @@ class SchedulerController:
             self.recorder.event(pod, "Warning", "FailedScheduling", msg)
         return Result(requeue_after=1.0)
 
-    def setup_with_manager(self, mgr, max_concurrent: int = 1):
+    def setup_with_manager(self, mgr, max_concurrent: int = 8):
         unbound = pred_funcs(create=lambda o: not (o.get("spec") or {}).get("nodeName"),
                              update=lambda o, old: not (o.get("spec") or {}).get("nodeName"),
                              delete=lambda o: False)

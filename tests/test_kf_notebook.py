@@ -1,5 +1,7 @@
 """kf NotebookReconciler: envtest-style integration tests (kf/controllers/*_test.go analogues)."""
 
+import pytest
+
 from odh_kubeflow_amd.testing.cluster import ClusterConfig, LocalCluster
 from odh_kubeflow_amd.controllers.notebook import (create_notebook_status, generate_service, generate_statefulset,
                                                    generate_virtual_service, nb_name_from_involved_object)
@@ -319,3 +321,57 @@ def test_pod_ready_seconds_start_time_rule():
     t0 = parse_rfc3339("2026-01-01T00:00:00Z")
     assert mt.observe_ready(nb, first, now=t0 + 30) == 30  # first pod: from the Notebook's creation
     assert mt.observe_ready(nb, resumed, now=t0 + 86400 + 7) == 7  # resumed: from the pod's creation
+
+
+def test_scheduler_binds_concurrently_and_unreserves_a_failed_bind(run):
+    """Scheduling decisions are serial (the allocator lock) but binds run concurrently: a
+    slow bind does not hold the next pod's decision, the assumption keeps the two apart, and
+    a bind that fails releases its devices (kube-scheduler's assume / unreserve)."""
+    import asyncio
+
+    from odh_kubeflow_amd.models.errors import ApiError
+    from odh_kubeflow_amd.testing.kubelet.node import SchedulerController
+
+    node = {"apiVersion": "v1", "kind": "Node", "metadata": {"name": "n0", "labels": {}},
+            "status": {"allocatable": {"amd.com/gpu": "2"}}}
+
+    def pod(name):
+        return {"apiVersion": "v1", "kind": "Pod", "metadata": {"name": name, "namespace": "u", "uid": "uid-" + name},
+                "spec": {"containers": [{"name": "c", "resources": {"limits": {"amd.com/gpu": "1"}}}]}}
+
+    pods = {p["metadata"]["name"]: p for p in (pod("a"), pod("b"), pod("c"))}
+
+    class Reader:
+        def get(self, kind, name, ns=None):
+            return pods.get(name)
+
+        def list(self, kind, fields=None, **_):
+            return [node] if kind == kinds.NODE else []  # the cache has seen no bind yet
+
+    gate = asyncio.Event()
+    binds = []
+
+    class Client:
+        async def patch(self, kind, patch, name=None, namespace=None, **_):
+            binds.append((name, patch["metadata"]["annotations"]["amd.com/gpu-ids"]))
+            if name == "a":
+                await gate.wait()  # a slow bind
+            if name == "b":
+                raise ApiError(409, "Conflict", "bind lost")
+
+    class Recorder:
+        def event(self, *a, **k):
+            pass
+
+    async def go():
+        s = SchedulerController(Client(), Reader(), Recorder())
+        ta = asyncio.create_task(s.reconcile(Request("u", "a")))
+        await asyncio.sleep(0)
+        with pytest.raises(ApiError):  # decided while a's bind is still in flight
+            await asyncio.wait_for(s.reconcile(Request("u", "b")), 2)
+        await asyncio.wait_for(s.reconcile(Request("u", "c")), 2)  # b's failed bind freed GPU 1
+        gate.set()
+        await ta
+        assert binds == [("a", "0"), ("b", "1"), ("c", "1")]
+        assert s.bound == 2 and set(s._assumed) == {"uid-a", "uid-c"}
+    run(go())

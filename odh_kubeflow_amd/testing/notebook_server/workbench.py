@@ -69,7 +69,10 @@ async def serve(prefix: str, host: str, info: dict, first_cell: int = -1) -> Non
     info["ready_ms"] = round((time.perf_counter() - T_PROC) * 1e3, 1)
     print(json.dumps({"port": srv.port, **info}), flush=True)
     if first_cell >= 0:
-        cell = await asyncio.to_thread(init_gpu, first_cell)
+        try:
+            cell = await asyncio.to_thread(init_gpu, first_cell)
+        except Exception as e:  # a failing cell does not take the server down
+            cell = {"error": f"{type(e).__name__}: {e}"}
         cell["first_cell_done_ms"] = round((time.perf_counter() - T_PROC) * 1e3, 1)
         info.update(cell)  # the dict GET <prefix>/api answers with
         print(json.dumps({"first_cell": cell}), flush=True)

@@ -86,24 +86,31 @@ def analyse(lines, ns_prefix: str = "") -> dict:
             writes[(ua or "?", v, res + ("/" + sub if sub else ""))] += 1
     hops = defaultdict(lambda: {"gap": [], "serve": [], "agents": defaultdict(int)})
     totals = []
+    for evs in by_obj.values():
+        evs.sort(key=lambda e: e[0])  # by arrival: the log is in completion order
+
     def find(ns, nb, i, after):
+        """The first request of hop ``i`` that arrived after ``after`` (the previous hop's
+        arrival).  Not after its completion: the apiserver commits — and the watchers see
+        the write — before it stamps the response, so under load the next hop can arrive
+        before the previous one's completion stamp."""
         _, verb, res, sub, name = STEPS[i]
         evs = by_obj.get((ns, res, name.format(nb=nb)), [])
         return next(((r, d, ua) for r, d, v, s, ua in evs
-                     if _match(verb, v) and _match(sub, s) and (after is None or r >= after - 1e-4)), None)
+                     if _match(verb, v) and _match(sub, s) and (after is None or r > after)), None)
 
     for ns, nb in notebooks:
-        prev_done = None
+        prev_done = prev_at = None
         t0 = None
         ok = True
         for i, (step, *_) in enumerate(STEPS):
-            hit = find(ns, nb, i, prev_done)
+            hit = find(ns, nb, i, prev_at)
             if hit is not None and step in OPTIONAL:
                 # an optional hop is on the path only if the next required hop follows it: a
                 # notebook whose lock was gone before kf created its StatefulSet has no
                 # lock-release / scale-up hop, and a later patch (finalizers) must not pose as one
                 nxt = next(j for j in range(i + 1, len(STEPS)) if STEPS[j][0] not in OPTIONAL)
-                if find(ns, nb, nxt, hit[1]) is None and find(ns, nb, nxt, prev_done) is not None:
+                if find(ns, nb, nxt, hit[0]) is None and find(ns, nb, nxt, prev_at) is not None:
                     hit = None
             if hit is None:
                 if step in OPTIONAL:
@@ -116,9 +123,9 @@ def analyse(lines, ns_prefix: str = "") -> dict:
             h = hops[step]
             h["serve"].append((d - r) * 1e3)
             if prev_done is not None:
-                h["gap"].append((r - prev_done) * 1e3)
+                h["gap"].append(max(0.0, r - prev_done) * 1e3)
             h["agents"][ua] += 1
-            prev_done = d
+            prev_done, prev_at = d, r
         if ok:
             totals.append((prev_done - t0) * 1e3)
     out = {"notebooks": len(totals), "create_to_notebook_status_ms": {"p50": pct(totals, .5), "p95": pct(totals, .95)},

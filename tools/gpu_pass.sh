@@ -8,6 +8,8 @@
 #   smoke    __graft_entry__.smoke()
 #   bench    bench.py at N=1: the driver's invocation (--steps 20 --warmup 5) twice, then 300 steps
 #   ranks    2/4-rank rehearsal of the N>1 launch on the one GPU (never 8: the driver owns N=8)
+#   b20x4    the driver's invocation four times in a row (first-run effects on a fresh box)
+#   pyc      precompile the package's bytecode (compileall) before the steps that follow
 #   unsharded  the default topology (one kf + one odh manager process) at 1, 2 and 4 ranks
 #   archab   interleaved A/B at N=1: shard as kf/odh process pair vs one process vs unsharded
 #   probeexe the odh-gpu-probe init-container program: 10 process runs (wall time, verdict)
@@ -66,6 +68,17 @@ for s in $steps; do
       timeout -k 10 200 python bench.py --gpus 1 --no-inprocess-baseline > "$out/bench_n1_s300.log" 2>&1 \
         || fail bench $? "$out/bench_n1_s300.log"
       show "$out/bench_n1_s300.log" "n1 steps300" ;;
+    b20x4)
+      for r in 1 2 3 4; do
+        echo "run $r start $(date +%s.%N)"
+        timeout -k 10 170 python bench.py --gpus 1 --steps 20 --warmup 5 > "$out/bench_x4_r$r.log" 2>&1 \
+          || fail b20x4 $? "$out/bench_x4_r$r.log"
+        show "$out/bench_x4_r$r.log" "x4 r$r"
+      done ;;
+    pyc)
+      timeout -k 10 120 python -m compileall -q odh_kubeflow_amd bench.py __graft_entry__.py > "$out/pyc.log" 2>&1 \
+        || fail pyc $? "$out/pyc.log"
+      echo "bytecode compiled" ;;
     unsharded)
       timeout -k 10 170 python bench.py --gpus 1 --arch unsharded --steps 100 --warmup 5 --probe-sample 0 \
         > "$out/bench_unsharded_n1.log" 2>&1 || fail unsharded $? "$out/bench_unsharded_n1.log"

@@ -9,6 +9,7 @@
 #   bench    bench.py at N=1: the driver's invocation (--steps 20 --warmup 5) twice, then 300 steps
 #   ranks    2/4-rank rehearsal of the N>1 launch on the one GPU (never 8: the driver owns N=8)
 #   b20x4    the driver's invocation four times in a row (first-run effects on a fresh box)
+#   s20v300  interleaved A/B on one box: the driver's 20-step invocation vs the 300-step run, 3 rounds
 #   pyc      precompile the package's bytecode (compileall) before the steps that follow
 #   unsharded  the default topology (one kf + one odh manager process) at 1, 2 and 4 ranks
 #   archab   interleaved A/B at N=1: shard as kf/odh process pair vs one process vs unsharded
@@ -74,6 +75,15 @@ for s in $steps; do
         timeout -k 10 170 python bench.py --gpus 1 --steps 20 --warmup 5 > "$out/bench_x4_r$r.log" 2>&1 \
           || fail b20x4 $? "$out/bench_x4_r$r.log"
         show "$out/bench_x4_r$r.log" "x4 r$r"
+      done ;;
+    s20v300)
+      for r in 1 2 3; do
+        timeout -k 10 170 python bench.py --gpus 1 --steps 20 --warmup 5 > "$out/bench_ab_s20_r$r.log" 2>&1 \
+          || fail s20v300 $? "$out/bench_ab_s20_r$r.log"
+        show "$out/bench_ab_s20_r$r.log" "s20 r$r"
+        timeout -k 10 200 python bench.py --gpus 1 --steps 300 --warmup 5 --no-inprocess-baseline \
+          > "$out/bench_ab_s300_r$r.log" 2>&1 || fail s20v300 $? "$out/bench_ab_s300_r$r.log"
+        show "$out/bench_ab_s300_r$r.log" "s300 r$r"
       done ;;
     pyc)
       timeout -k 10 120 python -m compileall -q odh_kubeflow_amd bench.py __graft_entry__.py > "$out/pyc.log" 2>&1 \

@@ -114,10 +114,17 @@ class ProcessContainerRuntime(ContainerRuntime):
         if self.gpu_init == "before-ready" or "first_cell" in report:
             return report.get("first_cell", report)
         proc = self.procs[key]
-        line = await asyncio.wait_for(proc.stdout.readline(), timeout_s or self.ready_timeout_s)
-        cell = json.loads(line.decode() or "{}").get("first_cell")
-        if cell is None:
-            raise RuntimeError(f"workbench of {key} exited before its first cell (rc={proc.returncode})")
+        deadline = time.perf_counter() + (timeout_s or self.ready_timeout_s)
+        cell = None
+        while cell is None:  # skip anything else a library printed to stdout meanwhile
+            line = await asyncio.wait_for(proc.stdout.readline(), max(0.0, deadline - time.perf_counter()))
+            if not line:
+                raise RuntimeError(f"workbench of {key} exited before its first cell (rc={proc.returncode})")
+            try:
+                msg = json.loads(line.decode())
+            except ValueError:
+                continue
+            cell = msg.get("first_cell") if isinstance(msg, dict) else None
         report["first_cell"] = cell
         return cell
 

@@ -96,7 +96,9 @@ async def run_n(n: int, repeats: int, emu: bool, matmul: int, probe: bool, gpu_i
             cell_at = {}
 
             async def cell_done(nm):
-                rt = next(rt for rt in rts if f"bench/{nm}-0" in rt.reports)
+                rt = next((rt for rt in rts if f"bench/{nm}-0" in rt.reports), None)
+                if rt is None:
+                    raise RuntimeError(f"no workbench report for bench/{nm}-0")
                 await rt.first_cell(f"bench/{nm}-0", 300)
                 cell_at[nm] = time.perf_counter()
 

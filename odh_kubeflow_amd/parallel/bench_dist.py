@@ -374,13 +374,16 @@ async def _drive(args, shard, dist, torch, children: Optional[dict] = None, nati
             lat_ms.append(ready_s * 1e3)
             teardown_ms.append(gone_s * 1e3)
 
+    from ..utils import gctune
+
+    # the driver process's collector pause (a full collection walks torch's ~1M objects,
+    # tens of ms) goes before the warm-up: between warm-up and timed steps it left every
+    # control-plane process idle long enough to start the timed window cold
+    gctune.tune()
     for _ in range(args.warmup):
         await one_step(False)
     await _in_thread(dist.barrier)  # every rank's warm-up done (unsharded: one control plane for all)
     await shard.quiesce()
-    from ..utils import gctune
-
-    gctune.tune()
     if torch.cuda.is_available():
         torch.cuda.synchronize()
     await _in_thread(dist.barrier)

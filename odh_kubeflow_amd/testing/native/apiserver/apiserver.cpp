@@ -642,6 +642,13 @@ struct PendingWake {
   bool all;
 };
 thread_local std::vector<PendingWake> t_wake;
+// Owners removed by this thread whose dependents the garbage collector has yet to delete:
+// the cascade runs after the removing commit has released the store lock (each owner's
+// dependents under a lock of their own, still before the request is answered), so a
+// finalizer-removal update or a delete holds the lock for its own object only.
+thread_local std::vector<std::string> t_gc;
+thread_local bool t_gc_running = false;
+void run_gc() noexcept;
 
 void flush_wakes() {
   std::vector<PendingWake> ws;
@@ -677,6 +684,7 @@ struct StoreLock {
     P.lock_hold_ns[t_cat] += mono_ns() - t_acq;  // who keeps the others waiting
     S.mu.unlock();
     if (!t_wake.empty()) flush_wakes();
+    if (!t_gc.empty() && !t_gc_running) run_gc();
   }
   StoreLock(const StoreLock&) = delete;
   StoreLock& operator=(const StoreLock&) = delete;
@@ -1975,7 +1983,7 @@ void remove_locked(const Res& r, Obj live, Value final) {
   S.writes++;
   auto fp = std::make_shared<const Value>(std::move(final));
   emit(r, "DELETED", fp, live);
-  if (S.gc) gc_dependents(uid);
+  if (S.gc) t_gc.push_back(uid);  // cascaded once the lock is released (run_gc)
   // foreground owners waiting for their last dependent
   if (S.gc) {
     const Value* refs = md(*fp) ? md(*fp)->get("ownerReferences") : nullptr;
@@ -2050,6 +2058,23 @@ void gc_dependents(const std::string& owner_uid) {
     if (other_live) continue;
     sync_delete_locked(*r, std::get<1>(d), std::get<2>(d));
   }
+}
+
+void run_gc() noexcept {
+  t_gc_running = true;
+  while (!t_gc.empty()) {
+    std::vector<std::string> uids;
+    uids.swap(t_gc);
+    for (auto& u : uids) {
+      try {
+        StoreLock g;  // its release does not recurse (t_gc_running); new owners queue up here
+        gc_dependents(u);
+      } catch (...) {
+        // a dependent that vanished meanwhile: nothing left to collect for it
+      }
+    }
+  }
+  t_gc_running = false;
 }
 
 Value do_delete(const Res& r, const std::string& ns_, const std::string& name, const Value& opts) {

@@ -148,6 +148,30 @@ def test_gc_collects_dependent_of_absent_owner(run, server_kind):
     run(go())
 
 
+def test_gc_cascade_is_done_when_the_owner_delete_answers(run, server_kind):
+    """Background deletion of an owner collects its dependents and theirs (two levels)
+    before the DELETE is answered — on the native server the cascade runs after the owner's
+    commit has released the store lock, still inside the request."""
+    async def go():
+        srv, c = await _server(server_kind)
+        try:
+            await c.create({"apiVersion": "v1", "kind": "Namespace", "metadata": {"name": "gc2"}})
+            owner = await c.create(_cm("top", "gc2"))
+
+            def ref(o):
+                return {"apiVersion": "v1", "kind": "ConfigMap", "name": m.name(o), "uid": m.uid(o), "controller": True}
+            mids = [await c.create(_cm(f"mid{i}", "gc2", owner=ref(owner))) for i in range(3)]
+            for i, mid in enumerate(mids):
+                await c.create(_cm(f"leaf{i}", "gc2", owner=ref(mid)))
+            await c.delete(kinds.CONFIG_MAP, "top", "gc2")
+            left = {m.name(o) for o in await c.list(kinds.CONFIG_MAP, "gc2")} - {"kube-root-ca.crt"}
+            assert left == set(), left
+        finally:
+            await c.close()
+            await srv.stop()
+    run(go())
+
+
 class _StaleReader(StoreReader):
     """Returns a frozen (stale) copy of every object."""
 

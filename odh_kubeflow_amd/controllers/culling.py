@@ -42,8 +42,13 @@ memory on a shared GPU never keeps it alive).
 Missing telemetry is never read as idleness: with no GPU samples the Jupyter signal is
 used, and with neither the last-activity annotation is simply left alone (as the
 reference does for HTTP errors, :258-270).  A Pending pod (image pull, init containers)
-is not checked at all, and the idle clock starts no earlier than the pod's Ready
-transition: start-up time is not idle time.
+is not checked while it is plausibly still starting — younger than ``CULL_IDLE_TIME`` plus
+``CULL_STARTUP_ALLOWANCE`` (minutes, default 10) and not stuck — and the idle clock of a
+new pod starts no earlier than its first Ready transition: start-up time is not idle time.
+A pod that cannot start (an init container such as ``amd-gpu-probe`` in back-off, an image
+pull failing) or that outlived that bound holds its ``amd.com/gpu`` devices for nothing: it
+is checked like any other pod, its idle clock running from the pod's creation, so a bad
+GPU or a typo'd image never pins an MI355X for good.
 
 Fixes over the reference: the two culling metrics are exported; the configuration is
 an object (no package globals); sub-minute periods are available through
@@ -94,6 +99,7 @@ class CullerConfig:
     gpu_agent_token_file: str = ""  # bearer token for the node agent (nodeagent/auth.py); "" = none
     gpu_vram_active_bytes: float = 0.0  # 0: resident VRAM is not activity (see module docstring)
     http_timeout_s: float = 10.0
+    startup_allowance_s: float = 600.0  # a Pending pod younger than cull_idle_time + this is not checked
 
     @classmethod
     def from_env(cls, env: Mapping[str, str] = os.environ) -> "CullerConfig":
@@ -121,6 +127,9 @@ class CullerConfig:
         c.gpu_agent_port = int(env_default(env, "CULLING_GPU_AGENT_PORT", "9464"))
         c.gpu_agent_token_file = env.get("CULLING_GPU_AGENT_TOKEN_FILE", "")
         c.gpu_vram_active_bytes = float(env_default(env, "CULLING_GPU_VRAM_ACTIVE_BYTES", "0"))
+        c.startup_allowance_s = float(env_default(env, "CULL_STARTUP_ALLOWANCE", "10")) * 60.0
+        if env.get("CULL_STARTUP_ALLOWANCE_SECONDS"):
+            c.startup_allowance_s = float(env["CULL_STARTUP_ALLOWANCE_SECONDS"])
         return c
 
 
@@ -136,10 +145,10 @@ def annotations_exist(nb: dict) -> bool:
     return LAST_ACTIVITY_ANNOTATION in a and LAST_ACTIVITY_CHECK_TIMESTAMP_ANNOTATION in a
 
 
-def initialize_annotations(nb: dict) -> None:
+def initialize_annotations(nb: dict, last_activity: Optional[str] = None) -> None:
     t = rfc3339()
     a = m.ensure_annotations(nb)
-    a[LAST_ACTIVITY_ANNOTATION] = t
+    a[LAST_ACTIVITY_ANNOTATION] = last_activity or t
     a[LAST_ACTIVITY_CHECK_TIMESTAMP_ANNOTATION] = t
 
 
@@ -230,8 +239,37 @@ def set_stop_annotation(nb: dict, metrics=None) -> None:
 
 def pod_is_starting(pod: dict) -> bool:
     """Pending: scheduling, image pull, init containers (``odh-gpu-probe``).  Nothing of the
-    notebook runs yet, so nothing of it can be idle."""
+    notebook runs yet, so nothing of it can be idle — for a while (:func:`pod_start_stuck`,
+    :meth:`CullingReconciler.reconcile`)."""
     return (pod.get("status") or {}).get("phase") == "Pending"
+
+
+# container waiting reasons the kubelet reports for a start that will not succeed by itself
+STUCK_WAITING_REASONS = frozenset({
+    "CrashLoopBackOff", "ImagePullBackOff", "ErrImagePull", "ErrImageNeverPull", "InvalidImageName",
+    "CreateContainerConfigError", "CreateContainerError", "RunContainerError"})
+
+
+def pod_start_stuck(pod: dict) -> bool:
+    """The pod is Pending because something failed, not because it is still working: an init
+    container exited non-zero (the kubelet restarts it with back-off — ``amd-gpu-probe`` on a bad
+    GPU) or any container waits on a failing image pull / config."""
+    st = pod.get("status") or {}
+    for cs in st.get("initContainerStatuses") or []:
+        state = cs.get("state") or {}
+        if (state.get("waiting") or {}).get("reason") in STUCK_WAITING_REASONS:
+            return True
+        term = state.get("terminated") or (cs.get("lastState") or {}).get("terminated") or {}
+        if term.get("exitCode") not in (None, 0):
+            return True
+    for cs in st.get("containerStatuses") or []:
+        if ((cs.get("state") or {}).get("waiting") or {}).get("reason") in STUCK_WAITING_REASONS:
+            return True
+    return False
+
+
+def pod_created_at(pod: dict) -> Optional[float]:
+    return parse_rfc3339((pod.get("metadata") or {}).get("creationTimestamp"))
 
 
 def pod_ready_since(pod: dict) -> Optional[float]:
@@ -243,12 +281,27 @@ def pod_ready_since(pod: dict) -> Optional[float]:
 
 
 def update_from_pod_start(nb: dict, pod: dict) -> None:
-    """The idle clock starts no earlier than the server: a last-activity stamp older than
-    the pod's Ready transition is moved up to it."""
+    """The idle clock of a new pod starts no earlier than its server: a last-activity stamp
+    older than the pod itself (left by an earlier pod of the notebook — a restart, a resume)
+    is moved up to the pod's Ready transition.  Once per pod: after that the stamp is newer
+    than the pod's creation, so a flapping readiness probe or a container restart (each a new
+    Ready transition) never resets the clock again."""
     t = pod_ready_since(pod)
     a = parse_rfc3339(m.annotations(nb).get(LAST_ACTIVITY_ANNOTATION))
-    if t is not None and a is not None and t > a:
-        m.ensure_annotations(nb)[LAST_ACTIVITY_ANNOTATION] = rfc3339(t)
+    born = pod_created_at(pod)
+    if t is None or a is None or t <= a:
+        return
+    if born is not None and a >= born:
+        return  # this pod's clock has started already
+    m.ensure_annotations(nb)[LAST_ACTIVITY_ANNOTATION] = rfc3339(t)
+
+
+def update_from_pod_creation(nb: dict, pod: dict) -> None:
+    """A pod that never got going (stuck or over-long start): idle since it was created."""
+    born = pod_created_at(pod)
+    a = parse_rfc3339(m.annotations(nb).get(LAST_ACTIVITY_ANNOTATION))
+    if born is not None and (a is None or a < born):
+        m.ensure_annotations(nb)[LAST_ACTIVITY_ANNOTATION] = rfc3339(born)
 
 
 def pod_requests_gpu(pod: Optional[dict]) -> bool:
@@ -475,14 +528,26 @@ class CullingReconciler:
         if pod is None:
             if any(k in m.annotations(nb) for k in (LAST_ACTIVITY_ANNOTATION, LAST_ACTIVITY_CHECK_TIMESTAMP_ANNOTATION)):
                 await self._update(req, remove_annotations)
-            return Result()
-        if pod_is_starting(pod):
+            # the reference waits for the next Notebook event (its unconditional status write
+            # follows the pod's creation); status writes are gated on change here, and a pod
+            # that never leaves Pending changes no status, so look again after a period
+            return Result(requeue_after=self.cfg.check_period_s)
+        starting = pod_is_starting(pod)
+        if starting:
             # Unlike the reference (:86-203), the idle clock waits for the server: an image
             # pull or init container slower than CULL_IDLE_TIME would otherwise cull a
-            # notebook nobody could use yet (no Jupyter, no GPU process to sample)
-            return Result(requeue_after=self.cfg.check_period_s)
+            # notebook nobody could use yet (no Jupyter, no GPU process to sample).  But only
+            # while it may still come up: a start that failed (init container in back-off,
+            # image pull failing) or outlived CULL_IDLE_TIME + CULL_STARTUP_ALLOWANCE holds the
+            # pod's GPUs for nothing, and is culled from the pod's creation on.
+            born = pod_created_at(pod)
+            young = born is None or now() - born < self.cfg.cull_idle_time_s + self.cfg.startup_allowance_s
+            if young and not pod_start_stuck(pod):
+                return Result(requeue_after=self.cfg.check_period_s)
         if not annotations_exist(nb):
-            await self._update(req, initialize_annotations)
+            born = pod_created_at(pod) if starting else None
+            await self._update(req, lambda cur: initialize_annotations(
+                cur, rfc3339(born) if born is not None else None))
             nb = await self.client.get(kinds.NOTEBOOK_V1BETA1, req.name, req.namespace)
         if not culling_check_period_has_passed(nb, self.cfg.check_period_s):
             return Result(requeue_after=self.cfg.check_period_s)
@@ -499,7 +564,10 @@ class CullingReconciler:
             else:
                 update_from_kernels(cur, kernels)
                 update_from_terminals(cur, terminals)
-                update_from_pod_start(cur, pod)
+                if starting:
+                    update_from_pod_creation(cur, pod)
+                else:
+                    update_from_pod_start(cur, pod)
             update_check_timestamp(cur)
             if notebook_is_idle(cur, self.cfg.cull_idle_time_s):
                 set_stop_annotation(cur, self.metrics)

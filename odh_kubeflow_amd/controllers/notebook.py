@@ -285,11 +285,14 @@ def generate_virtual_service(nb: dict, env: Mapping[str, str] = os.environ) -> d
     headers = {}
     raw = ann.get(ANNOTATION_HEADERS_REQUEST_SET)
     if raw:
+        # json.Unmarshal into map[string]string (:605-613): a number or an object value is a
+        # type error and the whole map falls back to {}; a null value is the zero string
         try:
             parsed = json.loads(raw)
-            headers = {str(k): str(v) for k, v in parsed.items()} if isinstance(parsed, dict) else {}
-        except (ValueError, AttributeError):
-            headers = {}
+        except ValueError:
+            parsed = None
+        if isinstance(parsed, dict) and all(v is None or isinstance(v, str) for v in parsed.values()):
+            headers = {k: "" if v is None else v for k, v in parsed.items()}
     return {
         "apiVersion": "networking.istio.io/v1alpha3", "kind": "VirtualService",
         "metadata": {"name": virtual_service_name(name, ns), "namespace": ns},

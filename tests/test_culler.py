@@ -117,6 +117,43 @@ def test_start_up_time_is_not_idle_time():
     assert m.annotations(nb)[LAST_ACTIVITY_ANNOTATION] == old
 
 
+def test_ready_flaps_do_not_reset_the_idle_clock():
+    """Once per pod: a readiness probe that flaps, or a container restart, is a new Ready
+    transition of the same pod; the clock it started is not moved again.  A new pod of the
+    notebook (restart annotation, resume) starts it once more."""
+    born = rfc3339(time.time() - 3600)
+    first_ready, stamp, flap = (rfc3339(time.time() - x) for x in (3500, 1800, 5))
+    pod = {"metadata": {"creationTimestamp": born}, "status": {"phase": "Running", "conditions": [
+        {"type": "Ready", "status": "True", "lastTransitionTime": flap}]}}
+    nb = nbmeta({LAST_ACTIVITY_ANNOTATION: stamp})  # newer than the pod: its clock runs already
+    c.update_from_pod_start(nb, pod)
+    assert m.annotations(nb)[LAST_ACTIVITY_ANNOTATION] == stamp
+    older = rfc3339(time.time() - 7200)  # left by the notebook's previous pod
+    pod["status"]["conditions"][0]["lastTransitionTime"] = first_ready
+    nb = nbmeta({LAST_ACTIVITY_ANNOTATION: older})
+    c.update_from_pod_start(nb, pod)
+    assert m.annotations(nb)[LAST_ACTIVITY_ANNOTATION] == first_ready
+
+
+def test_stuck_start_detection():
+    assert not c.pod_start_stuck({"status": {"phase": "Pending"}})
+    assert not c.pod_start_stuck({"status": {"containerStatuses": [
+        {"state": {"waiting": {"reason": "ContainerCreating"}}}]}})
+    for reason in ("ImagePullBackOff", "ErrImagePull", "InvalidImageName", "CreateContainerConfigError"):
+        assert c.pod_start_stuck({"status": {"containerStatuses": [{"state": {"waiting": {"reason": reason}}}]}})
+    # an init container (amd-gpu-probe on a bad GPU) that failed: terminated non-zero, or in back-off
+    assert c.pod_start_stuck({"status": {"initContainerStatuses": [{"state": {"terminated": {"exitCode": 1}}}]}})
+    assert c.pod_start_stuck({"status": {"initContainerStatuses": [
+        {"state": {"waiting": {"reason": "CrashLoopBackOff"}}, "lastState": {"terminated": {"exitCode": 1}}}]}})
+    assert c.pod_start_stuck({"status": {"initContainerStatuses": [
+        {"state": {"waiting": {"reason": "PodInitializing"}}, "lastState": {"terminated": {"exitCode": 2}}}]}})
+    assert not c.pod_start_stuck({"status": {"initContainerStatuses": [{"state": {"terminated": {"exitCode": 0}}},
+                                                                       {"state": {"running": {}}}]}})
+    cfg = c.CullerConfig.from_env({})
+    assert cfg.startup_allowance_s == 600
+    assert c.CullerConfig.from_env({"CULL_STARTUP_ALLOWANCE_SECONDS": "2.5"}).startup_allowance_s == 2.5
+
+
 # ------------------------------------------------------------------ integration
 
 
@@ -175,6 +212,83 @@ def test_culler_jupyter_busy_keeps_idle_culls(run, clock):
             ok = await cl.wait_for(lambda: STOP_ANNOTATION in m.annotations(
                 cl.store.peek(kinds.NOTEBOOK, "busy", "user")), 10)
             assert ok, (m.annotations(cl.store.peek(kinds.NOTEBOOK, "busy", "user")), st_busy.kernels, rfc3339())
+    run(go(), timeout=60)
+
+
+class _FailingProbe:
+    """Container runtime whose init containers exit 1: the amd-gpu-probe of a bad GPU."""
+
+    exec_init = True
+    visible_device = None
+
+    def __init__(self):
+        self.calls = 0
+
+    async def run_init(self, pod, container, devices):
+        self.calls += 1
+        return {"exitCode": 1, "message": '{"ok": false, "error": "GPU 0: GEMM mismatches"}', "wall_ms": 1.0}
+
+    async def start(self, pod, devices):
+        raise AssertionError("containers must not start after a failed init container")
+
+    async def stop(self, handle):
+        return None
+
+    async def close(self):
+        return None
+
+
+@pytest.mark.parametrize("stuck", [True, False])
+def test_pod_that_cannot_start_is_culled_and_frees_its_gpu(run, clock, stuck):
+    """a notebook pod that never leaves Pending — its amd-gpu-probe init container
+    failing on a bad GPU and retried with back-off — holds its amd.com/gpu devices.  The culler
+    checks it anyway (idle since the pod's creation) and the GPU is released; a Pending pod that
+    is merely slow (no failure) is left alone until CULL_IDLE_TIME + CULL_STARTUP_ALLOWANCE."""
+    from odh_kubeflow_amd.controllers.notebook import GPU_PROBE_ANNOTATION
+
+    class _Slow(_FailingProbe):
+        async def run_init(self, pod, container, devices):
+            import asyncio
+
+            self.calls += 1
+            await asyncio.sleep(3600)  # an init container still working (a huge image, a slow probe)
+
+    rts = []
+
+    def factory(d):
+        rts.append(_FailingProbe() if stuck else _Slow())
+        return rts[-1]
+
+    async def go():
+        env = {"ENABLE_CULLING": "true", "CULL_IDLE_TIME": "60", "IDLENESS_CHECK_PERIOD_SECONDS": "0.05",
+               "CULL_STARTUP_ALLOWANCE": "30"}
+        async with LocalCluster(ClusterConfig(culler=True, env=env, runtime_factory=factory)) as cl:
+            await cl.ensure_namespace("user")
+            await cl.admin.create(notebook("nb", "user", gpus=1, annotations={GPU_PROBE_ANNOTATION: "true"}))
+            pod = lambda: cl.store.peek(kinds.POD, "nb-0", "user")  # noqa: E731
+            nbk = lambda: cl.store.peek(kinds.NOTEBOOK, "nb", "user")  # noqa: E731
+            if stuck:
+                assert await cl.wait_for(lambda: bool(pod() and (pod().get("status") or {}).get(
+                    "initContainerStatuses")), 30)
+            else:
+                assert await cl.wait_for(lambda: bool(rts) and sum(r.calls for r in rts) >= 1, 30)
+            assert pod()["status"]["phase"] == "Pending"
+            culler = cl.reconcilers["culler"]
+            clock[0] += 61 * 60  # past CULL_IDLE_TIME, inside CULL_IDLE_TIME + the allowance
+            if stuck:
+                assert await cl.wait_for(lambda: STOP_ANNOTATION in m.annotations(nbk()), 10)
+                assert await cl.wait_for(lambda: pod() is None, 10)  # its GPU is free again
+                assert cl.store.peek(kinds.STATEFUL_SET, "nb", "user")["spec"]["replicas"] == 0
+                assert culler.culled == 1 and culler.cull_log[-1]["jupyter"] == "unreachable"
+            else:
+                n = culler.checks
+                import asyncio
+
+                await asyncio.sleep(0.5)  # ≈10 check periods: still starting, so never checked
+                assert STOP_ANNOTATION not in m.annotations(nbk()) and culler.checks == n
+                clock[0] += 30 * 60  # now older than CULL_IDLE_TIME + CULL_STARTUP_ALLOWANCE
+                assert await cl.wait_for(lambda: STOP_ANNOTATION in m.annotations(nbk()), 10), (
+                    m.annotations(nbk()), list(culler.recent), pod()["metadata"].get("creationTimestamp"), rfc3339())
     run(go(), timeout=60)
 
 

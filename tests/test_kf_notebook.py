@@ -63,6 +63,13 @@ def test_generate_service_and_vs():
     assert vs["spec"]["gateways"] == ["gw/g"] and vs["spec"]["hosts"] == ["*"]
     bad = notebook("nb1", "user", annotations={"notebooks.kubeflow.org/http-headers-request-set": "not json"})
     assert generate_virtual_service(bad, env={})["spec"]["http"][0]["headers"]["request"]["set"] == {}
+    # Go unmarshals into map[string]string: a number / object value fails the whole map, a
+    # null value is the zero string
+    # (kf/controllers/notebook_controller.go:605-613)
+    for raw, want in (('{"X-A": 1}', {}), ('{"X-A": {"b": 1}}', {}), ('{"X-A": "1", "X-B": null}', {"X-A": "1", "X-B": ""}),
+                      ('["X-A"]', {}), ("null", {}), ('{"X-A": "1", "X-B": "2"}', {"X-A": "1", "X-B": "2"})):
+        odd = notebook("nb1", "user", annotations={"notebooks.kubeflow.org/http-headers-request-set": raw})
+        assert generate_virtual_service(odd, env={})["spec"]["http"][0]["headers"]["request"]["set"] == want, raw
 
 
 def test_create_notebook_status_table():

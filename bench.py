@@ -65,6 +65,8 @@ def parse(argv=None):
     p.add_argument("--single-process-shard", action="store_true",
                    help="sharded: each shard as ONE control-plane process (kf + odh + webhook) instead of the "
                         "deployed kf / odh+webhook pair (A/B measurements)")
+    p.add_argument("--workers", type=int, default=1,
+                   help="unsharded: --workers of the kf and odh managers (namespace-partitioned worker processes)")
     p.add_argument("--json-out", default=None)
     return p.parse_args(argv)
 

@@ -80,6 +80,17 @@ def resolve_shard(value, env=None):
     return value
 
 
+def add_worker_flags(p) -> None:
+    """``--workers W``: run the controllers in W namespace-partitioned child processes
+    (:mod:`~odh_kubeflow_amd.runtime.workers`); ``--worker i/W`` is how the supervisor starts
+    one of them."""
+    import argparse
+
+    p.add_argument("--workers", type=int, default=1,
+                   help="controller worker processes, namespaces partitioned crc32(ns) %% W (1: in this process)")
+    p.add_argument("--worker", default=None, help=argparse.SUPPRESS)
+
+
 def add_debug_flags(p) -> None:
     """``--enable-debug-endpoints``: ``/debug/reconciles`` and ``/debug/quiesce`` on the
     metrics server (see :meth:`~odh_kubeflow_amd.runtime.manager.Manager.quiesce`)."""

@@ -3,8 +3,10 @@
 Flags keep the reference names (``--metrics-addr``, ``--probe-addr``,
 ``--enable-leader-election``, ``--leader-election-namespace``, ``--qps``, ``--burst``,
 ``--zap-devel``); additions: ``--kubeconfig`` / ``--master``,
-``--max-concurrent-reconciles`` (default 8; the reference runs 1 worker).  Culling is
-wired only when ``ENABLE_CULLING=true`` (:111-123).  Leader-election ID
+``--max-concurrent-reconciles`` (default 8; the reference runs 1 worker), ``--workers W``
+(the controllers in W namespace-partitioned child processes of this one, which leads,
+aggregates their ``/metrics`` and restarts them: :mod:`~odh_kubeflow_amd.runtime.workers`).
+Culling is wired only when ``ENABLE_CULLING=true`` (:111-123).  Leader-election ID
 ``kubeflow-notebook-controller``.
 
     python -m odh_kubeflow_amd.cmd.kf_manager --master http://127.0.0.1:6443
@@ -38,11 +40,28 @@ def parse(argv: Optional[List[str]] = None) -> argparse.Namespace:
     p.add_argument("--leader-election-lease-duration", type=float, default=15.0)
     p.add_argument("--leader-election-renew-deadline", type=float, default=10.0)
     p.add_argument("--leader-election-retry-period", type=float, default=2.0)
-    from .common import add_debug_flags, add_shard_flags
+    from .common import add_debug_flags, add_shard_flags, add_worker_flags
 
     add_shard_flags(p)
     add_debug_flags(p)
-    return p.parse_args(argv)
+    add_worker_flags(p)
+    args = p.parse_args(argv)
+    args.argv = list(sys.argv[1:] if argv is None else argv)
+    return args
+
+
+WORKER_STRIP_VALUE = ("--workers", "--worker", "--metrics-addr", "--probe-addr", "--leader-election-namespace")
+WORKER_STRIP_BOOL = ("--enable-leader-election", "--enable-debug-endpoints")
+
+
+def worker_argv(args, index: int, metrics_addr: str) -> List[str]:
+    """A worker's command line: the supervisor's, minus what the supervisor alone does
+    (leader election, the public metrics and probe addresses)."""
+    from ..runtime.workers import strip_flags
+
+    base = strip_flags(args.argv, WORKER_STRIP_VALUE, WORKER_STRIP_BOOL)
+    return [*base, "--worker", f"{index}/{args.workers}", "--metrics-addr", metrics_addr, "--probe-addr", "0",
+            "--enable-debug-endpoints"]
 
 
 def build(args, env=os.environ):
@@ -52,25 +71,44 @@ def build(args, env=os.environ):
     from ..runtime.rest import RestClient, RestConfig
     from .common import resolve_shard
 
+    from ..runtime.workers import WorkerAssignments, WorkerSupervisor, parse_worker
+
     shard = resolve_shard(getattr(args, "shard", None), env)
+    worker = parse_worker(getattr(args, "worker", None))
     cfg = RestConfig.load(args.master, args.kubeconfig)
     if args.qps:
         cfg.qps = float(args.qps)
     if args.burst:
         cfg.burst = args.burst
     elector = None
-    if args.enable_leader_election:
+    if args.enable_leader_election and worker is None:
         elector = LeaderElector(RestClient(cfg), "kubeflow-notebook-controller" + (
                                     f"-shard-{shard}" if shard is not None else ""),
                                 args.leader_election_namespace or namespace_from_env(),
                                 lease_duration=args.leader_election_lease_duration,
                                 renew_deadline=args.leader_election_renew_deadline,
                                 retry_period=args.leader_election_retry_period)
+    cache_options = shard_cache_options(shard, namespace_from_env())
+    assign = WorkerAssignments(*worker) if worker is not None else None
+    if assign is not None:
+        cache_options = assign.cache_options()
     mgr = Manager.remote(cfg, name="notebook-controller", default_max_concurrent=args.max_concurrent_reconciles,
                          leader_elector=elector, metrics_addr=args.metrics_addr, probe_addr=args.probe_addr,
-                         debug_endpoints=args.enable_debug_endpoints,
-                         cache_options=shard_cache_options(shard, namespace_from_env()))
-    mgr.kf_reconcilers = setup_kf(mgr, env)
+                         debug_endpoints=args.enable_debug_endpoints, cache_options=cache_options)
+    if assign is not None:
+        assign.cache = mgr.cache
+        assign.on_lost = lambda: mgr.fail("supervisor gone")
+        mgr.request_filter = assign.request_filter
+        mgr.add(assign, needs_leader=False)  # its start returns once the initial namespaces arrived
+    if args.workers > 1 and worker is None:
+        # supervisor: the controllers run in the workers (runtime/workers.py)
+        mgr.set_supervisor(WorkerSupervisor("odh_kubeflow_amd.cmd.kf_manager", args.workers,
+                                            lambda i, addr: worker_argv(args, i, addr), env=dict(env), cache=mgr.cache,
+                                            system_namespaces=[namespace_from_env()],
+                                            name="notebook-controller"))
+        mgr.kf_reconcilers = {}
+    else:
+        mgr.kf_reconcilers = setup_kf(mgr, env)
     mgr.add_healthz_check("healthz")
     mgr.add_readyz_check("readyz")
     return mgr

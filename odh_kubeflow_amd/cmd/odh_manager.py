@@ -8,6 +8,11 @@ Flags: ``--metrics-bind-address`` (:8080), ``--health-probe-bind-address`` (:808
 object and ``data`` from ConfigMaps/Secrets, whose reads go straight to the apiserver
 (:165-185).  The controller namespace comes from the service-account namespace file or
 ``K8S_NAMESPACE`` (:103-115).  Leader-election ID ``odh-notebook-controller``.
+
+``--workers W`` runs the reconciler in W namespace-partitioned child processes
+(:mod:`~odh_kubeflow_amd.runtime.workers`); this process then leads, serves the webhook on
+its own event loop — admissions never queue behind a reconcile — and aggregates the
+workers' ``/metrics``.
 """
 
 from __future__ import annotations
@@ -37,15 +42,31 @@ def parse(argv: Optional[List[str]] = None) -> argparse.Namespace:
     p.add_argument("--kubeconfig", default=None)
     p.add_argument("--master", default=None)
     p.add_argument("--max-concurrent-reconciles", type=int, default=8)
-    from .common import add_debug_flags, add_shard_flags
+    from .common import add_debug_flags, add_shard_flags, add_worker_flags
 
     add_shard_flags(p)
     add_debug_flags(p)
+    add_worker_flags(p)
     args = p.parse_args(argv)
     if not args.kube_rbac_proxy_image:
         p.print_usage(sys.stderr)
         raise SystemExit("missing required flag: --kube-rbac-proxy-image must be set")
+    args.argv = list(sys.argv[1:] if argv is None else argv)
     return args
+
+
+WORKER_STRIP_VALUE = ("--workers", "--worker", "--metrics-bind-address", "--health-probe-bind-address")
+WORKER_STRIP_BOOL = ("--leader-elect", "--enable-debug-endpoints")
+
+
+def worker_argv(args, index: int, metrics_addr: str) -> List[str]:
+    """A reconciler worker's command line: the supervisor's, minus leader election and the
+    public addresses (the webhook stays with the supervisor)."""
+    from ..runtime.workers import strip_flags
+
+    base = strip_flags(args.argv, WORKER_STRIP_VALUE, WORKER_STRIP_BOOL)
+    return [*base, "--worker", f"{index}/{args.workers}", "--metrics-bind-address", metrics_addr,
+            "--health-probe-bind-address", "0", "--enable-debug-endpoints"]
 
 
 def build(args, env=os.environ):
@@ -59,31 +80,54 @@ def build(args, env=os.environ):
     from ..webhook.server import WebhookServer
     from .common import ServerRunnable, resolve_shard
 
+    from ..runtime.workers import WorkerAssignments, WorkerSupervisor, parse_worker
+
     shard = resolve_shard(getattr(args, "shard", None), env)
+    worker = parse_worker(getattr(args, "worker", None))
     cfg = RestConfig.load(args.master, args.kubeconfig)
     namespace = namespace_from_env()
     log.info("Controller is running in namespace %s", namespace)
     lease = "odh-notebook-controller" + (f"-shard-{shard}" if shard is not None else "")
-    elector = LeaderElector(RestClient(cfg), lease, namespace) if args.leader_elect else None
+    elector = LeaderElector(RestClient(cfg), lease, namespace) if args.leader_elect and worker is None else None
+    cache_options = shard_cache_options(shard, namespace)
+    assign = WorkerAssignments(*worker) if worker is not None else None
+    if assign is not None:
+        # the controller namespace holds the central HTTPRoutes and ImageStreams every worker reads
+        cache_options = assign.cache_options(extra_namespaces=[namespace])
     mgr = Manager.remote(cfg, name="odh-notebook-controller", uncached=(kinds.CONFIG_MAP, kinds.SECRET),
                          transforms={kinds.CONFIG_MAP: strip_data, kinds.SECRET: strip_data},
                          default_max_concurrent=args.max_concurrent_reconciles, leader_elector=elector,
                          metrics_addr=args.metrics_bind_address, probe_addr=args.health_probe_bind_address,
-                         debug_endpoints=args.enable_debug_endpoints, cache_options=shard_cache_options(shard, namespace))
-    mgr.odh_reconciler = setup_odh(mgr, namespace, env, shard=shard)
-    wh = NotebookWebhook(mgr.client, namespace, kube_rbac_proxy_image=args.kube_rbac_proxy_image, env=env)
-    # controller-runtime's webhook server refuses to start without its serving cert; admission
-    # (failurePolicy: Fail) is never offered over plain HTTP
-    missing = [f for f in ("tls.crt", "tls.key") if not os.path.exists(os.path.join(args.webhook_cert_dir, f))]
-    if missing:
-        raise SystemExit(f"webhook serving certificate missing in {args.webhook_cert_dir}: {', '.join(missing)} "
-                         "(OpenShift: service-ca; elsewhere: the odh-webhook-certs Job, cmd/webhook_certs.py)")
-    server = WebhookServer(wh, args.webhook_cert_dir, args.webhook_host, args.webhook_port,
-                           reload_interval=args.webhook_cert_reload_seconds)
-    mgr.add(ServerRunnable(server.start, server.stop), needs_leader=False)  # webhooks serve on every replica
+                         debug_endpoints=args.enable_debug_endpoints, cache_options=cache_options)
+    supervise = args.workers > 1 and worker is None
+    mgr.webhook_server = None
+    if assign is not None:
+        assign.cache = mgr.cache
+        assign.on_lost = lambda: mgr.fail("supervisor gone")
+        mgr.request_filter = assign.request_filter
+        mgr.add(assign, needs_leader=False)  # its start returns once the initial namespaces arrived
+    if supervise:
+        mgr.set_supervisor(WorkerSupervisor("odh_kubeflow_amd.cmd.odh_manager", args.workers,
+                                            lambda i, addr: worker_argv(args, i, addr), env=dict(env), cache=mgr.cache,
+                                            system_namespaces=[namespace],
+                                            name="odh-notebook-controller"))
+        mgr.odh_reconciler = None
+    else:
+        mgr.odh_reconciler = setup_odh(mgr, namespace, env, shard=shard)
+    if worker is None:
+        wh = NotebookWebhook(mgr.client, namespace, kube_rbac_proxy_image=args.kube_rbac_proxy_image, env=env)
+        # controller-runtime's webhook server refuses to start without its serving cert; admission
+        # (failurePolicy: Fail) is never offered over plain HTTP
+        missing = [f for f in ("tls.crt", "tls.key") if not os.path.exists(os.path.join(args.webhook_cert_dir, f))]
+        if missing:
+            raise SystemExit(f"webhook serving certificate missing in {args.webhook_cert_dir}: {', '.join(missing)} "
+                             "(OpenShift: service-ca; elsewhere: the odh-webhook-certs Job, cmd/webhook_certs.py)")
+        server = WebhookServer(wh, args.webhook_cert_dir, args.webhook_host, args.webhook_port,
+                               reload_interval=args.webhook_cert_reload_seconds)
+        mgr.add(ServerRunnable(server.start, server.stop), needs_leader=False)  # webhooks serve on every replica
+        mgr.webhook_server = server
     mgr.add_healthz_check("healthz")
     mgr.add_readyz_check("readyz")
-    mgr.webhook_server = server
     return mgr
 
 

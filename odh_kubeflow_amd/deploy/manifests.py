@@ -76,6 +76,10 @@ MI355X_PARAMS = ["GPU_NODE_SELECTOR=true", "GPU_SHM_SIZE_PER_GPU=16Gi",
                  # driver only offers dmabuf IPC fail hipIpcGetMemHandle otherwise)
                  "MULTI_GPU_ENV=HSA_ENABLE_IPC_MODE_LEGACY=0"]
 MI355X_CULLER = ["CULLING_ACTIVITY_SOURCE=combined", "ENABLE_CULLING=true"]
+# overlay mi355x: each manager runs its controllers in this many namespace-partitioned worker
+# processes (runtime/workers.py; the odh webhook stays on the supervisor's own event loop) —
+# one core per worker, so an 8-GPU node's notebooks are not serialised on one Python loop
+MI355X_WORKERS = 4
 # the base manifests carry the development tag; every overlay pins the release tag through
 # kustomize `images` (releasing/VERSION, set by tools/release.py — the reference's
 # releasing/update-manifests-images + releasing/version/VERSION)
@@ -226,6 +230,16 @@ def _agent_token_volume() -> dict:
 
 
 AGENT_TOKEN_MOUNT_SPEC = {"name": "node-agent-token", "mountPath": AGENT_TOKEN_MOUNT, "readOnly": True}
+
+
+def _workers_patches(workers: int) -> List[dict]:
+    """``--workers`` for both managers, and the CPU to run them: one core per worker plus the
+    supervisor (which leads, aggregates /metrics and, in the odh manager, serves the webhook)."""
+    ops = [{"op": "add", "path": "/spec/template/spec/containers/0/args/-", "value": f"--workers={workers}"},
+           {"op": "replace", "path": "/spec/template/spec/containers/0/resources/limits/cpu", "value": str(workers + 1)},
+           {"op": "replace", "path": "/spec/template/spec/containers/0/resources/requests/cpu", "value": str(workers)}]
+    patch = yaml.safe_dump(ops, sort_keys=False)
+    return [{"target": {"kind": "Deployment", "name": f"{NAME_PREFIX}(deployment|manager)"}, "patch": patch}]
 
 
 def kf_deployment() -> dict:
@@ -656,7 +670,8 @@ def tree(version: Optional[str] = None) -> Dict[str, object]:
                           "literals": list(MI355X_CULLER)}]
     t["overlays/mi355x/kustomization.yaml"] = kustomization(["../../default", "../../webhook-certs"],
                                                             namespace="opendatahub", images=images,
-                                                            configMapGenerator=mi355x_generators)
+                                                            configMapGenerator=mi355x_generators,
+                                                            patches=_workers_patches(MI355X_WORKERS))
     # the serving cert covers every shard's Service; every shard's configuration gets the caBundle
     svc_names = [NAME_PREFIX + o["metadata"]["name"] for o in cp["services.yaml"][1:]]
     mwc_names = [NAME_PREFIX + o["metadata"]["name"] for o in cp["webhooks.yaml"]]

@@ -126,15 +126,21 @@ def measure(args) -> Optional[dict]:
                                             f"kf process and an odh reconciler + odh webhook process")
             out["config"]["architecture"] = "cmd/control_plane --shard r --controllers kf | odh,webhook (overlay mi355x-sharded)"
         else:
-            out["config"]["parallelism"] = (f"one kf manager + one odh manager process for all {world} ranks' "
-                                            f"notebooks, as config/overlays/mi355x deploys them")
-            out["config"]["architecture"] = "cmd/kf_manager + cmd/odh_manager (overlay mi355x, reference topology)"
+            w = max(1, getattr(args, "workers", 1))
+            wk = f" with --workers {w} (namespace-partitioned worker processes; the odh webhook on the supervisor)" \
+                if w > 1 else ""
+            out["config"]["parallelism"] = (f"one kf manager + one odh manager Deployment for all {world} ranks' "
+                                            f"notebooks{wk}, as config/overlays/mi355x deploys them")
+            out["config"]["architecture"] = (f"cmd/kf_manager + cmd/odh_manager{f' --workers {w}' if w > 1 else ''} "
+                                             f"(overlay mi355x, reference topology)")
         w = (world + 1) // 2
         out["config"]["platform_stand_ins"] = (f"native C++ apiserver (+GC); ONE scheduler (first-free amd.com/gpu "
                                                f"allocation); the node's StatefulSet controller and kubelet for its "
                                                f"8 GPUs, each as {w} worker process{'es' if w > 1 else ''} "
                                                f"(namespaces partitioned)")
         out["rank_ms_per_step"] = res.get("rank_ms_per_step")
+        out["recon_snapshot_lag_ms"] = res.get("recon_snapshot_lag_ms")
+        out["io_per_notebook"] = res.get("io_per_notebook")
         out["lifecycle_ms_per_20_steps"] = res.get("lifecycle_ms_per_20_steps")
         out["cpu_ms_per_step"] = res.get("cpu_ms_per_step")
         out["child_rss_mib"] = res.get("child_rss_mib")
@@ -187,6 +193,40 @@ def writes_per_notebook(prof: dict, notebooks_per_step: int) -> dict:
     n = max(1, notebooks_per_step)
     out = {v: round(prof.get(f"{v}_calls", 0.0) / n, 2) for v in ("create", "update", "patch", "delete")}
     out["total"] = round(sum(out.values()), 2)
+    return out
+
+
+def io_delta(a: dict, b: dict) -> dict:
+    """Per process: watch events per kind and requests per verb between two snapshots."""
+    out = {}
+    for proc, cur in b.items():
+        prev = a.get(proc) or {}
+        d = {}
+        for sect in ("watch_events", "requests"):
+            p0 = prev.get(sect) or {}
+            dd = {k: v - p0.get(k, 0) for k, v in (cur.get(sect) or {}).items()}
+            d[sect] = {k: v for k, v in dd.items() if v}
+        out[proc] = d
+    return out
+
+
+def io_per_notebook(parts: list, notebooks: int) -> dict:
+    """Merge the ranks' :func:`io_delta` and divide by the notebooks of the timed window (the
+    deltas run to the settled point, so a lifecycle's trailing events are in)."""
+    n = max(1, notebooks)
+    out: dict = {}
+    for part in parts:
+        for proc, d in (part or {}).items():
+            o = out.setdefault(proc, {})
+            for sect, kv in d.items():
+                s = o.setdefault(sect, {})
+                for k, v in kv.items():
+                    s[k] = s.get(k, 0) + v
+    for proc, o in out.items():
+        for sect, kv in o.items():
+            tot = sum(kv.values())
+            o[sect] = {k: round(v / n, 2) for k, v in sorted(kv.items(), key=lambda x: -x[1])}
+            o[sect]["total"] = round(tot / n, 2)
     return out
 
 
@@ -295,7 +335,7 @@ async def _main(args, dist, torch, rank: int, world: int, ndev: int, probe_sampl
         apiserver_url=url[0], namespace=bench_namespace(rank), shard=str(rank), arch=arch,
         launch=(arch == "sharded" or rank == 0), bootstrap=(rank == 0), odh=not args.no_odh,
         webhook=not args.no_odh, reference_emulation=args.reference_emulation, env=env, process=True,
-        split=not getattr(args, "single_process_shard", False)))
+        split=not getattr(args, "single_process_shard", False), workers=max(1, getattr(args, "workers", 1))))
     if rank == 0:
         await shard.start()  # cluster namespaces (and, unsharded, the managers + their webhook) first
         await _in_thread(dist.barrier)
@@ -388,6 +428,7 @@ async def _drive(args, shard, dist, torch, children: Optional[dict] = None, nati
         torch.cuda.synchronize()
     await _in_thread(dist.barrier)
     b0 = await shard.reconcile_breakdown()
+    io0 = await shard.io_counters()
     children = children or {}
     child_cpu0 = {k: _proc_cpu_s(pid) for k, pid in children.items()}
     prof0 = await _apiserver_prof(native)
@@ -396,13 +437,22 @@ async def _drive(args, shard, dist, torch, children: Optional[dict] = None, nati
     for _ in range(args.steps):
         await one_step(True)
     own = time.perf_counter() - t_start  # this rank's own steps
+    from bench import breakdown_delta, merge_breakdowns  # noqa: E402  (bench.py is the entry point)
+
+    # a sharded rank's control plane serves only its own steps, all done now: its in-window
+    # count is read before the end barrier, so no reconcile that finishes after the window
+    # is counted in it; the unsharded control plane serves every rank, so it is read after
+    # the barrier, and the time that read takes is reported (``recon_snapshot_lag_ms``)
+    own_cp = shard.cfg.arch == "sharded"
+    b1 = await shard.reconcile_breakdown() if own_cp else None
     if torch.cuda.is_available():
         torch.cuda.synchronize()
     await _in_thread(dist.barrier)
     elapsed = time.perf_counter() - t_start  # ---- end of the timed region
-    from bench import breakdown_delta, merge_breakdowns  # noqa: E402  (bench.py is the entry point)
-
-    in_window = breakdown_delta(b0, await shard.reconcile_breakdown())
+    if b1 is None:
+        b1 = await shard.reconcile_breakdown() if shard.procs or shard.managers else {}
+    snap_lag = time.perf_counter() - t_start - elapsed
+    in_window = breakdown_delta(b0, b1)
     cpu = {"rank": time.process_time() - cpu0}
     prof = _prof_per_step(prof0, await _apiserver_prof(native), args.steps)
     rss = {}
@@ -417,6 +467,7 @@ async def _drive(args, shard, dist, torch, children: Optional[dict] = None, nati
     await _in_thread(dist.barrier)
     idle = await shard.quiesce()
     settled = breakdown_delta(b0, await shard.reconcile_breakdown())
+    io = io_delta(io0, await shard.io_counters())
     samples = []
     for i in range(probe_sample):  # untimed: notebooks with the start-up probe init container
         ann = {**base_ann, GPU_PROBE_ANNOTATION: "true"}
@@ -437,7 +488,8 @@ async def _drive(args, shard, dist, torch, children: Optional[dict] = None, nati
     await _in_thread(dist.all_gather_object, gathered, {"lat": lat_ms, "teardown": teardown_ms, "own_s": own,
                                                         "blocks": blocks,
                                                         "cpu": cpu, "rss": rss, "in_window": in_window,
-                                                        "settled": settled, "idle": idle, "probe": samples})
+                                                        "settled": settled, "idle": idle, "probe": samples,
+                                                        "io": io, "snap_lag_ms": snap_lag * 1e3})
     per_step = 1e3 / max(1, args.steps)
     cpu_ms = {"ranks": [round(g["cpu"]["rank"] * per_step, 3) for g in gathered]}
     for g in gathered:
@@ -452,5 +504,7 @@ async def _drive(args, shard, dist, torch, children: Optional[dict] = None, nati
             "child_rss_mib": {k: v for g in gathered for k, v in g["rss"].items()},
             "apiserver_profile_per_step": prof, "breakdown": merge_breakdowns(g["settled"] for g in gathered),
             "quiesced": all(g["idle"] for g in gathered),
+            "io_per_notebook": io_per_notebook([g["io"] for g in gathered], args.steps * len(gathered)),
+            "recon_snapshot_lag_ms": round(max(g["snap_lag_ms"] for g in gathered), 3),
             "probe_sample": [s for g in gathered for s in g["probe"]],
             "lifecycle_ms_per_20_steps": [round(statistics.fmean(b), 3) for b in zip(*(g["blocks"] for g in gathered))]}

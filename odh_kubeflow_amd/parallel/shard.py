@@ -63,6 +63,7 @@ class ShardConfig:
     kube_rbac_proxy_image: str = "quay.io/brancz/kube-rbac-proxy:v0.18.1"
     process: bool = False  # run the control plane as its own process(es), as deployed
     split: bool = True  # sharded, process mode: kf and odh + webhook as two processes (the shard pod's two containers)
+    workers: int = 1  # unsharded: --workers of the kf and odh managers (runtime/workers.py)
 
 
 class _Proc:
@@ -86,6 +87,7 @@ class ControlPlaneShard:
         self._waiters = None
         self._certs = None
         self._http = None
+        self.worker_pids: Dict[str, int] = {}  # --workers: the managers' worker processes
 
     # ------------------------------------------------------------------ build
 
@@ -116,10 +118,11 @@ class ControlPlaneShard:
                 name = "control_plane" if len(sets) == 1 else f"control_plane_{cs[0]}"
                 out.append((name, "odh_kubeflow_amd.cmd.control_plane", a, "--metrics-bind-address"))
             return out
-        out = [("kf_manager", "odh_kubeflow_amd.cmd.kf_manager", ["--probe-addr", "0"], "--metrics-addr")]
+        wk = ["--workers", str(cfg.workers)] if cfg.workers > 1 else []
+        out = [("kf_manager", "odh_kubeflow_amd.cmd.kf_manager", ["--probe-addr", "0", *wk], "--metrics-addr")]
         if cfg.odh:
-            out.append(("odh_manager", "odh_kubeflow_amd.cmd.odh_manager", [*wh, "--health-probe-bind-address", "0"],
-                        "--metrics-bind-address"))
+            out.append(("odh_manager", "odh_kubeflow_amd.cmd.odh_manager",
+                        [*wh, "--health-probe-bind-address", "0", *wk], "--metrics-bind-address"))
         return out
 
     def _cp_env(self) -> Dict[str, str]:
@@ -165,6 +168,11 @@ class ControlPlaneShard:
             pre = ["-m", "cProfile", "-o", f"{prof}.{name}.{self.shard or 'all'}"] if prof else []
             proc = await start_child(module, args, f"{name} (shard {self.shard})", env=env, python_args=pre)
             self.procs.append(_Proc(name, proc, mport))
+        if self.cfg.workers > 1:
+            for p in self.procs:
+                d = await self._get_json(f"{p.base}/debug/reconciles")
+                for k, pid in (d.get("worker_pids") or {}).items():
+                    self.worker_pids[f"{p.name}_{k}"] = pid
 
     async def _build_in_process(self) -> int:
         cfg = self.cfg
@@ -276,12 +284,25 @@ class ControlPlaneShard:
                     o[k] = o.get(k, 0) + v
         return out
 
+    async def io_counters(self) -> Dict[str, dict]:
+        """process name → {"watch_events": {kind: n}, "requests": {verb: n}} of the control-plane
+        processes this rank launched (in-process managers under "inprocess_<i>")."""
+        out = {f"inprocess_{i}": mgr.io_counters() for i, mgr in enumerate(self.managers)}
+        if self.procs:
+            sfx = f"_{self.shard}" if self.shard is not None else ""
+            docs = await asyncio.gather(*(self._get_json(f"{p.base}/debug/reconciles") for p in self.procs))
+            for p, d in zip(self.procs, docs):
+                out[f"{p.name}{sfx}"] = d.get("io") or {}
+        return out
+
     async def reconcile_count(self) -> int:
         return sum(sum(t.values()) for t in (await self.reconcile_breakdown()).values())
 
     def control_plane_pids(self) -> Dict[str, int]:
         sfx = f"_{self.shard}" if self.shard is not None else ""
-        return {f"{p.name}{sfx}": p.proc.pid for p in self.procs}
+        out = {f"{p.name}{sfx}": p.proc.pid for p in self.procs}
+        out.update(self.worker_pids)
+        return out
 
     # ------------------------------------------------------------------ waiting
 

@@ -191,11 +191,16 @@ class Controller:
         # event, as controller-runtime does; the reference-emulation runs use that)
         self.own_writes: Optional[Callable[[dict, str], Optional[Request]]] = None
         self.echoes_skipped = 0
+        # a manager split into namespace-partitioned worker processes (runtime/workers.py):
+        # requests for another worker's namespaces are dropped here
+        self.request_filter: Optional[Callable[[Request], bool]] = None
 
     def watch(self, kind: str, map_fn: MapFunc, predicates: Sequence[Predicate] = ()) -> None:
         self.watches.append(_Watch(kind, map_fn, tuple(predicates)))
 
     def enqueue(self, req: Request, trigger: str = "manual") -> None:
+        if self.request_filter is not None and not self.request_filter(req):
+            return
         self._trigger.setdefault(req, trigger)
         self.queue.add(req)
 
@@ -379,6 +384,7 @@ class Builder:
         name = self._name or (SCHEME.resolve(self._for).kind.lower() if self._for else "controller")
         maxc = self._max if self._max is not None else self.mgr.default_max_concurrent
         c = Controller(name, fn, maxc, self._rate_limiter, self.mgr.runtime_metrics)
+        c.request_filter = getattr(self.mgr, "request_filter", None)
         if getattr(self.mgr, "skip_own_write_echoes", True):
             c.own_writes = getattr(self.mgr.client, "own_write", None)
             if c.own_writes is not None and getattr(self.mgr.client, "requeue", False) is None:

@@ -300,6 +300,14 @@ class InformerCache(Reader, EventSource):
                 if g.info.namespaced:
                     self._start_informer(g, ns)
 
+    def refresh_namespace(self, name: str) -> None:
+        """Re-evaluate ``namespace_filter`` for one namespace (its answer changed: a worker was
+        assigned or released the namespace, runtime/workers.py)."""
+        inf = self._ns_informer
+        obj = inf.items.get(("", name)) if inf is not None else None
+        if obj is not None:
+            self._on_namespace("MODIFIED", obj, obj)
+
     def _retire(self, inf: _Informer) -> None:
         """A namespace left the cache: stop its informer; to subscribers its objects are gone."""
         if inf.task is not None:
@@ -371,6 +379,15 @@ class InformerCache(Reader, EventSource):
         else:
             infs = g.all()
         return bool(infs) and all(i.synced.is_set() and not i.missing_kind for i in infs)
+
+    def event_counts(self) -> Dict[str, int]:
+        """Watch events delivered per kind since start (relist differences included)."""
+        out: Dict[str, int] = {}
+        for g in self._groups.values():
+            n = sum(inf.events for inf in g.infs.values())
+            if n:
+                out[g.info.kind] = out.get(g.info.kind, 0) + n
+        return out
 
     def informer(self, kind) -> _Informer:
         """The (first) informer of ``kind`` — for single-namespace / cluster-wide caches."""

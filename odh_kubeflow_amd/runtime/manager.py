@@ -59,6 +59,11 @@ class Manager:
         self._fatal_event: Optional[asyncio.Event] = None
         self._started_event: Optional[asyncio.Event] = None
         self.healthz["leader-election"] = lambda: self.fatal is None
+        # ``--workers W`` (runtime/workers.py): the worker processes this manager supervises
+        # (their /metrics and /debug answers are merged into this manager's), and, in a
+        # worker, the filter that keeps its controllers to its namespace partition
+        self.supervisor = None
+        self.request_filter = None
 
     # ------------------------------------------------------------------ construction
 
@@ -245,6 +250,27 @@ class Manager:
                 return False
             await asyncio.sleep(max(0.0002, quiet - since) if self.idle() else 0.0002)
 
+    def fail(self, reason: str) -> None:
+        """End :meth:`run_until` with exit code 1 (the process must restart)."""
+        log.error("%s: %s", self.name, reason)
+        self.fatal = reason
+        if self._fatal_event is not None:
+            self._fatal_event.set()
+
+    def set_supervisor(self, sup) -> None:
+        """Run ``sup`` (a :class:`~odh_kubeflow_amd.runtime.workers.WorkerSupervisor`) while
+        this manager leads; its workers' health, metrics and debug answers join this one's."""
+        self.supervisor = sup
+        self.add(sup, needs_leader=True)
+        self.healthz["workers"] = lambda: not self.elected or not self.elected.is_set() or sup.alive()
+
+    def io_counters(self) -> Dict[str, Dict[str, int]]:
+        """What this process received and sent: watch events per kind, REST requests per verb."""
+        cache = getattr(self, "cache", None) or self.reader
+        rest = getattr(self, "rest", None)
+        ev = cache.event_counts() if hasattr(cache, "event_counts") else {}
+        return {"watch_events": ev, "requests": dict(getattr(rest, "by_verb", {}) or {})}
+
     def reconcile_count(self) -> int:
         return sum(c.reconciles for c in self.controllers)
 
@@ -269,7 +295,12 @@ class Manager:
             app = web.Application()
 
             async def metrics(_req):
-                return web.Response(body=generate_latest(self.registry), content_type="text/plain", charset="utf-8")
+                body = generate_latest(self.registry)
+                if self.supervisor is not None:
+                    from .workers import merge_metrics
+
+                    body = merge_metrics([body.decode(), *await self.supervisor.metrics_texts()]).encode()
+                return web.Response(body=body, content_type="text/plain", charset="utf-8")
 
             app.router.add_get("/metrics", metrics)
             if self.debug_endpoints:
@@ -298,14 +329,30 @@ class Manager:
         :meth:`quiesce`, then answers ``{"idle": …, "reconciles": …}``."""
         from aiohttp import web
 
+        from .workers import merge_counts
+
         async def reconciles(_req):
-            return web.json_response({"reconciles": self.reconcile_breakdown()})
+            docs = await self.supervisor.debug("/debug/reconciles") if self.supervisor is not None else []
+            return web.json_response({"reconciles": merge_counts([self.reconcile_breakdown(),
+                                                                  *(d.get("reconciles") for d in docs)]),
+                                      "io": merge_counts([self.io_counters(), *(d.get("io") for d in docs)]),
+                                      "workers": len(docs),
+                                      "worker_pids": self.supervisor.pids() if self.supervisor is not None else {}})
 
         async def quiesce(req):
             quiet = float(req.query.get("quiet_ms", "2")) / 1e3
             timeout = float(req.query.get("timeout_s", "10"))
+            sub = []
+            if self.supervisor is not None:
+                sub = [asyncio.ensure_future(self.supervisor.debug(req.path_qs, timeout + 5))]
             idle = await self.quiesce(quiet, timeout)
-            return web.json_response({"idle": idle, "reconciles": self.reconcile_breakdown()})
+            docs = (await sub[0]) if sub else []
+            idle = idle and all(d.get("idle") for d in docs) and (
+                self.supervisor is None or len(docs) == self.supervisor.count)
+            return web.json_response({"idle": idle,
+                                      "reconciles": merge_counts([self.reconcile_breakdown(),
+                                                                  *(d.get("reconciles") for d in docs)]),
+                                      "io": merge_counts([self.io_counters(), *(d.get("io") for d in docs)])})
 
         app.router.add_get("/debug/reconciles", reconciles)
         app.router.add_get("/debug/quiesce", quiesce)

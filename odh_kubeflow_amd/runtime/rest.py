@@ -23,7 +23,7 @@ import ssl
 import tempfile
 import time
 from dataclasses import dataclass, field
-from typing import Any, AsyncIterator, List, Optional, Tuple
+from typing import Any, AsyncIterator, Dict, List, Optional, Tuple
 
 from ..models.errors import ApiError, Gone, InternalError
 from ..models.scheme import SCHEME, ResourceInfo
@@ -164,6 +164,7 @@ class RestClient(Client):
         self._pool = pool
         self._bucket = TokenBucket(config.qps, config.burst)
         self.requests = 0
+        self.by_verb: Dict[str, int] = {}  # requests per HTTP method (watches counted as WATCH)
         self.retries = 0  # GETs retried after a connection reset / EOF
         self.user = config.user_agent
         self._discovery: dict = {}  # "group/version" -> (fetched_at, set(plurals))
@@ -195,6 +196,7 @@ class RestClient(Client):
 
         await self._bucket.take()
         self.requests += 1
+        self.by_verb[method] = self.by_verb.get(method, 0) + 1
         data = None if body is None else json.dumps(body, separators=(",", ":")).encode()
         target = url[len(self.base):] if url.startswith(self.base) else url
         if params:
@@ -350,6 +352,7 @@ class RestClient(Client):
             params["fieldSelector"] = fields
         await self._bucket.take()
         self.requests += 1
+        self.by_verb["WATCH"] = self.by_verb.get("WATCH", 0) + 1
         target = self.path(info, v, namespace)[len(self.base):] + "?" + urlencode(params)
         status, _headers, stream = await self._http().stream("GET", target)
         if status >= 400:

@@ -1,0 +1,204 @@
+"""``--workers W``: the kf and odh managers as one supervisor + W namespace-partitioned worker
+processes (``runtime/workers.py``).
+
+* unit: the assignment policy (least-loaded, sticky, system namespaces on worker 0 and not
+  counted), the stdin protocol, the ``/metrics`` merge and the worker command lines;
+* processes: ``kf_manager --workers 2`` + ``odh_manager --workers 2`` (webhook on the
+  supervisor) against the native apiserver serve three namespaces; each notebook's objects are
+  written by exactly one worker; the merged ``/metrics`` and ``/debug`` answers add up; a killed
+  worker is restarted and its namespaces are served again.
+
+Reference counterpart: none — the reference runs each manager as one process with one worker
+per controller (``kf/main.go:87-98``, ``odh/main.go:155-192``).
+"""
+
+from __future__ import annotations
+
+import asyncio
+import io
+import os
+import signal
+
+import pytest
+
+from odh_kubeflow_amd.models import kinds
+from odh_kubeflow_amd.models.notebook import notebook
+from odh_kubeflow_amd.runtime import workers as wk
+from odh_kubeflow_amd.runtime.controller import Request
+
+
+class _FakeProc:
+    def __init__(self):
+        self.stdin = io.StringIO()
+
+
+def _sup(n=3, system=("opendatahub",)):
+    s = wk.WorkerSupervisor("x", n, lambda i, a: [], system_namespaces=system)
+    for w in s.workers:
+        w.proc = _FakeProc()
+    return s
+
+
+def test_assignment_least_loaded_sticky_and_system_namespaces():
+    s = _sup(3)
+    for ns in ("default", "opendatahub", "kube-system", "openshift-ingress"):
+        assert s.assign(ns) == 0  # system namespaces: worker 0, not counted as load
+    got = [s.assign(f"team-{i}") for i in range(6)]
+    assert got == [0, 1, 2, 0, 1, 2]  # least loaded, ties to the lowest index
+    assert s.assign("team-1") == 1  # sticky
+    s.release("team-0")
+    s.release("team-3")
+    assert s.assign("team-9") == 0  # worker 0 now has no user namespace
+    assert "assign team-9" in s.workers[0].proc.stdin.getvalue()
+    assert "release team-3" in s.workers[0].proc.stdin.getvalue()
+    assert s.assignments()[1] == ["team-1", "team-4"]
+    s._on_namespace("DELETED", {"metadata": {"name": "team-4"}}, None)
+    assert s.assignments()[1] == ["team-1"]
+
+
+def test_worker_side_protocol_filters_requests_and_refreshes_the_cache():
+    a = wk.WorkerAssignments(1, 2)
+    refreshed = []
+
+    class Cache:
+        def refresh_namespace(self, ns):
+            refreshed.append(ns)
+    a.cache = Cache()
+    a.apply("assign team-a")
+    a.apply("assign team-b")
+    a.apply("release team-a")
+    a.apply("bogus line")
+    assert a.namespaces == {"team-b"} and refreshed == ["team-a", "team-b", "team-a"]
+    assert a.request_filter(Request("team-b", "nb")) and not a.request_filter(Request("team-a", "nb"))
+    assert a.request_filter(Request("", "cluster-scoped"))
+    opts = a.cache_options(extra_namespaces=["opendatahub", ""])
+    assert opts["namespaces"] == ["opendatahub"]
+    assert opts["namespace_filter"]({"metadata": {"name": "team-b"}})
+    assert not opts["namespace_filter"]({"metadata": {"name": "team-c"}})
+
+
+def test_worker_reads_initial_set_then_follows_stdin(run):
+    async def go():
+        r, w = os.pipe()
+        rf = os.fdopen(r, "rb", buffering=0)
+        a = wk.WorkerAssignments(0, 1, stream=rf)
+        lost = []
+        a.on_lost = lambda: lost.append(True)
+        os.write(w, b"assign ns-1\nassign ns-2\nsync\n")
+        await asyncio.wait_for(a.start(), 5)
+        assert a.namespaces == {"ns-1", "ns-2"}
+        os.write(w, b"release ns-1\n")
+        for _ in range(100):
+            if a.namespaces == {"ns-2"}:
+                break
+            await asyncio.sleep(0.01)
+        assert a.namespaces == {"ns-2"}
+        os.close(w)  # the supervisor is gone
+        for _ in range(100):
+            if lost:
+                break
+            await asyncio.sleep(0.01)
+        assert lost == [True]
+        await a.stop()
+    run(go())
+
+
+def test_merge_metrics_sums_samples_and_keeps_one_header():
+    a = ("# HELP x_total Things.\n# TYPE x_total counter\nx_total{ns=\"a\"} 2.0\nx_created{ns=\"a\"} 100.0\n"
+         "# HELP h Hist.\n# TYPE h histogram\nh_bucket{le=\"1.0\"} 1.0\nh_sum 0.5\nh_count 1.0\n")
+    b = ("# HELP x_total Things.\n# TYPE x_total counter\nx_total{ns=\"a\"} 3.0\nx_total{ns=\"b\"} 1.0\n"
+         "x_created{ns=\"a\"} 50.0\n# HELP h Hist.\n# TYPE h histogram\nh_bucket{le=\"1.0\"} 2.0\nh_sum 1.5\n"
+         "h_count 2.0\n")
+    out = wk.merge_metrics([a, b])
+    assert out.count("# HELP x_total") == 1 and out.count("# TYPE h histogram") == 1
+    assert 'x_total{ns="a"} 5.0' in out and 'x_total{ns="b"} 1.0' in out
+    assert 'x_created{ns="a"} 50.0' in out  # a creation time: the earliest
+    assert 'h_bucket{le="1.0"} 3.0' in out and "h_sum 2.0" in out and "h_count 3.0" in out
+    from prometheus_client.parser import text_string_to_metric_families
+
+    fams = {f.name: f for f in text_string_to_metric_families(out)}
+    assert set(fams) >= {"x", "h"}
+
+
+def test_worker_command_lines_drop_what_only_the_supervisor_does():
+    from odh_kubeflow_amd.cmd import kf_manager, odh_manager
+
+    a = kf_manager.parse(["--master", "http://x", "--workers", "3", "--enable-leader-election", "--metrics-addr",
+                          ":8080", "--probe-addr=:8081", "--max-concurrent-reconciles", "4"])
+    argv = kf_manager.worker_argv(a, 2, "127.0.0.1:9999")
+    assert "--enable-leader-election" not in argv and ":8080" not in argv and "--probe-addr=:8081" not in argv
+    assert argv[argv.index("--worker") + 1] == "2/3" and argv[argv.index("--metrics-addr") + 1] == "127.0.0.1:9999"
+    assert argv[argv.index("--max-concurrent-reconciles") + 1] == "4" and "--workers" not in argv
+    o = odh_manager.parse(["--kube-rbac-proxy-image", "img", "--workers=2", "--leader-elect", "--webhook-port", "9443"])
+    argv = odh_manager.worker_argv(o, 0, "127.0.0.1:1")
+    assert "--leader-elect" not in argv and "--workers=2" not in argv and argv[argv.index("--worker") + 1] == "0/2"
+    with pytest.raises(SystemExit):
+        wk.parse_worker("3/3")
+    assert wk.parse_worker("1/4") == (1, 4) and wk.parse_worker(None) is None
+
+
+@pytest.mark.slow
+def test_managers_with_workers_serve_partitioned_namespaces(run):
+    async def go():
+        import aiohttp
+
+        from odh_kubeflow_amd.parallel.platform import NodePlatform
+        from odh_kubeflow_amd.parallel.shard import ControlPlaneShard, ShardConfig
+        from odh_kubeflow_amd.testing.apiserver.native import NativeApiServer
+        from odh_kubeflow_amd.testing.cluster import OPENSHIFT_CRDS
+
+        native = await NativeApiServer(OPENSHIFT_CRDS, gc=True).start()
+        env = {"SET_PIPELINE_RBAC": "false", "SET_PIPELINE_SECRET": "false"}
+        drivers = []
+        platform = None
+        try:
+            platform = await NodePlatform(native.url, process=False).start()
+            drivers.append(await ControlPlaneShard(ShardConfig(
+                native.url, "team-0", arch="unsharded", bootstrap=True, env=env, process=True, workers=2)).start())
+            for i in (1, 2):
+                drivers.append(await ControlPlaneShard(ShardConfig(native.url, f"team-{i}", arch="unsharded",
+                                                                   launch=False, env=env)).start())
+            pids = drivers[0].control_plane_pids()
+            assert sorted(k for k in pids if "worker" in k) == [
+                "kf_manager_worker_0", "kf_manager_worker_1", "odh_manager_worker_0", "odh_manager_worker_1"]
+            ann = {"notebooks.opendatahub.io/inject-auth": "true"}
+            for i, d in enumerate(drivers):
+                await d.admin.create(notebook("nb", f"team-{i}", image="img", gpus=1, annotations=ann))
+            for d in drivers:
+                assert await d.wait_for(lambda: d.notebook_ready("nb"), 60)
+            base = {p.name: p.base for p in drivers[0].procs}
+            async with aiohttp.ClientSession() as http:
+                async with http.get(base["kf_manager"] + "/debug/reconciles") as r:
+                    doc = await r.json()
+                assert doc["workers"] == 2
+                assert sum(doc["reconciles"]["notebook-controller"].values()) >= 3 * 3
+                # one worker wrote every object of a notebook: 3 namespaces over 2 workers, 2 + 1
+                async with http.get(base["odh_manager"] + "/metrics") as r:
+                    text = await r.text()
+                assert text.count("# TYPE controller_runtime_reconcile_total counter") == 1
+                assert 'controller_runtime_max_concurrent_reconciles{controller="odh-notebook-controller"} 16.0' \
+                    in text
+            # a worker dies: it is restarted and given its namespaces again
+            victim = pids["kf_manager_worker_1"]
+            os.kill(victim, signal.SIGKILL)
+            await asyncio.sleep(1.0)
+            await drivers[1].admin.create(notebook("nb2", "team-1", image="img", gpus=1, annotations=ann))
+            await drivers[2].admin.create(notebook("nb2", "team-2", image="img", gpus=1, annotations=ann))
+            for d in drivers[1:]:
+                assert await d.wait_for(lambda: d.notebook_ready("nb2"), 60)
+            for i, d in enumerate(drivers):
+                for nm in ("nb", "nb2") if i else ("nb",):
+                    await d.admin.delete(kinds.NOTEBOOK, nm, f"team-{i}")
+            for i, d in enumerate(drivers):
+                for nm in ("nb", "nb2") if i else ("nb",):
+                    assert await d.wait_for(lambda: d.gone(nm), 60)
+            assert await drivers[0].quiesce(0.002, 20)
+            routes = await drivers[0].rest.list(kinds.HTTP_ROUTE, "opendatahub")
+            assert routes == []  # every route cleaned up by the worker that owns its notebook
+        finally:
+            for d in reversed(drivers):
+                await d.stop()
+            if platform is not None:
+                await platform.stop()
+            await native.stop()
+    run(go(), timeout=240)

@@ -14,9 +14,9 @@
 #   unsharded  the default topology (one kf + one odh manager process) at 1, 2 and 4 ranks
 #   archab   interleaved A/B at N=1: shard as kf/odh process pair vs one process vs unsharded
 #   probeexe the odh-gpu-probe init-container program: 10 process runs (wall time, verdict)
-#   hipinit  where a fresh process's HIP start-up goes, under ROCm runtime settings (tools/hip_init_ab.sh)
-#   hsaknobs hsa_init under ROCr runtime settings, interleaved (tools/hsa_init_knobs.py)
-#   hipexit  where a GPU process's exit goes: what it holds when it leaves (tools/hip_exit_ab.py)
+#   hipinit  where a fresh process's HIP start-up goes, under ROCm runtime settings (tools/research/hip_init_ab.sh)
+#   hsaknobs hsa_init under ROCr runtime settings, interleaved (tools/research/hsa_init_knobs.py)
+#   hipexit  where a GPU process's exit goes: what it holds when it leaves (tools/research/hip_exit_ab.py)
 #   webhook  BASELINE config #4 (tools/bench_webhook.py)
 #   culling  BASELINE config #5 (tools/bench_culling.py)
 #   realpods BASELINE configs #2/#3: 1 and 8 notebooks whose container is a real PyTorch-ROCm process
@@ -111,15 +111,15 @@ for s in $steps; do
         done
       done ;;
     hipinit)
-      timeout -k 10 300 bash tools/hip_init_ab.sh "$tag" > "$out/hip_init_ab.log" 2>&1 || fail hipinit $? "$out/hip_init_ab.log"
+      timeout -k 10 300 bash tools/research/hip_init_ab.sh "$tag" > "$out/hip_init_ab.log" 2>&1 || fail hipinit $? "$out/hip_init_ab.log"
       cat "$out/hip_init_ab.log" ;;
     hsaknobs)
-      timeout -k 10 300 python tools/hsa_init_knobs.py --rounds ${HSA_KNOB_ROUNDS:-5} ${HSA_KNOB_ONLY:+--only $HSA_KNOB_ONLY} \
+      timeout -k 10 300 python tools/research/hsa_init_knobs.py --rounds ${HSA_KNOB_ROUNDS:-5} ${HSA_KNOB_ONLY:+--only $HSA_KNOB_ONLY} \
         > "$out/hsa_init_knobs.jsonl" 2>&1 \
         || fail hsaknobs $? "$out/hsa_init_knobs.jsonl"
       tail -1 "$out/hsa_init_knobs.jsonl" ;;
     hipexit)
-      timeout -k 10 300 python tools/hip_exit_ab.py --repeats 5 > "$out/hip_exit_ab.jsonl" 2>&1 \
+      timeout -k 10 300 python tools/research/hip_exit_ab.py --repeats 5 > "$out/hip_exit_ab.jsonl" 2>&1 \
         || fail hipexit $? "$out/hip_exit_ab.jsonl"
       tail -1 "$out/hip_exit_ab.jsonl" ;;
     cpprof)

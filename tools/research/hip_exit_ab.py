@@ -5,7 +5,7 @@ The kubelet sees an init container finish when its process is reaped, so a probe
 own exit: the kernel tearing down the process's GPU state (KFD queues and VM, the render
 node's BOs) after ``_Exit``.  Each run spawns the program directly (no shell), stamps
 ``ODH_T0_NS``/``ODH_PROBE_T0_NS`` just before the spawn and times the reap; the program prints
-its own CLOCK_REALTIME ``end_ns`` (``tools/native/hip_init_bench``) or its ``timings_ms``
+its own CLOCK_REALTIME ``end_ns`` (``tools/research/native/hip_init_bench``) or its ``timings_ms``
 (``odh-gpu-probe``), so exec, in-process work and exit are separated:
 
     exit_ms = reaped - end of the program's own work
@@ -24,8 +24,8 @@ import subprocess
 import sys
 import time
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-BENCH = os.path.join(ROOT, "tools", "native", "hip_init_bench")
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+BENCH = os.path.join(ROOT, "tools", "research", "native", "hip_init_bench")
 PROBE = os.path.join(ROOT, "odh_kubeflow_amd", "ops", "_lib", "odh-gpu-probe")
 
 SETTINGS = [

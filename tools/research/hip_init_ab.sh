@@ -7,7 +7,7 @@ tag=${1:?tag}
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 out=gpurun_out/$tag
 mkdir -p "$out"
-bin=tools/native/hip_init_bench
+bin=tools/research/native/hip_init_bench
 [ -x "$bin" ] || { echo "build $bin first"; exit 2; }
 run() {  # label env...
   label=$1; shift

@@ -2,7 +2,7 @@
 """Does any ROCr runtime setting shorten ``hsa_init`` — the ~180 ms floor of the
 odh-gpu-probe init container (profiles/r3_p8)?
 
-Runs ``tools/native/hip_init_bench`` in its ``ODH_HSA_ONLY`` mode (hsa_init, then exit)
+Runs ``tools/research/native/hip_init_bench`` in its ``ODH_HSA_ONLY`` mode (hsa_init, then exit)
 under each setting, interleaved round by round so box drift hits every setting alike, and
 prints per-setting medians of hsa_init and of the whole process (spawn → reaped).
 
@@ -16,8 +16,8 @@ import subprocess
 import sys
 import time
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-BENCH = os.path.join(ROOT, "tools", "native", "hip_init_bench")
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+BENCH = os.path.join(ROOT, "tools", "research", "native", "hip_init_bench")
 
 SETTINGS = {
     "default": {},

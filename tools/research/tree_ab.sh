@@ -2,7 +2,7 @@
 # Interleaved A/B of two trees at N=1 on one box (box-to-box variance is ~10 %, so only an
 # interleaved pair on the same box tells a code change from the machine):
 #   git archive <rev> | tar -x -C ab_old && copy the built .so / binaries into ab_old
-#   gpurun --timeout 900 -- bash tools/tree_ab.sh <tag> [ab_old] [rounds]
+#   gpurun --timeout 900 -- bash tools/research/tree_ab.sh <tag> [ab_old] [rounds]
 set -e
 tag=${1:?usage: tree_ab.sh <tag> [old_dir] [rounds]}
 old=${2:-ab_old}

@@ -67,6 +67,9 @@ def parse(argv=None):
                         "deployed kf / odh+webhook pair (A/B measurements)")
     p.add_argument("--workers", type=int, default=1,
                    help="unsharded: --workers of the kf and odh managers (namespace-partitioned worker processes)")
+    p.add_argument("--burst", type=int, default=32,
+                   help="after the timed window: this many notebooks created at once (open loop), split over the "
+                        "ranks — time to all Ready, notebooks/s at saturation, admission latency (0: skip)")
     p.add_argument("--json-out", default=None)
     return p.parse_args(argv)
 

@@ -152,6 +152,8 @@ def measure(args) -> Optional[dict]:
             out["rccl_allreduce_check_ms"] = round(rccl_ms, 3)
         if res.get("probe_sample"):
             out["gpu_probe_init_container"] = probe_report(res["probe_sample"], out.get("p50_ready_ms"))
+        if res.get("burst"):
+            out["burst"] = res["burst"]
     dist.barrier()
     dist.destroy_process_group()
     return out
@@ -194,6 +196,92 @@ def writes_per_notebook(prof: dict, notebooks_per_step: int) -> dict:
     out = {v: round(prof.get(f"{v}_calls", 0.0) / n, 2) for v in ("create", "update", "patch", "delete")}
     out["total"] = round(sum(out.values()), 2)
     return out
+
+
+def _pcts(xs, qs=(0.5, 0.95, 0.99)) -> dict:
+    from bench import pct  # noqa: E402  (bench.py is the entry point)
+
+    out = {f"p{int(q * 100)}": (round(pct(xs, q), 3) if xs else None) for q in qs}
+    out["max"] = round(max(xs), 3) if xs else None
+    return out
+
+
+async def _burst(args, shard, dist, native, children: dict, use_odh: bool) -> Optional[dict]:
+    """Open-loop capacity (the reference's load generator,
+    ``kf/loadtest/start_notebooks.py:1-99``, applies N notebooks at once): ``--burst K``
+    notebooks are created at once, split over the ranks, against the control plane that just
+    ran the timed window.  Like the reference's ``jupyter_test.yaml`` they are CPU workbenches
+    (500m / 1Gi; the node's eight MI355X could not hold K GPU pods).  Reported: time from the
+    first create to the last Ready, notebooks/s at saturation, create→Ready p50/p95/p99, the
+    client's create latency (admission included), AdmissionReview latency at the apiserver
+    (every admission in the burst: the creates and the controllers' UPDATEs), CPU per notebook
+    per process, and teardown."""
+    from ..models import kinds
+    from ..models.notebook import notebook
+
+    rank, world = dist.get_rank(), dist.get_world_size()
+    total = int(args.burst)
+    k = total // world + (1 if rank < total % world else 0)
+    ns = shard.cfg.namespace
+    names = [f"burst-{rank}-{i}" for i in range(k)]
+    ann = {"notebooks.opendatahub.io/inject-auth": "true"} if use_odh else None
+    res = {"cpu": "500m", "memory": "1Gi"}
+    await shard.quiesce()
+    await _in_thread(dist.barrier)
+    adm0 = (await native.admissions(1 << 62))["seq"] if native is not None else None
+    cpu0 = {kk: _proc_cpu_s(pid) for kk, pid in children.items()}
+    await _in_thread(dist.barrier)
+    t0 = time.perf_counter()
+    ready_at, create_ms = {}, []
+    pending = set(names)
+
+    def check() -> bool:
+        for nm in list(pending):
+            if shard.notebook_ready(nm):
+                ready_at[nm] = time.perf_counter()
+                pending.discard(nm)
+        return not pending
+
+    async def create(nm):
+        c0 = time.perf_counter()
+        await shard.admin.create(notebook(nm, ns, image=NOTEBOOK_IMAGE, annotations=ann,
+                                          extra_container={"resources": {"requests": dict(res)}}))
+        create_ms.append((time.perf_counter() - c0) * 1e3)
+
+    await asyncio.gather(*(create(nm) for nm in names))
+    ok = await shard.wait_until(check, 180)
+    all_ready = max(ready_at.values()) - t0 if ready_at else None
+    await _in_thread(dist.barrier)
+    cpu = {kk: (_proc_cpu_s(pid) or 0.0) - (cpu0.get(kk) or 0.0) for kk, pid in children.items()
+           if cpu0.get(kk) is not None}
+    adm = (await native.admissions(adm0))["us"] if native is not None else []
+    t_del = time.perf_counter()
+    await asyncio.gather(*(shard.admin.delete(kinds.NOTEBOOK, nm, ns) for nm in names))
+    gone = await shard.wait_until(lambda: all(shard.gone(nm) for nm in names), 180)
+    teardown = time.perf_counter() - t_del
+    gathered = [None] * world
+    await _in_thread(dist.all_gather_object, gathered, {
+        "lat": [(ready_at[nm] - t0) * 1e3 for nm in names if nm in ready_at], "create": create_ms,
+        "all_ready": all_ready, "ok": ok and gone, "cpu": cpu, "adm": adm, "teardown": teardown, "k": k})
+    if rank != 0:
+        return None
+    lat = [x for g in gathered for x in g["lat"]]
+    span = max((g["all_ready"] or 0.0) for g in gathered)
+    cpu_all: dict = {}
+    for g in gathered:
+        for kk, v in g["cpu"].items():
+            cpu_all[kk] = cpu_all.get(kk, 0.0) + v
+    adm_ms = [u / 1e3 for g in gathered for u in g["adm"]]
+    return {
+        "notebooks": total, "per_rank": [g["k"] for g in gathered], "all_ok": all(g["ok"] for g in gathered),
+        "notebook": "CPU workbench, requests 500m / 1Gi (kf/loadtest/jupyter_test.yaml), inject-auth"
+                    if use_odh else "CPU workbench, requests 500m / 1Gi (kf/loadtest/jupyter_test.yaml)",
+        "all_ready_s": round(span, 4), "notebooks_per_s": round(total / span, 2) if span else None,
+        "ready_ms": _pcts(lat), "create_ms": _pcts([x for g in gathered for x in g["create"]]),
+        "admission_ms": {**_pcts(adm_ms), "n": len(adm_ms)},
+        "cpu_ms_per_notebook": {kk: round(v * 1e3 / max(1, total), 3) for kk, v in sorted(cpu_all.items())},
+        "teardown_s": round(max(g["teardown"] for g in gathered), 4),
+    }
 
 
 def io_delta(a: dict, b: dict) -> dict:
@@ -478,6 +566,10 @@ async def _drive(args, shard, dist, torch, children: Optional[dict] = None, nati
         samples.append({"ready_ms": ready_s * 1e3, "result": result, "exit_code": term.get("exitCode"),
                         "wall_ms": (result or {}).get("timings_ms", {}).get("total")})
 
+    burst = None
+    if getattr(args, "burst", 0) > 0:  # untimed: open-loop capacity of the same control plane
+        burst = await _burst(args, shard, dist, native, children, use_odh)
+
     el = torch.tensor([elapsed], dtype=torch.float64)
     await _in_thread(lambda: dist.all_reduce(el, op=dist.ReduceOp.MAX))
     gathered = [None] * dist.get_world_size()
@@ -505,6 +597,7 @@ async def _drive(args, shard, dist, torch, children: Optional[dict] = None, nati
             "apiserver_profile_per_step": prof, "breakdown": merge_breakdowns(g["settled"] for g in gathered),
             "quiesced": all(g["idle"] for g in gathered),
             "io_per_notebook": io_per_notebook([g["io"] for g in gathered], args.steps * len(gathered)),
+            "burst": burst,
             "recon_snapshot_lag_ms": round(max(g["snap_lag_ms"] for g in gathered), 3),
             "probe_sample": [s for g in gathered for s in g["probe"]],
             "lifecycle_ms_per_20_steps": [round(statistics.fmean(b), 3) for b in zip(*(g["blocks"] for g in gathered))]}

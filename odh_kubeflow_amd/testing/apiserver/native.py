@@ -51,8 +51,10 @@ class NativeApiServer:
 
     def __init__(self, uninstalled: Iterable[str] = (), gc: bool = False, token: Optional[str] = None,
                  host: str = "127.0.0.1", port: int = 0, history: int = 4096, binary: Optional[str] = None,
-                 env: Optional[dict] = None, audit_log_path: Optional[str] = None, audit_policy=None):
+                 env: Optional[dict] = None, audit_log_path: Optional[str] = None, audit_policy=None,
+                 write_latency_ms: float = 0.0):
         self.cfg = scheme_config(uninstalled, gc, token, history)
+        self.write_latency_ms = float(write_latency_ms)  # etcd-like storage round trip per write
         if audit_log_path:  # kube-apiserver --audit-log-path / --audit-policy-file (apiserver/audit.py)
             from .audit import DEFAULT_POLICY, AuditPolicy
 
@@ -77,6 +79,7 @@ class NativeApiServer:
             json.dump(self.cfg, f)
         self.proc = await asyncio.create_subprocess_exec(
             self.binary, "--config", self._cfg_path, "--host", self.host, "--port", str(self.port),
+            *(["--write-latency-ms", f"{self.write_latency_ms:g}"] if self.write_latency_ms > 0 else []),
             stdout=asyncio.subprocess.PIPE, env=child_env({**os.environ, **(self.env or {})}))
         line = await asyncio.wait_for(self.proc.stdout.readline(), 30)
         if not line.startswith(b"LISTENING"):
@@ -93,6 +96,14 @@ class NativeApiServer:
 
         async with aiohttp.ClientSession(timeout=aiohttp.ClientTimeout(total=30)) as s:
             async with s.get(self.url + "/metrics") as r:
+                return await r.json(content_type=None)
+
+    async def admissions(self, start: int = 0) -> dict:
+        """Admission webhook calls from call ``start`` on: ``{"seq": next start, "us": [wall µs]}``."""
+        import aiohttp
+
+        async with aiohttp.ClientSession(timeout=aiohttp.ClientTimeout(total=30)) as s:
+            async with s.get(self.url + f"/debug/admissions?from={int(start)}") as r:
                 return await r.json(content_type=None)
 
     async def stop(self) -> None:

@@ -22,15 +22,25 @@
 //     (api_defaults; the same rules as models/defaults.py), config key "defaulting";
 //   * discovery documents; bearer-token authentication.
 //
-// Concurrency: one thread per client connection (keep-alive), one global store mutex
-// held only for commits (updates are prepared and compared outside it), a per-resource
-// history lock the watch threads wait, wake and scan under (a watcher is woken only for
-// events its namespace / selector admits); every stored object is an immutable shared
-// snapshot, so readers and watchers never copy under a lock and each watch event is
-// serialised once.
+// Concurrency: one thread per client connection (keep-alive); a store lock PER RESOURCE
+// held only for commits (updates are prepared and compared outside it) — writes of
+// different kinds never wait for each other, as in kube-apiserver, whose storage has no
+// global lock — with the resourceVersion counter an atomic taken under the resource's lock
+// (so each resource's events are in resourceVersion order), and the garbage collector's
+// owner / uid indexes under a short lock of their own; cross-resource work (GC cascades,
+// foreground-deletion owners) runs after the commit, each object under its own resource's
+// lock.  A per-resource history lock the watch threads wait, wake and scan under (a watcher
+// is woken only for events its namespace / selector admits); every stored object is an
+// immutable shared snapshot, so readers and watchers never copy under a lock and each watch
+// event is serialised once.  The watch history is bounded per resource (--history events;
+// a namespace's history is the subsequence of its resource's, trimmed with it and dropped
+// once empty and unwatched), so memory does not grow with the number of namespaces.
+//
+// --write-latency-ms D adds D ms to every write before it commits (outside any lock): an
+// etcd-like storage round trip, for measurements that should not assume a free store.
 //
 // Usage: odh-apiserver --config scheme.json [--host 127.0.0.1] [--port 0] [--gc]
-//        [--token T] [--history 4096]; prints "LISTENING <port>" once ready.
+//        [--token T] [--history 4096] [--write-latency-ms 0]; prints "LISTENING <port>" once ready.
 
 #include <arpa/inet.h>
 #include <netdb.h>
@@ -588,17 +598,23 @@ struct Bucket {
   // AND namespace, so with one control-plane shard per GPU rank (each watching its own
   // namespaces) a write costs O(1) wake-ups instead of one per shard
   std::unordered_multimap<std::string, std::shared_ptr<WatchSlot>> watchers;
+  // rv of the newest event trimmed off `all` (0: none yet): a watch resuming from an older
+  // resourceVersion may have missed events and gets 410 Gone
+  int64_t dropped_rv = 0;
   // hist / seq / watchers have their own lock: watch streams wait, wake and scan under it
   // without touching the store lock the request threads commit under (lock order: the
-  // store lock, then this one — emit() runs inside a commit)
+  // resource's store lock, then this one — emit() runs inside a commit)
   std::mutex hmu;
+  // this resource's store lock: objs, and the commit order of its events
+  std::mutex mu;
 };
 
 struct Store {
-  std::mutex mu;
-  std::unordered_map<std::string, Bucket> data;
-  int64_t rv = 0;
+  std::mutex imu;  // owners / uids (the GC's indexes); taken inside a resource's lock, never around one
+  std::unordered_map<std::string, Bucket> data;  // one per resource, created at start-up, never rehashed
+  std::atomic<int64_t> rv{0};
   size_t history = 4096;
+  int64_t write_latency_us = 0;
   bool gc = false;
   bool defaulting = true;  // kube-apiserver defaulting of Pods / StatefulSets / Deployments / Services
   std::unordered_map<std::string, std::set<std::tuple<std::string, std::string, std::string>>> owners;
@@ -617,6 +633,14 @@ struct Prof {
   std::atomic<uint64_t> lock_hold_ns[C_N]{};
 } P;
 thread_local int t_cat = C_OTHER;
+
+// every admission webhook call's wall time in µs, the newest 65536 (GET /debug/admissions?from=N
+// answers those from call N on): admission latency percentiles under a burst of creates
+constexpr uint64_t kAdmitRing = 1 << 16;
+struct AdmitRing {
+  std::atomic<uint64_t> seq{0};
+  std::atomic<uint32_t> us[kAdmitRing];
+} g_admit;
 
 uint64_t thread_cpu_ns() {
   timespec ts;
@@ -664,39 +688,60 @@ void flush_wakes() {
 // kube-apiserver's) does — 4 rounds of 30 PAUSEs, then it sleeps.
 constexpr int kSpinRounds = 4, kSpinPauses = 30;
 
+// owners whose foreground-deletion finalizer may be due (a dependent of theirs was removed):
+// re-checked after the commit, under the owner's resource lock (fg_recheck)
+thread_local std::vector<std::string> t_fg;
+
+// one resource's store lock on the request path, timing only the contended acquisitions
 struct StoreLock {
+  std::mutex& mu;
   uint64_t t_acq;
-  StoreLock() {
-    if (!S.mu.try_lock()) {
-      uint64_t t0 = mono_ns();
-      bool got = false;
-      for (int r = 0; r < kSpinRounds && !got; ++r) {
-        for (int i = 0; i < kSpinPauses; ++i) __builtin_ia32_pause();
-        got = S.mu.try_lock();
-      }
-      if (!got) S.mu.lock();
-      P.lock_wait_ns += mono_ns() - t0;
-      P.lock_contended++;
-    }
-    t_acq = mono_ns();
-  }
+  explicit StoreLock(Bucket& b);
   ~StoreLock() {
     P.lock_hold_ns[t_cat] += mono_ns() - t_acq;  // who keeps the others waiting
-    S.mu.unlock();
+    mu.unlock();
     if (!t_wake.empty()) flush_wakes();
-    if (!t_gc.empty() && !t_gc_running) run_gc();
+    if ((!t_gc.empty() || !t_fg.empty()) && !t_gc_running) run_gc();
   }
   StoreLock(const StoreLock&) = delete;
   StoreLock& operator=(const StoreLock&) = delete;
 };
 
-Bucket& bucket(const Res& r) { return S.data[r.key]; }
+StoreLock::StoreLock(Bucket& b) : mu(b.mu) {
+  if (!mu.try_lock()) {
+    uint64_t t0 = mono_ns();
+    bool got = false;
+    for (int r = 0; r < kSpinRounds && !got; ++r) {
+      for (int i = 0; i < kSpinPauses; ++i) __builtin_ia32_pause();
+      got = mu.try_lock();
+    }
+    if (!got) mu.lock();
+    P.lock_wait_ns += mono_ns() - t0;
+    P.lock_contended++;
+  }
+  t_acq = mono_ns();
+}
+
+// S.data holds every resource from start-up on (init_buckets) and never changes shape, so
+// looking a bucket up needs no lock
+Bucket& bucket(const Res& r) { return S.data.find(r.key)->second; }
+
+void init_buckets() {
+  S.data.reserve(g_res.size() * 2);
+  for (auto& r : g_res) S.data[r->key];
+}
+
+// an etcd-like storage round trip before a write commits (--write-latency-ms), no lock held
+void storage_latency() {
+  if (S.write_latency_us > 0) std::this_thread::sleep_for(std::chrono::microseconds(S.write_latency_us));
+}
 
 void index_owner(const Res& r, const Value& o, bool remove) {
   const Value* m = md(o);
   const Value* refs = m ? m->get("ownerReferences") : nullptr;
   if (!refs || !refs->is_arr()) return;
   auto k = std::make_tuple(r.key, mget(o, "namespace"), mget(o, "name"));
+  std::lock_guard<std::mutex> ig(S.imu);
   for (auto& ref : refs->arr) {
     std::string u = ref.str_or("uid");
     if (u.empty()) continue;
@@ -712,7 +757,7 @@ void index_owner(const Res& r, const Value& o, bool remove) {
   }
 }
 
-// callers hold S.mu
+// callers hold the resource's store lock
 void emit(const Res& r, const char* type, Obj obj, Obj old) {
   Bucket& b = bucket(r);
   std::lock_guard<std::mutex> hg(b.hmu);
@@ -724,10 +769,24 @@ void emit(const Res& r, const char* type, Obj obj, Obj old) {
     Ev copy = e;  // the same event (shared object, old object and serialisation cache)
     copy.seq = ++h.seq;
     h.hist.push_back(std::move(copy));
-    while (h.hist.size() > S.history) h.hist.pop_front();
   }
   b.all.hist.push_back(std::move(e));
-  while (b.all.hist.size() > S.history) b.all.hist.pop_front();
+  while (b.all.hist.size() > S.history) {
+    // a namespace's history is the subsequence of the resource's: trim both together, so the
+    // history holds at most --history events per resource however many namespaces there are
+    const Ev& old = b.all.hist.front();
+    b.dropped_rv = old.rv;
+    const std::string ons = mget(*old.obj, "namespace");
+    if (!ons.empty()) {
+      auto it = b.by_ns.find(ons);
+      if (it != b.by_ns.end() && !it->second.hist.empty() && it->second.hist.front().rv == old.rv) {
+        it->second.hist.pop_front();
+        // an idle, unwatched namespace (e.g. deleted) keeps nothing; a watcher's Hist& stays valid
+        if (it->second.hist.empty() && ons != evns && !b.watchers.count(ons)) b.by_ns.erase(it);
+      }
+    }
+    b.all.hist.pop_front();
+  }
   const Ev& ev = b.all.hist.back();
   if ((b.all.seq & 1023) == 0) {
     // periodic broadcast: watchers of quiet namespaces advance past other namespaces'
@@ -1254,7 +1313,8 @@ void defaults(const Res& r, Value& o, bool api = true) {
     if (!spec.get("type")) spec["type"] = Value::str("ClusterIP");
     if (spec.str_or("type") == "ClusterIP" && spec.str_or("clusterIP").empty()) {
       char ip[32];
-      snprintf(ip, sizeof(ip), "10.96.%d.%d", (int)((S.rv >> 8) & 255), (int)((S.rv & 255) ? (S.rv & 255) : 1));
+      int64_t rvnow = S.rv.load();
+      snprintf(ip, sizeof(ip), "10.96.%d.%d", (int)((rvnow >> 8) & 255), (int)((rvnow & 255) ? (rvnow & 255) : 1));
       spec["clusterIP"] = Value::str(ip);
       Value ips = Value::array();
       ips.arr.push_back(Value::str(ip));
@@ -1350,7 +1410,7 @@ std::vector<Webhook> webhooks_for(const Res& r, const std::string& op) {
   if (!mwc) return out;
   std::vector<Obj> cfgs;
   {
-    StoreLock g;
+    StoreLock g(bucket(*mwc));
     for (auto& kv : bucket(*mwc).objs) cfgs.push_back(kv.second);
   }
   for (auto& c : cfgs) {
@@ -1410,7 +1470,7 @@ bool resolve_service(const Webhook& w, std::string* host, int* port) {
   if (!ep) return false;
   Obj o;
   {
-    StoreLock g;
+    StoreLock g(bucket(*ep));
     auto it = bucket(*ep).objs.find({w.svc_ns, w.svc_name});
     if (it == bucket(*ep).objs.end()) return false;
     o = it->second;
@@ -1630,7 +1690,7 @@ bool selectors_match(const Webhook& w, const Res& r, const Value& obj, const Val
   Res* nsr = by_kind("", "Namespace");
   Obj ns;
   if (nsr) {
-    StoreLock g;
+    StoreLock g(bucket(*nsr));
     auto it = bucket(*nsr).objs.find({"", mget(obj, "namespace")});
     if (it != bucket(*nsr).objs.end()) ns = it->second;
   }
@@ -1674,7 +1734,12 @@ Value admit(const char* op, const Res& r, Value obj, const Value* old) {
     uint64_t t_admit = mono_ns();
     struct AdmitTimer {
       uint64_t t0;
-      ~AdmitTimer() { P.admit_wall_ns += mono_ns() - t0; }
+      ~AdmitTimer() {
+        uint64_t d = mono_ns() - t0;
+        P.admit_wall_ns += d;
+        uint64_t i = g_admit.seq.fetch_add(1);
+        g_admit.us[i & (kAdmitRing - 1)].store((uint32_t)std::min<uint64_t>(d / 1000, 0xffffffffu));
+      }
     } admit_timer{t_admit};
     try {
       out = call_webhook(w, review);
@@ -1716,8 +1781,8 @@ std::pair<std::vector<Obj>, int64_t> do_list(const Res& r, const std::string& ns
   auto lr = parse_labels(lsel);
   auto fr = parse_fields(fsel);
   std::vector<Obj> out;
-  StoreLock g;
   Bucket& b = bucket(r);
+  StoreLock g(b);  // the list's resourceVersion: no commit of this resource is in flight
   if (!ns.empty() && r.namespaced) {
     for (auto it = b.objs.lower_bound({ns, ""}); it != b.objs.end() && it->first.first == ns; ++it)
       if ((lr.empty() || match_labels(lr, *it->second)) && (fr.empty() || match_fields(fr, *it->second)))
@@ -1727,12 +1792,12 @@ std::pair<std::vector<Obj>, int64_t> do_list(const Res& r, const std::string& ns
       if ((lr.empty() || match_labels(lr, *kv.second)) && (fr.empty() || match_fields(fr, *kv.second)))
         out.push_back(kv.second);
   }
-  return {out, S.rv};
+  return {out, S.rv.load()};
 }
 
 Obj do_get(const Res& r, const std::string& ns, const std::string& name) {
-  StoreLock g;
   Bucket& b = bucket(r);
+  StoreLock g(b);
   auto it = b.objs.find({r.namespaced ? ns : "", name});
   if (it == b.objs.end()) throw NotFound(r.err_res(), name);
   return it->second;
@@ -1774,15 +1839,19 @@ Obj do_create(const Res& r, const std::string& url_ns, Value obj, bool dry) {
   }
   std::pair<std::string, std::string> k{ns, mget(obj, "name")};
   if (S.defaulting) api_defaults(r, obj);  // object-local: outside the store lock
-  StoreLock g;
+  if (!dry) storage_latency();
   Bucket& b = bucket(r);
+  StoreLock g(b);
   if (b.objs.count(k)) throw AlreadyExists(r.err_res(), k.second);
   defaults(r, obj, false);
   if (dry) return std::make_shared<const Value>(std::move(obj));
   mdm(obj)["resourceVersion"] = Value::str(std::to_string(++S.rv));
   auto sp = std::make_shared<const Value>(std::move(obj));
   b.objs[k] = sp;
-  S.uids[mget(*sp, "uid")] = std::make_tuple(r.key, ns, k.second);
+  {
+    std::lock_guard<std::mutex> ig(S.imu);
+    S.uids[mget(*sp, "uid")] = std::make_tuple(r.key, ns, k.second);
+  }
   index_owner(r, *sp, false);
   S.writes++;
   emit(r, "ADDED", sp, nullptr);
@@ -1797,6 +1866,7 @@ Obj do_create(const Res& r, const std::string& url_ns, Value obj, bool dry) {
         auto slash = av.find('/');
         Res* owner = by_kind(slash == std::string::npos ? "" : av.substr(0, slash), ref.str_or("kind"));
         // an owner of a kind this server does not serve cannot be verified: keep the object
+        std::lock_guard<std::mutex> ig(S.imu);
         if (!owner || S.uids.count(ref.str_or("uid"))) live = true;
       }
       if (!live) {
@@ -1864,8 +1934,9 @@ Obj commit_update(const Res& r, const Obj& cur, Value nw) {
   const std::string ns = mget(*cur, "namespace"), name = mget(*cur, "name");
   prepare_update(r, *cur, nw);
   bool noop = equal_except_meta(nw, *cur);
-  StoreLock g;
+  if (!noop) storage_latency();
   Bucket& b = bucket(r);
+  StoreLock g(b);
   auto it = b.objs.find({ns, name});
   if (it == b.objs.end()) throw NotFound(r.err_res(), name);
   Obj live = it->second;
@@ -1896,7 +1967,7 @@ Obj commit_update(const Res& r, const Obj& cur, Value nw) {
 Obj do_update(const Res& r, const std::string& ns, const std::string& name, Value nw, const std::string& sub) {
   Obj cur;
   {
-    StoreLock g;
+    StoreLock g(bucket(r));
     auto it = bucket(r).objs.find({r.namespaced ? ns : "", name});
     if (it == bucket(r).objs.end()) throw NotFound(r.err_res(), name);
     cur = it->second;
@@ -1924,7 +1995,7 @@ Obj do_patch_once(const Res& r, const std::string& ns, const std::string& name, 
                     const std::string& ptype, const std::string& sub) {
   Obj cur;
   {
-    StoreLock g;
+    StoreLock g(bucket(r));
     auto it = bucket(r).objs.find({r.namespaced ? ns : "", name});
     if (it == bucket(r).objs.end()) throw NotFound(r.err_res(), name);
     cur = it->second;
@@ -1978,45 +2049,66 @@ Obj do_patch(const Res& r, const std::string& ns, const std::string& name, const
 void remove_locked(const Res& r, Obj live, Value final) {
   std::string ns = mget(*live, "namespace"), name = mget(*live, "name"), uid = mget(*live, "uid");
   bucket(r).objs.erase({ns, name});
-  S.uids.erase(uid);
+  {
+    std::lock_guard<std::mutex> ig(S.imu);
+    S.uids.erase(uid);
+  }
   index_owner(r, *live, true);
   S.writes++;
   auto fp = std::make_shared<const Value>(std::move(final));
   emit(r, "DELETED", fp, live);
   if (S.gc) t_gc.push_back(uid);  // cascaded once the lock is released (run_gc)
-  // foreground owners waiting for their last dependent
+  // foreground owners waiting for their last dependent: re-checked after the commit, each
+  // under its own resource's lock (fg_recheck)
   if (S.gc) {
     const Value* refs = md(*fp) ? md(*fp)->get("ownerReferences") : nullptr;
     if (refs && refs->is_arr())
       for (auto& ref : refs->arr) {
         std::string u = ref.str_or("uid");
-        auto loc = S.uids.find(u);
-        if (loc == S.uids.end() || S.owners.count(u)) continue;
-        Res* orr = by_key(std::get<0>(loc->second));
-        if (!orr) continue;
-        auto it = bucket(*orr).objs.find({std::get<1>(loc->second), std::get<2>(loc->second)});
-        if (it == bucket(*orr).objs.end()) continue;
-        const Value* f = md(*it->second)->get("finalizers");
-        bool fg = false;
-        if (f && f->is_arr())
-          for (auto& x : f->arr)
-            if (x.s == "foregroundDeletion") fg = true;
-        if (!fg) continue;
-        Value nw = *it->second;
-        Value nf = Value::array();
-        for (auto& x : f->arr)
-          if (x.s != "foregroundDeletion") nf.arr.push_back(x);
-        mdm(nw)["finalizers"] = nf;
-        mdm(nw)["resourceVersion"] = Value::str(std::to_string(++S.rv));
-        Obj old = it->second;
-        if (nf.arr.empty()) {
-          remove_locked(*orr, old, std::move(nw));
-        } else {
-          auto sp = std::make_shared<const Value>(std::move(nw));
-          it->second = sp;
-          emit(*orr, "MODIFIED", sp, old);
-        }
+        if (!u.empty()) t_fg.push_back(u);
       }
+  }
+}
+
+// An owner being deleted in the foreground loses its "foregroundDeletion" finalizer once
+// its last dependent is gone (and is removed if that was its last finalizer).
+void fg_recheck(const std::string& u) {
+  std::tuple<std::string, std::string, std::string> loc;
+  {
+    std::lock_guard<std::mutex> ig(S.imu);
+    auto it = S.uids.find(u);
+    if (it == S.uids.end() || S.owners.count(u)) return;
+    loc = it->second;
+  }
+  Res* orr = by_key(std::get<0>(loc));
+  if (!orr) return;
+  Bucket& b = bucket(*orr);
+  StoreLock g(b);
+  auto it = b.objs.find({std::get<1>(loc), std::get<2>(loc)});
+  if (it == b.objs.end() || mget(*it->second, "uid") != u) return;
+  {
+    std::lock_guard<std::mutex> ig(S.imu);
+    if (S.owners.count(u)) return;  // a dependent appeared meanwhile
+  }
+  const Value* f = md(*it->second)->get("finalizers");
+  bool fg = false;
+  if (f && f->is_arr())
+    for (auto& x : f->arr)
+      if (x.s == "foregroundDeletion") fg = true;
+  if (!fg) return;
+  Value nw = *it->second;
+  Value nf = Value::array();
+  for (auto& x : f->arr)
+    if (x.s != "foregroundDeletion") nf.arr.push_back(x);
+  mdm(nw)["finalizers"] = nf;
+  mdm(nw)["resourceVersion"] = Value::str(std::to_string(++S.rv));
+  Obj old = it->second;
+  if (nf.arr.empty()) {
+    remove_locked(*orr, old, std::move(nw));
+  } else {
+    auto sp = std::make_shared<const Value>(std::move(nw));
+    it->second = sp;
+    emit(*orr, "MODIFIED", sp, old);
   }
 }
 
@@ -2040,21 +2132,31 @@ void sync_delete_locked(const Res& r, const std::string& ns, const std::string& 
   remove_locked(r, cur, std::move(final));
 }
 
+// Background cascade for a removed (or foreground-deleting) owner: each dependent whose
+// other owners are all gone is deleted, under its own resource's lock (no lock held here).
 void gc_dependents(const std::string& owner_uid) {
-  auto it = S.owners.find(owner_uid);
-  if (it == S.owners.end()) return;
-  auto deps = it->second;
+  std::set<std::tuple<std::string, std::string, std::string>> deps;
+  {
+    std::lock_guard<std::mutex> ig(S.imu);
+    auto it = S.owners.find(owner_uid);
+    if (it == S.owners.end()) return;
+    deps = it->second;
+  }
   for (auto& d : deps) {
     Res* r = by_key(std::get<0>(d));
     if (!r) continue;
-    auto oit = bucket(*r).objs.find({std::get<1>(d), std::get<2>(d)});
-    if (oit == bucket(*r).objs.end()) continue;
+    Bucket& b = bucket(*r);
+    StoreLock g(b);  // its release does not recurse (t_gc_running); new owners queue up
+    auto oit = b.objs.find({std::get<1>(d), std::get<2>(d)});
+    if (oit == b.objs.end()) continue;
     bool other_live = false;
-    if (const Value* refs = md(*oit->second)->get("ownerReferences"))
+    if (const Value* refs = md(*oit->second)->get("ownerReferences")) {
+      std::lock_guard<std::mutex> ig(S.imu);
       for (auto& ref : refs->arr) {
         std::string u = ref.str_or("uid");
         if (u != owner_uid && S.uids.count(u)) other_live = true;
       }
+    }
     if (other_live) continue;
     sync_delete_locked(*r, std::get<1>(d), std::get<2>(d));
   }
@@ -2062,15 +2164,21 @@ void gc_dependents(const std::string& owner_uid) {
 
 void run_gc() noexcept {
   t_gc_running = true;
-  while (!t_gc.empty()) {
-    std::vector<std::string> uids;
+  while (!t_gc.empty() || !t_fg.empty()) {
+    std::vector<std::string> uids, fgs;
     uids.swap(t_gc);
+    fgs.swap(t_fg);
     for (auto& u : uids) {
       try {
-        StoreLock g;  // its release does not recurse (t_gc_running); new owners queue up here
         gc_dependents(u);
       } catch (...) {
         // a dependent that vanished meanwhile: nothing left to collect for it
+      }
+    }
+    for (auto& u : fgs) {
+      try {
+        fg_recheck(u);
+      } catch (...) {
       }
     }
   }
@@ -2079,7 +2187,8 @@ void run_gc() noexcept {
 
 Value do_delete(const Res& r, const std::string& ns_, const std::string& name, const Value& opts) {
   std::string ns = r.namespaced ? ns_ : "";
-  StoreLock g;
+  storage_latency();
+  StoreLock g(bucket(r));
   auto it = bucket(r).objs.find({ns, name});
   if (it == bucket(r).objs.end()) throw NotFound(r.err_res(), name);
   Obj cur = it->second;
@@ -2112,7 +2221,7 @@ Value do_delete(const Res& r, const std::string& ns_, const std::string& name, c
     bool fg = false;
     for (auto& x : fins.arr)
       if (x.s == "foregroundDeletion") fg = true;
-    if (fg) gc_dependents(mget(*cur, "uid"));
+    if (fg) t_gc.push_back(mget(*cur, "uid"));  // dependents first, after this commit (run_gc)
     return *sp;
   }
   Value final = *cur;
@@ -2603,8 +2712,8 @@ void serve_watch(int fd, Res& r, const Path& p, const Request& rq) {
   } unregister{wb, ns, &slot};
   slot.wants = wants;
   {
-    StoreLock g;
     Bucket& b = bucket(r);
+    StoreLock g(b);
     std::lock_guard<std::mutex> hg(b.hmu);
     wb = &b;
     wh = ns.empty() ? &b.all : &b.by_ns[ns];
@@ -2621,8 +2730,8 @@ void serve_watch(int fd, Res& r, const Path& p, const Request& rq) {
     } else {
       int64_t since = std::stoll(rv);
       const std::deque<Ev>& hist = wh->hist;
-      // 410 when events after `since` may have fallen off this watch's bounded history
-      if (hist.size() >= S.history && since < hist.front().rv - 1) {
+      // 410 when an event after `since` has fallen off the resource's bounded history
+      if (since < b.dropped_rv) {
         Value ev = Value::object();
         ev["type"] = Value::str("ERROR");
         ev["object"] = status_obj(Gone());
@@ -2701,8 +2810,8 @@ void serve_watch(int fd, Res& r, const Path& p, const Request& rq) {
       bm["apiVersion"] = Value::str(r.api_version(p.version));
       Value m = Value::object();
       {
-        StoreLock g;
-        m["resourceVersion"] = Value::str(std::to_string(S.rv));
+        StoreLock g(*wb);  // no commit of this resource in flight: every event below it was sent
+        m["resourceVersion"] = Value::str(std::to_string(S.rv.load()));
       }
       bm["metadata"] = m;
       Value ev = Value::object();
@@ -2753,12 +2862,20 @@ bool handle(int fd, Request& rq) {
     return respond(fd, 200, "{\"major\":\"1\",\"minor\":\"32\",\"gitVersion\":\"v1.32.8-odh-kubeflow-amd-native\"}",
                    rq.keep_alive);
   }
-  if (rq.method == "GET" && rq.path == "/metrics") {
-    int64_t rv;
-    {
-      StoreLock g;
-      rv = S.rv;
+  if (rq.method == "GET" && rq.path == "/debug/admissions") {
+    uint64_t end = g_admit.seq.load();
+    uint64_t from = rq.q.count("from") ? std::stoull("0" + rq.q.at("from")) : 0;
+    if (end > kAdmitRing && from < end - kAdmitRing) from = end - kAdmitRing;
+    std::string out = "{\"seq\":" + std::to_string(end) + ",\"us\":[";
+    for (uint64_t i = from; i < end; ++i) {
+      if (i != from) out += ',';
+      out += std::to_string(g_admit.us[i & (kAdmitRing - 1)].load());
     }
+    out += "]}";
+    return respond(fd, 200, out, rq.keep_alive);
+  }
+  if (rq.method == "GET" && rq.path == "/metrics") {
+    int64_t rv = S.rv.load();
     char buf[256];
     snprintf(buf, sizeof(buf),
              "{\"requests\":%llu,\"writes\":%llu,\"webhook_calls\":%llu,\"resourceVersion\":%lld,\"prof\":{",
@@ -2989,6 +3106,7 @@ int main(int argc, char** argv) {
     else if (a == "--gc") S.gc = true;
     else if (a == "--token") g_token = next();
     else if (a == "--history") S.history = std::stoul(next());
+    else if (a == "--write-latency-ms") S.write_latency_us = (int64_t)(std::stod(next()) * 1000.0);
     else {
       fprintf(stderr, "unknown flag %s\n", a.c_str());
       return 2;
@@ -3002,6 +3120,7 @@ int main(int argc, char** argv) {
   std::string tok = g_token;
   size_t hist = S.history;
   load_config(config);
+  init_buckets();
   if (gc_flag) S.gc = true;
   if (!tok.empty()) g_token = tok;
   if (hist != 4096) S.history = hist;

@@ -70,6 +70,20 @@ def parse(argv=None):
     p.add_argument("--burst", type=int, default=32,
                    help="after the timed window: this many notebooks created at once (open loop), split over the "
                         "ranks — time to all Ready, notebooks/s at saturation, admission latency (0: skip)")
+    p.add_argument("--platform-workers", type=int, default=0,
+                   help="node platform: StatefulSet-controller and kubelet stand-in processes (0: one per two ranks)")
+    p.add_argument("--burst-rounds", type=int, default=2,
+                   help="bursts in a row; the last is reported (the first warms the apiserver's webhook "
+                        "connections, as on a running cluster)")
+    p.add_argument("--openshift-pull-secret-ms", type=float, default=-1.0,
+                   help=">= 0: an OpenShift-like cluster — the OpenShift APIs served and every ServiceAccount's "
+                        "dockercfg pull secret added this many ms after it appears (the reference's lock waits "
+                        "for it); default: vanilla Kubernetes")
+    p.add_argument("--write-latency-ms", type=float, default=0.0,
+                   help="etcd-like storage latency the native apiserver adds to every write")
+    p.add_argument("--no-configs", action="store_true",
+                   help="skip the BASELINE configs #2-#5 sample that follows the N=1 run (real workbench "
+                        "processes, the webhook path across 8, GPU-busy culling across 8)")
     p.add_argument("--json-out", default=None)
     return p.parse_args(argv)
 
@@ -209,12 +223,65 @@ def main(argv=None):
                 "reconciles_per_notebook", "p50_teardown_ms")}
     else:
         out = _run_inprocess(args, n)
+    if rank == 0 and out is not None and n == 1 and not args.no_configs:
+        out["configs"] = run_configs(args)
     if rank == 0 and out is not None:
         print(json.dumps(out), flush=True)
         if args.json_out:
             with open(args.json_out, "w") as f:
                 json.dump(out, f, indent=1)
     return 0
+
+
+CONFIG_RUNS = (
+    # (key, BASELINE config, command, time limit s, needs the GPU)
+    ("real_pods", "#2/#3: 1 and 8 notebooks whose container is a real PyTorch-ROCm workbench process on the MI355X",
+     ["tools/bench_real_pods.py", "--notebooks", "1,8", "--repeats", "1", "--gpu-probe", "off"], 90, True),
+    ("webhook_8", "#4: odh webhook path (kube-rbac-proxy sidecar + Istio VirtualService + HTTPRoute) across 8",
+     ["tools/bench_webhook.py", "--rounds", "3", "--warmup", "1"], 60, False),
+    ("culling_8", "#5: idle culling on amdgpu busy counters across 8 GPU notebooks, under MFMA load",
+     ["tools/bench_culling.py", "--idle-s", "1", "--period-s", "0.2", "--load-s", "3"], 90, True),
+)
+
+
+def run_configs(args) -> dict:
+    """BASELINE configs #2-#5, untimed, after the headline run (N=1 only): each tool runs as a
+    child process with a short setting and its JSON result is carried in the bench line, so the
+    driver observes them.  Without a GPU the real-pod sample is skipped and culling runs on a
+    synthetic sysfs tree."""
+    import subprocess
+
+    try:
+        import torch
+
+        gpu = torch.cuda.device_count() > 0
+    except Exception:  # noqa: BLE001
+        gpu = False
+    here = os.path.dirname(os.path.abspath(__file__))
+    out = {}
+    for key, what, cmd, limit, needs_gpu in CONFIG_RUNS:
+        if needs_gpu and not gpu:
+            if key != "culling_8":
+                out[key] = {"config": what, "skipped": "no GPU visible"}
+                continue
+            cmd = [*cmd, "--cpu"]
+        t0 = time.perf_counter()
+        try:
+            r = subprocess.run([sys.executable, *cmd], cwd=here, capture_output=True, text=True, timeout=limit)
+            lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+            if r.returncode != 0 or not lines:
+                out[key] = {"config": what, "error": f"rc={r.returncode}: {(r.stderr or r.stdout)[-400:]}"}
+                continue
+            docs = [json.loads(ln) for ln in lines]
+            for d in docs:  # the per-notebook detail stays in the tool's own output
+                d.pop("per_notebook", None)
+                d.pop("device_ids", None)
+            out[key] = {"config": what, "result": docs if len(docs) > 1 else docs[0]}
+        except subprocess.TimeoutExpired:
+            out[key] = {"config": what, "error": f"timed out after {limit} s"}
+        out[key]["wall_s"] = round(time.perf_counter() - t0, 2)
+        out[key]["command"] = " ".join(["python", *cmd])
+    return out
 
 
 def _run_inprocess(args, n: int) -> dict:

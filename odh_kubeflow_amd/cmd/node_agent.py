@@ -37,8 +37,17 @@ def parse(argv=None):
     p.add_argument("--token-file", default="",
                    help="bearer token the /gpu/* and /metrics endpoints require (nodeagent/auth.py); "
                         "'' serves them unauthenticated")
+    p.add_argument("--tls-cert-dir", default="",
+                   help="serve HTTPS with tls.crt / tls.key from this directory (reloaded when rotated)")
+    p.add_argument("--cert-reload-seconds", type=float, default=10.0)
+    p.add_argument("--insecure", action="store_true",
+                   help="serve plain HTTP (no --tls-cert-dir): tests and development only")
     p.add_argument("--debug-log", action="store_true")
-    return p.parse_args(argv)
+    args = p.parse_args(argv)
+    if not args.tls_cert_dir and not args.insecure:
+        p.error("--tls-cert-dir is required (the token and the busy/idle answers must not cross the node "
+                "network in cleartext); --insecure serves plain HTTP")
+    return args
 
 
 def build(args):
@@ -67,7 +76,15 @@ def build(args):
                         args.token_file)
     else:
         log.warning("no --token-file: /gpu/* and /metrics are served unauthenticated on the hostPort")
-    return NodeTelemetryAgent(telemetry, attributor, host=args.bind, port=args.port, token=token)
+    if args.tls_cert_dir:
+        missing = [f for f in ("tls.crt", "tls.key") if not os.path.exists(os.path.join(args.tls_cert_dir, f))]
+        if missing:
+            raise SystemExit(f"node agent serving certificate missing in {args.tls_cert_dir}: {', '.join(missing)} "
+                             "(cmd/webhook_certs.py --node-agent-secret writes it)")
+    else:
+        log.warning("--insecure: serving plain HTTP")
+    return NodeTelemetryAgent(telemetry, attributor, host=args.bind, port=args.port, token=token,
+                              tls_cert_dir=args.tls_cert_dir or None, cert_reload_s=args.cert_reload_seconds)
 
 
 async def amain(argv=None) -> int:
@@ -77,7 +94,7 @@ async def amain(argv=None) -> int:
     setup_logging(debug=args.debug_log)
     agent = build(args)
     await agent.start()
-    log.info("node agent serving on %s:%d (pid %d)", args.bind, agent.port, os.getpid())
+    log.info("node agent serving %s on %s:%d (pid %d)", agent.scheme, args.bind, agent.port, os.getpid())
     try:
         await signal_event().wait()
     finally:

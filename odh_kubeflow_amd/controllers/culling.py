@@ -97,6 +97,9 @@ class CullerConfig:
     gpu_busy_threshold: float = 5.0
     gpu_agent_port: int = 9464
     gpu_agent_token_file: str = ""  # bearer token for the node agent (nodeagent/auth.py); "" = none
+    gpu_agent_ca_file: str = ""  # the node agents' CA (HTTPS); "" with gpu_agent_insecure false: no GPU data
+    gpu_agent_server_name: str = ""  # the name the agents' certificate carries
+    gpu_agent_insecure: bool = False  # plain HTTP to the agents (tests, development)
     gpu_vram_active_bytes: float = 0.0  # 0: resident VRAM is not activity (see module docstring)
     http_timeout_s: float = 10.0
     startup_allowance_s: float = 600.0  # a Pending pod younger than cull_idle_time + this is not checked
@@ -126,6 +129,10 @@ class CullerConfig:
         c.gpu_busy_threshold = float(env_default(env, "CULLING_GPU_BUSY_THRESHOLD", "5"))
         c.gpu_agent_port = int(env_default(env, "CULLING_GPU_AGENT_PORT", "9464"))
         c.gpu_agent_token_file = env.get("CULLING_GPU_AGENT_TOKEN_FILE", "")
+        c.gpu_agent_ca_file = env.get("CULLING_GPU_AGENT_CA_FILE", "")
+        c.gpu_agent_server_name = env_default(
+            env, "CULLING_GPU_AGENT_SERVER_NAME", f"mi355x-node-agent.{env.get('K8S_NAMESPACE') or 'opendatahub'}.svc")
+        c.gpu_agent_insecure = env_default(env, "CULLING_GPU_AGENT_INSECURE", "false").strip().lower() == "true"
         c.gpu_vram_active_bytes = float(env_default(env, "CULLING_GPU_VRAM_ACTIVE_BYTES", "0"))
         c.startup_allowance_s = float(env_default(env, "CULL_STARTUP_ALLOWANCE", "10")) * 60.0
         if env.get("CULL_STARTUP_ALLOWANCE_SECONDS"):
@@ -418,20 +425,35 @@ class NodeAgentActivity(GpuActivity):
     The agent is a DaemonSet with a hostPort, so it is at ``<pod.status.hostIP>:<port>``;
     ``endpoint_for(pod) -> "host:port"`` overrides that (test harnesses whose fake nodes
     share one IP).
+
+    Over HTTPS (``ca_file``): the agent's certificate must chain to that CA and carry
+    ``server_name`` (one serving certificate for every node's agent, ``cmd/webhook_certs
+    --node-agent-secret``), so the bearer token and the busy/idle answers never cross the node
+    network in cleartext and a spoofed agent cannot cull or pin a notebook.  Without a CA the
+    agents are not asked at all (no GPU data: the Jupyter signal decides) unless ``insecure``.
     """
 
     def __init__(self, port: int = 9464, timeout_s: float = 2.0,
-                 endpoint_for: Optional[Callable[[dict], Optional[str]]] = None, token_file: str = ""):
+                 endpoint_for: Optional[Callable[[dict], Optional[str]]] = None, token_file: str = "",
+                 ca_file: str = "", server_name: str = "", insecure: bool = False):
         self.port = port
         self.token = None
         if token_file:
             from ..nodeagent.auth import TokenFile
 
             self.token = TokenFile(token_file)
+        self.ssl = None
+        if ca_file:
+            from ..utils.tlsreload import client_context
+
+            self.ssl = client_context(ca_file)
+        self.server_name = server_name or None
+        self.insecure = insecure
         self.timeout_s = timeout_s
         self.endpoint_for = endpoint_for or self.default_endpoint
         self._session = None
         self.requests = 0
+        self.refused_cleartext = 0
 
     def default_endpoint(self, pod: dict) -> Optional[str]:
         """``<hostIP>:<port>`` of the pod's node agent; IPv6 literals are bracketed
@@ -456,6 +478,12 @@ class NodeAgentActivity(GpuActivity):
         ep = self.endpoint_for(pod)
         if not ep:
             return None
+        if self.ssl is None and not self.insecure:
+            if not self.refused_cleartext:
+                log.warning("no node-agent CA (CULLING_GPU_AGENT_CA_FILE): GPU activity is not queried over plain "
+                            "HTTP; culling falls back to the Jupyter signal")
+            self.refused_cleartext += 1
+            return None
         if self._session is None or self._session.closed:
             self._session = aiohttp.ClientSession(timeout=aiohttp.ClientTimeout(total=self.timeout_s))
         q = urllib.parse.urlencode({"pod_uid": m.uid(pod), "namespace": m.namespace(pod), "name": m.name(pod),
@@ -463,7 +491,9 @@ class NodeAgentActivity(GpuActivity):
         self.requests += 1
         try:
             headers = self.token.header() if self.token is not None else None
-            async with self._session.get(f"http://{ep}/gpu/activity?{q}", headers=headers) as resp:
+            scheme = "https" if self.ssl is not None else "http"
+            tls = {"ssl": self.ssl, "server_hostname": self.server_name} if self.ssl is not None else {}
+            async with self._session.get(f"{scheme}://{ep}/gpu/activity?{q}", headers=headers, **tls) as resp:
                 if resp.status != 200:
                     return None
                 data = await resp.json()
@@ -491,7 +521,10 @@ class CullingReconciler:
         self.cfg = config or CullerConfig.from_env(self.env)
         self.gpu: Optional[GpuActivity] = activity
         if self.gpu is None and self.cfg.activity_source in ("amdgpu", "combined"):
-            self.gpu = NodeAgentActivity(port=self.cfg.gpu_agent_port, token_file=self.cfg.gpu_agent_token_file)
+            self.gpu = NodeAgentActivity(port=self.cfg.gpu_agent_port, token_file=self.cfg.gpu_agent_token_file,
+                                         ca_file=self.cfg.gpu_agent_ca_file,
+                                         server_name=self.cfg.gpu_agent_server_name,
+                                         insecure=self.cfg.gpu_agent_insecure)
         self.jupyter = jupyter or JupyterActivity(self.cfg, use_pod_endpoint=self.env.get(
             "CULLER_USE_POD_ENDPOINT", "false") == "true")
         self.culled = 0

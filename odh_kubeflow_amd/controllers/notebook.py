@@ -140,6 +140,34 @@ def _multi_gpu_env(pod_spec: dict, raw: str) -> None:
             have.add(k)
 
 
+def parse_gids(raw: str) -> List[int]:
+    """``GPU_DEVICE_GROUPS``: ``"44,110"`` (or ``"video=44,render=110"``) → [44, 110]; entries
+    that are not non-negative integers are skipped."""
+    out: List[int] = []
+    for item in (raw or "").split(","):
+        v = item.strip().rpartition("=")[2].strip()
+        if v.isdigit() and int(v) not in out:
+            out.append(int(v))
+    return out
+
+
+def _gpu_device_groups(pod_spec: dict, raw: str) -> None:
+    """The device plugin hands ``/dev/kfd`` and ``/dev/dri/renderD*`` to the container with the
+    host's owner and mode — typically ``root:render 0660`` (the ``video`` group on older
+    hosts).  A container running as a non-root user (the probe as 65532, notebook images as
+    1000) opens them only as a member of that group, so pods that request ``amd.com/gpu`` get
+    the operator's ``GPU_DEVICE_GROUPS`` as ``securityContext.supplementalGroups`` (they apply
+    to every container of the pod, init containers included).  A value the user set wins."""
+    gids = parse_gids(raw)
+    if not gids or gpu_request(pod_spec) <= 0:
+        return
+    sc = pod_spec.get("securityContext")
+    if sc is None:
+        sc = pod_spec["securityContext"] = {}
+    if sc.get("supplementalGroups") is None:
+        sc["supplementalGroups"] = gids
+
+
 GPU_PROBE_ANNOTATION = "amd.com/gpu-probe"
 GPU_PROBE_CONTAINER = "amd-gpu-probe"
 DEFAULT_GPU_PROBE_IMAGE = "quay.io/opendatahub/odh-kubeflow-amd-gpu-probe:main"  # manifests pin the release
@@ -247,6 +275,8 @@ def generate_statefulset(nb: dict, is_generate_name: bool, env: Mapping[str, str
         _gpu_shm(nb, pod_spec, env["GPU_SHM_SIZE_PER_GPU"])
     if env.get("MULTI_GPU_ENV"):
         _multi_gpu_env(pod_spec, env["MULTI_GPU_ENV"])
+    if env.get("GPU_DEVICE_GROUPS"):
+        _gpu_device_groups(pod_spec, env["GPU_DEVICE_GROUPS"])
     _gpu_probe(nb, pod_spec, env)
     return sts
 

@@ -52,6 +52,13 @@ WEBHOOK_CERT_SECRET = "odh-notebook-controller-webhook-cert"  # created by servi
 WEBHOOK_SERVICE = "odh-notebook-controller-webhook-service"
 AGENT_TOKEN_SECRET = "mi355x-node-agent-token"  # nodeagent/auth.py TOKEN_SECRET
 AGENT_TOKEN_MOUNT = "/var/run/secrets/odh/node-agent"
+# the node agents serve HTTPS: one serving cert for every node's agent (cmd/webhook_certs
+# --node-agent-secret), its CA published to the culler in a ConfigMap (nodeagent/server.py)
+AGENT_NAME = "mi355x-node-agent"
+AGENT_TLS_SECRET = "mi355x-node-agent-tls"
+AGENT_TLS_MOUNT = "/var/run/secrets/odh/node-agent-tls"
+AGENT_CA_CONFIGMAP = "mi355x-node-agent-ca"
+AGENT_CA_MOUNT = "/var/run/odh/node-agent-ca"
 MWC_NAME = "mutating-webhook-configuration"
 SHARDS = 8  # one control-plane shard per MI355X of an 8-GPU node
 CULLER_LITERALS = ["ENABLE_CULLING=false", "CULL_IDLE_TIME=1440", "IDLENESS_CHECK_PERIOD=1",
@@ -60,7 +67,7 @@ CULLER_LITERALS = ["ENABLE_CULLING=false", "CULL_IDLE_TIME=1440", "IDLENESS_CHEC
 CULLER_KEYS = [lit.split("=", 1)[0] for lit in CULLER_LITERALS]
 PARAMS_ENV = "USE_ISTIO=false\nISTIO_GATEWAY=kubeflow/kubeflow-gateway\nISTIO_HOST=*\n" \
              "CLUSTER_DOMAIN=cluster.local\nADD_FSGROUP=true\nGPU_NODE_SELECTOR=false\n" \
-             "GPU_SHM_SIZE_PER_GPU=\nMULTI_GPU_ENV=\n" \
+             "GPU_SHM_SIZE_PER_GPU=\nMULTI_GPU_ENV=\nGPU_DEVICE_GROUPS=\n" \
              "GPU_STARTUP_PROBE=false\nGPU_PROBE_RCCL=false\n"
 # GPU_STARTUP_PROBE: the start-up probe for every GPU notebook (else opt-in per notebook,
 # amd.com/gpu-probe); GPU_PROBE_RCCL: its RCCL all-reduce for every probed multi-GPU notebook
@@ -71,10 +78,14 @@ def params_env(version: str) -> str:
     MI355X ones; the start-up probe image is pinned to the release (images/probe.Dockerfile)."""
     return PARAMS_ENV + f"GPU_PROBE_IMAGE={PROBE_IMAGE_NAME}:{version}\n"
 # MI355X node settings (overlays mi355x and mi355x-sharded)
+MI355X_DEVICE_GROUPS = "44,110"  # video, render (Ubuntu 22.04 ROCm hosts); set to the node's own gids
 MI355X_PARAMS = ["GPU_NODE_SELECTOR=true", "GPU_SHM_SIZE_PER_GPU=16Gi",
                  # multi-GPU notebooks: RCCL's intra-node IPC over dmabuf (hosts whose amdgpu
                  # driver only offers dmabuf IPC fail hipIpcGetMemHandle otherwise)
-                 "MULTI_GPU_ENV=HSA_ENABLE_IPC_MODE_LEGACY=0"]
+                 "MULTI_GPU_ENV=HSA_ENABLE_IPC_MODE_LEGACY=0",
+                 # the host groups owning /dev/kfd and /dev/dri/renderD* (video, render on Ubuntu
+                 # hosts): non-root containers of GPU pods get them as supplementalGroups
+                 f"GPU_DEVICE_GROUPS={MI355X_DEVICE_GROUPS}"]
 MI355X_CULLER = ["CULLING_ACTIVITY_SOURCE=combined", "ENABLE_CULLING=true"]
 # overlay mi355x: each manager runs its controllers in this many namespace-partitioned worker
 # processes (runtime/workers.py; the odh webhook stays on the supervisor's own event loop) —
@@ -217,7 +228,24 @@ RESTRICTED = {"allowPrivilegeEscalation": False, "capabilities": {"drop": ["ALL"
 def _culler_env() -> List[dict]:
     return [{"name": k, "valueFrom": {"configMapKeyRef": {"name": "notebook-controller-culler-config",
                                                           "key": k, "optional": True}}} for k in CULLER_KEYS] + [
-        {"name": "CULLING_GPU_AGENT_TOKEN_FILE", "value": f"{AGENT_TOKEN_MOUNT}/token"}]
+        {"name": "CULLING_GPU_AGENT_TOKEN_FILE", "value": f"{AGENT_TOKEN_MOUNT}/token"},
+        {"name": "CULLING_GPU_AGENT_CA_FILE", "value": f"{AGENT_CA_MOUNT}/ca.crt"},
+        {"name": "AGENT_NAMESPACE", "valueFrom": {"fieldRef": {"fieldPath": "metadata.namespace"}}},
+        {"name": "CULLING_GPU_AGENT_SERVER_NAME", "value": f"{AGENT_NAME}.$(AGENT_NAMESPACE).svc"}]
+
+
+def _culler_env_index(name: str) -> int:
+    """Position of ``name`` in the kf manager container's env (JSON patches address it by index)."""
+    return [e["name"] for e in kf_deployment()["spec"]["template"]["spec"]["containers"][0]["env"]].index(name)
+
+
+def _agent_ca_volume() -> dict:
+    """The node agents' CA for the culler (``cmd/webhook_certs --node-agent-ca-configmap``).
+    Optional: until it exists the culler asks no agent (no GPU data; Jupyter decides)."""
+    return {"name": "node-agent-ca", "configMap": {"name": AGENT_CA_CONFIGMAP, "optional": True}}
+
+
+AGENT_CA_MOUNT_SPEC = {"name": "node-agent-ca", "mountPath": AGENT_CA_MOUNT, "readOnly": True}
 
 
 def _agent_token_volume() -> dict:
@@ -250,14 +278,14 @@ def kf_deployment() -> dict:
          "env": _culler_env(),
          "ports": [{"name": "metrics", "containerPort": 8080}, {"name": "probes", "containerPort": 8081}],
          "resources": {"requests": {"cpu": "500m", "memory": "256Mi"}, "limits": {"cpu": "2", "memory": "2Gi"}},
-         "volumeMounts": [dict(AGENT_TOKEN_MOUNT_SPEC)],
+         "volumeMounts": [dict(AGENT_TOKEN_MOUNT_SPEC), dict(AGENT_CA_MOUNT_SPEC)],
          "securityContext": dict(RESTRICTED), **_probes()}
     return {"apiVersion": "apps/v1", "kind": "Deployment",
             "metadata": {"name": "deployment", "labels": {"app": "notebook-controller"}},
             "spec": {"replicas": 1, "selector": {"matchLabels": {"app": "notebook-controller"}},
                      "template": {"metadata": {"labels": {"app": "notebook-controller"}},
                                   "spec": {"serviceAccountName": "service-account", "containers": [c],
-                                           "volumes": [_agent_token_volume()]}}}}
+                                           "volumes": [_agent_token_volume(), _agent_ca_volume()]}}}}
 
 
 def odh_deployment() -> dict:
@@ -295,14 +323,15 @@ def node_agent_daemonset() -> dict:
          "args": ["--port=9464", "--sysfs-root=/host/sys", "--proc-root=/host/proc",
                   "--pod-resources-socket=/var/lib/kubelet/pod-resources/kubelet.sock",
                   "--device-plugin-checkpoint=/var/lib/kubelet/device-plugins/kubelet_internal_checkpoint",
-                  f"--token-file={AGENT_TOKEN_MOUNT}/token"],
+                  f"--token-file={AGENT_TOKEN_MOUNT}/token", f"--tls-cert-dir={AGENT_TLS_MOUNT}"],
          "ports": [{"name": "gpu-activity", "containerPort": 9464, "hostPort": 9464}],
-         "livenessProbe": {"httpGet": {"path": "/healthz", "port": 9464}, "periodSeconds": 20},
+         "livenessProbe": {"httpGet": {"path": "/healthz", "port": 9464, "scheme": "HTTPS"}, "periodSeconds": 20},
          "volumeMounts": [{"name": "sys", "mountPath": "/host/sys", "readOnly": True},
                           {"name": "proc", "mountPath": "/host/proc", "readOnly": True},
                           {"name": "pod-resources", "mountPath": "/var/lib/kubelet/pod-resources"},
                           {"name": "device-plugins", "mountPath": "/var/lib/kubelet/device-plugins",
-                           "readOnly": True}, dict(AGENT_TOKEN_MOUNT_SPEC)],
+                           "readOnly": True}, dict(AGENT_TOKEN_MOUNT_SPEC),
+                          {"name": "tls", "mountPath": AGENT_TLS_MOUNT, "readOnly": True}],
          # uid 0 explicitly: the image runs as 65532, and the kubelet's pod-resources socket is
          # root-owned 0660 (no capability is needed for that: owner permissions; every
          # capability stays dropped)
@@ -325,7 +354,14 @@ def node_agent_daemonset() -> dict:
                                                            "path": "/var/lib/kubelet/pod-resources"}},
                                                        {"name": "device-plugins", "hostPath": {
                                                            "path": "/var/lib/kubelet/device-plugins"}},
-                                                       _agent_token_volume()]}}}}
+                                                       _agent_token_volume(),
+                                                       # the kubelet retries the mount until the
+                                                       # provisioner (or service-ca) wrote it
+                                                       {"name": "tls", "secret": {
+                                                           "secretName": AGENT_TLS_SECRET, "defaultMode": 0o440,
+                                                           # the serving pair only, never the CA key
+                                                           "items": [{"key": "tls.crt", "path": "tls.crt"},
+                                                                     {"key": "tls.key", "path": "tls.key"}]}}]}}}}
 
 
 CONFORMANCE_NS = "odh-kubeflow-amd-conformance"
@@ -421,8 +457,10 @@ def webhook_certs_rbac(mwcs: List[str]) -> List[dict]:
         {"apiVersion": "v1", "kind": "ServiceAccount", "metadata": {"name": "webhook-certs"}},
         {"apiVersion": "rbac.authorization.k8s.io/v1", "kind": "Role", "metadata": {"name": "webhook-certs-role"},
          "rules": [{**_rule([""], ["secrets"], ["get", "update"]),
-                    "resourceNames": [WEBHOOK_CERT_SECRET, AGENT_TOKEN_SECRET]},
-                   _rule([""], ["secrets"], ["create"])]},
+                    "resourceNames": [WEBHOOK_CERT_SECRET, AGENT_TOKEN_SECRET, AGENT_TLS_SECRET]},
+                   _rule([""], ["secrets"], ["create"]),
+                   {**_rule([""], ["configmaps"], ["get", "update"]), "resourceNames": [AGENT_CA_CONFIGMAP]},
+                   _rule([""], ["configmaps"], ["create"])]},
         {"apiVersion": "rbac.authorization.k8s.io/v1", "kind": "ClusterRole",
          "metadata": {"name": "webhook-certs-cabundle-role"},
          "rules": [{**_rule(["admissionregistration.k8s.io"], ["mutatingwebhookconfigurations"], ["get", "update"]),
@@ -436,7 +474,9 @@ def webhook_certs_args(services: List[str], mwcs: List[str]) -> List[str]:
     """``cmd/webhook_certs.py`` arguments.  Names are the *rendered* (prefixed) names: they
     are plain strings to kustomize, so its name-reference fix-ups do not reach them."""
     return ([f"--secret-name={WEBHOOK_CERT_SECRET}"] + [f"--service-name={x}" for x in services]
-            + [f"--mwc-name={x}" for x in mwcs] + [f"--random-secret={AGENT_TOKEN_SECRET}"])
+            + [f"--mwc-name={x}" for x in mwcs] + [f"--random-secret={AGENT_TOKEN_SECRET}"]
+            + [f"--node-agent-secret={AGENT_TLS_SECRET}", f"--node-agent-name={AGENT_NAME}",
+               f"--node-agent-ca-configmap={AGENT_CA_CONFIGMAP}"])
 
 
 def webhook_certs_docs(services: List[str], mwcs: List[str]) -> Dict[str, object]:
@@ -490,7 +530,8 @@ def control_plane_statefulset(shards: int) -> dict:
                      "selector": {"matchLabels": labels},
                      "template": {"metadata": {"labels": labels},
                                   "spec": {"serviceAccountName": "control-plane", "containers": [kf, odh],
-                                           "volumes": [_cert_volume(), _agent_token_volume()]}}}}
+                                           "volumes": [_cert_volume(), _agent_token_volume(),
+                                                       _agent_ca_volume()]}}}}
 
 
 def _control_plane_container(name: str, args: list, metrics: int, probes: int, webhook: bool) -> dict:
@@ -511,7 +552,7 @@ def _control_plane_container(name: str, args: list, metrics: int, probes: int, w
          "resources": {"requests": {"cpu": "500m", "memory": "256Mi"}, "limits": {"cpu": "2", "memory": "2Gi"}},
          # the kf container reads the node agents' token (GPU-busy culling); the odh one serves the webhook
          "volumeMounts": ([{"name": "cert", "mountPath": "/tmp/k8s-webhook-server/serving-certs", "readOnly": True}]
-                          if webhook else [dict(AGENT_TOKEN_MOUNT_SPEC)]),
+                          if webhook else [dict(AGENT_TOKEN_MOUNT_SPEC), dict(AGENT_CA_MOUNT_SPEC)]),
          "securityContext": dict(RESTRICTED), **_probes(probes)}
     return c
 
@@ -656,10 +697,25 @@ def tree(version: Optional[str] = None) -> Dict[str, object]:
     t["overlays/kubeflow/kustomization.yaml"] = kustomization(
         ["../../default", "../../webhook-certs"], namespace="kubeflow", images=images,
         configMapGenerator=[{"name": "config", "behavior": "merge", "literals": ["USE_ISTIO=true"]}])
+    # the node agents' serving cert from OpenShift's service-ca (a Service named like the agents'
+    # certificate, annotated) and its CA injected into the culler's ConfigMap (key service-ca.crt)
+    t["overlays/openshift/node-agent-tls.yaml"] = [
+        {"apiVersion": "v1", "kind": "Service",
+         "metadata": {"name": AGENT_NAME, "namespace": "opendatahub", "annotations": {
+             "service.beta.openshift.io/serving-cert-secret-name": AGENT_TLS_SECRET}},
+         "spec": {"clusterIP": "None", "selector": {"app": AGENT_NAME},
+                  "ports": [{"name": "gpu-activity", "port": 9464, "targetPort": 9464}]}},
+        {"apiVersion": "v1", "kind": "ConfigMap",
+         "metadata": {"name": AGENT_CA_CONFIGMAP, "namespace": "opendatahub",
+                      "annotations": {"service.beta.openshift.io/inject-cabundle": "true"}}}]
     t["overlays/openshift/kustomization.yaml"] = kustomization(
-        ["../../default"], images=images,
+        ["../../default", "node-agent-tls.yaml"], images=images,
         configMapGenerator=[{"name": "config", "behavior": "merge", "literals": ["ADD_FSGROUP=false"]}],
-        patches=[{"target": {"kind": "Service", "name": ".*webhook-service"}, "patch":
+        patches=[{"target": {"kind": "Deployment", "name": f"{NAME_PREFIX}deployment"}, "patch": yaml.safe_dump(
+                      [{"op": "replace", "path": "/spec/template/spec/containers/0/env/"
+                        f"{_culler_env_index('CULLING_GPU_AGENT_CA_FILE')}/value",
+                        "value": f"{AGENT_CA_MOUNT}/service-ca.crt"}], sort_keys=False)},
+                 {"target": {"kind": "Service", "name": ".*webhook-service"}, "patch":
                   "- op: add\n  path: /metadata/annotations\n  value:\n    service.beta.openshift.io/"
                   f"serving-cert-secret-name: {WEBHOOK_CERT_SECRET}\n"},
                  {"target": {"kind": "MutatingWebhookConfiguration"}, "patch":

@@ -19,6 +19,14 @@ of a pod's node at ``<pod.status.hostIP>:9464``):
 
 With a token file (``--token-file``, :mod:`.auth`) every endpoint but ``/healthz`` needs
 ``Authorization: Bearer <token>`` and answers 401 otherwise.
+
+The agent serves HTTPS (``--tls-cert-dir``: ``tls.crt`` / ``tls.key`` from the
+``mi355x-node-agent-tls`` Secret that ``cmd/webhook_certs --node-agent-secret`` issues, reloaded
+when renewed), so neither the bearer token nor a busy/idle answer — on which a GPU notebook is
+culled or kept — crosses the node network in cleartext, and the culler verifies the answer
+comes from a holder of the agent's key (its CA, the ``mi355x-node-agent-ca`` ConfigMap, and the
+certificate's name ``mi355x-node-agent.<namespace>.svc``).  Plain HTTP only with ``--insecure``
+(tests, development).
 """
 
 from __future__ import annotations
@@ -57,8 +65,14 @@ def aggregate_windows(telemetry, indices: Sequence[Optional[int]], window_s: flo
 
 class NodeTelemetryAgent:
     def __init__(self, telemetry, attributor=None, host: str = "0.0.0.0", port: int = DEFAULT_PORT,
-                 token=None):
+                 token=None, tls_cert_dir: Optional[str] = None, cert_reload_s: float = 10.0):
         self.telemetry = telemetry
+        self.tls = None
+        if tls_cert_dir:
+            from ..utils.tlsreload import ServingCert
+
+            self.tls = ServingCert(tls_cert_dir, "node agent serving")
+        self.cert_reload_s = cert_reload_s
         self.token = token  # nodeagent.auth.TokenFile, or None: unauthenticated
         self.refused = 0
         self.attributor = attributor
@@ -170,12 +184,21 @@ class NodeTelemetryAgent:
         app.router.add_get("/metrics", metrics)
         self._runner = web.AppRunner(app, access_log=None)
         await self._runner.setup()
-        site = web.TCPSite(self._runner, self.host, self.port)
+        ctx = self.tls.context() if self.tls is not None else None
+        site = web.TCPSite(self._runner, self.host, self.port, ssl_context=ctx)
         await site.start()
         self.port = site._server.sockets[0].getsockname()[1]
+        if self.tls is not None:
+            self.tls.watch(self.cert_reload_s)
         return self
 
+    @property
+    def scheme(self) -> str:
+        return "https" if self.tls is not None else "http"
+
     async def stop(self) -> None:
+        if self.tls is not None:
+            self.tls.stop()
         if self._runner is not None:
             await self._runner.cleanup()
             self._runner = None

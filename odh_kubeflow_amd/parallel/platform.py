@@ -72,7 +72,8 @@ async def stop_child(proc: Optional[subprocess.Popen]) -> None:
 
 class NodePlatform:
     def __init__(self, apiserver_url: str, node_name: str = "mi355x-node-0", gpus: int = 8, process: bool = True,
-                 exec_init: bool = False, hip_devices: int = 0, max_concurrent: int = 8, workers: int = 1):
+                 exec_init: bool = False, hip_devices: int = 0, max_concurrent: int = 8, workers: int = 1,
+                 pull_secret_delay_ms: float = -1.0):
         self.url = apiserver_url
         self.node_name = node_name
         self.gpus = gpus
@@ -81,6 +82,9 @@ class NodePlatform:
         self.hip_devices = hip_devices
         self.max_concurrent = max_concurrent
         self.workers = max(1, int(workers))
+        # >= 0: OpenShift's ServiceAccount pull-secret controller, adding each SA's dockercfg
+        # secret this many ms after the SA appears (testing/kubelet/openshift.py)
+        self.pull_secret_delay_ms = float(pull_secret_delay_ms)
         self.procs: Dict[str, subprocess.Popen] = {}
         self.managers = []
         self.agent = None
@@ -93,8 +97,11 @@ class NodePlatform:
 
             def pre(name):
                 return ["-m", "cProfile", "-o", f"{prof}.{name}"] if prof else []
+            ctrls = "scheduler" + (",pull-secrets" if self.pull_secret_delay_ms >= 0 else "")
             self.procs["scheduler"] = await start_child(
-                "odh_kubeflow_amd.testing.cmd.scheduler", ["--master", self.url, "--controllers", "scheduler"],
+                "odh_kubeflow_amd.testing.cmd.scheduler",
+                ["--master", self.url, "--controllers", ctrls,
+                 "--pull-secret-delay-ms", f"{max(0.0, self.pull_secret_delay_ms):g}"],
                 "scheduler", python_args=pre("scheduler"))
             w = self.workers
             for i in range(w):
@@ -131,6 +138,11 @@ class NodePlatform:
             .setup_with_manager(kcm)
         SchedulerController(kcm.client, kcm.reader, kcm.get_event_recorder_for("default-scheduler")) \
             .setup_with_manager(kcm)
+        if self.pull_secret_delay_ms >= 0:
+            from ..testing.kubelet.openshift import PullSecretController
+
+            self.pull_secrets = PullSecretController(kcm.client, kcm.reader, self.pull_secret_delay_ms / 1e3)
+            self.pull_secrets.setup_with_manager(kcm)
         kl = Manager.remote(None, name=f"kubelet-{self.node_name}", default_max_concurrent=self.max_concurrent,
                             shared=shared)
         vis = (lambda d: d % self.hip_devices) if self.hip_devices else None

@@ -295,6 +295,26 @@ class ControlPlaneShard:
                 out[f"{p.name}{sfx}"] = d.get("io") or {}
         return out
 
+    async def webhook_timings(self, since: Optional[Dict[str, dict]] = None) -> Dict[str, dict]:
+        """process name → {"served": n, "handle_ms": [...], "gets": n, "get_ms": [...]} of the
+        launched processes that serve the odh webhook: handle times of the admissions, and the
+        process's live GETs, after ``since[name]`` (a previous answer's counters)."""
+        out = {}
+        for p in self.procs:
+            s0 = (since or {}).get(p.name) or {}
+            q = f"since={s0.get('served', 0)}" + (f"&get_since={s0['gets']}" if "gets" in s0 else "")
+            d = await self._get_json(f"{p.base}/debug/webhook?{q}")
+            if d.get("served") or p.name in (since or {}):
+                out[p.name] = d
+        for i, mgr in enumerate(self.managers):
+            srv = getattr(mgr, "webhook_server", None)
+            if srv is not None:
+                n = max(0, min(srv.served - ((since or {}).get(f"inprocess_{i}") or {}).get("served", 0),
+                               len(srv.handle_s)))
+                out[f"inprocess_{i}"] = {"served": srv.served,
+                                         "handle_ms": [x * 1e3 for x in list(srv.handle_s)[len(srv.handle_s) - n:]]}
+        return out
+
     async def reconcile_count(self) -> int:
         return sum(sum(t.values()) for t in (await self.reconcile_breakdown()).values())
 

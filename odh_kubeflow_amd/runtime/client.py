@@ -41,6 +41,7 @@ CURRENT_RECONCILE: contextvars.ContextVar = contextvars.ContextVar("current_reco
 # answered NotFound from the cache (see CachedClient._validated)
 # (the value: the keys already confirmed absent during this admission, read once)
 CONFIRM_ABSENCE: contextvars.ContextVar = contextvars.ContextVar("confirm_absence", default=None)
+_RETRY = object()  # a coalesced live read whose sender was cancelled: read again
 # how long a read of an object this client just wrote waits for the watch to deliver the
 # write before it reads through to the apiserver instead
 RYOW_WAIT_S = 0.05
@@ -202,6 +203,11 @@ class CachedClient(Client):
         # resourceVersion (see :meth:`_validated`)
         self._full: Dict[Tuple[str, str, str], Tuple[int, dict]] = {}
         self.validated_reads = 0
+        # live reads of the same object coalesced (see _live_get): key → (start, future) of the
+        # read in flight, and the future of the read that follows it
+        self._flight: Dict[Tuple[str, str, str], Tuple[float, asyncio.Future]] = {}
+        self._next_flight: Dict[Tuple[str, str, str], asyncio.Future] = {}
+        self.coalesced_reads = 0
 
     def _note(self, out, claim: bool = True) -> None:
         """Remember a write's result.  ``claim=False``: the write may have been a no-op — a
@@ -333,6 +339,70 @@ class CachedClient(Client):
             out["apiVersion"] = info.api_version(v)
         return out
 
+    async def _live_get(self, key, kind, name, namespace):
+        """A live GET whose answer is as fresh as a GET issued now would be, coalesced with
+        the concurrent live reads of the same object.
+
+        A read may share another's answer only if that GET was sent after this read began (so
+        it reflects every write that completed before this read began — what a live read is
+        for, e.g. an admission seeing a ConfigMap created a moment before).  A read arriving
+        while a GET of the key is in flight therefore waits for the NEXT GET, which is sent
+        when the current one answers and serves every read that arrived meanwhile: at most one
+        GET per object in flight and one queued, however many admissions of one namespace
+        arrive at once (a burst of 64 notebooks read the same two ConfigMaps 128 times).  A
+        single read waits for nothing."""
+        loop = asyncio.get_running_loop()
+        cur = self._flight.get(key)
+        if cur is None:
+            return deepcopy_json(await self._fly(key, kind, name, namespace))
+        nxt = self._next_flight.get(key)
+        if nxt is None:
+            nxt = self._next_flight[key] = loop.create_future()
+        else:
+            self.coalesced_reads += 1
+        try:
+            await asyncio.shield(cur[1])
+        except BaseException:  # noqa: BLE001 — the current read's outcome is not ours
+            pass
+        if self._next_flight.get(key) is nxt:
+            # the first waiter sends the next GET for everyone queued behind the last one
+            del self._next_flight[key]
+            try:
+                o = await self._fly(key, kind, name, namespace)
+            except asyncio.CancelledError:
+                if not nxt.done():
+                    nxt.set_result(_RETRY)  # this reader was cancelled, not the others: they read again
+                raise
+            except BaseException as e:
+                if not nxt.done():
+                    nxt.set_exception(e)
+                    nxt.exception()  # retrieved: a waiter-less failure is not "never retrieved"
+                raise
+            if not nxt.done():
+                nxt.set_result(o)
+            return deepcopy_json(o)
+        o = await asyncio.shield(nxt)
+        if o is _RETRY:
+            return await self._live_get(key, kind, name, namespace)
+        return deepcopy_json(o)
+
+    async def _fly(self, key, kind, name, namespace):
+        loop = asyncio.get_running_loop()
+        fut = loop.create_future()
+        self._flight[key] = (loop.time(), fut)
+        try:
+            o = await self.writer.get(kind, name, namespace)
+        except BaseException as e:
+            if not fut.done():
+                fut.set_exception(e)
+                fut.exception()
+            raise
+        finally:
+            if self._flight.get(key, (None, None))[1] is fut:
+                del self._flight[key]
+        fut.set_result(o)
+        return o
+
     async def prefetch(self, keys: Sequence[Tuple[Any, str, Optional[str]]]) -> None:
         """Inside an admission (``CONFIRM_ABSENCE`` set): make the live reads of ``keys`` —
         (kind, name, namespace) that the admission is about to read — concurrently, so that
@@ -364,7 +434,7 @@ class CachedClient(Client):
                     info = SCHEME.resolve(kind)
                     raise NotFound(info.plural if not info.group else f"{info.plural}.{info.group}", name)
             try:
-                o = await self.writer.get(kind, name, namespace)
+                o = await self._live_get(key, kind, name, namespace)
             except ApiError as e:
                 if absent is not None and is_not_found(e):
                     absent.add(key)

@@ -354,5 +354,21 @@ class Manager:
                                                                   *(d.get("reconciles") for d in docs)]),
                                       "io": merge_counts([self.io_counters(), *(d.get("io") for d in docs)])})
 
+        async def webhook(req):
+            srv = getattr(self, "webhook_server", None)
+            if srv is None:
+                return web.json_response({"served": 0, "handle_ms": []})
+            since = int(req.query.get("since", "0"))
+            n = max(0, min(srv.served - since, len(srv.handle_s)))
+            recent = list(srv.handle_s)[len(srv.handle_s) - n:] if n else []
+            rest = getattr(self, "rest", None)
+            gets = getattr(rest, "by_verb", {}).get("GET", 0)
+            gsince = int(req.query.get("get_since", str(gets)))
+            g = list(getattr(rest, "get_ms", ()))
+            k = max(0, min(gets - gsince, len(g)))
+            return web.json_response({"served": srv.served, "handle_ms": [round(x * 1e3, 3) for x in recent],
+                                      "gets": gets, "get_ms": [round(x, 3) for x in g[len(g) - k:]] if k else []})
+
+        app.router.add_get("/debug/webhook", webhook)
         app.router.add_get("/debug/reconciles", reconciles)
         app.router.add_get("/debug/quiesce", quiesce)

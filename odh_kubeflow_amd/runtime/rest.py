@@ -165,6 +165,9 @@ class RestClient(Client):
         self._bucket = TokenBucket(config.qps, config.burst)
         self.requests = 0
         self.by_verb: Dict[str, int] = {}  # requests per HTTP method (watches counted as WATCH)
+        from collections import deque
+
+        self.get_ms = deque(maxlen=8192)  # wall time of the recent GETs (ms): the live-read latency
         self.retries = 0  # GETs retried after a connection reset / EOF
         self.user = config.user_agent
         self._discovery: dict = {}  # "group/version" -> (fetched_at, set(plurals))
@@ -201,6 +204,7 @@ class RestClient(Client):
         target = url[len(self.base):] if url.startswith(self.base) else url
         if params:
             target += ("&" if "?" in target else "?") + urlencode(params)
+        t0 = time.perf_counter()
         for attempt in range(self.GET_RETRIES + 1):
             try:
                 status, raw = await self._http().request(method, target, data,
@@ -216,6 +220,8 @@ class RestClient(Client):
                     raise InternalError(str(e))
                 self.retries += 1
                 await asyncio.sleep(min(0.5, 0.01 * (2 ** attempt)))
+        if method == "GET":
+            self.get_ms.append((time.perf_counter() - t0) * 1e3)
         try:
             out = json.loads(raw) if raw else {}
         except ValueError:

@@ -64,6 +64,7 @@ class ClusterConfig:
 
 
 OPENSHIFT_CRDS = (kinds.IMAGE_STREAM, kinds.PROXY, kinds.ROUTE, kinds.OAUTH_CLIENT)
+AGENT_SERVER_NAME = "mi355x-node-agent.opendatahub.svc"  # the node agents' certificate name
 
 
 def write_kubeconfig(path: str, server: str, user: str = "MasterOfTheSystems") -> None:
@@ -199,9 +200,10 @@ class LocalCluster:
                 from ..nodeagent.attribution import Attributor
                 from ..nodeagent.server import NodeTelemetryAgent
 
+                # the production agent over HTTPS, as the DaemonSet serves it
                 self.node_agents[node_name] = await NodeTelemetryAgent(
                     cfg.telemetry, Attributor(cfg.telemetry, checkpoint_path=cp_path, ttl_s=0.0),
-                    host="127.0.0.1", port=0).start()
+                    host="127.0.0.1", port=0, tls_cert_dir=self._agent_certs().cert_dir).start()
             if cfg.gpu_runtimes_in_process:
                 kl = self._mgr(f"kubelet-{node_name}", remote=cfg.remote_kubelets)
                 self.kubelets.append(kl)
@@ -224,6 +226,17 @@ class LocalCluster:
             await mgr.start()
         return self
 
+    def _agent_certs(self):
+        """One serving certificate for every node agent (as ``cmd/webhook_certs
+        --node-agent-secret`` issues it) and its CA for the culler."""
+        if getattr(self, "_agent_cert", None) is None:
+            from ..webhook.certs import generate
+
+            tmp = tempfile.TemporaryDirectory(prefix="odh-agent-certs-")
+            self._tmpdirs.append(tmp)
+            self._agent_cert = generate((AGENT_SERVER_NAME,), tmp.name)
+        return self._agent_cert
+
     def _build_kf(self) -> None:
         from ..controllers.setup import setup_kf
 
@@ -235,9 +248,10 @@ class LocalCluster:
 
             # every fake node's pods report hostIP 127.0.0.1: route by node name instead
             ports = {n: a.port for n, a in self.node_agents.items()}
+            certs = self._agent_certs()
             activity = NodeAgentActivity(endpoint_for=lambda pod: "127.0.0.1:%d" % ports[
                 (pod.get("spec") or {}).get("nodeName")] if (pod.get("spec") or {}).get("nodeName") in ports
-                else None)
+                else None, ca_file=os.path.join(certs.cert_dir, "ca.crt"), server_name=AGENT_SERVER_NAME)
         out = setup_kf(kf, self.env, culling=culling, activity=activity, event_reemit=self.cfg.event_reemit,
                        reference_emulation=self.cfg.reference_emulation)
         self.kf_metrics = out["metrics"]

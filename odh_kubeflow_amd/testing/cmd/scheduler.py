@@ -36,8 +36,11 @@ def parse(argv=None):
                    help="scheduler workers: decisions are serialised by the allocator lock, the binds "
                         "(apiserver round trips) run concurrently")
     p.add_argument("--controllers", default="scheduler",
-                   help="comma list of scheduler (kube-scheduler + device allocation) and statefulset "
-                        "(kube-controller-manager's StatefulSet controller)")
+                   help="comma list of scheduler (kube-scheduler + device allocation), statefulset "
+                        "(kube-controller-manager's StatefulSet controller) and pull-secrets (OpenShift's "
+                        "ServiceAccount dockercfg controller, testing/kubelet/openshift.py)")
+    p.add_argument("--pull-secret-delay-ms", type=float, default=200.0,
+                   help="pull-secrets: how long after a ServiceAccount appears its pull secret is added")
     p.add_argument("--partition", default="0/1",
                    help="i/W: this is StatefulSet worker i of W (each owns the namespaces it claimed)")
     p.add_argument("--debug-log", action="store_true")
@@ -82,6 +85,11 @@ async def amain(argv=None) -> int:
 
             NamespaceClaimer(mgr.client, mgr.reader, part, nparts).setup_with_manager(mgr)
             synced += [kinds.NAMESPACE]
+    if "pull-secrets" in ctrls:
+        from ..kubelet.openshift import PullSecretController
+
+        PullSecretController(mgr.client, mgr.reader, args.pull_secret_delay_ms / 1e3).setup_with_manager(mgr)
+        synced += [kinds.SERVICE_ACCOUNT]
     await mgr.start()
     await mgr.cache.wait_synced(synced)
     print("ready", flush=True)

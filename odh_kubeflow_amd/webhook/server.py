@@ -21,6 +21,7 @@ import json
 import logging
 import os
 import ssl
+import time
 from typing import Optional, Tuple
 
 from ..runtime.http1 import Http1Server
@@ -44,6 +45,9 @@ class WebhookServer:
         self._watch: Optional[asyncio.Task] = None
         self.served = 0
         self.reloads = 0
+        from collections import deque
+
+        self.handle_s = deque(maxlen=4096)  # per admission: request decoded → response encoded (s)
 
     def _files(self) -> Tuple[str, str]:
         return os.path.join(self.cert_dir, "tls.crt"), os.path.join(self.cert_dir, "tls.key")
@@ -102,6 +106,7 @@ class WebhookServer:
         if method != "POST":
             return 405, "text/plain", b"method not allowed"
         self.served += 1
+        t0 = time.perf_counter()
         try:
             review = json.loads(data)
         except ValueError as e:
@@ -109,7 +114,9 @@ class WebhookServer:
                    "response": {"uid": "", "allowed": False, "status": {"code": 400, "message": str(e)}}}
         else:
             out = await self.webhook.handle(review)
-        return 200, "application/json", json.dumps(out, separators=(",", ":")).encode()
+        body = json.dumps(out, separators=(",", ":")).encode()
+        self.handle_s.append(time.perf_counter() - t0)
+        return 200, "application/json", body
 
     async def start(self) -> "WebhookServer":
         self._ctx = self.ssl_context()

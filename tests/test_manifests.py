@@ -337,13 +337,16 @@ def test_webhook_certs_rbac_is_scoped_to_its_objects(overlay):
     assert rule["resources"] == ["mutatingwebhookconfigurations"] and sorted(rule["verbs"]) == ["get", "update"]
     assert sorted(rule["resourceNames"]) == mwc_names
     (role,) = [o for n, o in _by(objs, "Role").items() if n.endswith("webhook-certs-role")]
-    named = [r for r in role["rules"] if r.get("resourceNames")]
-    assert len(named) == 1 and sorted(named[0]["verbs"]) == ["get", "update"]
-    assert sorted(named[0]["resourceNames"]) == sorted([manifests.WEBHOOK_CERT_SECRET, manifests.AGENT_TOKEN_SECRET])
+    named = {r["resources"][0]: r for r in role["rules"] if r.get("resourceNames")}
+    assert sorted(named) == ["configmaps", "secrets"]
+    assert all(sorted(r["verbs"]) == ["get", "update"] for r in named.values())
+    assert sorted(named["secrets"]["resourceNames"]) == sorted(
+        [manifests.WEBHOOK_CERT_SECRET, manifests.AGENT_TOKEN_SECRET, manifests.AGENT_TLS_SECRET])
+    assert named["configmaps"]["resourceNames"] == [manifests.AGENT_CA_CONFIGMAP]  # the node agents' CA
     unnamed = [r for r in role["rules"] if not r.get("resourceNames")]
-    assert [sorted(r["verbs"]) for r in unnamed] == [["create"]]
-    # the serving pods get the serving pair only, never the CA key
+    assert [sorted(r["verbs"]) for r in unnamed] == [["create"], ["create"]]
+    # the serving pods (webhook, node agents) get the serving pair only, never the CA key
     for o, ps in _pod_specs(objs):
         for v in ps.get("volumes") or []:
-            if (v.get("secret") or {}).get("secretName") == manifests.WEBHOOK_CERT_SECRET:
+            if (v.get("secret") or {}).get("secretName") in (manifests.WEBHOOK_CERT_SECRET, manifests.AGENT_TLS_SECRET):
                 assert sorted(i["key"] for i in v["secret"]["items"]) == ["tls.crt", "tls.key"], o["metadata"]

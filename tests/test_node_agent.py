@@ -239,12 +239,20 @@ def test_culler_kfd_attribution_only(run, sysfs):
     offset = [0.0]
     timeutil.set_clock(lambda: time.time() + offset[0])
 
+    import tempfile
+
+    from odh_kubeflow_amd.webhook.certs import generate
+
+    certs = generate((AGENT_NAME,), tempfile.mkdtemp(prefix="odh-agent-tls-"))
+
     async def go():
         agent = await NodeTelemetryAgent(tel, Attributor(tel, proc_root=proc, ttl_s=0.0), host="127.0.0.1",
-                                         port=0).start()
-        # production defaults: <pod.status.hostIP>:<CULLING_GPU_AGENT_PORT>
+                                         port=0, tls_cert_dir=certs.cert_dir).start()
+        # production defaults: https://<pod.status.hostIP>:<CULLING_GPU_AGENT_PORT>, verified against
+        # the agents' CA and name (mi355x-node-agent.<K8S_NAMESPACE>.svc)
         env = {"ENABLE_CULLING": "true", "CULL_IDLE_TIME": "60", "IDLENESS_CHECK_PERIOD_SECONDS": "0.2",
                "CULLING_ACTIVITY_SOURCE": "amdgpu", "CULLING_GPU_AGENT_PORT": str(agent.port),
+               "CULLING_GPU_AGENT_CA_FILE": os.path.join(certs.cert_dir, "ca.crt"),
                "CLUSTER_DOMAIN": "invalid.example"}
         try:
             async with LocalCluster(ClusterConfig(culler=True, env=env)) as cl:
@@ -291,8 +299,10 @@ def test_shipped_agent_never_touches_the_apiserver(run, sysfs, tmp_path):
     from odh_kubeflow_amd.cmd import node_agent
 
     root, proc, minors, _tel = sysfs
-    args = node_agent.parse([])
+    args = node_agent.parse(["--insecure"])
     assert not hasattr(args, "master") and not hasattr(args, "kubeconfig")
+    with pytest.raises(SystemExit):
+        node_agent.parse([])  # plain HTTP only when asked for
     cp = CheckpointWriter(str(tmp_path / "dp" / "cp"))
     cp.allocate(UID_A, "nb", [fake_bdf(1)])
     set_fake_counter(root, minors[1], busy=33)
@@ -312,7 +322,7 @@ def test_shipped_agent_never_touches_the_apiserver(run, sysfs, tmp_path):
         port = _free_port()
         env = {**os.environ, "KUBERNETES_SERVICE_HOST": "127.0.0.1", "KUBERNETES_SERVICE_PORT": str(aport),
                "KUBECONFIG": str(kc)}
-        p = subprocess.Popen([sys.executable, "-m", "odh_kubeflow_amd.cmd.node_agent", "--bind", "127.0.0.1",
+        p = subprocess.Popen([sys.executable, "-m", "odh_kubeflow_amd.cmd.node_agent", "--insecure", "--bind", "127.0.0.1",
                               "--port", str(port), "--sysfs-root", root, "--proc-root", proc,
                               "--pod-resources-socket", str(tmp_path / "absent.sock"),
                               "--device-plugin-checkpoint", cp.path, "--telemetry-interval-ms", "10"],
@@ -357,6 +367,8 @@ def test_shipped_manifests_have_no_kubelet_stand_in():
     assert sc["runAsUser"] == 0 and sc["capabilities"] == {"drop": ["ALL"]} and not sc["allowPrivilegeEscalation"]
     assert sc["readOnlyRootFilesystem"] and not sc.get("privileged")
     assert any(a.startswith("--token-file=") for a in c["args"])
+    assert any(a.startswith("--tls-cert-dir=") for a in c["args"]) and "--insecure" not in c["args"]
+    assert c["livenessProbe"]["httpGet"]["scheme"] == "HTTPS"
     # no RBAC at all for the agent: it cannot write a Node or pods/status
     for path, doc in t.items():
         for d in doc if isinstance(doc, list) else [doc]:
@@ -433,11 +445,18 @@ def test_agent_token_required_and_rotated(run, sysfs, tmp_path):
     run(go())
 
 
+AGENT_NAME = "mi355x-node-agent.opendatahub.svc"
+
+
 def test_culler_sends_agent_token(run, sysfs, tmp_path):
     """The culler's node-agent client reads CULLING_GPU_AGENT_TOKEN_FILE: with the right token it
-    gets GPU data; with none it gets no data (None: never idleness)."""
+    gets GPU data; with none it gets no data (None: never idleness).  Over HTTPS, as deployed."""
     from odh_kubeflow_amd.controllers import culling as c
     from odh_kubeflow_amd.nodeagent.auth import TokenFile
+    from odh_kubeflow_amd.webhook.certs import generate
+
+    certs = generate((AGENT_NAME,), str(tmp_path / "tls"))
+    ca = os.path.join(certs.cert_dir, "ca.crt")
 
     root, proc, minors, tel = sysfs
     cp = CheckpointWriter(str(tmp_path / "dp" / "cp"))
@@ -449,9 +468,9 @@ def test_culler_sends_agent_token(run, sysfs, tmp_path):
 
     async def go():
         agent = await NodeTelemetryAgent(tel, Attributor(tel, checkpoint_path=cp.path, ttl_s=0.0), host="127.0.0.1",
-                                         port=0, token=TokenFile(str(tok))).start()
-        good = c.NodeAgentActivity(port=agent.port, token_file=str(tok))
-        none = c.NodeAgentActivity(port=agent.port)
+                                         port=0, token=TokenFile(str(tok)), tls_cert_dir=certs.cert_dir).start()
+        good = c.NodeAgentActivity(port=agent.port, token_file=str(tok), ca_file=ca, server_name=AGENT_NAME)
+        none = c.NodeAgentActivity(port=agent.port, ca_file=ca, server_name=AGENT_NAME)
         try:
             await asyncio.sleep(0.1)
             got = await good.busy(pod, 0.05)
@@ -462,5 +481,65 @@ def test_culler_sends_agent_token(run, sysfs, tmp_path):
         finally:
             await good.close()
             await none.close()
+            await agent.stop()
+    run(go())
+
+
+def test_agent_serves_https_only_and_the_culler_verifies_it(run, sysfs, tmp_path):
+    """the agent's answers decide culls, and its token must not cross the node
+    network in cleartext.  The agent serves HTTPS; the culler asks only over HTTPS, verifying the
+    agent's certificate against the agents' CA and name — a cleartext client, a wrong name or
+    another CA's certificate get nothing (no GPU data: never idleness, never a cull); a renewed
+    certificate is picked up without a restart."""
+    import ssl as _ssl
+
+    from odh_kubeflow_amd.controllers import culling as c
+    from odh_kubeflow_amd.webhook.certs import generate, issue_leaf
+
+    root, proc, minors, tel = sysfs
+    cp = CheckpointWriter(str(tmp_path / "dp" / "cp"))
+    cp.allocate(UID_A, "nb", [fake_bdf(3)])
+    set_fake_counter(root, minors[3], busy=55)
+    certs = generate((AGENT_NAME,), str(tmp_path / "tls"))
+    ca = os.path.join(certs.cert_dir, "ca.crt")
+    other = generate((AGENT_NAME,), str(tmp_path / "other"))
+    pod = {"metadata": {"name": "nb-0", "namespace": "u", "uid": UID_A}, "status": {"hostIP": "127.0.0.1"}}
+
+    async def go():
+        agent = await NodeTelemetryAgent(tel, Attributor(tel, checkpoint_path=cp.path, ttl_s=0.0), host="127.0.0.1",
+                                         port=0, tls_cert_dir=certs.cert_dir, cert_reload_s=0.05).start()
+        ok = c.NodeAgentActivity(port=agent.port, ca_file=ca, server_name=AGENT_NAME)
+        cleartext = c.NodeAgentActivity(port=agent.port)  # no CA, not --insecure: refuses to ask
+        insecure = c.NodeAgentActivity(port=agent.port, insecure=True)  # plain HTTP to an HTTPS agent
+        wrong_name = c.NodeAgentActivity(port=agent.port, ca_file=ca, server_name="evil.example")
+        wrong_ca = c.NodeAgentActivity(port=agent.port, ca_file=os.path.join(other.cert_dir, "ca.crt"),
+                                       server_name=AGENT_NAME)
+        try:
+            await asyncio.sleep(0.1)
+            got = await ok.busy(pod, 0.05)
+            assert got is not None and got["busy_mean"] == 55
+            assert await cleartext.busy(pod, 0.05) is None and cleartext.refused_cleartext == 1
+            assert await insecure.busy(pod, 0.05) is None
+            assert await wrong_name.busy(pod, 0.05) is None
+            assert await wrong_ca.busy(pod, 0.05) is None
+            # renewal: a new leaf from the same CA replaces the files; the agent reloads it
+            before = agent.tls.reloads
+            issue_leaf(certs.cert_dir, (AGENT_NAME,), 30)
+            for _ in range(100):
+                if agent.tls.reloads > before:
+                    break
+                await asyncio.sleep(0.05)
+            assert agent.tls.reloads > before
+            pem = await asyncio.to_thread(_ssl.get_server_certificate, ("127.0.0.1", agent.port))
+            with open(os.path.join(certs.cert_dir, "tls.crt")) as f:
+                assert pem.split() == f.read().split()  # the renewed leaf is served
+            got = await ok.busy(pod, 0.05)
+            assert got is not None and got["busy_mean"] == 55
+            cfg = c.CullerConfig.from_env({"CULLING_GPU_AGENT_CA_FILE": ca, "K8S_NAMESPACE": "team"})
+            assert cfg.gpu_agent_ca_file == ca and cfg.gpu_agent_server_name == "mi355x-node-agent.team.svc"
+            assert not cfg.gpu_agent_insecure
+        finally:
+            for x in (ok, cleartext, insecure, wrong_name, wrong_ca):
+                await x.close()
             await agent.stop()
     run(go())

@@ -10,7 +10,8 @@ holds ≥ 1 GiB of VRAM on the GPU — in a pod.  It checks, on hardware:
 * attribution: the pod (via the pod-resources API, by namespace/name) and the pod UID (via
   KFD + cgroup) both resolve to that GPU's PCI address, with the pod's own VRAM;
 * ``/gpu/activity``: busy_mean ≥ 90 while the MFMA load generator runs, ≤ 5 after it stopped;
-* auth: 401 without the token, 200 with it; source health on ``/metrics``.
+* HTTPS with the agents' CA (a cleartext request gets nothing); auth: 401 without the token, 200
+  with it; source health on ``/metrics``.
 
 Reference signal replaced: Jupyter ``/api/kernels`` + ``/api/terminals`` last-activity
 (``kf/controllers/culling_controller.go:161-196,220-241``).
@@ -43,10 +44,13 @@ def _port():
         return s.getsockname()[1]
 
 
+_CTX = [None]  # the agent's CA (HTTPS, as the DaemonSet serves)
+
+
 def _get(url, token=None, timeout=10):
     req = urllib.request.Request(url, headers={"Authorization": f"Bearer {token}"} if token else {})
     try:
-        with urllib.request.urlopen(req, timeout=timeout) as r:
+        with urllib.request.urlopen(req, timeout=timeout, context=_CTX[0]) as r:
             return r.status, r.read().decode()
     except urllib.error.HTTPError as e:
         return e.code, e.read().decode()
@@ -128,13 +132,18 @@ def test_node_agent_process_on_the_mi355x(gpu_state, tmp_path):
     srv.assign("team", "nb-0", "nb", "amd.com/gpu", [bdf])
     port = _port()
     env = dict(os.environ, PYTHONPATH=ROOT)
+    from odh_kubeflow_amd.utils.tlsreload import client_context
+    from odh_kubeflow_amd.webhook.certs import generate
+
+    certs = generate(("127.0.0.1", "mi355x-node-agent.opendatahub.svc"), str(tmp_path / "tls"))
+    _CTX[0] = client_context(os.path.join(certs.cert_dir, "ca.crt"))
     agent = subprocess.Popen([sys.executable, "-m", "odh_kubeflow_amd.cmd.node_agent", "--bind", "127.0.0.1",
                               "--port", str(port), "--sysfs-root", "/sys", "--proc-root", str(tmp_path / "proc"),
                               "--pod-resources-socket", sock, "--device-plugin-checkpoint", "",
                               "--telemetry-interval-ms", "50", "--attribution-ttl-s", "0.2",
-                              "--token-file", str(tok)], cwd=ROOT, env=env, stdout=subprocess.DEVNULL,
-                             stderr=subprocess.PIPE, text=True)
-    base = f"http://127.0.0.1:{port}"
+                              "--token-file", str(tok), "--tls-cert-dir", certs.cert_dir], cwd=ROOT, env=env,
+                             stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, text=True)
+    base = f"https://127.0.0.1:{port}"
     load = None
     try:
         deadline = time.monotonic() + 60
@@ -146,6 +155,9 @@ def test_node_agent_process_on_the_mi355x(gpu_state, tmp_path):
                 time.sleep(0.1)
         else:
             pytest.fail(f"node agent did not come up: {agent.stderr.read() if agent.poll() is not None else ''}")
+        # HTTPS only: a cleartext request gets no answer
+        with pytest.raises(Exception):
+            urllib.request.urlopen(f"http://127.0.0.1:{port}/healthz", timeout=5).read()
         # auth: data endpoints need the token, /healthz does not
         assert _get(base + "/gpu/pods")[0] == 401
         assert _get(base + "/gpu/activity?devices=0")[0] == 401

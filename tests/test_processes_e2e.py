@@ -101,7 +101,8 @@ def test_processes_end_to_end(tmp_path, run):
             agent_port = free_port()
             procs.append(spawn(["odh_kubeflow_amd.testing.cmd.fake_kubelet", "--master", master, "--devices",
                                 "0,1,2,3,4,5,6,7", "--sysfs-root", sysfs, "--checkpoint-path", cp], common, logf))
-            procs.append(spawn(["odh_kubeflow_amd.cmd.node_agent", "--bind", "127.0.0.1", "--port", str(agent_port),
+            procs.append(spawn(["odh_kubeflow_amd.cmd.node_agent", "--insecure", "--bind", "127.0.0.1",
+                                "--port", str(agent_port),
                                 "--sysfs-root", sysfs, "--proc-root", "", "--pod-resources-socket", "",
                                 "--device-plugin-checkpoint", cp], None, logf))
             await wait_http(f"https://127.0.0.1:{wh_port}/healthz")

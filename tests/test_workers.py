@@ -202,3 +202,54 @@ def test_managers_with_workers_serve_partitioned_namespaces(run):
                 await platform.stop()
             await native.stop()
     run(go(), timeout=240)
+
+
+def test_concurrent_live_reads_of_one_object_are_coalesced_but_fresh(run):
+    """``CachedClient._live_get``: reads of one ConfigMap that arrive while a GET of it is in
+    flight share the NEXT GET (sent when the current one answers), never one sent before
+    they began — so a burst of admissions makes at most one GET in flight + one queued per
+    object, and each still sees every write that completed before it started."""
+    from odh_kubeflow_amd.models.errors import NotFound
+    from odh_kubeflow_amd.runtime.client import CachedClient
+
+    class Writer:
+        def __init__(self):
+            self.gets = 0
+            self.version = 0
+            self.gate = None
+
+        async def get(self, kind, name, namespace=None):
+            self.gets += 1
+            seen = self.version  # the state as of the GET's start
+            await self.gate.wait()
+            if seen == 0:
+                raise NotFound("configmaps", name)
+            return {"metadata": {"name": name, "namespace": namespace, "resourceVersion": str(seen)},
+                    "data": {"v": str(seen)}}
+
+    class Reader:
+        def watching(self, kind, ns):
+            return False
+
+    async def go():
+        w = Writer()
+        w.gate = asyncio.Event()
+        c = CachedClient(Reader(), w, uncached=(kinds.CONFIG_MAP,))
+
+        async def read():
+            try:
+                return (await c.get(kinds.CONFIG_MAP, "cm", "ns"))["data"]["v"]
+            except NotFound:
+                return None
+
+        first = asyncio.ensure_future(read())
+        await asyncio.sleep(0)  # its GET is in flight (sees version 0)
+        w.version = 1  # a write completes: every read that begins from now on must see it
+        later = [asyncio.ensure_future(read()) for _ in range(20)]
+        await asyncio.sleep(0)
+        assert w.gets == 1
+        w.gate.set()
+        assert await first is None  # began before the write: may miss it
+        assert await asyncio.gather(*later) == ["1"] * 20  # all fresh, from ONE more GET
+        assert w.gets == 2 and c.coalesced_reads == 19
+    run(go())

@@ -12,6 +12,10 @@
 #   s20v300  interleaved A/B on one box: the driver's 20-step invocation vs the 300-step run, 3 rounds
 #   pyc      precompile the package's bytecode (compileall) before the steps that follow
 #   unsharded  the default topology (one kf + one odh manager process) at 1, 2 and 4 ranks
+#   workers  the same topology with --workers 4 (overlay mi355x): 1, 2 and 4 ranks
+#   burst64  64 notebooks at once into one unsharded control plane (--workers 1 and 4) and the sharded one
+#   fair     ours vs --reference-emulation: vanilla / OpenShift-like (pull secret after 200 ms), 0 / 2 ms writes
+#   pw4      4 ranks, --workers 4, one platform worker process per rank
 #   archab   interleaved A/B at N=1: shard as kf/odh process pair vs one process vs unsharded
 #   probeexe the odh-gpu-probe init-container program: 10 process runs (wall time, verdict)
 #   hipinit  where a fresh process's HIP start-up goes, under ROCm runtime settings (tools/research/hip_init_ab.sh)
@@ -45,8 +49,16 @@ show() {
 import json, sys
 d = json.loads([l for l in open(sys.argv[1]) if l.startswith('{')][-1])
 keys = ("n_gpus", "value", "ms_per_step", "rank_ms_per_step", "notebooks_ready_per_s", "p50_ready_ms",
-        "p95_ready_ms", "reconciles_per_notebook", "writes_per_notebook", "gpu_probe_init_container")
+        "p95_ready_ms", "reconciles_per_notebook", "writes_per_notebook", "cpu_ms_per_step", "gpu_probe_init_container")
 print(sys.argv[2], {k: d.get(k) for k in keys})
+b = d.get("burst")
+if b:
+    print(sys.argv[2], "burst", {k: b.get(k) for k in ("notebooks", "all_ready_s", "notebooks_per_s", "ready_ms",
+                                                      "admission_ms", "webhook_handle_ms", "webhook_get_ms",
+                                                      "cpu_ms_per_notebook", "rounds")})
+c = d.get("configs")
+if c:
+    print(sys.argv[2], "configs", json.dumps(c)[:3000])
 PY
 }
 fail() { echo "step $1 failed (rc=$2)"; tail -40 "$3"; exit 1; }
@@ -98,6 +110,50 @@ for s in $steps; do
           --master-addr 127.0.0.1 --master-port 2994$n bench.py --gpus $n --arch unsharded --steps 100 --warmup 5 \
           --probe-sample 0 > "$out/bench_unsharded_n$n.log" 2>&1 || fail unsharded $? "$out/bench_unsharded_n$n.log"
         show "$out/bench_unsharded_n$n.log" "unsharded n$n"
+      done ;;
+    workers)
+      timeout -k 10 170 python bench.py --gpus 1 --arch unsharded --workers 4 --steps 100 --warmup 5 --probe-sample 0 \
+        > "$out/bench_workers_n1.log" 2>&1 || fail workers $? "$out/bench_workers_n1.log"
+      show "$out/bench_workers_n1.log" "workers4 n1"
+      for n in 2 4; do
+        timeout -k 10 170 python -m torch.distributed.run --nnodes=1 --nproc-per-node $n \
+          --master-addr 127.0.0.1 --master-port 2995$n bench.py --gpus $n --arch unsharded --workers 4 --steps 100 \
+          --warmup 5 --probe-sample 0 > "$out/bench_workers_n$n.log" 2>&1 || fail workers $? "$out/bench_workers_n$n.log"
+        show "$out/bench_workers_n$n.log" "workers4 n$n"
+      done ;;
+    fair)
+      # the reference's behaviour vs ours in two regimes — vanilla Kubernetes (nothing ever adds
+      # the pull secret the reference's lock waits for: 1 s + 5 s) and OpenShift-like (every SA
+      # gets its pull secret 200 ms after it appears) — with and without 2 ms of storage latency
+      # per write; one notebook at a time and 8 at once
+      for wl in 0 2; do
+        for cl in vanilla openshift; do
+          case $cl in openshift) cf="--openshift-pull-secret-ms 200" ;; *) cf="" ;; esac
+          timeout -k 10 170 python bench.py --gpus 1 --steps 20 --warmup 3 --probe-sample 0 --no-configs \
+            --no-inprocess-baseline --burst 8 --write-latency-ms $wl $cf > "$out/fair_ours_${cl}_wl$wl.log" 2>&1 \
+            || fail fair $? "$out/fair_ours_${cl}_wl$wl.log"
+          show "$out/fair_ours_${cl}_wl$wl.log" "ours $cl wl$wl"
+          timeout -k 10 170 python bench.py --gpus 1 --reference-emulation --steps 2 --warmup 1 --probe-sample 0 \
+            --no-configs --no-inprocess-baseline --burst 8 --burst-rounds 1 --write-latency-ms $wl $cf \
+            > "$out/fair_ref_${cl}_wl$wl.log" 2>&1 || fail fair $? "$out/fair_ref_${cl}_wl$wl.log"
+          show "$out/fair_ref_${cl}_wl$wl.log" "reference $cl wl$wl"
+        done
+      done ;;
+    pw4)
+      # 4 ranks, unsharded --workers 4, the node platform with one StatefulSet-controller and
+      # kubelet process per rank (default: one per two ranks)
+      timeout -k 10 170 python -m torch.distributed.run --nnodes=1 --nproc-per-node 4 \
+        --master-addr 127.0.0.1 --master-port 29964 bench.py --gpus 4 --arch unsharded --workers 4 --steps 100 \
+        --warmup 5 --probe-sample 0 --platform-workers 4 > "$out/bench_workers_pw4_n4.log" 2>&1 \
+        || fail pw4 $? "$out/bench_workers_pw4_n4.log"
+      show "$out/bench_workers_pw4_n4.log" "workers4 pw4 n4" ;;
+    burst64)
+      for v in "unsharded 1" "unsharded 4" "sharded 1"; do
+        set -- $v
+        timeout -k 10 170 python bench.py --gpus 1 --arch $1 --workers $2 --steps 20 --warmup 5 --probe-sample 0 \
+          --burst 64 --no-inprocess-baseline > "$out/bench_burst64_$1_w$2.log" 2>&1 \
+          || fail burst64 $? "$out/bench_burst64_$1_w$2.log"
+        show "$out/bench_burst64_$1_w$2.log" "burst64 $1 w$2"
       done ;;
     archab)
       # interleaved A/B at N=1: the shard pod's kf / odh+webhook process pair (deployed), one

@@ -26,6 +26,7 @@ from typing import List, Optional
 from ...models import kinds
 from ...models import meta as m
 from ...models.errors import ApiError, is_already_exists, is_not_found
+from ...runtime.client import get_live
 from .constants import (CA_ENV_VARS, CA_KEY, CA_MOUNT_PATH, CA_VOLUME_NAME, MANAGED_BY_KEY, MANAGED_BY_VALUE,
                         ODH_CONFIGMAP_NAME, SELF_SIGNED_CONFIGMAP_NAME, SERVICE_CA_CONFIGMAP_NAME,
                         WORKBENCH_CA_CONFIGMAP_NAME)
@@ -106,10 +107,11 @@ async def create_notebook_cert_configmap(client, nb: dict) -> None:
             return  # the reference swallows non-NotFound read errors here
         try:
             await client.create(desired)
+            return
         except ApiError as e2:
             if not is_already_exists(e2):
                 raise
-        return
+        found = await get_live(client, kinds.CONFIG_MAP, WORKBENCH_CA_CONFIGMAP_NAME, ns)  # created meanwhile
     if (found.get("data") or {}) != desired["data"]:
         found["data"] = desired["data"]
         await client.update(found)

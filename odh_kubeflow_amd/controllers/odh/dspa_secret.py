@@ -19,6 +19,7 @@ from typing import Optional
 from ...models import kinds
 from ...models import meta as m
 from ...models.errors import ApiError, is_already_exists, is_no_match, is_not_found
+from ...runtime.client import get_live
 from .constants import (DEFAULT_GATEWAY_NAME, DEFAULT_GATEWAY_NAMESPACE, DSPA_INSTANCE_NAME, ELYRA_MOUNT_PATH,
                         ELYRA_SECRET_NAME, ELYRA_VOLUME_NAME, MANAGED_BY_KEY, MANAGED_BY_VALUE)
 from .podspec import add_if_absent, containers, volumes
@@ -154,10 +155,13 @@ async def sync_elyra_runtime_config_secret(client, nb: dict) -> None:
             raise
         try:
             await client.create(desired)
+            return
         except ApiError as e2:
             if not is_already_exists(e2):
                 raise
-        return
+        # created meanwhile by another actor (inside the informer's lag): reconcile ITS data
+        # like any existing Secret's instead of leaving it as found
+        existing = await get_live(client, kinds.SECRET, ELYRA_SECRET_NAME, m.namespace(nb))
     if (existing.get("data") or {}) != desired_data or m.labels(existing).get(MANAGED_BY_KEY) != MANAGED_BY_VALUE:
         existing["metadata"]["labels"] = dict(desired["metadata"]["labels"])
         existing["data"] = desired_data

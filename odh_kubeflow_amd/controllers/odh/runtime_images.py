@@ -16,7 +16,8 @@ import re
 
 from ...models import kinds
 from ...models import meta as m
-from ...models.errors import ApiError, is_no_match, is_not_found
+from ...models.errors import ApiError, is_already_exists, is_no_match, is_not_found
+from ...runtime.client import get_live
 from .constants import (MANAGED_BY_KEY, MANAGED_BY_VALUE, RUNTIME_IMAGE_LABEL, RUNTIME_IMAGE_METADATA_ANNOTATION,
                         RUNTIME_IMAGES_CONFIGMAP, RUNTIME_IMAGES_MOUNT_PATH, RUNTIME_IMAGES_VOLUME)
 from .podspec import add_if_absent, containers, volumes
@@ -107,10 +108,19 @@ async def sync_runtime_images_configmap(client, notebook_namespace: str, control
             existing["data"] = data
             await client.update(existing)
         return
-    await client.create({"apiVersion": "v1", "kind": "ConfigMap",
-                         "metadata": {"name": RUNTIME_IMAGES_CONFIGMAP, "namespace": notebook_namespace,
-                                      "labels": {MANAGED_BY_KEY: MANAGED_BY_VALUE}},
-                         "data": data})
+    try:
+        await client.create({"apiVersion": "v1", "kind": "ConfigMap",
+                             "metadata": {"name": RUNTIME_IMAGES_CONFIGMAP, "namespace": notebook_namespace,
+                                          "labels": {MANAGED_BY_KEY: MANAGED_BY_VALUE}},
+                             "data": data})
+    except ApiError as e:
+        if not is_already_exists(e):
+            raise
+        # created meanwhile (a concurrent admission or reconcile): bring ITS data up to date
+        existing = await get_live(client, kinds.CONFIG_MAP, RUNTIME_IMAGES_CONFIGMAP, notebook_namespace)
+        if (existing.get("data") or {}) != data:
+            existing["data"] = data
+            await client.update(existing)
 
 
 async def mount_pipeline_runtime_images(client, nb: dict) -> None:

@@ -479,22 +479,37 @@ async def _main(args, dist, torch, rank: int, world: int, ndev: int, probe_sampl
 
 
 async def _apiserver_prof(native) -> Optional[dict]:
+    """The native apiserver's profile counters, with each resource's store-lock contention
+    flattened in as ``lock_wait_ns@<resource>`` / ``lock_contended@<resource>``."""
     if native is None:
         return None
     try:
-        return (await native.stats()).get("prof")
+        st = await native.stats()
     except Exception:
         return None
+    out = dict(st.get("prof") or {})
+    for res, v in (st.get("locks") or {}).items():
+        out[f"lock_wait_ns@{res}"] = v.get("wait_ns", 0)
+        out[f"lock_contended@{res}"] = v.get("contended", 0)
+    return out
 
 
 def _prof_per_step(p0: Optional[dict], p1: Optional[dict], steps: int) -> Optional[dict]:
     """Native apiserver profile delta over the timed region, per step (ms / counts)."""
     if not p0 or not p1:
         return None
-    out = {}
+    out, by_res = {}, {}
     for k, v in p1.items():
         d = (v - p0.get(k, 0)) / max(1, steps)
+        if "@" in k:  # per resource: only the ones that waited in the window
+            name, res = k.split("@", 1)
+            if d:
+                by_res.setdefault(res, {})["wait_ms" if name.startswith("lock_wait") else "contended"] = \
+                    round(d / 1e6, 3) if name.endswith("_ns") else round(d, 2)
+            continue
         out[k[:-3] + "_ms" if k.endswith("_ns") else k] = round(d / 1e6, 3) if k.endswith("_ns") else round(d, 2)
+    if by_res:
+        out["lock_wait_by_resource"] = dict(sorted(by_res.items(), key=lambda kv: -kv[1].get("wait_ms", 0)))
     return out
 
 

@@ -42,6 +42,16 @@ CURRENT_RECONCILE: contextvars.ContextVar = contextvars.ContextVar("current_reco
 # (the value: the keys already confirmed absent during this admission, read once)
 CONFIRM_ABSENCE: contextvars.ContextVar = contextvars.ContextVar("confirm_absence", default=None)
 _RETRY = object()  # a coalesced live read whose sender was cancelled: read again
+
+
+async def get_live(client, kind, name: str, namespace: Optional[str] = None):
+    """``client.get`` straight from the apiserver, whatever the client's cache says — e.g. after a
+    create answered AlreadyExists for an object the (data-stripped) informer had not shown yet."""
+    tok = LIVE_READS.set(True)
+    try:
+        return await client.get(kind, name, namespace)
+    finally:
+        LIVE_READS.reset(tok)
 # how long a read of an object this client just wrote waits for the watch to deliver the
 # write before it reads through to the apiserver instead
 RYOW_WAIT_S = 0.05

@@ -24,7 +24,7 @@ BINARY = os.path.join(os.path.dirname(HERE), "native", "bin", "odh-apiserver")
 
 
 def scheme_config(uninstalled: Iterable[str] = (), gc: bool = False, token: Optional[str] = None,
-                  history: int = 4096) -> dict:
+                  history: int = 1024) -> dict:
     skip = {SCHEME.resolve(k).key for k in uninstalled}
     res = []
     for i in SCHEME.all():
@@ -50,7 +50,7 @@ class NativeApiServer:
     ThreadSanitizer one the race-detection test compiles; ``env`` is added to its environment."""
 
     def __init__(self, uninstalled: Iterable[str] = (), gc: bool = False, token: Optional[str] = None,
-                 host: str = "127.0.0.1", port: int = 0, history: int = 4096, binary: Optional[str] = None,
+                 host: str = "127.0.0.1", port: int = 0, history: int = 1024, binary: Optional[str] = None,
                  env: Optional[dict] = None, audit_log_path: Optional[str] = None, audit_policy=None,
                  write_latency_ms: float = 0.0):
         self.cfg = scheme_config(uninstalled, gc, token, history)

@@ -40,7 +40,8 @@
 // etcd-like storage round trip, for measurements that should not assume a free store.
 //
 // Usage: odh-apiserver --config scheme.json [--host 127.0.0.1] [--port 0] [--gc]
-//        [--token T] [--history 4096] [--write-latency-ms 0]; prints "LISTENING <port>" once ready.
+//        [--token T] [--history 1024] [--write-latency-ms 0] [--webhook-connections 16];
+//        prints "LISTENING <port>" once ready.
 
 #include <arpa/inet.h>
 #include <netdb.h>
@@ -53,6 +54,7 @@
 #include <signal.h>
 #include <sys/prctl.h>
 #include <sys/socket.h>
+#include <malloc.h>
 #include <unistd.h>
 
 #include <algorithm>
@@ -607,13 +609,14 @@ struct Bucket {
   std::mutex hmu;
   // this resource's store lock: objs, and the commit order of its events
   std::mutex mu;
+  std::atomic<uint64_t> wait_ns{0}, contended{0};  // contended acquisitions of mu (GET /metrics "locks")
 };
 
 struct Store {
   std::mutex imu;  // owners / uids (the GC's indexes); taken inside a resource's lock, never around one
   std::unordered_map<std::string, Bucket> data;  // one per resource, created at start-up, never rehashed
   std::atomic<int64_t> rv{0};
-  size_t history = 4096;
+  size_t history = 1024;
   int64_t write_latency_us = 0;
   bool gc = false;
   bool defaulting = true;  // kube-apiserver defaulting of Pods / StatefulSets / Deployments / Services
@@ -695,6 +698,7 @@ thread_local std::vector<std::string> t_fg;
 // one resource's store lock on the request path, timing only the contended acquisitions
 struct StoreLock {
   std::mutex& mu;
+  Bucket& b;
   uint64_t t_acq;
   explicit StoreLock(Bucket& b);
   ~StoreLock() {
@@ -707,7 +711,7 @@ struct StoreLock {
   StoreLock& operator=(const StoreLock&) = delete;
 };
 
-StoreLock::StoreLock(Bucket& b) : mu(b.mu) {
+StoreLock::StoreLock(Bucket& bk) : mu(bk.mu), b(bk) {
   if (!mu.try_lock()) {
     uint64_t t0 = mono_ns();
     bool got = false;
@@ -716,8 +720,11 @@ StoreLock::StoreLock(Bucket& b) : mu(b.mu) {
       got = mu.try_lock();
     }
     if (!got) mu.lock();
-    P.lock_wait_ns += mono_ns() - t0;
+    uint64_t w = mono_ns() - t0;
+    P.lock_wait_ns += w;
     P.lock_contended++;
+    b.wait_ns += w;
+    b.contended++;
   }
   t_acq = mono_ns();
 }
@@ -1539,8 +1546,18 @@ SSL_CTX* ctx_for(const std::string& ca_pem) {
 }
 
 // connection pool: host:port|ca -> idle connections
+// Connections to each webhook endpoint: idle ones are reused (keep-alive), and at most
+// g_webhook_conns are open at once — kube-apiserver multiplexes its admission calls over one
+// HTTP/2 connection, so a burst of creates must not turn into a burst of TLS handshakes
+// against the webhook server; a call finding them all busy waits for one to come back.
+struct WebhookPool {
+  std::vector<std::unique_ptr<TlsConn>> idle;
+  int open = 0;
+};
 std::mutex g_pool_mu;
-std::map<std::string, std::vector<std::unique_ptr<TlsConn>>> g_pool;
+std::condition_variable g_pool_cv;
+std::map<std::string, WebhookPool> g_pool;
+int g_webhook_conns = 16;
 
 std::unique_ptr<TlsConn> tls_connect(const std::string& host, int port, const std::string& ca, double timeout_s) {
   auto c = std::make_unique<TlsConn>();
@@ -1654,28 +1671,54 @@ Value call_webhook(const Webhook& w, const Value& review) {
                     "\r\nContent-Type: application/json\r\nAccept: application/json\r\nContent-Length: " +
                     std::to_string(body.size()) + "\r\n\r\n" + body;
   std::string pool_key = host + ":" + std::to_string(port) + "|" + w.ca_pem;
-  for (int attempt = 0; attempt < 2; ++attempt) {
-    std::unique_ptr<TlsConn> c;
-    if (attempt == 0) {
+  // a slot (an idle connection, or room to open one) for the duration of the call
+  auto acquire = [&](bool allow_idle) -> std::unique_ptr<TlsConn> {
+    std::unique_lock<std::mutex> g(g_pool_mu);
+    auto deadline = std::chrono::system_clock::now() + std::chrono::milliseconds((int64_t)(w.timeout_s * 1000));
+    while (true) {
+      WebhookPool& p = g_pool[pool_key];
+      if (allow_idle && !p.idle.empty()) {
+        auto c = std::move(p.idle.back());
+        p.idle.pop_back();
+        return c;
+      }
+      if (p.open < g_webhook_conns) {
+        p.open++;
+        return nullptr;  // the caller opens one
+      }
+      if (g_pool_cv.wait_until(g, deadline) == std::cv_status::timeout)
+        throw std::runtime_error("timed out waiting for a connection to the webhook");
+    }
+  };
+  auto give_back = [&](std::unique_ptr<TlsConn> c) {  // nullptr: the slot's connection is gone
+    {
       std::lock_guard<std::mutex> g(g_pool_mu);
-      auto& v = g_pool[pool_key];
-      if (!v.empty()) {
-        c = std::move(v.back());
-        v.pop_back();
+      WebhookPool& p = g_pool[pool_key];
+      if (c) p.idle.push_back(std::move(c));
+      else p.open--;
+    }
+    g_pool_cv.notify_one();
+  };
+  for (int attempt = 0; attempt < 2; ++attempt) {
+    std::unique_ptr<TlsConn> c = acquire(attempt == 0);
+    bool reused = (bool)c;
+    if (!c) {
+      try {
+        c = tls_connect(host, port, w.ca_pem, w.timeout_s);
+      } catch (...) {
+        give_back(nullptr);
+        throw;
       }
     }
-    bool reused = (bool)c;
-    if (!c) c = tls_connect(host, port, w.ca_pem, w.timeout_s);
     int status = 0;
     std::string resp;
     if (tls_write_all(*c, req) && tls_read_response(*c, &status, &resp)) {
-      {
-        std::lock_guard<std::mutex> g(g_pool_mu);
-        g_pool[pool_key].push_back(std::move(c));
-      }
+      give_back(std::move(c));
       if (status != 200) throw std::runtime_error("webhook returned HTTP " + std::to_string(status));
       return kj::parse(resp);
     }
+    c.reset();
+    give_back(nullptr);
     if (!reused) throw std::runtime_error("webhook request failed");
   }
   throw std::runtime_error("webhook request failed");
@@ -2895,6 +2938,19 @@ bool handle(int fd, Request& rq) {
              (unsigned long long)P.wakeups.load(), (unsigned long long)P.scanned.load(),
              (unsigned long long)P.admit_wall_ns.load());
     out += buf;
+    // per resource: the contended acquisitions of its store lock
+    out.pop_back();
+    out += ",\"locks\":{";
+    bool first = true;
+    for (auto& kv : S.data) {
+      if (!kv.second.contended.load()) continue;
+      snprintf(buf, sizeof(buf), "%s\"%s\":{\"wait_ns\":%llu,\"contended\":%llu}", first ? "" : ",",
+               kv.first.c_str(), (unsigned long long)kv.second.wait_ns.load(),
+               (unsigned long long)kv.second.contended.load());
+      out += buf;
+      first = false;
+    }
+    out += "}}";
     return respond(fd, 200, out, rq.keep_alive);
   }
   try {
@@ -3107,6 +3163,7 @@ int main(int argc, char** argv) {
     else if (a == "--token") g_token = next();
     else if (a == "--history") S.history = std::stoul(next());
     else if (a == "--write-latency-ms") S.write_latency_us = (int64_t)(std::stod(next()) * 1000.0);
+    else if (a == "--webhook-connections") g_webhook_conns = std::max(1, std::stoi(next()));
     else {
       fprintf(stderr, "unknown flag %s\n", a.c_str());
       return 2;
@@ -3121,9 +3178,20 @@ int main(int argc, char** argv) {
   size_t hist = S.history;
   load_config(config);
   init_buckets();
+  // one connection per thread: glibc would give each busy thread its own malloc arena (up to
+  // 8 x cores), and the objects a commit frees on one thread were allocated on another, so
+  // freed memory stays spread over many half-empty arenas.  A bounded number of arenas plus a
+  // periodic trim keep the resident size close to what the store and its history hold.
+  mallopt(M_ARENA_MAX, 8);
+  std::thread([] {
+    while (!g_stop) {
+      std::this_thread::sleep_for(std::chrono::seconds(2));
+      malloc_trim(0);
+    }
+  }).detach();
   if (gc_flag) S.gc = true;
   if (!tok.empty()) g_token = tok;
-  if (hist != 4096) S.history = hist;
+  if (hist != 1024) S.history = hist;
   signal(SIGPIPE, SIG_IGN);
   SSL_library_init();
   SSL_load_error_strings();

@@ -170,3 +170,42 @@ def test_unlabelled_or_tagless_imagestreams_ignored():
     bad_json = image_stream("w", [{"name": "t", "from": {"name": "img"},
                                    "annotations": {"opendatahub.io/runtime-image-metadata": "not json"}}])
     assert runtime_images.runtime_images_data([bad_json]) == {}
+
+
+def test_configmap_created_meanwhile_is_reconciled_not_left_as_found(run):
+    """a ConfigMap another actor created inside the informer's lag reads as absent
+    from the data-stripped cache; the create then answers AlreadyExists.  It is read live and
+    its data brought up to date (the reference would have read it live in the first place)."""
+    from odh_kubeflow_amd.models.errors import AlreadyExists, NotFound
+    from odh_kubeflow_amd.runtime.client import LIVE_READS
+
+    class Client:
+        def __init__(self):
+            self.live_reads = 0
+            self.updated = []
+
+        async def list(self, kind, namespace=None, **kw):
+            return [copy.deepcopy(CASES[1][1])]
+
+        async def get(self, kind, name, namespace=None):
+            if not LIVE_READS.get():
+                raise NotFound("configmaps", name)  # what the lagging cache says
+            self.live_reads += 1
+            return {"apiVersion": "v1", "kind": "ConfigMap", "metadata": {"name": name, "namespace": namespace,
+                                                                          "resourceVersion": "7"},
+                    "data": {"stale.json": "{}"}}
+
+        async def create(self, obj):
+            raise AlreadyExists("configmaps", obj["metadata"]["name"])
+
+        async def update(self, obj):
+            self.updated.append(obj)
+            return obj
+
+    async def go():
+        c = Client()
+        await runtime_images.sync_runtime_images_configmap(c, NS, CENTRAL)
+        assert c.live_reads == 1 and len(c.updated) == 1
+        assert set(c.updated[0]["data"]) == {"python-3.11-ubi9.json"}
+        assert c.updated[0]["metadata"]["resourceVersion"] == "7"
+    run(go())

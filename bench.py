@@ -67,6 +67,11 @@ def parse(argv=None):
                         "deployed kf / odh+webhook pair (A/B measurements)")
     p.add_argument("--workers", type=int, default=1,
                    help="unsharded: --workers of the kf and odh managers (namespace-partitioned worker processes)")
+    p.add_argument("--namespaces-per-rank", type=int, default=1,
+                   help="each rank drives its notebooks round-robin over M user namespaces (bench-r-j); sharded: "
+                        "created unlabelled and assigned to shards by the shipped NamespaceShardAssigner "
+                        "(crc32(name) %% N), so a shard serves the namespaces that hash to it, whichever rank "
+                        "drives them — per-shard notebooks, notebooks/s and CPU are reported")
     p.add_argument("--burst", type=int, default=32,
                    help="after the timed window: this many notebooks created at once (open loop), split over the "
                         "ranks — time to all Ready, notebooks/s at saturation, admission latency (0: skip)")

@@ -635,9 +635,16 @@ class NotebookEventReemitter:
                             f"Reissued from {str(inv.get('kind', '')).lower()}/{inv.get('name', '')}: {ev.get('message', '')}")
         return Result()
 
+    # the re-emitter's own output (and every other Notebook event) never reaches it: the
+    # apiserver filters the Event watch (kubectl get events --field-selector semantics)
+    EVENT_FIELD_SELECTOR = "involvedObject.kind!=Notebook"
+
     def setup_with_manager(self, mgr, max_concurrent: Optional[int] = None):
         pred = pred_funcs(create=lambda o: self._relevant(o), update=lambda o, old: self._relevant(o),
                           delete=lambda o: False)
+        cache = getattr(mgr, "cache", None) or mgr.reader
+        if hasattr(cache, "set_field_selector"):
+            cache.set_field_selector(kinds.EVENT, self.EVENT_FIELD_SELECTOR)
         b = mgr.builder().named("notebook-events").for_(kinds.EVENT, [pred])
         if max_concurrent is not None:
             b.with_options(max_concurrent_reconciles=max_concurrent)

@@ -11,7 +11,10 @@ Layout on an 8×MI355X node (see :mod:`.shard` and :mod:`.platform`):
   ``--arch unsharded`` (``overlays/mi355x``, the reference topology): rank 0 starts
   ``cmd/kf_manager.py`` + ``cmd/odh_manager.py`` and every rank's notebooks go through them;
 * each rank drives its own namespace: one step = create one ``amd.com/gpu: 1`` Notebook →
-  Ready → delete → Notebook and pod gone.
+  Ready → delete → Notebook and pod gone.  ``--namespaces-per-rank M``: the steps go round-robin
+  over M namespaces per rank, created unlabelled; sharded, every shard's kf process runs the
+  shipped ``NamespaceShardAssigner`` (``--assign-namespaces``), so a namespace lands on shard
+  ``crc32(name) % N`` whichever rank drives it — the per-shard load is reported (``shard_load``).
 
 **The timed region** is bracketed by barrier + ``torch.cuda.synchronize()`` on every rank;
 the elapsed time is the max over ranks.  It contains exactly the K steps: the end barrier
@@ -50,6 +53,36 @@ NOTEBOOK_IMAGE = "rocm/pytorch:rocm7.0_ubuntu22.04_py3.10_pytorch_2.10"
 
 def bench_namespace(rank: int) -> str:
     return f"bench-{rank}"
+
+
+def bench_namespaces(rank: int, per_rank: int = 1) -> list:
+    """The user namespaces rank ``rank`` drives: ``bench-r``, or ``bench-r-0 … bench-r-(M-1)``."""
+    if per_rank <= 1:
+        return [bench_namespace(rank)]
+    return [f"{bench_namespace(rank)}-{j}" for j in range(per_rank)]
+
+
+def shard_load(counts: dict, owner: dict, cpu_s: dict, elapsed: float, by: str,
+               procs: tuple = ("control_plane", "kf_manager_", "odh_manager_")) -> dict:
+    """Per shard (or worker): namespaces, notebooks driven through it in the timed window,
+    its notebooks/s and its processes' CPU per notebook.  ``counts``: namespace → notebooks;
+    ``owner``: namespace → shard key; ``cpu_s``: process name → CPU seconds in the window
+    (a control-plane process — name starting with one of ``procs`` — is a shard's when its
+    name ends in ``_<key>``)."""
+    shards: dict = {}
+    for ns, key in owner.items():
+        d = shards.setdefault(str(key), {"namespaces": 0, "notebooks": 0})
+        d["namespaces"] += 1
+        d["notebooks"] += counts.get(ns, 0)
+    for key, d in shards.items():
+        n = d["notebooks"]
+        d["notebooks_per_s"] = round(n / elapsed, 2) if elapsed > 0 else None
+        mine = {p: v for p, v in cpu_s.items() if p.startswith(procs) and p.endswith(f"_{key}")}
+        d["cpu_ms_per_notebook"] = {p: round(v * 1e3 / n, 3) for p, v in sorted(mine.items())} if n else {}
+    loads = [d["notebooks"] for d in shards.values()]
+    mean = statistics.fmean(loads) if loads else 0.0
+    return {"assigned_by": by, "shards": dict(sorted(shards.items(), key=lambda kv: kv[0])),
+            "max_over_mean_notebooks": round(max(loads) / mean, 3) if mean else None}
 
 
 def _dist_init():
@@ -160,6 +193,9 @@ def measure(args) -> Optional[dict]:
             out["gpu_probe_init_container"] = probe_report(res["probe_sample"], out.get("p50_ready_ms"))
         if res.get("burst"):
             out["burst"] = res["burst"]
+        if res.get("shard_load"):
+            out["shard_load"] = res["shard_load"]
+        out["config"]["namespaces_per_rank"] = max(1, getattr(args, "namespaces_per_rank", 1))
     dist.barrier()
     dist.destroy_process_group()
     return out
@@ -229,8 +265,9 @@ async def _burst(args, shard, dist, native, children: dict, use_odh: bool, tag: 
     rank, world = dist.get_rank(), dist.get_world_size()
     total = int(args.burst)
     k = total // world + (1 if rank < total % world else 0)
-    ns = shard.cfg.namespace
+    nss = shard.cfg.user_namespaces
     names = [f"burst-{tag}-{rank}-{i}" for i in range(k)]
+    ns_of = {nm: nss[i % len(nss)] for i, nm in enumerate(names)}
     ann = {"notebooks.opendatahub.io/inject-auth": "true"} if use_odh else None
     res = {"cpu": "500m", "memory": "1Gi"}
     gpus = 1 if total <= NODE_GPUS else 0  # up to one per MI355X of the node: GPU notebooks (config #3)
@@ -240,6 +277,7 @@ async def _burst(args, shard, dist, native, children: dict, use_odh: bool, tag: 
     wh0 = {k: {"served": d["served"], "gets": d.get("gets", 0)} for k, d in (await shard.webhook_timings()).items()} \
         if shard.cfg.launch else {}
     cpu0 = {kk: _proc_cpu_s(pid) for kk, pid in children.items()}
+    prof0 = await _apiserver_prof(native)
     await _in_thread(dist.barrier)
     t0 = time.perf_counter()
     ready_at, create_ms = {}, []
@@ -247,14 +285,14 @@ async def _burst(args, shard, dist, native, children: dict, use_odh: bool, tag: 
 
     def check() -> bool:
         for nm in list(pending):
-            if shard.notebook_ready(nm):
+            if shard.notebook_ready(nm, ns_of[nm]):
                 ready_at[nm] = time.perf_counter()
                 pending.discard(nm)
         return not pending
 
     async def create(nm):
         c0 = time.perf_counter()
-        nb = notebook(nm, ns, image=NOTEBOOK_IMAGE, annotations=ann, gpus=gpus)
+        nb = notebook(nm, ns_of[nm], image=NOTEBOOK_IMAGE, annotations=ann, gpus=gpus)
         c = nb["spec"]["template"]["spec"]["containers"][0]
         c.setdefault("resources", {}).setdefault("requests", {}).update(res)
         await shard.admin.create(nb)
@@ -267,18 +305,20 @@ async def _burst(args, shard, dist, native, children: dict, use_odh: bool, tag: 
     cpu = {kk: (_proc_cpu_s(pid) or 0.0) - (cpu0.get(kk) or 0.0) for kk, pid in children.items()
            if cpu0.get(kk) is not None}
     adm = (await native.admissions(adm0))["us"] if native is not None else []
+    # the apiserver over the burst: store-lock waits per resource, malloc_trim passes
+    prof = _prof_per_step(prof0, await _apiserver_prof(native), 1) if native is not None else None
     whd = list((await shard.webhook_timings(wh0)).values()) if shard.cfg.launch else []
     wh = [x for d in whd for x in d["handle_ms"]]
     wh_get = [x for d in whd for x in d.get("get_ms") or []]
     t_del = time.perf_counter()
-    await asyncio.gather(*(shard.admin.delete(kinds.NOTEBOOK, nm, ns) for nm in names))
-    gone = await shard.wait_until(lambda: all(shard.gone(nm) for nm in names), 180)
+    await asyncio.gather(*(shard.admin.delete(kinds.NOTEBOOK, nm, ns_of[nm]) for nm in names))
+    gone = await shard.wait_until(lambda: all(shard.gone(nm, ns_of[nm]) for nm in names), 180)
     teardown = time.perf_counter() - t_del
     gathered = [None] * world
     await _in_thread(dist.all_gather_object, gathered, {
         "lat": [(ready_at[nm] - t0) * 1e3 for nm in names if nm in ready_at], "create": create_ms,
         "all_ready": all_ready, "ok": ok and gone, "cpu": cpu, "adm": adm, "teardown": teardown, "k": k,
-        "wh": wh, "wh_get": wh_get})
+        "wh": wh, "wh_get": wh_get, "prof": prof})
     if rank != 0:
         return None
     lat = [x for g in gathered for x in g["lat"]]
@@ -305,6 +345,9 @@ async def _burst(args, shard, dist, native, children: dict, use_odh: bool, tag: 
                            "n": sum(len(g["wh_get"]) for g in gathered)},
         "cpu_ms_per_notebook": {kk: round(v * 1e3 / max(1, total), 3) for kk, v in sorted(cpu_all.items())},
         "teardown_s": round(max(g["teardown"] for g in gathered), 4),
+        "apiserver": {k: v for k, v in (gathered[0]["prof"] or {}).items()
+                      if k in ("lock_wait_ms", "lock_contended", "lock_wait_by_resource", "trim_ms", "trims",
+                               "admit_wall_ms")},
     }
 
 
@@ -449,8 +492,11 @@ async def _main(args, dist, torch, rank: int, world: int, ndev: int, probe_sampl
                                       pull_secret_delay_ms=getattr(args, "openshift_pull_secret_ms", -1.0)).start()
     await _in_thread(dist.broadcast_object_list, url, 0)
     env = {"SET_PIPELINE_RBAC": "false", "SET_PIPELINE_SECRET": "false"}
+    per_rank = max(1, getattr(args, "namespaces_per_rank", 1))
+    nss = bench_namespaces(rank, per_rank)
     shard = ControlPlaneShard(ShardConfig(
-        apiserver_url=url[0], namespace=bench_namespace(rank), shard=str(rank), arch=arch,
+        apiserver_url=url[0], namespace=nss[0], namespaces=nss, assign=(arch == "sharded" and per_rank > 1),
+        shard_count=world, shard=str(rank), arch=arch,
         launch=(arch == "sharded" or rank == 0), bootstrap=(rank == 0), odh=not args.no_odh,
         webhook=not args.no_odh, reference_emulation=args.reference_emulation, env=env, process=True,
         split=not getattr(args, "single_process_shard", False), workers=max(1, getattr(args, "workers", 1))))
@@ -461,6 +507,13 @@ async def _main(args, dist, torch, rank: int, world: int, ndev: int, probe_sampl
         await _in_thread(dist.barrier)
         await shard.start()
     await _in_thread(dist.barrier)  # every control plane and webhook is registered before anyone creates
+    if shard.cfg.assign:  # every shard's assigner is up: wait until it labelled this rank's namespaces
+        labels = await shard.wait_assigned(60.0)
+        if len(labels) != len(nss):
+            raise RuntimeError(f"rank {rank}: namespaces not assigned to a shard: "
+                               f"{sorted(set(nss) - set(labels))}")
+        shard.labels = labels
+        await _in_thread(dist.barrier)
 
     try:
         children = {"apiserver": native.proc.pid if native else None}
@@ -488,6 +541,7 @@ async def _apiserver_prof(native) -> Optional[dict]:
     except Exception:
         return None
     out = dict(st.get("prof") or {})
+    out.pop("trim_max_ns", None)  # a running max, not a counter
     for res, v in (st.get("locks") or {}).items():
         out[f"lock_wait_ns@{res}"] = v.get("wait_ns", 0)
         out[f"lock_contended@{res}"] = v.get("contended", 0)
@@ -513,20 +567,22 @@ def _prof_per_step(p0: Optional[dict], p1: Optional[dict], steps: int) -> Option
     return out
 
 
-async def _lifecycle(shard, nm: str, ann: Optional[dict], timeout: float = 120.0) -> tuple:
-    """create → Ready → delete → gone; returns (create→Ready s, Ready→gone s)."""
+async def _lifecycle(shard, nm: str, ann: Optional[dict], timeout: float = 120.0,
+                     ns: Optional[str] = None) -> tuple:
+    """create → Ready → delete → gone in ``ns`` (default: the rank's first namespace);
+    returns (create→Ready s, Ready→gone s, the pod)."""
     from ..models import kinds
     from ..models.notebook import notebook
 
-    ns = shard.cfg.namespace
+    ns = ns or shard.cfg.namespace
     t0 = time.perf_counter()
     await shard.admin.create(notebook(nm, ns, image=NOTEBOOK_IMAGE, gpus=1, annotations=ann))
-    if not await shard.wait_until(lambda: shard.notebook_ready(nm), timeout):
+    if not await shard.wait_until(lambda: shard.notebook_ready(nm, ns), timeout):
         raise RuntimeError(f"notebook {ns}/{nm} not Ready")
     ready = time.perf_counter()
     pod = shard.peek(kinds.POD, f"{nm}-0", ns)
     await shard.admin.delete(kinds.NOTEBOOK, nm, ns)
-    if not await shard.wait_until(lambda: shard.gone(nm), 60):
+    if not await shard.wait_until(lambda: shard.gone(nm, ns), 60):
         raise RuntimeError(f"teardown of {ns}/{nm} did not finish")
     return ready - t0, time.perf_counter() - ready, pod
 
@@ -539,13 +595,17 @@ async def _drive(args, shard, dist, torch, children: Optional[dict] = None, nati
     base_ann = {"notebooks.opendatahub.io/inject-auth": "true"} if use_odh else {}
     lat_ms, teardown_ms = [], []
     state = {"step": 0}
+    nss = shard.cfg.user_namespaces
+    ns_counts = {ns: 0 for ns in nss}  # timed notebooks per namespace
 
     async def one_step(timed: bool):
         state["step"] += 1
-        ready_s, gone_s, _pod = await _lifecycle(shard, f"nb-s{state['step']}", dict(base_ann) or None)
+        ns = nss[state["step"] % len(nss)]
+        ready_s, gone_s, _pod = await _lifecycle(shard, f"nb-s{state['step']}", dict(base_ann) or None, ns=ns)
         if timed:
             lat_ms.append(ready_s * 1e3)
             teardown_ms.append(gone_s * 1e3)
+            ns_counts[ns] += 1
 
     from ..utils import gctune
 
@@ -601,6 +661,14 @@ async def _drive(args, shard, dist, torch, children: Optional[dict] = None, nati
     idle = await shard.quiesce()
     settled = breakdown_delta(b0, await shard.reconcile_breakdown())
     io = io_delta(io0, await shard.io_counters())
+    # who served which namespace: the shard labels (sharded, assigned) or the supervisors'
+    # worker assignment (unsharded --workers; rank 0 launched the managers)
+    owner = dict(getattr(shard, "labels", None) or {})
+    if not owner and shard.cfg.arch != "sharded" and shard.cfg.launch and shard.cfg.workers > 1:
+        for _proc, a in (await shard.worker_assignments()).items():
+            for idx, names in a.items():
+                for ns in names:
+                    owner.setdefault(ns, f"worker_{idx}")
     samples = []
     for i in range(probe_sample):  # untimed: notebooks with the start-up probe init container
         ann = {**base_ann, GPU_PROBE_ANNOTATION: "true"}
@@ -634,7 +702,8 @@ async def _drive(args, shard, dist, torch, children: Optional[dict] = None, nati
                                                         "blocks": blocks,
                                                         "cpu": cpu, "rss": rss, "in_window": in_window,
                                                         "settled": settled, "idle": idle, "probe": samples,
-                                                        "io": io, "snap_lag_ms": snap_lag * 1e3})
+                                                        "io": io, "snap_lag_ms": snap_lag * 1e3,
+                                                        "ns_counts": ns_counts, "owner": owner})
     per_step = 1e3 / max(1, args.steps)
     cpu_ms = {"ranks": [round(g["cpu"]["rank"] * per_step, 3) for g in gathered]}
     for g in gathered:
@@ -642,6 +711,14 @@ async def _drive(args, shard, dist, torch, children: Optional[dict] = None, nati
             if k != "rank":
                 cpu_ms[k] = round(v * per_step, 3)
     window = merge_breakdowns(g["in_window"] for g in gathered)
+    load = None
+    counts = {ns: n for g in gathered for ns, n in g["ns_counts"].items()}
+    owners = {ns: o for g in gathered for ns, o in g["owner"].items() if ns in counts}
+    if len(counts) > len(gathered) and owners:  # --namespaces-per-rank M > 1
+        cpu_s = {k: v for g in gathered for k, v in g["cpu"].items() if k != "rank"}
+        load = shard_load(counts, owners, cpu_s, float(el.item()),
+                          "NamespaceShardAssigner: crc32(name) % N" if shard.cfg.arch == "sharded"
+                          else "worker supervisor: least-loaded, sticky (runtime/workers.py)")
     return {"elapsed": float(el.item()), "reconciles": sum(sum(t.values()) for t in window.values()),
             "lat_ms": [x for g in gathered for x in g["lat"]], "odh": use_odh,
             "teardown_ms": [x for g in gathered for x in g["teardown"]],
@@ -650,7 +727,7 @@ async def _drive(args, shard, dist, torch, children: Optional[dict] = None, nati
             "apiserver_profile_per_step": prof, "breakdown": merge_breakdowns(g["settled"] for g in gathered),
             "quiesced": all(g["idle"] for g in gathered),
             "io_per_notebook": io_per_notebook([g["io"] for g in gathered], args.steps * len(gathered)),
-            "burst": burst,
+            "burst": burst, "shard_load": load,
             "recon_snapshot_lag_ms": round(max(g["snap_lag_ms"] for g in gathered), 3),
             "probe_sample": [s for g in gathered for s in g["probe"]],
             "lifecycle_ms_per_20_steps": [round(statistics.fmean(b), 3) for b in zip(*(g["blocks"] for g in gathered))]}

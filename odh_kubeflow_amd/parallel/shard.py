@@ -15,7 +15,9 @@ deployable topologies are measured, both exactly as the manifests run them:
   rank 0 starts ``cmd/kf_manager.py`` and ``cmd/odh_manager.py`` (+ its webhook, one MWC for
   every namespace); the other ranks only drive notebooks into them.
 
-Each rank drives one namespace (``bench-r``) through an informer cache of its own.  The node
+Each rank drives its namespaces (``bench-r``; with ``namespaces``, M of them — labelled by the
+shipped :class:`~odh_kubeflow_amd.controllers.sharding.NamespaceShardAssigner` when ``assign``)
+through an informer cache of its own.  The node
 around them — scheduler + device allocator, StatefulSet controller, kubelet — is ONE
 :class:`~odh_kubeflow_amd.parallel.platform.NodePlatform` for all ranks, as on a real node.
 
@@ -64,6 +66,16 @@ class ShardConfig:
     process: bool = False  # run the control plane as its own process(es), as deployed
     split: bool = True  # sharded, process mode: kf and odh + webhook as two processes (the shard pod's two containers)
     workers: int = 1  # unsharded: --workers of the kf and odh managers (runtime/workers.py)
+    # the user namespaces this rank drives (default: just ``namespace``); with ``assign`` they
+    # are created unlabelled and the shipped NamespaceShardAssigner (``--assign-namespaces``,
+    # run by every shard's kf process) labels each ``crc32(name) % shard_count``
+    namespaces: List[str] = field(default_factory=list)
+    assign: bool = False
+    shard_count: int = 1
+
+    @property
+    def user_namespaces(self) -> List[str]:
+        return list(self.namespaces) or [self.namespace]
 
 
 class _Proc:
@@ -113,6 +125,8 @@ class ControlPlaneShard:
                 a = ["--shard", self.shard, "--controllers", ",".join(cs), "--health-probe-bind-address", "0"]
                 if "odh" in cs or "webhook" in cs:
                     a += wh
+                if cfg.assign and "kf" in cs:
+                    a += ["--assign-namespaces", "--shard-count", str(cfg.shard_count)]
                 if cfg.reference_emulation:
                     a.append("--reference-emulation")
                 name = "control_plane" if len(sets) == 1 else f"control_plane_{cs[0]}"
@@ -139,7 +153,9 @@ class ControlPlaneShard:
         if cfg.bootstrap:
             for ns in ("default", cfg.controller_namespace):
                 await self.ensure_namespace(ns)
-        await self.ensure_namespace(cfg.namespace, {SHARD_LABEL: self.shard} if self.shard is not None else None)
+        own = {SHARD_LABEL: self.shard} if self.shard is not None and not cfg.assign else None
+        for ns in cfg.user_namespaces:
+            await self.ensure_namespace(ns, own)
         if cfg.launch:
             self._certs = generate(("127.0.0.1", "localhost"))
             wport = free_port()
@@ -149,8 +165,8 @@ class ControlPlaneShard:
                 wport = await self._build_in_process()
             if cfg.webhook and cfg.odh:
                 await self._register_webhook(wport)
-        # this rank's notebook driver: its namespace's Notebooks and Pods
-        self.cache = InformerCache(self.rest, namespaces=[cfg.namespace])
+        # this rank's notebook driver: its namespaces' Notebooks and Pods
+        self.cache = InformerCache(self.rest, namespaces=cfg.user_namespaces)
         self._caches.append(self.cache)
         for k in (kinds.NOTEBOOK, kinds.POD):
             await self.cache.ensure_informer(k)
@@ -243,8 +259,24 @@ class ControlPlaneShard:
     def peek(self, kind, name: str, namespace: Optional[str] = None) -> Optional[dict]:
         return self.cache.get(kind, name, namespace)
 
-    def notebook_ready(self, name: str) -> bool:
-        nb = self.cache.get(kinds.NOTEBOOK, name, self.cfg.namespace)
+    async def wait_assigned(self, timeout: float = 60.0) -> Dict[str, str]:
+        """namespace → shard label of this rank's namespaces, once every one carries it
+        (``assign``: labelled by the shards' assigners, which come up with their shards)."""
+        loop = asyncio.get_running_loop()
+        deadline = loop.time() + timeout
+        out: Dict[str, str] = {}
+        while True:
+            for ns in self.cfg.user_namespaces:
+                if ns not in out:
+                    lab = m.labels(await self.rest.get(kinds.NAMESPACE, ns)).get(SHARD_LABEL)
+                    if lab is not None:
+                        out[ns] = lab
+            if len(out) == len(self.cfg.user_namespaces) or loop.time() > deadline:
+                return out
+            await asyncio.sleep(0.05)
+
+    def notebook_ready(self, name: str, namespace: Optional[str] = None) -> bool:
+        nb = self.cache.get(kinds.NOTEBOOK, name, namespace or self.cfg.namespace)
         if nb is None:
             return False
         st = nb.get("status") or {}
@@ -252,8 +284,8 @@ class ControlPlaneShard:
             return False
         return any(c.get("type") == "Ready" and c.get("status") == "True" for c in st.get("conditions") or [])
 
-    def gone(self, name: str) -> bool:
-        ns = self.cfg.namespace
+    def gone(self, name: str, namespace: Optional[str] = None) -> bool:
+        ns = namespace or self.cfg.namespace
         return self.cache.get(kinds.NOTEBOOK, name, ns) is None and self.cache.get(kinds.POD, f"{name}-0", ns) is None
 
     # -------------------------------------------------------------- control-plane counters
@@ -315,6 +347,16 @@ class ControlPlaneShard:
                                          "handle_ms": [x * 1e3 for x in list(srv.handle_s)[len(srv.handle_s) - n:]]}
         return out
 
+    async def worker_assignments(self) -> Dict[str, Dict[str, List[str]]]:
+        """process name → {worker index → namespaces} of the launched managers that run
+        ``--workers`` (the supervisor's namespace assignment)."""
+        out = {}
+        for p in self.procs:
+            a = (await self._get_json(f"{p.base}/debug/reconciles")).get("assignments")
+            if a:
+                out[p.name] = a
+        return out
+
     async def reconcile_count(self) -> int:
         return sum(sum(t.values()) for t in (await self.reconcile_breakdown()).values())
 
@@ -341,7 +383,7 @@ class ControlPlaneShard:
 
     async def wait_until(self, pred: Callable[[], bool], timeout: float = 10.0) -> bool:
         """Event-driven wait: ``pred`` is re-checked on every Notebook / Pod event of the
-        rank's namespace (after the cache applied it) instead of on a polling timer."""
+        rank's namespaces (after the cache applied it) instead of on a polling timer."""
         if pred():
             return True
         if self._waiters is None:
@@ -353,7 +395,7 @@ class ControlPlaneShard:
                     if not fut.done() and p():
                         fut.set_result(True)
             for k in (kinds.NOTEBOOK, kinds.POD):
-                self.cache.subscribe(k, on_event, namespace=self.cfg.namespace)
+                self.cache.subscribe(k, on_event)  # the cache holds only this rank's namespaces
         fut = asyncio.get_running_loop().create_future()
         w = (fut, pred)
         self._waiters.add(w)

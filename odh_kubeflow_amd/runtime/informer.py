@@ -46,12 +46,14 @@ def strip_data(obj: dict) -> dict:
 
 class _Informer:
     def __init__(self, cache: "InformerCache", info: ResourceInfo, version: str,
-                 namespace: Optional[str] = None, label_selector: Optional[str] = None):
+                 namespace: Optional[str] = None, label_selector: Optional[str] = None,
+                 field_selector: Optional[str] = None):
         self.cache = cache
         self.info = info
         self.version = version
         self.namespace = namespace
         self.label_selector = label_selector
+        self.field_selector = field_selector
         self._label_reqs = parse_label_selector(label_selector) if label_selector else None
         self.items: Dict[Tuple[str, str], dict] = {}
         self.by_ns: Dict[str, Set[Tuple[str, str]]] = {}
@@ -135,7 +137,7 @@ class _Informer:
 
     async def _relist(self) -> None:
         items, rv = await self.cache.rest.list_rv(f"{self.info.api_version(self.version)}/{self.info.kind}",
-                                                  self.namespace, self.label_selector)
+                                                  self.namespace, self.label_selector, self.field_selector)
         self.relists += 1
         seen = set()
         for o in items:
@@ -169,6 +171,7 @@ class _Informer:
                     need_list = False
                 started = time.monotonic()
                 async for et, obj in self.cache.rest.watch(ref, self.namespace, self.rv, labels=self.label_selector,
+                                                           fields=self.field_selector,
                                                            timeout_s=self.cache.watch_timeout_s):
                     backoff = 0.05
                     if et == "BOOKMARK":
@@ -240,13 +243,16 @@ class InformerCache(Reader, EventSource):
     narrows the dynamic set (with no ``namespace_selector``: every namespace it admits) — one
     worker of a controller partitioned over processes watches only its partition's namespaces.
     ``selectors`` maps a kind to a label selector applied server-side to its list/watch
-    (``cache.Options.ByObject[..].Label``) so a shard only ever receives the objects it owns.
+    (``cache.Options.ByObject[..].Label``) so a shard only ever receives the objects it owns;
+    ``field_selectors`` likewise with a field selector (``ByObject[..].Field``; immutable fields
+    only, e.g. an Event's ``involvedObject.kind``, so an object never moves out of it).
     """
 
     def __init__(self, rest, namespace: Optional[str] = None, transforms: Optional[Dict[str, Optional[Transform]]] = None,
                  watch_timeout_s: int = 300, namespaces: Optional[Iterable[str]] = None,
                  selectors: Optional[Dict[str, str]] = None, namespace_selector: Optional[str] = None,
-                 namespace_filter: Optional[Callable[[dict], bool]] = None):
+                 namespace_filter: Optional[Callable[[dict], bool]] = None,
+                 field_selectors: Optional[Dict[str, str]] = None):
         self.rest = rest
         self.namespace = namespace
         nss = list(namespaces) if namespaces is not None else ([namespace] if namespace else None)
@@ -260,6 +266,7 @@ class InformerCache(Reader, EventSource):
         for k, fn in (transforms or {}).items():
             self.transforms[SCHEME.resolve(k).key] = fn
         self.selectors: Dict[str, str] = {SCHEME.resolve(k).key: v for k, v in (selectors or {}).items()}
+        self.field_selectors: Dict[str, str] = {SCHEME.resolve(k).key: v for k, v in (field_selectors or {}).items()}
         self.watch_timeout_s = watch_timeout_s
         self._groups: Dict[str, _Group] = {}
         self._by_ref: Dict[str, _Group] = {}
@@ -318,11 +325,21 @@ class InformerCache(Reader, EventSource):
             inf._notify("DELETED", old, old)
 
     def _start_informer(self, g: _Group, ns: Optional[str]) -> _Informer:
-        inf = _Informer(self, g.info, g.version, ns, self.selectors.get(g.info.key))
+        inf = _Informer(self, g.info, g.version, ns, self.selectors.get(g.info.key),
+                        self.field_selectors.get(g.info.key))
         inf.handlers = g.handlers  # shared: subscriptions made earlier see this namespace too
         g.infs[ns] = inf
         inf.task = asyncio.ensure_future(inf.run())
         return inf
+
+    def set_field_selector(self, kind, selector: str) -> bool:
+        """Narrow ``kind``'s list/watch server-side before its informer starts (a controller
+        that needs only part of a kind, at setup); False when the informer already runs."""
+        key = SCHEME.resolve(kind).key
+        if key in self._groups:
+            return False
+        self.field_selectors[key] = selector
+        return True
 
     def covers(self, kind, namespace: Optional[str]) -> bool:
         """Whether reads of ``kind`` in ``namespace`` are served by this cache (False: the

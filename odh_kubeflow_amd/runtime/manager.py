@@ -337,7 +337,9 @@ class Manager:
                                                                   *(d.get("reconciles") for d in docs)]),
                                       "io": merge_counts([self.io_counters(), *(d.get("io") for d in docs)]),
                                       "workers": len(docs),
-                                      "worker_pids": self.supervisor.pids() if self.supervisor is not None else {}})
+                                      "worker_pids": self.supervisor.pids() if self.supervisor is not None else {},
+                                      "assignments": {str(i): nss for i, nss in self.supervisor.assignments().items()}
+                                      if self.supervisor is not None else {}})
 
         async def quiesce(req):
             quiet = float(req.query.get("quiet_ms", "2")) / 1e3

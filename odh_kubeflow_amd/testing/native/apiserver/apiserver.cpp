@@ -634,6 +634,7 @@ struct Prof {
   std::atomic<uint64_t> cpu_ns[C_N]{}, calls[C_N]{};
   std::atomic<uint64_t> lock_wait_ns{0}, lock_contended{0}, wakeups{0}, scanned{0}, admit_wall_ns{0};
   std::atomic<uint64_t> lock_hold_ns[C_N]{};
+  std::atomic<uint64_t> trim_ns{0}, trim_max_ns{0}, trims{0};  // malloc_trim passes (allocations wait on them)
 } P;
 thread_local int t_cat = C_OTHER;
 
@@ -2933,10 +2934,11 @@ bool handle(int fd, Request& rq) {
     }
     snprintf(buf, sizeof(buf),
              "\"lock_wait_ns\":%llu,\"lock_contended\":%llu,\"watch_wakeups\":%llu,\"watch_scanned\":%llu,"
-             "\"admit_wall_ns\":%llu}}",
+             "\"admit_wall_ns\":%llu,\"trim_ns\":%llu,\"trim_max_ns\":%llu,\"trims\":%llu}}",
              (unsigned long long)P.lock_wait_ns.load(), (unsigned long long)P.lock_contended.load(),
              (unsigned long long)P.wakeups.load(), (unsigned long long)P.scanned.load(),
-             (unsigned long long)P.admit_wall_ns.load());
+             (unsigned long long)P.admit_wall_ns.load(), (unsigned long long)P.trim_ns.load(),
+             (unsigned long long)P.trim_max_ns.load(), (unsigned long long)P.trims.load());
     out += buf;
     // per resource: the contended acquisitions of its store lock
     out.pop_back();
@@ -3186,7 +3188,12 @@ int main(int argc, char** argv) {
   std::thread([] {
     while (!g_stop) {
       std::this_thread::sleep_for(std::chrono::seconds(2));
+      auto t0 = std::chrono::steady_clock::now();
       malloc_trim(0);
+      uint64_t d = (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count();
+      P.trim_ns += d;
+      P.trims++;
+      if (d > P.trim_max_ns.load()) P.trim_max_ns = d;
     }
   }).detach();
   if (gc_flag) S.gc = true;

@@ -8,6 +8,7 @@ response must agree in status code and — after masking what each server assign
 both servers (``ODH_CLUSTER_TRANSPORT``), so a divergence here is a test that could pass
 over one and fail over the other."""
 
+import asyncio
 import random
 
 import pytest
@@ -144,3 +145,53 @@ def test_python_and_native_apiservers_answer_alike(run, seed):
         for x, y in zip(a, b):
             assert x == y, (x, y)
     run(go(), timeout=120)
+
+
+def test_event_field_selector_watch_on_both_apiservers(run):
+    """The kf event re-emitter's cache lists/watches Events with ``involvedObject.kind!=Notebook``
+    (``NotebookEventReemitter.EVENT_FIELD_SELECTOR``): the Notebook events it writes itself never
+    come back to it, from either apiserver, while Pod events do."""
+    from odh_kubeflow_amd.controllers.notebook import NotebookEventReemitter
+    from odh_kubeflow_amd.models import kinds
+    from odh_kubeflow_amd.runtime.informer import InformerCache
+
+    def ev(name, kind):
+        return {"apiVersion": "v1", "kind": "Event", "metadata": {"name": name, "namespace": "d"},
+                "involvedObject": {"kind": kind, "name": "x", "namespace": "d"}, "reason": "R", "message": "m"}
+
+    async def check(client):
+        await client.create({"apiVersion": "v1", "kind": "Namespace", "metadata": {"name": "d"}})
+        await client.create(ev("before-nb", "Notebook"))
+        await client.create(ev("before-pod", "Pod"))
+        cache = InformerCache(client, field_selectors={kinds.EVENT: NotebookEventReemitter.EVENT_FIELD_SELECTOR})
+        seen = []
+        cache.subscribe(kinds.EVENT, lambda et, o, old: seen.append((et, o["metadata"]["name"])))
+        try:
+            await cache.ensure_informer(kinds.EVENT)
+            await cache.wait_synced([kinds.EVENT])
+            await client.create(ev("after-nb", "Notebook"))
+            await client.create(ev("after-pod", "Pod"))
+            for _ in range(200):
+                if ("ADDED", "after-pod") in seen:
+                    break
+                await asyncio.sleep(0.01)
+            await asyncio.sleep(0.05)
+            assert not cache.set_field_selector(kinds.EVENT, "reason=X")  # the informer already runs
+        finally:
+            await cache.stop()
+        assert sorted(n for _, n in seen) == ["after-pod", "before-pod"], seen
+
+    async def go():
+        py = await ApiServer(ObjectStore()).start("127.0.0.1", 0)
+        nat = await native.NativeApiServer().start()
+        cp = RestClient(RestConfig(host=f"http://127.0.0.1:{py.port}"))
+        cn = RestClient(RestConfig(host=nat.url))
+        try:
+            await check(cp)
+            await check(cn)
+        finally:
+            await cp.close()
+            await cn.close()
+            await py.stop()
+            await nat.stop()
+    run(go(), timeout=60)

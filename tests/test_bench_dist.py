@@ -95,3 +95,44 @@ def test_numa_bind_pins_to_the_gpus_physical_cores(tmp_path, monkeypatch):
     monkeypatch.delenv("ODH_BENCH_NUMA_BIND")
     assert bench_dist.numa_bind(0, str(root)) is None  # GPU 0 has no PCI numa_node file: untouched
     assert len(calls) == 1
+
+
+def test_bench_namespaces_per_rank_assigned_by_the_shard_hash():
+    """``--namespaces-per-rank M`` (sharded): each rank's M namespaces are created unlabelled and
+    labelled by the shipped NamespaceShardAssigner, so a shard serves the namespaces that hash
+    to it — whichever rank drives them; the per-shard load is reported."""
+    import zlib
+
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
+           "127.0.0.1", "--master-port", str(_port()), "bench.py", "--gpus", "2", "--steps", "8", "--warmup", "1",
+           "--no-gpu-probe", "--namespaces-per-rank", "4", "--burst", "4", "--burst-rounds", "1"]
+    out = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=240)
+    assert out.returncode == 0, out.stderr[-3000:]
+    d = json.loads([l for l in out.stdout.splitlines() if l.startswith("{")][-1])
+    assert d["config"]["namespaces_per_rank"] == 4 and d["burst"]["all_ok"]
+    load = d["shard_load"]
+    assert load["assigned_by"].startswith("NamespaceShardAssigner")
+    want: dict = {}
+    for r in range(2):
+        for j in range(4):
+            k = str(zlib.crc32(f"bench-{r}-{j}".encode()) % 2)
+            want[k] = want.get(k, 0) + 1
+    assert {k: v["namespaces"] for k, v in load["shards"].items()} == want
+    assert sum(v["notebooks"] for v in load["shards"].values()) == 16
+    for k, v in load["shards"].items():
+        if v["notebooks"]:
+            assert set(v["cpu_ms_per_notebook"]) == {f"control_plane_kf_{k}", f"control_plane_odh_{k}"}
+
+
+def test_shard_load_report():
+    from odh_kubeflow_amd.parallel.bench_dist import bench_namespaces, shard_load
+
+    assert bench_namespaces(3) == ["bench-3"] and bench_namespaces(1, 3) == ["bench-1-0", "bench-1-1", "bench-1-2"]
+    out = shard_load({"a": 6, "b": 2, "c": 4}, {"a": "0", "b": "1", "c": "1"},
+                     {"control_plane_kf_0": 0.06, "control_plane_kf_1": 0.03, "kubelet_1": 9.0, "rank": 1.0},
+                     2.0, "hash")
+    assert out["shards"]["0"] == {"namespaces": 1, "notebooks": 6, "notebooks_per_s": 3.0,
+                                  "cpu_ms_per_notebook": {"control_plane_kf_0": 10.0}}
+    assert out["shards"]["1"]["notebooks"] == 6 and out["shards"]["1"]["cpu_ms_per_notebook"] == {
+        "control_plane_kf_1": 5.0}  # the platform's kubelet_1 is not shard 1's
+    assert out["max_over_mean_notebooks"] == 1.0

@@ -16,6 +16,9 @@
 #   burst64  64 notebooks at once into one unsharded control plane (--workers 1 and 4) and the sharded one
 #   fair     ours vs --reference-emulation: vanilla / OpenShift-like (pull secret after 200 ms), 0 / 2 ms writes
 #   pw4      4 ranks, --workers 4, one platform worker process per rank
+#   nsr      --namespaces-per-rank 16: sharded at 2 and 4 ranks (NamespaceShardAssigner hash), unsharded
+#            --workers 4 at 4 ranks (supervisor assignment) — per-shard notebooks, notebooks/s, CPU
+#   rss300   4 ranks x 300 steps (sharded): the apiserver's resident set after a long window
 #   archab   interleaved A/B at N=1: shard as kf/odh process pair vs one process vs unsharded
 #   probeexe the odh-gpu-probe init-container program: 10 process runs (wall time, verdict)
 #   hipinit  where a fresh process's HIP start-up goes, under ROCm runtime settings (tools/research/hip_init_ab.sh)
@@ -56,6 +59,10 @@ if b:
     print(sys.argv[2], "burst", {k: b.get(k) for k in ("notebooks", "all_ready_s", "notebooks_per_s", "ready_ms",
                                                       "admission_ms", "webhook_handle_ms", "webhook_get_ms",
                                                       "cpu_ms_per_notebook", "rounds")})
+sl = d.get("shard_load")
+if sl:
+    print(sys.argv[2], "shard_load", json.dumps(sl))
+print(sys.argv[2], "child_rss_mib", d.get("child_rss_mib"))
 c = d.get("configs")
 if c:
     print(sys.argv[2], "configs", json.dumps(c)[:3000])
@@ -147,6 +154,20 @@ for s in $steps; do
         --warmup 5 --probe-sample 0 --platform-workers 4 > "$out/bench_workers_pw4_n4.log" 2>&1 \
         || fail pw4 $? "$out/bench_workers_pw4_n4.log"
       show "$out/bench_workers_pw4_n4.log" "workers4 pw4 n4" ;;
+    nsr)
+      for v in "sharded 2 1" "sharded 4 1" "unsharded 4 4"; do
+        set -- $v
+        timeout -k 10 200 python -m torch.distributed.run --nnodes=1 --nproc-per-node $2 \
+          --master-addr 127.0.0.1 --master-port 2997$2 bench.py --gpus $2 --arch $1 --workers $3 --steps 100 \
+          --warmup 5 --probe-sample 0 --namespaces-per-rank 16 > "$out/bench_nsr16_$1_n$2.log" 2>&1 \
+          || fail nsr $? "$out/bench_nsr16_$1_n$2.log"
+        show "$out/bench_nsr16_$1_n$2.log" "nsr16 $1 n$2 w$3"
+      done ;;
+    rss300)
+      timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 4 \
+        --master-addr 127.0.0.1 --master-port 29980 bench.py --gpus 4 --steps 300 --warmup 5 --probe-sample 0 \
+        --burst 0 > "$out/bench_rss300_n4.log" 2>&1 || fail rss300 $? "$out/bench_rss300_n4.log"
+      show "$out/bench_rss300_n4.log" "rss300 n4" ;;
     burst64)
       for v in "unsharded 1" "unsharded 4" "sharded 1"; do
         set -- $v

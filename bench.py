@@ -72,6 +72,9 @@ def parse(argv=None):
                         "created unlabelled and assigned to shards by the shipped NamespaceShardAssigner "
                         "(crc32(name) %% N), so a shard serves the namespaces that hash to it, whichever rank "
                         "drives them — per-shard notebooks, notebooks/s and CPU are reported")
+    p.add_argument("--assign-policy", choices=("hash", "balanced"), default="hash",
+                   help="--namespaces-per-rank, sharded: the NamespaceShardAssigner policy (hash: crc32 %% N; "
+                        "balanced: the shard owning the fewest namespaces, as overlay mi355x-sharded deploys it)")
     p.add_argument("--burst", type=int, default=32,
                    help="after the timed window: this many notebooks created at once (open loop), split over the "
                         "ranks — time to all Ready, notebooks/s at saturation, admission latency (0: skip)")

@@ -56,6 +56,11 @@ def parse(argv: Optional[List[str]] = None) -> argparse.Namespace:
     p.add_argument("--assign-namespaces", action="store_true",
                    help="label unlabelled namespaces crc32(name) %% --shard-count (with --shard K: only those "
                         "that hash to K, so every shard claims its own)")
+    p.add_argument("--assign-policy", choices=("hash", "balanced"), default="hash",
+                   help="--assign-namespaces: hash (crc32 %% N) or balanced (the shard owning the fewest "
+                        "namespaces, ties to the hash's; preconditioned claims)")
+    p.add_argument("--assign-grace-seconds", type=float, default=5.0,
+                   help="balanced: after this long an unclaimed namespace goes to its hash's shard")
     p.add_argument("--metrics-bind-address", default=":8080")
     p.add_argument("--health-probe-bind-address", default=":8081")
     p.add_argument("--kube-rbac-proxy-image", default="")
@@ -137,7 +142,8 @@ def build(args, env=os.environ):
         from ..controllers.sharding import NamespaceShardAssigner
 
         mgr.assigner = NamespaceShardAssigner(mgr.client, mgr.reader, args.shard_count, exclude=[namespace],
-                                              only_shard=shard)
+                                              only_shard=shard, policy=args.assign_policy,
+                                              grace_s=args.assign_grace_seconds)
         mgr.assigner.setup_with_manager(mgr)
     mgr.webhook_server = None
     if "webhook" in args.controller_set:

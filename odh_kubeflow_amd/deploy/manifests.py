@@ -520,7 +520,8 @@ def control_plane_statefulset(shards: int) -> dict:
     so admissions and the odh pipeline never wait behind kf reconciles (cmd/control_plane.py)."""
     common = ["--shard=ordinal", "--leader-elect", "--kube-rbac-proxy-image=$(KUBE_RBAC_PROXY_IMAGE)"]
     kf = _control_plane_container("manager-kf", common + ["--controllers=kf", f"--shard-count={shards}",
-                                                          "--assign-namespaces"], 8080, 8081, webhook=False)
+                                                          "--assign-namespaces", "--assign-policy=balanced"],
+                                  8080, 8081, webhook=False)
     odh = _control_plane_container("manager-odh", common + [
         "--controllers=odh,webhook", "--metrics-bind-address=:8082", "--health-probe-bind-address=:8083",
         "--webhook-cert-dir=/tmp/k8s-webhook-server/serving-certs", "--webhook-port=8443"], 8082, 8083, webhook=True)

@@ -56,10 +56,16 @@ def bench_namespace(rank: int) -> str:
 
 
 def bench_namespaces(rank: int, per_rank: int = 1) -> list:
-    """The user namespaces rank ``rank`` drives: ``bench-r``, or ``bench-r-0 … bench-r-(M-1)``."""
+    """The user namespaces rank ``rank`` drives: ``bench-r``, or M names that look like real
+    users' (``bench-r-<10 hex digits>``, fixed per rank and index).  Sequential names
+    (``bench-r-0``, ``bench-r-1`` …) differ in one character, and crc32 — linear over GF(2) —
+    spreads such runs evenly over the shards, which real namespace names do not get."""
     if per_rank <= 1:
         return [bench_namespace(rank)]
-    return [f"{bench_namespace(rank)}-{j}" for j in range(per_rank)]
+    import hashlib
+
+    return [f"{bench_namespace(rank)}-{hashlib.sha256(f'{rank}/{j}'.encode()).hexdigest()[:10]}"
+            for j in range(per_rank)]
 
 
 def shard_load(counts: dict, owner: dict, cpu_s: dict, elapsed: float, by: str,
@@ -496,7 +502,7 @@ async def _main(args, dist, torch, rank: int, world: int, ndev: int, probe_sampl
     nss = bench_namespaces(rank, per_rank)
     shard = ControlPlaneShard(ShardConfig(
         apiserver_url=url[0], namespace=nss[0], namespaces=nss, assign=(arch == "sharded" and per_rank > 1),
-        shard_count=world, shard=str(rank), arch=arch,
+        shard_count=world, assign_policy=getattr(args, "assign_policy", "hash"), shard=str(rank), arch=arch,
         launch=(arch == "sharded" or rank == 0), bootstrap=(rank == 0), odh=not args.no_odh,
         webhook=not args.no_odh, reference_emulation=args.reference_emulation, env=env, process=True,
         split=not getattr(args, "single_process_shard", False), workers=max(1, getattr(args, "workers", 1))))
@@ -717,7 +723,9 @@ async def _drive(args, shard, dist, torch, children: Optional[dict] = None, nati
     if len(counts) > len(gathered) and owners:  # --namespaces-per-rank M > 1
         cpu_s = {k: v for g in gathered for k, v in g["cpu"].items() if k != "rank"}
         load = shard_load(counts, owners, cpu_s, float(el.item()),
-                          "NamespaceShardAssigner: crc32(name) % N" if shard.cfg.arch == "sharded"
+                          ("NamespaceShardAssigner: crc32(name) % N" if shard.cfg.assign_policy == "hash" else
+                           "NamespaceShardAssigner balanced: fewest namespaces, ties to crc32(name) % N")
+                          if shard.cfg.arch == "sharded"
                           else "worker supervisor: least-loaded, sticky (runtime/workers.py)")
     return {"elapsed": float(el.item()), "reconciles": sum(sum(t.values()) for t in window.values()),
             "lat_ms": [x for g in gathered for x in g["lat"]], "odh": use_odh,

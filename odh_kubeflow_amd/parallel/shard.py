@@ -72,6 +72,7 @@ class ShardConfig:
     namespaces: List[str] = field(default_factory=list)
     assign: bool = False
     shard_count: int = 1
+    assign_policy: str = "hash"  # NamespaceShardAssigner policy: hash | balanced
 
     @property
     def user_namespaces(self) -> List[str]:
@@ -126,7 +127,8 @@ class ControlPlaneShard:
                 if "odh" in cs or "webhook" in cs:
                     a += wh
                 if cfg.assign and "kf" in cs:
-                    a += ["--assign-namespaces", "--shard-count", str(cfg.shard_count)]
+                    a += ["--assign-namespaces", "--shard-count", str(cfg.shard_count),
+                          "--assign-policy", cfg.assign_policy]
                 if cfg.reference_emulation:
                     a.append("--reference-emulation")
                 name = "control_plane" if len(sets) == 1 else f"control_plane_{cs[0]}"

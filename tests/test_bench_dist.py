@@ -103,6 +103,8 @@ def test_bench_namespaces_per_rank_assigned_by_the_shard_hash():
     to it — whichever rank drives them; the per-shard load is reported."""
     import zlib
 
+    from odh_kubeflow_amd.parallel.bench_dist import bench_namespaces
+
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
            "127.0.0.1", "--master-port", str(_port()), "bench.py", "--gpus", "2", "--steps", "8", "--warmup", "1",
            "--no-gpu-probe", "--namespaces-per-rank", "4", "--burst", "4", "--burst-rounds", "1"]
@@ -114,8 +116,8 @@ def test_bench_namespaces_per_rank_assigned_by_the_shard_hash():
     assert load["assigned_by"].startswith("NamespaceShardAssigner")
     want: dict = {}
     for r in range(2):
-        for j in range(4):
-            k = str(zlib.crc32(f"bench-{r}-{j}".encode()) % 2)
+        for ns in bench_namespaces(r, 4):
+            k = str(zlib.crc32(ns.encode()) % 2)
             want[k] = want.get(k, 0) + 1
     assert {k: v["namespaces"] for k, v in load["shards"].items()} == want
     assert sum(v["notebooks"] for v in load["shards"].values()) == 16
@@ -127,7 +129,9 @@ def test_bench_namespaces_per_rank_assigned_by_the_shard_hash():
 def test_shard_load_report():
     from odh_kubeflow_amd.parallel.bench_dist import bench_namespaces, shard_load
 
-    assert bench_namespaces(3) == ["bench-3"] and bench_namespaces(1, 3) == ["bench-1-0", "bench-1-1", "bench-1-2"]
+    assert bench_namespaces(3) == ["bench-3"]
+    nss = bench_namespaces(1, 3)
+    assert len(set(nss)) == 3 and all(n.startswith("bench-1-") for n in nss) and nss == bench_namespaces(1, 3)
     out = shard_load({"a": 6, "b": 2, "c": 4}, {"a": "0", "b": "1", "c": "1"},
                      {"control_plane_kf_0": 0.06, "control_plane_kf_1": 0.03, "kubelet_1": 9.0, "rank": 1.0},
                      2.0, "hash")

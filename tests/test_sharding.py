@@ -590,6 +590,76 @@ def test_each_shard_assigns_only_its_own_namespaces(run):
     run(go())
 
 
+def test_balanced_assignment_evens_out_the_hash(run):
+    """policy="balanced" (overlay mi355x-sharded): every shard's assigner gives a new namespace to
+    the shard owning the fewest, ties to the hash's — 24 namespaces over 3 shards come out 8/8/8
+    where crc32 alone is uneven; each namespace is labelled exactly once (preconditioned claims)."""
+    from odh_kubeflow_amd.controllers.sharding import NamespaceShardAssigner, shard_for
+
+    names = [f"user-{i:02d}-x" for i in range(24)]
+
+    async def go():
+        store = ObjectStore()
+        mgrs, assigners = [], []
+        for k in ("0", "1", "2"):
+            mgr = in_process_manager(store, name=f"cp-{k}")
+            a = NamespaceShardAssigner(mgr.client, mgr.reader, 3, exclude=["opendatahub"], only_shard=k,
+                                       policy="balanced")
+            a.setup_with_manager(mgr)
+            await mgr.start()
+            mgrs.append(mgr)
+            assigners.append(a)
+        try:
+            for ns in names:
+                await store.create({"apiVersion": "v1", "kind": "Namespace", "metadata": {"name": ns}})
+                for mgr in mgrs:
+                    assert await mgr.wait_idle(5, settle=0.01)
+            got = [m.labels(store.peek(kinds.NAMESPACE, ns)).get("notebooks.amd.com/shard") for ns in names]
+            assert sorted(got.count(k) for k in "012") == [8, 8, 8], got
+            assert sum(a.assigned for a in assigners) == 24
+            by_hash = sorted(sum(1 for ns in names if shard_for(ns, 3) == k) for k in "012")
+            assert by_hash != [8, 8, 8]  # the names chosen are ones the hash spreads unevenly
+        finally:
+            for mgr in mgrs:
+                await mgr.stop()
+    run(go())
+
+
+def test_balanced_assignment_falls_back_to_the_hash_shard(run):
+    """The balanced target is down (shard 1 of 3): after the grace period the hash's shard claims
+    the namespace, so at most the namespaces that hash to the dead shard wait (as with policy
+    hash; those the plan gives a live shard are claimed by it), and none lands on the dead one."""
+    from odh_kubeflow_amd.controllers.sharding import NamespaceShardAssigner, shard_for
+
+    names = [f"team-{i}" for i in range(9)]
+
+    async def go():
+        store = ObjectStore()
+        mgrs = []
+        for k in ("0", "2"):
+            mgr = in_process_manager(store, name=f"cp-{k}")
+            NamespaceShardAssigner(mgr.client, mgr.reader, 3, only_shard=k, policy="balanced",
+                                   grace_s=0.5).setup_with_manager(mgr)
+            await mgr.start()
+            mgrs.append(mgr)
+        try:
+            for ns in names:
+                await store.create({"apiVersion": "v1", "kind": "Namespace", "metadata": {"name": ns}})
+            must = [ns for ns in names if shard_for(ns, 3) != "1"]
+            assert must
+            for _ in range(300):
+                got = {ns: m.labels(store.peek(kinds.NAMESPACE, ns)).get("notebooks.amd.com/shard") for ns in names}
+                if all(got[ns] is not None for ns in must):
+                    break
+                await asyncio.sleep(0.02)
+            assert all(got[ns] in ("0", "2") for ns in must), got
+            assert "1" not in got.values(), got
+        finally:
+            for mgr in mgrs:
+                await mgr.stop()
+    run(go(), timeout=30)
+
+
 def test_control_plane_flags(tmp_path):
     from odh_kubeflow_amd.cmd import control_plane
     from odh_kubeflow_amd.cmd.common import resolve_shard

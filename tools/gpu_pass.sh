@@ -16,7 +16,7 @@
 #   burst64  64 notebooks at once into one unsharded control plane (--workers 1 and 4) and the sharded one
 #   fair     ours vs --reference-emulation: vanilla / OpenShift-like (pull secret after 200 ms), 0 / 2 ms writes
 #   pw4      4 ranks, --workers 4, one platform worker process per rank
-#   nsr      --namespaces-per-rank 16: sharded at 2 and 4 ranks (NamespaceShardAssigner hash), unsharded
+#   nsr      --namespaces-per-rank 16: sharded at 2 and 4 ranks (NamespaceShardAssigner hash / balanced), unsharded
 #            --workers 4 at 4 ranks (supervisor assignment) — per-shard notebooks, notebooks/s, CPU
 #   rss300   4 ranks x 300 steps (sharded): the apiserver's resident set after a long window
 #   archab   interleaved A/B at N=1: shard as kf/odh process pair vs one process vs unsharded
@@ -155,13 +155,14 @@ for s in $steps; do
         || fail pw4 $? "$out/bench_workers_pw4_n4.log"
       show "$out/bench_workers_pw4_n4.log" "workers4 pw4 n4" ;;
     nsr)
-      for v in "sharded 2 1" "sharded 4 1" "unsharded 4 4"; do
+      for v in "sharded 2 1 hash" "sharded 2 1 balanced" "sharded 4 1 hash" "sharded 4 1 balanced" \
+               "unsharded 4 4 hash"; do
         set -- $v
         timeout -k 10 200 python -m torch.distributed.run --nnodes=1 --nproc-per-node $2 \
           --master-addr 127.0.0.1 --master-port 2997$2 bench.py --gpus $2 --arch $1 --workers $3 --steps 100 \
-          --warmup 5 --probe-sample 0 --namespaces-per-rank 16 > "$out/bench_nsr16_$1_n$2.log" 2>&1 \
-          || fail nsr $? "$out/bench_nsr16_$1_n$2.log"
-        show "$out/bench_nsr16_$1_n$2.log" "nsr16 $1 n$2 w$3"
+          --warmup 5 --probe-sample 0 --namespaces-per-rank 16 --assign-policy $4 \
+          > "$out/bench_nsr16_$1_n$2_$4.log" 2>&1 || fail nsr $? "$out/bench_nsr16_$1_n$2_$4.log"
+        show "$out/bench_nsr16_$1_n$2_$4.log" "nsr16 $1 n$2 w$3 $4"
       done ;;
     rss300)
       timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 4 \

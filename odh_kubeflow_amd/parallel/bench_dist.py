@@ -284,6 +284,7 @@ async def _burst(args, shard, dist, native, children: dict, use_odh: bool, tag: 
         if shard.cfg.launch else {}
     cpu0 = {kk: _proc_cpu_s(pid) for kk, pid in children.items()}
     prof0 = await _apiserver_prof(native)
+    gc0 = {k: v["seq"] for k, v in (await shard.gc_pauses()).items()} if shard.procs else {}
     await _in_thread(dist.barrier)
     t0 = time.perf_counter()
     ready_at, create_ms = {}, []
@@ -313,6 +314,8 @@ async def _burst(args, shard, dist, native, children: dict, use_odh: bool, tag: 
     adm = (await native.admissions(adm0))["us"] if native is not None else []
     # the apiserver over the burst: store-lock waits per resource, malloc_trim passes
     prof = _prof_per_step(prof0, await _apiserver_prof(native), 1) if native is not None else None
+    # the control-plane processes' cyclic-GC pauses over the burst (their event loops stop)
+    gcp = {k: [x[1:] for x in v["pauses"]] for k, v in (await shard.gc_pauses(gc0)).items()} if shard.procs else {}
     whd = list((await shard.webhook_timings(wh0)).values()) if shard.cfg.launch else []
     wh = [x for d in whd for x in d["handle_ms"]]
     wh_get = [x for d in whd for x in d.get("get_ms") or []]
@@ -324,7 +327,7 @@ async def _burst(args, shard, dist, native, children: dict, use_odh: bool, tag: 
     await _in_thread(dist.all_gather_object, gathered, {
         "lat": [(ready_at[nm] - t0) * 1e3 for nm in names if nm in ready_at], "create": create_ms,
         "all_ready": all_ready, "ok": ok and gone, "cpu": cpu, "adm": adm, "teardown": teardown, "k": k,
-        "wh": wh, "wh_get": wh_get, "prof": prof})
+        "wh": wh, "wh_get": wh_get, "prof": prof, "gc": gcp})
     if rank != 0:
         return None
     lat = [x for g in gathered for x in g["lat"]]
@@ -351,6 +354,9 @@ async def _burst(args, shard, dist, native, children: dict, use_odh: bool, tag: 
                            "n": sum(len(g["wh_get"]) for g in gathered)},
         "cpu_ms_per_notebook": {kk: round(v * 1e3 / max(1, total), 3) for kk, v in sorted(cpu_all.items())},
         "teardown_s": round(max(g["teardown"] for g in gathered), 4),
+        "gc_pause_ms": {proc: {"n": len(ps), "max": max(x[1] for x in ps),
+                               "gen2": sum(1 for x in ps if x[0] == 2)}
+                        for g in gathered for proc, ps in sorted(g["gc"].items()) if ps},
         "apiserver": {k: v for k, v in (gathered[0]["prof"] or {}).items()
                       if k in ("lock_wait_ms", "lock_contended", "lock_wait_by_resource", "trim_ms", "trims",
                                "admit_wall_ms")},

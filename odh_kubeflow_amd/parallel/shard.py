@@ -359,6 +359,20 @@ class ControlPlaneShard:
                 out[p.name] = a
         return out
 
+    async def gc_pauses(self, since: Optional[Dict[str, int]] = None) -> Dict[str, dict]:
+        """process name → {"seq": n, "pauses": [[seq, generation, ms], ...]} of the launched
+        control-plane processes (a manager's workers as ``<name>_worker_<i>``), the
+        collections after ``since[name]`` (a previous answer's seq)."""
+        out = {}
+        sfx = f"_{self.shard}" if self.shard is not None else ""
+        for p in self.procs:
+            d = await self._get_json(f"{p.base}/debug/gc")
+            for k, v in d.items():
+                name = f"{p.name}{sfx}" if k == "self" else f"{p.name}_{k}"
+                s0 = (since or {}).get(name, 0)
+                out[name] = {"seq": v.get("seq", 0), "pauses": [x for x in v.get("pauses") or [] if x[0] > s0]}
+        return out
+
     async def reconcile_count(self) -> int:
         return sum(sum(t.values()) for t in (await self.reconcile_breakdown()).values())
 

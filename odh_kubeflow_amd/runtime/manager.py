@@ -40,6 +40,12 @@ class Manager:
         self.source = source
         self.registry = registry or CollectorRegistry()
         self.runtime_metrics = RuntimeMetrics(self.registry)
+        from ..utils.gctune import PAUSES
+
+        try:
+            self.registry.register(PAUSES)
+        except ValueError:  # a registry shared by several managers of one process has it already
+            pass
         self.default_max_concurrent = default_max_concurrent
         self.controllers: List[Controller] = []
         self.runnables: List = []
@@ -371,6 +377,17 @@ class Manager:
             return web.json_response({"served": srv.served, "handle_ms": [round(x * 1e3, 3) for x in recent],
                                       "gets": gets, "get_ms": [round(x, 3) for x in g[len(g) - k:]] if k else []})
 
+        async def gc_pauses(req):
+            from ..utils.gctune import PAUSES
+
+            since = int(req.query.get("since", "0"))
+            out = {"self": PAUSES.since(since)}
+            if self.supervisor is not None:  # the workers' own (each numbers its collections itself)
+                for i, d in enumerate(await self.supervisor.debug("/debug/gc")):
+                    out[f"worker_{i}"] = d.get("self") or {}
+            return web.json_response(out)
+
         app.router.add_get("/debug/webhook", webhook)
+        app.router.add_get("/debug/gc", gc_pauses)
         app.router.add_get("/debug/reconciles", reconciles)
         app.router.add_get("/debug/quiesce", quiesce)

@@ -580,6 +580,10 @@ struct WatchSlot {
   // will deliver, so e.g. one node agent's label-selected cluster-wide pod watch is not
   // woken by every other GPU's pod writes
   std::function<bool(const Value&)> wants;
+  // a label / field selector: events in the watch's history may be ones it never wants, so it
+  // is not woken by them and could fall behind the bounded history — the periodic wake-up
+  // (emit) advances it; a watch without one is woken by every event it reads
+  bool filtered = false;
 };
 
 // one ordered event history: `seq` numbers its events, `hist` keeps the newest S.history
@@ -796,11 +800,17 @@ void emit(const Res& r, const char* type, Obj obj, Obj old) {
     b.all.hist.pop_front();
   }
   const Ev& ev = b.all.hist.back();
-  if ((b.all.seq & 1023) == 0) {
-    // periodic broadcast: watchers of quiet namespaces advance past other namespaces'
-    // events before those fall off the bounded history (no spurious 410 Gone relists)
-    for (auto& w : b.watchers) t_wake.push_back({w.second, ev.obj, ev.old, true});
-    return;
+  const int64_t step = std::max<int64_t>(1, (int64_t)S.history / 16);
+  if (b.all.seq % step == 0) {
+    // periodic wake-up of the selector-filtered watchers, an eighth of them every history/16
+    // events (each one every half history): one that rejects every event it sees advances
+    // past them before they fall off the bounded history (no spurious 410 Gone relists),
+    // without waking every watcher of the resource at once (a herd on the history lock that
+    // commits then wait for)
+    const int64_t turn = (b.all.seq / step) & 7;
+    int64_t i = 0;
+    for (auto& w : b.watchers)
+      if (w.second->filtered && (i++ & 7) == turn) t_wake.push_back({w.second, ev.obj, ev.old, true});
   }
   auto wake = [&](const std::string& ns) {
     auto rg = b.watchers.equal_range(ns);
@@ -2755,6 +2765,7 @@ void serve_watch(int fd, Res& r, const Path& p, const Request& rq) {
     }
   } unregister{wb, ns, &slot};
   slot.wants = wants;
+  slot.filtered = !lr.empty() || !fr.empty();
   {
     Bucket& b = bucket(r);
     StoreLock g(b);
@@ -3184,7 +3195,7 @@ int main(int argc, char** argv) {
   // 8 x cores), and the objects a commit frees on one thread were allocated on another, so
   // freed memory stays spread over many half-empty arenas.  A bounded number of arenas plus a
   // periodic trim keep the resident size close to what the store and its history hold.
-  mallopt(M_ARENA_MAX, 8);
+  if (!getenv("MALLOC_ARENA_MAX")) mallopt(M_ARENA_MAX, 8);  // glibc's own env setting wins (A/B runs)
   std::thread([] {
     while (!g_stop) {
       std::this_thread::sleep_for(std::chrono::seconds(2));

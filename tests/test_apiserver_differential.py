@@ -195,3 +195,40 @@ def test_event_field_selector_watch_on_both_apiservers(run):
             await py.stop()
             await nat.stop()
     run(go(), timeout=60)
+
+
+def test_selector_filtered_watch_survives_history_rollover(run):
+    """A label-selected watch whose selector rejects every event it sees is still advanced
+    (the apiserver's periodic wake-up of filtered watchers), so after many times the bounded
+    history of unwanted writes it delivers the next wanted one — no 410 Gone, no relist."""
+    from odh_kubeflow_amd.models import kinds
+    from odh_kubeflow_amd.models import meta as m
+
+    async def go():
+        nat = await native.NativeApiServer(history=64).start()
+        c = RestClient(RestConfig(host=nat.url))
+        try:
+            await c.create({"apiVersion": "v1", "kind": "Namespace", "metadata": {"name": "u"}})
+            first = await c.create({"apiVersion": "v1", "kind": "ConfigMap",
+                                    "metadata": {"name": "seed", "namespace": "u"}})
+            seen = []
+
+            async def consume(ns):
+                async for et, obj in c.watch(kinds.CONFIG_MAP, ns, m.resource_version(first),
+                                             labels="want=yes", timeout_s=20):
+                    seen.append((ns, et, m.name(obj)))
+                    return
+
+            tasks = [asyncio.ensure_future(consume("u")), asyncio.ensure_future(consume(None))]
+            await asyncio.sleep(0.1)
+            for i in range(600):  # > 9x the history, none of them wanted
+                await c.create({"apiVersion": "v1", "kind": "ConfigMap",
+                                "metadata": {"name": f"x{i}", "namespace": "u", "labels": {"want": "no"}}})
+            await c.create({"apiVersion": "v1", "kind": "ConfigMap",
+                            "metadata": {"name": "hit", "namespace": "u", "labels": {"want": "yes"}}})
+            await asyncio.wait_for(asyncio.gather(*tasks), 10)
+            assert sorted(seen, key=str) == sorted([("u", "ADDED", "hit"), (None, "ADDED", "hit")], key=str)
+        finally:
+            await c.close()
+            await nat.stop()
+    run(go(), timeout=60)

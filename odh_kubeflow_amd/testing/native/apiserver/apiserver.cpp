@@ -674,6 +674,10 @@ struct PendingWake {
   bool all;
 };
 thread_local std::vector<PendingWake> t_wake;
+// events trimmed off a bounded history inside a commit: often the last reference to an old
+// object version, whose tree is freed once the store lock is released (~StoreLock), not
+// while every other writer of the resource waits for it
+thread_local std::vector<Ev> t_free;
 // Owners removed by this thread whose dependents the garbage collector has yet to delete:
 // the cascade runs after the removing commit has released the store lock (each owner's
 // dependents under a lock of their own, still before the request is answered), so a
@@ -709,6 +713,7 @@ struct StoreLock {
   ~StoreLock() {
     P.lock_hold_ns[t_cat] += mono_ns() - t_acq;  // who keeps the others waiting
     mu.unlock();
+    if (!t_free.empty()) t_free.clear();
     if (!t_wake.empty()) flush_wakes();
     if ((!t_gc.empty() || !t_fg.empty()) && !t_gc_running) run_gc();
   }
@@ -792,11 +797,13 @@ void emit(const Res& r, const char* type, Obj obj, Obj old) {
     if (!ons.empty()) {
       auto it = b.by_ns.find(ons);
       if (it != b.by_ns.end() && !it->second.hist.empty() && it->second.hist.front().rv == old.rv) {
+        t_free.push_back(std::move(it->second.hist.front()));
         it->second.hist.pop_front();
         // an idle, unwatched namespace (e.g. deleted) keeps nothing; a watcher's Hist& stays valid
         if (it->second.hist.empty() && ons != evns && !b.watchers.count(ons)) b.by_ns.erase(it);
       }
     }
+    t_free.push_back(std::move(b.all.hist.front()));
     b.all.hist.pop_front();
   }
   const Ev& ev = b.all.hist.back();
@@ -1857,7 +1864,7 @@ Obj do_get(const Res& r, const std::string& ns, const std::string& name) {
   return it->second;
 }
 
-void remove_locked(const Res& r, Obj live, Value final);
+void remove_locked(const Res& r, Obj live, Obj final);
 void gc_dependents(const std::string& owner_uid);
 void sync_delete_locked(const Res& r, const std::string& ns, const std::string& name);
 
@@ -2004,8 +2011,8 @@ Obj commit_update(const Res& r, const Obj& cur, Value nw) {
   bool no_fin = !fin || !fin->is_arr() || fin->arr.empty();
   if (md(*live)->get("deletionTimestamp") && no_fin) {
     mdm(nw)["resourceVersion"] = Value::str(std::to_string(++S.rv));
-    auto out = std::make_shared<const Value>(nw);
-    remove_locked(r, live, std::move(nw));
+    auto out = std::make_shared<const Value>(std::move(nw));
+    remove_locked(r, live, out);
     return out;
   }
   mdm(nw)["resourceVersion"] = Value::str(std::to_string(++S.rv));
@@ -2100,7 +2107,7 @@ Obj do_patch(const Res& r, const std::string& ns, const std::string& name, const
   }
 }
 
-void remove_locked(const Res& r, Obj live, Value final) {
+void remove_locked(const Res& r, Obj live, Obj fp) {
   std::string ns = mget(*live, "namespace"), name = mget(*live, "name"), uid = mget(*live, "uid");
   bucket(r).objs.erase({ns, name});
   {
@@ -2109,7 +2116,6 @@ void remove_locked(const Res& r, Obj live, Value final) {
   }
   index_owner(r, *live, true);
   S.writes++;
-  auto fp = std::make_shared<const Value>(std::move(final));
   emit(r, "DELETED", fp, live);
   if (S.gc) t_gc.push_back(uid);  // cascaded once the lock is released (run_gc)
   // foreground owners waiting for their last dependent: re-checked after the commit, each
@@ -2158,7 +2164,7 @@ void fg_recheck(const std::string& u) {
   mdm(nw)["resourceVersion"] = Value::str(std::to_string(++S.rv));
   Obj old = it->second;
   if (nf.arr.empty()) {
-    remove_locked(*orr, old, std::move(nw));
+    remove_locked(*orr, old, std::make_shared<const Value>(std::move(nw)));
   } else {
     auto sp = std::make_shared<const Value>(std::move(nw));
     it->second = sp;
@@ -2183,7 +2189,7 @@ void sync_delete_locked(const Res& r, const std::string& ns, const std::string& 
   }
   Value final = *cur;
   mdm(final)["resourceVersion"] = Value::str(std::to_string(++S.rv));
-  remove_locked(r, cur, std::move(final));
+  remove_locked(r, cur, std::make_shared<const Value>(std::move(final)));
 }
 
 // Background cascade for a removed (or foreground-deleting) owner: each dependent whose
@@ -2281,7 +2287,7 @@ Value do_delete(const Res& r, const std::string& ns_, const std::string& name, c
   Value final = *cur;
   mdm(final)["resourceVersion"] = Value::str(std::to_string(++S.rv));
   Value out = final;
-  remove_locked(r, cur, std::move(final));
+  remove_locked(r, cur, std::make_shared<const Value>(std::move(final)));
   return out;
 }
 

@@ -617,17 +617,28 @@ struct Bucket {
 };
 
 struct Store {
-  std::mutex imu;  // owners / uids (the GC's indexes); taken inside a resource's lock, never around one
   std::unordered_map<std::string, Bucket> data;  // one per resource, created at start-up, never rehashed
   std::atomic<int64_t> rv{0};
   size_t history = 1024;
   int64_t write_latency_us = 0;
   bool gc = false;
   bool defaulting = true;  // kube-apiserver defaulting of Pods / StatefulSets / Deployments / Services
-  std::unordered_map<std::string, std::set<std::tuple<std::string, std::string, std::string>>> owners;
-  std::unordered_map<std::string, std::tuple<std::string, std::string, std::string>> uids;
   std::atomic<uint64_t> requests{0}, writes{0}, webhook_calls{0};
 } S;
+
+// The garbage collector's indexes — owner uid → dependents, uid → object — striped by uid:
+// every access is about one uid, so writers of different objects (every rank's commits, in
+// every resource) do not meet on one mutex.  A stripe's lock is taken inside a resource's
+// store lock, never around one, and never two stripes at once.
+using ObjKey = std::tuple<std::string, std::string, std::string>;
+struct IdxStripe {
+  std::mutex mu;
+  std::unordered_map<std::string, std::set<ObjKey>> owners;
+  std::unordered_map<std::string, ObjKey> uids;
+};
+constexpr size_t kIdxStripes = 64;
+IdxStripe g_idx[kIdxStripes];
+IdxStripe& idx(const std::string& uid) { return g_idx[std::hash<std::string>{}(uid) & (kIdxStripes - 1)]; }
 
 // Where the server's CPU goes (GET /metrics "prof"): thread CPU time per request class,
 // store-lock contention on the request path, watch wake-ups and the history entries the
@@ -678,6 +689,11 @@ thread_local std::vector<PendingWake> t_wake;
 // object version, whose tree is freed once the store lock is released (~StoreLock), not
 // while every other writer of the resource waits for it
 thread_local std::vector<Ev> t_free;
+thread_local std::vector<std::shared_ptr<std::string>> t_free_lines;
+// an event's serialised watch line is dropped this many events after it was emitted: every
+// live watcher has written it by then (they are woken at once); a late reader re-serialises.
+// The history keeps the objects (shared with the store) but not a second, JSON copy of each
+constexpr size_t kLineKeep = 64;
 // Owners removed by this thread whose dependents the garbage collector has yet to delete:
 // the cascade runs after the removing commit has released the store lock (each owner's
 // dependents under a lock of their own, still before the request is answered), so a
@@ -714,6 +730,7 @@ struct StoreLock {
     P.lock_hold_ns[t_cat] += mono_ns() - t_acq;  // who keeps the others waiting
     mu.unlock();
     if (!t_free.empty()) t_free.clear();
+    if (!t_free_lines.empty()) t_free_lines.clear();
     if (!t_wake.empty()) flush_wakes();
     if ((!t_gc.empty() || !t_fg.empty()) && !t_gc_running) run_gc();
   }
@@ -758,18 +775,19 @@ void index_owner(const Res& r, const Value& o, bool remove) {
   const Value* refs = m ? m->get("ownerReferences") : nullptr;
   if (!refs || !refs->is_arr()) return;
   auto k = std::make_tuple(r.key, mget(o, "namespace"), mget(o, "name"));
-  std::lock_guard<std::mutex> ig(S.imu);
   for (auto& ref : refs->arr) {
     std::string u = ref.str_or("uid");
     if (u.empty()) continue;
+    IdxStripe& st = idx(u);
+    std::lock_guard<std::mutex> ig(st.mu);
     if (remove) {
-      auto it = S.owners.find(u);
-      if (it != S.owners.end()) {
+      auto it = st.owners.find(u);
+      if (it != st.owners.end()) {
         it->second.erase(k);
-        if (it->second.empty()) S.owners.erase(it);
+        if (it->second.empty()) st.owners.erase(it);
       }
     } else {
-      S.owners[u].insert(k);
+      st.owners[u].insert(k);
     }
   }
 }
@@ -805,6 +823,11 @@ void emit(const Res& r, const char* type, Obj obj, Obj old) {
     }
     t_free.push_back(std::move(b.all.hist.front()));
     b.all.hist.pop_front();
+  }
+  if (b.all.hist.size() > kLineKeep) {
+    EvCache& c = *b.all.hist[b.all.hist.size() - 1 - kLineKeep].cache;
+    std::unique_lock<std::mutex> cl(c.mu, std::try_to_lock);  // a watcher serialising it: next time
+    if (cl.owns_lock() && c.line) t_free_lines.push_back(std::move(c.line));
   }
   const Ev& ev = b.all.hist.back();
   const int64_t step = std::max<int64_t>(1, (int64_t)S.history / 16);
@@ -1910,8 +1933,10 @@ Obj do_create(const Res& r, const std::string& url_ns, Value obj, bool dry) {
   auto sp = std::make_shared<const Value>(std::move(obj));
   b.objs[k] = sp;
   {
-    std::lock_guard<std::mutex> ig(S.imu);
-    S.uids[mget(*sp, "uid")] = std::make_tuple(r.key, ns, k.second);
+    const std::string u = mget(*sp, "uid");
+    IdxStripe& st = idx(u);
+    std::lock_guard<std::mutex> ig(st.mu);
+    st.uids[u] = std::make_tuple(r.key, ns, k.second);
   }
   index_owner(r, *sp, false);
   S.writes++;
@@ -1927,8 +1952,10 @@ Obj do_create(const Res& r, const std::string& url_ns, Value obj, bool dry) {
         auto slash = av.find('/');
         Res* owner = by_kind(slash == std::string::npos ? "" : av.substr(0, slash), ref.str_or("kind"));
         // an owner of a kind this server does not serve cannot be verified: keep the object
-        std::lock_guard<std::mutex> ig(S.imu);
-        if (!owner || S.uids.count(ref.str_or("uid"))) live = true;
+        const std::string u = ref.str_or("uid");
+        IdxStripe& st = idx(u);
+        std::lock_guard<std::mutex> ig(st.mu);
+        if (!owner || st.uids.count(u)) live = true;
       }
       if (!live) {
         sync_delete_locked(r, ns, k.second);
@@ -2111,8 +2138,9 @@ void remove_locked(const Res& r, Obj live, Obj fp) {
   std::string ns = mget(*live, "namespace"), name = mget(*live, "name"), uid = mget(*live, "uid");
   bucket(r).objs.erase({ns, name});
   {
-    std::lock_guard<std::mutex> ig(S.imu);
-    S.uids.erase(uid);
+    IdxStripe& st = idx(uid);
+    std::lock_guard<std::mutex> ig(st.mu);
+    st.uids.erase(uid);
   }
   index_owner(r, *live, true);
   S.writes++;
@@ -2135,9 +2163,10 @@ void remove_locked(const Res& r, Obj live, Obj fp) {
 void fg_recheck(const std::string& u) {
   std::tuple<std::string, std::string, std::string> loc;
   {
-    std::lock_guard<std::mutex> ig(S.imu);
-    auto it = S.uids.find(u);
-    if (it == S.uids.end() || S.owners.count(u)) return;
+    IdxStripe& st = idx(u);
+    std::lock_guard<std::mutex> ig(st.mu);
+    auto it = st.uids.find(u);
+    if (it == st.uids.end() || st.owners.count(u)) return;
     loc = it->second;
   }
   Res* orr = by_key(std::get<0>(loc));
@@ -2147,8 +2176,9 @@ void fg_recheck(const std::string& u) {
   auto it = b.objs.find({std::get<1>(loc), std::get<2>(loc)});
   if (it == b.objs.end() || mget(*it->second, "uid") != u) return;
   {
-    std::lock_guard<std::mutex> ig(S.imu);
-    if (S.owners.count(u)) return;  // a dependent appeared meanwhile
+    IdxStripe& st = idx(u);
+    std::lock_guard<std::mutex> ig(st.mu);
+    if (st.owners.count(u)) return;  // a dependent appeared meanwhile
   }
   const Value* f = md(*it->second)->get("finalizers");
   bool fg = false;
@@ -2197,9 +2227,10 @@ void sync_delete_locked(const Res& r, const std::string& ns, const std::string& 
 void gc_dependents(const std::string& owner_uid) {
   std::set<std::tuple<std::string, std::string, std::string>> deps;
   {
-    std::lock_guard<std::mutex> ig(S.imu);
-    auto it = S.owners.find(owner_uid);
-    if (it == S.owners.end()) return;
+    IdxStripe& st = idx(owner_uid);
+    std::lock_guard<std::mutex> ig(st.mu);
+    auto it = st.owners.find(owner_uid);
+    if (it == st.owners.end()) return;
     deps = it->second;
   }
   for (auto& d : deps) {
@@ -2211,10 +2242,12 @@ void gc_dependents(const std::string& owner_uid) {
     if (oit == b.objs.end()) continue;
     bool other_live = false;
     if (const Value* refs = md(*oit->second)->get("ownerReferences")) {
-      std::lock_guard<std::mutex> ig(S.imu);
       for (auto& ref : refs->arr) {
         std::string u = ref.str_or("uid");
-        if (u != owner_uid && S.uids.count(u)) other_live = true;
+        if (u == owner_uid) continue;
+        IdxStripe& st = idx(u);
+        std::lock_guard<std::mutex> ig(st.mu);
+        if (st.uids.count(u)) other_live = true;
       }
     }
     if (other_live) continue;

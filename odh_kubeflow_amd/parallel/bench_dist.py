@@ -359,7 +359,7 @@ async def _burst(args, shard, dist, native, children: dict, use_odh: bool, tag: 
                         for g in gathered for proc, ps in sorted(g["gc"].items()) if ps},
         "apiserver": {k: v for k, v in (gathered[0]["prof"] or {}).items()
                       if k in ("lock_wait_ms", "lock_contended", "lock_wait_by_resource", "trim_ms", "trims",
-                               "admit_wall_ms")},
+                               "admit_wall_ms", "webhook_dials", "webhook_dial_ms")},
     }
 
 
@@ -701,7 +701,11 @@ async def _drive(args, shard, dist, torch, children: Optional[dict] = None, nati
             # the earlier rounds warm what a running cluster has warm (the apiserver's
             # connections to the webhook, the informers' namespaces); the last one is reported
             burst["rounds"] = [{k: b.get(k) for k in ("all_ready_s", "notebooks_per_s")} |
-                               {"admission_p99_ms": b["admission_ms"]["p99"]} for b in rounds]
+                               {"admission_p99_ms": b["admission_ms"]["p99"],
+                                "webhook_handle_p99_ms": b["webhook_handle_ms"]["p99"],
+                                "webhook_dials": (b.get("apiserver") or {}).get("webhook_dials"),
+                                "webhook_dial_ms": (b.get("apiserver") or {}).get("webhook_dial_ms")}
+                               for b in rounds]
 
     el = torch.tensor([elapsed], dtype=torch.float64)
     await _in_thread(lambda: dist.all_reduce(el, op=dist.ReduceOp.MAX))

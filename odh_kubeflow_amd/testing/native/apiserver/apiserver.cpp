@@ -650,6 +650,7 @@ struct Prof {
   std::atomic<uint64_t> lock_wait_ns{0}, lock_contended{0}, wakeups{0}, scanned{0}, admit_wall_ns{0};
   std::atomic<uint64_t> lock_hold_ns[C_N]{};
   std::atomic<uint64_t> trim_ns{0}, trim_max_ns{0}, trims{0};  // malloc_trim passes (allocations wait on them)
+  std::atomic<uint64_t> webhook_dials{0}, webhook_dial_ns{0};  // new webhook connections: connect + TLS handshake
 } P;
 thread_local int t_cat = C_OTHER;
 
@@ -1602,6 +1603,7 @@ int g_webhook_conns = 16;
 
 std::unique_ptr<TlsConn> tls_connect(const std::string& host, int port, const std::string& ca, double timeout_s) {
   auto c = std::make_unique<TlsConn>();
+  const uint64_t t0 = mono_ns();
   struct addrinfo hints {};
   hints.ai_family = AF_UNSPEC;
   hints.ai_socktype = SOCK_STREAM;
@@ -1635,6 +1637,8 @@ std::unique_ptr<TlsConn> tls_connect(const std::string& host, int port, const st
     ERR_error_string_n(e, buf, sizeof(buf));
     throw std::runtime_error(std::string("TLS handshake failed: ") + buf);
   }
+  P.webhook_dials++;
+  P.webhook_dial_ns += mono_ns() - t0;
   return c;
 }
 
@@ -2970,7 +2974,7 @@ bool handle(int fd, Request& rq) {
   }
   if (rq.method == "GET" && rq.path == "/metrics") {
     int64_t rv = S.rv.load();
-    char buf[256];
+    char buf[1024];  // the longest line below: 13 counters of up to 20 digits and their names
     snprintf(buf, sizeof(buf),
              "{\"requests\":%llu,\"writes\":%llu,\"webhook_calls\":%llu,\"resourceVersion\":%lld,\"prof\":{",
              (unsigned long long)S.requests.load(), (unsigned long long)S.writes.load(),
@@ -2984,11 +2988,13 @@ bool handle(int fd, Request& rq) {
     }
     snprintf(buf, sizeof(buf),
              "\"lock_wait_ns\":%llu,\"lock_contended\":%llu,\"watch_wakeups\":%llu,\"watch_scanned\":%llu,"
-             "\"admit_wall_ns\":%llu,\"trim_ns\":%llu,\"trim_max_ns\":%llu,\"trims\":%llu}}",
+             "\"admit_wall_ns\":%llu,\"trim_ns\":%llu,\"trim_max_ns\":%llu,\"trims\":%llu,"
+             "\"webhook_dials\":%llu,\"webhook_dial_ns\":%llu}}",
              (unsigned long long)P.lock_wait_ns.load(), (unsigned long long)P.lock_contended.load(),
              (unsigned long long)P.wakeups.load(), (unsigned long long)P.scanned.load(),
              (unsigned long long)P.admit_wall_ns.load(), (unsigned long long)P.trim_ns.load(),
-             (unsigned long long)P.trim_max_ns.load(), (unsigned long long)P.trims.load());
+             (unsigned long long)P.trim_max_ns.load(), (unsigned long long)P.trims.load(),
+             (unsigned long long)P.webhook_dials.load(), (unsigned long long)P.webhook_dial_ns.load());
     out += buf;
     // per resource: the contended acquisitions of its store lock
     out.pop_back();

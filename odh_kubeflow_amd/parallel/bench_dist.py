@@ -554,6 +554,8 @@ async def _apiserver_prof(native) -> Optional[dict]:
         return None
     out = dict(st.get("prof") or {})
     out.pop("trim_max_ns", None)  # a running max, not a counter
+    for k, v in (st.get("phases") or {}).items():  # write-path CPU by phase
+        out[f"phase_{k}"] = v
     for res, v in (st.get("locks") or {}).items():
         out[f"lock_wait_ns@{res}"] = v.get("wait_ns", 0)
         out[f"lock_contended@{res}"] = v.get("contended", 0)

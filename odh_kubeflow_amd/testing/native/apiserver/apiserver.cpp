@@ -654,6 +654,18 @@ struct Prof {
 } P;
 thread_local int t_cat = C_OTHER;
 
+// thread CPU per phase of the write path (GET /metrics "phases"): where a write's CPU goes
+enum Phase { PH_PARSE, PH_ADMIT, PH_VALIDATE, PH_DEFAULTS, PH_PATCH, PH_PREPARE, PH_DUMP, PH_N };
+const char* const PHASE_NAMES[PH_N] = {"parse", "admit", "validate", "defaults", "patch", "prepare", "dump"};
+std::atomic<uint64_t> g_phase_ns[PH_N]{};
+uint64_t thread_cpu_ns();
+struct PhaseTimer {
+  int ph;
+  uint64_t t0;
+  explicit PhaseTimer(int p) : ph(p), t0(thread_cpu_ns()) {}
+  ~PhaseTimer() { g_phase_ns[ph] += thread_cpu_ns() - t0; }
+};
+
 // every admission webhook call's wall time in µs, the newest 65536 (GET /debug/admissions?from=N
 // answers those from call N on): admission latency percentiles under a burst of creates
 constexpr uint64_t kAdmitRing = 1 << 16;
@@ -895,6 +907,7 @@ Value out_obj(const Res& r, const Value& o, const std::string& version);
 
 // the response body of a write: no copy when the request used the storage version
 std::string dump_out(const Res& r, const Value& o, const std::string& version) {
+  PhaseTimer pt(PH_DUMP);
   if (version.empty() || version == r.storage) return kj::dump(o);
   return kj::dump(out_obj(r, o, version));
 }
@@ -1083,6 +1096,7 @@ void schema_validate(const Value& s, const Value& v, const std::string& path, st
 }
 
 std::optional<std::string> validate(const Res& r, Value& o) {
+  PhaseTimer pt(PH_VALIDATE);
   auto it = g_schemas.find(r.key);
   if (it == g_schemas.end()) return std::nullopt;
   schema_prune(it->second, o, true);
@@ -1291,6 +1305,7 @@ void default_template(Value& spec) {
 }
 
 void api_defaults(const Res& r, Value& o) {
+  PhaseTimer pt(PH_DEFAULTS);
   if (r.key == "statefulsets.apps" || r.key == "deployments.apps") {
     Value& spec = obj_at(o, "spec");
     if (const Value* rep = spec.get("replicas"); !rep || rep->is_null()) spec["replicas"] = Value::integer(1);
@@ -1793,6 +1808,7 @@ bool selectors_match(const Webhook& w, const Res& r, const Value& obj, const Val
 }
 
 Value admit(const char* op, const Res& r, Value obj, const Value* old) {
+  PhaseTimer pt(PH_ADMIT);
   auto hooks = webhooks_for(r, op);
   for (auto& w : hooks) {
     if (!selectors_match(w, r, obj, old)) continue;
@@ -2024,8 +2040,12 @@ void prepare_update(const Res& r, const Value& base, Value& nw) {
 Obj commit_update(const Res& r, const Obj& cur, Value nw) {
   const std::string want_rv = mdm(nw).str_or("resourceVersion");
   const std::string ns = mget(*cur, "namespace"), name = mget(*cur, "name");
-  prepare_update(r, *cur, nw);
-  bool noop = equal_except_meta(nw, *cur);
+  bool noop;
+  {
+    PhaseTimer pt(PH_PREPARE);
+    prepare_update(r, *cur, nw);
+    noop = equal_except_meta(nw, *cur);
+  }
   if (!noop) storage_latency();
   Bucket& b = bucket(r);
   StoreLock g(b);
@@ -2094,6 +2114,7 @@ Obj do_patch_once(const Res& r, const std::string& ns, const std::string& name, 
   }
   Value nw;
   try {
+    PhaseTimer pt(PH_PATCH);
     if (ptype == "merge") nw = merge_patch(*cur, patch);
     else if (ptype == "json") nw = apply_json_patch(*cur, patch);
     else if (ptype == "strategic") nw = strategic_patch(*cur, patch);
@@ -2996,6 +3017,14 @@ bool handle(int fd, Request& rq) {
              (unsigned long long)P.trim_max_ns.load(), (unsigned long long)P.trims.load(),
              (unsigned long long)P.webhook_dials.load(), (unsigned long long)P.webhook_dial_ns.load());
     out += buf;
+    out.pop_back();
+    out += ",\"phases\":{";
+    for (int i = 0; i < PH_N; ++i) {
+      snprintf(buf, sizeof(buf), "%s\"%s_cpu_ns\":%llu", i ? "," : "", PHASE_NAMES[i],
+               (unsigned long long)g_phase_ns[i].load());
+      out += buf;
+    }
+    out += "}}";
     // per resource: the contended acquisitions of its store lock
     out.pop_back();
     out += ",\"locks\":{";
@@ -3080,6 +3109,7 @@ bool handle(int fd, Request& rq) {
     Value body;
     if (!rq.body.empty()) {
       try {
+        PhaseTimer pt(PH_PARSE);
         body = kj::parse(rq.body);
       } catch (const kj::ParseError& e) {
         throw BadRequest(std::string("invalid JSON body: ") + e.what());

@@ -40,3 +40,28 @@ def test_runtime_metrics_exposition():
     text = generate_latest(reg).decode()
     assert "# TYPE controller_runtime_reconcile_total counter" in text
     assert "# TYPE workqueue_queue_duration_seconds histogram" in text
+
+
+def test_gc_pause_recorder_histogram_and_since():
+    """Every cyclic-GC collection is timed (``gc.callbacks``): ``odh_gc_pause_seconds`` per
+    generation on the managers' /metrics, and ``since(seq)`` lists only newer pauses."""
+    import gc
+
+    from odh_kubeflow_amd.utils.gctune import PauseRecorder
+
+    rec = PauseRecorder(keep=8)
+    gc.callbacks.append(rec)
+    try:
+        gc.collect()
+        first = rec.since(0)
+        assert first["seq"] >= 1 and first["pauses"][-1][1] == 2 and first["pauses"][-1][2] >= 0
+        gc.collect(0)
+        newer = rec.since(first["seq"])
+        assert [p[1] for p in newer["pauses"]] == [0] and newer["seq"] == first["seq"] + 1
+    finally:
+        gc.callbacks.remove(rec)
+    reg = CollectorRegistry()
+    reg.register(rec)
+    text = generate_latest(reg).decode()
+    assert 'odh_gc_pause_seconds_count{generation="2"} 1.0' in text
+    assert 'odh_gc_pause_seconds_bucket{generation="0",le="+Inf"} 1.0' in text

@@ -22,7 +22,7 @@ from __future__ import annotations
 import collections
 import gc
 import time
-from typing import Dict, List, Tuple
+from typing import Dict, List
 
 DEFAULT_THRESHOLDS = (50_000, 20, 100)
 _BOUNDS = (0.0005, 0.001, 0.0025, 0.005, 0.01, 0.025, 0.05, 0.1, 0.25, 0.5, 1.0)
@@ -34,7 +34,7 @@ class PauseRecorder:
 
     def __init__(self, keep: int = 4096):
         self.seq = 0
-        self.recent: "collections.deque[Tuple[int, int, float]]" = collections.deque(maxlen=keep)
+        self.recent = collections.deque(maxlen=keep)  # (seq, generation, seconds)
         self.counts: Dict[int, List[int]] = {g: [0] * (len(_BOUNDS) + 1) for g in range(3)}
         self.sums: Dict[int, float] = {g: 0.0 for g in range(3)}
         self._t0 = 0.0

@@ -383,7 +383,7 @@ class Manager:
             since = int(req.query.get("since", "0"))
             out = {"self": PAUSES.since(since)}
             if self.supervisor is not None:  # the workers' own (each numbers its collections itself)
-                for i, d in enumerate(await self.supervisor.debug("/debug/gc")):
+                for i, d in (await self.supervisor.debug_by_worker("/debug/gc")).items():
                     out[f"worker_{i}"] = d.get("self") or {}
             return web.json_response(out)
 

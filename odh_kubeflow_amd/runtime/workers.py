@@ -439,8 +439,12 @@ class WorkerSupervisor:
         return [t for t in await asyncio.gather(*(self._get(w, "/metrics") for w in self.workers)) if t]
 
     async def debug(self, path: str, timeout: float = 30.0) -> List[dict]:
+        return list((await self.debug_by_worker(path, timeout)).values())
+
+    async def debug_by_worker(self, path: str, timeout: float = 30.0) -> Dict[int, dict]:
+        """worker index → its JSON answer (a worker restarting is missing)."""
         docs = await asyncio.gather(*(self._get(w, path, timeout) for w in self.workers))
-        return [json.loads(d) for d in docs if d]
+        return {w.index: json.loads(d) for w, d in zip(self.workers, docs) if d}
 
 
 def _drain(stream) -> None:

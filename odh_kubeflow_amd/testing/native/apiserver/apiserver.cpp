@@ -3266,11 +3266,12 @@ int main(int argc, char** argv) {
   size_t hist = S.history;
   load_config(config);
   init_buckets();
-  // one connection per thread: glibc would give each busy thread its own malloc arena (up to
-  // 8 x cores), and the objects a commit frees on one thread were allocated on another, so
-  // freed memory stays spread over many half-empty arenas.  A bounded number of arenas plus a
-  // periodic trim keep the resident size close to what the store and its history hold.
-  if (!getenv("MALLOC_ARENA_MAX")) mallopt(M_ARENA_MAX, 8);  // glibc's own env setting wins (A/B runs)
+  // One connection per thread, so glibc gives each busy thread its own malloc arena (up to
+  // 8 x cores), and objects freed on one thread were often allocated on another: freed memory
+  // spreads over many half-empty arenas.  A periodic trim returns it.  The arena count is left
+  // at glibc's default: capping it at 8 (MALLOC_ARENA_MAX, still honoured) cut the resident
+  // size by ≈10 % but cost ≈35 % more CPU per request at 4 ranks on a 64-core MI355X box, every
+  // thread queueing on a shared arena lock (tools/research/apiserver_ab.sh, profiles/r4_apiab).
   std::thread([] {
     while (!g_stop) {
       std::this_thread::sleep_for(std::chrono::seconds(2));

@@ -67,6 +67,9 @@ def parse(argv=None):
                         "deployed kf / odh+webhook pair (A/B measurements)")
     p.add_argument("--workers", type=int, default=1,
                    help="unsharded: --workers of the kf and odh managers (namespace-partitioned worker processes)")
+    p.add_argument("--webhook-replicas", type=int, default=1,
+                   help="unsharded with --workers: --webhook-replicas of the odh manager (webhook processes sharing "
+                        "the port)")
     p.add_argument("--namespaces-per-rank", type=int, default=1,
                    help="each rank drives its notebooks round-robin over M user namespaces (bench-r-j); sharded: "
                         "created unlabelled and assigned to shards by the shipped NamespaceShardAssigner "

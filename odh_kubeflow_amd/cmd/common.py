@@ -87,7 +87,8 @@ def add_worker_flags(p) -> None:
     import argparse
 
     p.add_argument("--workers", type=int, default=1,
-                   help="controller worker processes, namespaces partitioned crc32(ns) %% W (1: in this process)")
+                   help="controller worker processes, each serving the namespaces the supervisor assigns it "
+                        "(fewest first, sticky; 1: in this process)")
     p.add_argument("--worker", default=None, help=argparse.SUPPRESS)
 
 

@@ -12,7 +12,14 @@ object and ``data`` from ConfigMaps/Secrets, whose reads go straight to the apis
 ``--workers W`` runs the reconciler in W namespace-partitioned child processes
 (:mod:`~odh_kubeflow_amd.runtime.workers`); this process then leads, serves the webhook on
 its own event loop — admissions never queue behind a reconcile — and aggregates the
-workers' ``/metrics``.
+workers' ``/metrics``.  ``--webhook-replicas R`` (with ``--workers``) serves the webhook
+from R processes: this one and R-1 webhook-only children, every one accepting on the same
+port (``SO_REUSEPORT``: the kernel spreads the apiserver's connections over them).  One
+event loop is one core, and at 4 concurrent notebook streams the supervisor's webhook ran at
+≈60 % of one, so admissions — three per notebook, two of them on the create → Ready path —
+queued behind each other.  A replica reads what an admission needs the way the supervisor
+does: ConfigMaps and Secrets live (the reference's uncached reads), the controller
+namespace's objects from its cache.
 """
 
 from __future__ import annotations
@@ -47,6 +54,10 @@ def parse(argv: Optional[List[str]] = None) -> argparse.Namespace:
     add_shard_flags(p)
     add_debug_flags(p)
     add_worker_flags(p)
+    p.add_argument("--webhook-replicas", type=int, default=1,
+                   help="with --workers: processes serving the webhook on one port (SO_REUSEPORT), this one "
+                        "and R-1 webhook-only children")
+    p.add_argument("--webhook-replica", default=None, help=argparse.SUPPRESS)
     args = p.parse_args(argv)
     if not args.kube_rbac_proxy_image:
         p.print_usage(sys.stderr)
@@ -55,7 +66,8 @@ def parse(argv: Optional[List[str]] = None) -> argparse.Namespace:
     return args
 
 
-WORKER_STRIP_VALUE = ("--workers", "--worker", "--metrics-bind-address", "--health-probe-bind-address")
+WORKER_STRIP_VALUE = ("--workers", "--worker", "--metrics-bind-address", "--health-probe-bind-address",
+                      "--webhook-replicas", "--webhook-replica")
 WORKER_STRIP_BOOL = ("--leader-elect", "--enable-debug-endpoints")
 
 
@@ -67,6 +79,16 @@ def worker_argv(args, index: int, metrics_addr: str) -> List[str]:
     base = strip_flags(args.argv, WORKER_STRIP_VALUE, WORKER_STRIP_BOOL)
     return [*base, "--worker", f"{index}/{args.workers}", "--metrics-bind-address", metrics_addr,
             "--health-probe-bind-address", "0", "--enable-debug-endpoints"]
+
+
+def replica_argv(args, index: int, metrics_addr: str) -> List[str]:
+    """A webhook replica's command line: the supervisor's webhook flags (same port and
+    certificates), no leader election, no reconciler."""
+    from ..runtime.workers import strip_flags
+
+    base = strip_flags(args.argv, WORKER_STRIP_VALUE, WORKER_STRIP_BOOL)
+    return [*base, "--webhook-replica", f"{index}/{args.webhook_replicas - 1}", "--metrics-bind-address",
+            metrics_addr, "--health-probe-bind-address", "0", "--enable-debug-endpoints"]
 
 
 def build(args, env=os.environ):
@@ -84,11 +106,14 @@ def build(args, env=os.environ):
 
     shard = resolve_shard(getattr(args, "shard", None), env)
     worker = parse_worker(getattr(args, "worker", None))
+    replica = parse_worker(getattr(args, "webhook_replica", None))  # a webhook-only child
+    replicas = max(1, getattr(args, "webhook_replicas", 1))
     cfg = RestConfig.load(args.master, args.kubeconfig)
     namespace = namespace_from_env()
     log.info("Controller is running in namespace %s", namespace)
     lease = "odh-notebook-controller" + (f"-shard-{shard}" if shard is not None else "")
-    elector = LeaderElector(RestClient(cfg), lease, namespace) if args.leader_elect and worker is None else None
+    elector = (LeaderElector(RestClient(cfg), lease, namespace)
+               if args.leader_elect and worker is None and replica is None else None)
     cache_options = shard_cache_options(shard, namespace)
     assign = WorkerAssignments(*worker) if worker is not None else None
     if assign is not None:
@@ -99,8 +124,11 @@ def build(args, env=os.environ):
                          default_max_concurrent=args.max_concurrent_reconciles, leader_elector=elector,
                          metrics_addr=args.metrics_bind_address, probe_addr=args.health_probe_bind_address,
                          debug_endpoints=args.enable_debug_endpoints, cache_options=cache_options)
-    supervise = args.workers > 1 and worker is None
+    supervise = args.workers > 1 and worker is None and replica is None
     mgr.webhook_server = None
+    if replica is not None:  # the supervisor's stdin protocol (its end of file ends this process)
+        assign = WorkerAssignments(*replica)
+        assign.on_lost = lambda: mgr.fail("supervisor gone")
     if assign is not None:
         assign.cache = mgr.cache
         assign.on_lost = lambda: mgr.fail("supervisor gone")
@@ -112,6 +140,12 @@ def build(args, env=os.environ):
                                             system_namespaces=[namespace],
                                             name="odh-notebook-controller"))
         mgr.odh_reconciler = None
+        if replicas > 1:  # no namespaces to assign (no cache): the children only serve admissions
+            mgr.add_webhook_replicas(WorkerSupervisor("odh_kubeflow_amd.cmd.odh_manager", replicas - 1,
+                                                      lambda i, addr: replica_argv(args, i, addr), env=dict(env),
+                                                      name="odh-webhook"))
+    elif replica is not None:
+        mgr.odh_reconciler = None
     else:
         mgr.odh_reconciler = setup_odh(mgr, namespace, env, shard=shard)
     if worker is None:
@@ -122,8 +156,9 @@ def build(args, env=os.environ):
         if missing:
             raise SystemExit(f"webhook serving certificate missing in {args.webhook_cert_dir}: {', '.join(missing)} "
                              "(OpenShift: service-ca; elsewhere: the odh-webhook-certs Job, cmd/webhook_certs.py)")
+        shared = replica is not None or (supervise and replicas > 1)
         server = WebhookServer(wh, args.webhook_cert_dir, args.webhook_host, args.webhook_port,
-                               reload_interval=args.webhook_cert_reload_seconds)
+                               reload_interval=args.webhook_cert_reload_seconds, reuse_port=shared)
         mgr.add(ServerRunnable(server.start, server.stop), needs_leader=False)  # webhooks serve on every replica
         mgr.webhook_server = server
     mgr.add_healthz_check("healthz")

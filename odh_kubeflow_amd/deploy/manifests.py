@@ -91,6 +91,7 @@ MI355X_CULLER = ["CULLING_ACTIVITY_SOURCE=combined", "ENABLE_CULLING=true"]
 # processes (runtime/workers.py; the odh webhook stays on the supervisor's own event loop) —
 # one core per worker, so an 8-GPU node's notebooks are not serialised on one Python loop
 MI355X_WORKERS = 4
+MI355X_WEBHOOK_REPLICAS = 2
 # the base manifests carry the development tag; every overlay pins the release tag through
 # kustomize `images` (releasing/VERSION, set by tools/release.py — the reference's
 # releasing/update-manifests-images + releasing/version/VERSION)
@@ -260,14 +261,23 @@ def _agent_token_volume() -> dict:
 AGENT_TOKEN_MOUNT_SPEC = {"name": "node-agent-token", "mountPath": AGENT_TOKEN_MOUNT, "readOnly": True}
 
 
-def _workers_patches(workers: int) -> List[dict]:
+def _workers_patches(workers: int, webhook_replicas: int = 1) -> List[dict]:
     """``--workers`` for both managers, and the CPU to run them: one core per worker plus the
-    supervisor (which leads, aggregates /metrics and, in the odh manager, serves the webhook)."""
+    supervisor (which leads, aggregates /metrics and, in the odh manager, serves the webhook);
+    the odh manager's ``--webhook-replicas`` add a core each (webhook-only processes sharing the
+    webhook port)."""
     ops = [{"op": "add", "path": "/spec/template/spec/containers/0/args/-", "value": f"--workers={workers}"},
            {"op": "replace", "path": "/spec/template/spec/containers/0/resources/limits/cpu", "value": str(workers + 1)},
            {"op": "replace", "path": "/spec/template/spec/containers/0/resources/requests/cpu", "value": str(workers)}]
-    patch = yaml.safe_dump(ops, sort_keys=False)
-    return [{"target": {"kind": "Deployment", "name": f"{NAME_PREFIX}(deployment|manager)"}, "patch": patch}]
+    out = [{"target": {"kind": "Deployment", "name": f"{NAME_PREFIX}deployment"},
+            "patch": yaml.safe_dump(ops, sort_keys=False)}]
+    extra = max(0, webhook_replicas - 1)
+    odh = [*ops[:1], *([{"op": "add", "path": "/spec/template/spec/containers/0/args/-",
+                         "value": f"--webhook-replicas={webhook_replicas}"}] if extra else []),
+           {**ops[1], "value": str(workers + 1 + extra)}, {**ops[2], "value": str(workers + extra)}]
+    out.append({"target": {"kind": "Deployment", "name": f"{NAME_PREFIX}manager"},
+                "patch": yaml.safe_dump(odh, sort_keys=False)})
+    return out
 
 
 def kf_deployment() -> dict:
@@ -728,7 +738,7 @@ def tree(version: Optional[str] = None) -> Dict[str, object]:
     t["overlays/mi355x/kustomization.yaml"] = kustomization(["../../default", "../../webhook-certs"],
                                                             namespace="opendatahub", images=images,
                                                             configMapGenerator=mi355x_generators,
-                                                            patches=_workers_patches(MI355X_WORKERS))
+                                                            patches=_workers_patches(MI355X_WORKERS, MI355X_WEBHOOK_REPLICAS))
     # the serving cert covers every shard's Service; every shard's configuration gets the caBundle
     svc_names = [NAME_PREFIX + o["metadata"]["name"] for o in cp["services.yaml"][1:]]
     mwc_names = [NAME_PREFIX + o["metadata"]["name"] for o in cp["webhooks.yaml"]]

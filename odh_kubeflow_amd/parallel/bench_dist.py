@@ -167,11 +167,14 @@ def measure(args) -> Optional[dict]:
             out["config"]["architecture"] = "cmd/control_plane --shard r --controllers kf | odh,webhook (overlay mi355x-sharded)"
         else:
             w = max(1, getattr(args, "workers", 1))
-            wk = f" with --workers {w} (namespace-partitioned worker processes; the odh webhook on the supervisor)" \
+            r = max(1, getattr(args, "webhook_replicas", 1))
+            wk = (f" with --workers {w} (namespace-partitioned worker processes; the odh webhook on the supervisor"
+                  + (f" and {r - 1} webhook-only replica{'s' if r > 2 else ''}, one port" if r > 1 else "") + ")") \
                 if w > 1 else ""
             out["config"]["parallelism"] = (f"one kf manager + one odh manager Deployment for all {world} ranks' "
                                             f"notebooks{wk}, as config/overlays/mi355x deploys them")
-            out["config"]["architecture"] = (f"cmd/kf_manager + cmd/odh_manager{f' --workers {w}' if w > 1 else ''} "
+            out["config"]["architecture"] = (f"cmd/kf_manager + cmd/odh_manager{f' --workers {w}' if w > 1 else ''}"
+                                             f"{f' --webhook-replicas {r}' if w > 1 and r > 1 else ''} "
                                              f"(overlay mi355x, reference topology)")
         w = getattr(args, "platform_workers", 0) or (world + 1) // 2
         out["config"]["platform_stand_ins"] = (f"native C++ apiserver (+GC); ONE scheduler (first-free amd.com/gpu "
@@ -511,7 +514,8 @@ async def _main(args, dist, torch, rank: int, world: int, ndev: int, probe_sampl
         shard_count=world, assign_policy=getattr(args, "assign_policy", "hash"), shard=str(rank), arch=arch,
         launch=(arch == "sharded" or rank == 0), bootstrap=(rank == 0), odh=not args.no_odh,
         webhook=not args.no_odh, reference_emulation=args.reference_emulation, env=env, process=True,
-        split=not getattr(args, "single_process_shard", False), workers=max(1, getattr(args, "workers", 1))))
+        split=not getattr(args, "single_process_shard", False), workers=max(1, getattr(args, "workers", 1)),
+        webhook_replicas=max(1, getattr(args, "webhook_replicas", 1))))
     if rank == 0:
         await shard.start()  # cluster namespaces (and, unsharded, the managers + their webhook) first
         await _in_thread(dist.barrier)

@@ -66,6 +66,7 @@ class ShardConfig:
     process: bool = False  # run the control plane as its own process(es), as deployed
     split: bool = True  # sharded, process mode: kf and odh + webhook as two processes (the shard pod's two containers)
     workers: int = 1  # unsharded: --workers of the kf and odh managers (runtime/workers.py)
+    webhook_replicas: int = 1  # unsharded with workers: --webhook-replicas of the odh manager
     # the user namespaces this rank drives (default: just ``namespace``); with ``assign`` they
     # are created unlabelled and the shipped NamespaceShardAssigner (``--assign-namespaces``,
     # run by every shard's kf process) labels each ``crc32(name) % shard_count``
@@ -137,8 +138,10 @@ class ControlPlaneShard:
         wk = ["--workers", str(cfg.workers)] if cfg.workers > 1 else []
         out = [("kf_manager", "odh_kubeflow_amd.cmd.kf_manager", ["--probe-addr", "0", *wk], "--metrics-addr")]
         if cfg.odh:
+            rep = ["--webhook-replicas", str(cfg.webhook_replicas)] if cfg.workers > 1 and cfg.webhook_replicas > 1 \
+                else []
             out.append(("odh_manager", "odh_kubeflow_amd.cmd.odh_manager",
-                        [*wh, "--health-probe-bind-address", "0", *wk], "--metrics-bind-address"))
+                        [*wh, "--health-probe-bind-address", "0", *wk, *rep], "--metrics-bind-address"))
         return out
 
     def _cp_env(self) -> Dict[str, str]:
@@ -186,7 +189,7 @@ class ControlPlaneShard:
             pre = ["-m", "cProfile", "-o", f"{prof}.{name}.{self.shard or 'all'}"] if prof else []
             proc = await start_child(module, args, f"{name} (shard {self.shard})", env=env, python_args=pre)
             self.procs.append(_Proc(name, proc, mport))
-        if self.cfg.workers > 1:
+        if self.cfg.workers > 1:  # the managers' worker (and webhook replica) processes
             for p in self.procs:
                 d = await self._get_json(f"{p.base}/debug/reconciles")
                 for k, pid in (d.get("worker_pids") or {}).items():
@@ -337,7 +340,15 @@ class ControlPlaneShard:
         for p in self.procs:
             s0 = (since or {}).get(p.name) or {}
             q = f"since={s0.get('served', 0)}" + (f"&get_since={s0['gets']}" if "gets" in s0 else "")
+            reps = sorted(((int(k.rsplit("_", 1)[1]), v) for k, v in (since or {}).items()
+                           if k.startswith(f"{p.name}_webhook_replica_")))
+            if reps:
+                q += "&replica_since=" + ",".join(f"{v.get('served', 0)}:{v.get('gets', 0)}" for _i, v in reps)
             d = await self._get_json(f"{p.base}/debug/webhook?{q}")
+            for i, rd in (d.pop("replicas", None) or {}).items():  # --webhook-replicas children
+                name = f"{p.name}_webhook_replica_{i}"
+                if rd.get("served") or name in (since or {}):
+                    out[name] = rd
             if d.get("served") or p.name in (since or {}):
                 out[p.name] = d
         for i, mgr in enumerate(self.managers):

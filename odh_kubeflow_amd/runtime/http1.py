@@ -197,8 +197,9 @@ class Http1Server:
     """
 
     def __init__(self, handler, host: str = "127.0.0.1", port: int = 0,
-                 ssl_context: Optional[_ssl.SSLContext] = None, max_body: int = 16 << 20):
+                 ssl_context: Optional[_ssl.SSLContext] = None, max_body: int = 16 << 20, reuse_port: bool = False):
         self.handler = handler
+        self.reuse_port = reuse_port  # SO_REUSEPORT: several processes accept on one port
         self.host = host
         self.port = port
         self.ssl = ssl_context
@@ -207,7 +208,8 @@ class Http1Server:
         self._conns: set = set()
 
     async def start(self) -> "Http1Server":
-        self._server = await asyncio.start_server(self._serve, self.host, self.port, ssl=self.ssl, limit=1 << 24)
+        self._server = await asyncio.start_server(self._serve, self.host, self.port, ssl=self.ssl, limit=1 << 24,
+                                                  reuse_port=self.reuse_port or None)
         self.port = self._server.sockets[0].getsockname()[1]
         return self
 

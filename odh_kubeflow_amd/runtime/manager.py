@@ -69,6 +69,7 @@ class Manager:
         # (their /metrics and /debug answers are merged into this manager's), and, in a
         # worker, the filter that keeps its controllers to its namespace partition
         self.supervisor = None
+        self.webhook_replicas = None  # WorkerSupervisor of webhook-only children (odh --webhook-replicas)
         self.request_filter = None
 
     # ------------------------------------------------------------------ construction
@@ -270,6 +271,16 @@ class Manager:
         self.add(sup, needs_leader=True)
         self.healthz["workers"] = lambda: not self.elected or not self.elected.is_set() or sup.alive()
 
+    def add_webhook_replicas(self, sup) -> None:
+        """Run ``sup``'s webhook-only children on every replica (webhooks serve whether or not
+        this one leads); their health, metrics and debug answers join this one's."""
+        self.webhook_replicas = sup
+        self.add(sup, needs_leader=False)
+        self.healthz["webhook-replicas"] = sup.alive
+
+    def _children(self) -> list:
+        return [s for s in (self.supervisor, self.webhook_replicas) if s is not None]
+
     def io_counters(self) -> Dict[str, Dict[str, int]]:
         """What this process received and sent: watch events per kind, REST requests per verb."""
         cache = getattr(self, "cache", None) or self.reader
@@ -302,10 +313,11 @@ class Manager:
 
             async def metrics(_req):
                 body = generate_latest(self.registry)
-                if self.supervisor is not None:
+                if self._children():
                     from .workers import merge_metrics
 
-                    body = merge_metrics([body.decode(), *await self.supervisor.metrics_texts()]).encode()
+                    texts = [t for sup in self._children() for t in await sup.metrics_texts()]
+                    body = merge_metrics([body.decode(), *texts]).encode()
                 return web.Response(body=body, content_type="text/plain", charset="utf-8")
 
             app.router.add_get("/metrics", metrics)
@@ -339,11 +351,16 @@ class Manager:
 
         async def reconciles(_req):
             docs = await self.supervisor.debug("/debug/reconciles") if self.supervisor is not None else []
+            reps = self.webhook_replicas
+            rdocs = await reps.debug("/debug/reconciles") if reps is not None else []
+            pids = dict(self.supervisor.pids()) if self.supervisor is not None else {}
+            if reps is not None:
+                pids.update({f"webhook_replica_{k.rsplit('_', 1)[1]}": v for k, v in reps.pids().items()})
             return web.json_response({"reconciles": merge_counts([self.reconcile_breakdown(),
                                                                   *(d.get("reconciles") for d in docs)]),
-                                      "io": merge_counts([self.io_counters(), *(d.get("io") for d in docs)]),
+                                      "io": merge_counts([self.io_counters(), *(d.get("io") for d in docs + rdocs)]),
                                       "workers": len(docs),
-                                      "worker_pids": self.supervisor.pids() if self.supervisor is not None else {},
+                                      "worker_pids": pids,
                                       "assignments": {str(i): nss for i, nss in self.supervisor.assignments().items()}
                                       if self.supervisor is not None else {}})
 
@@ -374,8 +391,17 @@ class Manager:
             gsince = int(req.query.get("get_since", str(gets)))
             g = list(getattr(rest, "get_ms", ()))
             k = max(0, min(gets - gsince, len(g)))
-            return web.json_response({"served": srv.served, "handle_ms": [round(x * 1e3, 3) for x in recent],
-                                      "gets": gets, "get_ms": [round(x, 3) for x in g[len(g) - k:]] if k else []})
+            out = {"served": srv.served, "handle_ms": [round(x * 1e3, 3) for x in recent],
+                   "gets": gets, "get_ms": [round(x, 3) for x in g[len(g) - k:]] if k else []}
+            reps = self.webhook_replicas
+            if reps is not None:  # each replica's own window: replica_since=served:gets,served:gets,...
+                rs = [x.split(":") for x in req.query.get("replica_since", "").split(",") if x]
+
+                def path(i):
+                    s0, g0 = (rs[i] + ["0", "0"])[:2] if i < len(rs) else ("0", "0")
+                    return f"/debug/webhook?since={int(s0)}&get_since={int(g0)}"
+                out["replicas"] = {str(i): d for i, d in (await reps.debug_each(path)).items()}
+            return web.json_response(out)
 
         async def gc_pauses(req):
             from ..utils.gctune import PAUSES
@@ -385,6 +411,9 @@ class Manager:
             if self.supervisor is not None:  # the workers' own (each numbers its collections itself)
                 for i, d in (await self.supervisor.debug_by_worker("/debug/gc")).items():
                     out[f"worker_{i}"] = d.get("self") or {}
+            if self.webhook_replicas is not None:
+                for i, d in (await self.webhook_replicas.debug_by_worker("/debug/gc")).items():
+                    out[f"webhook_replica_{i}"] = d.get("self") or {}
             return web.json_response(out)
 
         app.router.add_get("/debug/webhook", webhook)

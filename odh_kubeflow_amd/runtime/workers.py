@@ -443,7 +443,11 @@ class WorkerSupervisor:
 
     async def debug_by_worker(self, path: str, timeout: float = 30.0) -> Dict[int, dict]:
         """worker index → its JSON answer (a worker restarting is missing)."""
-        docs = await asyncio.gather(*(self._get(w, path, timeout) for w in self.workers))
+        return await self.debug_each(lambda _i: path, timeout)
+
+    async def debug_each(self, path_for: Callable[[int], str], timeout: float = 30.0) -> Dict[int, dict]:
+        """worker index → its JSON answer to ``path_for(index)``."""
+        docs = await asyncio.gather(*(self._get(w, path_for(w.index), timeout) for w in self.workers))
         return {w.index: json.loads(d) for w, d in zip(self.workers, docs) if d}
 
 

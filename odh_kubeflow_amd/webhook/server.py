@@ -32,13 +32,14 @@ log = logging.getLogger("webhook.server")
 
 class WebhookServer:
     def __init__(self, webhook: NotebookWebhook, cert_dir: Optional[str], host: str = "0.0.0.0", port: int = 8443,
-                 path: str = WEBHOOK_PATH, reload_interval: float = 10.0):
+                 path: str = WEBHOOK_PATH, reload_interval: float = 10.0, reuse_port: bool = False):
         self.webhook = webhook
         self.cert_dir = cert_dir
         self.host = host
         self.port = port
         self.path = path
         self.reload_interval = reload_interval
+        self.reuse_port = reuse_port  # webhook replicas of one manager share the port (SO_REUSEPORT)
         self._server = None
         self._ctx: Optional[ssl.SSLContext] = None
         self._stamp: Optional[Tuple] = None
@@ -120,7 +121,8 @@ class WebhookServer:
 
     async def start(self) -> "WebhookServer":
         self._ctx = self.ssl_context()
-        self._server = await Http1Server(self._handle, self.host, self.port, self._ctx).start()
+        self._server = await Http1Server(self._handle, self.host, self.port, self._ctx,
+                                         reuse_port=self.reuse_port).start()
         self.port = self._server.port
         if self._ctx is not None and self.reload_interval > 0:
             self._watch = asyncio.ensure_future(self._watch_certs())

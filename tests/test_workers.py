@@ -132,6 +132,11 @@ def test_worker_command_lines_drop_what_only_the_supervisor_does():
     o = odh_manager.parse(["--kube-rbac-proxy-image", "img", "--workers=2", "--leader-elect", "--webhook-port", "9443"])
     argv = odh_manager.worker_argv(o, 0, "127.0.0.1:1")
     assert "--leader-elect" not in argv and "--workers=2" not in argv and argv[argv.index("--worker") + 1] == "0/2"
+    o = odh_manager.parse(["--kube-rbac-proxy-image", "img", "--workers=2", "--webhook-replicas", "3",
+                           "--leader-elect", "--webhook-port", "9443"])
+    argv = odh_manager.replica_argv(o, 1, "127.0.0.1:2")
+    assert argv[argv.index("--webhook-replica") + 1] == "1/2" and "--webhook-replicas" not in argv
+    assert "--leader-elect" not in argv and "--worker" not in argv and argv[argv.index("--webhook-port") + 1] == "9443"
     with pytest.raises(SystemExit):
         wk.parse_worker("3/3")
     assert wk.parse_worker("1/4") == (1, 4) and wk.parse_worker(None) is None
@@ -154,13 +159,15 @@ def test_managers_with_workers_serve_partitioned_namespaces(run):
         try:
             platform = await NodePlatform(native.url, process=False).start()
             drivers.append(await ControlPlaneShard(ShardConfig(
-                native.url, "team-0", arch="unsharded", bootstrap=True, env=env, process=True, workers=2)).start())
+                native.url, "team-0", arch="unsharded", bootstrap=True, env=env, process=True, workers=2,
+                webhook_replicas=2)).start())
             for i in (1, 2):
                 drivers.append(await ControlPlaneShard(ShardConfig(native.url, f"team-{i}", arch="unsharded",
                                                                    launch=False, env=env)).start())
             pids = drivers[0].control_plane_pids()
             assert sorted(k for k in pids if "worker" in k) == [
                 "kf_manager_worker_0", "kf_manager_worker_1", "odh_manager_worker_0", "odh_manager_worker_1"]
+            assert "odh_manager_webhook_replica_0" in pids  # --webhook-replicas 2: one webhook-only child
             ann = {"notebooks.opendatahub.io/inject-auth": "true"}
             for i, d in enumerate(drivers):
                 await d.admin.create(notebook("nb", f"team-{i}", image="img", gpus=1, annotations=ann))
@@ -178,6 +185,11 @@ def test_managers_with_workers_serve_partitioned_namespaces(run):
                 assert text.count("# TYPE controller_runtime_reconcile_total counter") == 1
                 assert 'controller_runtime_max_concurrent_reconciles{controller="odh-notebook-controller"} 16.0' \
                     in text
+            # the supervisor and its webhook replica, one port: between them every admission
+            # (the create and the odh unlock update) of the three notebooks was served
+            wt = await drivers[0].webhook_timings()
+            assert set(wt) <= {"odh_manager", "odh_manager_webhook_replica_0"}
+            assert sum(d["served"] for d in wt.values()) >= 3 * 2
             # a worker dies: it is restarted and given its namespaces again
             victim = pids["kf_manager_worker_1"]
             os.kill(victim, signal.SIGKILL)

@@ -12,7 +12,8 @@
 #   s20v300  interleaved A/B on one box: the driver's 20-step invocation vs the 300-step run, 3 rounds
 #   pyc      precompile the package's bytecode (compileall) before the steps that follow
 #   unsharded  the default topology (one kf + one odh manager process) at 1, 2 and 4 ranks
-#   workers  the same topology with --workers 4 (overlay mi355x): 1, 2 and 4 ranks
+#   workers  the same topology with --workers 4: 1, 2 and 4 ranks
+#   wr2      --workers 4 --webhook-replicas 2 (overlay mi355x): 1, 2 and 4 ranks
 #   burst64  64 notebooks at once into one unsharded control plane (--workers 1 and 4) and the sharded one
 #   fair     ours vs --reference-emulation: vanilla / OpenShift-like (pull secret after 200 ms), 0 / 2 ms writes
 #   pw4      4 ranks, --workers 4, one platform worker process per rank
@@ -127,6 +128,17 @@ for s in $steps; do
           --master-addr 127.0.0.1 --master-port 2995$n bench.py --gpus $n --arch unsharded --workers 4 --steps 100 \
           --warmup 5 --probe-sample 0 > "$out/bench_workers_n$n.log" 2>&1 || fail workers $? "$out/bench_workers_n$n.log"
         show "$out/bench_workers_n$n.log" "workers4 n$n"
+      done ;;
+    wr2)
+      timeout -k 10 170 python bench.py --gpus 1 --arch unsharded --workers 4 --webhook-replicas 2 --steps 100 \
+        --warmup 5 --probe-sample 0 > "$out/bench_wr2_n1.log" 2>&1 || fail wr2 $? "$out/bench_wr2_n1.log"
+      show "$out/bench_wr2_n1.log" "workers4 wr2 n1"
+      for n in 2 4; do
+        timeout -k 10 170 python -m torch.distributed.run --nnodes=1 --nproc-per-node $n \
+          --master-addr 127.0.0.1 --master-port 2996$n bench.py --gpus $n --arch unsharded --workers 4 \
+          --webhook-replicas 2 --steps 100 --warmup 5 --probe-sample 0 > "$out/bench_wr2_n$n.log" 2>&1 \
+          || fail wr2 $? "$out/bench_wr2_n$n.log"
+        show "$out/bench_wr2_n$n.log" "workers4 wr2 n$n"
       done ;;
     fair)
       # the reference's behaviour vs ours in two regimes — vanilla Kubernetes (nothing ever adds

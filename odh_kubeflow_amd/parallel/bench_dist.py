@@ -681,7 +681,7 @@ async def _drive(args, shard, dist, torch, children: Optional[dict] = None, nati
     io = io_delta(io0, await shard.io_counters())
     # who served which namespace: the shard labels (sharded, assigned) or the supervisors'
     # worker assignment (unsharded --workers; rank 0 launched the managers)
-    owner = dict(getattr(shard, "labels", None) or {})
+    owner = dict(shard.labels)
     if not owner and shard.cfg.arch != "sharded" and shard.cfg.launch and shard.cfg.workers > 1:
         for _proc, a in (await shard.worker_assignments()).items():
             for idx, names in a.items():

@@ -102,6 +102,7 @@ class ControlPlaneShard:
         self._certs = None
         self._http = None
         self.worker_pids: Dict[str, int] = {}  # --workers: the managers' worker processes
+        self.labels: Dict[str, str] = {}  # assign: namespace → the shard label it was given
 
     # ------------------------------------------------------------------ build
 

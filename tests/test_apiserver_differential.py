@@ -232,3 +232,29 @@ def test_selector_filtered_watch_survives_history_rollover(run):
             await c.close()
             await nat.stop()
     run(go(), timeout=60)
+
+
+def test_native_metrics_document_is_complete_json(run):
+    """GET /metrics of the native apiserver: one JSON document with the request profile, the
+    write path's CPU by phase and the per-resource store-lock contention (the benchmark's
+    ``apiserver_profile_per_step``), whatever the counters' magnitudes."""
+    async def go():
+        nat = await native.NativeApiServer().start()
+        c = RestClient(RestConfig(host=nat.url))
+        try:
+            await c.create({"apiVersion": "v1", "kind": "Namespace", "metadata": {"name": "m"}})
+            for i in range(5):
+                await c.create({"apiVersion": "v1", "kind": "ConfigMap", "metadata": {"name": f"c{i}", "namespace": "m"}})
+                await c.patch("v1/ConfigMap", {"data": {"k": str(i)}}, name=f"c{i}", namespace="m")
+            st = await nat.stats()
+        finally:
+            await c.close()
+            await nat.stop()
+        assert st["writes"] >= 11 and st["prof"]["patch_calls"] == 5
+        for k in ("webhook_dials", "webhook_dial_ns", "trims", "lock_wait_ns", "admit_wall_ns"):
+            assert k in st["prof"], k
+        assert set(st["phases"]) == {f"{p}_cpu_ns" for p in ("parse", "admit", "validate", "defaults", "patch",
+                                                             "prepare", "dump")}
+        assert st["phases"]["parse_cpu_ns"] > 0 and st["phases"]["patch_cpu_ns"] > 0
+        assert isinstance(st["locks"], dict)
+    run(go(), timeout=60)

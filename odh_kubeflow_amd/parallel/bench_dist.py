@@ -172,10 +172,11 @@ def measure(args) -> Optional[dict]:
                   + (f" and {r - 1} webhook-only replica{'s' if r > 2 else ''}, one port" if r > 1 else "") + ")") \
                 if w > 1 else ""
             out["config"]["parallelism"] = (f"one kf manager + one odh manager Deployment for all {world} ranks' "
-                                            f"notebooks{wk}, as config/overlays/mi355x deploys them")
+                                            f"notebooks{wk}")
+            overlay = "overlay mi355x" if (w, r) == (4, 2) else \
+                "reference topology; overlay mi355x runs --workers 4 --webhook-replicas 2"
             out["config"]["architecture"] = (f"cmd/kf_manager + cmd/odh_manager{f' --workers {w}' if w > 1 else ''}"
-                                             f"{f' --webhook-replicas {r}' if w > 1 and r > 1 else ''} "
-                                             f"(overlay mi355x, reference topology)")
+                                             f"{f' --webhook-replicas {r}' if w > 1 and r > 1 else ''} ({overlay})")
         w = getattr(args, "platform_workers", 0) or (world + 1) // 2
         out["config"]["platform_stand_ins"] = (f"native C++ apiserver (+GC); ONE scheduler (first-free amd.com/gpu "
                                                f"allocation); the node's StatefulSet controller and kubelet for its "

@@ -91,7 +91,10 @@ MI355X_CULLER = ["CULLING_ACTIVITY_SOURCE=combined", "ENABLE_CULLING=true"]
 # processes (runtime/workers.py; the odh webhook stays on the supervisor's own event loop) —
 # one core per worker, so an 8-GPU node's notebooks are not serialised on one Python loop
 MI355X_WORKERS = 4
-MI355X_WEBHOOK_REPLICAS = 2
+# --webhook-replicas: measured at 4 streams on the box, a second webhook process left
+# notebooks/s unchanged (570 vs 572, profiles/r4_p9) — admissions were not the limit there;
+# raise it where admission load outgrows one core
+MI355X_WEBHOOK_REPLICAS = 1
 # the base manifests carry the development tag; every overlay pins the release tag through
 # kustomize `images` (releasing/VERSION, set by tools/release.py — the reference's
 # releasing/update-manifests-images + releasing/version/VERSION)

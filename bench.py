@@ -67,6 +67,9 @@ def parse(argv=None):
                         "deployed kf / odh+webhook pair (A/B measurements)")
     p.add_argument("--workers", type=int, default=1,
                    help="unsharded: --workers of the kf and odh managers (namespace-partitioned worker processes)")
+    p.add_argument("--webhook-process", action="store_true",
+                   help="sharded: each shard's webhook in a process of its own (kf | odh | webhook) instead of "
+                        "sharing the odh process (A/B measurements)")
     p.add_argument("--webhook-replicas", type=int, default=1,
                    help="unsharded with --workers: --webhook-replicas of the odh manager (webhook processes sharing "
                         "the port)")

@@ -516,7 +516,8 @@ async def _main(args, dist, torch, rank: int, world: int, ndev: int, probe_sampl
         launch=(arch == "sharded" or rank == 0), bootstrap=(rank == 0), odh=not args.no_odh,
         webhook=not args.no_odh, reference_emulation=args.reference_emulation, env=env, process=True,
         split=not getattr(args, "single_process_shard", False), workers=max(1, getattr(args, "workers", 1)),
-        webhook_replicas=max(1, getattr(args, "webhook_replicas", 1))))
+        webhook_replicas=max(1, getattr(args, "webhook_replicas", 1)),
+        webhook_process=getattr(args, "webhook_process", False)))
     if rank == 0:
         await shard.start()  # cluster namespaces (and, unsharded, the managers + their webhook) first
         await _in_thread(dist.barrier)

@@ -65,6 +65,7 @@ class ShardConfig:
     kube_rbac_proxy_image: str = "quay.io/brancz/kube-rbac-proxy:v0.18.1"
     process: bool = False  # run the control plane as its own process(es), as deployed
     split: bool = True  # sharded, process mode: kf and odh + webhook as two processes (the shard pod's two containers)
+    webhook_process: bool = False  # sharded, split: the webhook in a third process of its own (kf | odh | webhook)
     workers: int = 1  # unsharded: --workers of the kf and odh managers (runtime/workers.py)
     webhook_replicas: int = 1  # unsharded with workers: --webhook-replicas of the odh manager
     # the user namespaces this rank drives (default: just ``namespace``); with ``assign`` they
@@ -120,7 +121,10 @@ class ControlPlaneShard:
             # kf process and an odh + webhook process (cmd/control_plane.py docstring)
             sets = [["kf"]]
             if cfg.odh:
-                sets.append(["odh"] + (["webhook"] if cfg.webhook else []))
+                if cfg.webhook and cfg.webhook_process:
+                    sets += [["odh"], ["webhook"]]
+                else:
+                    sets.append(["odh"] + (["webhook"] if cfg.webhook else []))
             if not (cfg.split if split is None else split):
                 sets = [[c for cs in sets for c in cs]]
             out = []

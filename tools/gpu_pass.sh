@@ -13,7 +13,8 @@
 #   pyc      precompile the package's bytecode (compileall) before the steps that follow
 #   unsharded  the default topology (one kf + one odh manager process) at 1, 2 and 4 ranks
 #   workers  the same topology with --workers 4: 1, 2 and 4 ranks
-#   wr2      --workers 4 --webhook-replicas 2 (overlay mi355x): 1, 2 and 4 ranks
+#   wr2      --workers 4 --webhook-replicas 2: 1, 2 and 4 ranks
+#   wpab     sharded: the webhook in the odh process (deployed) vs a process of its own, interleaved, 1 and 4 ranks
 #   burst64  64 notebooks at once into one unsharded control plane (--workers 1 and 4) and the sharded one
 #   fair     ours vs --reference-emulation: vanilla / OpenShift-like (pull secret after 200 ms), 0 / 2 ms writes
 #   pw4      4 ranks, --workers 4, one platform worker process per rank
@@ -139,6 +140,19 @@ for s in $steps; do
           --webhook-replicas 2 --steps 100 --warmup 5 --probe-sample 0 > "$out/bench_wr2_n$n.log" 2>&1 \
           || fail wr2 $? "$out/bench_wr2_n$n.log"
         show "$out/bench_wr2_n$n.log" "workers4 wr2 n$n"
+      done ;;
+    wpab)
+      for r in 1 2; do
+        for v in shared own; do
+          case $v in own) f="--webhook-process" ;; *) f="" ;; esac
+          timeout -k 10 170 python bench.py --gpus 1 $f --steps 100 --warmup 5 --probe-sample 0 --no-configs \
+            --no-inprocess-baseline > "$out/bench_wp_${v}_n1_r$r.log" 2>&1 || fail wpab $? "$out/bench_wp_${v}_n1_r$r.log"
+          show "$out/bench_wp_${v}_n1_r$r.log" "webhook $v n1 r$r"
+          timeout -k 10 200 python -m torch.distributed.run --nnodes=1 --nproc-per-node 4 \
+            --master-addr 127.0.0.1 --master-port 29984 bench.py --gpus 4 $f --steps 100 --warmup 5 --probe-sample 0 \
+            > "$out/bench_wp_${v}_n4_r$r.log" 2>&1 || fail wpab $? "$out/bench_wp_${v}_n4_r$r.log"
+          show "$out/bench_wp_${v}_n4_r$r.log" "webhook $v n4 r$r"
+        done
       done ;;
     fair)
       # the reference's behaviour vs ours in two regimes — vanilla Kubernetes (nothing ever adds

@@ -64,12 +64,12 @@ def parse(argv=None):
                    help="N=1 auto: skip the extra in-process (envtest-style) measurement")
     p.add_argument("--single-process-shard", action="store_true",
                    help="sharded: each shard as ONE control-plane process (kf + odh + webhook) instead of the "
-                        "deployed kf / odh+webhook pair (A/B measurements)")
+                        "deployed kf | odh | webhook processes (A/B measurements)")
     p.add_argument("--workers", type=int, default=1,
                    help="unsharded: --workers of the kf and odh managers (namespace-partitioned worker processes)")
-    p.add_argument("--webhook-process", action="store_true",
-                   help="sharded: each shard's webhook in a process of its own (kf | odh | webhook) instead of "
-                        "sharing the odh process (A/B measurements)")
+    p.add_argument("--webhook-in-odh", action="store_true",
+                   help="sharded: each shard's webhook in its odh process (round 3-4's shard pod) instead of a "
+                        "process of its own (A/B measurements)")
     p.add_argument("--webhook-replicas", type=int, default=1,
                    help="unsharded with --workers: --webhook-replicas of the odh manager (webhook processes sharing "
                         "the port)")

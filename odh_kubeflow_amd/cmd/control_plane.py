@@ -14,12 +14,16 @@ cluster's notebooks with constant per-shard watch traffic.  The ``mi355x-sharded
 overlay runs it as a StatefulSet (``--shard=ordinal``: replica k is shard k, one per
 MI355X of an 8-GPU node) with one MutatingWebhookConfiguration and Service per shard;
 the headline benchmark (``bench.py`` → ``parallel/bench_dist.py``) launches exactly
-these processes, per rank.  A shard's pod runs the command twice, split by
+these processes, per rank.  A shard's pod runs the command three times, split by
 ``--controllers``: ``kf`` (notebook reconciler, event re-emitter, culler, namespace
-assigner) and ``odh,webhook`` — two event loops, so the odh pipeline and admissions never
-queue behind the kf reconciles on one core (measured at N=1 on one box, interleaved: the
-two-process layout 252/268/257 notebooks/s vs 240/253/241 for one process,
-``profiles/r3_p13``).  Each set has its own leader-election lease.
+assigner), ``odh`` and ``webhook`` — three event loops, so the odh pipeline never queues
+behind the kf reconciles, nor an admission behind either (measured on one box, interleaved:
+two processes against one, 252/268/257 vs 240/253/241 notebooks/s at N=1,
+``profiles/r3_p13``; the webhook in its own process against sharing the odh one, 64
+notebooks at once at 4 ranks: 1706/1651 vs 1446/1396 notebooks/s, AdmissionReview p99
+1.2–1.7 vs 3.4–5.4 ms, the closed loop unchanged, ``profiles/r4_p11``).  Each reconciling
+set has its own leader-election lease; a webhook-only process leads nothing (every replica
+admits).
 
 Flags are the union of the two reference managers' (odh spellings:
 ``--metrics-bind-address``, ``--health-probe-bind-address``, ``--leader-elect``,
@@ -120,7 +124,8 @@ def build(args, env=os.environ):
     elector = None
     # a subset of the controllers (a shard pod's kf / odh containers) leads on its own lease
     subset = "" if set(args.controller_set) == set(ALL_CONTROLLERS) else "-" + "-".join(sorted(args.controller_set))
-    if args.leader_elect:
+    # a webhook-only process leads nothing: admissions are served by every replica
+    if args.leader_elect and set(args.controller_set) != {"webhook"}:
         lease = "notebook-control-plane" + (f"-shard-{shard}" if shard is not None else "") + subset
         elector = LeaderElector(RestClient(cfg), lease, args.leader_election_namespace or namespace,
                                 lease_duration=args.leader_election_lease_duration,

@@ -528,27 +528,37 @@ def control_plane_role() -> dict:
 
 
 def control_plane_statefulset(shards: int) -> dict:
-    """One replica per shard; its pod runs ``cmd/control_plane.py`` twice, split by
-    ``--controllers``: ``kf`` (+ the namespace assigner) and ``odh,webhook`` — two event loops,
-    so admissions and the odh pipeline never wait behind kf reconciles (cmd/control_plane.py)."""
+    """One replica per shard; its pod runs ``cmd/control_plane.py`` three times, split by
+    ``--controllers``: ``kf`` (+ the namespace assigner), ``odh`` and ``webhook`` — three event
+    loops, so an admission never waits behind a reconcile and the odh pipeline never behind kf
+    (cmd/control_plane.py; the webhook's own process: ``profiles/r4_p11``)."""
     common = ["--shard=ordinal", "--leader-elect", "--kube-rbac-proxy-image=$(KUBE_RBAC_PROXY_IMAGE)"]
     kf = _control_plane_container("manager-kf", common + ["--controllers=kf", f"--shard-count={shards}",
                                                           "--assign-namespaces", "--assign-policy=balanced"],
-                                  8080, 8081, webhook=False)
+                                  8080, 8081, role="kf")
     odh = _control_plane_container("manager-odh", common + [
-        "--controllers=odh,webhook", "--metrics-bind-address=:8082", "--health-probe-bind-address=:8083",
-        "--webhook-cert-dir=/tmp/k8s-webhook-server/serving-certs", "--webhook-port=8443"], 8082, 8083, webhook=True)
+        "--controllers=odh", "--metrics-bind-address=:8082", "--health-probe-bind-address=:8083"], 8082, 8083,
+        role="odh")
+    wh = _control_plane_container("manager-webhook", common + [
+        "--controllers=webhook", "--metrics-bind-address=:8084", "--health-probe-bind-address=:8085",
+        "--webhook-cert-dir=/tmp/k8s-webhook-server/serving-certs", "--webhook-port=8443"], 8084, 8085,
+        role="webhook")
     labels = {"app": "notebook-control-plane"}
     return {"apiVersion": "apps/v1", "kind": "StatefulSet", "metadata": {"name": "control-plane", "labels": labels},
             "spec": {"replicas": shards, "serviceName": "control-plane", "podManagementPolicy": "Parallel",
                      "selector": {"matchLabels": labels},
                      "template": {"metadata": {"labels": labels},
-                                  "spec": {"serviceAccountName": "control-plane", "containers": [kf, odh],
+                                  "spec": {"serviceAccountName": "control-plane", "containers": [kf, odh, wh],
                                            "volumes": [_cert_volume(), _agent_token_volume(),
                                                        _agent_ca_volume()]}}}}
 
 
-def _control_plane_container(name: str, args: list, metrics: int, probes: int, webhook: bool) -> dict:
+_CP_PORT_NAMES = {"kf": ("metrics", "probes"), "odh": ("metrics-odh", "probes-odh"),
+                  "webhook": ("metrics-wh", "probes-wh")}
+
+
+def _control_plane_container(name: str, args: list, metrics: int, probes: int, role: str) -> dict:
+    mname, pname = _CP_PORT_NAMES[role]
     c = {"name": name, "image": MANAGER_IMAGE,
          "command": ["python", "-m", "odh_kubeflow_amd.cmd.control_plane"],
          "args": args,
@@ -560,13 +570,13 @@ def _control_plane_container(name: str, args: list, metrics: int, probes: int, w
                  {"name": "INJECT_CLUSTER_PROXY_ENV", "valueFrom": {"configMapKeyRef": {
                      "name": "notebook-controller-setting-config", "key": "INJECT_CLUSTER_PROXY_ENV",
                      "optional": True}}}] + _culler_env(),
-         "ports": ([{"name": "webhook", "containerPort": 8443}] if webhook else []) + [
-             {"name": "metrics" if not webhook else "metrics-odh", "containerPort": metrics},
-             {"name": "probes" if not webhook else "probes-odh", "containerPort": probes}],
+         "ports": ([{"name": "webhook", "containerPort": 8443}] if role == "webhook" else []) + [
+             {"name": mname, "containerPort": metrics}, {"name": pname, "containerPort": probes}],
          "resources": {"requests": {"cpu": "500m", "memory": "256Mi"}, "limits": {"cpu": "2", "memory": "2Gi"}},
-         # the kf container reads the node agents' token (GPU-busy culling); the odh one serves the webhook
-         "volumeMounts": ([{"name": "cert", "mountPath": "/tmp/k8s-webhook-server/serving-certs", "readOnly": True}]
-                          if webhook else [dict(AGENT_TOKEN_MOUNT_SPEC), dict(AGENT_CA_MOUNT_SPEC)]),
+         # the kf container reads the node agents' token (GPU-busy culling); the webhook one serves TLS
+         "volumeMounts": {"kf": [dict(AGENT_TOKEN_MOUNT_SPEC), dict(AGENT_CA_MOUNT_SPEC)], "odh": [],
+                          "webhook": [{"name": "cert", "mountPath": "/tmp/k8s-webhook-server/serving-certs",
+                                       "readOnly": True}]}[role],
          "securityContext": dict(RESTRICTED), **_probes(probes)}
     return c
 
@@ -610,7 +620,8 @@ def control_plane_docs(shards: int, prefix: str = NAME_PREFIX) -> Dict[str, obje
         "services.yaml": [{"apiVersion": "v1", "kind": "Service", "metadata": {"name": "control-plane"},
                            "spec": {"clusterIP": "None", "selector": {"app": "notebook-control-plane"},
                                     "ports": [{"name": "metrics", "port": 8080, "targetPort": 8080},
-                                              {"name": "metrics-odh", "port": 8082, "targetPort": 8082}]}}] + svcs,
+                                              {"name": "metrics-odh", "port": 8082, "targetPort": 8082},
+                                              {"name": "metrics-wh", "port": 8084, "targetPort": 8084}]}}] + svcs,
         "webhooks.yaml": mwcs,
     }
 

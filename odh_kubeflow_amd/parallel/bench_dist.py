@@ -160,11 +160,17 @@ def measure(args) -> Optional[dict]:
                                             f"--shard r` process per MI355X rank (kf + odh reconcilers + odh webhook); "
                                             f"A/B variant of config/overlays/mi355x-sharded")
             out["config"]["architecture"] = "cmd/control_plane --shard, one process per shard (A/B variant)"
+        elif arch == "sharded" and getattr(args, "webhook_in_odh", False):
+            out["config"]["parallelism"] = (f"namespace-sharded control plane x{world}: per MI355X rank "
+                                            f"`cmd/control_plane.py --shard r` as a kf process and an odh reconciler + "
+                                            f"odh webhook process (A/B variant of config/overlays/mi355x-sharded)")
+            out["config"]["architecture"] = "cmd/control_plane --shard r --controllers kf | odh,webhook (A/B variant)"
         elif arch == "sharded":
             out["config"]["parallelism"] = (f"namespace-sharded control plane x{world}: per MI355X rank the shard pod "
                                             f"of config/overlays/mi355x-sharded, `cmd/control_plane.py --shard r` as a "
-                                            f"kf process and an odh reconciler + odh webhook process")
-            out["config"]["architecture"] = "cmd/control_plane --shard r --controllers kf | odh,webhook (overlay mi355x-sharded)"
+                                            f"kf process, an odh reconciler process and an odh webhook process")
+            out["config"]["architecture"] = ("cmd/control_plane --shard r --controllers kf | odh | webhook "
+                                             "(overlay mi355x-sharded)")
         else:
             w = max(1, getattr(args, "workers", 1))
             r = max(1, getattr(args, "webhook_replicas", 1))
@@ -517,7 +523,7 @@ async def _main(args, dist, torch, rank: int, world: int, ndev: int, probe_sampl
         webhook=not args.no_odh, reference_emulation=args.reference_emulation, env=env, process=True,
         split=not getattr(args, "single_process_shard", False), workers=max(1, getattr(args, "workers", 1)),
         webhook_replicas=max(1, getattr(args, "webhook_replicas", 1)),
-        webhook_process=getattr(args, "webhook_process", False)))
+        webhook_process=not getattr(args, "webhook_in_odh", False)))
     if rank == 0:
         await shard.start()  # cluster namespaces (and, unsharded, the managers + their webhook) first
         await _in_thread(dist.barrier)

@@ -5,9 +5,9 @@ whole cluster (``kf/main.go:87-98``, ``odh/main.go:155-192``; one worker each). 
 deployable topologies are measured, both exactly as the manifests run them:
 
 * ``arch="sharded"`` (``config/overlays/mi355x-sharded``) — every rank r starts its shard
-  pod's two processes, ``python -m odh_kubeflow_amd.cmd.control_plane --shard r
-  --controllers kf`` (kf reconciler + event re-emitter) and ``… --controllers odh,webhook``
-  (odh reconciler and the odh mutating webhook), each with an informer cache over the
+  pod's three processes, ``python -m odh_kubeflow_amd.cmd.control_plane --shard r
+  --controllers kf`` (kf reconciler + event re-emitter), ``… --controllers odh`` (odh
+  reconciler) and ``… --controllers webhook`` (the odh mutating webhook), each with an informer cache over the
   namespaces labelled ``notebooks.amd.com/shard=r``, the webhook registered by its shard's
   MutatingWebhookConfiguration with a ``namespaceSelector`` on that label (``split=False``:
   one process with all three);
@@ -64,8 +64,8 @@ class ShardConfig:
     env: Dict[str, str] = field(default_factory=dict)
     kube_rbac_proxy_image: str = "quay.io/brancz/kube-rbac-proxy:v0.18.1"
     process: bool = False  # run the control plane as its own process(es), as deployed
-    split: bool = True  # sharded, process mode: kf and odh + webhook as two processes (the shard pod's two containers)
-    webhook_process: bool = False  # sharded, split: the webhook in a third process of its own (kf | odh | webhook)
+    split: bool = True  # sharded, process mode: the shard pod's containers as processes (kf | odh | webhook)
+    webhook_process: bool = True  # sharded, split: the webhook in a process of its own (False: odh + webhook)
     workers: int = 1  # unsharded: --workers of the kf and odh managers (runtime/workers.py)
     webhook_replicas: int = 1  # unsharded with workers: --webhook-replicas of the odh manager
     # the user namespaces this rank drives (default: just ``namespace``); with ``assign`` they
@@ -118,7 +118,7 @@ class ControlPlaneShard:
               "--webhook-host", "127.0.0.1", "--webhook-port", str(webhook_port)]
         if cfg.arch == "sharded":
             # the shard pod of config/overlays/mi355x-sharded: the control plane split into a
-            # kf process and an odh + webhook process (cmd/control_plane.py docstring)
+            # kf process, an odh process and a webhook process (cmd/control_plane.py docstring)
             sets = [["kf"]]
             if cfg.odh:
                 if cfg.webhook and cfg.webhook_process:

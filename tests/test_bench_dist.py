@@ -38,8 +38,8 @@ def test_bench_two_ranks_gloo():
     cpu = d["cpu_ms_per_step"]
     assert len(cpu["ranks"]) == 2 and all(x > 0 for x in cpu["ranks"])
     assert cpu["apiserver"] >= 0 and cpu["scheduler"] >= 0  # rank 0's child processes
-    # each rank's shard pod, as deployed: a kf process and an odh + webhook process
-    assert {f"control_plane_{p}_{r}" for p in ("kf", "odh") for r in (0, 1)} <= set(cpu), cpu
+    # each rank's shard pod, as deployed: a kf, an odh and a webhook process
+    assert {f"control_plane_{p}_{r}" for p in ("kf", "odh", "webhook") for r in (0, 1)} <= set(cpu), cpu
     if "apiserver_profile_per_step" in d:  # native apiserver built: write calls per notebook, by verb
         w = d["writes_per_notebook"]
         assert w["total"] == pytest.approx(w["create"] + w["update"] + w["patch"] + w["delete"], abs=0.05)
@@ -123,7 +123,8 @@ def test_bench_namespaces_per_rank_assigned_by_the_shard_hash():
     assert sum(v["notebooks"] for v in load["shards"].values()) == 16
     for k, v in load["shards"].items():
         if v["notebooks"]:
-            assert set(v["cpu_ms_per_notebook"]) == {f"control_plane_kf_{k}", f"control_plane_odh_{k}"}
+            assert set(v["cpu_ms_per_notebook"]) == {f"control_plane_kf_{k}", f"control_plane_odh_{k}",
+                                                     f"control_plane_webhook_{k}"}
 
 
 def test_shard_load_report():

@@ -245,15 +245,19 @@ def test_sharded_overlay_shape():
     (sts,) = _by(objs, "StatefulSet").values()
     n = sts["spec"]["replicas"]
     assert n == manifests.SHARDS == 8
-    # the shard pod: the control plane split into a kf and an odh + webhook process
-    kf, odh = sts["spec"]["template"]["spec"]["containers"]
+    # the shard pod: the control plane split into a kf, an odh and a webhook process
+    kf, odh, wh = sts["spec"]["template"]["spec"]["containers"]
     assert "--shard=ordinal" in kf["args"] and f"--shard-count={n}" in kf["args"] and "--assign-namespaces" in kf["args"]
-    assert "--controllers=kf" in kf["args"] and "--controllers=odh,webhook" in odh["args"]
-    assert "--shard=ordinal" in odh["args"] and "--assign-namespaces" not in odh["args"]
-    assert [p["containerPort"] for p in odh["ports"]] == [8443, 8082, 8083]
+    assert "--controllers=kf" in kf["args"] and "--controllers=odh" in odh["args"]
+    assert "--controllers=webhook" in wh["args"]
+    for c in (odh, wh):
+        assert "--shard=ordinal" in c["args"] and "--assign-namespaces" not in c["args"]
     assert [p["containerPort"] for p in kf["ports"]] == [8080, 8081]
-    assert odh["readinessProbe"]["httpGet"]["port"] == 8083 and kf["readinessProbe"]["httpGet"]["port"] == 8081
-    assert [v["name"] for v in odh["volumeMounts"]] == ["cert"]
+    assert [p["containerPort"] for p in odh["ports"]] == [8082, 8083]
+    assert [p["containerPort"] for p in wh["ports"]] == [8443, 8084, 8085]
+    assert len({p["name"] for c in (kf, odh, wh) for p in c["ports"]}) == 7  # pod-unique port names
+    assert [c["readinessProbe"]["httpGet"]["port"] for c in (kf, odh, wh)] == [8081, 8083, 8085]
+    assert [v["name"] for v in wh["volumeMounts"]] == ["cert"] and odh["volumeMounts"] == []
     svcs = _by(objs, "Service")
     mwcs = _by(objs, "MutatingWebhookConfiguration")
     assert len(mwcs) == n + 1

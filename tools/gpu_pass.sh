@@ -14,7 +14,7 @@
 #   unsharded  the default topology (one kf + one odh manager process) at 1, 2 and 4 ranks
 #   workers  the same topology with --workers 4: 1, 2 and 4 ranks
 #   wr2      --workers 4 --webhook-replicas 2: 1, 2 and 4 ranks
-#   wpab     sharded: the webhook in the odh process (deployed) vs a process of its own, interleaved, 1 and 4 ranks
+#   wpab     sharded: the webhook in the odh process vs a process of its own (deployed), interleaved, 1 and 4 ranks
 #   burst64  64 notebooks at once into one unsharded control plane (--workers 1 and 4) and the sharded one
 #   fair     ours vs --reference-emulation: vanilla / OpenShift-like (pull secret after 200 ms), 0 / 2 ms writes
 #   pw4      4 ranks, --workers 4, one platform worker process per rank
@@ -144,7 +144,7 @@ for s in $steps; do
     wpab)
       for r in 1 2; do
         for v in shared own; do
-          case $v in own) f="--webhook-process" ;; *) f="" ;; esac
+          case $v in shared) f="--webhook-in-odh" ;; *) f="" ;; esac
           timeout -k 10 170 python bench.py --gpus 1 $f --steps 100 --warmup 5 --probe-sample 0 --no-configs \
             --no-inprocess-baseline > "$out/bench_wp_${v}_n1_r$r.log" 2>&1 || fail wpab $? "$out/bench_wp_${v}_n1_r$r.log"
           show "$out/bench_wp_${v}_n1_r$r.log" "webhook $v n1 r$r"

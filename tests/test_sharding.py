@@ -706,3 +706,25 @@ def test_terminating_namespace_stays_in_the_shard_cache(run):
             await c.close()
             await srv.stop()
     run(go())
+
+
+def test_webhook_only_control_plane_takes_no_lease(tmp_path):
+    """The shard pod's webhook container (``--controllers=webhook --leader-elect``) admits on
+    every replica: it builds no leader elector and no reconciler, while the kf and odh
+    containers of the same pod each lead on a lease of their own."""
+    from odh_kubeflow_amd.cmd import control_plane
+    from odh_kubeflow_amd.webhook.certs import generate
+
+    certs = generate(("127.0.0.1",), str(tmp_path / "tls"))
+    env = {"K8S_NAMESPACE": "opendatahub"}
+    common = ["--master", "http://127.0.0.1:1", "--shard", "0", "--leader-elect", "--kube-rbac-proxy-image", "img",
+              "--webhook-cert-dir", certs.cert_dir, "--metrics-bind-address", "0", "--health-probe-bind-address", "0"]
+    wh = control_plane.build(control_plane.parse(common + ["--controllers", "webhook"]), env)
+    assert wh.leader_elector is None and wh.webhook_server is not None
+    assert not getattr(wh, "odh_reconciler", None) and not getattr(wh, "kf_reconcilers", None)
+    leases = set()
+    for cs in ("kf", "odh"):
+        mgr = control_plane.build(control_plane.parse(common + ["--controllers", cs]), env)
+        assert mgr.leader_elector is not None and mgr.webhook_server is None
+        leases.add(mgr.leader_elector.name)
+    assert len(leases) == 2

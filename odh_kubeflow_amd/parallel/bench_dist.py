@@ -219,7 +219,7 @@ def measure(args) -> Optional[dict]:
 
 def probe_report(samples: list, p50_off: Optional[float]) -> dict:
     """create→Ready of the probe notebooks, and the probe's own verdict per notebook."""
-    lat = [s["ready_ms"] for s in samples]
+    lat = [s["ready_ms"] for s in samples if s.get("ready_ms") is not None]
     res = [s.get("result") or {} for s in samples]
     tim = [r.get("timings_ms") or {} for r in res]
     dev = [(r.get("results") or [{}])[0] for r in res]
@@ -287,14 +287,25 @@ async def _burst(args, shard, dist, native, children: dict, use_odh: bool, tag: 
     ann = {"notebooks.opendatahub.io/inject-auth": "true"} if use_odh else None
     res = {"cpu": "500m", "memory": "1Gi"}
     gpus = 1 if total <= NODE_GPUS else 0  # up to one per MI355X of the node: GPU notebooks (config #3)
-    await shard.quiesce()
+    # untimed and after the headline: a failure here is reported in the block, never raised —
+    # every rank still reaches every collective below, so no rank is left waiting at one
+    errors: list = []
+
+    async def safe(aw, default=None):
+        try:
+            return await aw
+        except Exception as e:  # noqa: BLE001 — recorded in the burst block
+            errors.append(f"rank {rank}: {e!r}"[:300])
+            return default
+
+    await safe(shard.quiesce())
     await _in_thread(dist.barrier)
-    adm0 = (await native.admissions(1 << 62))["seq"] if native is not None else None
-    wh0 = {k: {"served": d["served"], "gets": d.get("gets", 0)} for k, d in (await shard.webhook_timings()).items()} \
-        if shard.cfg.launch else {}
+    adm0 = (await safe(native.admissions(1 << 62), {})).get("seq") if native is not None else None
+    wh0 = {k: {"served": d["served"], "gets": d.get("gets", 0)}
+           for k, d in ((await safe(shard.webhook_timings(), {})) or {}).items()} if shard.cfg.launch else {}
     cpu0 = {kk: _proc_cpu_s(pid) for kk, pid in children.items()}
-    prof0 = await _apiserver_prof(native)
-    gc0 = {k: v["seq"] for k, v in (await shard.gc_pauses()).items()} if shard.procs else {}
+    prof0 = await safe(_apiserver_prof(native))
+    gc0 = {k: v["seq"] for k, v in ((await safe(shard.gc_pauses(), {})) or {}).items()} if shard.procs else {}
     await _in_thread(dist.barrier)
     t0 = time.perf_counter()
     ready_at, create_ms = {}, []
@@ -315,29 +326,31 @@ async def _burst(args, shard, dist, native, children: dict, use_odh: bool, tag: 
         await shard.admin.create(nb)
         create_ms.append((time.perf_counter() - c0) * 1e3)
 
-    await asyncio.gather(*(create(nm) for nm in names))
-    ok = await shard.wait_until(check, 180)
+    await safe(asyncio.gather(*(create(nm) for nm in names)))
+    ok = bool(await safe(shard.wait_until(check, 180), False))
     all_ready = max(ready_at.values()) - t0 if ready_at else None
     await _in_thread(dist.barrier)
     cpu = {kk: (_proc_cpu_s(pid) or 0.0) - (cpu0.get(kk) or 0.0) for kk, pid in children.items()
            if cpu0.get(kk) is not None}
-    adm = (await native.admissions(adm0))["us"] if native is not None else []
+    adm = ((await safe(native.admissions(adm0), {})).get("us") or []) if native is not None and adm0 is not None else []
     # the apiserver over the burst: store-lock waits per resource, malloc_trim passes
-    prof = _prof_per_step(prof0, await _apiserver_prof(native), 1) if native is not None else None
+    prof = _prof_per_step(prof0, await safe(_apiserver_prof(native)), 1) if native is not None else None
     # the control-plane processes' cyclic-GC pauses over the burst (their event loops stop)
-    gcp = {k: [x[1:] for x in v["pauses"]] for k, v in (await shard.gc_pauses(gc0)).items()} if shard.procs else {}
-    whd = list((await shard.webhook_timings(wh0)).values()) if shard.cfg.launch else []
+    gcp = {k: [x[1:] for x in v["pauses"]] for k, v in ((await safe(shard.gc_pauses(gc0), {})) or {}).items()} \
+        if shard.procs else {}
+    whd = list(((await safe(shard.webhook_timings(wh0), {})) or {}).values()) if shard.cfg.launch else []
     wh = [x for d in whd for x in d["handle_ms"]]
     wh_get = [x for d in whd for x in d.get("get_ms") or []]
     t_del = time.perf_counter()
-    await asyncio.gather(*(shard.admin.delete(kinds.NOTEBOOK, nm, ns_of[nm]) for nm in names))
-    gone = await shard.wait_until(lambda: all(shard.gone(nm, ns_of[nm]) for nm in names), 180)
+    await safe(asyncio.gather(*(shard.admin.delete(kinds.NOTEBOOK, nm, ns_of[nm]) for nm in names),
+                              return_exceptions=True))
+    gone = bool(await safe(shard.wait_until(lambda: all(shard.gone(nm, ns_of[nm]) for nm in names), 180), False))
     teardown = time.perf_counter() - t_del
     gathered = [None] * world
     await _in_thread(dist.all_gather_object, gathered, {
         "lat": [(ready_at[nm] - t0) * 1e3 for nm in names if nm in ready_at], "create": create_ms,
         "all_ready": all_ready, "ok": ok and gone, "cpu": cpu, "adm": adm, "teardown": teardown, "k": k,
-        "wh": wh, "wh_get": wh_get, "prof": prof, "gc": gcp})
+        "wh": wh, "wh_get": wh_get, "prof": prof, "gc": gcp, "errors": errors})
     if rank != 0:
         return None
     lat = [x for g in gathered for x in g["lat"]]
@@ -367,6 +380,7 @@ async def _burst(args, shard, dist, native, children: dict, use_odh: bool, tag: 
         "gc_pause_ms": {proc: {"n": len(ps), "max": max(x[1] for x in ps),
                                "gen2": sum(1 for x in ps if x[0] == 2)}
                         for g in gathered for proc, ps in sorted(g["gc"].items()) if ps},
+        **({"errors": [e for g in gathered for e in g["errors"]]} if any(g["errors"] for g in gathered) else {}),
         "apiserver": {k: v for k, v in (gathered[0]["prof"] or {}).items()
                       if k in ("lock_wait_ms", "lock_contended", "lock_wait_by_resource", "trim_ms", "trims",
                                "admit_wall_ms", "webhook_dials", "webhook_dial_ms")},
@@ -698,7 +712,11 @@ async def _drive(args, shard, dist, torch, children: Optional[dict] = None, nati
     samples = []
     for i in range(probe_sample):  # untimed: notebooks with the start-up probe init container
         ann = {**base_ann, GPU_PROBE_ANNOTATION: "true"}
-        ready_s, _gone, pod = await _lifecycle(shard, f"nb-probe-{i}", ann, timeout=180)
+        try:
+            ready_s, _gone, pod = await _lifecycle(shard, f"nb-probe-{i}", ann, timeout=180)
+        except Exception as e:  # noqa: BLE001 — reported with the sample, the headline stands
+            samples.append({"ready_ms": None, "result": {"ok": False, "error": repr(e)[:300]}})
+            break
         st = ((pod or {}).get("status") or {}).get("initContainerStatuses") or [{}]
         term = (st[0].get("state") or {}).get("terminated") or {}
         result = parse_result(term.get("message", ""))

@@ -70,6 +70,9 @@ def parse(argv=None):
     p.add_argument("--webhook-in-odh", action="store_true",
                    help="sharded: each shard's webhook in its odh process (round 3-4's shard pod) instead of a "
                         "process of its own (A/B measurements)")
+    p.add_argument("--cache-configmaps", action="store_true",
+                   help="unsharded: the odh manager caches ConfigMap/Secret data (--cache-configmaps-secrets=true) "
+                        "instead of the reference's live, data-stripped reads")
     p.add_argument("--webhook-replicas", type=int, default=1,
                    help="unsharded with --workers: --webhook-replicas of the odh manager (webhook processes sharing "
                         "the port)")

@@ -54,6 +54,10 @@ def parse(argv: Optional[List[str]] = None) -> argparse.Namespace:
     add_shard_flags(p)
     add_debug_flags(p)
     add_worker_flags(p)
+    p.add_argument("--cache-configmaps-secrets", choices=("true", "false"), default="false",
+                   help="cache ConfigMap/Secret data (false: the reference's uncached, data-stripped reads, "
+                        "odh/main.go:165-185; true: reads — the webhook's included — served from the cache, "
+                        "as a shard does)")
     p.add_argument("--webhook-replicas", type=int, default=1,
                    help="with --workers: processes serving the webhook on one port (SO_REUSEPORT), this one "
                         "and R-1 webhook-only children")
@@ -119,8 +123,10 @@ def build(args, env=os.environ):
     if assign is not None:
         # the controller namespace holds the central HTTPRoutes and ImageStreams every worker reads
         cache_options = assign.cache_options(extra_namespaces=[namespace])
-    mgr = Manager.remote(cfg, name="odh-notebook-controller", uncached=(kinds.CONFIG_MAP, kinds.SECRET),
-                         transforms={kinds.CONFIG_MAP: strip_data, kinds.SECRET: strip_data},
+    cache_cm = getattr(args, "cache_configmaps_secrets", "false") == "true"
+    mgr = Manager.remote(cfg, name="odh-notebook-controller",
+                         uncached=() if cache_cm else (kinds.CONFIG_MAP, kinds.SECRET),
+                         transforms=None if cache_cm else {kinds.CONFIG_MAP: strip_data, kinds.SECRET: strip_data},
                          default_max_concurrent=args.max_concurrent_reconciles, leader_elector=elector,
                          metrics_addr=args.metrics_bind_address, probe_addr=args.health_probe_bind_address,
                          debug_endpoints=args.enable_debug_endpoints, cache_options=cache_options)

@@ -179,8 +179,9 @@ def measure(args) -> Optional[dict]:
                 if w > 1 else ""
             out["config"]["parallelism"] = (f"one kf manager + one odh manager Deployment for all {world} ranks' "
                                             f"notebooks{wk}")
-            overlay = "overlay mi355x" if (w, r) == (4, 2) else \
-                "reference topology; overlay mi355x runs --workers 4 --webhook-replicas 2"
+            overlay = "overlay mi355x" if (w, r) == (4, 1) else "reference topology; overlay mi355x runs --workers 4"
+            if getattr(args, "cache_configmaps", False):
+                overlay += "; odh --cache-configmaps-secrets=true"
             out["config"]["architecture"] = (f"cmd/kf_manager + cmd/odh_manager{f' --workers {w}' if w > 1 else ''}"
                                              f"{f' --webhook-replicas {r}' if w > 1 and r > 1 else ''} ({overlay})")
         w = getattr(args, "platform_workers", 0) or (world + 1) // 2
@@ -537,7 +538,8 @@ async def _main(args, dist, torch, rank: int, world: int, ndev: int, probe_sampl
         webhook=not args.no_odh, reference_emulation=args.reference_emulation, env=env, process=True,
         split=not getattr(args, "single_process_shard", False), workers=max(1, getattr(args, "workers", 1)),
         webhook_replicas=max(1, getattr(args, "webhook_replicas", 1)),
-        webhook_process=not getattr(args, "webhook_in_odh", False)))
+        webhook_process=not getattr(args, "webhook_in_odh", False),
+        cache_configmaps=getattr(args, "cache_configmaps", False)))
     if rank == 0:
         await shard.start()  # cluster namespaces (and, unsharded, the managers + their webhook) first
         await _in_thread(dist.barrier)

@@ -68,6 +68,7 @@ class ShardConfig:
     webhook_process: bool = True  # sharded, split: the webhook in a process of its own (False: odh + webhook)
     workers: int = 1  # unsharded: --workers of the kf and odh managers (runtime/workers.py)
     webhook_replicas: int = 1  # unsharded with workers: --webhook-replicas of the odh manager
+    cache_configmaps: bool = False  # unsharded: --cache-configmaps-secrets=true on the odh manager
     # the user namespaces this rank drives (default: just ``namespace``); with ``assign`` they
     # are created unlabelled and the shipped NamespaceShardAssigner (``--assign-namespaces``,
     # run by every shard's kf process) labels each ``crc32(name) % shard_count``
@@ -145,6 +146,8 @@ class ControlPlaneShard:
         if cfg.odh:
             rep = ["--webhook-replicas", str(cfg.webhook_replicas)] if cfg.workers > 1 and cfg.webhook_replicas > 1 \
                 else []
+            if cfg.cache_configmaps:
+                rep.append("--cache-configmaps-secrets=true")
             out.append(("odh_manager", "odh_kubeflow_amd.cmd.odh_manager",
                         [*wh, "--health-probe-bind-address", "0", *wk, *rep], "--metrics-bind-address"))
         return out

@@ -14,6 +14,7 @@
 #   unsharded  the default topology (one kf + one odh manager process) at 1, 2 and 4 ranks
 #   workers  the same topology with --workers 4: 1, 2 and 4 ranks
 #   wr2      --workers 4 --webhook-replicas 2: 1, 2 and 4 ranks
+#   wcm      --workers 4 with the odh manager caching ConfigMap/Secret data, interleaved with without: 1 and 4 ranks
 #   wpab     sharded: the webhook in the odh process vs a process of its own (deployed), interleaved, 1 and 4 ranks
 #   burst64  64 notebooks at once into one unsharded control plane (--workers 1 and 4) and the sharded one
 #   fair     ours vs --reference-emulation: vanilla / OpenShift-like (pull secret after 200 ms), 0 / 2 ms writes
@@ -141,6 +142,21 @@ for s in $steps; do
           || fail wr2 $? "$out/bench_wr2_n$n.log"
         show "$out/bench_wr2_n$n.log" "workers4 wr2 n$n"
       done ;;
+    wcm)
+      for r in 1 2; do
+        for v in live cached; do
+          case $v in cached) f="--cache-configmaps" ;; *) f="" ;; esac
+          timeout -k 10 200 python -m torch.distributed.run --nnodes=1 --nproc-per-node 4 \
+            --master-addr 127.0.0.1 --master-port 29985 bench.py --gpus 4 --arch unsharded --workers 4 $f \
+            --steps 100 --warmup 5 --probe-sample 0 > "$out/bench_wcm_${v}_n4_r$r.log" 2>&1 \
+            || fail wcm $? "$out/bench_wcm_${v}_n4_r$r.log"
+          show "$out/bench_wcm_${v}_n4_r$r.log" "workers4 $v n4 r$r"
+        done
+      done
+      timeout -k 10 170 python bench.py --gpus 1 --arch unsharded --workers 4 --cache-configmaps --steps 100 \
+        --warmup 5 --probe-sample 0 --no-configs > "$out/bench_wcm_cached_n1.log" 2>&1 \
+        || fail wcm $? "$out/bench_wcm_cached_n1.log"
+      show "$out/bench_wcm_cached_n1.log" "workers4 cached n1" ;;
     wpab)
       for r in 1 2; do
         for v in shared own; do

@@ -95,6 +95,10 @@ MI355X_WORKERS = 4
 # notebooks/s unchanged (570 vs 572, profiles/r4_p9) — admissions were not the limit there;
 # raise it where admission load outgrows one core
 MI355X_WEBHOOK_REPLICAS = 1
+# the odh manager caches ConfigMap/Secret data, as a shard does: the webhook and the reconcilers
+# read them from the cache instead of confirming absences live (+12 % notebooks/s at 4 streams,
+# interleaved on one box, profiles/r4_p16); the reference's overlays keep its uncached reads
+MI355X_CACHE_CONFIGMAPS = True
 # the base manifests carry the development tag; every overlay pins the release tag through
 # kustomize `images` (releasing/VERSION, set by tools/release.py — the reference's
 # releasing/update-manifests-images + releasing/version/VERSION)
@@ -264,7 +268,7 @@ def _agent_token_volume() -> dict:
 AGENT_TOKEN_MOUNT_SPEC = {"name": "node-agent-token", "mountPath": AGENT_TOKEN_MOUNT, "readOnly": True}
 
 
-def _workers_patches(workers: int, webhook_replicas: int = 1) -> List[dict]:
+def _workers_patches(workers: int, webhook_replicas: int = 1, cache_configmaps: bool = False) -> List[dict]:
     """``--workers`` for both managers, and the CPU to run them: one core per worker plus the
     supervisor (which leads, aggregates /metrics and, in the odh manager, serves the webhook);
     the odh manager's ``--webhook-replicas`` add a core each (webhook-only processes sharing the
@@ -277,6 +281,8 @@ def _workers_patches(workers: int, webhook_replicas: int = 1) -> List[dict]:
     extra = max(0, webhook_replicas - 1)
     odh = [*ops[:1], *([{"op": "add", "path": "/spec/template/spec/containers/0/args/-",
                          "value": f"--webhook-replicas={webhook_replicas}"}] if extra else []),
+           *([{"op": "add", "path": "/spec/template/spec/containers/0/args/-",
+               "value": "--cache-configmaps-secrets=true"}] if cache_configmaps else []),
            {**ops[1], "value": str(workers + 1 + extra)}, {**ops[2], "value": str(workers + extra)}]
     out.append({"target": {"kind": "Deployment", "name": f"{NAME_PREFIX}manager"},
                 "patch": yaml.safe_dump(odh, sort_keys=False)})
@@ -752,7 +758,8 @@ def tree(version: Optional[str] = None) -> Dict[str, object]:
     t["overlays/mi355x/kustomization.yaml"] = kustomization(["../../default", "../../webhook-certs"],
                                                             namespace="opendatahub", images=images,
                                                             configMapGenerator=mi355x_generators,
-                                                            patches=_workers_patches(MI355X_WORKERS, MI355X_WEBHOOK_REPLICAS))
+                                                            patches=_workers_patches(MI355X_WORKERS, MI355X_WEBHOOK_REPLICAS,
+                                                                                     MI355X_CACHE_CONFIGMAPS))
     # the serving cert covers every shard's Service; every shard's configuration gets the caBundle
     svc_names = [NAME_PREFIX + o["metadata"]["name"] for o in cp["services.yaml"][1:]]
     mwc_names = [NAME_PREFIX + o["metadata"]["name"] for o in cp["webhooks.yaml"]]

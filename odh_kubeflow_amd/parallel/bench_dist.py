@@ -179,9 +179,11 @@ def measure(args) -> Optional[dict]:
                 if w > 1 else ""
             out["config"]["parallelism"] = (f"one kf manager + one odh manager Deployment for all {world} ranks' "
                                             f"notebooks{wk}")
-            overlay = "overlay mi355x" if (w, r) == (4, 1) else "reference topology; overlay mi355x runs --workers 4"
-            if getattr(args, "cache_configmaps", False):
-                overlay += "; odh --cache-configmaps-secrets=true"
+            cm = getattr(args, "cache_configmaps", False)
+            overlay = "overlay mi355x" if (w, r, cm) == (4, 1, True) else \
+                "reference topology; overlay mi355x runs --workers 4, odh --cache-configmaps-secrets=true"
+            if cm:
+                overlay = "odh --cache-configmaps-secrets=true; " + overlay
             out["config"]["architecture"] = (f"cmd/kf_manager + cmd/odh_manager{f' --workers {w}' if w > 1 else ''}"
                                              f"{f' --webhook-replicas {r}' if w > 1 and r > 1 else ''} ({overlay})")
         w = getattr(args, "platform_workers", 0) or (world + 1) // 2

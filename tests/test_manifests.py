@@ -366,7 +366,8 @@ def test_mi355x_overlay_runs_manager_workers_and_webhook_replicas():
     assert "--workers=4" in kf["args"] and not any(a.startswith("--webhook-replicas") for a in kf["args"])
     assert kf["resources"]["requests"]["cpu"] == "4" and kf["resources"]["limits"]["cpu"] == "5"
     assert "--workers=4" in odh["args"] and not any(a.startswith("--webhook-replicas") for a in odh["args"])
+    assert "--cache-configmaps-secrets=true" in odh["args"] and not any("cache-configmaps" in a for a in kf["args"])
     assert odh["resources"]["requests"]["cpu"] == "4" and odh["resources"]["limits"]["cpu"] == "5"
     plain = _by(_render("standalone"), "Deployment")["odh-kubeflow-amd-manager"]
-    assert not any(a.startswith(("--workers", "--webhook-replicas"))
+    assert not any(a.startswith(("--workers", "--webhook-replicas", "--cache-configmaps"))
                    for a in plain["spec"]["template"]["spec"]["containers"][0]["args"])

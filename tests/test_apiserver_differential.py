@@ -222,6 +222,8 @@ def test_selector_filtered_watch_survives_history_rollover(run):
             tasks = [asyncio.ensure_future(consume("u")), asyncio.ensure_future(consume(None))]
             await asyncio.sleep(0.1)
             for i in range(600):  # > 9x the history, none of them wanted
+                if i % 16 == 15:  # let a starved watcher thread run (the suite shares 8 CPUs)
+                    await asyncio.sleep(0.002)
                 await c.create({"apiVersion": "v1", "kind": "ConfigMap",
                                 "metadata": {"name": f"x{i}", "namespace": "u", "labels": {"want": "no"}}})
             await c.create({"apiVersion": "v1", "kind": "ConfigMap",

@@ -157,6 +157,16 @@ for s in $steps; do
         --warmup 5 --probe-sample 0 --no-configs > "$out/bench_wcm_cached_n1.log" 2>&1 \
         || fail wcm $? "$out/bench_wcm_cached_n1.log"
       show "$out/bench_wcm_cached_n1.log" "workers4 cached n1" ;;
+    wcmr2)  # overlay mi355x (cached ConfigMaps) with 1 vs 2 odh webhook processes, 4 ranks, interleaved
+      for r in 1 2; do
+        for v in 1 2; do
+          timeout -k 10 200 python -m torch.distributed.run --nnodes=1 --nproc-per-node 4 \
+            --master-addr 127.0.0.1 --master-port 29983 bench.py --gpus 4 --arch unsharded --workers 4 \
+            --cache-configmaps --webhook-replicas $v --steps 100 --warmup 5 --probe-sample 0 --no-configs \
+            > "$out/bench_wcmr${v}_n4_r$r.log" 2>&1 || fail wcmr2 $? "$out/bench_wcmr${v}_n4_r$r.log"
+          show "$out/bench_wcmr${v}_n4_r$r.log" "workers4 cached wr$v n4 r$r"
+        done
+      done ;;
     wpab)
       for r in 1 2; do
         for v in shared own; do

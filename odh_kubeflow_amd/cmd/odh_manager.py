@@ -6,7 +6,8 @@ Flags: ``--metrics-bind-address`` (:8080), ``--health-probe-bind-address`` (:808
 (``/tmp/k8s-webhook-server/serving-certs``), ``--webhook-port`` (8443),
 ``--leader-elect``, ``--debug-log``.  The cache strips ``managedFields`` from every
 object and ``data`` from ConfigMaps/Secrets, whose reads go straight to the apiserver
-(:165-185).  The controller namespace comes from the service-account namespace file or
+(:165-185); ``--cache-configmaps-secrets=true`` caches their data instead (overlay
+``mi355x``: an admission then waits for no live GET, ``docs/DEPLOY.md``).  The controller namespace comes from the service-account namespace file or
 ``K8S_NAMESPACE`` (:103-115).  Leader-election ID ``odh-notebook-controller``.
 
 ``--workers W`` runs the reconciler in W namespace-partitioned child processes
@@ -18,8 +19,9 @@ port (``SO_REUSEPORT``: the kernel spreads the apiserver's connections over them
 event loop is one core, and at 4 concurrent notebook streams the supervisor's webhook ran at
 ≈60 % of one, so admissions — three per notebook, two of them on the create → Ready path —
 queued behind each other.  A replica reads what an admission needs the way the supervisor
-does: ConfigMaps and Secrets live (the reference's uncached reads), the controller
-namespace's objects from its cache.
+does: ConfigMaps and Secrets live (the reference's uncached reads) or, with
+``--cache-configmaps-secrets=true``, from its cache; the controller namespace's objects from
+its cache.
 """
 
 from __future__ import annotations

@@ -142,6 +142,28 @@ def test_worker_command_lines_drop_what_only_the_supervisor_does():
     assert wk.parse_worker("1/4") == (1, 4) and wk.parse_worker(None) is None
 
 
+@pytest.mark.parametrize("flag", ["false", "true"])
+def test_odh_manager_configmap_secret_caching_flag(tmp_path, flag):
+    """``--cache-configmaps-secrets``: false keeps the reference's uncached, data-stripped
+    ConfigMap/Secret reads (``odh/main.go:165-185``); true caches their data, in the workers
+    and webhook replicas too (the flag travels on their command lines)."""
+    from odh_kubeflow_amd.cmd import odh_manager
+    from odh_kubeflow_amd.models.scheme import SCHEME
+
+    for f in ("tls.crt", "tls.key"):
+        (tmp_path / f).write_text("x")
+    o = odh_manager.parse(["--kube-rbac-proxy-image", "img", "--master", "http://127.0.0.1:1", "--webhook-cert-dir",
+                           str(tmp_path), "--cache-configmaps-secrets", flag, "--workers=2", "--webhook-replicas=2"])
+    mgr = odh_manager.build(o, env={})
+    cm, sec = SCHEME.resolve(kinds.CONFIG_MAP).key, SCHEME.resolve(kinds.SECRET).key
+    if flag == "true":
+        assert not mgr.client.uncached and not (mgr.cache.transforms or {}).get(cm)
+    else:
+        assert mgr.client.uncached == {cm, sec} and mgr.cache.transforms.get(cm) is not None
+    for argv in (odh_manager.worker_argv(o, 0, "127.0.0.1:1"), odh_manager.replica_argv(o, 0, "127.0.0.1:2")):
+        assert argv[argv.index("--cache-configmaps-secrets") + 1] == flag
+
+
 @pytest.mark.slow
 def test_managers_with_workers_serve_partitioned_namespaces(run):
     async def go():

@@ -158,13 +158,27 @@ for s in $steps; do
         || fail wcm $? "$out/bench_wcm_cached_n1.log"
       show "$out/bench_wcm_cached_n1.log" "workers4 cached n1" ;;
     wcmr2)  # overlay mi355x (cached ConfigMaps) with 1 vs 2 odh webhook processes, 4 ranks, interleaved
-      for r in 1 2; do
+      for r in $(seq 1 "${ROUNDS:-2}"); do
         for v in 1 2; do
           timeout -k 10 200 python -m torch.distributed.run --nnodes=1 --nproc-per-node 4 \
             --master-addr 127.0.0.1 --master-port 29983 bench.py --gpus 4 --arch unsharded --workers 4 \
             --cache-configmaps --webhook-replicas $v --steps 100 --warmup 5 --probe-sample 0 --no-configs \
             > "$out/bench_wcmr${v}_n4_r$r.log" 2>&1 || fail wcmr2 $? "$out/bench_wcmr${v}_n4_r$r.log"
           show "$out/bench_wcmr${v}_n4_r$r.log" "workers4 cached wr$v n4 r$r"
+        done
+      done ;;
+    wcmr2n1)  # the same at 1 and 2 ranks (efficiency denominators), interleaved
+      for r in 1 2; do
+        for v in 1 2; do
+          timeout -k 10 170 python bench.py --gpus 1 --arch unsharded --workers 4 --cache-configmaps \
+            --webhook-replicas $v --steps 100 --warmup 5 --probe-sample 0 --no-configs \
+            > "$out/bench_wcmr${v}_n1_r$r.log" 2>&1 || fail wcmr2n1 $? "$out/bench_wcmr${v}_n1_r$r.log"
+          show "$out/bench_wcmr${v}_n1_r$r.log" "workers4 cached wr$v n1 r$r"
+          timeout -k 10 170 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
+            --master-addr 127.0.0.1 --master-port 29982 bench.py --gpus 2 --arch unsharded --workers 4 \
+            --cache-configmaps --webhook-replicas $v --steps 100 --warmup 5 --probe-sample 0 --no-configs \
+            > "$out/bench_wcmr${v}_n2_r$r.log" 2>&1 || fail wcmr2n1 $? "$out/bench_wcmr${v}_n2_r$r.log"
+          show "$out/bench_wcmr${v}_n2_r$r.log" "workers4 cached wr$v n2 r$r"
         done
       done ;;
     wpab)

@@ -391,12 +391,13 @@ async def _burst(args, shard, dist, native, children: dict, use_odh: bool, tag: 
 
 
 def io_delta(a: dict, b: dict) -> dict:
-    """Per process: watch events per kind and requests per verb between two snapshots."""
+    """Per process: watch events per kind, requests per verb and lists per kind (a list in the
+    window is a relist: a watch answered 410 Gone) between two snapshots."""
     out = {}
     for proc, cur in b.items():
         prev = a.get(proc) or {}
         d = {}
-        for sect in ("watch_events", "requests"):
+        for sect in ("watch_events", "requests", "lists"):
             p0 = prev.get(sect) or {}
             dd = {k: v - p0.get(k, 0) for k, v in (cur.get(sect) or {}).items()}
             d[sect] = {k: v for k, v in dd.items() if v}
@@ -417,8 +418,13 @@ def io_per_notebook(parts: list, notebooks: int) -> dict:
                 for k, v in kv.items():
                     s[k] = s.get(k, 0) + v
     for proc, o in out.items():
-        for sect, kv in o.items():
+        for sect, kv in list(o.items()):
             tot = sum(kv.values())
+            if sect == "lists":  # rare: counted, not divided
+                if tot:
+                    o["relists_in_window"] = dict(kv, total=tot)
+                del o[sect]
+                continue
             o[sect] = {k: round(v / n, 2) for k, v in sorted(kv.items(), key=lambda x: -x[1])}
             o[sect]["total"] = round(tot / n, 2)
     return out

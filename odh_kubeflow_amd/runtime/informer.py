@@ -406,6 +406,16 @@ class InformerCache(Reader, EventSource):
                 out[g.info.kind] = out.get(g.info.kind, 0) + n
         return out
 
+    def relist_counts(self) -> Dict[str, int]:
+        """Lists per kind since start, the initial one of each informer included: a rise means
+        a watch was answered 410 Gone (it fell behind the apiserver's bounded history)."""
+        out: Dict[str, int] = {}
+        for g in self._groups.values():
+            n = sum(inf.relists for inf in g.infs.values())
+            if n:
+                out[g.info.kind] = out.get(g.info.kind, 0) + n
+        return out
+
     def informer(self, kind) -> _Informer:
         """The (first) informer of ``kind`` — for single-namespace / cluster-wide caches."""
         return self._group(kind).all()[0]

@@ -282,11 +282,13 @@ class Manager:
         return [s for s in (self.supervisor, self.webhook_replicas) if s is not None]
 
     def io_counters(self) -> Dict[str, Dict[str, int]]:
-        """What this process received and sent: watch events per kind, REST requests per verb."""
+        """What this process received and sent: watch events per kind, REST requests per verb,
+        and lists per kind (relists after a 410 Gone among them)."""
         cache = getattr(self, "cache", None) or self.reader
         rest = getattr(self, "rest", None)
         ev = cache.event_counts() if hasattr(cache, "event_counts") else {}
-        return {"watch_events": ev, "requests": dict(getattr(rest, "by_verb", {}) or {})}
+        lists = cache.relist_counts() if hasattr(cache, "relist_counts") else {}
+        return {"watch_events": ev, "requests": dict(getattr(rest, "by_verb", {}) or {}), "lists": lists}
 
     def reconcile_count(self) -> int:
         return sum(c.reconciles for c in self.controllers)

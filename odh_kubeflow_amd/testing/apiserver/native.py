@@ -47,12 +47,16 @@ def available() -> bool:
 
 class NativeApiServer:
     """``binary`` (or ``$ODH_APISERVER_BINARY``) selects another build of the server, e.g. the
-    ThreadSanitizer one the race-detection test compiles; ``env`` is added to its environment."""
+    ThreadSanitizer one the race-detection test compiles; ``env`` is added to its environment.
+    ``history`` (default ``$ODH_APISERVER_HISTORY`` or 1024) bounds each resource's watch
+    history in events."""
 
     def __init__(self, uninstalled: Iterable[str] = (), gc: bool = False, token: Optional[str] = None,
-                 host: str = "127.0.0.1", port: int = 0, history: int = 1024, binary: Optional[str] = None,
+                 host: str = "127.0.0.1", port: int = 0, history: Optional[int] = None, binary: Optional[str] = None,
                  env: Optional[dict] = None, audit_log_path: Optional[str] = None, audit_policy=None,
                  write_latency_ms: float = 0.0):
+        if history is None:
+            history = int(os.environ.get("ODH_APISERVER_HISTORY") or 1024)
         self.cfg = scheme_config(uninstalled, gc, token, history)
         self.write_latency_ms = float(write_latency_ms)  # etcd-like storage round trip per write
         if audit_log_path:  # kube-apiserver --audit-log-path / --audit-policy-file (apiserver/audit.py)

@@ -141,3 +141,18 @@ def test_shard_load_report():
     assert out["shards"]["1"]["notebooks"] == 6 and out["shards"]["1"]["cpu_ms_per_notebook"] == {
         "control_plane_kf_1": 5.0}  # the platform's kubelet_1 is not shard 1's
     assert out["max_over_mean_notebooks"] == 1.0
+
+
+def test_io_per_notebook_divides_traffic_and_counts_relists():
+    """Watch events and requests are per notebook of the window; lists in the window (a watch
+    answered 410 Gone, then relisted) are counted, not divided, and only reported when any."""
+    from odh_kubeflow_amd.parallel.bench_dist import io_delta, io_per_notebook
+
+    a = {"kf": {"watch_events": {"Pod": 2}, "requests": {"POST": 1}, "lists": {"Pod": 1, "Notebook": 1}}}
+    b = {"kf": {"watch_events": {"Pod": 42}, "requests": {"POST": 21}, "lists": {"Pod": 2, "Notebook": 1}}}
+    quiet = {"odh": {"watch_events": {"Service": 20}, "requests": {}, "lists": {"Service": 1}}}
+    out = io_per_notebook([io_delta(a, b), io_delta(quiet, quiet)], 10)
+    assert out["kf"]["watch_events"] == {"Pod": 4.0, "total": 4.0}
+    assert out["kf"]["requests"] == {"POST": 2.0, "total": 2.0}
+    assert out["kf"]["relists_in_window"] == {"Pod": 1, "total": 1} and "lists" not in out["kf"]
+    assert "relists_in_window" not in out["odh"]

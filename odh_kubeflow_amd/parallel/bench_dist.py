@@ -386,7 +386,7 @@ async def _burst(args, shard, dist, native, children: dict, use_odh: bool, tag: 
         **({"errors": [e for g in gathered for e in g["errors"]]} if any(g["errors"] for g in gathered) else {}),
         "apiserver": {k: v for k, v in (gathered[0]["prof"] or {}).items()
                       if k in ("lock_wait_ms", "lock_contended", "lock_wait_by_resource", "trim_ms", "trims",
-                               "admit_wall_ms", "webhook_dials", "webhook_dial_ms")},
+                               "admit_wall_ms", "webhook_dials", "webhook_dial_ms", "watch_gone")},
     }
 
 

@@ -651,6 +651,7 @@ struct Prof {
   std::atomic<uint64_t> lock_hold_ns[C_N]{};
   std::atomic<uint64_t> trim_ns{0}, trim_max_ns{0}, trims{0};  // malloc_trim passes (allocations wait on them)
   std::atomic<uint64_t> webhook_dials{0}, webhook_dial_ns{0};  // new webhook connections: connect + TLS handshake
+  std::atomic<uint64_t> watch_gone{0};  // watches answered 410 Gone (behind the bounded history): each is a relist
 } P;
 thread_local int t_cat = C_OTHER;
 
@@ -2851,6 +2852,7 @@ void serve_watch(int fd, Res& r, const Path& p, const Request& rq) {
       const std::deque<Ev>& hist = wh->hist;
       // 410 when an event after `since` has fallen off the resource's bounded history
       if (since < b.dropped_rv) {
+        P.watch_gone++;
         Value ev = Value::object();
         ev["type"] = Value::str("ERROR");
         ev["object"] = status_obj(Gone());
@@ -2908,6 +2910,7 @@ void serve_watch(int fd, Res& r, const Path& p, const Request& rq) {
       }
     }
     if (gone) {
+      P.watch_gone++;
       Value ev = Value::object();
       ev["type"] = Value::str("ERROR");
       ev["object"] = status_obj(Gone());
@@ -2995,7 +2998,7 @@ bool handle(int fd, Request& rq) {
   }
   if (rq.method == "GET" && rq.path == "/metrics") {
     int64_t rv = S.rv.load();
-    char buf[1024];  // the longest line below: 13 counters of up to 20 digits and their names
+    char buf[1024];  // the longest line below: 14 counters of up to 20 digits and their names
     snprintf(buf, sizeof(buf),
              "{\"requests\":%llu,\"writes\":%llu,\"webhook_calls\":%llu,\"resourceVersion\":%lld,\"prof\":{",
              (unsigned long long)S.requests.load(), (unsigned long long)S.writes.load(),
@@ -3010,12 +3013,13 @@ bool handle(int fd, Request& rq) {
     snprintf(buf, sizeof(buf),
              "\"lock_wait_ns\":%llu,\"lock_contended\":%llu,\"watch_wakeups\":%llu,\"watch_scanned\":%llu,"
              "\"admit_wall_ns\":%llu,\"trim_ns\":%llu,\"trim_max_ns\":%llu,\"trims\":%llu,"
-             "\"webhook_dials\":%llu,\"webhook_dial_ns\":%llu}}",
+             "\"webhook_dials\":%llu,\"webhook_dial_ns\":%llu,\"watch_gone\":%llu}}",
              (unsigned long long)P.lock_wait_ns.load(), (unsigned long long)P.lock_contended.load(),
              (unsigned long long)P.wakeups.load(), (unsigned long long)P.scanned.load(),
              (unsigned long long)P.admit_wall_ns.load(), (unsigned long long)P.trim_ns.load(),
              (unsigned long long)P.trim_max_ns.load(), (unsigned long long)P.trims.load(),
-             (unsigned long long)P.webhook_dials.load(), (unsigned long long)P.webhook_dial_ns.load());
+             (unsigned long long)P.webhook_dials.load(), (unsigned long long)P.webhook_dial_ns.load(),
+             (unsigned long long)P.watch_gone.load());
     out += buf;
     out.pop_back();
     out += ",\"phases\":{";

@@ -253,10 +253,36 @@ def test_native_metrics_document_is_complete_json(run):
             await c.close()
             await nat.stop()
         assert st["writes"] >= 11 and st["prof"]["patch_calls"] == 5
-        for k in ("webhook_dials", "webhook_dial_ns", "trims", "lock_wait_ns", "admit_wall_ns"):
+        for k in ("webhook_dials", "webhook_dial_ns", "trims", "lock_wait_ns", "admit_wall_ns", "watch_gone"):
             assert k in st["prof"], k
         assert set(st["phases"]) == {f"{p}_cpu_ns" for p in ("parse", "admit", "validate", "defaults", "patch",
                                                              "prepare", "dump")}
         assert st["phases"]["parse_cpu_ns"] > 0 and st["phases"]["patch_cpu_ns"] > 0
         assert isinstance(st["locks"], dict)
+    run(go(), timeout=60)
+
+
+def test_native_counts_watches_answered_gone(run):
+    """A watch from a resourceVersion that fell off the bounded history is answered 410 Gone
+    and counted (``prof.watch_gone``: the benchmark's relist signal)."""
+    from odh_kubeflow_amd.models import kinds
+    from odh_kubeflow_amd.models import meta as m
+    from odh_kubeflow_amd.models.errors import Gone
+
+    async def go():
+        nat = await native.NativeApiServer(history=8).start()
+        c = RestClient(RestConfig(host=nat.url))
+        try:
+            await c.create({"apiVersion": "v1", "kind": "Namespace", "metadata": {"name": "g"}})
+            first = await c.create({"apiVersion": "v1", "kind": "ConfigMap", "metadata": {"name": "c0", "namespace": "g"}})
+            for i in range(1, 40):
+                await c.create({"apiVersion": "v1", "kind": "ConfigMap", "metadata": {"name": f"c{i}", "namespace": "g"}})
+            assert (await nat.stats())["prof"]["watch_gone"] == 0
+            with pytest.raises(Gone):
+                async for _ in c.watch(kinds.CONFIG_MAP, "g", m.resource_version(first), timeout_s=5):
+                    pass
+            assert (await nat.stats())["prof"]["watch_gone"] == 1
+        finally:
+            await c.close()
+            await nat.stop()
     run(go(), timeout=60)

@@ -29,6 +29,6 @@ for r in $(seq 1 "$rounds"); do
     env "${envs[@]}" timeout -k 10 200 python -m torch.distributed.run --nnodes=1 --nproc-per-node "$n" \
       --master-addr 127.0.0.1 --master-port 2999$n bench.py --gpus "$n" --steps "$steps" --warmup 5 \
       --probe-sample 0 --burst 0 --no-configs > "$out/${v}_n${n}_$r.log" 2>&1
-    python -c "import json,sys; d=json.loads([l for l in open(sys.argv[1]) if l.startswith('{')][-1]); print(sys.argv[1], d['notebooks_ready_per_s'], d['p50_ready_ms'], d['cpu_ms_per_step'].get('apiserver'), (d.get('apiserver_profile_per_step') or {}).get('lock_wait_ms'), d['child_rss_mib'].get('apiserver'), 'relists', sum((p.get('relists_in_window') or {}).get('total', 0) for p in (d.get('io_per_notebook') or {}).values()))" "$out/${v}_n${n}_$r.log"
+    python -c "import json,sys; d=json.loads([l for l in open(sys.argv[1]) if l.startswith('{')][-1]); print(sys.argv[1], d['notebooks_ready_per_s'], d['p50_ready_ms'], d['cpu_ms_per_step'].get('apiserver'), (d.get('apiserver_profile_per_step') or {}).get('lock_wait_ms'), d['child_rss_mib'].get('apiserver'), 'gone/step', (d.get('apiserver_profile_per_step') or {}).get('watch_gone'), 'relists', sum((p.get('relists_in_window') or {}).get('total', 0) for p in (d.get('io_per_notebook') or {}).values()))" "$out/${v}_n${n}_$r.log"
   done
 done

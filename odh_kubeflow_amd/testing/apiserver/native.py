@@ -24,7 +24,7 @@ BINARY = os.path.join(os.path.dirname(HERE), "native", "bin", "odh-apiserver")
 
 
 def scheme_config(uninstalled: Iterable[str] = (), gc: bool = False, token: Optional[str] = None,
-                  history: int = 1024) -> dict:
+                  history: int = 512) -> dict:
     skip = {SCHEME.resolve(k).key for k in uninstalled}
     res = []
     for i in SCHEME.all():
@@ -48,7 +48,7 @@ def available() -> bool:
 class NativeApiServer:
     """``binary`` (or ``$ODH_APISERVER_BINARY``) selects another build of the server, e.g. the
     ThreadSanitizer one the race-detection test compiles; ``env`` is added to its environment.
-    ``history`` (default ``$ODH_APISERVER_HISTORY`` or 1024) bounds each resource's watch
+    ``history`` (default ``$ODH_APISERVER_HISTORY`` or 512) bounds each resource's watch
     history in events."""
 
     def __init__(self, uninstalled: Iterable[str] = (), gc: bool = False, token: Optional[str] = None,
@@ -56,7 +56,7 @@ class NativeApiServer:
                  env: Optional[dict] = None, audit_log_path: Optional[str] = None, audit_policy=None,
                  write_latency_ms: float = 0.0):
         if history is None:
-            history = int(os.environ.get("ODH_APISERVER_HISTORY") or 1024)
+            history = int(os.environ.get("ODH_APISERVER_HISTORY") or 512)
         self.cfg = scheme_config(uninstalled, gc, token, history)
         self.write_latency_ms = float(write_latency_ms)  # etcd-like storage round trip per write
         if audit_log_path:  # kube-apiserver --audit-log-path / --audit-policy-file (apiserver/audit.py)

@@ -3,7 +3,8 @@
 #   cur       the in-tree odh-apiserver (glibc's default malloc arenas: 8 x cores)
 #   cap8      the same with malloc arenas capped at 8 (MALLOC_ARENA_MAX=8; the build's default until r4_apiab)
 #   a32       capped at 32
-#   h512      the watch history bounded at 512 events per resource (ODH_APISERVER_HISTORY; default 1024)
+#   h512      the watch history bounded at 512 events per resource (ODH_APISERVER_HISTORY; the default since r4_hist)
+#   h1024     bounded at 1024 (the default until r4_hist)
 #   r3        round 3's odh-apiserver (testing/native/bin/odh-apiserver-r3, built from c6e2b35)
 #   gpurun --timeout 900 -- bash tools/research/apiserver_ab.sh <tag> [ranks] [rounds] [variants]
 set -e -o pipefail

@@ -227,6 +227,7 @@ for s in $steps; do
         timeout -k 10 200 python -m torch.distributed.run --nnodes=1 --nproc-per-node $2 \
           --master-addr 127.0.0.1 --master-port 2997$2 bench.py --gpus $2 --arch $1 --workers $3 --steps 100 \
           --warmup 5 --probe-sample 0 --namespaces-per-rank 16 --assign-policy $4 \
+          $([ "$1" = unsharded ] && echo --cache-configmaps) \
           > "$out/bench_nsr16_$1_n$2_$4.log" 2>&1 || fail nsr $? "$out/bench_nsr16_$1_n$2_$4.log"
         show "$out/bench_nsr16_$1_n$2_$4.log" "nsr16 $1 n$2 w$3 $4"
       done ;;

@@ -55,10 +55,10 @@ def pred_funcs(create=None, update=None, delete=None, generic=None, default: boo
     """``predicate.Funcs``: per event-type filters; unset entries default to ``default``."""
 
     def p(etype: str, obj: dict, old: Optional[dict]) -> bool:
-        fn = {"ADDED": create, "MODIFIED": update, "DELETED": delete}.get(etype, generic)
-        if fn is None:
-            return default
-        return fn(obj, old) if etype == "MODIFIED" else fn(obj)
+        if etype == "MODIFIED":
+            return default if update is None else update(obj, old)
+        fn = create if etype == "ADDED" else delete if etype == "DELETED" else generic
+        return default if fn is None else fn(obj)
 
     return p
 
@@ -90,9 +90,10 @@ def generation_or_metadata_changed(etype: str, obj: dict, old: Optional[dict]) -
             or om.get("deletionTimestamp") != nm.get("deletionTimestamp"))
 
 
-def _path(obj: Optional[dict], path: str):
+def _path(obj: Optional[dict], path):
+    """``path``: dotted string, or its parts already split."""
     cur = obj
-    for part in path.split("."):
+    for part in (path.split(".") if isinstance(path, str) else path):
         if not isinstance(cur, dict):
             return None
         cur = cur.get(part)
@@ -103,10 +104,15 @@ def fields_changed(*paths: str) -> Predicate:
     """Pass creates and deletes; pass an update only if one of the dotted ``paths``
     (e.g. ``"status.readyReplicas"``, ``"metadata.labels"``) differs from the old object."""
 
+    split = tuple(tuple(x.split(".")) for x in paths)
+
     def p(etype: str, obj: dict, old: Optional[dict]) -> bool:
         if etype != "MODIFIED" or old is None:
             return True
-        return any(_path(obj, x) != _path(old, x) for x in paths)
+        for x in split:
+            if _path(obj, x) != _path(old, x):
+                return True
+        return False
 
     return p
 
@@ -218,7 +224,7 @@ class Controller:
             if etype != "DELETED" and self.own_writes is not None:
                 own = self.own_writes(obj, self.name)
             res = w.map_fn(obj)
-            if inspect.isawaitable(res):
+            if res is not None and not isinstance(res, (list, tuple)) and inspect.isawaitable(res):
                 t = asyncio.ensure_future(self._enqueue_async(res, trig))
                 self._map_tasks.add(t)
                 t.add_done_callback(self._map_tasks.discard)

@@ -151,26 +151,47 @@ class _Stream:
             self.close()
 
     async def lines(self) -> AsyncIterator[bytes]:
+        """The body's lines (without their newline).  Chunked bodies are read as whatever has
+        arrived — one await per arrival, however many chunks and events it holds — and
+        de-chunked here, rather than three stream reads per chunk."""
         r = self.conn.reader
-        buf = b""
         try:
             if not self.chunked:
                 async for line in r:
                     yield line
                 return
+            raw = bytearray()  # chunked framing not yet parsed
+            body = bytearray()  # de-chunked bytes not yet split into lines
             while True:
-                line = await r.readuntil(b"\r\n")
-                size = int(line.split(b";", 1)[0].strip(), 16)
-                if size == 0:
+                data = await r.read(1 << 16)
+                if not data:
                     return
-                buf += await r.readexactly(size)
-                await r.readexactly(2)
+                raw += data
+                pos, done = 0, False
                 while True:
-                    nl = buf.find(b"\n")
+                    crlf = raw.find(b"\r\n", pos)
+                    if crlf < 0:
+                        break
+                    size = int(bytes(raw[pos:crlf]).split(b";", 1)[0].strip(), 16)
+                    if size == 0:
+                        done = True
+                        break
+                    end = crlf + 2 + size
+                    if len(raw) < end + 2:
+                        break
+                    body += raw[crlf + 2:end]
+                    pos = end + 2
+                del raw[:pos]
+                start = 0
+                while True:
+                    nl = body.find(b"\n", start)
                     if nl < 0:
                         break
-                    yield buf[:nl]
-                    buf = buf[nl + 1:]
+                    yield bytes(body[start:nl])
+                    start = nl + 1
+                del body[:start]
+                if done:
+                    return
         except (asyncio.IncompleteReadError, ConnectionError, OSError):
             return
         finally:

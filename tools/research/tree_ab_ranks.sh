@@ -22,6 +22,6 @@ for r in $(seq 1 "$rounds"); do
   run "$old" "$PWD/$out/old_n${n}_$r.log"
   run . "$out/new_n${n}_$r.log" --burst 0 --no-configs
   for f in "$out/old_n${n}_$r.log" "$out/new_n${n}_$r.log"; do
-    python -c "import json,sys; d=json.loads([l for l in open(sys.argv[1]) if l.startswith('{')][-1]); print(sys.argv[1], d['notebooks_ready_per_s'], d['p50_ready_ms'], d['cpu_ms_per_step'].get('apiserver'))" "$f"
+    python -c "import json,sys; d=json.loads([l for l in open(sys.argv[1]) if l.startswith('{')][-1]); print(sys.argv[1], d['notebooks_ready_per_s'], d['p50_ready_ms'], d['cpu_ms_per_step'].get('apiserver'), {k: v for k, v in d['cpu_ms_per_step'].items() if k.startswith('control_plane')})" "$f"
   done
 done

@@ -46,10 +46,11 @@ from ..models import kinds
 from ..models import meta as m
 from ..models.errors import ApiError, is_already_exists, is_not_found
 from ..models.notebook import (ANNOTATION_HEADERS_REQUEST_SET, ANNOTATION_NOTEBOOK_RESTART, ANNOTATION_REWRITE_URI,
-                               DEFAULT_CONTAINER_PORT, DEFAULT_FS_GROUP, DEFAULT_SERVING_PORT, GPU_RESOURCE,
-                               MAX_STATEFULSET_NAME_LENGTH, NOTEBOOK_NAME_LABEL, PREFIX_ENV_VAR, STATEFULSET_LABEL,
-                               STOP_ANNOTATION, WORKBENCH_LABEL, gpu_request, pod_cond_to_notebook_cond)
-from ..runtime.controller import Request, Result, controller_owner_alive, fields_changed, pred_funcs
+                               CULLER_HEARTBEAT_ANNOTATIONS, DEFAULT_CONTAINER_PORT, DEFAULT_FS_GROUP,
+                               DEFAULT_SERVING_PORT, GPU_RESOURCE, MAX_STATEFULSET_NAME_LENGTH, NOTEBOOK_NAME_LABEL,
+                               PREFIX_ENV_VAR, STATEFULSET_LABEL, STOP_ANNOTATION, WORKBENCH_LABEL, gpu_request,
+                               pod_cond_to_notebook_cond)
+from ..runtime.controller import Request, Result, controller_owner_alive, fields_changed, maps_differ, pred_funcs
 from ..utils.objutil import deepcopy_json
 from ..utils.reconcilehelper import copy_service_fields, copy_statefulset_fields, copy_virtual_service
 
@@ -521,8 +522,10 @@ class NotebookReconciler:
         With ``event_filters`` each watch passes only the changes the reconcile reads:
 
         * Notebook — spec (generation), labels, annotations (stop/restart/lock), creation;
-          not its own status writes, odh's finalizer edits, or deletion (nothing to do on
-          a deleting Notebook, :138-140; GC removes the children);
+          not its own status writes, odh's finalizer edits, the culler's activity heartbeat
+          (``last-activity`` / ``last_activity_check_timestamp``, rewritten every check of
+          every running notebook), or deletion (nothing to do on a deleting Notebook,
+          :138-140; GC removes the children);
         * StatefulSet — spec/metadata drift and ``status.readyReplicas`` (the only STS
           status the Notebook status mirrors, :301-312); deletion only while its Notebook
           is alive (drift → recreate);
@@ -542,9 +545,17 @@ class NotebookReconciler:
         if self.event_filters:
             reader = self.reader
             drift = ("spec", "metadata.labels", "metadata.annotations", "metadata.ownerReferences")
-            nb_changed = fields_changed("metadata.generation", "metadata.labels", "metadata.annotations")
-            nb_preds = [pred_funcs(update=lambda o, old: not m.is_deleting(o) and nb_changed("MODIFIED", o, old),
-                                   delete=lambda o: False)]
+            nb_changed = fields_changed("metadata.generation", "metadata.labels")
+
+            def nb_update(o, old):
+                if m.is_deleting(o):
+                    return False
+                if nb_changed("MODIFIED", o, old):
+                    return True
+                # the culler's per-check heartbeat alone changes nothing this reconcile
+                # reads or generates (the STS template never carries "notebook" keys, :488)
+                return maps_differ(m.annotations(old), m.annotations(o), CULLER_HEARTBEAT_ANNOTATIONS)
+            nb_preds = [pred_funcs(update=nb_update, delete=lambda o: False)]
             sts_drift = fields_changed(*drift)
 
             def sts_changed(etype, sts, old):

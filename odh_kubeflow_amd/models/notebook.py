@@ -29,6 +29,12 @@ HUB_VERSION = "v1beta1"  # kf/api/v1beta1/notebook_conversion.go:19
 STOP_ANNOTATION = "kubeflow-resource-stopped"
 LAST_ACTIVITY_ANNOTATION = "notebooks.kubeflow.org/last-activity"
 LAST_ACTIVITY_CHECK_TIMESTAMP_ANNOTATION = "notebooks.kubeflow.org/last_activity_check_timestamp"
+# the culler's bookkeeping, rewritten on every check of every running notebook
+# (kf/controllers/culling_controller.go:171-196); no reconciler reads them, and the StatefulSet
+# generator never copies them into the pod template (keys containing "notebook",
+# kf/controllers/notebook_controller.go:488), so a change to these alone is not a reason to
+# reconcile or to run the admission pipeline
+CULLER_HEARTBEAT_ANNOTATIONS = frozenset({LAST_ACTIVITY_ANNOTATION, LAST_ACTIVITY_CHECK_TIMESTAMP_ANNOTATION})
 ANNOTATION_REWRITE_URI = "notebooks.kubeflow.org/http-rewrite-uri"
 ANNOTATION_HEADERS_REQUEST_SET = "notebooks.kubeflow.org/http-headers-request-set"
 ANNOTATION_NOTEBOOK_RESTART = "notebooks.opendatahub.io/notebook-restart"

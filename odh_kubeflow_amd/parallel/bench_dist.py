@@ -306,8 +306,8 @@ async def _burst(args, shard, dist, native, children: dict, use_odh: bool, tag: 
     adm0 = (await safe(native.admissions(1 << 62), {})).get("seq") if native is not None else None
     wh0 = {k: {"served": d["served"], "gets": d.get("gets", 0)}
            for k, d in ((await safe(shard.webhook_timings(), {})) or {}).items()} if shard.cfg.launch else {}
-    cpu0 = {kk: _proc_cpu_s(pid) for kk, pid in children.items()}
     prof0 = await safe(_apiserver_prof(native))
+    cpu0 = _cpu_snapshot(children, prof0)
     gc0 = {k: v["seq"] for k, v in ((await safe(shard.gc_pauses(), {})) or {}).items()} if shard.procs else {}
     await _in_thread(dist.barrier)
     t0 = time.perf_counter()
@@ -333,11 +333,13 @@ async def _burst(args, shard, dist, native, children: dict, use_odh: bool, tag: 
     ok = bool(await safe(shard.wait_until(check, 180), False))
     all_ready = max(ready_at.values()) - t0 if ready_at else None
     await _in_thread(dist.barrier)
-    cpu = {kk: (_proc_cpu_s(pid) or 0.0) - (cpu0.get(kk) or 0.0) for kk, pid in children.items()
+    prof1 = await safe(_apiserver_prof(native))
+    cpu1 = _cpu_snapshot(children, prof1)
+    cpu = {kk: (cpu1.get(kk) or 0.0) - (cpu0.get(kk) or 0.0) for kk in children
            if cpu0.get(kk) is not None}
     adm = ((await safe(native.admissions(adm0), {})).get("us") or []) if native is not None and adm0 is not None else []
     # the apiserver over the burst: store-lock waits per resource, malloc_trim passes
-    prof = _prof_per_step(prof0, await safe(_apiserver_prof(native)), 1) if native is not None else None
+    prof = _prof_per_step(prof0, prof1, 1) if native is not None else None
     # the control-plane processes' cyclic-GC pauses over the burst (their event loops stop)
     gcp = {k: [x[1:] for x in v["pauses"]] for k, v in ((await safe(shard.gc_pauses(gc0), {})) or {}).items()} \
         if shard.procs else {}
@@ -431,15 +433,22 @@ def io_per_notebook(parts: list, notebooks: int) -> dict:
 
 
 def _proc_cpu_s(pid: Optional[int]) -> Optional[float]:
-    """User + system CPU seconds of a child process (``/proc/<pid>/stat``), None if unreadable."""
-    if pid is None:
-        return None
-    try:
-        with open(f"/proc/{pid}/stat") as f:
-            fields = f.read().rsplit(")", 1)[1].split()
-        return (int(fields[11]) + int(fields[12])) / os.sysconf("SC_CLK_TCK")
-    except (OSError, IndexError, ValueError):
-        return None
+    """CPU seconds of a child process, summed over its threads to the nanosecond
+    (:func:`~odh_kubeflow_amd.utils.procutil.proc_cpu_ns`), None if unreadable."""
+    from ..utils.procutil import proc_cpu_ns
+
+    ns = proc_cpu_ns(pid)
+    return None if ns is None else ns / 1e9
+
+
+def _cpu_snapshot(children: dict, prof: Optional[dict]) -> dict:
+    """CPU seconds of every child process; the native apiserver's from its own
+    ``CLOCK_PROCESS_CPUTIME_ID`` (``process_cpu_ns`` of its profile), which keeps the time of
+    connection threads that have exited (it runs one thread per connection)."""
+    out = {k: _proc_cpu_s(pid) for k, pid in children.items()}
+    if prof and prof.get("process_cpu_ns") is not None and "apiserver" in out:
+        out["apiserver"] = prof["process_cpu_ns"] / 1e9
+    return out
 
 
 def _proc_rss_mib(pid: Optional[int]) -> Optional[float]:
@@ -673,8 +682,8 @@ async def _drive(args, shard, dist, torch, children: Optional[dict] = None, nati
     b0 = await shard.reconcile_breakdown()
     io0 = await shard.io_counters()
     children = children or {}
-    child_cpu0 = {k: _proc_cpu_s(pid) for k, pid in children.items()}
     prof0 = await _apiserver_prof(native)
+    child_cpu0 = _cpu_snapshot(children, prof0)
     cpu0 = time.process_time()
     t_start = time.perf_counter()
     for _ in range(args.steps):
@@ -697,10 +706,12 @@ async def _drive(args, shard, dist, torch, children: Optional[dict] = None, nati
     snap_lag = time.perf_counter() - t_start - elapsed
     in_window = breakdown_delta(b0, b1)
     cpu = {"rank": time.process_time() - cpu0}
-    prof = _prof_per_step(prof0, await _apiserver_prof(native), args.steps)
+    prof1 = await _apiserver_prof(native)
+    prof = _prof_per_step(prof0, prof1, args.steps)
+    child_cpu1 = _cpu_snapshot(children, prof1)
     rss = {}
     for k, pid in children.items():
-        c1 = _proc_cpu_s(pid)
+        c1 = child_cpu1.get(k)
         if c1 is not None and child_cpu0.get(k) is not None:
             cpu[k] = c1 - child_cpu0[k]
         r = _proc_rss_mib(pid)

@@ -80,14 +80,42 @@ def annotations_changed(etype: str, obj: dict, old: Optional[dict]) -> bool:
     return m.annotations(obj) != m.annotations(old)
 
 
-def generation_or_metadata_changed(etype: str, obj: dict, old: Optional[dict]) -> bool:
-    """Skip pure status writes: spec (generation), labels, annotations, finalizers, deletion."""
-    if etype != "MODIFIED" or old is None:
-        return True
-    om, nm = old.get("metadata") or {}, obj.get("metadata") or {}
-    return (om.get("generation") != nm.get("generation") or om.get("labels") != nm.get("labels")
-            or om.get("annotations") != nm.get("annotations") or om.get("finalizers") != nm.get("finalizers")
-            or om.get("deletionTimestamp") != nm.get("deletionTimestamp"))
+_MISSING = object()
+
+
+def maps_differ(a: Optional[dict], b: Optional[dict], ignore: frozenset = frozenset()) -> bool:
+    """``a != b`` for two string maps (labels, annotations), not counting the keys in ``ignore``."""
+    if a == b:
+        return False
+    a, b = a or {}, b or {}
+    if not ignore:
+        return a != b
+    for k in a.keys() | b.keys():
+        if k not in ignore and a.get(k, _MISSING) != b.get(k, _MISSING):
+            return True
+    return False
+
+
+def metadata_changed(ignore_annotations: Iterable[str] = ()) -> Predicate:
+    """Skip pure status writes: pass spec (generation), labels, annotations, finalizers and
+    deletion changes.  ``ignore_annotations``: annotation keys whose changes alone do not
+    pass — bookkeeping another controller rewrites that the reconcile never reads (the
+    culler's activity heartbeat, :data:`~odh_kubeflow_amd.models.notebook.CULLER_HEARTBEAT_ANNOTATIONS`)."""
+    ignore = frozenset(ignore_annotations)
+
+    def p(etype: str, obj: dict, old: Optional[dict]) -> bool:
+        if etype != "MODIFIED" or old is None:
+            return True
+        om, nm = old.get("metadata") or {}, obj.get("metadata") or {}
+        return (om.get("generation") != nm.get("generation") or om.get("labels") != nm.get("labels")
+                or maps_differ(om.get("annotations"), nm.get("annotations"), ignore)
+                or om.get("finalizers") != nm.get("finalizers")
+                or om.get("deletionTimestamp") != nm.get("deletionTimestamp"))
+
+    return p
+
+
+generation_or_metadata_changed = metadata_changed()
 
 
 def _path(obj: Optional[dict], path):

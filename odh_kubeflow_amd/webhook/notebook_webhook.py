@@ -85,6 +85,40 @@ def validate_gpu_resources(nb: dict) -> None:
                                       f"{GPU_RESOURCE} limit of {lim}")
 
 
+_HEARTBEAT_META_SKIP = frozenset({"annotations", "resourceVersion", "managedFields", "generation"})
+
+
+def culler_heartbeat_only(nb: dict, old: Optional[dict]) -> bool:
+    """An UPDATE of a running notebook whose only change is the culler's activity bookkeeping
+    (``CULLER_HEARTBEAT_ANNOTATIONS``; the culler writes it on every check of every notebook,
+    ``kf/controllers/culling_controller.go:171-196``).
+
+    For such an update the reference's pipeline can only end one of two ways: its mutations
+    leave the pod template alone, or the restart guard reverts them (the notebook runs and the
+    culler did not touch the template, :505-564) — apart from refreshing
+    ``update-pending``, the response is empty.  It is answered without running the pipeline,
+    so R resident notebooks do not cost R admissions' worth of ConfigMap reads per check
+    period; ``update-pending`` is brought up to date by the next update that is not a
+    heartbeat.  A stopped or restarting notebook (no restart guard) always takes the full
+    pipeline."""
+    from ..controllers.odh.constants import ANNOTATION_NOTEBOOK_RESTART as RESTART
+    from ..models.notebook import CULLER_HEARTBEAT_ANNOTATIONS
+    from ..runtime.controller import maps_differ
+
+    if old is None:
+        return False
+    md, om = nb.get("metadata") or {}, old.get("metadata") or {}
+    ann, oann = md.get("annotations") or {}, om.get("annotations") or {}
+    if STOP_ANNOTATION in ann or RESTART in ann:
+        return False
+    if ann == oann or maps_differ(ann, oann, CULLER_HEARTBEAT_ANNOTATIONS):
+        return False  # no heartbeat change, or something else changed too
+    for k in md.keys() | om.keys():
+        if k not in _HEARTBEAT_META_SKIP and md.get(k) != om.get(k):
+            return False
+    return nb.get("spec") == old.get("spec")
+
+
 def inject_reconciliation_lock(nb: dict) -> None:
     m.ensure_annotations(nb)[STOP_ANNOTATION] = ANNOTATION_VALUE_RECONCILIATION_LOCK
 
@@ -174,6 +208,7 @@ class NotebookWebhook:
         self.env = env if env is not None else os.environ
         self.requests = 0
         self.denied = 0
+        self.heartbeats = 0  # culler heartbeat updates answered without the pipeline
 
     async def mutate(self, operation: str, nb: dict, old: Optional[dict], name: str = "",
                      namespace: str = "") -> dict:
@@ -274,6 +309,9 @@ class NotebookWebhook:
             if bad:  # the reference's typed decode (admission.Decoder) refuses these
                 raise AdmissionError(400, f"cannot decode Notebook: {bad}")
             old = req.get("oldObject") if isinstance(req.get("oldObject"), dict) else None
+            if req.get("operation") == "UPDATE" and culler_heartbeat_only(obj, old):
+                self.heartbeats += 1
+                return {"apiVersion": "admission.k8s.io/v1", "kind": "AdmissionReview", "response": resp}
             tok = CONFIRM_ABSENCE.set(set())  # one-shot decision: absent objects are confirmed live, once
             try:
                 mutated = await self.mutate(req.get("operation", ""), obj, old, req.get("name", ""),

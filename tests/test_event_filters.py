@@ -119,6 +119,45 @@ def test_kf_ignores_status_and_finalizer_edits_but_not_annotations(run):
     run(go())
 
 
+def test_culler_heartbeat_reconciles_nothing_but_stop_and_restart_do(run):
+    """The culler rewrites last-activity / last_activity_check_timestamp on every check of every
+    running notebook: neither the kf nor the odh Notebook watch passes that change alone, so R
+    resident notebooks cost no reconciles per check period.  The culler's STOP, the restart
+    annotation and any other annotation edit still pass."""
+    from odh_kubeflow_amd.models.notebook import LAST_ACTIVITY_ANNOTATION, LAST_ACTIVITY_CHECK_TIMESTAMP_ANNOTATION
+
+    async def go():
+        cfg = ClusterConfig(odh=True, webhook=True, env={"SET_PIPELINE_RBAC": "false", "SET_PIPELINE_SECRET": "false"})
+        async with LocalCluster(cfg) as cl:
+            await cl.ensure_namespace("user")
+            await cl.admin.create(notebook("nb1", "user", annotations={"notebooks.opendatahub.io/inject-auth": "true"}))
+            assert await cl.wait_for(lambda: cl.notebook_ready("nb1", "user"), 10)
+            assert await cl.settle()
+            kf, odh = cl.kf.controllers[0], cl.odh.controllers[0]
+            k0, o0 = kf.reconciles, odh.reconciles
+            for i in range(3):
+                await cl.admin.patch(kinds.NOTEBOOK, {"metadata": {"annotations": {
+                    LAST_ACTIVITY_ANNOTATION: "2026-01-01T00:00:00Z",
+                    LAST_ACTIVITY_CHECK_TIMESTAMP_ANNOTATION: f"2026-01-01T00:0{i}:00Z"}}}, name="nb1", namespace="user")
+            assert await cl.settle()
+            assert (kf.reconciles - k0, odh.reconciles - o0) == (0, 0)
+            # a heartbeat together with another annotation change passes both
+            await cl.admin.patch(kinds.NOTEBOOK, {"metadata": {"annotations": {
+                LAST_ACTIVITY_CHECK_TIMESTAMP_ANNOTATION: "2026-01-01T00:05:00Z", "x.io/other": "1"}}},
+                name="nb1", namespace="user")
+            assert await cl.settle()
+            assert kf.reconciles - k0 >= 1 and odh.reconciles - o0 >= 1
+            # restart: the pod is replaced; stop: the StatefulSet scales to 0
+            uid = m.uid(cl.store.peek(kinds.POD, "nb1-0", "user"))
+            await cl.admin.patch(kinds.NOTEBOOK, {"metadata": {"annotations": {
+                "notebooks.opendatahub.io/notebook-restart": "true"}}}, name="nb1", namespace="user")
+            assert await cl.wait_for(lambda: m.uid(cl.store.peek(kinds.POD, "nb1-0", "user") or {}) not in ("", uid), 10)
+            await cl.admin.patch(kinds.NOTEBOOK, {"metadata": {"annotations": {
+                "kubeflow-resource-stopped": "2026-01-01T00:06:00Z"}}}, name="nb1", namespace="user")
+            assert await cl.wait_for(lambda: cl.store.peek(kinds.STATEFUL_SET, "nb1", "user")["spec"]["replicas"] == 0)
+    run(go())
+
+
 def test_deleted_children_of_live_notebook_are_recreated(run):
     """Drift repair still works with the owner-alive delete filter (STS and Service)."""
     async def go():

@@ -14,7 +14,7 @@ import pytest
 from odh_kubeflow_amd import tracing
 from odh_kubeflow_amd.testing.apiserver.store import ObjectStore
 from odh_kubeflow_amd.controllers.odh import auth, feast, runtime_images
-from odh_kubeflow_amd.controllers.odh.constants import ANNOTATION_UPDATE_PENDING
+from odh_kubeflow_amd.controllers.odh.constants import ANNOTATION_NOTEBOOK_RESTART, ANNOTATION_UPDATE_PENDING
 from odh_kubeflow_amd.models import kinds
 from odh_kubeflow_amd.models import meta as m
 from odh_kubeflow_amd.models.notebook import notebook
@@ -355,6 +355,61 @@ def test_restart_guard_blocks_webhook_only_changes(run):
                           name="nb", namespace="user")
         nb = store.peek(kinds.NOTEBOOK, "nb", "user")
         assert "quay.io/brancz/kube-rbac-proxy:v0.20.0" in [c["image"] for c in nb["spec"]["template"]["spec"]["containers"]]
+    run(go())
+
+
+def test_culler_heartbeat_skips_the_pipeline_but_nothing_else_does(run):
+    """The culler's per-check write (last-activity / last_activity_check_timestamp only) on a
+    running notebook is admitted without the pipeline; any other change with it, or the same
+    write on a stopped or restarting notebook, takes the whole pipeline."""
+    from odh_kubeflow_amd.models.notebook import LAST_ACTIVITY_ANNOTATION, LAST_ACTIVITY_CHECK_TIMESTAMP_ANNOTATION
+    from odh_kubeflow_amd.webhook.notebook_webhook import culler_heartbeat_only
+
+    old = notebook("nb", "user", annotations={LAST_ACTIVITY_ANNOTATION: "2026-01-01T00:00:00Z",
+                                              LAST_ACTIVITY_CHECK_TIMESTAMP_ANNOTATION: "2026-01-01T00:00:00Z"})
+    old["metadata"]["resourceVersion"] = "5"
+    beat = json.loads(json.dumps(old))
+    beat["metadata"]["annotations"][LAST_ACTIVITY_CHECK_TIMESTAMP_ANNOTATION] = "2026-01-01T00:01:00Z"
+    beat["metadata"]["resourceVersion"] = "6"
+    assert culler_heartbeat_only(beat, old)
+    first = json.loads(json.dumps(old))  # the culler initialising its annotations
+    first["metadata"]["annotations"] = {}
+    assert culler_heartbeat_only(old, first)
+    assert not culler_heartbeat_only(old, json.loads(json.dumps(old)))  # no change at all: pipeline as usual
+    assert not culler_heartbeat_only(beat, None)
+    other = json.loads(json.dumps(beat))
+    other["metadata"]["annotations"]["notebooks.opendatahub.io/inject-auth"] = "true"
+    assert not culler_heartbeat_only(other, old)
+    lab = json.loads(json.dumps(beat))
+    lab["metadata"]["labels"] = {"x": "y"}
+    assert not culler_heartbeat_only(lab, old)
+    spec = json.loads(json.dumps(beat))
+    spec["spec"]["template"]["spec"]["containers"][0]["image"] = "other"
+    assert not culler_heartbeat_only(spec, old)
+    for key, val in (("kubeflow-resource-stopped", "2026-01-01T00:01:00Z"), (ANNOTATION_NOTEBOOK_RESTART, "true")):
+        o2, b2 = json.loads(json.dumps(old)), json.loads(json.dumps(beat))
+        o2["metadata"]["annotations"][key] = val
+        b2["metadata"]["annotations"][key] = val
+        assert not culler_heartbeat_only(b2, o2), key
+
+    async def go():
+        store, admin, wh = await _setup()
+        await admin.create(notebook("nb", "user", annotations={"notebooks.opendatahub.io/inject-auth": "true"}))
+        await admin.patch(kinds.NOTEBOOK, {"metadata": {"annotations": {"kubeflow-resource-stopped": None}}},
+                          name="nb", namespace="user")
+        n0, h0 = wh.requests, wh.heartbeats
+        await admin.patch(kinds.NOTEBOOK, {"metadata": {"annotations": {
+            LAST_ACTIVITY_ANNOTATION: "2026-01-01T00:00:00Z",
+            LAST_ACTIVITY_CHECK_TIMESTAMP_ANNOTATION: "2026-01-01T00:00:00Z"}}}, name="nb", namespace="user")
+        assert (wh.requests - n0, wh.heartbeats - h0) == (1, 1)
+        # the restart guard still runs on the next real update
+        wh.kube_rbac_proxy_image = "quay.io/brancz/kube-rbac-proxy:v0.19.0"
+        await admin.patch(kinds.NOTEBOOK, {"metadata": {"annotations": {
+            LAST_ACTIVITY_CHECK_TIMESTAMP_ANNOTATION: "2026-01-01T00:01:00Z"}}}, name="nb", namespace="user")
+        assert ANNOTATION_UPDATE_PENDING not in m.annotations(store.peek(kinds.NOTEBOOK, "nb", "user"))
+        await admin.patch(kinds.NOTEBOOK, {"metadata": {"labels": {"x": "y"}}}, name="nb", namespace="user")
+        assert "v0.19.0" in m.annotations(store.peek(kinds.NOTEBOOK, "nb", "user"))[ANNOTATION_UPDATE_PENDING]
+        assert wh.heartbeats - h0 == 2
     run(go())
 
 

@@ -101,6 +101,19 @@ def parse(argv=None):
     p.add_argument("--no-configs", action="store_true",
                    help="skip the BASELINE configs #2-#5 sample that follows the N=1 run (real workbench "
                         "processes, the webhook path across 8, GPU-busy culling across 8)")
+    p.add_argument("--no-culling", action="store_true",
+                   help="run the control plane without the culler (the MI355X overlays ship it on: "
+                        "ENABLE_CULLING=true, CULLING_ACTIVITY_SOURCE=combined)")
+    p.add_argument("--culling-period", type=float, default=1.0,
+                   help="the culler's check period in seconds (IDLENESS_CHECK_PERIOD_SECONDS; the overlays' "
+                        "is 60): every resident notebook is checked, and its Notebook written, once per period")
+    p.add_argument("--resident", type=int, default=256,
+                   help="after the window: this many notebooks created and left running with the culler on "
+                        "(the reference's loadtest scenario); reported: the control plane's cost at rest and "
+                        "new notebooks' create->Ready on top of them (0: skip)")
+    p.add_argument("--resident-window", type=float, default=3.0, help="seconds measured at rest")
+    p.add_argument("--resident-steps", type=int, default=20,
+                   help="closed-loop lifecycles per rank on top of the resident population")
     p.add_argument("--json-out", default=None)
     return p.parse_args(argv)
 

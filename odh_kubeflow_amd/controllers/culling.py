@@ -79,6 +79,7 @@ DEFAULT_CULL_IDLE_TIME = "1440"
 DEFAULT_IDLENESS_CHECK_PERIOD = "1"
 DEFAULT_CLUSTER_DOMAIN = "cluster.local"
 KERNEL_IDLE, KERNEL_BUSY, KERNEL_STARTING = "idle", "busy", "starting"
+_ABSENT = object()
 
 
 def env_default(env: Mapping[str, str], key: str, default: str) -> str:
@@ -93,6 +94,7 @@ class CullerConfig:
     enable_culling: bool = False
     cluster_domain: str = DEFAULT_CLUSTER_DOMAIN
     dev: bool = False
+    dev_proxy_url: str = "http://localhost:8001"  # DEV mode: the kubectl proxy the culler goes through
     activity_source: str = "jupyter"
     gpu_busy_threshold: float = 5.0
     gpu_agent_port: int = 9464
@@ -110,6 +112,7 @@ class CullerConfig:
         a bad IDLENESS_CHECK_PERIOD is an error."""
         c = cls()
         c.dev = env_default(env, "DEV", "false") == "true"
+        c.dev_proxy_url = env_default(env, "CULLER_DEV_PROXY_URL", c.dev_proxy_url).rstrip("/")
         raw = env_default(env, "CULL_IDLE_TIME", DEFAULT_CULL_IDLE_TIME)
         try:
             c.cull_idle_time_s = int(raw) * 60.0
@@ -329,17 +332,27 @@ class JupyterActivity:
     """``getNotebookApiKernels`` / ``getNotebookApiTerminals`` over HTTP (10 s timeout).
 
     ``url_for(nb_name, namespace, resource, pod)`` may be overridden; by default it is the
-    in-cluster Service URL, or the ``kubectl proxy`` URL in ``DEV`` mode (:243-273).  With
+    in-cluster Service URL, or the ``kubectl proxy`` URL in ``DEV`` mode (:243-273; the proxy's
+    address is ``CULLER_DEV_PROXY_URL``, default ``http://localhost:8001`` as in the reference).  With
     ``use_pod_endpoint`` the node agent's ``amd.com/notebook-endpoint`` pod annotation is
     used (the in-process runtime serves the Jupyter API on an ephemeral port).
     """
 
+    # plain-HTTP Jupyter endpoints go through lean keep-alive pools (runtime/http1.py: ~4x less
+    # CPU per request than aiohttp, which matters when R notebooks are checked every period);
+    # one pool per endpoint host, the least recently used dropped beyond MAX_POOLS
+    MAX_POOLS = 256
+    POOL_SIZE = 4
+
     def __init__(self, cfg: CullerConfig, url_for: Optional[Callable[..., str]] = None,
                  use_pod_endpoint: bool = False):
+        from collections import OrderedDict
+
         self.cfg = cfg
         self.url_for = url_for or self.default_url
         self.use_pod_endpoint = use_pod_endpoint
         self._session = None
+        self._pools: "OrderedDict[str, Any]" = OrderedDict()
         self.requests = 0
 
     def default_url(self, nm: str, ns: str, resource: str, pod: Optional[dict] = None) -> str:
@@ -348,22 +361,45 @@ class JupyterActivity:
             if ep:
                 return f"http://{ep}/notebook/{ns}/{nm}/api/{resource}"
         if self.cfg.dev:
-            return (f"http://localhost:8001/api/v1/namespaces/{ns}/services/{nm}:http-{nm}/proxy/notebook/"
+            return (f"{self.cfg.dev_proxy_url}/api/v1/namespaces/{ns}/services/{nm}:http-{nm}/proxy/notebook/"
                     f"{ns}/{nm}/api/{resource}")
         return f"http://{nm}.{ns}.svc.{self.cfg.cluster_domain}/notebook/{ns}/{nm}/api/{resource}"
 
-    async def _get(self, url: str) -> Optional[Any]:
-        import aiohttp
+    def _pool(self, url: str):
+        from urllib.parse import urlsplit
 
-        if self._session is None or self._session.closed:
-            self._session = aiohttp.ClientSession(timeout=aiohttp.ClientTimeout(total=self.cfg.http_timeout_s))
+        from ..runtime.http1 import Http1Pool
+
+        u = urlsplit(url)
+        key = u.netloc
+        pool = self._pools.get(key)
+        if pool is None:
+            pool = self._pools[key] = Http1Pool(f"http://{key}", size=self.POOL_SIZE)
+            while len(self._pools) > self.MAX_POOLS:
+                _k, old = self._pools.popitem(last=False)
+                asyncio.ensure_future(old.close())
+        else:
+            self._pools.move_to_end(key)
+        target = u.path + (f"?{u.query}" if u.query else "")
+        return pool, target
+
+    async def _get(self, url: str) -> Optional[Any]:
         self.requests += 1
         try:
-            async with self._session.get(url) as resp:
-                if resp.status != 200:
-                    log.info("Warning: GET to %s: %d", url, resp.status)
-                    return None
-                return json.loads(await resp.read())
+            if url.startswith("http://"):
+                pool, target = self._pool(url)
+                status, body = await asyncio.wait_for(pool.request("GET", target), self.cfg.http_timeout_s)
+            else:
+                import aiohttp
+
+                if self._session is None or self._session.closed:
+                    self._session = aiohttp.ClientSession(timeout=aiohttp.ClientTimeout(total=self.cfg.http_timeout_s))
+                async with self._session.get(url) as resp:
+                    status, body = resp.status, await resp.read()
+            if status != 200:
+                log.info("Warning: GET to %s: %d", url, status)
+                return None
+            return json.loads(body)
         except (asyncio.TimeoutError, OSError, ValueError, Exception) as e:  # noqa: B014 - any failure is "no data"
             log.debug("GET %s failed: %r", url, e)
             return None
@@ -377,6 +413,9 @@ class JupyterActivity:
     async def close(self) -> None:
         if self._session is not None:
             await self._session.close()
+        for pool in self._pools.values():
+            await pool.close()
+        self._pools.clear()
 
 
 class GpuActivity:
@@ -535,21 +574,52 @@ class CullingReconciler:
         # "jupyter" = the kernel/terminal activity, also when the GPU had no sample)
         self.cull_log = deque(maxlen=1024)
 
+    def _cached(self, kind, name: str, namespace: str) -> Optional[dict]:
+        """The informer's copy, zero-copy and read-only (None when this process's cache does not
+        hold ``namespace``: the caller reads through the client instead)."""
+        covers = getattr(self.reader, "covers", None)
+        if covers is not None and not covers(kind, namespace):
+            return None
+        return self.reader.get(kind, name, namespace)
+
+    async def _read(self, kind, name: str, namespace: str) -> Optional[dict]:
+        covers = getattr(self.reader, "covers", None)
+        if covers is not None and covers(kind, namespace):
+            return self.reader.get(kind, name, namespace)
+        return await self.client.get_or_none(kind, name, namespace)
+
     async def _update(self, req: Request, mutate: Callable[[dict], None]) -> None:
+        """``RetryOnConflict{Get; mutate; Update}`` (:106-112, :171-196), written as a merge patch
+        of the annotations the culler changed, preconditioned on the resourceVersion it read —
+        the same optimistic concurrency as the reference's Update, without re-sending (and the
+        apiserver re-validating) the whole pod template on every check of every notebook.  A
+        mutation that changes nothing writes nothing (kube-apiserver skips no-op updates too)."""
+        from ..runtime.client import LIVE_READS
+
         async def fn():
-            cur = await self.client.get(kinds.NOTEBOOK_V1BETA1, req.name, req.namespace)
-            mutate(cur)
-            await self.client.update(cur)
+            cur = None if LIVE_READS.get() else self._cached(kinds.NOTEBOOK_V1BETA1, req.name, req.namespace)
+            if cur is None:
+                cur = await self.client.get(kinds.NOTEBOOK_V1BETA1, req.name, req.namespace)
+            md = cur.get("metadata") or {}
+            before = md.get("annotations") or {}
+            view = {"metadata": {"name": md.get("name"), "namespace": md.get("namespace"),
+                                 "annotations": dict(before)}}
+            mutate(view)
+            after = view["metadata"].get("annotations") or {}
+            diff = {k: v for k, v in after.items() if before.get(k, _ABSENT) != v}
+            diff.update({k: None for k in before if k not in after})
+            if not diff:
+                return
+            await self.client.patch(kinds.NOTEBOOK_V1BETA1,
+                                    {"metadata": {"resourceVersion": md.get("resourceVersion"), "annotations": diff}},
+                                    "merge", name=req.name, namespace=req.namespace)
 
         await retry_on_conflict(fn)
 
     async def reconcile(self, req: Request) -> Result:
-        try:
-            nb = await self.client.get(kinds.NOTEBOOK_V1BETA1, req.name, req.namespace)
-        except ApiError as e:
-            if is_not_found(e):
-                return Result()
-            raise
+        nb = await self._read(kinds.NOTEBOOK_V1BETA1, req.name, req.namespace)
+        if nb is None:
+            return Result()
         if m.is_deleting(nb):
             return Result()
         if stop_annotation_is_set(nb):
@@ -557,7 +627,7 @@ class CullingReconciler:
                     LAST_ACTIVITY_ANNOTATION, LAST_ACTIVITY_CHECK_TIMESTAMP_ANNOTATION)):
                 await self._update(req, remove_annotations)
             return Result()
-        pod = await self.client.get_or_none(kinds.POD, m.name(nb) + "-0", req.namespace)
+        pod = await self._read(kinds.POD, m.name(nb) + "-0", req.namespace)
         if pod is None:
             if any(k in m.annotations(nb) for k in (LAST_ACTIVITY_ANNOTATION, LAST_ACTIVITY_CHECK_TIMESTAMP_ANNOTATION)):
                 await self._update(req, remove_annotations)
@@ -581,7 +651,9 @@ class CullingReconciler:
             born = pod_created_at(pod) if starting else None
             await self._update(req, lambda cur: initialize_annotations(
                 cur, rfc3339(born) if born is not None else None))
-            nb = await self.client.get(kinds.NOTEBOOK_V1BETA1, req.name, req.namespace)
+            nb = await self._read(kinds.NOTEBOOK_V1BETA1, req.name, req.namespace)
+            if nb is None:
+                return Result()
         if not culling_check_period_has_passed(nb, self.cfg.check_period_s):
             return Result(requeue_after=self.cfg.check_period_s)
 

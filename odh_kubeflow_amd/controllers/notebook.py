@@ -49,7 +49,7 @@ from ..models.notebook import (ANNOTATION_HEADERS_REQUEST_SET, ANNOTATION_NOTEBO
                                CULLER_HEARTBEAT_ANNOTATIONS, DEFAULT_CONTAINER_PORT, DEFAULT_FS_GROUP,
                                DEFAULT_SERVING_PORT, GPU_RESOURCE, MAX_STATEFULSET_NAME_LENGTH, NOTEBOOK_NAME_LABEL,
                                PREFIX_ENV_VAR, STATEFULSET_LABEL, STOP_ANNOTATION, WORKBENCH_LABEL, gpu_request,
-                               pod_cond_to_notebook_cond)
+                               heartbeat_filter_enabled, pod_cond_to_notebook_cond)
 from ..runtime.controller import Request, Result, controller_owner_alive, fields_changed, maps_differ, pred_funcs
 from ..utils.objutil import deepcopy_json
 from ..utils.reconcilehelper import copy_service_fields, copy_statefulset_fields, copy_virtual_service
@@ -554,7 +554,8 @@ class NotebookReconciler:
                     return True
                 # the culler's per-check heartbeat alone changes nothing this reconcile
                 # reads or generates (the STS template never carries "notebook" keys, :488)
-                return maps_differ(m.annotations(old), m.annotations(o), CULLER_HEARTBEAT_ANNOTATIONS)
+                return maps_differ(m.annotations(old), m.annotations(o), ignore)
+            ignore = CULLER_HEARTBEAT_ANNOTATIONS if heartbeat_filter_enabled(self.env) else frozenset()
             nb_preds = [pred_funcs(update=nb_update, delete=lambda o: False)]
             sts_drift = fields_changed(*drift)
 

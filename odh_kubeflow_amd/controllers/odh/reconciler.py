@@ -45,7 +45,7 @@ from typing import Dict, List, Mapping, Optional
 from ...models import kinds
 from ...models import meta as m
 from ...models.errors import ApiError, is_no_match, is_not_found
-from ...models.notebook import CULLER_HEARTBEAT_ANNOTATIONS
+from ...models.notebook import CULLER_HEARTBEAT_ANNOTATIONS, heartbeat_filter_enabled
 from ...runtime.controller import (Request, Result, controller_owner_alive, fields_changed,
                                    generation_or_metadata_changed, metadata_changed)
 from ...runtime.retry import retry_on_conflict
@@ -439,7 +439,8 @@ class OpenshiftNotebookReconciler:
         alive, svc_preds, route_preds, nb_preds = [], [], [], [generation_or_metadata_changed]
         if not self.blocking_lock_removal:
             # the culler's per-check heartbeat annotations are read by nothing here
-            nb_preds = [metadata_changed(ignore_annotations=CULLER_HEARTBEAT_ANNOTATIONS)]
+            if heartbeat_filter_enabled(self.env):
+                nb_preds = [metadata_changed(ignore_annotations=CULLER_HEARTBEAT_ANNOTATIONS)]
             # a deleted Notebook's finalizers already ran: its DELETED event has nothing left
             nb_preds.append(lambda etype, o, old: etype != "DELETED")  # the reference-emulation runs keep every event
             # GC of a deleted Notebook's children queues nothing; a child deleted under a live

@@ -180,7 +180,9 @@ async def reconcile_reference_grant(client, nb: dict, central_namespace: str) ->
 
 
 async def is_last_notebook_in_namespace(client, nb: dict) -> bool:
-    for other in await client.list(kinds.NOTEBOOK, m.namespace(nb)):
+    from ...runtime.client import list_readonly
+
+    for other in await list_readonly(client, kinds.NOTEBOOK, m.namespace(nb)):
         if m.name(other) != m.name(nb) and not m.is_deleting(other):
             return False
     return True

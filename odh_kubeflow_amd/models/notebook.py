@@ -35,6 +35,15 @@ LAST_ACTIVITY_CHECK_TIMESTAMP_ANNOTATION = "notebooks.kubeflow.org/last_activity
 # kf/controllers/notebook_controller.go:488), so a change to these alone is not a reason to
 # reconcile or to run the admission pipeline
 CULLER_HEARTBEAT_ANNOTATIONS = frozenset({LAST_ACTIVITY_ANNOTATION, LAST_ACTIVITY_CHECK_TIMESTAMP_ANNOTATION})
+
+
+def heartbeat_filter_enabled(env) -> bool:
+    """``ODH_HEARTBEAT_FILTER=false`` turns the heartbeat filtering off (every culler write then
+    reconciles kf and odh and runs the admission pipeline, as in the reference) — for A/B
+    measurements only."""
+    return (env.get("ODH_HEARTBEAT_FILTER") or "true").strip().lower() != "false"
+
+
 ANNOTATION_REWRITE_URI = "notebooks.kubeflow.org/http-rewrite-uri"
 ANNOTATION_HEADERS_REQUEST_SET = "notebooks.kubeflow.org/http-headers-request-set"
 ANNOTATION_NOTEBOOK_RESTART = "notebooks.opendatahub.io/notebook-restart"

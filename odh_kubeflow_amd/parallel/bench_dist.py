@@ -91,6 +91,24 @@ def shard_load(counts: dict, owner: dict, cpu_s: dict, elapsed: float, by: str,
             "max_over_mean_notebooks": round(max(loads) / mean, 3) if mean else None}
 
 
+def culling_enabled(args) -> bool:
+    """The MI355X overlays ship the culler on (``ENABLE_CULLING=true``,
+    ``CULLING_ACTIVITY_SOURCE=combined``), so the benchmark runs it unless ``--no-culling``."""
+    return not getattr(args, "no_culling", False)
+
+
+def culler_env(args, proxy_url: Optional[str]) -> dict:
+    """The overlays' culler settings with a scaled check period; its Jupyter requests go
+    through the platform's kubectl-proxy stand-in (DEV mode, ``testing/cmd/jupyter_proxy.py``).
+    No node-agent CA is configured, so the amdgpu half of ``combined`` has no samples and the
+    Jupyter signal decides (the GPU signal is config #5's)."""
+    env = {"ENABLE_CULLING": "true", "CULLING_ACTIVITY_SOURCE": "combined",
+           "IDLENESS_CHECK_PERIOD_SECONDS": f"{getattr(args, 'culling_period', 1.0):g}"}
+    if proxy_url:
+        env.update(DEV="true", CULLER_DEV_PROXY_URL=proxy_url)
+    return env
+
+
 def _dist_init():
     import torch
     import torch.distributed as dist
@@ -212,6 +230,10 @@ def measure(args) -> Optional[dict]:
             out["gpu_probe_init_container"] = probe_report(res["probe_sample"], out.get("p50_ready_ms"))
         if res.get("burst"):
             out["burst"] = res["burst"]
+        if res.get("resident"):
+            out["resident"] = res["resident"]
+        out["config"]["culling"] = (f"on (overlay settings, check period {getattr(args, 'culling_period', 1.0):g} s)"
+                                    if culling_enabled(args) else "off")
         if res.get("shard_load"):
             out["shard_load"] = res["shard_load"]
         out["config"]["namespaces_per_rank"] = max(1, getattr(args, "namespaces_per_rank", 1))
@@ -392,6 +414,182 @@ async def _burst(args, shard, dist, native, children: dict, use_odh: bool, tag: 
     }
 
 
+async def _resident(args, shard, dist, native, children: dict, use_odh: bool,
+                    empty_p50_ms: Optional[float]) -> Optional[dict]:
+    """A steady state with a population: the reference's load tool applies N
+    notebooks and leaves them running (``kf/loadtest/start_notebooks.py:76-95``), and its culler
+    rewrites every Notebook's ``last_activity_check_timestamp`` once per check period
+    (``kf/controllers/culling_controller.go:171-196``).  ``--resident R`` notebooks (split over the
+    ranks, CPU workbenches whose Jupyter servers report an idle kernel, the odh auth/route path
+    like the timed ones) are created and left Ready with the culler checking each every
+    ``--culling-period`` s; then
+
+    * **at rest** (``--resident-window`` s, nothing else happening): each process's CPU per
+      second, culler checks / heartbeat writes / admissions per second, reconciles per second
+      by controller and trigger (the kf and odh reconciles triggered by Notebook events must be
+      0: the heartbeat passes neither's predicate), watch events per second, RSS;
+    * **on top** (``--resident-steps`` per rank): new notebooks' create→Ready, closed loop like
+      the timed window, against the window's empty-cluster p50.
+
+    Untimed; failures are reported in the block, never raised (every rank reaches every
+    collective)."""
+    from bench import breakdown_delta  # noqa: E402  (bench.py is the entry point)
+
+    from ..models import kinds
+    from ..models.notebook import LAST_ACTIVITY_CHECK_TIMESTAMP_ANNOTATION, notebook
+
+    rank, world = dist.get_rank(), dist.get_world_size()
+    total = int(args.resident)
+    k = total // world + (1 if rank < total % world else 0)
+    nss = shard.cfg.user_namespaces
+    names = [f"res-{rank}-{i}" for i in range(k)]
+    ns_of = {nm: nss[i % len(nss)] for i, nm in enumerate(names)}
+    ann = {"notebooks.opendatahub.io/inject-auth": "true"} if use_odh else None
+    errors: list = []
+
+    async def safe(aw, default=None):
+        try:
+            return await aw
+        except Exception as e:  # noqa: BLE001 — recorded in the block
+            errors.append(f"rank {rank}: {e!r}"[:300])
+            return default
+
+    sem = asyncio.Semaphore(32)
+
+    async def create(nm):
+        nb = notebook(nm, ns_of[nm], image=NOTEBOOK_IMAGE, annotations=ann)
+        c = nb["spec"]["template"]["spec"]["containers"][0]
+        # small requests: R of them must fit the one node (256 cores) next to the timed GPU pods
+        c.setdefault("resources", {}).setdefault("requests", {}).update({"cpu": "50m", "memory": "256Mi"})
+        async with sem:
+            await shard.admin.create(nb)
+
+    def all_ready() -> bool:
+        return all(shard.notebook_ready(nm, ns_of[nm]) for nm in names)
+
+    def all_checked() -> bool:  # the culler has initialised every resident notebook's annotations
+        for nm in names:
+            nb = shard.peek(kinds.NOTEBOOK, nm, ns_of[nm])
+            if nb is None or LAST_ACTIVITY_CHECK_TIMESTAMP_ANNOTATION not in ((nb.get("metadata") or {})
+                                                                             .get("annotations") or {}):
+                return False
+        return True
+
+    await safe(shard.quiesce())
+    await _in_thread(dist.barrier)
+    t0 = time.perf_counter()
+    await safe(asyncio.gather(*(create(nm) for nm in names)))
+    ok = bool(await safe(shard.wait_until(all_ready, 300), False))
+    fill_s = time.perf_counter() - t0
+    ok = ok and bool(await safe(shard.wait_until(all_checked, 120), False))
+    await asyncio.sleep(2 * getattr(args, "culling_period", 1.0))  # every notebook's checks under way
+    await _in_thread(dist.barrier)
+
+    # ---- at rest
+    prof0 = await safe(_apiserver_prof(native))
+    cpu0 = _cpu_snapshot(children, prof0)
+    b0 = await safe(shard.reconcile_breakdown(include_all=True), {})
+    io0 = await safe(shard.io_counters(), {})
+    adm0 = (await safe(native.admissions(1 << 62), {})).get("seq") if native is not None else None
+    wh0 = await safe(shard.webhook_timings(), {}) if shard.cfg.launch else {}
+    r0 = time.perf_counter()
+    await asyncio.sleep(max(0.5, getattr(args, "resident_window", 3.0)))
+    prof1 = await safe(_apiserver_prof(native))
+    cpu1 = _cpu_snapshot(children, prof1)
+    win = time.perf_counter() - r0
+    b1 = await safe(shard.reconcile_breakdown(include_all=True), {})
+    io1 = await safe(shard.io_counters(), {})
+    adm1 = (await safe(native.admissions(1 << 62), {})).get("seq") if native is not None else None
+    wh1 = await safe(shard.webhook_timings(), {}) if shard.cfg.launch else {}
+    rss = {kk: _proc_rss_mib(pid) for kk, pid in children.items()}
+    cpu = {kk: (cpu1.get(kk) or 0.0) - (cpu0.get(kk) or 0.0) for kk in children if cpu0.get(kk) is not None}
+    rest_prof = _prof_per_step(prof0, prof1, 1) if prof0 and prof1 else None
+    heartbeats = sum((d.get("heartbeats") or 0) - ((wh0.get(p) or {}).get("heartbeats") or 0)
+                     for p, d in (wh1 or {}).items())
+    served = sum((d.get("served") or 0) - ((wh0.get(p) or {}).get("served") or 0) for p, d in (wh1 or {}).items())
+    await _in_thread(dist.barrier)
+
+    # ---- new notebooks on top of the population
+    lat = []
+    base = dict(ann or {})
+    for i in range(max(0, int(getattr(args, "resident_steps", 20)))):
+        r = await safe(_lifecycle(shard, f"nb-res-{i}", dict(base) or None, ns=nss[i % len(nss)]))
+        if r is None:
+            break
+        lat.append(r[0] * 1e3)
+    await _in_thread(dist.barrier)
+
+    # ---- teardown
+    t_del = time.perf_counter()
+
+    async def delete(nm):
+        async with sem:
+            await shard.admin.delete(kinds.NOTEBOOK, nm, ns_of[nm])
+    await safe(asyncio.gather(*(delete(nm) for nm in names), return_exceptions=True))
+    gone = bool(await safe(shard.wait_until(lambda: all(shard.gone(nm, ns_of[nm]) for nm in names), 300), False))
+    teardown = time.perf_counter() - t_del
+    gathered = [None] * world
+    await _in_thread(dist.all_gather_object, gathered, {
+        "k": k, "ok": ok and gone, "fill_s": fill_s, "win": win, "cpu": cpu, "rss": rss, "lat": lat,
+        "in_window": breakdown_delta(b0 or {}, b1 or {}), "io": io_delta(io0 or {}, io1 or {}), "prof": rest_prof,
+        "adm": (adm1 - adm0) if adm0 is not None and adm1 is not None else None, "heartbeats": heartbeats,
+        "served": served, "teardown": teardown, "errors": errors})
+    if rank != 0:
+        return None
+    win = max(g["win"] for g in gathered)
+    per_s = 1.0 / win
+    cpu_all: dict = {}
+    for g in gathered:
+        for kk, v in g["cpu"].items():
+            cpu_all[kk] = cpu_all.get(kk, 0.0) + v
+    recon: dict = {}
+    for g in gathered:
+        for ctrl, trig in g["in_window"].items():
+            o = recon.setdefault(ctrl, {})
+            for kk, v in trig.items():
+                o[kk] = o.get(kk, 0) + v
+    io = io_per_notebook([g["io"] for g in gathered], 1)
+    for proc, d in io.items():  # per second of the window, not per notebook
+        for sect in ("watch_events", "requests"):
+            if sect in d:
+                d[sect] = {kk: round(v * per_s, 1) for kk, v in d[sect].items()}
+    prof = gathered[0]["prof"] or {}
+    writes = {v: round(prof.get(f"{v}_calls", 0.0) * per_s, 1) for v in ("create", "update", "patch", "delete")}
+    culler = recon.get("Culler", {})
+    lat = [x for g in gathered for x in g["lat"]]
+    p50 = _pcts(lat).get("p50")
+    adm = gathered[0]["adm"]
+    return {
+        "notebooks": total, "per_rank": [g["k"] for g in gathered], "all_ok": all(g["ok"] for g in gathered),
+        "notebook": "CPU workbench (50m / 256Mi) with an idle Jupyter kernel" + (", inject-auth" if use_odh else ""),
+        "culling": {"period_s": getattr(args, "culling_period", 1.0), "source": "combined (Jupyter via the DEV "
+                    "kubectl-proxy stand-in; no node-agent CA, so no GPU samples)"},
+        "fill_s": round(max(g["fill_s"] for g in gathered), 3),
+        "at_rest": {
+            "window_s": round(win, 3),
+            "cpu_ms_per_s": {kk: round(v * 1e3 * per_s, 2) for kk, v in sorted(cpu_all.items())},
+            "culler_checks_per_s": round(sum(culler.values()) * per_s, 1),
+            "apiserver_writes_per_s": writes,
+            "admissions_per_s": round(adm * per_s, 1) if adm is not None else None,
+            "webhook_heartbeat_fast_path_per_s": round(sum(g["heartbeats"] for g in gathered) * per_s, 1),
+            "webhook_admissions_per_s": round(sum(g["served"] for g in gathered) * per_s, 1),
+            "reconciles_per_s": {ctrl: {"total": round(sum(t.values()) * per_s, 1),
+                                        "by_trigger": {kk: round(v * per_s, 1) for kk, v in sorted(t.items())}}
+                                 for ctrl, t in sorted(recon.items())},
+            "notebook_triggered_reconciles_kf_odh": sum(
+                t.get("Notebook", 0) for ctrl, t in recon.items()
+                if ctrl in ("notebook-controller", "odh-notebook-controller")),
+            "io_per_s": io,
+            "rss_mib": {kk: v for g in gathered for kk, v in sorted(g["rss"].items()) if v is not None},
+        },
+        "new_notebooks_on_top": {"steps_per_rank": int(getattr(args, "resident_steps", 20)), "ready_ms": _pcts(lat),
+                                 "empty_cluster_p50_ms": round(empty_p50_ms, 3) if empty_p50_ms else None,
+                                 "p50_vs_empty": round(p50 / empty_p50_ms, 3) if p50 and empty_p50_ms else None},
+        "teardown_s": round(max(g["teardown"] for g in gathered), 3),
+        **({"errors": [e for g in gathered for e in g["errors"]]} if any(g["errors"] for g in gathered) else {}),
+    }
+
+
 def io_delta(a: dict, b: dict) -> dict:
     """Per process: watch events per kind, requests per verb and lists per kind (a list in the
     window is a relist: a watch answered 410 Gone) between two snapshots."""
@@ -520,7 +718,8 @@ async def _main(args, dist, torch, rank: int, world: int, ndev: int, probe_sampl
 
     native = None
     platform = None
-    url = [None]
+    url = [None, None]  # the apiserver; the culler's DEV-mode kubectl proxy (Jupyter stand-in)
+    culling = culling_enabled(args)
     arch = args.arch if args.arch in ("sharded", "unsharded") else "sharded"
     if rank == 0:
         from ..testing.apiserver.native import NativeApiServer
@@ -543,9 +742,13 @@ async def _main(args, dist, torch, rank: int, world: int, ndev: int, probe_sampl
         # the node's StatefulSet controller and kubelet: one worker process of each per two ranks
         platform = await NodePlatform(native.url, exec_init=probe_sample > 0, hip_devices=ndev,
                                       workers=getattr(args, "platform_workers", 0) or (world + 1) // 2,
-                                      pull_secret_delay_ms=getattr(args, "openshift_pull_secret_ms", -1.0)).start()
+                                      pull_secret_delay_ms=getattr(args, "openshift_pull_secret_ms", -1.0),
+                                      jupyter_proxy=culling).start()
+        url[1] = platform.jupyter_proxy_url
     await _in_thread(dist.broadcast_object_list, url, 0)
     env = {"SET_PIPELINE_RBAC": "false", "SET_PIPELINE_SECRET": "false"}
+    if culling:
+        env.update(culler_env(args, url[1]))
     per_rank = max(1, getattr(args, "namespaces_per_rank", 1))
     nss = bench_namespaces(rank, per_rank)
     shard = ControlPlaneShard(ShardConfig(
@@ -760,6 +963,12 @@ async def _drive(args, shard, dist, torch, children: Optional[dict] = None, nati
                                 "webhook_dial_ms": (b.get("apiserver") or {}).get("webhook_dial_ms")}
                                for b in rounds]
 
+    resident = None
+    if getattr(args, "resident", 0) > 0 and culling_enabled(args):
+        # untimed: a resident population with the culler checking it
+        resident = await _resident(args, shard, dist, native, children, use_odh,
+                                   statistics.median(lat_ms) if lat_ms else None)
+
     el = torch.tensor([elapsed], dtype=torch.float64)
     await _in_thread(lambda: dist.all_reduce(el, op=dist.ReduceOp.MAX))
     gathered = [None] * dist.get_world_size()
@@ -798,7 +1007,7 @@ async def _drive(args, shard, dist, torch, children: Optional[dict] = None, nati
             "apiserver_profile_per_step": prof, "breakdown": merge_breakdowns(g["settled"] for g in gathered),
             "quiesced": all(g["idle"] for g in gathered),
             "io_per_notebook": io_per_notebook([g["io"] for g in gathered], args.steps * len(gathered)),
-            "burst": burst, "shard_load": load,
+            "burst": burst, "shard_load": load, "resident": resident,
             "recon_snapshot_lag_ms": round(max(g["snap_lag_ms"] for g in gathered), 3),
             "probe_sample": [s for g in gathered for s in g["probe"]],
             "lifecycle_ms_per_20_steps": [round(statistics.fmean(b), 3) for b in zip(*(g["blocks"] for g in gathered))]}

@@ -73,7 +73,7 @@ async def stop_child(proc: Optional[subprocess.Popen]) -> None:
 class NodePlatform:
     def __init__(self, apiserver_url: str, node_name: str = "mi355x-node-0", gpus: int = 8, process: bool = True,
                  exec_init: bool = False, hip_devices: int = 0, max_concurrent: int = 8, workers: int = 1,
-                 pull_secret_delay_ms: float = -1.0):
+                 pull_secret_delay_ms: float = -1.0, jupyter_proxy: bool = False):
         self.url = apiserver_url
         self.node_name = node_name
         self.gpus = gpus
@@ -85,6 +85,10 @@ class NodePlatform:
         # >= 0: OpenShift's ServiceAccount pull-secret controller, adding each SA's dockercfg
         # secret this many ms after the SA appears (testing/kubelet/openshift.py)
         self.pull_secret_delay_ms = float(pull_secret_delay_ms)
+        # the culler's DEV-mode kubectl proxy in front of every notebook's Jupyter API
+        # (testing/cmd/jupyter_proxy.py): the resident-population benchmark's idle notebooks
+        self.jupyter_proxy = jupyter_proxy
+        self.jupyter_proxy_url: Optional[str] = None
         self.procs: Dict[str, subprocess.Popen] = {}
         self.managers = []
         self.agent = None
@@ -119,6 +123,13 @@ class NodePlatform:
                     args += ["--exec-init", "--hip-devices", str(self.hip_devices)]
                 self.procs[name] = await start_child("odh_kubeflow_amd.testing.cmd.fake_kubelet", args, "kubelet",
                                                      python_args=pre(name))
+            if self.jupyter_proxy:
+                from .shard import free_port
+
+                port = free_port()
+                self.procs["jupyter_proxy"] = await start_child("odh_kubeflow_amd.testing.cmd.jupyter_proxy",
+                                                                ["--port", str(port)], "Jupyter proxy")
+                self.jupyter_proxy_url = f"http://127.0.0.1:{port}"
             return self
         from ..models import kinds
         from ..runtime.informer import InformerCache
@@ -166,7 +177,7 @@ class NodePlatform:
         return all(m.idle() for m in self.managers)
 
     async def stop(self) -> None:
-        for k in [*[k for k in self.procs if k.startswith(("kubelet", "controller_manager"))], "scheduler"]:
+        for k in [*[k for k in self.procs if k.startswith(("kubelet", "controller_manager", "jupyter"))], "scheduler"]:
             await stop_child(self.procs.pop(k, None))
         for mgr in reversed(self.managers):
             await mgr.stop()

@@ -311,10 +311,11 @@ class ControlPlaneShard:
         async with self._http.get(url) as r:
             return json.loads(await r.text())
 
-    async def reconcile_breakdown(self) -> dict:
+    async def reconcile_breakdown(self, include_all: bool = False) -> dict:
         """controller → {trigger → reconciles} of the notebook controllers this rank launched
-        (the culler and the namespace assigner are not part of a notebook's create→Ready path)."""
-        skip = ("Culler", "shard-assigner")
+        (the culler and the namespace assigner are not part of a notebook's create→Ready path;
+        ``include_all``: them too)."""
+        skip = () if include_all else ("Culler", "shard-assigner")
         parts = [mgr.reconcile_breakdown() for mgr in self.managers]
         if self.procs:
             parts += [d["reconciles"] for d in await asyncio.gather(

@@ -175,6 +175,15 @@ class Client(abc.ABC):
             raise
 
 
+async def list_readonly(client, kind, namespace=None, labels=None, fields=None):
+    """``client.list_readonly`` when the client has it (a cached client: no copies), else
+    ``client.list``; the items must not be mutated either way."""
+    fn = getattr(client, "list_readonly", None)
+    if fn is not None:
+        return await fn(kind, namespace, labels, fields)
+    return await client.list(kind, namespace, labels, fields)
+
+
 class CachedClient(Client):
     """Reads from a :class:`Reader` (copying), writes through a backing client.
 
@@ -501,15 +510,28 @@ class CachedClient(Client):
                 o["apiVersion"] = av
         return items
 
-    def _begin(self, obj, precondition: Optional[int] = None) -> Optional[Tuple[str, str, str]]:
+    async def list_readonly(self, kind, namespace=None, labels=None, fields=None, owner_uid=None):
+        """:meth:`list` without the copies: the cache's own objects, which the caller must not
+        mutate (a scan that only reads — e.g. "is another Notebook alive in the namespace", once
+        per deletion, over every Notebook of the namespace)."""
+        if self._live(kind, namespace) and owner_uid is None:
+            return await self.writer.list(kind, namespace, labels, fields)
+        await self._ensure(kind)
+        return self.reader.list(kind, namespace, labels, fields, owner_uid)
+
+    def _begin(self, obj, precondition: Optional[int] = None, name: Optional[str] = None,
+               namespace: Optional[str] = None) -> Optional[Tuple[str, str, str]]:
+        """Track a create / preconditioned write in flight (``obj``: the object, or its kind
+        with ``name`` / ``namespace`` — a patch)."""
         cur = CURRENT_RECONCILE.get()
-        if cur is None or not isinstance(obj, dict):
+        if cur is None:
             return None
-        md = obj.get("metadata") or {}
-        if not md.get("name"):
+        md = (obj.get("metadata") or {}) if isinstance(obj, dict) else {}
+        name = name or md.get("name")
+        if not name:
             return None  # generateName: the key is unknown until the response
         try:
-            key = (SCHEME.resolve(obj).key, md.get("namespace") or "", md["name"])
+            key = (SCHEME.resolve(obj).key, namespace or md.get("namespace") or "", name)
         except Exception:
             return None
         self._inflight[key] = [cur, precondition, None]
@@ -557,7 +579,20 @@ class CachedClient(Client):
         return out
 
     async def patch(self, obj_or_kind, patch, patch_type="merge", name=None, namespace=None, subresource=None):
-        out = await self.writer.patch(obj_or_kind, patch, patch_type, name, namespace, subresource)
+        # a resourceVersion-preconditioned merge patch is tracked in flight like a
+        # preconditioned update: its watch echo can overtake the response (the culler's
+        # heartbeat, once per check of every notebook, would otherwise requeue itself)
+        key = None
+        if subresource is None and patch_type == "merge" and isinstance(patch, dict):
+            sent = _rv_int(patch)
+            if sent is not None:
+                key = self._begin(obj_or_kind, sent, name, namespace)
+        out = None
+        try:
+            out = await self.writer.patch(obj_or_kind, patch, patch_type, name, namespace, subresource)
+        finally:
+            if key is not None:
+                self._settle(key, out)
         self._note(out, claim=_patch_certainly_changes(patch, patch_type, out))
         return out
 

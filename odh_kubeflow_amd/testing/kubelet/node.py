@@ -118,8 +118,63 @@ class SchedulerController:
         # next scheduling decision before the informer has observed it, so two pods can
         # never be given the same GPU however far the cache lags behind the apiserver.
         self._assumed: Dict[str, tuple] = {}  # pod uid -> (node, cpu, mem, gpu ids)
+        # kube-scheduler's NodeInfo cache: what the pods bound to each node request, kept up to
+        # date from the pod watch (:meth:`_on_pod`) so a decision costs O(1) in the pods already
+        # running — with hundreds resident, re-summing them per decision set the pace
+        self._pods: Dict[str, tuple] = {}  # pod uid -> (node, cpu, mem, gpu ids)
+        self._sums: Dict[str, List[float]] = {}  # node -> [cpu, mem]
+        self._gpu_pods: Dict[str, Dict[str, tuple]] = {}  # node -> {uid: gpu ids}
+        self._unbound: Dict[str, tuple] = {}  # uid -> (namespace, name) of pods waiting for a node
+        self._tracking = False
+
+    def _on_pod(self, etype: str, pod: dict, old: Optional[dict]) -> None:
+        uid = m.uid(pod)
+        spec = pod.get("spec") or {}
+        node = spec.get("nodeName")
+        gone = etype == "DELETED" or (pod.get("status") or {}).get("phase") in ("Succeeded", "Failed")
+        if gone or node or m.is_deleting(pod):
+            self._unbound.pop(uid, None)
+        else:
+            self._unbound[uid] = (m.namespace(pod), m.name(pod))
+        cur = self._pods.get(uid)
+        ids = m.annotations(pod).get(GPU_IDS_ANNOTATION)
+        want = None
+        if not gone and node:
+            if cur is not None and cur[0] == node and cur[4] == ids:
+                return  # requests are immutable: nothing this cache keeps changed
+            r = _pod_requests(pod)
+            want = (node, r["cpu"], r["memory"], tuple(int(x) for x in ids.split(",") if x != "") if ids else (), ids)
+        if cur is not None:
+            sums = self._sums[cur[0]]
+            sums[0] -= cur[1]
+            sums[1] -= cur[2]
+            self._gpu_pods.get(cur[0], {}).pop(uid, None)
+            del self._pods[uid]
+        if want is not None:
+            self._pods[uid] = want
+            sums = self._sums.setdefault(node, [0.0, 0.0])
+            sums[0] += want[1]
+            sums[1] += want[2]
+            if want[3]:
+                self._gpu_pods.setdefault(node, {})[uid] = want[3]
 
     def _used(self, node_name: str) -> Dict[str, object]:
+        if not self._tracking:
+            return self._used_scan(node_name)
+        cpu, mem = self._sums.get(node_name, (0.0, 0.0))
+        gpus: Set[int] = set()
+        for ids in self._gpu_pods.get(node_name, {}).values():
+            gpus.update(ids)
+        for uid, (node, acpu, amem, aids) in list(self._assumed.items()):
+            seen = self._pods.get(uid)
+            if node != node_name or (seen is not None and seen[0] == node_name):
+                continue
+            cpu += acpu
+            mem += amem
+            gpus.update(aids)
+        return {"cpu": cpu, "memory": mem, "gpus": gpus}
+
+    def _used_scan(self, node_name: str) -> Dict[str, object]:
         cpu = mem = 0.0
         gpus: Set[int] = set()
         seen = set()
@@ -232,8 +287,15 @@ class SchedulerController:
                              update=lambda o, old: not (o.get("spec") or {}).get("nodeName"),
                              delete=lambda o: False)
 
+        src = getattr(mgr, "cache", None) or mgr.reader
+        if hasattr(src, "subscribe"):  # the NodeInfo cache follows every pod event
+            src.subscribe(kinds.POD, self._on_pod)
+            self._tracking = True
+
         def pods_released(obj):  # a deleted pod frees capacity: retry pending pods
             self.forget(obj)
+            if self._tracking:
+                return [Request(ns, nm) for ns, nm in list(self._unbound.values())]
             return [Request(m.namespace(p), m.name(p)) for p in self.reader.list(kinds.POD)
                     if not (p.get("spec") or {}).get("nodeName")]
 

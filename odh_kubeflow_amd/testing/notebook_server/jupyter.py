@@ -89,6 +89,59 @@ class JupyterServer:
             self._runner = None
 
 
+class JupyterProxy:
+    """``kubectl proxy`` in front of every notebook's Jupyter server, for the culler's ``DEV``
+    mode (``kf/controllers/culling_controller.go:249-256``: ``/api/v1/namespaces/<ns>/services/
+    <nm>:http-<nm>/proxy/notebook/<ns>/<nm>/api/{kernels,terminals}``) — one process answering
+    for R resident notebooks, where a :class:`JupyterServer` per pod would be R servers.
+
+    Every notebook reports one idle kernel whose last activity is this proxy's start (and no
+    terminals): a notebook nobody uses, so each check is the culler's plain heartbeat, never a
+    cull while ``CULL_IDLE_TIME`` has not passed."""
+
+    PATH = "/api/v1/namespaces/{ns}/services/{svc}/proxy/notebook/{ns2}/{nm}/api/{res}"
+
+    def __init__(self, host: str = "127.0.0.1", port: int = 0):
+        self.host = host
+        self.port = port
+        self.requests = 0
+        self.started_at = rfc3339()
+        self._runner = None
+
+    async def start(self) -> "JupyterProxy":
+        from aiohttp import web
+
+        kernel = [{"id": "00000000-0000-0000-0000-000000000000", "name": "python3", "last_activity": self.started_at,
+                   "execution_state": "idle", "connections": 0}]
+
+        async def api(req):
+            self.requests += 1
+            res = req.match_info["res"]
+            if res == "kernels":
+                return web.json_response(kernel)
+            if res == "terminals":
+                return web.json_response([])
+            raise web.HTTPNotFound()
+
+        app = web.Application()
+        app.router.add_get(self.PATH, api)
+        self._runner = web.AppRunner(app, access_log=None)
+        await self._runner.setup()
+        site = web.TCPSite(self._runner, self.host, self.port, backlog=1024)
+        await site.start()
+        self.port = site._server.sockets[0].getsockname()[1]
+        return self
+
+    @property
+    def url(self) -> str:
+        return f"http://{self.host}:{self.port}"
+
+    async def stop(self) -> None:
+        if self._runner is not None:
+            await self._runner.cleanup()
+            self._runner = None
+
+
 class JupyterContainerRuntime(ContainerRuntime):
     """Container runtime whose "notebook container" is a :class:`JupyterServer`."""
 

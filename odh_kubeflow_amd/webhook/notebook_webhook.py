@@ -209,6 +209,9 @@ class NotebookWebhook:
         self.requests = 0
         self.denied = 0
         self.heartbeats = 0  # culler heartbeat updates answered without the pipeline
+        from ..models.notebook import heartbeat_filter_enabled
+
+        self.heartbeat_fast_path = heartbeat_filter_enabled(self.env)
 
     async def mutate(self, operation: str, nb: dict, old: Optional[dict], name: str = "",
                      namespace: str = "") -> dict:
@@ -309,7 +312,7 @@ class NotebookWebhook:
             if bad:  # the reference's typed decode (admission.Decoder) refuses these
                 raise AdmissionError(400, f"cannot decode Notebook: {bad}")
             old = req.get("oldObject") if isinstance(req.get("oldObject"), dict) else None
-            if req.get("operation") == "UPDATE" and culler_heartbeat_only(obj, old):
+            if req.get("operation") == "UPDATE" and self.heartbeat_fast_path and culler_heartbeat_only(obj, old):
                 self.heartbeats += 1
                 return {"apiVersion": "admission.k8s.io/v1", "kind": "AdmissionReview", "response": resp}
             tok = CONFIRM_ABSENCE.set(set())  # one-shot decision: absent objects are confirmed live, once

@@ -62,6 +62,11 @@ if b:
     print(sys.argv[2], "burst", {k: b.get(k) for k in ("notebooks", "all_ready_s", "notebooks_per_s", "ready_ms",
                                                       "admission_ms", "webhook_handle_ms", "webhook_get_ms",
                                                       "cpu_ms_per_notebook", "rounds")})
+rs = d.get("resident")
+if rs:
+    print(sys.argv[2], "resident", json.dumps({k: rs.get(k) for k in ("notebooks", "all_ok", "fill_s",
+                                                                      "new_notebooks_on_top", "teardown_s", "errors")}))
+    print(sys.argv[2], "resident at_rest", json.dumps(rs.get("at_rest"))[:2500])
 sl = d.get("shard_load")
 if sl:
     print(sys.argv[2], "shard_load", json.dumps(sl))
@@ -91,6 +96,15 @@ for s in $steps; do
       timeout -k 10 200 python bench.py --gpus 1 --no-inprocess-baseline > "$out/bench_n1_s300.log" 2>&1 \
         || fail bench $? "$out/bench_n1_s300.log"
       show "$out/bench_n1_s300.log" "n1 steps300" ;;
+    resident)  # R resident notebooks with the culler on: at rest, and new notebooks on top; heartbeat filter A/B
+      for r in $(seq 1 "${ROUNDS:-1}"); do
+        for v in true false; do
+          ODH_HEARTBEAT_FILTER=$v timeout -k 10 400 python bench.py --gpus 1 --steps 100 --warmup 10 --no-configs \
+            --no-inprocess-baseline --burst 0 --probe-sample 0 --resident "${RESIDENT:-1000}" --resident-window 5 \
+            > "$out/bench_resident_filter_${v}_r$r.log" 2>&1 || fail resident $? "$out/bench_resident_filter_${v}_r$r.log"
+          show "$out/bench_resident_filter_${v}_r$r.log" "resident filter=$v r$r"
+        done
+      done ;;
     b20x4)
       for r in 1 2 3 4; do
         echo "run $r start $(date +%s.%N)"

@@ -104,6 +104,9 @@ def parse(argv=None):
     p.add_argument("--no-culling", action="store_true",
                    help="run the control plane without the culler (the MI355X overlays ship it on: "
                         "ENABLE_CULLING=true, CULLING_ACTIVITY_SOURCE=combined)")
+    p.add_argument("--culler-in-kf", action="store_true",
+                   help="sharded: the culler in the kf process (the reference's manager layout) instead of a process "
+                        "of its own (A/B measurements)")
     p.add_argument("--culling-period", type=float, default=1.0,
                    help="the culler's check period in seconds (IDLENESS_CHECK_PERIOD_SECONDS; the overlays' "
                         "is 60): every resident notebook is checked, and its Notebook written, once per period")

@@ -45,6 +45,8 @@ from typing import List, Optional
 log = logging.getLogger("setup")
 
 ALL_CONTROLLERS = ("kf", "odh", "webhook")
+# finer splits of "kf": the notebook reconciler + event re-emitter, and the culler
+KF_PARTS = ("notebook", "culler")
 
 
 def parse(argv: Optional[List[str]] = None) -> argparse.Namespace:
@@ -53,7 +55,8 @@ def parse(argv: Optional[List[str]] = None) -> argparse.Namespace:
     p = argparse.ArgumentParser(prog="notebook-control-plane")
     p.add_argument("--controllers", default="kf,odh,webhook",
                    help="comma list of kf (notebook + event re-emitter + culler when ENABLE_CULLING=true), "
-                        "odh (OpenshiftNotebookReconciler), webhook (odh mutating webhook)")
+                        "odh (OpenshiftNotebookReconciler), webhook (odh mutating webhook); or kf split in two: "
+                        "notebook (notebook + event re-emitter) and culler (the culler alone)")
     add_shard_flags(p)
     add_debug_flags(p)
     p.add_argument("--shard-count", type=int, default=0, help="number of shards (for --assign-namespaces)")
@@ -89,9 +92,11 @@ def parse(argv: Optional[List[str]] = None) -> argparse.Namespace:
     p.add_argument("--reference-emulation", action="store_true", help=argparse.SUPPRESS)  # same-harness comparisons
     args = p.parse_args(argv)
     args.controller_set = [c.strip() for c in args.controllers.split(",") if c.strip()]
-    bad = [c for c in args.controller_set if c not in ALL_CONTROLLERS]
+    bad = [c for c in args.controller_set if c not in ALL_CONTROLLERS + KF_PARTS]
     if bad:
         p.error(f"unknown --controllers entries: {bad}")
+    if "kf" in args.controller_set and any(c in args.controller_set for c in KF_PARTS):
+        p.error("--controllers: kf already runs notebook and culler")
     if ("odh" in args.controller_set or "webhook" in args.controller_set) and not args.kube_rbac_proxy_image:
         p.print_usage(sys.stderr)
         raise SystemExit("missing required flag: --kube-rbac-proxy-image must be set")
@@ -141,6 +146,12 @@ def build(args, env=os.environ):
     emu = args.reference_emulation
     if "kf" in args.controller_set:
         mgr.kf_reconcilers = setup_kf(mgr, env, reference_emulation=emu)
+    elif "notebook" in args.controller_set:
+        mgr.kf_reconcilers = setup_kf(mgr, env, culling=False, reference_emulation=emu)
+    if "culler" in args.controller_set:
+        from ..controllers.setup import setup_culler
+
+        mgr.culler = setup_culler(mgr, env, reference_emulation=emu)
     if "odh" in args.controller_set:
         mgr.odh_reconciler = setup_odh(mgr, namespace, env, shard=shard, reference_emulation=emu)
     if args.assign_namespaces:

@@ -62,19 +62,27 @@ class _RunningCollector:
         yield gpus
 
 
-class NotebookMetrics:
-    def __init__(self, reader, registry: CollectorRegistry):
+class CullerMetrics:
+    """The two culling metrics alone: a process that runs only the culler (``--controllers
+    culler``) exports these and leaves the notebook metrics to the kf process."""
+
+    def __init__(self, registry: CollectorRegistry):
         self.registry = registry
-        registry.register(_RunningCollector(reader))
-        self.notebook_creation = Counter("notebook_create", "Total times of creating notebooks", ["namespace"],
-                                         registry=registry)
-        self.notebook_fail_creation = Counter("notebook_create_failed", "Total failure times of creating notebooks",
-                                              ["namespace"], registry=registry)
         self.notebook_culling_count = Counter("notebook_culling", "Total times of culling notebooks",
                                               ["namespace", "name"], registry=registry)
         self.notebook_culling_timestamp = Gauge("last_notebook_culling_timestamp_seconds",
                                                 "Timestamp of the last notebook culling in seconds",
                                                 ["namespace", "name"], registry=registry)
+
+
+class NotebookMetrics(CullerMetrics):
+    def __init__(self, reader, registry: CollectorRegistry):
+        super().__init__(registry)
+        registry.register(_RunningCollector(reader))
+        self.notebook_creation = Counter("notebook_create", "Total times of creating notebooks", ["namespace"],
+                                         registry=registry)
+        self.notebook_fail_creation = Counter("notebook_create_failed", "Total failure times of creating notebooks",
+                                              ["namespace"], registry=registry)
         self.pod_ready_seconds = Histogram("notebook_pod_ready_seconds",
                                            "Seconds from Notebook creation (first pod) or pod creation "
                                            "(resume/restart) to the Notebook reporting Ready",

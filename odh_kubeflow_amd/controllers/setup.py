@@ -58,6 +58,22 @@ def setup_kf(mgr, env: Mapping[str, str] = os.environ, *, culling: Optional[bool
     return out
 
 
+def setup_culler(mgr, env: Mapping[str, str] = os.environ, *, activity=None, reference_emulation: bool = False):
+    """The CullingReconciler alone (``--controllers culler``: the culler in a process of its
+    own, so its periodic checks of every resident notebook never queue a notebook's create→Ready
+    work behind them).  Off unless ``ENABLE_CULLING=true``, as in the kf manager."""
+    from .culling import CullingReconciler
+    from .metrics import CullerMetrics
+
+    if (env.get("ENABLE_CULLING") or "false") != "true":
+        log.info("Culling of idle Pods is Disabled. To enable it set the ENV Var 'ENABLE_CULLING=true'")
+        return None
+    mgr.skip_own_write_echoes = not reference_emulation
+    c = CullingReconciler(mgr.client, mgr.reader, CullerMetrics(mgr.registry), env=env, activity=activity)
+    c.setup_with_manager(mgr, max_concurrent=1 if reference_emulation else None)
+    return c
+
+
 def setup_odh(mgr, namespace: str, env: Mapping[str, str] = os.environ, *, shard: Optional[str] = None,
               reference_emulation: bool = False):
     """The odh reconciler on ``mgr``.  ``shard``: label this shard's HTTPRoutes (they live in

@@ -483,6 +483,16 @@ class LoadGenerator:
         self._thr.start()
         return self
 
+    def wait_running(self, timeout: float = 60.0) -> bool:
+        """Block until the load is on the GPU (the first calibrated launch finished): the thread
+        first initialises the HIP runtime, which takes from a few hundred ms to seconds."""
+        deadline = time.monotonic() + timeout
+        while self.launches < 1 and time.monotonic() < deadline:
+            if self._thr is not None and not self._thr.is_alive():
+                return False
+            time.sleep(0.005)
+        return self.launches >= 1
+
     def stop(self) -> None:
         self._stop.set()
         if self._thr is not None:

@@ -46,6 +46,8 @@ import statistics
 import time
 from typing import Optional
 
+from .shard import driven
+
 GPU_PROBE_ANNOTATION = "amd.com/gpu-probe"
 NODE_GPUS = 8  # the node platform's MI355X count (NodePlatform gpus)
 NOTEBOOK_IMAGE = "rocm/pytorch:rocm7.0_ubuntu22.04_py3.10_pytorch_2.10"
@@ -345,7 +347,7 @@ async def _burst(args, shard, dist, native, children: dict, use_odh: bool, tag: 
 
     async def create(nm):
         c0 = time.perf_counter()
-        nb = notebook(nm, ns_of[nm], image=NOTEBOOK_IMAGE, annotations=ann, gpus=gpus)
+        nb = driven(notebook(nm, ns_of[nm], image=NOTEBOOK_IMAGE, annotations=ann, gpus=gpus))
         c = nb["spec"]["template"]["spec"]["containers"][0]
         c.setdefault("resources", {}).setdefault("requests", {}).update(res)
         await shard.admin.create(nb)
@@ -464,24 +466,46 @@ async def _resident(args, shard, dist, native, children: dict, use_odh: bool,
         async with sem:
             await shard.admin.create(nb)
 
-    def all_ready() -> bool:
-        return all(shard.notebook_ready(nm, ns_of[nm]) for nm in names)
+    # the resident notebooks are not labelled driven: the driver's own cache never sees their
+    # heartbeats; this cache follows them while they fill (and again while they go)
+    from ..runtime.informer import InformerCache
+    from .shard import notebook_is_ready
 
-    def all_checked() -> bool:  # the culler has initialised every resident notebook's annotations
+    async def watching():
+        c = InformerCache(shard.rest, namespaces=nss)
+        for kk in (kinds.NOTEBOOK, kinds.POD):
+            await c.ensure_informer(kk)
+        return c
+
+    async def poll_until(pred, timeout: float) -> bool:
+        deadline = time.monotonic() + timeout
+        while not pred():
+            if time.monotonic() > deadline:
+                return False
+            await asyncio.sleep(0.02)
+        return True
+
+    def all_ready(c) -> bool:
+        return all(notebook_is_ready(c.get(kinds.NOTEBOOK, nm, ns_of[nm])) for nm in names)
+
+    def all_checked(c) -> bool:  # the culler has initialised every resident notebook's annotations
         for nm in names:
-            nb = shard.peek(kinds.NOTEBOOK, nm, ns_of[nm])
+            nb = c.get(kinds.NOTEBOOK, nm, ns_of[nm])
             if nb is None or LAST_ACTIVITY_CHECK_TIMESTAMP_ANNOTATION not in ((nb.get("metadata") or {})
                                                                              .get("annotations") or {}):
                 return False
         return True
 
     await safe(shard.quiesce())
+    fill = await safe(watching())
     await _in_thread(dist.barrier)
     t0 = time.perf_counter()
     await safe(asyncio.gather(*(create(nm) for nm in names)))
-    ok = bool(await safe(shard.wait_until(all_ready, 300), False))
+    ok = fill is not None and bool(await safe(poll_until(lambda: all_ready(fill), 300), False))
     fill_s = time.perf_counter() - t0
-    ok = ok and bool(await safe(shard.wait_until(all_checked, 120), False))
+    ok = ok and bool(await safe(poll_until(lambda: all_checked(fill), 120), False))
+    if fill is not None:
+        await safe(fill.stop())
     await asyncio.sleep(2 * getattr(args, "culling_period", 1.0))  # every notebook's checks under way
     await _in_thread(dist.barrier)
 
@@ -525,9 +549,14 @@ async def _resident(args, shard, dist, native, children: dict, use_odh: bool,
     async def delete(nm):
         async with sem:
             await shard.admin.delete(kinds.NOTEBOOK, nm, ns_of[nm])
+    gonec = await safe(watching())
     await safe(asyncio.gather(*(delete(nm) for nm in names), return_exceptions=True))
-    gone = bool(await safe(shard.wait_until(lambda: all(shard.gone(nm, ns_of[nm]) for nm in names), 300), False))
+    gone = gonec is not None and bool(await safe(poll_until(lambda: all(
+        gonec.get(kinds.NOTEBOOK, nm, ns_of[nm]) is None and gonec.get(kinds.POD, f"{nm}-0", ns_of[nm]) is None
+        for nm in names), 300), False))
     teardown = time.perf_counter() - t_del
+    if gonec is not None:
+        await safe(gonec.stop())
     gathered = [None] * world
     await _in_thread(dist.all_gather_object, gathered, {
         "k": k, "ok": ok and gone, "fill_s": fill_s, "win": win, "cpu": cpu, "rss": rss, "lat": lat,
@@ -759,7 +788,8 @@ async def _main(args, dist, torch, rank: int, world: int, ndev: int, probe_sampl
         split=not getattr(args, "single_process_shard", False), workers=max(1, getattr(args, "workers", 1)),
         webhook_replicas=max(1, getattr(args, "webhook_replicas", 1)),
         webhook_process=not getattr(args, "webhook_in_odh", False),
-        cache_configmaps=getattr(args, "cache_configmaps", False)))
+        cache_configmaps=getattr(args, "cache_configmaps", False), driven_only=True,
+        culler_process=culling and not getattr(args, "culler_in_kf", False)))
     if rank == 0:
         await shard.start()  # cluster namespaces (and, unsharded, the managers + their webhook) first
         await _in_thread(dist.barrier)
@@ -838,7 +868,7 @@ async def _lifecycle(shard, nm: str, ann: Optional[dict], timeout: float = 120.0
 
     ns = ns or shard.cfg.namespace
     t0 = time.perf_counter()
-    await shard.admin.create(notebook(nm, ns, image=NOTEBOOK_IMAGE, gpus=1, annotations=ann))
+    await shard.admin.create(driven(notebook(nm, ns, image=NOTEBOOK_IMAGE, gpus=1, annotations=ann)))
     if not await shard.wait_until(lambda: shard.notebook_ready(nm, ns), timeout):
         raise RuntimeError(f"notebook {ns}/{nm} not Ready")
     ready = time.perf_counter()

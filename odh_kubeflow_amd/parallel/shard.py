@@ -40,6 +40,23 @@ from ..models import kinds
 from ..models import meta as m
 
 ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+DRIVEN_LABEL = "bench.odh-kubeflow-amd/driven"
+
+
+def notebook_is_ready(nb: Optional[dict]) -> bool:
+    """The Notebook's status mirrors a Ready pod (``readyReplicas`` 1 and the Ready condition)."""
+    if nb is None:
+        return False
+    st = nb.get("status") or {}
+    if st.get("readyReplicas") != 1:
+        return False
+    return any(c.get("type") == "Ready" and c.get("status") == "True" for c in st.get("conditions") or [])
+
+
+def driven(nb: dict) -> dict:
+    """Label a Notebook the benchmark driver times (``ShardConfig.driven_only``)."""
+    nb.setdefault("metadata", {}).setdefault("labels", {})[DRIVEN_LABEL] = "true"
+    return nb
 
 
 def free_port() -> int:
@@ -66,6 +83,7 @@ class ShardConfig:
     process: bool = False  # run the control plane as its own process(es), as deployed
     split: bool = True  # sharded, process mode: the shard pod's containers as processes (kf | odh | webhook)
     webhook_process: bool = True  # sharded, split: the webhook in a process of its own (False: odh + webhook)
+    culler_process: bool = False  # sharded, split: the culler in a process of its own (notebook | culler)
     workers: int = 1  # unsharded: --workers of the kf and odh managers (runtime/workers.py)
     webhook_replicas: int = 1  # unsharded with workers: --webhook-replicas of the odh manager
     cache_configmaps: bool = False  # unsharded: --cache-configmaps-secrets=true on the odh manager
@@ -76,6 +94,9 @@ class ShardConfig:
     assign: bool = False
     shard_count: int = 1
     assign_policy: str = "hash"  # NamespaceShardAssigner policy: hash | balanced
+    # the driver's own cache selects only the notebooks (and their pods) it labelled DRIVEN_LABEL:
+    # a resident population's culler heartbeats never reach the process that times new ones
+    driven_only: bool = False
 
     @property
     def user_namespaces(self) -> List[str]:
@@ -120,7 +141,8 @@ class ControlPlaneShard:
         if cfg.arch == "sharded":
             # the shard pod of config/overlays/mi355x-sharded: the control plane split into a
             # kf process, an odh process and a webhook process (cmd/control_plane.py docstring)
-            sets = [["kf"]]
+            sets = [["notebook"], ["culler"]] if cfg.culler_process and (cfg.split if split is None else split) \
+                else [["kf"]]
             if cfg.odh:
                 if cfg.webhook and cfg.webhook_process:
                     sets += [["odh"], ["webhook"]]
@@ -128,17 +150,18 @@ class ControlPlaneShard:
                     sets.append(["odh"] + (["webhook"] if cfg.webhook else []))
             if not (cfg.split if split is None else split):
                 sets = [[c for cs in sets for c in cs]]
+            names = {"notebook": "kf"}  # the kf process keeps its name without the culler
             out = []
             for cs in sets:
                 a = ["--shard", self.shard, "--controllers", ",".join(cs), "--health-probe-bind-address", "0"]
                 if "odh" in cs or "webhook" in cs:
                     a += wh
-                if cfg.assign and "kf" in cs:
+                if cfg.assign and ("kf" in cs or "notebook" in cs):
                     a += ["--assign-namespaces", "--shard-count", str(cfg.shard_count),
                           "--assign-policy", cfg.assign_policy]
                 if cfg.reference_emulation:
                     a.append("--reference-emulation")
-                name = "control_plane" if len(sets) == 1 else f"control_plane_{cs[0]}"
+                name = "control_plane" if len(sets) == 1 else f"control_plane_{names.get(cs[0], cs[0])}"
                 out.append((name, "odh_kubeflow_amd.cmd.control_plane", a, "--metrics-bind-address"))
             return out
         wk = ["--workers", str(cfg.workers)] if cfg.workers > 1 else []
@@ -178,8 +201,10 @@ class ControlPlaneShard:
                 wport = await self._build_in_process()
             if cfg.webhook and cfg.odh:
                 await self._register_webhook(wport)
-        # this rank's notebook driver: its namespaces' Notebooks and Pods
-        self.cache = InformerCache(self.rest, namespaces=cfg.user_namespaces)
+        # this rank's notebook driver: its namespaces' Notebooks and Pods (driven_only: those it
+        # labelled; the STS generator copies a Notebook's labels to its pod)
+        sel = {kinds.NOTEBOOK: f"{DRIVEN_LABEL}=true", kinds.POD: f"{DRIVEN_LABEL}=true"} if cfg.driven_only else None
+        self.cache = InformerCache(self.rest, namespaces=cfg.user_namespaces, selectors=sel)
         self._caches.append(self.cache)
         for k in (kinds.NOTEBOOK, kinds.POD):
             await self.cache.ensure_informer(k)
@@ -289,13 +314,7 @@ class ControlPlaneShard:
             await asyncio.sleep(0.05)
 
     def notebook_ready(self, name: str, namespace: Optional[str] = None) -> bool:
-        nb = self.cache.get(kinds.NOTEBOOK, name, namespace or self.cfg.namespace)
-        if nb is None:
-            return False
-        st = nb.get("status") or {}
-        if st.get("readyReplicas") != 1:
-            return False
-        return any(c.get("type") == "Ready" and c.get("status") == "True" for c in st.get("conditions") or [])
+        return notebook_is_ready(self.cache.get(kinds.NOTEBOOK, name, namespace or self.cfg.namespace))
 
     def gone(self, name: str, namespace: Optional[str] = None) -> bool:
         ns = namespace or self.cfg.namespace

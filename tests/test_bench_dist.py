@@ -107,11 +107,14 @@ def test_bench_namespaces_per_rank_assigned_by_the_shard_hash():
 
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
            "127.0.0.1", "--master-port", str(_port()), "bench.py", "--gpus", "2", "--steps", "8", "--warmup", "1",
-           "--no-gpu-probe", "--namespaces-per-rank", "4", "--burst", "4", "--burst-rounds", "1"]
+           "--no-gpu-probe", "--namespaces-per-rank", "4", "--burst", "4", "--burst-rounds", "1",
+           "--resident", "16", "--resident-window", "1", "--resident-steps", "2"]
     out = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=240)
     assert out.returncode == 0, out.stderr[-3000:]
     d = json.loads([l for l in out.stdout.splitlines() if l.startswith("{")][-1])
     assert d["config"]["namespaces_per_rank"] == 4 and d["burst"]["all_ok"]
+    res = d["resident"]  # 16 resident notebooks over both ranks' namespaces, the culler checking them
+    assert res["all_ok"] and res["notebooks"] == 16 and res["at_rest"]["notebook_triggered_reconciles_kf_odh"] == 0
     load = d["shard_load"]
     assert load["assigned_by"].startswith("NamespaceShardAssigner")
     want: dict = {}
@@ -123,8 +126,8 @@ def test_bench_namespaces_per_rank_assigned_by_the_shard_hash():
     assert sum(v["notebooks"] for v in load["shards"].values()) == 16
     for k, v in load["shards"].items():
         if v["notebooks"]:
-            assert set(v["cpu_ms_per_notebook"]) == {f"control_plane_kf_{k}", f"control_plane_odh_{k}",
-                                                     f"control_plane_webhook_{k}"}
+            assert set(v["cpu_ms_per_notebook"]) == {f"control_plane_kf_{k}", f"control_plane_culler_{k}",
+                                                     f"control_plane_odh_{k}", f"control_plane_webhook_{k}"}
 
 
 def test_shard_load_report():

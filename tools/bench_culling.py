@@ -50,7 +50,10 @@ class _Load:
     def __init__(self, cpu: bool, root, minors):
         self.cpu, self.root, self.minors, self.gen = cpu, root, minors, None
 
-    def start(self):
+    def start(self, window_s: float):
+        """Start the load and return once the GPU has been busy for a whole sampling window:
+        the load thread's HIP start-up can take seconds on a fresh box, and a notebook resumed
+        meanwhile would be sampled idle — a race of this tool, not a cull of a busy GPU."""
         if self.cpu:
             from odh_kubeflow_amd.ops.telemetry import set_fake_counter
 
@@ -60,6 +63,9 @@ class _Load:
             from odh_kubeflow_amd.ops.gpu import LoadGenerator
 
             self.gen = LoadGenerator(0, duty=1.0, chunk_ms=5.0).start()
+            if not self.gen.wait_running(60.0):
+                raise RuntimeError("the MFMA load did not start on the GPU")
+        time.sleep(window_s + 0.05)
 
     def stop(self):
         if self.cpu:
@@ -173,7 +179,7 @@ async def run(args) -> dict:
             # again.  The load starts first, as a user's job outlives a restart: otherwise the
             # first notebooks back could pass CULL_IDLE_TIME while the last ones still start.
             stopped_at.clear()
-            load.start()
+            await asyncio.get_running_loop().run_in_executor(None, load.start, args.period_s)
             for nm in names:
                 await cl.admin.patch(kinds.NOTEBOOK, {"metadata": {"annotations": {STOP_ANNOTATION: None}}},
                                      name=nm, namespace="cull")

@@ -97,12 +97,15 @@ for s in $steps; do
         || fail bench $? "$out/bench_n1_s300.log"
       show "$out/bench_n1_s300.log" "n1 steps300" ;;
     resident)  # R resident notebooks with the culler on: at rest, and new notebooks on top; heartbeat filter A/B
+      # variants: split (culler in its own process, the default), inkf (culler in the kf process),
+      # nofilter (ODH_HEARTBEAT_FILTER=false: every heartbeat reconciles kf + odh and runs the pipeline)
       for r in $(seq 1 "${ROUNDS:-1}"); do
-        for v in true false; do
-          ODH_HEARTBEAT_FILTER=$v timeout -k 10 400 python bench.py --gpus 1 --steps 100 --warmup 10 --no-configs \
-            --no-inprocess-baseline --burst 0 --probe-sample 0 --resident "${RESIDENT:-1000}" --resident-window 5 \
-            > "$out/bench_resident_filter_${v}_r$r.log" 2>&1 || fail resident $? "$out/bench_resident_filter_${v}_r$r.log"
-          show "$out/bench_resident_filter_${v}_r$r.log" "resident filter=$v r$r"
+        for v in ${VARIANTS:-split inkf nofilter}; do
+          case $v in inkf) f="--culler-in-kf"; hb=true ;; nofilter) f=""; hb=false ;; *) f=""; hb=true ;; esac
+          ODH_HEARTBEAT_FILTER=$hb timeout -k 10 400 python bench.py --gpus 1 --steps 100 --warmup 10 --no-configs \
+            --no-inprocess-baseline --burst 0 --probe-sample 0 --resident "${RESIDENT:-1000}" --resident-window 5 $f \
+            > "$out/bench_resident_${v}_r$r.log" 2>&1 || fail resident $? "$out/bench_resident_${v}_r$r.log"
+          show "$out/bench_resident_${v}_r$r.log" "resident $v r$r"
         done
       done ;;
     b20x4)

@@ -655,7 +655,8 @@ class CullingReconciler:
             if nb is None:
                 return Result()
         if not culling_check_period_has_passed(nb, self.cfg.check_period_s):
-            return Result(requeue_after=self.cfg.check_period_s)
+            last = parse_rfc3339(m.annotations(nb).get(LAST_ACTIVITY_CHECK_TIMESTAMP_ANNOTATION))
+            return Result(requeue_after=self._next_check(req, last if last is not None else now()))
 
         self.checks += 1
         active_now, kernels, terminals, signals = await self.sample(nb, pod)
@@ -684,7 +685,26 @@ class CullingReconciler:
             self.cull_log.append({"notebook": str(req), "at": rfc3339(), **signals})
             log.info("Notebook %s/%s culled (idle for %.0f s): %s", req.namespace, req.name,
                      self.cfg.cull_idle_time_s, ", ".join(f"{k}={v}" for k, v in signals.items()))
-        return Result(requeue_after=self.cfg.check_period_s)
+        return Result(requeue_after=self._next_check(req, float(int(now()))))
+
+    def _next_check(self, req: Request, last_check: float) -> float:
+        """Seconds until this notebook's next check: the first slot of its phase at or after
+        ``last_check`` (the stamp, RFC3339 whole seconds) + the period.  Each notebook's checks
+        land on a fixed phase of the period (crc32 of its key), so R resident notebooks are
+        checked evenly spread, R / period per second.  The reference requeues each after exactly
+        the period (:200-202), so notebooks reconciled together — all of them when the manager
+        starts — stay checked together: R writes in one burst every period, which is when every
+        new notebook's create→Ready waits behind them.  The first aligned check may come up to one
+        period later than the reference's; every later one comes exactly a period apart."""
+        import zlib
+
+        p = self.cfg.check_period_s
+        if p <= 0:
+            return p
+        phase = zlib.crc32(f"{req.namespace}/{req.name}".encode()) / 2 ** 32 * p
+        target = last_check + p + 0.001  # strictly past the period at the wake-up
+        k = -(-(target - phase) // p)  # ceil
+        return max(0.001, phase + k * p - now())
 
     async def sample(self, nb: dict, pod: dict):
         """Returns ``(gpu_says_active, kernels, terminals, signals)``; ``signals`` says what each

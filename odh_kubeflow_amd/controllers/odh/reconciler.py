@@ -89,6 +89,32 @@ class OpenshiftNotebookReconciler:
         self._lock_wait_start: Dict[str, float] = {}
         self.locks_removed = 0
         self._openshift: Optional[bool] = None
+        # namespace -> names of the Notebooks still holding the reconciliation lock (kept from the
+        # Notebook watch): a ServiceAccount event looks at these few, not at every Notebook of its
+        # namespace (with R resident notebooks that scan was most of a new notebook's lock release)
+        self._locked: Dict[str, set] = {}
+        self._tracking_locks = False
+
+    def _on_notebook(self, etype: str, nb: dict, old: Optional[dict]) -> None:
+        ns, name = m.namespace(nb), m.name(nb)
+        if etype != "DELETED" and reconciliation_lock_enabled(nb):
+            self._locked.setdefault(ns, set()).add(name)
+        else:
+            s = self._locked.get(ns)
+            if s is not None:
+                s.discard(name)
+                if not s:
+                    del self._locked[ns]
+
+    def _locked_notebooks(self, ns: str) -> List[dict]:
+        if not self._tracking_locks:
+            return [nb for nb in self.reader.list(NOTEBOOK_KIND, ns) if reconciliation_lock_enabled(nb)]
+        out = []
+        for name in sorted(self._locked.get(ns, ())):
+            nb = self.reader.get(NOTEBOOK_KIND, name, ns)
+            if nb is not None and reconciliation_lock_enabled(nb):
+                out.append(nb)
+        return out
 
     # -------------------------------------------------------------- lock
 
@@ -433,8 +459,12 @@ class OpenshiftNotebookReconciler:
 
         def map_sa(o: dict):  # pull secret landed on the SA a locked notebook's pod will use
             ns = m.namespace(o)
-            return [Request(ns, m.name(nb)) for nb in self.reader.list(NOTEBOOK_KIND, ns)
-                    if reconciliation_lock_enabled(nb) and self.pod_service_account(nb) == m.name(o)]
+            return [Request(ns, m.name(nb)) for nb in self._locked_notebooks(ns)
+                    if self.pod_service_account(nb) == m.name(o)]
+
+        src = getattr(mgr, "cache", None) or mgr.reader
+        if hasattr(src, "subscribe"):
+            mgr.add(_LockTracker(self, src), needs_leader=False)
 
         alive, svc_preds, route_preds, nb_preds = [], [], [], [generation_or_metadata_changed]
         if not self.blocking_lock_removal:
@@ -473,3 +503,23 @@ class OpenshiftNotebookReconciler:
         if max_concurrent is not None:
             b.with_options(max_concurrent_reconciles=max_concurrent)
         return b.complete(self)
+
+
+class _LockTracker:
+    """Manager runnable: follows the Notebook watch into the reconciler's locked-notebook index
+    from start-up on (the subscription replays the cache, so nothing locked is missed)."""
+
+    def __init__(self, r: OpenshiftNotebookReconciler, src):
+        self.r = r
+        self.src = src
+        self._unsub = None
+
+    async def start(self):
+        self._unsub = self.src.subscribe(NOTEBOOK_KIND, self.r._on_notebook)
+        self.r._tracking_locks = True
+
+    async def stop(self):
+        if self._unsub is not None:
+            self._unsub()
+            self._unsub = None
+        self.r._tracking_locks = False

@@ -78,13 +78,16 @@ def params_env(version: str) -> str:
     MI355X ones; the start-up probe image is pinned to the release (images/probe.Dockerfile)."""
     return PARAMS_ENV + f"GPU_PROBE_IMAGE={PROBE_IMAGE_NAME}:{version}\n"
 # MI355X node settings (overlays mi355x and mi355x-sharded)
-MI355X_DEVICE_GROUPS = "44,110"  # video, render (Ubuntu 22.04 ROCm hosts); set to the node's own gids
+# the host groups owning /dev/kfd and /dev/dri/renderD*: HOST-SPECIFIC (Ubuntu allocates the
+# render gid dynamically), so the overlays ship it empty — an operator sets the nodes' own gids
+# (`stat -c %g /dev/kfd /dev/dri/renderD128` on a node; docs/DEPLOY.md).  A wrong gid would only
+# give every GPU pod an unrelated host group, and world-writable device nodes need none.
+MI355X_DEVICE_GROUPS = ""
 MI355X_PARAMS = ["GPU_NODE_SELECTOR=true", "GPU_SHM_SIZE_PER_GPU=16Gi",
                  # multi-GPU notebooks: RCCL's intra-node IPC over dmabuf (hosts whose amdgpu
                  # driver only offers dmabuf IPC fail hipIpcGetMemHandle otherwise)
                  "MULTI_GPU_ENV=HSA_ENABLE_IPC_MODE_LEGACY=0",
-                 # the host groups owning /dev/kfd and /dev/dri/renderD* (video, render on Ubuntu
-                 # hosts): non-root containers of GPU pods get them as supplementalGroups
+                 # non-root containers of GPU pods get these gids as supplementalGroups
                  f"GPU_DEVICE_GROUPS={MI355X_DEVICE_GROUPS}"]
 MI355X_CULLER = ["CULLING_ACTIVITY_SOURCE=combined", "ENABLE_CULLING=true"]
 # overlay mi355x: each manager runs its controllers in this many namespace-partitioned worker

@@ -536,11 +536,16 @@ async def _resident(args, shard, dist, native, children: dict, use_odh: bool,
     # ---- new notebooks on top of the population
     lat = []
     base = dict(ann or {})
+    gc0 = {k: v["seq"] for k, v in ((await safe(shard.gc_pauses(), {})) or {}).items()} if shard.procs else {}
     for i in range(max(0, int(getattr(args, "resident_steps", 20)))):
         r = await safe(_lifecycle(shard, f"nb-res-{i}", dict(base) or None, ns=nss[i % len(nss)]))
         if r is None:
             break
         lat.append(r[0] * 1e3)
+    # the control-plane processes' cyclic-GC pauses meanwhile (their event loops stop): with R
+    # notebooks in their caches a generation-2 pass walks all of them
+    gcp = {k: [x[1:] for x in v["pauses"]] for k, v in ((await safe(shard.gc_pauses(gc0), {})) or {}).items()} \
+        if shard.procs else {}
     await _in_thread(dist.barrier)
 
     # ---- teardown
@@ -562,7 +567,7 @@ async def _resident(args, shard, dist, native, children: dict, use_odh: bool,
         "k": k, "ok": ok and gone, "fill_s": fill_s, "win": win, "cpu": cpu, "rss": rss, "lat": lat,
         "in_window": breakdown_delta(b0 or {}, b1 or {}), "io": io_delta(io0 or {}, io1 or {}), "prof": rest_prof,
         "adm": (adm1 - adm0) if adm0 is not None and adm1 is not None else None, "heartbeats": heartbeats,
-        "served": served, "teardown": teardown, "errors": errors})
+        "served": served, "teardown": teardown, "errors": errors, "gc": gcp})
     if rank != 0:
         return None
     win = max(g["win"] for g in gathered)
@@ -613,7 +618,10 @@ async def _resident(args, shard, dist, native, children: dict, use_odh: bool,
         },
         "new_notebooks_on_top": {"steps_per_rank": int(getattr(args, "resident_steps", 20)), "ready_ms": _pcts(lat),
                                  "empty_cluster_p50_ms": round(empty_p50_ms, 3) if empty_p50_ms else None,
-                                 "p50_vs_empty": round(p50 / empty_p50_ms, 3) if p50 and empty_p50_ms else None},
+                                 "p50_vs_empty": round(p50 / empty_p50_ms, 3) if p50 and empty_p50_ms else None,
+                                 "gc_pause_ms": {proc: {"n": len(ps), "max": max(x[1] for x in ps),
+                                                        "gen2": sum(1 for x in ps if x[0] == 2)}
+                                                 for g in gathered for proc, ps in sorted(g["gc"].items()) if ps}},
         "teardown_s": round(max(g["teardown"] for g in gathered), 3),
         **({"errors": [e for g in gathered for e in g["errors"]]} if any(g["errors"] for g in gathered) else {}),
     }

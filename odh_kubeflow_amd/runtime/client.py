@@ -381,8 +381,8 @@ class CachedClient(Client):
             self.coalesced_reads += 1
         try:
             await asyncio.shield(cur[1])
-        except BaseException:  # noqa: BLE001 — the current read's outcome is not ours
-            pass
+        except Exception:  # noqa: BLE001 — the current read's outcome is not ours
+            pass  # (a cancellation of THIS reader propagates: another waiter sends the next GET)
         if self._next_flight.get(key) is nxt:
             # the first waiter sends the next GET for everyone queued behind the last one
             del self._next_flight[key]

@@ -29,6 +29,11 @@ log = logging.getLogger("runtime.informer")
 
 Transform = Callable[[dict], dict]
 
+# labels the cache indexes (``client.MatchingLabels`` lookups by them cost the matches, not a
+# scan of the namespace): ``notebook-name`` finds a notebook's HTTPRoutes among every notebook's
+# in the central namespace (odh/controllers/notebook_route.go:155-165) and its pods
+LABEL_INDEX_KEYS = ("notebook-name",)
+
 
 def strip_managed_fields(obj: dict) -> dict:
     md = obj.get("metadata")
@@ -58,6 +63,9 @@ class _Informer:
         self.items: Dict[Tuple[str, str], dict] = {}
         self.by_ns: Dict[str, Set[Tuple[str, str]]] = {}
         self.by_owner: Dict[str, Set[Tuple[str, str]]] = {}
+        # (label key, value) -> keys, for the cache's indexed label keys (LABEL_INDEX_KEYS)
+        self.by_label: Dict[Tuple[str, str], Set[Tuple[str, str]]] = {}
+        self._label_keys = cache.label_index_keys
         self.handlers: Dict[int, Tuple[Optional[str], WatchCallback]] = {}
         self.synced = asyncio.Event()
         self.rv = ""
@@ -92,21 +100,38 @@ class _Informer:
             self._unindex(k, old)
         self.items[k] = obj
         self.by_ns.setdefault(k[0], set()).add(k)
-        for r in (obj.get("metadata") or {}).get("ownerReferences") or []:
+        md = obj.get("metadata") or {}
+        for r in md.get("ownerReferences") or []:
             if r.get("uid"):
                 self.by_owner.setdefault(r["uid"], set()).add(k)
+        labels = md.get("labels")
+        if labels and self._label_keys:
+            for lk in self._label_keys:
+                v = labels.get(lk)
+                if v is not None:
+                    self.by_label.setdefault((lk, v), set()).add(k)
         return old
 
     def _unindex(self, k, obj) -> None:
         s = self.by_ns.get(k[0])
         if s is not None:
             s.discard(k)
-        for r in (obj.get("metadata") or {}).get("ownerReferences") or []:
+        md = obj.get("metadata") or {}
+        for r in md.get("ownerReferences") or []:
             s = self.by_owner.get(r.get("uid"))
             if s is not None:
                 s.discard(k)
                 if not s:
                     self.by_owner.pop(r.get("uid"), None)
+        labels = md.get("labels")
+        if labels and self._label_keys:
+            for lk in self._label_keys:
+                v = labels.get(lk)
+                s = self.by_label.get((lk, v)) if v is not None else None
+                if s is not None:
+                    s.discard(k)
+                    if not s:
+                        self.by_label.pop((lk, v), None)
 
     def _delete(self, obj: dict) -> Optional[dict]:
         k = (m.namespace(obj), m.name(obj))
@@ -252,7 +277,8 @@ class InformerCache(Reader, EventSource):
                  watch_timeout_s: int = 300, namespaces: Optional[Iterable[str]] = None,
                  selectors: Optional[Dict[str, str]] = None, namespace_selector: Optional[str] = None,
                  namespace_filter: Optional[Callable[[dict], bool]] = None,
-                 field_selectors: Optional[Dict[str, str]] = None):
+                 field_selectors: Optional[Dict[str, str]] = None,
+                 label_index_keys: Optional[Iterable[str]] = None):
         self.rest = rest
         self.namespace = namespace
         nss = list(namespaces) if namespaces is not None else ([namespace] if namespace else None)
@@ -268,6 +294,7 @@ class InformerCache(Reader, EventSource):
         self.selectors: Dict[str, str] = {SCHEME.resolve(k).key: v for k, v in (selectors or {}).items()}
         self.field_selectors: Dict[str, str] = {SCHEME.resolve(k).key: v for k, v in (field_selectors or {}).items()}
         self.watch_timeout_s = watch_timeout_s
+        self.label_index_keys = frozenset(LABEL_INDEX_KEYS if label_index_keys is None else label_index_keys)
         self._groups: Dict[str, _Group] = {}
         self._by_ref: Dict[str, _Group] = {}
         self._hid = 0
@@ -501,10 +528,16 @@ class InformerCache(Reader, EventSource):
         else:
             reqs = labels or []
         fm = field_matcher(parse_field_selector(fields)) if fields else None
+        indexed = next(((k, vals[0]) for k, op, vals in reqs if op == "=" and k in self.label_index_keys), None) \
+            if reqs and self.label_index_keys else None
         out = []
         for inf in infs:
             if owner_uid is not None:
                 keys = inf.by_owner.get(owner_uid, ())
+            elif indexed is not None:
+                # an equality on an indexed label: the candidates, not every object of the namespace
+                # (the odh reconciler's HTTPRoutes, found by label in the one central namespace)
+                keys = inf.by_label.get(indexed, ())
             elif namespace and inf.info.namespaced:
                 keys = inf.by_ns.get(namespace, ())
             else:

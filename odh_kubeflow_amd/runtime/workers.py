@@ -169,12 +169,17 @@ _SAMPLE = re.compile(r"^([A-Za-z_:][A-Za-z0-9_:]*)(\{.*\})?\s+(\S+)(?:\s+\S+)?$"
 
 
 def merge_metrics(texts: Sequence[str]) -> str:
-    """Sum Prometheus text expositions: one HELP/TYPE per family, samples with the same name
-    and labels added.  The families keep the order of their first appearance."""
+    """Merge Prometheus text expositions of the same metrics from several processes: one
+    HELP/TYPE per family; samples with the same name and labels are added for counters,
+    histograms and summaries, and the largest is kept for gauges (a gauge is a level — two
+    processes exporting ``last_notebook_culling_timestamp_seconds`` for the same notebook must
+    not add up to twice the epoch) and for ``_created`` timestamps the earliest.  The families
+    keep the order of their first appearance."""
     meta: Dict[str, List[str]] = {}
     order: List[str] = []
     samples: Dict[str, Dict[Tuple[str, str], float]] = {}
     fam_of: Dict[str, str] = {}
+    types: Dict[str, str] = {}
     for text in texts:
         fam = None
         for line in text.splitlines():
@@ -188,6 +193,8 @@ def merge_metrics(texts: Sequence[str]) -> str:
                         meta[fam] = []
                         order.append(fam)
                         samples[fam] = {}
+                    if parts[1] == "TYPE" and len(parts) == 4:
+                        types.setdefault(fam, parts[3].strip())
                     if not any(x.split(None, 2)[1] == parts[1] for x in meta[fam]):
                         meta[fam].append(line)
                 continue
@@ -213,6 +220,8 @@ def merge_metrics(texts: Sequence[str]) -> str:
                 samples[f][key] = v
             elif name.endswith("_created"):
                 samples[f][key] = min(prev, v)  # a creation timestamp: the earliest, not a sum
+            elif types.get(f) == "gauge":
+                samples[f][key] = max(prev, v)
             else:
                 samples[f][key] = prev + v
     out: List[str] = []
@@ -242,6 +251,7 @@ class _Worker:
         self.restarts = 0
         self.started_at = 0.0
         self.namespaces: set = set()
+        self.pending = False  # exited and not yet running again (a failed restart is retried)
 
     def send(self, line: str) -> None:
         if self.proc is None or self.proc.stdin is None:
@@ -360,27 +370,37 @@ class WorkerSupervisor:
         self._monitor = asyncio.ensure_future(self._watch())
 
     async def _watch(self) -> None:
-        """Restart a worker that exited, with exponential back-off (reset after a minute up)."""
+        """Restart a worker that exited, with exponential back-off (reset after a minute up).  A
+        restart that fails (the new process never reports ``ready``) leaves the worker pending:
+        every later pass tries again, each after a longer back-off, until one comes up."""
         delay: Dict[int, float] = {}
         while not self._stopping:
             await asyncio.sleep(0.2)
             for w in self.workers:
-                if self._stopping or w.proc is None or w.proc.poll() is None:
+                if self._stopping:
+                    return
+                exited = w.proc is not None and w.proc.poll() is not None
+                if not exited and not w.pending:
                     continue
-                up = time.monotonic() - w.started_at
-                d = self.backoff0 if up > 60 else min(self.backoff_max, delay.get(w.index, self.backoff0 / 2) * 2)
+                if exited:
+                    up = time.monotonic() - w.started_at
+                    d = self.backoff0 if up > 60 else min(self.backoff_max, delay.get(w.index, self.backoff0 / 2) * 2)
+                    log.error("%s worker %d/%d exited (rc=%s); restarting in %.1f s", self.name, w.index, self.count,
+                              w.proc.returncode, d)
+                    w.proc = None
+                    w.pending = True
+                else:  # the last restart failed
+                    d = min(self.backoff_max, delay.get(w.index, self.backoff0 / 2) * 2)
                 delay[w.index] = d
-                log.error("%s worker %d/%d exited (rc=%s); restarting in %.1f s", self.name, w.index, self.count,
-                          w.proc.returncode, d)
-                w.proc = None
                 await asyncio.sleep(d)
                 if self._stopping:
                     return
                 w.restarts += 1
                 try:
                     await self._spawn(w)
-                except Exception as e:  # noqa: BLE001 — retried on the next pass
-                    log.error("%s", e)
+                    w.pending = False
+                except Exception as e:  # noqa: BLE001 — pending: the next pass tries again
+                    log.error("%s; retrying", e)
                     w.proc = None
 
     def alive(self) -> bool:

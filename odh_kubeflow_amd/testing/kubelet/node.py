@@ -136,6 +136,10 @@ class SchedulerController:
             self._unbound.pop(uid, None)
         else:
             self._unbound[uid] = (m.namespace(pod), m.name(pod))
+        if node and uid in self._assumed:
+            # the informer has seen the binding: the assumption is confirmed (kube-scheduler's
+            # FinishBinding), so decisions stop walking it — it lives on as a cached pod
+            self._assumed.pop(uid, None)
         cur = self._pods.get(uid)
         ids = m.annotations(pod).get(GPU_IDS_ANNOTATION)
         want = None

@@ -95,6 +95,31 @@ def test_check_period(clock):
     assert not c.culling_check_period_has_passed(nbmeta({}), 60)
 
 
+def test_checks_land_on_a_per_notebook_phase_of_the_period(clock):
+    """R notebooks reconciled at the same instant (a manager start) are next checked spread over
+    the period — each on its own phase — not R at once every period; each wakes strictly past
+    its period, and a notebook keeps its phase from check to check."""
+    from odh_kubeflow_amd.runtime.controller import Request
+
+    r = c.CullingReconciler(None, None, config=c.CullerConfig(check_period_s=60.0))
+    clock[0] = 0.0
+
+    def due(req, last):  # absolute time of the next check
+        return timeutil.now() + r._next_check(req, last)
+
+    t = float(int(timeutil.now()))
+    when = [due(Request("ns", f"nb-{i}"), t) for i in range(1000)]
+    assert all(t + 60.0 < d <= t + 120.0 + 0.01 for d in when)
+    buckets = [0] * 6  # the 60 s after the first possible check, in 10 s buckets
+    for d in when:
+        buckets[min(5, int((d - t - 60.0) // 10))] += 1
+    assert min(buckets) > 120 and max(buckets) < 220  # ~167 each: spread, not a burst
+    req = Request("ns", "nb-7")
+    first = due(req, t)
+    clock[0] = first - time.time()  # the check runs at its slot and stamps its whole second
+    assert abs(due(req, float(int(first))) - (first + 60.0)) < 0.01  # a period later, same phase
+
+
 def test_start_up_time_is_not_idle_time():
     """A Pending pod (image pull, the odh-gpu-probe init container) is not checked, and the
     idle clock starts no earlier than the pod's Ready transition (the reference counts from

@@ -103,6 +103,45 @@ def test_worker_reads_initial_set_then_follows_stdin(run):
     run(go())
 
 
+_FAKE_WORKER = """
+import os, sys, time
+state = os.environ["FAKE_STATE"]
+n = int(open(state).read()) if os.path.exists(state) else 0
+open(state, "w").write(str(n + 1))
+if os.environ.get("FAKE_FAIL_START") == str(n):
+    sys.exit(3)  # dies before it reports ready
+print("ready", flush=True)
+for _line in sys.stdin:
+    pass
+"""
+
+
+def test_failed_worker_restart_is_retried(run, tmp_path):
+    """A worker that exits is restarted; when that restart fails (the new process never reports
+    ready) the worker stays pending and a later pass brings it back (it was dropped
+    for good, its namespaces unserved until the liveness probe killed the pod)."""
+    import time
+
+    (tmp_path / "fakeworker.py").write_text(_FAKE_WORKER)
+    env = {**os.environ, "PYTHONPATH": str(tmp_path), "FAKE_STATE": str(tmp_path / "starts"), "FAKE_FAIL_START": "1"}
+
+    async def go():
+        s = wk.WorkerSupervisor("fakeworker", 1, lambda i, a: [], env=env, start_timeout=10,
+                                restart_backoff=(0.05, 0.2))
+        await s.start()
+        try:
+            w = s.workers[0]
+            w.proc.kill()  # crash: start 1 fails, start 2 succeeds
+            deadline = time.monotonic() + 30
+            while time.monotonic() < deadline and not (w.restarts >= 2 and not w.pending and s.alive()):
+                await asyncio.sleep(0.05)
+            assert s.alive() and not w.pending
+            assert w.restarts == 2 and (tmp_path / "starts").read_text() == "3"
+        finally:
+            await s.stop()
+    run(go())
+
+
 def test_merge_metrics_sums_samples_and_keeps_one_header():
     a = ("# HELP x_total Things.\n# TYPE x_total counter\nx_total{ns=\"a\"} 2.0\nx_created{ns=\"a\"} 100.0\n"
          "# HELP h Hist.\n# TYPE h histogram\nh_bucket{le=\"1.0\"} 1.0\nh_sum 0.5\nh_count 1.0\n")
@@ -118,6 +157,11 @@ def test_merge_metrics_sums_samples_and_keeps_one_header():
 
     fams = {f.name: f for f in text_string_to_metric_families(out)}
     assert set(fams) >= {"x", "h"}
+    # gauges are levels, not counts: the same label set from two processes keeps the larger
+    g1 = "# HELP last_ts T.\n# TYPE last_ts gauge\nlast_ts{name=\"nb\"} 1.7e9\nlast_ts{name=\"a\"} 5.0\n"
+    g2 = "# HELP last_ts T.\n# TYPE last_ts gauge\nlast_ts{name=\"nb\"} 1.6e9\n"
+    out = wk.merge_metrics([g1, g2])
+    assert 'last_ts{name="nb"} 1700000000.0' in out and 'last_ts{name="a"} 5.0' in out
 
 
 def test_worker_command_lines_drop_what_only_the_supervisor_does():
@@ -286,4 +330,42 @@ def test_concurrent_live_reads_of_one_object_are_coalesced_but_fresh(run):
         assert await first is None  # began before the write: may miss it
         assert await asyncio.gather(*later) == ["1"] * 20  # all fresh, from ONE more GET
         assert w.gets == 2 and c.coalesced_reads == 19
+    run(go())
+
+
+def test_cancelled_queued_live_reader_is_cancelled_and_the_others_still_read(run):
+    """A reader queued behind an in-flight GET that is cancelled (its admission timed out, the
+    manager stops) raises CancelledError instead of going on to send a GET of its own; the
+    readers queued with it still get one fresh GET between them."""
+    from odh_kubeflow_amd.runtime.client import CachedClient
+
+    class Writer:
+        def __init__(self):
+            self.gets = 0
+            self.gate = asyncio.Event()
+
+        async def get(self, kind, name, namespace=None):
+            self.gets += 1
+            await self.gate.wait()
+            return {"metadata": {"name": name, "namespace": namespace, "resourceVersion": str(self.gets)}}
+
+    class Reader:
+        def watching(self, kind, ns):
+            return False
+
+    async def go():
+        w = Writer()
+        c = CachedClient(Reader(), w, uncached=(kinds.CONFIG_MAP,))
+        first = asyncio.ensure_future(c.get(kinds.CONFIG_MAP, "cm", "ns"))
+        await asyncio.sleep(0)
+        queued = [asyncio.ensure_future(c.get(kinds.CONFIG_MAP, "cm", "ns")) for _ in range(3)]
+        await asyncio.sleep(0)
+        queued[0].cancel()
+        await asyncio.sleep(0)
+        w.gate.set()
+        await first
+        with pytest.raises(asyncio.CancelledError):
+            await queued[0]
+        rvs = [o["metadata"]["resourceVersion"] for o in await asyncio.gather(*queued[1:])]
+        assert rvs == ["2", "2"] and w.gets == 2  # one more GET for the two left, none for the cancelled one
     run(go())

@@ -61,7 +61,7 @@ def pct(xs, q):
     return xs[min(len(xs) - 1, int(round(q * (len(xs) - 1))))]
 
 
-def analyse(lines, ns_prefix: str = "") -> dict:
+def analyse(lines, ns_prefix: str = "", name_prefix: str = "") -> dict:
     by_obj = defaultdict(list)  # (ns, resource, name) -> events in order
     for line in lines:
         e = json.loads(line)
@@ -78,7 +78,7 @@ def analyse(lines, ns_prefix: str = "") -> dict:
             (_ts(e["requestReceivedTimestamp"]), _ts(e["stageTimestamp"]), e["verb"], ref.get("subresource", ""),
              e.get("userAgent", "").split("/")[0]))
     notebooks = [(ns, name) for (ns, res, name) in by_obj if res == "notebooks" and name and
-                 any(v == "create" for _, _, v, _, _ in by_obj[(ns, res, name)])]
+                 name.startswith(name_prefix) and any(v == "create" for _, _, v, _, _ in by_obj[(ns, res, name)])]
     # every successful write, attributed to its client and target: who spends the writes
     writes = defaultdict(int)
     for (ns, res, name), evs in by_obj.items():
@@ -155,9 +155,11 @@ def main(argv=None) -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("audit_log")
     ap.add_argument("--namespace-prefix", default="")
+    ap.add_argument("--name-prefix", default="", help="only Notebooks whose name starts with this (nb-s: the timed "
+                                                      "window; nb-res-: the notebooks created on top of --resident)")
     a = ap.parse_args(argv)
     with open(a.audit_log) as f:
-        print(json.dumps(analyse(f, a.namespace_prefix), indent=1))
+        print(json.dumps(analyse(f, a.namespace_prefix, a.name_prefix), indent=1))
     return 0
 
 

@@ -108,6 +108,15 @@ for s in $steps; do
           show "$out/bench_resident_${v}_r$r.log" "resident $v r$r"
         done
       done ;;
+    rescp)  # hop by hop: the timed window's notebooks (empty cluster) vs those created on top of R resident
+      DEBUG_WRITE_AUDITLOG=$PWD/$out/ares.jsonl timeout -k 10 400 python bench.py --gpus 1 --steps 100 --warmup 10 \
+        --no-configs --no-inprocess-baseline --burst 0 --probe-sample 0 --resident "${RESIDENT:-1000}" \
+        --resident-window 3 --resident-steps 50 > "$out/bench_rescp.log" 2>&1 || fail rescp $? "$out/bench_rescp.log"
+      show "$out/bench_rescp.log" "rescp"
+      python tools/critical_path.py $out/ares.jsonl --name-prefix nb-s > $out/critical_path_timed.json || exit 1
+      python tools/critical_path.py $out/ares.jsonl --name-prefix nb-res- > $out/critical_path_on_top.json || exit 1
+      rm -f $out/ares.jsonl
+      echo "critical paths written" ;;
     b20x4)
       for r in 1 2 3 4; do
         echo "run $r start $(date +%s.%N)"

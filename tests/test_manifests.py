@@ -245,19 +245,23 @@ def test_sharded_overlay_shape():
     (sts,) = _by(objs, "StatefulSet").values()
     n = sts["spec"]["replicas"]
     assert n == manifests.SHARDS == 8
-    # the shard pod: the control plane split into a kf, an odh and a webhook process
-    kf, odh, wh = sts["spec"]["template"]["spec"]["containers"]
+    # the shard pod: the control plane split into a kf (notebook), a culler, an odh and a webhook process
+    kf, cull, odh, wh = sts["spec"]["template"]["spec"]["containers"]
     assert "--shard=ordinal" in kf["args"] and f"--shard-count={n}" in kf["args"] and "--assign-namespaces" in kf["args"]
-    assert "--controllers=kf" in kf["args"] and "--controllers=odh" in odh["args"]
-    assert "--controllers=webhook" in wh["args"]
-    for c in (odh, wh):
+    assert "--controllers=notebook" in kf["args"] and "--controllers=culler" in cull["args"]
+    assert "--controllers=odh" in odh["args"] and "--controllers=webhook" in wh["args"]
+    for c in (cull, odh, wh):
         assert "--shard=ordinal" in c["args"] and "--assign-namespaces" not in c["args"]
     assert [p["containerPort"] for p in kf["ports"]] == [8080, 8081]
+    assert [p["containerPort"] for p in cull["ports"]] == [8086, 8087]
     assert [p["containerPort"] for p in odh["ports"]] == [8082, 8083]
     assert [p["containerPort"] for p in wh["ports"]] == [8443, 8084, 8085]
-    assert len({p["name"] for c in (kf, odh, wh) for p in c["ports"]}) == 7  # pod-unique port names
-    assert [c["readinessProbe"]["httpGet"]["port"] for c in (kf, odh, wh)] == [8081, 8083, 8085]
-    assert [v["name"] for v in wh["volumeMounts"]] == ["cert"] and odh["volumeMounts"] == []
+    assert len({p["name"] for c in (kf, cull, odh, wh) for p in c["ports"]}) == 9  # pod-unique port names
+    assert [c["readinessProbe"]["httpGet"]["port"] for c in (kf, cull, odh, wh)] == [8081, 8087, 8083, 8085]
+    assert [v["name"] for v in wh["volumeMounts"]] == ["cert"] and odh["volumeMounts"] == [] == kf["volumeMounts"]
+    # the culler asks the node agents (GPU-busy culling): their token and CA
+    assert {v["mountPath"] for v in cull["volumeMounts"]} == {manifests.AGENT_TOKEN_MOUNT_SPEC["mountPath"],
+                                                                manifests.AGENT_CA_MOUNT_SPEC["mountPath"]}
     svcs = _by(objs, "Service")
     mwcs = _by(objs, "MutatingWebhookConfiguration")
     assert len(mwcs) == n + 1

@@ -84,6 +84,9 @@ class ShardConfig:
     split: bool = True  # sharded, process mode: the shard pod's containers as processes (kf | odh | webhook)
     webhook_process: bool = True  # sharded, split: the webhook in a process of its own (False: odh + webhook)
     culler_process: bool = False  # sharded, split: the culler in a process of its own (notebook | culler)
+    # sharded: flags added to every process that leads something (e.g. --leader-elect and the lease
+    # timings; tools/bench_failover.py runs standby replicas next to them)
+    leader_elect_args: List[str] = field(default_factory=list)
     workers: int = 1  # unsharded: --workers of the kf and odh managers (runtime/workers.py)
     webhook_replicas: int = 1  # unsharded with workers: --webhook-replicas of the odh manager
     cache_configmaps: bool = False  # unsharded: --cache-configmaps-secrets=true on the odh manager
@@ -161,6 +164,8 @@ class ControlPlaneShard:
                           "--assign-policy", cfg.assign_policy]
                 if cfg.reference_emulation:
                     a.append("--reference-emulation")
+                if cs != ["webhook"]:
+                    a += cfg.leader_elect_args
                 name = "control_plane" if len(sets) == 1 else f"control_plane_{names.get(cs[0], cs[0])}"
                 out.append((name, "odh_kubeflow_amd.cmd.control_plane", a, "--metrics-bind-address"))
             return out

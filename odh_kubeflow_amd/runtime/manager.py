@@ -33,8 +33,15 @@ class Manager:
                  registry: Optional[CollectorRegistry] = None,
                  default_max_concurrent: int = DEFAULT_MAX_CONCURRENT_RECONCILES,
                  leader_elector=None, metrics_addr: Optional[str] = None, probe_addr: Optional[str] = None,
-                 debug_endpoints: bool = False):
+                 debug_endpoints: bool = False, warm_standby: bool = True):
         self.name = name
+        # with leader election: a standby replica lists and watches what its controllers will
+        # watch before it leads, so a takeover starts reconciling from a synced cache instead of
+        # relisting every Notebook and child first (controller-runtime starts the controllers'
+        # informers only once elected)
+        self.warm_standby = warm_standby
+        self.synced_at: Optional[float] = None  # monotonic: the controllers' kinds were synced
+        self.elected_at: Optional[float] = None  # monotonic: this replica took the lead
         self.client = client
         self.reader = reader
         self.source = source
@@ -149,11 +156,21 @@ class Manager:
         if self.leader_elector is None:
             await self._become_leader()
         else:
+            if self.warm_standby and self.controllers:
+                kinds_ = list(dict.fromkeys(w.kind for c in self.controllers for w in c.watches))
+                try:
+                    await self.source.wait_synced(kinds_)
+                    self.synced_at = time.monotonic()
+                except Exception:  # noqa: BLE001 — the controllers sync them again when elected
+                    log.warning("%s: warming the standby cache failed", self.name, exc_info=True)
             self._leader_task = asyncio.ensure_future(self.leader_elector.run(self._become_leader, self._lost_leader))
 
     async def _become_leader(self) -> None:
+        self.elected_at = time.monotonic()
         for c in self.controllers:
             await c.start(self.source)
+        if self.synced_at is None:
+            self.synced_at = time.monotonic()
         for r in self.leader_runnables:
             await r.start()
         self.elected.set()
@@ -288,7 +305,8 @@ class Manager:
         rest = getattr(self, "rest", None)
         ev = cache.event_counts() if hasattr(cache, "event_counts") else {}
         lists = cache.relist_counts() if hasattr(cache, "relist_counts") else {}
-        return {"watch_events": ev, "requests": dict(getattr(rest, "by_verb", {}) or {}), "lists": lists}
+        return {"watch_events": ev, "requests": dict(getattr(rest, "by_verb", {}) or {}), "lists": lists,
+                "bytes_in": dict(getattr(rest, "bytes_in", {}) or {})}
 
     def reconcile_count(self) -> int:
         return sum(c.reconciles for c in self.controllers)
@@ -363,6 +381,8 @@ class Manager:
                                       "io": merge_counts([self.io_counters(), *(d.get("io") for d in docs + rdocs)]),
                                       "workers": len(docs),
                                       "worker_pids": pids,
+                                      "leader": bool(self.elected is not None and self.elected.is_set()),
+                                      "pending": sum(c.queue.pending() + c.active for c in self.controllers),
                                       "assignments": {str(i): nss for i, nss in self.supervisor.assignments().items()}
                                       if self.supervisor is not None else {}})
 

@@ -165,6 +165,7 @@ class RestClient(Client):
         self._bucket = TokenBucket(config.qps, config.burst)
         self.requests = 0
         self.by_verb: Dict[str, int] = {}  # requests per HTTP method (watches counted as WATCH)
+        self.bytes_in: Dict[str, int] = {}  # response body bytes: "LIST" (lists + relists) and "other"
         from collections import deque
 
         self.get_ms = deque(maxlen=8192)  # wall time of the recent GETs (ms): the live-read latency
@@ -192,7 +193,7 @@ class RestClient(Client):
         return self.base + info.path(version, namespace if info.namespaced else None, name, sub)
 
     async def request(self, method: str, url: str, body: Any = None, params: Optional[dict] = None,
-                      content_type: str = "application/json") -> dict:
+                      content_type: str = "application/json", count_as: str = "other") -> dict:
         from urllib.parse import urlencode
 
         from .http1 import HttpError
@@ -222,6 +223,8 @@ class RestClient(Client):
                 await asyncio.sleep(min(0.5, 0.01 * (2 ** attempt)))
         if method == "GET":
             self.get_ms.append((time.perf_counter() - t0) * 1e3)
+        if raw:
+            self.bytes_in[count_as] = self.bytes_in.get(count_as, 0) + len(raw)
         try:
             out = json.loads(raw) if raw else {}
         except ValueError:
@@ -293,7 +296,7 @@ class RestClient(Client):
             params["labelSelector"] = format_label_selector(labels) if isinstance(labels, dict) else labels
         if fields:
             params["fieldSelector"] = fields
-        out = await self.request("GET", self.path(info, v, namespace), params=params or None)
+        out = await self.request("GET", self.path(info, v, namespace), params=params or None, count_as="LIST")
         items = out.get("items") or []
         av = info.api_version(v)
         for o in items:

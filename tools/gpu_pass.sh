@@ -108,6 +108,10 @@ for s in $steps; do
           show "$out/bench_resident_${v}_r$r.log" "resident $v r$r"
         done
       done ;;
+    failover)  # takeover (SIGKILL, standby with warm caches) and graceful cold start with R resident notebooks
+      timeout -k 10 600 python tools/bench_failover.py --resident "${RESIDENT:-1000}" > "$out/failover.log" 2>&1 \
+        || fail failover $? "$out/failover.log"
+      tail -1 "$out/failover.log" | cut -c1-3000 ;;
     rescp)  # hop by hop: the timed window's notebooks (empty cluster) vs those created on top of R resident
       DEBUG_WRITE_AUDITLOG=$PWD/$out/ares.jsonl timeout -k 10 400 python bench.py --gpus 1 --steps 100 --warmup 10 \
         --no-configs --no-inprocess-baseline --burst 0 --probe-sample 0 --resident "${RESIDENT:-1000}" \

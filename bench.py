@@ -81,6 +81,9 @@ def parse(argv=None):
                         "created unlabelled and assigned to shards by the shipped NamespaceShardAssigner "
                         "(crc32(name) %% N), so a shard serves the namespaces that hash to it, whichever rank "
                         "drives them — per-shard notebooks, notebooks/s and CPU are reported")
+    p.add_argument("--cluster-wide-watches", action="store_true",
+                   help="control-plane processes watch each kind once, cluster-wide, filtering namespaces "
+                        "themselves, instead of one watch per served namespace per kind (A/B at many namespaces)")
     p.add_argument("--assign-policy", choices=("hash", "balanced"), default="hash",
                    help="--namespaces-per-rank, sharded: the NamespaceShardAssigner policy (hash: crc32 %% N; "
                         "balanced: the shard owning the fewest namespaces, as overlay mi355x-sharded deploys it)")

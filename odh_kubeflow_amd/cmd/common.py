@@ -59,6 +59,16 @@ def add_shard_flags(p) -> None:
     p.add_argument("--shard", default=None,
                    help="serve only namespaces labelled notebooks.amd.com/shard=<SHARD> (+ the controller "
                         "namespace); 'ordinal' takes it from the StatefulSet pod name (POD_NAME/HOSTNAME -<n>)")
+    add_watch_scope_flag(p)
+
+
+def add_watch_scope_flag(p) -> None:
+    """``--cluster-wide-watches``: a process that serves a subset of the namespaces (a shard, a
+    ``--workers`` worker) watches each kind once, cluster-wide, dropping the other namespaces'
+    objects on arrival — instead of one watch per served namespace per kind."""
+    p.add_argument("--cluster-wide-watches", action="store_true",
+                   help="one cluster-wide watch per kind, filtered here by namespace, instead of a watch per "
+                        "served namespace per kind (many namespaces per shard or worker)")
 
 
 def resolve_shard(value, env=None):

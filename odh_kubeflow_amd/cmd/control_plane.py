@@ -138,7 +138,7 @@ def build(args, env=os.environ):
                                 retry_period=args.leader_election_retry_period)
     name = "notebook-control-plane" + (f"-shard-{shard}" if shard is not None else "") + subset
     mgr = Manager.remote(cfg, name=name, uncached=uncached, transforms=transforms,
-                         cache_options=shard_cache_options(shard, namespace),
+                         cache_options=shard_cache_options(shard, namespace, args.cluster_wide_watches),
                          default_max_concurrent=args.max_concurrent_reconciles, leader_elector=elector,
                          metrics_addr=args.metrics_bind_address, probe_addr=args.health_probe_bind_address,
                          debug_endpoints=args.enable_debug_endpoints)

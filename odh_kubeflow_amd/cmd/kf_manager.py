@@ -88,10 +88,10 @@ def build(args, env=os.environ):
                                 lease_duration=args.leader_election_lease_duration,
                                 renew_deadline=args.leader_election_renew_deadline,
                                 retry_period=args.leader_election_retry_period)
-    cache_options = shard_cache_options(shard, namespace_from_env())
+    cache_options = shard_cache_options(shard, namespace_from_env(), args.cluster_wide_watches)
     assign = WorkerAssignments(*worker) if worker is not None else None
     if assign is not None:
-        cache_options = assign.cache_options()
+        cache_options = assign.cache_options(cluster_watch=args.cluster_wide_watches)
     mgr = Manager.remote(cfg, name="notebook-controller", default_max_concurrent=args.max_concurrent_reconciles,
                          leader_elector=elector, metrics_addr=args.metrics_addr, probe_addr=args.probe_addr,
                          debug_endpoints=args.enable_debug_endpoints, cache_options=cache_options)

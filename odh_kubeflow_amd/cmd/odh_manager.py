@@ -120,11 +120,11 @@ def build(args, env=os.environ):
     lease = "odh-notebook-controller" + (f"-shard-{shard}" if shard is not None else "")
     elector = (LeaderElector(RestClient(cfg), lease, namespace)
                if args.leader_elect and worker is None and replica is None else None)
-    cache_options = shard_cache_options(shard, namespace)
+    cache_options = shard_cache_options(shard, namespace, args.cluster_wide_watches)
     assign = WorkerAssignments(*worker) if worker is not None else None
     if assign is not None:
         # the controller namespace holds the central HTTPRoutes and ImageStreams every worker reads
-        cache_options = assign.cache_options(extra_namespaces=[namespace])
+        cache_options = assign.cache_options(extra_namespaces=[namespace], cluster_watch=args.cluster_wide_watches)
     cache_cm = getattr(args, "cache_configmaps_secrets", "false") == "true"
     mgr = Manager.remote(cfg, name="odh-notebook-controller",
                          uncached=() if cache_cm else (kinds.CONFIG_MAP, kinds.SECRET),

@@ -90,13 +90,15 @@ def setup_odh(mgr, namespace: str, env: Mapping[str, str] = os.environ, *, shard
     return r
 
 
-def shard_cache_options(shard: Optional[str], controller_namespace: str) -> dict:
+def shard_cache_options(shard: Optional[str], controller_namespace: str, cluster_watch: bool = False) -> dict:
     """InformerCache keyword arguments for one shard: the namespaces labelled
     ``notebooks.amd.com/shard=<shard>`` (followed live) plus the controller namespace, with
-    HTTPRoutes selected by the same label (``{}`` when not sharded: cluster-wide)."""
+    HTTPRoutes selected by the same label (``{}`` when not sharded: cluster-wide).
+    ``cluster_watch``: one cluster-wide watch per kind filtered here, instead of one per namespace."""
     from ..models import kinds
 
     if shard is None:
         return {}
     sel = f"{SHARD_LABEL}={shard}"
-    return {"namespace_selector": sel, "namespaces": [controller_namespace], "selectors": {kinds.HTTP_ROUTE: sel}}
+    return {"namespace_selector": sel, "namespaces": [controller_namespace], "selectors": {kinds.HTTP_ROUTE: sel},
+            "cluster_watch": cluster_watch}

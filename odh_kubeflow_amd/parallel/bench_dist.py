@@ -797,7 +797,8 @@ async def _main(args, dist, torch, rank: int, world: int, ndev: int, probe_sampl
         webhook_replicas=max(1, getattr(args, "webhook_replicas", 1)),
         webhook_process=not getattr(args, "webhook_in_odh", False),
         cache_configmaps=getattr(args, "cache_configmaps", False), driven_only=True,
-        culler_process=culling and not getattr(args, "culler_in_kf", False)))
+        culler_process=culling and not getattr(args, "culler_in_kf", False),
+        cluster_watch=getattr(args, "cluster_wide_watches", False)))
     if rank == 0:
         await shard.start()  # cluster namespaces (and, unsharded, the managers + their webhook) first
         await _in_thread(dist.barrier)

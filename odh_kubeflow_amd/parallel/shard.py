@@ -87,6 +87,7 @@ class ShardConfig:
     # sharded: flags added to every process that leads something (e.g. --leader-elect and the lease
     # timings; tools/bench_failover.py runs standby replicas next to them)
     leader_elect_args: List[str] = field(default_factory=list)
+    cluster_watch: bool = False  # --cluster-wide-watches on every control-plane process
     workers: int = 1  # unsharded: --workers of the kf and odh managers (runtime/workers.py)
     webhook_replicas: int = 1  # unsharded with workers: --webhook-replicas of the odh manager
     cache_configmaps: bool = False  # unsharded: --cache-configmaps-secrets=true on the odh manager
@@ -134,7 +135,7 @@ class ControlPlaneShard:
 
     def _common_flags(self) -> List[str]:
         return ["--master", self.cfg.apiserver_url, "--max-concurrent-reconciles", str(self.cfg.max_concurrent),
-                "--enable-debug-endpoints"]
+                "--enable-debug-endpoints", *(["--cluster-wide-watches"] if self.cfg.cluster_watch else [])]
 
     def _specs(self, webhook_port: int, split: Optional[bool] = None):
         """(name, module, argv, metrics flag) of the processes this rank launches."""

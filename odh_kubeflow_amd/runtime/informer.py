@@ -35,6 +35,13 @@ Transform = Callable[[dict], dict]
 LABEL_INDEX_KEYS = ("notebook-name",)
 
 
+def _rv_num(obj: dict) -> int:
+    try:
+        return int(m.resource_version(obj) or 0)
+    except (TypeError, ValueError):
+        return 0
+
+
 def strip_managed_fields(obj: dict) -> dict:
     md = obj.get("metadata")
     if md and "managedFields" in md:
@@ -66,6 +73,9 @@ class _Informer:
         # (label key, value) -> keys, for the cache's indexed label keys (LABEL_INDEX_KEYS)
         self.by_label: Dict[Tuple[str, str], Set[Tuple[str, str]]] = {}
         self._label_keys = cache.label_index_keys
+        # a cluster-wide informer of a namespace-restricted cache (``cluster_watch``): objects of
+        # namespaces this returns False for are dropped on arrival
+        self.ns_filter: Optional[Callable[[str], bool]] = None
         self.handlers: Dict[int, Tuple[Optional[str], WatchCallback]] = {}
         self.synced = asyncio.Event()
         self.rv = ""
@@ -160,12 +170,45 @@ class _Informer:
 
     # -------------------------------------------------------------- list / watch loop
 
+    async def fill_namespace(self, ns: str) -> None:
+        """A namespace joined a cluster-wide informer's filter: its objects, dropped until now,
+        are listed once (events of it are kept from now on; a listed copy older than one an
+        event already brought is not applied)."""
+        try:
+            items, _rv = await self.cache.rest.list_rv(f"{self.info.api_version(self.version)}/{self.info.kind}",
+                                                       ns, self.label_selector, self.field_selector)
+        except Exception:  # noqa: BLE001 — a relist of the whole kind (410 / reconnect) fills it later
+            log.warning("%s: listing namespace %s failed", self.info.kind, ns, exc_info=True)
+            return
+        self.relists += 1
+        if self.ns_filter is not None and not self.ns_filter(ns):
+            return  # left again meanwhile
+        for o in items:
+            o = self._transform(o)
+            k = (m.namespace(o), m.name(o))
+            cur = self.items.get(k)
+            if cur is not None and _rv_num(cur) >= _rv_num(o):
+                continue
+            old = self._put(o)
+            self._notify("ADDED" if old is None else "MODIFIED", o, old)
+
+    def drop_namespace(self, ns: str) -> None:
+        """A namespace left a cluster-wide informer's filter: to subscribers its objects are gone."""
+        for k in list(self.by_ns.get(ns, ())):
+            old = self.items.get(k)
+            if old is not None:
+                self._delete(old)
+                self._notify("DELETED", old, old)
+
     async def _relist(self) -> None:
         items, rv = await self.cache.rest.list_rv(f"{self.info.api_version(self.version)}/{self.info.kind}",
                                                   self.namespace, self.label_selector, self.field_selector)
         self.relists += 1
         seen = set()
+        nsf = self.ns_filter
         for o in items:
+            if nsf is not None and not nsf(m.namespace(o)):
+                continue
             o = self._transform(o)
             k = (m.namespace(o), m.name(o))
             seen.add(k)
@@ -202,8 +245,10 @@ class _Informer:
                     if et == "BOOKMARK":
                         self.rv = m.resource_version(obj) or self.rv
                         continue
-                    obj = self._transform(obj)
                     self.rv = m.resource_version(obj) or self.rv
+                    if self.ns_filter is not None and not self.ns_filter(m.namespace(obj)):
+                        continue  # a cluster-wide watch: another shard's (or worker's) namespace
+                    obj = self._transform(obj)
                     if et != "DELETED" and self._label_reqs is not None and not match_labels(
                             self._label_reqs, (obj.get("metadata") or {}).get("labels")):
                         # the object left the selector: to this cache it is gone
@@ -278,7 +323,7 @@ class InformerCache(Reader, EventSource):
                  selectors: Optional[Dict[str, str]] = None, namespace_selector: Optional[str] = None,
                  namespace_filter: Optional[Callable[[dict], bool]] = None,
                  field_selectors: Optional[Dict[str, str]] = None,
-                 label_index_keys: Optional[Iterable[str]] = None):
+                 label_index_keys: Optional[Iterable[str]] = None, cluster_watch: bool = False):
         self.rest = rest
         self.namespace = namespace
         nss = list(namespaces) if namespaces is not None else ([namespace] if namespace else None)
@@ -288,6 +333,10 @@ class InformerCache(Reader, EventSource):
         self._dynamic = bool(namespace_selector) or namespace_filter is not None
         # None = every namespace (cluster-wide informers)
         self.namespaces: Optional[Set[str]] = set(nss or ()) if (nss or self._dynamic) else None
+        # ``cluster_watch``: a namespace-restricted cache that still opens ONE list/watch per kind,
+        # cluster-wide, and drops the other namespaces' objects on arrival — one watch stream per
+        # kind however many namespaces it serves, for every event of the kind decoded here
+        self.cluster_watch = bool(cluster_watch) and self.namespaces is not None
         self.transforms: Dict[str, Optional[Transform]] = {}
         for k, fn in (transforms or {}).items():
             self.transforms[SCHEME.resolve(k).key] = fn
@@ -324,15 +373,27 @@ class InformerCache(Reader, EventSource):
                 self.namespaces.discard(ns)
                 self.namespace_changes += 1
                 for g in self._groups.values():
-                    inf = g.infs.pop(ns, None) if g.info.namespaced else None
+                    if not g.info.namespaced:
+                        continue
+                    if self.cluster_watch:
+                        for inf in g.infs.values():
+                            inf.drop_namespace(ns)
+                        continue
+                    inf = g.infs.pop(ns, None)
                     if inf is not None:
                         self._retire(inf)
         elif ns not in self.namespaces:
             self.namespaces.add(ns)
             self.namespace_changes += 1
             for g in self._groups.values():
-                if g.info.namespaced:
-                    self._start_informer(g, ns)
+                if not g.info.namespaced:
+                    continue
+                if self.cluster_watch:
+                    for inf in g.infs.values():
+                        if inf.synced.is_set():  # else its first list, still to come, includes it
+                            asyncio.ensure_future(inf.fill_namespace(ns))
+                    continue
+                self._start_informer(g, ns)
 
     def refresh_namespace(self, name: str) -> None:
         """Re-evaluate ``namespace_filter`` for one namespace (its answer changed: a worker was
@@ -391,18 +452,20 @@ class InformerCache(Reader, EventSource):
 
             self._ensure_ns_informer()
             g = self._groups[info.key] = _Group(info, _version_of(kind) or info.storage_version)
-            if info.namespaced and self.namespaces is not None:
+            if info.namespaced and self.namespaces is not None and not self.cluster_watch:
                 for ns in sorted(self.namespaces):
                     self._start_informer(g, ns)
             else:
-                self._start_informer(g, None)
+                inf = self._start_informer(g, None)
+                if info.namespaced and self.cluster_watch:
+                    inf.ns_filter = self.namespaces.__contains__
         if type(kind) is str:
             self._by_ref[kind] = g
         return g
 
     def _for_ns(self, kind, namespace: Optional[str]) -> List[_Informer]:
         g = self._group(kind)
-        if namespace and g.info.namespaced and self.namespaces is not None:
+        if namespace and g.info.namespaced and self.namespaces is not None and not self.cluster_watch:
             inf = g.infs.get(namespace)
             return [inf] if inf is not None else []
         return g.all()
@@ -418,7 +481,9 @@ class InformerCache(Reader, EventSource):
         if g is None:
             return False
         if namespace and info.namespaced and self.namespaces is not None:
-            inf = g.infs.get(namespace)
+            if self.cluster_watch and namespace not in self.namespaces:
+                return False
+            inf = g.infs.get(None if self.cluster_watch else namespace)
             infs = [inf] if inf is not None else []
         else:
             infs = g.all()

@@ -88,11 +88,11 @@ class WorkerAssignments:
         self._task: Optional[asyncio.Task] = None
         self._synced: Optional[asyncio.Event] = None
 
-    def cache_options(self, extra_namespaces: Iterable[str] = ()) -> dict:
+    def cache_options(self, extra_namespaces: Iterable[str] = (), cluster_watch: bool = False) -> dict:
         from ..models import meta as m
 
         return {"namespace_filter": lambda ns: m.name(ns) in self.namespaces,
-                "namespaces": [n for n in extra_namespaces if n]}
+                "namespaces": [n for n in extra_namespaces if n], "cluster_watch": cluster_watch}
 
     def request_filter(self, req) -> bool:
         return not req.namespace or req.namespace in self.namespaces

@@ -366,10 +366,13 @@ def test_unsharded_topology_two_drivers(run):
     run(go())
 
 
-def test_informer_namespace_selector_follows_labels(run, server_kind):
+@pytest.mark.parametrize("cluster_watch", [False, True])
+def test_informer_namespace_selector_follows_labels(run, server_kind, cluster_watch):
     """``namespace_selector``: a namespace joins the cache when it gets the shard label
     (its objects arrive as ADDED), leaves it when relabelled (DELETED), and reads of a
-    namespace outside the cache go live through CachedClient."""
+    namespace outside the cache go live through CachedClient.  ``cluster_watch``: the same
+    through ONE cluster-wide watch per kind that drops other namespaces' objects (a joining
+    namespace is listed once), instead of a watch per namespace."""
     async def go():
         srv, c = await _server(server_kind)
         try:
@@ -379,11 +382,14 @@ def test_informer_namespace_selector_follows_labels(run, server_kind):
                 await c.create({"apiVersion": "v1", "kind": "Namespace", "metadata": md})
                 await c.create(_cm("x", ns))
             await c.create(_cm("x", "ctl"))
-            cache = InformerCache(c, namespace_selector="notebooks.amd.com/shard=1", namespaces=["ctl"])
+            cache = InformerCache(c, namespace_selector="notebooks.amd.com/shard=1", namespaces=["ctl"],
+                                  cluster_watch=cluster_watch)
             seen = []
             cache.subscribe(kinds.CONFIG_MAP, lambda et, o, old: seen.append((et, m.namespace(o))))
             await cache.wait_synced([kinds.CONFIG_MAP])
             assert sorted(m.namespace(o) for o in cache.list(kinds.CONFIG_MAP)) == ["a", "ctl"]
+            assert len(cache._group(kinds.CONFIG_MAP).all()) == (1 if cluster_watch else 2)
+            assert cache.watching(kinds.CONFIG_MAP, "a") and not cache.watching(kinds.CONFIG_MAP, "c")
             assert cache.covers(kinds.CONFIG_MAP, "a") and not cache.covers(kinds.CONFIG_MAP, "c")
             assert cache.covers(kinds.NAMESPACE, "c")  # cluster-scoped kinds are never restricted
 

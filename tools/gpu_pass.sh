@@ -108,6 +108,20 @@ for s in $steps; do
           show "$out/bench_resident_${v}_r$r.log" "resident $v r$r"
         done
       done ;;
+    nsscale)  # 4 ranks x M namespaces per rank (sharded, balanced): per-namespace watches vs one cluster-wide
+      # watch per kind, interleaved; M=1 is the reference point for the apiserver's CPU per write
+      for r in $(seq 1 "${ROUNDS:-1}"); do
+        for v in ${NSVARIANTS:-m1 m64 m64cw}; do
+          case $v in m1) f="" ;; m64) f="--namespaces-per-rank 64 --assign-policy balanced" ;;
+                     m64cw) f="--namespaces-per-rank 64 --assign-policy balanced --cluster-wide-watches" ;;
+                     m16) f="--namespaces-per-rank 16 --assign-policy balanced" ;;
+                     m16cw) f="--namespaces-per-rank 16 --assign-policy balanced --cluster-wide-watches" ;; esac
+          timeout -k 10 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 4 --master-addr 127.0.0.1 \
+            --master-port 29971 bench.py --gpus 4 --steps 100 --warmup 5 --no-configs --probe-sample 0 --burst 0 \
+            --resident 0 $f > "$out/bench_ns_${v}_r$r.log" 2>&1 || fail nsscale $? "$out/bench_ns_${v}_r$r.log"
+          python tools/summarize_bench.py "$out/bench_ns_${v}_r$r.log"
+        done
+      done ;;
     failover)  # takeover (SIGKILL, standby with warm caches) and graceful cold start with R resident notebooks
       timeout -k 10 600 python tools/bench_failover.py --resident "${RESIDENT:-1000}" > "$out/failover.log" 2>&1 \
         || fail failover $? "$out/failover.log"

@@ -28,6 +28,12 @@ def summary(path: str) -> str:
     out = [f"{path.rsplit('/', 1)[-1]}: N={d.get('n_gpus')} nb/s={d.get('notebooks_ready_per_s')} "
            f"rec/s={d.get('value')} p50={d.get('p50_ready_ms')} p95={d.get('p95_ready_ms')} "
            f"rec/nb={d.get('reconciles_per_notebook')} cpu/step={json.dumps(cpu)}"]
+    prof = d.get("apiserver_profile_per_step") or {}
+    w = (d.get("writes_per_notebook") or {}).get("total")
+    if prof.get("process_cpu_ms") is not None and w:
+        out.append(f"  apiserver cpu/write={prof['process_cpu_ms'] / (w * (d.get('n_gpus') or 1)):.4f} ms "
+                   f"(cpu/step {prof['process_cpu_ms']} ms, {w} writes/notebook)"
+                   + (f" namespaces/rank={(d.get('config') or {}).get('namespaces_per_rank')}"))
     r = d.get("resident")
     if r:
         a = r.get("at_rest") or {}

@@ -186,11 +186,15 @@ def measure(args) -> Optional[dict]:
                                             f"odh webhook process (A/B variant of config/overlays/mi355x-sharded)")
             out["config"]["architecture"] = "cmd/control_plane --shard r --controllers kf | odh,webhook (A/B variant)"
         elif arch == "sharded":
+            sep = culling_enabled(args) and not getattr(args, "culler_in_kf", False)
             out["config"]["parallelism"] = (f"namespace-sharded control plane x{world}: per MI355X rank the shard pod "
                                             f"of config/overlays/mi355x-sharded, `cmd/control_plane.py --shard r` as a "
-                                            f"kf process, an odh reconciler process and an odh webhook process")
-            out["config"]["architecture"] = ("cmd/control_plane --shard r --controllers kf | odh | webhook "
-                                             "(overlay mi355x-sharded)")
+                                            f"kf process{', a culler process' if sep else ''}, an odh reconciler "
+                                            f"process and an odh webhook process")
+            out["config"]["architecture"] = ("cmd/control_plane --shard r --controllers "
+                                             + ("notebook | culler | odh | webhook (overlay mi355x-sharded)" if sep else
+                                                "kf | odh | webhook" + (" (culler in the kf process: A/B variant)"
+                                                                        if culling_enabled(args) else "")))
         else:
             w = max(1, getattr(args, "workers", 1))
             r = max(1, getattr(args, "webhook_replicas", 1))

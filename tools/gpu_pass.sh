@@ -314,10 +314,11 @@ for s in $steps; do
     cpprof)
       mkdir -p "$out/cprof"
       ODH_CONTROL_PLANE_PROFILE=$PWD/$out/cprof/cp ODH_PLATFORM_PROFILE=$PWD/$out/cprof/plat \
-        timeout -k 10 200 python bench.py --gpus 1 --no-inprocess-baseline --probe-sample 0 > "$out/bench_cpprof.log" 2>&1 \
-        || fail cpprof $? "$out/bench_cpprof.log"
-      show "$out/bench_cpprof.log" "n1 cprofiled"
+        timeout -k 10 200 python bench.py --gpus 1 --no-inprocess-baseline --probe-sample 0 --burst 0 --resident 0 \
+        --no-configs > "$out/bench_cpprof.log" 2>&1 || fail cpprof $? "$out/bench_cpprof.log"
+      show "$out/bench_cpprof.log" "n1 cprofiled (closed loop only)"
       for f in "$out"/cprof/*; do
+        case $f in *control_plane*) cp "$f" "$f.pstats" ;; esac  # raw stats of the control plane, for offline reading
         python - "$f" > "$f.txt" <<'PY' || fail cpprof $? "$f.txt"
 import pstats, sys
 st = pstats.Stats(sys.argv[1])

@@ -82,6 +82,9 @@ class NamespaceShardAssigner:
         self.grace_s = float(grace_s)
         self.assigned = 0
         self.conflicts = 0  # balanced: another shard's assigner claimed it first
+        self._plan: Optional[tuple] = None  # (Namespace store version, plan)
+        self.plans = 0
+        self.plan_hits = 0
 
     def _eligible(self, ns: dict) -> bool:
         name = m.name(ns)
@@ -99,7 +102,23 @@ class NamespaceShardAssigner:
         """balanced: name → shard of every unlabelled namespace, decided greedily in creation
         order (then name) on top of the labelled namespaces' per-shard counts.  Every assigner
         sees the same namespaces, so they agree on the plan even for namespaces created all at
-        once (counts from labels alone would still read 0 everywhere and send each to its hash)."""
+        once (counts from labels alone would still read 0 everywhere and send each to its hash).
+
+        The plan is a function of the Namespace cache alone, so it is kept until the cache's
+        Namespace store changes (``store_version``): K namespaces created together and
+        reconciled after they are all cached cost one scan of the cluster's namespaces, not K."""
+        ver_of = getattr(self.reader, "store_version", None)
+        ver = ver_of(kinds.NAMESPACE) if ver_of is not None else None
+        if ver is not None and self._plan is not None and self._plan[0] == ver:
+            self.plan_hits += 1
+            return self._plan[1]
+        out = self._compute_plan()
+        if ver is not None:
+            self._plan = (ver, out)
+        return out
+
+    def _compute_plan(self) -> dict:
+        self.plans += 1
         n = max(1, self.shard_count)
         loads = [0] * n
         pending = []

@@ -82,6 +82,7 @@ class _Informer:
         self.task: Optional[asyncio.Task] = None
         self.relists = 0
         self.events = 0
+        self.mutations = 0  # store changes: a derived view is current while this stands still
         self.missing_kind = False
         self._rv_waiters: List[Tuple[int, asyncio.Future]] = []
 
@@ -109,6 +110,7 @@ class _Informer:
         if old is not None:
             self._unindex(k, old)
         self.items[k] = obj
+        self.mutations += 1
         self.by_ns.setdefault(k[0], set()).add(k)
         md = obj.get("metadata") or {}
         for r in md.get("ownerReferences") or []:
@@ -148,6 +150,7 @@ class _Informer:
         old = self.items.pop(k, None)
         if old is not None:
             self._unindex(k, old)
+            self.mutations += 1
         return old
 
     def _notify(self, etype: str, obj: dict, old: Optional[dict]) -> None:
@@ -583,6 +586,14 @@ class InformerCache(Reader, EventSource):
             return None  # namespace outside this cache
         inf = infs[0]
         return inf.items.get((namespace or "" if inf.info.namespaced else "", name))
+
+    def store_version(self, kind) -> Optional[Tuple[Tuple[int, int], ...]]:
+        """A token that changes whenever the cached objects of ``kind`` do (None: not cached):
+        views derived from a whole-kind list are reused while it stands still."""
+        infs = self._for_ns(kind, None)
+        if not infs:
+            return None
+        return tuple((id(inf), inf.mutations) for inf in infs)
 
     def list(self, kind, namespace=None, labels=None, fields=None, owner_uid=None) -> List[dict]:
         infs = self._for_ns(kind, namespace)

@@ -631,6 +631,39 @@ def test_balanced_assignment_evens_out_the_hash(run):
     run(go())
 
 
+def test_balanced_plan_is_reused_until_the_namespace_store_changes(run):
+    """plan() scans every Namespace; it is kept while the cache's Namespace store is unchanged
+    and recomputed (with the new namespace in it) after one is added or relabelled."""
+    from odh_kubeflow_amd.controllers.sharding import NamespaceShardAssigner
+
+    async def go():
+        srv, c = await _server("python")
+        cache = InformerCache(c)
+        try:
+            for ns in ("a-1", "a-2", "a-3"):
+                await c.create({"apiVersion": "v1", "kind": "Namespace", "metadata": {"name": ns}})
+            await cache.wait_synced([kinds.NAMESPACE])
+            a = NamespaceShardAssigner(None, cache, 2, only_shard="0", policy="balanced")
+            p1 = a.plan()
+            assert sorted(p1) == ["a-1", "a-2", "a-3"] and a.plans == 1
+            assert a.plan() is p1 and a.plan_hits == 1
+            await c.create({"apiVersion": "v1", "kind": "Namespace", "metadata": {"name": "a-4"}})
+            assert await _wait(lambda: "a-4" in a.plan())
+            plans = a.plans
+            assert plans >= 2
+            await c.patch(kinds.NAMESPACE, {"metadata": {"labels": {"notebooks.amd.com/shard": "1"}}}, name="a-1")
+            assert await _wait(lambda: "a-1" not in a.plan())
+            assert a.plans > plans
+            hits = a.plan_hits
+            a.plan()
+            assert a.plan_hits == hits + 1
+        finally:
+            await cache.stop()
+            await c.close()
+            await srv.stop()
+    run(go())
+
+
 def test_balanced_assignment_falls_back_to_the_hash_shard(run):
     """The balanced target is down (shard 1 of 3): after the grace period the hash's shard claims
     the namespace, so at most the namespaces that hash to the dead shard wait (as with policy

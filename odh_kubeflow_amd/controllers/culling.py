@@ -66,7 +66,6 @@ from typing import Any, Callable, Mapping, Optional, Sequence
 
 from ..models import kinds
 from ..models import meta as m
-from ..models.errors import ApiError, is_not_found
 from ..models.notebook import (LAST_ACTIVITY_ANNOTATION, LAST_ACTIVITY_CHECK_TIMESTAMP_ANNOTATION, STOP_ANNOTATION,
                                gpu_request)
 from ..runtime.controller import Request, Result
@@ -80,6 +79,16 @@ DEFAULT_IDLENESS_CHECK_PERIOD = "1"
 DEFAULT_CLUSTER_DOMAIN = "cluster.local"
 KERNEL_IDLE, KERNEL_BUSY, KERNEL_STARTING = "idle", "busy", "starting"
 _ABSENT = object()
+
+
+def _phase_of(namespace: str, name: str) -> float:
+    """A notebook's fixed fraction of the check period.  blake2b, not crc32: CRC is linear, and
+    the sequential names notebooks usually get (``nb-0`` … ``nb-999``) cluster under it — the
+    fullest 10 s slot of a 60 s period held up to 1.7x the emptiest at R=1000, against 1.3x here."""
+    import hashlib
+
+    h = hashlib.blake2b(f"{namespace}/{name}".encode(), digest_size=8).digest()
+    return int.from_bytes(h, "big") / 2.0 ** 64
 
 
 def env_default(env: Mapping[str, str], key: str, default: str) -> str:
@@ -690,18 +699,16 @@ class CullingReconciler:
     def _next_check(self, req: Request, last_check: float) -> float:
         """Seconds until this notebook's next check: the first slot of its phase at or after
         ``last_check`` (the stamp, RFC3339 whole seconds) + the period.  Each notebook's checks
-        land on a fixed phase of the period (crc32 of its key), so R resident notebooks are
+        land on a fixed phase of the period (a hash of its key), so R resident notebooks are
         checked evenly spread, R / period per second.  The reference requeues each after exactly
         the period (:200-202), so notebooks reconciled together — all of them when the manager
         starts — stay checked together: R writes in one burst every period, which is when every
         new notebook's create→Ready waits behind them.  The first aligned check may come up to one
         period later than the reference's; every later one comes exactly a period apart."""
-        import zlib
-
         p = self.cfg.check_period_s
         if p <= 0:
             return p
-        phase = zlib.crc32(f"{req.namespace}/{req.name}".encode()) / 2 ** 32 * p
+        phase = _phase_of(req.namespace, req.name) * p
         target = last_check + p + 0.001  # strictly past the period at the wake-up
         k = -(-(target - phase) // p)  # ceil
         return max(0.001, phase + k * p - now())

@@ -1,11 +1,14 @@
-"""Lean HTTP/1.1 client for the apiserver REST path (asyncio streams, keep-alive pool).
+"""Lean HTTP/1.1 client for the apiserver REST path (asyncio protocol, keep-alive pool).
 
 A control-plane process spends most of its CPU time talking to the apiserver; a generic
 client (aiohttp) costs ~4× the raw socket round trip per request on this path (measured
 0.14 ms vs 0.03 ms for a GET on loopback).  This client does only what the Kubernetes
 REST API needs: persistent connections, ``Content-Length`` or ``chunked`` bodies,
-optional TLS, and a streaming mode for watches.  Stale pooled connections (closed by the
-server while idle) are retried once for requests other than POST.
+optional TLS, and a streaming mode for watches.  Responses are parsed in the protocol's
+``data_received`` (one future per response; a watch wakes its consumer once per arrival with
+all the events it holds), not through StreamReader waits.  A pooled connection the server
+closed while idle is skipped; a request that met such a close is retried once unless it is
+a POST.
 """
 
 from __future__ import annotations
@@ -20,22 +23,7 @@ class HttpError(Exception):
     pass
 
 
-class _Conn:
-    __slots__ = ("reader", "writer")
-
-    def __init__(self, reader, writer):
-        self.reader = reader
-        self.writer = writer
-
-    def close(self) -> None:
-        try:
-            self.writer.close()
-        except Exception:
-            pass
-
-
-async def _read_head(reader) -> Tuple[int, Dict[str, str]]:
-    raw = await reader.readuntil(b"\r\n\r\n")
+def _parse_head(raw: bytes) -> Tuple[int, Dict[str, str]]:
     lines = raw.decode("latin-1").split("\r\n")
     parts = lines[0].split(" ", 2)
     if len(parts) < 2 or not parts[0].startswith("HTTP/"):
@@ -48,16 +36,194 @@ async def _read_head(reader) -> Tuple[int, Dict[str, str]]:
     return int(parts[1]), headers
 
 
-async def _read_chunked(reader) -> bytes:
-    out = bytearray()
+def _dechunk(raw: bytearray, body: bytearray) -> bool:
+    """Move the complete chunks at the front of ``raw`` into ``body``; True once the last chunk
+    and its (empty) trailer are in — the connection may carry the next response after it."""
+    pos = 0
+    done = False
     while True:
-        line = await reader.readuntil(b"\r\n")
-        size = int(line.split(b";", 1)[0].strip(), 16)
+        crlf = raw.find(b"\r\n", pos)
+        if crlf < 0:
+            break
+        size = int(bytes(raw[pos:crlf]).split(b";", 1)[0].strip(), 16)
         if size == 0:
-            await reader.readuntil(b"\r\n")
-            return bytes(out)
-        out += await reader.readexactly(size)
-        await reader.readexactly(2)
+            end = raw.find(b"\r\n\r\n", crlf)
+            if end >= 0:
+                done = True
+                pos = end + 4
+            break
+        end = crlf + 2 + size
+        if len(raw) < end + 2:
+            break
+        body += raw[crlf + 2:end]
+        pos = end + 2
+    del raw[:pos]
+    return done
+
+
+class _Conn(asyncio.Protocol):
+    """One keep-alive connection whose responses are parsed in ``data_received``.
+
+    A request is one future, resolved when its response is complete however many reads that
+    took — not a StreamReader wait per head / chunk / body part, each its own event-loop
+    wake-up and task step.  A streaming (watch) response is de-chunked and split into lines
+    as bytes arrive, and its consumer is woken once per arrival with every complete line."""
+
+    def __init__(self):
+        self.transport = None
+        self.buf = bytearray()
+        self.closed = False
+        self._waiter: Optional[asyncio.Future] = None
+        self._head: Optional[Tuple[int, Dict[str, str]]] = None
+        self._body = bytearray()
+        self._want = -1  # Content-Length body size; -2: chunked; -3: until EOF
+        self._streaming = False
+        self._lines: List[bytes] = []
+        self._got = 0
+        self._eof = False
+
+    # ---------------------------------------------------------------- asyncio.Protocol
+
+    def connection_made(self, transport) -> None:
+        self.transport = transport
+
+    def data_received(self, data: bytes) -> None:
+        self.buf += data
+        if self._waiter is not None or self._streaming:
+            self._advance()
+
+    def eof_received(self):
+        return False  # close the transport: connection_lost follows
+
+    def connection_lost(self, exc) -> None:
+        self.closed = True
+        self._eof = True
+        w, self._waiter = self._waiter, None
+        if w is None or w.done():
+            return
+        if self._streaming:
+            w.set_result(None)  # stream(): no head (None) / next_lines(): the body ended
+        elif self._want == -3 and self._head is not None:
+            self._body += self.buf
+            self.buf.clear()
+            w.set_result((self._head[0], bytes(self._body), True))
+        else:
+            w.set_exception(ConnectionResetError(f"connection lost mid-response: {exc!r}"))
+
+    # ---------------------------------------------------------------- parsing
+
+    def _advance(self) -> None:
+        w = self._waiter
+        try:
+            if self._head is None:
+                i = self.buf.find(b"\r\n\r\n")
+                if i < 0:
+                    return
+                self._head = _parse_head(bytes(self.buf[:i]))
+                del self.buf[:i + 4]
+                h = self._head[1]
+                if h.get("transfer-encoding", "").lower() == "chunked":
+                    self._want = -2
+                elif "content-length" in h:
+                    self._want = int(h["content-length"])
+                else:
+                    self._want = -3
+                if self._streaming:  # stream() waits for the head alone
+                    self._waiter = None
+                    if w is not None and not w.done():
+                        w.set_result(self._head)
+            if self._streaming:
+                self._stream_advance()
+                return
+            if self._want >= 0:
+                if len(self.buf) < self._want:
+                    return
+                data = bytes(self.buf[:self._want])
+                del self.buf[:self._want]
+            elif self._want == -2:
+                if not _dechunk(self.buf, self._body):
+                    return
+                data = bytes(self._body)
+                self._body.clear()
+            else:
+                return  # delimited by EOF: connection_lost completes it
+            status, headers = self._head
+            self._head = None
+            self._waiter = None
+            if w is not None and not w.done():
+                w.set_result((status, data, headers.get("connection", "").lower() == "close"))
+        except Exception as e:  # noqa: BLE001 — a malformed response fails its request, not the loop
+            self._waiter = None
+            self.close()
+            if w is not None and not w.done():
+                w.set_exception(HttpError(f"bad response: {e!r}"))
+
+    def _stream_advance(self) -> None:
+        if self._want == -2:
+            done = _dechunk(self.buf, self._body)
+        else:
+            self._got += len(self.buf)
+            self._body += self.buf
+            self.buf.clear()
+            done = 0 <= self._want <= self._got  # a Content-Length body (an error Status)
+        body = self._body
+        start = 0
+        while True:
+            nl = body.find(b"\n", start)
+            if nl < 0:
+                break
+            self._lines.append(bytes(body[start:nl]))
+            start = nl + 1
+        if start:
+            del body[:start]
+        if done:
+            self._eof = True
+            self.close()
+        w = self._waiter
+        if (self._lines or self._eof) and w is not None and not w.done():
+            self._waiter = None
+            w.set_result(None)
+
+    # ---------------------------------------------------------------- client side
+
+    async def roundtrip(self, payload: bytes) -> Tuple[int, bytes, bool]:
+        if self.closed:
+            raise ConnectionResetError("connection closed")
+        self._waiter = w = asyncio.get_running_loop().create_future()
+        self.transport.write(payload)
+        if self.buf:  # bytes that arrived before the request (a server error, an early close)
+            self._advance()
+        return await w
+
+    async def open_stream(self, payload: bytes) -> Tuple[int, Dict[str, str]]:
+        if self.closed:
+            raise ConnectionResetError("connection closed")
+        self._streaming = True
+        self._waiter = w = asyncio.get_running_loop().create_future()
+        self.transport.write(payload)
+        got = await w
+        if got is None:
+            raise ConnectionResetError("connection lost before the response head")
+        return got
+
+    async def next_lines(self) -> List[bytes]:
+        """The complete lines received since the last call; [] once the body ended."""
+        while not self._lines:
+            if self._eof or self.closed:
+                return []
+            self._waiter = w = asyncio.get_running_loop().create_future()
+            try:
+                await w
+            finally:
+                if self._waiter is w:
+                    self._waiter = None
+        out, self._lines = self._lines, []
+        return out
+
+    def close(self) -> None:
+        self.closed = True
+        if self.transport is not None:
+            self.transport.close()
 
 
 class Http1Pool:
@@ -75,9 +241,9 @@ class Http1Pool:
         self.opened = 0
 
     async def _connect(self) -> _Conn:
-        reader, writer = await asyncio.open_connection(self.host, self.port, ssl=self.ssl,
-                                                       limit=1 << 24)
-        sock = writer.get_extra_info("socket")
+        loop = asyncio.get_running_loop()
+        transport, conn = await loop.create_connection(_Conn, self.host, self.port, ssl=self.ssl)
+        sock = transport.get_extra_info("socket")
         if sock is not None:
             import socket
 
@@ -86,7 +252,7 @@ class Http1Pool:
             except OSError:
                 pass
         self.opened += 1
-        return _Conn(reader, writer)
+        return conn
 
     def _head(self, method: str, target: str, body: Optional[bytes], content_type: Optional[str]) -> bytes:
         h = f"{method} {target} HTTP/1.1\r\n{self._static}"
@@ -94,29 +260,35 @@ class Http1Pool:
             h += f"Content-Type: {content_type or 'application/json'}\r\nContent-Length: {len(body)}\r\n"
         return (h + "\r\n").encode("latin-1") + (body or b"")
 
+    def _take_idle(self) -> Optional[_Conn]:
+        while self._idle:
+            c = self._idle.pop()
+            if not c.closed:
+                return c
+        return None
+
     async def request(self, method: str, target: str, body: Optional[bytes] = None,
                       content_type: Optional[str] = None) -> Tuple[int, bytes]:
         payload = self._head(method, target, body, content_type)
         for attempt in (0, 1):
-            reused = bool(self._idle)
-            conn = self._idle.pop() if reused else await self._connect()
+            conn = self._take_idle()
+            reused = conn is not None
             try:
-                conn.writer.write(payload)
-                status, headers = await _read_head(conn.reader)
-                if headers.get("transfer-encoding", "").lower() == "chunked":
-                    data = await _read_chunked(conn.reader)
-                else:
-                    n = int(headers.get("content-length", "0"))
-                    data = await conn.reader.readexactly(n) if n else b""
-            except (asyncio.IncompleteReadError, ConnectionError, OSError) as e:
-                conn.close()
+                if conn is None:
+                    conn = await self._connect()
+                status, data, close = await conn.roundtrip(payload)
+            except (ConnectionError, OSError) as e:
+                if conn is not None:
+                    conn.close()
+                # a pooled connection the server closed while idle: once more on a fresh one
                 if reused and attempt == 0 and method != "POST":
                     continue
                 raise HttpError(f"{method} {target}: {e!r}") from e
             except BaseException:
-                conn.close()
+                if conn is not None:
+                    conn.close()
                 raise
-            if headers.get("connection", "").lower() == "close" or len(self._idle) >= self.size:
+            if close or len(self._idle) >= self.size:
                 conn.close()
             else:
                 self._idle.append(conn)
@@ -125,9 +297,12 @@ class Http1Pool:
 
     async def stream(self, method: str, target: str) -> Tuple[int, Dict[str, str], "_Stream"]:
         conn = await self._connect()
-        conn.writer.write(self._head(method, target, None, None))
-        status, headers = await _read_head(conn.reader)
-        return status, headers, _Stream(conn, headers)
+        try:
+            status, headers = await conn.open_stream(self._head(method, target, None, None))
+        except BaseException:
+            conn.close()
+            raise
+        return status, headers, _Stream(conn)
 
     async def close(self) -> None:
         for c in self._idle:
@@ -136,66 +311,39 @@ class Http1Pool:
 
 
 class _Stream:
-    """Body of a streaming (watch) response; iterate lines, then close."""
+    """Body of a streaming (watch) response: iterate batches of lines, then close."""
 
-    def __init__(self, conn: _Conn, headers: Dict[str, str]):
+    def __init__(self, conn: _Conn):
         self.conn = conn
-        self.chunked = headers.get("transfer-encoding", "").lower() == "chunked"
 
     async def read_all(self) -> bytes:
         try:
-            if self.chunked:
-                return await _read_chunked(self.conn.reader)
-            return await self.conn.reader.read()
+            out = []
+            while True:
+                got = await self.conn.next_lines()
+                if not got:
+                    break
+                out += [x + b"\n" for x in got]
+            return b"".join(out) + bytes(self.conn._body)
+        finally:
+            self.close()
+
+    async def batches(self) -> AsyncIterator[List[bytes]]:
+        """The complete lines (without their newline) of each arrival, until the body or the
+        connection ends."""
+        try:
+            while True:
+                got = await self.conn.next_lines()
+                if not got:
+                    return
+                yield got
         finally:
             self.close()
 
     async def lines(self) -> AsyncIterator[bytes]:
-        """The body's lines (without their newline).  Chunked bodies are read as whatever has
-        arrived — one await per arrival, however many chunks and events it holds — and
-        de-chunked here, rather than three stream reads per chunk."""
-        r = self.conn.reader
-        try:
-            if not self.chunked:
-                async for line in r:
-                    yield line
-                return
-            raw = bytearray()  # chunked framing not yet parsed
-            body = bytearray()  # de-chunked bytes not yet split into lines
-            while True:
-                data = await r.read(1 << 16)
-                if not data:
-                    return
-                raw += data
-                pos, done = 0, False
-                while True:
-                    crlf = raw.find(b"\r\n", pos)
-                    if crlf < 0:
-                        break
-                    size = int(bytes(raw[pos:crlf]).split(b";", 1)[0].strip(), 16)
-                    if size == 0:
-                        done = True
-                        break
-                    end = crlf + 2 + size
-                    if len(raw) < end + 2:
-                        break
-                    body += raw[crlf + 2:end]
-                    pos = end + 2
-                del raw[:pos]
-                start = 0
-                while True:
-                    nl = body.find(b"\n", start)
-                    if nl < 0:
-                        break
-                    yield bytes(body[start:nl])
-                    start = nl + 1
-                del body[:start]
-                if done:
-                    return
-        except (asyncio.IncompleteReadError, ConnectionError, OSError):
-            return
-        finally:
-            self.close()
+        async for batch in self.batches():
+            for line in batch:
+                yield line
 
     def close(self) -> None:
         self.conn.close()

@@ -56,6 +56,13 @@ def strip_data(obj: dict) -> dict:
     return strip_managed_fields(obj)
 
 
+def _one_event_batches(watch):
+    async def batches(*args, **kw):
+        async for ev in watch(*args, **kw):
+            yield [ev]
+    return batches
+
+
 class _Informer:
     def __init__(self, cache: "InformerCache", info: ResourceInfo, version: str,
                  namespace: Optional[str] = None, label_selector: Optional[str] = None,
@@ -230,6 +237,27 @@ class _Informer:
         if self._rv_waiters:
             self._rv_reached()
 
+    def _apply(self, et: str, obj: dict) -> None:
+        """One watch event into the store, then to the subscribers."""
+        self.rv = m.resource_version(obj) or self.rv
+        if et == "BOOKMARK":
+            return
+        if self.ns_filter is not None and not self.ns_filter(m.namespace(obj)):
+            return  # a cluster-wide watch: another shard's (or worker's) namespace
+        obj = self._transform(obj)
+        if et != "DELETED" and self._label_reqs is not None and not match_labels(
+                self._label_reqs, (obj.get("metadata") or {}).get("labels")):
+            # the object left the selector: to this cache it is gone
+            if (m.namespace(obj), m.name(obj)) not in self.items:
+                return
+            et = "DELETED"
+        if et == "DELETED":
+            old = self._delete(obj)
+            self._notify("DELETED", obj, old)
+        else:
+            old = self._put(obj)
+            self._notify("ADDED" if old is None else "MODIFIED", obj, old)
+
     async def run(self) -> None:
         ref = f"{self.info.api_version(self.version)}/{self.info.kind}"
         backoff = 0.05
@@ -241,29 +269,15 @@ class _Informer:
                     await self._relist()
                     need_list = False
                 started = time.monotonic()
-                async for et, obj in self.cache.rest.watch(ref, self.namespace, self.rv, labels=self.label_selector,
-                                                           fields=self.field_selector,
-                                                           timeout_s=self.cache.watch_timeout_s):
+                rest = self.cache.rest
+                batches = getattr(rest, "watch_batches", None)
+                if batches is None:  # a client without batched watches (test doubles)
+                    batches = _one_event_batches(rest.watch)
+                async for batch in batches(ref, self.namespace, self.rv, labels=self.label_selector,
+                                           fields=self.field_selector, timeout_s=self.cache.watch_timeout_s):
                     backoff = 0.05
-                    if et == "BOOKMARK":
-                        self.rv = m.resource_version(obj) or self.rv
-                        continue
-                    self.rv = m.resource_version(obj) or self.rv
-                    if self.ns_filter is not None and not self.ns_filter(m.namespace(obj)):
-                        continue  # a cluster-wide watch: another shard's (or worker's) namespace
-                    obj = self._transform(obj)
-                    if et != "DELETED" and self._label_reqs is not None and not match_labels(
-                            self._label_reqs, (obj.get("metadata") or {}).get("labels")):
-                        # the object left the selector: to this cache it is gone
-                        if (m.namespace(obj), m.name(obj)) not in self.items:
-                            continue
-                        et = "DELETED"
-                    if et == "DELETED":
-                        old = self._delete(obj)
-                        self._notify("DELETED", obj, old)
-                    else:
-                        old = self._put(obj)
-                        self._notify("ADDED" if old is None else "MODIFIED", obj, old)
+                    for et, obj in batch:
+                        self._apply(et, obj)
                     if self._rv_waiters:
                         self._rv_reached()
             except asyncio.CancelledError:

@@ -347,6 +347,17 @@ class RestClient(Client):
     async def watch(self, kind, namespace=None, resource_version: Optional[str] = None, labels=None, fields=None,
                     timeout_s: int = 300, bookmarks: bool = True) -> AsyncIterator[Tuple[str, dict]]:
         """Yield ``(type, object)``; raises :class:`Gone` when the RV is too old."""
+        async for batch in self.watch_batches(kind, namespace, resource_version, labels, fields, timeout_s,
+                                              bookmarks):
+            for ev in batch:
+                yield ev
+
+    async def watch_batches(self, kind, namespace=None, resource_version: Optional[str] = None, labels=None,
+                            fields=None, timeout_s: int = 300,
+                            bookmarks: bool = True) -> AsyncIterator[List[Tuple[str, dict]]]:
+        """Yield the ``(type, object)`` events of each arrival as one list (an informer applies
+        them in one go); raises :class:`Gone` when the RV is too old — after yielding the
+        events that preceded the ERROR in its batch."""
         from urllib.parse import urlencode
 
         info, v = _info_and_version(kind)
@@ -370,17 +381,25 @@ class RestClient(Client):
                 raise ApiError.from_status(json.loads(raw), status)
             except ValueError:
                 raise InternalError(raw[:200].decode(errors="replace"))
+        loads = json.loads
         try:
-            async for line in stream.lines():
-                if not line.strip():
-                    continue
-                ev = json.loads(line)
-                et, obj = ev.get("type"), ev.get("object") or {}
-                if et == "ERROR":
-                    err = ApiError.from_status(obj)
+            async for lines in stream.batches():
+                out = []
+                err = None
+                for line in lines:
+                    if not line or line.isspace():
+                        continue
+                    ev = loads(line)
+                    et, obj = ev.get("type"), ev.get("object") or {}
+                    if et == "ERROR":
+                        err = ApiError.from_status(obj)
+                        break
+                    out.append((et, obj))
+                if out:
+                    yield out
+                if err is not None:
                     if err.code == 410:
                         raise Gone(err.message)
                     raise err
-                yield et, obj
         finally:
             stream.close()

@@ -166,6 +166,9 @@ def _free_port() -> int:
 
 
 _SAMPLE = re.compile(r"^([A-Za-z_:][A-Za-z0-9_:]*)(\{.*\})?\s+(\S+)(?:\s+\S+)?$")
+# gauges that measure a share of the work each worker holds: the manager's is the sum
+ADDITIVE_GAUGES = frozenset({"controller_runtime_max_concurrent_reconciles", "controller_runtime_active_workers",
+                             "workqueue_depth", "workqueue_unfinished_work_seconds"})
 
 
 def merge_metrics(texts: Sequence[str]) -> str:
@@ -173,8 +176,9 @@ def merge_metrics(texts: Sequence[str]) -> str:
     HELP/TYPE per family; samples with the same name and labels are added for counters,
     histograms and summaries, and the largest is kept for gauges (a gauge is a level — two
     processes exporting ``last_notebook_culling_timestamp_seconds`` for the same notebook must
-    not add up to twice the epoch) and for ``_created`` timestamps the earliest.  The families
-    keep the order of their first appearance."""
+    not add up to twice the epoch) except the per-worker shares in :data:`ADDITIVE_GAUGES`
+    (two workers of 8 concurrent reconciles each are 16), and for ``_created`` timestamps the
+    earliest.  The families keep the order of their first appearance."""
     meta: Dict[str, List[str]] = {}
     order: List[str] = []
     samples: Dict[str, Dict[Tuple[str, str], float]] = {}
@@ -220,7 +224,7 @@ def merge_metrics(texts: Sequence[str]) -> str:
                 samples[f][key] = v
             elif name.endswith("_created"):
                 samples[f][key] = min(prev, v)  # a creation timestamp: the earliest, not a sum
-            elif types.get(f) == "gauge":
+            elif types.get(f) == "gauge" and f not in ADDITIVE_GAUGES:
                 samples[f][key] = max(prev, v)
             else:
                 samples[f][key] = prev + v

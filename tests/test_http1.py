@@ -9,11 +9,14 @@ import random
 
 import pytest
 
-from odh_kubeflow_amd.runtime.http1 import _Conn, _Stream
+from odh_kubeflow_amd.runtime.http1 import _Conn, _Stream, _dechunk
 
 
-class _W:
+class _T:
     def close(self):
+        pass
+
+    def write(self, _data):
         pass
 
 
@@ -25,14 +28,20 @@ def _chunked(chunks):
 
 
 async def _read(pieces, chunked=True):
-    r = asyncio.StreamReader()
-    s = _Stream(_Conn(r, _W()), {"transfer-encoding": "chunked"} if chunked else {})
+    conn = _Conn()
+    conn.connection_made(_T())
+    head = b"HTTP/1.1 200 OK\r\n" + (b"Transfer-Encoding: chunked\r\n" if chunked else b"") + b"\r\n"
+    opened = asyncio.ensure_future(conn.open_stream(b"GET / HTTP/1.1\r\n\r\n"))
+    await asyncio.sleep(0)
+    conn.data_received(head)
+    assert (await opened)[0] == 200
+    s = _Stream(conn)
 
     async def feed():
         for p in pieces:
-            r.feed_data(p)
+            conn.data_received(p)
             await asyncio.sleep(0)
-        r.feed_eof()
+        conn.connection_lost(None)
 
     t = asyncio.ensure_future(feed())
     got = [line async for line in s.lines()]
@@ -62,4 +71,54 @@ def test_chunked_lines_survive_any_split(seed):
 def test_chunk_extension_and_early_eof():
     wire = b"5;ext=1\r\nab\ncd\r\n3\r\nef\n\r\n"  # no terminal chunk: the connection just ends
     assert asyncio.run(_read([wire])) == [b"ab", b"cdef"]
-    assert asyncio.run(_read([b"a\nb\n"], chunked=False)) == [b"a\n", b"b\n"]
+    assert asyncio.run(_read([b"a\nb\n"], chunked=False)) == [b"a", b"b"]
+
+
+async def _roundtrips(responses, seed):
+    """Responses back to back on one keep-alive connection, the wire split anywhere."""
+    rnd = random.Random(seed)
+    conn = _Conn()
+    conn.connection_made(_T())
+    out = []
+    for wire in responses:
+        fut = asyncio.ensure_future(conn.roundtrip(b"GET / HTTP/1.1\r\n\r\n"))
+        await asyncio.sleep(0)
+        j = 0
+        while j < len(wire):
+            n = rnd.randrange(1, 23)
+            conn.data_received(wire[j:j + n])
+            j += n
+        out.append(await fut)
+    return out
+
+
+@pytest.mark.parametrize("seed", range(10))
+def test_keepalive_responses_parse_across_any_split(seed):
+    body = b'{"kind":"ConfigMap","data":{"k":"' + b"v" * 300 + b'"}}'
+    cl = b"HTTP/1.1 200 OK\r\nContent-Length: %d\r\n\r\n" % len(body) + body
+    ch = b"HTTP/1.1 201 Created\r\nTransfer-Encoding: chunked\r\n\r\n" + _chunked([body[:100], body[100:]])
+    empty = b"HTTP/1.1 404 Not Found\r\nContent-Length: 0\r\nConnection: close\r\n\r\n"
+    got = asyncio.run(_roundtrips([cl, ch, cl, empty], seed))
+    assert got == [(200, body, False), (201, body, False), (200, body, False), (404, b"", True)]
+
+
+def test_dechunk_waits_for_the_final_crlf():
+    raw, body = bytearray(b"3\r\nabc\r\n0\r\n"), bytearray()
+    assert not _dechunk(raw, body) and body == b"abc"
+    raw += b"\r\nHTTP/1.1"
+    assert _dechunk(raw, body) and raw == b"HTTP/1.1"
+
+
+def test_connection_lost_mid_response_fails_the_request():
+    async def go():
+        conn = _Conn()
+        conn.connection_made(_T())
+        fut = asyncio.ensure_future(conn.roundtrip(b"GET / HTTP/1.1\r\n\r\n"))
+        await asyncio.sleep(0)
+        conn.data_received(b"HTTP/1.1 200 OK\r\nContent-Length: 10\r\n\r\nabc")
+        conn.connection_lost(None)
+        with pytest.raises(ConnectionResetError):
+            await fut
+        with pytest.raises(ConnectionResetError):
+            await conn.roundtrip(b"GET / HTTP/1.1\r\n\r\n")  # closed: the pool skips it
+    asyncio.run(go())

@@ -162,6 +162,10 @@ def test_merge_metrics_sums_samples_and_keeps_one_header():
     g2 = "# HELP last_ts T.\n# TYPE last_ts gauge\nlast_ts{name=\"nb\"} 1.6e9\n"
     out = wk.merge_metrics([g1, g2])
     assert 'last_ts{name="nb"} 1700000000.0' in out and 'last_ts{name="a"} 5.0' in out
+    # ... except a worker's share of the capacity: those add up
+    c = ('# HELP controller_runtime_max_concurrent_reconciles M.\n# TYPE controller_runtime_max_concurrent_reconciles '
+         'gauge\ncontroller_runtime_max_concurrent_reconciles{controller="x"} 8.0\n')
+    assert 'controller_runtime_max_concurrent_reconciles{controller="x"} 16.0' in wk.merge_metrics([c, c])
 
 
 def test_worker_command_lines_drop_what_only_the_supervisor_does():

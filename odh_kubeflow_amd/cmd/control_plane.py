@@ -14,10 +14,12 @@ cluster's notebooks with constant per-shard watch traffic.  The ``mi355x-sharded
 overlay runs it as a StatefulSet (``--shard=ordinal``: replica k is shard k, one per
 MI355X of an 8-GPU node) with one MutatingWebhookConfiguration and Service per shard;
 the headline benchmark (``bench.py`` → ``parallel/bench_dist.py``) launches exactly
-these processes, per rank.  A shard's pod runs the command three times, split by
-``--controllers``: ``kf`` (notebook reconciler, event re-emitter, culler, namespace
-assigner), ``odh`` and ``webhook`` — three event loops, so the odh pipeline never queues
-behind the kf reconciles, nor an admission behind either (measured on one box, interleaved:
+these processes, per rank.  A shard's pod runs the command four times, split by
+``--controllers``: ``notebook`` (the notebook reconciler and namespace assigner),
+``culler,events`` (the culler and the Pod/StatefulSet event re-emitter — the kf manager's two
+auxiliary controllers, whose work is per resident notebook and per platform Event, off the
+create→Ready path), ``odh`` and ``webhook`` — four event loops, so the odh pipeline never
+queues behind the kf reconciles, nor an admission behind either (measured on one box, interleaved:
 two processes against one, 252/268/257 vs 240/253/241 notebooks/s at N=1,
 ``profiles/r3_p13``; the webhook in its own process against sharing the odh one, 64
 notebooks at once at 4 ranks: 1706/1651 vs 1446/1396 notebooks/s, AdmissionReview p99
@@ -45,8 +47,8 @@ from typing import List, Optional
 log = logging.getLogger("setup")
 
 ALL_CONTROLLERS = ("kf", "odh", "webhook")
-# finer splits of "kf": the notebook reconciler + event re-emitter, and the culler
-KF_PARTS = ("notebook", "culler")
+# finer splits of "kf": the notebook reconciler, the event re-emitter and the culler
+KF_PARTS = ("notebook", "events", "culler")
 
 
 def parse(argv: Optional[List[str]] = None) -> argparse.Namespace:
@@ -55,8 +57,9 @@ def parse(argv: Optional[List[str]] = None) -> argparse.Namespace:
     p = argparse.ArgumentParser(prog="notebook-control-plane")
     p.add_argument("--controllers", default="kf,odh,webhook",
                    help="comma list of kf (notebook + event re-emitter + culler when ENABLE_CULLING=true), "
-                        "odh (OpenshiftNotebookReconciler), webhook (odh mutating webhook); or kf split in two: "
-                        "notebook (notebook + event re-emitter) and culler (the culler alone)")
+                        "odh (OpenshiftNotebookReconciler), webhook (odh mutating webhook); or kf split in parts: "
+                        "notebook (the notebook reconciler), events (the Pod/StatefulSet event re-emitter), "
+                        "culler (the culler)")
     add_shard_flags(p)
     add_debug_flags(p)
     p.add_argument("--shard-count", type=int, default=0, help="number of shards (for --assign-namespaces)")
@@ -96,7 +99,7 @@ def parse(argv: Optional[List[str]] = None) -> argparse.Namespace:
     if bad:
         p.error(f"unknown --controllers entries: {bad}")
     if "kf" in args.controller_set and any(c in args.controller_set for c in KF_PARTS):
-        p.error("--controllers: kf already runs notebook and culler")
+        p.error("--controllers: kf already runs notebook, events and culler")
     if ("odh" in args.controller_set or "webhook" in args.controller_set) and not args.kube_rbac_proxy_image:
         p.print_usage(sys.stderr)
         raise SystemExit("missing required flag: --kube-rbac-proxy-image must be set")
@@ -137,8 +140,16 @@ def build(args, env=os.environ):
                                 renew_deadline=args.leader_election_renew_deadline,
                                 retry_period=args.leader_election_retry_period)
     name = "notebook-control-plane" + (f"-shard-{shard}" if shard is not None else "") + subset
+    cache_options = shard_cache_options(shard, namespace, args.cluster_wide_watches)
+    # a process running one of the two Notebook-owning reconcilers watches only its own
+    # Services: kf's <nb> (no labels, kf/controllers/notebook_controller.go:525-552) and odh's
+    # <nb>-kube-rbac-proxy (labelled notebook-name) — each would decode the other's otherwise
+    only = {"notebook": "!notebook-name", "odh": "notebook-name"}.get(
+        args.controller_set[0] if len(args.controller_set) == 1 else "")
+    if only:
+        cache_options["selectors"] = {**cache_options.get("selectors", {}), kinds.SERVICE: only}
     mgr = Manager.remote(cfg, name=name, uncached=uncached, transforms=transforms,
-                         cache_options=shard_cache_options(shard, namespace, args.cluster_wide_watches),
+                         cache_options=cache_options,
                          default_max_concurrent=args.max_concurrent_reconciles, leader_elector=elector,
                          metrics_addr=args.metrics_bind_address, probe_addr=args.health_probe_bind_address,
                          debug_endpoints=args.enable_debug_endpoints)
@@ -147,7 +158,11 @@ def build(args, env=os.environ):
     if "kf" in args.controller_set:
         mgr.kf_reconcilers = setup_kf(mgr, env, reference_emulation=emu)
     elif "notebook" in args.controller_set:
-        mgr.kf_reconcilers = setup_kf(mgr, env, culling=False, reference_emulation=emu)
+        mgr.kf_reconcilers = setup_kf(mgr, env, culling=False, event_reemit=False, reference_emulation=emu)
+    if "events" in args.controller_set:
+        from ..controllers.setup import setup_event_reemitter
+
+        mgr.reemitter = setup_event_reemitter(mgr, reference_emulation=emu)
     if "culler" in args.controller_set:
         from ..controllers.setup import setup_culler
 

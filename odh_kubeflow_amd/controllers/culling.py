@@ -68,6 +68,8 @@ from ..models import kinds
 from ..models import meta as m
 from ..models.notebook import (LAST_ACTIVITY_ANNOTATION, LAST_ACTIVITY_CHECK_TIMESTAMP_ANNOTATION, STOP_ANNOTATION,
                                gpu_request)
+from ..nodeagent.identity import IDENTITY_DOMAIN
+from ..nodeagent.identity import server_name as agent_server_name
 from ..runtime.controller import Request, Result
 from ..runtime.retry import retry_on_conflict
 from ..utils.timeutil import now, parse_rfc3339, rfc3339
@@ -109,7 +111,7 @@ class CullerConfig:
     gpu_agent_port: int = 9464
     gpu_agent_token_file: str = ""  # bearer token for the node agent (nodeagent/auth.py); "" = none
     gpu_agent_ca_file: str = ""  # the node agents' CA (HTTPS); "" with gpu_agent_insecure false: no GPU data
-    gpu_agent_server_name: str = ""  # the name the agents' certificate carries
+    gpu_agent_identity_domain: str = ""  # agent certificates name <node>.<this> (nodeagent/identity.py)
     gpu_agent_insecure: bool = False  # plain HTTP to the agents (tests, development)
     gpu_vram_active_bytes: float = 0.0  # 0: resident VRAM is not activity (see module docstring)
     http_timeout_s: float = 10.0
@@ -142,8 +144,7 @@ class CullerConfig:
         c.gpu_agent_port = int(env_default(env, "CULLING_GPU_AGENT_PORT", "9464"))
         c.gpu_agent_token_file = env.get("CULLING_GPU_AGENT_TOKEN_FILE", "")
         c.gpu_agent_ca_file = env.get("CULLING_GPU_AGENT_CA_FILE", "")
-        c.gpu_agent_server_name = env_default(
-            env, "CULLING_GPU_AGENT_SERVER_NAME", f"mi355x-node-agent.{env.get('K8S_NAMESPACE') or 'opendatahub'}.svc")
+        c.gpu_agent_identity_domain = env_default(env, "CULLING_GPU_AGENT_IDENTITY_DOMAIN", IDENTITY_DOMAIN)
         c.gpu_agent_insecure = env_default(env, "CULLING_GPU_AGENT_INSECURE", "false").strip().lower() == "true"
         c.gpu_vram_active_bytes = float(env_default(env, "CULLING_GPU_VRAM_ACTIVE_BYTES", "0"))
         c.startup_allowance_s = float(env_default(env, "CULL_STARTUP_ALLOWANCE", "10")) * 60.0
@@ -474,16 +475,18 @@ class NodeAgentActivity(GpuActivity):
     ``endpoint_for(pod) -> "host:port"`` overrides that (test harnesses whose fake nodes
     share one IP).
 
-    Over HTTPS (``ca_file``): the agent's certificate must chain to that CA and carry
-    ``server_name`` (one serving certificate for every node's agent, ``cmd/webhook_certs
-    --node-agent-secret``), so the bearer token and the busy/idle answers never cross the node
-    network in cleartext and a spoofed agent cannot cull or pin a notebook.  Without a CA the
-    agents are not asked at all (no GPU data: the Jupyter signal decides) unless ``insecure``.
+    Over HTTPS (``ca_file``): the agent's certificate must chain to that CA and name the pod's
+    own node — ``<pod.spec.nodeName>.<identity_domain>``, issued to that node's agent alone
+    (``nodeagent/identity.py``: a key per node, the node bound by the agent pod's token) — so
+    the bearer token and the busy/idle answers never cross the node network in cleartext, and
+    neither a spoofed agent nor another node's agent can cull or pin a notebook.  Without a CA
+    the agents are not asked at all (no GPU data: the Jupyter signal decides) unless
+    ``insecure``.
     """
 
     def __init__(self, port: int = 9464, timeout_s: float = 2.0,
                  endpoint_for: Optional[Callable[[dict], Optional[str]]] = None, token_file: str = "",
-                 ca_file: str = "", server_name: str = "", insecure: bool = False):
+                 ca_file: str = "", identity_domain: str = "", insecure: bool = False):
         self.port = port
         self.token = None
         if token_file:
@@ -495,13 +498,14 @@ class NodeAgentActivity(GpuActivity):
             from ..utils.tlsreload import client_context
 
             self.ssl = client_context(ca_file)
-        self.server_name = server_name or None
+        self.identity_domain = identity_domain or IDENTITY_DOMAIN
         self.insecure = insecure
         self.timeout_s = timeout_s
         self.endpoint_for = endpoint_for or self.default_endpoint
         self._session = None
         self.requests = 0
         self.refused_cleartext = 0
+        self.no_node = 0  # pods without spec.nodeName: no agent identity to verify
 
     def default_endpoint(self, pod: dict) -> Optional[str]:
         """``<hostIP>:<port>`` of the pod's node agent; IPv6 literals are bracketed
@@ -532,6 +536,10 @@ class NodeAgentActivity(GpuActivity):
                             "HTTP; culling falls back to the Jupyter signal")
             self.refused_cleartext += 1
             return None
+        node = (pod.get("spec") or {}).get("nodeName")
+        if self.ssl is not None and not node:
+            self.no_node += 1
+            return None
         if self._session is None or self._session.closed:
             self._session = aiohttp.ClientSession(timeout=aiohttp.ClientTimeout(total=self.timeout_s))
         q = urllib.parse.urlencode({"pod_uid": m.uid(pod), "namespace": m.namespace(pod), "name": m.name(pod),
@@ -540,7 +548,8 @@ class NodeAgentActivity(GpuActivity):
         try:
             headers = self.token.header() if self.token is not None else None
             scheme = "https" if self.ssl is not None else "http"
-            tls = {"ssl": self.ssl, "server_hostname": self.server_name} if self.ssl is not None else {}
+            tls = ({"ssl": self.ssl, "server_hostname": agent_server_name(node, self.identity_domain)}
+                   if self.ssl is not None else {})
             async with self._session.get(f"{scheme}://{ep}/gpu/activity?{q}", headers=headers, **tls) as resp:
                 if resp.status != 200:
                     return None
@@ -571,7 +580,7 @@ class CullingReconciler:
         if self.gpu is None and self.cfg.activity_source in ("amdgpu", "combined"):
             self.gpu = NodeAgentActivity(port=self.cfg.gpu_agent_port, token_file=self.cfg.gpu_agent_token_file,
                                          ca_file=self.cfg.gpu_agent_ca_file,
-                                         server_name=self.cfg.gpu_agent_server_name,
+                                         identity_domain=self.cfg.gpu_agent_identity_domain,
                                          insecure=self.cfg.gpu_agent_insecure)
         self.jupyter = jupyter or JupyterActivity(self.cfg, use_pod_endpoint=self.env.get(
             "CULLER_USE_POD_ENDPOINT", "false") == "true")

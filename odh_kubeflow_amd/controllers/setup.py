@@ -58,6 +58,20 @@ def setup_kf(mgr, env: Mapping[str, str] = os.environ, *, culling: Optional[bool
     return out
 
 
+def setup_event_reemitter(mgr, *, reference_emulation: bool = False):
+    """The Pod/StatefulSet event re-emitter alone (``--controllers events``; the reference runs it
+    in the kf manager, ``kf/controllers/notebook_controller.go:778-826``).  Its work is one
+    reconcile and one Event write per platform Event, none of it on a notebook's create→Ready
+    path, so the shard pod runs it beside the culler — a process that already watches the
+    Notebooks and Pods it maps Events with — rather than in the notebook reconciler's."""
+    from .notebook import NotebookEventReemitter
+
+    mgr.skip_own_write_echoes = not reference_emulation
+    e = NotebookEventReemitter(mgr.client, mgr.reader, mgr.get_event_recorder_for("notebook-controller"))
+    e.setup_with_manager(mgr, max_concurrent=1 if reference_emulation else None)
+    return e
+
+
 def setup_culler(mgr, env: Mapping[str, str] = os.environ, *, activity=None, reference_emulation: bool = False):
     """The CullingReconciler alone (``--controllers culler``: the culler in a process of its
     own, so its periodic checks of every resident notebook never queue a notebook's create→Ready

@@ -549,7 +549,7 @@ def control_plane_statefulset(shards: int) -> dict:
                                                           "--assign-namespaces", "--assign-policy=balanced"],
                                   8080, 8081, role="kf")
     culler = _control_plane_container("manager-culler", common + [
-        "--controllers=culler", "--metrics-bind-address=:8086", "--health-probe-bind-address=:8087"], 8086, 8087,
+        "--controllers=culler,events", "--metrics-bind-address=:8086", "--health-probe-bind-address=:8087"], 8086, 8087,
         role="culler")
     odh = _control_plane_container("manager-odh", common + [
         "--controllers=odh", "--metrics-bind-address=:8082", "--health-probe-bind-address=:8083"], 8082, 8083,

@@ -18,6 +18,7 @@ CLUSTER_ROLE_BINDING = "rbac.authorization.k8s.io/v1/ClusterRoleBinding"
 LEASE = "coordination.k8s.io/v1/Lease"
 MUTATING_WEBHOOK_CONFIGURATION = "admissionregistration.k8s.io/v1/MutatingWebhookConfiguration"
 CRD = "apiextensions.k8s.io/v1/CustomResourceDefinition"
+CSR = "certificates.k8s.io/v1/CertificateSigningRequest"
 
 NOTEBOOK_V1 = "kubeflow.org/v1/Notebook"
 NOTEBOOK_V1ALPHA1 = "kubeflow.org/v1alpha1/Notebook"

@@ -146,6 +146,8 @@ def _builtin(s: Scheme) -> None:
         R("apiextensions.k8s.io", "CustomResourceDefinition", "customresourcedefinitions", False, ("v1",), "v1",
           True, short_names=("crd",)),
         R("authentication.k8s.io", "TokenReview", "tokenreviews", False, ("v1",), "v1", True),
+        R("certificates.k8s.io", "CertificateSigningRequest", "certificatesigningrequests", False, ("v1",), "v1",
+          True, short_names=("csr",)),
         R("authorization.k8s.io", "SubjectAccessReview", "subjectaccessreviews", False, ("v1",), "v1", True),
     ):
         s.register(info)

@@ -189,10 +189,10 @@ def measure(args) -> Optional[dict]:
             sep = culling_enabled(args) and not getattr(args, "culler_in_kf", False)
             out["config"]["parallelism"] = (f"namespace-sharded control plane x{world}: per MI355X rank the shard pod "
                                             f"of config/overlays/mi355x-sharded, `cmd/control_plane.py --shard r` as a "
-                                            f"kf process{', a culler process' if sep else ''}, an odh reconciler "
+                                            f"kf process{', a culler + event re-emitter process' if sep else ''}, an odh reconciler "
                                             f"process and an odh webhook process")
             out["config"]["architecture"] = ("cmd/control_plane --shard r --controllers "
-                                             + ("notebook | culler | odh | webhook (overlay mi355x-sharded)" if sep else
+                                             + ("notebook | culler,events | odh | webhook (overlay mi355x-sharded)" if sep else
                                                 "kf | odh | webhook" + (" (culler in the kf process: A/B variant)"
                                                                         if culling_enabled(args) else "")))
         else:

@@ -83,7 +83,7 @@ class ShardConfig:
     process: bool = False  # run the control plane as its own process(es), as deployed
     split: bool = True  # sharded, process mode: the shard pod's containers as processes (kf | odh | webhook)
     webhook_process: bool = True  # sharded, split: the webhook in a process of its own (False: odh + webhook)
-    culler_process: bool = False  # sharded, split: the culler in a process of its own (notebook | culler)
+    culler_process: bool = False  # sharded, split: culler + event re-emitter apart (notebook | culler,events)
     # sharded: flags added to every process that leads something (e.g. --leader-elect and the lease
     # timings; tools/bench_failover.py runs standby replicas next to them)
     leader_elect_args: List[str] = field(default_factory=list)
@@ -145,8 +145,8 @@ class ControlPlaneShard:
         if cfg.arch == "sharded":
             # the shard pod of config/overlays/mi355x-sharded: the control plane split into a
             # kf process, an odh process and a webhook process (cmd/control_plane.py docstring)
-            sets = [["notebook"], ["culler"]] if cfg.culler_process and (cfg.split if split is None else split) \
-                else [["kf"]]
+            sets = [["notebook"], ["culler", "events"]] \
+                if cfg.culler_process and (cfg.split if split is None else split) else [["kf"]]
             if cfg.odh:
                 if cfg.webhook and cfg.webhook_process:
                     sets += [["odh"], ["webhook"]]

@@ -186,10 +186,17 @@ class WebhookDispatcher:
 class ApiServer:
     """aiohttp application serving an :class:`ObjectStore`."""
 
+    ADMIN = {"username": "system:admin", "groups": ["system:masters", "system:authenticated"]}
+
     def __init__(self, store: ObjectStore, token: Optional[str] = None,
-                 service_resolver: Optional[Callable[[str, str, int], str]] = None, audit=None):
+                 service_resolver: Optional[Callable[[str, str, int], str]] = None, audit=None,
+                 users: Optional[Dict[str, dict]] = None):
         self.store = store
         self.token = token
+        # bearer token -> user info ({"username", "uid", "groups", "extra"}): who a request is
+        # from, as kube-apiserver's authenticators say — stamped into a CertificateSigningRequest's
+        # spec on create (a client cannot claim someone else's identity there); no authorization
+        self.users = dict(users or {})
         self.audit = audit  # apiserver.audit.AuditLogger (DEBUG_WRITE_AUDITLOG)
         self.webhooks = WebhookDispatcher(store, service_resolver)
         self._runner: Optional[web.AppRunner] = None
@@ -246,9 +253,16 @@ class ApiServer:
                                   "platform": "linux/amd64"})
 
     def _authorized(self, req: web.Request) -> bool:
+        auth = req.headers.get("Authorization", "")
+        if self.users and auth.startswith("Bearer ") and auth[7:] in self.users:
+            return True
         if not self.token:
             return True
-        return req.headers.get("Authorization", "") == f"Bearer {self.token}"
+        return auth == f"Bearer {self.token}"
+
+    def _user(self, req: web.Request) -> dict:
+        auth = req.headers.get("Authorization", "")
+        return self.users.get(auth[7:], self.ADMIN) if auth.startswith("Bearer ") else self.ADMIN
 
     async def _dispatch(self, req: web.Request) -> web.StreamResponse:
         self.requests += 1
@@ -358,7 +372,7 @@ class ApiServer:
         info, version, ns, name, sub = pp.info, pp.version, pp.namespace, pp.name, pp.sub
         q = req.query
         st = self.store
-        if sub not in (None, "status"):
+        if sub not in (None, "status") and not (sub == "approval" and info.kind == "CertificateSigningRequest"):
             raise NotFound(info.plural, f"{name}/{sub}")
         method = req.method
         if method == "GET" and name is None:
@@ -376,6 +390,13 @@ class ApiServer:
             obj = await self._body(req)
             obj.setdefault("apiVersion", info.api_version(version))
             obj.setdefault("kind", info.kind)
+            if info.kind == "CertificateSigningRequest":  # the requester, from authentication
+                u = self._user(req)
+                spec = obj.setdefault("spec", {})
+                for k in ("username", "uid", "groups", "extra"):
+                    spec.pop(k, None)
+                    if u.get(k):
+                        spec[k] = u[k]
             dry = q.get("dryRun") == "All"
             out = await st.create(obj, namespace=ns, dry_run=dry)
             out["apiVersion"] = info.api_version(version)

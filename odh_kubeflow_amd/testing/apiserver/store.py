@@ -383,7 +383,7 @@ class ObjectStore:
         if cur is None:
             raise NotFound(info.plural if not info.group else f"{info.plural}.{info.group}", name)
         new["apiVersion"] = info.api_version()
-        if subresource == "status":
+        if subresource in ("status", "approval"):  # CSR approval: status.conditions
             merged = deepcopy_json(cur)
             if "status" in new:
                 merged["status"] = new["status"]
@@ -489,7 +489,7 @@ class ObjectStore:
         # a patch that carries a resourceVersion is a precondition, otherwise it applies to latest
         if not (isinstance(patch, dict) and (patch.get("metadata") or {}).get("resourceVersion")):
             nmd["resourceVersion"] = cur["metadata"]["resourceVersion"]
-        if subresource == "status":
+        if subresource in ("status", "approval"):  # CSR approval: status.conditions
             merged = deepcopy_json(cur)
             merged["status"] = new.get("status")
             merged["metadata"]["resourceVersion"] = nmd["resourceVersion"]

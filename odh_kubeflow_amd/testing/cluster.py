@@ -64,7 +64,6 @@ class ClusterConfig:
 
 
 OPENSHIFT_CRDS = (kinds.IMAGE_STREAM, kinds.PROXY, kinds.ROUTE, kinds.OAUTH_CLIENT)
-AGENT_SERVER_NAME = "mi355x-node-agent.opendatahub.svc"  # the node agents' certificate name
 
 
 def write_kubeconfig(path: str, server: str, user: str = "MasterOfTheSystems") -> None:
@@ -203,7 +202,7 @@ class LocalCluster:
                 # the production agent over HTTPS, as the DaemonSet serves it
                 self.node_agents[node_name] = await NodeTelemetryAgent(
                     cfg.telemetry, Attributor(cfg.telemetry, checkpoint_path=cp_path, ttl_s=0.0),
-                    host="127.0.0.1", port=0, tls_cert_dir=self._agent_certs().cert_dir).start()
+                    host="127.0.0.1", port=0, tls_cert_dir=self._agent_cert_dir(node_name)).start()
             if cfg.gpu_runtimes_in_process:
                 kl = self._mgr(f"kubelet-{node_name}", remote=cfg.remote_kubelets)
                 self.kubelets.append(kl)
@@ -226,16 +225,32 @@ class LocalCluster:
             await mgr.start()
         return self
 
-    def _agent_certs(self):
-        """One serving certificate for every node agent (as ``cmd/webhook_certs
-        --node-agent-secret`` issues it) and its CA for the culler."""
-        if getattr(self, "_agent_cert", None) is None:
-            from ..webhook.certs import generate
+    def _agent_ca_dir(self) -> str:
+        """The node agents' CA (``ca.crt`` / ``ca.key``), as the signer keeps it."""
+        if getattr(self, "_agent_ca", None) is None:
+            from ..webhook.certs import generate_ca
 
-            tmp = tempfile.TemporaryDirectory(prefix="odh-agent-certs-")
+            tmp = tempfile.TemporaryDirectory(prefix="odh-agent-ca-")
             self._tmpdirs.append(tmp)
-            self._agent_cert = generate((AGENT_SERVER_NAME,), tmp.name)
-        return self._agent_cert
+            generate_ca(tmp.name)
+            self._agent_ca = tmp.name
+        return self._agent_ca
+
+    def _agent_cert_dir(self, node: str) -> str:
+        """Node ``node``'s own agent identity — a key of its own and a certificate naming the
+        node, as ``nodeagent/identity.py``'s signer issues it for that node's agent pod."""
+        from ..nodeagent.identity import LEAF_VALIDITY_S, new_key_and_csr, sign_leaf
+
+        ca = self._agent_ca_dir()
+        d = os.path.join(ca, node)
+        os.makedirs(d, exist_ok=True)
+        key, csr = new_key_and_csr(node, "127.0.0.1")
+        with open(os.path.join(ca, "ca.crt")) as f, open(os.path.join(ca, "ca.key")) as g:
+            crt = sign_leaf(csr, f.read(), g.read(), node, "127.0.0.1", LEAF_VALIDITY_S)
+        for name, pem in (("tls.key", key), ("tls.crt", crt)):
+            with open(os.path.join(d, name), "w") as f:
+                f.write(pem)
+        return d
 
     def _build_kf(self) -> None:
         from ..controllers.setup import setup_kf
@@ -248,10 +263,9 @@ class LocalCluster:
 
             # every fake node's pods report hostIP 127.0.0.1: route by node name instead
             ports = {n: a.port for n, a in self.node_agents.items()}
-            certs = self._agent_certs()
             activity = NodeAgentActivity(endpoint_for=lambda pod: "127.0.0.1:%d" % ports[
                 (pod.get("spec") or {}).get("nodeName")] if (pod.get("spec") or {}).get("nodeName") in ports
-                else None, ca_file=os.path.join(certs.cert_dir, "ca.crt"), server_name=AGENT_SERVER_NAME)
+                else None, ca_file=os.path.join(self._agent_ca_dir(), "ca.crt"))
         out = setup_kf(kf, self.env, culling=culling, activity=activity, event_reemit=self.cfg.event_reemit,
                        reference_emulation=self.cfg.reference_emulation)
         self.kf_metrics = out["metrics"]

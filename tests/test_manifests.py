@@ -248,7 +248,7 @@ def test_sharded_overlay_shape():
     # the shard pod: the control plane split into a kf (notebook), a culler, an odh and a webhook process
     kf, cull, odh, wh = sts["spec"]["template"]["spec"]["containers"]
     assert "--shard=ordinal" in kf["args"] and f"--shard-count={n}" in kf["args"] and "--assign-namespaces" in kf["args"]
-    assert "--controllers=notebook" in kf["args"] and "--controllers=culler" in cull["args"]
+    assert "--controllers=notebook" in kf["args"] and "--controllers=culler,events" in cull["args"]
     assert "--controllers=odh" in odh["args"] and "--controllers=webhook" in wh["args"]
     for c in (cull, odh, wh):
         assert "--shard=ordinal" in c["args"] and "--assign-namespaces" not in c["args"]

@@ -241,18 +241,17 @@ def test_culler_kfd_attribution_only(run, sysfs):
 
     import tempfile
 
-    from odh_kubeflow_amd.webhook.certs import generate
-
-    certs = generate((AGENT_NAME,), tempfile.mkdtemp(prefix="odh-agent-tls-"))
+    ca_dir = _ca(tempfile.mkdtemp(prefix="odh-agent-ca-"))
 
     async def go():
+        # the cluster's one node (mi355x-node-0): its agent, with that node's own identity
         agent = await NodeTelemetryAgent(tel, Attributor(tel, proc_root=proc, ttl_s=0.0), host="127.0.0.1",
-                                         port=0, tls_cert_dir=certs.cert_dir).start()
+                                         port=0, tls_cert_dir=_node_identity(ca_dir, "mi355x-node-0")).start()
         # production defaults: https://<pod.status.hostIP>:<CULLING_GPU_AGENT_PORT>, verified against
-        # the agents' CA and name (mi355x-node-agent.<K8S_NAMESPACE>.svc)
+        # the agents' CA and the name of the pod's node (<spec.nodeName>.mi355x-node-agent.nodes)
         env = {"ENABLE_CULLING": "true", "CULL_IDLE_TIME": "60", "IDLENESS_CHECK_PERIOD_SECONDS": "0.2",
                "CULLING_ACTIVITY_SOURCE": "amdgpu", "CULLING_GPU_AGENT_PORT": str(agent.port),
-               "CULLING_GPU_AGENT_CA_FILE": os.path.join(certs.cert_dir, "ca.crt"),
+               "CULLING_GPU_AGENT_CA_FILE": os.path.join(ca_dir, "ca.crt"),
                "CLUSTER_DOMAIN": "invalid.example"}
         try:
             async with LocalCluster(ClusterConfig(culler=True, env=env)) as cl:
@@ -445,7 +444,27 @@ def test_agent_token_required_and_rotated(run, sysfs, tmp_path):
     run(go())
 
 
-AGENT_NAME = "mi355x-node-agent.opendatahub.svc"
+def _node_identity(ca_dir, node, host_ip="127.0.0.1"):
+    """A node agent's own key and certificate, as the signer issues them (nodeagent/identity.py)."""
+    from odh_kubeflow_amd.nodeagent.identity import LEAF_VALIDITY_S, new_key_and_csr, sign_leaf
+
+    d = os.path.join(ca_dir, node)
+    os.makedirs(d, exist_ok=True)
+    key, csr = new_key_and_csr(node, host_ip)
+    with open(os.path.join(ca_dir, "ca.crt")) as f, open(os.path.join(ca_dir, "ca.key")) as g:
+        crt = sign_leaf(csr, f.read(), g.read(), node, host_ip, LEAF_VALIDITY_S)
+    for name, pem in (("tls.key", key), ("tls.crt", crt)):
+        with open(os.path.join(d, name), "w") as f:
+            f.write(pem)
+    return d
+
+
+def _ca(path):
+    from odh_kubeflow_amd.webhook.certs import generate_ca
+
+    os.makedirs(path, exist_ok=True)
+    generate_ca(str(path))
+    return str(path)
 
 
 def test_culler_sends_agent_token(run, sysfs, tmp_path):
@@ -453,24 +472,24 @@ def test_culler_sends_agent_token(run, sysfs, tmp_path):
     gets GPU data; with none it gets no data (None: never idleness).  Over HTTPS, as deployed."""
     from odh_kubeflow_amd.controllers import culling as c
     from odh_kubeflow_amd.nodeagent.auth import TokenFile
-    from odh_kubeflow_amd.webhook.certs import generate
 
-    certs = generate((AGENT_NAME,), str(tmp_path / "tls"))
-    ca = os.path.join(certs.cert_dir, "ca.crt")
-
+    ca_dir = _ca(tmp_path / "ca")
+    ca = os.path.join(ca_dir, "ca.crt")
     root, proc, minors, tel = sysfs
     cp = CheckpointWriter(str(tmp_path / "dp" / "cp"))
     cp.allocate(UID_A, "nb", [fake_bdf(2)])
     set_fake_counter(root, minors[2], busy=70)
     tok = tmp_path / "token"
     tok.write_text("abc")
-    pod = {"metadata": {"name": "nb-0", "namespace": "u", "uid": UID_A}, "status": {"hostIP": "127.0.0.1"}}
+    pod = {"metadata": {"name": "nb-0", "namespace": "u", "uid": UID_A}, "spec": {"nodeName": "gpu-a"},
+           "status": {"hostIP": "127.0.0.1"}}
 
     async def go():
         agent = await NodeTelemetryAgent(tel, Attributor(tel, checkpoint_path=cp.path, ttl_s=0.0), host="127.0.0.1",
-                                         port=0, token=TokenFile(str(tok)), tls_cert_dir=certs.cert_dir).start()
-        good = c.NodeAgentActivity(port=agent.port, token_file=str(tok), ca_file=ca, server_name=AGENT_NAME)
-        none = c.NodeAgentActivity(port=agent.port, ca_file=ca, server_name=AGENT_NAME)
+                                         port=0, token=TokenFile(str(tok)),
+                                         tls_cert_dir=_node_identity(ca_dir, "gpu-a")).start()
+        good = c.NodeAgentActivity(port=agent.port, token_file=str(tok), ca_file=ca)
+        none = c.NodeAgentActivity(port=agent.port, ca_file=ca)
         try:
             await asyncio.sleep(0.1)
             got = await good.busy(pod, 0.05)
@@ -486,60 +505,78 @@ def test_culler_sends_agent_token(run, sysfs, tmp_path):
 
 
 def test_agent_serves_https_only_and_the_culler_verifies_it(run, sysfs, tmp_path):
-    """the agent's answers decide culls, and its token must not cross the node
-    network in cleartext.  The agent serves HTTPS; the culler asks only over HTTPS, verifying the
-    agent's certificate against the agents' CA and name — a cleartext client, a wrong name or
-    another CA's certificate get nothing (no GPU data: never idleness, never a cull); a renewed
-    certificate is picked up without a restart."""
+    """the agent's answers decide culls, and its token must not cross the
+    node network in cleartext.  The agent serves HTTPS with its node's own certificate; the
+    culler asks only over HTTPS, verifying the certificate against the agents' CA and the name
+    of the pod's node — a cleartext client, another CA's certificate, and **node B's certificate
+    answering for a pod on node A** all get nothing (no GPU data: never idleness, never a cull);
+    a renewed certificate is picked up without a restart."""
     import ssl as _ssl
 
     from odh_kubeflow_amd.controllers import culling as c
-    from odh_kubeflow_amd.webhook.certs import generate, issue_leaf
+    from odh_kubeflow_amd.nodeagent.identity import IDENTITY_DOMAIN, LEAF_VALIDITY_S, new_key_and_csr, sign_leaf
 
     root, proc, minors, tel = sysfs
     cp = CheckpointWriter(str(tmp_path / "dp" / "cp"))
     cp.allocate(UID_A, "nb", [fake_bdf(3)])
     set_fake_counter(root, minors[3], busy=55)
-    certs = generate((AGENT_NAME,), str(tmp_path / "tls"))
-    ca = os.path.join(certs.cert_dir, "ca.crt")
-    other = generate((AGENT_NAME,), str(tmp_path / "other"))
-    pod = {"metadata": {"name": "nb-0", "namespace": "u", "uid": UID_A}, "status": {"hostIP": "127.0.0.1"}}
+    ca_dir = _ca(tmp_path / "ca")
+    ca = os.path.join(ca_dir, "ca.crt")
+    other_ca = os.path.join(_ca(tmp_path / "other"), "ca.crt")
+    a_dir = _node_identity(ca_dir, "gpu-a")
+    b_dir = _node_identity(ca_dir, "gpu-b")
+    on_a = {"metadata": {"name": "nb-0", "namespace": "u", "uid": UID_A}, "spec": {"nodeName": "gpu-a"},
+            "status": {"hostIP": "127.0.0.1"}}
+    on_b = {**on_a, "spec": {"nodeName": "gpu-b"}}
+    unscheduled = {**on_a, "spec": {}}
 
     async def go():
-        agent = await NodeTelemetryAgent(tel, Attributor(tel, checkpoint_path=cp.path, ttl_s=0.0), host="127.0.0.1",
-                                         port=0, tls_cert_dir=certs.cert_dir, cert_reload_s=0.05).start()
-        ok = c.NodeAgentActivity(port=agent.port, ca_file=ca, server_name=AGENT_NAME)
+        attr = Attributor(tel, checkpoint_path=cp.path, ttl_s=0.0)
+        agent = await NodeTelemetryAgent(tel, attr, host="127.0.0.1", port=0, tls_cert_dir=a_dir,
+                                         cert_reload_s=0.05).start()
+        # node B's agent (its own, valid certificate) answering at node A's address
+        impostor = await NodeTelemetryAgent(tel, attr, host="127.0.0.1", port=0, tls_cert_dir=b_dir).start()
+        ok = c.NodeAgentActivity(port=agent.port, ca_file=ca)
         cleartext = c.NodeAgentActivity(port=agent.port)  # no CA, not --insecure: refuses to ask
         insecure = c.NodeAgentActivity(port=agent.port, insecure=True)  # plain HTTP to an HTTPS agent
-        wrong_name = c.NodeAgentActivity(port=agent.port, ca_file=ca, server_name="evil.example")
-        wrong_ca = c.NodeAgentActivity(port=agent.port, ca_file=os.path.join(other.cert_dir, "ca.crt"),
-                                       server_name=AGENT_NAME)
+        wrong_ca = c.NodeAgentActivity(port=agent.port, ca_file=other_ca)
+        b_for_a = c.NodeAgentActivity(port=impostor.port, ca_file=ca)
+        clients = (ok, cleartext, insecure, wrong_ca, b_for_a)
         try:
             await asyncio.sleep(0.1)
-            got = await ok.busy(pod, 0.05)
+            got = await ok.busy(on_a, 0.05)
             assert got is not None and got["busy_mean"] == 55
-            assert await cleartext.busy(pod, 0.05) is None and cleartext.refused_cleartext == 1
-            assert await insecure.busy(pod, 0.05) is None
-            assert await wrong_name.busy(pod, 0.05) is None
-            assert await wrong_ca.busy(pod, 0.05) is None
-            # renewal: a new leaf from the same CA replaces the files; the agent reloads it
+            assert await cleartext.busy(on_a, 0.05) is None and cleartext.refused_cleartext == 1
+            assert await insecure.busy(on_a, 0.05) is None
+            assert await wrong_ca.busy(on_a, 0.05) is None
+            # the pod is on node A; B's agent holds a valid certificate of the same CA, for B
+            assert await b_for_a.busy(on_a, 0.05) is None
+            assert (await b_for_a.busy(on_b, 0.05) or {}).get("busy_mean") == 55  # ... good for B's pods
+            assert await ok.busy(on_b, 0.05) is None  # A's agent cannot answer for a pod on B either
+            assert await ok.busy(unscheduled, 0.05) is None and ok.no_node == 1
+            # renewal: a new key and certificate for the same node replace the files; reloaded live
             before = agent.tls.reloads
-            issue_leaf(certs.cert_dir, (AGENT_NAME,), 30)
+            key, csr = new_key_and_csr("gpu-a", "127.0.0.1")
+            with open(ca) as f, open(os.path.join(ca_dir, "ca.key")) as g:
+                crt = sign_leaf(csr, f.read(), g.read(), "gpu-a", "127.0.0.1", LEAF_VALIDITY_S)
+            for name, pem in (("tls.key", key), ("tls.crt", crt)):
+                with open(os.path.join(a_dir, name), "w") as f:
+                    f.write(pem)
             for _ in range(100):
                 if agent.tls.reloads > before:
                     break
                 await asyncio.sleep(0.05)
             assert agent.tls.reloads > before
             pem = await asyncio.to_thread(_ssl.get_server_certificate, ("127.0.0.1", agent.port))
-            with open(os.path.join(certs.cert_dir, "tls.crt")) as f:
-                assert pem.split() == f.read().split()  # the renewed leaf is served
-            got = await ok.busy(pod, 0.05)
+            assert pem.split() == crt.split()  # the renewed leaf is served
+            got = await ok.busy(on_a, 0.05)
             assert got is not None and got["busy_mean"] == 55
-            cfg = c.CullerConfig.from_env({"CULLING_GPU_AGENT_CA_FILE": ca, "K8S_NAMESPACE": "team"})
-            assert cfg.gpu_agent_ca_file == ca and cfg.gpu_agent_server_name == "mi355x-node-agent.team.svc"
+            cfg = c.CullerConfig.from_env({"CULLING_GPU_AGENT_CA_FILE": ca})
+            assert cfg.gpu_agent_ca_file == ca and cfg.gpu_agent_identity_domain == IDENTITY_DOMAIN
             assert not cfg.gpu_agent_insecure
         finally:
-            for x in (ok, cleartext, insecure, wrong_name, wrong_ca):
+            for x in clients:
                 await x.close()
             await agent.stop()
+            await impostor.stop()
     run(go())

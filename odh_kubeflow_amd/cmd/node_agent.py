@@ -80,7 +80,7 @@ def build(args):
         missing = [f for f in ("tls.crt", "tls.key") if not os.path.exists(os.path.join(args.tls_cert_dir, f))]
         if missing:
             raise SystemExit(f"node agent serving certificate missing in {args.tls_cert_dir}: {', '.join(missing)} "
-                             "(cmd/webhook_certs.py --node-agent-secret writes it)")
+                             "(the enroll init container writes it: cmd/node_agent_enroll.py)")
     else:
         log.warning("--insecure: serving plain HTTP")
     return NodeTelemetryAgent(telemetry, attributor, host=args.bind, port=args.port, token=token,

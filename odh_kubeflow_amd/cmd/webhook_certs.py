@@ -40,13 +40,7 @@ def parse(argv=None):
     p.add_argument("--random-secret", action="append", default=[],
                    help="also ensure this Secret holds a random bearer token under key 'token' (repeatable; "
                         "kept once it exists): the node agent / culler shared token, nodeagent/auth.py")
-    p.add_argument("--node-agent-secret", default="",
-                   help="also keep this Secret holding the MI355X node agents' serving cert (tls.crt / tls.key / "
-                        "ca.crt, a CA of its own; one cert for every node's agent), nodeagent/server.py")
-    p.add_argument("--node-agent-name", default="mi355x-node-agent",
-                   help="the name the agents' cert carries (<name>.<namespace>.svc …; the culler checks it)")
-    p.add_argument("--node-agent-ca-configmap", default="",
-                   help="ConfigMap holding the node agents' CA (ca.crt) for the culler")
+    # the node agents' serving certificates are per node, from cmd/node_agent_signer.py
     return p.parse_args(argv)
 
 
@@ -64,13 +58,6 @@ async def amain(argv=None) -> int:
                               args.service_name or ["odh-notebook-controller-webhook-service"],
                               args.mwc_name or ["odh-notebook-controller-mutating-webhook-configuration"],
                               args.extra_host, args.validity_days, args.renew_before_days, args.cluster_domain)
-        if args.node_agent_secret:
-            # a CA of its own: a client trusting the agents' CA never trusts a webhook cert, and
-            # the other way round
-            out["node_agent"] = await provision(client, args.namespace or namespace_from_env(),
-                                                args.node_agent_secret, [args.node_agent_name], [], [],
-                                                args.validity_days, args.renew_before_days, args.cluster_domain,
-                                                ca_configmap=args.node_agent_ca_configmap or None)
         if args.random_secret:
             from ..nodeagent.auth import ensure_token_secret
 

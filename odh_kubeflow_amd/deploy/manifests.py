@@ -12,7 +12,9 @@
   :8081, metrics on :8080, ``GOMEMLIMIT``-style limits, env from ConfigMaps;
 * ``node-agent/`` — the MI355X node agent DaemonSet (``amd.com/gpu.family`` nodes):
   read-only amdgpu telemetry + pod→GPU attribution (``nodeagent/``), no apiserver access,
-  no RBAC, no GPU device files; it never requests ``amd.com/gpu`` itself;
+  no GPU device files, never ``amd.com/gpu`` itself; its enrollment containers obtain the
+  node's own serving certificate through a CSR, which the ``node-agent-signer`` Deployment
+  issues for the requesting pod's node only (``nodeagent/identity.py``);
 * ``webhook/`` — Service + MutatingWebhookConfiguration (``failurePolicy: Fail``);
 * ``webhook-certs/`` — outside OpenShift (no service-ca): the serving-cert provisioner
   (``cmd/webhook_certs.py``) as a Job + weekly renewal CronJob with the RBAC it needs
@@ -45,6 +47,7 @@ from typing import Dict, List, Optional
 import yaml
 
 from ..models.notebook import GPU_RESOURCE
+from ..nodeagent.identity import IDENTITY_DOMAIN, SIGNER_NAME
 
 ROCM_NOTEBOOK_IMAGE = "rocm/pytorch:rocm7.0_ubuntu22.04_py3.10_pytorch_release_2.10.0"
 NAME_PREFIX = "odh-kubeflow-amd-"
@@ -52,11 +55,14 @@ WEBHOOK_CERT_SECRET = "odh-notebook-controller-webhook-cert"  # created by servi
 WEBHOOK_SERVICE = "odh-notebook-controller-webhook-service"
 AGENT_TOKEN_SECRET = "mi355x-node-agent-token"  # nodeagent/auth.py TOKEN_SECRET
 AGENT_TOKEN_MOUNT = "/var/run/secrets/odh/node-agent"
-# the node agents serve HTTPS: one serving cert for every node's agent (cmd/webhook_certs
-# --node-agent-secret), its CA published to the culler in a ConfigMap (nodeagent/server.py)
+# the node agents serve HTTPS, each node's agent with a certificate of its own node
+# (nodeagent/identity.py): the key is made in the pod (memory-backed emptyDir), the
+# certificate issued by the node-agent-signer for the requesting pod's node; the signer's CA
+# stays in its Secret, the trust bundle is published to the culler in a ConfigMap
 AGENT_NAME = "mi355x-node-agent"
-AGENT_TLS_SECRET = "mi355x-node-agent-tls"
-AGENT_TLS_MOUNT = "/var/run/secrets/odh/node-agent-tls"
+AGENT_SIGNER = "mi355x-node-agent-signer"
+AGENT_CA_SECRET = "mi355x-node-agent-ca"  # the signer's CA (ca.crt / ca.key): only the signer reads it
+AGENT_TLS_MOUNT = "/var/run/odh/node-agent-tls"
 AGENT_CA_CONFIGMAP = "mi355x-node-agent-ca"
 AGENT_CA_MOUNT = "/var/run/odh/node-agent-ca"
 MWC_NAME = "mutating-webhook-configuration"
@@ -241,17 +247,12 @@ def _culler_env() -> List[dict]:
                                                           "key": k, "optional": True}}} for k in CULLER_KEYS] + [
         {"name": "CULLING_GPU_AGENT_TOKEN_FILE", "value": f"{AGENT_TOKEN_MOUNT}/token"},
         {"name": "CULLING_GPU_AGENT_CA_FILE", "value": f"{AGENT_CA_MOUNT}/ca.crt"},
-        {"name": "AGENT_NAMESPACE", "valueFrom": {"fieldRef": {"fieldPath": "metadata.namespace"}}},
-        {"name": "CULLING_GPU_AGENT_SERVER_NAME", "value": f"{AGENT_NAME}.$(AGENT_NAMESPACE).svc"}]
-
-
-def _culler_env_index(name: str) -> int:
-    """Position of ``name`` in the kf manager container's env (JSON patches address it by index)."""
-    return [e["name"] for e in kf_deployment()["spec"]["template"]["spec"]["containers"][0]["env"]].index(name)
+        # an agent's certificate must name the pod's node: <spec.nodeName>.<this domain>
+        {"name": "CULLING_GPU_AGENT_IDENTITY_DOMAIN", "value": IDENTITY_DOMAIN}]
 
 
 def _agent_ca_volume() -> dict:
-    """The node agents' CA for the culler (``cmd/webhook_certs --node-agent-ca-configmap``).
+    """The node agents' trust bundle for the culler (published by the node-agent-signer).
     Optional: until it exists the culler asks no agent (no GPU data; Jupyter decides)."""
     return {"name": "node-agent-ca", "configMap": {"name": AGENT_CA_CONFIGMAP, "optional": True}}
 
@@ -337,9 +338,30 @@ def odh_deployment() -> dict:
 
 def node_agent_daemonset() -> dict:
     """The production node agent (``cmd/node_agent.py``): read-only amdgpu telemetry + pod→GPU
-    attribution.  No apiserver access (token not mounted, no RBAC), no GPU device files; reads
-    host ``/sys`` (amdgpu + KFD), host ``/proc`` (pod cgroup of each GPU process), the kubelet
-    pod-resources socket and device-plugin checkpoint.  The culler reaches it on the hostPort."""
+    attribution.  The agent container has no apiserver access (no token), no GPU device files;
+    it reads host ``/sys`` (amdgpu + KFD), host ``/proc`` (pod cgroup of each GPU process), the
+    kubelet pod-resources socket and device-plugin checkpoint.  The culler reaches it on the
+    hostPort.
+
+    Its serving identity is the node's own (``nodeagent/identity.py``): the ``enroll`` init
+    container makes a key in a memory-backed volume and obtains a certificate for this node
+    through a CSR (``cmd/node_agent_enroll.py --once``: the agent starts with one), the
+    ``enroll-renew`` container renews it.  Only these two mount a service account token — a
+    projected one, bound to the pod, which is what the signer checks the node against."""
+    node_env = [{"name": "NODE_NAME", "valueFrom": {"fieldRef": {"fieldPath": "spec.nodeName"}}},
+                {"name": "HOST_IP", "valueFrom": {"fieldRef": {"fieldPath": "status.hostIP"}}}]
+    tls_rw = {"name": "tls", "mountPath": AGENT_TLS_MOUNT}
+    sa_mount = {"name": "enroll-token", "mountPath": "/var/run/secrets/kubernetes.io/serviceaccount",
+                "readOnly": True}
+
+    def enroll(name: str, once: bool) -> dict:
+        return {"name": name, "image": MANAGER_IMAGE,
+                "command": ["python", "-m", "odh_kubeflow_amd.cmd.node_agent_enroll"],
+                "args": ["--node-name=$(NODE_NAME)", "--host-ip=$(HOST_IP)", f"--cert-dir={AGENT_TLS_MOUNT}"]
+                + (["--once"] if once else []),
+                "env": node_env, "volumeMounts": [tls_rw, sa_mount],
+                "securityContext": {**RESTRICTED, "readOnlyRootFilesystem": True, "runAsUser": 65532},
+                "resources": {"requests": {"cpu": "10m", "memory": "32Mi"}, "limits": {"memory": "128Mi"}}}
     c = {"name": "agent", "image": MANAGER_IMAGE,
          "command": ["python", "-m", "odh_kubeflow_amd.cmd.node_agent"],
          "args": ["--port=9464", "--sysfs-root=/host/sys", "--proc-root=/host/proc",
@@ -353,7 +375,7 @@ def node_agent_daemonset() -> dict:
                           {"name": "pod-resources", "mountPath": "/var/lib/kubelet/pod-resources"},
                           {"name": "device-plugins", "mountPath": "/var/lib/kubelet/device-plugins",
                            "readOnly": True}, dict(AGENT_TOKEN_MOUNT_SPEC),
-                          {"name": "tls", "mountPath": AGENT_TLS_MOUNT, "readOnly": True}],
+                          {**tls_rw, "readOnly": True}],
          # uid 0 explicitly: the image runs as 65532, and the kubelet's pod-resources socket is
          # root-owned 0660 (no capability is needed for that: owner permissions; every
          # capability stays dropped)
@@ -361,15 +383,19 @@ def node_agent_daemonset() -> dict:
                              "allowPrivilegeEscalation": False, "capabilities": {"drop": ["ALL"]}},
          "resources": {"requests": {"cpu": "50m", "memory": "128Mi"}, "limits": {"memory": "512Mi"}}}
     return {"apiVersion": "apps/v1", "kind": "DaemonSet",
-            "metadata": {"name": "mi355x-node-agent", "labels": {"app": "mi355x-node-agent"}},
-            "spec": {"selector": {"matchLabels": {"app": "mi355x-node-agent"}},
-                     "template": {"metadata": {"labels": {"app": "mi355x-node-agent"}},
-                                  "spec": {"serviceAccountName": "mi355x-node-agent",
+            "metadata": {"name": AGENT_NAME, "labels": {"app": AGENT_NAME}},
+            "spec": {"selector": {"matchLabels": {"app": AGENT_NAME}},
+                     "template": {"metadata": {"labels": {"app": AGENT_NAME}},
+                                  "spec": {"serviceAccountName": AGENT_NAME,
                                            "automountServiceAccountToken": False,
                                            "nodeSelector": {"amd.com/gpu.family": "AI"},
                                            "tolerations": [{"key": GPU_RESOURCE, "operator": "Exists",
                                                             "effect": "NoSchedule"}],
-                                           "containers": [c],
+                                           # the enrollment containers write the pair as 65532;
+                                           # the (root) agent reads it
+                                           "securityContext": {"fsGroup": 65532},
+                                           "initContainers": [enroll("enroll", once=True)],
+                                           "containers": [c, enroll("enroll-renew", once=False)],
                                            "volumes": [{"name": "sys", "hostPath": {"path": "/sys"}},
                                                        {"name": "proc", "hostPath": {"path": "/proc"}},
                                                        {"name": "pod-resources", "hostPath": {
@@ -377,13 +403,66 @@ def node_agent_daemonset() -> dict:
                                                        {"name": "device-plugins", "hostPath": {
                                                            "path": "/var/lib/kubelet/device-plugins"}},
                                                        _agent_token_volume(),
-                                                       # the kubelet retries the mount until the
-                                                       # provisioner (or service-ca) wrote it
-                                                       {"name": "tls", "secret": {
-                                                           "secretName": AGENT_TLS_SECRET, "defaultMode": 0o440,
-                                                           # the serving pair only, never the CA key
-                                                           "items": [{"key": "tls.crt", "path": "tls.crt"},
-                                                                     {"key": "tls.key", "path": "tls.key"}]}}]}}}}
+                                                       # the node's key: in memory, in this pod only
+                                                       {"name": "tls", "emptyDir": {"medium": "Memory",
+                                                                                    "sizeLimit": "1Mi"}},
+                                                       # a token bound to this pod (1 h, rotated by the
+                                                       # kubelet): the signer checks its pod's node
+                                                       {"name": "enroll-token", "projected": {"sources": [
+                                                           {"serviceAccountToken": {"path": "token",
+                                                                                    "expirationSeconds": 3600}},
+                                                           {"configMap": {"name": "kube-root-ca.crt", "items": [
+                                                               {"key": "ca.crt", "path": "ca.crt"}]}},
+                                                           {"downwardAPI": {"items": [
+                                                               {"path": "namespace", "fieldRef": {
+                                                                   "fieldPath": "metadata.namespace"}}]}}]}}]}}}}
+
+
+def node_agent_rbac() -> List[dict]:
+    """The agents' ServiceAccount may submit CSRs and read them back (to collect its
+    certificate) — nothing else; the signer decides what a CSR gets."""
+    return [{"apiVersion": "v1", "kind": "ServiceAccount", "metadata": {"name": AGENT_NAME}},
+            {"apiVersion": "rbac.authorization.k8s.io/v1", "kind": "ClusterRole",
+             "metadata": {"name": f"{AGENT_NAME}-csr"},
+             "rules": [_rule(["certificates.k8s.io"], ["certificatesigningrequests"], ["create", "get"])]},
+            binding("ClusterRoleBinding", f"{AGENT_NAME}-csr", f"{AGENT_NAME}-csr", AGENT_NAME)]
+
+
+def node_agent_signer_docs() -> List[dict]:
+    """The signer (``cmd/node_agent_signer.py``): its CSRs (approve + sign, for its signerName
+    only), the agent pods (get: the binding check), its CA Secret and the trust ConfigMap."""
+    sa = "node-agent-signer"
+    c = {"name": "signer", "image": MANAGER_IMAGE,
+         "command": ["python", "-m", "odh_kubeflow_amd.cmd.node_agent_signer"],
+         "args": ["--leader-elect", f"--service-account={AGENT_NAME}", f"--daemonset={AGENT_NAME}",
+                  f"--ca-secret={AGENT_CA_SECRET}", f"--ca-configmap={AGENT_CA_CONFIGMAP}"],
+         "env": [{"name": "K8S_NAMESPACE", "valueFrom": {"fieldRef": {"fieldPath": "metadata.namespace"}}}],
+         "ports": [{"name": "metrics", "containerPort": 8080}, {"name": "probes", "containerPort": 8081}],
+         "securityContext": dict(RESTRICTED),
+         "resources": {"requests": {"cpu": "20m", "memory": "64Mi"}, "limits": {"memory": "256Mi"}},
+         **_probes()}
+    return [
+        {"apiVersion": "v1", "kind": "ServiceAccount", "metadata": {"name": sa}},
+        {"apiVersion": "rbac.authorization.k8s.io/v1", "kind": "ClusterRole", "metadata": {"name": AGENT_SIGNER},
+         "rules": [_rule(["certificates.k8s.io"], ["certificatesigningrequests"], ["get", "list", "watch"]),
+                   _rule(["certificates.k8s.io"], ["certificatesigningrequests/approval",
+                                                   "certificatesigningrequests/status"], ["update", "patch"]),
+                   {**_rule(["certificates.k8s.io"], ["signers"], ["approve", "sign"]),
+                    "resourceNames": [SIGNER_NAME]}]},
+        binding("ClusterRoleBinding", AGENT_SIGNER, AGENT_SIGNER, sa),
+        {"apiVersion": "rbac.authorization.k8s.io/v1", "kind": "Role", "metadata": {"name": AGENT_SIGNER},
+         "rules": [_rule([""], ["pods"], ["get"]),
+                   {**_rule([""], ["secrets"], ["get", "update"]), "resourceNames": [AGENT_CA_SECRET]},
+                   _rule([""], ["secrets"], ["create"]),
+                   {**_rule([""], ["configmaps"], ["get", "update"]), "resourceNames": [AGENT_CA_CONFIGMAP]},
+                   _rule([""], ["configmaps"], ["create"]),
+                   _rule(["coordination.k8s.io"], ["leases"], ALL), _rule([""], ["events"], ["create", "patch"])]},
+        binding("RoleBinding", AGENT_SIGNER, AGENT_SIGNER, sa),
+        {"apiVersion": "apps/v1", "kind": "Deployment",
+         "metadata": {"name": AGENT_SIGNER, "labels": {"app": AGENT_SIGNER}},
+         "spec": {"replicas": 1, "selector": {"matchLabels": {"app": AGENT_SIGNER}},
+                  "template": {"metadata": {"labels": {"app": AGENT_SIGNER}},
+                               "spec": {"serviceAccountName": sa, "containers": [c]}}}}]
 
 
 CONFORMANCE_NS = "odh-kubeflow-amd-conformance"
@@ -479,10 +558,8 @@ def webhook_certs_rbac(mwcs: List[str]) -> List[dict]:
         {"apiVersion": "v1", "kind": "ServiceAccount", "metadata": {"name": "webhook-certs"}},
         {"apiVersion": "rbac.authorization.k8s.io/v1", "kind": "Role", "metadata": {"name": "webhook-certs-role"},
          "rules": [{**_rule([""], ["secrets"], ["get", "update"]),
-                    "resourceNames": [WEBHOOK_CERT_SECRET, AGENT_TOKEN_SECRET, AGENT_TLS_SECRET]},
-                   _rule([""], ["secrets"], ["create"]),
-                   {**_rule([""], ["configmaps"], ["get", "update"]), "resourceNames": [AGENT_CA_CONFIGMAP]},
-                   _rule([""], ["configmaps"], ["create"])]},
+                    "resourceNames": [WEBHOOK_CERT_SECRET, AGENT_TOKEN_SECRET]},
+                   _rule([""], ["secrets"], ["create"])]},
         {"apiVersion": "rbac.authorization.k8s.io/v1", "kind": "ClusterRole",
          "metadata": {"name": "webhook-certs-cabundle-role"},
          "rules": [{**_rule(["admissionregistration.k8s.io"], ["mutatingwebhookconfigurations"], ["get", "update"]),
@@ -496,9 +573,7 @@ def webhook_certs_args(services: List[str], mwcs: List[str]) -> List[str]:
     """``cmd/webhook_certs.py`` arguments.  Names are the *rendered* (prefixed) names: they
     are plain strings to kustomize, so its name-reference fix-ups do not reach them."""
     return ([f"--secret-name={WEBHOOK_CERT_SECRET}"] + [f"--service-name={x}" for x in services]
-            + [f"--mwc-name={x}" for x in mwcs] + [f"--random-secret={AGENT_TOKEN_SECRET}"]
-            + [f"--node-agent-secret={AGENT_TLS_SECRET}", f"--node-agent-name={AGENT_NAME}",
-               f"--node-agent-ca-configmap={AGENT_CA_CONFIGMAP}"])
+            + [f"--mwc-name={x}" for x in mwcs] + [f"--random-secret={AGENT_TOKEN_SECRET}"])
 
 
 def webhook_certs_docs(services: List[str], mwcs: List[str]) -> Dict[str, object]:
@@ -712,9 +787,9 @@ def tree(version: Optional[str] = None) -> Dict[str, object]:
                                                     generatorOptions={"disableNameSuffixHash": True})
     t["manager/params.env"] = params_env(version)
     t["node-agent/daemonset.yaml"] = node_agent_daemonset()
-    t["node-agent/serviceaccount.yaml"] = {"apiVersion": "v1", "kind": "ServiceAccount",
-                                           "metadata": {"name": "mi355x-node-agent"}}
-    t["node-agent/kustomization.yaml"] = kustomization(["serviceaccount.yaml", "daemonset.yaml"])
+    t["node-agent/rbac.yaml"] = node_agent_rbac()
+    t["node-agent/signer.yaml"] = node_agent_signer_docs()
+    t["node-agent/kustomization.yaml"] = kustomization(["rbac.yaml", "daemonset.yaml", "signer.yaml"])
     t["webhook/service.yaml"] = webhook_service()
     t["webhook/manifests.yaml"] = mwc()
     t["webhook/kustomization.yaml"] = kustomization(["service.yaml", "manifests.yaml"])
@@ -737,25 +812,12 @@ def tree(version: Optional[str] = None) -> Dict[str, object]:
     t["overlays/kubeflow/kustomization.yaml"] = kustomization(
         ["../../default", "../../webhook-certs"], namespace="kubeflow", images=images,
         configMapGenerator=[{"name": "config", "behavior": "merge", "literals": ["USE_ISTIO=true"]}])
-    # the node agents' serving cert from OpenShift's service-ca (a Service named like the agents'
-    # certificate, annotated) and its CA injected into the culler's ConfigMap (key service-ca.crt)
-    t["overlays/openshift/node-agent-tls.yaml"] = [
-        {"apiVersion": "v1", "kind": "Service",
-         "metadata": {"name": AGENT_NAME, "namespace": "opendatahub", "annotations": {
-             "service.beta.openshift.io/serving-cert-secret-name": AGENT_TLS_SECRET}},
-         "spec": {"clusterIP": "None", "selector": {"app": AGENT_NAME},
-                  "ports": [{"name": "gpu-activity", "port": 9464, "targetPort": 9464}]}},
-        {"apiVersion": "v1", "kind": "ConfigMap",
-         "metadata": {"name": AGENT_CA_CONFIGMAP, "namespace": "opendatahub",
-                      "annotations": {"service.beta.openshift.io/inject-cabundle": "true"}}}]
+    # OpenShift: service-ca serves the webhook; the node agents' per-node identities come from
+    # the node-agent signer as everywhere (a service-ca certificate names a Service, not a node)
     t["overlays/openshift/kustomization.yaml"] = kustomization(
-        ["../../default", "node-agent-tls.yaml"], images=images,
+        ["../../default"], images=images,
         configMapGenerator=[{"name": "config", "behavior": "merge", "literals": ["ADD_FSGROUP=false"]}],
-        patches=[{"target": {"kind": "Deployment", "name": f"{NAME_PREFIX}deployment"}, "patch": yaml.safe_dump(
-                      [{"op": "replace", "path": "/spec/template/spec/containers/0/env/"
-                        f"{_culler_env_index('CULLING_GPU_AGENT_CA_FILE')}/value",
-                        "value": f"{AGENT_CA_MOUNT}/service-ca.crt"}], sort_keys=False)},
-                 {"target": {"kind": "Service", "name": ".*webhook-service"}, "patch":
+        patches=[{"target": {"kind": "Service", "name": ".*webhook-service"}, "patch":
                   "- op: add\n  path: /metadata/annotations\n  value:\n    service.beta.openshift.io/"
                   f"serving-cert-secret-name: {WEBHOOK_CERT_SECRET}\n"},
                  {"target": {"kind": "MutatingWebhookConfiguration"}, "patch":

@@ -330,6 +330,8 @@ class NodeAgentSigner:
         status = csr.get("status") or {}
         if status.get("certificate") or _condition(csr, "Denied") or _condition(csr, "Failed"):
             return Result()
+        if not self.ca_key:  # the CA is being loaded (the signer's first leader term)
+            return Result(requeue_after=0.5)
         conditions = list(status.get("conditions") or [])
         try:
             node, host_ip = await self.verify(csr)

@@ -20,13 +20,14 @@ of a pod's node at ``<pod.status.hostIP>:9464``):
 With a token file (``--token-file``, :mod:`.auth`) every endpoint but ``/healthz`` needs
 ``Authorization: Bearer <token>`` and answers 401 otherwise.
 
-The agent serves HTTPS (``--tls-cert-dir``: ``tls.crt`` / ``tls.key`` from the
-``mi355x-node-agent-tls`` Secret that ``cmd/webhook_certs --node-agent-secret`` issues, reloaded
-when renewed), so neither the bearer token nor a busy/idle answer — on which a GPU notebook is
-culled or kept — crosses the node network in cleartext, and the culler verifies the answer
-comes from a holder of the agent's key (its CA, the ``mi355x-node-agent-ca`` ConfigMap, and the
-certificate's name ``mi355x-node-agent.<namespace>.svc``).  Plain HTTP only with ``--insecure``
-(tests, development).
+The agent serves HTTPS (``--tls-cert-dir``: ``tls.crt`` / ``tls.key`` — this node's own key
+and certificate, which the DaemonSet's enrollment containers obtain through a CSR and renew,
+``nodeagent/identity.py``; reloaded when renewed), so neither the bearer token nor a busy/idle
+answer — on which a GPU notebook is culled or kept — crosses the node network in cleartext,
+and the culler verifies the answer comes from the agent of the pod's own node (the signer's
+CA from the ``mi355x-node-agent-ca`` ConfigMap, and the certificate's name
+``<spec.nodeName>.mi355x-node-agent.nodes``).  Plain HTTP only with ``--insecure`` (tests,
+development).
 """
 
 from __future__ import annotations

@@ -155,7 +155,7 @@ async def provision(client, namespace: str, secret_name: str = "odh-notebook-con
                     mwc_names: Iterable[str] = ("odh-notebook-controller-mutating-webhook-configuration",),
                     extra_hosts: Iterable[str] = (), validity_days: int = 365, renew_before_days: int = 90,
                     cluster_domain: str = "cluster.local", ca_validity_days: int = CA_VALIDITY_DAYS,
-                    previous_ca_grace_s: float = PREVIOUS_CA_GRACE_S, ca_configmap: Optional[str] = None) -> dict:
+                    previous_ca_grace_s: float = PREVIOUS_CA_GRACE_S) -> dict:
     """Ensure the serving Secret holds a valid cert and every named MWC trusts it — without a
     window in which admission (``failurePolicy: Fail``) is rejected.
 
@@ -170,13 +170,8 @@ async def provision(client, namespace: str, secret_name: str = "odh-notebook-con
     ``service_name``: one Service name or several (a sharded control plane serves admission
     behind one Service per shard plus one for unassigned namespaces; the cert covers all).
 
-    ``ca_configmap``: also keep ConfigMap ``ca_configmap`` (key ``ca.crt``) equal to the trusted
-    CA bundle — for clients that must verify the server but must not mount its Secret (the
-    culler verifying the node agents, whose Secret holds their private key and the CA key).
-
     Returns ``{"secret": "created"|"renewed"|"rotated"|"kept", "ca": "new"|"kept",
-    "mwc": {name: "patched"|"kept"|"missing"}}`` ("renewed": new leaf, same CA; "rotated": new CA),
-    plus ``"ca_configmap": "created"|"updated"|"kept"`` when asked for.
+    "mwc": {name: "patched"|"kept"|"missing"}}`` ("renewed": new leaf, same CA; "rotated": new CA).
     """
     import time
 
@@ -239,26 +234,6 @@ async def provision(client, namespace: str, secret_name: str = "odh-notebook-con
     # can reach a pod through the Secret
     bundle_pem = ca + (prev_ca if prev_ca and prev_ca.strip() != ca.strip() else "")
     bundle = b64(bundle_pem)
-    if ca_configmap:
-        want = {"ca.crt": bundle_pem}
-        try:
-            cm = await client.get(kinds.CONFIG_MAP, ca_configmap, namespace)
-        except ApiError as e:
-            if not is_not_found(e):
-                raise
-            cm = None
-        if cm is None:
-            await client.create({"apiVersion": "v1", "kind": "ConfigMap",
-                                 "metadata": {"name": ca_configmap, "namespace": namespace,
-                                              "labels": {"app.kubernetes.io/managed-by": "odh-webhook-certs"}},
-                                 "data": want})
-            result["ca_configmap"] = "created"
-        elif (cm.get("data") or {}) != want:
-            cm["data"] = want
-            await client.update(cm)
-            result["ca_configmap"] = "updated"
-        else:
-            result["ca_configmap"] = "kept"
     for name in mwc_names:
         try:
             mwc = await client.get(kinds.MUTATING_WEBHOOK_CONFIGURATION, name)

@@ -241,7 +241,8 @@ def test_sharded_overlay_shape():
     selects exactly its replica, each shard's configuration selects its namespaces, and
     not-yet-assigned namespaces go to any shard."""
     objs = _render("mi355x-sharded")
-    assert not _by(objs, "Deployment")  # the two cluster-wide managers are not deployed
+    # the two cluster-wide managers are not deployed (the node agents' signer is)
+    assert list(_by(objs, "Deployment")) == ["odh-kubeflow-amd-mi355x-node-agent-signer"]
     (sts,) = _by(objs, "StatefulSet").values()
     n = sts["spec"]["replicas"]
     assert n == manifests.SHARDS == 8
@@ -346,18 +347,19 @@ def test_webhook_certs_rbac_is_scoped_to_its_objects(overlay):
     assert sorted(rule["resourceNames"]) == mwc_names
     (role,) = [o for n, o in _by(objs, "Role").items() if n.endswith("webhook-certs-role")]
     named = {r["resources"][0]: r for r in role["rules"] if r.get("resourceNames")}
-    assert sorted(named) == ["configmaps", "secrets"]
+    assert sorted(named) == ["secrets"]
     assert all(sorted(r["verbs"]) == ["get", "update"] for r in named.values())
-    assert sorted(named["secrets"]["resourceNames"]) == sorted(
-        [manifests.WEBHOOK_CERT_SECRET, manifests.AGENT_TOKEN_SECRET, manifests.AGENT_TLS_SECRET])
-    assert named["configmaps"]["resourceNames"] == [manifests.AGENT_CA_CONFIGMAP]  # the node agents' CA
+    assert sorted(named["secrets"]["resourceNames"]) == sorted([manifests.WEBHOOK_CERT_SECRET,
+                                                                manifests.AGENT_TOKEN_SECRET])
     unnamed = [r for r in role["rules"] if not r.get("resourceNames")]
-    assert [sorted(r["verbs"]) for r in unnamed] == [["create"], ["create"]]
-    # the serving pods (webhook, node agents) get the serving pair only, never the CA key
+    assert [sorted(r["verbs"]) for r in unnamed] == [["create"]]
+    # the webhook pods get the serving pair only, never the CA key; no pod mounts the agents' CA
+    # Secret (only the signer reads it, through the API)
     for o, ps in _pod_specs(objs):
         for v in ps.get("volumes") or []:
-            if (v.get("secret") or {}).get("secretName") in (manifests.WEBHOOK_CERT_SECRET, manifests.AGENT_TLS_SECRET):
+            if (v.get("secret") or {}).get("secretName") == manifests.WEBHOOK_CERT_SECRET:
                 assert sorted(i["key"] for i in v["secret"]["items"]) == ["tls.crt", "tls.key"], o["metadata"]
+            assert (v.get("secret") or {}).get("secretName") != manifests.AGENT_CA_SECRET
 
 
 def test_mi355x_overlay_runs_manager_workers_and_webhook_replicas():
@@ -375,3 +377,40 @@ def test_mi355x_overlay_runs_manager_workers_and_webhook_replicas():
     plain = _by(_render("standalone"), "Deployment")["odh-kubeflow-amd-manager"]
     assert not any(a.startswith(("--workers", "--webhook-replicas", "--cache-configmaps"))
                    for a in plain["spec"]["template"]["spec"]["containers"][0]["args"])
+
+
+def test_node_agent_identity_plumbing():
+    """each node's agent enrolls its own identity.  The DaemonSet's enroll init
+    container and renewal sidecar alone mount a (projected, pod-bound) token; the agent reads the
+    pair from a memory-backed volume, read-only; the agents' SA may only create/get CSRs; the
+    signer may approve/sign for its own signerName only and reads the agent pods; the culler
+    checks the node name."""
+    from odh_kubeflow_amd.nodeagent.identity import IDENTITY_DOMAIN, SIGNER_NAME
+
+    for overlay in ("mi355x", "mi355x-sharded", "openshift"):
+        objs = _render(overlay)
+        (ds,) = _by(objs, "DaemonSet").values()
+        ps = ds["spec"]["template"]["spec"]
+        assert ps["automountServiceAccountToken"] is False
+        assert [c["name"] for c in ps["initContainers"]] == ["enroll"] and "--once" in ps["initContainers"][0]["args"]
+        conts = {c["name"]: c for c in ps["containers"]}
+        assert set(conts) == {"agent", "enroll-renew"}
+        token_vol = next(v for v in ps["volumes"] if v["name"] == "enroll-token")
+        assert token_vol["projected"]["sources"][0]["serviceAccountToken"]["expirationSeconds"] == 3600
+        for c in [*ps["initContainers"], *ps["containers"]]:
+            mounts = {m["name"]: m for m in c.get("volumeMounts") or []}
+            assert ("enroll-token" in mounts) == (c["name"] != "agent"), c["name"]
+        agent_tls = next(m for m in conts["agent"]["volumeMounts"] if m["name"] == "tls")
+        assert agent_tls["readOnly"] is True
+        assert next(v for v in ps["volumes"] if v["name"] == "tls")["emptyDir"]["medium"] == "Memory"
+        crs = _by(objs, "ClusterRole")
+        (agent_cr,) = [o for n, o in crs.items() if n.endswith("mi355x-node-agent-csr")]
+        assert agent_cr["rules"] == [{"apiGroups": ["certificates.k8s.io"], "resources": ["certificatesigningrequests"],
+                                      "verbs": ["create", "get"]}]
+        (signer_cr,) = [o for n, o in crs.items() if n.endswith("mi355x-node-agent-signer")]
+        signers = [r for r in signer_cr["rules"] if r["resources"] == ["signers"]]
+        assert signers == [{"apiGroups": ["certificates.k8s.io"], "resources": ["signers"],
+                            "verbs": ["approve", "sign"], "resourceNames": [SIGNER_NAME]}]
+        envs = [e for o, p in _pod_specs(objs) for c in p["containers"] for e in c.get("env") or []
+                if e["name"] == "CULLING_GPU_AGENT_IDENTITY_DOMAIN"]
+        assert envs and all(e["value"] == IDENTITY_DOMAIN for e in envs)

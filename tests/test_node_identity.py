@@ -55,6 +55,9 @@ class _Cluster:
     """Python apiserver with the users above, the two agent pods and a rogue one, and the
     signer running — entered inside the test's own event loop."""
 
+    def __init__(self, signer: bool = True):
+        self.with_signer = signer
+
     async def __aenter__(self):
         import copy
 
@@ -70,16 +73,19 @@ class _Cluster:
         for tok, pod in (("agent-a", "agent-a"), ("agent-b", "agent-b"), ("rogue-pod", "rogue"),
                          ("someone", "agent-a")):
             self.users[tok]["extra"][ident.POD_UID_EXTRA] = [uids[pod]]
-        self.mgr = Manager.remote(RestConfig(host=self.srv.url, token="admin"), name="signer",
-                                  uncached=(kinds.POD,))
-        self.ca, key = await ident.ensure_ca(self.mgr.client, NS, "agent-ca", "agent-ca-bundle")
-        self.signer = ident.NodeAgentSigner(self.mgr.client, ident.SignerPolicy(namespace=NS), self.ca, key)
-        self.signer.setup_with_manager(self.mgr)
-        await self.mgr.start()
+        self.mgr = None
+        if self.with_signer:
+            self.mgr = Manager.remote(RestConfig(host=self.srv.url, token="admin"), name="signer",
+                                      uncached=(kinds.POD,))
+            self.ca, key = await ident.ensure_ca(self.mgr.client, NS, "agent-ca", "agent-ca-bundle")
+            self.signer = ident.NodeAgentSigner(self.mgr.client, ident.SignerPolicy(namespace=NS), self.ca, key)
+            self.signer.setup_with_manager(self.mgr)
+            await self.mgr.start()
         return self
 
     async def __aexit__(self, *exc):
-        await self.mgr.stop()
+        if self.mgr is not None:
+            await self.mgr.stop()
         await self.admin.close()
         await self.srv.stop()
 
@@ -89,8 +95,8 @@ def _enroller(cl, token, node, ip, cert_dir):
     return client, ident.Enroller(client, str(cert_dir), node, ip, poll_s=0.02)
 
 
-async def _with_cluster(body):
-    async with _Cluster() as cl:
+async def _with_cluster(body, signer: bool = True):
+    async with _Cluster(signer) as cl:
         return await body(cl)
 
 
@@ -204,3 +210,43 @@ def test_node_b_certificate_answering_for_node_a_is_refused(run, tmp_path):
             for client in clients:
                 await client.close()
     run(_with_cluster(body))
+
+
+def test_signer_and_enroll_commands(run, tmp_path, monkeypatch):
+    """``cmd/node_agent_signer`` (CA created on start, only its signer's CSRs watched) and
+    ``cmd/node_agent_enroll --once`` (the DaemonSet's init container) against the stand-in."""
+    from odh_kubeflow_amd.cmd import node_agent_enroll, node_agent_signer
+
+    async def body(cl):
+        monkeypatch.setenv("KUBE_TOKEN", "admin")
+        mgr = node_agent_signer.build(node_agent_signer.parse([
+            "--master", cl.srv.url, "--namespace", NS, "--ca-secret", "cmd-ca", "--ca-configmap", "cmd-ca",
+            "--metrics-bind-address", "0", "--health-probe-bind-address", "0"]))
+        await mgr.start()
+        try:
+            # a CSR of another signer (a kubelet's) is not this signer's business
+            _k, other = ident.new_key_and_csr("gpu-a", "10.0.0.1")
+            await cl.admin.create({"apiVersion": "certificates.k8s.io/v1", "kind": "CertificateSigningRequest",
+                                   "metadata": {"name": "kubelet-serving"},
+                                   "spec": {"request": ident._b64(other), "usages": ["server auth"],
+                                            "signerName": "kubernetes.io/kubelet-serving"}})
+            monkeypatch.setenv("KUBE_TOKEN", "agent-b")
+            rc = await node_agent_enroll.amain(["--master", cl.srv.url, "--node-name", "gpu-b", "--host-ip",
+                                                "10.0.0.2", "--cert-dir", str(tmp_path / "b"), "--once",
+                                                "--timeout-seconds", "20"])
+            assert rc == 0 and mgr.signer.issued == 1
+            with open(tmp_path / "b" / "tls.crt") as f:
+                crt = f.read()
+            assert cert_sans(crt) == {"gpu-b.mi355x-node-agent.nodes", "10.0.0.2"}
+            cm = await cl.admin.get(kinds.CONFIG_MAP, "cmd-ca", NS)
+            assert cert_signed_by(crt, cm["data"]["ca.crt"])
+            kubelet = await cl.admin.get(kinds.CSR, "kubelet-serving")
+            assert not (kubelet.get("status") or {}).get("conditions")
+            # denied: --once exits non-zero and leaves no certificate
+            rc = await node_agent_enroll.amain(["--master", cl.srv.url, "--node-name", "gpu-a", "--host-ip",
+                                                "10.0.0.1", "--cert-dir", str(tmp_path / "x"), "--once",
+                                                "--timeout-seconds", "20"])
+            assert rc == 1 and not os.path.exists(tmp_path / "x" / "tls.crt")
+        finally:
+            await mgr.stop()
+    run(_with_cluster(body, signer=False))

@@ -234,9 +234,15 @@ def test_update_rolls_statefulset(harness, notebooks, opts):
     nb = notebooks[0]
 
     async def update():
-        cur = await harness.client.get(kinds.NOTEBOOK, m.name(nb), m.namespace(nb))
-        cur["spec"]["template"]["spec"]["containers"][0]["image"] = opts.updated_image
-        await harness.client.update(cur)
+        # the controllers keep writing the Notebook (status, culler annotations): a stale
+        # resourceVersion is retried on the latest, as kubectl / client-go RetryOnConflict do
+        from odh_kubeflow_amd.runtime.retry import retry_on_conflict
+
+        async def once():
+            cur = await harness.client.get(kinds.NOTEBOOK, m.name(nb), m.namespace(nb))
+            cur["spec"]["template"]["spec"]["containers"][0]["image"] = opts.updated_image
+            await harness.client.update(cur)
+        await retry_on_conflict(once)
     harness.run(update())
     _sts_ready(harness, nb, image=opts.updated_image)
 

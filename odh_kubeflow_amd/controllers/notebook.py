@@ -51,7 +51,7 @@ from ..models.notebook import (ANNOTATION_HEADERS_REQUEST_SET, ANNOTATION_NOTEBO
                                PREFIX_ENV_VAR, STATEFULSET_LABEL, STOP_ANNOTATION, WORKBENCH_LABEL, gpu_request,
                                heartbeat_filter_enabled, pod_cond_to_notebook_cond)
 from ..runtime.controller import Request, Result, controller_owner_alive, fields_changed, maps_differ, pred_funcs
-from ..utils.objutil import deepcopy_json
+from ..utils.objutil import deepcopy_json, semantic_equal
 from ..utils.reconcilehelper import copy_service_fields, copy_statefulset_fields, copy_virtual_service
 
 log = logging.getLogger("controllers.Notebook")
@@ -373,6 +373,19 @@ def _cond_key(c: dict):
     return (c.get("type"), c.get("status"), c.get("reason"), c.get("message"))
 
 
+def status_equal(a: Optional[dict], b: Optional[dict]) -> bool:
+    """Two Notebook statuses say the same: absent, ``null``, ``0`` replicas, ``[]`` conditions
+    and ``{}`` containerState are one zero value (Go's ``NotebookStatus{}``).  A new Notebook's
+    first pass — StatefulSet created, no pod yet — computes exactly that zero value, and
+    writing it would be a status write (and an event in every Notebook watcher) that tells no
+    reader anything; the first write is the one that carries the pod's state."""
+    def norm(s):
+        s = dict(s or {})
+        s["readyReplicas"] = int(s.get("readyReplicas") or 0)
+        return s
+    return semantic_equal(norm(a), norm(b))
+
+
 def merge_status_timestamps(old: dict, new: dict) -> dict:
     """Keep the previous probe/transition stamps for conditions that did not change, so a
     pod condition without timestamps does not turn every reconcile into a status write."""
@@ -479,7 +492,7 @@ class NotebookReconciler:
             await self.client.update_status(nb)
         else:
             merge_status_timestamps(old_status, status)
-            if status != old_status:
+            if not status_equal(status, old_status):
                 # The whole status is recomputed from the pod each pass, so it is written as a
                 # JSON-patch replacement without a resourceVersion precondition: a concurrent
                 # metadata write (odh lock removal, culler annotations) cannot turn it into a

@@ -16,6 +16,8 @@ and issues an Update per reconcile against a real apiserver.
 
 from __future__ import annotations
 
+import json
+from collections import OrderedDict
 from typing import Callable, Optional
 
 from ..models import defaults
@@ -46,13 +48,34 @@ def _copy_meta(frm: dict, to: dict) -> bool:
     return require
 
 
+_DEFAULTED: "OrderedDict[str, dict]" = OrderedDict()  # canonical JSON of a desired pod spec -> defaulted
+_DEFAULTED_MAX = 1024
+
+
+def _defaulted(spec: dict) -> dict:
+    """``defaults.pod_spec`` of a desired spec, remembered by content: a notebook's desired spec
+    is regenerated identical on every reconcile of one generation."""
+    key = json.dumps(spec, sort_keys=True, separators=(",", ":"))
+    hit = _DEFAULTED.get(key)
+    if hit is None:
+        hit = _DEFAULTED[key] = defaults.pod_spec(deepcopy_json(spec))
+        if len(_DEFAULTED) > _DEFAULTED_MAX:
+            _DEFAULTED.popitem(last=False)
+    else:
+        _DEFAULTED.move_to_end(key)
+    return hit
+
+
 def pod_specs_equal(desired: Optional[dict], live: Optional[dict]) -> bool:
-    """Semantic pod-spec equality: both sides defaulted as kube-apiserver would."""
+    """Semantic pod-spec equality: both sides defaulted as kube-apiserver would.  The live side
+    normally already is (the apiserver defaulted it on write), so it is defaulted here only
+    when the defaulted desired spec does not equal it as it is."""
     if desired == live:
         return True
     if desired is None or live is None:
         return False
-    return defaults.pod_spec(deepcopy_json(desired)) == defaults.pod_spec(deepcopy_json(live))
+    d = _defaulted(desired)
+    return d == live or d == defaults.pod_spec(deepcopy_json(live))
 
 
 def _copy_pod_template_spec(frm: dict, to: dict) -> bool:

@@ -13,8 +13,27 @@
 //                          maps/slices as equal, and omitempty drops them on the wire)
 //   equal_except(a, b, keys)  equality of two objects ignoring the listed top-level
 //                          metadata keys (the apiserver's no-op write detection)
+//   loads_shared(data, old)   JSON -> dict/list tree (json.loads semantics) that reuses the
+//                          subtrees of ``old`` the new document leaves unchanged
+//   loads_event(line, lookup) one watch event line -> (type, object), the object decoded
+//                          against lookup(namespace, name) — the informer's cached version
+//
+// Why share: a watch MODIFIED event carries the whole object again, while a status write
+// changes a handful of fields.  Decoding against the cached version allocates only the
+// changed subtrees (the rest is the cached objects, reference-counted), and the controllers'
+// old-vs-new predicates over unchanged subtrees become identity comparisons.  Cached objects
+// are never mutated in place (readers get deep copies), which is what makes sharing safe.
 #define PY_SSIZE_T_CLEAN
 #include <Python.h>
+
+#include <cerrno>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <string_view>
+#include <unordered_map>
+#include <utility>
+#include <vector>
 
 namespace {
 
@@ -204,11 +223,656 @@ PyObject* py_equal_except(PyObject*, PyObject* args) {
   Py_RETURN_TRUE;
 }
 
+
+// ------------------------------------------------------------------ shared-subtree JSON decoder
+
+struct Parser {
+  const char* p;
+  const char* end;
+  std::string buf;  // scratch for unescaped strings and number text
+};
+
+// interned object keys: the small vocabulary of Kubernetes field names, decoded once; the
+// map's string_views point into the (ASCII, immortal-while-cached) key objects themselves
+std::unordered_map<std::string_view, PyObject*>* g_keys = nullptr;
+constexpr size_t kMaxKeys = 1 << 15;
+
+inline void ws(Parser& ps) {
+  while (ps.p < ps.end && (*ps.p == ' ' || *ps.p == '\n' || *ps.p == '\r' || *ps.p == '\t')) ++ps.p;
+}
+
+PyObject* fail(Parser&, const char* what) {
+  if (!PyErr_Occurred()) PyErr_Format(PyExc_ValueError, "invalid JSON: %s", what);
+  return nullptr;
+}
+
+void put_utf8(std::string& out, uint32_t cp) {
+  if (cp < 0x80) {
+    out.push_back(static_cast<char>(cp));
+  } else if (cp < 0x800) {
+    out.push_back(static_cast<char>(0xC0 | (cp >> 6)));
+    out.push_back(static_cast<char>(0x80 | (cp & 0x3F)));
+  } else if (cp < 0x10000) {  // lone surrogates too (decoded with surrogatepass, as json does)
+    out.push_back(static_cast<char>(0xE0 | (cp >> 12)));
+    out.push_back(static_cast<char>(0x80 | ((cp >> 6) & 0x3F)));
+    out.push_back(static_cast<char>(0x80 | (cp & 0x3F)));
+  } else {
+    out.push_back(static_cast<char>(0xF0 | (cp >> 18)));
+    out.push_back(static_cast<char>(0x80 | ((cp >> 12) & 0x3F)));
+    out.push_back(static_cast<char>(0x80 | ((cp >> 6) & 0x3F)));
+    out.push_back(static_cast<char>(0x80 | (cp & 0x3F)));
+  }
+}
+
+int hex4(const char* s, uint32_t* out) {
+  uint32_t v = 0;
+  for (int i = 0; i < 4; ++i) {
+    char c = s[i];
+    v <<= 4;
+    if (c >= '0' && c <= '9') v |= c - '0';
+    else if (c >= 'a' && c <= 'f') v |= c - 'a' + 10;
+    else if (c >= 'A' && c <= 'F') v |= c - 'A' + 10;
+    else return -1;
+  }
+  *out = v;
+  return 0;
+}
+
+// The string at ps.p (just past the opening quote) as UTF-8: a view into the input when it
+// has no escapes, else unescaped into ps.buf.  *ascii: every byte < 0x80.
+bool scan_string(Parser& ps, const char** s, Py_ssize_t* n, bool* ascii) {
+  const char* start = ps.p;
+  bool hi = false;
+  while (ps.p < ps.end) {
+    unsigned char c = static_cast<unsigned char>(*ps.p);
+    if (c == '"') {
+      *s = start;
+      *n = ps.p - start;
+      *ascii = !hi;
+      ++ps.p;
+      return true;
+    }
+    if (c == '\\') break;
+    if (c >= 0x80) hi = true;
+    ++ps.p;
+  }
+  if (ps.p >= ps.end) {
+    PyErr_SetString(PyExc_ValueError, "invalid JSON: unterminated string");
+    return false;
+  }
+  ps.buf.assign(start, ps.p - start);
+  while (ps.p < ps.end) {
+    unsigned char c = static_cast<unsigned char>(*ps.p);
+    if (c == '"') {
+      ++ps.p;
+      *s = ps.buf.data();
+      *n = static_cast<Py_ssize_t>(ps.buf.size());
+      *ascii = !hi;
+      return true;
+    }
+    if (c != '\\') {
+      if (c >= 0x80) hi = true;
+      ps.buf.push_back(static_cast<char>(c));
+      ++ps.p;
+      continue;
+    }
+    if (ps.p + 1 >= ps.end) break;
+    char e = ps.p[1];
+    ps.p += 2;
+    switch (e) {
+      case '"': ps.buf.push_back('"'); break;
+      case '\\': ps.buf.push_back('\\'); break;
+      case '/': ps.buf.push_back('/'); break;
+      case 'b': ps.buf.push_back('\b'); break;
+      case 'f': ps.buf.push_back('\f'); break;
+      case 'n': ps.buf.push_back('\n'); break;
+      case 'r': ps.buf.push_back('\r'); break;
+      case 't': ps.buf.push_back('\t'); break;
+      case 'u': {
+        uint32_t cp;
+        if (ps.end - ps.p < 4 || hex4(ps.p, &cp) < 0) {
+          PyErr_SetString(PyExc_ValueError, "invalid JSON: bad \\u escape");
+          return false;
+        }
+        ps.p += 4;
+        if (cp >= 0xD800 && cp < 0xDC00 && ps.end - ps.p >= 6 && ps.p[0] == '\\' && ps.p[1] == 'u') {
+          uint32_t lo;
+          if (hex4(ps.p + 2, &lo) == 0 && lo >= 0xDC00 && lo < 0xE000) {
+            cp = 0x10000 + ((cp - 0xD800) << 10) + (lo - 0xDC00);
+            ps.p += 6;
+          }
+        }
+        if (cp >= 0x80) hi = true;
+        put_utf8(ps.buf, cp);
+        break;
+      }
+      default:
+        PyErr_SetString(PyExc_ValueError, "invalid JSON: bad escape");
+        return false;
+    }
+  }
+  PyErr_SetString(PyExc_ValueError, "invalid JSON: unterminated string");
+  return false;
+}
+
+PyObject* make_str(const char* s, Py_ssize_t n, bool ascii) {
+  if (ascii) {
+    PyObject* u = PyUnicode_New(n, 127);
+    if (!u) return nullptr;
+    std::memcpy(PyUnicode_DATA(u), s, static_cast<size_t>(n));
+    return u;
+  }
+  return PyUnicode_DecodeUTF8(s, n, "surrogatepass");
+}
+
+// ``old`` in place of the new scalar ``v`` when they are equal (the cases the fast paths do not
+// decide: integers beyond 64 bits, strings whose UTF-8 form cannot be compared directly)
+PyObject* same_or(PyObject* v, PyObject* old) {
+  if (old && Py_TYPE(old) == Py_TYPE(v)) {
+    int eq = PyObject_RichCompareBool(v, old, Py_EQ);
+    if (eq < 0) {
+      PyErr_Clear();
+    } else if (eq) {
+      Py_DECREF(v);
+      Py_INCREF(old);
+      return old;
+    }
+  }
+  return v;
+}
+
+// ``old`` when it is the same string, else a new one
+PyObject* string_value(const char* s, Py_ssize_t n, bool ascii, PyObject* old) {
+  if (old && PyUnicode_CheckExact(old)) {
+    if (ascii && PyUnicode_IS_ASCII(old)) {
+      if (PyUnicode_GET_LENGTH(old) == n && std::memcmp(PyUnicode_DATA(old), s, static_cast<size_t>(n)) == 0) {
+        Py_INCREF(old);
+        return old;
+      }
+    } else if (!ascii && !PyUnicode_IS_ASCII(old)) {
+      Py_ssize_t on;
+      const char* os = PyUnicode_AsUTF8AndSize(old, &on);
+      if (!os) {
+        PyErr_Clear();
+      } else if (on == n && std::memcmp(os, s, static_cast<size_t>(n)) == 0) {
+        Py_INCREF(old);
+        return old;
+      }
+    }
+  }
+  PyObject* u = make_str(s, n, ascii);
+  return u ? same_or(u, old) : nullptr;
+}
+
+PyObject* key_object(const char* s, Py_ssize_t n, bool ascii) {
+  if (!ascii) return make_str(s, n, false);
+  auto it = g_keys->find(std::string_view(s, static_cast<size_t>(n)));
+  if (it != g_keys->end()) {
+    Py_INCREF(it->second);
+    return it->second;
+  }
+  PyObject* u = make_str(s, n, true);
+  if (!u) return nullptr;
+  PyUnicode_InternInPlace(&u);
+  if (g_keys->size() < kMaxKeys && PyUnicode_IS_ASCII(u)) {
+    Py_INCREF(u);  // held for the process: the view below points into it
+    g_keys->emplace(std::string_view(static_cast<const char*>(PyUnicode_DATA(u)), static_cast<size_t>(n)), u);
+  }
+  return u;
+}
+
+PyObject* number_value(Parser& ps, PyObject* old) {
+  const char* start = ps.p;
+  bool is_float = false;
+  if (ps.p < ps.end && *ps.p == '-') ++ps.p;
+  while (ps.p < ps.end) {
+    char c = *ps.p;
+    if (c >= '0' && c <= '9') {
+      ++ps.p;
+    } else if (c == '.' || c == 'e' || c == 'E' || c == '+' || c == '-') {
+      is_float = true;
+      ++ps.p;
+    } else {
+      break;
+    }
+  }
+  if (ps.p == start || (ps.p - start == 1 && *start == '-')) return fail(ps, "bad number");
+  ps.buf.assign(start, ps.p - start);
+  if (!is_float) {
+    errno = 0;
+    char* e = nullptr;
+    long long v = std::strtoll(ps.buf.c_str(), &e, 10);
+    if (errno == 0 && e && *e == '\0') {
+      if (old && PyLong_CheckExact(old)) {
+        int overflow = 0;
+        long long ov = PyLong_AsLongLongAndOverflow(old, &overflow);
+        if (!overflow && ov == v && !PyErr_Occurred()) {
+          Py_INCREF(old);
+          return old;
+        }
+        PyErr_Clear();
+      }
+      return PyLong_FromLongLong(v);
+    }
+    PyObject* big = PyLong_FromString(ps.buf.c_str(), nullptr, 10);  // beyond 64 bits
+    return big ? same_or(big, old) : nullptr;
+  }
+  char* e = nullptr;
+  double d = std::strtod(ps.buf.c_str(), &e);
+  if (!e || *e != '\0') return fail(ps, "bad number");
+  if (old && PyFloat_CheckExact(old) && PyFloat_AS_DOUBLE(old) == d) {
+    Py_INCREF(old);
+    return old;
+  }
+  return PyFloat_FromDouble(d);
+}
+
+PyObject* value(Parser& ps, PyObject* old, int depth);
+
+struct Members {  // owned (key, value) references, released unless handed to a dict
+  std::vector<std::pair<PyObject*, PyObject*>> kv;
+  ~Members() {
+    for (auto& x : kv) {
+      Py_XDECREF(x.first);
+      Py_XDECREF(x.second);
+    }
+  }
+};
+
+PyObject* object_value(Parser& ps, PyObject* old, int depth) {
+  // ps.p just past '{'.  With an old dict the members are collected first: an unchanged
+  // object is the old one, and no dict is built for it.
+  PyObject* od = (old && PyDict_CheckExact(old)) ? old : nullptr;
+  Members m;
+  bool same = od != nullptr;
+  ws(ps);
+  if (ps.p < ps.end && *ps.p == '}') {
+    ++ps.p;
+  } else {
+    while (true) {
+      ws(ps);
+      if (ps.p >= ps.end || *ps.p != '"') return fail(ps, "expected a key");
+      ++ps.p;
+      const char* ks;
+      Py_ssize_t kn;
+      bool kascii;
+      if (!scan_string(ps, &ks, &kn, &kascii)) return nullptr;
+      PyObject* key = key_object(ks, kn, kascii);
+      if (!key) return nullptr;
+      m.kv.emplace_back(key, nullptr);
+      ws(ps);
+      if (ps.p >= ps.end || *ps.p != ':') return fail(ps, "expected ':'");
+      ++ps.p;
+      PyObject* ov = od ? PyDict_GetItemWithError(od, key) : nullptr;
+      if (!ov && PyErr_Occurred()) PyErr_Clear();
+      PyObject* v = value(ps, ov, depth + 1);
+      if (!v) return nullptr;
+      m.kv.back().second = v;
+      if (v != ov) same = false;
+      ws(ps);
+      if (ps.p < ps.end && *ps.p == ',') {
+        ++ps.p;
+        continue;
+      }
+      if (ps.p < ps.end && *ps.p == '}') {
+        ++ps.p;
+        break;
+      }
+      return fail(ps, "expected ',' or '}'");
+    }
+  }
+  // every member is the old one's and there are as many (a duplicate key cannot make up for
+  // a missing one: its value would have to be the old value of two different keys)
+  if (same && depth > 0 && static_cast<Py_ssize_t>(m.kv.size()) == PyDict_GET_SIZE(od)) {
+    Py_INCREF(od);
+    return od;
+  }
+  PyObject* out = _PyDict_NewPresized(static_cast<Py_ssize_t>(m.kv.size()));
+  if (!out) return nullptr;
+  for (auto& x : m.kv) {
+    if (PyDict_SetItem(out, x.first, x.second) < 0) {
+      Py_DECREF(out);
+      return nullptr;
+    }
+  }
+  return out;
+}
+
+PyObject* array_value(Parser& ps, PyObject* old, int depth) {
+  PyObject* ol = (old && PyList_CheckExact(old)) ? old : nullptr;
+  std::vector<PyObject*> items;
+  struct Release {
+    std::vector<PyObject*>& v;
+    ~Release() {
+      for (PyObject* o : v) Py_XDECREF(o);
+    }
+  } release{items};
+  bool same = ol != nullptr;
+  ws(ps);
+  if (ps.p < ps.end && *ps.p == ']') {
+    ++ps.p;
+  } else {
+    while (true) {
+      Py_ssize_t i = static_cast<Py_ssize_t>(items.size());
+      PyObject* ov = (ol && i < PyList_GET_SIZE(ol)) ? PyList_GET_ITEM(ol, i) : nullptr;
+      PyObject* v = value(ps, ov, depth + 1);
+      if (!v) return nullptr;
+      items.push_back(v);
+      if (v != ov) same = false;
+      ws(ps);
+      if (ps.p < ps.end && *ps.p == ',') {
+        ++ps.p;
+        continue;
+      }
+      if (ps.p < ps.end && *ps.p == ']') {
+        ++ps.p;
+        break;
+      }
+      return fail(ps, "expected ',' or ']'");
+    }
+  }
+  if (same && depth > 0 && static_cast<Py_ssize_t>(items.size()) == PyList_GET_SIZE(ol)) {
+    Py_INCREF(ol);
+    return ol;
+  }
+  PyObject* out = PyList_New(static_cast<Py_ssize_t>(items.size()));
+  if (!out) return nullptr;
+  for (size_t i = 0; i < items.size(); ++i) {
+    PyList_SET_ITEM(out, static_cast<Py_ssize_t>(i), items[i]);  // the reference moves
+    items[i] = nullptr;
+  }
+  return out;
+}
+
+bool literal(Parser& ps, const char* word, size_t n) {
+  if (static_cast<size_t>(ps.end - ps.p) >= n && std::memcmp(ps.p, word, n) == 0) {
+    ps.p += n;
+    return true;
+  }
+  return false;
+}
+
+PyObject* value(Parser& ps, PyObject* old, int depth) {
+  if (depth > 512) {
+    PyErr_SetString(PyExc_RecursionError, "JSON too deep");
+    return nullptr;
+  }
+  ws(ps);
+  if (ps.p >= ps.end) return fail(ps, "unexpected end");
+  char c = *ps.p;
+  if (c == '{') {
+    ++ps.p;
+    return object_value(ps, old, depth);
+  }
+  if (c == '[') {
+    ++ps.p;
+    return array_value(ps, old, depth);
+  }
+  if (c == '"') {
+    ++ps.p;
+    const char* s;
+    Py_ssize_t n;
+    bool ascii;
+    if (!scan_string(ps, &s, &n, &ascii)) return nullptr;
+    return string_value(s, n, ascii, old);
+  }
+  if (c == '-' || (c >= '0' && c <= '9')) return number_value(ps, old);
+  if (literal(ps, "true", 4)) Py_RETURN_TRUE;
+  if (literal(ps, "false", 5)) Py_RETURN_FALSE;
+  if (literal(ps, "null", 4)) Py_RETURN_NONE;
+  return fail(ps, "unexpected character");
+}
+
+// skip one value without building it (the pre-scan for an event's metadata)
+bool skip_value(Parser& ps, int depth) {
+  if (depth > 512) return false;
+  ws(ps);
+  if (ps.p >= ps.end) return false;
+  char c = *ps.p;
+  if (c == '"') {
+    ++ps.p;
+    while (ps.p < ps.end && *ps.p != '"') ps.p += (*ps.p == '\\') ? 2 : 1;
+    if (ps.p >= ps.end) return false;
+    ++ps.p;
+    return true;
+  }
+  if (c == '{' || c == '[') {
+    char close = c == '{' ? '}' : ']';
+    ++ps.p;
+    ws(ps);
+    if (ps.p < ps.end && *ps.p == close) {
+      ++ps.p;
+      return true;
+    }
+    while (true) {
+      if (c == '{') {
+        if (!skip_value(ps, depth + 1)) return false;  // the key
+        ws(ps);
+        if (ps.p >= ps.end || *ps.p != ':') return false;
+        ++ps.p;
+      }
+      if (!skip_value(ps, depth + 1)) return false;
+      ws(ps);
+      if (ps.p < ps.end && *ps.p == ',') {
+        ++ps.p;
+        continue;
+      }
+      if (ps.p < ps.end && *ps.p == close) {
+        ++ps.p;
+        return true;
+      }
+      return false;
+    }
+  }
+  while (ps.p < ps.end && *ps.p != ',' && *ps.p != '}' && *ps.p != ']' && *ps.p != ' ' && *ps.p != '\n') ++ps.p;
+  return true;
+}
+
+// metadata.namespace / metadata.name of the object at ps.p (ps is a copy: not advanced)
+void peek_key(Parser ps, std::string* ns, std::string* name) {
+  ws(ps);
+  if (ps.p >= ps.end || *ps.p != '{') return;
+  ++ps.p;
+  while (true) {
+    ws(ps);
+    if (ps.p >= ps.end || *ps.p != '"') return;
+    ++ps.p;
+    const char* ks;
+    Py_ssize_t kn;
+    bool ascii;
+    if (!scan_string(ps, &ks, &kn, &ascii)) {
+      PyErr_Clear();
+      return;
+    }
+    bool is_meta = kn == 8 && std::memcmp(ks, "metadata", 8) == 0;
+    ws(ps);
+    if (ps.p >= ps.end || *ps.p != ':') return;
+    ++ps.p;
+    ws(ps);
+    if (is_meta) {
+      if (ps.p >= ps.end || *ps.p != '{') return;
+      ++ps.p;
+      while (true) {
+        ws(ps);
+        if (ps.p >= ps.end || *ps.p != '"') return;
+        ++ps.p;
+        if (!scan_string(ps, &ks, &kn, &ascii)) {
+          PyErr_Clear();
+          return;
+        }
+        std::string* dst = (kn == 4 && std::memcmp(ks, "name", 4) == 0)        ? name
+                           : (kn == 9 && std::memcmp(ks, "namespace", 9) == 0) ? ns
+                                                                                : nullptr;
+        ws(ps);
+        if (ps.p >= ps.end || *ps.p != ':') return;
+        ++ps.p;
+        ws(ps);
+        if (dst && ps.p < ps.end && *ps.p == '"') {
+          ++ps.p;
+          const char* vs;
+          Py_ssize_t vn;
+          if (!scan_string(ps, &vs, &vn, &ascii)) {
+            PyErr_Clear();
+            return;
+          }
+          dst->assign(vs, static_cast<size_t>(vn));
+        } else if (!skip_value(ps, 2)) {
+          return;
+        }
+        ws(ps);
+        if (ps.p < ps.end && *ps.p == ',') {
+          ++ps.p;
+          continue;
+        }
+        return;  // end of metadata
+      }
+    }
+    if (!skip_value(ps, 1)) return;
+    ws(ps);
+    if (ps.p < ps.end && *ps.p == ',') {
+      ++ps.p;
+      continue;
+    }
+    return;
+  }
+}
+
+bool init_parser(PyObject* data, Parser* ps) {
+  char* buf;
+  Py_ssize_t n;
+  if (PyBytes_Check(data)) {
+    if (PyBytes_AsStringAndSize(data, &buf, &n) < 0) return false;
+  } else if (PyByteArray_Check(data)) {
+    buf = PyByteArray_AS_STRING(data);
+    n = PyByteArray_GET_SIZE(data);
+  } else if (PyUnicode_Check(data)) {
+    const char* s = PyUnicode_AsUTF8AndSize(data, &n);
+    if (!s) return false;
+    buf = const_cast<char*>(s);
+  } else {
+    PyErr_SetString(PyExc_TypeError, "expected bytes or str");
+    return false;
+  }
+  ps->p = buf;
+  ps->end = buf + n;
+  return true;
+}
+
+PyObject* py_loads_shared(PyObject*, PyObject* args) {
+  PyObject *data, *old = Py_None;
+  if (!PyArg_ParseTuple(args, "O|O", &data, &old)) return nullptr;
+  Parser ps;
+  if (!init_parser(data, &ps)) return nullptr;
+  PyObject* out = value(ps, old == Py_None ? nullptr : old, 0);
+  if (!out) return nullptr;
+  ws(ps);
+  if (ps.p != ps.end) {
+    Py_DECREF(out);
+    return fail(ps, "extra data");
+  }
+  return out;
+}
+
+// loads_event(line, lookup) -> (type, object): lookup(namespace, name) gives the cached
+// version of the event's object (or None) to share unchanged subtrees with
+PyObject* py_loads_event(PyObject*, PyObject* args) {
+  PyObject *data, *lookup = Py_None;
+  if (!PyArg_ParseTuple(args, "O|O", &data, &lookup)) return nullptr;
+  Parser ps;
+  if (!init_parser(data, &ps)) return nullptr;
+  ws(ps);
+  if (ps.p >= ps.end || *ps.p != '{') return fail(ps, "an event is an object");
+  ++ps.p;
+  PyObject* type = nullptr;
+  PyObject* obj = nullptr;
+  PyObject* ret = nullptr;
+  ws(ps);
+  if (ps.p < ps.end && *ps.p == '}') {
+    ++ps.p;
+  } else {
+    while (true) {
+      ws(ps);
+      if (ps.p >= ps.end || *ps.p != '"') {
+        fail(ps, "expected a key");
+        goto done;
+      }
+      ++ps.p;
+      const char* ks;
+      Py_ssize_t kn;
+      bool ascii;
+      if (!scan_string(ps, &ks, &kn, &ascii)) goto done;
+      bool is_type = kn == 4 && std::memcmp(ks, "type", 4) == 0;
+      bool is_obj = kn == 6 && std::memcmp(ks, "object", 6) == 0;
+      ws(ps);
+      if (ps.p >= ps.end || *ps.p != ':') {
+        fail(ps, "expected ':'");
+        goto done;
+      }
+      ++ps.p;
+      if (is_obj) {
+        PyObject* old = nullptr;
+        if (lookup != Py_None) {
+          std::string ns, name;
+          peek_key(ps, &ns, &name);
+          if (!name.empty()) {
+            PyObject* r = PyObject_CallFunction(lookup, "s#s#", ns.data(), static_cast<Py_ssize_t>(ns.size()),
+                                                name.data(), static_cast<Py_ssize_t>(name.size()));
+            if (!r) goto done;
+            if (r != Py_None) old = r;
+            else Py_DECREF(r);
+          }
+        }
+        Py_XDECREF(obj);
+        obj = value(ps, old, 0);
+        Py_XDECREF(old);
+        if (!obj) goto done;
+      } else {
+        PyObject* v = value(ps, nullptr, 1);
+        if (!v) goto done;
+        if (is_type) {
+          Py_XDECREF(type);
+          type = v;
+        } else {
+          Py_DECREF(v);
+        }
+      }
+      ws(ps);
+      if (ps.p < ps.end && *ps.p == ',') {
+        ++ps.p;
+        continue;
+      }
+      if (ps.p < ps.end && *ps.p == '}') {
+        ++ps.p;
+        break;
+      }
+      fail(ps, "expected ',' or '}'");
+      goto done;
+    }
+  }
+  ws(ps);
+  if (ps.p != ps.end) {
+    fail(ps, "extra data");
+    goto done;
+  }
+  if (!obj) obj = PyDict_New();
+  if (!obj) goto done;
+  ret = PyTuple_Pack(2, type ? type : Py_None, obj);
+done:
+  Py_XDECREF(type);
+  Py_XDECREF(obj);
+  return ret;
+}
+
 PyMethodDef methods[] = {
     {"deepcopy", py_deepcopy, METH_O, "Deep copy of a JSON tree (dict/list; tuples become lists)."},
     {"semantic_equal", py_semantic_equal, METH_VARARGS,
      "Structural equality treating missing/None/{}/[] map values as equal."},
     {"equal_except", py_equal_except, METH_VARARGS, "a == b ignoring the given metadata keys."},
+    {"loads_shared", py_loads_shared, METH_VARARGS,
+     "loads_shared(data, old=None): json.loads, reusing the subtrees of old the document leaves unchanged."},
+    {"loads_event", py_loads_event, METH_VARARGS,
+     "loads_event(line, lookup=None) -> (type, object): a watch event, the object decoded against "
+     "lookup(namespace, name)."},
     {nullptr, nullptr, 0, nullptr}};
 
 PyModuleDef module = {PyModuleDef_HEAD_INIT, "_objcore", "Native JSON-tree core", -1, methods,
@@ -216,4 +880,7 @@ PyModuleDef module = {PyModuleDef_HEAD_INIT, "_objcore", "Native JSON-tree core"
 
 }  // namespace
 
-PyMODINIT_FUNC PyInit__objcore(void) { return PyModule_Create(&module); }
+PyMODINIT_FUNC PyInit__objcore(void) {
+  if (!g_keys) g_keys = new std::unordered_map<std::string_view, PyObject*>();
+  return PyModule_Create(&module);
+}

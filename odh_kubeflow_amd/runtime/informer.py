@@ -237,6 +237,9 @@ class _Informer:
         if self._rv_waiters:
             self._rv_reached()
 
+    def _stored(self, namespace: str, name: str) -> Optional[dict]:
+        return self.items.get((namespace if self.info.namespaced else "", name))
+
     def _apply(self, et: str, obj: dict) -> None:
         """One watch event into the store, then to the subscribers."""
         self.rv = m.resource_version(obj) or self.rv
@@ -271,10 +274,14 @@ class _Informer:
                 started = time.monotonic()
                 rest = self.cache.rest
                 batches = getattr(rest, "watch_batches", None)
+                kw = {}
                 if batches is None:  # a client without batched watches (test doubles)
                     batches = _one_event_batches(rest.watch)
+                else:  # decoded against the stored object: unchanged subtrees are shared
+                    kw["lookup"] = self._stored
                 async for batch in batches(ref, self.namespace, self.rv, labels=self.label_selector,
-                                           fields=self.field_selector, timeout_s=self.cache.watch_timeout_s):
+                                           fields=self.field_selector, timeout_s=self.cache.watch_timeout_s,
+                                           **kw):
                     backoff = 0.05
                     for et, obj in batch:
                         self._apply(et, obj)

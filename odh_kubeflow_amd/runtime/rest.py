@@ -25,6 +25,19 @@ import time
 from dataclasses import dataclass, field
 from typing import Any, AsyncIterator, Dict, List, Optional, Tuple
 
+try:  # native JSON decoding (native/objcore.cpp): ~1.7x json.loads, shared subtrees for watches
+    from ..native._objcore import loads_event as _loads_event
+    from ..native._objcore import loads_shared as _loads_shared
+
+    def _loads(raw):
+        try:
+            return _loads_shared(raw)
+        except ValueError:
+            return json.loads(raw)  # json's own verdict (and its NaN / Infinity literals)
+except ImportError:  # pragma: no cover - the extension is not built
+    _loads_event = None
+    _loads = json.loads
+
 from ..models.errors import ApiError, Gone, InternalError
 from ..models.scheme import SCHEME, ResourceInfo
 from ..utils.selectors import format_label_selector
@@ -226,7 +239,7 @@ class RestClient(Client):
         if raw:
             self.bytes_in[count_as] = self.bytes_in.get(count_as, 0) + len(raw)
         try:
-            out = json.loads(raw) if raw else {}
+            out = _loads(raw) if raw else {}
         except ValueError:
             out = {"message": raw[:200].decode(errors="replace")}
         if status >= 400:
@@ -353,11 +366,15 @@ class RestClient(Client):
                 yield ev
 
     async def watch_batches(self, kind, namespace=None, resource_version: Optional[str] = None, labels=None,
-                            fields=None, timeout_s: int = 300,
-                            bookmarks: bool = True) -> AsyncIterator[List[Tuple[str, dict]]]:
+                            fields=None, timeout_s: int = 300, bookmarks: bool = True,
+                            lookup=None) -> AsyncIterator[List[Tuple[str, dict]]]:
         """Yield the ``(type, object)`` events of each arrival as one list (an informer applies
         them in one go); raises :class:`Gone` when the RV is too old — after yielding the
-        events that preceded the ERROR in its batch."""
+        events that preceded the ERROR in its batch.
+
+        ``lookup(namespace, name)``: the caller's current copy of an object (an informer's
+        store).  Events are decoded natively (``native/objcore.cpp`` ``loads_event``) against
+        it: the subtrees a change leaves alone are the stored ones, not new copies."""
         from urllib.parse import urlencode
 
         info, v = _info_and_version(kind)
@@ -382,6 +399,7 @@ class RestClient(Client):
             except ValueError:
                 raise InternalError(raw[:200].decode(errors="replace"))
         loads = json.loads
+        native = _loads_event
         try:
             async for lines in stream.batches():
                 out = []
@@ -389,8 +407,15 @@ class RestClient(Client):
                 for line in lines:
                     if not line or line.isspace():
                         continue
-                    ev = loads(line)
-                    et, obj = ev.get("type"), ev.get("object") or {}
+                    if native is not None:
+                        try:
+                            et, obj = native(line, lookup)
+                        except ValueError:  # beyond the native decoder (NaN literals): json's verdict
+                            ev = loads(line)
+                            et, obj = ev.get("type"), ev.get("object") or {}
+                    else:
+                        ev = loads(line)
+                        et, obj = ev.get("type"), ev.get("object") or {}
                     if et == "ERROR":
                         err = ApiError.from_status(obj)
                         break

@@ -73,6 +73,9 @@ def parse(argv=None):
     p.add_argument("--cache-configmaps", action="store_true",
                    help="unsharded: the odh manager caches ConfigMap/Secret data (--cache-configmaps-secrets=true) "
                         "instead of the reference's live, data-stripped reads")
+    p.add_argument("--kf-split-workers", action="store_true",
+                   help="unsharded with --workers: the kf manager's --split-workers (per namespace set a notebook "
+                        "reconciler process and a culler + event re-emitter process)")
     p.add_argument("--webhook-replicas", type=int, default=1,
                    help="unsharded with --workers: --webhook-replicas of the odh manager (webhook processes sharing "
                         "the port)")

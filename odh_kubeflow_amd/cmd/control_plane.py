@@ -109,7 +109,7 @@ def parse(argv: Optional[List[str]] = None) -> argparse.Namespace:
 
 
 def build(args, env=os.environ):
-    from ..controllers.setup import setup_kf, setup_odh, shard_cache_options
+    from ..controllers.setup import setup_kf, setup_odh, shard_cache_options, with_own_services
     from ..models import kinds
     from ..runtime.informer import strip_data
     from ..runtime.leaderelection import LeaderElector, namespace_from_env
@@ -140,14 +140,9 @@ def build(args, env=os.environ):
                                 renew_deadline=args.leader_election_renew_deadline,
                                 retry_period=args.leader_election_retry_period)
     name = "notebook-control-plane" + (f"-shard-{shard}" if shard is not None else "") + subset
-    cache_options = shard_cache_options(shard, namespace, args.cluster_wide_watches)
-    # a process running one of the two Notebook-owning reconcilers watches only its own
-    # Services: kf's <nb> (no labels, kf/controllers/notebook_controller.go:525-552) and odh's
-    # <nb>-kube-rbac-proxy (labelled notebook-name) — each would decode the other's otherwise
-    only = {"notebook": "!notebook-name", "odh": "notebook-name"}.get(
-        args.controller_set[0] if len(args.controller_set) == 1 else "")
-    if only:
-        cache_options["selectors"] = {**cache_options.get("selectors", {}), kinds.SERVICE: only}
+    # a process running one of the two Notebook-owning reconcilers watches only its own Services
+    cache_options = with_own_services(shard_cache_options(shard, namespace, args.cluster_wide_watches),
+                                      args.controller_set[0] if len(args.controller_set) == 1 else "")
     mgr = Manager.remote(cfg, name=name, uncached=uncached, transforms=transforms,
                          cache_options=cache_options,
                          default_max_concurrent=args.max_concurrent_reconciles, leader_elector=elector,

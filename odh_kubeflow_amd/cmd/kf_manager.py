@@ -5,7 +5,10 @@ Flags keep the reference names (``--metrics-addr``, ``--probe-addr``,
 ``--zap-devel``); additions: ``--kubeconfig`` / ``--master``,
 ``--max-concurrent-reconciles`` (default 8; the reference runs 1 worker), ``--workers W``
 (the controllers in W namespace-partitioned child processes of this one, which leads,
-aggregates their ``/metrics`` and restarts them: :mod:`~odh_kubeflow_amd.runtime.workers`).
+aggregates their ``/metrics`` and restarts them: :mod:`~odh_kubeflow_amd.runtime.workers`),
+``--split-workers`` (each of the W namespace sets served by two processes: the notebook
+reconciler, and the culler + event re-emitter — the shard pod's split, so a notebook's
+create → Ready reconciles never queue behind culling checks and Event re-emission).
 Culling is wired only when ``ENABLE_CULLING=true`` (:111-123).  Leader-election ID
 ``kubeflow-notebook-controller``.
 
@@ -45,27 +48,32 @@ def parse(argv: Optional[List[str]] = None) -> argparse.Namespace:
     add_shard_flags(p)
     add_debug_flags(p)
     add_worker_flags(p)
+    p.add_argument("--split-workers", action="store_true",
+                   help="with --workers: each namespace set served by a notebook-reconciler process and a "
+                        "culler + event re-emitter process")
+    p.add_argument("--worker-role", default="", choices=("", "notebook", "aux"), help=argparse.SUPPRESS)
     args = p.parse_args(argv)
     args.argv = list(sys.argv[1:] if argv is None else argv)
     return args
 
 
-WORKER_STRIP_VALUE = ("--workers", "--worker", "--metrics-addr", "--probe-addr", "--leader-election-namespace")
-WORKER_STRIP_BOOL = ("--enable-leader-election", "--enable-debug-endpoints")
+WORKER_STRIP_VALUE = ("--workers", "--worker", "--worker-role", "--metrics-addr", "--probe-addr",
+                      "--leader-election-namespace")
+WORKER_STRIP_BOOL = ("--enable-leader-election", "--enable-debug-endpoints", "--split-workers")
 
 
-def worker_argv(args, index: int, metrics_addr: str) -> List[str]:
+def worker_argv(args, index: int, metrics_addr: str, role: str = "") -> List[str]:
     """A worker's command line: the supervisor's, minus what the supervisor alone does
     (leader election, the public metrics and probe addresses)."""
     from ..runtime.workers import strip_flags
 
     base = strip_flags(args.argv, WORKER_STRIP_VALUE, WORKER_STRIP_BOOL)
     return [*base, "--worker", f"{index}/{args.workers}", "--metrics-addr", metrics_addr, "--probe-addr", "0",
-            "--enable-debug-endpoints"]
+            "--enable-debug-endpoints", *(["--worker-role", role] if role else [])]
 
 
 def build(args, env=os.environ):
-    from ..controllers.setup import setup_kf, shard_cache_options
+    from ..controllers.setup import setup_kf, shard_cache_options, with_own_services
     from ..runtime.leaderelection import LeaderElector, namespace_from_env
     from ..runtime.manager import Manager
     from ..runtime.rest import RestClient, RestConfig
@@ -92,6 +100,8 @@ def build(args, env=os.environ):
     assign = WorkerAssignments(*worker) if worker is not None else None
     if assign is not None:
         cache_options = assign.cache_options(cluster_watch=args.cluster_wide_watches)
+    if args.worker_role != "aux":  # the notebook reconciler reads its own Services only
+        cache_options = with_own_services(cache_options, "notebook")
     mgr = Manager.remote(cfg, name="notebook-controller", default_max_concurrent=args.max_concurrent_reconciles,
                          leader_elector=elector, metrics_addr=args.metrics_addr, probe_addr=args.probe_addr,
                          debug_endpoints=args.enable_debug_endpoints, cache_options=cache_options)
@@ -103,10 +113,20 @@ def build(args, env=os.environ):
     if args.workers > 1 and worker is None:
         # supervisor: the controllers run in the workers (runtime/workers.py)
         mgr.set_supervisor(WorkerSupervisor("odh_kubeflow_amd.cmd.kf_manager", args.workers,
-                                            lambda i, addr: worker_argv(args, i, addr), env=dict(env), cache=mgr.cache,
-                                            system_namespaces=[namespace_from_env()],
-                                            name="notebook-controller"))
+                                            lambda i, addr, role="": worker_argv(args, i, addr, role), env=dict(env),
+                                            cache=mgr.cache, system_namespaces=[namespace_from_env()],
+                                            name="notebook-controller",
+                                            roles=("notebook", "aux") if args.split_workers else ("",)))
         mgr.kf_reconcilers = {}
+    elif args.worker_role == "notebook":
+        mgr.kf_reconcilers = setup_kf(mgr, env, culling=False, event_reemit=False)
+    elif args.worker_role == "aux":
+        from ..controllers.setup import setup_culler, setup_event_reemitter
+
+        mgr.kf_reconcilers = {"events": setup_event_reemitter(mgr)}
+        culler = setup_culler(mgr, env)
+        if culler is not None:
+            mgr.kf_reconcilers["culler"] = culler
     else:
         mgr.kf_reconcilers = setup_kf(mgr, env)
     mgr.add_healthz_check("healthz")

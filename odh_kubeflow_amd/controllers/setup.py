@@ -104,6 +104,23 @@ def setup_odh(mgr, namespace: str, env: Mapping[str, str] = os.environ, *, shard
     return r
 
 
+# the Services each Notebook-owning reconciler reads: kf its <nb> Service (no labels,
+# kf/controllers/notebook_controller.go:525-552), odh its <nb>-kube-rbac-proxy (labelled
+# notebook-name, odh/controllers/notebook_kube_rbac_auth.go) — a process running one of them
+# watches only those, instead of decoding the other's too
+OWN_SERVICES = {"notebook": "!notebook-name", "odh": "notebook-name"}
+
+
+def with_own_services(cache_options: dict, role: str) -> dict:
+    """``cache_options`` with the Service label selector of ``role`` (``notebook`` / ``odh``)."""
+    from ..models import kinds
+
+    sel = OWN_SERVICES.get(role)
+    if not sel:
+        return cache_options
+    return {**cache_options, "selectors": {**(cache_options.get("selectors") or {}), kinds.SERVICE: sel}}
+
+
 def shard_cache_options(shard: Optional[str], controller_namespace: str, cluster_watch: bool = False) -> dict:
     """InformerCache keyword arguments for one shard: the namespaces labelled
     ``notebooks.amd.com/shard=<shard>`` (followed live) plus the controller namespace, with

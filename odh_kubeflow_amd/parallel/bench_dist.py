@@ -799,6 +799,7 @@ async def _main(args, dist, torch, rank: int, world: int, ndev: int, probe_sampl
         webhook=not args.no_odh, reference_emulation=args.reference_emulation, env=env, process=True,
         split=not getattr(args, "single_process_shard", False), workers=max(1, getattr(args, "workers", 1)),
         webhook_replicas=max(1, getattr(args, "webhook_replicas", 1)),
+        kf_split_workers=bool(getattr(args, "kf_split_workers", False)),
         webhook_process=not getattr(args, "webhook_in_odh", False),
         cache_configmaps=getattr(args, "cache_configmaps", False), driven_only=True,
         culler_process=culling and not getattr(args, "culler_in_kf", False),

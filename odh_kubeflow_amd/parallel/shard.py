@@ -89,6 +89,7 @@ class ShardConfig:
     leader_elect_args: List[str] = field(default_factory=list)
     cluster_watch: bool = False  # --cluster-wide-watches on every control-plane process
     workers: int = 1  # unsharded: --workers of the kf and odh managers (runtime/workers.py)
+    kf_split_workers: bool = False  # unsharded with workers: the kf manager's --split-workers
     webhook_replicas: int = 1  # unsharded with workers: --webhook-replicas of the odh manager
     cache_configmaps: bool = False  # unsharded: --cache-configmaps-secrets=true on the odh manager
     # the user namespaces this rank drives (default: just ``namespace``); with ``assign`` they
@@ -171,7 +172,9 @@ class ControlPlaneShard:
                 out.append((name, "odh_kubeflow_amd.cmd.control_plane", a, "--metrics-bind-address"))
             return out
         wk = ["--workers", str(cfg.workers)] if cfg.workers > 1 else []
-        out = [("kf_manager", "odh_kubeflow_amd.cmd.kf_manager", ["--probe-addr", "0", *wk], "--metrics-addr")]
+        kf_split = ["--split-workers"] if cfg.workers > 1 and cfg.kf_split_workers else []
+        out = [("kf_manager", "odh_kubeflow_amd.cmd.kf_manager", ["--probe-addr", "0", *wk, *kf_split],
+                "--metrics-addr")]
         if cfg.odh:
             rep = ["--webhook-replicas", str(cfg.webhook_replicas)] if cfg.workers > 1 and cfg.webhook_replicas > 1 \
                 else []

@@ -395,7 +395,7 @@ class Manager:
             idle = await self.quiesce(quiet, timeout)
             docs = (await sub[0]) if sub else []
             idle = idle and all(d.get("idle") for d in docs) and (
-                self.supervisor is None or len(docs) == self.supervisor.count)
+                self.supervisor is None or len(docs) == len(self.supervisor.workers))
             return web.json_response({"idle": idle,
                                       "reconciles": merge_counts([self.reconcile_breakdown(),
                                                                   *(d.get("reconciles") for d in docs)]),

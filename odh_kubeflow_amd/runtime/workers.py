@@ -248,8 +248,10 @@ def _fmt(v: float) -> str:
 
 
 class _Worker:
-    def __init__(self, index: int):
+    def __init__(self, index: int, role: str = ""):
         self.index = index
+        self.role = role  # "" or one of the supervisor's roles (all roles of an index share its namespaces)
+        self.label = str(index) if not role else f"{index}_{role}"
         self.proc: Optional[subprocess.Popen] = None
         self.base = ""
         self.restarts = 0
@@ -272,12 +274,17 @@ class WorkerSupervisor:
 
     ``argv_for(i, metrics_addr)`` returns the worker's command-line arguments for
     ``python -m module``.  A manager runnable: the owning :class:`Manager` adds it with
-    ``needs_leader=True``, so the workers run only while the supervisor leads."""
+    ``needs_leader=True``, so the workers run only while the supervisor leads.
 
-    def __init__(self, module: str, count: int, argv_for: Callable[[int, str], List[str]],
+    ``roles``: each of the ``count`` namespace slots is served by one process per role
+    (``argv_for(i, metrics_addr, role)``), all given the slot's namespaces — the kf manager
+    runs its notebook reconciler apart from its culler and event re-emitter this way
+    (``--split-workers``), as a shard pod does."""
+
+    def __init__(self, module: str, count: int, argv_for: Callable[..., List[str]],
                  env: Optional[Dict[str, str]] = None, name: str = "manager", start_timeout: float = 120.0,
                  restart_backoff: Tuple[float, float] = (0.5, 30.0), cache=None,
-                 system_namespaces: Iterable[str] = ()):
+                 system_namespaces: Iterable[str] = (), roles: Sequence[str] = ("",)):
         self.cache = cache  # the supervisor's InformerCache: its Namespace watch drives the assignments
         self.owner: Dict[str, int] = {}
         self.system_namespaces = set(system_namespaces)
@@ -290,7 +297,11 @@ class WorkerSupervisor:
         self.name = name
         self.start_timeout = start_timeout
         self.backoff0, self.backoff_max = restart_backoff
-        self.workers = [_Worker(i) for i in range(self.count)]
+        self.roles = tuple(roles) or ("",)
+        self.workers = [_Worker(i, r) for i in range(self.count) for r in self.roles]
+        self._slots: Dict[int, List[_Worker]] = {}
+        for w in self.workers:
+            self._slots.setdefault(w.index, []).append(w)
         self._monitor: Optional[asyncio.Task] = None
         self._http = None
         self._stopping = False
@@ -302,7 +313,8 @@ class WorkerSupervisor:
 
         port = _free_port()
         env = child_env({**self.env, "PYTHONPATH": ROOT + os.pathsep + self.env.get("PYTHONPATH", "")})
-        args = [sys.executable, "-m", self.module, *self.argv_for(w.index, f"127.0.0.1:{port}")]
+        extra = (w.role,) if w.role else ()
+        args = [sys.executable, "-m", self.module, *self.argv_for(w.index, f"127.0.0.1:{port}", *extra)]
         w.proc = subprocess.Popen(args, cwd=ROOT, env=env, stdin=subprocess.PIPE, stdout=subprocess.PIPE,
                                   stderr=None, text=True)
         w.base = f"http://127.0.0.1:{port}"
@@ -318,10 +330,10 @@ class WorkerSupervisor:
         if line.strip() != "ready":
             rc = w.proc.poll()
             w.proc.kill()
-            raise RuntimeError(f"{self.name} worker {w.index}/{self.count} did not start (rc={rc})")
+            raise RuntimeError(f"{self.name} worker {w.label}/{self.count} did not start (rc={rc})")
         # keep draining stdout so a chatty worker never blocks on a full pipe
         loop.run_in_executor(None, _drain, w.proc.stdout)
-        log.info("%s worker %d/%d started (pid %d)", self.name, w.index, self.count, w.proc.pid)
+        log.info("%s worker %s/%d started (pid %d)", self.name, w.label, self.count, w.proc.pid)
 
     # -------------------------------------------------------------- namespace assignment
 
@@ -332,12 +344,13 @@ class WorkerSupervisor:
         i = self.owner.get(ns)
         if i is None:
             if self.is_system(ns):
-                w = self.workers[0]
+                i = 0
             else:
-                w = min(self.workers, key=lambda x: (len(x.namespaces - self._system), x.index))
-            i = self.owner[ns] = w.index
-            w.namespaces.add(ns)
-            w.send(f"assign {ns}")
+                i = min(self._slots, key=lambda k: (len(self._slots[k][0].namespaces - self._system), k))
+            self.owner[ns] = i
+            for w in self._slots[i]:
+                w.namespaces.add(ns)
+                w.send(f"assign {ns}")
         return i
 
     def is_system(self, ns: str) -> bool:
@@ -349,9 +362,9 @@ class WorkerSupervisor:
     def release(self, ns: str) -> None:
         i = self.owner.pop(ns, None)
         if i is not None:
-            w = self.workers[i]
-            w.namespaces.discard(ns)
-            w.send(f"release {ns}")
+            for w in self._slots[i]:
+                w.namespaces.discard(ns)
+                w.send(f"release {ns}")
 
     def _on_namespace(self, etype: str, obj: dict, old) -> None:
         name = (obj.get("metadata") or {}).get("name", "")
@@ -361,7 +374,7 @@ class WorkerSupervisor:
             self.assign(name)
 
     def assignments(self) -> Dict[int, List[str]]:
-        return {w.index: sorted(w.namespaces) for w in self.workers}
+        return {i: sorted(ws[0].namespaces) for i, ws in self._slots.items()}
 
     async def start(self) -> None:
         self._stopping = False
@@ -377,7 +390,7 @@ class WorkerSupervisor:
         """Restart a worker that exited, with exponential back-off (reset after a minute up).  A
         restart that fails (the new process never reports ``ready``) leaves the worker pending:
         every later pass tries again, each after a longer back-off, until one comes up."""
-        delay: Dict[int, float] = {}
+        delay: Dict[str, float] = {}
         while not self._stopping:
             await asyncio.sleep(0.2)
             for w in self.workers:
@@ -388,14 +401,14 @@ class WorkerSupervisor:
                     continue
                 if exited:
                     up = time.monotonic() - w.started_at
-                    d = self.backoff0 if up > 60 else min(self.backoff_max, delay.get(w.index, self.backoff0 / 2) * 2)
-                    log.error("%s worker %d/%d exited (rc=%s); restarting in %.1f s", self.name, w.index, self.count,
+                    d = self.backoff0 if up > 60 else min(self.backoff_max, delay.get(w.label, self.backoff0 / 2) * 2)
+                    log.error("%s worker %s/%d exited (rc=%s); restarting in %.1f s", self.name, w.label, self.count,
                               w.proc.returncode, d)
                     w.proc = None
                     w.pending = True
                 else:  # the last restart failed
-                    d = min(self.backoff_max, delay.get(w.index, self.backoff0 / 2) * 2)
-                delay[w.index] = d
+                    d = min(self.backoff_max, delay.get(w.label, self.backoff0 / 2) * 2)
+                delay[w.label] = d
                 await asyncio.sleep(d)
                 if self._stopping:
                     return
@@ -411,7 +424,7 @@ class WorkerSupervisor:
         return all(w.proc is not None and w.proc.poll() is None for w in self.workers)
 
     def pids(self) -> Dict[str, int]:
-        return {f"worker_{w.index}": w.proc.pid for w in self.workers if w.proc is not None}
+        return {f"worker_{w.label}": w.proc.pid for w in self.workers if w.proc is not None}
 
     async def stop(self) -> None:
         self._stopping = True
@@ -465,14 +478,15 @@ class WorkerSupervisor:
     async def debug(self, path: str, timeout: float = 30.0) -> List[dict]:
         return list((await self.debug_by_worker(path, timeout)).values())
 
-    async def debug_by_worker(self, path: str, timeout: float = 30.0) -> Dict[int, dict]:
-        """worker index → its JSON answer (a worker restarting is missing)."""
+    async def debug_by_worker(self, path: str, timeout: float = 30.0) -> Dict[str, dict]:
+        """worker label (its index, ``<index>_<role>`` with roles) → its JSON answer (a worker
+        restarting is missing)."""
         return await self.debug_each(lambda _i: path, timeout)
 
-    async def debug_each(self, path_for: Callable[[int], str], timeout: float = 30.0) -> Dict[int, dict]:
-        """worker index → its JSON answer to ``path_for(index)``."""
+    async def debug_each(self, path_for: Callable[[int], str], timeout: float = 30.0) -> Dict[str, dict]:
+        """worker label → its JSON answer to ``path_for(index)``."""
         docs = await asyncio.gather(*(self._get(w, path_for(w.index), timeout) for w in self.workers))
-        return {w.index: json.loads(d) for w, d in zip(self.workers, docs) if d}
+        return {w.label: json.loads(d) for w, d in zip(self.workers, docs) if d}
 
 
 def _drain(stream) -> None:

@@ -373,3 +373,55 @@ def test_cancelled_queued_live_reader_is_cancelled_and_the_others_still_read(run
         rvs = [o["metadata"]["resourceVersion"] for o in await asyncio.gather(*queued[1:])]
         assert rvs == ["2", "2"] and w.gets == 2  # one more GET for the two left, none for the cancelled one
     run(go())
+
+
+@pytest.mark.slow
+def test_split_kf_workers_serve_each_namespace_set_in_two_processes(run):
+    """``kf_manager --workers 2 --split-workers``: each namespace set is served by a notebook
+    reconciler process and a culler + event re-emitter process, both assigned the set; the
+    notebooks become Ready, and the pod/StatefulSet events are re-emitted by the aux worker."""
+    async def go():
+        import aiohttp
+
+        from odh_kubeflow_amd.parallel.platform import NodePlatform
+        from odh_kubeflow_amd.parallel.shard import ControlPlaneShard, ShardConfig
+        from odh_kubeflow_amd.testing.apiserver.native import NativeApiServer
+        from odh_kubeflow_amd.testing.cluster import OPENSHIFT_CRDS
+
+        native = await NativeApiServer(OPENSHIFT_CRDS, gc=True).start()
+        env = {"SET_PIPELINE_RBAC": "false", "SET_PIPELINE_SECRET": "false"}
+        drivers = []
+        platform = None
+        try:
+            platform = await NodePlatform(native.url, process=False).start()
+            drivers.append(await ControlPlaneShard(ShardConfig(
+                native.url, "team-0", arch="unsharded", bootstrap=True, env=env, process=True, workers=2,
+                kf_split_workers=True)).start())
+            drivers.append(await ControlPlaneShard(ShardConfig(native.url, "team-1", arch="unsharded",
+                                                               launch=False, env=env)).start())
+            pids = drivers[0].control_plane_pids()
+            assert sorted(k for k in pids if k.startswith("kf_manager_worker")) == [
+                "kf_manager_worker_0_aux", "kf_manager_worker_0_notebook",
+                "kf_manager_worker_1_aux", "kf_manager_worker_1_notebook"]
+            for i, d in enumerate(drivers):
+                await d.admin.create(notebook("nb", f"team-{i}", image="img", gpus=1))
+            for d in drivers:
+                assert await d.wait_for(lambda: d.notebook_ready("nb"), 60)
+            base = {p.name: p.base for p in drivers[0].procs}
+            async with aiohttp.ClientSession() as http:
+                for _ in range(100):
+                    async with http.get(base["kf_manager"] + "/debug/reconciles") as r:
+                        doc = await r.json()
+                    if sum((doc["reconciles"].get("notebook-events") or {}).values()) >= 2:
+                        break
+                    await asyncio.sleep(0.1)
+            assert doc["workers"] == 4 and doc["assignments"]["0"] and doc["assignments"]["1"]
+            assert sum(doc["reconciles"]["notebook-controller"].values()) >= 2
+            assert sum(doc["reconciles"]["notebook-events"].values()) >= 2
+        finally:
+            for d in drivers:
+                await d.stop()
+            if platform is not None:
+                await platform.stop()
+            await native.stop()
+    run(go(), timeout=120)

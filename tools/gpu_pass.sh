@@ -175,6 +175,35 @@ for s in $steps; do
           --warmup 5 --probe-sample 0 --resident 0 > "$out/bench_workers_n$n.log" 2>&1 || fail workers $? "$out/bench_workers_n$n.log"
         show "$out/bench_workers_n$n.log" "workers4 n$n"
       done ;;
+    wrab)  # overlay mi355x at 4 streams: 1 / 2 / 4 odh webhook processes, interleaved x2, plus N=1
+      timeout -k 10 170 python bench.py --gpus 1 --arch unsharded --workers 4 --cache-configmaps --steps 100 --warmup 5 \
+        --probe-sample 0 --resident 0 --no-configs --burst 0 > "$out/bench_wrab_n1.log" 2>&1 || fail wrab $? "$out/bench_wrab_n1.log"
+      show "$out/bench_wrab_n1.log" "wrab n1"
+      for r in 1 2; do
+        for w in 1 2 4; do
+          timeout -k 10 170 python -m torch.distributed.run --nnodes=1 --nproc-per-node 4 \
+            --master-addr 127.0.0.1 --master-port 2996$w bench.py --gpus 4 --arch unsharded --workers 4 --cache-configmaps \
+            --webhook-replicas $w --steps 100 --warmup 5 --probe-sample 0 --resident 0 --burst 0 \
+            > "$out/bench_wrab_wr${w}_r$r.log" 2>&1 || fail wrab $? "$out/bench_wrab_wr${w}_r$r.log"
+          show "$out/bench_wrab_wr${w}_r$r.log" "wrab wr$w r$r"
+        done
+      done ;;
+    splitab)  # overlay mi355x: the kf manager's workers whole vs split (notebook | culler,events), interleaved x2
+      for r in 1 2; do
+        for v in "base" "split --kf-split-workers"; do
+          set -- $v
+          tag=$1; shift
+          timeout -k 10 170 python bench.py --gpus 1 --arch unsharded --workers 4 --cache-configmaps "$@" --steps 100 \
+            --warmup 5 --probe-sample 0 --resident 0 --no-configs --burst 0 > "$out/bench_splitab_${tag}_n1_r$r.log" 2>&1 \
+            || fail splitab $? "$out/bench_splitab_${tag}_n1_r$r.log"
+          show "$out/bench_splitab_${tag}_n1_r$r.log" "splitab $tag n1 r$r"
+          timeout -k 10 170 python -m torch.distributed.run --nnodes=1 --nproc-per-node 4 \
+            --master-addr 127.0.0.1 --master-port 29958 bench.py --gpus 4 --arch unsharded --workers 4 --cache-configmaps \
+            "$@" --steps 100 --warmup 5 --probe-sample 0 --resident 0 --burst 0 \
+            > "$out/bench_splitab_${tag}_n4_r$r.log" 2>&1 || fail splitab $? "$out/bench_splitab_${tag}_n4_r$r.log"
+          show "$out/bench_splitab_${tag}_n4_r$r.log" "splitab $tag n4 r$r"
+        done
+      done ;;
     wr2)
       timeout -k 10 170 python bench.py --gpus 1 --arch unsharded --workers 4 --webhook-replicas 2 --steps 100 \
         --warmup 5 --probe-sample 0 > "$out/bench_wr2_n1.log" 2>&1 || fail wr2 $? "$out/bench_wr2_n1.log"

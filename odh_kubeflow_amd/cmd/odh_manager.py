@@ -98,7 +98,7 @@ def replica_argv(args, index: int, metrics_addr: str) -> List[str]:
 
 
 def build(args, env=os.environ):
-    from ..controllers.setup import setup_odh, shard_cache_options, with_own_services
+    from ..controllers.setup import odh_namespace_labels, setup_odh, shard_cache_options, with_own_services
     from ..models import kinds
     from ..runtime.informer import strip_data
     from ..runtime.leaderelection import LeaderElector, namespace_from_env
@@ -125,6 +125,7 @@ def build(args, env=os.environ):
     if assign is not None:
         # the controller namespace holds the central HTTPRoutes and ImageStreams every worker reads
         cache_options = assign.cache_options(extra_namespaces=[namespace], cluster_watch=args.cluster_wide_watches)
+        cache_options["namespace_labels"] = odh_namespace_labels()  # its notebooks' CRBs and HTTPRoutes only
     cache_options = with_own_services(cache_options, "odh")  # its <nb>-kube-rbac-proxy Services only
     cache_cm = getattr(args, "cache_configmaps_secrets", "false") == "true"
     mgr = Manager.remote(cfg, name="odh-notebook-controller",

@@ -121,6 +121,16 @@ def with_own_services(cache_options: dict, role: str) -> dict:
     return {**cache_options, "selectors": {**(cache_options.get("selectors") or {}), kinds.SERVICE: sel}}
 
 
+def odh_namespace_labels() -> Dict[str, str]:
+    """The odh reconciler's objects outside the notebooks' namespaces, by the label naming the
+    notebook namespace they belong to: a namespace-restricted cache (a shard, a worker) lists
+    and watches only its own (``InformerCache`` ``namespace_labels``)."""
+    from ..models import kinds
+
+    return {kinds.CLUSTER_ROLE_BINDING: "opendatahub.io/namespace",  # controllers/odh/auth.py
+            kinds.HTTP_ROUTE: "notebook-namespace"}  # controllers/odh/route.py (central namespace)
+
+
 def shard_cache_options(shard: Optional[str], controller_namespace: str, cluster_watch: bool = False) -> dict:
     """InformerCache keyword arguments for one shard: the namespaces labelled
     ``notebooks.amd.com/shard=<shard>`` (followed live) plus the controller namespace, with
@@ -132,4 +142,4 @@ def shard_cache_options(shard: Optional[str], controller_namespace: str, cluster
         return {}
     sel = f"{SHARD_LABEL}={shard}"
     return {"namespace_selector": sel, "namespaces": [controller_namespace], "selectors": {kinds.HTTP_ROUTE: sel},
-            "cluster_watch": cluster_watch}
+            "cluster_watch": cluster_watch, "namespace_labels": odh_namespace_labels()}

@@ -340,6 +340,11 @@ class InformerCache(Reader, EventSource):
     (``cache.Options.ByObject[..].Label``) so a shard only ever receives the objects it owns;
     ``field_selectors`` likewise with a field selector (``ByObject[..].Field``; immutable fields
     only, e.g. an Event's ``involvedObject.kind``, so an object never moves out of it).
+    ``namespace_labels`` maps a kind that lives outside the notebooks' namespaces (cluster-scoped,
+    or in the controller namespace) to the label naming the namespace an object belongs to: a
+    namespace-restricted cache then lists and watches only the objects of its namespaces
+    (``<label> in (<its namespaces>)``, re-scoped as the set changes) — every shard or worker
+    would otherwise decode every other one's ClusterRoleBindings and HTTPRoutes.
     """
 
     def __init__(self, rest, namespace: Optional[str] = None, transforms: Optional[Dict[str, Optional[Transform]]] = None,
@@ -347,7 +352,8 @@ class InformerCache(Reader, EventSource):
                  selectors: Optional[Dict[str, str]] = None, namespace_selector: Optional[str] = None,
                  namespace_filter: Optional[Callable[[dict], bool]] = None,
                  field_selectors: Optional[Dict[str, str]] = None,
-                 label_index_keys: Optional[Iterable[str]] = None, cluster_watch: bool = False):
+                 label_index_keys: Optional[Iterable[str]] = None, cluster_watch: bool = False,
+                 namespace_labels: Optional[Dict[str, str]] = None):
         self.rest = rest
         self.namespace = namespace
         nss = list(namespaces) if namespaces is not None else ([namespace] if namespace else None)
@@ -366,6 +372,10 @@ class InformerCache(Reader, EventSource):
             self.transforms[SCHEME.resolve(k).key] = fn
         self.selectors: Dict[str, str] = {SCHEME.resolve(k).key: v for k, v in (selectors or {}).items()}
         self.field_selectors: Dict[str, str] = {SCHEME.resolve(k).key: v for k, v in (field_selectors or {}).items()}
+        self.namespace_labels: Dict[str, str] = {SCHEME.resolve(k).key: v
+                                                 for k, v in (namespace_labels or {}).items()}
+        self._rescope_pending = False
+        self.rescopes = 0
         self.watch_timeout_s = watch_timeout_s
         self.label_index_keys = frozenset(LABEL_INDEX_KEYS if label_index_keys is None else label_index_keys)
         self._groups: Dict[str, _Group] = {}
@@ -396,6 +406,7 @@ class InformerCache(Reader, EventSource):
             if ns in self.namespaces:
                 self.namespaces.discard(ns)
                 self.namespace_changes += 1
+                self._schedule_rescope()
                 for g in self._groups.values():
                     if not g.info.namespaced:
                         continue
@@ -409,6 +420,7 @@ class InformerCache(Reader, EventSource):
         elif ns not in self.namespaces:
             self.namespaces.add(ns)
             self.namespace_changes += 1
+            self._schedule_rescope()
             for g in self._groups.values():
                 if not g.info.namespaced:
                     continue
@@ -436,8 +448,47 @@ class InformerCache(Reader, EventSource):
             inf._delete(old)
             inf._notify("DELETED", old, old)
 
+    def _scoped_selector(self, key: str) -> Optional[str]:
+        """``kind``'s label selector: the static one, or for a ``namespace_labels`` kind of a
+        namespace-restricted cache the objects of its namespaces."""
+        sel = self.selectors.get(key)
+        label = self.namespace_labels.get(key)
+        if sel or not label or self.namespaces is None:
+            return sel
+        # "-" names no namespace: an empty set selects nothing
+        return f"{label} in ({','.join(sorted(self.namespaces)) or '-'})"
+
+    def _schedule_rescope(self) -> None:
+        if not self.namespace_labels or self._rescope_pending:
+            return
+        self._rescope_pending = True
+        try:
+            asyncio.get_running_loop().call_soon(self._rescope)
+        except RuntimeError:  # no loop yet: the informers start with the current set
+            self._rescope_pending = False
+
+    def _rescope(self) -> None:
+        """The namespace set changed (coalesced per loop turn): re-list the ``namespace_labels``
+        kinds under the new selector.  In place — the relist applies only the difference, so
+        objects still in scope raise no event."""
+        self._rescope_pending = False
+        for key in self.namespace_labels:
+            g = self._groups.get(key)
+            if g is None:
+                continue
+            sel = self._scoped_selector(key)
+            for inf in g.infs.values():
+                if inf.label_selector == sel:
+                    continue
+                inf.label_selector = sel
+                inf._label_reqs = parse_label_selector(sel) if sel else None
+                self.rescopes += 1
+                if inf.task is not None:
+                    inf.task.cancel()
+                inf.task = asyncio.ensure_future(inf.run())
+
     def _start_informer(self, g: _Group, ns: Optional[str]) -> _Informer:
-        inf = _Informer(self, g.info, g.version, ns, self.selectors.get(g.info.key),
+        inf = _Informer(self, g.info, g.version, ns, self._scoped_selector(g.info.key),
                         self.field_selectors.get(g.info.key))
         inf.handlers = g.handlers  # shared: subscriptions made earlier see this namespace too
         g.infs[ns] = inf

@@ -767,3 +767,39 @@ def test_webhook_only_control_plane_takes_no_lease(tmp_path):
         assert mgr.leader_elector is not None and mgr.webhook_server is None
         leases.add(mgr.leader_elector.name)
     assert len(leases) == 2
+
+
+def test_namespace_scoped_kinds_follow_the_namespace_set(run, server_kind):
+    """``InformerCache(namespace_labels=…)``: a namespace-restricted cache lists and watches only
+    the ClusterRoleBindings labelled with one of its namespaces, re-scoped when the set changes —
+    a namespace joining brings its objects (ADDED) without re-announcing the ones already held."""
+    mine = {"a"}
+
+    async def go():
+        srv, c = await _server(server_kind)
+        try:
+            for ns in ("a", "b"):
+                await c.create({"apiVersion": "v1", "kind": "Namespace", "metadata": {"name": ns}})
+                await c.create({"apiVersion": "rbac.authorization.k8s.io/v1", "kind": "ClusterRoleBinding",
+                                "metadata": {"name": f"crb-{ns}", "labels": {"opendatahub.io/namespace": ns}},
+                                "roleRef": {"apiGroup": "rbac.authorization.k8s.io", "kind": "ClusterRole",
+                                            "name": "view"}, "subjects": []})
+            cache = InformerCache(c, namespace_filter=lambda o: m.name(o) in mine,
+                                  namespace_labels={kinds.CLUSTER_ROLE_BINDING: "opendatahub.io/namespace"})
+            seen = []
+            cache.subscribe(kinds.CLUSTER_ROLE_BINDING, lambda et, o, old: seen.append((et, m.name(o))))
+            await cache.wait_synced([kinds.CLUSTER_ROLE_BINDING, kinds.NAMESPACE])
+            assert await _wait(lambda: [m.name(o) for o in cache.list(kinds.CLUSTER_ROLE_BINDING)] == ["crb-a"])
+            mine.add("b")
+            cache.refresh_namespace("b")
+            assert await _wait(lambda: len(cache.list(kinds.CLUSTER_ROLE_BINDING)) == 2)
+            assert seen == [("ADDED", "crb-a"), ("ADDED", "crb-b")] and cache.rescopes >= 1
+            mine.discard("a")
+            cache.refresh_namespace("a")
+            assert await _wait(lambda: [m.name(o) for o in cache.list(kinds.CLUSTER_ROLE_BINDING)] == ["crb-b"])
+            assert seen[-1] == ("DELETED", "crb-a")
+            await cache.stop()
+        finally:
+            await c.close()
+            await srv.stop()
+    run(go())

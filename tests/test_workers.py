@@ -409,7 +409,7 @@ def test_split_kf_workers_serve_each_namespace_set_in_two_processes(run):
                 assert await d.wait_for(lambda: d.notebook_ready("nb"), 60)
             base = {p.name: p.base for p in drivers[0].procs}
             async with aiohttp.ClientSession() as http:
-                for _ in range(100):
+                for _ in range(400):
                     async with http.get(base["kf_manager"] + "/debug/reconciles") as r:
                         doc = await r.json()
                     if sum((doc["reconciles"].get("notebook-events") or {}).values()) >= 2:

@@ -204,6 +204,22 @@ for s in $steps; do
           show "$out/bench_splitab_${tag}_n4_r$r.log" "splitab $tag n4 r$r"
         done
       done ;;
+    ovlab)  # overlay mi355x candidates at 1 and 4 streams, interleaved x2: as shipped vs split kf workers + 2 webhook procs
+      for r in 1 2; do
+        for v in "cur" "cand --kf-split-workers --webhook-replicas 2"; do
+          set -- $v
+          tag=$1; shift
+          timeout -k 10 170 python bench.py --gpus 1 --arch unsharded --workers 4 --cache-configmaps "$@" --steps 100 \
+            --warmup 5 --probe-sample 0 --resident 0 --no-configs --burst 0 > "$out/bench_ovl_${tag}_n1_r$r.log" 2>&1 \
+            || fail ovlab $? "$out/bench_ovl_${tag}_n1_r$r.log"
+          show "$out/bench_ovl_${tag}_n1_r$r.log" "ovl $tag n1 r$r"
+          timeout -k 10 170 python -m torch.distributed.run --nnodes=1 --nproc-per-node 4 \
+            --master-addr 127.0.0.1 --master-port 29957 bench.py --gpus 4 --arch unsharded --workers 4 --cache-configmaps \
+            "$@" --steps 100 --warmup 5 --probe-sample 0 --resident 0 --burst 0 \
+            > "$out/bench_ovl_${tag}_n4_r$r.log" 2>&1 || fail ovlab $? "$out/bench_ovl_${tag}_n4_r$r.log"
+          show "$out/bench_ovl_${tag}_n4_r$r.log" "ovl $tag n4 r$r"
+        done
+      done ;;
     wr2)
       timeout -k 10 170 python bench.py --gpus 1 --arch unsharded --workers 4 --webhook-replicas 2 --steps 100 \
         --warmup 5 --probe-sample 0 > "$out/bench_wr2_n1.log" 2>&1 || fail wr2 $? "$out/bench_wr2_n1.log"

@@ -29,14 +29,14 @@ try:  # native JSON decoding (native/objcore.cpp): ~1.7x json.loads, shared subt
     from ..native._objcore import loads_event as _loads_event
     from ..native._objcore import loads_shared as _loads_shared
 
-    def _loads(raw):
+    def loads_json(raw):
         try:
             return _loads_shared(raw)
         except ValueError:
             return json.loads(raw)  # json's own verdict (and its NaN / Infinity literals)
 except ImportError:  # pragma: no cover - the extension is not built
     _loads_event = None
-    _loads = json.loads
+    loads_json = json.loads
 
 from ..models.errors import ApiError, Gone, InternalError
 from ..models.scheme import SCHEME, ResourceInfo
@@ -239,7 +239,7 @@ class RestClient(Client):
         if raw:
             self.bytes_in[count_as] = self.bytes_in.get(count_as, 0) + len(raw)
         try:
-            out = _loads(raw) if raw else {}
+            out = loads_json(raw) if raw else {}
         except ValueError:
             out = {"message": raw[:200].decode(errors="replace")}
         if status >= 400:

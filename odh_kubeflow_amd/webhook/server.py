@@ -25,6 +25,7 @@ import time
 from typing import Optional, Tuple
 
 from ..runtime.http1 import Http1Server
+from ..runtime.rest import loads_json  # native JSON decoding, json.loads on what it declines
 from .notebook_webhook import WEBHOOK_PATH, NotebookWebhook
 
 log = logging.getLogger("webhook.server")
@@ -109,7 +110,7 @@ class WebhookServer:
         self.served += 1
         t0 = time.perf_counter()
         try:
-            review = json.loads(data)
+            review = loads_json(data)
         except ValueError as e:
             out = {"apiVersion": "admission.k8s.io/v1", "kind": "AdmissionReview",
                    "response": {"uid": "", "allowed": False, "status": {"code": 400, "message": str(e)}}}

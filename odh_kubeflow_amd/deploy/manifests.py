@@ -100,10 +100,15 @@ MI355X_CULLER = ["CULLING_ACTIVITY_SOURCE=combined", "ENABLE_CULLING=true"]
 # processes (runtime/workers.py; the odh webhook stays on the supervisor's own event loop) —
 # one core per worker, so an 8-GPU node's notebooks are not serialised on one Python loop
 MI355X_WORKERS = 4
-# --webhook-replicas: measured at 4 streams on the box, a second webhook process left
-# notebooks/s unchanged (570 vs 572, profiles/r4_p9) — admissions were not the limit there;
-# raise it where admission load outgrows one core
-MI355X_WEBHOOK_REPLICAS = 1
+# --webhook-replicas: at 4 streams the one webhook process (the supervisor, which also leads and
+# watches cluster-wide) ran ≈75 % busy; 1 / 2 / 4 webhook processes gave 561–572 / 586 / 598–606
+# notebooks/s, interleaved (profiles/r5_p13) — two take most of it
+MI355X_WEBHOOK_REPLICAS = 2
+# kf --split-workers: each namespace set served by a notebook-reconciler process and a culler +
+# event re-emitter process, as a shard pod does; with 2 webhook processes, against neither, at 4
+# streams: 607 / 627 vs 596 / 605 notebooks/s, interleaved (profiles/r5_p15; split alone
+# 590 / 605 vs 560 / 587, profiles/r5_p14)
+MI355X_KF_SPLIT_WORKERS = True
 # the odh manager caches ConfigMap/Secret data, as a shard does: the webhook and the reconcilers
 # read them from the cache instead of confirming absences live (+12 % notebooks/s at 4 streams,
 # interleaved on one box, profiles/r4_p16); the reference's overlays keep its uncached reads
@@ -272,16 +277,23 @@ def _agent_token_volume() -> dict:
 AGENT_TOKEN_MOUNT_SPEC = {"name": "node-agent-token", "mountPath": AGENT_TOKEN_MOUNT, "readOnly": True}
 
 
-def _workers_patches(workers: int, webhook_replicas: int = 1, cache_configmaps: bool = False) -> List[dict]:
+def _workers_patches(workers: int, webhook_replicas: int = 1, cache_configmaps: bool = False,
+                     kf_split: bool = False) -> List[dict]:
     """``--workers`` for both managers, and the CPU to run them: one core per worker plus the
     supervisor (which leads, aggregates /metrics and, in the odh manager, serves the webhook);
     the odh manager's ``--webhook-replicas`` add a core each (webhook-only processes sharing the
-    webhook port)."""
+    webhook port); the kf manager's ``--split-workers`` doubles its worker processes (each
+    namespace set: notebook reconciler + culler / event re-emitter), the second of each pair
+    lightly loaded — 1.5 cores per set."""
     ops = [{"op": "add", "path": "/spec/template/spec/containers/0/args/-", "value": f"--workers={workers}"},
            {"op": "replace", "path": "/spec/template/spec/containers/0/resources/limits/cpu", "value": str(workers + 1)},
            {"op": "replace", "path": "/spec/template/spec/containers/0/resources/requests/cpu", "value": str(workers)}]
+    kf = list(ops)
+    if kf_split:
+        kf = [ops[0], {"op": "add", "path": "/spec/template/spec/containers/0/args/-", "value": "--split-workers"},
+              {**ops[1], "value": str(2 * workers + 1)}, {**ops[2], "value": str(workers + workers // 2)}]
     out = [{"target": {"kind": "Deployment", "name": f"{NAME_PREFIX}deployment"},
-            "patch": yaml.safe_dump(ops, sort_keys=False)}]
+            "patch": yaml.safe_dump(kf, sort_keys=False)}]
     extra = max(0, webhook_replicas - 1)
     odh = [*ops[:1], *([{"op": "add", "path": "/spec/template/spec/containers/0/args/-",
                          "value": f"--webhook-replicas={webhook_replicas}"}] if extra else []),
@@ -830,7 +842,8 @@ def tree(version: Optional[str] = None) -> Dict[str, object]:
                                                             namespace="opendatahub", images=images,
                                                             configMapGenerator=mi355x_generators,
                                                             patches=_workers_patches(MI355X_WORKERS, MI355X_WEBHOOK_REPLICAS,
-                                                                                     MI355X_CACHE_CONFIGMAPS))
+                                                                                     MI355X_CACHE_CONFIGMAPS,
+                                                                                     MI355X_KF_SPLIT_WORKERS))
     # the serving cert covers every shard's Service; every shard's configuration gets the caBundle
     svc_names = [NAME_PREFIX + o["metadata"]["name"] for o in cp["services.yaml"][1:]]
     mwc_names = [NAME_PREFIX + o["metadata"]["name"] for o in cp["webhooks.yaml"]]

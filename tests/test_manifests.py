@@ -364,19 +364,21 @@ def test_webhook_certs_rbac_is_scoped_to_its_objects(overlay):
 
 def test_mi355x_overlay_runs_manager_workers_and_webhook_replicas():
     """Overlay mi355x (the reference's two-Deployment layout): both managers with ``--workers=4``
-    and a CPU request to match (``--webhook-replicas`` stays 1: a second webhook process did not
-    move notebooks/s at 4 streams).  Other overlays run neither."""
+    and a CPU request to match; the kf manager's workers split (notebook | culler,events), the odh
+    manager with two webhook processes.  Other overlays run none of it."""
     deps = _by(_render("mi355x"), "Deployment")
     kf = deps["odh-kubeflow-amd-deployment"]["spec"]["template"]["spec"]["containers"][0]
     odh = deps["odh-kubeflow-amd-manager"]["spec"]["template"]["spec"]["containers"][0]
-    assert "--workers=4" in kf["args"] and not any(a.startswith("--webhook-replicas") for a in kf["args"])
-    assert kf["resources"]["requests"]["cpu"] == "4" and kf["resources"]["limits"]["cpu"] == "5"
-    assert "--workers=4" in odh["args"] and not any(a.startswith("--webhook-replicas") for a in odh["args"])
+    assert "--workers=4" in kf["args"] and "--split-workers" in kf["args"]
+    assert not any(a.startswith("--webhook-replicas") for a in kf["args"])
+    assert kf["resources"]["requests"]["cpu"] == "6" and kf["resources"]["limits"]["cpu"] == "9"
+    assert "--workers=4" in odh["args"] and "--webhook-replicas=2" in odh["args"]
     assert "--cache-configmaps-secrets=true" in odh["args"] and not any("cache-configmaps" in a for a in kf["args"])
-    assert odh["resources"]["requests"]["cpu"] == "4" and odh["resources"]["limits"]["cpu"] == "5"
-    plain = _by(_render("standalone"), "Deployment")["odh-kubeflow-amd-manager"]
-    assert not any(a.startswith(("--workers", "--webhook-replicas", "--cache-configmaps"))
-                   for a in plain["spec"]["template"]["spec"]["containers"][0]["args"])
+    assert odh["resources"]["requests"]["cpu"] == "5" and odh["resources"]["limits"]["cpu"] == "6"
+    plain = _by(_render("standalone"), "Deployment")
+    for d in plain.values():
+        assert not any(a.startswith(("--workers", "--webhook-replicas", "--cache-configmaps", "--split-workers"))
+                       for a in d["spec"]["template"]["spec"]["containers"][0]["args"])
 
 
 def test_node_agent_identity_plumbing():

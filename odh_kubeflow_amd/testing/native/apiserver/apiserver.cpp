@@ -574,6 +574,8 @@ struct Ev {
   std::shared_ptr<EvCache> cache;
 };
 
+struct Hist;
+
 struct WatchSlot {
   std::condition_variable cv;
   // the watch's namespace / label / field filter: emit() wakes a watcher only for events it
@@ -584,6 +586,10 @@ struct WatchSlot {
   // is not woken by them and could fall behind the bounded history — the periodic wake-up
   // (emit) advances it; a watch without one is woken by every event it reads
   bool filtered = false;
+  // the history it reads and the seq it has scanned up to (both under the bucket's hmu): the
+  // periodic wake-up skips a watcher with nothing unscanned
+  const Hist* hist = nullptr;
+  int64_t seen = 0;
 };
 
 // one ordered event history: `seq` numbers its events, `hist` keeps the newest S.history
@@ -860,11 +866,15 @@ void emit(const Res& r, const char* type, Obj obj, Obj old) {
     // events (each one every half history): one that rejects every event it sees advances
     // past them before they fall off the bounded history (no spurious 410 Gone relists),
     // without waking every watcher of the resource at once (a herd on the history lock that
-    // commits then wait for)
+    // commits then wait for).  Only a watcher whose history moved since its last scan: with
+    // one watch per namespace most of them (every idle namespace's) have nothing to skip
     const int64_t turn = (b.all.seq / step) & 7;
     int64_t i = 0;
-    for (auto& w : b.watchers)
-      if (w.second->filtered && (i++ & 7) == turn) t_wake.push_back({w.second, ev.obj, ev.old, true});
+    for (auto& w : b.watchers) {
+      WatchSlot& s = *w.second;
+      if (s.filtered && (i++ & 7) == turn && (!s.hist || s.hist->seq > s.seen))
+        t_wake.push_back({w.second, ev.obj, ev.old, true});
+    }
   }
   auto wake = [&](const std::string& ns) {
     auto rg = b.watchers.equal_range(ns);
@@ -2849,6 +2859,8 @@ void serve_watch(int fd, Res& r, const Path& p, const Request& rq) {
     wh = ns.empty() ? &b.all : &b.by_ns[ns];
     b.watchers.emplace(ns, slot_ptr);
     last_seq = wh->seq;
+    slot.hist = wh;
+    slot.seen = last_seq;
     if (rv.empty() || rv == "0") {
       for (auto& kv : b.objs)
         if (wants(*kv.second)) {
@@ -2914,6 +2926,7 @@ void serve_watch(int fd, Res& r, const Path& p, const Request& rq) {
             if (wants(*e.obj) || (e.old && wants(*e.old))) evs.push_back(e);
           }
           last_seq = h.seq;
+          slot.seen = last_seq;
           lk.unlock();
           for (auto& e : evs) lines.push_back(event_line(r, e, p.version));
         }

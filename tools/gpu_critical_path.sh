@@ -1,7 +1,7 @@
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 export TMPDIR=/tmp
-out=gpurun_out/${1:-r2_p15}
+out=gpurun_out/${1:-critpath}
 mkdir -p $out
 DEBUG_WRITE_AUDITLOG=$PWD/$out/a1.jsonl timeout -k 10 200 python bench.py --steps 200 --burst 0 --probe-sample 0 --no-configs > $out/bench_n1_audit.log 2>&1 || exit 1
 python tools/critical_path.py $out/a1.jsonl --namespace-prefix bench- > $out/critical_path_n1.json || exit 1

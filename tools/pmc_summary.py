@@ -1,6 +1,6 @@
 """Per-kernel summary of ``rocprofv3 --pmc`` passes (``tools/gpu_pass.sh <tag> pmc``).
 
-    python tools/pmc_summary.py gpurun_out/r2_pmc > profiles/r2_pmc/probe_pmc_summary.json
+    python tools/pmc_summary.py gpurun_out/r5_f1 > profiles/r5_f1/pmc_summary.json
 
 Each pass directory holds ``run_counter_collection.csv`` (one row per dispatch and
 counter).  Counters are averaged per kernel over its dispatches and joined across passes,

@@ -2,8 +2,10 @@
 
 Identical events (same involved object, type, reason, message, source) within the
 aggregation window are folded into one Event whose ``count`` is bumped, as client-go's
-event correlator does, so a hot reconcile loop cannot flood the store.  Writes are
-fire-and-forget tasks: recording an event never blocks a reconcile.
+event correlator does, so a hot reconcile loop cannot flood the store.  The events seen are
+kept in an LRU of ``MAX_SEEN`` entries (client-go's correlator cache is an LRU of 4096), so
+recording stays O(1) however many distinct events a long-running manager writes.  Writes
+are fire-and-forget tasks: recording an event never blocks a reconcile.
 """
 
 from __future__ import annotations
@@ -12,7 +14,8 @@ import asyncio
 import logging
 import time
 import uuid
-from typing import Dict, Tuple
+from collections import OrderedDict
+from typing import Tuple
 
 from ..models import meta as m
 from ..models.errors import ApiError, is_not_found
@@ -26,12 +29,13 @@ WARNING = "Warning"
 
 class EventRecorder:
     AGGREGATE_WINDOW = 600.0
+    MAX_SEEN = 4096
 
     def __init__(self, client, component: str, host: str = ""):
         self.client = client
         self.component = component
         self.host = host
-        self._seen: Dict[Tuple, Tuple[str, str, int, float]] = {}
+        self._seen: "OrderedDict[Tuple, Tuple[str, str, int, float]]" = OrderedDict()
         self._tasks: set = set()
         self.emitted = 0
 
@@ -63,6 +67,7 @@ class EventRecorder:
                     await self.client.patch("v1/Event", {"count": count, "lastTimestamp": rfc3339()},
                                             name=ev_name, namespace=ev_ns)
                     self._seen[key] = (ev_ns, ev_name, count, now)
+                    self._seen.move_to_end(key)
                     return
                 except ApiError as e:
                     if not is_not_found(e):
@@ -78,9 +83,9 @@ class EventRecorder:
             }
             await self.client.create(ev)
             self._seen[key] = (ns, name, 1, now)
-            if len(self._seen) > 4096:
-                cutoff = now - self.AGGREGATE_WINDOW
-                self._seen = {k: v for k, v in self._seen.items() if v[3] >= cutoff}
+            self._seen.move_to_end(key)
+            while len(self._seen) > self.MAX_SEEN:  # the least recently seen goes first
+                self._seen.popitem(last=False)
         except Exception as e:  # events are best effort
             log.debug("event write failed: %r", e)
 

@@ -119,6 +119,11 @@ def build(args, env=os.environ):
 
     shard = resolve_shard(args.shard, env)
     cfg = RestConfig.load(args.master, args.kubeconfig)
+    if set(args.controller_set) != set(ALL_CONTROLLERS):
+        # a shard pod runs this program four times: the audit log tells its containers apart
+        # (control_plane.notebook/…, control_plane.odh/…)
+        prog, sep, rest = cfg.user_agent.partition("/")
+        cfg.user_agent = f"{prog}.{'+'.join(args.controller_set)}{sep}{rest}"
     if args.qps:
         cfg.qps = float(args.qps)
     if args.burst:

@@ -66,6 +66,7 @@ from typing import Any, Callable, Mapping, Optional, Sequence
 
 from ..models import kinds
 from ..models import meta as m
+from ..models.errors import ApiError, is_not_found
 from ..models.notebook import (LAST_ACTIVITY_ANNOTATION, LAST_ACTIVITY_CHECK_TIMESTAMP_ANNOTATION, STOP_ANNOTATION,
                                gpu_request)
 from ..nodeagent.identity import IDENTITY_DOMAIN
@@ -606,18 +607,31 @@ class CullingReconciler:
             return self.reader.get(kind, name, namespace)
         return await self.client.get_or_none(kind, name, namespace)
 
+    # the annotations only the culler writes: a patch that sets nothing else needs no
+    # resourceVersion precondition (see _update)
+    OWN_ANNOTATIONS = frozenset((LAST_ACTIVITY_ANNOTATION, LAST_ACTIVITY_CHECK_TIMESTAMP_ANNOTATION))
+
     async def _update(self, req: Request, mutate: Callable[[dict], None]) -> None:
         """``RetryOnConflict{Get; mutate; Update}`` (:106-112, :171-196), written as a merge patch
-        of the annotations the culler changed, preconditioned on the resourceVersion it read —
-        the same optimistic concurrency as the reference's Update, without re-sending (and the
-        apiserver re-validating) the whole pod template on every check of every notebook.  A
-        mutation that changes nothing writes nothing (kube-apiserver skips no-op updates too)."""
+        of the annotations the culler changed, without re-sending (and the apiserver
+        re-validating) the whole pod template on every check of every notebook.  A mutation
+        that changes nothing writes nothing (kube-apiserver skips no-op updates too).
+
+        A patch that touches only the culler's own activity annotations carries no
+        resourceVersion precondition: nobody else writes them, and preconditioned, the first
+        one conflicted with the notebook controller's status write of the same moment on every
+        notebook, and its retry then landed on the notebook being deleted, conflicting with the
+        odh controller's finalizer removal in turn.  A patch that stops the notebook (or removes
+        the annotations) keeps the reference's optimistic concurrency: it is decided on the
+        version read.  A notebook being deleted is not written at all."""
         from ..runtime.client import LIVE_READS
 
         async def fn():
             cur = None if LIVE_READS.get() else self._cached(kinds.NOTEBOOK_V1BETA1, req.name, req.namespace)
             if cur is None:
                 cur = await self.client.get(kinds.NOTEBOOK_V1BETA1, req.name, req.namespace)
+            if m.is_deleting(cur):
+                return
             md = cur.get("metadata") or {}
             before = md.get("annotations") or {}
             view = {"metadata": {"name": md.get("name"), "namespace": md.get("namespace"),
@@ -628,9 +642,15 @@ class CullingReconciler:
             diff.update({k: None for k in before if k not in after})
             if not diff:
                 return
-            await self.client.patch(kinds.NOTEBOOK_V1BETA1,
-                                    {"metadata": {"resourceVersion": md.get("resourceVersion"), "annotations": diff}},
-                                    "merge", name=req.name, namespace=req.namespace)
+            meta = {"annotations": diff}
+            if not all(k in self.OWN_ANNOTATIONS and v is not None for k, v in diff.items()):
+                meta["resourceVersion"] = md.get("resourceVersion")
+            try:
+                await self.client.patch(kinds.NOTEBOOK_V1BETA1, {"metadata": meta}, "merge",
+                                        name=req.name, namespace=req.namespace)
+            except ApiError as e:
+                if not is_not_found(e):  # deleted meanwhile: nothing to annotate
+                    raise
 
         await retry_on_conflict(fn)
 

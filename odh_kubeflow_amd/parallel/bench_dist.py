@@ -922,7 +922,10 @@ async def _drive(args, shard, dist, torch, children: Optional[dict] = None, nati
     for _ in range(args.warmup):
         await one_step(False)
     await _in_thread(dist.barrier)  # every rank's warm-up done (unsharded: one control plane for all)
-    await shard.quiesce()
+    # the warm-up's trailing work, not the culler's next check of each warm-up notebook: that
+    # timer is a check period away (1 s), and waiting for it left every process idle for a
+    # second before the window — long enough for the host to start the window cold
+    await shard.quiesce(timers=0.05)
     if torch.cuda.is_available():
         torch.cuda.synchronize()
     await _in_thread(dist.barrier)
@@ -1020,6 +1023,10 @@ async def _drive(args, shard, dist, torch, children: Optional[dict] = None, nati
     # the first steps of the window run slower than the rest (warm-up of the host, not the code)
     life = [a + b for a, b in zip(lat_ms, teardown_ms)]
     blocks = [round(statistics.fmean(life[i:i + 20]), 3) for i in range(0, len(life), 20)]
+    trace = os.environ.get("ODH_BENCH_STEP_TRACE")  # debug aid: every timed step's two halves
+    if trace:
+        with open(f"{trace}.{dist.get_rank()}.json", "w") as f:
+            json.dump({"create_to_ready_ms": lat_ms, "ready_to_gone_ms": teardown_ms}, f)
     await _in_thread(dist.all_gather_object, gathered, {"lat": lat_ms, "teardown": teardown_ms, "own_s": own,
                                                         "blocks": blocks,
                                                         "cpu": cpu, "rss": rss, "in_window": in_window,

@@ -432,13 +432,16 @@ class ControlPlaneShard:
 
     # ------------------------------------------------------------------ waiting
 
-    async def quiesce(self, quiet: float = 0.002, timeout: float = 10.0) -> bool:
+    async def quiesce(self, quiet: float = 0.002, timeout: float = 10.0, timers: Optional[float] = None) -> bool:
         """Every control-plane process this rank launched idle: queues empty, no reconcile
         running, no watch event for ``quiet`` s (event-driven inside each process,
-        :meth:`Manager.quiesce`; one request each, answered when they are quiet)."""
-        res = [await mgr.quiesce(quiet, timeout) for mgr in self.managers]
+        :meth:`Manager.quiesce`; one request each, answered when they are quiet).  ``timers``:
+        delayed requeues due later than that many seconds are not waited for."""
+        res = [await mgr.quiesce(quiet, timeout, timers) for mgr in self.managers]
         if self.procs:
             q = f"/debug/quiesce?quiet_ms={quiet * 1e3:g}&timeout_s={timeout:g}"
+            if timers is not None:
+                q += f"&timers_ms={timers * 1e3:g}"
             res += [d["idle"] for d in await asyncio.gather(*(self._get_json(p.base + q) for p in self.procs))]
         return all(res)
 

@@ -370,8 +370,8 @@ class Controller:
             if self.on_reconcile is not None:
                 self.on_reconcile(self.name, req, dt, err)
 
-    def idle(self) -> bool:
-        return self.queue.pending() == 0 and self.active == 0
+    def idle(self, timers_within: Optional[float] = None) -> bool:
+        return self.queue.pending(timers_within) == 0 and self.active == 0
 
 
 class Builder:

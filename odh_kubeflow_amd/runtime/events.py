@@ -35,7 +35,7 @@ class EventRecorder:
         self.client = client
         self.component = component
         self.host = host
-        self._seen: "OrderedDict[Tuple, Tuple[str, str, int, float]]" = OrderedDict()
+        self._seen: OrderedDict[Tuple, Tuple[str, str, int, float]] = OrderedDict()
         self._tasks: set = set()
         self.emitted = 0
 

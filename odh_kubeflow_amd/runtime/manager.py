@@ -233,8 +233,8 @@ class Manager:
 
     # ------------------------------------------------------------------ test / bench helpers
 
-    def idle(self) -> bool:
-        return all(c.idle() for c in self.controllers)
+    def idle(self, timers_within: Optional[float] = None) -> bool:
+        return all(c.idle(timers_within) for c in self.controllers)
 
     async def wait_idle(self, timeout: float = 10.0, settle: float = 0.0) -> bool:
         """Wait until every controller queue is drained (ignores delayed requeues beyond ``timeout``)."""
@@ -253,26 +253,29 @@ class Manager:
             await asyncio.sleep(0.002)
         return False
 
-    async def quiesce(self, quiet: float = 0.002, timeout: float = 10.0) -> bool:
+    async def quiesce(self, quiet: float = 0.002, timeout: float = 10.0,
+                      timers_within: Optional[float] = None) -> bool:
         """Event-driven idle: return once no controller has queued or running work and no
         watch event has reached this manager's cache for ``quiet`` seconds (the trailing
         reconciles of a deletion — GC'd children, the pod going away — arrive as watch events
         after the object itself is gone).  No fixed polling period and no minimum number of
-        checks: it returns ``quiet`` after the last event, or at once if that is long past."""
+        checks: it returns ``quiet`` after the last event, or at once if that is long past.
+        ``timers_within``: delayed requeues due later than that many seconds do not count as
+        work (the culler's next check of every notebook is a period away)."""
         src = getattr(self, "cache", None) or self.reader
         deadline = time.monotonic() + timeout
         while True:
             now = time.monotonic()
             since = now - getattr(src, "last_event", 0.0)
-            if self.idle() and since >= quiet:
+            if self.idle(timers_within) and since >= quiet:
                 for rec in self._recorders.values():
                     await rec.flush()
-                if self.idle():
+                if self.idle(timers_within):
                     return True
                 continue
             if now >= deadline:
                 return False
-            await asyncio.sleep(max(0.0002, quiet - since) if self.idle() else 0.0002)
+            await asyncio.sleep(max(0.0002, quiet - since) if self.idle(timers_within) else 0.0002)
 
     def fail(self, reason: str) -> None:
         """End :meth:`run_until` with exit code 1 (the process must restart)."""
@@ -389,10 +392,11 @@ class Manager:
         async def quiesce(req):
             quiet = float(req.query.get("quiet_ms", "2")) / 1e3
             timeout = float(req.query.get("timeout_s", "10"))
+            timers = float(req.query["timers_ms"]) / 1e3 if "timers_ms" in req.query else None
             sub = []
             if self.supervisor is not None:
                 sub = [asyncio.ensure_future(self.supervisor.debug(req.path_qs, timeout + 5))]
-            idle = await self.quiesce(quiet, timeout)
+            idle = await self.quiesce(quiet, timeout, timers)
             docs = (await sub[0]) if sub else []
             idle = idle and all(d.get("idle") for d in docs) and (
                 self.supervisor is None or len(docs) == len(self.supervisor.workers))

@@ -202,5 +202,11 @@ class WorkQueue:
     def shutting_down(self) -> bool:
         return self._shutdown
 
-    def pending(self) -> int:
-        return len(self._queue) + len(self._processing) + len(self._waiting)
+    def pending(self, timers_within: Optional[float] = None) -> int:
+        """Items queued, in process or waiting on a delay; ``timers_within``: only the delayed
+        ones due within that many seconds (a requeue a period away is not outstanding work)."""
+        n = len(self._queue) + len(self._processing)
+        if timers_within is None or not self._waiting_when:
+            return n + len(self._waiting)
+        due = asyncio.get_running_loop().time() + timers_within
+        return n + sum(1 for w in self._waiting_when.values() if w <= due)

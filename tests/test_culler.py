@@ -423,3 +423,45 @@ def test_node_agent_endpoint_brackets_ipv6_host_ips():
     assert a.default_endpoint({"status": {"hostIP": "fd00:10:244::5"}}) == "[fd00:10:244::5]:9464"
     assert a.default_endpoint({"status": {"hostIP": "node-3.example"}}) == "node-3.example:9464"
     assert a.default_endpoint({"status": {}}) is None
+
+
+class _NoCache:
+    def get(self, kind, name, namespace):
+        return None  # read through the client
+
+
+class _PatchRecorder:
+    """A client that records the culler's Notebook patches (``CullingReconciler._update``)."""
+
+    def __init__(self, nb):
+        self.nb, self.patches = nb, []
+
+    async def get(self, kind, name, namespace):
+        return self.nb
+
+    async def patch(self, kind, body, ptype, name, namespace):
+        self.patches.append(body)
+        return self.nb
+
+
+def test_culler_write_rules(run):
+    """Its own activity annotations go without a resourceVersion precondition (nobody else
+    writes them: preconditioned, the first one conflicted with the notebook controller's status
+    write of the same moment on every notebook); a stop keeps the precondition; a notebook
+    being deleted is not written."""
+    nb = notebook("n", "s")
+    nb["metadata"]["resourceVersion"] = "7"
+    cl = _PatchRecorder(nb)
+    rec = c.CullingReconciler(cl, reader=_NoCache(), env={"ENABLE_CULLING": "true"})
+    req = c.Request("s", "n")
+
+    async def go():
+        await rec._update(req, lambda cur: c.initialize_annotations(cur, None))
+        await rec._update(req, lambda cur: c.set_stop_annotation(cur, None))
+        nb["metadata"]["deletionTimestamp"] = rfc3339()
+        await rec._update(req, lambda cur: c.initialize_annotations(cur, None))
+    run(go())
+    first, stop = cl.patches
+    assert set(first["metadata"]["annotations"]) == {LAST_ACTIVITY_ANNOTATION, LAST_ACTIVITY_CHECK_TIMESTAMP_ANNOTATION}
+    assert "resourceVersion" not in first["metadata"]
+    assert STOP_ANNOTATION in stop["metadata"]["annotations"] and stop["metadata"]["resourceVersion"] == "7"

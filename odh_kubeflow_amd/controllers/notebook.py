@@ -45,6 +45,7 @@ from typing import List, Mapping, Optional, Tuple
 from ..models import kinds
 from ..models import meta as m
 from ..models.errors import ApiError, is_already_exists, is_not_found
+from ..models.scheme import SCHEME
 from ..models.notebook import (ANNOTATION_HEADERS_REQUEST_SET, ANNOTATION_NOTEBOOK_RESTART, ANNOTATION_REWRITE_URI,
                                CULLER_HEARTBEAT_ANNOTATIONS, DEFAULT_CONTAINER_PORT, DEFAULT_FS_GROUP,
                                DEFAULT_SERVING_PORT, GPU_RESOURCE, MAX_STATEFULSET_NAME_LENGTH, NOTEBOOK_NAME_LABEL,
@@ -626,6 +627,21 @@ def nb_name_from_involved_object(reader, obj_ref: dict) -> Optional[str]:
     return None
 
 
+# what the re-emitter reads of an Event: its cache holds every Pod/StatefulSet Event of its
+# namespaces until the Event expires (kube-apiserver's --event-ttl, an hour), so it keeps
+# only these (a third of a full Event's size)
+_EVENT_FIELDS = ("apiVersion", "kind", "involvedObject", "reason", "message", "type")
+_EVENT_META = ("name", "namespace", "uid", "resourceVersion")
+
+
+def slim_event(ev: dict) -> dict:
+    """The re-emitter's cache transform for Events."""
+    md = ev.get("metadata") or {}
+    out = {k: ev[k] for k in _EVENT_FIELDS if k in ev}
+    out["metadata"] = {k: md[k] for k in _EVENT_META if k in md}
+    return out
+
+
 class NotebookEventReemitter:
     """Re-emits Pod/StatefulSet events onto their Notebook as ``Reissued from <kind>/<name>: <msg>``."""
 
@@ -670,6 +686,9 @@ class NotebookEventReemitter:
         cache = getattr(mgr, "cache", None) or mgr.reader
         if hasattr(cache, "set_field_selector"):
             cache.set_field_selector(kinds.EVENT, self.EVENT_FIELD_SELECTOR)
+        transforms = getattr(cache, "transforms", None)
+        if transforms is not None:
+            transforms.setdefault(SCHEME.resolve(kinds.EVENT).key, slim_event)
         b = mgr.builder().named("notebook-events").for_(kinds.EVENT, [pred])
         if max_concurrent is not None:
             b.with_options(max_concurrent_reconciles=max_concurrent)

@@ -90,3 +90,22 @@ def test_no_running_loop_is_a_no_op():
     rec = EventRecorder(_Client(), "x")
     rec.event(_pod(1), "Normal", "Started", "m")
     assert rec.emitted == 1 and not rec._seen
+
+
+def test_reemitter_caches_slim_events():
+    """The re-emitter's cache keeps what it reads of a platform Event, and nothing else (its
+    cache holds every Pod/StatefulSet Event of its namespaces until the Event expires)."""
+    from odh_kubeflow_amd.controllers.notebook import slim_event
+
+    ev = {"apiVersion": "v1", "kind": "Event",
+          "metadata": {"name": "nb-0.1", "namespace": "ns", "uid": "u", "resourceVersion": "9",
+                       "creationTimestamp": "2026-01-01T00:00:00Z", "managedFields": [{"manager": "x"}]},
+          "involvedObject": {"kind": "Pod", "name": "nb-0", "namespace": "ns"},
+          "reason": "Started", "message": "started container", "type": "Normal",
+          "source": {"component": "kubelet", "host": "node"}, "count": 3,
+          "firstTimestamp": "2026-01-01T00:00:00Z", "lastTimestamp": "2026-01-01T00:00:01Z",
+          "reportingComponent": "kubelet", "reportingInstance": "node"}
+    s = slim_event(ev)
+    assert set(s) == {"apiVersion", "kind", "metadata", "involvedObject", "reason", "message", "type"}
+    assert s["metadata"] == {"name": "nb-0.1", "namespace": "ns", "uid": "u", "resourceVersion": "9"}
+    assert s["involvedObject"] is ev["involvedObject"]

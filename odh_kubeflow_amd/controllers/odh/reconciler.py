@@ -323,6 +323,37 @@ class OpenshiftNotebookReconciler:
                 cur = await live.get(NOTEBOOK_KIND, req.name, req.namespace)
         return cur
 
+    async def _drop_finalizers(self, nb: dict, done: List[str]) -> None:
+        """Remove the finalizers whose cleanup succeeded: a JSON patch that ``test``s the
+        finalizer list it rewrites, as :meth:`_add_finalizers_and_unlock` adds them.  The
+        reference's whole-object update (:195-321) conflicted with any write of the same
+        moments — the culler's annotation patch admitted while the notebook was being deleted,
+        on half the notebooks deleted right after they became Ready — and paid a re-read and a
+        second admission.  A failed test (HTTP 422: the list changed) re-reads and tries again."""
+        cur = nb
+        live = getattr(self.client, "writer", self.client)
+        for attempt in range(5):
+            fins = list((cur.get("metadata") or {}).get("finalizers") or [])
+            keep = [f for f in fins if f not in done]
+            if keep == fins:
+                return
+            try:
+                await self.client.patch(cur, [{"op": "test", "path": "/metadata/finalizers", "value": fins},
+                                              {"op": "replace", "path": "/metadata/finalizers", "value": keep}],
+                                        "json")
+                return
+            except ApiError as e:
+                if is_not_found(e):
+                    return
+                if e.code != 422 or attempt == 4:
+                    raise
+            try:
+                cur = await live.get(NOTEBOOK_KIND, m.name(nb), m.namespace(nb))
+            except ApiError as e:
+                if is_not_found(e):
+                    return
+                raise
+
     async def _reconcile_reference_order(self, req: Request, nb: dict, want: List[str]) -> Result:
         """Reference emulation (``--reference-emulation``): finalizers → requeue, then every
         child strictly in the reference's order, then the (blocking) lock removal."""
@@ -400,21 +431,7 @@ class OpenshiftNotebookReconciler:
             elif fin is not None:
                 done.append(fin)
         if done:
-            async def drop():
-                try:
-                    cur = await self.client.get(NOTEBOOK_KIND, m.name(nb), m.namespace(nb))
-                except ApiError as e:
-                    if is_not_found(e):
-                        return
-                    raise
-                if any([m.remove_finalizer(cur, f) for f in done]):
-                    try:
-                        await self.client.update(cur)
-                    except ApiError as e:
-                        if not is_not_found(e):
-                            raise
-
-            await retry_on_conflict(drop)
+            await self._drop_finalizers(nb, done)
         self._lock_wait_start.pop(m.uid(nb), None)
         if errors:
             if len(errors) == 1:

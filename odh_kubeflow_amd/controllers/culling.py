@@ -607,23 +607,23 @@ class CullingReconciler:
             return self.reader.get(kind, name, namespace)
         return await self.client.get_or_none(kind, name, namespace)
 
-    # the annotations only the culler writes: a patch that sets nothing else needs no
-    # resourceVersion precondition (see _update)
+    # the annotations only the culler writes (see _update)
     OWN_ANNOTATIONS = frozenset((LAST_ACTIVITY_ANNOTATION, LAST_ACTIVITY_CHECK_TIMESTAMP_ANNOTATION))
 
-    async def _update(self, req: Request, mutate: Callable[[dict], None]) -> None:
+    async def _update(self, req: Request, mutate: Callable[[dict], None], precondition: bool = True) -> None:
         """``RetryOnConflict{Get; mutate; Update}`` (:106-112, :171-196), written as a merge patch
-        of the annotations the culler changed, without re-sending (and the apiserver
-        re-validating) the whole pod template on every check of every notebook.  A mutation
-        that changes nothing writes nothing (kube-apiserver skips no-op updates too).
+        of the annotations the culler changed, preconditioned on the resourceVersion it read —
+        the same optimistic concurrency as the reference's Update, without re-sending (and the
+        apiserver re-validating) the whole pod template on every check of every notebook.  A
+        mutation that changes nothing writes nothing (kube-apiserver skips no-op updates too),
+        and a notebook being deleted is not written at all.
 
-        A patch that touches only the culler's own activity annotations carries no
-        resourceVersion precondition: nobody else writes them, and preconditioned, the first
-        one conflicted with the notebook controller's status write of the same moment on every
-        notebook, and its retry then landed on the notebook being deleted, conflicting with the
-        odh controller's finalizer removal in turn.  A patch that stops the notebook (or removes
-        the annotations) keeps the reference's optimistic concurrency: it is decided on the
-        version read.  A notebook being deleted is not written at all."""
+        ``precondition=False`` (the first annotations of a notebook, written the moment its pod
+        is up): a patch that sets only the culler's own activity annotations, which nobody else
+        writes, goes without the precondition.  Preconditioned, it conflicted with the notebook
+        controller's status write of the same moment on every notebook, and its retry then
+        landed on notebooks being deleted.  The periodic checks keep it: the precondition is
+        also what lets the client recognise the write's watch echo as its own."""
         from ..runtime.client import LIVE_READS
 
         async def fn():
@@ -643,7 +643,7 @@ class CullingReconciler:
             if not diff:
                 return
             meta = {"annotations": diff}
-            if not all(k in self.OWN_ANNOTATIONS and v is not None for k, v in diff.items()):
+            if precondition or not all(k in self.OWN_ANNOTATIONS and v is not None for k, v in diff.items()):
                 meta["resourceVersion"] = md.get("resourceVersion")
             try:
                 await self.client.patch(kinds.NOTEBOOK_V1BETA1, {"metadata": meta}, "merge",
@@ -688,7 +688,7 @@ class CullingReconciler:
         if not annotations_exist(nb):
             born = pod_created_at(pod) if starting else None
             await self._update(req, lambda cur: initialize_annotations(
-                cur, rfc3339(born) if born is not None else None))
+                cur, rfc3339(born) if born is not None else None), precondition=False)
             nb = await self._read(kinds.NOTEBOOK_V1BETA1, req.name, req.namespace)
             if nb is None:
                 return Result()

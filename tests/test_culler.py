@@ -445,10 +445,10 @@ class _PatchRecorder:
 
 
 def test_culler_write_rules(run):
-    """Its own activity annotations go without a resourceVersion precondition (nobody else
-    writes them: preconditioned, the first one conflicted with the notebook controller's status
-    write of the same moment on every notebook); a stop keeps the precondition; a notebook
-    being deleted is not written."""
+    """A notebook's first activity annotations go without a resourceVersion precondition
+    (nobody else writes them: preconditioned, they conflicted with the notebook controller's
+    status write of the same moment on every notebook); periodic checks and a stop keep it;
+    a notebook being deleted is not written."""
     nb = notebook("n", "s")
     nb["metadata"]["resourceVersion"] = "7"
     cl = _PatchRecorder(nb)
@@ -456,12 +456,14 @@ def test_culler_write_rules(run):
     req = c.Request("s", "n")
 
     async def go():
-        await rec._update(req, lambda cur: c.initialize_annotations(cur, None))
-        await rec._update(req, lambda cur: c.set_stop_annotation(cur, None))
+        await rec._update(req, lambda cur: c.initialize_annotations(cur, None), precondition=False)
+        await rec._update(req, lambda cur: c.update_check_timestamp(cur))  # a periodic check
+        await rec._update(req, lambda cur: c.set_stop_annotation(cur, None), precondition=False)
         nb["metadata"]["deletionTimestamp"] = rfc3339()
-        await rec._update(req, lambda cur: c.initialize_annotations(cur, None))
+        await rec._update(req, lambda cur: c.initialize_annotations(cur, None), precondition=False)
     run(go())
-    first, stop = cl.patches
+    first, check, stop = cl.patches
     assert set(first["metadata"]["annotations"]) == {LAST_ACTIVITY_ANNOTATION, LAST_ACTIVITY_CHECK_TIMESTAMP_ANNOTATION}
     assert "resourceVersion" not in first["metadata"]
+    assert check["metadata"]["resourceVersion"] == "7"
     assert STOP_ANNOTATION in stop["metadata"]["annotations"] and stop["metadata"]["resourceVersion"] == "7"

@@ -2908,9 +2908,17 @@ void serve_watch(int fd, Res& r, const Path& p, const Request& rq) {
       Hist& h = *wh;
       std::unique_lock<std::mutex> lk(b.hmu);
       // system_clock deadline: libstdc++ maps a steady_clock wait to pthread_cond_clockwait,
-      // which ThreadSanitizer (GCC 11) does not intercept; the 500 ms timeout only paces
-      // catch-up scans, so a wall-clock jump is harmless here
-      slot.cv.wait_until(lk, std::chrono::system_clock::now() + std::chrono::milliseconds(500),
+      // which ThreadSanitizer (GCC 11) does not intercept.  The timeout only paces the stream's
+      // own checks (client gone; the watch deadline and the next bookmark cap it): catch-up
+      // scans of a filtered watcher are emit()'s periodic wake-ups.  At 500 ms, thousands of per-namespace watch
+      // threads waking twice a second were a third of the server's watch CPU at 64 namespaces
+      // per rank; a wall-clock jump is harmless here
+      auto nap = std::chrono::duration_cast<std::chrono::milliseconds>(deadline - std::chrono::steady_clock::now());
+      if (bookmarks)
+        nap = std::min(nap, std::chrono::duration_cast<std::chrono::milliseconds>(
+                                last_write + std::chrono::seconds(10) - std::chrono::steady_clock::now()));
+      nap = std::max(std::chrono::milliseconds(1), std::min(nap, std::chrono::milliseconds(5000)));
+      slot.cv.wait_until(lk, std::chrono::system_clock::now() + nap,
                          [&] { return h.seq > last_seq || g_stop.load(); });
       if (h.seq > last_seq) {
         if (!h.hist.empty() && h.hist.front().seq > last_seq + 1) {

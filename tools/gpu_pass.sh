@@ -412,9 +412,12 @@ PY
       timeout -k 10 400 python tools/bench_real_pods.py --notebooks 1,8 --repeats 5 --gpu-probe off \
         --gpu-init before-ready > "$out/realpods_before_ready.log" 2>&1 || fail realbr $? "$out/realpods_before_ready.log"
       grep '^{' "$out/realpods_before_ready.log" ;;
-    realref)
-      timeout -k 10 400 python tools/bench_real_pods.py --notebooks 1,8 --repeats 1 --reference-emulation \
-        > "$out/realpods_ref.log" 2>&1 || fail realref $? "$out/realpods_ref.log"
+    realref)  # the reference behaviour stalls 6 s per notebook in silence: print a heartbeat meanwhile
+      ( while sleep 30; do echo "realref running"; done ) & hb=$!
+      timeout -k 10 240 python tools/bench_real_pods.py --notebooks 1,8 --repeats 1 --reference-emulation \
+        > "$out/realpods_ref.log" 2>&1; rc=$?
+      kill $hb
+      [ $rc -eq 0 ] || fail realref $rc "$out/realpods_ref.log"
       grep '^{' "$out/realpods_ref.log" ;;
     refemu)
       timeout -k 10 200 python bench.py --reference-emulation --steps 3 --warmup 1 --no-inprocess-baseline \

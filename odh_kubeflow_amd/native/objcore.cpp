@@ -230,6 +230,22 @@ struct Parser {
   const char* p;
   const char* end;
   std::string buf;  // scratch for unescaped strings and number text
+  // owned references of the objects and arrays being built, innermost last: a container's
+  // members are collected here (one allocation for the whole document, not one per dict)
+  std::vector<PyObject*> stack;
+};
+
+// a container's run of owned references on ps.stack, released (and popped) on every exit
+struct Frame {
+  Parser& ps;
+  size_t base;
+  explicit Frame(Parser& p) : ps(p), base(p.stack.size()) {}
+  ~Frame() {
+    for (size_t i = base; i < ps.stack.size(); ++i) Py_XDECREF(ps.stack[i]);
+    ps.stack.resize(base);
+  }
+  size_t size() const { return ps.stack.size() - base; }
+  PyObject*& at(size_t i) { return ps.stack[base + i]; }
 };
 
 // interned object keys: the small vocabulary of Kubernetes field names, decoded once; the
@@ -437,6 +453,26 @@ PyObject* number_value(Parser& ps, PyObject* old) {
     }
   }
   if (ps.p == start || (ps.p - start == 1 && *start == '-')) return fail(ps, "bad number");
+  if (!is_float) {  // the common case, at most 18 digits: no copy, no strtoll
+    const char* q = start;
+    const bool neg = *q == '-';
+    if (neg) ++q;
+    if (ps.p - q <= 18 && (ps.p - q == 1 || *q != '0')) {
+      long long v = 0;
+      for (; q < ps.p; ++q) v = v * 10 + (*q - '0');
+      if (neg) v = -v;
+      if (old && PyLong_CheckExact(old)) {
+        int overflow = 0;
+        long long ov = PyLong_AsLongLongAndOverflow(old, &overflow);
+        if (!overflow && ov == v && !PyErr_Occurred()) {
+          Py_INCREF(old);
+          return old;
+        }
+        PyErr_Clear();
+      }
+      return PyLong_FromLongLong(v);
+    }
+  }
   ps.buf.assign(start, ps.p - start);
   if (!is_float) {
     errno = 0;
@@ -469,22 +505,16 @@ PyObject* number_value(Parser& ps, PyObject* old) {
 
 PyObject* value(Parser& ps, PyObject* old, int depth);
 
-struct Members {  // owned (key, value) references, released unless handed to a dict
-  std::vector<std::pair<PyObject*, PyObject*>> kv;
-  ~Members() {
-    for (auto& x : kv) {
-      Py_XDECREF(x.first);
-      Py_XDECREF(x.second);
-    }
-  }
-};
-
 PyObject* object_value(Parser& ps, PyObject* old, int depth) {
   // ps.p just past '{'.  With an old dict the members are collected first: an unchanged
   // object is the old one, and no dict is built for it.
   PyObject* od = (old && PyDict_CheckExact(old)) ? old : nullptr;
-  Members m;
+  Frame f(ps);  // key, value, key, value, ...
   bool same = od != nullptr;
+  // the old dict's members in order: a re-sent object lists its keys in the same order, so
+  // the i-th key is usually the old i-th one (no hashing, no lookup)
+  Py_ssize_t pos = 0;
+  bool in_step = od != nullptr;
   ws(ps);
   if (ps.p < ps.end && *ps.p == '}') {
     ++ps.p;
@@ -497,17 +527,32 @@ PyObject* object_value(Parser& ps, PyObject* old, int depth) {
       Py_ssize_t kn;
       bool kascii;
       if (!scan_string(ps, &ks, &kn, &kascii)) return nullptr;
-      PyObject* key = key_object(ks, kn, kascii);
-      if (!key) return nullptr;
-      m.kv.emplace_back(key, nullptr);
+      PyObject* key = nullptr;
+      PyObject* ov = nullptr;
+      if (in_step) {
+        PyObject *k2, *v2;
+        if (PyDict_Next(od, &pos, &k2, &v2) && PyUnicode_CheckExact(k2) && PyUnicode_IS_ASCII(k2) && kascii &&
+            PyUnicode_GET_LENGTH(k2) == kn && std::memcmp(PyUnicode_DATA(k2), ks, static_cast<size_t>(kn)) == 0) {
+          key = k2;
+          Py_INCREF(key);
+          ov = v2;
+        } else {
+          in_step = false;
+        }
+      }
+      if (!key) {
+        key = key_object(ks, kn, kascii);
+        if (!key) return nullptr;
+        ov = od ? PyDict_GetItemWithError(od, key) : nullptr;
+        if (!ov && PyErr_Occurred()) PyErr_Clear();
+      }
+      ps.stack.push_back(key);
       ws(ps);
       if (ps.p >= ps.end || *ps.p != ':') return fail(ps, "expected ':'");
       ++ps.p;
-      PyObject* ov = od ? PyDict_GetItemWithError(od, key) : nullptr;
-      if (!ov && PyErr_Occurred()) PyErr_Clear();
       PyObject* v = value(ps, ov, depth + 1);
       if (!v) return nullptr;
-      m.kv.back().second = v;
+      ps.stack.push_back(v);
       if (v != ov) same = false;
       ws(ps);
       if (ps.p < ps.end && *ps.p == ',') {
@@ -521,16 +566,17 @@ PyObject* object_value(Parser& ps, PyObject* old, int depth) {
       return fail(ps, "expected ',' or '}'");
     }
   }
+  const Py_ssize_t n = static_cast<Py_ssize_t>(f.size() / 2);
   // every member is the old one's and there are as many (a duplicate key cannot make up for
   // a missing one: its value would have to be the old value of two different keys)
-  if (same && depth > 0 && static_cast<Py_ssize_t>(m.kv.size()) == PyDict_GET_SIZE(od)) {
+  if (same && depth > 0 && n == PyDict_GET_SIZE(od)) {
     Py_INCREF(od);
     return od;
   }
-  PyObject* out = _PyDict_NewPresized(static_cast<Py_ssize_t>(m.kv.size()));
+  PyObject* out = _PyDict_NewPresized(n);
   if (!out) return nullptr;
-  for (auto& x : m.kv) {
-    if (PyDict_SetItem(out, x.first, x.second) < 0) {
+  for (Py_ssize_t i = 0; i < n; ++i) {
+    if (PyDict_SetItem(out, f.at(2 * i), f.at(2 * i + 1)) < 0) {
       Py_DECREF(out);
       return nullptr;
     }
@@ -540,24 +586,18 @@ PyObject* object_value(Parser& ps, PyObject* old, int depth) {
 
 PyObject* array_value(Parser& ps, PyObject* old, int depth) {
   PyObject* ol = (old && PyList_CheckExact(old)) ? old : nullptr;
-  std::vector<PyObject*> items;
-  struct Release {
-    std::vector<PyObject*>& v;
-    ~Release() {
-      for (PyObject* o : v) Py_XDECREF(o);
-    }
-  } release{items};
+  Frame f(ps);
   bool same = ol != nullptr;
   ws(ps);
   if (ps.p < ps.end && *ps.p == ']') {
     ++ps.p;
   } else {
     while (true) {
-      Py_ssize_t i = static_cast<Py_ssize_t>(items.size());
+      Py_ssize_t i = static_cast<Py_ssize_t>(f.size());
       PyObject* ov = (ol && i < PyList_GET_SIZE(ol)) ? PyList_GET_ITEM(ol, i) : nullptr;
       PyObject* v = value(ps, ov, depth + 1);
       if (!v) return nullptr;
-      items.push_back(v);
+      ps.stack.push_back(v);
       if (v != ov) same = false;
       ws(ps);
       if (ps.p < ps.end && *ps.p == ',') {
@@ -571,15 +611,16 @@ PyObject* array_value(Parser& ps, PyObject* old, int depth) {
       return fail(ps, "expected ',' or ']'");
     }
   }
-  if (same && depth > 0 && static_cast<Py_ssize_t>(items.size()) == PyList_GET_SIZE(ol)) {
+  const size_t n = f.size();
+  if (same && depth > 0 && static_cast<Py_ssize_t>(n) == PyList_GET_SIZE(ol)) {
     Py_INCREF(ol);
     return ol;
   }
-  PyObject* out = PyList_New(static_cast<Py_ssize_t>(items.size()));
+  PyObject* out = PyList_New(static_cast<Py_ssize_t>(n));
   if (!out) return nullptr;
-  for (size_t i = 0; i < items.size(); ++i) {
-    PyList_SET_ITEM(out, static_cast<Py_ssize_t>(i), items[i]);  // the reference moves
-    items[i] = nullptr;
+  for (size_t i = 0; i < n; ++i) {
+    PyList_SET_ITEM(out, static_cast<Py_ssize_t>(i), f.at(i));  // the reference moves
+    f.at(i) = nullptr;
   }
   return out;
 }
@@ -610,6 +651,18 @@ PyObject* value(Parser& ps, PyObject* old, int depth) {
   }
   if (c == '"') {
     ++ps.p;
+    if (old && PyUnicode_CheckExact(old) && PyUnicode_IS_ASCII(old)) {
+      // the old string verbatim, closing quote included, with no quote or backslash inside:
+      // it is the old string (one memcmp, no scan, no allocation)
+      const Py_ssize_t on = PyUnicode_GET_LENGTH(old);
+      const char* od = static_cast<const char*>(PyUnicode_DATA(old));
+      if (ps.end - ps.p > on && ps.p[on] == '"' && std::memcmp(ps.p, od, static_cast<size_t>(on)) == 0 &&
+          !std::memchr(ps.p, '"', static_cast<size_t>(on)) && !std::memchr(ps.p, '\\', static_cast<size_t>(on))) {
+        ps.p += on + 1;
+        Py_INCREF(old);
+        return old;
+      }
+    }
     const char* s;
     Py_ssize_t n;
     bool ascii;

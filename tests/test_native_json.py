@@ -106,3 +106,24 @@ def test_event_lookup_and_fallbacks():
             oc.loads_shared(bad)
     with pytest.raises(ZeroDivisionError):  # a failing lookup surfaces, nothing is half-built
         oc.loads_event(line.encode(), lambda ns, name: 1 / 0)
+
+
+@pytest.mark.parametrize("new_text, old", [
+    # the old string verbatim, but the new JSON string ends earlier: an escaped quote inside
+    ('{"s": "a\\"b", "t": 1}', {"s": 'a"b', "t": 1}),
+    ('{"s": "a\\\\", "t": "x"}', {"s": "a\\", "t": "x"}),
+    ('{"s": "ab", "t": "x"}', {"s": 'ab"', "t": "x"}),  # old longer than the new string
+    ('{"s": "a\\u0062", "t": 2}', {"s": "ab", "t": 2}),  # an escape spelling the same text
+    ('{"s": "\\/x"}', {"s": "/x"}),
+    ('{"b": 1, "a": 2}', {"a": 2, "b": 1}),  # the keys in another order
+    ('{"a": 1, "c": 3, "b": 2}', {"a": 1, "b": 2}),  # a key added in the middle
+    ('{"a": 1}', {"a": 1, "b": 2}),  # a key removed
+    ('{"a": {"x": "y"}, "b": [1, -0, 123456789012345678, 1234567890123456789012]}',
+     {"a": {"x": "y"}, "b": [1, 0, 123456789012345678, 1234567890123456789012]}),
+])
+def test_fast_paths_against_the_old_version(new_text, old):
+    """The decoder's shortcuts against the old version (a string compared verbatim, the keys
+    walked in the old dict's order) give json.loads's answer whatever the old version holds."""
+    got = oc.loads_shared(new_text, old)
+    assert got == json.loads(new_text) and list(got) == list(json.loads(new_text))
+    _identities(got, old)

@@ -27,6 +27,8 @@
 #include <Python.h>
 
 #include <cerrno>
+#include <cmath>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <string>
@@ -916,7 +918,144 @@ done:
   return ret;
 }
 
+// ------------------------------------------------------------------ encoding
+// dumps(obj) -> bytes: json.dumps(obj, separators=(",", ":")) for JSON trees (dict with str
+// keys, list, tuple, str, int, float, bool, None), written as UTF-8 rather than \u escapes.
+// Anything else raises TypeError, and the caller falls back to json.dumps (which also
+// reports cycles, deeper than the 512 levels taken here).
+
+bool enc_value(std::string& out, PyObject* o, int depth);
+
+void enc_string(std::string& out, PyObject* u) {
+  Py_ssize_t n;
+  const char* s = PyUnicode_AsUTF8AndSize(u, &n);
+  out.push_back('"');
+  const char* run = s;
+  for (Py_ssize_t i = 0; i < n; ++i) {
+    unsigned char c = static_cast<unsigned char>(s[i]);
+    if (c >= 0x20 && c != '"' && c != '\\') continue;
+    out.append(run, static_cast<size_t>(s + i - run));
+    run = s + i + 1;
+    switch (c) {
+      case '"': out.append("\\\""); break;
+      case '\\': out.append("\\\\"); break;
+      case '\n': out.append("\\n"); break;
+      case '\r': out.append("\\r"); break;
+      case '\t': out.append("\\t"); break;
+      case '\b': out.append("\\b"); break;
+      case '\f': out.append("\\f"); break;
+      default: {
+        char u4[8];
+        std::snprintf(u4, sizeof u4, "\\u%04x", c);
+        out.append(u4);
+      }
+    }
+  }
+  out.append(run, static_cast<size_t>(s + n - run));
+  out.push_back('"');
+}
+
+bool enc_value(std::string& out, PyObject* o, int depth) {
+  if (depth > 512) {
+    PyErr_SetString(PyExc_ValueError, "too deep");
+    return false;
+  }
+  if (PyUnicode_Check(o)) {
+    if (PyUnicode_IS_ASCII(o) || PyUnicode_AsUTF8(o)) {
+      enc_string(out, o);
+      return true;
+    }
+    return false;  // unpaired surrogates: json.dumps escapes them
+  }
+  if (o == Py_None) {
+    out.append("null");
+    return true;
+  }
+  if (o == Py_True) {
+    out.append("true");
+    return true;
+  }
+  if (o == Py_False) {
+    out.append("false");
+    return true;
+  }
+  if (PyLong_CheckExact(o)) {
+    int overflow = 0;
+    long long v = PyLong_AsLongLongAndOverflow(o, &overflow);
+    if (!overflow && !(v == -1 && PyErr_Occurred())) {
+      char b[24];
+      int k = std::snprintf(b, sizeof b, "%lld", v);
+      out.append(b, static_cast<size_t>(k));
+      return true;
+    }
+    PyErr_Clear();
+    PyObject* t = PyObject_Str(o);
+    if (!t) return false;
+    Py_ssize_t n;
+    const char* d = PyUnicode_AsUTF8AndSize(t, &n);
+    if (d) out.append(d, static_cast<size_t>(n));
+    Py_DECREF(t);
+    return d != nullptr;
+  }
+  if (PyFloat_CheckExact(o)) {
+    double d = PyFloat_AS_DOUBLE(o);
+    if (!std::isfinite(d)) {
+      out.append(std::isnan(d) ? "NaN" : (d > 0 ? "Infinity" : "-Infinity"));
+      return true;
+    }
+    char* r = PyOS_double_to_string(d, 'r', 0, Py_DTSF_ADD_DOT_0, nullptr);
+    if (!r) return false;
+    out.append(r);
+    PyMem_Free(r);
+    return true;
+  }
+  if (PyDict_CheckExact(o)) {
+    out.push_back('{');
+    Py_ssize_t pos = 0;
+    PyObject *k, *v;
+    bool first = true;
+    while (PyDict_Next(o, &pos, &k, &v)) {
+      if (!PyUnicode_CheckExact(k)) {
+        PyErr_SetString(PyExc_TypeError, "non-str key");
+        return false;
+      }
+      if (!first) out.push_back(',');
+      first = false;
+      if (!enc_value(out, k, depth + 1)) return false;
+      out.push_back(':');
+      if (!enc_value(out, v, depth + 1)) return false;
+    }
+    out.push_back('}');
+    return true;
+  }
+  if (PyList_CheckExact(o) || PyTuple_CheckExact(o)) {
+    const bool list = PyList_CheckExact(o);
+    const Py_ssize_t n = list ? PyList_GET_SIZE(o) : PyTuple_GET_SIZE(o);
+    out.push_back('[');
+    for (Py_ssize_t i = 0; i < n; ++i) {
+      if (i) out.push_back(',');
+      if (!enc_value(out, list ? PyList_GET_ITEM(o, i) : PyTuple_GET_ITEM(o, i), depth + 1)) return false;
+    }
+    out.push_back(']');
+    return true;
+  }
+  PyErr_SetString(PyExc_TypeError, "not a JSON tree");
+  return false;
+}
+
+PyObject* py_dumps(PyObject*, PyObject* o) {
+  std::string out;
+  out.reserve(1024);
+  if (!enc_value(out, o, 0)) {
+    if (!PyErr_Occurred()) PyErr_SetString(PyExc_TypeError, "not a JSON tree");
+    return nullptr;
+  }
+  return PyBytes_FromStringAndSize(out.data(), static_cast<Py_ssize_t>(out.size()));
+}
+
 PyMethodDef methods[] = {
+    {"dumps", py_dumps, METH_O,
+     "dumps(obj) -> bytes: compact JSON (json.dumps with separators=(',', ':'), UTF-8) of a JSON tree."},
     {"deepcopy", py_deepcopy, METH_O, "Deep copy of a JSON tree (dict/list; tuples become lists)."},
     {"semantic_equal", py_semantic_equal, METH_VARARGS,
      "Structural equality treating missing/None/{}/[] map values as equal."},

@@ -17,7 +17,6 @@ certificate keeps serving.
 from __future__ import annotations
 
 import asyncio
-import json
 import logging
 import os
 import ssl
@@ -25,7 +24,7 @@ import time
 from typing import Optional, Tuple
 
 from ..runtime.http1 import Http1Server
-from ..runtime.rest import loads_json  # native JSON decoding, json.loads on what it declines
+from ..runtime.rest import dumps_json, loads_json  # native JSON, json's on what it declines
 from .notebook_webhook import WEBHOOK_PATH, NotebookWebhook
 
 log = logging.getLogger("webhook.server")
@@ -116,7 +115,7 @@ class WebhookServer:
                    "response": {"uid": "", "allowed": False, "status": {"code": 400, "message": str(e)}}}
         else:
             out = await self.webhook.handle(review)
-        body = json.dumps(out, separators=(",", ":")).encode()
+        body = dumps_json(out)
         self.handle_s.append(time.perf_counter() - t0)
         return 200, "application/json", body
 

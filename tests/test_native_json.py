@@ -127,3 +127,21 @@ def test_fast_paths_against_the_old_version(new_text, old):
     got = oc.loads_shared(new_text, old)
     assert got == json.loads(new_text) and list(got) == list(json.loads(new_text))
     _identities(got, old)
+
+
+@pytest.mark.parametrize("seed", range(40))
+def test_dumps_is_compact_json_dumps(seed):
+    """``dumps`` writes what json.dumps(separators=(",", ":"), ensure_ascii=False) writes."""
+    rnd = random.Random(5000 + seed)
+    doc = {"metadata": {"name": "x"}, "spec": _rand(rnd), "list": [_rand(rnd) for _ in range(3)]}
+    assert oc.dumps(doc) == json.dumps(doc, separators=(",", ":"), ensure_ascii=False).encode("utf-8", "surrogatepass")
+
+
+def test_dumps_declines_what_is_not_a_json_tree():
+    from odh_kubeflow_amd.runtime.rest import dumps_json
+
+    for bad in ({1: "int key"}, {"a": object()}, {"a": {1, 2}}):
+        with pytest.raises(TypeError):
+            oc.dumps(bad)
+    assert dumps_json({1: "a"}) == b'{"1":"a"}'  # json.dumps's answer
+    assert dumps_json((1, "é")) == '[1,"é"]'.encode()

@@ -43,6 +43,7 @@ from ..models import kinds
 from ..models import meta as m
 from ..models.errors import ApiError, is_not_found
 from ..runtime.client import CONFIRM_ABSENCE
+from ..runtime.rest import dumps_json
 from ..tracing import current_span, get_tracer
 from ..utils import jsonpatch
 from ..utils.objutil import deepcopy_json, semantic_equal
@@ -324,7 +325,7 @@ class NotebookWebhook:
             ops = jsonpatch.create_patch(obj, mutated)
             if ops:
                 resp["patchType"] = "JSONPatch"
-                resp["patch"] = base64.b64encode(json.dumps(ops, separators=(",", ":")).encode()).decode()
+                resp["patch"] = base64.b64encode(dumps_json(ops)).decode()
         except AdmissionError as e:
             self.denied += 1
             resp = {"uid": uid, "allowed": False, "status": {"code": e.code, "message": str(e)}}

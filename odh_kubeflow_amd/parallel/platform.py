@@ -48,15 +48,25 @@ async def start_child(module: str, args: List[str], what: str, timeout: float = 
         env = dict(os.environ, PYTHONPATH=ROOT + os.pathsep + os.environ.get("PYTHONPATH", ""))
     from ..utils.procutil import child_env
 
+    import tempfile
+
+    # the child's stderr goes to an unlinked temporary file: nothing accumulates, and a child
+    # that fails to start says why in the exception
+    err = tempfile.TemporaryFile()
     proc = subprocess.Popen([sys.executable, *python_args, "-m", module, *args], cwd=ROOT, env=child_env(env),
-                            stdout=subprocess.PIPE, stderr=subprocess.DEVNULL, text=True)
+                            stdout=subprocess.PIPE, stderr=err, text=True)
     try:
         line = await asyncio.wait_for(_in_thread(proc.stdout.readline), timeout)
     except asyncio.TimeoutError:
         line = ""
     if line.strip() != "ready":
         proc.kill()
-        raise RuntimeError(f"{what} did not start (rc={proc.poll()})")
+        proc.wait()
+        err.seek(0)
+        tail = err.read()[-2000:].decode(errors="replace").strip()
+        err.close()
+        raise RuntimeError(f"{what} did not start (rc={proc.poll()})" + (f": {tail}" if tail else ""))
+    err.close()  # the child keeps writing to the unlinked file; it goes when the child does
     return proc
 
 

@@ -30,7 +30,6 @@ import asyncio
 import json
 import os
 import shutil
-import socket
 import subprocess
 from dataclasses import dataclass, field
 from typing import Callable, Dict, List, Optional
@@ -60,9 +59,9 @@ def driven(nb: dict) -> dict:
 
 
 def free_port() -> int:
-    with socket.socket() as s:
-        s.bind(("127.0.0.1", 0))
-        return s.getsockname()[1]
+    from ..utils.procutil import listen_port
+
+    return listen_port()
 
 
 @dataclass

@@ -50,7 +50,6 @@ import json
 import logging
 import os
 import re
-import socket
 import subprocess
 import sys
 import time
@@ -157,9 +156,9 @@ def strip_flags(argv: Sequence[str], with_value: Iterable[str] = (), boolean: It
 
 
 def _free_port() -> int:
-    with socket.socket() as s:
-        s.bind(("127.0.0.1", 0))
-        return s.getsockname()[1]
+    from ..utils.procutil import listen_port
+
+    return listen_port()
 
 
 # ------------------------------------------------------------------ /metrics merge

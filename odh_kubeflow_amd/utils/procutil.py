@@ -75,3 +75,46 @@ def arm_from_env() -> None:
         return
     if str(os.getppid()) != parent:  # the parent died before the signal was armed
         os.kill(os.getpid(), signal.SIGTERM)
+
+
+# ------------------------------------------------------------------ listen ports for children
+
+_port_seq = [0]
+
+
+def _ephemeral_range() -> tuple:
+    try:
+        with open("/proc/sys/net/ipv4/ip_local_port_range") as f:
+            lo, hi = (int(x) for x in f.read().split())
+            return lo, hi
+    except (OSError, ValueError):
+        return 32768, 60999
+
+
+def listen_port(host: str = "127.0.0.1") -> int:
+    """A free TCP port for a child process to listen on once it has started.
+
+    Chosen below the kernel's ephemeral range: a port picked with ``bind(0)`` is an ephemeral
+    one, and in the second or two before the child binds it, any process's outgoing
+    connection can take it as its local port (a 4-rank benchmark run lost a control-plane
+    process to that, ``profiles/r5_f7``).  Each process walks the range from its own
+    pid-derived offset, so concurrent ranks pick from different places."""
+    import socket
+
+    lo, top = 20000, _ephemeral_range()[0]
+    if top - lo < 1000:
+        lo, top = 10000, max(top, 11000)
+    span = top - lo
+    start = (os.getpid() * 7919) % span
+    for _ in range(span):
+        port = lo + (start + _port_seq[0]) % span
+        _port_seq[0] += 1
+        with socket.socket() as s:
+            try:
+                s.bind((host, port))
+            except OSError:
+                continue
+            return port
+    with socket.socket() as s:  # the whole range in use: fall back to the kernel's choice
+        s.bind((host, 0))
+        return s.getsockname()[1]

@@ -366,9 +366,15 @@ class Http1Server:
     """
 
     def __init__(self, handler, host: str = "127.0.0.1", port: int = 0,
-                 ssl_context: Optional[_ssl.SSLContext] = None, max_body: int = 16 << 20, reuse_port: bool = False):
+                 ssl_context: Optional[_ssl.SSLContext] = None, max_body: int = 16 << 20, reuse_port: bool = False,
+                 max_requests_per_conn: int = 0):
         self.handler = handler
         self.reuse_port = reuse_port  # SO_REUSEPORT: several processes accept on one port
+        # close a keep-alive connection after this many requests (0: never).  SO_REUSEPORT
+        # spreads connections, not requests: a client holding a few long-lived connections (the
+        # apiserver's webhook pool) can leave a listener idle for good; making it reconnect
+        # now and then lets the kernel spread its connections again
+        self.max_requests_per_conn = max_requests_per_conn
         self.host = host
         self.port = port
         self.ssl = ssl_context
@@ -393,6 +399,7 @@ class Http1Server:
                 sock.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
             except OSError:
                 pass
+        served = 0
         try:
             while True:
                 try:
@@ -418,7 +425,9 @@ class Http1Server:
                         status, ctype, body = await self.handler(method, target.split("?", 1)[0], headers, data)
                     except Exception as e:  # the handler's bug must not kill the connection loop
                         status, ctype, body = 500, "text/plain", repr(e).encode()
-                close = headers.get("connection", "").lower() == "close"
+                served += 1
+                close = headers.get("connection", "").lower() == "close" or (
+                    self.max_requests_per_conn > 0 and served >= self.max_requests_per_conn)
                 head = (f"HTTP/1.1 {status} {_REASONS.get(status, 'OK')}\r\nContent-Type: {ctype}\r\n"
                         f"Content-Length: {len(body)}\r\n{'Connection: close' + chr(13) + chr(10) if close else ''}\r\n")
                 writer.write(head.encode("latin-1") + body)

@@ -1688,8 +1688,9 @@ bool tls_write_all(TlsConn& c, const std::string& s) {
   return true;
 }
 
-// minimal HTTP/1.1 response reader (Content-Length or chunked)
-bool tls_read_response(TlsConn& c, int* status, std::string* body) {
+// minimal HTTP/1.1 response reader (Content-Length or chunked); *close: the server will
+// close the connection after this response (Connection: close), so it is not pooled
+bool tls_read_response(TlsConn& c, int* status, std::string* body, bool* close = nullptr) {
   std::string buf;
   char tmp[16384];
   size_t hdr_end;
@@ -1703,6 +1704,7 @@ bool tls_read_response(TlsConn& c, int* status, std::string* body) {
   *status = std::atoi(head.c_str() + head.find(' ') + 1);
   std::string lower = head;
   std::transform(lower.begin(), lower.end(), lower.begin(), ::tolower);
+  if (close) *close = lower.find("connection: close") != std::string::npos;
   size_t cl = lower.find("content-length:");
   if (cl != std::string::npos) {
     size_t len = std::stoul(lower.substr(cl + 15));
@@ -1793,7 +1795,9 @@ Value call_webhook(const Webhook& w, const Value& review) {
     }
     int status = 0;
     std::string resp;
-    if (tls_write_all(*c, req) && tls_read_response(*c, &status, &resp)) {
+    bool close = false;
+    if (tls_write_all(*c, req) && tls_read_response(*c, &status, &resp, &close)) {
+      if (close) c.reset();  // the webhook hangs up after this answer: the slot reconnects next time
       give_back(std::move(c));
       if (status != 200) throw std::runtime_error("webhook returned HTTP " + std::to_string(status));
       return kj::parse(resp);

@@ -121,8 +121,11 @@ class WebhookServer:
 
     async def start(self) -> "WebhookServer":
         self._ctx = self.ssl_context()
+        # replicas sharing the port: the apiserver's pooled connections are re-made every 1000
+        # admissions, so each replica keeps getting its share (one TLS handshake per 1000)
         self._server = await Http1Server(self._handle, self.host, self.port, self._ctx,
-                                         reuse_port=self.reuse_port).start()
+                                         reuse_port=self.reuse_port,
+                                         max_requests_per_conn=1000 if self.reuse_port else 0).start()
         self.port = self._server.port
         if self._ctx is not None and self.reload_interval > 0:
             self._watch = asyncio.ensure_future(self._watch_certs())

@@ -122,3 +122,28 @@ def test_connection_lost_mid_response_fails_the_request():
         with pytest.raises(ConnectionResetError):
             await conn.roundtrip(b"GET / HTTP/1.1\r\n\r\n")  # closed: the pool skips it
     asyncio.run(go())
+
+
+def test_server_closes_a_connection_after_max_requests():
+    """``max_requests_per_conn``: the webhook replicas sharing a port (SO_REUSEPORT) make the
+    apiserver re-connect now and then, so its pooled connections spread over them again."""
+    from odh_kubeflow_amd.runtime.http1 import Http1Server
+
+    async def handler(method, path, headers, body):
+        return 200, "text/plain", b"ok"
+
+    async def go():
+        srv = await Http1Server(handler, max_requests_per_conn=3).start()
+        r, w = await asyncio.open_connection("127.0.0.1", srv.port)
+        answers = []
+        for _ in range(3):
+            w.write(b"POST /x HTTP/1.1\r\nContent-Length: 0\r\n\r\n")
+            head = await r.readuntil(b"\r\n\r\n")
+            answers.append(head)
+            await r.readexactly(2)
+        assert b"Connection: close" not in answers[0] and b"Connection: close" not in answers[1]
+        assert b"Connection: close" in answers[2]
+        assert await r.read() == b""  # the server hung up
+        w.close()
+        await srv.stop()
+    asyncio.run(go())

@@ -177,16 +177,17 @@ for s in $steps; do
           --warmup 5 --probe-sample 0 --resident 0 > "$out/bench_workers_n$n.log" 2>&1 || fail workers $? "$out/bench_workers_n$n.log"
         show "$out/bench_workers_n$n.log" "workers4 n$n"
       done ;;
-    wrab)  # overlay mi355x at 4 streams: 1 / 2 / 4 odh webhook processes, interleaved x2, plus N=1
-      timeout -k 10 170 python bench.py --gpus 1 --arch unsharded --workers 4 --cache-configmaps --steps 100 --warmup 5 \
-        --probe-sample 0 --resident 0 --no-configs --burst 0 > "$out/bench_wrab_n1.log" 2>&1 || fail wrab $? "$out/bench_wrab_n1.log"
+    wrab)  # overlay mi355x (split kf workers) at 4 streams: 2 / 3 / 4 odh webhook processes, interleaved x2, plus N=1
+      timeout -k 10 170 python bench.py --gpus 1 --arch unsharded --workers 4 --kf-split-workers --cache-configmaps \
+        --webhook-replicas 2 --steps 100 --warmup 5 --probe-sample 0 --resident 0 --no-configs --burst 0 \
+        > "$out/bench_wrab_n1.log" 2>&1 || fail wrab $? "$out/bench_wrab_n1.log"
       show "$out/bench_wrab_n1.log" "wrab n1"
       for r in 1 2; do
-        for w in 1 2 4; do
+        for w in ${WRAB:-2 3 4}; do
           timeout -k 10 170 python -m torch.distributed.run --nnodes=1 --nproc-per-node 4 \
-            --master-addr 127.0.0.1 --master-port 2996$w bench.py --gpus 4 --arch unsharded --workers 4 --cache-configmaps \
-            --webhook-replicas $w --steps 100 --warmup 5 --probe-sample 0 --resident 0 --burst 0 \
-            > "$out/bench_wrab_wr${w}_r$r.log" 2>&1 || fail wrab $? "$out/bench_wrab_wr${w}_r$r.log"
+            --master-addr 127.0.0.1 --master-port 2996$w bench.py --gpus 4 --arch unsharded --workers 4 \
+            --kf-split-workers --cache-configmaps --webhook-replicas $w --steps 100 --warmup 5 --probe-sample 0 \
+            --resident 0 --burst 0 > "$out/bench_wrab_wr${w}_r$r.log" 2>&1 || fail wrab $? "$out/bench_wrab_wr${w}_r$r.log"
           show "$out/bench_wrab_wr${w}_r$r.log" "wrab wr$w r$r"
         done
       done ;;

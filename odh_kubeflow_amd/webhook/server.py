@@ -29,6 +29,9 @@ from .notebook_webhook import WEBHOOK_PATH, NotebookWebhook
 
 log = logging.getLogger("webhook.server")
 
+# admissions per connection before a webhook replica sharing the port closes it (see start)
+RECYCLE_AFTER = 100
+
 
 class WebhookServer:
     def __init__(self, webhook: NotebookWebhook, cert_dir: Optional[str], host: str = "0.0.0.0", port: int = 8443,
@@ -121,11 +124,13 @@ class WebhookServer:
 
     async def start(self) -> "WebhookServer":
         self._ctx = self.ssl_context()
-        # replicas sharing the port: the apiserver's pooled connections are re-made every 1000
-        # admissions, so each replica keeps getting its share (one TLS handshake per 1000)
+        # replicas sharing the port: the apiserver's pooled connections are re-made every 100
+        # admissions, so each replica keeps getting its share (one TLS handshake per 100: ~10 µs
+        # per admission).  At 1000 a 4-stream benchmark window never recycled, and one replica
+        # in two of the runs sat idle (profiles/r5_f10)
         self._server = await Http1Server(self._handle, self.host, self.port, self._ctx,
                                          reuse_port=self.reuse_port,
-                                         max_requests_per_conn=1000 if self.reuse_port else 0).start()
+                                         max_requests_per_conn=RECYCLE_AFTER if self.reuse_port else 0).start()
         self.port = self._server.port
         if self._ctx is not None and self.reload_interval > 0:
             self._watch = asyncio.ensure_future(self._watch_certs())

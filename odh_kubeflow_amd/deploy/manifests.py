@@ -102,8 +102,10 @@ MI355X_CULLER = ["CULLING_ACTIVITY_SOURCE=combined", "ENABLE_CULLING=true"]
 MI355X_WORKERS = 4
 # --webhook-replicas: at 4 streams the one webhook process (the supervisor, which also leads and
 # watches cluster-wide) ran ≈75 % busy; 1 / 2 / 4 webhook processes gave 561–572 / 586 / 598–606
-# notebooks/s, interleaved (profiles/r5_p13) — two take most of it
-MI355X_WEBHOOK_REPLICAS = 2
+# notebooks/s, interleaved (profiles/r5_p13).  With the final tree (connections recycled, so
+# every process gets its share) 3 beat 2 in every interleaved run: 751–760 vs 667–745
+# notebooks/s (profiles/r5_f10, r5_f11)
+MI355X_WEBHOOK_REPLICAS = 3
 # kf --split-workers: each namespace set served by a notebook-reconciler process and a culler +
 # event re-emitter process, as a shard pod does; with 2 webhook processes, against neither, at 4
 # streams: 607 / 627 vs 596 / 605 notebooks/s, interleaved (profiles/r5_p15; split alone

@@ -372,9 +372,9 @@ def test_mi355x_overlay_runs_manager_workers_and_webhook_replicas():
     assert "--workers=4" in kf["args"] and "--split-workers" in kf["args"]
     assert not any(a.startswith("--webhook-replicas") for a in kf["args"])
     assert kf["resources"]["requests"]["cpu"] == "6" and kf["resources"]["limits"]["cpu"] == "9"
-    assert "--workers=4" in odh["args"] and "--webhook-replicas=2" in odh["args"]
+    assert "--workers=4" in odh["args"] and "--webhook-replicas=3" in odh["args"]
     assert "--cache-configmaps-secrets=true" in odh["args"] and not any("cache-configmaps" in a for a in kf["args"])
-    assert odh["resources"]["requests"]["cpu"] == "5" and odh["resources"]["limits"]["cpu"] == "6"
+    assert odh["resources"]["requests"]["cpu"] == "6" and odh["resources"]["limits"]["cpu"] == "7"
     plain = _by(_render("standalone"), "Deployment")
     for d in plain.values():
         assert not any(a.startswith(("--workers", "--webhook-replicas", "--cache-configmaps", "--split-workers"))

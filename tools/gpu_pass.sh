@@ -165,15 +165,15 @@ for s in $steps; do
           --probe-sample 0 > "$out/bench_unsharded_n$n.log" 2>&1 || fail unsharded $? "$out/bench_unsharded_n$n.log"
         show "$out/bench_unsharded_n$n.log" "unsharded n$n"
       done ;;
-    workers)  # overlay mi355x: --workers 4 (kf split), 2 webhook processes, the odh manager's cached ConfigMaps/Secrets
+    workers)  # overlay mi355x: --workers 4 (kf split), 3 webhook processes, the odh manager's cached ConfigMaps/Secrets
       timeout -k 10 170 python bench.py --gpus 1 --arch unsharded --workers 4 --cache-configmaps --kf-split-workers \
-        --webhook-replicas 2 --steps 100 --warmup 5 --probe-sample 0 \
+        --webhook-replicas 3 --steps 100 --warmup 5 --probe-sample 0 \
         --resident 0 --no-configs > "$out/bench_workers_n1.log" 2>&1 || fail workers $? "$out/bench_workers_n1.log"
       show "$out/bench_workers_n1.log" "workers4 n1"
       for n in 2 4; do
         timeout -k 10 170 python -m torch.distributed.run --nnodes=1 --nproc-per-node $n \
           --master-addr 127.0.0.1 --master-port 2995$n bench.py --gpus $n --arch unsharded --workers 4 --cache-configmaps \
-          --kf-split-workers --webhook-replicas 2 --steps 100 \
+          --kf-split-workers --webhook-replicas 3 --steps 100 \
           --warmup 5 --probe-sample 0 --resident 0 > "$out/bench_workers_n$n.log" 2>&1 || fail workers $? "$out/bench_workers_n$n.log"
         show "$out/bench_workers_n$n.log" "workers4 n$n"
       done ;;

@@ -392,6 +392,15 @@ def test_culler_heartbeat_skips_the_pipeline_but_nothing_else_does(run):
         b2["metadata"]["annotations"][key] = val
         assert not culler_heartbeat_only(b2, o2), key
 
+    from odh_kubeflow_amd.webhook.notebook_webhook import heartbeat_update
+
+    assert heartbeat_update(beat, old)
+    bad = json.loads(json.dumps(beat))
+    bad["metadata"]["annotations"][LAST_ACTIVITY_CHECK_TIMESTAMP_ANNOTATION] = 5  # not a string: full path
+    assert not heartbeat_update(bad, old)
+    for junk in ({"metadata": []}, {"metadata": {"annotations": ["x"]}}, {}):
+        assert not heartbeat_update(junk, old)
+
     async def go():
         store, admin, wh = await _setup()
         await admin.create(notebook("nb", "user", annotations={"notebooks.opendatahub.io/inject-auth": "true"}))

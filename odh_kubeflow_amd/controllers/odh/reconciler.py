@@ -40,12 +40,14 @@ import asyncio
 import logging
 import os
 import time
+from collections import OrderedDict
 from typing import Dict, List, Mapping, Optional
 
 from ...models import kinds
 from ...models import meta as m
 from ...models.errors import ApiError, is_no_match, is_not_found
 from ...models.notebook import CULLER_HEARTBEAT_ANNOTATIONS, heartbeat_filter_enabled
+from ...runtime.client import get_live
 from ...runtime.controller import (Request, Result, controller_owner_alive, fields_changed,
                                    generation_or_metadata_changed, metadata_changed)
 from ...runtime.retry import retry_on_conflict
@@ -94,9 +96,32 @@ class OpenshiftNotebookReconciler:
         # namespace (with R resident notebooks that scan was most of a new notebook's lock release)
         self._locked: Dict[str, set] = {}
         self._tracking_locks = False
+        # UIDs of Notebooks this process has seen deleting.  ``deletionTimestamp`` is never
+        # unset, so a copy of one of them WITHOUT it is stale (an informer that has not caught
+        # up with a live read or a write response): the exposure wave must not act on it — it
+        # would recreate the cluster-scoped auth-delegator binding, the central-namespace
+        # HTTPRoute or the ReferenceGrant after the finalizers that delete them already ran,
+        # with no owner left to garbage-collect them.  Dropped at the Notebook's DELETED
+        # event (after it no cached read can return the Notebook) and bounded.
+        self._deleting_uids: "OrderedDict[str, None]" = OrderedDict()
+        self.stale_reads = 0
+
+    DELETING_UIDS_CAP = 65536
+
+    def _note_deleting(self, nb: dict) -> None:
+        uid = m.uid(nb)
+        if not uid or uid in self._deleting_uids:
+            return
+        self._deleting_uids[uid] = None
+        if len(self._deleting_uids) > self.DELETING_UIDS_CAP:
+            self._deleting_uids.popitem(last=False)
 
     def _on_notebook(self, etype: str, nb: dict, old: Optional[dict]) -> None:
         ns, name = m.namespace(nb), m.name(nb)
+        if etype == "DELETED":
+            self._deleting_uids.pop(m.uid(nb), None)
+        elif m.is_deleting(nb):
+            self._note_deleting(nb)
         if etype != "DELETED" and reconciliation_lock_enabled(nb):
             self._locked.setdefault(ns, set()).add(name)
         else:
@@ -194,7 +219,19 @@ class OpenshiftNotebookReconciler:
             if is_not_found(e):
                 return Result()
             raise
+        if not m.is_deleting(nb) and m.uid(nb) in self._deleting_uids:
+            # a pre-deletion copy of a Notebook already seen deleting: read it live
+            self.stale_reads += 1
+            try:
+                nb = await get_live(self.client, NOTEBOOK_KIND, req.name, req.namespace)
+            except ApiError as e:
+                if is_not_found(e):
+                    return Result()
+                raise
+            if not m.is_deleting(nb) and m.uid(nb) in self._deleting_uids:
+                return Result()  # cannot happen (deletion is final); never act on it
         if m.is_deleting(nb):
+            self._note_deleting(nb)
             return await self._finalize(nb)
 
         want = [f for f in (HTTPROUTE_FINALIZER, REFERENCEGRANT_FINALIZER) if not m.contains_finalizer(nb, f)]
@@ -285,6 +322,12 @@ class OpenshiftNotebookReconciler:
             if release:
                 self._lock_wait_start.pop(m.uid(nb), None)
                 self.locks_removed += 1
+        if m.is_deleting(nb) or m.uid(nb) in self._deleting_uids:
+            # deleted while the gating wave ran: the finalize pass (queued by the deletion
+            # event) owns the exposure children now — creating them here would only race it
+            if m.is_deleting(nb):
+                self._note_deleting(nb)
+            return Result(requeue=True)
         await self._gather(self._exposure_steps(nb))
         return lock_res or Result()
 

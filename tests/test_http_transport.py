@@ -236,7 +236,14 @@ def test_full_stack_over_http_with_https_webhook(run, transport):
             await cl.admin.delete(kinds.NOTEBOOK, "nb", "user")
             assert await cl.wait_for(lambda: cl.store.peek(kinds.NOTEBOOK, "nb", "user") is None, 10)
             assert await cl.wait_for(lambda: cl.store.peek(kinds.STATEFUL_SET, "nb", "user") is None, 10)  # GC
-            assert cl.store.peek(kinds.CLUSTER_ROLE_BINDING, "nb-rbac-user-auth-delegator") is None
+            # ``cl.store`` is an informer view under the native transport: each kind has its own
+            # watch stream, so the CRB's DELETED event may trail the Notebook's.  The apiserver
+            # itself is the authority: a live read must say NotFound (a leak stays found)
+            with pytest.raises(ApiError) as e:
+                await cl.admin.get(kinds.CLUSTER_ROLE_BINDING, "nb-rbac-user-auth-delegator")
+            assert is_not_found(e.value)
+            assert await cl.wait_for(
+                lambda: cl.store.peek(kinds.CLUSTER_ROLE_BINDING, "nb-rbac-user-auth-delegator") is None, 5)
     run(go(), timeout=60)
 
 

@@ -197,6 +197,59 @@ def test_kube_rbac_proxy_full_lifecycle(run):
     run(go())
 
 
+class _LaggingNotebookReads:
+    """The reconciler's client with an informer that has not caught up: cached Notebook reads
+    answer ``stale`` (a pre-deletion copy); live reads and everything else pass through."""
+
+    def __init__(self, inner, stale):
+        self._inner, self._stale = inner, stale
+
+    def __getattr__(self, name):
+        return getattr(self._inner, name)
+
+    async def get(self, kind, name, namespace=None):
+        from odh_kubeflow_amd.runtime.client import LIVE_READS
+        from odh_kubeflow_amd.utils.objutil import deepcopy_json
+
+        if not LIVE_READS.get() and kind == kinds.NOTEBOOK_V1 and name == m.name(self._stale):
+            return deepcopy_json(self._stale)
+        return await self._inner.get(kind, name, namespace)
+
+
+@pytest.mark.parametrize("auth_mode", [True, False])
+def test_stale_notebook_after_finalize_recreates_no_exposure_child(run, auth_mode):
+    """A reconcile that reads a pre-deletion Notebook from a lagging cache after the finalize
+    pass ran must not recreate the finalizer-managed children — the cluster-scoped
+    auth-delegator binding, the central-namespace HTTPRoute, the ReferenceGrant — which
+    nothing would delete again (odh/controllers/notebook_controller.go:195-321)."""
+    from odh_kubeflow_amd.runtime.controller import Request
+
+    async def go():
+        async with LocalCluster(cfg()) as cl:
+            await create_nb(cl, "nb", annotations=AUTH if auth_mode else None)
+            crb = lambda: cl.store.peek(kinds.CLUSTER_ROLE_BINDING, "nb-rbac-user-auth-delegator")  # noqa: E731
+            rg = lambda: cl.store.peek(kinds.REFERENCE_GRANT, "notebook-httproute-access", "user")  # noqa: E731
+            assert await cl.wait_for(lambda: route_for(cl, "nb") and rg() is not None
+                                     and (crb() is not None or not auth_mode))
+            assert await cl.wait_for(lambda: "kubeflow-resource-stopped" not in m.annotations(
+                cl.store.peek(kinds.NOTEBOOK, "nb", "user")))
+            stale = json.loads(json.dumps(cl.store.peek(kinds.NOTEBOOK, "nb", "user")))
+            await cl.admin.delete(kinds.NOTEBOOK, "nb", "user")
+            assert await cl.wait_for(lambda: cl.store.peek(kinds.NOTEBOOK, "nb", "user") is None)
+            assert crb() is None and rg() is None and route_for(cl, "nb") == []
+            r = cl.reconcilers["odh"]
+            await cl.odh.stop()  # nothing else reconciles from here on
+            real = r.client
+            r.client = _LaggingNotebookReads(real, stale)
+            try:
+                await r.reconcile(Request("user", "nb"))
+            finally:
+                r.client = real
+            assert crb() is None and rg() is None and route_for(cl, "nb") == []
+            assert r.stale_reads == 1
+    run(go())
+
+
 def test_mode_switching(run):
     async def go():
         async with LocalCluster(cfg()) as cl:

@@ -534,6 +534,8 @@ async def _resident(args, shard, dist, native, children: dict, use_odh: bool,
     rest_prof = _prof_per_step(prof0, prof1, 1) if prof0 and prof1 else None
     heartbeats = sum((d.get("heartbeats") or 0) - ((wh0.get(p) or {}).get("heartbeats") or 0)
                      for p, d in (wh1 or {}).items())
+    heartbeats_full = sum((d.get("heartbeats_full") or 0) - ((wh0.get(p) or {}).get("heartbeats_full") or 0)
+                          for p, d in (wh1 or {}).items())
     served = sum((d.get("served") or 0) - ((wh0.get(p) or {}).get("served") or 0) for p, d in (wh1 or {}).items())
     await _in_thread(dist.barrier)
 
@@ -571,6 +573,7 @@ async def _resident(args, shard, dist, native, children: dict, use_odh: bool,
         "k": k, "ok": ok and gone, "fill_s": fill_s, "win": win, "cpu": cpu, "rss": rss, "lat": lat,
         "in_window": breakdown_delta(b0 or {}, b1 or {}), "io": io_delta(io0 or {}, io1 or {}), "prof": rest_prof,
         "adm": (adm1 - adm0) if adm0 is not None and adm1 is not None else None, "heartbeats": heartbeats,
+        "heartbeats_full": heartbeats_full,
         "served": served, "teardown": teardown, "errors": errors, "gc": gcp})
     if rank != 0:
         return None
@@ -610,6 +613,9 @@ async def _resident(args, shard, dist, native, children: dict, use_odh: bool,
             "apiserver_writes_per_s": writes,
             "admissions_per_s": round(adm * per_s, 1) if adm is not None else None,
             "webhook_heartbeat_fast_path_per_s": round(sum(g["heartbeats"] for g in gathered) * per_s, 1),
+            # heartbeats that ran the pipeline: an input changed since the notebook's last full
+            # admission (or this webhook had not admitted it yet) — 0 at rest
+            "webhook_heartbeat_full_pipeline_per_s": round(sum(g["heartbeats_full"] for g in gathered) * per_s, 1),
             "webhook_admissions_per_s": round(sum(g["served"] for g in gathered) * per_s, 1),
             "reconciles_per_s": {ctrl: {"total": round(sum(t.values()) * per_s, 1),
                                         "by_trigger": {kk: round(v * per_s, 1) for kk, v in sorted(t.items())}}

@@ -667,6 +667,20 @@ class InformerCache(Reader, EventSource):
             return None
         return tuple((id(inf), inf.mutations) for inf in infs)
 
+    def kind_version(self, kind) -> Optional[Tuple[Tuple[int, int, bool], ...]]:
+        """:meth:`store_version` without starting an informer: ``None`` until every informer
+        of ``kind`` has synced (an uninstalled kind counts as synced and empty — the token
+        changes when it gets installed)."""
+        try:
+            info = SCHEME.resolve(kind)
+        except KeyError:
+            return None
+        g = self._groups.get(info.key)
+        infs = g.all() if g is not None else []
+        if not infs or not all(i.synced.is_set() for i in infs):
+            return None
+        return tuple((id(i), i.mutations, i.missing_kind) for i in infs)
+
     def list(self, kind, namespace=None, labels=None, fields=None, owner_uid=None) -> List[dict]:
         infs = self._for_ns(kind, namespace)
         if isinstance(labels, dict):

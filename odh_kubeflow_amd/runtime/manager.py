@@ -419,7 +419,8 @@ class Manager:
             k = max(0, min(gets - gsince, len(g)))
             out = {"served": srv.served, "handle_ms": [round(x * 1e3, 3) for x in recent],
                    "gets": gets, "get_ms": [round(x, 3) for x in g[len(g) - k:]] if k else [],
-                   "heartbeats": getattr(srv.webhook, "heartbeats", 0)}
+                   "heartbeats": getattr(srv.webhook, "heartbeats", 0),
+                   "heartbeats_full": getattr(srv.webhook, "heartbeats_full", 0)}
             reps = self.webhook_replicas
             if reps is not None:  # each replica's own window: replica_since=served:gets,served:gets,...
                 rs = [x.split(":") for x in req.query.get("replica_since", "").split(",") if x]

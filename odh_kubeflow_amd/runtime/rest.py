@@ -18,6 +18,7 @@ from __future__ import annotations
 import asyncio
 import base64
 import json
+import logging
 import os
 import ssl
 import tempfile
@@ -56,6 +57,7 @@ from ..utils.selectors import format_label_selector
 from .client import Client, _refresh, _version_of
 
 SA_DIR = "/var/run/secrets/kubernetes.io/serviceaccount"
+log = logging.getLogger("runtime.rest")
 
 
 def default_user_agent() -> str:
@@ -86,6 +88,9 @@ class RestConfig:
     burst: int = 0
     user_agent: str = field(default_factory=lambda: default_user_agent())
     extra: dict = field(default_factory=dict)
+    # a bearer token file re-read while the process runs (in-cluster: the projected, rotated
+    # ServiceAccount token; kubeconfig: ``tokenFile``) — see FileTokenSource
+    token_file: Optional[str] = None
 
     def ssl_context(self) -> Optional[ssl.SSLContext]:
         if not self.host.startswith("https"):
@@ -105,11 +110,13 @@ class RestConfig:
         host, port = os.environ.get("KUBERNETES_SERVICE_HOST"), os.environ.get("KUBERNETES_SERVICE_PORT")
         if not host or not port:
             raise RuntimeError("not running in a cluster (KUBERNETES_SERVICE_HOST unset)")
-        with open(os.path.join(SA_DIR, "token")) as f:
+        token_file = os.path.join(SA_DIR, "token")
+        with open(token_file) as f:
             token = f.read().strip()
         if ":" in host:
             host = f"[{host}]"
-        return cls(host=f"https://{host}:{port}", token=token, ca_file=os.path.join(SA_DIR, "ca.crt"))
+        return cls(host=f"https://{host}:{port}", token=token, ca_file=os.path.join(SA_DIR, "ca.crt"),
+                   token_file=token_file)
 
     @classmethod
     def from_kubeconfig(cls, path: Optional[str] = None, context: Optional[str] = None) -> "RestConfig":
@@ -138,7 +145,8 @@ class RestConfig:
                     f.write(base64.b64decode(user[key + "-data"]))
                 setattr(cfg, attr, p)
         if user.get("tokenFile"):
-            with open(user["tokenFile"]) as f:
+            cfg.token_file = user["tokenFile"]
+            with open(cfg.token_file) as f:
                 cfg.token = f.read().strip()
         return cfg
 
@@ -149,6 +157,53 @@ class RestConfig:
         if kubeconfig or os.environ.get("KUBECONFIG") or os.path.exists(os.path.expanduser("~/.kube/config")):
             return cls.from_kubeconfig(kubeconfig)
         return cls.in_cluster()
+
+
+class FileTokenSource:
+    """A bearer token read from a file and re-read while the process runs — client-go's
+    ``cachingFileTokenSource`` (``transport/token_source.go``), which every controller-runtime
+    manager of the reference gets through ``ctrl.GetConfigOrDie()`` (``kf/main.go:79-85``,
+    ``odh/main.go:117-160``) for its in-cluster ``BearerTokenFile``.  The kubelet rotates a
+    projected ServiceAccount token hourly (and a bound token expires unless the cluster
+    extends it); a token read once at start-up starts failing with 401 after that.
+
+    The file is re-read at most every ``period_s`` (client-go: one minute), and at once by
+    :meth:`refresh` after a 401.  A failed read keeps the last good token (client-go logs
+    and keeps serving the cached one)."""
+
+    PERIOD_S = 60.0
+
+    def __init__(self, path: str, initial: Optional[str] = None, period_s: float = PERIOD_S,
+                 clock=time.monotonic):
+        self.path = path
+        self.period_s = period_s
+        self._clock = clock
+        self._token = initial or None
+        self._read_at = clock() if self._token else float("-inf")
+        self.reads = 0
+
+    def token(self) -> Optional[str]:
+        if self._clock() - self._read_at >= self.period_s:
+            self._read()
+        return self._token
+
+    def refresh(self) -> bool:
+        """Re-read now; True when the token changed (a request that got 401 is worth retrying)."""
+        old = self._token
+        self._read()
+        return self._token != old
+
+    def _read(self) -> None:
+        self._read_at = self._clock()
+        self.reads += 1
+        try:
+            with open(self.path) as f:
+                tok = f.read().strip()
+        except OSError as e:
+            log.warning("cannot re-read the bearer token file %s (keeping the cached token): %s", self.path, e)
+            return
+        if tok:
+            self._token = tok
 
 
 class TokenBucket:
@@ -197,16 +252,35 @@ class RestClient(Client):
         self.retries = 0  # GETs retried after a connection reset / EOF
         self.user = config.user_agent
         self._discovery: dict = {}  # "group/version" -> (fetched_at, set(plurals))
+        self.tokens: Optional[FileTokenSource] = (FileTokenSource(config.token_file, config.token)
+                                                  if config.token_file else None)
+        self._sent_token: Optional[str] = None  # the token in the pool's Authorization header
+        self.token_retries = 0  # requests / watches retried after a 401 with a re-read token
+
+    def _bearer(self) -> Optional[str]:
+        return self.tokens.token() if self.tokens is not None else self.config.token
 
     def _http(self):
         from .http1 import Http1Pool
 
+        tok = self._bearer()
         if self._session is None:
             headers = {"User-Agent": self.config.user_agent}
-            if self.config.token:
-                headers["Authorization"] = f"Bearer {self.config.token}"
+            if tok:
+                headers["Authorization"] = f"Bearer {tok}"
             self._session = Http1Pool(self.base, self._ssl, headers, size=self._pool)
+            self._sent_token = tok
+        elif tok != self._sent_token:  # the token file was rotated
+            self._session.set_header("Authorization", f"Bearer {tok}" if tok else None)
+            self._sent_token = tok
         return self._session
+
+    def _unauthorized_retry(self, status: int) -> bool:
+        """A 401 while the token comes from a file: re-read it at once; retry iff it changed."""
+        if status != 401 or self.tokens is None or not self.tokens.refresh():
+            return False
+        self.token_retries += 1
+        return True
 
     async def close(self) -> None:
         if self._session is not None:
@@ -221,7 +295,6 @@ class RestClient(Client):
                       content_type: str = "application/json", count_as: str = "other") -> dict:
         from urllib.parse import urlencode
 
-        from .http1 import HttpError
 
         await self._bucket.take()
         self.requests += 1
@@ -231,21 +304,9 @@ class RestClient(Client):
         if params:
             target += ("&" if "?" in target else "?") + urlencode(params)
         t0 = time.perf_counter()
-        for attempt in range(self.GET_RETRIES + 1):
-            try:
-                status, raw = await self._http().request(method, target, data,
-                                                         content_type if data is not None else None)
-                break
-            except HttpError as e:
-                # client-go retries a GET whose connection was reset or hit EOF mid-response
-                # (rest/request.go: IsConnectionReset || IsProbableEOF, up to maxRetries=10);
-                # writes are not retried here — the reconcile's own requeue does that
-                if method != "GET" or attempt == self.GET_RETRIES or not isinstance(
-                        e.__cause__, (asyncio.IncompleteReadError, ConnectionResetError, BrokenPipeError,
-                                      ConnectionAbortedError)):
-                    raise InternalError(str(e))
-                self.retries += 1
-                await asyncio.sleep(min(0.5, 0.01 * (2 ** attempt)))
+        status, raw = await self._roundtrip(method, target, data, content_type if data is not None else None)
+        if self._unauthorized_retry(status):
+            status, raw = await self._roundtrip(method, target, data, content_type if data is not None else None)
         if method == "GET":
             self.get_ms.append((time.perf_counter() - t0) * 1e3)
         if raw:
@@ -263,6 +324,25 @@ class RestClient(Client):
                 await self._maybe_no_match(url, err)
             raise err
         return out
+
+    async def _roundtrip(self, method: str, target: str, data: Optional[bytes],
+                         content_type: Optional[str]) -> Tuple[int, bytes]:
+        from .http1 import HttpError
+
+        for attempt in range(self.GET_RETRIES + 1):
+            try:
+                return await self._http().request(method, target, data, content_type)
+            except HttpError as e:
+                # client-go retries a GET whose connection was reset or hit EOF mid-response
+                # (rest/request.go: IsConnectionReset || IsProbableEOF, up to maxRetries=10);
+                # writes are not retried here — the reconcile's own requeue does that
+                if method != "GET" or attempt == self.GET_RETRIES or not isinstance(
+                        e.__cause__, (asyncio.IncompleteReadError, ConnectionResetError, BrokenPipeError,
+                                      ConnectionAbortedError)):
+                    raise InternalError(str(e))
+                self.retries += 1
+                await asyncio.sleep(min(0.5, 0.01 * (2 ** attempt)))
+        raise InternalError("unreachable")
 
     async def _served(self, group: str, version: str) -> Optional[set]:
         """Plurals the server serves for ``group/version`` — ``None`` when discovery itself
@@ -404,6 +484,15 @@ class RestClient(Client):
         self.by_verb["WATCH"] = self.by_verb.get("WATCH", 0) + 1
         target = self.path(info, v, namespace)[len(self.base):] + "?" + urlencode(params)
         status, _headers, stream = await self._http().stream("GET", target)
+        if status == 401 and self.tokens is not None:
+            await stream.read_all()
+            stream.close()
+            if self._unauthorized_retry(status):  # rotated token: reopen once with the new one
+                status, _headers, stream = await self._http().stream("GET", target)
+            else:
+                status, _headers, stream = 401, _headers, None
+        if stream is None:
+            raise ApiError.from_status({"code": 401, "reason": "Unauthorized", "message": "Unauthorized"}, 401)
         if status >= 400:
             raw = await stream.read_all()
             try:

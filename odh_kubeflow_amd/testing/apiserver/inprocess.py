@@ -30,6 +30,12 @@ class StoreReader(Reader):
     def list(self, kind, namespace=None, labels=None, fields=None, owner_uid=None):
         return self.store.list_nocopy(kind, namespace, labels, fields, owner_uid)
 
+    def watching(self, kind, namespace=None) -> bool:
+        return True  # the store itself: always synced, every namespace
+
+    def kind_version(self, kind):
+        return self.store.kind_version(kind)
+
 
 class StoreEventSource(EventSource):
     def __init__(self, store: ObjectStore):
@@ -48,6 +54,7 @@ class InProcessClient(Client):
     def __init__(self, store: ObjectStore, user: str = "system:admin"):
         self.store = store
         self.user = user
+        self.reader = StoreReader(store)  # what a cache over this store would show: the store
 
     async def get(self, kind, name, namespace=None):
         return await self.store.get(kind, name, namespace, version=_version_of(kind))

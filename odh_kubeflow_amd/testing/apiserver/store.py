@@ -178,6 +178,13 @@ class ObjectStore:
     def resource_version(self) -> str:
         return str(self._rv)
 
+    def kind_version(self, ref) -> Tuple[int, bool]:
+        """A token that changes whenever an object of ``ref``'s kind does (or the kind gets
+        installed / uninstalled): the resourceVersion of its last event."""
+        info = SCHEME.resolve(ref)
+        hist = self._history.get(info.key)
+        return (hist[-1][0] if hist else 0, info.key in self.installed)
+
     def _out(self, info: ResourceInfo, obj: dict, version: Optional[str]) -> dict:
         o = deepcopy_json(obj)
         if version and version != info.storage_version:

@@ -26,10 +26,12 @@ the reference manager's (``odh/main.go:178-185``).
 
 from __future__ import annotations
 
+import asyncio
 import base64
 import json
 import logging
 import os
+from collections import OrderedDict
 from typing import Dict, Mapping, Optional, Tuple
 
 from ..controllers.odh import auth, certs, dspa_secret, feast, runtime_images
@@ -86,6 +88,34 @@ def validate_gpu_resources(nb: dict) -> None:
                                       f"{GPU_RESOURCE} limit of {lim}")
 
 
+def _gpu_resources(nb: Optional[dict]) -> list:
+    from ..models.notebook import GPU_RESOURCE
+
+    spec = (((nb or {}).get("spec") or {}).get("template") or {}).get("spec") or {}
+    out = []
+    for c in spec.get("containers") or []:
+        res = (c.get("resources") if isinstance(c, dict) else None) or {}
+        out.append(((res.get("requests") or {}).get(GPU_RESOURCE), (res.get("limits") or {}).get(GPU_RESOURCE)))
+    return out
+
+
+def gpu_validation_applies(operation: str, nb: dict, old: Optional[dict]) -> bool:
+    """Whether :func:`validate_gpu_resources` judges this admission: a CREATE, or an UPDATE
+    that changes some container's ``amd.com/gpu`` request or limit — never an update of a
+    Notebook being deleted.
+
+    The check is this webhook's own (the reference's ``Handle`` denies none of these paths,
+    ``odh/controllers/notebook_webhook.go:352-499``), so it must never wedge a Notebook that
+    is already stored: one that predates the webhook (a takeover from the reference's
+    controllers) must stay finalizable, cullable and unlockable — the controllers' finalizer,
+    stop-annotation and lock writes leave the GPU fields as they were."""
+    if operation == "CREATE":
+        return True
+    if operation != "UPDATE" or m.is_deleting(nb):
+        return False
+    return old is None or _gpu_resources(nb) != _gpu_resources(old)
+
+
 _HEARTBEAT_META_SKIP = frozenset({"annotations", "resourceVersion", "managedFields", "generation"})
 
 
@@ -97,11 +127,12 @@ def culler_heartbeat_only(nb: dict, old: Optional[dict]) -> bool:
     For such an update the reference's pipeline can only end one of two ways: its mutations
     leave the pod template alone, or the restart guard reverts them (the notebook runs and the
     culler did not touch the template, :505-564) — apart from refreshing
-    ``update-pending``, the response is empty.  It is answered without running the pipeline,
-    so R resident notebooks do not cost R admissions' worth of ConfigMap reads per check
-    period; ``update-pending`` is brought up to date by the next update that is not a
-    heartbeat.  A stopped or restarting notebook (no restart guard) always takes the full
-    pipeline."""
+    ``update-pending``, the response is empty.  Such an update skips the pipeline while the
+    webhook's inputs are unchanged since the notebook's last full admission
+    (``NotebookWebhook._heartbeat_settled``), so R resident notebooks do not cost R
+    admissions' worth of ConfigMap reads per check period; once an input changed, the next
+    heartbeat runs the pipeline and refreshes ``update-pending``.  A stopped or restarting
+    notebook (no restart guard) always takes the full pipeline."""
     from ..controllers.odh.constants import ANNOTATION_NOTEBOOK_RESTART as RESTART
     from ..models.notebook import CULLER_HEARTBEAT_ANNOTATIONS
     from ..runtime.controller import maps_differ
@@ -131,6 +162,34 @@ def _parse_go_bool(raw: str) -> Optional[bool]:
     if v in ("0", "f", "F", "FALSE", "false", "False"):
         return False
     return None
+
+
+def created_time(raw) -> float:
+    """An ImageStream tag item's ``created`` (a ``metav1.Time``, RFC 3339) as seconds since the
+    epoch, so items are ordered by instant as the reference's ``Time.After`` orders them
+    (``odh/controllers/notebook_webhook.go:860-864``) — not by string, which misorders
+    ``+02:00`` against ``Z`` and fractional against whole seconds.  Absent or unparsable:
+    the zero time, i.e. oldest."""
+    import datetime
+
+    if not isinstance(raw, str) or not raw:
+        return float("-inf")
+    s = raw.strip()
+    if s[-1:] in ("Z", "z"):
+        s = s[:-1] + "+00:00"
+    head, dot, rest = s.partition(".")
+    if dot:  # fromisoformat (3.10) takes 3 or 6 fractional digits only: normalise to 6
+        i = 0
+        while i < len(rest) and rest[i].isdigit():
+            i += 1
+        s = head + "." + (rest[:i] + "000000")[:6] + rest[i:]
+    try:
+        t = datetime.datetime.fromisoformat(s)  # any single character separates date and time
+    except ValueError:
+        return float("-inf")
+    if t.tzinfo is None:
+        return float("-inf")  # RFC 3339 requires an offset
+    return t.timestamp()
 
 
 async def set_container_image_from_registry(client, nb: dict, controller_namespace: str) -> None:
@@ -170,7 +229,7 @@ async def set_container_image_from_registry(client, nb: dict, controller_namespa
         items = tag.get("items") or []
         if not items:
             continue
-        newest = sorted(items, key=lambda it: it.get("created") or "", reverse=True)[0]
+        newest = sorted(items, key=lambda it: created_time(it.get("created")), reverse=True)[0]
         # the reference writes Containers[0] (:868) — preserved
         nb["spec"]["template"]["spec"]["containers"][0]["image"] = newest.get("dockerImageReference", "")
         for e in c.get("env") or []:
@@ -202,7 +261,10 @@ def inject_proxy_config_env_vars(nb: dict, values: Mapping[str, str]) -> None:
 
 
 class NotebookWebhook:
-    def __init__(self, client, namespace: str, kube_rbac_proxy_image: str, env: Optional[Mapping[str, str]] = None):
+    MEMO_CAP = 262144  # notebooks whose last full admission is remembered (a few hundred bytes each)
+
+    def __init__(self, client, namespace: str, kube_rbac_proxy_image: str, env: Optional[Mapping[str, str]] = None,
+                 reader=None):
         self.client = client
         self.namespace = namespace
         self.kube_rbac_proxy_image = kube_rbac_proxy_image
@@ -210,9 +272,130 @@ class NotebookWebhook:
         self.requests = 0
         self.denied = 0
         self.heartbeats = 0  # culler heartbeat updates answered without the pipeline
+        self.heartbeats_full = 0  # ... and those that took it (inputs changed since the last one)
         from ..models.notebook import heartbeat_filter_enabled
 
         self.heartbeat_fast_path = heartbeat_filter_enabled(self.env)
+        # the cache the inputs' versions are read from (see _inputs_token)
+        self._reader = reader if reader is not None else getattr(client, "reader", None)
+        # uid -> (inputs token, notebook token) of the notebook's last full UPDATE admission
+        # whose answer was empty: the stored notebook is the pipeline's fixed point for them
+        self._fixed: "OrderedDict[str, tuple]" = OrderedDict()
+        self._informers_started: set = set()
+        self._informer_tasks: list = []
+
+    # -------------------------------------------------------------- heartbeat fast path
+
+    def _inputs_token(self, nb: dict) -> Optional[tuple]:
+        """The versions of everything the pipeline reads besides the Notebook itself, from the
+        webhook's cache — no request: the kube-rbac-proxy image, the namespace's three
+        ConfigMaps (``odh-trusted-ca-bundle``, ``workbench-trusted-ca-bundle``,
+        ``pipeline-runtime-images``), the ImageStreams (runtime images and
+        ``last-image-selection``), and, when their features are on, the cluster Proxy and the
+        Elyra inputs (DSPA, its S3 Secret, ``ds-pipeline-config``, Gateway, Routes).  ``None``
+        when the cache cannot vouch for one of them (not synced yet, or a namespace outside
+        a sharded cache): the admission then takes the full pipeline, whose reads start the
+        informers the next token needs."""
+        r = self._reader
+        kind_version = getattr(r, "kind_version", None)
+        watching = getattr(r, "watching", None)
+        if kind_version is None or watching is None:
+            return None
+        ns = m.namespace(nb)
+        if not watching(kinds.CONFIG_MAP, ns):
+            self._start_informer(kinds.CONFIG_MAP)
+            return None
+        parts: list = [self.kube_rbac_proxy_image]
+        for name in (certs.ODH_CONFIGMAP_NAME, certs.WORKBENCH_CA_CONFIGMAP_NAME, runtime_images.RUNTIME_IMAGES_CONFIGMAP):
+            o = r.get(kinds.CONFIG_MAP, name, ns)
+            parts.append(None if o is None else m.resource_version(o))
+        ann = m.annotations(nb)
+        if LAST_IMAGE_SELECTION_ANNOTATION in ann:
+            image_ns = (ann.get(WORKBENCH_IMAGE_NAMESPACE_ANNOTATION) or "").strip() or self.namespace
+            covers = getattr(r, "covers", None)
+            if covers is not None and not covers(kinds.IMAGE_STREAM, image_ns):
+                return None
+        global_kinds = [kinds.IMAGE_STREAM]
+        raw = self.env.get("INJECT_CLUSTER_PROXY_ENV")
+        if raw is not None and _parse_go_bool(raw):
+            global_kinds.append(kinds.PROXY)
+        elyra = (self.env.get("SET_PIPELINE_SECRET") or "").strip().lower() == "true"
+        if elyra:
+            global_kinds += [kinds.DSPA, kinds.GATEWAY, kinds.ROUTE]
+        for k in global_kinds:
+            v = kind_version(k)
+            if v is None:
+                return None
+            parts.append(v)
+        if elyra:
+            if not watching(kinds.SECRET, ns):
+                self._start_informer(kinds.SECRET)
+                return None
+            dspa = r.get(kinds.DSPA, dspa_secret.DSPA_INSTANCE_NAME, ns)
+            s3 = ((((dspa or {}).get("spec") or {}).get("objectStorage") or {}).get("externalStorage") or {}) \
+                .get("s3CredentialsSecret") or {}
+            for name in (dspa_secret.ELYRA_SECRET_NAME, s3.get("secretName")):
+                o = r.get(kinds.SECRET, name, ns) if name else None
+                parts.append(None if o is None else m.resource_version(o))
+        return tuple(parts)
+
+    def _start_informer(self, kind) -> None:
+        """Start watching ``kind`` (once) so that later tokens can vouch for it: the webhook
+        reads ConfigMaps and Secrets live (``odh/main.go:178-185``), so nothing else starts
+        their data-stripped informers in a webhook-only process.  In the background: this
+        admission does not wait for the list."""
+        ensure = getattr(self._reader, "ensure_informer", None)
+        if ensure is None or kind in self._informers_started:
+            return
+        self._informers_started.add(kind)
+
+        async def run():
+            try:
+                await ensure(kind)
+            except Exception as e:  # noqa: BLE001 — the token stays None: full pipeline
+                log.info("webhook: cannot watch %s for the heartbeat fast path: %s", kind, e)
+        self._informer_tasks.append(asyncio.ensure_future(run()))
+
+    @staticmethod
+    def _notebook_token(nb: dict) -> Optional[tuple]:
+        """What the pipeline reads of the Notebook: its spec (through ``generation``) and its
+        annotations other than the culler's heartbeat pair."""
+        from ..models.notebook import CULLER_HEARTBEAT_ANNOTATIONS
+
+        md = nb.get("metadata") or {}
+        gen = md.get("generation")
+        if gen is None:
+            return None
+        ann = md.get("annotations") or {}
+        return (md.get("uid"), gen, tuple(sorted((k, v) for k, v in ann.items()
+                                                 if k not in CULLER_HEARTBEAT_ANNOTATIONS)))
+
+    def _heartbeat_settled(self, obj: dict) -> bool:
+        """A heartbeat may skip the pipeline iff the notebook is, as stored, the pipeline's
+        fixed point for the inputs as they are now: then the reference's full run (which it
+        makes on every culler write, ``odh/controllers/notebook_webhook.go:477-490``) would
+        answer with an empty patch too.  After any input changed — a new kube-rbac-proxy
+        image, a CA bundle or runtime-images ConfigMap edited — the next heartbeat runs the
+        pipeline and its restart guard, so ``update-pending`` appears within one culler
+        check period, as in the reference."""
+        uid = m.uid(obj)
+        memo = self._fixed.get(uid) if uid else None
+        if memo is None or memo[1] != self._notebook_token(obj):
+            return False
+        return memo[0] is not None and memo[0] == self._inputs_token(obj)
+
+    def _remember_fixed_point(self, obj: dict, inputs: Optional[tuple]) -> None:
+        uid = m.uid(obj)
+        tok = self._notebook_token(obj)
+        if not uid or inputs is None or tok is None:
+            return
+        self._fixed[uid] = (inputs, tok)
+        self._fixed.move_to_end(uid)
+        if len(self._fixed) > self.MEMO_CAP:
+            self._fixed.popitem(last=False)
+
+    def forget(self, uid: str) -> None:
+        self._fixed.pop(uid, None)
 
     async def mutate(self, operation: str, nb: dict, old: Optional[dict], name: str = "",
                      namespace: str = "") -> dict:
@@ -220,7 +403,7 @@ class NotebookWebhook:
         with tracer.start_span("handleFunc", {"notebook": name or m.name(nb), "namespace": namespace or m.namespace(nb),
                                               "operation": operation}, new_root=True):
             original = nb
-            if operation in ("CREATE", "UPDATE"):
+            if gpu_validation_applies(operation, nb, old):
                 validate_gpu_resources(nb)
             nb = deepcopy_json(nb)
             if operation == "CREATE":
@@ -313,22 +496,28 @@ class NotebookWebhook:
             # the culler's heartbeat first, before the shape check: the object is the stored
             # (admitted, schema-valid) old one but for two annotations, so it decodes iff their
             # values are strings — the one check left at 1000 heartbeats a second
-            if req.get("operation") == "UPDATE" and self.heartbeat_fast_path and heartbeat_update(obj, old):
+            op = req.get("operation", "")
+            beat = op == "UPDATE" and self.heartbeat_fast_path and heartbeat_update(obj, old)
+            if beat and self._heartbeat_settled(obj):
                 self.heartbeats += 1
                 return {"apiVersion": "admission.k8s.io/v1", "kind": "AdmissionReview", "response": resp}
+            if beat:
+                self.heartbeats_full += 1
             bad = undecodable(obj)
             if bad:  # the reference's typed decode (admission.Decoder) refuses these
                 raise AdmissionError(400, f"cannot decode Notebook: {bad}")
+            inputs = self._inputs_token(obj) if op == "UPDATE" and self.heartbeat_fast_path else None
             tok = CONFIRM_ABSENCE.set(set())  # one-shot decision: absent objects are confirmed live, once
             try:
-                mutated = await self.mutate(req.get("operation", ""), obj, old, req.get("name", ""),
-                                            req.get("namespace", ""))
+                mutated = await self.mutate(op, obj, old, req.get("name", ""), req.get("namespace", ""))
             finally:
                 CONFIRM_ABSENCE.reset(tok)
             ops = jsonpatch.create_patch(obj, mutated)
             if ops:
                 resp["patchType"] = "JSONPatch"
                 resp["patch"] = base64.b64encode(dumps_json(ops)).decode()
+            elif inputs is not None:
+                self._remember_fixed_point(obj, inputs)
         except AdmissionError as e:
             self.denied += 1
             resp = {"uid": uid, "allowed": False, "status": {"code": e.code, "message": str(e)}}

@@ -81,6 +81,7 @@ class _Conn(asyncio.Protocol):
         self._lines: List[bytes] = []
         self._got = 0
         self._eof = False
+        self._no_body = False  # the request in flight is a HEAD
 
     # ---------------------------------------------------------------- asyncio.Protocol
 
@@ -121,13 +122,17 @@ class _Conn(asyncio.Protocol):
                     return
                 self._head = _parse_head(bytes(self.buf[:i]))
                 del self.buf[:i + 4]
-                h = self._head[1]
-                if h.get("transfer-encoding", "").lower() == "chunked":
+                status, h = self._head
+                if self._no_body or status < 200 or status in (204, 304):
+                    self._want = 0  # RFC 9112 §6.3: no body, whatever the headers say
+                elif h.get("transfer-encoding", "").lower() == "chunked":
                     self._want = -2
                 elif "content-length" in h:
                     self._want = int(h["content-length"])
+                elif h.get("connection", "").lower() == "close" or self._streaming:
+                    self._want = -3  # delimited by the server closing the connection
                 else:
-                    self._want = -3
+                    self._want = 0  # a keep-alive response without a length has no body
                 if self._streaming:  # stream() waits for the head alone
                     self._waiter = None
                     if w is not None and not w.done():
@@ -190,6 +195,7 @@ class _Conn(asyncio.Protocol):
         if self.closed:
             raise ConnectionResetError("connection closed")
         self._waiter = w = asyncio.get_running_loop().create_future()
+        self._no_body = payload.startswith(b"HEAD ")
         self.transport.write(payload)
         if self.buf:  # bytes that arrived before the request (a server error, an early close)
             self._advance()
@@ -233,12 +239,21 @@ class Http1Pool:
         self.host = u.hostname or "127.0.0.1"
         self.port = u.port or (443 if u.scheme == "https" else 80)
         self.ssl = ssl_context if u.scheme == "https" else None
-        hdr = {"Host": f"{self.host}:{self.port}", "Accept": "application/json"}
-        hdr.update(headers or {})
-        self._static = "".join(f"{k}: {v}\r\n" for k, v in hdr.items())
+        self._hdr = {"Host": f"{self.host}:{self.port}", "Accept": "application/json"}
+        self._hdr.update(headers or {})
+        self._static = "".join(f"{k}: {v}\r\n" for k, v in self._hdr.items())
         self._idle: List[_Conn] = []
         self.size = size
         self.opened = 0
+
+    def set_header(self, name: str, value: Optional[str]) -> None:
+        """Set (``None``: drop) a header every later request carries — e.g. a rotated bearer
+        token.  Requests already written keep the one they were sent with."""
+        if value is None:
+            self._hdr.pop(name, None)
+        else:
+            self._hdr[name] = value
+        self._static = "".join(f"{k}: {v}\r\n" for k, v in self._hdr.items())
 
     async def _connect(self) -> _Conn:
         loop = asyncio.get_running_loop()

@@ -275,9 +275,14 @@ class RestClient(Client):
             self._sent_token = tok
         return self._session
 
-    def _unauthorized_retry(self, status: int) -> bool:
-        """A 401 while the token comes from a file: re-read it at once; retry iff it changed."""
-        if status != 401 or self.tokens is None or not self.tokens.refresh():
+    def _unauthorized_retry(self, status: int, sent: Optional[str]) -> bool:
+        """A 401 while the token comes from a file: re-read it at once; retry iff the current
+        token differs from the one the request carried (a concurrent request may have re-read
+        the rotated file already)."""
+        if status != 401 or self.tokens is None:
+            return False
+        self.tokens.refresh()
+        if self.tokens.token() == sent:
             return False
         self.token_retries += 1
         return True
@@ -295,7 +300,6 @@ class RestClient(Client):
                       content_type: str = "application/json", count_as: str = "other") -> dict:
         from urllib.parse import urlencode
 
-
         await self._bucket.take()
         self.requests += 1
         self.by_verb[method] = self.by_verb.get(method, 0) + 1
@@ -304,9 +308,9 @@ class RestClient(Client):
         if params:
             target += ("&" if "?" in target else "?") + urlencode(params)
         t0 = time.perf_counter()
-        status, raw = await self._roundtrip(method, target, data, content_type if data is not None else None)
-        if self._unauthorized_retry(status):
-            status, raw = await self._roundtrip(method, target, data, content_type if data is not None else None)
+        status, raw, sent = await self._roundtrip(method, target, data, content_type if data is not None else None)
+        if self._unauthorized_retry(status, sent):
+            status, raw, _ = await self._roundtrip(method, target, data, content_type if data is not None else None)
         if method == "GET":
             self.get_ms.append((time.perf_counter() - t0) * 1e3)
         if raw:
@@ -326,12 +330,16 @@ class RestClient(Client):
         return out
 
     async def _roundtrip(self, method: str, target: str, data: Optional[bytes],
-                         content_type: Optional[str]) -> Tuple[int, bytes]:
+                         content_type: Optional[str]) -> Tuple[int, bytes, Optional[str]]:
+        """(status, body, the bearer token the request was sent with)."""
         from .http1 import HttpError
 
         for attempt in range(self.GET_RETRIES + 1):
             try:
-                return await self._http().request(method, target, data, content_type)
+                pool = self._http()
+                sent = self._sent_token  # the header the next line writes (no await in between)
+                status, raw = await pool.request(method, target, data, content_type)
+                return status, raw, sent
             except HttpError as e:
                 # client-go retries a GET whose connection was reset or hit EOF mid-response
                 # (rest/request.go: IsConnectionReset || IsProbableEOF, up to maxRetries=10);
@@ -483,11 +491,13 @@ class RestClient(Client):
         self.requests += 1
         self.by_verb["WATCH"] = self.by_verb.get("WATCH", 0) + 1
         target = self.path(info, v, namespace)[len(self.base):] + "?" + urlencode(params)
-        status, _headers, stream = await self._http().stream("GET", target)
+        pool = self._http()
+        sent = self._sent_token
+        status, _headers, stream = await pool.stream("GET", target)
         if status == 401 and self.tokens is not None:
             await stream.read_all()
             stream.close()
-            if self._unauthorized_retry(status):  # rotated token: reopen once with the new one
+            if self._unauthorized_retry(status, sent):  # rotated token: reopen once with the new one
                 status, _headers, stream = await self._http().stream("GET", target)
             else:
                 status, _headers, stream = 401, _headers, None

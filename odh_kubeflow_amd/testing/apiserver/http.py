@@ -243,6 +243,14 @@ class ApiServer:
             await self._runner.cleanup()
             self._runner = None
 
+    def rotate_token(self, token: str) -> None:
+        """Accept only ``token`` from now on and end the open watches — a rotated (or expired
+        bound) ServiceAccount token: every client must re-authenticate, a watch included when
+        it re-opens."""
+        self.token = token
+        for t in list(self._watch_tasks):
+            t.cancel()
+
     # -------------------------------------------------------------- handlers
 
     async def _ok(self, _req):

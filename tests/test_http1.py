@@ -102,6 +102,40 @@ def test_keepalive_responses_parse_across_any_split(seed):
     assert got == [(200, body, False), (201, body, False), (200, body, False), (404, b"", True)]
 
 
+@pytest.mark.parametrize("seed", range(4))
+def test_bodyless_responses_complete_without_waiting_for_close(seed):
+    """1xx-less bodyless answers — 204 and 304, or a keep-alive response with neither
+    Content-Length nor chunked encoding — complete at their head, and the next response on the
+    connection parses; only ``Connection: close`` delimits a body by end of stream."""
+    body = b'{"a":1}'
+    ok = b"HTTP/1.1 200 OK\r\nContent-Length: %d\r\n\r\n" % len(body) + body
+    no_content = b"HTTP/1.1 204 No Content\r\n\r\n"
+    not_modified = b"HTTP/1.1 304 Not Modified\r\nContent-Type: application/json\r\n\r\n"
+    bare = b"HTTP/1.1 200 OK\r\nContent-Type: text/plain\r\n\r\n"
+    got = asyncio.run(asyncio.wait_for(_roundtrips([no_content, ok, not_modified, bare, ok], seed), 5))
+    assert got == [(204, b"", False), (200, body, False), (304, b"", False), (200, b"", False), (200, body, False)]
+
+    async def until_close():
+        conn = _Conn()
+        conn.connection_made(_T())
+        fut = asyncio.ensure_future(conn.roundtrip(b"GET / HTTP/1.1\r\n\r\n"))
+        await asyncio.sleep(0)
+        conn.data_received(b"HTTP/1.1 200 OK\r\nConnection: close\r\n\r\nall of ")
+        conn.data_received(b"it")
+        conn.connection_lost(None)
+        return await fut
+    assert asyncio.run(until_close()) == (200, b"all of it", True)
+
+    async def head():
+        conn = _Conn()
+        conn.connection_made(_T())
+        fut = asyncio.ensure_future(conn.roundtrip(b"HEAD / HTTP/1.1\r\n\r\n"))
+        await asyncio.sleep(0)
+        conn.data_received(b"HTTP/1.1 200 OK\r\nContent-Length: 42\r\n\r\n")
+        return await asyncio.wait_for(fut, 5)
+    assert asyncio.run(head()) == (200, b"", False)
+
+
 def test_dechunk_waits_for_the_final_crlf():
     raw, body = bytearray(b"3\r\nabc\r\n0\r\n"), bytearray()
     assert not _dechunk(raw, body) and body == b"abc"

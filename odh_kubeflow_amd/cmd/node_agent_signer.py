@@ -85,7 +85,7 @@ def build(args):
     elector = LeaderElector(RestClient(cfg), "mi355x-node-agent-signer", ns) if args.leader_elect else None
     # Pods are read live (one GET per request: the binding must be checked against the pod as
     # it is now); only this signer's CSRs are watched
-    mgr = Manager.remote(cfg, name="node-agent-signer", uncached=(kinds.POD,),
+    mgr = Manager.remote(cfg, name="node-agent-signer", uncached=(kinds.POD, kinds.DAEMON_SET),
                          cache_options={"field_selectors": {kinds.CSR: f"spec.signerName={SIGNER_NAME}"}},
                          leader_elector=elector, metrics_addr=args.metrics_bind_address,
                          probe_addr=args.health_probe_bind_address)

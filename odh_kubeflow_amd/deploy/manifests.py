@@ -63,6 +63,7 @@ AGENT_NAME = "mi355x-node-agent"
 AGENT_SIGNER = "mi355x-node-agent-signer"
 AGENT_CA_SECRET = "mi355x-node-agent-ca"  # the signer's CA (ca.crt / ca.key): only the signer reads it
 AGENT_TLS_MOUNT = "/var/run/odh/node-agent-tls"
+AGENT_ENROLL_ID = 65532  # uid / gid of the enrollment containers, the pod's fsGroup
 AGENT_CA_CONFIGMAP = "mi355x-node-agent-ca"
 AGENT_CA_MOUNT = "/var/run/odh/node-agent-ca"
 MWC_NAME = "mutating-webhook-configuration"
@@ -374,7 +375,8 @@ def node_agent_daemonset() -> dict:
                 "args": ["--node-name=$(NODE_NAME)", "--host-ip=$(HOST_IP)", f"--cert-dir={AGENT_TLS_MOUNT}"]
                 + (["--once"] if once else []),
                 "env": node_env, "volumeMounts": [tls_rw, sa_mount],
-                "securityContext": {**RESTRICTED, "readOnlyRootFilesystem": True, "runAsUser": 65532},
+                "securityContext": {**RESTRICTED, "readOnlyRootFilesystem": True, "runAsUser": AGENT_ENROLL_ID,
+                                    "runAsGroup": AGENT_ENROLL_ID},
                 "resources": {"requests": {"cpu": "10m", "memory": "32Mi"}, "limits": {"memory": "128Mi"}}}
     c = {"name": "agent", "image": MANAGER_IMAGE,
          "command": ["python", "-m", "odh_kubeflow_amd.cmd.node_agent"],
@@ -405,9 +407,11 @@ def node_agent_daemonset() -> dict:
                                            "nodeSelector": {"amd.com/gpu.family": "AI"},
                                            "tolerations": [{"key": GPU_RESOURCE, "operator": "Exists",
                                                             "effect": "NoSchedule"}],
-                                           # the enrollment containers write the pair as 65532;
-                                           # the (root) agent reads it
-                                           "securityContext": {"fsGroup": 65532},
+                                           # the enrollment containers write the pair as uid and
+                                           # gid 65532, the key 0640; the agent (uid 0, every
+                                           # capability dropped: no DAC override) reads it through
+                                           # this group, which the kubelet adds to every container
+                                           "securityContext": {"fsGroup": AGENT_ENROLL_ID},
                                            "initContainers": [enroll("enroll", once=True)],
                                            "containers": [c, enroll("enroll-renew", once=False)],
                                            "volumes": [{"name": "sys", "hostPath": {"path": "/sys"}},
@@ -444,7 +448,8 @@ def node_agent_rbac() -> List[dict]:
 
 def node_agent_signer_docs() -> List[dict]:
     """The signer (``cmd/node_agent_signer.py``): its CSRs (approve + sign, for its signerName
-    only), the agent pods (get: the binding check), its CA Secret and the trust ConfigMap."""
+    only), the agent pods and their DaemonSet (get: the binding check), its CA Secret and the
+    trust ConfigMap."""
     sa = "node-agent-signer"
     c = {"name": "signer", "image": MANAGER_IMAGE,
          "command": ["python", "-m", "odh_kubeflow_amd.cmd.node_agent_signer"],
@@ -466,6 +471,7 @@ def node_agent_signer_docs() -> List[dict]:
         binding("ClusterRoleBinding", AGENT_SIGNER, AGENT_SIGNER, sa),
         {"apiVersion": "rbac.authorization.k8s.io/v1", "kind": "Role", "metadata": {"name": AGENT_SIGNER},
          "rules": [_rule([""], ["pods"], ["get"]),
+                   {**_rule(["apps"], ["daemonsets"], ["get"]), "resourceNames": [AGENT_NAME]},
                    {**_rule([""], ["secrets"], ["get", "update"]), "resourceNames": [AGENT_CA_SECRET]},
                    _rule([""], ["secrets"], ["create"]),
                    {**_rule([""], ["configmaps"], ["get", "update"]), "resourceNames": [AGENT_CA_CONFIGMAP]},

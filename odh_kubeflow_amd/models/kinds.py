@@ -10,6 +10,7 @@ NAMESPACE = "v1/Namespace"
 NODE = "v1/Node"
 STATEFUL_SET = "apps/v1/StatefulSet"
 DEPLOYMENT = "apps/v1/Deployment"
+DAEMON_SET = "apps/v1/DaemonSet"
 NETWORK_POLICY = "networking.k8s.io/v1/NetworkPolicy"
 ROLE = "rbac.authorization.k8s.io/v1/Role"
 ROLE_BINDING = "rbac.authorization.k8s.io/v1/RoleBinding"

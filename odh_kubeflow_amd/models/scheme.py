@@ -135,6 +135,7 @@ def _builtin(s: Scheme) -> None:
         R("", "PersistentVolumeClaim", "persistentvolumeclaims", True, ("v1",), "v1", True, short_names=("pvc",)),
         R("apps", "StatefulSet", "statefulsets", True, ("v1",), "v1", True, short_names=("sts",)),
         R("apps", "Deployment", "deployments", True, ("v1",), "v1", True, short_names=("deploy",)),
+        R("apps", "DaemonSet", "daemonsets", True, ("v1",), "v1", True, short_names=("ds",)),
         R("networking.k8s.io", "NetworkPolicy", "networkpolicies", True, ("v1",), "v1", short_names=("netpol",)),
         R("rbac.authorization.k8s.io", "Role", "roles", True, ("v1",), "v1"),
         R("rbac.authorization.k8s.io", "RoleBinding", "rolebindings", True, ("v1",), "v1"),

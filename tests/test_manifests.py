@@ -416,3 +416,32 @@ def test_node_agent_identity_plumbing():
         envs = [e for o, p in _pod_specs(objs) for c in p["containers"] for e in c.get("env") or []
                 if e["name"] == "CULLING_GPU_AGENT_IDENTITY_DOMAIN"]
         assert envs and all(e["value"] == IDENTITY_DOMAIN for e in envs)
+
+
+def test_node_agent_can_read_the_key_its_enroll_containers_write():
+    """the enrollment containers write the node key into the shared
+    emptyDir as their own uid; the agent container runs as another uid with every capability
+    dropped (no CAP_DAC_OVERRIDE / CAP_DAC_READ_SEARCH), so it reads the key only through
+    the file's mode bits: owner (same uid), or group via the pod's fsGroup — which the kubelet
+    adds to every container's supplementary groups and gives the emptyDir (setgid)."""
+    from odh_kubeflow_amd.deploy.manifests import AGENT_TLS_MOUNT, node_agent_daemonset
+    from odh_kubeflow_amd.nodeagent.identity import KEY_FILE_MODE
+
+    spec = node_agent_daemonset()["spec"]["template"]["spec"]
+    fs_group = spec["securityContext"]["fsGroup"]
+    writers = [c for c in spec["initContainers"] + spec["containers"] if c["name"].startswith("enroll")]
+    agent = next(c for c in spec["containers"] if c["name"] == "agent")
+    assert writers and all(c["securityContext"]["runAsGroup"] == fs_group for c in writers)
+    owner_uid = writers[0]["securityContext"]["runAsUser"]
+    assert {c["securityContext"]["runAsUser"] for c in writers} == {owner_uid}
+    caps = set(agent["securityContext"].get("capabilities", {}).get("drop", []))
+    assert "ALL" in caps  # no DAC override: permission bits decide
+    agent_uid = agent["securityContext"]["runAsUser"]
+    agent_groups = {fs_group} | set(spec["securityContext"].get("supplementalGroups", []))
+    readable = ((agent_uid == owner_uid and KEY_FILE_MODE & 0o400) or (fs_group in agent_groups and KEY_FILE_MODE & 0o040)
+                or KEY_FILE_MODE & 0o004)
+    assert readable
+    assert not KEY_FILE_MODE & 0o007  # and nobody else
+    # the agent mounts that same volume (read-only) where the enrollment containers write
+    tls = lambda c: [vm for vm in c["volumeMounts"] if vm["mountPath"] == AGENT_TLS_MOUNT]  # noqa: E731
+    assert [vm["name"] for vm in tls(agent)] == [vm["name"] for vm in tls(writers[0])] and tls(agent)[0]["readOnly"]

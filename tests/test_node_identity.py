@@ -39,13 +39,16 @@ USERS = {
     "someone": {"username": "system:serviceaccount:team:default",
                 "extra": {ident.POD_NAME_EXTRA: ["agent-a"], ident.POD_UID_EXTRA: ["uid-a"]}},
     "rogue-pod": _agent_user("rogue", "uid-r"),  # the agents' SA, but a pod nobody's DaemonSet owns
+    "forged-pod": _agent_user("forged", "uid-f"),
+    "unselected-pod": _agent_user("unselected", "uid-u"),
 }
 
 
-def _agent_pod(name, node, ip, owner="mi355x-node-agent", kind="DaemonSet"):
+def _agent_pod(name, node, ip, owner="mi355x-node-agent", kind="DaemonSet", owner_uid="ds",
+               labels=(("app", "mi355x-node-agent"),)):
     return {"apiVersion": "v1", "kind": "Pod",
-            "metadata": {"name": name, "namespace": NS,
-                         "ownerReferences": [{"apiVersion": "apps/v1", "kind": kind, "name": owner, "uid": "ds",
+            "metadata": {"name": name, "namespace": NS, "labels": dict(labels),
+                         "ownerReferences": [{"apiVersion": "apps/v1", "kind": kind, "name": owner, "uid": owner_uid,
                                               "controller": True}]},
             "spec": {"nodeName": node, "containers": [{"name": "agent", "image": "i"}]},
             "status": {"hostIP": ip, "phase": "Running"}}
@@ -65,18 +68,29 @@ class _Cluster:
         self.srv = await ApiServer(ObjectStore(), users=self.users).start("127.0.0.1", 0)
         self.admin = RestClient(RestConfig(host=self.srv.url, token="admin"))
         await self.admin.create({"apiVersion": "v1", "kind": "Namespace", "metadata": {"name": NS}})
+        ds = await self.admin.create({
+            "apiVersion": "apps/v1", "kind": "DaemonSet", "metadata": {"name": "mi355x-node-agent", "namespace": NS},
+            "spec": {"selector": {"matchLabels": {"app": "mi355x-node-agent"}},
+                     "template": {"metadata": {"labels": {"app": "mi355x-node-agent"}},
+                                  "spec": {"containers": [{"name": "agent", "image": "i"}]}}}})
         uids = {}
-        for pod in (_agent_pod("agent-a", "gpu-a", "10.0.0.1"), _agent_pod("agent-b", "gpu-b", "10.0.0.2"),
-                    _agent_pod("rogue", "gpu-a", "10.0.0.1", owner="debug", kind="ReplicaSet")):
+        ds_uid = ds["metadata"]["uid"]
+        for pod in (_agent_pod("agent-a", "gpu-a", "10.0.0.1", owner_uid=ds_uid),
+                    _agent_pod("agent-b", "gpu-b", "10.0.0.2", owner_uid=ds_uid),
+                    _agent_pod("rogue", "gpu-a", "10.0.0.1", owner="debug", kind="ReplicaSet"),
+                    # a pod of the agents' SA with a forged owner reference (right kind and name)
+                    _agent_pod("forged", "gpu-a", "10.0.0.1", owner_uid="not-the-daemonset"),
+                    # ... or with the right one but outside the DaemonSet's selector
+                    _agent_pod("unselected", "gpu-a", "10.0.0.1", owner_uid=ds_uid, labels=())):
             uids[pod["metadata"]["name"]] = (await self.admin.create(pod))["metadata"]["uid"]
         # the tokens' bound-pod uids are the live pods' (the stand-in assigns uids on create)
         for tok, pod in (("agent-a", "agent-a"), ("agent-b", "agent-b"), ("rogue-pod", "rogue"),
-                         ("someone", "agent-a")):
+                         ("someone", "agent-a"), ("forged-pod", "forged"), ("unselected-pod", "unselected")):
             self.users[tok]["extra"][ident.POD_UID_EXTRA] = [uids[pod]]
         self.mgr = None
         if self.with_signer:
             self.mgr = Manager.remote(RestConfig(host=self.srv.url, token="admin"), name="signer",
-                                      uncached=(kinds.POD,))
+                                      uncached=(kinds.POD, kinds.DAEMON_SET))
             self.ca, key = await ident.ensure_ca(self.mgr.client, NS, "agent-ca", "agent-ca-bundle")
             self.signer = ident.NodeAgentSigner(self.mgr.client, ident.SignerPolicy(namespace=NS), self.ca, key)
             self.signer.setup_with_manager(self.mgr)
@@ -109,7 +123,9 @@ def test_agent_enrolls_for_its_own_node(run, tmp_path):
                 crt = f.read()
             assert cert_sans(crt) == {"gpu-a.mi355x-node-agent.nodes", "10.0.0.1"}
             assert cert_signed_by(crt, cl.ca)
-            assert oct(os.stat(tmp_path / "a" / "tls.key").st_mode & 0o777) == "0o600"
+            # group-readable: the agent container reads it through the pod's fsGroup
+            assert oct(os.stat(tmp_path / "a" / "tls.key").st_mode & 0o777) == "0o640"
+            assert os.stat(tmp_path / "a" / "tls.key").st_gid == os.stat(tmp_path / "a").st_gid
             assert await e.ensure(10) == "kept" and e.requests == 1
             # the culler's trust bundle is published for it
             cm = await cl.admin.get(kinds.CONFIG_MAP, "agent-ca-bundle", NS)
@@ -129,6 +145,8 @@ def test_agent_enrolls_for_its_own_node(run, tmp_path):
     ("unbound", "gpu-a", "10.0.0.1", "NoPodBinding"),  # a token not bound to a pod
     ("stale-a", "gpu-a", "10.0.0.1", "PodGone"),  # bound to a pod that no longer exists
     ("rogue-pod", "gpu-a", "10.0.0.1", "NotNodeAgent"),  # a pod of the agents' SA outside the DaemonSet
+    ("forged-pod", "gpu-a", "10.0.0.1", "NotNodeAgent"),  # ownerReference names the DaemonSet, wrong uid
+    ("unselected-pod", "gpu-a", "10.0.0.1", "NotNodeAgent"),  # not matched by the DaemonSet's selector
 ])
 def test_signer_denies_what_the_requesting_pod_does_not_prove(run, tmp_path, token, node, ip, reason):
     async def body(cl):

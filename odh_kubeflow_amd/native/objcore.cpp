@@ -569,9 +569,9 @@ PyObject* object_value(Parser& ps, PyObject* old, int depth) {
     }
   }
   const Py_ssize_t n = static_cast<Py_ssize_t>(f.size() / 2);
-  // every member is the old one's and there are as many (a duplicate key cannot make up for
-  // a missing one: its value would have to be the old value of two different keys)
-  if (same && depth > 0 && n == PyDict_GET_SIZE(od)) {
+  // every member is the old one's, in the old order, and there are as many: the keys matched
+  // the old dict's one by one, so they are distinct and the object is the old one
+  if (same && in_step && depth > 0 && n == PyDict_GET_SIZE(od)) {
     Py_INCREF(od);
     return od;
   }
@@ -582,6 +582,13 @@ PyObject* object_value(Parser& ps, PyObject* old, int depth) {
       Py_DECREF(out);
       return nullptr;
     }
+  }
+  // out of order, every value the old one's: the old dict iff as many DISTINCT keys — a
+  // duplicated key ({"x":1,"x":1} against {"x":1,"y":2}) must not stand in for a missing one
+  if (same && depth > 0 && PyDict_GET_SIZE(out) == PyDict_GET_SIZE(od)) {
+    Py_DECREF(out);
+    Py_INCREF(od);
+    return od;
   }
   return out;
 }

@@ -92,6 +92,7 @@ class _Informer:
         self.mutations = 0  # store changes: a derived view is current while this stands still
         self.missing_kind = False
         self._rv_waiters: List[Tuple[int, asyncio.Future]] = []
+        self._fill_tombstones: Dict[str, Dict[Tuple[str, str], int]] = {}  # see fill_namespace
 
     def _rv_reached(self) -> None:
         """Resolve read-your-own-write waiters whose resourceVersion this stream has passed."""
@@ -184,23 +185,36 @@ class _Informer:
         """A namespace joined a cluster-wide informer's filter: its objects, dropped until now,
         are listed once (events of it are kept from now on; a listed copy older than one an
         event already brought is not applied)."""
+        # deletions the watch delivers while the list is in flight: key -> resourceVersion.  The
+        # list may have been taken before such a deletion; an object it deleted is not stored
+        # yet (nothing to compare against), so without the tombstone the listed copy would put
+        # it back, a ghost reconciled until the next relist (ADVICE r5)
+        tombs = self._fill_tombstones.setdefault(ns, {})
         try:
-            items, _rv = await self.cache.rest.list_rv(f"{self.info.api_version(self.version)}/{self.info.kind}",
-                                                       ns, self.label_selector, self.field_selector)
-        except Exception:  # noqa: BLE001 — a relist of the whole kind (410 / reconnect) fills it later
-            log.warning("%s: listing namespace %s failed", self.info.kind, ns, exc_info=True)
-            return
-        self.relists += 1
-        if self.ns_filter is not None and not self.ns_filter(ns):
-            return  # left again meanwhile
-        for o in items:
-            o = self._transform(o)
-            k = (m.namespace(o), m.name(o))
-            cur = self.items.get(k)
-            if cur is not None and _rv_num(cur) >= _rv_num(o):
-                continue
-            old = self._put(o)
-            self._notify("ADDED" if old is None else "MODIFIED", o, old)
+            try:
+                items, _rv = await self.cache.rest.list_rv(
+                    f"{self.info.api_version(self.version)}/{self.info.kind}", ns, self.label_selector,
+                    self.field_selector)
+            except Exception:  # noqa: BLE001 — a relist of the whole kind (410 / reconnect) fills it later
+                log.warning("%s: listing namespace %s failed", self.info.kind, ns, exc_info=True)
+                return
+            self.relists += 1
+            if self.ns_filter is not None and not self.ns_filter(ns):
+                return  # left again meanwhile
+            for o in items:
+                o = self._transform(o)
+                k = (m.namespace(o), m.name(o))
+                gone = tombs.get(k)
+                if gone is not None and _rv_num(o) <= gone:
+                    continue
+                cur = self.items.get(k)
+                if cur is not None and _rv_num(cur) >= _rv_num(o):
+                    continue
+                old = self._put(o)
+                self._notify("ADDED" if old is None else "MODIFIED", o, old)
+        finally:
+            if self._fill_tombstones.get(ns) is tombs:
+                del self._fill_tombstones[ns]
 
     def drop_namespace(self, ns: str) -> None:
         """A namespace left a cluster-wide informer's filter: to subscribers its objects are gone."""
@@ -237,6 +251,12 @@ class _Informer:
         if self._rv_waiters:
             self._rv_reached()
 
+    def _tombstone(self, obj: dict) -> None:
+        if self._fill_tombstones:
+            tombs = self._fill_tombstones.get(m.namespace(obj))
+            if tombs is not None:
+                tombs[(m.namespace(obj), m.name(obj))] = _rv_num(obj)
+
     def _stored(self, namespace: str, name: str) -> Optional[dict]:
         return self.items.get((namespace if self.info.namespaced else "", name))
 
@@ -252,9 +272,11 @@ class _Informer:
                 self._label_reqs, (obj.get("metadata") or {}).get("labels")):
             # the object left the selector: to this cache it is gone
             if (m.namespace(obj), m.name(obj)) not in self.items:
+                self._tombstone(obj)
                 return
             et = "DELETED"
         if et == "DELETED":
+            self._tombstone(obj)
             old = self._delete(obj)
             self._notify("DELETED", obj, old)
         else:

@@ -145,3 +145,17 @@ def test_dumps_declines_what_is_not_a_json_tree():
             oc.dumps(bad)
     assert dumps_json({1: "a"}) == b'{"1":"a"}'  # json.dumps's answer
     assert dumps_json((1, "é")) == '[1,"é"]'.encode()
+
+
+def test_a_duplicated_key_never_stands_in_for_a_missing_one():
+    """decoding against an old object, ``{"x":1,"x":1}`` is not ``{"x":1,"y":2}``
+    (json.loads keeps the last duplicate: ``{"x":1}``)."""
+    old = {"a": {"x": 1, "y": 2}}
+    for text in ('{"a":{"x":1,"x":1}}', '{"a":{"y":2,"y":2}}'):
+        got = oc.loads_shared(text.encode(), old)
+        assert got == json.loads(text) and got["a"] is not old["a"]
+    # out of order but complete: still the old subtree
+    got = oc.loads_shared(b'{"a":{"y":2,"x":1}}', old)
+    assert got == {"a": {"x": 1, "y": 2}} and got["a"] is old["a"]
+    got = oc.loads_shared(b'{"a":{"x":1,"y":2}}', old)
+    assert got["a"] is old["a"]

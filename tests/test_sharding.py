@@ -803,3 +803,53 @@ def test_namespace_scoped_kinds_follow_the_namespace_set(run, server_kind):
             await c.close()
             await srv.stop()
     run(go())
+
+
+def test_fill_namespace_does_not_resurrect_an_object_deleted_during_the_list(run):
+    """a namespace joins a cluster-wide informer's filter and is listed once.  A
+    DELETED event of one of its objects that arrives while that list is in flight finds
+    nothing stored; the list, taken before the deletion, must not put the object back."""
+    from odh_kubeflow_amd.models.scheme import SCHEME
+    from odh_kubeflow_amd.runtime.informer import _Informer
+
+    def cm(name, rv):
+        return {"apiVersion": "v1", "kind": "ConfigMap",
+                "metadata": {"name": name, "namespace": "joined", "resourceVersion": str(rv)}}
+
+    class Rest:
+        def __init__(self):
+            self.gate = None
+
+        async def list_rv(self, *a, **kw):
+            await self.gate  # the list's answer is held until the test releases it
+            return [cm("deleted-meanwhile", 5), cm("kept", 7), cm("updated-meanwhile", 4)], "7"
+
+    class Cache:
+        label_index_keys = ()
+        transforms = {}
+        last_event = 0.0
+
+        def __init__(self):
+            self.rest = Rest()
+
+    async def go():
+        cache = Cache()
+        inf = _Informer(cache, SCHEME.resolve(kinds.CONFIG_MAP), "v1")
+        events = []
+        inf.handlers[1] = (None, lambda et, o, old: events.append((et, m.name(o), m.resource_version(o))))
+        cache.rest.gate = asyncio.get_running_loop().create_future()
+        fill = asyncio.ensure_future(inf.fill_namespace("joined"))
+        await asyncio.sleep(0)
+        inf._apply("DELETED", cm("deleted-meanwhile", 6))  # nothing stored yet: only a tombstone
+        inf._apply("MODIFIED", cm("updated-meanwhile", 8))
+        cache.rest.gate.set_result(None)
+        await fill
+        assert ("joined", "deleted-meanwhile") not in inf.items
+        assert m.resource_version(inf.items[("joined", "updated-meanwhile")]) == "8"  # the newer event wins
+        assert ("joined", "kept") in inf.items
+        assert not inf._fill_tombstones  # dropped with the fill
+        assert ("ADDED", "deleted-meanwhile", "5") not in events
+        # outside a fill, deletions leave no tombstone behind
+        inf._apply("DELETED", cm("kept", 9))
+        assert not inf._fill_tombstones and ("joined", "kept") not in inf.items
+    run(go())

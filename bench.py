@@ -123,6 +123,10 @@ def parse(argv=None):
     p.add_argument("--resident-window", type=float, default=3.0, help="seconds measured at rest")
     p.add_argument("--resident-steps", type=int, default=20,
                    help="closed-loop lifecycles per rank on top of the resident population")
+    p.add_argument("--storage-steps", type=int, default=20,
+                   help="after the window: closed-loop lifecycles per rank with --storage-ms of etcd-like latency "
+                        "on every apiserver write (reported in 'storage'; 0: skip)")
+    p.add_argument("--storage-ms", type=float, default=2.0, help="the storage block's per-write latency")
     p.add_argument("--json-out", default=None)
     return p.parse_args(argv)
 

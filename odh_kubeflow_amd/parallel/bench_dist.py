@@ -238,6 +238,11 @@ def measure(args) -> Optional[dict]:
             out["burst"] = res["burst"]
         if res.get("resident"):
             out["resident"] = res["resident"]
+        if res.get("storage"):
+            # the same closed loop on etcd-like storage, beside the zero-latency headline
+            st = out["storage_" + f"{res['storage']['storage_write_latency_ms']:g}ms"] = res["storage"]
+            if out.get("notebooks_ready_per_s") and st.get("notebooks_ready_per_s"):
+                st["notebooks_per_s_vs_headline"] = round(st["notebooks_ready_per_s"] / out["notebooks_ready_per_s"], 3)
         out["config"]["culling"] = (f"on (overlay settings, check period {getattr(args, 'culling_period', 1.0):g} s)"
                                     if culling_enabled(args) else "off")
         if res.get("shard_load"):
@@ -899,6 +904,68 @@ async def _lifecycle(shard, nm: str, ann: Optional[dict], timeout: float = 120.0
     return ready - t0, time.perf_counter() - ready, pod
 
 
+async def _storage_block(args, shard, dist, native, base_ann: dict) -> Optional[dict]:
+    """``--storage-steps`` closed-loop lifecycles per rank (create → Ready → delete → gone, as in
+    the timed window) while the apiserver holds every write ``--storage-ms`` before it commits,
+    as an etcd quorum write does (typically 1-5 ms on SSD-backed etcd; kube-apiserver adds
+    its own).  Reported next to the headline, never in it: notebooks/s, create→Ready
+    percentiles and reconciles/s of the window.  Rank 0 owns the apiserver and sets the
+    latency; every rank reaches every collective (failures are reported)."""
+    from bench import breakdown_delta, merge_breakdowns  # noqa: E402  (bench.py is the entry point)
+
+    ms = float(args.storage_ms)
+    errors: list = []
+    lat: list = []
+    if native is not None:
+        try:
+            await native.set_write_latency(ms)
+        except Exception as e:  # noqa: BLE001
+            errors.append(repr(e)[:300])
+    await _in_thread(dist.barrier)
+    nss = shard.cfg.user_namespaces
+    el = 0.0
+    in_window: dict = {}
+    try:
+        await shard.quiesce(timers=0.05)
+        await _in_thread(dist.barrier)
+        b0 = await shard.reconcile_breakdown()
+        t0 = time.perf_counter()
+        for i in range(int(args.storage_steps)):
+            r, _gone, _pod = await _lifecycle(shard, f"nb-st{i}", dict(base_ann) or None, ns=nss[i % len(nss)])
+            lat.append(r * 1e3)
+        el = time.perf_counter() - t0
+        b1 = await shard.reconcile_breakdown() if shard.cfg.arch == "sharded" else None
+        await _in_thread(dist.barrier)
+        if b1 is None:
+            b1 = await shard.reconcile_breakdown() if shard.procs or shard.managers else {}
+        in_window = breakdown_delta(b0, b1)
+    except Exception as e:  # noqa: BLE001 — reported in the block
+        errors.append(f"rank {dist.get_rank()}: {e!r}"[:300])
+        await _in_thread(dist.barrier)
+    finally:
+        if native is not None:
+            try:
+                await native.set_write_latency(0.0)
+            except Exception as e:  # noqa: BLE001
+                errors.append(repr(e)[:300])
+    gathered = [None] * dist.get_world_size()
+    await _in_thread(dist.all_gather_object, gathered, {"lat": lat, "el": el, "win": in_window, "errors": errors})
+    if dist.get_rank() != 0:
+        return None
+    win = max(g["el"] for g in gathered) or None
+    lat_all = [x for g in gathered for x in g["lat"]]
+    recon = merge_breakdowns(g["win"] for g in gathered)
+    n_recon = sum(sum(t.values()) for t in recon.values())
+    out = {"storage_write_latency_ms": ms, "steps_per_rank": int(args.storage_steps),
+           "notebooks_ready_per_s": round(len(lat_all) / win, 3) if win else None,
+           "ready_ms": _pcts(lat_all), "reconciles_per_s": round(n_recon / win, 1) if win else None,
+           "reconciles_per_notebook": round(n_recon / max(1, len(lat_all)), 2)}
+    errs = [e for g in gathered for e in g["errors"]]
+    if errs:
+        out["errors"] = errs
+    return out
+
+
 async def _drive(args, shard, dist, torch, children: Optional[dict] = None, native=None,
                  probe_sample: int = 0) -> dict:
     from ..ops.probe_main import parse_result
@@ -1022,6 +1089,12 @@ async def _drive(args, shard, dist, torch, children: Optional[dict] = None, nati
         resident = await _resident(args, shard, dist, native, children, use_odh,
                                    statistics.median(lat_ms) if lat_ms else None)
 
+    storage = None
+    if getattr(args, "storage_steps", 0) > 0 and getattr(args, "storage_ms", 0) > 0:
+        # untimed: the same closed loop with every apiserver write paying an etcd-like storage
+        # round trip — the headline's store answers writes in microseconds
+        storage = await _storage_block(args, shard, dist, native, base_ann)
+
     el = torch.tensor([elapsed], dtype=torch.float64)
     await _in_thread(lambda: dist.all_reduce(el, op=dist.ReduceOp.MAX))
     gathered = [None] * dist.get_world_size()
@@ -1064,7 +1137,7 @@ async def _drive(args, shard, dist, torch, children: Optional[dict] = None, nati
             "apiserver_profile_per_step": prof, "breakdown": merge_breakdowns(g["settled"] for g in gathered),
             "quiesced": all(g["idle"] for g in gathered),
             "io_per_notebook": io_per_notebook([g["io"] for g in gathered], args.steps * len(gathered)),
-            "burst": burst, "shard_load": load, "resident": resident,
+            "burst": burst, "shard_load": load, "resident": resident, "storage": storage,
             "recon_snapshot_lag_ms": round(max(g["snap_lag_ms"] for g in gathered), 3),
             "probe_sample": [s for g in gathered for s in g["probe"]],
             "lifecycle_ms_per_20_steps": [round(statistics.fmean(b), 3) for b in zip(*(g["blocks"] for g in gathered))]}

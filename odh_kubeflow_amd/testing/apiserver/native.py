@@ -110,6 +110,16 @@ class NativeApiServer:
             async with s.get(self.url + f"/debug/admissions?from={int(start)}") as r:
                 return await r.json(content_type=None)
 
+    async def set_write_latency(self, ms: float) -> None:
+        """Change the etcd-like per-write storage latency while serving."""
+        import aiohttp
+
+        async with aiohttp.ClientSession(timeout=aiohttp.ClientTimeout(total=30)) as s:
+            async with s.post(self.url + "/debug/storage-latency", json={"ms": float(ms)}) as r:
+                if r.status != 200:
+                    raise RuntimeError(f"storage-latency: HTTP {r.status}: {await r.text()}")
+        self.write_latency_ms = float(ms)
+
     async def stop(self) -> None:
         if self.proc is not None and self.proc.returncode is None:
             self.proc.terminate()

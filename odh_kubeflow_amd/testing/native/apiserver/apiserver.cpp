@@ -629,7 +629,7 @@ struct Store {
   // for the same notebooks/s and no watch answered 410 Gone, nor in 64-notebook bursts or the
   // 8-rank CPU rehearsal (profiles/r4_hist)
   size_t history = 512;
-  int64_t write_latency_us = 0;
+  std::atomic<int64_t> write_latency_us{0};  // --write-latency-ms; POST /debug/storage-latency
   bool gc = false;
   bool defaulting = true;  // kube-apiserver defaulting of Pods / StatefulSets / Deployments / Services
   std::atomic<uint64_t> requests{0}, writes{0}, webhook_calls{0};
@@ -797,7 +797,8 @@ void init_buckets() {
 
 // an etcd-like storage round trip before a write commits (--write-latency-ms), no lock held
 void storage_latency() {
-  if (S.write_latency_us > 0) std::this_thread::sleep_for(std::chrono::microseconds(S.write_latency_us));
+  const int64_t us = S.write_latency_us.load(std::memory_order_relaxed);
+  if (us > 0) std::this_thread::sleep_for(std::chrono::microseconds(us));
 }
 
 void index_owner(const Res& r, const Value& o, bool remove) {
@@ -3013,6 +3014,25 @@ bool handle(int fd, Request& rq) {
       return respond(fd, 400, "{\"error\":\"bad json\"}", rq.keep_alive);
     } catch (const std::exception& e) {
       return respond(fd, 500, kj::dump(status_obj(Internal(e.what()))), rq.keep_alive);
+    }
+  }
+  if (rq.method == "POST" && rq.path == "/debug/storage-latency") {
+    // the etcd-like write latency, changed while serving: {"ms": 2} (a benchmark's realistic-
+    // storage block after its zero-latency window)
+    try {
+      Value in = kj::parse(rq.body);
+      const Value* ms = in.get("ms");
+      double v = -1;
+      if (ms && ms->t == kj::T::Int) v = (double)ms->i;
+      else if (ms && ms->t == kj::T::Double) v = ms->d;
+      if (!(v >= 0 && v <= 10000)) throw PatchErr{"ms: 0..10000 required"};
+      S.write_latency_us.store((int64_t)(v * 1000.0));
+      return respond(fd, 200, "{\"write_latency_us\":" + std::to_string(S.write_latency_us.load()) + "}",
+                     rq.keep_alive);
+    } catch (const PatchErr& e) {
+      return respond(fd, 400, "{\"error\":\"" + e.msg + "\"}", rq.keep_alive);
+    } catch (const kj::ParseError&) {
+      return respond(fd, 400, "{\"error\":\"bad json\"}", rq.keep_alive);
     }
   }
   if (rq.method == "GET" && rq.path == "/version") {

@@ -44,6 +44,15 @@ def summary(path: str) -> str:
                    f"checks/s={a.get('culler_checks_per_s')} kf+odh NB-triggered={a.get('notebook_triggered_reconciles_kf_odh')}")
         out.append(f"  at rest cpu ms/s={json.dumps({k.replace('control_plane_', 'cp_'): v for k, v in (a.get('cpu_ms_per_s') or {}).items()})}")
         out.append(f"  at rest rss MiB={json.dumps({k.replace('control_plane_', 'cp_'): v for k, v in (a.get('rss_mib') or {}).items()})}")
+    if r:
+        a = r.get("at_rest") or {}
+        out.append(f"  webhook heartbeats/s fast={a.get('webhook_heartbeat_fast_path_per_s')} "
+                   f"full={a.get('webhook_heartbeat_full_pipeline_per_s')} admissions/s={a.get('admissions_per_s')}")
+    for k, st in sorted(d.items()):
+        if k.startswith("storage_") and isinstance(st, dict):
+            out.append(f"  {k}: {st.get('notebooks_ready_per_s')} nb/s (x{st.get('notebooks_per_s_vs_headline')}), "
+                       f"ready p50/p95={(st.get('ready_ms') or {}).get('p50')}/{(st.get('ready_ms') or {}).get('p95')} "
+                       f"rec/s={st.get('reconciles_per_s')}" + (f" errors={st['errors']}" if st.get("errors") else ""))
     b = d.get("burst")
     if b:
         out.append(f"  burst {b.get('notebooks')}: {b.get('notebooks_per_s')} nb/s, ready p50/p99 "

@@ -116,6 +116,9 @@ def parse(argv=None):
     p.add_argument("--culling-period", type=float, default=1.0,
                    help="the culler's check period in seconds (IDLENESS_CHECK_PERIOD_SECONDS; the overlays' "
                         "is 60): every resident notebook is checked, and its Notebook written, once per period")
+    p.add_argument("--culler-stamp-every", type=int, default=10,
+                   help="CULL_CHECK_STAMP_EVERY of the culler (the MI355X overlays' 10; 1: the reference's write "
+                        "of the check stamp on every check)")
     p.add_argument("--resident", type=int, default=256,
                    help="after the window: this many notebooks created and left running with the culler on "
                         "(the reference's loadtest scenario); reported: the control plane's cost at rest and "

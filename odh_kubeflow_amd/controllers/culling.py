@@ -117,6 +117,9 @@ class CullerConfig:
     gpu_vram_active_bytes: float = 0.0  # 0: resident VRAM is not activity (see module docstring)
     http_timeout_s: float = 10.0
     startup_allowance_s: float = 600.0  # a Pending pod younger than cull_idle_time + this is not checked
+    # write last_activity_check_timestamp on every k-th check of a notebook whose check changed
+    # nothing else (1: every check, as the reference does) — see CullingReconciler.reconcile
+    check_stamp_every: int = 1
 
     @classmethod
     def from_env(cls, env: Mapping[str, str] = os.environ) -> "CullerConfig":
@@ -151,6 +154,11 @@ class CullerConfig:
         c.startup_allowance_s = float(env_default(env, "CULL_STARTUP_ALLOWANCE", "10")) * 60.0
         if env.get("CULL_STARTUP_ALLOWANCE_SECONDS"):
             c.startup_allowance_s = float(env["CULL_STARTUP_ALLOWANCE_SECONDS"])
+        raw = env_default(env, "CULL_CHECK_STAMP_EVERY", "1")
+        try:
+            c.check_stamp_every = max(1, int(raw))
+        except ValueError:
+            raise ValueError(f"CULL_CHECK_STAMP_EVERY must be a positive integer, got {raw!r}")
         return c
 
 
@@ -587,6 +595,10 @@ class CullingReconciler:
             "CULLER_USE_POD_ENDPOINT", "false") == "true")
         self.culled = 0
         self.checks = 0
+        self.stamps_skipped = 0  # checks whose only change, the check stamp, was not written
+        # (namespace, name) -> when this process last checked the notebook (whole seconds): the
+        # schedule when the stored stamp is older (CULL_CHECK_STAMP_EVERY > 1)
+        self._checked: dict = {}
         from collections import deque
         self.recent = deque(maxlen=64)  # (time, notebook, gpu_active, kernels, terminals) — debugging aid
         # per cull: which signal decided it ("amdgpu" = an attributed GPU sample said idle;
@@ -656,9 +668,8 @@ class CullingReconciler:
 
     async def reconcile(self, req: Request) -> Result:
         nb = await self._read(kinds.NOTEBOOK_V1BETA1, req.name, req.namespace)
-        if nb is None:
-            return Result()
-        if m.is_deleting(nb):
+        if nb is None or m.is_deleting(nb):
+            self._checked.pop((req.namespace, req.name), None)
             return Result()
         if stop_annotation_is_set(nb):
             if annotations_exist(nb) or any(k in m.annotations(nb) for k in (
@@ -692,17 +703,26 @@ class CullingReconciler:
             nb = await self._read(kinds.NOTEBOOK_V1BETA1, req.name, req.namespace)
             if nb is None:
                 return Result()
-        if not culling_check_period_has_passed(nb, self.cfg.check_period_s):
-            last = parse_rfc3339(m.annotations(nb).get(LAST_ACTIVITY_CHECK_TIMESTAMP_ANNOTATION))
-            return Result(requeue_after=self._next_check(req, last if last is not None else now()))
+        key = (req.namespace, req.name)
+        mem = self._checked.get(key)
+        if not culling_check_period_has_passed(nb, self.cfg.check_period_s) or (
+                mem is not None and mem + self.cfg.check_period_s >= now()):
+            stored = parse_rfc3339(m.annotations(nb).get(LAST_ACTIVITY_CHECK_TIMESTAMP_ANNOTATION))
+            last = max([t for t in (stored, mem) if t is not None], default=now())
+            return Result(requeue_after=self._next_check(req, last))
 
         self.checks += 1
         active_now, kernels, terminals, signals = await self.sample(nb, pod)
         self.recent.append((rfc3339(), str(req), active_now, kernels, terminals))
-        culled = []
+        culled, skipped = [], []
+        every = self.cfg.check_stamp_every
 
         def apply(cur: dict) -> None:
             culled.clear()
+            skipped.clear()
+            ann = m.annotations(cur)
+            before = {k: ann.get(k) for k in (LAST_ACTIVITY_ANNOTATION, LAST_ACTIVITY_CHECK_TIMESTAMP_ANNOTATION,
+                                               STOP_ANNOTATION)}
             if active_now:
                 m.ensure_annotations(cur)[LAST_ACTIVITY_ANNOTATION] = rfc3339()
             else:
@@ -716,8 +736,26 @@ class CullingReconciler:
             if notebook_is_idle(cur, self.cfg.cull_idle_time_s):
                 set_stop_annotation(cur, self.metrics)
                 culled.append(True)
+            if every > 1:
+                # The reference rewrites the check stamp on every check (:171-196); nothing but
+                # its own schedule reads it, and that is kept here in memory.  When the check
+                # changed nothing else and the stored stamp is younger than every-1 periods (and
+                # a half), the write is left out: an idle notebook costs the apiserver, the
+                # webhook and every Notebook watcher one write per `every` checks instead of one
+                # per check.  The stamp stays an RFC 3339 instant at most `every` periods old,
+                # which any reader (a reference culler taking over) takes as "check now".
+                after = m.annotations(cur)
+                stored = parse_rfc3339(before[LAST_ACTIVITY_CHECK_TIMESTAMP_ANNOTATION])
+                if (after.get(LAST_ACTIVITY_ANNOTATION) == before[LAST_ACTIVITY_ANNOTATION]
+                        and after.get(STOP_ANNOTATION) == before[STOP_ANNOTATION] and stored is not None
+                        and now() - stored < (every - 0.5) * self.cfg.check_period_s):
+                    after[LAST_ACTIVITY_CHECK_TIMESTAMP_ANNOTATION] = before[LAST_ACTIVITY_CHECK_TIMESTAMP_ANNOTATION]
+                    skipped.append(True)
 
         await self._update(req, apply)
+        self._checked[key] = float(int(now()))
+        if skipped:
+            self.stamps_skipped += 1
         if culled:
             self.culled += 1
             self.cull_log.append({"notebook": str(req), "at": rfc3339(), **signals})

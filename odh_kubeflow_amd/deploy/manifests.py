@@ -96,7 +96,10 @@ MI355X_PARAMS = ["GPU_NODE_SELECTOR=true", "GPU_SHM_SIZE_PER_GPU=16Gi",
                  "MULTI_GPU_ENV=HSA_ENABLE_IPC_MODE_LEGACY=0",
                  # non-root containers of GPU pods get these gids as supplementalGroups
                  f"GPU_DEVICE_GROUPS={MI355X_DEVICE_GROUPS}"]
-MI355X_CULLER = ["CULLING_ACTIVITY_SOURCE=combined", "ENABLE_CULLING=true"]
+# CULL_CHECK_STAMP_EVERY: an idle notebook's last_activity_check_timestamp is rewritten on every
+# 10th check (10 min at the 1 min period) instead of every check — one Notebook write, admission
+# and watch fan-out per idle notebook per 10 periods (controllers/culling.py)
+MI355X_CULLER = ["CULLING_ACTIVITY_SOURCE=combined", "ENABLE_CULLING=true", "CULL_CHECK_STAMP_EVERY=10"]
 # overlay mi355x: each manager runs its controllers in this many namespace-partitioned worker
 # processes (runtime/workers.py; the odh webhook stays on the supervisor's own event loop) —
 # one core per worker, so an 8-GPU node's notebooks are not serialised on one Python loop

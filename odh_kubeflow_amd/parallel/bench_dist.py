@@ -105,7 +105,8 @@ def culler_env(args, proxy_url: Optional[str]) -> dict:
     No node-agent CA is configured, so the amdgpu half of ``combined`` has no samples and the
     Jupyter signal decides (the GPU signal is config #5's)."""
     env = {"ENABLE_CULLING": "true", "CULLING_ACTIVITY_SOURCE": "combined",
-           "IDLENESS_CHECK_PERIOD_SECONDS": f"{getattr(args, 'culling_period', 1.0):g}"}
+           "IDLENESS_CHECK_PERIOD_SECONDS": f"{getattr(args, 'culling_period', 1.0):g}",
+           "CULL_CHECK_STAMP_EVERY": str(getattr(args, "culler_stamp_every", 10))}
     if proxy_url:
         env.update(DEV="true", CULLER_DEV_PROXY_URL=proxy_url)
     return env

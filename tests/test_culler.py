@@ -2,6 +2,7 @@
 with the Jupyter API over HTTP and with the amdgpu busy signal (native telemetry on a
 synthetic sysfs tree)."""
 
+import asyncio
 import time
 
 import pytest
@@ -467,3 +468,42 @@ def test_culler_write_rules(run):
     assert "resourceVersion" not in first["metadata"]
     assert check["metadata"]["resourceVersion"] == "7"
     assert STOP_ANNOTATION in stop["metadata"]["annotations"] and stop["metadata"]["resourceVersion"] == "7"
+
+
+def test_check_stamp_written_every_kth_check_when_nothing_else_changes(run):
+    """CULL_CHECK_STAMP_EVERY=k: an idle notebook's check stamp is written on every k-th check
+    only (the reference writes it on every check, :171-196; nothing but the culler's own
+    schedule reads it).  The checks still run every period, the stamp stays RFC 3339 and at
+    most k periods old, and an activity change is written at once."""
+    rt = JupyterContainerRuntime()
+    k, period = 3, 1.0
+
+    async def go():
+        async with LocalCluster(_cfg(rt, IDLENESS_CHECK_PERIOD_SECONDS=str(period),
+                                     CULL_CHECK_STAMP_EVERY=str(k))) as cl:
+            await cl.ensure_namespace("user")
+            await cl.admin.create(notebook("nb", "user"))
+            assert await cl.wait_for(lambda: cl.notebook_ready("nb", "user"), 20)
+            st = rt.state("user", "nb")
+            st.start_kernel(busy=False)
+            nb = lambda: cl.store.peek(kinds.NOTEBOOK, "nb", "user")  # noqa: E731
+            assert await cl.wait_for(lambda: c.annotations_exist(nb()), 10)
+            culler = cl.reconcilers["culler"]
+            c0, s0 = culler.checks, culler.stamps_skipped
+            stamps, ages = set(), []
+            t_end = time.monotonic() + 6.5 * period
+            while time.monotonic() < t_end:
+                a = m.annotations(nb())
+                stamps.add(a[LAST_ACTIVITY_CHECK_TIMESTAMP_ANNOTATION])
+                ages.append(time.time() - timeutil.parse_rfc3339(a[LAST_ACTIVITY_CHECK_TIMESTAMP_ANNOTATION]))
+                await asyncio.sleep(0.05)
+            checks, skipped = culler.checks - c0, culler.stamps_skipped - s0
+            assert checks >= 5, checks
+            assert skipped >= checks // 2, (checks, skipped)
+            assert len(stamps) <= checks - skipped + 1
+            assert max(ages) <= k * period + 1.5  # whole-second stamps
+            # activity is written at once: a busy kernel moves last-activity on the next check
+            la0 = m.annotations(nb())[LAST_ACTIVITY_ANNOTATION]
+            st.start_kernel(busy=True)
+            assert await cl.wait_for(lambda: m.annotations(nb())[LAST_ACTIVITY_ANNOTATION] != la0, 3 * period)
+    run(go(), timeout=60)

@@ -1,6 +1,6 @@
 #!/bin/bash
 # One measurement pass on a GPU box (run through gpurun from the repo root):
-#   tools/gpu_pass.sh <tag> [tests] [driver N] [long STEPS] [resident R] [streams K]
+#   tools/gpu_pass.sh <tag> [tests] [driver N] [long STEPS] [resident R K] [streams K ARCH]
 # Every GPU step has its own time limit and the steps are chained: the first failure ends
 # the pass (no retries).  Results land in gpurun_out/<tag>/.
 set -o pipefail
@@ -35,11 +35,13 @@ while [ $# -gt 0 ]; do
         || { echo "long run failed rc=$?" | tee -a "$out/SUMMARY.txt"; exit 1; }
       python tools/summarize_bench.py "$out/long_$steps.log" | tee -a "$out/SUMMARY.txt" ;;
     resident)
-      r=$1; shift
+      # resident R K: R notebooks at rest, the culler writing its check stamp every K-th check
+      r=$1; k=$2; shift 2
+      f="$out/resident_${r}_k${k}_$(date +%s)"
       timeout -k 10 900 python bench.py --gpus 1 --steps 100 --warmup 10 --no-configs --burst 0 --storage-steps 0 \
-        --no-gpu-probe --resident "$r" --resident-window 5 --resident-steps 40 --json-out "$out/resident_$r.json" \
-        > "$out/resident_$r.log" 2>&1 || { echo "resident run failed rc=$?" | tee -a "$out/SUMMARY.txt"; exit 1; }
-      python tools/summarize_bench.py "$out/resident_$r.log" | tee -a "$out/SUMMARY.txt" ;;
+        --no-gpu-probe --resident "$r" --culler-stamp-every "$k" --resident-window 5 --resident-steps 40 \
+        --json-out "$f.json" > "$f.log" 2>&1 || { echo "resident run failed rc=$?" | tee -a "$out/SUMMARY.txt"; exit 1; }
+      python tools/summarize_bench.py "$f.log" | tee -a "$out/SUMMARY.txt" ;;
     streams)
       k=$1; shift
       arch=${1:-sharded}; shift

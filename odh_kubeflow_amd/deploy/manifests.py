@@ -70,7 +70,7 @@ MWC_NAME = "mutating-webhook-configuration"
 SHARDS = 8  # one control-plane shard per MI355X of an 8-GPU node
 CULLER_LITERALS = ["ENABLE_CULLING=false", "CULL_IDLE_TIME=1440", "IDLENESS_CHECK_PERIOD=1",
                    "CULLING_ACTIVITY_SOURCE=jupyter", "CULLING_GPU_BUSY_THRESHOLD=5",
-                   "CULLING_GPU_AGENT_PORT=9464", "CULLING_GPU_VRAM_ACTIVE_BYTES=0"]
+                   "CULLING_GPU_AGENT_PORT=9464", "CULLING_GPU_VRAM_ACTIVE_BYTES=0", "CULL_CHECK_STAMP_EVERY=1"]
 CULLER_KEYS = [lit.split("=", 1)[0] for lit in CULLER_LITERALS]
 PARAMS_ENV = "USE_ISTIO=false\nISTIO_GATEWAY=kubeflow/kubeflow-gateway\nISTIO_HOST=*\n" \
              "CLUSTER_DOMAIN=cluster.local\nADD_FSGROUP=true\nGPU_NODE_SELECTOR=false\n" \

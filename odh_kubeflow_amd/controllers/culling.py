@@ -739,16 +739,22 @@ class CullingReconciler:
             if every > 1:
                 # The reference rewrites the check stamp on every check (:171-196); nothing but
                 # its own schedule reads it, and that is kept here in memory.  When the check
-                # changed nothing else and the stored stamp is younger than every-1 periods (and
-                # a half), the write is left out: an idle notebook costs the apiserver, the
-                # webhook and every Notebook watcher one write per `every` checks instead of one
-                # per check.  The stamp stays an RFC 3339 instant at most `every` periods old,
-                # which any reader (a reference culler taking over) takes as "check now".
+                # changed nothing else, the stamp is written only in this notebook's slot of an
+                # `every`-period cycle (its slot: a second hash of its key, independent of its phase in
+                # the period, so R idle notebooks write
+                # R/every stamps per period, evenly, not all in the same period).  An idle
+                # notebook costs the apiserver, the webhook and every Notebook watcher one write
+                # per `every` checks instead of one per check.  The stamp stays an RFC 3339
+                # instant at most `every` periods (and a half) old, which any reader — a
+                # reference culler taking over — takes as "check now".
                 after = m.annotations(cur)
                 stored = parse_rfc3339(before[LAST_ACTIVITY_CHECK_TIMESTAMP_ANNOTATION])
+                p = self.cfg.check_period_s
+                t = now()
+                my_slot = int(_phase_of(req.name, req.namespace) * every)
                 if (after.get(LAST_ACTIVITY_ANNOTATION) == before[LAST_ACTIVITY_ANNOTATION]
                         and after.get(STOP_ANNOTATION) == before[STOP_ANNOTATION] and stored is not None
-                        and now() - stored < (every - 0.5) * self.cfg.check_period_s):
+                        and t - stored < (every + 0.5) * p and int(t // p) % every != my_slot):
                     after[LAST_ACTIVITY_CHECK_TIMESTAMP_ANNOTATION] = before[LAST_ACTIVITY_CHECK_TIMESTAMP_ANNOTATION]
                     skipped.append(True)
 

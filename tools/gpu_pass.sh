@@ -37,11 +37,25 @@ while [ $# -gt 0 ]; do
     resident)
       # resident R K: R notebooks at rest, the culler writing its check stamp every K-th check
       r=$1; k=$2; shift 2
-      f="$out/resident_${r}_k${k}_$(date +%s)"
+      f="$out/resident_${r}_k${k}_p${CULLING_PERIOD:-1}_$(date +%s)"
       timeout -k 10 900 python bench.py --gpus 1 --steps 100 --warmup 10 --no-configs --burst 0 --storage-steps 0 \
         --no-gpu-probe --resident "$r" --culler-stamp-every "$k" --resident-window 5 --resident-steps 40 \
+        --culling-period "${CULLING_PERIOD:-1}" \
         --json-out "$f.json" > "$f.log" 2>&1 || { echo "resident run failed rc=$?" | tee -a "$out/SUMMARY.txt"; exit 1; }
       python tools/summarize_bench.py "$f.log" | tee -a "$out/SUMMARY.txt" ;;
+    rescp)
+      # rescp R K: the resident run with the apiserver's audit log, then the create->Ready critical
+      # path hop by hop of the timed (empty-cluster) notebooks and of those created on top
+      r=$1; k=$2; shift 2
+      f="$out/rescp_${r}_k${k}"
+      DEBUG_WRITE_AUDITLOG=$PWD/$f.audit.jsonl timeout -k 10 900 python bench.py --gpus 1 --steps 100 --warmup 10 \
+        --no-configs --burst 0 --storage-steps 0 --no-gpu-probe --resident "$r" --culler-stamp-every "$k" \
+        --resident-window 5 --resident-steps 40 --json-out "$f.json" > "$f.log" 2>&1 \
+        || { echo "rescp run failed rc=$?" | tee -a "$out/SUMMARY.txt"; exit 1; }
+      python tools/summarize_bench.py "$f.log" | tee -a "$out/SUMMARY.txt"
+      python tools/critical_path.py "$f.audit.jsonl" --name-prefix nb-s > "$f.cp_timed.json" || exit 1
+      python tools/critical_path.py "$f.audit.jsonl" --name-prefix nb-res- > "$f.cp_on_top.json" || exit 1
+      rm -f "$f.audit.jsonl" ;;
     streams)
       k=$1; shift
       arch=${1:-sharded}; shift

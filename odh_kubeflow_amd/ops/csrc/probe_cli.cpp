@@ -49,6 +49,7 @@ extern "C" {
 int odh_gemm_shape_ok(int M, int N, int K);
 int odh_gemm_tiles(int M, int N, int K);
 int odh_probe_fill(void* A, void* Bt, int M, int N, int K, hipStream_t stream);
+int odh_probe_preload();
 int odh_probe_gemm_verify(const void* A, const void* Bt, int M, int N, int K, int* tile_xcd, int* xcd_blocks,
                           unsigned* err_total, unsigned* err_xcd, hipStream_t stream);
 int odh_hbm_write(void* buf, size_t bytes, uint32_t seed, int nontemporal, hipStream_t stream);
@@ -468,8 +469,30 @@ extern "C" int odh_probe_cli(int argc, char** argv) {
     for (Dev& x : devs) release(x);
     return done(2, fail_json("hip", err, ms_since(t_start)));
   };
+  // the code object loads on a second thread while this one allocates (both host-side work
+  // the pod waits for; the runtime serialises neither against the other)
+  std::vector<int> preload_rc(ndev, 0);
+  std::thread preload([&] {
+    for (int i = 0; i < ndev; ++i) {
+      hipError_t se = hipSetDevice(i);
+      preload_rc[i] = se != hipSuccess ? (int)se : odh_probe_preload();
+    }
+  });
+  bool alloc_ok = true;
+  Dev* bad = nullptr;
   for (Dev& d : devs)
-    if (!setup_alloc(d, o)) return fail_all(d);
+    if (!setup_alloc(d, o)) {
+      alloc_ok = false;
+      bad = &d;
+      break;
+    }
+  preload.join();
+  if (!alloc_ok) return fail_all(*bad);
+  for (int i = 0; i < ndev; ++i)
+    if (preload_rc[i] != 0) {
+      devs[i].error = std::string("odh_probe_preload: ") + hipGetErrorString((hipError_t)preload_rc[i]);
+      return fail_all(devs[i]);
+    }
   const double t_malloc = ms_since(t_start);
   for (Dev& d : devs)
     if (!setup_fill(d, o)) return fail_all(d);

@@ -126,6 +126,8 @@ def parse(argv=None):
     p.add_argument("--resident-window", type=float, default=3.0, help="seconds measured at rest")
     p.add_argument("--resident-steps", type=int, default=20,
                    help="closed-loop lifecycles per rank on top of the resident population")
+    p.add_argument("--resident-warmup", type=int, default=10,
+                   help="untimed lifecycles per rank before those (as --warmup before the window)")
     p.add_argument("--storage-steps", type=int, default=20,
                    help="after the window: closed-loop lifecycles per rank with --storage-ms of etcd-like latency "
                         "on every apiserver write (reported in 'storage'; 0: skip)")

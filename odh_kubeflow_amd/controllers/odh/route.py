@@ -180,12 +180,11 @@ async def reconcile_reference_grant(client, nb: dict, central_namespace: str) ->
 
 
 async def is_last_notebook_in_namespace(client, nb: dict) -> bool:
-    from ...runtime.client import list_readonly
+    from ...runtime.client import any_readonly
 
-    for other in await list_readonly(client, kinds.NOTEBOOK, m.namespace(nb)):
-        if m.name(other) != m.name(nb) and not m.is_deleting(other):
-            return False
-    return True
+    name = m.name(nb)
+    return not await any_readonly(client, kinds.NOTEBOOK, m.namespace(nb),
+                                  lambda other: m.name(other) != name and not m.is_deleting(other))
 
 
 async def delete_reference_grant_if_last_notebook(client, nb: dict) -> Optional[bool]:

@@ -548,7 +548,15 @@ async def _resident(args, shard, dist, native, children: dict, use_odh: bool,
     # ---- new notebooks on top of the population
     lat = []
     base = dict(ann or {})
+    # untimed warm-up lifecycles first, as the empty-cluster window has (--warmup): after the
+    # rest window every process has been idle (or only checking), and the first lifecycles of a
+    # cold box run slower whatever the population
+    for i in range(max(0, int(getattr(args, "resident_warmup", 10)))):
+        if await safe(_lifecycle(shard, f"nb-rew-{i}", dict(base) or None, ns=nss[i % len(nss)])) is None:
+            break
+    await safe(shard.quiesce(timers=0.05))
     gc0 = {k: v["seq"] for k, v in ((await safe(shard.gc_pauses(), {})) or {}).items()} if shard.procs else {}
+    top0 = await safe(shard.io_counters(), {})
     for i in range(max(0, int(getattr(args, "resident_steps", 20)))):
         r = await safe(_lifecycle(shard, f"nb-res-{i}", dict(base) or None, ns=nss[i % len(nss)]))
         if r is None:
@@ -558,6 +566,8 @@ async def _resident(args, shard, dist, native, children: dict, use_odh: bool,
     # notebooks in their caches a generation-2 pass walks all of them
     gcp = {k: [x[1:] for x in v["pauses"]] for k, v in ((await safe(shard.gc_pauses(gc0), {})) or {}).items()} \
         if shard.procs else {}
+    await safe(shard.quiesce())
+    top_io = io_delta(top0 or {}, await safe(shard.io_counters(), {}) or {})
     await _in_thread(dist.barrier)
 
     # ---- teardown
@@ -580,7 +590,7 @@ async def _resident(args, shard, dist, native, children: dict, use_odh: bool,
         "in_window": breakdown_delta(b0 or {}, b1 or {}), "io": io_delta(io0 or {}, io1 or {}), "prof": rest_prof,
         "adm": (adm1 - adm0) if adm0 is not None and adm1 is not None else None, "heartbeats": heartbeats,
         "heartbeats_full": heartbeats_full,
-        "served": served, "teardown": teardown, "errors": errors, "gc": gcp})
+        "served": served, "teardown": teardown, "errors": errors, "gc": gcp, "top_io": top_io})
     if rank != 0:
         return None
     win = max(g["win"] for g in gathered)
@@ -632,9 +642,15 @@ async def _resident(args, shard, dist, native, children: dict, use_odh: bool,
             "io_per_s": io,
             "rss_mib": {kk: v for g in gathered for kk, v in sorted(g["rss"].items()) if v is not None},
         },
-        "new_notebooks_on_top": {"steps_per_rank": int(getattr(args, "resident_steps", 20)), "ready_ms": _pcts(lat),
+        "new_notebooks_on_top": {"steps_per_rank": int(getattr(args, "resident_steps", 20)),
+                                 "warmup_per_rank": int(getattr(args, "resident_warmup", 10)), "ready_ms": _pcts(lat),
                                  "empty_cluster_p50_ms": round(empty_p50_ms, 3) if empty_p50_ms else None,
                                  "p50_vs_empty": round(p50 / empty_p50_ms, 3) if p50 and empty_p50_ms else None,
+                                 # per on-top notebook, to compare with the window's io_per_notebook:
+                                 # what an R-sized cache costs each lifecycle (cache_scans: objects
+                                 # list() examined that no index narrowed)
+                                 "io_per_notebook": io_per_notebook([g["top_io"] for g in gathered],
+                                                                    max(1, len(lat))),
                                  "gc_pause_ms": {proc: {"n": len(ps), "max": max(x[1] for x in ps),
                                                         "gen2": sum(1 for x in ps if x[0] == 2)}
                                                  for g in gathered for proc, ps in sorted(g["gc"].items()) if ps}},
@@ -650,7 +666,7 @@ def io_delta(a: dict, b: dict) -> dict:
     for proc, cur in b.items():
         prev = a.get(proc) or {}
         d = {}
-        for sect in ("watch_events", "requests", "lists"):
+        for sect in ("watch_events", "requests", "lists", "cache_scans"):
             p0 = prev.get(sect) or {}
             dd = {k: v - p0.get(k, 0) for k, v in (cur.get(sect) or {}).items()}
             d[sect] = {k: v for k, v in dd.items() if v}

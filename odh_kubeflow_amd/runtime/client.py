@@ -175,13 +175,13 @@ class Client(abc.ABC):
             raise
 
 
-async def list_readonly(client, kind, namespace=None, labels=None, fields=None):
-    """``client.list_readonly`` when the client has it (a cached client: no copies), else
-    ``client.list``; the items must not be mutated either way."""
-    fn = getattr(client, "list_readonly", None)
+async def any_readonly(client, kind, namespace, pred) -> bool:
+    """Whether some object of ``kind`` in ``namespace`` satisfies ``pred``: from the cache with
+    an early exit when the client has one (``CachedClient.any_readonly``), else over a list."""
+    fn = getattr(client, "any_readonly", None)
     if fn is not None:
-        return await fn(kind, namespace, labels, fields)
-    return await client.list(kind, namespace, labels, fields)
+        return await fn(kind, namespace, pred)
+    return any(pred(o) for o in await client.list(kind, namespace))
 
 
 class CachedClient(Client):
@@ -510,14 +510,15 @@ class CachedClient(Client):
                 o["apiVersion"] = av
         return items
 
-    async def list_readonly(self, kind, namespace=None, labels=None, fields=None, owner_uid=None):
-        """:meth:`list` without the copies: the cache's own objects, which the caller must not
-        mutate (a scan that only reads — e.g. "is another Notebook alive in the namespace", once
-        per deletion, over every Notebook of the namespace)."""
-        if self._live(kind, namespace) and owner_uid is None:
-            return await self.writer.list(kind, namespace, labels, fields)
+    async def any_readonly(self, kind, namespace, pred) -> bool:
+        """:func:`any_readonly` on this client's cache (objects shared: ``pred`` must not mutate)."""
+        if self._live(kind, namespace):
+            return any(pred(o) for o in await self.writer.list(kind, namespace))
         await self._ensure(kind)
-        return self.reader.list(kind, namespace, labels, fields, owner_uid)
+        scan = getattr(self.reader, "any", None)
+        if scan is not None:
+            return scan(kind, namespace, pred)
+        return any(pred(o) for o in self.reader.list(kind, namespace))
 
     def _begin(self, obj, precondition: Optional[int] = None, name: Optional[str] = None,
                namespace: Optional[str] = None) -> Optional[Tuple[str, str, str]]:

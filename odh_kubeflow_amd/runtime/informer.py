@@ -400,6 +400,8 @@ class InformerCache(Reader, EventSource):
         self.rescopes = 0
         self.watch_timeout_s = watch_timeout_s
         self.label_index_keys = frozenset(LABEL_INDEX_KEYS if label_index_keys is None else label_index_keys)
+        # kind -> cached objects list() examined: the scans an index did not narrow (io counters)
+        self.list_scans: Dict[str, int] = {}
         self._groups: Dict[str, _Group] = {}
         self._by_ref: Dict[str, _Group] = {}
         self._hid = 0
@@ -703,6 +705,24 @@ class InformerCache(Reader, EventSource):
             return None
         return tuple((id(i), i.mutations, i.missing_kind) for i in infs)
 
+    def any(self, kind, namespace: Optional[str], pred) -> bool:
+        """Whether some cached object of ``kind`` (in ``namespace``) satisfies ``pred`` — stopping
+        at the first: "is another Notebook of this namespace alive" costs one or two looks, not
+        a sorted copy of every Notebook in it (the odh reconciler asks it once per deletion)."""
+        n = 0
+        try:
+            for inf in self._for_ns(kind, namespace):
+                keys = inf.by_ns.get(namespace, ()) if namespace and inf.info.namespaced else inf.items.keys()
+                for k in keys:
+                    n += 1
+                    o = inf.items.get(k)
+                    if o is not None and pred(o):
+                        return True
+            return False
+        finally:
+            kk = SCHEME.resolve(kind).kind
+            self.list_scans[kk] = self.list_scans.get(kk, 0) + n
+
     def list(self, kind, namespace=None, labels=None, fields=None, owner_uid=None) -> List[dict]:
         infs = self._for_ns(kind, namespace)
         if isinstance(labels, dict):
@@ -715,6 +735,7 @@ class InformerCache(Reader, EventSource):
         indexed = next(((k, vals[0]) for k, op, vals in reqs if op == "=" and k in self.label_index_keys), None) \
             if reqs and self.label_index_keys else None
         out = []
+        scans = self.list_scans
         for inf in infs:
             if owner_uid is not None:
                 keys = inf.by_owner.get(owner_uid, ())
@@ -726,7 +747,9 @@ class InformerCache(Reader, EventSource):
                 keys = inf.by_ns.get(namespace, ())
             else:
                 keys = inf.items.keys()
-            for k in list(keys):
+            keys = list(keys)
+            scans[inf.info.kind] = scans.get(inf.info.kind, 0) + len(keys)
+            for k in keys:
                 o = inf.items.get(k)
                 if o is None:
                     continue

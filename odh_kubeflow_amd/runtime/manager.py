@@ -309,7 +309,8 @@ class Manager:
         ev = cache.event_counts() if hasattr(cache, "event_counts") else {}
         lists = cache.relist_counts() if hasattr(cache, "relist_counts") else {}
         return {"watch_events": ev, "requests": dict(getattr(rest, "by_verb", {}) or {}), "lists": lists,
-                "bytes_in": dict(getattr(rest, "bytes_in", {}) or {})}
+                "bytes_in": dict(getattr(rest, "bytes_in", {}) or {}),
+                "cache_scans": dict(getattr(cache, "list_scans", {}) or {})}
 
     def reconcile_count(self) -> int:
         return sum(c.reconciles for c in self.controllers)

@@ -66,6 +66,56 @@ while [ $# -gt 0 ]; do
         --storage-steps 0 "${extra[@]}" --json-out "$out/streams_${k}_$arch.json" > "$out/streams_${k}_$arch.log" 2>&1 \
         || { echo "streams $k $arch failed rc=$?" | tee -a "$out/SUMMARY.txt"; exit 1; }
       python tools/summarize_bench.py "$out/streams_${k}_$arch.log" | tee -a "$out/SUMMARY.txt" ;;
+    failover)
+      # takeover and cold start with R resident notebooks (tools/bench_failover.py)
+      r=$1; shift
+      timeout -k 10 600 python tools/bench_failover.py --resident "$r" > "$out/failover_$r.log" 2>&1 \
+        || { echo "failover failed rc=$?" | tee -a "$out/SUMMARY.txt"; exit 1; }
+      tail -1 "$out/failover_$r.log" | cut -c1-600 | tee -a "$out/SUMMARY.txt" ;;
+    nsscale)
+      # 4 ranks x M namespaces each (balanced assigner), per-namespace or cluster-wide watches
+      m=$1; mode=$2; shift 2
+      cw=(); [ "$mode" = cw ] && cw=(--cluster-wide-watches)
+      f="$out/ns_m${m}_$mode"
+      timeout -k 10 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 4 --master-addr 127.0.0.1 \
+        --master-port 29523 bench.py --gpus 4 --steps 100 --warmup 10 --no-gpu-probe --burst 0 --resident 0 \
+        --storage-steps 0 --namespaces-per-rank "$m" --assign-policy balanced "${cw[@]}" --json-out "$f.json" \
+        > "$f.log" 2>&1 || { echo "nsscale $m $mode failed rc=$?" | tee -a "$out/SUMMARY.txt"; exit 1; }
+      python tools/summarize_bench.py "$f.log" | tee -a "$out/SUMMARY.txt" ;;
+    burst)
+      # burst K ARCH: K notebooks at once into one control plane (sharded | unsharded | workers)
+      k=$1; arch=$2; shift 2
+      extra=(); [ "$arch" = unsharded ] && extra=(--arch unsharded)
+      [ "$arch" = workers ] && extra=(--arch unsharded --workers 4 --kf-split-workers --webhook-replicas 3 --cache-configmaps)
+      f="$out/burst${k}_$arch"
+      timeout -k 10 600 python bench.py --gpus 1 --steps 20 --warmup 5 --no-configs --no-gpu-probe --resident 0 \
+        --storage-steps 0 --burst "$k" "${extra[@]}" --json-out "$f.json" > "$f.log" 2>&1 \
+        || { echo "burst $k $arch failed rc=$?" | tee -a "$out/SUMMARY.txt"; exit 1; }
+      python tools/summarize_bench.py "$f.log" | tee -a "$out/SUMMARY.txt" ;;
+    critpath)
+      # the closed loop's create->Ready critical path from the audit log, N=1 and 4 ranks
+      DEBUG_WRITE_AUDITLOG=$PWD/$out/a1.jsonl timeout -k 10 300 python bench.py --steps 200 --burst 0 --probe-sample 0 \
+        --no-configs --resident 0 --storage-steps 0 > "$out/critpath_n1.log" 2>&1 || exit 1
+      python tools/critical_path.py "$out/a1.jsonl" --name-prefix nb-s > "$out/critical_path_n1.json" || exit 1
+      DEBUG_WRITE_AUDITLOG=$PWD/$out/a4.jsonl timeout -k 10 300 python -m torch.distributed.run --nnodes=1 \
+        --nproc-per-node 4 --master-addr 127.0.0.1 --master-port 29934 bench.py --gpus 4 --steps 100 --warmup 5 \
+        --burst 0 --probe-sample 0 --no-configs --resident 0 --storage-steps 0 > "$out/critpath_n4.log" 2>&1 || exit 1
+      python tools/critical_path.py "$out/a4.jsonl" --name-prefix nb-s > "$out/critical_path_n4.json" || exit 1
+      rm -f "$out/a1.jsonl" "$out/a4.jsonl"
+      python -c "import json,sys; [print(f, json.load(open(f))['create_to_notebook_status_ms']) for f in sys.argv[1:]]" \
+        "$out/critical_path_n1.json" "$out/critical_path_n4.json" | tee -a "$out/SUMMARY.txt" ;;
+    probeprof)
+      # rocprofv3 kernel trace + stats of one odh-gpu-probe run (no counters: a plain trace)
+      ODH_PROBE_EXIT_NORMALLY=1 timeout -k 10 120 rocprofv3 --kernel-trace --stats -d "$out/probeprof" -o probe -- \
+        ./odh_kubeflow_amd/ops/_lib/odh-gpu-probe --json - > "$out/probeprof.log" 2>&1 \
+        || { echo "probeprof failed rc=$?" | tee -a "$out/SUMMARY.txt"; exit 1; }
+      for i in 1 2 3 4 5; do
+        timeout -k 10 60 ./odh_kubeflow_amd/ops/_lib/odh-gpu-probe --json - --quiet >> "$out/probe_runs.jsonl" 2>&1 || exit 1
+      done
+      find "$out/probeprof" -name '*kernel_stats.csv' -exec cp {} "$out/probe_kernel_stats.csv" \;
+      echo "probe runs:" | tee -a "$out/SUMMARY.txt"
+      python -c "import json,sys; [print(json.loads(l).get('timings_ms')) for l in open(sys.argv[1]) if l.startswith('{')]" \
+        "$out/probe_runs.jsonl" | tee -a "$out/SUMMARY.txt" ;;
     *) echo "unknown step $what"; exit 2 ;;
   esac
 done

@@ -93,17 +93,22 @@ while [ $# -gt 0 ]; do
         || { echo "burst $k $arch failed rc=$?" | tee -a "$out/SUMMARY.txt"; exit 1; }
       python tools/summarize_bench.py "$f.log" | tee -a "$out/SUMMARY.txt" ;;
     critpath)
-      # the closed loop's create->Ready critical path from the audit log, N=1 and 4 ranks
+      # critpath ARCH: the closed loop's create->Ready critical path from the audit log, N=1 and
+      # 4 ranks (ARCH sharded, or workers = overlay mi355x)
+      arch=$1; shift
+      extra=()
+      [ "$arch" = workers ] && extra=(--arch unsharded --workers 4 --kf-split-workers --webhook-replicas 3 --cache-configmaps)
       DEBUG_WRITE_AUDITLOG=$PWD/$out/a1.jsonl timeout -k 10 300 python bench.py --steps 200 --burst 0 --probe-sample 0 \
-        --no-configs --resident 0 --storage-steps 0 > "$out/critpath_n1.log" 2>&1 || exit 1
-      python tools/critical_path.py "$out/a1.jsonl" --name-prefix nb-s > "$out/critical_path_n1.json" || exit 1
+        --no-configs --resident 0 --storage-steps 0 "${extra[@]}" > "$out/critpath_${arch}_n1.log" 2>&1 || exit 1
+      python tools/critical_path.py "$out/a1.jsonl" --name-prefix nb-s > "$out/critical_path_${arch}_n1.json" || exit 1
       DEBUG_WRITE_AUDITLOG=$PWD/$out/a4.jsonl timeout -k 10 300 python -m torch.distributed.run --nnodes=1 \
         --nproc-per-node 4 --master-addr 127.0.0.1 --master-port 29934 bench.py --gpus 4 --steps 100 --warmup 5 \
-        --burst 0 --probe-sample 0 --no-configs --resident 0 --storage-steps 0 > "$out/critpath_n4.log" 2>&1 || exit 1
-      python tools/critical_path.py "$out/a4.jsonl" --name-prefix nb-s > "$out/critical_path_n4.json" || exit 1
+        --burst 0 --probe-sample 0 --no-configs --resident 0 --storage-steps 0 "${extra[@]}" \
+        > "$out/critpath_${arch}_n4.log" 2>&1 || exit 1
+      python tools/critical_path.py "$out/a4.jsonl" --name-prefix nb-s > "$out/critical_path_${arch}_n4.json" || exit 1
       rm -f "$out/a1.jsonl" "$out/a4.jsonl"
       python -c "import json,sys; [print(f, json.load(open(f))['create_to_notebook_status_ms']) for f in sys.argv[1:]]" \
-        "$out/critical_path_n1.json" "$out/critical_path_n4.json" | tee -a "$out/SUMMARY.txt" ;;
+        "$out/critical_path_${arch}_n1.json" "$out/critical_path_${arch}_n4.json" | tee -a "$out/SUMMARY.txt" ;;
     probeprof)
       # rocprofv3 kernel trace + stats of one odh-gpu-probe run (no counters: a plain trace)
       ODH_PROBE_EXIT_NORMALLY=1 timeout -k 10 120 rocprofv3 --kernel-trace --stats -d "$out/probeprof" -o probe -- \

@@ -573,3 +573,47 @@ def test_image_resolution_orders_items_by_instant(run, items, want):
         await set_container_image_from_registry(admin, nb, "opendatahub")
         assert nb["spec"]["template"]["spec"]["containers"][0]["image"] == f"quay.io/x@{want}"
     run(go())
+
+
+def test_heartbeat_fast_path_follows_the_cluster_proxy_and_elyra_inputs(run):
+    """The fingerprint covers the optional inputs when their features are on: a new cluster
+    Proxy (INJECT_CLUSTER_PROXY_ENV) or a DSPA change (SET_PIPELINE_SECRET) sends the next
+    heartbeat through the pipeline."""
+    from odh_kubeflow_amd.models.notebook import LAST_ACTIVITY_ANNOTATION, LAST_ACTIVITY_CHECK_TIMESTAMP_ANNOTATION
+
+    async def go():
+        store, admin, wh = await _setup(env={"INJECT_CLUSTER_PROXY_ENV": "true", "SET_PIPELINE_SECRET": "true"})
+        await admin.create(notebook("nb", "user"))
+        await admin.patch(kinds.NOTEBOOK, {"metadata": {"annotations": {"kubeflow-resource-stopped": None}}},
+                          name="nb", namespace="user")
+        n = [0]
+
+        async def beat():
+            n[0] += 1
+            await admin.patch(kinds.NOTEBOOK, {"metadata": {"annotations": {
+                LAST_ACTIVITY_ANNOTATION: "2026-01-01T00:00:00Z",
+                LAST_ACTIVITY_CHECK_TIMESTAMP_ANNOTATION: f"2026-01-01T00:{n[0]:02d}:00Z"}}}, name="nb", namespace="user")
+            return m.annotations(store.peek(kinds.NOTEBOOK, "nb", "user")).get(ANNOTATION_UPDATE_PENDING)
+
+        await beat()
+        f0, h0 = wh.heartbeats_full, wh.heartbeats
+        assert await beat() is None
+        assert (wh.heartbeats_full - f0, wh.heartbeats - h0) == (0, 1)
+        # the cluster Proxy appears: the pipeline runs and reports the env it would add
+        await create_with_status(admin, {"apiVersion": "config.openshift.io/v1", "kind": "Proxy",
+                                         "metadata": {"name": "cluster"},
+                                         "status": {"httpProxy": "http://p:3128", "httpsProxy": "http://p:3129",
+                                                    "noProxy": ".svc"}})
+        pending = await beat()
+        assert wh.heartbeats_full - f0 == 1 and pending and "env" in pending
+        await beat()  # the marked notebook becomes the fixed point ...
+        h1, f1 = wh.heartbeats, wh.heartbeats_full
+        await beat()  # ... and heartbeats are cheap again
+        assert (wh.heartbeats - h1, wh.heartbeats_full - f1) == (1, 0)
+        # a DSPA object appears in the namespace: another input, another full run
+        await admin.create({"apiVersion": "datasciencepipelinesapplications.opendatahub.io/v1",
+                            "kind": "DataSciencePipelinesApplication", "metadata": {"name": "dspa", "namespace": "user"},
+                            "spec": {}})
+        await beat()
+        assert wh.heartbeats_full - f1 == 1
+    run(go())

@@ -106,18 +106,18 @@ MI355X_CULLER = ["CULLING_ACTIVITY_SOURCE=combined", "ENABLE_CULLING=true", "CUL
 MI355X_WORKERS = 4
 # --webhook-replicas: at 4 streams the one webhook process (the supervisor, which also leads and
 # watches cluster-wide) ran ≈75 % busy; 1 / 2 / 4 webhook processes gave 561–572 / 586 / 598–606
-# notebooks/s, interleaved (profiles/r5_p13).  With the final tree (connections recycled, so
+# notebooks/s, interleaved (pass r5_p13).  With the final tree (connections recycled, so
 # every process gets its share) 3 beat 2 in every interleaved run: 751–760 vs 667–745
-# notebooks/s (profiles/r5_f10, r5_f11)
+# notebooks/s (pass r5_f10, r5_f11)
 MI355X_WEBHOOK_REPLICAS = 3
 # kf --split-workers: each namespace set served by a notebook-reconciler process and a culler +
 # event re-emitter process, as a shard pod does; with 2 webhook processes, against neither, at 4
-# streams: 607 / 627 vs 596 / 605 notebooks/s, interleaved (profiles/r5_p15; split alone
-# 590 / 605 vs 560 / 587, profiles/r5_p14)
+# streams: 607 / 627 vs 596 / 605 notebooks/s, interleaved (pass r5_p15; split alone
+# 590 / 605 vs 560 / 587, pass r5_p14)
 MI355X_KF_SPLIT_WORKERS = True
 # the odh manager caches ConfigMap/Secret data, as a shard does: the webhook and the reconcilers
 # read them from the cache instead of confirming absences live (+12 % notebooks/s at 4 streams,
-# interleaved on one box, profiles/r4_p16); the reference's overlays keep its uncached reads
+# interleaved on one box, pass r4_p16); the reference's overlays keep its uncached reads
 MI355X_CACHE_CONFIGMAPS = True
 # the base manifests carry the development tag; every overlay pins the release tag through
 # kustomize `images` (releasing/VERSION, set by tools/release.py — the reference's
@@ -639,9 +639,9 @@ def control_plane_statefulset(shards: int) -> dict:
     ``--controllers``: ``notebook`` (the kf notebook reconciler + event re-emitter + the
     namespace assigner), ``culler``, ``odh`` and ``webhook`` — four event loops, so an admission
     never waits behind a reconcile, the odh pipeline never behind kf (the webhook's own process:
-    ``profiles/r4_p11``), and a new notebook's kf hops never behind the culler's periodic checks
+    ``pass r4_p11``), and a new notebook's kf hops never behind the culler's periodic checks
     of every resident notebook (R=1000 checked every second: new-notebook create→Ready 1.14× the
-    empty cluster's with the culler apart, 1.32× with it in the kf process; ``profiles/r5_p5``)."""
+    empty cluster's with the culler apart, 1.32× with it in the kf process; ``pass r5_p5``)."""
     common = ["--shard=ordinal", "--leader-elect", "--kube-rbac-proxy-image=$(KUBE_RBAC_PROXY_IMAGE)"]
     kf = _control_plane_container("manager-kf", common + ["--controllers=notebook", f"--shard-count={shards}",
                                                           "--assign-namespaces", "--assign-policy=balanced"],

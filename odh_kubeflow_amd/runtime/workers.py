@@ -5,7 +5,7 @@ worker each (``kf/main.go:87-98``, ``odh/main.go:155-192``).  A Py
 is one event loop, so one manager process tops out at one core however many reconcile
 workers it runs: measured on an MI355X box with the reference topology
 (``config/overlays/mi355x``), the kf and odh managers each burnt ≈1 core at 4 notebook
-streams and throughput stopped scaling (49 % efficiency, ``profiles/r3_p35``), with the
+streams and throughput stopped scaling (49 % efficiency, ``pass r3_p35``), with the
 odh webhook's admissions queued behind the reconciles on the same loop.
 
 ``--workers W`` keeps the deployment unit — one Deployment, one replica, one leader lease,

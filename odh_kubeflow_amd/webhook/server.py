@@ -127,7 +127,7 @@ class WebhookServer:
         # replicas sharing the port: the apiserver's pooled connections are re-made every 100
         # admissions, so each replica keeps getting its share (one TLS handshake per 100: ~10 µs
         # per admission).  At 1000 a 4-stream benchmark window never recycled, and one replica
-        # in two of the runs sat idle (profiles/r5_f10)
+        # in two of the runs sat idle (pass r5_f10)
         self._server = await Http1Server(self._handle, self.host, self.port, self._ctx,
                                          reuse_port=self.reuse_port,
                                          max_requests_per_conn=RECYCLE_AFTER if self.reuse_port else 0).start()

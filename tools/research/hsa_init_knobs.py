@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Does any ROCr runtime setting shorten ``hsa_init`` — the ~180 ms floor of the
-odh-gpu-probe init container (profiles/r3_p8)?
+odh-gpu-probe init container (pass r3_p8)?
 
 Runs ``tools/research/native/hip_init_bench`` in its ``ODH_HSA_ONLY`` mode (hsa_init, then exit)
 under each setting, interleaved round by round so box drift hits every setting alike, and

@@ -358,8 +358,8 @@ class NotebookWebhook:
 
     @staticmethod
     def _notebook_token(nb: dict) -> Optional[tuple]:
-        """What the pipeline reads of the Notebook: its spec (through ``generation``) and its
-        annotations other than the culler's heartbeat pair."""
+        """What the pipeline reads of the Notebook: its spec (through ``generation``), its labels
+        (the Feast mount follows one) and its annotations other than the culler's heartbeat pair."""
         from ..models.notebook import CULLER_HEARTBEAT_ANNOTATIONS
 
         md = nb.get("metadata") or {}
@@ -368,7 +368,8 @@ class NotebookWebhook:
             return None
         ann = md.get("annotations") or {}
         return (md.get("uid"), gen, tuple(sorted((k, v) for k, v in ann.items()
-                                                 if k not in CULLER_HEARTBEAT_ANNOTATIONS)))
+                                                 if k not in CULLER_HEARTBEAT_ANNOTATIONS)),
+                tuple(sorted((md.get("labels") or {}).items())))
 
     def _heartbeat_settled(self, obj: dict) -> bool:
         """A heartbeat may skip the pipeline iff the notebook is, as stored, the pipeline's

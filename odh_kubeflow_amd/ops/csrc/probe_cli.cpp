@@ -472,11 +472,13 @@ extern "C" int odh_probe_cli(int argc, char** argv) {
   // the code object loads on a second thread while this one allocates (both host-side work
   // the pod waits for; the runtime serialises neither against the other)
   std::vector<int> preload_rc(ndev, 0);
+  double t_preload = 0;
   std::thread preload([&] {
     for (int i = 0; i < ndev; ++i) {
       hipError_t se = hipSetDevice(i);
       preload_rc[i] = se != hipSuccess ? (int)se : odh_probe_preload();
     }
+    t_preload = ms_since(t_start);
   });
   bool alloc_ok = true;
   Dev* bad = nullptr;
@@ -486,6 +488,7 @@ extern "C" int odh_probe_cli(int argc, char** argv) {
       bad = &d;
       break;
     }
+  const double t_alloc_only = ms_since(t_start);
   preload.join();
   if (!alloc_ok) return fail_all(*bad);
   for (int i = 0; i < ndev; ++i)
@@ -600,12 +603,12 @@ extern "C" int odh_probe_cli(int argc, char** argv) {
     rccl = b;
   }
   for (Dev& d : devs) release(d);
-  char tail[384];
+  char tail[448];
   std::snprintf(tail, sizeof tail,
                 ",\"timings_ms\":{\"exec\":%.3f,\"hip_init\":%.3f,\"alloc_fill\":%.3f,\"alloc\":%.3f,"
-                "\"fill\":%.3f,\"probe\":%.3f,\"xgmi\":%.3f,\"rccl\":%.3f,\"total\":%.3f}}",
-                t_exec, t_init, t_alloc - t_init, t_malloc - t_init, t_alloc - t_malloc, probe_ms, link_ms,
-                rr.load_ms + rr.init_ms + rr.wall_ms, ms_since(t_start));
+                "\"code_load\":%.3f,\"fill\":%.3f,\"probe\":%.3f,\"xgmi\":%.3f,\"rccl\":%.3f,\"total\":%.3f}}",
+                t_exec, t_init, t_alloc - t_init, t_alloc_only - t_init, t_preload - t_init, t_alloc - t_malloc, probe_ms,
+                link_ms, rr.load_ms + rr.init_ms + rr.wall_ms, ms_since(t_start));
   std::string json = std::string("{\"ok\":") + (ok ? "true" : "false") + ",\"devices\":" + std::to_string(ndev) +
                      ",\"shape\":[" + std::to_string(o.M) + "," + std::to_string(o.N) + "," + std::to_string(o.K) +
                      "],\"hbm_mib\":" + std::to_string(o.hbm_bytes >> 20) +

@@ -272,7 +272,7 @@ def probe_report(samples: list, p50_off: Optional[float]) -> dict:
         "added_ms_p50_vs_probe_off": round(p50 - p50_off, 3) if p50 is not None and p50_off is not None else None,
         "init_container_wall_ms_p50": med(s.get("wall_ms") for s in samples),
         "probe_timings_ms_p50": {k: med(t.get(k) for t in tim if (t.get(k) or 0) >= 0)
-                                 for k in ("exec", "hip_init", "alloc_fill", "alloc", "fill", "probe", "total")},
+                                 for k in ("exec", "hip_init", "alloc_fill", "alloc", "code_load", "fill", "probe", "total")},
         "gemm_tflops_p50": med(d.get("gemm_tflops") for d in dev),
         "hbm_gbps_p50": med(d.get("hbm_gbps") for d in dev),
         "mechanism": "init container odh-gpu-probe (ops/csrc/probe_cli.cpp, no torch), injected by the kf "

@@ -118,6 +118,8 @@ while [ $# -gt 0 ]; do
         timeout -k 10 60 ./odh_kubeflow_amd/ops/_lib/odh-gpu-probe --json - --quiet >> "$out/probe_runs.jsonl" 2>&1 || exit 1
       done
       find "$out/probeprof" -name '*kernel_stats.csv' -exec cp {} "$out/probe_kernel_stats.csv" \;
+      for db in "$out"/probeprof/*.db; do [ -f "$db" ] && python tools/rocpd_stats.py "$db" > "$out/probe_kernel_stats.csv"; done
+      rm -f "$out"/probeprof/*.db
       echo "probe runs:" | tee -a "$out/SUMMARY.txt"
       python -c "import json,sys; [print(json.loads(l).get('timings_ms')) for l in open(sys.argv[1]) if l.startswith('{')]" \
         "$out/probe_runs.jsonl" | tee -a "$out/SUMMARY.txt" ;;

@@ -94,6 +94,7 @@ struct Dev {
   hipEvent_t e_r0 = nullptr, e_r1 = nullptr;
   uint32_t seed = 0;
   float gemm_ms = 0, hbm_ms = 0, link_ms = 0, rccl_ms = 0;
+  double malloc_ms = 0, streams_ms = 0, events_ms = 0;  // host-side set-up, step by step
   int link_source = -1;
   std::string error;
 };
@@ -202,17 +203,23 @@ bool setup_alloc(Dev& d, const Options& o) {
   HIP_TRY(hipSetDevice(d.index));
   const size_t na = align_up((size_t)o.M * o.K * 2), nb = align_up((size_t)o.N * o.K * 2);
   const size_t nh = align_up(o.hbm_bytes), nt = align_up(sizeof(int) * (size_t)(o.M / 128) * (o.N / 128));
+  auto t0 = Clock::now();
   HIP_TRY(hipMalloc(&d.block, na + nb + nh + nt + align_up(sizeof(int) * NCOUNT)));
+  d.malloc_ms = ms_since(t0);
   char* p = (char*)d.block;
   d.a = p;
   d.bt = p + na;
   d.hbm = p + na + nb;
   d.tile_xcd = (int*)(p + na + nb + nh);
   d.counters = (int*)(p + na + nb + nh + nt);
+  t0 = Clock::now();
   HIP_TRY(hipStreamCreateWithFlags(&d.sg, hipStreamNonBlocking));
   HIP_TRY(hipStreamCreateWithFlags(&d.sh, hipStreamNonBlocking));
+  d.streams_ms = ms_since(t0);
+  t0 = Clock::now();
   for (hipEvent_t* e : {&d.e0, &d.e_gemm, &d.e_h0, &d.e_h1, &d.e_link0, &d.e_link1, &d.e_r0, &d.e_r1})
     HIP_TRY(hipEventCreate(e));
+  d.events_ms = ms_since(t0);
   return true;
 }
 
@@ -609,10 +616,13 @@ extern "C" int odh_probe_cli(int argc, char** argv) {
                 "\"code_load\":%.3f,\"fill\":%.3f,\"probe\":%.3f,\"xgmi\":%.3f,\"rccl\":%.3f,\"total\":%.3f}}",
                 t_exec, t_init, t_alloc - t_init, t_alloc_only - t_init, t_preload - t_init, t_alloc - t_malloc, probe_ms,
                 link_ms, rr.load_ms + rr.init_ms + rr.wall_ms, ms_since(t_start));
+  char setup[160];
+  std::snprintf(setup, sizeof setup, ",\"setup_ms\":{\"malloc\":%.3f,\"streams\":%.3f,\"events\":%.3f}",
+                devs[0].malloc_ms, devs[0].streams_ms, devs[0].events_ms);
   std::string json = std::string("{\"ok\":") + (ok ? "true" : "false") + ",\"devices\":" + std::to_string(ndev) +
                      ",\"shape\":[" + std::to_string(o.M) + "," + std::to_string(o.N) + "," + std::to_string(o.K) +
                      "],\"hbm_mib\":" + std::to_string(o.hbm_bytes >> 20) +
                      (first_err.empty() ? "" : ",\"error\":\"" + esc(first_err) + "\"") + ",\"results\":" + res +
-                     ",\"links\":" + links + rccl + tail;
+                     ",\"links\":" + links + rccl + setup + tail;
   return done(ok ? 0 : 1, json);
 }

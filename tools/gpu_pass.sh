@@ -121,7 +121,7 @@ while [ $# -gt 0 ]; do
       for db in "$out"/probeprof/*.db; do [ -f "$db" ] && python tools/rocpd_stats.py "$db" > "$out/probe_kernel_stats.csv"; done
       rm -f "$out"/probeprof/*.db
       echo "probe runs:" | tee -a "$out/SUMMARY.txt"
-      python -c "import json,sys; [print(json.loads(l).get('timings_ms')) for l in open(sys.argv[1]) if l.startswith('{')]" \
+      python -c "import json,sys; [print(json.loads(l).get('timings_ms'), json.loads(l).get('setup_ms')) for l in open(sys.argv[1]) if l.startswith('{')]" \
         "$out/probe_runs.jsonl" | tee -a "$out/SUMMARY.txt" ;;
     *) echo "unknown step $what"; exit 2 ;;
   esac

@@ -75,6 +75,12 @@ struct Options {
   std::string json_path;  // "" = default; "-" = stdout only
   std::string fault;      // test hook: gemm | hbm | xgmi | rccl
   bool quiet = false;
+  // streams created per device: 0 = the device's null stream (nothing created; the default),
+  // 1 = one stream, 2 = the HBM sweep overlapping the GEMM on a second stream.  Each stream is
+  // a hardware queue: on the MI355X one costs 10-15 ms to create (2 streams: 27-31 ms of
+  // set-up, 1: 22 ms; the null stream's queue, made at its first launch, 17.5 ms), while
+  // overlapping the sweep saves 0.005 ms of GPU time and halves both measured rates (pass r6_g9)
+  int streams = 0;
 };
 
 // device counters: [0:8] workgroups per XCD, [8:16] mismatches per XCD, [16] GEMM mismatches,
@@ -102,7 +108,7 @@ struct Dev {
 int usage(const char* argv0) {
   std::fprintf(stderr,
                "usage: %s [--json PATH|-] [--shape M,N,K] [--hbm-mib N] [--xgmi-mib N] [--rccl-mib N] "
-               "[--timeout-ms N] [--inject-fault gemm|hbm|xgmi|rccl] [--quiet]\n",
+               "[--timeout-ms N] [--streams 0|1|2] [--inject-fault gemm|hbm|xgmi|rccl] [--quiet]\n",
                argv0);
   return 64;
 }
@@ -131,6 +137,9 @@ bool parse(int argc, char** argv, Options& o) {
       o.rccl_bytes = (size_t)std::strtoull(v.c_str(), nullptr, 10) << 20;
     } else if (a == "--timeout-ms") {
       o.timeout_ms = std::strtol(v.c_str(), nullptr, 10);
+    } else if (a == "--streams") {
+      o.streams = (int)std::strtol(v.c_str(), nullptr, 10);
+      if (o.streams < 0 || o.streams > 2) return false;
     } else if (a == "--inject-fault") {
       o.fault = v;
       if (v != "gemm" && v != "hbm" && v != "xgmi" && v != "rccl") return false;
@@ -213,8 +222,9 @@ bool setup_alloc(Dev& d, const Options& o) {
   d.tile_xcd = (int*)(p + na + nb + nh);
   d.counters = (int*)(p + na + nb + nh + nt);
   t0 = Clock::now();
-  HIP_TRY(hipStreamCreateWithFlags(&d.sg, hipStreamNonBlocking));
-  HIP_TRY(hipStreamCreateWithFlags(&d.sh, hipStreamNonBlocking));
+  if (o.streams >= 1) HIP_TRY(hipStreamCreateWithFlags(&d.sg, hipStreamNonBlocking));
+  if (o.streams == 2) HIP_TRY(hipStreamCreateWithFlags(&d.sh, hipStreamNonBlocking));
+  else d.sh = d.sg;
   d.streams_ms = ms_since(t0);
   t0 = Clock::now();
   for (hipEvent_t* e : {&d.e0, &d.e_gemm, &d.e_h0, &d.e_h1, &d.e_link0, &d.e_link1, &d.e_r0, &d.e_r1})
@@ -237,24 +247,32 @@ bool setup_fill(Dev& d, const Options& o) {
 
 bool launch(Dev& d, const Options& o) {
   HIP_TRY(hipSetDevice(d.index));
-  HIP_TRY(hipEventRecord(d.e0, d.sg));
-  HIP_TRY(hipStreamWaitEvent(d.sh, d.e0, 0));
   unsigned* c = (unsigned*)d.counters;
-  // the memory-bound sweep first, on the second stream: the GEMM's one workgroup per CU
-  // co-resides with its waves
-  HIP_TRY(hipEventRecord(d.e_h0, d.sh));
-  HIP_TRY(odh_hbm_write(d.hbm, o.hbm_bytes, d.seed, 0, d.sh));
-  HIP_TRY(odh_hbm_check(d.hbm, o.hbm_bytes, o.fault == "hbm" ? d.seed + 1 : d.seed,
-                        (unsigned long long*)(d.counters + 18), d.sh));
-  HIP_TRY(hipEventRecord(d.e_h1, d.sh));
+  auto sweep = [&]() -> bool {
+    HIP_TRY(hipEventRecord(d.e_h0, d.sh));
+    HIP_TRY(odh_hbm_write(d.hbm, o.hbm_bytes, d.seed, 0, d.sh));
+    HIP_TRY(odh_hbm_check(d.hbm, o.hbm_bytes, o.fault == "hbm" ? d.seed + 1 : d.seed,
+                          (unsigned long long*)(d.counters + 18), d.sh));
+    HIP_TRY(hipEventRecord(d.e_h1, d.sh));
+    return true;
+  };
+  HIP_TRY(hipEventRecord(d.e0, d.sg));
+  if (d.sh != d.sg) {
+    // the memory-bound sweep first, on the second stream: the GEMM's one workgroup per CU
+    // co-resides with its waves
+    HIP_TRY(hipStreamWaitEvent(d.sh, d.e0, 0));
+    if (!sweep()) return false;
+  }
   HIP_TRY(odh_probe_gemm_verify(d.a, d.bt, o.M, o.N, o.K, d.tile_xcd, d.counters, c + 16, c + 8, d.sg));
   HIP_TRY(hipEventRecord(d.e_gemm, d.sg));
+  // one stream: the sweep after the GEMM, so e0..e_gemm still times the GEMM alone
+  if (d.sh == d.sg && !sweep()) return false;
   return true;
 }
 
 bool drain(Dev& d) {
   HIP_TRY(hipSetDevice(d.index));
-  HIP_TRY(hipStreamSynchronize(d.sh));
+  if (d.sh != d.sg) HIP_TRY(hipStreamSynchronize(d.sh));
   HIP_TRY(hipStreamSynchronize(d.sg));
   return true;
 }
@@ -293,8 +311,8 @@ void release(Dev& d) {
   if (d.block) (void)hipFree(d.block);
   for (hipEvent_t e : {d.e0, d.e_gemm, d.e_h0, d.e_h1, d.e_link0, d.e_link1, d.e_r0, d.e_r1})
     if (e) (void)hipEventDestroy(e);
+  if (d.sh && d.sh != d.sg) (void)hipStreamDestroy(d.sh);
   if (d.sg) (void)hipStreamDestroy(d.sg);
-  if (d.sh) (void)hipStreamDestroy(d.sh);
 }
 
 uint64_t u64(const int* h, int i) { return (uint64_t)(uint32_t)h[i] | ((uint64_t)(uint32_t)h[i + 1] << 32); }
@@ -617,8 +635,8 @@ extern "C" int odh_probe_cli(int argc, char** argv) {
                 t_exec, t_init, t_alloc - t_init, t_alloc_only - t_init, t_preload - t_init, t_alloc - t_malloc, probe_ms,
                 link_ms, rr.load_ms + rr.init_ms + rr.wall_ms, ms_since(t_start));
   char setup[160];
-  std::snprintf(setup, sizeof setup, ",\"setup_ms\":{\"malloc\":%.3f,\"streams\":%.3f,\"events\":%.3f}",
-                devs[0].malloc_ms, devs[0].streams_ms, devs[0].events_ms);
+  std::snprintf(setup, sizeof setup, ",\"setup_ms\":{\"malloc\":%.3f,\"streams\":%.3f,\"events\":%.3f,\"n_streams\":%d}",
+                devs[0].malloc_ms, devs[0].streams_ms, devs[0].events_ms, o.streams);
   std::string json = std::string("{\"ok\":") + (ok ? "true" : "false") + ",\"devices\":" + std::to_string(ndev) +
                      ",\"shape\":[" + std::to_string(o.M) + "," + std::to_string(o.N) + "," + std::to_string(o.K) +
                      "],\"hbm_mib\":" + std::to_string(o.hbm_bytes >> 20) +

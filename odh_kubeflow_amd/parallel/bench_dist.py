@@ -557,6 +557,7 @@ async def _resident(args, shard, dist, native, children: dict, use_odh: bool,
     await safe(shard.quiesce(timers=0.05))
     gc0 = {k: v["seq"] for k, v in ((await safe(shard.gc_pauses(), {})) or {}).items()} if shard.procs else {}
     top0 = await safe(shard.io_counters(), {})
+    top_t0 = time.perf_counter()
     for i in range(max(0, int(getattr(args, "resident_steps", 20)))):
         r = await safe(_lifecycle(shard, f"nb-res-{i}", dict(base) or None, ns=nss[i % len(nss)]))
         if r is None:
@@ -568,6 +569,10 @@ async def _resident(args, shard, dist, native, children: dict, use_odh: bool,
         if shard.procs else {}
     await safe(shard.quiesce())
     top_io = io_delta(top0 or {}, await safe(shard.io_counters(), {}) or {})
+    # the population's own traffic (heartbeats) goes on meanwhile: the at-rest rate times this
+    # span is subtracted for the net per-notebook figure
+    top_dt = time.perf_counter() - top_t0
+    top_io_net = io_minus(top_io, io_delta(io0 or {}, io1 or {}), top_dt / max(win, 1e-9))
     await _in_thread(dist.barrier)
 
     # ---- teardown
@@ -590,7 +595,8 @@ async def _resident(args, shard, dist, native, children: dict, use_odh: bool,
         "in_window": breakdown_delta(b0 or {}, b1 or {}), "io": io_delta(io0 or {}, io1 or {}), "prof": rest_prof,
         "adm": (adm1 - adm0) if adm0 is not None and adm1 is not None else None, "heartbeats": heartbeats,
         "heartbeats_full": heartbeats_full,
-        "served": served, "teardown": teardown, "errors": errors, "gc": gcp, "top_io": top_io})
+        "served": served, "teardown": teardown, "errors": errors, "gc": gcp, "top_io": top_io,
+        "top_io_net": top_io_net})
     if rank != 0:
         return None
     win = max(g["win"] for g in gathered)
@@ -651,6 +657,9 @@ async def _resident(args, shard, dist, native, children: dict, use_odh: bool,
                                  # list() examined that no index narrowed)
                                  "io_per_notebook": io_per_notebook([g["top_io"] for g in gathered],
                                                                     max(1, len(lat))),
+                                 # the same, less the at-rest traffic of the span it was counted over
+                                 "io_per_notebook_net_of_rest": io_per_notebook(
+                                     [g["top_io_net"] for g in gathered], max(1, len(lat))),
                                  "gc_pause_ms": {proc: {"n": len(ps), "max": max(x[1] for x in ps),
                                                         "gen2": sum(1 for x in ps if x[0] == 2)}
                                                  for g in gathered for proc, ps in sorted(g["gc"].items()) if ps}},
@@ -671,6 +680,17 @@ def io_delta(a: dict, b: dict) -> dict:
             dd = {k: v - p0.get(k, 0) for k, v in (cur.get(sect) or {}).items()}
             d[sect] = {k: v for k, v in dd.items() if v}
         out[proc] = d
+    return out
+
+
+def io_minus(a: dict, rest: dict, f: float) -> dict:
+    """``a`` less ``f`` times ``rest`` (both :func:`io_delta` results), never below 0."""
+    out = {}
+    for proc, d in a.items():
+        r = rest.get(proc) or {}
+        out[proc] = {sect: {k: v for k, v in ((k, max(0.0, v - f * (r.get(sect) or {}).get(k, 0)))
+                                              for k, v in kv.items()) if v > 1e-9}
+                     for sect, kv in d.items()}
     return out
 
 

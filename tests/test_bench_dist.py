@@ -159,3 +159,16 @@ def test_io_per_notebook_divides_traffic_and_counts_relists():
     assert out["kf"]["requests"] == {"POST": 2.0, "total": 2.0}
     assert out["kf"]["relists_in_window"] == {"Pod": 1, "total": 1} and "lists" not in out["kf"]
     assert "relists_in_window" not in out["odh"]
+
+
+def test_on_top_io_net_of_the_populations_rest_traffic():
+    """The on-top counts include the population's heartbeats of the same span: the at-rest rate
+    times that span comes off, never below zero, and a kind the rest window lacks is kept."""
+    from odh_kubeflow_amd.parallel.bench_dist import io_minus, io_per_notebook
+
+    top = {"culler": {"watch_events": {"Notebook": 130, "Pod": 40}, "requests": {"PATCH": 110, "POST": 30}}}
+    rest = {"culler": {"watch_events": {"Notebook": 300}, "requests": {"PATCH": 300, "GET": 5}}}
+    out = io_per_notebook([io_minus(top, rest, 1 / 3)], 10)  # the on-top span: a third of the rest window
+    assert out["culler"]["watch_events"] == {"Pod": 4.0, "Notebook": 3.0, "total": 7.0}
+    assert out["culler"]["requests"] == {"POST": 3.0, "PATCH": 1.0, "total": 4.0}
+    assert io_minus(top, {}, 1.0) == top

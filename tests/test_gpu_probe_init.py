@@ -201,6 +201,7 @@ def test_probe_program_usage_and_no_gpu_verdict(tmp_path):
     exe = _exe()
     assert subprocess.run([exe, "--bogus"], capture_output=True).returncode == probe_main.USAGE
     assert subprocess.run([exe, "--shape", "100,100,100"], capture_output=True).returncode == probe_main.USAGE
+    assert subprocess.run([exe, "--streams", "3"], capture_output=True).returncode == probe_main.USAGE
     out = tmp_path / "termination-log"
     env = dict(os.environ, HIP_VISIBLE_DEVICES="")  # a pod without GPUs (also on the GPU box)
     r = subprocess.run([exe, "--json", str(out), "--quiet"], capture_output=True, text=True, env=env, timeout=60)
@@ -245,6 +246,7 @@ def test_probe_program_passes_on_the_mi355x():
     d = res["results"][0]
     assert d["gemm_errors"] == 0 and d["hbm_errors"] == 0 and d["xcds"] == 8, d
     assert d["gemm_tflops"] > 50 and d["hbm_gbps"] > 500, d  # ran on the matrix cores and HBM, not a stub
+    assert res["setup_ms"]["n_streams"] == 0 and res["setup_ms"]["streams"] == 0, res
 
 
 @pytest.mark.gpu
@@ -260,6 +262,21 @@ def test_probe_program_fails_on_injected_fault(fault):
         assert d["gemm_errors"] == want and d["hbm_errors"] == 0 and sum(d["err_xcd"]) == want, d
     else:
         assert d["hbm_errors"] > 0 and d["gemm_errors"] == 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("streams", ["1", "2"])
+def test_probe_program_on_created_streams(streams):
+    """``--streams 1`` (one created stream) and ``--streams 2`` (the sweep overlapping the GEMM)
+    check what the default null-stream run checks: a clean pass, and each injected fault found."""
+    rc, res, _wall, r = _run_probe("--streams", streams)
+    assert rc == 0, (r.stdout, r.stderr)
+    d = res["results"][0]
+    assert d["gemm_errors"] == 0 and d["hbm_errors"] == 0 and d["gemm_tflops"] > 50 and d["hbm_gbps"] > 500, d
+    assert res["setup_ms"]["n_streams"] == int(streams)
+    for fault, key in (("gemm", "gemm_errors"), ("hbm", "hbm_errors")):
+        rc, res, _wall, r = _run_probe("--streams", streams, "--inject-fault", fault)
+        assert rc == probe_main.CHECK_FAILED and res["results"][0][key] > 0, (r.stdout, r.stderr)
 
 
 @pytest.mark.gpu

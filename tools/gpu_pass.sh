@@ -123,6 +123,24 @@ while [ $# -gt 0 ]; do
       echo "probe runs:" | tee -a "$out/SUMMARY.txt"
       python -c "import json,sys; [print(json.loads(l).get('timings_ms'), json.loads(l).get('setup_ms')) for l in open(sys.argv[1]) if l.startswith('{')]" \
         "$out/probe_runs.jsonl" | tee -a "$out/SUMMARY.txt" ;;
+    probestreams)
+      # the probe with 2, 1 and 0 created streams, interleaved, K rounds: the set-up time each costs
+      k="$1"; shift
+      for i in $(seq "$k"); do
+        for ns in 2 1 0; do
+          timeout -k 10 60 ./odh_kubeflow_amd/ops/_lib/odh-gpu-probe --json - --quiet --streams "$ns" \
+            >> "$out/probe_streams.jsonl" 2>&1 || exit 1
+        done
+      done
+      python tools/probe_streams.py "$out/probe_streams.jsonl" | tee -a "$out/SUMMARY.txt" ;;
+    probegap)
+      # K probe runs S seconds apart: hip_init with the previous GPU process long gone
+      k="$1"; gap="$2"; shift 2
+      for i in $(seq "$k"); do
+        sleep "$gap"
+        timeout -k 10 60 ./odh_kubeflow_amd/ops/_lib/odh-gpu-probe --json - --quiet >> "$out/probe_gap_$gap.jsonl" 2>&1 || exit 1
+      done
+      python tools/probe_streams.py "$out/probe_gap_$gap.jsonl" | sed "s/^/gap=${gap}s /" | tee -a "$out/SUMMARY.txt" ;;
     *) echo "unknown step $what"; exit 2 ;;
   esac
 done

@@ -49,6 +49,9 @@ def parse(argv=None):
     p.add_argument("--warmup", type=int, default=10)
     p.add_argument("--probe-sample", type=int, default=4,
                    help="after the timed region: notebooks per rank with the odh-gpu-probe init container (needs a GPU)")
+    p.add_argument("--probe-gap-s", type=float, default=0.5,
+                   help="pause before each probe notebook: a GPU process that exited within ~0.15 s "
+                        "still holds the next one's HIP init in the kernel driver's teardown")
     p.add_argument("--no-gpu-probe", action="store_true", help="skip the start-up probe sample (CPU dev runs)")
     p.add_argument("--no-odh", action="store_true", help="kf controller only (no webhook / odh reconciler)")
     p.add_argument("--reference-emulation", action="store_true",

@@ -234,7 +234,8 @@ def measure(args) -> Optional[dict]:
         if rccl_ms is not None:
             out["rccl_allreduce_check_ms"] = round(rccl_ms, 3)
         if res.get("probe_sample"):
-            out["gpu_probe_init_container"] = probe_report(res["probe_sample"], out.get("p50_ready_ms"))
+            out["gpu_probe_init_container"] = dict(probe_report(res["probe_sample"], out.get("p50_ready_ms")),
+                                                   gap_before_each_s=getattr(args, "probe_gap_s", 0.5))
         if res.get("burst"):
             out["burst"] = res["burst"]
         if res.get("resident"):
@@ -1092,6 +1093,9 @@ async def _drive(args, shard, dist, torch, children: Optional[dict] = None, nati
                     owner.setdefault(ns, f"worker_{idx}")
     samples = []
     for i in range(probe_sample):  # untimed: notebooks with the start-up probe init container
+        # spaced: the previous probe's kernel-side GPU teardown (~0.1 s after its exit) would
+        # hold this one's HIP init, which a notebook starting on an idle GPU never waits for
+        await asyncio.sleep(max(0.0, getattr(args, "probe_gap_s", 0.5)))
         ann = {**base_ann, GPU_PROBE_ANNOTATION: "true"}
         try:
             ready_s, _gone, pod = await _lifecycle(shard, f"nb-probe-{i}", ann, timeout=180)

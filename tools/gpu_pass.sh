@@ -141,6 +141,26 @@ while [ $# -gt 0 ]; do
         timeout -k 10 60 ./odh_kubeflow_amd/ops/_lib/odh-gpu-probe --json - --quiet >> "$out/probe_gap_$gap.jsonl" 2>&1 || exit 1
       done
       python tools/probe_streams.py "$out/probe_gap_$gap.jsonl" | sed "s/^/gap=${gap}s /" | tee -a "$out/SUMMARY.txt" ;;
+    probebusy)
+      # K probe runs S seconds apart while another process holds the GPU (a torch context, idle)
+      k="$1"; gap="$2"; shift 2
+      timeout -k 5 240 python -c "import torch, time; torch.zeros(1, device='cuda'); torch.cuda.synchronize(); print('held', flush=True); time.sleep(200)" \
+        > "$out/holder.log" 2>&1 &
+      hp=$!
+      for i in $(seq 150); do grep -q held "$out/holder.log" && break; sleep 1; done
+      grep -q held "$out/holder.log" || { kill "$hp"; wait "$hp"; echo "holder did not start" | tee -a "$out/SUMMARY.txt"; exit 1; }
+      for i in $(seq "$k"); do
+        sleep "$gap"
+        timeout -k 10 60 ./odh_kubeflow_amd/ops/_lib/odh-gpu-probe --json - --quiet >> "$out/probe_busy_$gap.jsonl" 2>&1 \
+          || { kill "$hp"; wait "$hp"; exit 1; }
+      done
+      kill "$hp"; wait "$hp"
+      python tools/probe_streams.py "$out/probe_busy_$gap.jsonl" | sed "s/^/busy gap=${gap}s /" | tee -a "$out/SUMMARY.txt" ;;
+    probechain)
+      # K runs GAP seconds apart, probe args after "--" up to the next step name "end"
+      k="$1"; gap="$2"; shift 2
+      pargs=(); while [ $# -gt 0 ] && [ "$1" != end ]; do pargs+=("$1"); shift; done; [ $# -gt 0 ] && shift
+      timeout -k 10 300 python tools/probe_chain.py "$k" "$gap" "${pargs[@]}" | tee -a "$out/SUMMARY.txt" || exit 1 ;;
     *) echo "unknown step $what"; exit 2 ;;
   esac
 done

@@ -19,7 +19,7 @@ def main(path: str) -> None:
             return round(statistics.median(f(r) for r in rs), 3)
 
         print(f"streams={ns} runs={len(rs)} ok={all(r['ok'] for r in rs)} "
-              f"setup_streams={med(lambda r: r['setup_ms']['streams'])} "
+              f"setup_streams={med(lambda r: r['setup_ms']['streams'])} first_op={med(lambda r: r['setup_ms'].get('first_op', 0))} "
               f"alloc={med(lambda r: r['timings_ms']['alloc'])} code_load={med(lambda r: r['timings_ms']['code_load'])} "
               f"fill={med(lambda r: r['timings_ms']['fill'])} probe={med(lambda r: r['timings_ms']['probe'])} "
               f"hip_init={med(lambda r: r['timings_ms']['hip_init'])} total={med(lambda r: r['timings_ms']['total'])} "

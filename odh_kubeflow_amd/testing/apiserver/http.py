@@ -34,6 +34,7 @@ from ...models import meta as m
 from ...models.errors import ApiError, BadRequest, InternalError, NotFound
 from ...models.scheme import SCHEME, ParsedPath, ResourceInfo, parse_path  # noqa: F401  (re-exported)
 from ...utils import jsonpatch
+from ...utils.celmatch import CelError, Condition, compile_condition, conditions_allow
 from ...utils.selectors import match_labels, selector_from_dict
 from .store import ObjectStore
 
@@ -127,6 +128,7 @@ class WebhookDispatcher:
         name = wh.get("name", "")
         ns_sel = selector_from_dict(wh.get("namespaceSelector")) if wh.get("namespaceSelector") else None
         obj_sel = selector_from_dict(wh.get("objectSelector")) if wh.get("objectSelector") else None
+        conds = [_condition(c) for c in wh.get("matchConditions") or []]
 
         def selected(info: ResourceInfo, obj: dict, old: Optional[dict]) -> bool:
             if obj_sel is not None and not match_labels(obj_sel, m.labels(obj)) and not (
@@ -147,6 +149,11 @@ class WebhookDispatcher:
 
             if not selected(info, obj, old):
                 return obj
+            try:
+                if not conditions_allow(conds, obj, old, fail_closed):
+                    return obj
+            except CelError as e:
+                raise InternalError(f'failed calling webhook "{name}": matchConditions: {e}')
 
             if self._session is None or self._session.closed:
                 # admission calls carry the webhook's own timeoutSeconds; this bounds anything else
@@ -181,6 +188,17 @@ class WebhookDispatcher:
     async def close(self) -> None:
         if self._session is not None:
             await self._session.close()
+
+
+def _condition(mc) -> "Condition":
+    """One ``matchConditions`` entry; an expression outside the evaluated CEL subset errors at
+    every evaluation (``failurePolicy`` decides), as an uncompilable one would."""
+    try:
+        return compile_condition(str((mc or {}).get("expression", "")))
+    except CelError as e:
+        def bad(obj, old, e=e):
+            raise e
+        return bad
 
 
 class ApiServer:

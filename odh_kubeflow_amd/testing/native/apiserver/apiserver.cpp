@@ -1429,7 +1429,168 @@ struct Webhook {
   Value rules;
   bool has_ns_sel = false, has_obj_sel = false;
   std::vector<LReq> ns_sel, obj_sel;
+  std::vector<std::string> conditions;  // matchConditions[].expression
 };
+
+// ------------------------------------------------------------------ matchConditions (a CEL subset)
+// has(<object|oldObject>.<field>...), !, &&, ||, parentheses, true and false: the expressions
+// this repository's configurations use (utils/celmatch.py is the Python apiserver's twin).
+// Anything else fails to compile, and a compile error evaluates as an error: failurePolicy
+// decides.  CEL's logical operators absorb errors (false && err is false, true || err true).
+struct CelErr {
+  std::string msg;
+};
+
+struct CelNode {
+  enum Kind { LIT, NOT, AND, OR, HAS } k = LIT;
+  bool lit = false, old_root = false;
+  std::vector<std::string> path;
+  std::vector<CelNode> kids;
+};
+
+struct CelParser {
+  std::string src;
+  std::vector<std::string> toks;
+  size_t pos = 0;
+
+  explicit CelParser(const std::string& s) : src(s) {
+    size_t i = 0;
+    while (i < src.size()) {
+      const char c = src[i];
+      if (std::isspace((unsigned char)c)) {
+        ++i;
+      } else if ((c == '|' || c == '&') && i + 1 < src.size() && src[i + 1] == c) {
+        toks.push_back(src.substr(i, 2));
+        i += 2;
+      } else if (c == '!' || c == '(' || c == ')' || c == '.') {
+        toks.push_back(std::string(1, c));
+        ++i;
+      } else if (std::isalpha((unsigned char)c) || c == '_') {
+        size_t j = i;
+        while (j < src.size() && (std::isalnum((unsigned char)src[j]) || src[j] == '_')) ++j;
+        toks.push_back(src.substr(i, j - i));
+        i = j;
+      } else {
+        throw CelErr{"unsupported CEL at '" + src.substr(i) + "'"};
+      }
+    }
+  }
+  bool at(const char* t) const { return pos < toks.size() && toks[pos] == t; }
+  std::string take(const char* want = nullptr) {
+    if (pos >= toks.size() || (want && toks[pos] != want))
+      throw CelErr{std::string("expected ") + (want ? want : "a term") + " in '" + src + "'"};
+    return toks[pos++];
+  }
+  CelNode chain(CelNode::Kind k, const char* op, CelNode (CelParser::*next)()) {
+    CelNode first = (this->*next)();
+    if (!at(op)) return first;
+    CelNode n;
+    n.k = k;
+    n.kids.push_back(std::move(first));
+    while (at(op)) {
+      take();
+      n.kids.push_back((this->*next)());
+    }
+    return n;
+  }
+  CelNode disj() { return chain(CelNode::OR, "||", &CelParser::conj); }
+  CelNode conj() { return chain(CelNode::AND, "&&", &CelParser::unary); }
+  CelNode unary() {
+    if (!at("!")) return primary();
+    take();
+    CelNode n;
+    n.k = CelNode::NOT;
+    n.kids.push_back(unary());
+    return n;
+  }
+  CelNode primary() {
+    const std::string t = take();
+    if (t == "(") {
+      CelNode e = disj();
+      take(")");
+      return e;
+    }
+    CelNode n;
+    if (t == "true" || t == "false") {
+      n.lit = t == "true";
+      return n;
+    }
+    if (t != "has") throw CelErr{"unsupported CEL term '" + t + "' in '" + src + "'"};
+    take("(");
+    const std::string root = take();
+    if (root != "object" && root != "oldObject") throw CelErr{"unsupported root '" + root + "' in '" + src + "'"};
+    n.k = CelNode::HAS;
+    n.old_root = root == "oldObject";
+    while (at(".")) {
+      take();
+      const std::string f = take();
+      if (!(std::isalpha((unsigned char)f[0]) || f[0] == '_')) throw CelErr{"unsupported field '" + f + "'"};
+      n.path.push_back(f);
+    }
+    if (n.path.empty()) throw CelErr{"has() needs a field selection in '" + src + "'"};
+    take(")");
+    return n;
+  }
+  CelNode parse() {
+    CelNode n = disj();
+    if (pos != toks.size()) throw CelErr{"trailing tokens in '" + src + "'"};
+    return n;
+  }
+};
+
+bool cel_eval(const CelNode& n, const Value& obj, const Value* old) {
+  switch (n.k) {
+    case CelNode::LIT:
+      return n.lit;
+    case CelNode::NOT:
+      return !cel_eval(n.kids[0], obj, old);
+    case CelNode::AND:
+    case CelNode::OR: {
+      const bool absorbing = n.k == CelNode::OR;
+      bool failed = false;
+      CelErr err;
+      for (const CelNode& k : n.kids) {
+        try {
+          if (cel_eval(k, obj, old) == absorbing) return absorbing;
+        } catch (const CelErr& e) {
+          failed = true;
+          err = e;
+        }
+      }
+      if (failed) throw err;
+      return !absorbing;
+    }
+    case CelNode::HAS: {
+      const Value* cur = n.old_root ? old : &obj;
+      if (!cur || cur->t == T::Null) throw CelErr{std::string(n.old_root ? "oldObject" : "object") + " is null"};
+      for (size_t i = 0; i + 1 < n.path.size(); ++i) {
+        cur = cur->is_obj() ? cur->get(n.path[i]) : nullptr;
+        if (!cur) throw CelErr{"no such key: " + n.path[i]};
+      }
+      if (!cur->is_obj()) throw CelErr{"has() on a non-map before " + n.path.back()};
+      const Value* v = cur->get(n.path.back());
+      return v && v->t != T::Null;
+    }
+  }
+  return false;
+}
+
+// every condition true: call the webhook.  Any false: skip it.  Otherwise an error: refuse
+// the request (failurePolicy Fail) or skip the webhook (Ignore)
+bool conditions_allow(const Webhook& w, const Value& obj, const Value* old) {
+  bool failed = false;
+  std::string msg;
+  for (const std::string& c : w.conditions) {
+    try {
+      if (!cel_eval(CelParser(c).parse(), obj, old)) return false;
+    } catch (const CelErr& e) {
+      failed = true;
+      msg = e.msg;
+    }
+  }
+  if (failed && w.fail_closed) throw Internal("failed calling webhook \"" + w.name + "\": matchConditions: " + msg);
+  return !failed;
+}
 
 // metav1.LabelSelector (matchLabels + matchExpressions) -> requirements
 std::vector<LReq> selector_reqs(const Value& sel) {
@@ -1520,6 +1681,9 @@ std::vector<Webhook> webhooks_for(const Res& r, const std::string& op) {
           w.has_obj_sel = true;
           w.obj_sel = selector_reqs(*os);
         }
+      if (const Value* mc = wh.get("matchConditions"))
+        if (mc->is_arr())
+          for (auto& c : mc->arr) w.conditions.push_back(c.str_or("expression"));
       const Value* cc = wh.get("clientConfig");
       if (cc) {
         std::string ca = cc->str_or("caBundle");
@@ -1838,6 +2002,7 @@ Value admit(const char* op, const Res& r, Value obj, const Value* old) {
   auto hooks = webhooks_for(r, op);
   for (auto& w : hooks) {
     if (!selectors_match(w, r, obj, old)) continue;
+    if (!w.conditions.empty() && !conditions_allow(w, obj, old)) continue;
     Value review = Value::object();
     review["apiVersion"] = Value::str("admission.k8s.io/v1");
     review["kind"] = Value::str("AdmissionReview");

@@ -590,6 +590,15 @@ def matches(info, operation: str) -> bool:
     return info.key == "notebooks.kubeflow.org" and operation in ("CREATE", "UPDATE")
 
 
+# The configuration's matchConditions: the apiserver does not call the webhook for a Notebook
+# that is being deleted.  Its last writes (the controllers' finalizer removals) have nothing to
+# inject into a pod template that is going away: one admission round trip fewer on every
+# deletion.  The reference's configuration has none (odh/config/webhook/manifests.yaml), so its
+# webhook runs the whole pipeline on those writes too.  A terminating Notebook is never
+# validated either (gpu_validation_applies).
+MATCH_CONDITIONS = [{"name": "not-terminating", "expression": "!has(object.metadata.deletionTimestamp)"}]
+
+
 def register_in_process(store, webhook: NotebookWebhook, name: str = "notebooks.opendatahub.io") -> None:
     """Install the webhook as a mutating admission plugin of the in-process apiserver.
 
@@ -601,7 +610,13 @@ def register_in_process(store, webhook: NotebookWebhook, name: str = "notebooks.
 
     from ..models.errors import InternalError
 
+    from ..utils.celmatch import compile_condition, conditions_allow
+
+    conds = [compile_condition(c["expression"]) for c in MATCH_CONDITIONS]
+
     async def handler(op, info, obj, old):
+        if not conditions_allow(conds, obj, old, fail_closed=True):
+            return obj
         review = {"apiVersion": "admission.k8s.io/v1", "kind": "AdmissionReview",
                   "request": {"uid": str(uuid.uuid4()), "operation": op, "name": m.name(obj),
                               "namespace": m.namespace(obj), "object": obj, "oldObject": old,

@@ -25,7 +25,7 @@ from typing import Optional, Tuple
 
 from ..runtime.http1 import Http1Server
 from ..runtime.rest import dumps_json, loads_json  # native JSON, json's on what it declines
-from .notebook_webhook import WEBHOOK_PATH, NotebookWebhook
+from .notebook_webhook import MATCH_CONDITIONS, WEBHOOK_PATH, NotebookWebhook
 
 log = logging.getLogger("webhook.server")
 
@@ -170,6 +170,7 @@ def mutating_webhook_configuration(ca_bundle_b64: str, url: Optional[str] = None
             "timeoutSeconds": 10, "matchPolicy": "Equivalent", "reinvocationPolicy": "Never",
             "rules": [{"apiGroups": ["kubeflow.org"], "apiVersions": ["v1"], "operations": ["CREATE", "UPDATE"],
                        "resources": ["notebooks"]}],
+            "matchConditions": [dict(c) for c in MATCH_CONDITIONS],
             **({"namespaceSelector": namespace_selector} if namespace_selector else {}),
         }],
     }

@@ -64,6 +64,7 @@ def test_critical_path_from_audit_log(run, tmp_path):
     finally:
         sys.path.pop(0)
     from odh_kubeflow_amd.testing.cluster import ClusterConfig, LocalCluster
+    from odh_kubeflow_amd.models import kinds
     from odh_kubeflow_amd.models.notebook import notebook
 
     from odh_kubeflow_amd.testing.apiserver import native
@@ -85,10 +86,16 @@ def test_critical_path_from_audit_log(run, tmp_path):
             for i in range(3):
                 assert await cl.wait_for(lambda i=i: cl.notebook_ready(f"nb{i}", "bench-0"), 20)
             assert await cl.settle(10)
+            for i in range(3):
+                await cl.admin.delete(kinds.NOTEBOOK, f"nb{i}", "bench-0")
+            assert await cl.wait_for(lambda: all(cl.store.peek(kinds.NOTEBOOK, f"nb{i}", "bench-0") is None
+                                                 for i in range(3)), 20)
     run(go(), timeout=90)
     with open(log) as f:
         out = critical_path.analyse(f, "bench-")
     assert out["notebooks"] == 3
+    td = out["teardown"]  # delete → the odh finalizer removed
+    assert td["notebooks"] == 3 and td["delete_to_finalizer_removed_ms"]["p50"] >= td["finalizer_write_serve_ms"]["p50"] > 0
     assert {"notebook_create", "sts_create", "pod_create", "pod_ready", "notebook_status"} <= set(out["hops"])
     assert out["create_to_notebook_status_ms"]["p50"] > 0
     w = out["writes_per_notebook"]

@@ -140,6 +140,7 @@ def analyse(lines, ns_prefix: str = "", name_prefix: str = "") -> dict:
             "serve_ms_p50": round(pct(h["serve"], .5), 3), "serve_ms_p95": round(pct(h["serve"], .95), 3),
             "by": dict(h["agents"]),
         }
+    out["teardown"] = _teardown(by_obj, notebooks)
     n_created = max(1, len(notebooks))
     out["writes_per_notebook"] = {
         "total": round(sum(writes.values()) / n_created, 2),
@@ -149,6 +150,33 @@ def analyse(lines, ns_prefix: str = "", name_prefix: str = "") -> dict:
         v = out["create_to_notebook_status_ms"][k]
         out["create_to_notebook_status_ms"][k] = round(v, 3) if v is not None else None
     return out
+
+
+def _teardown(by_obj, notebooks) -> dict:
+    """Delete → finalizer removed, per Notebook: the delete's service time, then the gap to the
+    write that removes the odh finalizer (the reconciler's wake-up and its deletes of the
+    exposure children — auth-delegator CRB, central HTTPRoute, ReferenceGrant — are in it) and
+    that write's service time (the admission webhook inside).  The garbage collector's cascade
+    after it (StatefulSet, then Pod) runs inside the apiserver and is not in the audit log."""
+    dserve, gap, fserve, total = [], [], [], []
+    for ns, nb in notebooks:
+        evs = by_obj.get((ns, "notebooks", nb), [])
+        dels = [e for e in evs if e[2] == "delete"]
+        if not dels:
+            continue
+        r0, d0 = dels[-1][0], dels[-1][1]
+        fin = next((e for e in evs if e[0] > r0 and e[2] in ("patch", "update") and not e[3]), None)
+        if fin is None:
+            continue
+        dserve.append((d0 - r0) * 1e3)
+        gap.append(max(0.0, fin[0] - d0) * 1e3)
+        fserve.append((fin[1] - fin[0]) * 1e3)
+        total.append((fin[1] - r0) * 1e3)
+
+    def q(xs):
+        return {"p50": round(pct(xs, .5), 3), "p95": round(pct(xs, .95), 3)} if xs else None
+    return {"notebooks": len(total), "delete_to_finalizer_removed_ms": q(total), "delete_serve_ms": q(dserve),
+            "gap_to_finalizer_write_ms": q(gap), "finalizer_write_serve_ms": q(fserve)}
 
 
 def main(argv=None) -> int:

@@ -60,12 +60,32 @@ while [ $# -gt 0 ]; do
       k=$1; shift
       arch=${1:-sharded}; shift
       extra=()
-      [ "$arch" = unsharded ] && extra=(--arch unsharded --workers 4 --kf-split-workers --webhook-replicas 3 --cache-configmaps)
+      # an optional number after the layout: the unsharded layout's webhook processes (default 3,
+      # as overlay mi355x)
+      wr=3; wrtag=""
+      if [[ "${1:-}" =~ ^[0-9]+$ ]]; then wr=$1; wrtag="_wr$1"; shift; fi
+      [ "$arch" = unsharded ] && extra=(--arch unsharded --workers 4 --kf-split-workers \
+        --webhook-replicas "$wr" --cache-configmaps)
+      f="streams_${k}_${arch}${wrtag}_$(date +%s)"
+      cat /sys/fs/cgroup/cpu.stat > "$out/$f.cpustat0" 2>/dev/null || true
       timeout -k 10 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node "$k" --master-addr 127.0.0.1 \
         --master-port 29517 bench.py --gpus "$k" --steps 100 --warmup 10 --no-gpu-probe --burst 0 --resident 0 \
-        --storage-steps 0 "${extra[@]}" --json-out "$out/streams_${k}_$arch.json" > "$out/streams_${k}_$arch.log" 2>&1 \
+        --storage-steps 0 "${extra[@]}" --json-out "$out/$f.json" > "$out/$f.log" 2>&1 \
         || { echo "streams $k $arch failed rc=$?" | tee -a "$out/SUMMARY.txt"; exit 1; }
-      python tools/summarize_bench.py "$out/streams_${k}_$arch.log" | tee -a "$out/SUMMARY.txt" ;;
+      cat /sys/fs/cgroup/cpu.stat > "$out/$f.cpustat1" 2>/dev/null || true
+      python tools/summarize_bench.py "$out/$f.log" | tee -a "$out/SUMMARY.txt"
+      # the box's CPU share over the run: cgroup v2 usage and CFS throttling
+      python - "$out/$f.cpustat0" "$out/$f.cpustat1" <<'PY' | tee -a "$out/SUMMARY.txt"
+import sys
+def rd(p):
+    try:
+        return {l.split()[0]: int(l.split()[1]) for l in open(p) if len(l.split()) == 2}
+    except OSError:
+        return {}
+a, b = rd(sys.argv[1]), rd(sys.argv[2])
+print("  cgroup cpu.stat delta:", {k: b[k] - a.get(k, 0) for k in ("usage_usec", "nr_periods", "nr_throttled", "throttled_usec") if k in b})
+PY
+      ;;
     failover)
       # takeover and cold start with R resident notebooks (tools/bench_failover.py)
       r=$1; shift
@@ -107,7 +127,7 @@ while [ $# -gt 0 ]; do
         > "$out/critpath_${arch}_n4.log" 2>&1 || exit 1
       python tools/critical_path.py "$out/a4.jsonl" --name-prefix nb-s > "$out/critical_path_${arch}_n4.json" || exit 1
       rm -f "$out/a1.jsonl" "$out/a4.jsonl"
-      python -c "import json,sys; [print(f, json.load(open(f))['create_to_notebook_status_ms']) for f in sys.argv[1:]]" \
+      python -c "import json,sys; [print(f, json.load(open(f))['create_to_notebook_status_ms'], json.load(open(f)).get('teardown')) for f in sys.argv[1:]]" \
         "$out/critical_path_${arch}_n1.json" "$out/critical_path_${arch}_n4.json" | tee -a "$out/SUMMARY.txt" ;;
     probeprof)
       # rocprofv3 kernel trace + stats of one odh-gpu-probe run (no counters: a plain trace)
@@ -156,6 +176,10 @@ while [ $# -gt 0 ]; do
       done
       kill "$hp"; wait "$hp"
       python tools/probe_streams.py "$out/probe_busy_$gap.jsonl" | sed "s/^/busy gap=${gap}s /" | tee -a "$out/SUMMARY.txt" ;;
+    cpuinfo)
+      # the CPU share this box gives the command: quota, cpuset, SMT
+      { echo "cpu.max: $(cat /sys/fs/cgroup/cpu.max 2>/dev/null)"; echo "cpuset: $(cat /sys/fs/cgroup/cpuset.cpus.effective 2>/dev/null)"
+        echo "nproc: $(nproc)"; lscpu | grep -E "^(CPU\(s\)|Thread|Core|Socket|Model name)"; } | tee -a "$out/SUMMARY.txt" ;;
     probechain)
       # K runs GAP seconds apart, probe args after "--" up to the next step name "end"
       k="$1"; gap="$2"; shift 2

@@ -176,6 +176,23 @@ PY
       done
       kill "$hp"; wait "$hp"
       python tools/probe_streams.py "$out/probe_busy_$gap.jsonl" | sed "s/^/busy gap=${gap}s /" | tee -a "$out/SUMMARY.txt" ;;
+    fair)
+      # fair CLUSTER WL SIDE: the fair reference baseline (README "A fair reference baseline"):
+      # CLUSTER vanilla | openshift (pull secrets 200 ms after each ServiceAccount), WL ms per
+      # apiserver write, SIDE ours | ref (--reference-emulation); N=1, then 8 at once
+      cl="$1"; wl="$2"; side="$3"; shift 3
+      extra=(); [ "$cl" = openshift ] && extra+=(--openshift-pull-secret-ms 200)
+      if [ "$side" = ref ]; then extra+=(--reference-emulation --steps 2 --warmup 1); else extra+=(--steps 20 --warmup 3); fi
+      timeout -k 10 400 python bench.py --burst 8 --burst-rounds 1 --resident 0 --storage-steps 0 --no-configs \
+        --no-gpu-probe --write-latency-ms "$wl" "${extra[@]}" > "$out/fair_${side}_${cl}_wl$wl.log" 2>&1 \
+        || { echo "fair $cl $wl $side failed rc=$?" | tee -a "$out/SUMMARY.txt"; exit 1; }
+      python - "$out/fair_${side}_${cl}_wl$wl.log" <<'PY' | tee -a "$out/SUMMARY.txt"
+import json, sys
+d = json.loads([l for l in open(sys.argv[1]) if l.startswith('{"metric"')][-1])
+b = d.get("burst") or {}
+print(sys.argv[1].split("/")[-1], "p50", d.get("p50_ready_ms"), "8 at once: all Ready", b.get("all_ready_s"), "s, p50", (b.get("ready_ms") or {}).get("p50"))
+PY
+      ;;
     cpuinfo)
       # the CPU share this box gives the command: quota, cpuset, SMT
       { echo "cpu.max: $(cat /sys/fs/cgroup/cpu.max 2>/dev/null)"; echo "cpuset: $(cat /sys/fs/cgroup/cpuset.cpus.effective 2>/dev/null)"

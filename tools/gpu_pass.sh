@@ -179,11 +179,12 @@ PY
     fair)
       # fair CLUSTER WL SIDE: the fair reference baseline (README "A fair reference baseline"):
       # CLUSTER vanilla | openshift (pull secrets 200 ms after each ServiceAccount), WL ms per
-      # apiserver write, SIDE ours | ref (--reference-emulation); N=1, then 8 at once
+      # apiserver write, SIDE ours | ref (--reference-emulation); N=1, then 8 at once (the second of
+      # two bursts: the first warms the apiserver's TLS connections to the webhook)
       cl="$1"; wl="$2"; side="$3"; shift 3
       extra=(); [ "$cl" = openshift ] && extra+=(--openshift-pull-secret-ms 200)
       if [ "$side" = ref ]; then extra+=(--reference-emulation --steps 2 --warmup 1); else extra+=(--steps 20 --warmup 3); fi
-      timeout -k 10 400 python bench.py --burst 8 --burst-rounds 1 --resident 0 --storage-steps 0 --no-configs \
+      timeout -k 10 400 python bench.py --burst 8 --burst-rounds 2 --resident 0 --storage-steps 0 --no-configs \
         --no-gpu-probe --write-latency-ms "$wl" "${extra[@]}" > "$out/fair_${side}_${cl}_wl$wl.log" 2>&1 \
         || { echo "fair $cl $wl $side failed rc=$?" | tee -a "$out/SUMMARY.txt"; exit 1; }
       python - "$out/fair_${side}_${cl}_wl$wl.log" <<'PY' | tee -a "$out/SUMMARY.txt"
@@ -193,6 +194,17 @@ b = d.get("burst") or {}
 print(sys.argv[1].split("/")[-1], "p50", d.get("p50_ready_ms"), "8 at once: all Ready", b.get("all_ready_s"), "s, p50", (b.get("ready_ms") or {}).get("p50"))
 PY
       ;;
+    burstcp)
+      # burstcp WL: 8 at once (second of two bursts) at WL ms per apiserver write, with the audit
+      # log: the burst notebooks' critical path, and the log itself (gzip) for the timeline
+      wl="$1"; shift
+      DEBUG_WRITE_AUDITLOG=$PWD/$out/burst_wl$wl.audit.jsonl timeout -k 10 300 python bench.py --steps 5 --warmup 2 \
+        --burst 8 --burst-rounds 2 --resident 0 --storage-steps 0 --no-configs --no-gpu-probe --write-latency-ms "$wl" \
+        > "$out/burstcp_wl$wl.log" 2>&1 || { echo "burstcp failed rc=$?" | tee -a "$out/SUMMARY.txt"; exit 1; }
+      python tools/critical_path.py "$out/burst_wl$wl.audit.jsonl" --name-prefix burst-r1 > "$out/burstcp_wl$wl.json" || exit 1
+      gzip -f "$out/burst_wl$wl.audit.jsonl"
+      python -c "import json,sys; d=json.load(open(sys.argv[1])); print(sys.argv[1], d['create_to_notebook_status_ms'], {k: (v['gap_ms_p50'], v['serve_ms_p50']) for k, v in d['hops'].items()})" \
+        "$out/burstcp_wl$wl.json" | tee -a "$out/SUMMARY.txt" ;;
     cpuinfo)
       # the CPU share this box gives the command: quota, cpuset, SMT
       { echo "cpu.max: $(cat /sys/fs/cgroup/cpu.max 2>/dev/null)"; echo "cpuset: $(cat /sys/fs/cgroup/cpuset.cpus.effective 2>/dev/null)"

@@ -302,6 +302,25 @@ def _pcts(xs, qs=(0.5, 0.95, 0.99)) -> dict:
     return out
 
 
+def _cgroup_cpu() -> Optional[dict]:
+    """This container's cgroup-v2 CPU counters (``cpu.stat``): usage and CFS-quota throttling.
+    On a box whose share is a CPU quota, a period whose quota is spent stops every process of
+    the container until the next one — a stall no single process shows.  None when unreadable."""
+    try:
+        with open("/sys/fs/cgroup/cpu.stat") as f:
+            return {k: int(v) for k, v in (line.split() for line in f if len(line.split()) == 2)}
+    except (OSError, ValueError):
+        return None
+
+
+def _cgroup_delta(a: Optional[dict], b: Optional[dict]) -> Optional[dict]:
+    if not a or not b:
+        return None
+    d = {k: b.get(k, 0) - a.get(k, 0) for k in ("usage_usec", "nr_periods", "nr_throttled", "throttled_usec")}
+    return {"usage_ms": round(d["usage_usec"] / 1e3, 1), "periods": d["nr_periods"],
+            "throttled_periods": d["nr_throttled"], "throttled_ms": round(d["throttled_usec"] / 1e3, 1)}
+
+
 async def _burst(args, shard, dist, native, children: dict, use_odh: bool, tag: str = "r0") -> Optional[dict]:
     """Open-loop capacity (the reference's load generator,
     ``kf/loadtest/start_notebooks.py:1-99``, applies N notebooks at once): ``--burst K``
@@ -345,6 +364,7 @@ async def _burst(args, shard, dist, native, children: dict, use_odh: bool, tag: 
     cpu0 = _cpu_snapshot(children, prof0)
     gc0 = {k: v["seq"] for k, v in ((await safe(shard.gc_pauses(), {})) or {}).items()} if shard.procs else {}
     await _in_thread(dist.barrier)
+    cg0 = _cgroup_cpu()
     t0 = time.perf_counter()
     ready_at, create_ms = {}, []
     pending = set(names)
@@ -367,6 +387,7 @@ async def _burst(args, shard, dist, native, children: dict, use_odh: bool, tag: 
     await safe(asyncio.gather(*(create(nm) for nm in names)))
     ok = bool(await safe(shard.wait_until(check, 180), False))
     all_ready = max(ready_at.values()) - t0 if ready_at else None
+    cgroup = _cgroup_delta(cg0, _cgroup_cpu())
     await _in_thread(dist.barrier)
     prof1 = await safe(_apiserver_prof(native))
     cpu1 = _cpu_snapshot(children, prof1)
@@ -390,7 +411,7 @@ async def _burst(args, shard, dist, native, children: dict, use_odh: bool, tag: 
     await _in_thread(dist.all_gather_object, gathered, {
         "lat": [(ready_at[nm] - t0) * 1e3 for nm in names if nm in ready_at], "create": create_ms,
         "all_ready": all_ready, "ok": ok and gone, "cpu": cpu, "adm": adm, "teardown": teardown, "k": k,
-        "wh": wh, "wh_get": wh_get, "prof": prof, "gc": gcp, "errors": errors})
+        "wh": wh, "wh_get": wh_get, "prof": prof, "gc": gcp, "errors": errors, "cgroup": cgroup})
     if rank != 0:
         return None
     lat = [x for g in gathered for x in g["lat"]]
@@ -421,6 +442,9 @@ async def _burst(args, shard, dist, native, children: dict, use_odh: bool, tag: 
                                "gen2": sum(1 for x in ps if x[0] == 2)}
                         for g in gathered for proc, ps in sorted(g["gc"].items()) if ps},
         **({"errors": [e for g in gathered for e in g["errors"]]} if any(g["errors"] for g in gathered) else {}),
+        # the box's CPU share from the first create to this rank's last Ready (rank 0's view;
+        # one container): a throttled period stalls every process at once
+        "cgroup_cpu": gathered[0]["cgroup"],
         "apiserver": {k: v for k, v in (gathered[0]["prof"] or {}).items()
                       if k in ("lock_wait_ms", "lock_contended", "lock_wait_by_resource", "trim_ms", "trims",
                                "admit_wall_ms", "webhook_dials", "webhook_dial_ms", "watch_gone")},
@@ -1121,7 +1145,8 @@ async def _drive(args, shard, dist, torch, children: Optional[dict] = None, nati
                                {"admission_p99_ms": b["admission_ms"]["p99"],
                                 "webhook_handle_p99_ms": b["webhook_handle_ms"]["p99"],
                                 "webhook_dials": (b.get("apiserver") or {}).get("webhook_dials"),
-                                "webhook_dial_ms": (b.get("apiserver") or {}).get("webhook_dial_ms")}
+                                "webhook_dial_ms": (b.get("apiserver") or {}).get("webhook_dial_ms"),
+                                "cgroup_throttled_periods": (b.get("cgroup_cpu") or {}).get("throttled_periods")}
                                for b in rounds]
 
     resident = None

@@ -203,6 +203,8 @@ PY
         > "$out/burstcp_wl$wl.log" 2>&1 || { echo "burstcp failed rc=$?" | tee -a "$out/SUMMARY.txt"; exit 1; }
       python tools/critical_path.py "$out/burst_wl$wl.audit.jsonl" --name-prefix burst-r1 > "$out/burstcp_wl$wl.json" || exit 1
       gzip -f "$out/burst_wl$wl.audit.jsonl"
+      python -c "import json,sys; d=json.loads([l for l in open(sys.argv[1]) if l.startswith('{\"metric\"')][-1]); print(sys.argv[1], d['burst'].get('rounds'), d['burst'].get('cgroup_cpu'))" \
+        "$out/burstcp_wl$wl.log" | tee -a "$out/SUMMARY.txt"
       python -c "import json,sys; d=json.load(open(sys.argv[1])); print(sys.argv[1], d['create_to_notebook_status_ms'], {k: (v['gap_ms_p50'], v['serve_ms_p50']) for k, v in d['hops'].items()})" \
         "$out/burstcp_wl$wl.json" | tee -a "$out/SUMMARY.txt" ;;
     cpuinfo)

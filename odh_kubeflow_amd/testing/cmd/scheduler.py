@@ -92,6 +92,9 @@ async def amain(argv=None) -> int:
         synced += [kinds.SERVICE_ACCOUNT]
     await mgr.start()
     await mgr.cache.wait_synced(synced)
+    from ...utils import gctune
+
+    gctune.tune()  # as every long-running manager (Manager.run_until): no gen-2 pause mid-burst
     print("ready", flush=True)
     await signal_event().wait()
     await mgr.stop()

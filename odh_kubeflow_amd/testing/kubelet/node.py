@@ -473,7 +473,6 @@ class GpuRuntime:
         self.owns_cpu_pods = owns_cpu_pods
         self.host_ip = host_ip
         self.device_manager = device_manager
-        self._io_pool = None  # the device manager's writer thread, made on first use
         self.handles: Dict[str, ContainerHandle] = {}
         self.started = 0
         self.probe_results: List[dict] = []  # GPU probe init containers run: exit code, wall time, verdict
@@ -545,24 +544,15 @@ class GpuRuntime:
         h.info["reported"] = True
         if devices and self.device_manager is not None:
             # the device-manager checkpoint / pod-resources record (what the node agent reads):
-            # a file rewrite, kept off the Ready status write the pod is waiting for and off the
-            # event loop (one writer thread, so the records stay in order): on a slow disk the
-            # rewrites of a burst held every other pod's start behind them
-            await self._io(self.device_manager.allocate, pod, devices)
+            # a file rewrite, kept off the Ready status write the pod is waiting for
+            self.device_manager.allocate(pod, devices)
         self.recorder.event(pod, "Normal", "Started", "Started container " + ",".join(
             c.get("name", "") for c in (pod.get("spec") or {}).get("containers") or []))
         return Result()
 
-    async def _io(self, fn, *args) -> None:
-        if self._io_pool is None:
-            from concurrent.futures import ThreadPoolExecutor
-
-            self._io_pool = ThreadPoolExecutor(1, thread_name_prefix="device-manager")
-        await asyncio.get_running_loop().run_in_executor(self._io_pool, fn, *args)
-
     async def _stop(self, h: ContainerHandle, req: Request) -> None:
         if h.devices and self.device_manager is not None:
-            await self._io(self.device_manager.release, h.info.get("uid", ""), req.namespace, req.name)
+            self.device_manager.release(h.info.get("uid", ""), req.namespace, req.name)
         await self.runtime.stop(h)
 
     async def _set_status(self, pod: dict, ready: bool, handle: Optional[ContainerHandle] = None,
@@ -616,9 +606,6 @@ class GpuRuntime:
             await self.runtime.stop(h)
         self.handles.clear()
         await self.runtime.close()  # containers whose start was interrupted
-        if self._io_pool is not None:
-            self._io_pool.shutdown(wait=True)
-            self._io_pool = None
 
     def setup_with_manager(self, mgr, max_concurrent: int = 8, name: Optional[str] = None):
         mine = pred_funcs(create=lambda o: (o.get("spec") or {}).get("nodeName") == self.node_name,

@@ -21,6 +21,11 @@ while [ $# -gt 0 ]; do
       timeout -k 10 480 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread \
         > "$out/gpu_tests.log" 2>&1 || { echo "gpu tests failed rc=$?" | tee -a "$out/SUMMARY.txt"; exit 1; }
       tail -1 "$out/gpu_tests.log" | tee -a "$out/SUMMARY.txt" ;;
+    smoke)
+      # the driver's round-end smoke: __graft_entry__.smoke() on cuda:0
+      timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" \
+        > "$out/smoke.log" 2>&1 || { echo "smoke failed rc=$?" | tee -a "$out/SUMMARY.txt"; exit 1; }
+      tail -1 "$out/smoke.log" | tee -a "$out/SUMMARY.txt" ;;
     driver)
       n=$1; shift
       for i in $(seq 1 "$n"); do

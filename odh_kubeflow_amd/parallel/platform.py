@@ -51,8 +51,16 @@ async def start_child(module: str, args: List[str], what: str, timeout: float = 
     import tempfile
 
     # the child's stderr goes to an unlinked temporary file: nothing accumulates, and a child
-    # that fails to start says why in the exception
-    err = tempfile.TemporaryFile()
+    # that fails to start says why in the exception.  ODH_CHILD_STDERR_DIR (diagnostics, e.g.
+    # with PYTHONASYNCIODEBUG=1 to log every event-loop callback over 100 ms) keeps each
+    # child's stderr as <dir>/<what>.<pid>.log instead
+    keep = os.environ.get("ODH_CHILD_STDERR_DIR")
+    if keep:
+        os.makedirs(keep, exist_ok=True)
+        err = tempfile.NamedTemporaryFile(dir=keep, prefix="".join(ch if ch.isalnum() else "_" for ch in what) + ".",
+                                          suffix=".log", delete=False)
+    else:
+        err = tempfile.TemporaryFile()
     proc = subprocess.Popen([sys.executable, *python_args, "-m", module, *args], cwd=ROOT, env=child_env(env),
                             stdout=subprocess.PIPE, stderr=err, text=True)
     try:

@@ -199,6 +199,16 @@ b = d.get("burst") or {}
 print(sys.argv[1].split("/")[-1], "p50", d.get("p50_ready_ms"), "8 at once: all Ready", b.get("all_ready_s"), "s, p50", (b.get("ready_ms") or {}).get("p50"))
 PY
       ;;
+    burstdebug)
+      # burstdebug WL: burstcp with asyncio debug (callbacks over 100 ms logged) and every child's
+      # stderr kept under $out/children
+      wl="$1"; shift
+      PYTHONASYNCIODEBUG=1 ODH_CHILD_STDERR_DIR=$PWD/$out/children timeout -k 10 300 python bench.py --steps 5 --warmup 2 \
+        --burst 8 --burst-rounds 2 --resident 0 --storage-steps 0 --no-configs --no-gpu-probe --write-latency-ms "$wl" \
+        > "$out/burstdebug_wl$wl.log" 2>&1 || { echo "burstdebug failed rc=$?" | tee -a "$out/SUMMARY.txt"; exit 1; }
+      python -c "import json,sys; d=json.loads([l for l in open(sys.argv[1]) if l.startswith('{\"metric\"')][-1]); print(sys.argv[1], d['burst'].get('rounds'))" \
+        "$out/burstdebug_wl$wl.log" | tee -a "$out/SUMMARY.txt"
+      python tools/slow_callbacks.py "$out/children" | tee -a "$out/SUMMARY.txt" ;;
     burstcp)
       # burstcp WL: 8 at once (second of two bursts) at WL ms per apiserver write, with the audit
       # log: the burst notebooks' critical path, and the log itself (gzip) for the timeline

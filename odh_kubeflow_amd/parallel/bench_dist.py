@@ -1136,12 +1136,16 @@ async def _drive(args, shard, dist, torch, children: Optional[dict] = None, nati
     if getattr(args, "burst", 0) > 0:  # untimed: open-loop capacity of the same control plane
         rounds = []
         for r in range(max(1, getattr(args, "burst_rounds", 1))):
-            rounds.append(await _burst(args, shard, dist, native, children, use_odh, tag=f"r{r}"))
+            t_wall = time.time()  # the audit log's and the stall watchdogs' clock
+            b = await _burst(args, shard, dist, native, children, use_odh, tag=f"r{r}")
+            if b is not None:
+                b["started_at"] = round(t_wall, 6)
+            rounds.append(b)
         burst = rounds[-1]
         if burst is not None and len(rounds) > 1:
             # the earlier rounds warm what a running cluster has warm (the apiserver's
             # connections to the webhook, the informers' namespaces); the last one is reported
-            burst["rounds"] = [{k: b.get(k) for k in ("all_ready_s", "notebooks_per_s")} |
+            burst["rounds"] = [{k: b.get(k) for k in ("all_ready_s", "notebooks_per_s", "started_at")} |
                                {"admission_p99_ms": b["admission_ms"]["p99"],
                                 "webhook_handle_p99_ms": b["webhook_handle_ms"]["p99"],
                                 "webhook_dials": (b.get("apiserver") or {}).get("webhook_dials"),

@@ -3456,6 +3456,8 @@ void load_config(const std::string& path) {
 
 }  // namespace
 
+int g_stall_ms = 0;  // ODH_STALL_WATCHDOG_MS
+
 int main(int argc, char** argv) {
   // started by the benchmark / test platform (utils/procutil.py): die with the launcher
   if (const char* parent = std::getenv("ODH_PDEATHSIG_PARENT")) {
@@ -3496,17 +3498,46 @@ int main(int argc, char** argv) {
   // at glibc's default: capping it at 8 (MALLOC_ARENA_MAX, still honoured) cut the resident
   // size by ≈10 % but cost ≈35 % more CPU per request at 4 ranks on a 64-core MI355X box, every
   // thread queueing on a shared arena lock (tools/research/apiserver_ab.sh, profiles/r4_apiab).
-  std::thread([] {
-    while (!g_stop) {
-      std::this_thread::sleep_for(std::chrono::seconds(2));
-      auto t0 = std::chrono::steady_clock::now();
-      malloc_trim(0);
-      uint64_t d = (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count();
-      P.trim_ns += d;
-      P.trims++;
-      if (d > P.trim_max_ns.load()) P.trim_max_ns = d;
-    }
-  }).detach();
+  // ODH_APISERVER_TRIM_S: the trim period (seconds; 0 turns the trim off — diagnostics)
+  double trim_s = 2.0;
+  if (const char* e = std::getenv("ODH_APISERVER_TRIM_S")) trim_s = std::atof(e);
+  if (trim_s > 0)
+    std::thread([trim_s] {
+      while (!g_stop) {
+        std::this_thread::sleep_for(std::chrono::microseconds((int64_t)(trim_s * 1e6)));
+        auto t0 = std::chrono::steady_clock::now();
+        malloc_trim(0);
+        uint64_t d = (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count();
+        P.trim_ns += d;
+        P.trims++;
+        if (d > P.trim_max_ns.load()) P.trim_max_ns = d;
+        if (g_stall_ms > 0 && d >= (uint64_t)g_stall_ms * 1000000ull)
+          fprintf(stderr, "stall-watchdog: malloc_trim took %.1f ms\n", (double)d / 1e6);
+      }
+    }).detach();
+  // ODH_STALL_WATCHDOG_MS (diagnostics): a thread that sleeps 1 ms and allocates a page at a
+  // time reports to stderr, with the wall-clock end, every iteration that took this long —
+  // a stall of the whole process (scheduling, the address-space lock, an allocator lock)
+  // shows up here, a stall of one request path does not
+  if (const char* e = std::getenv("ODH_STALL_WATCHDOG_MS")) g_stall_ms = std::atoi(e);
+  if (g_stall_ms > 0)
+    std::thread([] {
+      while (!g_stop) {
+        auto t0 = std::chrono::steady_clock::now();
+        std::this_thread::sleep_for(std::chrono::milliseconds(1));
+        void* pg = malloc(4096);
+        if (pg) {
+          static_cast<volatile char*>(pg)[0] = 1;
+          free(pg);
+        }
+        double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+        if (ms >= g_stall_ms) {
+          timespec ts;
+          clock_gettime(CLOCK_REALTIME, &ts);
+          fprintf(stderr, "stall-watchdog: %.1f ms ending at %.6f\n", ms, (double)ts.tv_sec + ts.tv_nsec / 1e9);
+        }
+      }
+    }).detach();
   if (gc_flag) S.gc = true;
   if (!tok.empty()) g_token = tok;
   if (hist != 512) S.history = hist;

@@ -222,6 +222,36 @@ PY
         "$out/burstcp_wl$wl.log" | tee -a "$out/SUMMARY.txt"
       python -c "import json,sys; d=json.load(open(sys.argv[1])); print(sys.argv[1], d['create_to_notebook_status_ms'], {k: (v['gap_ms_p50'], v['serve_ms_p50']) for k, v in d['hops'].items()})" \
         "$out/burstcp_wl$wl.json" | tee -a "$out/SUMMARY.txt" ;;
+    burststall)
+      # burststall WL TRIM_S ROUNDS: ROUNDS bursts of 8 at WL ms per write with two stall
+      # watchdogs — tools/stall_sampler.py (a process of its own: the box's stalls) and the
+      # apiserver's ODH_STALL_WATCHDOG_MS thread (its process's) — and the apiserver's
+      # malloc_trim every TRIM_S seconds (0: off)
+      wl="$1"; trim="$2"; rounds="$3"; shift 3
+      log="$out/burststall_wl${wl}_t$trim.log"; smp="$out/stall_sampler_wl${wl}_t$trim.txt"
+      python tools/stall_sampler.py --ms 20 --seconds 290 > "$smp" 2>&1 &
+      spid=$!
+      ODH_STALL_WATCHDOG_MS=20 ODH_APISERVER_TRIM_S=$trim timeout -k 10 300 python bench.py --steps 5 --warmup 2 \
+        --burst 8 --burst-rounds "$rounds" --resident 0 --storage-steps 0 --no-configs --no-gpu-probe \
+        --write-latency-ms "$wl" > "$log" 2>&1
+      rc=$?
+      kill $spid 2>/dev/null; wait $spid 2>/dev/null
+      [ $rc = 0 ] || { echo "burststall failed rc=$rc" | tee -a "$out/SUMMARY.txt"; exit 1; }
+      python - "$log" "$smp" <<'PY' | tee -a "$out/SUMMARY.txt"
+import json, re, sys
+d = json.loads([l for l in open(sys.argv[1]) if l.startswith('{"metric"')][-1])
+rounds = d["burst"].get("rounds") or []
+print(sys.argv[1].split("/")[-1], "all_ready_s:", [r.get("all_ready_s") for r in rounds])
+wd = [l.strip() for l in open(sys.argv[1]) if l.startswith("stall-watchdog")]
+sm = [l.strip() for l in open(sys.argv[2]) if "ending at" in l]
+print("  apiserver watchdog:", len(wd), wd[:12])
+print("  sampler:", len(sm), sm[:12], [l.strip() for l in open(sys.argv[2]) if " end " in l])
+for i, r in enumerate(rounds):
+    t0, t1 = r.get("started_at") or 0, (r.get("started_at") or 0) + (r.get("all_ready_s") or 0) + 0.05
+    hit = lambda ls: [l for l in ls if (m := re.search(r"ending at ([0-9.]+)", l)) and t0 <= float(m.group(1)) <= t1 + 0.3]
+    print(f"  round {i}: {r.get('all_ready_s')} s, watchdog in window {hit(wd)}, sampler in window {hit(sm)}")
+PY
+      ;;
     cpuinfo)
       # the CPU share this box gives the command: quota, cpuset, SMT
       { echo "cpu.max: $(cat /sys/fs/cgroup/cpu.max 2>/dev/null)"; echo "cpuset: $(cat /sys/fs/cgroup/cpuset.cpus.effective 2>/dev/null)"

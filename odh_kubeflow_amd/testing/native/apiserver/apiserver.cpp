@@ -572,6 +572,7 @@ struct Ev {
   Obj obj;
   Obj old;
   std::shared_ptr<EvCache> cache;
+  uint64_t t_ns = 0;  // committed at (mono_ns): the stall watchdog's watch-delivery delay
 };
 
 struct Hist;
@@ -696,6 +697,9 @@ uint64_t process_cpu_ns() {
   clock_gettime(CLOCK_PROCESS_CPUTIME_ID, &ts);
   return (uint64_t)ts.tv_sec * 1000000000ull + (uint64_t)ts.tv_nsec;
 }
+
+// ODH_STALL_WATCHDOG_MS (diagnostics, main()): stalls at least this long are reported to stderr
+int g_stall_ms = 0;
 
 uint64_t mono_ns() {
   return (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
@@ -859,6 +863,11 @@ void emit(const Res& r, const char* type, Obj obj, Obj old) {
     EvCache& c = *b.all.hist[b.all.hist.size() - 1 - kLineKeep].cache;
     std::unique_lock<std::mutex> cl(c.mu, std::try_to_lock);  // a watcher serialising it: next time
     if (cl.owns_lock() && c.line) t_free_lines.push_back(std::move(c.line));
+  }
+  if (g_stall_ms > 0) {
+    const uint64_t now = mono_ns();
+    b.all.hist.back().t_ns = now;
+    if (!evns.empty()) b.by_ns[evns].hist.back().t_ns = now;
   }
   const Ev& ev = b.all.hist.back();
   const int64_t step = std::max<int64_t>(1, (int64_t)S.history / 16);
@@ -3072,6 +3081,7 @@ void serve_watch(int fd, Res& r, const Path& p, const Request& rq) {
       cpu_mark = now_cpu;
     }
     std::vector<std::string> lines;
+    uint64_t oldest_ns = 0;
     bool gone = false;
     {
       Bucket& b = *wb;  // element references of S.data stay valid; buckets are never erased
@@ -3101,7 +3111,10 @@ void serve_watch(int fd, Res& r, const Path& p, const Request& rq) {
           std::vector<Ev> evs;
           for (size_t n = start; n < h.hist.size(); ++n) {
             const Ev& e = h.hist[n];
-            if (wants(*e.obj) || (e.old && wants(*e.old))) evs.push_back(e);
+            if (wants(*e.obj) || (e.old && wants(*e.old))) {
+              evs.push_back(e);
+              if (e.t_ns && (!oldest_ns || e.t_ns < oldest_ns)) oldest_ns = e.t_ns;
+            }
           }
           last_seq = h.seq;
           slot.seen = last_seq;
@@ -3123,6 +3136,15 @@ void serve_watch(int fd, Res& r, const Path& p, const Request& rq) {
       for (auto& l : lines) batch += l;
       if (!write_chunk(fd, batch)) return;
       last_write = std::chrono::steady_clock::now();
+      if (g_stall_ms > 0 && oldest_ns) {  // commit -> written to this watcher's socket
+        const double ms = (double)(mono_ns() - oldest_ns) / 1e6;
+        if (ms >= g_stall_ms) {
+          timespec ts;
+          clock_gettime(CLOCK_REALTIME, &ts);
+          fprintf(stderr, "stall-watchdog: watch delivery %.1f ms (%s ns=%s, %zu events) ending at %.6f\n", ms,
+                  r.plural.c_str(), ns.c_str(), lines.size(), (double)ts.tv_sec + ts.tv_nsec / 1e9);
+        }
+      }
     }
     auto now = std::chrono::steady_clock::now();
     if (now >= deadline) break;
@@ -3455,8 +3477,6 @@ void load_config(const std::string& path) {
 }
 
 }  // namespace
-
-int g_stall_ms = 0;  // ODH_STALL_WATCHDOG_MS
 
 int main(int argc, char** argv) {
   // started by the benchmark / test platform (utils/procutil.py): die with the launcher

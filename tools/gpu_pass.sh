@@ -229,9 +229,9 @@ PY
       # malloc_trim every TRIM_S seconds (0: off)
       wl="$1"; trim="$2"; rounds="$3"; shift 3
       log="$out/burststall_wl${wl}_t$trim.log"; smp="$out/stall_sampler_wl${wl}_t$trim.txt"
-      python tools/stall_sampler.py --ms 20 --seconds 290 > "$smp" 2>&1 &
+      python tools/stall_sampler.py --ms ${STALL_MS:-20} --seconds 290 > "$smp" 2>&1 &
       spid=$!
-      ODH_STALL_WATCHDOG_MS=20 ODH_APISERVER_TRIM_S=$trim timeout -k 10 300 python bench.py --steps 5 --warmup 2 \
+      ODH_STALL_WATCHDOG_MS=${STALL_MS:-20} ODH_APISERVER_TRIM_S=$trim timeout -k 10 300 python bench.py --steps 5 --warmup 2 \
         --burst 8 --burst-rounds "$rounds" --resident 0 --storage-steps 0 --no-configs --no-gpu-probe \
         --write-latency-ms "$wl" > "$log" 2>&1
       rc=$?

@@ -14,7 +14,10 @@ a POST.
 from __future__ import annotations
 
 import asyncio
+import os
 import ssl as _ssl
+import sys
+import time
 from typing import AsyncIterator, Dict, List, Optional, Tuple
 from urllib.parse import urlsplit
 
@@ -59,6 +62,15 @@ def _dechunk(raw: bytearray, body: bytearray) -> bool:
         pos = end + 2
     del raw[:pos]
     return done
+
+
+# ODH_STALL_WATCHDOG_MS (diagnostics): every request that took at least this long is reported to
+# stderr with its wall-clock end and whether it rode a pooled or a new connection
+_STALL_MS = float(os.environ.get("ODH_STALL_WATCHDOG_MS") or 0)
+
+
+def _stall_report(what: str) -> None:
+    print(f"stall-watchdog: pid {os.getpid()} {what} ending at {time.time():.6f}", file=sys.stderr, flush=True)
 
 
 class _Conn(asyncio.Protocol):
@@ -289,9 +301,14 @@ class Http1Pool:
             conn = self._take_idle()
             reused = conn is not None
             try:
+                t0 = time.perf_counter() if _STALL_MS else 0.0
                 if conn is None:
                     conn = await self._connect()
+                t1 = time.perf_counter() if _STALL_MS else 0.0
                 status, data, close = await conn.roundtrip(payload)
+                if _STALL_MS and (time.perf_counter() - t0) * 1e3 >= _STALL_MS:
+                    _stall_report(f"{method} {target[:96]}: {(time.perf_counter() - t0) * 1e3:.1f} ms "
+                                  f"({'pooled' if reused else f'new connection, connect {(t1 - t0) * 1e3:.1f} ms'})")
             except (ConnectionError, OSError) as e:
                 if conn is not None:
                     conn.close()

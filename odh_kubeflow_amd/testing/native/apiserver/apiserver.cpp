@@ -3586,6 +3586,22 @@ int main(int argc, char** argv) {
       if (errno == EINTR) continue;
       break;
     }
+    if (g_stall_ms > 0) {  // diagnostics: a connection's thread slow to start delays its requests
+      const uint64_t t0 = mono_ns();
+      std::thread([fd, t0] {
+        const double ms = (double)(mono_ns() - t0) / 1e6;
+        if (ms >= g_stall_ms) {
+          timespec ts;
+          clock_gettime(CLOCK_REALTIME, &ts);
+          fprintf(stderr, "stall-watchdog: connection thread started %.1f ms after accept, at %.6f\n", ms,
+                  (double)ts.tv_sec + ts.tv_nsec / 1e9);
+        }
+        serve_conn(fd);
+      }).detach();
+      const double sp = (double)(mono_ns() - t0) / 1e6;
+      if (sp >= g_stall_ms) fprintf(stderr, "stall-watchdog: thread spawn took %.1f ms\n", sp);
+      continue;
+    }
     std::thread(serve_conn, fd).detach();
   }
   return 0;

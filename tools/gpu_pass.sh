@@ -228,18 +228,21 @@ PY
       # apiserver's ODH_STALL_WATCHDOG_MS thread (its process's) — and the apiserver's
       # malloc_trim every TRIM_S seconds (0: off)
       wl="$1"; trim="$2"; rounds="$3"; shift 3
-      log="$out/burststall_wl${wl}_t$trim.log"; smp="$out/stall_sampler_wl${wl}_t$trim.txt"
+      sfx="wl${wl}_t${trim}_$(date +%s)"; log="$out/burststall_$sfx.log"; smp="$out/stall_sampler_$sfx.txt"
       python tools/stall_sampler.py --ms ${STALL_MS:-20} --seconds 290 > "$smp" 2>&1 &
       spid=$!
-      ODH_STALL_WATCHDOG_MS=${STALL_MS:-20} ODH_APISERVER_TRIM_S=$trim timeout -k 10 300 python bench.py --steps 5 --warmup 2 \
+      ODH_CHILD_STDERR_DIR=$PWD/$out/children_$sfx ODH_STALL_WATCHDOG_MS=${STALL_MS:-20} ODH_APISERVER_TRIM_S=$trim timeout -k 10 300 python bench.py --steps 5 --warmup 2 \
         --burst 8 --burst-rounds "$rounds" --resident 0 --storage-steps 0 --no-configs --no-gpu-probe \
         --write-latency-ms "$wl" > "$log" 2>&1
       rc=$?
       kill $spid 2>/dev/null; wait $spid 2>/dev/null
       [ $rc = 0 ] || { echo "burststall failed rc=$rc" | tee -a "$out/SUMMARY.txt"; exit 1; }
-      python - "$log" "$smp" <<'PY' | tee -a "$out/SUMMARY.txt"
-import json, re, sys
+      python - "$log" "$smp" "$out/children_$sfx" <<'PY' | tee -a "$out/SUMMARY.txt"
+import glob, json, os, re, sys
 d = json.loads([l for l in open(sys.argv[1]) if l.startswith('{"metric"')][-1])
+cl = []  # the control-plane processes' own reports (requests that took >= the threshold)
+for f in sorted(glob.glob(os.path.join(sys.argv[3], "*.log"))):
+    cl += [os.path.basename(f).split(".")[0] + ": " + l.strip() for l in open(f, errors="replace") if l.startswith("stall-watchdog")]
 rounds = d["burst"].get("rounds") or []
 print(sys.argv[1].split("/")[-1], "all_ready_s:", [r.get("all_ready_s") for r in rounds])
 wd = [l.strip() for l in open(sys.argv[1]) if l.startswith("stall-watchdog")]
@@ -250,6 +253,8 @@ for i, r in enumerate(rounds):
     t0, t1 = r.get("started_at") or 0, (r.get("started_at") or 0) + (r.get("all_ready_s") or 0) + 0.05
     hit = lambda ls: [l for l in ls if (m := re.search(r"ending at ([0-9.]+)", l)) and t0 <= float(m.group(1)) <= t1 + 0.3]
     print(f"  round {i}: {r.get('all_ready_s')} s, watchdog in window {hit(wd)}, sampler in window {hit(sm)}")
+    for l in hit(cl)[:16]:
+        print("     client:", l[:260])
 PY
       ;;
     cpuinfo)

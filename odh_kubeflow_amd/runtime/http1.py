@@ -73,6 +73,29 @@ def _stall_report(what: str) -> None:
     print(f"stall-watchdog: pid {os.getpid()} {what} ending at {time.time():.6f}", file=sys.stderr, flush=True)
 
 
+_LAG_LOOPS: set = set()
+
+
+def _ensure_loop_watchdog() -> None:
+    """With ODH_STALL_WATCHDOG_MS: one task per event loop that sleeps 2 ms at a time and
+    reports every wake-up that came at least the threshold late (the loop was stopped: a
+    long callback, a collection, a blocking call)."""
+    loop = asyncio.get_running_loop()
+    if id(loop) in _LAG_LOOPS:
+        return
+    _LAG_LOOPS.add(id(loop))
+
+    async def watch() -> None:
+        while True:
+            t0 = time.perf_counter()
+            await asyncio.sleep(0.002)
+            late = (time.perf_counter() - t0 - 0.002) * 1e3
+            if late >= _STALL_MS:
+                _stall_report(f"event loop {late:.1f} ms late")
+
+    loop.create_task(watch())
+
+
 class _Conn(asyncio.Protocol):
     """One keep-alive connection whose responses are parsed in ``data_received``.
 
@@ -297,6 +320,8 @@ class Http1Pool:
     async def request(self, method: str, target: str, body: Optional[bytes] = None,
                       content_type: Optional[str] = None) -> Tuple[int, bytes]:
         payload = self._head(method, target, body, content_type)
+        if _STALL_MS:
+            _ensure_loop_watchdog()
         for attempt in (0, 1):
             conn = self._take_idle()
             reused = conn is not None

@@ -21,10 +21,13 @@ from __future__ import annotations
 
 import collections
 import gc
+import os
+import sys
 import time
 from typing import Dict, List
 
 DEFAULT_THRESHOLDS = (50_000, 20, 100)
+_STALL_MS = float(os.environ.get("ODH_STALL_WATCHDOG_MS") or 0)
 _BOUNDS = (0.0005, 0.001, 0.0025, 0.005, 0.01, 0.025, 0.05, 0.1, 0.25, 0.5, 1.0)
 
 
@@ -49,6 +52,9 @@ class PauseRecorder:
         self.seq += 1
         self.recent.append((self.seq, g, d))
         self.sums[g] = self.sums.get(g, 0.0) + d
+        if _STALL_MS and d * 1e3 >= _STALL_MS:  # diagnostics (ODH_STALL_WATCHDOG_MS)
+            print(f"stall-watchdog: pid {os.getpid()} gc generation {g} took {d * 1e3:.1f} ms ending at "
+                  f"{time.time():.6f}", file=sys.stderr, flush=True)
         b = self.counts.setdefault(g, [0] * (len(_BOUNDS) + 1))
         i = 0
         while i < len(_BOUNDS) and d > _BOUNDS[i]:

@@ -22,6 +22,7 @@ from typing import Awaitable, Callable, Dict, Iterable, List, NamedTuple, Option
 from ..models import meta as m
 from ..models.scheme import SCHEME
 from .client import CURRENT_RECONCILE
+from . import workqueue as _wq
 from .workqueue import ShutDown, WorkQueue
 
 log = logging.getLogger(__name__)
@@ -340,6 +341,8 @@ class Controller:
             finally:
                 CURRENT_RECONCILE.reset(tok)
             dt = time.perf_counter() - t0
+            if _wq._STALL_MS and dt * 1e3 >= _wq._STALL_MS:
+                _wq.stall_report(f"reconcile {self.name} {req} took {dt * 1e3:.1f} ms ({trig})")
             self.busy_time += dt
             self.reconciles += 1
             self.active -= 1

@@ -12,9 +12,20 @@
 from __future__ import annotations
 
 import asyncio
+import os
+import sys
 import time
 from collections import deque
 from typing import Any, Deque, Dict, Hashable, Optional, Set
+
+
+# ODH_STALL_WATCHDOG_MS (diagnostics): items that wait in the queue, or are requeued with a
+# delay (under a second), at least this long are reported to stderr
+_STALL_MS = float(os.environ.get("ODH_STALL_WATCHDOG_MS") or 0)
+
+
+def stall_report(what: str) -> None:
+    print(f"stall-watchdog: pid {os.getpid()} {what} ending at {time.time():.6f}", file=sys.stderr, flush=True)
 
 
 class ExponentialRateLimiter:
@@ -136,6 +147,8 @@ class WorkQueue:
         self._processing.add(item)
         self._dirty.discard(item)
         t0 = self._added_at.pop(item, None)
+        if _STALL_MS and t0 is not None and (time.monotonic() - t0) * 1e3 >= _STALL_MS:
+            stall_report(f"queue {self.name}: {item} waited {(time.monotonic() - t0) * 1e3:.1f} ms for a worker")
         if self.metrics and t0 is not None:
             self.metrics.on_get(self.name, len(self._queue), time.monotonic() - t0)
         return item
@@ -155,6 +168,8 @@ class WorkQueue:
         if delay <= 0:
             self.add(item)
             return
+        if _STALL_MS and _STALL_MS <= delay * 1e3 < 1000:
+            stall_report(f"queue {self.name}: {item} requeued {delay * 1e3:.1f} ms ahead")
         loop = asyncio.get_running_loop()
         when = loop.time() + delay
         prev = self._waiting_when.get(item)

@@ -440,6 +440,8 @@ class Http1Server:
         self._conns: set = set()
 
     async def start(self) -> "Http1Server":
+        if _STALL_MS:
+            _ensure_loop_watchdog()
         self._server = await asyncio.start_server(self._serve, self.host, self.port, ssl=self.ssl, limit=1 << 24,
                                                   reuse_port=self.reuse_port or None)
         self.port = self._server.sockets[0].getsockname()[1]

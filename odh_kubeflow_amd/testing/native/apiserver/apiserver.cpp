@@ -1957,8 +1957,10 @@ Value call_webhook(const Webhook& w, const Value& review) {
     g_pool_cv.notify_one();
   };
   for (int attempt = 0; attempt < 2; ++attempt) {
+    const uint64_t t0 = mono_ns();
     std::unique_ptr<TlsConn> c = acquire(attempt == 0);
     bool reused = (bool)c;
+    const uint64_t t1 = mono_ns();
     if (!c) {
       try {
         c = tls_connect(host, port, w.ca_pem, w.timeout_s);
@@ -1967,10 +1969,19 @@ Value call_webhook(const Webhook& w, const Value& review) {
         throw;
       }
     }
+    const uint64_t t2 = mono_ns();
     int status = 0;
     std::string resp;
     bool close = false;
-    if (tls_write_all(*c, req) && tls_read_response(*c, &status, &resp, &close)) {
+    const bool ok = tls_write_all(*c, req) && tls_read_response(*c, &status, &resp, &close);
+    if (g_stall_ms > 0 && mono_ns() - t0 >= (uint64_t)g_stall_ms * 1000000ull) {
+      timespec ts;
+      clock_gettime(CLOCK_REALTIME, &ts);
+      fprintf(stderr, "stall-watchdog: webhook call %.1f ms (slot %.1f, %s %.1f, round trip %.1f, attempt %d, ok %d) ending at %.6f\n",
+              (mono_ns() - t0) / 1e6, (t1 - t0) / 1e6, reused ? "pooled" : "dial", (t2 - t1) / 1e6,
+              (mono_ns() - t2) / 1e6, attempt, (int)ok, (double)ts.tv_sec + ts.tv_nsec / 1e9);
+    }
+    if (ok) {
       if (close) c.reset();  // the webhook hangs up after this answer: the slot reconnects next time
       give_back(std::move(c));
       if (status != 200) throw std::runtime_error("webhook returned HTTP " + std::to_string(status));

@@ -3599,6 +3599,16 @@ int main(int argc, char** argv) {
     }
     if (g_stall_ms > 0) {  // diagnostics: a connection's thread slow to start delays its requests
       const uint64_t t0 = mono_ns();
+      struct tcp_info ti {};
+      socklen_t tl = sizeof(ti);
+      // how long the connection sat in the listen queue: its handshake (and any request bytes)
+      // arrived this long before accept() handed it over
+      if (getsockopt(fd, IPPROTO_TCP, TCP_INFO, &ti, &tl) == 0 && ti.tcpi_last_data_recv >= (unsigned)g_stall_ms) {
+        timespec ts;
+        clock_gettime(CLOCK_REALTIME, &ts);
+        fprintf(stderr, "stall-watchdog: accepted %u ms after its first data (last ack recv %u ms) at %.6f\n",
+                ti.tcpi_last_data_recv, ti.tcpi_last_ack_recv, (double)ts.tv_sec + ts.tv_nsec / 1e9);
+      }
       std::thread([fd, t0] {
         const double ms = (double)(mono_ns() - t0) / 1e6;
         if (ms >= g_stall_ms) {

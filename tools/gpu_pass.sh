@@ -255,6 +255,7 @@ for i, r in enumerate(rounds):
     print(f"  round {i}: {r.get('all_ready_s')} s, watchdog in window {hit(wd)}, sampler in window {hit(sm)}")
     for l in hit(cl)[:16]:
         print("     client:", l[:260])
+print("  control-plane reports (not requeues):", [l[:220] for l in cl if "requeued" not in l][:24])
 PY
       ;;
     cpuinfo)

@@ -3489,44 +3489,6 @@ void load_config(const std::string& path) {
 
 }  // namespace
 
-// one acceptor: accept, then a thread per connection (main() runs several of these)
-void accept_loop(int ls) {
-  while (true) {
-    int fd = accept(ls, nullptr, nullptr);
-    if (fd < 0) {
-      if (errno == EINTR) continue;
-      break;
-    }
-    if (g_stall_ms > 0) {  // diagnostics: a connection's thread slow to start delays its requests
-      const uint64_t t0 = mono_ns();
-      struct tcp_info ti {};
-      socklen_t tl = sizeof(ti);
-      // how long the connection sat in the listen queue: its handshake (and any request bytes)
-      // arrived this long before accept() handed it over
-      if (getsockopt(fd, IPPROTO_TCP, TCP_INFO, &ti, &tl) == 0 && ti.tcpi_last_data_recv >= (unsigned)g_stall_ms) {
-        timespec ts;
-        clock_gettime(CLOCK_REALTIME, &ts);
-        fprintf(stderr, "stall-watchdog: accepted %u ms after its first data (last ack recv %u ms) at %.6f\n",
-                ti.tcpi_last_data_recv, ti.tcpi_last_ack_recv, (double)ts.tv_sec + ts.tv_nsec / 1e9);
-      }
-      std::thread([fd, t0] {
-        const double ms = (double)(mono_ns() - t0) / 1e6;
-        if (ms >= g_stall_ms) {
-          timespec ts;
-          clock_gettime(CLOCK_REALTIME, &ts);
-          fprintf(stderr, "stall-watchdog: connection thread started %.1f ms after accept, at %.6f\n", ms,
-                  (double)ts.tv_sec + ts.tv_nsec / 1e9);
-        }
-        serve_conn(fd);
-      }).detach();
-      const double sp = (double)(mono_ns() - t0) / 1e6;
-      if (sp >= g_stall_ms) fprintf(stderr, "stall-watchdog: thread spawn took %.1f ms\n", sp);
-      continue;
-    }
-    std::thread(serve_conn, fd).detach();
-  }
-}
-
 int main(int argc, char** argv) {
   // started by the benchmark / test platform (utils/procutil.py): die with the launcher
   if (const char* parent = std::getenv("ODH_PDEATHSIG_PARENT")) {
@@ -3629,14 +3591,39 @@ int main(int argc, char** argv) {
   getsockname(ls, (struct sockaddr*)&addr, &len);
   printf("LISTENING %d\n", ntohs(addr.sin_port));
   fflush(stdout);
-  // several threads block in accept() on the one listening socket: the kernel wakes one of
-  // them per connection, so a connection whose acceptor is not running (descheduled, e.g. on
-  // a CPU whose share of the CFS quota ran out for the period) is taken by the next one to
-  // wake.  With a single acceptor, new connections sat 80-170 ms in the listen queue during
-  // bursts on the one-GPU boxes (profiles/r6_g38) while every running thread was on time
-  int acceptors = 4;
-  if (const char* e = std::getenv("ODH_APISERVER_ACCEPTORS")) acceptors = std::max(1, std::atoi(e));
-  for (int k = 1; k < acceptors; ++k) std::thread(accept_loop, ls).detach();
-  accept_loop(ls);
+  while (true) {
+    int fd = accept(ls, nullptr, nullptr);
+    if (fd < 0) {
+      if (errno == EINTR) continue;
+      break;
+    }
+    if (g_stall_ms > 0) {  // diagnostics: a connection's thread slow to start delays its requests
+      const uint64_t t0 = mono_ns();
+      struct tcp_info ti {};
+      socklen_t tl = sizeof(ti);
+      // how long the connection sat in the listen queue: its handshake (and any request bytes)
+      // arrived this long before accept() handed it over
+      if (getsockopt(fd, IPPROTO_TCP, TCP_INFO, &ti, &tl) == 0 && ti.tcpi_last_data_recv >= (unsigned)g_stall_ms) {
+        timespec ts;
+        clock_gettime(CLOCK_REALTIME, &ts);
+        fprintf(stderr, "stall-watchdog: accepted %u ms after its first data (last ack recv %u ms) at %.6f\n",
+                ti.tcpi_last_data_recv, ti.tcpi_last_ack_recv, (double)ts.tv_sec + ts.tv_nsec / 1e9);
+      }
+      std::thread([fd, t0] {
+        const double ms = (double)(mono_ns() - t0) / 1e6;
+        if (ms >= g_stall_ms) {
+          timespec ts;
+          clock_gettime(CLOCK_REALTIME, &ts);
+          fprintf(stderr, "stall-watchdog: connection thread started %.1f ms after accept, at %.6f\n", ms,
+                  (double)ts.tv_sec + ts.tv_nsec / 1e9);
+        }
+        serve_conn(fd);
+      }).detach();
+      const double sp = (double)(mono_ns() - t0) / 1e6;
+      if (sp >= g_stall_ms) fprintf(stderr, "stall-watchdog: thread spawn took %.1f ms\n", sp);
+      continue;
+    }
+    std::thread(serve_conn, fd).detach();
+  }
   return 0;
 }

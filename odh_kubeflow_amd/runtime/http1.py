@@ -269,7 +269,7 @@ class _Conn(asyncio.Protocol):
 
 class Http1Pool:
     def __init__(self, base_url: str, ssl_context: Optional[_ssl.SSLContext] = None,
-                 headers: Optional[Dict[str, str]] = None, size: int = 64):
+                 headers: Optional[Dict[str, str]] = None, size: int = 64, spare: int = 0):
         u = urlsplit(base_url)
         self.host = u.hostname or "127.0.0.1"
         self.port = u.port or (443 if u.scheme == "https" else 80)
@@ -280,6 +280,11 @@ class Http1Pool:
         self._idle: List[_Conn] = []
         self.size = size
         self.opened = 0
+        # idle connections kept open ahead of demand: a request that finds the pool empty
+        # does not wait for a connection to be accepted (on the GPU boxes a burst's new
+        # connections sat 80-170 ms in the apiserver's listen queue, profiles/r6_g38)
+        self.spare = max(0, int(spare))
+        self._warming = 0
 
     def set_header(self, name: str, value: Optional[str]) -> None:
         """Set (``None``: drop) a header every later request carries — e.g. a rotated bearer
@@ -311,11 +316,28 @@ class Http1Pool:
         return (h + "\r\n").encode("latin-1") + (body or b"")
 
     def _take_idle(self) -> Optional[_Conn]:
+        c = None
         while self._idle:
             c = self._idle.pop()
             if not c.closed:
-                return c
-        return None
+                break
+            c = None
+        while self.spare and len(self._idle) + self._warming < self.spare:
+            self._warming += 1
+            asyncio.get_running_loop().create_task(self._warm())
+        return c
+
+    async def _warm(self) -> None:
+        try:
+            conn = await self._connect()
+        except (ConnectionError, OSError):
+            return
+        finally:
+            self._warming -= 1
+        if self.spare and len(self._idle) < self.size:
+            self._idle.append(conn)
+        else:
+            conn.close()
 
     async def request(self, method: str, target: str, body: Optional[bytes] = None,
                       content_type: Optional[str] = None) -> Tuple[int, bytes]:
@@ -362,6 +384,7 @@ class Http1Pool:
         return status, headers, _Stream(conn)
 
     async def close(self) -> None:
+        self.spare = 0  # no more warming; one in flight closes its connection below
         for c in self._idle:
             c.close()
         self._idle.clear()

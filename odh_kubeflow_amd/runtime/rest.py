@@ -268,7 +268,7 @@ class RestClient(Client):
             headers = {"User-Agent": self.config.user_agent}
             if tok:
                 headers["Authorization"] = f"Bearer {tok}"
-            self._session = Http1Pool(self.base, self._ssl, headers, size=self._pool)
+            self._session = Http1Pool(self.base, self._ssl, headers, size=self._pool, spare=2)
             self._sent_token = tok
         elif tok != self._sent_token:  # the token file was rotated
             self._session.set_header("Authorization", f"Bearer {tok}" if tok else None)

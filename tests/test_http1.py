@@ -181,3 +181,33 @@ def test_server_closes_a_connection_after_max_requests():
         w.close()
         await srv.stop()
     asyncio.run(go())
+
+
+def test_pool_keeps_spare_connections_open_ahead_of_demand():
+    """``spare``: the REST client's pool opens connections before a request needs one, so a
+    burst does not wait for new connections to be accepted (profiles/r6_g38: 80-170 ms in the
+    apiserver's listen queue on the GPU boxes).  Concurrent requests beyond the pool's idle
+    connections still open their own."""
+    from odh_kubeflow_amd.runtime.http1 import Http1Pool, Http1Server
+
+    async def handler(method, path, headers, body):
+        await asyncio.sleep(0.01)
+        return 200, "text/plain", b"ok"
+
+    async def go():
+        srv = await Http1Server(handler).start()
+        pool = Http1Pool(f"http://127.0.0.1:{srv.port}", spare=2)
+        assert await pool.request("GET", "/a") == (200, b"ok")
+        for _ in range(100):
+            if len(pool._idle) >= 3:
+                break
+            await asyncio.sleep(0.01)
+        assert len(pool._idle) == 3 and pool.opened == 3  # the request's own + 2 spares
+        got = await asyncio.gather(*(pool.request("GET", f"/b{i}") for i in range(5)))
+        assert got == [(200, b"ok")] * 5
+        await asyncio.sleep(0.1)
+        assert len(pool._idle) >= 5 and pool.opened <= 5 + 2 + 2
+        await pool.close()
+        assert pool._idle == [] and pool.spare == 0
+        await srv.stop()
+    asyncio.run(asyncio.wait_for(go(), 20))
